@@ -1,0 +1,227 @@
+#!/usr/bin/env python3
+"""bench.py — pods scheduled/sec at 1M nodes (BASELINE.json metric) on MI355X.
+
+Workload (BASELINE.json configs[2], "C3" of SURVEY.md §8(d)): a 1,000,000-node
+kwok-shaped heterogeneous cluster (cpu 8-96 cores, memory 32-512 Gi, 32/110
+pods, kwok NoSchedule taint; every node pre-filled with seeded pods to a
+random 0-50% of its CPU), and a stream of resource-only pods (cpu 50-4000m,
+memory 64Mi x 1..256, 10% best-effort, kwok tolerations).  Filter =
+NodeUnschedulable/NodeName/TaintToleration/NodeAffinity/NodeResourcesFit,
+Score = LeastAllocated + BalancedAllocation + TaintToleration (+ NodeAffinity
+skipped, ImageLocality 0), percentageOfNodesToScore = 100, deterministic
+lowest-slot tie-break, sequential-equivalent in-order commit.
+
+A "step" schedules one batch of pods (default 8192) to completion against the
+live cluster; inputs are resident in HBM before the timed region (the batch
+is compiled and uploaded by ks_batch_prepare beforehand).  With --gpus N the
+node slots are sharded across N ranks (one process per GPU, RCCL candidate
+all-gather); every rank schedules the same pods, so `value` is the job's
+pods/s (strong scaling: the cluster is fixed at 1M nodes).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "k8s-1m_amd"))
+
+B_NODE = 56  # algorithmic bytes per (pod, node) evaluation, resource-only
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--nodes", type=int, default=1_000_000)
+    ap.add_argument("--batch", type=int, default=8192, help="pods per step")
+    ap.add_argument("--pods-per-round", type=int, default=256)
+    ap.add_argument("--topk", type=int, default=0)
+    ap.add_argument("--nodes-per-lane", type=int, default=8)
+    ap.add_argument("--kind", default="hetero", choices=["hetero", "kwok", "labeled"])
+    ap.add_argument("--prefill", type=float, default=0.5)
+    ap.add_argument("--cpu-pods", type=int, default=40, help="oracle sample size (pods) for cpu_baseline")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pmc-file", default=os.environ.get("KS_PMC_FILE", ""),
+                    help="JSON with measured HBM bytes per sweep launch (rocprofv3 --pmc pass)")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    from ksched import Scheduler, synth
+    from ksched.framework import results_to_arrays
+
+    kind = {"hetero": synth.HETERO, "kwok": synth.KWOK, "labeled": synth.LABELED}[args.kind]
+    t_setup = time.time()
+    sched = Scheduler(args.nodes, device=local_rank if world > 1 else 0, pods_per_round=args.pods_per_round,
+                      topk=args.topk, nodes_per_lane=args.nodes_per_lane, world_size=world, rank=rank)
+    if world > 1:
+        import torch
+
+        uid = torch.zeros(128, dtype=torch.uint8, device="cuda")
+        if rank == 0:
+            uid.copy_(torch.frombuffer(bytearray(Scheduler.comm_unique_id()), dtype=torch.uint8))
+        dist.broadcast(uid, 0)
+        sched.comm_init(bytes(uid.cpu().numpy().tobytes()))
+
+    nodes = synth.nodes(kind, args.nodes, 1)
+    slots = synth.slot_array(args.nodes)
+    sched.upsert_nodes_raw(nodes.nodes, slots, args.nodes)
+    pre = None
+    if args.prefill > 0:
+        pre = synth.prefill(kind, args.nodes, 1, 3, args.prefill)
+        assert sched.lib.ks_pods_add(sched.ctx, pre.pods, pre.slot_ptr, pre.n_pods) == 0, \
+            sched.lib.ks_last_error(sched.ctx)
+    n_batches = args.warmup + args.steps
+    pods = synth.pods(kind, n_batches * args.batch, 2)
+    batches = [sched.prepare(pods.pods_at(b * args.batch), args.batch) for b in range(n_batches)]
+    setup_s = time.time() - t_setup
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    def sync():
+        if dist is not None:
+            import torch
+
+            torch.cuda.synchronize()
+
+    for b in range(args.warmup):
+        sched.run(batches[b])
+    sched.reset_stats()
+    sched.set_timing(True)
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    for b in range(args.warmup, n_batches):
+        sched.run(batches[b])
+    sync()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    sched.set_timing(False)
+    if dist is not None:
+        import torch
+
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    st = sched.stats()
+
+    # scheduled fraction of the timed pods (sanity for the reader)
+    scheduled = 0
+    for b in range(args.warmup, n_batches):
+        r = results_to_arrays(sched.results(batches[b], args.batch), args.batch)
+        scheduled += int((r["status"] == 0).sum())
+
+    pods_timed = args.steps * args.batch
+    value = pods_timed / elapsed
+    nodes_local = args.nodes // world
+    sweep_avg_ms = st.sweep_ms / max(1, st.sweep_launches)
+    evals_per_launch = st.sweep_evals / max(1, st.sweep_launches)
+    achieved = B_NODE * evals_per_launch / (sweep_avg_ms * 1e-3) / 1e9 if st.sweep_launches else None
+    traffic = None
+    if args.pmc_file and Path(args.pmc_file).exists():
+        traffic = json.loads(Path(args.pmc_file).read_text()).get("hbm_bytes_per_sweep_launch")
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_pods > 0:
+        cpu = cpu_baseline(args, kind, nodes, slots, pre, pods)
+
+    line = {
+        "metric": "pods scheduled/sec at 1M nodes (1/2/4/8 GPU) + % of HBM roofline",
+        "value": round(value, 1),
+        "unit": "pods/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "int64+f64",
+        "data": "synthetic (seeded kwok-shaped cluster and pod stream, libksynth)",
+        "config": {
+            "workload": f"C3: {args.nodes} {args.kind} nodes, prefill<{args.prefill:.0%} cpu, resource-only pods; "
+                        "Fit+LeastAllocated+BalancedAllocation+TaintToleration, pct=100, in-order commit",
+            "nodes": args.nodes,
+            "pods_per_step": args.batch,
+            "pods_per_round": args.pods_per_round,
+            "topk": args.topk or args.pods_per_round,
+            "parallelism": f"node-sharded x{world} (RCCL all-gather)" if world > 1 else "1 GPU",
+            "node_evals_per_pod": args.nodes,
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 1) if achieved else None,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+            "traffic": traffic,
+            "kernel": "ks::sweep_kernel",
+            "bytes_per_eval": B_NODE,
+            "evals_per_launch": int(evals_per_launch),
+            "avg_launch_ms": round(sweep_avg_ms, 4),
+        },
+        "cpu_baseline": cpu,
+        "extra": {
+            "rounds": int(st.rounds),
+            "pods_per_round_resolved": round(pods_timed / max(1, st.rounds), 2),
+            "resolve_ms_per_round": round(st.resolve_ms / max(1, st.resolve_launches), 4),
+            "sweep_ms_total": round(st.sweep_ms, 3),
+            "resolve_ms_total": round(st.resolve_ms, 3),
+            "scheduled_fraction": round(scheduled / pods_timed, 4),
+            "node_evals_per_s": round(value * args.nodes, 1),
+            "setup_s": round(setup_s, 2),
+        },
+    }
+    for b in batches:
+        sched.free(b)
+    sched.close()
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(args, kind, nodes, slots, pre, pods):
+    """The CPU oracle (oracle/oracle.cpp, C++ restatement of upstream v1.31.3) on
+    the same cluster, timed on a bounded pod sample, one host thread."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import pyoracle
+
+    o = pyoracle.Oracle(args.nodes)
+    o.upsert(nodes.nodes, slots, args.nodes)
+    if pre is not None:
+        o.add_pods(pre.pods, pre.slot_ptr, pre.n_pods)
+    n = args.cpu_pods
+    t0 = time.perf_counter()
+    o.schedule(pods.pods, n)
+    dt = time.perf_counter() - t0
+    o.close()
+    return {"value": round(n / dt, 2), "unit": "pods/s", "cores": 1, "kind": "port",
+            "sample": f"first {n} pods of the stream on the same {args.nodes}-node prefilled cluster "
+                      f"({n * args.nodes:.2e} node evaluations, {dt:.1f} s), single thread"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,308 @@
+/*
+ * ksched.h — C ABI of the MI355X-native dist-scheduler shard core (libksched.so).
+ *
+ * This is the drop-in boundary for ONE path of bchess/k8s-1m: the dist-scheduler
+ * shard's Filter -> Score -> NormalizeScore -> select -> commit loop.  In the
+ * reference that loop is the forked kube-scheduler's `schedulePod` (upstream
+ * k8s.io/kubernetes v1.31.3 pkg/scheduler/schedule_one.go), reached from
+ *   dist-scheduler/cmd/dist-scheduler/scheduler.go:543   (ScheduleOne goroutine)
+ * and its result is consumed by
+ *   dist-scheduler/pkg/distpermit/distpermit.go:51-72    (NodePluginScoresState -> TotalScore)
+ *   dist-scheduler/pkg/distpermit/distpermit.go:81-121   (SendScore, int32 score, 0 = no candidate)
+ *   dist-scheduler/cmd/dist-scheduler/scheduler.go:372-401 (podScheduleFailure: FitError path)
+ * A Go shim overrides the upstream `Scheduler.SchedulePod` function field next to
+ * the `NextPod` / `FailureHandler` overrides the reference already installs
+ * (scheduler.go:307-321) and calls these entry points through cgo; see
+ * INTEGRATION.md for the binding.
+ *
+ * Conventions
+ *  - Every entry point returns ks_status (0 = KS_OK).  No C++ exception crosses
+ *    the ABI; the last error text of a context is available via ks_last_error().
+ *  - All buffers are caller-owned.  Pointers passed in are only read during the
+ *    call; nothing is retained.  No callbacks.
+ *  - One ks_ctx per GPU.  Calls on one context must be externally serialised.
+ *  - Resource quantities are integers in canonical units: CPU in millicores
+ *    (Quantity.MilliValue()), memory in bytes (Quantity.Value()).
+ *  - Node identity is a caller-chosen slot index in [0, node_capacity); the
+ *    node index is also the deterministic tie-break key (lowest index wins).
+ */
+#ifndef KSCHED_H
+#define KSCHED_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KSCHED_ABI_VERSION 1
+
+/* ---------------------------------------------------------------- status */
+typedef int32_t ks_status;
+enum {
+  KS_OK = 0,
+  KS_ERR_INVALID = 1,     /* bad argument / malformed object                 */
+  KS_ERR_DEVICE = 2,      /* HIP runtime error (no device, launch failure)   */
+  KS_ERR_CAPACITY = 3,    /* dictionary / slot capacity exhausted            */
+  KS_ERR_UNSUPPORTED = 4, /* feature outside the implemented plugin subset   */
+  KS_ERR_RANGE = 5,       /* value outside the exact-arithmetic range        */
+  KS_ERR_NOT_FOUND = 6,   /* unknown node slot                               */
+  KS_ERR_COMM = 7,        /* RCCL error                                      */
+  KS_ERR_STALE = 8        /* batch compiled against an older node dictionary */
+};
+
+/* ------------------------------------------------------- k8s-shaped input */
+/* Mirrors k8s.io/api/core/v1 types restricted to the fields the path reads. */
+
+typedef struct {
+  const char *key;
+  const char *value;
+} ks_label;
+
+/* v1.TaintEffect */
+enum {
+  KS_EFFECT_ALL = 0, /* "" (only meaningful on a toleration: matches every effect) */
+  KS_EFFECT_NO_SCHEDULE = 1,
+  KS_EFFECT_PREFER_NO_SCHEDULE = 2,
+  KS_EFFECT_NO_EXECUTE = 3
+};
+
+typedef struct {
+  const char *key;
+  const char *value;
+  int32_t effect; /* KS_EFFECT_* (never KS_EFFECT_ALL on a taint) */
+  int32_t _pad;
+} ks_taint;
+
+/* v1.TolerationOperator */
+enum { KS_TOL_EQUAL = 0 /* "" or "Equal" */, KS_TOL_EXISTS = 1, KS_TOL_INVALID = 2 };
+
+typedef struct {
+  const char *key;   /* "" / NULL = any key (only valid with Exists)  */
+  const char *value; /* NULL treated as ""                             */
+  int32_t op;        /* KS_TOL_*                                       */
+  int32_t effect;    /* KS_EFFECT_* ; KS_EFFECT_ALL = "" (all effects) */
+} ks_toleration;
+
+/* v1.Node (name, labels, spec.taints, spec.unschedulable, status.allocatable) */
+typedef struct {
+  const char *name;
+  int64_t alloc_milli_cpu;
+  int64_t alloc_memory;
+  int64_t alloc_pods;
+  const ks_label *labels;
+  const ks_taint *taints;
+  uint32_t n_labels;
+  uint32_t n_taints;
+  uint32_t unschedulable;
+  uint32_t _pad;
+} ks_node;
+
+/* One container's resources.requests.  A resource that is ABSENT from the
+ * requests map is distinguished from an explicit 0 (upstream
+ * resourcehelper.PodRequests NonMissingContainerRequests semantics). */
+enum { KS_REQ_HAS_CPU = 1u, KS_REQ_HAS_MEMORY = 2u, KS_REQ_HAS_OTHER = 4u };
+typedef struct {
+  int64_t milli_cpu;
+  int64_t memory;
+  uint32_t flags;          /* KS_REQ_* presence bits; HAS_OTHER = any other resource (unsupported) */
+  uint32_t restart_always; /* init containers only: restartPolicy: Always (sidecar) */
+} ks_container;
+
+/* v1.NodeSelectorOperator */
+enum {
+  KS_OP_IN = 0,
+  KS_OP_NOT_IN = 1,
+  KS_OP_EXISTS = 2,
+  KS_OP_DOES_NOT_EXIST = 3,
+  KS_OP_GT = 4,
+  KS_OP_LT = 5,
+  KS_OP_INVALID = 6
+};
+
+typedef struct {
+  const char *key;
+  const char *const *values;
+  uint32_t n_values;
+  int32_t op; /* KS_OP_* */
+} ks_requirement;
+
+typedef struct {
+  const ks_requirement *match_expressions;
+  const ks_requirement *match_fields;
+  uint32_t n_expressions;
+  uint32_t n_fields;
+} ks_term;
+
+typedef struct {
+  ks_term preference;
+  int32_t weight;
+  int32_t _pad;
+} ks_preferred_term;
+
+/* v1.Pod restricted to scheduling-relevant fields. */
+typedef struct {
+  const char *ns;
+  const char *name;
+  const ks_container *containers;
+  const ks_container *init_containers;
+  const ks_toleration *tolerations;
+  const ks_label *node_selector;          /* spec.nodeSelector                     */
+  const ks_term *required_terms;          /* requiredDuringScheduling...NodeSelectorTerms */
+  const ks_preferred_term *preferred;     /* preferredDuringScheduling...          */
+  const char *node_name;                  /* spec.nodeName (NULL/"" = unset)       */
+  int64_t overhead_milli_cpu;             /* spec.overhead (if has_overhead)       */
+  int64_t overhead_memory;
+  uint32_t n_containers;
+  uint32_t n_init_containers;
+  uint32_t n_tolerations;
+  uint32_t n_node_selector;
+  uint32_t n_required_terms;
+  uint32_t has_required;  /* RequiredDuringSchedulingIgnoredDuringExecution != nil */
+  uint32_t n_preferred;
+  uint32_t has_preferred; /* PreferredDuringSchedulingIgnoredDuringExecution != nil */
+  uint32_t has_overhead;
+  uint32_t _pad;
+} ks_pod;
+
+/* ------------------------------------------------------------- outputs */
+/* Filter plugins in default-profile order (v1.31 apis/config/v1 default plugins). */
+enum {
+  KS_PLUGIN_NODE_UNSCHEDULABLE = 0,
+  KS_PLUGIN_NODE_NAME = 1,
+  KS_PLUGIN_TAINT_TOLERATION = 2,
+  KS_PLUGIN_NODE_AFFINITY = 3,
+  KS_PLUGIN_NODE_RESOURCES_FIT = 4,
+  KS_NUM_FILTER_PLUGINS = 5
+};
+
+enum {
+  KS_POD_SCHEDULED = 0,     /* node_index valid                                  */
+  KS_POD_UNSCHEDULABLE = 1, /* FitError: no feasible node; fail_counts = Diagnosis */
+  KS_POD_ERROR = 2          /* framework Error status (e.g. preferred-term parse error) */
+};
+
+enum { KS_RESULT_SINGLE_FEASIBLE = 1u /* upstream returns without scoring */ };
+
+/* ScheduleResult{SuggestedHost, EvaluatedNodes, FeasibleNodes} or FitError. */
+typedef struct {
+  int32_t node_index;     /* chosen node slot, -1 if none                        */
+  int32_t status;         /* KS_POD_*                                            */
+  int64_t total_score;    /* TotalScore of the chosen node (NodePluginScores)    */
+  uint32_t feasible_nodes;
+  uint32_t evaluated_nodes;
+  uint32_t fail_counts[KS_NUM_FILTER_PLUGINS]; /* nodes rejected first by each filter plugin */
+  uint32_t flags;         /* KS_RESULT_*                                         */
+} ks_result;
+
+/* Per-node plugin scores of one pod (parity dump; NodePluginScores analogue). */
+typedef struct {
+  int32_t status;        /* -1 feasible, else KS_PLUGIN_* of the first failing filter, -2 empty slot */
+  int32_t least_allocated;      /* NodeResourcesFit (LeastAllocated)     */
+  int32_t balanced_allocation;  /* NodeResourcesBalancedAllocation       */
+  int32_t taint_raw;            /* TaintToleration raw (before normalize) */
+  int32_t taint_score;          /* TaintToleration normalized            */
+  int32_t affinity_raw;         /* NodeAffinity raw                      */
+  int32_t affinity_score;       /* NodeAffinity normalized               */
+  int32_t image_locality;       /* ImageLocality (0: nodes report no images) */
+  int64_t total_score;          /* Σ weight × score over non-skipped plugins */
+} ks_node_score;
+
+/* Node resource state (NodeInfo.Requested / NonZeroRequested / len(Pods)). */
+typedef struct {
+  int64_t alloc_milli_cpu, alloc_memory;
+  int64_t req_milli_cpu, req_memory;
+  int64_t nonzero_milli_cpu, nonzero_memory;
+  int32_t alloc_pods;
+  int32_t pod_count; /* -1 for an empty slot */
+} ks_node_state;
+
+/* ------------------------------------------------------------- context */
+typedef struct {
+  int32_t device;            /* HIP device ordinal                               */
+  uint32_t node_capacity;    /* node slots (index space)                         */
+  uint32_t pods_per_round;   /* P: pods evaluated per sweep (0 = default 256)    */
+  uint32_t topk;             /* K: candidates kept per pod (0 = P)               */
+  uint32_t nodes_per_lane;   /* nodes held per GPU lane in the sweep (0 = 8)     */
+  uint32_t world_size;       /* GPUs sharding the node index space (1 = no RCCL) */
+  uint32_t rank;             /* this GPU's shard                                 */
+  uint32_t virtual_shards;   /* >1: emulate that many shards on this one device  */
+  /* Score plugin weights (default profile: 1, 1, 3, 2, 1). */
+  int32_t weight_fit;        /* NodeResourcesFit                                */
+  int32_t weight_balanced;   /* NodeResourcesBalancedAllocation                 */
+  int32_t weight_taint;      /* TaintToleration                                 */
+  int32_t weight_affinity;   /* NodeAffinity                                    */
+  int32_t weight_image;      /* ImageLocality                                   */
+  uint32_t _pad;
+} ks_config;
+
+typedef struct ks_ctx ks_ctx;
+typedef struct ks_batch ks_batch;
+
+/* Fill *cfg with the default-profile configuration. */
+void ks_config_default(ks_config *cfg);
+
+/* Scheduler construction (replaces scheduler.NewN's per-shard NodeInfo cache,
+ * dist-scheduler/cmd/dist-scheduler/scheduler.go:281-300). */
+ks_status ks_open(const ks_config *cfg, ks_ctx **out);
+void ks_close(ks_ctx *ctx);
+const char *ks_last_error(const ks_ctx *ctx);
+int32_t ks_abi_version(void);
+
+/* Node cache events (filtered node informer, scheduler.go:200-219 ->
+ * upstream internal/cache AddNode/UpdateNode/RemoveNode).  Upsert of an
+ * existing slot keeps its Requested/NonZeroRequested/pod count. */
+ks_status ks_nodes_upsert(ks_ctx *ctx, const ks_node *nodes, const uint32_t *slots, uint32_t n);
+ks_status ks_nodes_delete(ks_ctx *ctx, const uint32_t *slots, uint32_t n);
+
+/* Pod cache events: NodeInfo.AddPod (bind / assume) and RemovePod (delete). */
+ks_status ks_pods_add(ks_ctx *ctx, const ks_pod *pods, const uint32_t *slots, uint32_t n);
+ks_status ks_pods_remove(ks_ctx *ctx, const ks_pod *pods, const uint32_t *slots, uint32_t n);
+
+/* schedulePod for a stream of pods, in order: each pod is scheduled against
+ * the cache as left by the previous one (AssumePod commit), exactly as
+ * sequential ScheduleOne calls.  out[i] receives pod i's result. */
+ks_status ks_schedule(ks_ctx *ctx, const ks_pod *pods, uint32_t n, ks_result *out);
+
+/* Split form of ks_schedule: compile + upload once (prepare), then run with
+ * all inputs resident in HBM (the timed hot path), then fetch results. */
+ks_status ks_batch_prepare(ks_ctx *ctx, const ks_pod *pods, uint32_t n, ks_batch **out);
+ks_status ks_batch_run(ks_ctx *ctx, ks_batch *batch);
+ks_status ks_batch_results(ks_ctx *ctx, const ks_batch *batch, ks_result *out);
+void ks_batch_free(ks_ctx *ctx, ks_batch *batch);
+
+/* Per-plugin scores of `pod` on every node slot against the current cache
+ * (out has node_capacity entries).  Parity dump of NodePluginScores. */
+ks_status ks_plugin_scores(ks_ctx *ctx, const ks_pod *pod, ks_node_score *out);
+
+/* Read back node resource state. */
+ks_status ks_node_states(ks_ctx *ctx, const uint32_t *slots, uint32_t n, ks_node_state *out);
+
+/* Cross-GPU candidate gather over RCCL (replaces CollectScore fan-in,
+ * dist-scheduler/cmd/dist-scheduler/grpc_server.go:116-127 and
+ * pkg/scoreevaluator/scoreevaluator.go:45-126, for co-located shards). */
+#define KS_COMM_ID_BYTES 128
+ks_status ks_comm_unique_id(uint8_t out[KS_COMM_ID_BYTES]);
+ks_status ks_comm_init(ks_ctx *ctx, const uint8_t id[KS_COMM_ID_BYTES]);
+
+/* Counters for measurement. */
+typedef struct {
+  uint64_t rounds;          /* sweep rounds issued                         */
+  uint64_t pods_resolved;
+  uint64_t pods_scheduled;
+  uint64_t sweep_launches;  /* launches of the sweep kernel (timed)        */
+  double sweep_ms;          /* Σ device time of sweep launches (HIP events) */
+  uint64_t sweep_evals;     /* Σ (pod, node) evaluations by timed sweeps   */
+  double resolve_ms;        /* Σ device time of resolve launches           */
+  uint64_t resolve_launches;
+} ks_stats;
+ks_status ks_get_stats(ks_ctx *ctx, ks_stats *out);
+ks_status ks_reset_stats(ks_ctx *ctx);
+/* 1 = time every sweep/resolve launch with HIP events (adds syncs), 0 = off. */
+ks_status ks_set_timing(ks_ctx *ctx, int32_t enabled);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* KSCHED_H */

@@ -1,0 +1,148 @@
+// ksched_dev.hpp — device-resident formats of the shard hot path (shared by
+// the HIP kernels and the host encoder).  Layout rationale: DESIGN.md §3.
+#pragma once
+
+#include <stdint.h>
+
+namespace ks {
+
+// ------------------------------------------------------------------ limits
+constexpr int LW = 4;           // label bitset words per node (256 dictionary bits)
+constexpr int NNUM = 2;         // numeric label columns (Gt / Lt operands)
+constexpr int NFILT = 5;        // filter plugins (KS_PLUGIN_*)
+constexpr int WAVE = 64;
+constexpr int SWEEP_THREADS = 256;
+constexpr int BLOCK_KEYS = 4;   // candidates kept per sweep block and pod
+constexpr int MAX_SHARDS = 16;
+constexpr int MERGE_CAP = 4096; // candidates sorted per pod by the merge kernel
+constexpr uint64_t UNSCHED_BIT = 1ull << 63;  // hard-taint word: spec.unschedulable pseudo-taint
+
+// Filter status codes (first failing plugin); FEASIBLE = passed every filter.
+constexpr int ST_FEASIBLE = -1;
+constexpr int ST_EMPTY = -2;
+
+// ---------------------------------------------------------- node table (SoA)
+// Columns are indexed by POSITION, not slot: a shard's slots are permuted so
+// that (wave, lane, step) of the sweep read consecutive positions (coalesced)
+// while consecutive slots land in different waves (long candidate prefixes).
+struct NodeTable {
+  int64_t *acpu, *amem;   // Allocatable
+  int64_t *rcpu, *rmem;   // Requested
+  int64_t *zcpu, *zmem;   // NonZeroRequested
+  int32_t *apods;         // Allocatable pods; < 0 marks an empty slot
+  int32_t *npods;         // len(NodeInfo.Pods)
+  uint64_t *hard;         // untolerable-effect taint bits (+ UNSCHED_BIT)
+  uint64_t *prefer;       // PreferNoSchedule taint bits
+  uint64_t *lab;          // [LW][npos] label-pair / key-present / numeric-valid bits
+  int64_t *num;           // [NNUM][npos] parsed numeric label values
+  uint32_t npos;          // positions per column
+  uint32_t lw;            // label words in use (0..LW)
+};
+
+// Shard geometry.  Local index l = slot - lo; wave w = l % W;
+// lane t = (l / W) % 64; step j = l / (64 W); pos = base + w*64*npl + j*64 + t.
+struct Shard {
+  uint32_t lo, count;   // slot range [lo, lo + count)
+  uint32_t waves;       // W (multiple of 4)
+  uint32_t base;        // first position
+};
+
+__host__ __device__ inline uint32_t shard_pos(const Shard &s, uint32_t npl, uint32_t l) {
+  const uint32_t w = l % s.waves;
+  const uint32_t t = (l / s.waves) % WAVE;
+  const uint32_t j = l / (s.waves * WAVE);
+  return s.base + w * WAVE * npl + j * WAVE + t;
+}
+
+// ----------------------------------------------------------------- pods
+enum PodFlags : uint32_t {
+  PF_HAS_REQ = 1u,    // Fit checks cpu/memory (some request is non-zero)
+  PF_EXT = 2u,        // needs taint / label / name columns
+  PF_TT = 4u,         // TaintToleration raw score may be non-zero (normalisation active)
+  PF_NA = 8u,         // NodeAffinity preferred terms parsed (normalisation active)
+  PF_HAS_PREF = 16u,  // preferredDuringScheduling != nil (NodeAffinity not skipped)
+  PF_PREF_ERR = 32u,  // preferred terms failed to parse: PreScore error with >= 2 feasible
+  PF_AFF = 64u,       // required program present (nodeSelector and/or required terms)
+};
+
+struct alignas(16) PodDev {
+  int64_t req_cpu, req_mem;  // PodRequests (Fit filter, BalancedAllocation)
+  int64_t nz_cpu, nz_mem;    // PodRequests with non-missing defaults (LeastAllocated)
+  uint64_t tol_hard;         // hard-taint bits tolerated (+ UNSCHED_BIT)
+  uint64_t tol_prefer;       // prefer-taint bits tolerated by "" / PreferNoSchedule tolerations
+  uint32_t flags;
+  int32_t name_slot;         // spec.nodeName: -1 unset, -2 names no node, else slot
+  uint32_t req_off, req_len; // required program (clauses) in the clause buffer
+  uint32_t pref_off, pref_len;
+  uint32_t n_req_terms;      // OR terms after the mandatory nodeSelector group
+  uint32_t _pad[5];
+};
+static_assert(sizeof(PodDev) == 96, "PodDev layout");
+
+// A clause is one label-selector requirement, 6 x u64:
+//   w0 = kind | num_col << 8 | term << 16 | (uint64)weight << 32
+//   w1..w4 = LW mask words (ANY / NONE: the pair / key bits; GT / LT: the
+//            key's numeric-valid bit), w5 = GT / LT operand or NAME_* slot.
+// term 0 = nodeSelector (AND); terms >= 1 = required terms (OR of ANDs) or,
+// in the preferred program, preferred terms (sum of weights of matching terms).
+enum ClauseKind : uint32_t {
+  CK_ANY = 0,     // In / Exists: any mask bit present
+  CK_NONE = 1,    // NotIn / DoesNotExist: no mask bit present
+  CK_GT = 2,      // numeric label > value
+  CK_LT = 3,      // numeric label < value
+  CK_NAME_EQ = 4, // metadata.name In  (w5 = slot, or -1 = no such node)
+  CK_NAME_NE = 5, // metadata.name NotIn
+  CK_FALSE = 6,   // term with parse errors: never matches
+};
+constexpr int CLAUSE_WORDS = 6;
+
+// ----------------------------------------------------------- round records
+// Per (pod-in-round, sweep block): best keys of the block + bound + counts.
+struct alignas(16) BlockRec {
+  uint64_t keys[BLOCK_KEYS];  // descending; 0 = none
+  uint64_t bound;             // every feasible node of the block not listed has key <= bound
+  uint32_t feasible;
+  uint32_t fails[NFILT];
+  uint32_t tt_cnt, na_cnt;    // feasible nodes whose raw normalising score equals the max
+};
+static_assert(sizeof(BlockRec) == 80, "BlockRec layout");
+
+// Per (pod-in-round, shard): sorted candidate prefix.  Stored as a fixed
+// header followed by K keys (stride rec_words(K) u64).
+struct alignas(16) ShardRecHdr {
+  uint64_t bound;
+  uint32_t nkeys;
+  uint32_t feasible;
+  uint32_t fails[NFILT];
+  uint32_t tt_cnt, na_cnt;
+  uint32_t _pad;
+};
+static_assert(sizeof(ShardRecHdr) == 48, "ShardRecHdr layout");
+constexpr uint32_t REC_HDR_WORDS = 6;
+__host__ __device__ inline uint32_t rec_words(uint32_t k) { return REC_HDR_WORDS + k; }
+
+// Normalising-plugin maxima over feasible nodes: (max raw, #feasible at max).
+struct alignas(16) NormRec {
+  int64_t tt_max, na_max;
+  uint32_t tt_cnt, na_cnt;
+  uint32_t _pad[2];
+};
+static_assert(sizeof(NormRec) == 32, "NormRec layout");
+
+// Device copy of ks_result (identical layout).
+struct DevResult {
+  int32_t node_index;
+  int32_t status;
+  int64_t total_score;
+  uint32_t feasible_nodes;
+  uint32_t evaluated_nodes;
+  uint32_t fail_counts[NFILT];
+  uint32_t flags;
+};
+static_assert(sizeof(DevResult) == 48, "DevResult layout");
+
+struct Weights {
+  int32_t fit, ba, tt, na, il;
+};
+
+}  // namespace ks

@@ -1,0 +1,1258 @@
+// ksched_host.cpp — libksched C ABI (include/ksched.h): node cache encoder,
+// pod compiler, device-driven scheduling rounds, RCCL candidate gather.
+//
+// The encoder turns k8s-shaped nodes into the SoA node table of
+// ksched_dev.hpp (labels / taints as dictionary bitsets), and k8s-shaped pods
+// into PodDev descriptors + label-selector clauses.  Upstream semantics it
+// restates (k8s.io/kubernetes v1.31.3 unless noted):
+//   pkg/api/v1/resource/helpers.go#PodRequests           (pod requests, A2)
+//   framework/types.go#calculateResource                  (AddPod / RemovePod)
+//   k8s.io/api core/v1/toleration.go#ToleratesTaint       (taint masks, A8)
+//   component-helpers nodeaffinity.go#newNodeSelectorTerm (clauses, A9/A15)
+//   apimachinery labels.NewRequirement validation         (parse errors)
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "ksched.h"
+#include "ksched_dev.hpp"
+#include "ksched_kernels.hpp"
+
+using namespace ks;
+
+namespace {
+
+constexpr int64_t kDefaultMilliCPURequest = 100;             // schedutil.DefaultMilliCPURequest
+constexpr int64_t kDefaultMemoryRequest = 200ll * 1024 * 1024;  // schedutil.DefaultMemoryRequest
+constexpr int64_t kMaxExact = 1ll << 46;  // alloc bound for exact binary64 LeastAllocated
+
+std::string str(const char *p) { return p ? std::string(p) : std::string(); }
+
+// ------------------------------------------------- apimachinery validation
+// Character classes of qualifiedNameFmt / labelValueFmt / DNS-1123 subdomain.
+enum : uint8_t { C_ALNUM = 1, C_LOWER_ALNUM = 2, C_DASH = 4, C_UNDERSCORE_DOT = 8 };
+struct CharTable {
+  uint8_t c[256] = {};
+  CharTable() {
+    for (int i = 'a'; i <= 'z'; ++i) c[i] = C_ALNUM | C_LOWER_ALNUM;
+    for (int i = 'A'; i <= 'Z'; ++i) c[i] = C_ALNUM;
+    for (int i = '0'; i <= '9'; ++i) c[i] = C_ALNUM | C_LOWER_ALNUM;
+    c[(int)'-'] = C_DASH;
+    c[(int)'_'] = C_UNDERSCORE_DOT;
+    c[(int)'.'] = C_UNDERSCORE_DOT;
+  }
+};
+const CharTable kChars;
+inline uint8_t cls(char ch) { return kChars.c[(uint8_t)ch]; }
+
+// "([A-Za-z0-9][-A-Za-z0-9_.]*)?[A-Za-z0-9]", non-empty
+bool name_part_ok(const std::string &s) {
+  if (s.empty() || !(cls(s.front()) & C_ALNUM) || !(cls(s.back()) & C_ALNUM)) return false;
+  return std::all_of(s.begin(), s.end(), [](char ch) { return cls(ch) != 0; });
+}
+
+bool dns1123_subdomain_ok(const std::string &s) {
+  if (s.empty() || s.size() > 253) return false;
+  size_t b = 0;
+  for (;;) {
+    const size_t e = s.find('.', b);
+    const size_t len = (e == std::string::npos ? s.size() : e) - b;
+    if (len == 0) return false;
+    if (!(cls(s[b]) & C_LOWER_ALNUM) || !(cls(s[b + len - 1]) & C_LOWER_ALNUM)) return false;
+    for (size_t i = b; i < b + len; ++i)
+      if (!(cls(s[i]) & (C_LOWER_ALNUM | C_DASH))) return false;
+    if (e == std::string::npos) return true;
+    b = e + 1;
+  }
+}
+
+bool qualified_name_ok(const std::string &k) {  // validation.IsQualifiedName
+  const size_t slash = k.find('/');
+  if (slash == std::string::npos) return k.size() <= 63 && name_part_ok(k);
+  if (k.find('/', slash + 1) != std::string::npos) return false;
+  const std::string prefix = k.substr(0, slash), name = k.substr(slash + 1);
+  return dns1123_subdomain_ok(prefix) && name.size() <= 63 && name_part_ok(name);
+}
+
+bool label_value_ok(const std::string &v) {  // validation.IsValidLabelValue
+  return v.size() <= 63 && (v.empty() || name_part_ok(v));
+}
+
+bool parse_int64(const std::string &s, int64_t *out) {  // strconv.ParseInt(s, 10, 64)
+  size_t i = 0;
+  bool neg = false;
+  if (!s.empty() && (s[0] == '+' || s[0] == '-')) { neg = s[0] == '-'; i = 1; }
+  if (i == s.size()) return false;
+  uint64_t v = 0;
+  const uint64_t lim = neg ? (1ull << 63) : (uint64_t)INT64_MAX;
+  for (; i < s.size(); ++i) {
+    const unsigned d = (unsigned)(s[i] - '0');
+    if (d > 9) return false;
+    if (v > (lim - d) / 10) return false;
+    v = v * 10 + d;
+  }
+  *out = neg ? (int64_t)(0 - v) : (int64_t)v;
+  return true;
+}
+
+// ------------------------------------------------------------ host types
+
+struct Tol {
+  uint32_t key;  // string id; 0 = ""
+  uint32_t value;
+  int32_t op, effect;
+};
+
+struct HostNode {
+  bool present = false;
+  uint32_t name = 0;
+  int64_t acpu = 0, amem = 0, apods = 0;
+  bool unschedulable = false;
+  std::vector<std::pair<uint32_t, uint32_t>> labels;  // (key id, value id)
+  uint64_t hard = 0, prefer = 0;
+  uint64_t lab[LW] = {};
+  int64_t num[NNUM] = {};
+};
+
+struct TaintKey {
+  uint32_t key, value;
+  int32_t effect;
+  bool operator<(const TaintKey &o) const {
+    return std::tie(key, value, effect) < std::tie(o.key, o.value, o.effect);
+  }
+};
+
+struct NumCol {
+  uint32_t col;
+  uint32_t valid_bit;
+};
+
+}  // namespace
+
+// ================================================================= context
+
+struct ks_batch {
+  uint32_t n = 0;
+  uint32_t dict_version = 0;
+  bool ext = false, norm = false;
+  PodDev *d_pods = nullptr;
+  uint64_t *d_clauses = nullptr;
+  DevResult *d_results = nullptr;
+  std::vector<ks_result> host_status;  // compile-time errors (none so far)
+};
+
+struct ks_ctx {
+  ks_config cfg{};
+  std::string err;
+  hipStream_t stream = nullptr;
+  // geometry
+  uint32_t cap = 0, S = 1, npl = 8, P = 256, K = 256;
+  std::vector<Shard> shards;
+  uint32_t npos = 0;
+  std::vector<uint32_t> slot_pos;
+  // device state
+  NodeTable t{};
+  Shard *d_shards = nullptr;
+  uint32_t *d_slot_pos = nullptr;
+  uint32_t *d_start = nullptr;
+  uint32_t *h_start = nullptr;  // pinned
+  uint32_t *d_norm = nullptr;
+  BlockRec *d_brec = nullptr;
+  size_t brec_bytes = 0;
+  uint64_t *d_srec = nullptr, *d_frec = nullptr;
+  uint64_t *d_counters = nullptr;
+  // host mirror / dictionaries
+  std::vector<HostNode> nodes;
+  uint32_t n_present = 0;
+  std::unordered_map<std::string, uint32_t> str_ids{{"", 0}};
+  std::vector<std::string> strs{""};
+  std::unordered_map<uint32_t, uint32_t> name_slot;  // name id -> slot
+  std::map<TaintKey, uint32_t> hard_dict;             // NoSchedule / NoExecute taints
+  std::vector<TaintKey> hard_list;
+  std::map<std::pair<uint32_t, uint32_t>, uint32_t> prefer_dict;
+  std::vector<std::pair<uint32_t, uint32_t>> prefer_list;
+  uint64_t hard_in_use = 0, prefer_in_use = 0;
+  std::map<std::pair<uint32_t, uint32_t>, uint32_t> pair_bit;
+  std::unordered_map<uint32_t, uint32_t> key_bit;
+  std::unordered_map<uint32_t, NumCol> num_col;
+  uint32_t next_bit = 0, next_num = 0;
+  std::unordered_map<uint32_t, std::vector<uint32_t>> key_nodes;  // key id -> slots having it
+  uint32_t dict_version = 1;
+  std::vector<uint32_t> dirty_ext;
+  // comm
+  ncclComm_t comm = nullptr;
+  // stats
+  ks_stats stats{};
+  bool timing = false;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_sweep, ev_resolve;
+  std::vector<hipEvent_t> ev_pool;
+  uint64_t pending_sweep_evals = 0;
+
+  uint32_t intern(const char *p) {
+    std::string s = str(p);
+    auto it = str_ids.find(s);
+    if (it != str_ids.end()) return it->second;
+    const uint32_t id = (uint32_t)strs.size();
+    strs.push_back(s);
+    str_ids.emplace(std::move(s), id);
+    return id;
+  }
+  int32_t lookup(const char *p) const {
+    auto it = str_ids.find(str(p));
+    return it == str_ids.end() ? -1 : (int32_t)it->second;
+  }
+  ks_status fail(ks_status st, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    std::vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    err = buf;
+    return st;
+  }
+};
+
+#define HIPC(ctx, x)                                                                           \
+  do {                                                                                         \
+    hipError_t e_ = (x);                                                                       \
+    if (e_ != hipSuccess)                                                                      \
+      return (ctx)->fail(KS_ERR_DEVICE, "%s: %s (%s:%d)", #x, hipGetErrorString(e_), __FILE__, \
+                         __LINE__);                                                            \
+  } while (0)
+
+#define NCCLC(ctx, x)                                                                                  \
+  do {                                                                                                 \
+    ncclResult_t r_ = (x);                                                                             \
+    if (r_ != ncclSuccess) return (ctx)->fail(KS_ERR_COMM, "%s: %s", #x, ncclGetErrorString(r_)); \
+  } while (0)
+
+namespace {
+
+// --------------------------------------------------------- label encoding
+
+void node_ext_bits(ks_ctx *c, HostNode &n) {
+  uint64_t lab[LW] = {};
+  int64_t num[NNUM] = {};
+  for (auto &kv : n.labels) {
+    auto pb = c->pair_bit.find(kv);
+    if (pb != c->pair_bit.end()) lab[pb->second >> 6] |= 1ull << (pb->second & 63);
+    auto kb = c->key_bit.find(kv.first);
+    if (kb != c->key_bit.end()) lab[kb->second >> 6] |= 1ull << (kb->second & 63);
+    auto nc = c->num_col.find(kv.first);
+    if (nc != c->num_col.end()) {
+      int64_t v;
+      if (parse_int64(c->strs[kv.second], &v)) {
+        lab[nc->second.valid_bit >> 6] |= 1ull << (nc->second.valid_bit & 63);
+        num[nc->second.col] = v;
+      }
+    }
+  }
+  std::memcpy(n.lab, lab, sizeof lab);
+  std::memcpy(n.num, num, sizeof num);
+}
+
+ks_status alloc_bit(ks_ctx *c, uint32_t *bit) {
+  if (c->next_bit >= (uint32_t)LW * 64) return c->fail(KS_ERR_CAPACITY, "label dictionary full (%d bits)", LW * 64);
+  *bit = c->next_bit++;
+  c->t.lw = std::max(c->t.lw, (*bit >> 6) + 1);
+  return KS_OK;
+}
+
+void mark_key_nodes_dirty(ks_ctx *c, uint32_t key) {
+  auto it = c->key_nodes.find(key);
+  if (it == c->key_nodes.end()) return;
+  for (uint32_t s : it->second) {
+    if (!c->nodes[s].present) continue;
+    node_ext_bits(c, c->nodes[s]);
+    c->dirty_ext.push_back(s);
+  }
+}
+
+ks_status get_pair_bit(ks_ctx *c, uint32_t key, uint32_t value, uint32_t *bit) {
+  auto it = c->pair_bit.find({key, value});
+  if (it != c->pair_bit.end()) { *bit = it->second; return KS_OK; }
+  ks_status st = alloc_bit(c, bit);
+  if (st) return st;
+  c->pair_bit.emplace(std::make_pair(key, value), *bit);
+  mark_key_nodes_dirty(c, key);
+  return KS_OK;
+}
+
+ks_status get_key_bit(ks_ctx *c, uint32_t key, uint32_t *bit) {
+  auto it = c->key_bit.find(key);
+  if (it != c->key_bit.end()) { *bit = it->second; return KS_OK; }
+  ks_status st = alloc_bit(c, bit);
+  if (st) return st;
+  c->key_bit.emplace(key, *bit);
+  mark_key_nodes_dirty(c, key);
+  return KS_OK;
+}
+
+ks_status get_num_col(ks_ctx *c, uint32_t key, NumCol *out) {
+  auto it = c->num_col.find(key);
+  if (it != c->num_col.end()) { *out = it->second; return KS_OK; }
+  if (c->next_num >= (uint32_t)NNUM) return c->fail(KS_ERR_CAPACITY, "numeric label columns full (%d)", NNUM);
+  NumCol nc;
+  nc.col = c->next_num++;
+  ks_status st = alloc_bit(c, &nc.valid_bit);
+  if (st) return st;
+  c->num_col.emplace(key, nc);
+  mark_key_nodes_dirty(c, key);
+  *out = nc;
+  return KS_OK;
+}
+
+// ------------------------------------------------------------ pod compile
+
+bool tolerates(const ks_ctx *c, const std::vector<Tol> &tols, uint32_t key, uint32_t value, int32_t effect) {
+  for (auto &t : tols) {  // ToleratesTaint
+    if (t.effect != KS_EFFECT_ALL && t.effect != effect) continue;
+    if (t.key != 0 && t.key != key) continue;
+    if (t.op == KS_TOL_EXISTS) return true;
+    if (t.op == KS_TOL_EQUAL && t.value == value) return true;
+  }
+  return false;
+}
+
+// PodRequests (resourcehelper) for cpu / memory; non_missing applies the
+// scheduler's non-zero defaults to containers that omit a request.
+ks_status pod_requests(const ks_pod &p, bool non_missing, int64_t *cpu, int64_t *mem) {
+  auto req = [&](const ks_container &k, int64_t *a, int64_t *b) -> bool {
+    if (k.flags & KS_REQ_HAS_OTHER) return false;
+    *a = (k.flags & KS_REQ_HAS_CPU) ? k.milli_cpu : (non_missing ? kDefaultMilliCPURequest : 0);
+    *b = (k.flags & KS_REQ_HAS_MEMORY) ? k.memory : (non_missing ? kDefaultMemoryRequest : 0);
+    return true;
+  };
+  int64_t sum_c = 0, sum_m = 0;
+  for (uint32_t i = 0; i < p.n_containers; ++i) {
+    int64_t a, b;
+    if (!req(p.containers[i], &a, &b)) return KS_ERR_UNSUPPORTED;
+    sum_c += a;
+    sum_m += b;
+  }
+  // init containers: max over "sidecars so far + this init container"; sidecars also add to the sum
+  int64_t side_c = 0, side_m = 0, init_c = 0, init_m = 0;
+  for (uint32_t i = 0; i < p.n_init_containers; ++i) {
+    int64_t a, b;
+    if (!req(p.init_containers[i], &a, &b)) return KS_ERR_UNSUPPORTED;
+    int64_t use_c, use_m;
+    if (p.init_containers[i].restart_always) {
+      sum_c += a;
+      sum_m += b;
+      side_c += a;
+      side_m += b;
+      use_c = side_c;
+      use_m = side_m;
+    } else {
+      use_c = a + side_c;
+      use_m = b + side_m;
+    }
+    init_c = std::max(init_c, use_c);
+    init_m = std::max(init_m, use_m);
+  }
+  sum_c = std::max(sum_c, init_c);
+  sum_m = std::max(sum_m, init_m);
+  if (p.has_overhead) {
+    sum_c += p.overhead_milli_cpu;
+    sum_m += p.overhead_memory;
+  }
+  *cpu = sum_c;
+  *mem = sum_m;
+  return KS_OK;
+}
+
+struct ClauseBuf {
+  std::vector<uint64_t> w;
+  uint32_t count() const { return (uint32_t)(w.size() / CLAUSE_WORDS); }
+  void add(uint32_t kind, uint32_t term, int32_t weight, const uint64_t mask[LW], uint64_t operand,
+           uint32_t col = 0) {
+    w.push_back((uint64_t)kind | ((uint64_t)col << 8) | ((uint64_t)term << 16) | ((uint64_t)(uint32_t)weight << 32));
+    for (int k = 0; k < LW; ++k) w.push_back(mask ? mask[k] : 0);
+    w.push_back(operand);
+  }
+};
+
+inline void set_bit(uint64_t m[LW], uint32_t b) { m[b >> 6] |= 1ull << (b & 63); }
+
+// newNodeSelectorTerm -> clauses.  Returns false on a parse error (the term
+// then matches nothing in a required selector; a preferred term's PreScore
+// fails).  Capacity / unsupported errors propagate through *st.
+bool compile_term(ks_ctx *c, const ks_term &t, uint32_t term, int32_t weight, ClauseBuf &out, ks_status *st) {
+  ClauseBuf tmp;
+  bool ok = true;
+  for (uint32_t i = 0; i < t.n_expressions && ok; ++i) {
+    const ks_requirement &e = t.match_expressions[i];
+    const std::string key = str(e.key);
+    std::vector<std::string> vals;
+    for (uint32_t k = 0; k < e.n_values; ++k) vals.push_back(str(e.values[k]));
+    // labels.NewRequirement validation
+    switch (e.op) {
+      case KS_OP_IN:
+      case KS_OP_NOT_IN: ok = !vals.empty(); break;
+      case KS_OP_EXISTS:
+      case KS_OP_DOES_NOT_EXIST: ok = vals.empty(); break;
+      case KS_OP_GT:
+      case KS_OP_LT: {
+        int64_t x;
+        ok = vals.size() == 1 && parse_int64(vals[0], &x);
+        break;
+      }
+      default: ok = false;
+    }
+    for (auto &v : vals) ok = ok && label_value_ok(v);
+    ok = ok && qualified_name_ok(key);
+    if (!ok) break;
+    const uint32_t kid = c->intern(e.key);
+    uint64_t mask[LW] = {};
+    uint32_t bit;
+    switch (e.op) {
+      case KS_OP_IN:
+      case KS_OP_NOT_IN:
+        for (auto &v : vals) {
+          if ((*st = get_pair_bit(c, kid, c->intern(v.c_str()), &bit))) return false;
+          set_bit(mask, bit);
+        }
+        tmp.add(e.op == KS_OP_IN ? CK_ANY : CK_NONE, term, weight, mask, 0);
+        break;
+      case KS_OP_EXISTS:
+      case KS_OP_DOES_NOT_EXIST:
+        if ((*st = get_key_bit(c, kid, &bit))) return false;
+        set_bit(mask, bit);
+        tmp.add(e.op == KS_OP_EXISTS ? CK_ANY : CK_NONE, term, weight, mask, 0);
+        break;
+      default: {  // Gt / Lt
+        NumCol nc;
+        if ((*st = get_num_col(c, kid, &nc))) return false;
+        set_bit(mask, nc.valid_bit);
+        int64_t x = 0;
+        parse_int64(vals[0], &x);
+        tmp.add(e.op == KS_OP_GT ? CK_GT : CK_LT, term, weight, mask, (uint64_t)x, nc.col);
+      }
+    }
+  }
+  for (uint32_t i = 0; i < t.n_fields && ok; ++i) {  // nodeSelectorRequirementsAsFieldSelector
+    const ks_requirement &e = t.match_fields[i];
+    if (str(e.key) != "metadata.name" || e.n_values != 1 || (e.op != KS_OP_IN && e.op != KS_OP_NOT_IN)) {
+      ok = false;
+      break;
+    }
+    const int32_t nid = c->lookup(e.values[0]);
+    int64_t slot = -1;
+    if (nid >= 0) {
+      auto it = c->name_slot.find((uint32_t)nid);
+      if (it != c->name_slot.end()) slot = it->second;
+    }
+    tmp.add(e.op == KS_OP_IN ? CK_NAME_EQ : CK_NAME_NE, term, weight, nullptr, (uint64_t)slot);
+  }
+  if (!ok) return false;
+  out.w.insert(out.w.end(), tmp.w.begin(), tmp.w.end());
+  return true;
+}
+
+ks_status compile_pod(ks_ctx *c, const ks_pod &p, PodDev &d, ClauseBuf &cl) {
+  std::memset(&d, 0, sizeof d);
+  ks_status st;
+  if ((st = pod_requests(p, false, &d.req_cpu, &d.req_mem)) ||
+      (st = pod_requests(p, true, &d.nz_cpu, &d.nz_mem)))
+    return c->fail(st, "pod %s/%s requests a resource other than cpu/memory", str(p.ns).c_str(),
+                   str(p.name).c_str());
+  if (d.req_cpu < 0 || d.req_mem < 0 || d.req_cpu >= kMaxExact || d.req_mem >= kMaxExact)
+    return c->fail(KS_ERR_RANGE, "pod %s requests outside [0, 2^46)", str(p.name).c_str());
+  if (d.req_cpu != 0 || d.req_mem != 0) d.flags |= PF_HAS_REQ;
+  // tolerations -> dictionary masks
+  std::vector<Tol> tols, tols_prefer;
+  for (uint32_t i = 0; i < p.n_tolerations; ++i) {
+    const ks_toleration &t = p.tolerations[i];
+    const int32_t k = c->lookup(t.key), v = c->lookup(t.value);
+    // unseen strings can only match through wildcards: keep them as ids that match nothing
+    Tol x{k < 0 ? 0xFFFFFFFFu : (uint32_t)k, v < 0 ? 0xFFFFFFFFu : (uint32_t)v, t.op, t.effect};
+    if (str(t.key).empty()) x.key = 0;
+    if (str(t.value).empty()) x.value = 0;
+    tols.push_back(x);
+    if (t.effect == KS_EFFECT_ALL || t.effect == KS_EFFECT_PREFER_NO_SCHEDULE) tols_prefer.push_back(x);
+  }
+  for (size_t b = 0; b < c->hard_list.size(); ++b)
+    if (tolerates(c, tols, c->hard_list[b].key, c->hard_list[b].value, c->hard_list[b].effect))
+      d.tol_hard |= 1ull << b;
+  const int32_t uk = c->lookup("node.kubernetes.io/unschedulable");
+  if (tolerates(c, tols, uk < 0 ? 0xFFFFFFFEu : (uint32_t)uk, 0, KS_EFFECT_NO_SCHEDULE)) d.tol_hard |= UNSCHED_BIT;
+  for (size_t b = 0; b < c->prefer_list.size(); ++b)
+    if (tolerates(c, tols_prefer, c->prefer_list[b].first, c->prefer_list[b].second, KS_EFFECT_PREFER_NO_SCHEDULE))
+      d.tol_prefer |= 1ull << b;
+  if (c->prefer_in_use & ~d.tol_prefer) d.flags |= PF_TT;
+  // spec.nodeName
+  d.name_slot = -1;
+  if (p.node_name && p.node_name[0]) {
+    d.name_slot = -2;
+    const int32_t nid = c->lookup(p.node_name);
+    if (nid >= 0) {
+      auto it = c->name_slot.find((uint32_t)nid);
+      if (it != c->name_slot.end()) d.name_slot = (int32_t)it->second;
+    }
+  }
+  // required: nodeSelector (term 0) + RequiredDuringScheduling terms (1..)
+  d.req_off = cl.count();
+  for (uint32_t i = 0; i < p.n_node_selector; ++i) {
+    uint64_t mask[LW] = {};
+    uint32_t bit;
+    if ((st = get_pair_bit(c, c->intern(p.node_selector[i].key), c->intern(p.node_selector[i].value), &bit)))
+      return st;
+    set_bit(mask, bit);
+    cl.add(CK_ANY, 0, 0, mask, 0);
+  }
+  if (p.has_required) {
+    uint32_t nt = 0;
+    for (uint32_t i = 0; i < p.n_required_terms; ++i) {
+      const ks_term &t = p.required_terms[i];
+      if (t.n_expressions == 0 && t.n_fields == 0) continue;  // empty term selects nothing: skipped
+      ++nt;
+      st = KS_OK;
+      if (!compile_term(c, t, nt, 0, cl, &st)) {
+        if (st) return st;
+        cl.add(CK_FALSE, nt, 0, nullptr, 0);  // parse error: term never matches
+      }
+    }
+    if (nt == 0) {  // no usable term: nothing matches
+      cl.add(CK_FALSE, 1, 0, nullptr, 0);
+      nt = 1;
+    }
+    d.n_req_terms = nt;
+  }
+  d.req_len = cl.count() - d.req_off;
+  if (p.n_node_selector || p.has_required) d.flags |= PF_AFF;
+  // preferred terms
+  d.pref_off = cl.count();
+  if (p.has_preferred) {
+    d.flags |= PF_HAS_PREF;
+    uint32_t nt = 0;
+    for (uint32_t i = 0; i < p.n_preferred; ++i) {
+      const ks_preferred_term &t = p.preferred[i];
+      if (t.weight == 0 || (t.preference.n_expressions == 0 && t.preference.n_fields == 0)) continue;
+      if (t.weight < 0 || t.weight > 100)
+        return c->fail(KS_ERR_UNSUPPORTED, "preferred term weight %d outside 1..100", t.weight);
+      st = KS_OK;
+      const uint32_t mark = (uint32_t)cl.w.size();
+      if (!compile_term(c, t.preference, nt + 1, t.weight, cl, &st)) {
+        if (st) return st;
+        cl.w.resize(mark);
+        d.flags |= PF_PREF_ERR;
+        continue;
+      }
+      if (cl.w.size() == mark) cl.add(CK_ANY, nt + 1, t.weight, nullptr, 0);  // unreachable (non-empty)
+      ++nt;
+    }
+    if (nt) d.flags |= PF_NA;
+  }
+  d.pref_len = cl.count() - d.pref_off;
+  if ((c->hard_in_use & ~d.tol_hard) || d.name_slot != -1 || (d.flags & (PF_AFF | PF_TT | PF_NA)))
+    d.flags |= PF_EXT;
+  return KS_OK;
+}
+
+// --------------------------------------------------------------- devices
+
+ks_status upload_dirty_ext(ks_ctx *c) {
+  if (c->dirty_ext.empty()) return KS_OK;
+  std::sort(c->dirty_ext.begin(), c->dirty_ext.end());
+  c->dirty_ext.erase(std::unique(c->dirty_ext.begin(), c->dirty_ext.end()), c->dirty_ext.end());
+  const uint32_t n = (uint32_t)c->dirty_ext.size();
+  std::vector<uint32_t> pos(n);
+  std::vector<uint64_t> ext((size_t)n * (2 + LW + NNUM));
+  for (uint32_t i = 0; i < n; ++i) {
+    const HostNode &h = c->nodes[c->dirty_ext[i]];
+    pos[i] = c->slot_pos[c->dirty_ext[i]];
+    uint64_t *e = &ext[(size_t)i * (2 + LW + NNUM)];
+    e[0] = h.hard;
+    e[1] = h.prefer;
+    for (int k = 0; k < LW; ++k) e[2 + k] = h.lab[k];
+    for (int k = 0; k < NNUM; ++k) e[2 + LW + k] = (uint64_t)h.num[k];
+  }
+  uint32_t *d_pos;
+  uint64_t *d_ext;
+  HIPC(c, hipMallocAsync((void **)&d_pos, n * 4, c->stream));
+  HIPC(c, hipMallocAsync((void **)&d_ext, ext.size() * 8, c->stream));
+  HIPC(c, hipMemcpyAsync(d_pos, pos.data(), n * 4, hipMemcpyHostToDevice, c->stream));
+  HIPC(c, hipMemcpyAsync(d_ext, ext.data(), ext.size() * 8, hipMemcpyHostToDevice, c->stream));
+  HIPC(c, launch_scatter_rows(c->t, d_pos, nullptr, d_ext, n, 2u, c->stream));
+  HIPC(c, hipFreeAsync(d_pos, c->stream));
+  HIPC(c, hipFreeAsync(d_ext, c->stream));
+  HIPC(c, hipStreamSynchronize(c->stream));
+  c->dirty_ext.clear();
+  return KS_OK;
+}
+
+template <class T>
+ks_status dalloc(ks_ctx *c, T **p, size_t count) {
+  HIPC(c, hipMalloc((void **)p, std::max<size_t>(count, 1) * sizeof(T)));
+  HIPC(c, hipMemsetAsync(*p, 0, std::max<size_t>(count, 1) * sizeof(T), c->stream));
+  return KS_OK;
+}
+
+uint32_t blocks_per_shard(const Shard &s, uint32_t sub) { return (s.waves * sub + 3) / 4; }
+
+// Sweep / prescore kernel width: fewer nodes per lane when label/taint
+// columns are held too (register budget).
+uint32_t kernel_npl(const ks_ctx *c, bool ext) { return ext ? std::min<uint32_t>(c->npl, 2) : c->npl; }
+
+hipEvent_t get_event(ks_ctx *c) {
+  if (!c->ev_pool.empty()) {
+    hipEvent_t e = c->ev_pool.back();
+    c->ev_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+ks_status collect_timing(ks_ctx *c) {
+  for (auto &pr : c->ev_sweep) {
+    float ms = 0;
+    HIPC(c, hipEventElapsedTime(&ms, pr.first, pr.second));
+    c->stats.sweep_ms += ms;
+    c->stats.sweep_launches++;
+    c->ev_pool.push_back(pr.first);
+    c->ev_pool.push_back(pr.second);
+  }
+  for (auto &pr : c->ev_resolve) {
+    float ms = 0;
+    HIPC(c, hipEventElapsedTime(&ms, pr.first, pr.second));
+    c->stats.resolve_ms += ms;
+    c->stats.resolve_launches++;
+    c->ev_pool.push_back(pr.first);
+    c->ev_pool.push_back(pr.second);
+  }
+  c->stats.sweep_evals += c->pending_sweep_evals;
+  c->pending_sweep_evals = 0;
+  c->ev_sweep.clear();
+  c->ev_resolve.clear();
+  return KS_OK;
+}
+
+// One device-driven round (all kernels read the queue head from d_start).
+ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t host_start) {
+  const bool multi = c->cfg.world_size > 1;
+  const uint32_t nloc = multi ? 1 : c->S;
+  const uint32_t shard0 = multi ? c->cfg.rank : 0;
+  const uint32_t knpl = kernel_npl(c, b->ext);
+  const uint32_t sub = c->npl / knpl;
+  uint32_t bmax = 0;
+  for (uint32_t q = 0; q < nloc; ++q) bmax = std::max(bmax, blocks_per_shard(c->shards[shard0 + q], sub));
+  // pods per block: enough (block, pod-group) pairs to fill 256 CUs x 8 waves
+  const uint32_t want = 2048;
+  const uint32_t total_blocks = bmax * nloc;
+  uint32_t groups = (want + total_blocks - 1) / total_blocks;
+  groups = std::max<uint32_t>(1, std::min(groups, c->P));
+  uint32_t pg = (c->P + groups - 1) / groups;
+  pg = std::min<uint32_t>(std::max<uint32_t>(pg, 1), MAX_PG);
+  groups = (c->P + pg - 1) / pg;
+
+  RoundArgs a{};
+  a.t = c->t;
+  a.shards = c->d_shards;
+  a.total_shards = c->S;
+  a.shard0 = shard0;
+  a.npl = knpl;
+  a.sub = sub;
+  a.lnpl = c->npl;
+  a.P = c->P;
+  a.pg = pg;
+  a.K = c->K;
+  a.npods = b->n;
+  a.bstride = bmax;
+  a.evaluated = c->n_present;
+  a.pods = b->d_pods;
+  a.clauses = b->d_clauses;
+  a.d_start = c->d_start;
+  a.norm_max = c->d_norm;
+  a.brec = c->d_brec;
+  a.srec = c->d_srec;
+  a.frec = c->S == 1 ? c->d_srec : c->d_frec;
+  a.results = b->d_results;
+  a.counters = c->d_counters;
+  a.w = Weights{c->cfg.weight_fit, c->cfg.weight_balanced, c->cfg.weight_taint, c->cfg.weight_affinity,
+                c->cfg.weight_image};
+  if ((size_t)nloc * c->P * bmax * sizeof(BlockRec) > c->brec_bytes)
+    return c->fail(KS_ERR_INVALID, "block record buffer too small");
+
+  // Sweep-kernel geometry is expressed with the kernel's own nodes-per-lane:
+  // positions of layout wave w, steps [j0, j0 + knpl) are kernel wave w*sub + j0/knpl.
+  // The kernels address positions as base + wave*64*knpl + j*64 + lane, which
+  // equals the layout position when the layout's npl-step block of a wave is
+  // split into `sub` consecutive kernel waves; slots follow from the layout.
+  if (b->norm) {
+    HIPC(c, hipMemsetAsync(c->d_norm, 0, (size_t)2 * c->P * 4, c->stream));
+    HIPC(c, launch_prescore(a, bmax, groups, nloc, c->stream));
+    if (multi) NCCLC(c, ncclAllReduce(c->d_norm, c->d_norm, 2 * c->P, ncclUint32, ncclMax, c->comm, c->stream));
+  }
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (c->timing) {
+    e0 = get_event(c);
+    e1 = get_event(c);
+    HIPC(c, hipEventRecord(e0, c->stream));
+  }
+  HIPC(c, launch_sweep(a, b->ext, bmax, groups, nloc, c->stream));
+  if (c->timing) {
+    HIPC(c, hipEventRecord(e1, c->stream));
+    c->ev_sweep.emplace_back(e0, e1);
+    uint64_t nodes_local = 0;
+    for (uint32_t q = 0; q < nloc; ++q) nodes_local += c->shards[shard0 + q].count;
+    const uint64_t pods = std::min<uint64_t>(c->P, b->n - std::min(b->n, host_start));
+    c->pending_sweep_evals += pods * nodes_local;  // upper bound when the round resolves early
+  }
+  HIPC(c, launch_merge(a, nloc, c->stream));
+  if (multi) {
+    const size_t words = (size_t)c->P * rec_words(c->K);
+    NCCLC(c, ncclAllGather(c->d_srec + (size_t)c->cfg.rank * words, c->d_srec, words * 8, ncclUint8, c->comm,
+                           c->stream));
+  }
+  if (c->S > 1) HIPC(c, launch_merge_shards(a, c->stream));
+  if (c->timing) {
+    e0 = get_event(c);
+    e1 = get_event(c);
+    HIPC(c, hipEventRecord(e0, c->stream));
+  }
+  HIPC(c, launch_resolve(a, b->ext, c->stream));
+  if (c->timing) {
+    HIPC(c, hipEventRecord(e1, c->stream));
+    c->ev_resolve.emplace_back(e0, e1);
+  }
+  c->stats.rounds++;
+  return KS_OK;
+}
+
+}  // namespace
+
+// ================================================================== C ABI
+
+extern "C" {
+
+void ks_config_default(ks_config *cfg) {
+  std::memset(cfg, 0, sizeof *cfg);
+  cfg->device = 0;
+  cfg->node_capacity = 1024;
+  cfg->pods_per_round = 256;
+  cfg->topk = 0;
+  cfg->nodes_per_lane = 8;
+  cfg->world_size = 1;
+  cfg->rank = 0;
+  cfg->virtual_shards = 1;
+  cfg->weight_fit = 1;
+  cfg->weight_balanced = 1;
+  cfg->weight_taint = 3;
+  cfg->weight_affinity = 2;
+  cfg->weight_image = 1;
+}
+
+int32_t ks_abi_version(void) { return KSCHED_ABI_VERSION; }
+
+const char *ks_last_error(const ks_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
+  if (!cfg || !out) return KS_ERR_INVALID;
+  *out = nullptr;
+  auto c = std::make_unique<ks_ctx>();
+  c->cfg = *cfg;
+  if (cfg->node_capacity == 0) return KS_ERR_INVALID;
+  c->cap = cfg->node_capacity;
+  c->npl = cfg->nodes_per_lane ? cfg->nodes_per_lane : 8;
+  if (c->npl != 2 && c->npl != 4 && c->npl != 8) return KS_ERR_INVALID;
+  c->P = cfg->pods_per_round ? cfg->pods_per_round : 256;
+  if (c->P > (uint32_t)MAX_P) return KS_ERR_INVALID;
+  c->K = cfg->topk ? cfg->topk : c->P;
+  if (c->K > 512) return KS_ERR_INVALID;  // resolve: one listed candidate per thread
+  const uint32_t world = cfg->world_size ? cfg->world_size : 1;
+  c->cfg.world_size = world;
+  if (cfg->rank >= world) return KS_ERR_INVALID;
+  c->S = world > 1 ? world : std::max<uint32_t>(1, cfg->virtual_shards);
+  if (c->S > (uint32_t)MAX_SHARDS) return KS_ERR_INVALID;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return KS_ERR_DEVICE;
+  if (cfg->device < 0 || cfg->device >= ndev) return KS_ERR_DEVICE;
+  if (hipSetDevice(cfg->device) != hipSuccess) return KS_ERR_DEVICE;
+  ks_ctx *x = c.get();
+  HIPC(x, hipStreamCreateWithFlags(&x->stream, hipStreamNonBlocking));
+  // shard geometry: contiguous slot ranges; waves rounded to a multiple of 4
+  uint32_t base = 0;
+  for (uint32_t s = 0; s < x->S; ++s) {
+    Shard sh;
+    sh.lo = (uint32_t)((uint64_t)x->cap * s / x->S);
+    const uint32_t hi = (uint32_t)((uint64_t)x->cap * (s + 1) / x->S);
+    sh.count = hi - sh.lo;
+    uint32_t lanes = (sh.count + x->npl - 1) / x->npl;
+    uint32_t waves = (lanes + WAVE - 1) / WAVE;
+    waves = std::max<uint32_t>(4, (waves + 3) & ~3u);
+    sh.waves = waves;
+    sh.base = base;
+    base += waves * WAVE * x->npl;
+    x->shards.push_back(sh);
+  }
+  x->npos = base;
+  x->slot_pos.resize(x->cap);
+  for (auto &sh : x->shards)
+    for (uint32_t l = 0; l < sh.count; ++l) x->slot_pos[sh.lo + l] = shard_pos(sh, x->npl, l);
+  x->nodes.resize(x->cap);
+  // device table
+  ks_status st;
+  NodeTable &t = x->t;
+  t.npos = x->npos;
+  t.lw = 0;
+  if ((st = dalloc(x, &t.acpu, x->npos)) || (st = dalloc(x, &t.amem, x->npos)) ||
+      (st = dalloc(x, &t.rcpu, x->npos)) || (st = dalloc(x, &t.rmem, x->npos)) ||
+      (st = dalloc(x, &t.zcpu, x->npos)) || (st = dalloc(x, &t.zmem, x->npos)) ||
+      (st = dalloc(x, &t.apods, x->npos)) || (st = dalloc(x, &t.npods, x->npos)) ||
+      (st = dalloc(x, &t.hard, x->npos)) || (st = dalloc(x, &t.prefer, x->npos)) ||
+      (st = dalloc(x, &t.lab, (size_t)LW * x->npos)) || (st = dalloc(x, &t.num, (size_t)NNUM * x->npos)))
+    return st;
+  HIPC(x, hipMemsetAsync(t.apods, 0xFF, (size_t)x->npos * 4, x->stream));  // every position empty
+  if ((st = dalloc(x, &x->d_shards, x->S)) || (st = dalloc(x, &x->d_slot_pos, x->cap)) ||
+      (st = dalloc(x, &x->d_start, 1)) || (st = dalloc(x, &x->d_norm, 2 * (size_t)x->P)) ||
+      (st = dalloc(x, &x->d_counters, 4)))
+    return st;
+  HIPC(x, hipMemcpyAsync(x->d_shards, x->shards.data(), x->S * sizeof(Shard), hipMemcpyHostToDevice, x->stream));
+  HIPC(x, hipMemcpyAsync(x->d_slot_pos, x->slot_pos.data(), (size_t)x->cap * 4, hipMemcpyHostToDevice, x->stream));
+  HIPC(x, hipHostMalloc((void **)&x->h_start, 4, hipHostMallocDefault));
+  // round records: blocks of the widest kernel (npl 2 -> sub = npl / 2)
+  uint32_t bmax = 0;
+  for (auto &sh : x->shards) bmax = std::max(bmax, blocks_per_shard(sh, x->npl / std::min<uint32_t>(x->npl, 2)));
+  const uint32_t nloc = world > 1 ? 1 : x->S;
+  x->brec_bytes = (size_t)nloc * x->P * bmax * sizeof(BlockRec);
+  if ((st = dalloc(x, (uint8_t **)&x->d_brec, x->brec_bytes))) return st;
+  const size_t recs = (size_t)x->S * x->P * rec_words(x->K);
+  if ((st = dalloc(x, &x->d_srec, recs)) || (st = dalloc(x, &x->d_frec, (size_t)x->P * rec_words(x->K))))
+    return st;
+  HIPC(x, hipStreamSynchronize(x->stream));  // all initialisation is stream-ordered
+  *out = c.release();
+  return KS_OK;
+}
+
+void ks_close(ks_ctx *c) {
+  if (!c) return;
+  (void)hipSetDevice(c->cfg.device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->comm) ncclCommDestroy(c->comm);
+  void *bufs[] = {c->t.acpu, c->t.amem, c->t.rcpu, c->t.rmem, c->t.zcpu, c->t.zmem, c->t.apods,
+                  c->t.npods, c->t.hard, c->t.prefer, c->t.lab, c->t.num, c->d_shards, c->d_slot_pos,
+                  c->d_start, c->d_norm, c->d_brec, c->d_srec, c->d_frec, c->d_counters};
+  for (void *b : bufs)
+    if (b) (void)hipFree(b);
+  if (c->h_start) (void)hipHostFree(c->h_start);
+  for (auto &pr : c->ev_sweep) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
+  for (auto &pr : c->ev_resolve) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
+  for (auto e : c->ev_pool) (void)hipEventDestroy(e);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+ks_status ks_nodes_upsert(ks_ctx *c, const ks_node *nodes, const uint32_t *slots, uint32_t n) {
+  if (!c || (n && (!nodes || !slots))) return KS_ERR_INVALID;
+  HIPC(c, hipSetDevice(c->cfg.device));
+  std::vector<uint32_t> pos(n);
+  std::vector<int64_t> core((size_t)n * 8);
+  std::vector<uint64_t> ext((size_t)n * (2 + LW + NNUM));
+  bool grew = false;
+  for (uint32_t i = 0; i < n; ++i) {
+    const ks_node &s = nodes[i];
+    const uint32_t slot = slots[i];
+    if (slot >= c->cap) return c->fail(KS_ERR_NOT_FOUND, "slot %u >= capacity %u", slot, c->cap);
+    if (s.alloc_milli_cpu < 0 || s.alloc_milli_cpu >= kMaxExact || s.alloc_memory < 0 ||
+        s.alloc_memory >= kMaxExact || s.alloc_pods < 0 || s.alloc_pods > INT32_MAX - 1)
+      return c->fail(KS_ERR_RANGE, "node %s allocatable outside the exact range", str(s.name).c_str());
+    HostNode &h = c->nodes[slot];
+    const bool is_new = !h.present;
+    if (!is_new) {
+      c->name_slot.erase(h.name);
+      for (auto &kv : h.labels) {
+        auto &v = c->key_nodes[kv.first];
+        v.erase(std::remove(v.begin(), v.end(), slot), v.end());
+      }
+    } else {
+      c->n_present++;
+    }
+    h.present = true;
+    h.name = c->intern(s.name);
+    c->name_slot[h.name] = slot;
+    h.acpu = s.alloc_milli_cpu;
+    h.amem = s.alloc_memory;
+    h.apods = s.alloc_pods;
+    h.unschedulable = s.unschedulable != 0;
+    h.labels.clear();
+    for (uint32_t k = 0; k < s.n_labels; ++k) {
+      const uint32_t key = c->intern(s.labels[k].key);
+      h.labels.emplace_back(key, c->intern(s.labels[k].value));
+      c->key_nodes[key].push_back(slot);
+    }
+    h.hard = h.unschedulable ? UNSCHED_BIT : 0;
+    h.prefer = 0;
+    for (uint32_t k = 0; k < s.n_taints; ++k) {
+      const ks_taint &tt = s.taints[k];
+      const uint32_t key = c->intern(tt.key), val = c->intern(tt.value);
+      if (tt.effect == KS_EFFECT_NO_SCHEDULE || tt.effect == KS_EFFECT_NO_EXECUTE) {
+        TaintKey tk{key, val, tt.effect};
+        auto it = c->hard_dict.find(tk);
+        uint32_t b;
+        if (it == c->hard_dict.end()) {
+          if (c->hard_list.size() >= 63) return c->fail(KS_ERR_CAPACITY, "more than 63 distinct hard taints");
+          b = (uint32_t)c->hard_list.size();
+          c->hard_dict.emplace(tk, b);
+          c->hard_list.push_back(tk);
+          grew = true;
+        } else {
+          b = it->second;
+        }
+        h.hard |= 1ull << b;
+      } else if (tt.effect == KS_EFFECT_PREFER_NO_SCHEDULE) {
+        auto pk = std::make_pair(key, val);
+        auto it = c->prefer_dict.find(pk);
+        uint32_t b;
+        if (it == c->prefer_dict.end()) {
+          if (c->prefer_list.size() >= 64) return c->fail(KS_ERR_CAPACITY, "more than 64 distinct prefer taints");
+          b = (uint32_t)c->prefer_list.size();
+          c->prefer_dict.emplace(pk, b);
+          c->prefer_list.push_back(pk);
+          grew = true;
+        } else {
+          b = it->second;
+        }
+        h.prefer |= 1ull << b;
+      }
+      // other effects are ignored by both TaintToleration filters and scores
+    }
+    if ((h.hard & ~c->hard_in_use) || (h.prefer & ~c->prefer_in_use)) grew = true;
+    c->hard_in_use |= h.hard;
+    c->prefer_in_use |= h.prefer;
+    node_ext_bits(c, h);
+    pos[i] = c->slot_pos[slot];
+    int64_t *cr = &core[(size_t)i * 8];
+    cr[0] = h.acpu;
+    cr[1] = h.amem;
+    cr[2] = h.apods;
+    cr[3] = is_new ? 1 : 0;
+    uint64_t *e = &ext[(size_t)i * (2 + LW + NNUM)];
+    e[0] = h.hard;
+    e[1] = h.prefer;
+    for (int k = 0; k < LW; ++k) e[2 + k] = h.lab[k];
+    for (int k = 0; k < NNUM; ++k) e[2 + LW + k] = (uint64_t)h.num[k];
+  }
+  if (grew) c->dict_version++;
+  if (!n) return KS_OK;
+  uint32_t *d_pos;
+  int64_t *d_core;
+  uint64_t *d_ext;
+  HIPC(c, hipMalloc((void **)&d_pos, (size_t)n * 4));
+  HIPC(c, hipMalloc((void **)&d_core, core.size() * 8));
+  HIPC(c, hipMalloc((void **)&d_ext, ext.size() * 8));
+  HIPC(c, hipMemcpyAsync(d_pos, pos.data(), (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
+  HIPC(c, hipMemcpyAsync(d_core, core.data(), core.size() * 8, hipMemcpyHostToDevice, c->stream));
+  HIPC(c, hipMemcpyAsync(d_ext, ext.data(), ext.size() * 8, hipMemcpyHostToDevice, c->stream));
+  HIPC(c, launch_scatter_rows(c->t, d_pos, d_core, d_ext, n, 1u, c->stream));
+  HIPC(c, hipStreamSynchronize(c->stream));
+  (void)hipFree(d_pos);
+  (void)hipFree(d_core);
+  (void)hipFree(d_ext);
+  return KS_OK;
+}
+
+ks_status ks_nodes_delete(ks_ctx *c, const uint32_t *slots, uint32_t n) {
+  if (!c || (n && !slots)) return KS_ERR_INVALID;
+  HIPC(c, hipSetDevice(c->cfg.device));
+  std::vector<uint32_t> pos(n);
+  std::vector<int64_t> core((size_t)n * 8, 0);
+  for (uint32_t i = 0; i < n; ++i) {
+    if (slots[i] >= c->cap || !c->nodes[slots[i]].present)
+      return c->fail(KS_ERR_NOT_FOUND, "slot %u not present", slots[i]);
+    HostNode &h = c->nodes[slots[i]];
+    c->name_slot.erase(h.name);
+    for (auto &kv : h.labels) {
+      auto &v = c->key_nodes[kv.first];
+      v.erase(std::remove(v.begin(), v.end(), slots[i]), v.end());
+    }
+    h = HostNode();
+    c->n_present--;
+    pos[i] = c->slot_pos[slots[i]];
+    core[(size_t)i * 8 + 2] = -1;  // apods < 0: empty slot
+    core[(size_t)i * 8 + 3] = 1;   // reset requested state
+  }
+  if (!n) return KS_OK;
+  uint32_t *d_pos;
+  int64_t *d_core;
+  HIPC(c, hipMalloc((void **)&d_pos, (size_t)n * 4));
+  HIPC(c, hipMalloc((void **)&d_core, core.size() * 8));
+  HIPC(c, hipMemcpyAsync(d_pos, pos.data(), (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
+  HIPC(c, hipMemcpyAsync(d_core, core.data(), core.size() * 8, hipMemcpyHostToDevice, c->stream));
+  HIPC(c, launch_scatter_rows(c->t, d_pos, d_core, nullptr, n, 0u, c->stream));
+  HIPC(c, hipStreamSynchronize(c->stream));
+  (void)hipFree(d_pos);
+  (void)hipFree(d_core);
+  return KS_OK;
+}
+
+static ks_status pods_delta(ks_ctx *c, const ks_pod *pods, const uint32_t *slots, uint32_t n, int sign) {
+  if (!c || (n && (!pods || !slots))) return KS_ERR_INVALID;
+  if (!n) return KS_OK;
+  HIPC(c, hipSetDevice(c->cfg.device));
+  std::vector<uint32_t> pos(n);
+  std::vector<int64_t> d((size_t)n * 5);
+  for (uint32_t i = 0; i < n; ++i) {
+    if (slots[i] >= c->cap || !c->nodes[slots[i]].present)
+      return c->fail(KS_ERR_NOT_FOUND, "slot %u not present", slots[i]);
+    int64_t rc, rm, zc, zm;
+    ks_status st;
+    if ((st = pod_requests(pods[i], false, &rc, &rm)) || (st = pod_requests(pods[i], true, &zc, &zm)))
+      return c->fail(st, "pod requests a resource other than cpu/memory");
+    pos[i] = c->slot_pos[slots[i]];
+    int64_t *x = &d[(size_t)i * 5];
+    x[0] = sign * rc;
+    x[1] = sign * rm;
+    x[2] = sign * zc;
+    x[3] = sign * zm;
+    x[4] = sign;
+  }
+  uint32_t *d_pos;
+  int64_t *d_d;
+  HIPC(c, hipMalloc((void **)&d_pos, (size_t)n * 4));
+  HIPC(c, hipMalloc((void **)&d_d, d.size() * 8));
+  HIPC(c, hipMemcpyAsync(d_pos, pos.data(), (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
+  HIPC(c, hipMemcpyAsync(d_d, d.data(), d.size() * 8, hipMemcpyHostToDevice, c->stream));
+  HIPC(c, launch_apply_deltas(c->t, d_pos, d_d, n, c->stream));
+  HIPC(c, hipStreamSynchronize(c->stream));
+  (void)hipFree(d_pos);
+  (void)hipFree(d_d);
+  return KS_OK;
+}
+
+ks_status ks_pods_add(ks_ctx *c, const ks_pod *pods, const uint32_t *slots, uint32_t n) {
+  return pods_delta(c, pods, slots, n, +1);
+}
+ks_status ks_pods_remove(ks_ctx *c, const ks_pod *pods, const uint32_t *slots, uint32_t n) {
+  return pods_delta(c, pods, slots, n, -1);
+}
+
+ks_status ks_batch_prepare(ks_ctx *c, const ks_pod *pods, uint32_t n, ks_batch **out) {
+  if (!c || !out || (n && !pods)) return KS_ERR_INVALID;
+  *out = nullptr;
+  HIPC(c, hipSetDevice(c->cfg.device));
+  auto b = std::make_unique<ks_batch>();
+  b->n = n;
+  std::vector<PodDev> dev(std::max<uint32_t>(n, 1));
+  ClauseBuf cl;
+  for (uint32_t i = 0; i < n; ++i) {
+    ks_status st = compile_pod(c, pods[i], dev[i], cl);
+    if (st) return st;
+    if (dev[i].flags & PF_EXT) b->ext = true;
+    if (dev[i].flags & (PF_TT | PF_NA)) b->norm = true;
+  }
+  if (b->norm) b->ext = true;
+  ks_status st = upload_dirty_ext(c);
+  if (st) return st;
+  b->dict_version = c->dict_version;
+  if (cl.w.empty()) cl.add(CK_FALSE, 0, 0, nullptr, 0);
+  HIPC(c, hipMalloc((void **)&b->d_pods, dev.size() * sizeof(PodDev)));
+  HIPC(c, hipMalloc((void **)&b->d_clauses, cl.w.size() * 8));
+  HIPC(c, hipMalloc((void **)&b->d_results, std::max<uint32_t>(n, 1) * sizeof(DevResult)));
+  HIPC(c, hipMemcpyAsync(b->d_pods, dev.data(), dev.size() * sizeof(PodDev), hipMemcpyHostToDevice, c->stream));
+  HIPC(c, hipMemcpyAsync(b->d_clauses, cl.w.data(), cl.w.size() * 8, hipMemcpyHostToDevice, c->stream));
+  HIPC(c, hipMemsetAsync(b->d_results, 0, std::max<uint32_t>(n, 1) * sizeof(DevResult), c->stream));
+  HIPC(c, hipStreamSynchronize(c->stream));
+  *out = b.release();
+  return KS_OK;
+}
+
+ks_status ks_batch_run(ks_ctx *c, ks_batch *b) {
+  if (!c || !b) return KS_ERR_INVALID;
+  if (b->dict_version != c->dict_version)
+    return c->fail(KS_ERR_STALE, "batch compiled against taint dictionary v%u, cache is at v%u", b->dict_version,
+                   c->dict_version);
+  if (c->cfg.world_size > 1 && !c->comm) return c->fail(KS_ERR_COMM, "world_size > 1 but ks_comm_init not called");
+  HIPC(c, hipSetDevice(c->cfg.device));
+  HIPC(c, hipMemsetAsync(c->d_start, 0, 4, c->stream));
+  uint32_t host_start = 0;
+  while (host_start < b->n) {
+    // every round resolves at least one pod; assume full windows and check
+    const uint32_t remaining = b->n - host_start;
+    uint32_t rounds = (remaining + c->P - 1) / c->P;
+    rounds = std::min<uint32_t>(rounds, 64);
+    for (uint32_t r = 0; r < rounds; ++r) {
+      ks_status st = enqueue_round(c, b, host_start + r * c->P);
+      if (st) return st;
+    }
+    HIPC(c, hipMemcpyAsync(c->h_start, c->d_start, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPC(c, hipStreamSynchronize(c->stream));
+    if (*c->h_start <= host_start) return c->fail(KS_ERR_DEVICE, "no progress in scheduling rounds");
+    host_start = *c->h_start;
+  }
+  if (c->timing) {
+    ks_status st = collect_timing(c);
+    if (st) return st;
+  }
+  c->stats.pods_resolved += b->n;
+  return KS_OK;
+}
+
+ks_status ks_batch_results(ks_ctx *c, const ks_batch *b, ks_result *out) {
+  if (!c || !b || (b->n && !out)) return KS_ERR_INVALID;
+  static_assert(sizeof(ks_result) == sizeof(DevResult), "result layout");
+  HIPC(c, hipSetDevice(c->cfg.device));
+  HIPC(c, hipMemcpyAsync(out, b->d_results, (size_t)b->n * sizeof(DevResult), hipMemcpyDeviceToHost, c->stream));
+  HIPC(c, hipStreamSynchronize(c->stream));
+  for (uint32_t i = 0; i < b->n; ++i)
+    if (out[i].status == KS_POD_SCHEDULED) c->stats.pods_scheduled++;
+  return KS_OK;
+}
+
+void ks_batch_free(ks_ctx *c, ks_batch *b) {
+  if (!b) return;
+  if (c) (void)hipSetDevice(c->cfg.device);
+  if (b->d_pods) (void)hipFree(b->d_pods);
+  if (b->d_clauses) (void)hipFree(b->d_clauses);
+  if (b->d_results) (void)hipFree(b->d_results);
+  delete b;
+}
+
+ks_status ks_schedule(ks_ctx *c, const ks_pod *pods, uint32_t n, ks_result *out) {
+  ks_batch *b = nullptr;
+  ks_status st = ks_batch_prepare(c, pods, n, &b);
+  if (st) return st;
+  st = ks_batch_run(c, b);
+  if (!st) st = ks_batch_results(c, b, out);
+  ks_batch_free(c, b);
+  return st;
+}
+
+ks_status ks_plugin_scores(ks_ctx *c, const ks_pod *pod, ks_node_score *out) {
+  if (!c || !pod || !out) return KS_ERR_INVALID;
+  HIPC(c, hipSetDevice(c->cfg.device));
+  PodDev d;
+  ClauseBuf cl;
+  ks_status st = compile_pod(c, *pod, d, cl);
+  if (st) return st;
+  if ((st = upload_dirty_ext(c))) return st;
+  if (cl.w.empty()) cl.add(CK_FALSE, 0, 0, nullptr, 0);
+  DumpArgs a{};
+  a.t = c->t;
+  a.nslots = c->cap;
+  a.w = Weights{c->cfg.weight_fit, c->cfg.weight_balanced, c->cfg.weight_taint, c->cfg.weight_affinity,
+                c->cfg.weight_image};
+  a.slot_pos = c->d_slot_pos;
+  PodDev *d_pod;
+  uint64_t *d_cl;
+  uint32_t *d_norm;
+  int32_t *d_out;
+  HIPC(c, hipMalloc((void **)&d_pod, sizeof(PodDev)));
+  HIPC(c, hipMalloc((void **)&d_cl, cl.w.size() * 8));
+  HIPC(c, hipMalloc((void **)&d_norm, 8));
+  HIPC(c, hipMalloc((void **)&d_out, (size_t)c->cap * 10 * 4));
+  HIPC(c, hipMemcpyAsync(d_pod, &d, sizeof d, hipMemcpyHostToDevice, c->stream));
+  HIPC(c, hipMemcpyAsync(d_cl, cl.w.data(), cl.w.size() * 8, hipMemcpyHostToDevice, c->stream));
+  HIPC(c, hipMemsetAsync(d_norm, 0, 8, c->stream));
+  a.pods = d_pod;
+  a.clauses = d_cl;
+  a.norm_max = d_norm;
+  a.out = d_out;
+  HIPC(c, launch_dump(a, c->stream));
+  std::vector<int32_t> raw((size_t)c->cap * 10);
+  HIPC(c, hipMemcpyAsync(raw.data(), d_out, raw.size() * 4, hipMemcpyDeviceToHost, c->stream));
+  HIPC(c, hipStreamSynchronize(c->stream));
+  (void)hipFree(d_pod);
+  (void)hipFree(d_cl);
+  (void)hipFree(d_norm);
+  (void)hipFree(d_out);
+  for (uint32_t i = 0; i < c->cap; ++i) {
+    const int32_t *o = &raw[(size_t)i * 10];
+    ks_node_score s{};
+    s.status = o[0];
+    s.least_allocated = o[1];
+    s.balanced_allocation = o[2];
+    s.taint_raw = o[3];
+    s.taint_score = o[4];
+    s.affinity_raw = o[5];
+    s.affinity_score = o[6];
+    s.image_locality = o[7];
+    s.total_score = (int64_t)(((uint64_t)(uint32_t)o[9] << 32) | (uint32_t)o[8]);
+    out[i] = s;
+  }
+  return KS_OK;
+}
+
+ks_status ks_node_states(ks_ctx *c, const uint32_t *slots, uint32_t n, ks_node_state *out) {
+  if (!c || (n && (!slots || !out))) return KS_ERR_INVALID;
+  if (!n) return KS_OK;
+  HIPC(c, hipSetDevice(c->cfg.device));
+  std::vector<uint32_t> pos(n);
+  for (uint32_t i = 0; i < n; ++i) {
+    if (slots[i] >= c->cap) return c->fail(KS_ERR_NOT_FOUND, "slot %u >= capacity", slots[i]);
+    pos[i] = c->slot_pos[slots[i]];
+  }
+  uint32_t *d_pos;
+  int64_t *d_out;
+  HIPC(c, hipMalloc((void **)&d_pos, (size_t)n * 4));
+  HIPC(c, hipMalloc((void **)&d_out, (size_t)n * 64));
+  HIPC(c, hipMemcpyAsync(d_pos, pos.data(), (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
+  HIPC(c, launch_gather_rows(c->t, d_pos, d_out, n, c->stream));
+  std::vector<int64_t> raw((size_t)n * 8);
+  HIPC(c, hipMemcpyAsync(raw.data(), d_out, raw.size() * 8, hipMemcpyDeviceToHost, c->stream));
+  HIPC(c, hipStreamSynchronize(c->stream));
+  (void)hipFree(d_pos);
+  (void)hipFree(d_out);
+  for (uint32_t i = 0; i < n; ++i) {
+    const int64_t *r = &raw[(size_t)i * 8];
+    ks_node_state s{};
+    s.alloc_milli_cpu = r[0];
+    s.alloc_memory = r[1];
+    s.req_milli_cpu = r[2];
+    s.req_memory = r[3];
+    s.nonzero_milli_cpu = r[4];
+    s.nonzero_memory = r[5];
+    s.alloc_pods = (int32_t)r[6];
+    s.pod_count = s.alloc_pods < 0 ? -1 : (int32_t)r[7];
+    if (s.alloc_pods < 0) s = ks_node_state{0, 0, 0, 0, 0, 0, 0, -1};
+    out[i] = s;
+  }
+  return KS_OK;
+}
+
+ks_status ks_comm_unique_id(uint8_t out[KS_COMM_ID_BYTES]) {
+  static_assert(sizeof(ncclUniqueId) == KS_COMM_ID_BYTES, "ncclUniqueId size");
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return KS_ERR_COMM;
+  std::memcpy(out, &id, sizeof id);
+  return KS_OK;
+}
+
+ks_status ks_comm_init(ks_ctx *c, const uint8_t id[KS_COMM_ID_BYTES]) {
+  if (!c || !id) return KS_ERR_INVALID;
+  HIPC(c, hipSetDevice(c->cfg.device));
+  ncclUniqueId uid;
+  std::memcpy(&uid, id, sizeof uid);
+  NCCLC(c, ncclCommInitRank(&c->comm, (int)c->cfg.world_size, uid, (int)c->cfg.rank));
+  return KS_OK;
+}
+
+ks_status ks_get_stats(ks_ctx *c, ks_stats *out) {
+  if (!c || !out) return KS_ERR_INVALID;
+  *out = c->stats;
+  return KS_OK;
+}
+
+ks_status ks_reset_stats(ks_ctx *c) {
+  if (!c) return KS_ERR_INVALID;
+  c->stats = ks_stats{};
+  return KS_OK;
+}
+
+ks_status ks_set_timing(ks_ctx *c, int32_t enabled) {
+  if (!c) return KS_ERR_INVALID;
+  c->timing = enabled != 0;
+  return KS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,1156 @@
+// ksched_kernels.hip — gfx950 kernels of the dist-scheduler shard hot path.
+//
+// One scheduling ROUND evaluates a window of P pending pods against the node
+// snapshot and then commits them in queue order:
+//
+//   prescore  (only pods with an active normalising plugin) per-pod max raw
+//             TaintToleration / NodeAffinity score over feasible nodes
+//   sweep     Filter + Score of every (pod, node) pair; per pod and block the
+//             best BLOCK_KEYS packed keys plus a bound      -> BlockRec
+//   merge     per pod: blocks -> sorted candidate prefix    -> shard record
+//   [RCCL all-gather of shard records across GPUs]
+//   merge_shards  per pod: shards -> final candidate prefix
+//   resolve   one workgroup walks the window in order; pod i's winner is the
+//             best of (a) its first listed candidate not modified by pods < i
+//             and (b) every modified node re-scored against the live state.
+//             If neither is provably the max the round ends at pod i.
+//
+// Exact arithmetic: int64 resource checks; the
+// LeastAllocated quotient floor((cap-req)*100/cap) is computed in binary64 and
+// corrected with an exact FMA remainder (all operands < 2^53); the
+// BalancedAllocation fractions use IEEE binary64 division; compiled with
+// -ffp-contract=off so that no product/sum is fused.  References:
+// upstream k8s.io/kubernetes v1.31.3 pkg/scheduler/framework/plugins/
+// noderesources/{fit.go, least_allocated.go, balanced_allocation.go,
+// resource_allocation.go}, tainttoleration/taint_toleration.go,
+// nodeaffinity/node_affinity.go, helper/normalize_score.go.
+#include <hip/hip_runtime.h>
+
+#include <utility>
+
+#include "ksched_dev.hpp"
+#include "ksched_kernels.hpp"
+
+namespace ks {
+
+// ============================================================ device helpers
+
+// Compile-time unrolled loop: keeps per-node register arrays statically indexed
+// (a runtime-indexed array would be demoted to scratch).
+template <class F, int... I>
+__device__ __forceinline__ void static_for_impl(F &&f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F &&f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    uint64_t o = __shfl_xor(v, m, WAVE);
+    v = o > v ? o : v;
+  }
+  return v;
+}
+
+// Optimal 19-comparator network, descending (static indices only).
+__device__ __forceinline__ void cx_desc(uint64_t &a, uint64_t &b) {
+  const uint64_t hi = a > b ? a : b, lo = a > b ? b : a;
+  a = hi;
+  b = lo;
+}
+__device__ __forceinline__ void sort8_desc(uint64_t *k) {
+  cx_desc(k[0], k[2]); cx_desc(k[1], k[3]); cx_desc(k[4], k[6]); cx_desc(k[5], k[7]);
+  cx_desc(k[0], k[4]); cx_desc(k[1], k[5]); cx_desc(k[2], k[6]); cx_desc(k[3], k[7]);
+  cx_desc(k[0], k[1]); cx_desc(k[2], k[3]); cx_desc(k[4], k[5]); cx_desc(k[6], k[7]);
+  cx_desc(k[2], k[4]); cx_desc(k[3], k[5]);
+  cx_desc(k[1], k[4]); cx_desc(k[3], k[6]);
+  cx_desc(k[1], k[2]); cx_desc(k[3], k[4]); cx_desc(k[5], k[6]);
+}
+
+__device__ __forceinline__ uint32_t popc_ballot(bool b) {
+  return (uint32_t)__popcll(__ballot(b));
+}
+
+__device__ __forceinline__ uint32_t uniform_u32(uint32_t v) {
+  return __builtin_amdgcn_readfirstlane(v);
+}
+
+// Node resource state held in registers for the whole pod loop.
+struct NodeRegs {
+  int64_t free_cpu, free_mem;   // Allocatable - Requested           (Fit)
+  int64_t rcpu, rmem;           // Requested                         (BalancedAllocation)
+  int64_t lfree_cpu, lfree_mem; // Allocatable - NonZeroRequested    (LeastAllocated)
+  double acpu_d, amem_d;        // Allocatable as binary64
+  double inv_cpu, inv_mem;      // RN(1 / Allocatable)
+  uint32_t slot;
+  uint32_t bits;                // 1 valid, 2 pods fit, 4 cpu alloc != 0, 8 mem alloc != 0
+};
+
+struct NodeExt {
+  uint64_t hard, prefer;
+  uint64_t lab[LW];
+  int64_t num[NNUM];
+};
+
+__device__ __forceinline__ void load_core(const NodeTable &t, uint32_t pos, uint32_t slot, bool in_range,
+                                          NodeRegs &r) {
+  r.slot = slot;
+  r.bits = 0;
+  int32_t ap = in_range ? t.apods[pos] : -1;
+  if (ap < 0) {
+    r.free_cpu = r.free_mem = r.rcpu = r.rmem = r.lfree_cpu = r.lfree_mem = 0;
+    r.acpu_d = r.amem_d = 1.0;
+    r.inv_cpu = r.inv_mem = 1.0;
+    return;
+  }
+  const int64_t acpu = t.acpu[pos], amem = t.amem[pos];
+  const int64_t rc = t.rcpu[pos], rm = t.rmem[pos];
+  const int64_t zc = t.zcpu[pos], zm = t.zmem[pos];
+  const int32_t np = t.npods[pos];
+  r.free_cpu = acpu - rc;
+  r.free_mem = amem - rm;
+  r.rcpu = rc;
+  r.rmem = rm;
+  r.lfree_cpu = acpu - zc;
+  r.lfree_mem = amem - zm;
+  r.acpu_d = (double)acpu;
+  r.amem_d = (double)amem;
+  r.inv_cpu = acpu ? 1.0 / r.acpu_d : 1.0;
+  r.inv_mem = amem ? 1.0 / r.amem_d : 1.0;
+  r.bits = 1u | ((int64_t)np + 1 <= (int64_t)ap ? 2u : 0u) | (acpu ? 4u : 0u) | (amem ? 8u : 0u);
+}
+
+__device__ __forceinline__ void load_ext(const NodeTable &t, uint32_t pos, bool valid, NodeExt &e) {
+  if (!valid) {
+    e.hard = e.prefer = 0;
+#pragma unroll
+    for (int k = 0; k < LW; ++k) e.lab[k] = 0;
+#pragma unroll
+    for (int k = 0; k < NNUM; ++k) e.num[k] = 0;
+    return;
+  }
+  e.hard = t.hard[pos];
+  e.prefer = t.prefer[pos];
+#pragma unroll
+  for (int k = 0; k < LW; ++k) e.lab[k] = k < (int)t.lw ? t.lab[(size_t)k * t.npos + pos] : 0ull;
+#pragma unroll
+  for (int k = 0; k < NNUM; ++k) e.num[k] = t.num[(size_t)k * t.npos + pos];
+}
+
+// One label-selector requirement (clause) against one node.  The node's
+// label words / numeric values are passed as scalars so that no runtime index
+// into the per-node register arrays can form (it would demote them to scratch).
+__device__ __forceinline__ bool clause_pass(const uint64_t *c, uint64_t l0, uint64_t l1, uint64_t l2, uint64_t l3,
+                                            int64_t n0, int64_t n1, uint32_t slot) {
+  const uint32_t kind = (uint32_t)c[0] & 0xFF;
+  const uint64_t any = (l0 & c[1]) | (l1 & c[2]) | (l2 & c[3]) | (l3 & c[4]);
+  switch (kind) {
+    case CK_ANY: return any != 0;
+    case CK_NONE: return any == 0;
+    case CK_GT:
+    case CK_LT: {
+      // mask words hold the key's numeric-valid bit; c[5] the operand
+      const bool col1 = (c[0] >> 8) & 1u;
+      const int64_t v = col1 ? n1 : n0;
+      const int64_t x = (int64_t)c[5];
+      return any != 0 && (kind == CK_GT ? v > x : v < x);
+    }
+    case CK_NAME_EQ: return (int64_t)slot == (int64_t)c[5];
+    case CK_NAME_NE: return (int64_t)slot != (int64_t)c[5];
+    default: return false;
+  }
+}
+
+__device__ __forceinline__ bool clause_pass(const uint64_t *c, const NodeExt &e, uint32_t slot) {
+  return clause_pass(c, e.lab[0], e.lab[1], e.lab[2], e.lab[3], e.num[0], e.num[1], slot);
+}
+
+// RequiredNodeAffinity.Match: nodeSelector group (term 0) AND (no required
+// terms OR any required term whose clauses all pass).
+__device__ __forceinline__ bool required_match(const PodDev &p, const uint64_t *clauses, const NodeExt &e,
+                                               uint32_t slot) {
+  bool sel = true, any = false, cur = true;
+  uint32_t curterm = 0;
+  const uint64_t *c = clauses + (size_t)p.req_off * CLAUSE_WORDS;
+  for (uint32_t k = 0; k < p.req_len; ++k, c += CLAUSE_WORDS) {
+    const uint32_t term = ((uint32_t)c[0] >> 16) & 0xFFFF;
+    if (term != curterm) {
+      if (curterm >= 1) any |= cur;
+      cur = true;
+      curterm = term;
+    }
+    const bool pass = clause_pass(c, e, slot);
+    if (term == 0) sel &= pass;
+    else cur &= pass;
+  }
+  if (curterm >= 1) any |= cur;
+  return sel && (p.n_req_terms == 0 || any);
+}
+
+// PreferredSchedulingTerms.Score: Σ weight of matching preferred terms.
+__device__ __forceinline__ int64_t preferred_raw(const PodDev &p, const uint64_t *clauses, const NodeExt &e,
+                                                 uint32_t slot) {
+  int64_t raw = 0;
+  bool cur = true;
+  uint32_t curterm = 0;
+  int64_t wcur = 0;
+  const uint64_t *c = clauses + (size_t)p.pref_off * CLAUSE_WORDS;
+  for (uint32_t k = 0; k < p.pref_len; ++k, c += CLAUSE_WORDS) {
+    const uint32_t term = ((uint32_t)c[0] >> 16) & 0xFFFF;
+    if (term != curterm) {
+      if (curterm >= 1 && cur) raw += wcur;
+      cur = true;
+      curterm = term;
+      wcur = (int64_t)(int32_t)(c[0] >> 32);
+    }
+    cur &= clause_pass(c, e, slot);
+  }
+  if (curterm >= 1 && cur) raw += wcur;
+  return raw;
+}
+
+// Filter chain in default-profile order; returns ST_FEASIBLE or KS_PLUGIN_*.
+template <bool EXT>
+__device__ __forceinline__ int filter(const PodDev &p, const uint64_t *clauses, const NodeRegs &r,
+                                      const NodeExt &e) {
+  if (EXT && (p.flags & PF_EXT)) {
+    const uint64_t untol = e.hard & ~p.tol_hard;
+    if (untol & UNSCHED_BIT) return 0;                              // NodeUnschedulable
+    if (p.name_slot != -1 && (int64_t)r.slot != (int64_t)p.name_slot) return 1;  // NodeName
+    if (untol) return 2;                                            // TaintToleration
+    if ((p.flags & PF_AFF) && !required_match(p, clauses, e, r.slot)) return 3;  // NodeAffinity
+  }
+  // NodeResourcesFit (fitsRequest): pod count, then cpu / memory vs Requested.
+  bool fail = !(r.bits & 2u);
+  if (p.flags & PF_HAS_REQ) {
+    fail |= (p.req_cpu > 0) & (p.req_cpu > r.free_cpu);
+    fail |= (p.req_mem > 0) & (p.req_mem > r.free_mem);
+  }
+  return fail ? 4 : ST_FEASIBLE;
+}
+
+// leastRequestedScore((cap - lfree) + pod_nz, cap) given lfree = cap - NonZeroRequested.
+__device__ __forceinline__ int64_t least_requested(int64_t lfree, int64_t pod_nz, double cap_d, double inv) {
+  const int64_t rem = lfree - pod_nz;  // capacity - requested
+  if (rem < 0) return 0;               // requested > capacity
+  const double x = (double)rem * 100.0;  // exact (< 2^53)
+  double q = floor(x * inv);             // within one of the true quotient
+  const double r = __builtin_fma(-q, cap_d, x);  // exact remainder x - q*cap
+  q += (r >= cap_d) ? 1.0 : 0.0;
+  q -= (r < 0.0) ? 1.0 : 0.0;
+  return (int64_t)q;
+}
+
+__device__ __forceinline__ int64_t score_la(const PodDev &p, const NodeRegs &r) {
+  int64_t s = 0, w = 0;
+  if (r.bits & 4u) { s += least_requested(r.lfree_cpu, p.nz_cpu, r.acpu_d, r.inv_cpu); w += 1; }
+  if (r.bits & 8u) { s += least_requested(r.lfree_mem, p.nz_mem, r.amem_d, r.inv_mem); w += 1; }
+  return w == 2 ? (s >> 1) : s;  // nodeScore / weightSum (w in {0,1,2}, s >= 0)
+}
+
+__device__ __forceinline__ int64_t score_ba(const PodDev &p, const NodeRegs &r) {
+  double f0 = 0.0, f1 = 0.0;
+  const bool c = r.bits & 4u, m = r.bits & 8u;
+  if (c) {
+    f0 = (double)(r.rcpu + p.req_cpu) / r.acpu_d;
+    if (f0 > 1) f0 = 1;
+  }
+  if (m) {
+    f1 = (double)(r.rmem + p.req_mem) / r.amem_d;
+    if (f1 > 1) f1 = 1;
+  }
+  double sd = 0.0;
+  if (c && m) sd = fabs((f0 - f1) / 2);
+  return (int64_t)((1 - sd) * 100.0);
+}
+
+__device__ __forceinline__ int64_t taint_raw(const PodDev &p, const NodeExt &e) {
+  return (int64_t)__popcll(e.prefer & ~p.tol_prefer);
+}
+
+// DefaultNormalizeScore(100, reverse) for one element.
+__device__ __forceinline__ int64_t normalize(int64_t raw, int64_t mx, bool reverse) {
+  if (mx == 0) return reverse ? 100 : 0;
+  const int64_t s = (int64_t)((uint32_t)(100 * raw) / (uint32_t)mx);  // 0 <= raw <= mx < 2^25
+  return reverse ? 100 - s : s;
+}
+
+template <bool EXT>
+__device__ __forceinline__ int64_t total_score(const PodDev &p, const uint64_t *clauses, const NodeRegs &r,
+                                               const NodeExt &e, const Weights &w, int64_t tt_max,
+                                               int64_t na_max) {
+  int64_t t = (int64_t)w.fit * score_la(p, r) + (int64_t)w.ba * score_ba(p, r);
+  int64_t tt = 100;
+  if (EXT && (p.flags & PF_TT)) tt = normalize(taint_raw(p, e), tt_max, true);
+  t += (int64_t)w.tt * tt;
+  if (p.flags & PF_HAS_PREF) {
+    int64_t na = 0;
+    if (EXT && (p.flags & PF_NA)) na = normalize(preferred_raw(p, clauses, e, r.slot), na_max, false);
+    t += (int64_t)w.na * na;
+  }
+  return t;  // + w.il * 0 (ImageLocality: nodes report no images)
+}
+
+__device__ __forceinline__ uint64_t pack_key(int64_t total, uint32_t slot) {
+  return ((uint64_t)(total + 1) << 32) | (uint64_t)(0xFFFFFFFFu - slot);
+}
+
+__device__ __forceinline__ PodDev load_pod(const PodDev *pods, uint32_t i) {
+  // Wave-uniform: lowered to scalar loads.
+  return pods[i];
+}
+
+// ================================================================= prescore
+// Per pod with PF_TT / PF_NA: max raw score over feasible nodes -> atomicMax.
+template <int NPL>
+__global__ __launch_bounds__(SWEEP_THREADS) void prescore_kernel(RoundArgs a) {
+  const uint32_t start = uniform_u32(*a.d_start);
+  const uint32_t sh = blockIdx.z;
+  const Shard s = a.shards[a.shard0 + sh];
+  const uint32_t kw = blockIdx.x * (SWEEP_THREADS / WAVE) + threadIdx.x / WAVE;  // kernel wave
+  if (kw >= s.waves * a.sub) return;
+  const uint32_t lane = threadIdx.x % WAVE;
+  const uint32_t lwave = kw / a.sub, j0 = (kw % a.sub) * NPL;  // layout wave / first step
+  const uint32_t p0 = start + blockIdx.y * a.pg;
+  const uint32_t p1 = min(min(p0 + a.pg, start + a.P), a.npods);
+  if (p0 >= p1) return;
+
+  NodeRegs nr[NPL];
+  NodeExt ne[NPL];
+  static_for<NPL>([&](auto J) {
+    constexpr int j = J;
+    const uint32_t l = (j0 + (uint32_t)j) * WAVE * s.waves + lane * s.waves + lwave;
+    const uint32_t pos = s.base + kw * WAVE * NPL + (uint32_t)j * WAVE + lane;
+    load_core(a.t, pos, s.lo + l, l < s.count, nr[j]);
+    load_ext(a.t, pos, nr[j].bits & 1u, ne[j]);
+  });
+  for (uint32_t pi = p0; pi < p1; ++pi) {
+    const PodDev p = load_pod(a.pods, pi);
+    if (!(p.flags & (PF_TT | PF_NA))) continue;
+    int64_t tmax = 0, nmax = 0;
+    static_for<NPL>([&](auto J) {
+      constexpr int j = J;
+      if (!(nr[j].bits & 1u)) return;
+      if (filter<true>(p, a.clauses, nr[j], ne[j]) != ST_FEASIBLE) return;
+      if (p.flags & PF_TT) tmax = max(tmax, taint_raw(p, ne[j]));
+      if (p.flags & PF_NA) nmax = max(nmax, preferred_raw(p, a.clauses, ne[j], nr[j].slot));
+    });
+    tmax = (int64_t)wave_max_u64((uint64_t)tmax);
+    nmax = (int64_t)wave_max_u64((uint64_t)nmax);
+    if (lane == 0) {
+      const uint32_t r = pi - start;
+      if (tmax) atomicMax(&a.norm_max[2 * r + 0], (uint32_t)tmax);
+      if (nmax) atomicMax(&a.norm_max[2 * r + 1], (uint32_t)nmax);
+    }
+  }
+}
+
+// =================================================================== sweep
+// grid: x = block within shard, y = pod group, z = local shard.
+template <int NPL, bool EXT>
+__global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
+  constexpr int NW = SWEEP_THREADS / WAVE;
+  __shared__ uint64_t s_keys[MAX_PG][NW][3];
+  __shared__ uint32_t s_cnt[MAX_PG][NW][NFILT + 3];
+
+  const uint32_t start = uniform_u32(*a.d_start);
+  const uint32_t sh = blockIdx.z;
+  const Shard s = a.shards[a.shard0 + sh];
+  const uint32_t wid = threadIdx.x / WAVE;
+  const uint32_t kw = blockIdx.x * NW + wid;  // kernel wave
+  const uint32_t kwaves = s.waves * a.sub;
+  const uint32_t lane = threadIdx.x % WAVE;
+  const uint32_t lwave = kw / a.sub, j0 = (kw % a.sub) * NPL;  // layout wave / first step
+  const uint32_t p0 = start + blockIdx.y * a.pg;
+  const uint32_t p1 = min(min(p0 + a.pg, start + a.P), a.npods);
+  if (p0 >= p1 || blockIdx.x * NW >= kwaves) return;
+
+  NodeRegs nr[NPL];
+  NodeExt ne[EXT ? NPL : 1];
+  static_for<NPL>([&](auto J) {
+    constexpr int j = J;
+    const uint32_t l = (j0 + (uint32_t)j) * WAVE * s.waves + lane * s.waves + lwave;
+    const uint32_t pos = s.base + kw * WAVE * NPL + (uint32_t)j * WAVE + lane;
+    load_core(a.t, pos, s.lo + l, kw < kwaves && l < s.count, nr[j]);
+    if constexpr (EXT) load_ext(a.t, pos, nr[j].bits & 1u, ne[j]);
+  });
+
+  for (uint32_t pi = p0; pi < p1; ++pi) {
+    const PodDev p = load_pod(a.pods, pi);
+    const uint32_t r = pi - start;
+    int64_t tt_max = 0, na_max = 0;
+    if (EXT && (p.flags & (PF_TT | PF_NA))) {
+      tt_max = a.norm_max[2 * r + 0];
+      na_max = a.norm_max[2 * r + 1];
+    }
+    uint64_t best = 0, second = 0;
+    uint32_t feas = 0, f0 = 0, f1 = 0, f2 = 0, f3 = 0, f4 = 0, ttc = 0, nac = 0;
+    static_for<NPL>([&](auto J) {
+      constexpr int j = J;
+      constexpr int je = EXT ? j : 0;
+      const bool valid = nr[j].bits & 1u;
+      int st = ST_EMPTY;
+      uint64_t key = 0;
+      bool at_tt = false, at_na = false;
+      if (valid) {
+        st = filter<EXT>(p, a.clauses, nr[j], ne[je]);
+        if (st == ST_FEASIBLE) {
+          key = pack_key(total_score<EXT>(p, a.clauses, nr[j], ne[je], a.w, tt_max, na_max), nr[j].slot);
+          if (EXT && (p.flags & PF_TT)) at_tt = taint_raw(p, ne[je]) == tt_max;
+          if (EXT && (p.flags & PF_NA)) at_na = preferred_raw(p, a.clauses, ne[je], nr[j].slot) == na_max;
+        }
+      }
+      // running top-2 as value selects (a branchy form sinks into a scratch store)
+      const bool gt1 = key > best, gt2 = key > second;
+      second = gt1 ? best : (gt2 ? key : second);
+      best = gt1 ? key : best;
+      feas += popc_ballot(st == ST_FEASIBLE);
+      f0 += popc_ballot(st == 0);
+      f1 += popc_ballot(st == 1);
+      f2 += popc_ballot(st == 2);
+      f3 += popc_ballot(st == 3);
+      f4 += popc_ballot(st == 4);
+      ttc += popc_ballot(at_tt);
+      nac += popc_ballot(at_na);
+    });
+    // Wave list: the lane bests above every lane's second best (top 2) + bound.
+    uint64_t bound = wave_max_u64(second);
+    uint64_t c = best > bound ? best : 0;
+    const uint64_t k1 = wave_max_u64(c);
+    if (c == k1) c = 0;
+    const uint64_t k2 = wave_max_u64(c);
+    if (c == k2) c = 0;
+    const uint64_t k3 = wave_max_u64(c);
+    bound = k3 > bound ? k3 : bound;
+    if (lane == 0) {
+      const uint32_t pl = pi - p0;
+      s_keys[pl][wid][0] = k1;
+      s_keys[pl][wid][1] = k2;
+      s_keys[pl][wid][2] = bound;
+      s_cnt[pl][wid][0] = feas;
+      s_cnt[pl][wid][1] = f0;
+      s_cnt[pl][wid][2] = f1;
+      s_cnt[pl][wid][3] = f2;
+      s_cnt[pl][wid][4] = f3;
+      s_cnt[pl][wid][5] = f4;
+      s_cnt[pl][wid][6] = ttc;
+      s_cnt[pl][wid][7] = nac;
+    }
+  }
+  __syncthreads();
+  // Block list per pod: top BLOCK_KEYS of the 4 wave lists above every bound.
+  const uint32_t npl = p1 - p0;
+  for (uint32_t pl = threadIdx.x; pl < npl; pl += blockDim.x) {
+    uint64_t k[2 * NW];
+    uint64_t bound = 0;
+    const uint32_t nwaves = min((uint32_t)NW, kwaves - blockIdx.x * NW);
+    static_for<NW>([&](auto W) {
+      constexpr int w = W;
+      const bool on = (uint32_t)w < nwaves;
+      k[2 * w] = on ? s_keys[pl][w][0] : 0ull;
+      k[2 * w + 1] = on ? s_keys[pl][w][1] : 0ull;
+      const uint64_t b = on ? s_keys[pl][w][2] : 0ull;
+      bound = b > bound ? b : bound;
+    });
+    sort8_desc(k);
+    bound = max(bound, k[BLOCK_KEYS]);
+    const uint32_t nk = 2 * NW;
+    BlockRec br;
+#pragma unroll
+    for (int i = 0; i < BLOCK_KEYS; ++i) br.keys[i] = (i < (int)nk && k[i] > bound) ? k[i] : 0ull;
+    br.bound = bound;
+    uint32_t cnt[NFILT + 3] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (uint32_t w = 0; w < nwaves; ++w)
+      for (int q = 0; q < NFILT + 3; ++q) cnt[q] += s_cnt[pl][w][q];
+    br.feasible = cnt[0];
+    for (int q = 0; q < NFILT; ++q) br.fails[q] = cnt[1 + q];
+    br.tt_cnt = cnt[6];
+    br.na_cnt = cnt[7];
+    const uint32_t r = p0 + pl - start;
+    a.brec[((size_t)sh * a.P + r) * a.bstride + blockIdx.x] = br;
+  }
+}
+
+// =================================================================== merge
+// Bitonic sort (descending) of s[0..m) in LDS, m a power of two.
+__device__ void bitonic_desc(uint64_t *s, uint32_t m) {
+  for (uint32_t k = 2; k <= m; k <<= 1) {
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
+        const uint32_t ixj = i ^ j;
+        if (ixj > i) {
+          const uint64_t x = s[i], y = s[ixj];
+          const bool desc = (i & k) == 0;
+          if (desc ? (x < y) : (x > y)) { s[i] = y; s[ixj] = x; }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+__device__ uint64_t block_max_u64(uint64_t v, uint64_t *scratch) {
+  v = wave_max_u64(v);
+  const uint32_t wid = threadIdx.x / WAVE, nw = (blockDim.x + WAVE - 1) / WAVE;
+  __syncthreads();
+  if (threadIdx.x % WAVE == 0) scratch[wid] = v;
+  __syncthreads();
+  uint64_t m = 0;
+  for (uint32_t i = 0; i < nw; ++i) m = scratch[i] > m ? scratch[i] : m;
+  __syncthreads();
+  return m;
+}
+
+__device__ uint32_t block_sum_u32(uint32_t v, uint32_t *scratch) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, WAVE);
+  const uint32_t wid = threadIdx.x / WAVE, nw = (blockDim.x + WAVE - 1) / WAVE;
+  __syncthreads();
+  if (threadIdx.x % WAVE == 0) scratch[wid] = v;
+  __syncthreads();
+  uint32_t s = 0;
+  for (uint32_t i = 0; i < nw; ++i) s += scratch[i];
+  __syncthreads();
+  return s;
+}
+
+// Combine `nl` sorted lists of `len` keys (each listing every key above its
+// own bound) into one sorted prefix of <= K keys with a single bound.
+// Writes header + keys to out.  Uses blockDim.x threads.
+__device__ void merge_lists(const uint64_t *keys, size_t list_stride, const uint64_t *bounds,
+                            size_t bound_stride, uint32_t nl, uint32_t len, uint32_t K, uint64_t *out,
+                            uint64_t *s_sort, uint64_t *s_scr, uint32_t *s_cnt, uint32_t *s_u32) {
+  uint64_t b = 0;
+  for (uint32_t i = threadIdx.x; i < nl; i += blockDim.x) b = max(b, bounds[i * bound_stride]);
+  b = block_max_u64(b, s_scr);
+  // Count candidates above the common bound; if more than MERGE_CAP, cut every
+  // list to c entries (raising the bound to the largest dropped key).
+  uint32_t cnt = 0;
+  for (uint32_t i = threadIdx.x; i < nl; i += blockDim.x)
+    for (uint32_t q = 0; q < len; ++q) cnt += keys[i * list_stride + q] > b;
+  cnt = block_sum_u32(cnt, s_u32);
+  if (cnt > MERGE_CAP) {
+    const uint32_t c = MERGE_CAP / nl;  // >= 1 whenever nl <= MERGE_CAP
+    uint64_t b2 = b;
+    for (uint32_t i = threadIdx.x; i < nl; i += blockDim.x)
+      if (c < len) b2 = max(b2, keys[i * list_stride + c]);
+    b = block_max_u64(b2, s_scr);
+  }
+  if (threadIdx.x == 0) *s_cnt = 0;
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < nl; i += blockDim.x)
+    for (uint32_t q = 0; q < len; ++q) {
+      const uint64_t k = keys[i * list_stride + q];
+      if (k > b) {
+        const uint32_t at = atomicAdd(s_cnt, 1u);
+        if (at < MERGE_CAP) s_sort[at] = k;
+      }
+    }
+  __syncthreads();
+  const uint32_t n = min(*s_cnt, (uint32_t)MERGE_CAP);
+  uint32_t m = 64;
+  while (m < n) m <<= 1;
+  for (uint32_t i = n + threadIdx.x; i < m; i += blockDim.x) s_sort[i] = 0;
+  __syncthreads();
+  bitonic_desc(s_sort, m);
+  const uint32_t keep = min(n, K);
+  if (n > K) b = max(b, s_sort[K]);
+  for (uint32_t i = threadIdx.x; i < K; i += blockDim.x) out[REC_HDR_WORDS + i] = i < keep ? s_sort[i] : 0ull;
+  if (threadIdx.x == 0) {
+    out[0] = b;
+    ((uint32_t *)out)[2] = keep;
+  }
+}
+
+// grid: x = pod in round, y = local shard.  Blocks -> shard record.
+__global__ __launch_bounds__(256) void merge_kernel(RoundArgs a) {
+  __shared__ uint64_t s_sort[MERGE_CAP];
+  __shared__ uint64_t s_scr[16];
+  __shared__ uint32_t s_u32[16];
+  __shared__ uint32_t s_cnt;
+  const uint32_t start = uniform_u32(*a.d_start);
+  const uint32_t r = blockIdx.x;
+  if (start + r >= a.npods || r >= a.P) return;
+  const uint32_t sh = blockIdx.y;
+  const Shard s = a.shards[a.shard0 + sh];
+  const uint32_t nb = (s.waves * a.sub + 3) / 4;
+  const BlockRec *br = a.brec + ((size_t)sh * a.P + r) * a.bstride;
+  uint64_t *out = a.srec + ((size_t)(a.shard0 + sh) * a.P + r) * rec_words(a.K);
+  merge_lists(&br[0].keys[0], sizeof(BlockRec) / 8, &br[0].bound, sizeof(BlockRec) / 8, nb, BLOCK_KEYS, a.K,
+              out, s_sort, s_scr, &s_cnt, s_u32);
+  // counts
+  uint32_t c[NFILT + 3];
+  for (int q = 0; q < NFILT + 3; ++q) c[q] = 0;
+  for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) {
+    c[0] += br[i].feasible;
+    for (int q = 0; q < NFILT; ++q) c[1 + q] += br[i].fails[q];
+    c[6] += br[i].tt_cnt;
+    c[7] += br[i].na_cnt;
+  }
+  for (int q = 0; q < NFILT + 3; ++q) c[q] = block_sum_u32(c[q], s_u32);
+  if (threadIdx.x == 0) {
+    ShardRecHdr *h = (ShardRecHdr *)out;
+    h->feasible = c[0];
+    for (int q = 0; q < NFILT; ++q) h->fails[q] = c[1 + q];
+    h->tt_cnt = c[6];
+    h->na_cnt = c[7];
+  }
+}
+
+// grid: x = pod in round.  Shard records -> final record.
+__global__ __launch_bounds__(256) void merge_shards_kernel(RoundArgs a) {
+  __shared__ uint64_t s_sort[MERGE_CAP];
+  __shared__ uint64_t s_scr[16];
+  __shared__ uint32_t s_u32[16];
+  __shared__ uint32_t s_cnt;
+  const uint32_t start = uniform_u32(*a.d_start);
+  const uint32_t r = blockIdx.x;
+  if (start + r >= a.npods || r >= a.P) return;
+  const uint32_t W = rec_words(a.K);
+  const uint64_t *in = a.srec + (size_t)r * W;
+  const size_t stride = (size_t)a.P * W;  // between shards
+  uint64_t *out = a.frec + (size_t)r * W;
+  merge_lists(in + REC_HDR_WORDS, stride, in, stride, a.total_shards, a.K, a.K, out, s_sort, s_scr, &s_cnt, s_u32);
+  if (threadIdx.x == 0) {
+    ShardRecHdr *h = (ShardRecHdr *)out;
+    uint32_t f = 0, ttc = 0, nac = 0, fl[NFILT] = {0, 0, 0, 0, 0};
+    for (uint32_t q = 0; q < a.total_shards; ++q) {
+      const ShardRecHdr *x = (const ShardRecHdr *)(in + q * stride);
+      f += x->feasible;
+      ttc += x->tt_cnt;
+      nac += x->na_cnt;
+      for (int z = 0; z < NFILT; ++z) fl[z] += x->fails[z];
+    }
+    h->feasible = f;
+    h->tt_cnt = ttc;
+    h->na_cnt = nac;
+    for (int z = 0; z < NFILT; ++z) h->fails[z] = fl[z];
+  }
+}
+
+// ================================================================= resolve
+// One workgroup walks the round's pods in queue order:
+// pod i's winner is the best of (a) its first listed candidate that no pod
+// < i modified (its key is unchanged: same row, same normalisation max) and
+// (b) every modified node re-scored against the live row.  If neither is
+// provably the maximum (every listed candidate modified and the best
+// modified key not above the list bound), or a normalising plugin's max may
+// have moved, the round ends before pod i and the next sweep restarts there.
+//
+// Latency design: every pod descriptor / record header of the round is
+// staged in LDS up front; the next pod's candidate keys and their S0 rows are
+// prefetched into registers while the current pod resolves; modified rows
+// (S0 and live) live in LDS; the decision is recomputed by every thread from
+// the per-wave partials, so each pod costs two barriers.
+constexpr int RESOLVE_THREADS = 512;
+constexpr int RNW = RESOLVE_THREADS / WAVE;
+constexpr int RHASH = 1024;
+
+__device__ __forceinline__ uint32_t rhash(uint32_t x) { return (x * 2654435761u) >> 22; }  // 10 bits
+
+__device__ __forceinline__ uint32_t slot_position(const RoundArgs &a, uint32_t slot) {
+  for (uint32_t q = 0; q < a.total_shards; ++q) {
+    const Shard sq = a.shards[q];
+    if (slot - sq.lo < sq.count) return shard_pos(sq, a.lnpl, slot - sq.lo);
+  }
+  return 0;
+}
+
+// A node row as prefetched into registers (S0 = round-start state).
+struct RowRegs {
+  int64_t acpu, amem, rc, rm, zc, zm;
+  int32_t apods, np;
+  uint32_t pos;
+};
+
+__device__ __forceinline__ void fetch_row(const RoundArgs &a, uint32_t pos, RowRegs &w) {
+  w.pos = pos;
+  w.acpu = a.t.acpu[pos];
+  w.amem = a.t.amem[pos];
+  w.rc = a.t.rcpu[pos];
+  w.rm = a.t.rmem[pos];
+  w.zc = a.t.zcpu[pos];
+  w.zm = a.t.zmem[pos];
+  w.apods = a.t.apods[pos];
+  w.np = a.t.npods[pos];
+}
+
+__device__ __forceinline__ NodeRegs regs_from(int64_t acpu, int64_t amem, int64_t rc, int64_t rm, int64_t zc,
+                                              int64_t zm, int32_t apods, int32_t np, uint32_t slot) {
+  NodeRegs r;
+  r.slot = slot;
+  r.free_cpu = acpu - rc;
+  r.free_mem = amem - rm;
+  r.rcpu = rc;
+  r.rmem = rm;
+  r.lfree_cpu = acpu - zc;
+  r.lfree_mem = amem - zm;
+  r.acpu_d = (double)acpu;
+  r.amem_d = (double)amem;
+  r.inv_cpu = acpu ? 1.0 / r.acpu_d : 1.0;
+  r.inv_mem = amem ? 1.0 / r.amem_d : 1.0;
+  r.bits = 1u | ((int64_t)np + 1 <= (int64_t)apods ? 2u : 0u) | (acpu ? 4u : 0u) | (amem ? 8u : 0u);
+  return r;
+}
+
+template <bool EXT>
+__global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
+  // round inputs
+  __shared__ PodDev s_pod[MAX_P];
+  __shared__ ShardRecHdr s_hdr[MAX_P];
+  __shared__ uint32_t s_norm[MAX_P][2];
+  // modified nodes: S0 row, live requested state, ext columns
+  __shared__ uint32_t s_mslot[MAX_P], s_mpos[MAX_P];
+  __shared__ int64_t s_acpu[MAX_P], s_amem[MAX_P];
+  __shared__ int64_t s_rc0[MAX_P], s_rm0[MAX_P], s_zc0[MAX_P], s_zm0[MAX_P];
+  __shared__ int64_t s_rc[MAX_P], s_rm[MAX_P], s_zc[MAX_P], s_zm[MAX_P];
+  __shared__ int32_t s_apods[MAX_P], s_np0[MAX_P], s_np[MAX_P];
+  __shared__ uint64_t s_ext[EXT ? MAX_P : 1][2 + LW + NNUM];
+  __shared__ uint32_t s_hkey[RHASH];
+  __shared__ uint16_t s_hval[RHASH];
+  // per-wave partials
+  __shared__ uint64_t s_wkey[RNW];      // best modified key
+  __shared__ uint32_t s_widx[RNW];      // first unmodified list index
+  __shared__ uint64_t s_wlk[RNW];       // its key
+  __shared__ int32_t s_wd[RNW][NFILT + 3];
+  __shared__ uint32_t s_wany[RNW];
+  __shared__ uint32_t s_nmod;
+  __shared__ uint32_t s_stop;
+
+  const uint32_t tid = threadIdx.x, lane = tid % WAVE, wid = tid / WAVE;
+  const uint32_t start = uniform_u32(*a.d_start);
+  if (start >= a.npods) return;
+  const uint32_t nround = min(a.P, a.npods - start);
+  const uint32_t RW = rec_words(a.K);
+  // ---- stage the round
+  for (uint32_t i = tid; i < nround; i += RESOLVE_THREADS) {
+    s_pod[i] = a.pods[start + i];
+    s_hdr[i] = *(const ShardRecHdr *)(a.frec + (size_t)i * RW);
+    s_norm[i][0] = a.norm_max[2 * i];
+    s_norm[i][1] = a.norm_max[2 * i + 1];
+  }
+  for (uint32_t i = tid; i < RHASH; i += RESOLVE_THREADS) s_hkey[i] = 0;
+  if (tid == 0) { s_nmod = 0; s_stop = nround; }
+  // prefetch pod 0's candidates (thread t holds list entry t) and their S0 rows
+  uint64_t ck = 0;
+  RowRegs crow{};
+  uint64_t cext[2 + LW + NNUM];
+  auto prefetch = [&](uint32_t r, uint64_t &k, RowRegs &w, uint64_t *ex) {
+    k = 0;
+    if (r < nround && tid < a.K) {
+      k = a.frec[(size_t)r * RW + REC_HDR_WORDS + tid];
+      if (k) {
+        fetch_row(a, slot_position(a, 0xFFFFFFFFu - (uint32_t)k), w);
+        if (EXT) {
+          ex[0] = a.t.hard[w.pos];
+          ex[1] = a.t.prefer[w.pos];
+#pragma unroll
+          for (int q = 0; q < LW; ++q) ex[2 + q] = a.t.lab[(size_t)q * a.t.npos + w.pos];
+#pragma unroll
+          for (int q = 0; q < NNUM; ++q) ex[2 + LW + q] = (uint64_t)a.t.num[(size_t)q * a.t.npos + w.pos];
+        }
+      }
+    }
+  };
+  prefetch(0, ck, crow, cext);
+  __syncthreads();
+
+  for (uint32_t r = 0; r < nround; ++r) {
+    const PodDev &p = s_pod[r];
+    const ShardRecHdr &hdr = s_hdr[r];
+    const uint32_t pi = start + r;
+    int64_t tt_max = 0, na_max = 0;
+    if (EXT) {
+      tt_max = s_norm[r][0];
+      na_max = s_norm[r][1];
+    }
+    // next pod's candidates: issued now, consumed next iteration
+    uint64_t nk;
+    RowRegs nrow{};
+    uint64_t next_ext[2 + LW + NNUM];
+    prefetch(r + 1, nk, nrow, next_ext);
+
+    // (a) re-score modified nodes against the live rows
+    const uint32_t nmod = s_nmod;
+    uint64_t mkey = 0;
+    int32_t d[NFILT + 3] = {0, 0, 0, 0, 0, 0, 0, 0};
+    bool dany = false;
+    for (uint32_t m = tid; m < nmod; m += RESOLVE_THREADS) {
+      NodeExt e;
+      if (EXT) {
+        e.hard = s_ext[m][0];
+        e.prefer = s_ext[m][1];
+#pragma unroll
+        for (int q = 0; q < LW; ++q) e.lab[q] = s_ext[m][2 + q];
+#pragma unroll
+        for (int q = 0; q < NNUM; ++q) e.num[q] = (int64_t)s_ext[m][2 + LW + q];
+      }
+      const uint32_t slot = s_mslot[m];
+      const NodeRegs r0 = regs_from(s_acpu[m], s_amem[m], s_rc0[m], s_rm0[m], s_zc0[m], s_zm0[m], s_apods[m],
+                                    s_np0[m], slot);
+      const NodeRegs ri = regs_from(s_acpu[m], s_amem[m], s_rc[m], s_rm[m], s_zc[m], s_zm[m], s_apods[m],
+                                    s_np[m], slot);
+      const int st0 = filter<EXT>(p, a.clauses, r0, e);
+      const int sti = filter<EXT>(p, a.clauses, ri, e);
+      if (sti == ST_FEASIBLE) {
+        const uint64_t k = pack_key(total_score<EXT>(p, a.clauses, ri, e, a.w, tt_max, na_max), slot);
+        mkey = k > mkey ? k : mkey;
+      }
+      if (st0 != sti) {
+        dany = true;
+        d[0] += (st0 == ST_FEASIBLE) - (sti == ST_FEASIBLE);
+#pragma unroll
+        for (int q = 0; q < NFILT; ++q) d[1 + q] += (sti == q) - (st0 == q);
+        if (EXT && st0 == ST_FEASIBLE) {
+          if (p.flags & PF_TT) d[6] += taint_raw(p, e) == tt_max;
+          if (p.flags & PF_NA) d[7] += preferred_raw(p, a.clauses, e, slot) == na_max;
+        }
+      }
+    }
+    // (b) is my listed candidate unmodified?
+    bool unmod = false;
+    if (ck != 0 && tid < hdr.nkeys) {
+      const uint32_t slot = 0xFFFFFFFFu - (uint32_t)ck;
+      uint32_t h = rhash(slot);
+      unmod = true;
+      while (s_hkey[h] != 0) {
+        if (s_hkey[h] == slot + 1) { unmod = false; break; }
+        h = (h + 1) & (RHASH - 1);
+      }
+    }
+    // wave partials
+    const uint64_t ub = __ballot(unmod);
+    const uint64_t wmkey = wave_max_u64(mkey);
+    const bool wdany = __ballot(dany) != 0;
+    if (wdany) {
+#pragma unroll
+      for (int q = 0; q < NFILT + 3; ++q) {
+        int32_t v = d[q];
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, WAVE);
+        d[q] = v;
+      }
+    }
+    if (lane == 0) {
+      s_wkey[wid] = wmkey;
+      s_wany[wid] = wdany;
+      if (wdany)
+        for (int q = 0; q < NFILT + 3; ++q) s_wd[wid][q] = d[q];
+    }
+    if (ub) {
+      const uint32_t first = (uint32_t)__builtin_ctzll(ub);
+      const uint64_t fk = __shfl(ck, (int)first, WAVE);
+      if (lane == 0) { s_widx[wid] = wid * WAVE + first; s_wlk[wid] = fk; }
+    } else if (lane == 0) {
+      s_widx[wid] = 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    // every thread combines the partials (identical decision, no broadcast barrier)
+    uint64_t bm = 0, ku = 0;
+    uint32_t fu = 0xFFFFFFFFu;
+    int32_t sum[NFILT + 3] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int w = 0; w < RNW; ++w) {
+      bm = s_wkey[w] > bm ? s_wkey[w] : bm;
+      if (s_widx[w] < fu) { fu = s_widx[w]; ku = s_wlk[w]; }
+      if (s_wany[w])
+        for (int q = 0; q < NFILT + 3; ++q) sum[q] += s_wd[w][q];
+    }
+    const uint32_t feasible = hdr.feasible - (uint32_t)sum[0];
+    int32_t status = 0;
+    bool stop = false;
+    uint64_t win = 0;
+    if (feasible == 0) {
+      status = 1;  // KS_POD_UNSCHEDULABLE
+    } else if ((p.flags & PF_PREF_ERR) && feasible >= 2) {
+      status = 2;  // KS_POD_ERROR (NodeAffinity PreScore)
+    } else if ((EXT && (p.flags & PF_TT) && hdr.tt_cnt - (uint32_t)sum[6] == 0) ||
+               (EXT && (p.flags & PF_NA) && hdr.na_cnt - (uint32_t)sum[7] == 0)) {
+      stop = true;  // a normaliser's max may have moved: re-sweep from this pod
+    } else if (fu != 0xFFFFFFFFu) {
+      win = ku > bm ? ku : bm;
+    } else if (bm > hdr.bound) {
+      win = bm;
+    } else {
+      stop = true;  // candidates exhausted
+    }
+    if (stop) {
+      if (tid == 0) s_stop = r;
+      break;  // uniform
+    }
+    if (tid == 0) {
+      DevResult res;
+      res.node_index = win ? (int32_t)(0xFFFFFFFFu - (uint32_t)win) : -1;
+      res.status = status;
+      res.total_score = win ? (int64_t)(win >> 32) - 1 : 0;
+      res.feasible_nodes = feasible;
+      res.evaluated_nodes = a.evaluated;
+      for (int q = 0; q < NFILT; ++q) res.fail_counts[q] = hdr.fails[q] + (uint32_t)sum[1 + q];
+      res.flags = (win && feasible == 1) ? 1u : 0u;
+      ((DevResult *)a.results)[pi] = res;
+    }
+    // commit (AssumePod -> NodeInfo.AddPod on the live row): exactly one thread
+    if (win) {
+      if (win == ku && fu != 0xFFFFFFFFu && tid == fu) {
+        // a listed, unmodified node: enters the modified set with its prefetched S0 row
+        const uint32_t slot = 0xFFFFFFFFu - (uint32_t)ck;
+        const uint32_t m = s_nmod;
+        uint32_t h = rhash(slot);
+        while (s_hkey[h] != 0) h = (h + 1) & (RHASH - 1);
+        s_hkey[h] = slot + 1;
+        s_hval[h] = (uint16_t)m;
+        s_mslot[m] = slot;
+        s_mpos[m] = crow.pos;
+        s_acpu[m] = crow.acpu;
+        s_amem[m] = crow.amem;
+        s_rc0[m] = crow.rc;
+        s_rm0[m] = crow.rm;
+        s_zc0[m] = crow.zc;
+        s_zm0[m] = crow.zm;
+        s_apods[m] = crow.apods;
+        s_np0[m] = crow.np;
+        s_rc[m] = crow.rc + p.req_cpu;
+        s_rm[m] = crow.rm + p.req_mem;
+        s_zc[m] = crow.zc + p.nz_cpu;
+        s_zm[m] = crow.zm + p.nz_mem;
+        s_np[m] = crow.np + 1;
+        if (EXT)
+          for (int q = 0; q < 2 + LW + NNUM; ++q) s_ext[m][q] = cext[q];
+        s_nmod = m + 1;
+      } else if (win == bm && win != ku) {
+        for (uint32_t m = tid; m < nmod; m += RESOLVE_THREADS) {
+          if (s_mslot[m] == 0xFFFFFFFFu - (uint32_t)win) {
+            s_rc[m] += p.req_cpu;
+            s_rm[m] += p.req_mem;
+            s_zc[m] += p.nz_cpu;
+            s_zm[m] += p.nz_mem;
+            s_np[m] += 1;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    ck = nk;
+    crow = nrow;
+    if (EXT)
+      for (int q = 0; q < 2 + LW + NNUM; ++q) cext[q] = next_ext[q];
+  }
+  __syncthreads();
+  // write back live rows of modified nodes and advance the queue
+  const uint32_t nmod = s_nmod;
+  for (uint32_t i = tid; i < nmod; i += RESOLVE_THREADS) {
+    const uint32_t pos = s_mpos[i];
+    a.t.rcpu[pos] = s_rc[i];
+    a.t.rmem[pos] = s_rm[i];
+    a.t.zcpu[pos] = s_zc[i];
+    a.t.zmem[pos] = s_zm[i];
+    a.t.npods[pos] = s_np[i];
+  }
+  if (tid == 0) {
+    *a.d_start = start + s_stop;
+    a.counters[0] += 1;                                   // rounds
+    a.counters[1] += s_stop;                              // pods resolved
+    a.counters[2] += nround;                              // pods swept
+  }
+}
+
+// ============================================================ table updates
+
+// Scatter full rows (upsert) into positions.
+__global__ void scatter_rows_kernel(NodeTable t, const uint32_t *pos, const int64_t *core, const uint64_t *ext,
+                                    uint32_t n, uint32_t flags) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t p = pos[i];
+  if (!(flags & 2u)) {  // core row (flags 0: core only, 1: core + ext, 2: ext only)
+    const int64_t *c = core + (size_t)i * 8;  // acpu amem apods new
+    t.acpu[p] = c[0];
+    t.amem[p] = c[1];
+    t.apods[p] = (int32_t)c[2];
+    if (c[3]) {  // new node or delete: reset requested state
+      t.rcpu[p] = 0;
+      t.rmem[p] = 0;
+      t.zcpu[p] = 0;
+      t.zmem[p] = 0;
+      t.npods[p] = 0;
+    }
+  }
+  if (flags & 3u) {
+    const uint64_t *e = ext + (size_t)i * (2 + LW + NNUM);
+    t.hard[p] = e[0];
+    t.prefer[p] = e[1];
+    for (int k = 0; k < LW; ++k) t.lab[(size_t)k * t.npos + p] = e[2 + k];
+    for (int k = 0; k < NNUM; ++k) t.num[(size_t)k * t.npos + p] = (int64_t)e[2 + LW + k];
+  }
+}
+
+// Pod add/remove events: atomic deltas on the requested state.
+__global__ void apply_deltas_kernel(NodeTable t, const uint32_t *pos, const int64_t *delta, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t p = pos[i];
+  const int64_t *d = delta + (size_t)i * 5;
+  atomicAdd((unsigned long long *)&t.rcpu[p], (unsigned long long)d[0]);
+  atomicAdd((unsigned long long *)&t.rmem[p], (unsigned long long)d[1]);
+  atomicAdd((unsigned long long *)&t.zcpu[p], (unsigned long long)d[2]);
+  atomicAdd((unsigned long long *)&t.zmem[p], (unsigned long long)d[3]);
+  atomicAdd(&t.npods[p], (int32_t)d[4]);
+}
+
+__global__ void gather_rows_kernel(NodeTable t, const uint32_t *pos, int64_t *out, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t p = pos[i];
+  int64_t *o = out + (size_t)i * 8;
+  o[0] = t.acpu[p];
+  o[1] = t.amem[p];
+  o[2] = t.rcpu[p];
+  o[3] = t.rmem[p];
+  o[4] = t.zcpu[p];
+  o[5] = t.zmem[p];
+  o[6] = t.apods[p];
+  o[7] = t.npods[p];
+}
+
+// Full relabel of one label word column (dictionary growth).
+__global__ void scatter_u64_kernel(uint64_t *col, const uint32_t *pos, const uint64_t *val, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) col[pos[i]] = val[i];
+}
+
+// ============================================================ score dump
+// One pod against every position of every shard: per-plugin scores.
+__global__ void dump_max_kernel(DumpArgs a) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.nslots) return;
+  const uint32_t pos = a.slot_pos[i];
+  if (pos == 0xFFFFFFFFu) return;
+  NodeRegs r;
+  NodeExt e;
+  load_core(a.t, pos, i, true, r);
+  if (!(r.bits & 1u)) return;
+  load_ext(a.t, pos, true, e);
+  const PodDev p = a.pods[0];
+  if (filter<true>(p, a.clauses, r, e) != ST_FEASIBLE) return;
+  if (p.flags & PF_TT) atomicMax(&a.norm_max[0], (uint32_t)taint_raw(p, e));
+  if (p.flags & PF_NA) atomicMax(&a.norm_max[1], (uint32_t)preferred_raw(p, a.clauses, e, i));
+}
+
+__global__ void dump_scores_kernel(DumpArgs a) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.nslots) return;
+  const uint32_t pos = a.slot_pos[i];
+  int32_t *o = a.out + (size_t)i * 10;
+  for (int q = 0; q < 10; ++q) o[q] = 0;
+  if (pos == 0xFFFFFFFFu) { o[0] = ST_EMPTY; return; }
+  NodeRegs r;
+  NodeExt e;
+  load_core(a.t, pos, i, true, r);
+  if (!(r.bits & 1u)) { o[0] = ST_EMPTY; return; }
+  load_ext(a.t, pos, true, e);
+  const PodDev p = a.pods[0];
+  const int st = filter<true>(p, a.clauses, r, e);
+  o[0] = st;
+  if (st != ST_FEASIBLE) return;
+  const int64_t tt_max = a.norm_max[0], na_max = a.norm_max[1];
+  o[1] = (int32_t)score_la(p, r);
+  o[2] = (int32_t)score_ba(p, r);
+  const int64_t tr = (p.flags & PF_TT) ? taint_raw(p, e) : 0;
+  o[3] = (int32_t)tr;
+  o[4] = (int32_t)normalize(tr, (p.flags & PF_TT) ? tt_max : 0, true);
+  const int64_t nr = (p.flags & PF_NA) ? preferred_raw(p, a.clauses, e, i) : 0;
+  o[5] = (int32_t)nr;
+  o[6] = (p.flags & PF_HAS_PREF) ? (int32_t)normalize(nr, (p.flags & PF_NA) ? na_max : 0, false) : 0;
+  o[7] = 0;
+  const int64_t tot = total_score<true>(p, a.clauses, r, e, a.w, tt_max, na_max);
+  o[8] = (int32_t)(tot & 0xFFFFFFFF);
+  o[9] = (int32_t)(tot >> 32);
+}
+
+// ============================================================== launchers
+
+#define KS_CHECK(x)                          \
+  do {                                       \
+    hipError_t e_ = (x);                     \
+    if (e_ != hipSuccess) return e_;         \
+  } while (0)
+
+hipError_t launch_prescore(const RoundArgs &a, uint32_t nblocks, uint32_t ngroups, uint32_t nshards,
+                           hipStream_t st) {
+  dim3 g(nblocks, ngroups, nshards);
+  if (a.npl == 2) prescore_kernel<2><<<g, SWEEP_THREADS, 0, st>>>(a);
+  else if (a.npl == 4) prescore_kernel<4><<<g, SWEEP_THREADS, 0, st>>>(a);
+  else prescore_kernel<8><<<g, SWEEP_THREADS, 0, st>>>(a);
+  return hipGetLastError();
+}
+
+hipError_t launch_sweep(const RoundArgs &a, bool ext, uint32_t nblocks, uint32_t ngroups, uint32_t nshards,
+                        hipStream_t st) {
+  dim3 g(nblocks, ngroups, nshards);
+  if (ext) {
+    if (a.npl == 2) sweep_kernel<2, true><<<g, SWEEP_THREADS, 0, st>>>(a);
+    else if (a.npl == 4) sweep_kernel<4, true><<<g, SWEEP_THREADS, 0, st>>>(a);
+    else sweep_kernel<8, true><<<g, SWEEP_THREADS, 0, st>>>(a);
+  } else {
+    if (a.npl == 2) sweep_kernel<2, false><<<g, SWEEP_THREADS, 0, st>>>(a);
+    else if (a.npl == 4) sweep_kernel<4, false><<<g, SWEEP_THREADS, 0, st>>>(a);
+    else sweep_kernel<8, false><<<g, SWEEP_THREADS, 0, st>>>(a);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_merge(const RoundArgs &a, uint32_t nshards, hipStream_t st) {
+  merge_kernel<<<dim3(a.P, nshards), 256, 0, st>>>(a);
+  return hipGetLastError();
+}
+
+hipError_t launch_merge_shards(const RoundArgs &a, hipStream_t st) {
+  merge_shards_kernel<<<dim3(a.P), 256, 0, st>>>(a);
+  return hipGetLastError();
+}
+
+hipError_t launch_resolve(const RoundArgs &a, bool ext, hipStream_t st) {
+  if (ext) resolve_kernel<true><<<1, RESOLVE_THREADS, 0, st>>>(a);
+  else resolve_kernel<false><<<1, RESOLVE_THREADS, 0, st>>>(a);
+  return hipGetLastError();
+}
+
+hipError_t launch_scatter_rows(const NodeTable &t, const uint32_t *pos, const int64_t *core, const uint64_t *ext,
+                               uint32_t n, uint32_t flags, hipStream_t st) {
+  if (!n) return hipSuccess;
+  scatter_rows_kernel<<<(n + 255) / 256, 256, 0, st>>>(t, pos, core, ext, n, flags);
+  return hipGetLastError();
+}
+
+hipError_t launch_apply_deltas(const NodeTable &t, const uint32_t *pos, const int64_t *delta, uint32_t n,
+                               hipStream_t st) {
+  if (!n) return hipSuccess;
+  apply_deltas_kernel<<<(n + 255) / 256, 256, 0, st>>>(t, pos, delta, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_gather_rows(const NodeTable &t, const uint32_t *pos, int64_t *out, uint32_t n, hipStream_t st) {
+  if (!n) return hipSuccess;
+  gather_rows_kernel<<<(n + 255) / 256, 256, 0, st>>>(t, pos, out, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_scatter_u64(uint64_t *col, const uint32_t *pos, const uint64_t *val, uint32_t n,
+                              hipStream_t st) {
+  if (!n) return hipSuccess;
+  scatter_u64_kernel<<<(n + 255) / 256, 256, 0, st>>>(col, pos, val, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_dump(const DumpArgs &a, hipStream_t st) {
+  const uint32_t g = (a.nslots + 255) / 256;
+  dump_max_kernel<<<g, 256, 0, st>>>(a);
+  KS_CHECK(hipGetLastError());
+  dump_scores_kernel<<<g, 256, 0, st>>>(a);
+  return hipGetLastError();
+}
+
+}  // namespace ks

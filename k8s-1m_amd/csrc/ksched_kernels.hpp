@@ -1,0 +1,66 @@
+// ksched_kernels.hpp — launch arguments and launchers of the gfx950 kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "ksched_dev.hpp"
+
+namespace ks {
+
+constexpr int MAX_PG = 64;    // pods per sweep block (LDS wave records)
+constexpr int MAX_P = 256;    // pods per round (resolve stages the round in LDS)
+
+struct RoundArgs {
+  NodeTable t;
+  const Shard *shards;        // geometry of every shard, device memory (global ids)
+  uint32_t total_shards;      // S
+  uint32_t shard0;            // first global shard handled by this launch (grid.z / grid.y)
+  uint32_t npl;               // nodes per lane of the sweep / prescore kernel
+  uint32_t sub;               // layout nodes-per-lane / kernel nodes-per-lane
+  uint32_t P;                 // pods per round
+  uint32_t pg;                // pods per sweep block
+  uint32_t K;                 // candidates per pod record
+  uint32_t npods;             // batch size
+  uint32_t bstride;           // BlockRec stride between pods (max blocks per shard)
+  uint32_t evaluated;         // present nodes (EvaluatedNodes with pct = 100)
+  uint32_t lnpl;              // layout nodes per lane (positions of committed slots)
+  const PodDev *pods;
+  const uint64_t *clauses;
+  uint32_t *d_start;          // next unresolved pod of the batch (device-driven rounds)
+  uint32_t *norm_max;         // [P][2] max raw TaintToleration / NodeAffinity (atomicMax, all shards)
+  BlockRec *brec;             // [local shards][P][bstride]
+  uint64_t *srec;             // [S][P][rec_words(K)]
+  uint64_t *frec;             // [P][rec_words(K)] (== srec when S == 1)
+  void *results;              // DevResult[npods]
+  uint64_t *counters;         // [0] rounds, [1] pods resolved
+  Weights w;
+};
+
+struct DumpArgs {
+  NodeTable t;
+  const uint32_t *slot_pos;   // position of each slot
+  uint32_t nslots;
+  const PodDev *pods;         // one pod
+  const uint64_t *clauses;
+  uint32_t *norm_max;         // [2], zeroed
+  int32_t *out;               // [nslots][10]
+  Weights w;
+};
+
+hipError_t launch_prescore(const RoundArgs &a, uint32_t nblocks, uint32_t ngroups, uint32_t nshards,
+                           hipStream_t st);
+hipError_t launch_sweep(const RoundArgs &a, bool ext, uint32_t nblocks, uint32_t ngroups, uint32_t nshards,
+                        hipStream_t st);
+hipError_t launch_merge(const RoundArgs &a, uint32_t nshards, hipStream_t st);
+hipError_t launch_merge_shards(const RoundArgs &a, hipStream_t st);
+hipError_t launch_resolve(const RoundArgs &a, bool ext, hipStream_t st);
+hipError_t launch_scatter_rows(const NodeTable &t, const uint32_t *pos, const int64_t *core, const uint64_t *ext,
+                               uint32_t n, uint32_t flags, hipStream_t st);
+hipError_t launch_apply_deltas(const NodeTable &t, const uint32_t *pos, const int64_t *delta, uint32_t n,
+                               hipStream_t st);
+hipError_t launch_gather_rows(const NodeTable &t, const uint32_t *pos, int64_t *out, uint32_t n, hipStream_t st);
+hipError_t launch_scatter_u64(uint64_t *col, const uint32_t *pos, const uint64_t *val, uint32_t n,
+                              hipStream_t st);
+hipError_t launch_dump(const DumpArgs &a, hipStream_t st);
+
+}  // namespace ks

@@ -1,0 +1,287 @@
+"""ctypes mirror of include/ksched.h and include/ksynth.h.
+
+Struct layouts must match the C headers byte for byte; tests/test_abi.py checks
+sizes and that every declared symbol is exported by the built libraries.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+LIB_DIR = Path(__file__).resolve().parent / "lib"
+
+c_char_p = C.c_char_p
+
+
+class KsLabel(C.Structure):
+    _fields_ = [("key", c_char_p), ("value", c_char_p)]
+
+
+class KsTaint(C.Structure):
+    _fields_ = [("key", c_char_p), ("value", c_char_p), ("effect", C.c_int32), ("_pad", C.c_int32)]
+
+
+class KsToleration(C.Structure):
+    _fields_ = [("key", c_char_p), ("value", c_char_p), ("op", C.c_int32), ("effect", C.c_int32)]
+
+
+class KsNode(C.Structure):
+    _fields_ = [
+        ("name", c_char_p),
+        ("alloc_milli_cpu", C.c_int64),
+        ("alloc_memory", C.c_int64),
+        ("alloc_pods", C.c_int64),
+        ("labels", C.POINTER(KsLabel)),
+        ("taints", C.POINTER(KsTaint)),
+        ("n_labels", C.c_uint32),
+        ("n_taints", C.c_uint32),
+        ("unschedulable", C.c_uint32),
+        ("_pad", C.c_uint32),
+    ]
+
+
+class KsContainer(C.Structure):
+    _fields_ = [
+        ("milli_cpu", C.c_int64),
+        ("memory", C.c_int64),
+        ("flags", C.c_uint32),
+        ("restart_always", C.c_uint32),
+    ]
+
+
+class KsRequirement(C.Structure):
+    _fields_ = [
+        ("key", c_char_p),
+        ("values", C.POINTER(c_char_p)),
+        ("n_values", C.c_uint32),
+        ("op", C.c_int32),
+    ]
+
+
+class KsTerm(C.Structure):
+    _fields_ = [
+        ("match_expressions", C.POINTER(KsRequirement)),
+        ("match_fields", C.POINTER(KsRequirement)),
+        ("n_expressions", C.c_uint32),
+        ("n_fields", C.c_uint32),
+    ]
+
+
+class KsPreferredTerm(C.Structure):
+    _fields_ = [("preference", KsTerm), ("weight", C.c_int32), ("_pad", C.c_int32)]
+
+
+class KsPod(C.Structure):
+    _fields_ = [
+        ("ns", c_char_p),
+        ("name", c_char_p),
+        ("containers", C.POINTER(KsContainer)),
+        ("init_containers", C.POINTER(KsContainer)),
+        ("tolerations", C.POINTER(KsToleration)),
+        ("node_selector", C.POINTER(KsLabel)),
+        ("required_terms", C.POINTER(KsTerm)),
+        ("preferred", C.POINTER(KsPreferredTerm)),
+        ("node_name", c_char_p),
+        ("overhead_milli_cpu", C.c_int64),
+        ("overhead_memory", C.c_int64),
+        ("n_containers", C.c_uint32),
+        ("n_init_containers", C.c_uint32),
+        ("n_tolerations", C.c_uint32),
+        ("n_node_selector", C.c_uint32),
+        ("n_required_terms", C.c_uint32),
+        ("has_required", C.c_uint32),
+        ("n_preferred", C.c_uint32),
+        ("has_preferred", C.c_uint32),
+        ("has_overhead", C.c_uint32),
+        ("_pad", C.c_uint32),
+    ]
+
+
+NUM_FILTER_PLUGINS = 5
+
+
+class KsResult(C.Structure):
+    _fields_ = [
+        ("node_index", C.c_int32),
+        ("status", C.c_int32),
+        ("total_score", C.c_int64),
+        ("feasible_nodes", C.c_uint32),
+        ("evaluated_nodes", C.c_uint32),
+        ("fail_counts", C.c_uint32 * NUM_FILTER_PLUGINS),
+        ("flags", C.c_uint32),
+    ]
+
+
+class KsNodeScore(C.Structure):
+    _fields_ = [
+        ("status", C.c_int32),
+        ("least_allocated", C.c_int32),
+        ("balanced_allocation", C.c_int32),
+        ("taint_raw", C.c_int32),
+        ("taint_score", C.c_int32),
+        ("affinity_raw", C.c_int32),
+        ("affinity_score", C.c_int32),
+        ("image_locality", C.c_int32),
+        ("total_score", C.c_int64),
+    ]
+
+
+class KsNodeState(C.Structure):
+    _fields_ = [
+        ("alloc_milli_cpu", C.c_int64),
+        ("alloc_memory", C.c_int64),
+        ("req_milli_cpu", C.c_int64),
+        ("req_memory", C.c_int64),
+        ("nonzero_milli_cpu", C.c_int64),
+        ("nonzero_memory", C.c_int64),
+        ("alloc_pods", C.c_int32),
+        ("pod_count", C.c_int32),
+    ]
+
+
+class KsConfig(C.Structure):
+    _fields_ = [
+        ("device", C.c_int32),
+        ("node_capacity", C.c_uint32),
+        ("pods_per_round", C.c_uint32),
+        ("topk", C.c_uint32),
+        ("nodes_per_lane", C.c_uint32),
+        ("world_size", C.c_uint32),
+        ("rank", C.c_uint32),
+        ("virtual_shards", C.c_uint32),
+        ("weight_fit", C.c_int32),
+        ("weight_balanced", C.c_int32),
+        ("weight_taint", C.c_int32),
+        ("weight_affinity", C.c_int32),
+        ("weight_image", C.c_int32),
+        ("_pad", C.c_uint32),
+    ]
+
+
+class KsStats(C.Structure):
+    _fields_ = [
+        ("rounds", C.c_uint64),
+        ("pods_resolved", C.c_uint64),
+        ("pods_scheduled", C.c_uint64),
+        ("sweep_launches", C.c_uint64),
+        ("sweep_ms", C.c_double),
+        ("sweep_evals", C.c_uint64),
+        ("resolve_ms", C.c_double),
+        ("resolve_launches", C.c_uint64),
+    ]
+
+
+# sizes from the C headers (checked in tests/test_abi.py against offsetof via the compiler)
+EXPECTED_SIZES = {
+    "ks_label": 16, "ks_taint": 24, "ks_toleration": 24, "ks_node": 64, "ks_container": 24,
+    "ks_requirement": 24, "ks_term": 24, "ks_preferred_term": 32, "ks_pod": 128, "ks_result": 48,
+    "ks_node_score": 40, "ks_node_state": 56, "ks_config": 56, "ks_stats": 64,
+}
+STRUCTS = {
+    "ks_label": KsLabel, "ks_taint": KsTaint, "ks_toleration": KsToleration, "ks_node": KsNode,
+    "ks_container": KsContainer, "ks_requirement": KsRequirement, "ks_term": KsTerm,
+    "ks_preferred_term": KsPreferredTerm, "ks_pod": KsPod, "ks_result": KsResult,
+    "ks_node_score": KsNodeScore, "ks_node_state": KsNodeState, "ks_config": KsConfig,
+    "ks_stats": KsStats,
+}
+
+KSCHED_SYMBOLS = [
+    "ks_config_default", "ks_open", "ks_close", "ks_last_error", "ks_abi_version", "ks_nodes_upsert",
+    "ks_nodes_delete", "ks_pods_add", "ks_pods_remove", "ks_schedule", "ks_batch_prepare", "ks_batch_run",
+    "ks_batch_results", "ks_batch_free", "ks_plugin_scores", "ks_node_states", "ks_comm_unique_id",
+    "ks_comm_init", "ks_get_stats", "ks_reset_stats", "ks_set_timing",
+]
+KSYNTH_SYMBOLS = [
+    "ksynth_nodes", "ksynth_pods", "ksynth_prefill", "ksynth_besteffort_pods", "ksynth_node_array",
+    "ksynth_pod_array", "ksynth_slots", "ksynth_free", "ksynth_fnv64",
+]
+
+
+class KschedError(RuntimeError):
+    def __init__(self, status: int, msg: str):
+        super().__init__(f"ksched status {status}: {msg}")
+        self.status = status
+
+
+def _load(name: str) -> C.CDLL:
+    path = LIB_DIR / name
+    if not path.exists():
+        raise ImportError(
+            f"{path} is missing: build the HIP extension first (python -c 'import __graft_entry__ as g; g.build()')"
+        )
+    return C.CDLL(str(path), mode=os.RTLD_NOW | os.RTLD_GLOBAL)
+
+
+_ksched = None
+_ksynth = None
+
+
+def ksched_lib() -> C.CDLL:
+    """libksched.so with argtypes declared.  Raises ImportError when absent."""
+    global _ksched
+    if _ksched is not None:
+        return _ksched
+    L = _load("libksched.so")
+    P = C.POINTER
+    vp = C.c_void_p
+    L.ks_config_default.argtypes = [P(KsConfig)]
+    L.ks_config_default.restype = None
+    L.ks_open.argtypes = [P(KsConfig), P(vp)]
+    L.ks_close.argtypes = [vp]
+    L.ks_close.restype = None
+    L.ks_last_error.argtypes = [vp]
+    L.ks_last_error.restype = c_char_p
+    L.ks_abi_version.restype = C.c_int32
+    L.ks_nodes_upsert.argtypes = [vp, P(KsNode), P(C.c_uint32), C.c_uint32]
+    L.ks_nodes_delete.argtypes = [vp, P(C.c_uint32), C.c_uint32]
+    L.ks_pods_add.argtypes = [vp, P(KsPod), P(C.c_uint32), C.c_uint32]
+    L.ks_pods_remove.argtypes = [vp, P(KsPod), P(C.c_uint32), C.c_uint32]
+    L.ks_schedule.argtypes = [vp, P(KsPod), C.c_uint32, P(KsResult)]
+    L.ks_batch_prepare.argtypes = [vp, P(KsPod), C.c_uint32, P(vp)]
+    L.ks_batch_run.argtypes = [vp, vp]
+    L.ks_batch_results.argtypes = [vp, vp, P(KsResult)]
+    L.ks_batch_free.argtypes = [vp, vp]
+    L.ks_batch_free.restype = None
+    L.ks_plugin_scores.argtypes = [vp, P(KsPod), P(KsNodeScore)]
+    L.ks_node_states.argtypes = [vp, P(C.c_uint32), C.c_uint32, P(KsNodeState)]
+    L.ks_comm_unique_id.argtypes = [P(C.c_uint8)]
+    L.ks_comm_init.argtypes = [vp, P(C.c_uint8)]
+    L.ks_get_stats.argtypes = [vp, P(KsStats)]
+    L.ks_reset_stats.argtypes = [vp]
+    L.ks_set_timing.argtypes = [vp, C.c_int32]
+    for f in KSCHED_SYMBOLS:
+        fn = getattr(L, f)
+        if fn.restype is C.c_int and f not in ("ks_abi_version",):
+            fn.restype = C.c_int32
+    _ksched = L
+    return L
+
+
+def ksynth_lib() -> C.CDLL:
+    global _ksynth
+    if _ksynth is not None:
+        return _ksynth
+    L = _load("libksynth.so")
+    vp = C.c_void_p
+    P = C.POINTER
+    L.ksynth_nodes.argtypes = [C.c_int32, C.c_uint32, C.c_uint64]
+    L.ksynth_nodes.restype = vp
+    L.ksynth_pods.argtypes = [C.c_int32, C.c_uint32, C.c_uint64]
+    L.ksynth_pods.restype = vp
+    L.ksynth_prefill.argtypes = [C.c_int32, C.c_uint32, C.c_uint64, C.c_uint64, C.c_double]
+    L.ksynth_prefill.restype = vp
+    L.ksynth_besteffort_pods.argtypes = [C.c_uint32]
+    L.ksynth_besteffort_pods.restype = vp
+    L.ksynth_node_array.argtypes = [vp, P(C.c_uint32)]
+    L.ksynth_node_array.restype = P(KsNode)
+    L.ksynth_pod_array.argtypes = [vp, P(C.c_uint32)]
+    L.ksynth_pod_array.restype = P(KsPod)
+    L.ksynth_slots.argtypes = [vp, P(C.c_uint32)]
+    L.ksynth_slots.restype = P(C.c_uint32)
+    L.ksynth_free.argtypes = [vp]
+    L.ksynth_free.restype = None
+    L.ksynth_fnv64.argtypes = [vp, C.c_uint64, C.c_uint64]
+    L.ksynth_fnv64.restype = C.c_uint64
+    _ksynth = L
+    return L

@@ -1,0 +1,163 @@
+"""k8s-shaped objects (the fields of k8s.io/api core/v1 this path reads) and
+their marshalling into the C ABI structs of include/ksched.h.
+
+Quantities are canonical integers: cpu in millicores (Quantity.MilliValue()),
+memory in bytes (Quantity.Value()).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+from . import _abi
+
+EFFECTS = {"": 0, "NoSchedule": 1, "PreferNoSchedule": 2, "NoExecute": 3}
+TOL_OPS = {"": 0, "Equal": 0, "Exists": 1}
+SEL_OPS = {"In": 0, "NotIn": 1, "Exists": 2, "DoesNotExist": 3, "Gt": 4, "Lt": 5}
+REQ_HAS_CPU, REQ_HAS_MEMORY, REQ_HAS_OTHER = 1, 2, 4
+
+
+@dataclass
+class Taint:
+    key: str
+    value: str = ""
+    effect: str = "NoSchedule"
+
+
+@dataclass
+class Toleration:
+    key: str = ""
+    operator: str = "Equal"
+    value: str = ""
+    effect: str = ""
+
+
+@dataclass
+class Container:
+    # resources.requests; an absent key is a MISSING request (not zero)
+    requests: Dict[str, int] = field(default_factory=dict)
+    restart_policy_always: bool = False  # init containers: sidecar
+
+
+@dataclass
+class NodeSelectorRequirement:
+    key: str
+    operator: str
+    values: List[str] = field(default_factory=list)
+
+
+@dataclass
+class NodeSelectorTerm:
+    match_expressions: List[NodeSelectorRequirement] = field(default_factory=list)
+    match_fields: List[NodeSelectorRequirement] = field(default_factory=list)
+
+
+@dataclass
+class PreferredSchedulingTerm:
+    weight: int
+    preference: NodeSelectorTerm
+
+
+@dataclass
+class Node:
+    name: str
+    allocatable: Dict[str, int]  # {"cpu": millicores, "memory": bytes, "pods": count}
+    labels: Dict[str, str] = field(default_factory=dict)
+    taints: List[Taint] = field(default_factory=list)
+    unschedulable: bool = False
+
+
+@dataclass
+class Pod:
+    name: str
+    namespace: str = "default"
+    containers: List[Container] = field(default_factory=lambda: [Container()])
+    init_containers: List[Container] = field(default_factory=list)
+    tolerations: List[Toleration] = field(default_factory=list)
+    node_selector: Dict[str, str] = field(default_factory=dict)
+    # affinity.nodeAffinity.requiredDuringSchedulingIgnoredDuringExecution.nodeSelectorTerms
+    # (None = the NodeSelector itself is nil)
+    required_terms: Optional[List[NodeSelectorTerm]] = None
+    # affinity.nodeAffinity.preferredDuringSchedulingIgnoredDuringExecution (None = nil)
+    preferred: Optional[List[PreferredSchedulingTerm]] = None
+    node_name: str = ""
+    overhead: Optional[Dict[str, int]] = None
+
+
+class Arena:
+    """Keeps the bytes / ctypes arrays a marshalled struct points into alive."""
+
+    def __init__(self):
+        self._keep = []
+
+    def s(self, text: Optional[str]):
+        if text is None:
+            return None
+        b = text.encode()
+        self._keep.append(b)
+        return b
+
+    def array(self, ctype, items):
+        arr = (ctype * max(1, len(items)))(*items)
+        self._keep.append(arr)
+        return C.cast(arr, C.POINTER(ctype)), len(items)
+
+
+def _container(c: Container) -> _abi.KsContainer:
+    flags = 0
+    for k in c.requests:
+        if k == "cpu":
+            flags |= REQ_HAS_CPU
+        elif k == "memory":
+            flags |= REQ_HAS_MEMORY
+        else:
+            flags |= REQ_HAS_OTHER
+    return _abi.KsContainer(c.requests.get("cpu", 0), c.requests.get("memory", 0), flags,
+                            1 if c.restart_policy_always else 0)
+
+
+def _requirement(r: NodeSelectorRequirement, a: Arena) -> _abi.KsRequirement:
+    vals, n = a.array(C.c_char_p, [a.s(v) for v in r.values])
+    return _abi.KsRequirement(a.s(r.key), vals, n, SEL_OPS.get(r.operator, 6))
+
+
+def _term(t: NodeSelectorTerm, a: Arena) -> _abi.KsTerm:
+    ex, nx = a.array(_abi.KsRequirement, [_requirement(r, a) for r in t.match_expressions])
+    fl, nf = a.array(_abi.KsRequirement, [_requirement(r, a) for r in t.match_fields])
+    return _abi.KsTerm(ex, fl, nx, nf)
+
+
+def node_to_c(n: Node, a: Arena) -> _abi.KsNode:
+    labels, nl = a.array(_abi.KsLabel, [_abi.KsLabel(a.s(k), a.s(v)) for k, v in n.labels.items()])
+    taints, nt = a.array(
+        _abi.KsTaint, [_abi.KsTaint(a.s(t.key), a.s(t.value), EFFECTS.get(t.effect, 9), 0) for t in n.taints])
+    al = n.allocatable
+    return _abi.KsNode(a.s(n.name), al.get("cpu", 0), al.get("memory", 0), al.get("pods", 0), labels, taints,
+                       nl, nt, 1 if n.unschedulable else 0, 0)
+
+
+def pod_to_c(p: Pod, a: Arena) -> _abi.KsPod:
+    cs, ncs = a.array(_abi.KsContainer, [_container(c) for c in p.containers])
+    ics, nics = a.array(_abi.KsContainer, [_container(c) for c in p.init_containers])
+    tols, ntol = a.array(_abi.KsToleration, [
+        _abi.KsToleration(a.s(t.key), a.s(t.value), TOL_OPS.get(t.operator, 2), EFFECTS.get(t.effect, 9))
+        for t in p.tolerations])
+    sel, nsel = a.array(_abi.KsLabel, [_abi.KsLabel(a.s(k), a.s(v)) for k, v in p.node_selector.items()])
+    req, nreq = a.array(_abi.KsTerm, [_term(t, a) for t in (p.required_terms or [])])
+    pref, npref = a.array(_abi.KsPreferredTerm, [
+        _abi.KsPreferredTerm(_term(t.preference, a), t.weight, 0) for t in (p.preferred or [])])
+    ov = p.overhead or {}
+    return _abi.KsPod(
+        a.s(p.namespace), a.s(p.name), cs, ics, tols, sel, req, pref, a.s(p.node_name),
+        ov.get("cpu", 0), ov.get("memory", 0), ncs, nics, ntol, nsel, nreq,
+        0 if p.required_terms is None else 1, npref, 0 if p.preferred is None else 1,
+        0 if p.overhead is None else 1, 0)
+
+
+def nodes_array(nodes: List[Node], a: Arena):
+    return a.array(_abi.KsNode, [node_to_c(n, a) for n in nodes])
+
+
+def pods_array(pods: List[Pod], a: Arena):
+    return a.array(_abi.KsPod, [pod_to_c(p, a) for p in pods])

@@ -1,0 +1,817 @@
+// oracle.cpp — CPU restatement of upstream kube-scheduler v1.31.3 for the
+// dist-scheduler shard path.  TEST INFRASTRUCTURE ONLY (see oracle.h).
+//
+// PARITY UNPINNED (oracle.h): the forked scheduler the reference compiles
+// (dist-scheduler/go.mod:133,138) is absent; this file restates the public
+// upstream v1.31.3 sources, cited as upstream:<file>#<func>.  It deliberately
+// works on the k8s-shaped objects (string maps, taint/toleration lists) with no
+// dictionary or bitset encoding, so that it also checks the product's encoder.
+//
+// Build: oracle/Makefile (g++ -O2 -ffp-contract=off).  Floating point follows
+// Go on amd64 (GOAMD64=v1: no FMA fusion), i.e. IEEE binary64 with one
+// rounding per operation.
+#include "oracle.h"
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <condition_variable>
+#include <cstring>
+#include <functional>
+#include <map>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace {
+
+constexpr int64_t kMaxNodeScore = 100;                      // framework.MaxNodeScore
+constexpr int64_t kDefaultMilliCPURequest = 100;            // upstream:pkg/scheduler/util#DefaultMilliCPURequest
+constexpr int64_t kDefaultMemoryRequest = 200 * 1024 * 1024; // upstream:pkg/scheduler/util#DefaultMemoryRequest
+
+std::string S(const char *p) { return p ? std::string(p) : std::string(); }
+
+// ------------------------------------------------------------------ objects
+
+struct Taint {
+  std::string key, value;
+  int32_t effect;
+};
+struct Toleration {
+  std::string key, value;
+  int32_t op, effect;
+};
+
+struct Node {
+  bool present = false;
+  std::string name;
+  int64_t alloc_cpu = 0, alloc_mem = 0, alloc_pods = 0;
+  std::map<std::string, std::string> labels;
+  std::vector<Taint> taints;
+  bool unschedulable = false;
+  // NodeInfo.Requested / NonZeroRequested / len(Pods)
+  int64_t req_cpu = 0, req_mem = 0, nz_cpu = 0, nz_mem = 0;
+  int64_t pods = 0;
+};
+
+// k8s.io/api/core/v1/toleration.go#ToleratesTaint
+bool ToleratesTaint(const Toleration &t, const Taint &taint) {
+  if (t.effect != KS_EFFECT_ALL && t.effect != taint.effect) return false;
+  if (!t.key.empty() && t.key != taint.key) return false;
+  switch (t.op) {
+    case KS_TOL_EQUAL: return t.value == taint.value;
+    case KS_TOL_EXISTS: return true;
+    default: return false;
+  }
+}
+
+// component-helpers/scheduling/corev1#TolerationsTolerateTaint
+bool TolerationsTolerateTaint(const std::vector<Toleration> &tols, const Taint &taint) {
+  for (auto &t : tols)
+    if (ToleratesTaint(t, taint)) return true;
+  return false;
+}
+
+// ---------------------------------------------- apimachinery validation
+
+bool alnum(char c) { return (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || (c >= '0' && c <= '9'); }
+
+// qualifiedNameFmt "([A-Za-z0-9][-A-Za-z0-9_.]*)?[A-Za-z0-9]"; labelValueFmt adds "empty ok".
+bool matches_qualified_name_part(const std::string &s) {
+  if (s.empty()) return false;
+  if (!alnum(s.front()) || !alnum(s.back())) return false;
+  for (char c : s)
+    if (!(alnum(c) || c == '-' || c == '_' || c == '.')) return false;
+  return true;
+}
+
+// validation.IsDNS1123Subdomain
+bool is_dns1123_subdomain(const std::string &s) {
+  if (s.empty() || s.size() > 253) return false;
+  size_t start = 0;
+  while (true) {
+    size_t dot = s.find('.', start);
+    std::string lab = s.substr(start, dot == std::string::npos ? std::string::npos : dot - start);
+    if (lab.empty()) return false;
+    auto lower_alnum = [](char c) { return (c >= 'a' && c <= 'z') || (c >= '0' && c <= '9'); };
+    if (!lower_alnum(lab.front()) || !lower_alnum(lab.back())) return false;
+    for (char c : lab)
+      if (!(lower_alnum(c) || c == '-')) return false;
+    if (dot == std::string::npos) break;
+    start = dot + 1;
+  }
+  return true;
+}
+
+// apimachinery/pkg/util/validation#IsQualifiedName
+bool IsQualifiedName(const std::string &v) {
+  std::string name;
+  size_t slash = v.find('/');
+  if (slash == std::string::npos) {
+    name = v;
+  } else {
+    if (v.find('/', slash + 1) != std::string::npos) return false;
+    std::string prefix = v.substr(0, slash);
+    name = v.substr(slash + 1);
+    if (prefix.empty() || !is_dns1123_subdomain(prefix)) return false;
+  }
+  if (name.empty() || name.size() > 63) return false;
+  return matches_qualified_name_part(name);
+}
+
+// apimachinery/pkg/util/validation#IsValidLabelValue
+bool IsValidLabelValue(const std::string &v) {
+  if (v.size() > 63) return false;
+  return v.empty() || matches_qualified_name_part(v);
+}
+
+// strconv.ParseInt(s, 10, 64)
+bool ParseInt64(const std::string &s, int64_t *out) {
+  if (s.empty()) return false;
+  size_t i = 0;
+  bool neg = false;
+  if (s[0] == '+' || s[0] == '-') {
+    neg = s[0] == '-';
+    i = 1;
+  }
+  if (i >= s.size()) return false;
+  unsigned __int128 acc = 0;
+  for (; i < s.size(); ++i) {
+    if (s[i] < '0' || s[i] > '9') return false;
+    acc = acc * 10 + (unsigned)(s[i] - '0');
+    if (acc > ((unsigned __int128)1 << 63)) return false;
+  }
+  if (!neg && acc > (unsigned __int128)INT64_MAX) return false;
+  *out = neg ? (int64_t)(-(__int128)acc) : (int64_t)acc;
+  return true;
+}
+
+// ------------------------------------------------- label selector requirement
+
+enum SelOp { SEL_IN, SEL_NOT_IN, SEL_EXISTS, SEL_DOES_NOT_EXIST, SEL_GT, SEL_LT, SEL_EQUALS };
+
+struct Requirement {  // apimachinery/pkg/labels#Requirement
+  std::string key;
+  SelOp op;
+  std::vector<std::string> values;
+};
+
+// labels.NewRequirement validation; returns false on any error.
+bool NewRequirement(const std::string &key, SelOp op, const std::vector<std::string> &vals,
+                    Requirement *out) {
+  bool ok = true;
+  switch (op) {
+    case SEL_IN:
+    case SEL_NOT_IN:
+      if (vals.empty()) ok = false;
+      break;
+    case SEL_EXISTS:
+    case SEL_DOES_NOT_EXIST:
+      if (!vals.empty()) ok = false;
+      break;
+    case SEL_GT:
+    case SEL_LT:
+      if (vals.size() != 1) ok = false;
+      for (auto &v : vals) {
+        int64_t x;
+        if (!ParseInt64(v, &x)) ok = false;
+      }
+      break;
+    default: ok = false;
+  }
+  for (auto &v : vals)
+    if (!IsValidLabelValue(v)) ok = false;
+  if (!IsQualifiedName(key)) ok = false;
+  if (ok) *out = Requirement{key, op, vals};
+  return ok;
+}
+
+// labels.Requirement.Matches
+bool Matches(const Requirement &r, const std::map<std::string, std::string> &ls) {
+  auto it = ls.find(r.key);
+  bool has = it != ls.end();
+  auto hasValue = [&](const std::string &v) {
+    return std::find(r.values.begin(), r.values.end(), v) != r.values.end();
+  };
+  switch (r.op) {
+    case SEL_IN:
+    case SEL_EQUALS:
+      if (!has) return false;
+      return hasValue(it->second);
+    case SEL_NOT_IN:
+      if (!has) return true;
+      return !hasValue(it->second);
+    case SEL_EXISTS: return has;
+    case SEL_DOES_NOT_EXIST: return !has;
+    case SEL_GT:
+    case SEL_LT: {
+      if (!has) return false;
+      int64_t lv, rv;
+      if (!ParseInt64(it->second, &lv)) return false;
+      if (r.values.size() != 1) return false;
+      if (!ParseInt64(r.values[0], &rv)) return false;
+      return (r.op == SEL_GT && lv > rv) || (r.op == SEL_LT && lv < rv);
+    }
+  }
+  return false;
+}
+
+// ------------------------------------------------------ node selector terms
+
+struct FieldReq {
+  std::string value;
+  bool equal;  // In -> name == value, NotIn -> name != value
+};
+
+// component-helpers/scheduling/corev1/nodeaffinity#nodeSelectorTerm
+struct NodeSelectorTerm {
+  bool has_labels = false;
+  std::vector<Requirement> labels;
+  bool has_fields = false;
+  std::vector<FieldReq> fields;
+  bool parse_error = false;
+
+  bool match(const Node &n) const {
+    if (parse_error) return false;
+    if (has_labels) {
+      for (auto &r : labels)
+        if (!Matches(r, n.labels)) return false;
+    }
+    if (has_fields && !n.name.empty()) {  // len(nodeFields) > 0
+      for (auto &f : fields)
+        if ((n.name == f.value) != f.equal) return false;
+    }
+    return true;
+  }
+};
+
+bool is_empty_term(const ks_term &t) { return t.n_expressions == 0 && t.n_fields == 0; }
+
+// nodeaffinity#newNodeSelectorTerm
+NodeSelectorTerm newNodeSelectorTerm(const ks_term &t) {
+  NodeSelectorTerm out;
+  if (t.n_expressions != 0) {
+    // nodeSelectorRequirementsAsSelector
+    out.has_labels = true;
+    for (uint32_t i = 0; i < t.n_expressions; ++i) {
+      const ks_requirement &e = t.match_expressions[i];
+      SelOp op;
+      switch (e.op) {
+        case KS_OP_IN: op = SEL_IN; break;
+        case KS_OP_NOT_IN: op = SEL_NOT_IN; break;
+        case KS_OP_EXISTS: op = SEL_EXISTS; break;
+        case KS_OP_DOES_NOT_EXIST: op = SEL_DOES_NOT_EXIST; break;
+        case KS_OP_GT: op = SEL_GT; break;
+        case KS_OP_LT: op = SEL_LT; break;
+        default: out.parse_error = true; continue;
+      }
+      std::vector<std::string> vals;
+      for (uint32_t k = 0; k < e.n_values; ++k) vals.push_back(S(e.values[k]));
+      Requirement r;
+      if (!NewRequirement(S(e.key), op, vals, &r)) out.parse_error = true;
+      else out.labels.push_back(r);
+    }
+  }
+  if (t.n_fields != 0) {
+    // nodeSelectorRequirementsAsFieldSelector
+    out.has_fields = true;
+    for (uint32_t i = 0; i < t.n_fields; ++i) {
+      const ks_requirement &e = t.match_fields[i];
+      if (S(e.key) != "metadata.name") { out.parse_error = true; continue; }
+      if (e.n_values != 1) { out.parse_error = true; continue; }
+      if (e.op == KS_OP_IN) out.fields.push_back({S(e.values[0]), true});
+      else if (e.op == KS_OP_NOT_IN) out.fields.push_back({S(e.values[0]), false});
+      else out.parse_error = true;
+    }
+  }
+  return out;
+}
+
+// ------------------------------------------------------------ pod state
+
+struct PodState {
+  // NodeResourcesFit PreFilter: computePodResourceRequest (actual requests)
+  int64_t req_cpu = 0, req_mem = 0;
+  bool req_other = false;
+  // resourceAllocationScorer: non-zero (LeastAllocated) and actual (BalancedAllocation)
+  int64_t nz_cpu = 0, nz_mem = 0;
+  std::vector<Toleration> tolerations;
+  std::vector<Toleration> tolerations_prefer;  // getAllTolerationPreferNoSchedule
+  std::string node_name;
+  // NodeAffinity PreFilter: GetRequiredNodeAffinity
+  bool affinity_skip = true;
+  std::vector<Requirement> node_selector;
+  bool has_required = false;
+  std::vector<NodeSelectorTerm> required;  // non-empty terms only
+  // NodeAffinity PreScore: PreferredSchedulingTerms
+  bool has_preferred = false;
+  bool preferred_error = false;
+  std::vector<std::pair<int64_t, NodeSelectorTerm>> preferred;
+};
+
+// upstream:pkg/api/v1/resource/helpers.go#PodRequests for cpu/memory.
+void PodRequests(const ks_pod &p, bool non_missing, int64_t *cpu, int64_t *mem, bool *other) {
+  auto get = [&](const ks_container &c, int64_t *ccpu, int64_t *cmem) {
+    *ccpu = (c.flags & KS_REQ_HAS_CPU) ? c.milli_cpu : (non_missing ? kDefaultMilliCPURequest : 0);
+    *cmem = (c.flags & KS_REQ_HAS_MEMORY) ? c.memory : (non_missing ? kDefaultMemoryRequest : 0);
+    if (c.flags & KS_REQ_HAS_OTHER) *other = true;
+  };
+  int64_t rc = 0, rm = 0;
+  for (uint32_t i = 0; i < p.n_containers; ++i) {
+    int64_t a, b;
+    get(p.containers[i], &a, &b);
+    rc += a;
+    rm += b;
+  }
+  int64_t sidecar_c = 0, sidecar_m = 0, init_c = 0, init_m = 0;
+  for (uint32_t i = 0; i < p.n_init_containers; ++i) {
+    int64_t a, b;
+    get(p.init_containers[i], &a, &b);
+    if (p.init_containers[i].restart_always) {
+      rc += a;
+      rm += b;
+      sidecar_c += a;
+      sidecar_m += b;
+      a = sidecar_c;
+      b = sidecar_m;
+    } else {
+      a += sidecar_c;
+      b += sidecar_m;
+    }
+    init_c = std::max(init_c, a);
+    init_m = std::max(init_m, b);
+  }
+  rc = std::max(rc, init_c);
+  rm = std::max(rm, init_m);
+  if (p.has_overhead) {
+    rc += p.overhead_milli_cpu;
+    rm += p.overhead_memory;
+  }
+  *cpu = rc;
+  *mem = rm;
+}
+
+PodState compile_pod(const ks_pod &p) {
+  PodState st;
+  bool other = false;
+  PodRequests(p, false, &st.req_cpu, &st.req_mem, &other);
+  PodRequests(p, true, &st.nz_cpu, &st.nz_mem, &other);
+  st.req_other = other;
+  for (uint32_t i = 0; i < p.n_tolerations; ++i) {
+    const ks_toleration &t = p.tolerations[i];
+    Toleration tt{S(t.key), S(t.value), t.op, t.effect};
+    st.tolerations.push_back(tt);
+    if (t.effect == KS_EFFECT_ALL || t.effect == KS_EFFECT_PREFER_NO_SCHEDULE)
+      st.tolerations_prefer.push_back(tt);
+  }
+  st.node_name = S(p.node_name);
+  // NodeAffinity.PreFilter: Skip when no required affinity and no nodeSelector.
+  st.has_required = p.has_required != 0;
+  st.affinity_skip = !st.has_required && p.n_node_selector == 0;
+  for (uint32_t i = 0; i < p.n_node_selector; ++i)
+    st.node_selector.push_back(
+        Requirement{S(p.node_selector[i].key), SEL_EQUALS, {S(p.node_selector[i].value)}});
+  for (uint32_t i = 0; i < p.n_required_terms; ++i) {
+    if (is_empty_term(p.required_terms[i])) continue;  // NewLazyErrorNodeSelector
+    st.required.push_back(newNodeSelectorTerm(p.required_terms[i]));
+  }
+  st.has_preferred = p.has_preferred != 0;
+  for (uint32_t i = 0; i < p.n_preferred; ++i) {
+    const ks_preferred_term &t = p.preferred[i];
+    if (t.weight == 0 || is_empty_term(t.preference)) continue;  // NewPreferredSchedulingTerms
+    NodeSelectorTerm term = newNodeSelectorTerm(t.preference);
+    if (term.parse_error) st.preferred_error = true;
+    else st.preferred.emplace_back((int64_t)t.weight, term);
+  }
+  return st;
+}
+
+// -------------------------------------------------------------- filters
+// Returns -1 (Success) or the KS_PLUGIN_* index of the first failing filter,
+// in default-profile order (frameworkImpl.RunFilterPlugins stops at the first
+// non-success status).
+
+int Filter(const PodState &st, const Node &n) {
+  // nodeunschedulable#Filter
+  if (n.unschedulable &&
+      !TolerationsTolerateTaint(st.tolerations,
+                                Taint{"node.kubernetes.io/unschedulable", "", KS_EFFECT_NO_SCHEDULE}))
+    return KS_PLUGIN_NODE_UNSCHEDULABLE;
+  // nodename#Filter
+  if (!st.node_name.empty() && st.node_name != n.name) return KS_PLUGIN_NODE_NAME;
+  // tainttoleration#Filter: FindMatchingUntoleratedTaint(DoNotScheduleTaintsFilterFunc)
+  for (auto &t : n.taints) {
+    if (t.effect != KS_EFFECT_NO_SCHEDULE && t.effect != KS_EFFECT_NO_EXECUTE) continue;
+    if (!TolerationsTolerateTaint(st.tolerations, t)) return KS_PLUGIN_TAINT_TOLERATION;
+  }
+  // nodeaffinity#Filter: RequiredNodeAffinity.Match (parse errors ignored)
+  if (!st.affinity_skip) {
+    for (auto &r : st.node_selector)
+      if (!Matches(r, n.labels)) return KS_PLUGIN_NODE_AFFINITY;
+    if (st.has_required) {
+      bool any = false;
+      for (auto &t : st.required)
+        if (t.match(n)) { any = true; break; }
+      if (!any) return KS_PLUGIN_NODE_AFFINITY;
+    }
+  }
+  // noderesources/fit.go#fitsRequest
+  bool fail = false;
+  if (n.pods + 1 > n.alloc_pods) fail = true;
+  if (!(st.req_cpu == 0 && st.req_mem == 0 && !st.req_other)) {
+    if (st.req_cpu > 0 && st.req_cpu > n.alloc_cpu - n.req_cpu) fail = true;
+    if (st.req_mem > 0 && st.req_mem > n.alloc_mem - n.req_mem) fail = true;
+  }
+  if (fail) return KS_PLUGIN_NODE_RESOURCES_FIT;
+  return -1;
+}
+
+// -------------------------------------------------------------- scores
+
+// noderesources/least_allocated.go#leastRequestedScore
+int64_t leastRequestedScore(int64_t requested, int64_t capacity) {
+  if (capacity == 0) return 0;
+  if (requested > capacity) return 0;
+  return ((capacity - requested) * kMaxNodeScore) / capacity;
+}
+
+// resource_allocation.go#score + least_allocated.go#leastResourceScorer (cpu:1, memory:1),
+// useRequested=false: node NonZeroRequested + pod non-zero request.
+int64_t LeastAllocated(int64_t acpu, int64_t amem, int64_t ncpu, int64_t nmem, int64_t pcpu, int64_t pmem) {
+  const int64_t alloc[2] = {acpu, amem};
+  const int64_t req[2] = {ncpu + pcpu, nmem + pmem};
+  int64_t nodeScore = 0, weightSum = 0;
+  for (int i = 0; i < 2; ++i) {
+    if (alloc[i] == 0) continue;
+    nodeScore += leastRequestedScore(req[i], alloc[i]) * 1;
+    weightSum += 1;
+  }
+  if (weightSum == 0) return 0;
+  return nodeScore / weightSum;
+}
+
+// balanced_allocation.go#balancedResourceScorer, useRequested=true.
+int64_t BalancedAllocation(int64_t acpu, int64_t amem, int64_t ncpu, int64_t nmem, int64_t pcpu, int64_t pmem) {
+  const int64_t alloc[2] = {acpu, amem};
+  const int64_t req[2] = {ncpu + pcpu, nmem + pmem};
+  double fractions[2];
+  int nf = 0;
+  double totalFraction = 0;
+  for (int i = 0; i < 2; ++i) {
+    if (alloc[i] == 0) continue;
+    double fraction = (double)req[i] / (double)alloc[i];
+    if (fraction > 1) fraction = 1;
+    totalFraction += fraction;
+    fractions[nf++] = fraction;
+  }
+  (void)totalFraction;
+  double std = 0.0;
+  if (nf == 2) std = std::fabs((fractions[0] - fractions[1]) / 2);
+  return (int64_t)((1 - std) * (double)kMaxNodeScore);
+}
+
+// tainttoleration#countIntolerableTaintsPreferNoSchedule
+int64_t TaintRaw(const PodState &st, const Node &n) {
+  int64_t c = 0;
+  for (auto &t : n.taints) {
+    if (t.effect != KS_EFFECT_PREFER_NO_SCHEDULE) continue;
+    if (!TolerationsTolerateTaint(st.tolerations_prefer, t)) ++c;
+  }
+  return c;
+}
+
+// nodeaffinity#PreferredSchedulingTerms.Score
+int64_t AffinityRaw(const PodState &st, const Node &n) {
+  int64_t s = 0;
+  for (auto &wt : st.preferred)
+    if (wt.second.match(n)) s += wt.first;
+  return s;
+}
+
+// plugins/helper/normalize_score.go#DefaultNormalizeScore for one element.
+int64_t Normalize(int64_t score, int64_t maxCount, bool reverse) {
+  if (maxCount == 0) return reverse ? kMaxNodeScore : 0;
+  int64_t s = kMaxNodeScore * score / maxCount;
+  return reverse ? kMaxNodeScore - s : s;
+}
+
+inline uint64_t PackKey(int64_t total, uint32_t slot) {
+  return ((uint64_t)(total + 1) << 32) | (uint64_t)(0xFFFFFFFFu - slot);
+}
+
+}  // namespace
+
+// ================================================================ oracle
+
+struct oracle {
+  std::vector<Node> nodes;
+  int64_t w_fit, w_ba, w_tt, w_na, w_il;
+  int threads = 1;
+
+  struct Eval {
+    int status;
+    int64_t la, ba, tt_raw, na_raw;
+  };
+
+  Eval eval(const PodState &st, const Node &n) const {
+    Eval e{};
+    e.status = Filter(st, n);
+    if (e.status >= 0) return e;
+    e.la = LeastAllocated(n.alloc_cpu, n.alloc_mem, n.nz_cpu, n.nz_mem, st.nz_cpu, st.nz_mem);
+    e.ba = BalancedAllocation(n.alloc_cpu, n.alloc_mem, n.req_cpu, n.req_mem, st.req_cpu, st.req_mem);
+    e.tt_raw = TaintRaw(st, n);
+    e.na_raw = st.has_preferred ? AffinityRaw(st, n) : 0;
+    return e;
+  }
+
+  int64_t total(const PodState &st, const Eval &e, int64_t tt_max, int64_t na_max) const {
+    // frameworkImpl.RunScorePlugins: Σ weight × normalized score.  ImageLocality
+    // scores 0 (nodes report no images); NodeAffinity is skipped without
+    // preferred terms (PreScore Skip) and contributes nothing either way.
+    int64_t t = w_fit * e.la + w_ba * e.ba + w_tt * Normalize(e.tt_raw, tt_max, true) + w_il * 0;
+    if (st.has_preferred) t += w_na * Normalize(e.na_raw, na_max, false);
+    return t;
+  }
+
+  void add_pod(Node &n, const ks_pod &p, int sign) {
+    // framework/types.go#NodeInfo.update via calculateResource
+    int64_t rc, rm, zc, zm;
+    bool other = false;
+    PodRequests(p, false, &rc, &rm, &other);
+    PodRequests(p, true, &zc, &zm, &other);
+    n.req_cpu += sign * rc;
+    n.req_mem += sign * rm;
+    n.nz_cpu += sign * zc;
+    n.nz_mem += sign * zm;
+    n.pods += sign;
+  }
+
+  // Parallel node loop: parallelize.Until chunking, chunk = min(sqrt(N), N/threads + 1).
+  void for_nodes(uint32_t lo, uint32_t hi, const std::function<void(uint32_t, uint32_t, int)> &fn) const {
+    const uint32_t N = hi - lo;
+    if (threads <= 1 || N < 1024) {
+      fn(lo, hi, 0);
+      return;
+    }
+    uint32_t chunk = std::min<uint32_t>((uint32_t)std::sqrt((double)N), N / threads + 1);
+    if (chunk == 0) chunk = 1;
+    std::atomic<uint32_t> next{lo};
+    std::vector<std::thread> ws;
+    for (int t = 0; t < threads; ++t) {
+      ws.emplace_back([&, t] {
+        while (true) {
+          uint32_t s = next.fetch_add(chunk);
+          if (s >= hi) break;
+          fn(s, std::min(hi, s + chunk), t);
+        }
+      });
+    }
+    for (auto &w : ws) w.join();
+  }
+
+  // schedulePod (schedule_one.go): findNodesThatFitPod -> prioritizeNodes -> selectHost.
+  ks_result schedule_one(const ks_pod &p) {
+    ks_result r{};
+    r.node_index = -1;
+    PodState st = compile_pod(p);
+    const uint32_t N = (uint32_t)nodes.size();
+    std::vector<Eval> ev(N);
+    for_nodes(0, N, [&](uint32_t a, uint32_t b, int) {
+      for (uint32_t i = a; i < b; ++i)
+        if (nodes[i].present) ev[i] = eval(st, nodes[i]);
+    });
+    uint32_t evaluated = 0, feasible = 0;
+    int64_t tt_max = 0, na_max = 0;
+    uint32_t only = 0;
+    for (uint32_t i = 0; i < N; ++i) {
+      if (!nodes[i].present) continue;
+      ++evaluated;
+      if (ev[i].status >= 0) {
+        r.fail_counts[ev[i].status]++;
+        continue;
+      }
+      ++feasible;
+      only = i;
+      tt_max = std::max(tt_max, ev[i].tt_raw);
+      na_max = std::max(na_max, ev[i].na_raw);
+    }
+    r.evaluated_nodes = evaluated;
+    r.feasible_nodes = feasible;
+    if (feasible == 0) {
+      r.status = KS_POD_UNSCHEDULABLE;  // FitError{NumAllNodes, Diagnosis}
+      return r;
+    }
+    if (feasible == 1) {
+      // "When only one node after predicate, just use it." No scoring upstream;
+      // the build still reports that node's TotalScore.
+      r.flags |= KS_RESULT_SINGLE_FEASIBLE;
+      r.node_index = (int32_t)only;
+      r.total_score = total(st, ev[only], tt_max, na_max);
+      r.status = KS_POD_SCHEDULED;
+      return r;
+    }
+    if (st.has_preferred && st.preferred_error) {  // NodeAffinity.PreScore error
+      r.status = KS_POD_ERROR;
+      return r;
+    }
+    uint64_t best = 0;
+    for (uint32_t i = 0; i < N; ++i) {
+      if (!nodes[i].present || ev[i].status >= 0) continue;
+      uint64_t k = PackKey(total(st, ev[i], tt_max, na_max), i);
+      if (k > best) best = k;  // max TotalScore, tie -> lowest slot
+    }
+    r.node_index = (int32_t)(0xFFFFFFFFu - (uint32_t)best);
+    r.total_score = (int64_t)(best >> 32) - 1;
+    r.status = KS_POD_SCHEDULED;
+    return r;
+  }
+};
+
+extern "C" {
+
+oracle *oracle_new(uint32_t cap, int32_t w_fit, int32_t w_ba, int32_t w_tt, int32_t w_na, int32_t w_il) {
+  auto *o = new oracle();
+  o->nodes.resize(cap);
+  o->w_fit = w_fit;
+  o->w_ba = w_ba;
+  o->w_tt = w_tt;
+  o->w_na = w_na;
+  o->w_il = w_il;
+  return o;
+}
+void oracle_free(oracle *o) { delete o; }
+void oracle_set_threads(oracle *o, int32_t t) { o->threads = t < 1 ? 1 : t; }
+
+int32_t oracle_nodes_upsert(oracle *o, const ks_node *nodes, const uint32_t *slots, uint32_t n) {
+  for (uint32_t i = 0; i < n; ++i) {
+    if (slots[i] >= o->nodes.size()) return KS_ERR_NOT_FOUND;
+    Node &d = o->nodes[slots[i]];
+    const ks_node &s = nodes[i];
+    if (!d.present) d = Node();
+    d.present = true;
+    d.name = S(s.name);
+    d.alloc_cpu = s.alloc_milli_cpu;
+    d.alloc_mem = s.alloc_memory;
+    d.alloc_pods = s.alloc_pods;
+    d.unschedulable = s.unschedulable != 0;
+    d.labels.clear();
+    for (uint32_t k = 0; k < s.n_labels; ++k) d.labels[S(s.labels[k].key)] = S(s.labels[k].value);
+    d.taints.clear();
+    for (uint32_t k = 0; k < s.n_taints; ++k)
+      d.taints.push_back({S(s.taints[k].key), S(s.taints[k].value), s.taints[k].effect});
+  }
+  return KS_OK;
+}
+
+int32_t oracle_nodes_delete(oracle *o, const uint32_t *slots, uint32_t n) {
+  for (uint32_t i = 0; i < n; ++i) {
+    if (slots[i] >= o->nodes.size()) return KS_ERR_NOT_FOUND;
+    o->nodes[slots[i]] = Node();
+  }
+  return KS_OK;
+}
+
+int32_t oracle_pods_add(oracle *o, const ks_pod *pods, const uint32_t *slots, uint32_t n) {
+  for (uint32_t i = 0; i < n; ++i) {
+    if (slots[i] >= o->nodes.size() || !o->nodes[slots[i]].present) return KS_ERR_NOT_FOUND;
+    o->add_pod(o->nodes[slots[i]], pods[i], +1);
+  }
+  return KS_OK;
+}
+
+int32_t oracle_pods_remove(oracle *o, const ks_pod *pods, const uint32_t *slots, uint32_t n) {
+  for (uint32_t i = 0; i < n; ++i) {
+    if (slots[i] >= o->nodes.size() || !o->nodes[slots[i]].present) return KS_ERR_NOT_FOUND;
+    o->add_pod(o->nodes[slots[i]], pods[i], -1);
+  }
+  return KS_OK;
+}
+
+int32_t oracle_schedule(oracle *o, const ks_pod *pods, uint32_t n, ks_result *out) {
+  for (uint32_t i = 0; i < n; ++i) {
+    out[i] = o->schedule_one(pods[i]);
+    if (out[i].status == KS_POD_SCHEDULED)
+      o->add_pod(o->nodes[out[i].node_index], pods[i], +1);  // assume -> NodeInfo.AddPod
+  }
+  return KS_OK;
+}
+
+int32_t oracle_plugin_scores(oracle *o, const ks_pod *pod, ks_node_score *out) {
+  PodState st = compile_pod(*pod);
+  const uint32_t N = (uint32_t)o->nodes.size();
+  std::vector<oracle::Eval> ev(N);
+  int64_t tt_max = 0, na_max = 0;
+  for (uint32_t i = 0; i < N; ++i) {
+    if (!o->nodes[i].present) continue;
+    ev[i] = o->eval(st, o->nodes[i]);
+    if (ev[i].status < 0) {
+      tt_max = std::max(tt_max, ev[i].tt_raw);
+      na_max = std::max(na_max, ev[i].na_raw);
+    }
+  }
+  for (uint32_t i = 0; i < N; ++i) {
+    ks_node_score s{};
+    if (!o->nodes[i].present) {
+      s.status = -2;
+    } else if (ev[i].status >= 0) {
+      s.status = ev[i].status;
+    } else {
+      s.status = -1;
+      s.least_allocated = (int32_t)ev[i].la;
+      s.balanced_allocation = (int32_t)ev[i].ba;
+      s.taint_raw = (int32_t)ev[i].tt_raw;
+      s.taint_score = (int32_t)Normalize(ev[i].tt_raw, tt_max, true);
+      s.affinity_raw = (int32_t)ev[i].na_raw;
+      s.affinity_score = st.has_preferred ? (int32_t)Normalize(ev[i].na_raw, na_max, false) : 0;
+      s.image_locality = 0;
+      s.total_score = o->total(st, ev[i], tt_max, na_max);
+    }
+    out[i] = s;
+  }
+  return KS_OK;
+}
+
+int32_t oracle_node_states(oracle *o, const uint32_t *slots, uint32_t n, ks_node_state *out) {
+  for (uint32_t i = 0; i < n; ++i) {
+    if (slots[i] >= o->nodes.size()) return KS_ERR_NOT_FOUND;
+    const Node &d = o->nodes[slots[i]];
+    ks_node_state s{};
+    if (d.present) {
+      s.alloc_milli_cpu = d.alloc_cpu;
+      s.alloc_memory = d.alloc_mem;
+      s.req_milli_cpu = d.req_cpu;
+      s.req_memory = d.req_mem;
+      s.nonzero_milli_cpu = d.nz_cpu;
+      s.nonzero_memory = d.nz_mem;
+      s.alloc_pods = (int32_t)d.alloc_pods;
+      s.pod_count = (int32_t)d.pods;
+    } else {
+      s.pod_count = -1;
+    }
+    out[i] = s;
+  }
+  return KS_OK;
+}
+
+int32_t oracle_shard_prescore_run(oracle *o, const ks_pod *pod, uint32_t lo, uint32_t hi,
+                                  oracle_shard_prescore *out) {
+  PodState st = compile_pod(*pod);
+  oracle_shard_prescore r{};
+  hi = std::min<uint32_t>(hi, (uint32_t)o->nodes.size());
+  for (uint32_t i = lo; i < hi; ++i) {
+    if (!o->nodes[i].present) continue;
+    oracle::Eval e = o->eval(st, o->nodes[i]);
+    if (e.status >= 0) {
+      r.fail_counts[e.status]++;
+      continue;
+    }
+    r.feasible++;
+    if (e.tt_raw > r.taint_max) { r.taint_max = e.tt_raw; r.taint_count = 0; }
+    if (e.tt_raw == r.taint_max) r.taint_count++;
+    if (e.na_raw > r.affinity_max) { r.affinity_max = e.na_raw; r.affinity_count = 0; }
+    if (e.na_raw == r.affinity_max) r.affinity_count++;
+  }
+  r.error = (st.has_preferred && st.preferred_error) ? 1 : 0;
+  *out = r;
+  return KS_OK;
+}
+
+uint64_t oracle_shard_best(oracle *o, const ks_pod *pod, uint32_t lo, uint32_t hi, int64_t tt_max,
+                           int64_t na_max) {
+  PodState st = compile_pod(*pod);
+  uint64_t best = 0;
+  hi = std::min<uint32_t>(hi, (uint32_t)o->nodes.size());
+  for (uint32_t i = lo; i < hi; ++i) {
+    if (!o->nodes[i].present) continue;
+    oracle::Eval e = o->eval(st, o->nodes[i]);
+    if (e.status >= 0) continue;
+    best = std::max(best, PackKey(o->total(st, e, tt_max, na_max), i));
+  }
+  return best;
+}
+
+int32_t oracle_commit(oracle *o, const ks_pod *pod, uint32_t slot) {
+  if (slot >= o->nodes.size() || !o->nodes[slot].present) return KS_ERR_NOT_FOUND;
+  o->add_pod(o->nodes[slot], *pod, +1);
+  return KS_OK;
+}
+
+int64_t oracle_least_allocated(int64_t acpu, int64_t amem, int64_t ncpu, int64_t nmem, int64_t pcpu,
+                               int64_t pmem) {
+  return LeastAllocated(acpu, amem, ncpu, nmem, pcpu, pmem);
+}
+
+int64_t oracle_balanced_allocation(int64_t acpu, int64_t amem, int64_t ncpu, int64_t nmem,
+                                   int64_t pcpu, int64_t pmem) {
+  return BalancedAllocation(acpu, amem, ncpu, nmem, pcpu, pmem);
+}
+
+int32_t oracle_pod_requests(const ks_pod *pod, int64_t out[4]) {
+  bool other = false;
+  PodRequests(*pod, false, &out[0], &out[1], &other);
+  PodRequests(*pod, true, &out[2], &out[3], &other);
+  return other ? KS_ERR_UNSUPPORTED : KS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,33 @@
+"""Shared comparison helpers for parity tests (oracle vs libksched)."""
+import ctypes as C
+
+import numpy as np
+
+from ksched import _abi
+
+RES_DT = np.dtype([("node_index", "<i4"), ("status", "<i4"), ("total_score", "<i8"), ("feasible", "<u4"),
+                   ("evaluated", "<u4"), ("fail", "<u4", (5,)), ("flags", "<u4")])
+
+
+def res_array(raw, n):
+    return np.frombuffer(C.string_at(C.addressof(raw), n * C.sizeof(_abi.KsResult)), dtype=RES_DT).copy()
+
+
+def assert_results_equal(got, want, n, what=""):
+    g, w = res_array(got, n), res_array(want, n)
+    if not np.array_equal(g, w):
+        bad = np.nonzero(g != w)[0]
+        i = int(bad[0])
+        raise AssertionError(
+            f"{what}: {len(bad)}/{n} results differ; first at pod {i}: got {g[i]} want {w[i]}")
+
+
+def state_array(states):
+    return np.array([(s.alloc_milli_cpu, s.alloc_memory, s.req_milli_cpu, s.req_memory, s.nonzero_milli_cpu,
+                      s.nonzero_memory, s.alloc_pods, s.pod_count) for s in states], dtype=np.int64)
+
+
+def scores_array(scores):
+    return np.array([(s.status, s.least_allocated, s.balanced_allocation, s.taint_raw, s.taint_score,
+                      s.affinity_raw, s.affinity_score, s.image_locality, s.total_score) for s in scores],
+                    dtype=np.int64)
