@@ -59,14 +59,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch
-        import torch.distributed as dist
-
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-
+    # No torch in this process: torch bundles its own libamdhip64 / librccl
+    # (ROCm 7.0) with the same sonames as the /opt/rocm 7.2 libraries
+    # libksched links, and one process must not mix the two runtimes.  The
+    # ranks rendezvous through a file on the node (RCCL unique id) and use the
+    # scheduler's own RCCL communicator for barriers and the max-over-ranks time.
     from ksched import Scheduler, synth
     from ksched.framework import results_to_arrays
 
@@ -75,13 +72,7 @@ def main():
     sched = Scheduler(args.nodes, device=local_rank if world > 1 else 0, pods_per_round=args.pods_per_round,
                       topk=args.topk, nodes_per_lane=args.nodes_per_lane, world_size=world, rank=rank)
     if world > 1:
-        import torch
-
-        uid = torch.zeros(128, dtype=torch.uint8, device="cuda")
-        if rank == 0:
-            uid.copy_(torch.frombuffer(bytearray(Scheduler.comm_unique_id()), dtype=torch.uint8))
-        dist.broadcast(uid, 0)
-        sched.comm_init(bytes(uid.cpu().numpy().tobytes()))
+        sched.comm_init(exchange_unique_id(rank, world))
 
     nodes = synth.nodes(kind, args.nodes, 1)
     slots = synth.slot_array(args.nodes)
@@ -97,14 +88,11 @@ def main():
     setup_s = time.time() - t_setup
 
     def barrier():
-        if dist is not None:
-            dist.barrier()
+        if world > 1:
+            sched.allreduce_max([0.0])  # RCCL all-reduce on the scheduler's stream
 
     def sync():
-        if dist is not None:
-            import torch
-
-            torch.cuda.synchronize()
+        pass  # ks_batch_run returns after hipStreamSynchronize on the scheduler stream
 
     for b in range(args.warmup):
         sched.run(batches[b])
@@ -119,12 +107,8 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     sched.set_timing(False)
-    if dist is not None:
-        import torch
-
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    if world > 1:
+        elapsed = sched.allreduce_max([elapsed])[0]
     st = sched.stats()
 
     # scheduled fraction of the timed pods (sanity for the reader)
@@ -199,8 +183,28 @@ def main():
     sched.close()
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+
+
+def exchange_unique_id(rank: int, world: int) -> bytes:
+    """Rank 0 publishes the RCCL unique id in a file every local rank reads."""
+    from ksched import Scheduler
+
+    key = "_".join([os.environ.get("TORCHELASTIC_RUN_ID", "run"), os.environ.get("MASTER_ADDR", "127.0.0.1"),
+                    os.environ.get("MASTER_PORT", "0")]).replace("/", "_")
+    path = Path(os.environ.get("TMPDIR", "/tmp")) / f"ksched_uid_{key}.bin"
+    if rank == 0:
+        tmp = path.with_suffix(".tmp")
+        tmp.write_bytes(Scheduler.comm_unique_id())
+        os.replace(tmp, path)
+        return path.read_bytes()
+    deadline = time.time() + 300
+    while time.time() < deadline:
+        if path.exists():
+            data = path.read_bytes()
+            if len(data) == 128:
+                return data
+        time.sleep(0.05)
+    raise TimeoutError(f"rank {rank}: no RCCL unique id at {path}")
 
 
 def cpu_baseline(args, kind, nodes, slots, pre, pods):

@@ -284,6 +284,8 @@ ks_status ks_node_states(ks_ctx *ctx, const uint32_t *slots, uint32_t n, ks_node
 #define KS_COMM_ID_BYTES 128
 ks_status ks_comm_unique_id(uint8_t out[KS_COMM_ID_BYTES]);
 ks_status ks_comm_init(ks_ctx *ctx, const uint8_t id[KS_COMM_ID_BYTES]);
+/* Element-wise max of n doubles over all ranks (in place); also a barrier. */
+ks_status ks_comm_allreduce_max(ks_ctx *ctx, double *values, uint32_t n);
 
 /* Counters for measurement. */
 typedef struct {
@@ -298,6 +300,9 @@ typedef struct {
 } ks_stats;
 ks_status ks_get_stats(ks_ctx *ctx, ks_stats *out);
 ks_status ks_reset_stats(ks_ctx *ctx);
+/* Raw device counters: [0] rounds [1] pods resolved [2] pods swept,
+ * [8..15] resolve phase cycle sums (diagnostic KS_STAMPS build only). */
+ks_status ks_debug_counters(ks_ctx *ctx, uint64_t out[16]);
 /* 1 = time every sweep/resolve launch with HIP events (adds syncs), 0 = off. */
 ks_status ks_set_timing(ks_ctx *ctx, int32_t enabled);
 

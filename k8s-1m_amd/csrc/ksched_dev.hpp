@@ -121,6 +121,19 @@ static_assert(sizeof(ShardRecHdr) == 48, "ShardRecHdr layout");
 constexpr uint32_t REC_HDR_WORDS = 6;
 __host__ __device__ inline uint32_t rec_words(uint32_t k) { return REC_HDR_WORDS + k; }
 
+// S0 row of a listed candidate, gathered next to its key after the merge so
+// the resolve's per-pod prefetch is one independent load per thread.
+struct alignas(16) CandRow {
+  int64_t acpu, amem, rc, rm, zc, zm;
+  int32_t apods, np;
+  uint32_t pos, _pad;
+};
+static_assert(sizeof(CandRow) == 64, "CandRow layout");
+struct alignas(16) CandExt {
+  uint64_t w[2 + LW + NNUM];  // hard, prefer, lab[LW], num[NNUM]
+};
+static_assert(sizeof(CandExt) == 64, "CandExt layout");
+
 // Normalising-plugin maxima over feasible nodes: (max raw, #feasible at max).
 struct alignas(16) NormRec {
   int64_t tt_max, na_max;

@@ -170,6 +170,8 @@ struct ks_ctx {
   size_t brec_bytes = 0;
   uint64_t *d_srec = nullptr, *d_frec = nullptr;
   uint64_t *d_counters = nullptr;
+  CandRow *d_crow = nullptr;
+  CandExt *d_cext = nullptr;
   // host mirror / dictionaries
   std::vector<HostNode> nodes;
   uint32_t n_present = 0;
@@ -195,7 +197,17 @@ struct ks_ctx {
   bool timing = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_sweep, ev_resolve;
   std::vector<hipEvent_t> ev_pool;
-  uint64_t pending_sweep_evals = 0;
+  uint64_t counters_base[4] = {0, 0, 0, 0};  // device counters at the last ks_reset_stats
+  // Host<->device transfers of one ABI call: a pinned host staging buffer and a
+  // device scratch buffer, both bump-allocated and reset at xfer_sync (no
+  // pageable hipMemcpyAsync anywhere).
+  uint8_t *pin = nullptr, *dscr = nullptr;
+  size_t pin_cap = 0, pin_used = 0, dscr_cap = 0, dscr_used = 0;
+  struct Pending {
+    void *dst;
+    size_t off, bytes;
+  };
+  std::vector<Pending> d2h_pending;
 
   uint32_t intern(const char *p) {
     std::string s = str(p);
@@ -237,6 +249,69 @@ struct ks_ctx {
 
 namespace {
 
+// --------------------------------------------------------------- transfers
+
+inline size_t xround(size_t b) { return (b + 255) & ~(size_t)255; }
+
+ks_status xfer_sync(ks_ctx *c) {
+  HIPC(c, hipStreamSynchronize(c->stream));
+  for (auto &p : c->d2h_pending) std::memcpy(p.dst, c->pin + p.off, p.bytes);
+  c->d2h_pending.clear();
+  c->pin_used = c->dscr_used = 0;
+  return KS_OK;
+}
+
+// Start an ABI call's transfers: completes earlier work, then guarantees
+// pin_bytes of staging and dev_bytes of device scratch (each segment is
+// rounded to 256 B: callers include that slack).
+ks_status xfer_begin(ks_ctx *c, size_t pin_bytes, size_t dev_bytes) {
+  ks_status st = xfer_sync(c);
+  if (st) return st;
+  if (pin_bytes > c->pin_cap) {
+    if (c->pin) HIPC(c, hipHostFree(c->pin));
+    c->pin = nullptr;
+    c->pin_cap = std::max<size_t>(pin_bytes, std::max<size_t>(2 * c->pin_cap, 1 << 20));
+    HIPC(c, hipHostMalloc((void **)&c->pin, c->pin_cap, hipHostMallocDefault));
+  }
+  if (dev_bytes > c->dscr_cap) {
+    if (c->dscr) HIPC(c, hipFree(c->dscr));
+    c->dscr = nullptr;
+    c->dscr_cap = std::max<size_t>(dev_bytes, std::max<size_t>(2 * c->dscr_cap, 1 << 20));
+    HIPC(c, hipMalloc((void **)&c->dscr, c->dscr_cap));
+  }
+  return KS_OK;
+}
+
+template <class T>
+T *dscratch(ks_ctx *c, size_t count) {
+  const size_t b = xround(std::max<size_t>(count, 1) * sizeof(T));
+  if (c->dscr_used + b > c->dscr_cap) return nullptr;
+  T *p = (T *)(c->dscr + c->dscr_used);
+  c->dscr_used += b;
+  return p;
+}
+
+ks_status h2d(ks_ctx *c, void *dst, const void *src, size_t bytes) {
+  if (!bytes) return KS_OK;
+  const size_t b = xround(bytes);
+  if (c->pin_used + b > c->pin_cap) return c->fail(KS_ERR_INVALID, "staging overflow (h2d %zu)", bytes);
+  std::memcpy(c->pin + c->pin_used, src, bytes);
+  HIPC(c, hipMemcpyAsync(dst, c->pin + c->pin_used, bytes, hipMemcpyHostToDevice, c->stream));
+  c->pin_used += b;
+  return KS_OK;
+}
+
+// Completed (copied to dst) at the next xfer_sync.
+ks_status d2h(ks_ctx *c, void *dst, const void *src, size_t bytes) {
+  if (!bytes) return KS_OK;
+  const size_t b = xround(bytes);
+  if (c->pin_used + b > c->pin_cap) return c->fail(KS_ERR_INVALID, "staging overflow (d2h %zu)", bytes);
+  HIPC(c, hipMemcpyAsync(c->pin + c->pin_used, src, bytes, hipMemcpyDeviceToHost, c->stream));
+  c->d2h_pending.push_back({dst, c->pin_used, bytes});
+  c->pin_used += b;
+  return KS_OK;
+}
+
 // --------------------------------------------------------- label encoding
 
 void node_ext_bits(ks_ctx *c, HostNode &n) {
@@ -267,14 +342,26 @@ ks_status alloc_bit(ks_ctx *c, uint32_t *bit) {
   return KS_OK;
 }
 
+// key_nodes lists are append-only (a slot is added for every label it is
+// upserted with); entries are re-validated here and the list compacted.
 void mark_key_nodes_dirty(ks_ctx *c, uint32_t key) {
   auto it = c->key_nodes.find(key);
   if (it == c->key_nodes.end()) return;
-  for (uint32_t s : it->second) {
-    if (!c->nodes[s].present) continue;
+  std::vector<uint32_t> &v = it->second;
+  std::sort(v.begin(), v.end());
+  v.erase(std::unique(v.begin(), v.end()), v.end());
+  size_t keep = 0;
+  for (uint32_t s : v) {
+    const HostNode &h = c->nodes[s];
+    if (!h.present) continue;
+    bool has = false;
+    for (auto &kv : h.labels) has |= kv.first == key;
+    if (!has) continue;
+    v[keep++] = s;
     node_ext_bits(c, c->nodes[s]);
     c->dirty_ext.push_back(s);
   }
+  v.resize(keep);
 }
 
 ks_status get_pair_bit(ks_ctx *c, uint32_t key, uint32_t value, uint32_t *bit) {
@@ -576,16 +663,13 @@ ks_status upload_dirty_ext(ks_ctx *c) {
     for (int k = 0; k < LW; ++k) e[2 + k] = h.lab[k];
     for (int k = 0; k < NNUM; ++k) e[2 + LW + k] = (uint64_t)h.num[k];
   }
-  uint32_t *d_pos;
-  uint64_t *d_ext;
-  HIPC(c, hipMallocAsync((void **)&d_pos, n * 4, c->stream));
-  HIPC(c, hipMallocAsync((void **)&d_ext, ext.size() * 8, c->stream));
-  HIPC(c, hipMemcpyAsync(d_pos, pos.data(), n * 4, hipMemcpyHostToDevice, c->stream));
-  HIPC(c, hipMemcpyAsync(d_ext, ext.data(), ext.size() * 8, hipMemcpyHostToDevice, c->stream));
+  ks_status st = xfer_begin(c, n * 4 + ext.size() * 8 + 1024, n * 4 + ext.size() * 8 + 1024);
+  if (st) return st;
+  uint32_t *d_pos = dscratch<uint32_t>(c, n);
+  uint64_t *d_ext = dscratch<uint64_t>(c, ext.size());
+  if ((st = h2d(c, d_pos, pos.data(), n * 4)) || (st = h2d(c, d_ext, ext.data(), ext.size() * 8))) return st;
   HIPC(c, launch_scatter_rows(c->t, d_pos, nullptr, d_ext, n, 2u, c->stream));
-  HIPC(c, hipFreeAsync(d_pos, c->stream));
-  HIPC(c, hipFreeAsync(d_ext, c->stream));
-  HIPC(c, hipStreamSynchronize(c->stream));
+  if ((st = xfer_sync(c))) return st;
   c->dirty_ext.clear();
   return KS_OK;
 }
@@ -631,8 +715,6 @@ ks_status collect_timing(ks_ctx *c) {
     c->ev_pool.push_back(pr.first);
     c->ev_pool.push_back(pr.second);
   }
-  c->stats.sweep_evals += c->pending_sweep_evals;
-  c->pending_sweep_evals = 0;
   c->ev_sweep.clear();
   c->ev_resolve.clear();
   return KS_OK;
@@ -679,6 +761,9 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t host_start) {
   a.frec = c->S == 1 ? c->d_srec : c->d_frec;
   a.results = b->d_results;
   a.counters = c->d_counters;
+  a.crow = c->d_crow;
+  a.cext = c->d_cext;
+  a.slot_pos = c->d_slot_pos;
   a.w = Weights{c->cfg.weight_fit, c->cfg.weight_balanced, c->cfg.weight_taint, c->cfg.weight_affinity,
                 c->cfg.weight_image};
   if ((size_t)nloc * c->P * bmax * sizeof(BlockRec) > c->brec_bytes)
@@ -704,10 +789,6 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t host_start) {
   if (c->timing) {
     HIPC(c, hipEventRecord(e1, c->stream));
     c->ev_sweep.emplace_back(e0, e1);
-    uint64_t nodes_local = 0;
-    for (uint32_t q = 0; q < nloc; ++q) nodes_local += c->shards[shard0 + q].count;
-    const uint64_t pods = std::min<uint64_t>(c->P, b->n - std::min(b->n, host_start));
-    c->pending_sweep_evals += pods * nodes_local;  // upper bound when the round resolves early
   }
   HIPC(c, launch_merge(a, nloc, c->stream));
   if (multi) {
@@ -716,6 +797,7 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t host_start) {
                            c->stream));
   }
   if (c->S > 1) HIPC(c, launch_merge_shards(a, c->stream));
+  HIPC(c, launch_gather_cand(a, b->ext, c->stream));
   if (c->timing) {
     e0 = get_event(c);
     e1 = get_event(c);
@@ -726,7 +808,6 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t host_start) {
     HIPC(c, hipEventRecord(e1, c->stream));
     c->ev_resolve.emplace_back(e0, e1);
   }
-  c->stats.rounds++;
   return KS_OK;
 }
 
@@ -816,10 +897,12 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
   HIPC(x, hipMemsetAsync(t.apods, 0xFF, (size_t)x->npos * 4, x->stream));  // every position empty
   if ((st = dalloc(x, &x->d_shards, x->S)) || (st = dalloc(x, &x->d_slot_pos, x->cap)) ||
       (st = dalloc(x, &x->d_start, 1)) || (st = dalloc(x, &x->d_norm, 2 * (size_t)x->P)) ||
-      (st = dalloc(x, &x->d_counters, 4)))
+      (st = dalloc(x, &x->d_counters, 16)))
     return st;
-  HIPC(x, hipMemcpyAsync(x->d_shards, x->shards.data(), x->S * sizeof(Shard), hipMemcpyHostToDevice, x->stream));
-  HIPC(x, hipMemcpyAsync(x->d_slot_pos, x->slot_pos.data(), (size_t)x->cap * 4, hipMemcpyHostToDevice, x->stream));
+  if ((st = xfer_begin(x, x->S * sizeof(Shard) + (size_t)x->cap * 4 + 1024, 0)) ||
+      (st = h2d(x, x->d_shards, x->shards.data(), x->S * sizeof(Shard))) ||
+      (st = h2d(x, x->d_slot_pos, x->slot_pos.data(), (size_t)x->cap * 4)))
+    return st;
   HIPC(x, hipHostMalloc((void **)&x->h_start, 4, hipHostMallocDefault));
   // round records: blocks of the widest kernel (npl 2 -> sub = npl / 2)
   uint32_t bmax = 0;
@@ -828,9 +911,10 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
   x->brec_bytes = (size_t)nloc * x->P * bmax * sizeof(BlockRec);
   if ((st = dalloc(x, (uint8_t **)&x->d_brec, x->brec_bytes))) return st;
   const size_t recs = (size_t)x->S * x->P * rec_words(x->K);
-  if ((st = dalloc(x, &x->d_srec, recs)) || (st = dalloc(x, &x->d_frec, (size_t)x->P * rec_words(x->K))))
+  if ((st = dalloc(x, &x->d_srec, recs)) || (st = dalloc(x, &x->d_frec, (size_t)x->P * rec_words(x->K))) ||
+      (st = dalloc(x, &x->d_crow, (size_t)x->P * x->K)) || (st = dalloc(x, &x->d_cext, (size_t)x->P * x->K)))
     return st;
-  HIPC(x, hipStreamSynchronize(x->stream));  // all initialisation is stream-ordered
+  if ((st = xfer_sync(x))) return st;  // all initialisation is stream-ordered
   *out = c.release();
   return KS_OK;
 }
@@ -842,10 +926,13 @@ void ks_close(ks_ctx *c) {
   if (c->comm) ncclCommDestroy(c->comm);
   void *bufs[] = {c->t.acpu, c->t.amem, c->t.rcpu, c->t.rmem, c->t.zcpu, c->t.zmem, c->t.apods,
                   c->t.npods, c->t.hard, c->t.prefer, c->t.lab, c->t.num, c->d_shards, c->d_slot_pos,
-                  c->d_start, c->d_norm, c->d_brec, c->d_srec, c->d_frec, c->d_counters};
+                  c->d_start, c->d_norm, c->d_brec, c->d_srec, c->d_frec, c->d_counters, c->d_crow,
+                  c->d_cext};
   for (void *b : bufs)
     if (b) (void)hipFree(b);
   if (c->h_start) (void)hipHostFree(c->h_start);
+  if (c->pin) (void)hipHostFree(c->pin);
+  if (c->dscr) (void)hipFree(c->dscr);
   for (auto &pr : c->ev_sweep) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
   for (auto &pr : c->ev_resolve) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
   for (auto e : c->ev_pool) (void)hipEventDestroy(e);
@@ -856,9 +943,12 @@ void ks_close(ks_ctx *c) {
 ks_status ks_nodes_upsert(ks_ctx *c, const ks_node *nodes, const uint32_t *slots, uint32_t n) {
   if (!c || (n && (!nodes || !slots))) return KS_ERR_INVALID;
   HIPC(c, hipSetDevice(c->cfg.device));
-  std::vector<uint32_t> pos(n);
-  std::vector<int64_t> core((size_t)n * 8);
-  std::vector<uint64_t> ext((size_t)n * (2 + LW + NNUM));
+  // Events are applied in order; a slot named twice in one call ends in its
+  // last state (one device row per distinct slot, so the scatter is race-free).
+  std::vector<uint32_t> pos;
+  std::vector<int64_t> core;
+  std::vector<uint64_t> ext;
+  std::unordered_map<uint32_t, uint32_t> row_of;  // slot -> row in the upload
   bool grew = false;
   for (uint32_t i = 0; i < n; ++i) {
     const ks_node &s = nodes[i];
@@ -869,15 +959,8 @@ ks_status ks_nodes_upsert(ks_ctx *c, const ks_node *nodes, const uint32_t *slots
       return c->fail(KS_ERR_RANGE, "node %s allocatable outside the exact range", str(s.name).c_str());
     HostNode &h = c->nodes[slot];
     const bool is_new = !h.present;
-    if (!is_new) {
-      c->name_slot.erase(h.name);
-      for (auto &kv : h.labels) {
-        auto &v = c->key_nodes[kv.first];
-        v.erase(std::remove(v.begin(), v.end(), slot), v.end());
-      }
-    } else {
-      c->n_present++;
-    }
+    if (!is_new) c->name_slot.erase(h.name);  // key_nodes entries are re-validated lazily
+    else c->n_present++;
     h.present = true;
     h.name = c->intern(s.name);
     c->name_slot[h.name] = slot;
@@ -931,35 +1014,38 @@ ks_status ks_nodes_upsert(ks_ctx *c, const ks_node *nodes, const uint32_t *slots
     c->hard_in_use |= h.hard;
     c->prefer_in_use |= h.prefer;
     node_ext_bits(c, h);
-    pos[i] = c->slot_pos[slot];
-    int64_t *cr = &core[(size_t)i * 8];
+    auto ins = row_of.emplace(slot, (uint32_t)pos.size());
+    const uint32_t row = ins.first->second;
+    if (ins.second) {
+      pos.push_back(c->slot_pos[slot]);
+      core.resize(core.size() + 8);
+      ext.resize(ext.size() + 2 + LW + NNUM);
+      core[(size_t)row * 8 + 3] = is_new ? 1 : 0;  // reset Requested iff absent before this call
+    }
+    int64_t *cr = &core[(size_t)row * 8];
     cr[0] = h.acpu;
     cr[1] = h.amem;
     cr[2] = h.apods;
-    cr[3] = is_new ? 1 : 0;
-    uint64_t *e = &ext[(size_t)i * (2 + LW + NNUM)];
+    uint64_t *e = &ext[(size_t)row * (2 + LW + NNUM)];
     e[0] = h.hard;
     e[1] = h.prefer;
     for (int k = 0; k < LW; ++k) e[2 + k] = h.lab[k];
     for (int k = 0; k < NNUM; ++k) e[2 + LW + k] = (uint64_t)h.num[k];
   }
   if (grew) c->dict_version++;
+  n = (uint32_t)pos.size();
   if (!n) return KS_OK;
-  uint32_t *d_pos;
-  int64_t *d_core;
-  uint64_t *d_ext;
-  HIPC(c, hipMalloc((void **)&d_pos, (size_t)n * 4));
-  HIPC(c, hipMalloc((void **)&d_core, core.size() * 8));
-  HIPC(c, hipMalloc((void **)&d_ext, ext.size() * 8));
-  HIPC(c, hipMemcpyAsync(d_pos, pos.data(), (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
-  HIPC(c, hipMemcpyAsync(d_core, core.data(), core.size() * 8, hipMemcpyHostToDevice, c->stream));
-  HIPC(c, hipMemcpyAsync(d_ext, ext.data(), ext.size() * 8, hipMemcpyHostToDevice, c->stream));
+  const size_t bytes = (size_t)n * 4 + core.size() * 8 + ext.size() * 8 + 1024;
+  ks_status st = xfer_begin(c, bytes, bytes);
+  if (st) return st;
+  uint32_t *d_pos = dscratch<uint32_t>(c, n);
+  int64_t *d_core = dscratch<int64_t>(c, core.size());
+  uint64_t *d_ext = dscratch<uint64_t>(c, ext.size());
+  if ((st = h2d(c, d_pos, pos.data(), (size_t)n * 4)) || (st = h2d(c, d_core, core.data(), core.size() * 8)) ||
+      (st = h2d(c, d_ext, ext.data(), ext.size() * 8)))
+    return st;
   HIPC(c, launch_scatter_rows(c->t, d_pos, d_core, d_ext, n, 1u, c->stream));
-  HIPC(c, hipStreamSynchronize(c->stream));
-  (void)hipFree(d_pos);
-  (void)hipFree(d_core);
-  (void)hipFree(d_ext);
-  return KS_OK;
+  return xfer_sync(c);
 }
 
 ks_status ks_nodes_delete(ks_ctx *c, const uint32_t *slots, uint32_t n) {
@@ -972,10 +1058,6 @@ ks_status ks_nodes_delete(ks_ctx *c, const uint32_t *slots, uint32_t n) {
       return c->fail(KS_ERR_NOT_FOUND, "slot %u not present", slots[i]);
     HostNode &h = c->nodes[slots[i]];
     c->name_slot.erase(h.name);
-    for (auto &kv : h.labels) {
-      auto &v = c->key_nodes[kv.first];
-      v.erase(std::remove(v.begin(), v.end(), slots[i]), v.end());
-    }
     h = HostNode();
     c->n_present--;
     pos[i] = c->slot_pos[slots[i]];
@@ -983,17 +1065,15 @@ ks_status ks_nodes_delete(ks_ctx *c, const uint32_t *slots, uint32_t n) {
     core[(size_t)i * 8 + 3] = 1;   // reset requested state
   }
   if (!n) return KS_OK;
-  uint32_t *d_pos;
-  int64_t *d_core;
-  HIPC(c, hipMalloc((void **)&d_pos, (size_t)n * 4));
-  HIPC(c, hipMalloc((void **)&d_core, core.size() * 8));
-  HIPC(c, hipMemcpyAsync(d_pos, pos.data(), (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
-  HIPC(c, hipMemcpyAsync(d_core, core.data(), core.size() * 8, hipMemcpyHostToDevice, c->stream));
+  const size_t bytes = (size_t)n * 4 + core.size() * 8 + 1024;
+  ks_status st = xfer_begin(c, bytes, bytes);
+  if (st) return st;
+  uint32_t *d_pos = dscratch<uint32_t>(c, n);
+  int64_t *d_core = dscratch<int64_t>(c, core.size());
+  if ((st = h2d(c, d_pos, pos.data(), (size_t)n * 4)) || (st = h2d(c, d_core, core.data(), core.size() * 8)))
+    return st;
   HIPC(c, launch_scatter_rows(c->t, d_pos, d_core, nullptr, n, 0u, c->stream));
-  HIPC(c, hipStreamSynchronize(c->stream));
-  (void)hipFree(d_pos);
-  (void)hipFree(d_core);
-  return KS_OK;
+  return xfer_sync(c);
 }
 
 static ks_status pods_delta(ks_ctx *c, const ks_pod *pods, const uint32_t *slots, uint32_t n, int sign) {
@@ -1017,17 +1097,14 @@ static ks_status pods_delta(ks_ctx *c, const ks_pod *pods, const uint32_t *slots
     x[3] = sign * zm;
     x[4] = sign;
   }
-  uint32_t *d_pos;
-  int64_t *d_d;
-  HIPC(c, hipMalloc((void **)&d_pos, (size_t)n * 4));
-  HIPC(c, hipMalloc((void **)&d_d, d.size() * 8));
-  HIPC(c, hipMemcpyAsync(d_pos, pos.data(), (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
-  HIPC(c, hipMemcpyAsync(d_d, d.data(), d.size() * 8, hipMemcpyHostToDevice, c->stream));
+  const size_t bytes = (size_t)n * 4 + d.size() * 8 + 1024;
+  ks_status st = xfer_begin(c, bytes, bytes);
+  if (st) return st;
+  uint32_t *d_pos = dscratch<uint32_t>(c, n);
+  int64_t *d_d = dscratch<int64_t>(c, d.size());
+  if ((st = h2d(c, d_pos, pos.data(), (size_t)n * 4)) || (st = h2d(c, d_d, d.data(), d.size() * 8))) return st;
   HIPC(c, launch_apply_deltas(c->t, d_pos, d_d, n, c->stream));
-  HIPC(c, hipStreamSynchronize(c->stream));
-  (void)hipFree(d_pos);
-  (void)hipFree(d_d);
-  return KS_OK;
+  return xfer_sync(c);
 }
 
 ks_status ks_pods_add(ks_ctx *c, const ks_pod *pods, const uint32_t *slots, uint32_t n) {
@@ -1059,10 +1136,12 @@ ks_status ks_batch_prepare(ks_ctx *c, const ks_pod *pods, uint32_t n, ks_batch *
   HIPC(c, hipMalloc((void **)&b->d_pods, dev.size() * sizeof(PodDev)));
   HIPC(c, hipMalloc((void **)&b->d_clauses, cl.w.size() * 8));
   HIPC(c, hipMalloc((void **)&b->d_results, std::max<uint32_t>(n, 1) * sizeof(DevResult)));
-  HIPC(c, hipMemcpyAsync(b->d_pods, dev.data(), dev.size() * sizeof(PodDev), hipMemcpyHostToDevice, c->stream));
-  HIPC(c, hipMemcpyAsync(b->d_clauses, cl.w.data(), cl.w.size() * 8, hipMemcpyHostToDevice, c->stream));
+  const size_t bytes = dev.size() * sizeof(PodDev) + cl.w.size() * 8 + 1024;
+  if ((st = xfer_begin(c, bytes, 0)) || (st = h2d(c, b->d_pods, dev.data(), dev.size() * sizeof(PodDev))) ||
+      (st = h2d(c, b->d_clauses, cl.w.data(), cl.w.size() * 8)))
+    return st;
   HIPC(c, hipMemsetAsync(b->d_results, 0, std::max<uint32_t>(n, 1) * sizeof(DevResult), c->stream));
-  HIPC(c, hipStreamSynchronize(c->stream));
+  if ((st = xfer_sync(c))) return st;
   *out = b.release();
   return KS_OK;
 }
@@ -1094,7 +1173,6 @@ ks_status ks_batch_run(ks_ctx *c, ks_batch *b) {
     ks_status st = collect_timing(c);
     if (st) return st;
   }
-  c->stats.pods_resolved += b->n;
   return KS_OK;
 }
 
@@ -1102,8 +1180,11 @@ ks_status ks_batch_results(ks_ctx *c, const ks_batch *b, ks_result *out) {
   if (!c || !b || (b->n && !out)) return KS_ERR_INVALID;
   static_assert(sizeof(ks_result) == sizeof(DevResult), "result layout");
   HIPC(c, hipSetDevice(c->cfg.device));
-  HIPC(c, hipMemcpyAsync(out, b->d_results, (size_t)b->n * sizeof(DevResult), hipMemcpyDeviceToHost, c->stream));
-  HIPC(c, hipStreamSynchronize(c->stream));
+  const size_t bytes = (size_t)b->n * sizeof(DevResult) + 1024;
+  ks_status st;
+  if ((st = xfer_begin(c, bytes, 0)) || (st = d2h(c, out, b->d_results, (size_t)b->n * sizeof(DevResult))) ||
+      (st = xfer_sync(c)))
+    return st;
   for (uint32_t i = 0; i < b->n; ++i)
     if (out[i].status == KS_POD_SCHEDULED) c->stats.pods_scheduled++;
   return KS_OK;
@@ -1143,29 +1224,21 @@ ks_status ks_plugin_scores(ks_ctx *c, const ks_pod *pod, ks_node_score *out) {
   a.w = Weights{c->cfg.weight_fit, c->cfg.weight_balanced, c->cfg.weight_taint, c->cfg.weight_affinity,
                 c->cfg.weight_image};
   a.slot_pos = c->d_slot_pos;
-  PodDev *d_pod;
-  uint64_t *d_cl;
-  uint32_t *d_norm;
-  int32_t *d_out;
-  HIPC(c, hipMalloc((void **)&d_pod, sizeof(PodDev)));
-  HIPC(c, hipMalloc((void **)&d_cl, cl.w.size() * 8));
-  HIPC(c, hipMalloc((void **)&d_norm, 8));
-  HIPC(c, hipMalloc((void **)&d_out, (size_t)c->cap * 10 * 4));
-  HIPC(c, hipMemcpyAsync(d_pod, &d, sizeof d, hipMemcpyHostToDevice, c->stream));
-  HIPC(c, hipMemcpyAsync(d_cl, cl.w.data(), cl.w.size() * 8, hipMemcpyHostToDevice, c->stream));
+  std::vector<int32_t> raw((size_t)c->cap * 10);
+  const size_t bytes = sizeof(PodDev) + cl.w.size() * 8 + 8 + raw.size() * 4 + 2048;
+  if ((st = xfer_begin(c, bytes, bytes))) return st;
+  PodDev *d_pod = dscratch<PodDev>(c, 1);
+  uint64_t *d_cl = dscratch<uint64_t>(c, cl.w.size());
+  uint32_t *d_norm = dscratch<uint32_t>(c, 2);
+  int32_t *d_out = dscratch<int32_t>(c, raw.size());
+  if ((st = h2d(c, d_pod, &d, sizeof d)) || (st = h2d(c, d_cl, cl.w.data(), cl.w.size() * 8))) return st;
   HIPC(c, hipMemsetAsync(d_norm, 0, 8, c->stream));
   a.pods = d_pod;
   a.clauses = d_cl;
   a.norm_max = d_norm;
   a.out = d_out;
   HIPC(c, launch_dump(a, c->stream));
-  std::vector<int32_t> raw((size_t)c->cap * 10);
-  HIPC(c, hipMemcpyAsync(raw.data(), d_out, raw.size() * 4, hipMemcpyDeviceToHost, c->stream));
-  HIPC(c, hipStreamSynchronize(c->stream));
-  (void)hipFree(d_pod);
-  (void)hipFree(d_cl);
-  (void)hipFree(d_norm);
-  (void)hipFree(d_out);
+  if ((st = d2h(c, raw.data(), d_out, raw.size() * 4)) || (st = xfer_sync(c))) return st;
   for (uint32_t i = 0; i < c->cap; ++i) {
     const int32_t *o = &raw[(size_t)i * 10];
     ks_node_score s{};
@@ -1192,17 +1265,15 @@ ks_status ks_node_states(ks_ctx *c, const uint32_t *slots, uint32_t n, ks_node_s
     if (slots[i] >= c->cap) return c->fail(KS_ERR_NOT_FOUND, "slot %u >= capacity", slots[i]);
     pos[i] = c->slot_pos[slots[i]];
   }
-  uint32_t *d_pos;
-  int64_t *d_out;
-  HIPC(c, hipMalloc((void **)&d_pos, (size_t)n * 4));
-  HIPC(c, hipMalloc((void **)&d_out, (size_t)n * 64));
-  HIPC(c, hipMemcpyAsync(d_pos, pos.data(), (size_t)n * 4, hipMemcpyHostToDevice, c->stream));
-  HIPC(c, launch_gather_rows(c->t, d_pos, d_out, n, c->stream));
   std::vector<int64_t> raw((size_t)n * 8);
-  HIPC(c, hipMemcpyAsync(raw.data(), d_out, raw.size() * 8, hipMemcpyDeviceToHost, c->stream));
-  HIPC(c, hipStreamSynchronize(c->stream));
-  (void)hipFree(d_pos);
-  (void)hipFree(d_out);
+  const size_t bytes = (size_t)n * 4 + raw.size() * 8 + 1024;
+  ks_status st = xfer_begin(c, bytes, bytes);
+  if (st) return st;
+  uint32_t *d_pos = dscratch<uint32_t>(c, n);
+  int64_t *d_out = dscratch<int64_t>(c, raw.size());
+  if ((st = h2d(c, d_pos, pos.data(), (size_t)n * 4))) return st;
+  HIPC(c, launch_gather_rows(c->t, d_pos, d_out, n, c->stream));
+  if ((st = d2h(c, raw.data(), d_out, raw.size() * 8)) || (st = xfer_sync(c))) return st;
   for (uint32_t i = 0; i < n; ++i) {
     const int64_t *r = &raw[(size_t)i * 8];
     ks_node_state s{};
@@ -1237,16 +1308,58 @@ ks_status ks_comm_init(ks_ctx *c, const uint8_t id[KS_COMM_ID_BYTES]) {
   return KS_OK;
 }
 
+ks_status ks_comm_allreduce_max(ks_ctx *c, double *values, uint32_t n) {
+  if (!c || (n && !values)) return KS_ERR_INVALID;
+  if (!c->comm) return c->fail(KS_ERR_COMM, "ks_comm_init not called");
+  HIPC(c, hipSetDevice(c->cfg.device));
+  ks_status st = xfer_begin(c, 2 * (size_t)n * 8 + 1024, (size_t)n * 8 + 1024);
+  if (st) return st;
+  double *d = dscratch<double>(c, n);
+  if ((st = h2d(c, d, values, (size_t)n * 8))) return st;
+  NCCLC(c, ncclAllReduce(d, d, n, ncclFloat64, ncclMax, c->comm, c->stream));
+  if ((st = d2h(c, values, d, (size_t)n * 8))) return st;
+  return xfer_sync(c);
+}
+
+static ks_status read_counters(ks_ctx *c, uint64_t out[4]) {
+  HIPC(c, hipSetDevice(c->cfg.device));
+  ks_status st;
+  if ((st = xfer_begin(c, 1024, 0)) || (st = d2h(c, out, c->d_counters, 4 * sizeof(uint64_t)))) return st;
+  return xfer_sync(c);
+}
+
 ks_status ks_get_stats(ks_ctx *c, ks_stats *out) {
   if (!c || !out) return KS_ERR_INVALID;
+  uint64_t k[4];
+  ks_status st = read_counters(c, k);
+  if (st) return st;
   *out = c->stats;
+  // (pod, node) evaluations of this rank's sweeps: pods swept x present local nodes
+  const bool multi = c->cfg.world_size > 1;
+  uint64_t local = 0;
+  for (uint32_t q = 0; q < c->S; ++q) {
+    if (multi && q != c->cfg.rank) continue;
+    const Shard &sh = c->shards[q];
+    for (uint32_t l = 0; l < sh.count; ++l) local += c->nodes[sh.lo + l].present;
+  }
+  out->sweep_evals = (k[2] - c->counters_base[2]) * local;
+  out->rounds = k[0] - c->counters_base[0];
+  out->pods_resolved = k[1] - c->counters_base[1];
   return KS_OK;
 }
 
 ks_status ks_reset_stats(ks_ctx *c) {
   if (!c) return KS_ERR_INVALID;
   c->stats = ks_stats{};
-  return KS_OK;
+  return read_counters(c, c->counters_base);
+}
+
+ks_status ks_debug_counters(ks_ctx *c, uint64_t out[16]) {
+  if (!c || !out) return KS_ERR_INVALID;
+  HIPC(c, hipSetDevice(c->cfg.device));
+  ks_status st;
+  if ((st = xfer_begin(c, 1024, 0)) || (st = d2h(c, out, c->d_counters, 16 * sizeof(uint64_t)))) return st;
+  return xfer_sync(c);
 }
 
 ks_status ks_set_timing(ks_ctx *c, int32_t enabled) {

@@ -631,6 +631,44 @@ __global__ __launch_bounds__(256) void merge_shards_kernel(RoundArgs a) {
   }
 }
 
+// ============================================================ gather rows
+// grid: x = pod in round.  For every listed candidate of the final record,
+// copy the node's S0 row (and label / taint columns) next to the key.
+template <bool EXT>
+__global__ __launch_bounds__(256) void gather_cand_kernel(RoundArgs a) {
+  const uint32_t start = uniform_u32(*a.d_start);
+  const uint32_t r = blockIdx.x;
+  if (start + r >= a.npods || r >= a.P) return;
+  const uint64_t *rec = a.frec + (size_t)r * rec_words(a.K);
+  const uint32_t nk = ((const ShardRecHdr *)rec)->nkeys;
+  for (uint32_t t = threadIdx.x; t < nk; t += blockDim.x) {
+    const uint64_t k = rec[REC_HDR_WORDS + t];
+    const uint32_t pos = a.slot_pos[0xFFFFFFFFu - (uint32_t)k];
+    CandRow w;
+    w.acpu = a.t.acpu[pos];
+    w.amem = a.t.amem[pos];
+    w.rc = a.t.rcpu[pos];
+    w.rm = a.t.rmem[pos];
+    w.zc = a.t.zcpu[pos];
+    w.zm = a.t.zmem[pos];
+    w.apods = a.t.apods[pos];
+    w.np = a.t.npods[pos];
+    w.pos = pos;
+    w._pad = 0;
+    a.crow[(size_t)r * a.K + t] = w;
+    if (EXT) {
+      CandExt x;
+      x.w[0] = a.t.hard[pos];
+      x.w[1] = a.t.prefer[pos];
+#pragma unroll
+      for (int q = 0; q < LW; ++q) x.w[2 + q] = a.t.lab[(size_t)q * a.t.npos + pos];
+#pragma unroll
+      for (int q = 0; q < NNUM; ++q) x.w[2 + LW + q] = (uint64_t)a.t.num[(size_t)q * a.t.npos + pos];
+      a.cext[(size_t)r * a.K + t] = x;
+    }
+  }
+}
+
 // ================================================================= resolve
 // One workgroup walks the round's pods in queue order:
 // pod i's winner is the best of (a) its first listed candidate that no pod
@@ -651,33 +689,6 @@ constexpr int RHASH = 1024;
 
 __device__ __forceinline__ uint32_t rhash(uint32_t x) { return (x * 2654435761u) >> 22; }  // 10 bits
 
-__device__ __forceinline__ uint32_t slot_position(const RoundArgs &a, uint32_t slot) {
-  for (uint32_t q = 0; q < a.total_shards; ++q) {
-    const Shard sq = a.shards[q];
-    if (slot - sq.lo < sq.count) return shard_pos(sq, a.lnpl, slot - sq.lo);
-  }
-  return 0;
-}
-
-// A node row as prefetched into registers (S0 = round-start state).
-struct RowRegs {
-  int64_t acpu, amem, rc, rm, zc, zm;
-  int32_t apods, np;
-  uint32_t pos;
-};
-
-__device__ __forceinline__ void fetch_row(const RoundArgs &a, uint32_t pos, RowRegs &w) {
-  w.pos = pos;
-  w.acpu = a.t.acpu[pos];
-  w.amem = a.t.amem[pos];
-  w.rc = a.t.rcpu[pos];
-  w.rm = a.t.rmem[pos];
-  w.zc = a.t.zcpu[pos];
-  w.zm = a.t.zmem[pos];
-  w.apods = a.t.apods[pos];
-  w.np = a.t.npods[pos];
-}
-
 __device__ __forceinline__ NodeRegs regs_from(int64_t acpu, int64_t amem, int64_t rc, int64_t rm, int64_t zc,
                                               int64_t zm, int32_t apods, int32_t np, uint32_t slot) {
   NodeRegs r;
@@ -695,6 +706,28 @@ __device__ __forceinline__ NodeRegs regs_from(int64_t acpu, int64_t amem, int64_
   r.bits = 1u | ((int64_t)np + 1 <= (int64_t)apods ? 2u : 0u) | (acpu ? 4u : 0u) | (amem ? 8u : 0u);
   return r;
 }
+
+// Workgroup barrier for LDS hand-offs only: __syncthreads() also drains vmcnt,
+// which would expose the next pod's prefetch latency on every iteration.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// Diagnostic build (-DKS_STAMPS): wave 0 accumulates s_memtime per phase into
+// a.stamps[0..7]; never compiled into the measured library.
+#ifdef KS_STAMPS
+#define STAMP(i)                                                                         \
+  do {                                                                                   \
+    __builtin_amdgcn_sched_barrier(0);                                                   \
+    uint64_t t_;                                                                         \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");            \
+    __builtin_amdgcn_sched_barrier(0);                                                   \
+    if (tid == 0) { stamp_acc[i] += t_ - stamp_last; }                                   \
+    stamp_last = t_;                                                                     \
+  } while (0)
+#else
+#define STAMP(i) do {} while (0)
+#endif
 
 template <bool EXT>
 __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
@@ -734,31 +767,28 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
   }
   for (uint32_t i = tid; i < RHASH; i += RESOLVE_THREADS) s_hkey[i] = 0;
   if (tid == 0) { s_nmod = 0; s_stop = nround; }
-  // prefetch pod 0's candidates (thread t holds list entry t) and their S0 rows
+  // prefetch pod 0's candidates (thread t holds list entry t, its key and S0 row):
+  // independent loads of the gathered candidate rows, consumed one pod later
   uint64_t ck = 0;
-  RowRegs crow{};
-  uint64_t cext[2 + LW + NNUM];
-  auto prefetch = [&](uint32_t r, uint64_t &k, RowRegs &w, uint64_t *ex) {
-    k = 0;
-    if (r < nround && tid < a.K) {
-      k = a.frec[(size_t)r * RW + REC_HDR_WORDS + tid];
-      if (k) {
-        fetch_row(a, slot_position(a, 0xFFFFFFFFu - (uint32_t)k), w);
-        if (EXT) {
-          ex[0] = a.t.hard[w.pos];
-          ex[1] = a.t.prefer[w.pos];
-#pragma unroll
-          for (int q = 0; q < LW; ++q) ex[2 + q] = a.t.lab[(size_t)q * a.t.npos + w.pos];
-#pragma unroll
-          for (int q = 0; q < NNUM; ++q) ex[2 + LW + q] = (uint64_t)a.t.num[(size_t)q * a.t.npos + w.pos];
-        }
-      }
-    }
+  CandRow crow{};
+  CandExt cext{};
+  auto prefetch = [&](uint32_t r, uint64_t &k, CandRow &w, CandExt &x) {
+    const bool on = r < nround && tid < a.K;
+    const uint32_t rr = on ? r : 0, tt = on ? tid : 0;
+    k = a.frec[(size_t)rr * RW + REC_HDR_WORDS + tt];
+    w = a.crow[(size_t)rr * a.K + tt];
+    if (EXT) x = a.cext[(size_t)rr * a.K + tt];
+    if (!on) k = 0;
   };
   prefetch(0, ck, crow, cext);
   __syncthreads();
+#ifdef KS_STAMPS
+  uint64_t stamp_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, stamp_last = 0;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(stamp_last)::"memory");
+#endif
 
   for (uint32_t r = 0; r < nround; ++r) {
+    STAMP(0);
     const PodDev &p = s_pod[r];
     const ShardRecHdr &hdr = s_hdr[r];
     const uint32_t pi = start + r;
@@ -769,8 +799,8 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
     }
     // next pod's candidates: issued now, consumed next iteration
     uint64_t nk;
-    RowRegs nrow{};
-    uint64_t next_ext[2 + LW + NNUM];
+    CandRow nrow;
+    CandExt next_ext;
     prefetch(r + 1, nk, nrow, next_ext);
 
     // (a) re-score modified nodes against the live rows
@@ -810,6 +840,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
         }
       }
     }
+    STAMP(1);
     // (b) is my listed candidate unmodified?
     bool unmod = false;
     if (ck != 0 && tid < hdr.nkeys) {
@@ -821,6 +852,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
         h = (h + 1) & (RHASH - 1);
       }
     }
+    STAMP(2);
     // wave partials
     const uint64_t ub = __ballot(unmod);
     const uint64_t wmkey = wave_max_u64(mkey);
@@ -847,7 +879,9 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
     } else if (lane == 0) {
       s_widx[wid] = 0xFFFFFFFFu;
     }
-    __syncthreads();
+    STAMP(3);
+    lds_barrier();
+    STAMP(4);
     // every thread combines the partials (identical decision, no broadcast barrier)
     uint64_t bm = 0, ku = 0;
     uint32_t fu = 0xFFFFFFFFu;
@@ -892,6 +926,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
       res.flags = (win && feasible == 1) ? 1u : 0u;
       ((DevResult *)a.results)[pi] = res;
     }
+    STAMP(5);
     // commit (AssumePod -> NodeInfo.AddPod on the live row): exactly one thread
     if (win) {
       if (win == ku && fu != 0xFFFFFFFFu && tid == fu) {
@@ -918,7 +953,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
         s_zm[m] = crow.zm + p.nz_mem;
         s_np[m] = crow.np + 1;
         if (EXT)
-          for (int q = 0; q < 2 + LW + NNUM; ++q) s_ext[m][q] = cext[q];
+          for (int q = 0; q < 2 + LW + NNUM; ++q) s_ext[m][q] = cext.w[q];
         s_nmod = m + 1;
       } else if (win == bm && win != ku) {
         for (uint32_t m = tid; m < nmod; m += RESOLVE_THREADS) {
@@ -932,11 +967,12 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
         }
       }
     }
-    __syncthreads();
+    STAMP(6);
+    lds_barrier();
+    STAMP(7);
     ck = nk;
     crow = nrow;
-    if (EXT)
-      for (int q = 0; q < 2 + LW + NNUM; ++q) cext[q] = next_ext[q];
+    if (EXT) cext = next_ext;
   }
   __syncthreads();
   // write back live rows of modified nodes and advance the queue
@@ -949,6 +985,10 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
     a.t.zmem[pos] = s_zm[i];
     a.t.npods[pos] = s_np[i];
   }
+#ifdef KS_STAMPS
+  if (tid == 0)
+    for (int i = 0; i < 8; ++i) atomicAdd((unsigned long long *)&a.counters[8 + i], (unsigned long long)stamp_acc[i]);
+#endif
   if (tid == 0) {
     *a.d_start = start + s_stop;
     a.counters[0] += 1;                                   // rounds
@@ -1109,6 +1149,12 @@ hipError_t launch_merge(const RoundArgs &a, uint32_t nshards, hipStream_t st) {
 
 hipError_t launch_merge_shards(const RoundArgs &a, hipStream_t st) {
   merge_shards_kernel<<<dim3(a.P), 256, 0, st>>>(a);
+  return hipGetLastError();
+}
+
+hipError_t launch_gather_cand(const RoundArgs &a, bool ext, hipStream_t st) {
+  if (ext) gather_cand_kernel<true><<<a.P, 256, 0, st>>>(a);
+  else gather_cand_kernel<false><<<a.P, 256, 0, st>>>(a);
   return hipGetLastError();
 }
 

@@ -32,6 +32,9 @@ struct RoundArgs {
   uint64_t *srec;             // [S][P][rec_words(K)]
   uint64_t *frec;             // [P][rec_words(K)] (== srec when S == 1)
   void *results;              // DevResult[npods]
+  CandRow *crow;              // [P][K] S0 rows of the final candidates
+  CandExt *cext;              // [P][K] their label / taint columns (EXT batches)
+  const uint32_t *slot_pos;   // slot -> position
   uint64_t *counters;         // [0] rounds, [1] pods resolved
   Weights w;
 };
@@ -53,6 +56,7 @@ hipError_t launch_sweep(const RoundArgs &a, bool ext, uint32_t nblocks, uint32_t
                         hipStream_t st);
 hipError_t launch_merge(const RoundArgs &a, uint32_t nshards, hipStream_t st);
 hipError_t launch_merge_shards(const RoundArgs &a, hipStream_t st);
+hipError_t launch_gather_cand(const RoundArgs &a, bool ext, hipStream_t st);
 hipError_t launch_resolve(const RoundArgs &a, bool ext, hipStream_t st);
 hipError_t launch_scatter_rows(const NodeTable &t, const uint32_t *pos, const int64_t *core, const uint64_t *ext,
                                uint32_t n, uint32_t flags, hipStream_t st);

@@ -10,6 +10,8 @@ import os
 from pathlib import Path
 
 LIB_DIR = Path(__file__).resolve().parent / "lib"
+# KSCHED_LIB_DIR selects a diagnostic libksched build (e.g. lib/stamps)
+KSCHED_DIR = Path(os.environ.get("KSCHED_LIB_DIR", LIB_DIR))
 
 c_char_p = C.c_char_p
 
@@ -190,7 +192,8 @@ KSCHED_SYMBOLS = [
     "ks_config_default", "ks_open", "ks_close", "ks_last_error", "ks_abi_version", "ks_nodes_upsert",
     "ks_nodes_delete", "ks_pods_add", "ks_pods_remove", "ks_schedule", "ks_batch_prepare", "ks_batch_run",
     "ks_batch_results", "ks_batch_free", "ks_plugin_scores", "ks_node_states", "ks_comm_unique_id",
-    "ks_comm_init", "ks_get_stats", "ks_reset_stats", "ks_set_timing",
+    "ks_comm_init", "ks_comm_allreduce_max", "ks_get_stats", "ks_reset_stats", "ks_set_timing",
+    "ks_debug_counters",
 ]
 KSYNTH_SYMBOLS = [
     "ksynth_nodes", "ksynth_pods", "ksynth_prefill", "ksynth_besteffort_pods", "ksynth_node_array",
@@ -204,8 +207,8 @@ class KschedError(RuntimeError):
         self.status = status
 
 
-def _load(name: str) -> C.CDLL:
-    path = LIB_DIR / name
+def _load(name: str, where: Path = LIB_DIR) -> C.CDLL:
+    path = where / name
     if not path.exists():
         raise ImportError(
             f"{path} is missing: build the HIP extension first (python -c 'import __graft_entry__ as g; g.build()')"
@@ -222,7 +225,7 @@ def ksched_lib() -> C.CDLL:
     global _ksched
     if _ksched is not None:
         return _ksched
-    L = _load("libksched.so")
+    L = _load("libksched.so", KSCHED_DIR)
     P = C.POINTER
     vp = C.c_void_p
     L.ks_config_default.argtypes = [P(KsConfig)]
@@ -247,9 +250,11 @@ def ksched_lib() -> C.CDLL:
     L.ks_node_states.argtypes = [vp, P(C.c_uint32), C.c_uint32, P(KsNodeState)]
     L.ks_comm_unique_id.argtypes = [P(C.c_uint8)]
     L.ks_comm_init.argtypes = [vp, P(C.c_uint8)]
+    L.ks_comm_allreduce_max.argtypes = [vp, P(C.c_double), C.c_uint32]
     L.ks_get_stats.argtypes = [vp, P(KsStats)]
     L.ks_reset_stats.argtypes = [vp]
     L.ks_set_timing.argtypes = [vp, C.c_int32]
+    L.ks_debug_counters.argtypes = [vp, P(C.c_uint64)]
     for f in KSCHED_SYMBOLS:
         fn = getattr(L, f)
         if fn.restype is C.c_int and f not in ("ks_abi_version",):

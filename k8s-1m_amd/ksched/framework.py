@@ -301,6 +301,12 @@ class Scheduler:
         buf = (C.c_uint8 * 128).from_buffer_copy(uid)
         self._ok(self.lib.ks_comm_init(self.ctx, buf))
 
+    def allreduce_max(self, values):
+        """Element-wise max over ranks (RCCL); doubles as a barrier."""
+        arr = (C.c_double * max(1, len(values)))(*values)
+        self._ok(self.lib.ks_comm_allreduce_max(self.ctx, arr, len(values)))
+        return list(arr)[: len(values)]
+
 
 def results_to_arrays(raw, n: int):
     """(node_index[int32], total_score[int64], status[int32], feasible[uint32]) numpy views."""

@@ -120,7 +120,7 @@ def test_capacity_with_empty_slots_and_deletes():
     cap, n = 2600, 2000
     ns = synth.nodes(synth.HETERO, n, 31)
     ps = synth.pods(synth.HETERO, 2000, 32)
-    slots = (C.c_uint32 * n)(*[i * 13 % cap for i in range(n)])  # scattered slots
+    slots = (C.c_uint32 * n)(*[i * 7 % cap for i in range(n)])  # scattered, distinct slots
     o = pyoracle.Oracle(cap)
     o.upsert(ns.nodes, slots, n)
     s = Scheduler(cap, pods_per_round=128)
@@ -135,6 +135,21 @@ def test_capacity_with_empty_slots_and_deletes():
     want2 = o.schedule(rest, 1000)
     got2 = s.schedule_raw(rest, 1000)
     assert_results_equal(got2, want2, 1000, "after delete")
+    s.close()
+
+
+def test_duplicate_slots_in_one_upsert():
+    # one call naming a slot several times: events apply in order (last state wins)
+    cap, n = 300, 1200
+    ns = synth.nodes(synth.LABELED, n, 51)
+    ps = synth.pods(synth.LABELED, 800, 52)
+    slots = (C.c_uint32 * n)(*[(i * 37) % cap for i in range(n)])
+    o = pyoracle.Oracle(cap)
+    o.upsert(ns.nodes, slots, n)
+    s = Scheduler(cap, pods_per_round=64)
+    s.upsert_nodes_raw(ns.nodes, slots, n)
+    assert_results_equal(s.schedule_raw(ps.pods, 800), o.schedule(ps.pods, 800), 800, "dup slots")
+    assert np.array_equal(state_array(s.node_states(list(range(cap)))), state_array(o.node_states(list(range(cap)))))
     s.close()
 
 

@@ -1,0 +1,32 @@
+"""Per-phase cycle breakdown of the resolve kernel (diagnostic KS_STAMPS build).
+
+KSCHED_LIB_DIR=k8s-1m_amd/ksched/lib/stamps python tools/resolve_stamps.py [nodes] [pods]
+Shares of wave 0's cycles per pod; the stamps' own cost inflates absolute times.
+"""
+import ctypes as C
+import os
+import sys
+
+sys.path.insert(0, "k8s-1m_amd")
+from ksched import Scheduler, synth  # noqa: E402
+
+nodes = int(sys.argv[1]) if len(sys.argv) > 1 else 200000
+npods = int(sys.argv[2]) if len(sys.argv) > 2 else 8192
+kind = synth.HETERO
+s = Scheduler(nodes, pods_per_round=256)
+ns = synth.nodes(kind, nodes, 1)
+s.upsert_nodes_raw(ns.nodes, synth.slot_array(nodes), nodes)
+pf = synth.prefill(kind, nodes, 1, 3, 0.5)
+assert s.lib.ks_pods_add(s.ctx, pf.pods, pf.slot_ptr, pf.n_pods) == 0
+ps = synth.pods(kind, npods, 2)
+b = s.prepare(ps.pods, npods)
+s.run(b)
+k = (C.c_uint64 * 16)()
+assert s.lib.ks_debug_counters(s.ctx, k) == 0
+names = ["top->modified", "modified eval", "list check", "wave partials", "barrier1", "decide", "commit", "barrier2"]
+tot = sum(k[8:16])
+pods = k[1]
+print(f"lib={os.environ.get('KSCHED_LIB_DIR', 'default')} rounds={k[0]} pods={pods}")
+for i, nm in enumerate(names):
+    print(f"  {nm:15s} {k[8 + i] / max(1, pods):10.0f} cyc/pod  {100 * k[8 + i] / max(1, tot):5.1f}%")
+print(f"  total {tot / max(1, pods):.0f} cyc/pod")
