@@ -44,7 +44,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=8192, help="pods per step")
     ap.add_argument("--pods-per-round", type=int, default=256)
     ap.add_argument("--topk", type=int, default=0)
-    ap.add_argument("--nodes-per-lane", type=int, default=8)
+    ap.add_argument("--nodes-per-lane", type=int, default=4)
     ap.add_argument("--kind", default="hetero", choices=["hetero", "kwok", "labeled"])
     ap.add_argument("--prefill", type=float, default=0.5)
     ap.add_argument("--cpu-pods", type=int, default=40, help="oracle sample size (pods) for cpu_baseline")

@@ -223,7 +223,7 @@ typedef struct {
   uint32_t node_capacity;    /* node slots (index space)                         */
   uint32_t pods_per_round;   /* P: pods evaluated per sweep (0 = default 256)    */
   uint32_t topk;             /* K: candidates kept per pod (0 = P)               */
-  uint32_t nodes_per_lane;   /* nodes held per GPU lane in the sweep (0 = 8)     */
+  uint32_t nodes_per_lane;   /* nodes held per GPU lane in the sweep (0 = 4)     */
   uint32_t world_size;       /* GPUs sharding the node index space (1 = no RCCL) */
   uint32_t rank;             /* this GPU's shard                                 */
   uint32_t virtual_shards;   /* >1: emulate that many shards on this one device  */

@@ -68,6 +68,7 @@ enum PodFlags : uint32_t {
 struct alignas(16) PodDev {
   int64_t req_cpu, req_mem;  // PodRequests (Fit filter, BalancedAllocation)
   int64_t nz_cpu, nz_mem;    // PodRequests with non-missing defaults (LeastAllocated)
+  double req_cpu_d, req_mem_d, nz_cpu_d, nz_mem_d;  // the same, exact in binary64 (< 2^46)
   uint64_t tol_hard;         // hard-taint bits tolerated (+ UNSCHED_BIT)
   uint64_t tol_prefer;       // prefer-taint bits tolerated by "" / PreferNoSchedule tolerations
   uint32_t flags;
@@ -77,7 +78,7 @@ struct alignas(16) PodDev {
   uint32_t n_req_terms;      // OR terms after the mandatory nodeSelector group
   uint32_t _pad[5];
 };
-static_assert(sizeof(PodDev) == 96, "PodDev layout");
+static_assert(sizeof(PodDev) == 128, "PodDev layout");
 
 // A clause is one label-selector requirement, 6 x u64:
 //   w0 = kind | num_col << 8 | term << 16 | (uint64)weight << 32

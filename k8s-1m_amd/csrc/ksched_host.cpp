@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -555,6 +556,12 @@ ks_status compile_pod(ks_ctx *c, const ks_pod &p, PodDev &d, ClauseBuf &cl) {
   if (d.req_cpu < 0 || d.req_mem < 0 || d.req_cpu >= kMaxExact || d.req_mem >= kMaxExact)
     return c->fail(KS_ERR_RANGE, "pod %s requests outside [0, 2^46)", str(p.name).c_str());
   if (d.req_cpu != 0 || d.req_mem != 0) d.flags |= PF_HAS_REQ;
+  if (d.nz_cpu >= kMaxExact || d.nz_mem >= kMaxExact)
+    return c->fail(KS_ERR_RANGE, "pod %s requests outside [0, 2^46)", str(p.name).c_str());
+  d.req_cpu_d = (double)d.req_cpu;
+  d.req_mem_d = (double)d.req_mem;
+  d.nz_cpu_d = (double)d.nz_cpu;
+  d.nz_mem_d = (double)d.nz_mem;
   // tolerations -> dictionary masks
   std::vector<Tol> tols, tols_prefer;
   for (uint32_t i = 0; i < p.n_tolerations; ++i) {
@@ -730,7 +737,10 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t host_start) {
   uint32_t bmax = 0;
   for (uint32_t q = 0; q < nloc; ++q) bmax = std::max(bmax, blocks_per_shard(c->shards[shard0 + q], sub));
   // pods per block: enough (block, pod-group) pairs to fill 256 CUs x 8 waves
-  const uint32_t want = 2048;
+  static const uint32_t want = [] {  // target (block, pod-group) pairs; KS_SWEEP_BLOCKS overrides
+    const char *e = std::getenv("KS_SWEEP_BLOCKS");
+    return e ? (uint32_t)std::max(1, std::atoi(e)) : 8192u;
+  }();
   const uint32_t total_blocks = bmax * nloc;
   uint32_t groups = (want + total_blocks - 1) / total_blocks;
   groups = std::max<uint32_t>(1, std::min(groups, c->P));
@@ -823,7 +833,7 @@ void ks_config_default(ks_config *cfg) {
   cfg->node_capacity = 1024;
   cfg->pods_per_round = 256;
   cfg->topk = 0;
-  cfg->nodes_per_lane = 8;
+  cfg->nodes_per_lane = 4;
   cfg->world_size = 1;
   cfg->rank = 0;
   cfg->virtual_shards = 1;
@@ -845,12 +855,12 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
   c->cfg = *cfg;
   if (cfg->node_capacity == 0) return KS_ERR_INVALID;
   c->cap = cfg->node_capacity;
-  c->npl = cfg->nodes_per_lane ? cfg->nodes_per_lane : 8;
+  c->npl = cfg->nodes_per_lane ? cfg->nodes_per_lane : 4;
   if (c->npl != 2 && c->npl != 4 && c->npl != 8) return KS_ERR_INVALID;
   c->P = cfg->pods_per_round ? cfg->pods_per_round : 256;
   if (c->P > (uint32_t)MAX_P) return KS_ERR_INVALID;
   c->K = cfg->topk ? cfg->topk : c->P;
-  if (c->K > 512) return KS_ERR_INVALID;  // resolve: one listed candidate per thread
+  if (c->K > 256) return KS_ERR_INVALID;  // resolve: one listed candidate per list thread
   const uint32_t world = cfg->world_size ? cfg->world_size : 1;
   c->cfg.world_size = world;
   if (cfg->rank >= world) return KS_ERR_INVALID;

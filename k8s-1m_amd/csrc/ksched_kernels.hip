@@ -78,16 +78,81 @@ __device__ __forceinline__ uint32_t uniform_u32(uint32_t v) {
   return __builtin_amdgcn_readfirstlane(v);
 }
 
+// DPP lane moves (no LDS): quad_perm(1,0,3,2) = 0xB1, quad_perm(2,3,0,1) = 0x4E,
+// row_half_mirror = 0x141, row_mirror = 0x140.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ uint64_t dpp64(uint64_t v) {
+  return ((uint64_t)dpp32<CTRL>((uint32_t)(v >> 32)) << 32) | dpp32<CTRL>((uint32_t)v);
+}
+__device__ __forceinline__ uint64_t max64(uint64_t a, uint64_t b) { return a > b ? a : b; }
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), l) << 32) |
+         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+}
+// max over each 8-lane group (every lane of the group holds it)
+__device__ __forceinline__ uint64_t max8_u64(uint64_t v) {
+  v = max64(v, dpp64<0xB1>(v));
+  v = max64(v, dpp64<0x4E>(v));
+  return max64(v, dpp64<0x141>(v));
+}
+// wave max, wave-uniform result
+__device__ __forceinline__ uint64_t wave_max_u64_dpp(uint64_t v) {
+  v = max8_u64(v);
+  v = max64(v, dpp64<0x140>(v));
+  return max64(max64(readlane64(v, 0), readlane64(v, 16)), max64(readlane64(v, 32), readlane64(v, 48)));
+}
+__device__ __forceinline__ uint32_t min8_u32(uint32_t v) {
+  v = min(v, dpp32<0xB1>(v));
+  v = min(v, dpp32<0x4E>(v));
+  return min(v, dpp32<0x141>(v));
+}
+__device__ __forceinline__ int32_t sum8_i32(int32_t v) {
+  v += (int32_t)dpp32<0xB1>((uint32_t)v);
+  v += (int32_t)dpp32<0x4E>((uint32_t)v);
+  return v + (int32_t)dpp32<0x141>((uint32_t)v);
+}
+__device__ __forceinline__ int32_t wave_sum_i32_dpp(int32_t v) {
+  v = sum8_i32(v);
+  v += (int32_t)dpp32<0x140>((uint32_t)v);
+  return __builtin_amdgcn_readlane(v, 0) + __builtin_amdgcn_readlane(v, 16) + __builtin_amdgcn_readlane(v, 32) +
+         __builtin_amdgcn_readlane(v, 48);
+}
+
 // Node resource state held in registers for the whole pod loop.
+// Every resource quantity is an integer of magnitude < 2^53, so it is held as an
+// exact binary64 and the sums / differences below are exact too: no int64
+// arithmetic or int->float conversion per (pod, node) evaluation.
 struct NodeRegs {
-  int64_t free_cpu, free_mem;   // Allocatable - Requested           (Fit)
-  int64_t rcpu, rmem;           // Requested                         (BalancedAllocation)
-  int64_t lfree_cpu, lfree_mem; // Allocatable - NonZeroRequested    (LeastAllocated)
-  double acpu_d, amem_d;        // Allocatable as binary64
+  double free_cpu, free_mem;    // Allocatable - Requested           (Fit)
+  double rcpu, rmem;            // Requested                         (BalancedAllocation)
+  double lfree_cpu, lfree_mem;  // Allocatable - NonZeroRequested    (LeastAllocated)
+  double acpu_d, amem_d;        // Allocatable
   double inv_cpu, inv_mem;      // RN(1 / Allocatable)
   uint32_t slot;
   uint32_t bits;                // 1 valid, 2 pods fit, 4 cpu alloc != 0, 8 mem alloc != 0
 };
+
+__device__ __forceinline__ NodeRegs make_regs(int64_t acpu, int64_t amem, int64_t rc, int64_t rm, int64_t zc,
+                                              int64_t zm, int32_t apods, int32_t np, uint32_t slot) {
+  NodeRegs r;
+  r.slot = slot;
+  r.free_cpu = (double)(acpu - rc);
+  r.free_mem = (double)(amem - rm);
+  r.rcpu = (double)rc;
+  r.rmem = (double)rm;
+  r.lfree_cpu = (double)(acpu - zc);
+  r.lfree_mem = (double)(amem - zm);
+  r.acpu_d = (double)acpu;
+  r.amem_d = (double)amem;
+  r.inv_cpu = acpu ? 1.0 / r.acpu_d : 1.0;
+  r.inv_mem = amem ? 1.0 / r.amem_d : 1.0;
+  r.bits = 1u | ((int64_t)np + 1 <= (int64_t)apods ? 2u : 0u) | (acpu ? 4u : 0u) | (amem ? 8u : 0u);
+  return r;
+}
 
 struct NodeExt {
   uint64_t hard, prefer;
@@ -106,21 +171,7 @@ __device__ __forceinline__ void load_core(const NodeTable &t, uint32_t pos, uint
     r.inv_cpu = r.inv_mem = 1.0;
     return;
   }
-  const int64_t acpu = t.acpu[pos], amem = t.amem[pos];
-  const int64_t rc = t.rcpu[pos], rm = t.rmem[pos];
-  const int64_t zc = t.zcpu[pos], zm = t.zmem[pos];
-  const int32_t np = t.npods[pos];
-  r.free_cpu = acpu - rc;
-  r.free_mem = amem - rm;
-  r.rcpu = rc;
-  r.rmem = rm;
-  r.lfree_cpu = acpu - zc;
-  r.lfree_mem = amem - zm;
-  r.acpu_d = (double)acpu;
-  r.amem_d = (double)amem;
-  r.inv_cpu = acpu ? 1.0 / r.acpu_d : 1.0;
-  r.inv_mem = amem ? 1.0 / r.amem_d : 1.0;
-  r.bits = 1u | ((int64_t)np + 1 <= (int64_t)ap ? 2u : 0u) | (acpu ? 4u : 0u) | (amem ? 8u : 0u);
+  r = make_regs(t.acpu[pos], t.amem[pos], t.rcpu[pos], t.rmem[pos], t.zcpu[pos], t.zmem[pos], ap, t.npods[pos], slot);
 }
 
 __device__ __forceinline__ void load_ext(const NodeTable &t, uint32_t pos, bool valid, NodeExt &e) {
@@ -226,17 +277,17 @@ __device__ __forceinline__ int filter(const PodDev &p, const uint64_t *clauses, 
   // NodeResourcesFit (fitsRequest): pod count, then cpu / memory vs Requested.
   bool fail = !(r.bits & 2u);
   if (p.flags & PF_HAS_REQ) {
-    fail |= (p.req_cpu > 0) & (p.req_cpu > r.free_cpu);
-    fail |= (p.req_mem > 0) & (p.req_mem > r.free_mem);
+    fail |= (p.req_cpu > 0) & (p.req_cpu_d > r.free_cpu);
+    fail |= (p.req_mem > 0) & (p.req_mem_d > r.free_mem);
   }
   return fail ? 4 : ST_FEASIBLE;
 }
 
 // leastRequestedScore((cap - lfree) + pod_nz, cap) given lfree = cap - NonZeroRequested.
-__device__ __forceinline__ int64_t least_requested(int64_t lfree, int64_t pod_nz, double cap_d, double inv) {
-  const int64_t rem = lfree - pod_nz;  // capacity - requested
-  if (rem < 0) return 0;               // requested > capacity
-  const double x = (double)rem * 100.0;  // exact (< 2^53)
+__device__ __forceinline__ int64_t least_requested(double lfree, double pod_nz, double cap_d, double inv) {
+  const double rem = lfree - pod_nz;  // capacity - requested (exact)
+  if (rem < 0.0) return 0;            // requested > capacity
+  const double x = rem * 100.0;       // exact (< 2^53)
   double q = floor(x * inv);             // within one of the true quotient
   const double r = __builtin_fma(-q, cap_d, x);  // exact remainder x - q*cap
   q += (r >= cap_d) ? 1.0 : 0.0;
@@ -246,20 +297,30 @@ __device__ __forceinline__ int64_t least_requested(int64_t lfree, int64_t pod_nz
 
 __device__ __forceinline__ int64_t score_la(const PodDev &p, const NodeRegs &r) {
   int64_t s = 0, w = 0;
-  if (r.bits & 4u) { s += least_requested(r.lfree_cpu, p.nz_cpu, r.acpu_d, r.inv_cpu); w += 1; }
-  if (r.bits & 8u) { s += least_requested(r.lfree_mem, p.nz_mem, r.amem_d, r.inv_mem); w += 1; }
+  if (r.bits & 4u) { s += least_requested(r.lfree_cpu, p.nz_cpu_d, r.acpu_d, r.inv_cpu); w += 1; }
+  if (r.bits & 8u) { s += least_requested(r.lfree_mem, p.nz_mem_d, r.amem_d, r.inv_mem); w += 1; }
   return w == 2 ? (s >> 1) : s;  // nodeScore / weightSum (w in {0,1,2}, s >= 0)
+}
+
+// RN(a / b) from y = RN(1 / b): q0 = RN(a y) is within one ulp of a/b, the
+// remainder a - b q0 is exact by FMA, and one correction q0 + r y rounds to the
+// IEEE quotient (Markstein).  Checked against true division over the operand
+// domain in tools/markstein_check.cpp and by every parity test.
+__device__ __forceinline__ double div_rn(double a, double b, double y) {
+  const double q0 = a * y;
+  const double r = __builtin_fma(-b, q0, a);
+  return __builtin_fma(r, y, q0);
 }
 
 __device__ __forceinline__ int64_t score_ba(const PodDev &p, const NodeRegs &r) {
   double f0 = 0.0, f1 = 0.0;
   const bool c = r.bits & 4u, m = r.bits & 8u;
   if (c) {
-    f0 = (double)(r.rcpu + p.req_cpu) / r.acpu_d;
+    f0 = div_rn(r.rcpu + p.req_cpu_d, r.acpu_d, r.inv_cpu);  // exact numerator
     if (f0 > 1) f0 = 1;
   }
   if (m) {
-    f1 = (double)(r.rmem + p.req_mem) / r.amem_d;
+    f1 = div_rn(r.rmem + p.req_mem_d, r.amem_d, r.inv_mem);
     if (f1 > 1) f1 = 1;
   }
   double sd = 0.0;
@@ -386,36 +447,49 @@ __global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
       tt_max = a.norm_max[2 * r + 0];
       na_max = a.norm_max[2 * r + 1];
     }
-    uint64_t best = 0, second = 0;
+    // lane top-2 as (TotalScore + 1, step): steps run in slot order, so an
+    // equal score never displaces an earlier step (lowest slot wins ties)
+    uint32_t bs = 0, bj = 0, ss = 0, sj = 0;
     uint32_t feas = 0, f0 = 0, f1 = 0, f2 = 0, f3 = 0, f4 = 0, ttc = 0, nac = 0;
     static_for<NPL>([&](auto J) {
       constexpr int j = J;
       constexpr int je = EXT ? j : 0;
       const bool valid = nr[j].bits & 1u;
       int st = ST_EMPTY;
-      uint64_t key = 0;
+      uint32_t sc = 0;
       bool at_tt = false, at_na = false;
       if (valid) {
         st = filter<EXT>(p, a.clauses, nr[j], ne[je]);
         if (st == ST_FEASIBLE) {
-          key = pack_key(total_score<EXT>(p, a.clauses, nr[j], ne[je], a.w, tt_max, na_max), nr[j].slot);
+          sc = (uint32_t)(total_score<EXT>(p, a.clauses, nr[j], ne[je], a.w, tt_max, na_max) + 1);
           if (EXT && (p.flags & PF_TT)) at_tt = taint_raw(p, ne[je]) == tt_max;
           if (EXT && (p.flags & PF_NA)) at_na = preferred_raw(p, a.clauses, ne[je], nr[j].slot) == na_max;
         }
       }
       // running top-2 as value selects (a branchy form sinks into a scratch store)
-      const bool gt1 = key > best, gt2 = key > second;
-      second = gt1 ? best : (gt2 ? key : second);
-      best = gt1 ? key : best;
-      feas += popc_ballot(st == ST_FEASIBLE);
-      f0 += popc_ballot(st == 0);
-      f1 += popc_ballot(st == 1);
-      f2 += popc_ballot(st == 2);
-      f3 += popc_ballot(st == 3);
-      f4 += popc_ballot(st == 4);
-      ttc += popc_ballot(at_tt);
-      nac += popc_ballot(at_na);
+      const bool gt1 = sc > bs, gt2 = sc > ss;
+      ss = gt1 ? bs : (gt2 ? sc : ss);
+      sj = gt1 ? bj : (gt2 ? (uint32_t)j : sj);
+      bs = gt1 ? sc : bs;
+      bj = gt1 ? (uint32_t)j : bj;
+      const uint64_t fb = __ballot(st == ST_FEASIBLE), vb = __ballot(valid);
+      feas += (uint32_t)__popcll(fb);
+      if (fb != vb) {  // some node failed a filter: per-plugin diagnosis counts
+        f0 += popc_ballot(st == 0);
+        f1 += popc_ballot(st == 1);
+        f2 += popc_ballot(st == 2);
+        f3 += popc_ballot(st == 3);
+        f4 += popc_ballot(st == 4);
+      }
+      if (EXT && (p.flags & (PF_TT | PF_NA))) {
+        ttc += popc_ballot(at_tt);
+        nac += popc_ballot(at_na);
+      }
     });
+    // back to packed keys ((score + 1) << 32 | ~slot)
+    const uint32_t slot0 = s.lo + j0 * WAVE * s.waves + lane * s.waves + lwave, jstride = WAVE * s.waves;
+    const uint64_t best = bs ? ((uint64_t)bs << 32) | (uint64_t)(0xFFFFFFFFu - (slot0 + bj * jstride)) : 0ull;
+    const uint64_t second = ss ? ((uint64_t)ss << 32) | (uint64_t)(0xFFFFFFFFu - (slot0 + sj * jstride)) : 0ull;
     // Wave list: the lane bests above every lane's second best (top 2) + bound.
     uint64_t bound = wave_max_u64(second);
     uint64_t c = best > bound ? best : 0;
@@ -689,24 +763,6 @@ constexpr int RHASH = 1024;
 
 __device__ __forceinline__ uint32_t rhash(uint32_t x) { return (x * 2654435761u) >> 22; }  // 10 bits
 
-__device__ __forceinline__ NodeRegs regs_from(int64_t acpu, int64_t amem, int64_t rc, int64_t rm, int64_t zc,
-                                              int64_t zm, int32_t apods, int32_t np, uint32_t slot) {
-  NodeRegs r;
-  r.slot = slot;
-  r.free_cpu = acpu - rc;
-  r.free_mem = amem - rm;
-  r.rcpu = rc;
-  r.rmem = rm;
-  r.lfree_cpu = acpu - zc;
-  r.lfree_mem = amem - zm;
-  r.acpu_d = (double)acpu;
-  r.amem_d = (double)amem;
-  r.inv_cpu = acpu ? 1.0 / r.acpu_d : 1.0;
-  r.inv_mem = amem ? 1.0 / r.amem_d : 1.0;
-  r.bits = 1u | ((int64_t)np + 1 <= (int64_t)apods ? 2u : 0u) | (acpu ? 4u : 0u) | (amem ? 8u : 0u);
-  return r;
-}
-
 // Workgroup barrier for LDS hand-offs only: __syncthreads() also drains vmcnt,
 // which would expose the next pod's prefetch latency on every iteration.
 __device__ __forceinline__ void lds_barrier() {
@@ -714,7 +770,7 @@ __device__ __forceinline__ void lds_barrier() {
 }
 
 // Diagnostic build (-DKS_STAMPS): wave 0 accumulates s_memtime per phase into
-// a.stamps[0..7]; never compiled into the measured library.
+// a.counters[8..15]; never compiled into the measured library.
 #ifdef KS_STAMPS
 #define STAMP(i)                                                                         \
   do {                                                                                   \
@@ -729,22 +785,28 @@ __device__ __forceinline__ void lds_barrier() {
 #define STAMP(i) do {} while (0)
 #endif
 
+// Roles: waves 0-3 own the listed candidates (thread t = list entry t, K <= 256),
+// waves 4-7 re-score the modified nodes (m = tid - 256), so the two halves of a
+// pod's work run side by side on different SIMDs.
+constexpr int RES_LIST_THREADS = RESOLVE_THREADS / 2;
+
 template <bool EXT>
 __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
   // round inputs
   __shared__ PodDev s_pod[MAX_P];
   __shared__ ShardRecHdr s_hdr[MAX_P];
   __shared__ uint32_t s_norm[MAX_P][2];
-  // modified nodes: S0 row, live requested state, ext columns
+  // modified nodes: S0 row, live requested state, binary64 constants, ext columns
   __shared__ uint32_t s_mslot[MAX_P], s_mpos[MAX_P];
   __shared__ int64_t s_acpu[MAX_P], s_amem[MAX_P];
   __shared__ int64_t s_rc0[MAX_P], s_rm0[MAX_P], s_zc0[MAX_P], s_zm0[MAX_P];
   __shared__ int64_t s_rc[MAX_P], s_rm[MAX_P], s_zc[MAX_P], s_zm[MAX_P];
+  __shared__ double s_dcpu[MAX_P], s_dmem[MAX_P], s_icpu[MAX_P], s_imem[MAX_P];
   __shared__ int32_t s_apods[MAX_P], s_np0[MAX_P], s_np[MAX_P];
   __shared__ uint64_t s_ext[EXT ? MAX_P : 1][2 + LW + NNUM];
   __shared__ uint32_t s_hkey[RHASH];
   __shared__ uint16_t s_hval[RHASH];
-  // per-wave partials
+  // per-wave partials (entries of waves that had no work keep identities)
   __shared__ uint64_t s_wkey[RNW];      // best modified key
   __shared__ uint32_t s_widx[RNW];      // first unmodified list index
   __shared__ uint64_t s_wlk[RNW];       // its key
@@ -758,6 +820,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
   if (start >= a.npods) return;
   const uint32_t nround = min(a.P, a.npods - start);
   const uint32_t RW = rec_words(a.K);
+  const bool list_role = tid < RES_LIST_THREADS;
   // ---- stage the round
   for (uint32_t i = tid; i < nround; i += RESOLVE_THREADS) {
     s_pod[i] = a.pods[start + i];
@@ -766,14 +829,20 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
     s_norm[i][1] = a.norm_max[2 * i + 1];
   }
   for (uint32_t i = tid; i < RHASH; i += RESOLVE_THREADS) s_hkey[i] = 0;
+  if (tid < RNW) {
+    s_wkey[tid] = 0;
+    s_widx[tid] = 0xFFFFFFFFu;
+    s_wlk[tid] = 0;
+    s_wany[tid] = 0;
+  }
   if (tid == 0) { s_nmod = 0; s_stop = nround; }
-  // prefetch pod 0's candidates (thread t holds list entry t, its key and S0 row):
-  // independent loads of the gathered candidate rows, consumed one pod later
+  // prefetch pod 0's candidates (list thread t holds entry t, its key and S0
+  // row): independent loads of the gathered candidate rows, consumed one pod later
   uint64_t ck = 0;
   CandRow crow{};
   CandExt cext{};
   auto prefetch = [&](uint32_t r, uint64_t &k, CandRow &w, CandExt &x) {
-    const bool on = r < nround && tid < a.K;
+    const bool on = r < nround && tid < a.K && list_role;
     const uint32_t rr = on ? r : 0, tt = on ? tid : 0;
     k = a.frec[(size_t)rr * RW + REC_HDR_WORDS + tt];
     w = a.crow[(size_t)rr * a.K + tt];
@@ -789,8 +858,8 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
 
   for (uint32_t r = 0; r < nround; ++r) {
     STAMP(0);
-    const PodDev &p = s_pod[r];
-    const ShardRecHdr &hdr = s_hdr[r];
+    const PodDev p = s_pod[r];
+    const ShardRecHdr hdr = s_hdr[r];
     const uint32_t pi = start + r;
     int64_t tt_max = 0, na_max = 0;
     if (EXT) {
@@ -802,96 +871,117 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
     CandRow nrow;
     CandExt next_ext;
     prefetch(r + 1, nk, nrow, next_ext);
-
-    // (a) re-score modified nodes against the live rows
     const uint32_t nmod = s_nmod;
-    uint64_t mkey = 0;
-    int32_t d[NFILT + 3] = {0, 0, 0, 0, 0, 0, 0, 0};
-    bool dany = false;
-    for (uint32_t m = tid; m < nmod; m += RESOLVE_THREADS) {
-      NodeExt e;
-      if (EXT) {
-        e.hard = s_ext[m][0];
-        e.prefer = s_ext[m][1];
-#pragma unroll
-        for (int q = 0; q < LW; ++q) e.lab[q] = s_ext[m][2 + q];
-#pragma unroll
-        for (int q = 0; q < NNUM; ++q) e.num[q] = (int64_t)s_ext[m][2 + LW + q];
-      }
-      const uint32_t slot = s_mslot[m];
-      const NodeRegs r0 = regs_from(s_acpu[m], s_amem[m], s_rc0[m], s_rm0[m], s_zc0[m], s_zm0[m], s_apods[m],
-                                    s_np0[m], slot);
-      const NodeRegs ri = regs_from(s_acpu[m], s_amem[m], s_rc[m], s_rm[m], s_zc[m], s_zm[m], s_apods[m],
-                                    s_np[m], slot);
-      const int st0 = filter<EXT>(p, a.clauses, r0, e);
-      const int sti = filter<EXT>(p, a.clauses, ri, e);
-      if (sti == ST_FEASIBLE) {
-        const uint64_t k = pack_key(total_score<EXT>(p, a.clauses, ri, e, a.w, tt_max, na_max), slot);
-        mkey = k > mkey ? k : mkey;
-      }
-      if (st0 != sti) {
-        dany = true;
-        d[0] += (st0 == ST_FEASIBLE) - (sti == ST_FEASIBLE);
-#pragma unroll
-        for (int q = 0; q < NFILT; ++q) d[1 + q] += (sti == q) - (st0 == q);
-        if (EXT && st0 == ST_FEASIBLE) {
-          if (p.flags & PF_TT) d[6] += taint_raw(p, e) == tt_max;
-          if (p.flags & PF_NA) d[7] += preferred_raw(p, a.clauses, e, slot) == na_max;
+
+    if (list_role) {
+      // (b) is my listed candidate unmodified by the pods before this one?
+      bool unmod = false;
+      if (ck != 0 && tid < hdr.nkeys) {
+        const uint32_t slot = 0xFFFFFFFFu - (uint32_t)ck;
+        uint32_t h = rhash(slot);
+        unmod = true;
+        while (s_hkey[h] != 0) {
+          if (s_hkey[h] == slot + 1) { unmod = false; break; }
+          h = (h + 1) & (RHASH - 1);
         }
       }
-    }
-    STAMP(1);
-    // (b) is my listed candidate unmodified?
-    bool unmod = false;
-    if (ck != 0 && tid < hdr.nkeys) {
-      const uint32_t slot = 0xFFFFFFFFu - (uint32_t)ck;
-      uint32_t h = rhash(slot);
-      unmod = true;
-      while (s_hkey[h] != 0) {
-        if (s_hkey[h] == slot + 1) { unmod = false; break; }
-        h = (h + 1) & (RHASH - 1);
+      STAMP(1);
+      const uint64_t ub = __ballot(unmod);
+      if (lane == 0) {
+        if (ub) {
+          const uint32_t first = (uint32_t)__builtin_ctzll(ub);
+          s_widx[wid] = wid * WAVE + first;
+          s_wlk[wid] = readlane64(ck, (int)first);
+        } else {
+          s_widx[wid] = 0xFFFFFFFFu;
+        }
       }
-    }
-    STAMP(2);
-    // wave partials
-    const uint64_t ub = __ballot(unmod);
-    const uint64_t wmkey = wave_max_u64(mkey);
-    const bool wdany = __ballot(dany) != 0;
-    if (wdany) {
+    } else {
+      // (a) re-score modified nodes: S0 row vs live row, both from LDS
+      uint64_t mkey = 0;
+      int32_t d[NFILT + 3] = {0, 0, 0, 0, 0, 0, 0, 0};
+      bool dany = false;
+      for (uint32_t m = tid - RES_LIST_THREADS; m < nmod; m += RESOLVE_THREADS - RES_LIST_THREADS) {
+        NodeExt e;
+        if (EXT) {
+          e.hard = s_ext[m][0];
+          e.prefer = s_ext[m][1];
 #pragma unroll
-      for (int q = 0; q < NFILT + 3; ++q) {
-        int32_t v = d[q];
+          for (int q = 0; q < LW; ++q) e.lab[q] = s_ext[m][2 + q];
 #pragma unroll
-        for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, WAVE);
-        d[q] = v;
+          for (int q = 0; q < NNUM; ++q) e.num[q] = (int64_t)s_ext[m][2 + LW + q];
+        }
+        const uint32_t slot = s_mslot[m];
+        const int64_t acpu = s_acpu[m], amem = s_amem[m];
+        const int32_t ap = s_apods[m];
+        NodeRegs ri;
+        ri.slot = slot;
+        ri.rcpu = (double)s_rc[m];
+        ri.rmem = (double)s_rm[m];
+        ri.free_cpu = (double)(acpu - s_rc[m]);
+        ri.free_mem = (double)(amem - s_rm[m]);
+        ri.lfree_cpu = (double)(acpu - s_zc[m]);
+        ri.lfree_mem = (double)(amem - s_zm[m]);
+        ri.acpu_d = s_dcpu[m];
+        ri.amem_d = s_dmem[m];
+        ri.inv_cpu = s_icpu[m];
+        ri.inv_mem = s_imem[m];
+        const uint32_t base = 1u | (acpu ? 4u : 0u) | (amem ? 8u : 0u);
+        ri.bits = base | ((int64_t)s_np[m] + 1 <= (int64_t)ap ? 2u : 0u);
+        NodeRegs r0 = ri;  // S0 row: only its filter status is needed
+        r0.free_cpu = (double)(acpu - s_rc0[m]);
+        r0.free_mem = (double)(amem - s_rm0[m]);
+        r0.bits = base | ((int64_t)s_np0[m] + 1 <= (int64_t)ap ? 2u : 0u);
+        const int st0 = filter<EXT>(p, a.clauses, r0, e);
+        const int sti = filter<EXT>(p, a.clauses, ri, e);
+        if (sti == ST_FEASIBLE) {
+          const uint64_t k = pack_key(total_score<EXT>(p, a.clauses, ri, e, a.w, tt_max, na_max), slot);
+          mkey = k > mkey ? k : mkey;
+        }
+        if (st0 != sti) {
+          dany = true;
+          d[0] += (st0 == ST_FEASIBLE) - (sti == ST_FEASIBLE);
+#pragma unroll
+          for (int q = 0; q < NFILT; ++q) d[1 + q] += (sti == q) - (st0 == q);
+          if (EXT && st0 == ST_FEASIBLE) {
+            if (p.flags & PF_TT) d[6] += taint_raw(p, e) == tt_max;
+            if (p.flags & PF_NA) d[7] += preferred_raw(p, a.clauses, e, slot) == na_max;
+          }
+        }
       }
-    }
-    if (lane == 0) {
-      s_wkey[wid] = wmkey;
-      s_wany[wid] = wdany;
-      if (wdany)
-        for (int q = 0; q < NFILT + 3; ++q) s_wd[wid][q] = d[q];
-    }
-    if (ub) {
-      const uint32_t first = (uint32_t)__builtin_ctzll(ub);
-      const uint64_t fk = __shfl(ck, (int)first, WAVE);
-      if (lane == 0) { s_widx[wid] = wid * WAVE + first; s_wlk[wid] = fk; }
-    } else if (lane == 0) {
-      s_widx[wid] = 0xFFFFFFFFu;
+      STAMP(2);
+      const uint64_t wmkey = wave_max_u64_dpp(mkey);
+      const bool wdany = __ballot(dany) != 0;
+      if (wdany) {
+#pragma unroll
+        for (int q = 0; q < NFILT + 3; ++q) d[q] = wave_sum_i32_dpp(d[q]);
+      }
+      if (lane == 0) {
+        s_wkey[wid] = wmkey;
+        s_wany[wid] = wdany;
+        if (wdany)
+          for (int q = 0; q < NFILT + 3; ++q) s_wd[wid][q] = d[q];
+      }
     }
     STAMP(3);
     lds_barrier();
     STAMP(4);
-    // every thread combines the partials (identical decision, no broadcast barrier)
-    uint64_t bm = 0, ku = 0;
-    uint32_t fu = 0xFFFFFFFFu;
+    // every wave combines the 8 partials in lanes 0-7 (identical decision everywhere)
+    const uint32_t l8 = lane & 7;
+    const uint64_t bm = readlane64(max8_u64(s_wkey[l8]), 0);
+    const uint32_t wi = s_widx[l8];
+    const uint32_t fu = (uint32_t)__builtin_amdgcn_readlane((int)min8_u32(wi), 0);
+    uint64_t ku = 0;
+    if (fu != 0xFFFFFFFFu) {
+      const uint64_t hit = __ballot(lane < 8 && wi == fu);
+      ku = readlane64(s_wlk[l8], (int)__builtin_ctzll(hit));
+    }
     int32_t sum[NFILT + 3] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const bool any = __ballot(lane < 8 && s_wany[l8] != 0) != 0;
+    if (any) {
+      const bool on = s_wany[l8] != 0;
 #pragma unroll
-    for (int w = 0; w < RNW; ++w) {
-      bm = s_wkey[w] > bm ? s_wkey[w] : bm;
-      if (s_widx[w] < fu) { fu = s_widx[w]; ku = s_wlk[w]; }
-      if (s_wany[w])
-        for (int q = 0; q < NFILT + 3; ++q) sum[q] += s_wd[w][q];
+      for (int q = 0; q < NFILT + 3; ++q) sum[q] = __builtin_amdgcn_readlane(sum8_i32(on ? s_wd[l8][q] : 0), 0);
     }
     const uint32_t feasible = hdr.feasible - (uint32_t)sum[0];
     int32_t status = 0;
@@ -915,6 +1005,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
       if (tid == 0) s_stop = r;
       break;  // uniform
     }
+    STAMP(5);
     if (tid == 0) {
       DevResult res;
       res.node_index = win ? (int32_t)(0xFFFFFFFFu - (uint32_t)win) : -1;
@@ -926,13 +1017,12 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
       res.flags = (win && feasible == 1) ? 1u : 0u;
       ((DevResult *)a.results)[pi] = res;
     }
-    STAMP(5);
     // commit (AssumePod -> NodeInfo.AddPod on the live row): exactly one thread
     if (win) {
       if (win == ku && fu != 0xFFFFFFFFu && tid == fu) {
-        // a listed, unmodified node: enters the modified set with its prefetched S0 row
+        // a listed, unmodified node enters the modified set with its prefetched S0 row
         const uint32_t slot = 0xFFFFFFFFu - (uint32_t)ck;
-        const uint32_t m = s_nmod;
+        const uint32_t m = nmod;
         uint32_t h = rhash(slot);
         while (s_hkey[h] != 0) h = (h + 1) & (RHASH - 1);
         s_hkey[h] = slot + 1;
@@ -952,12 +1042,18 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
         s_zc[m] = crow.zc + p.nz_cpu;
         s_zm[m] = crow.zm + p.nz_mem;
         s_np[m] = crow.np + 1;
+        const double dc = (double)crow.acpu, dm = (double)crow.amem;
+        s_dcpu[m] = dc;
+        s_dmem[m] = dm;
+        s_icpu[m] = crow.acpu ? 1.0 / dc : 1.0;
+        s_imem[m] = crow.amem ? 1.0 / dm : 1.0;
         if (EXT)
           for (int q = 0; q < 2 + LW + NNUM; ++q) s_ext[m][q] = cext.w[q];
         s_nmod = m + 1;
-      } else if (win == bm && win != ku) {
-        for (uint32_t m = tid; m < nmod; m += RESOLVE_THREADS) {
-          if (s_mslot[m] == 0xFFFFFFFFu - (uint32_t)win) {
+      } else if (win == bm && win != ku && !list_role) {
+        const uint32_t target = 0xFFFFFFFFu - (uint32_t)win;
+        for (uint32_t m = tid - RES_LIST_THREADS; m < nmod; m += RESOLVE_THREADS - RES_LIST_THREADS) {
+          if (s_mslot[m] == target) {
             s_rc[m] += p.req_cpu;
             s_rm[m] += p.req_mem;
             s_zc[m] += p.nz_cpu;

@@ -113,7 +113,7 @@ class Scheduler:
     """One shard's scheduling core on one GPU (a ks_ctx)."""
 
     def __init__(self, node_capacity: int, *, device: int = 0, pods_per_round: int = 256, topk: int = 0,
-                 nodes_per_lane: int = 8, world_size: int = 1, rank: int = 0, virtual_shards: int = 1,
+                 nodes_per_lane: int = 4, world_size: int = 1, rank: int = 0, virtual_shards: int = 1,
                  weights: Optional[Dict[str, int]] = None):
         self.lib = _abi.ksched_lib()
         cfg = _abi.KsConfig()
