@@ -729,7 +729,8 @@ ks_status collect_timing(ks_ctx *c) {
 
 // One device-driven round (all kernels read the queue head from d_start).
 ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t host_start) {
-  const bool multi = c->cfg.world_size > 1;
+  // RCCL path whenever a communicator exists (also a 1-rank one: exercised by tests)
+  const bool multi = c->comm != nullptr;
   const uint32_t nloc = multi ? 1 : c->S;
   const uint32_t shard0 = multi ? c->cfg.rank : 0;
   const uint32_t knpl = kernel_npl(c, b->ext);
@@ -1162,6 +1163,8 @@ ks_status ks_batch_run(ks_ctx *c, ks_batch *b) {
     return c->fail(KS_ERR_STALE, "batch compiled against taint dictionary v%u, cache is at v%u", b->dict_version,
                    c->dict_version);
   if (c->cfg.world_size > 1 && !c->comm) return c->fail(KS_ERR_COMM, "world_size > 1 but ks_comm_init not called");
+  if (c->comm && c->S != c->cfg.world_size)
+    return c->fail(KS_ERR_INVALID, "RCCL sharding needs one shard per rank (virtual_shards must be 1)");
   HIPC(c, hipSetDevice(c->cfg.device));
   HIPC(c, hipMemsetAsync(c->d_start, 0, 4, c->stream));
   uint32_t host_start = 0;
@@ -1345,7 +1348,7 @@ ks_status ks_get_stats(ks_ctx *c, ks_stats *out) {
   if (st) return st;
   *out = c->stats;
   // (pod, node) evaluations of this rank's sweeps: pods swept x present local nodes
-  const bool multi = c->cfg.world_size > 1;
+  const bool multi = c->comm != nullptr;
   uint64_t local = 0;
   for (uint32_t q = 0; q < c->S; ++q) {
     if (multi && q != c->cfg.rank) continue;

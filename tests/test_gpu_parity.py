@@ -177,3 +177,20 @@ def test_empty_cluster():
     got = res_array(s.schedule_raw(ps.pods, 10), 10)
     assert (got["status"] == 1).all() and (got["evaluated"] == 0).all() and (got["node_index"] == -1).all()
     s.close()
+
+
+def test_rccl_single_rank_path():
+    # the RCCL code path (all-reduce of normalisation maxima, all-gather of shard
+    # records, allreduce_max barrier) with a one-rank communicator
+    n = 1500
+    ns = synth.nodes(synth.LABELED, n, 61)
+    ps = synth.pods(synth.LABELED, 1200, 62)
+    slots = synth.slot_array(n)
+    o = pyoracle.Oracle(n)
+    o.upsert(ns.nodes, slots, n)
+    s = Scheduler(n, world_size=1, rank=0)
+    s.comm_init(Scheduler.comm_unique_id())
+    s.upsert_nodes_raw(ns.nodes, slots, n)
+    assert_results_equal(s.schedule_raw(ps.pods, 1200), o.schedule(ps.pods, 1200), 1200, "rccl 1 rank")
+    assert s.allreduce_max([1.5, -2.0]) == [1.5, -2.0]
+    s.close()
