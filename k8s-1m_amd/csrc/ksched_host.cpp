@@ -566,19 +566,16 @@ ks_status compile_pod(ks_ctx *c, const ks_pod &p, PodDev &d, ClauseBuf &cl) {
   std::vector<Tol> tols, tols_prefer;
   for (uint32_t i = 0; i < p.n_tolerations; ++i) {
     const ks_toleration &t = p.tolerations[i];
-    const int32_t k = c->lookup(t.key), v = c->lookup(t.value);
-    // unseen strings can only match through wildcards: keep them as ids that match nothing
-    Tol x{k < 0 ? 0xFFFFFFFFu : (uint32_t)k, v < 0 ? 0xFFFFFFFFu : (uint32_t)v, t.op, t.effect};
-    if (str(t.key).empty()) x.key = 0;
-    if (str(t.value).empty()) x.value = 0;
+    Tol x{c->intern(t.key), c->intern(t.value), t.op, t.effect};  // "" interns to id 0
     tols.push_back(x);
     if (t.effect == KS_EFFECT_ALL || t.effect == KS_EFFECT_PREFER_NO_SCHEDULE) tols_prefer.push_back(x);
   }
   for (size_t b = 0; b < c->hard_list.size(); ++b)
     if (tolerates(c, tols, c->hard_list[b].key, c->hard_list[b].value, c->hard_list[b].effect))
       d.tol_hard |= 1ull << b;
-  const int32_t uk = c->lookup("node.kubernetes.io/unschedulable");
-  if (tolerates(c, tols, uk < 0 ? 0xFFFFFFFEu : (uint32_t)uk, 0, KS_EFFECT_NO_SCHEDULE)) d.tol_hard |= UNSCHED_BIT;
+  // NodeUnschedulable: Taint{Key: node.kubernetes.io/unschedulable, Effect: NoSchedule}
+  if (tolerates(c, tols, c->intern("node.kubernetes.io/unschedulable"), 0, KS_EFFECT_NO_SCHEDULE))
+    d.tol_hard |= UNSCHED_BIT;
   for (size_t b = 0; b < c->prefer_list.size(); ++b)
     if (tolerates(c, tols_prefer, c->prefer_list[b].first, c->prefer_list[b].second, KS_EFFECT_PREFER_NO_SCHEDULE))
       d.tol_prefer |= 1ull << b;
