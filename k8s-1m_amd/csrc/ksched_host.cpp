@@ -864,6 +864,9 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
   if (cfg->rank >= world) return KS_ERR_INVALID;
   c->S = world > 1 ? world : std::max<uint32_t>(1, cfg->virtual_shards);
   if (c->S > (uint32_t)MAX_SHARDS) return KS_ERR_INVALID;
+  // weights are small non-negative integers (the kernels add them in 32 bits)
+  for (int32_t w : {cfg->weight_fit, cfg->weight_balanced, cfg->weight_taint, cfg->weight_affinity, cfg->weight_image})
+    if (w < 0 || w > 10000) return KS_ERR_INVALID;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return KS_ERR_DEVICE;
   if (cfg->device < 0 || cfg->device >= ndev) return KS_ERR_DEVICE;

@@ -105,6 +105,14 @@ __device__ __forceinline__ uint64_t wave_max_u64_dpp(uint64_t v) {
   v = max64(v, dpp64<0x140>(v));
   return max64(max64(readlane64(v, 0), readlane64(v, 16)), max64(readlane64(v, 32), readlane64(v, 48)));
 }
+__device__ __forceinline__ uint32_t wave_max_u32_dpp(uint32_t v) {
+  v = max(v, dpp32<0xB1>(v));
+  v = max(v, dpp32<0x4E>(v));
+  v = max(v, dpp32<0x141>(v));
+  v = max(v, dpp32<0x140>(v));
+  return max(max((uint32_t)__builtin_amdgcn_readlane((int)v, 0), (uint32_t)__builtin_amdgcn_readlane((int)v, 16)),
+             max((uint32_t)__builtin_amdgcn_readlane((int)v, 32), (uint32_t)__builtin_amdgcn_readlane((int)v, 48)));
+}
 __device__ __forceinline__ uint32_t min8_u32(uint32_t v) {
   v = min(v, dpp32<0xB1>(v));
   v = min(v, dpp32<0x4E>(v));
@@ -284,7 +292,7 @@ __device__ __forceinline__ int filter(const PodDev &p, const uint64_t *clauses, 
 }
 
 // leastRequestedScore((cap - lfree) + pod_nz, cap) given lfree = cap - NonZeroRequested.
-__device__ __forceinline__ int64_t least_requested(double lfree, double pod_nz, double cap_d, double inv) {
+__device__ __forceinline__ int32_t least_requested(double lfree, double pod_nz, double cap_d, double inv) {
   const double rem = lfree - pod_nz;  // capacity - requested (exact)
   if (rem < 0.0) return 0;            // requested > capacity
   const double x = rem * 100.0;       // exact (< 2^53)
@@ -292,11 +300,11 @@ __device__ __forceinline__ int64_t least_requested(double lfree, double pod_nz, 
   const double r = __builtin_fma(-q, cap_d, x);  // exact remainder x - q*cap
   q += (r >= cap_d) ? 1.0 : 0.0;
   q -= (r < 0.0) ? 1.0 : 0.0;
-  return (int64_t)q;
+  return (int32_t)q;  // in [0, 100]
 }
 
-__device__ __forceinline__ int64_t score_la(const PodDev &p, const NodeRegs &r) {
-  int64_t s = 0, w = 0;
+__device__ __forceinline__ int32_t score_la(const PodDev &p, const NodeRegs &r) {
+  int32_t s = 0, w = 0;
   if (r.bits & 4u) { s += least_requested(r.lfree_cpu, p.nz_cpu_d, r.acpu_d, r.inv_cpu); w += 1; }
   if (r.bits & 8u) { s += least_requested(r.lfree_mem, p.nz_mem_d, r.amem_d, r.inv_mem); w += 1; }
   return w == 2 ? (s >> 1) : s;  // nodeScore / weightSum (w in {0,1,2}, s >= 0)
@@ -312,7 +320,7 @@ __device__ __forceinline__ double div_rn(double a, double b, double y) {
   return __builtin_fma(r, y, q0);
 }
 
-__device__ __forceinline__ int64_t score_ba(const PodDev &p, const NodeRegs &r) {
+__device__ __forceinline__ int32_t score_ba(const PodDev &p, const NodeRegs &r) {
   double f0 = 0.0, f1 = 0.0;
   const bool c = r.bits & 4u, m = r.bits & 8u;
   if (c) {
@@ -325,7 +333,7 @@ __device__ __forceinline__ int64_t score_ba(const PodDev &p, const NodeRegs &r) 
   }
   double sd = 0.0;
   if (c && m) sd = fabs((f0 - f1) / 2);
-  return (int64_t)((1 - sd) * 100.0);
+  return (int32_t)((1 - sd) * 100.0);  // in [0, 100]
 }
 
 __device__ __forceinline__ int64_t taint_raw(const PodDev &p, const NodeExt &e) {
@@ -339,18 +347,21 @@ __device__ __forceinline__ int64_t normalize(int64_t raw, int64_t mx, bool rever
   return reverse ? 100 - s : s;
 }
 
+// Plugin scores are in [0, 100] and ks_open caps the weights at 10000, so the
+// weighted sum fits 23 bits: 24-bit multiplies, 32-bit adds.
 template <bool EXT>
-__device__ __forceinline__ int64_t total_score(const PodDev &p, const uint64_t *clauses, const NodeRegs &r,
+__device__ __forceinline__ int32_t total_score(const PodDev &p, const uint64_t *clauses, const NodeRegs &r,
                                                const NodeExt &e, const Weights &w, int64_t tt_max,
                                                int64_t na_max) {
-  int64_t t = (int64_t)w.fit * score_la(p, r) + (int64_t)w.ba * score_ba(p, r);
-  int64_t tt = 100;
-  if (EXT && (p.flags & PF_TT)) tt = normalize(taint_raw(p, e), tt_max, true);
-  t += (int64_t)w.tt * tt;
+  int32_t t = (int32_t)__umul24((uint32_t)w.fit, (uint32_t)score_la(p, r)) +
+              (int32_t)__umul24((uint32_t)w.ba, (uint32_t)score_ba(p, r));
+  int32_t tt = 100;
+  if (EXT && (p.flags & PF_TT)) tt = (int32_t)normalize(taint_raw(p, e), tt_max, true);
+  t += w.tt * tt;  // wave-uniform unless TaintToleration is normalised per node
   if (p.flags & PF_HAS_PREF) {
-    int64_t na = 0;
-    if (EXT && (p.flags & PF_NA)) na = normalize(preferred_raw(p, clauses, e, r.slot), na_max, false);
-    t += (int64_t)w.na * na;
+    int32_t na = 0;
+    if (EXT && (p.flags & PF_NA)) na = (int32_t)normalize(preferred_raw(p, clauses, e, r.slot), na_max, false);
+    t += (int32_t)__umul24((uint32_t)w.na, (uint32_t)na);
   }
   return t;  // + w.il * 0 (ImageLocality: nodes report no images)
 }
@@ -411,8 +422,11 @@ __global__ __launch_bounds__(SWEEP_THREADS) void prescore_kernel(RoundArgs a) {
 
 // =================================================================== sweep
 // grid: x = block within shard, y = pod group, z = local shard.
+constexpr uint32_t KEY32_POS_BITS = 9, KEY32_POS_MASK = (1u << KEY32_POS_BITS) - 1;
+
 template <int NPL, bool EXT>
 __global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
+  static_assert(NPL * WAVE <= (1 << KEY32_POS_BITS), "wave-local key position field");
   constexpr int NW = SWEEP_THREADS / WAVE;
   __shared__ uint64_t s_keys[MAX_PG][NW][3];
   __shared__ uint32_t s_cnt[MAX_PG][NW][NFILT + 3];
@@ -486,20 +500,36 @@ __global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
         nac += popc_ballot(at_na);
       }
     });
-    // back to packed keys ((score + 1) << 32 | ~slot)
-    const uint32_t slot0 = s.lo + j0 * WAVE * s.waves + lane * s.waves + lwave, jstride = WAVE * s.waves;
-    const uint64_t best = bs ? ((uint64_t)bs << 32) | (uint64_t)(0xFFFFFFFFu - (slot0 + bj * jstride)) : 0ull;
-    const uint64_t second = ss ? ((uint64_t)ss << 32) | (uint64_t)(0xFFFFFFFFu - (slot0 + sj * jstride)) : 0ull;
-    // Wave list: the lane bests above every lane's second best (top 2) + bound.
-    uint64_t bound = wave_max_u64(second);
-    uint64_t c = best > bound ? best : 0;
-    const uint64_t k1 = wave_max_u64(c);
-    if (c == k1) c = 0;
-    const uint64_t k2 = wave_max_u64(c);
-    if (c == k2) c = 0;
-    const uint64_t k3 = wave_max_u64(c);
-    bound = k3 > bound ? k3 : bound;
+    // Wave-local 32-bit keys (score + 1) << 9 | ~(step * 64 + lane): within a
+    // wave slot order is (step, lane) order, so these sort like packed keys.
+    const uint32_t best = bs ? (bs << KEY32_POS_BITS) | (KEY32_POS_MASK - (bj * WAVE + lane)) : 0u;
+    const uint32_t second = ss ? (ss << KEY32_POS_BITS) | (KEY32_POS_MASK - (sj * WAVE + lane)) : 0u;
+    // Wave list: the lane bests above every lane's second best (top 2) + bound,
+    // DPP reductions, skipping those the candidate count makes unnecessary.
+    uint32_t bound32 = wave_max_u32_dpp(second);
+    uint32_t c = best > bound32 ? best : 0u;
+    const uint32_t ncand = popc_ballot(c != 0u);
+    uint32_t c1 = 0, c2 = 0;
+    if (ncand) {
+      c1 = wave_max_u32_dpp(c);
+      if (ncand > 1) {
+        if (c == c1) c = 0;
+        c2 = wave_max_u32_dpp(c);
+        if (ncand > 2) {
+          if (c == c2) c = 0;
+          bound32 = max(bound32, wave_max_u32_dpp(c));
+        }
+      }
+    }
     if (lane == 0) {
+      // back to packed keys ((score + 1) << 32 | ~slot)
+      auto widen = [&](uint32_t k) -> uint64_t {
+        if (!k) return 0ull;
+        const uint32_t q = KEY32_POS_MASK - (k & KEY32_POS_MASK);
+        const uint32_t slot = s.lo + (j0 + q / WAVE) * WAVE * s.waves + (q % WAVE) * s.waves + lwave;
+        return ((uint64_t)(k >> KEY32_POS_BITS) << 32) | (uint64_t)(0xFFFFFFFFu - slot);
+      };
+      const uint64_t k1 = widen(c1), k2 = widen(c2), bound = widen(bound32);
       const uint32_t pl = pi - p0;
       s_keys[pl][wid][0] = k1;
       s_keys[pl][wid][1] = k2;
