@@ -47,10 +47,12 @@ def parse():
     ap.add_argument("--nodes-per-lane", type=int, default=4)
     ap.add_argument("--kind", default="hetero", choices=["hetero", "kwok", "labeled"])
     ap.add_argument("--prefill", type=float, default=0.5)
-    ap.add_argument("--cpu-pods", type=int, default=40, help="oracle sample size (pods) for cpu_baseline")
+    ap.add_argument("--cpu-pods", type=int, default=40, help="oracle sample size (pods), single thread")
+    ap.add_argument("--cpu-threads", type=int, default=16, help="oracle threads for cpu_baseline (box CPU share)")
+    ap.add_argument("--cpu-pods-mt", type=int, default=240, help="oracle sample size (pods), multi-thread")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--pmc-file", default=os.environ.get("KS_PMC_FILE", ""),
-                    help="JSON with measured HBM bytes per sweep launch (rocprofv3 --pmc pass)")
+    ap.add_argument("--pmc-file", default=os.environ.get("KS_PMC_FILE", str(ROOT / "profiles" / "pmc_sweep.json")),
+                    help="JSON with measured L2-fabric bytes per sweep launch (tools/pmc.sh + tools/pmc_summary.py)")
     return ap.parse_args()
 
 
@@ -123,9 +125,10 @@ def main():
     sweep_avg_ms = st.sweep_ms / max(1, st.sweep_launches)
     evals_per_launch = st.sweep_evals / max(1, st.sweep_launches)
     achieved = B_NODE * evals_per_launch / (sweep_avg_ms * 1e-3) / 1e9 if st.sweep_launches else None
-    traffic = None
+    traffic, pmc = None, {}
     if args.pmc_file and Path(args.pmc_file).exists():
-        traffic = json.loads(Path(args.pmc_file).read_text()).get("hbm_bytes_per_sweep_launch")
+        pmc = json.loads(Path(args.pmc_file).read_text())
+        traffic = pmc.get("hbm_bytes_per_sweep_launch")
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_pods > 0:
@@ -165,6 +168,10 @@ def main():
             "bytes_per_eval": B_NODE,
             "evals_per_launch": int(evals_per_launch),
             "avg_launch_ms": round(sweep_avg_ms, 4),
+            "traffic_source": (f"profiles/{Path(args.pmc_file).name} ({pmc.get('tag')}): 2 x FETCH_SIZE + WRITE_SIZE "
+                               "per launch at the default config; L2 memory-side bytes (Infinity-Cache hits "
+                               "included)") if traffic else None,
+            "valu_lane_ops_per_eval": pmc.get("valu_lane_ops_per_eval"),
         },
         "cpu_baseline": cpu,
         "extra": {
@@ -217,14 +224,28 @@ def cpu_baseline(args, kind, nodes, slots, pre, pods):
     o.upsert(nodes.nodes, slots, args.nodes)
     if pre is not None:
         o.add_pods(pre.pods, pre.slot_ptr, pre.n_pods)
-    n = args.cpu_pods
+    # single thread: the first cpu_pods pods of the stream
+    n1 = args.cpu_pods
+    t0 = time.perf_counter()
+    o.schedule(pods.pods, n1)
+    dt1 = time.perf_counter() - t0
+    o.close()
+    # threads with parallelize.Until's chunking (oracle.cpp), on a fresh replica
+    nt, n = max(1, args.cpu_threads), args.cpu_pods_mt
+    o = pyoracle.Oracle(args.nodes, threads=nt)
+    o.upsert(nodes.nodes, slots, args.nodes)
+    if pre is not None:
+        o.add_pods(pre.pods, pre.slot_ptr, pre.n_pods)
     t0 = time.perf_counter()
     o.schedule(pods.pods, n)
     dt = time.perf_counter() - t0
     o.close()
-    return {"value": round(n / dt, 2), "unit": "pods/s", "cores": 1, "kind": "port",
+    return {"value": round(n / dt, 2), "unit": "pods/s", "cores": nt, "kind": "port",
             "sample": f"first {n} pods of the stream on the same {args.nodes}-node prefilled cluster "
-                      f"({n * args.nodes:.2e} node evaluations, {dt:.1f} s), single thread"}
+                      f"({n * args.nodes:.2e} node evaluations, {dt:.1f} s), {nt} threads "
+                      "(parallelize.Until chunking)",
+            "single_thread": {"value": round(n1 / dt1, 2), "cores": 1,
+                              "sample": f"first {n1} pods, {dt1:.1f} s"}}
 
 
 if __name__ == "__main__":

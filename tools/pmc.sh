@@ -14,3 +14,4 @@ for ctr in "FETCH_SIZE" "WRITE_SIZE" "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_
   if [ $rc -ne 0 ]; then tail -5 "gpurun_out/pmc_${TAG}_p$i.err"; exit $rc; fi
 done
 find gpurun_out/pmc_$TAG -name '*counter_collection*' | head
+python3 tools/pmc_summary.py gpurun_out/pmc_$TAG --tag $TAG --out gpurun_out/pmc_$TAG/pmc_sweep.json
