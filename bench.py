@@ -112,6 +112,8 @@ def main():
     if world > 1:
         elapsed = sched.allreduce_max([elapsed])[0]
     st = sched.stats()
+    dbg = (C.c_uint64 * 16)()
+    sched.lib.ks_debug_counters(sched.ctx, dbg)
 
     # scheduled fraction of the timed pods (sanity for the reader)
     scheduled = 0
@@ -181,6 +183,7 @@ def main():
             "sweep_ms_total": round(st.sweep_ms, 3),
             "resolve_ms_total": round(st.resolve_ms, 3),
             "scheduled_fraction": round(scheduled / pods_timed, 4),
+            "speculated_rounds_wasted": int(dbg[3]),  # since open (warmup included)
             "node_evals_per_s": round(value * args.nodes, 1),
             "setup_s": round(setup_s, 2),
         },

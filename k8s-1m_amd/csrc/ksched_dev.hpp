@@ -136,6 +136,20 @@ struct alignas(16) CandExt {
 static_assert(sizeof(CandExt) == 64, "CandExt layout");
 
 // Normalising-plugin maxima over feasible nodes: (max raw, #feasible at max).
+// A node modified by round k's resolve, handed to round k+1's resolve (its
+// sweep ran concurrently with round k and saw the table before round k) and to
+// the write-back that lands round k in the table before sweep k+2.
+struct alignas(16) CarryRec {
+  int64_t acpu, amem;
+  int64_t rc0, rm0;          // Requested as sweep k+1 saw it (start of round k)
+  int64_t rc, rm, zc, zm;    // live state after round k
+  uint32_t slot, pos;
+  int32_t apods, np0, np;
+  uint32_t _pad;
+  uint64_t ext[2 + LW + NNUM];  // hard, prefer, label words, numeric labels (EXT batches)
+};
+static_assert(sizeof(CarryRec) == 160, "CarryRec layout");
+
 struct alignas(16) NormRec {
   int64_t tt_max, na_max;
   uint32_t tt_cnt, na_cnt;

@@ -154,7 +154,9 @@ struct ks_batch {
 struct ks_ctx {
   ks_config cfg{};
   std::string err;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;   // table updates, prescore / sweep / merge / gather, RCCL
+  hipStream_t rstream = nullptr;  // resolve (overlaps the next round's sweep)
+  hipEvent_t ev_sw[2] = {nullptr, nullptr}, ev_res[2] = {nullptr, nullptr};  // by round parity
   // geometry
   uint32_t cap = 0, S = 1, npl = 8, P = 256, K = 256;
   std::vector<Shard> shards;
@@ -173,6 +175,9 @@ struct ks_ctx {
   uint64_t *d_counters = nullptr;
   CandRow *d_crow = nullptr;
   CandExt *d_cext = nullptr;
+  // pipeline state: [0,1] sweep start, [2,3] actual start, [4,5] carry counts (by parity)
+  uint32_t *d_pipe = nullptr;
+  CarryRec *d_carry = nullptr;  // [2][MAX_P]
   // host mirror / dictionaries
   std::vector<HostNode> nodes;
   uint32_t n_present = 0;
@@ -725,7 +730,12 @@ ks_status collect_timing(ks_ctx *c) {
 }
 
 // One device-driven round (all kernels read the queue head from d_start).
-ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t host_start) {
+// Round k of a pipeline run (k = 0 starts it: the table holds every previous
+// round).  Stream order, with sweep k+1 overlapping resolve k:
+//   stream : [wait resolve k-2, write-back k-2] advance k, prescore k, sweep k,
+//            merge k, (RCCL), merge_shards k, gather k, record ev_sw[k]
+//   rstream: wait ev_sw[k], resolve k, record ev_res[k]
+ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k) {
   // RCCL path whenever a communicator exists (also a 1-rank one: exercised by tests)
   const bool multi = c->comm != nullptr;
   const uint32_t nloc = multi ? 1 : c->S;
@@ -762,15 +772,27 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t host_start) {
   a.evaluated = c->n_present;
   a.pods = b->d_pods;
   a.clauses = b->d_clauses;
+  const uint32_t q = k & 1u, pq = q ^ 1u;
+  const size_t RW = rec_words(c->K);
   a.d_start = c->d_start;
-  a.norm_max = c->d_norm;
+  a.sstart = c->d_pipe + q;
+  a.prev_sstart = c->d_pipe + pq;
+  a.act = c->d_pipe + 2 + q;
+  a.act_next = c->d_pipe + 2 + pq;
+  a.prev_act = c->d_pipe + 2 + pq;
+  a.carry_in = c->d_carry + (size_t)pq * MAX_P;
+  a.carry_in_n = c->d_pipe + 4 + pq;
+  a.carry_out = c->d_carry + (size_t)q * MAX_P;
+  a.carry_out_n = c->d_pipe + 4 + q;
+  a.first = k == 0;
+  a.norm_max = c->d_norm + (size_t)q * 2 * c->P;
   a.brec = c->d_brec;
-  a.srec = c->d_srec;
-  a.frec = c->S == 1 ? c->d_srec : c->d_frec;
+  a.srec = c->d_srec + (size_t)q * c->S * c->P * RW;
+  a.frec = c->S == 1 ? a.srec : c->d_frec + (size_t)q * c->P * RW;
   a.results = b->d_results;
   a.counters = c->d_counters;
-  a.crow = c->d_crow;
-  a.cext = c->d_cext;
+  a.crow = c->d_crow + (size_t)q * c->P * c->K;
+  a.cext = c->d_cext + (size_t)q * c->P * c->K;
   a.slot_pos = c->d_slot_pos;
   a.w = Weights{c->cfg.weight_fit, c->cfg.weight_balanced, c->cfg.weight_taint, c->cfg.weight_affinity,
                 c->cfg.weight_image};
@@ -782,10 +804,15 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t host_start) {
   // The kernels address positions as base + wave*64*knpl + j*64 + lane, which
   // equals the layout position when the layout's npl-step block of a wave is
   // split into `sub` consecutive kernel waves; slots follow from the layout.
+  if (k >= 2) {  // round k-2 lands in the table before sweep k (sweep k-1 has finished reading it)
+    HIPC(c, hipStreamWaitEvent(c->stream, c->ev_res[q], 0));
+    HIPC(c, launch_writeback(c->t, c->d_carry + (size_t)q * MAX_P, c->d_pipe + 4 + q, c->stream));
+  }
+  HIPC(c, launch_advance(a, c->stream));
   if (b->norm) {
-    HIPC(c, hipMemsetAsync(c->d_norm, 0, (size_t)2 * c->P * 4, c->stream));
+    HIPC(c, hipMemsetAsync(a.norm_max, 0, (size_t)2 * c->P * 4, c->stream));
     HIPC(c, launch_prescore(a, bmax, groups, nloc, c->stream));
-    if (multi) NCCLC(c, ncclAllReduce(c->d_norm, c->d_norm, 2 * c->P, ncclUint32, ncclMax, c->comm, c->stream));
+    if (multi) NCCLC(c, ncclAllReduce(a.norm_max, a.norm_max, 2 * c->P, ncclUint32, ncclMax, c->comm, c->stream));
   }
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (c->timing) {
@@ -800,22 +827,37 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t host_start) {
   }
   HIPC(c, launch_merge(a, nloc, c->stream));
   if (multi) {
-    const size_t words = (size_t)c->P * rec_words(c->K);
-    NCCLC(c, ncclAllGather(c->d_srec + (size_t)c->cfg.rank * words, c->d_srec, words * 8, ncclUint8, c->comm,
-                           c->stream));
+    const size_t words = (size_t)c->P * RW;
+    NCCLC(c, ncclAllGather(a.srec + (size_t)c->cfg.rank * words, a.srec, words * 8, ncclUint8, c->comm, c->stream));
   }
   if (c->S > 1) HIPC(c, launch_merge_shards(a, c->stream));
   HIPC(c, launch_gather_cand(a, b->ext, c->stream));
+  HIPC(c, hipEventRecord(c->ev_sw[q], c->stream));
+  HIPC(c, hipStreamWaitEvent(c->rstream, c->ev_sw[q], 0));
   if (c->timing) {
     e0 = get_event(c);
     e1 = get_event(c);
-    HIPC(c, hipEventRecord(e0, c->stream));
+    HIPC(c, hipEventRecord(e0, c->rstream));
   }
-  HIPC(c, launch_resolve(a, b->ext, c->stream));
+  HIPC(c, launch_resolve(a, b->ext, c->rstream));
   if (c->timing) {
-    HIPC(c, hipEventRecord(e1, c->stream));
+    HIPC(c, hipEventRecord(e1, c->rstream));
     c->ev_resolve.emplace_back(e0, e1);
   }
+  HIPC(c, hipEventRecord(c->ev_res[q], c->rstream));
+  return KS_OK;
+}
+
+// End of a pipeline run of `rounds` rounds: land the last two rounds in the
+// table and wait for everything.
+ks_status drain_rounds(ks_ctx *c, uint32_t rounds) {
+  for (uint32_t k = rounds >= 2 ? rounds - 2 : 0; k < rounds; ++k) {
+    const uint32_t q = k & 1u;
+    HIPC(c, hipStreamWaitEvent(c->stream, c->ev_res[q], 0));
+    HIPC(c, launch_writeback(c->t, c->d_carry + (size_t)q * MAX_P, c->d_pipe + 4 + q, c->stream));
+  }
+  HIPC(c, hipMemcpyAsync(c->h_start, c->d_start, 4, hipMemcpyDeviceToHost, c->stream));
+  HIPC(c, hipStreamSynchronize(c->stream));
   return KS_OK;
 }
 
@@ -872,7 +914,31 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
   if (cfg->device < 0 || cfg->device >= ndev) return KS_ERR_DEVICE;
   if (hipSetDevice(cfg->device) != hipSuccess) return KS_ERR_DEVICE;
   ks_ctx *x = c.get();
-  HIPC(x, hipStreamCreateWithFlags(&x->stream, hipStreamNonBlocking));
+  {
+    // Resolve runs on a high-priority stream.  KS_RESOLVE_CUS=n instead
+    // reserves n CUs for it (masking the main stream off them); measured 5 %
+    // slower at 1M nodes (the sweep loses a CU), so it is off by default.
+    const char *e = std::getenv("KS_RESOLVE_CUS");
+    const int nres = e ? std::max(0, std::atoi(e)) : 0;
+    hipDeviceProp_t prop{};
+    HIPC(x, hipGetDeviceProperties(&prop, cfg->device));
+    const int ncu = prop.multiProcessorCount;
+    if (nres > 0 && nres < ncu) {
+      std::vector<uint32_t> main_mask((ncu + 31) / 32, 0u), res_mask((ncu + 31) / 32, 0u);
+      for (int i = 0; i < ncu; ++i) (i >= ncu - nres ? res_mask : main_mask)[i / 32] |= 1u << (i % 32);
+      HIPC(x, hipExtStreamCreateWithCUMask(&x->stream, (uint32_t)main_mask.size(), main_mask.data()));
+      HIPC(x, hipExtStreamCreateWithCUMask(&x->rstream, (uint32_t)res_mask.size(), res_mask.data()));
+    } else {
+      int lo = 0, hi = 0;
+      HIPC(x, hipStreamCreateWithFlags(&x->stream, hipStreamNonBlocking));
+      HIPC(x, hipDeviceGetStreamPriorityRange(&lo, &hi));
+      HIPC(x, hipStreamCreateWithPriority(&x->rstream, hipStreamNonBlocking, hi));
+    }
+    for (int q = 0; q < 2; ++q) {
+      HIPC(x, hipEventCreateWithFlags(&x->ev_sw[q], hipEventDisableTiming));
+      HIPC(x, hipEventCreateWithFlags(&x->ev_res[q], hipEventDisableTiming));
+    }
+  }
   // shard geometry: contiguous slot ranges; waves rounded to a multiple of 4
   uint32_t base = 0;
   for (uint32_t s = 0; s < x->S; ++s) {
@@ -907,7 +973,8 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
     return st;
   HIPC(x, hipMemsetAsync(t.apods, 0xFF, (size_t)x->npos * 4, x->stream));  // every position empty
   if ((st = dalloc(x, &x->d_shards, x->S)) || (st = dalloc(x, &x->d_slot_pos, x->cap)) ||
-      (st = dalloc(x, &x->d_start, 1)) || (st = dalloc(x, &x->d_norm, 2 * (size_t)x->P)) ||
+      (st = dalloc(x, &x->d_start, 1)) || (st = dalloc(x, &x->d_norm, 2 * 2 * (size_t)x->P)) ||
+      (st = dalloc(x, &x->d_pipe, 8)) || (st = dalloc(x, &x->d_carry, 2 * (size_t)MAX_P)) ||
       (st = dalloc(x, &x->d_counters, 16)))
     return st;
   if ((st = xfer_begin(x, x->S * sizeof(Shard) + (size_t)x->cap * 4 + 1024, 0)) ||
@@ -921,9 +988,9 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
   const uint32_t nloc = world > 1 ? 1 : x->S;
   x->brec_bytes = (size_t)nloc * x->P * bmax * sizeof(BlockRec);
   if ((st = dalloc(x, (uint8_t **)&x->d_brec, x->brec_bytes))) return st;
-  const size_t recs = (size_t)x->S * x->P * rec_words(x->K);
-  if ((st = dalloc(x, &x->d_srec, recs)) || (st = dalloc(x, &x->d_frec, (size_t)x->P * rec_words(x->K))) ||
-      (st = dalloc(x, &x->d_crow, (size_t)x->P * x->K)) || (st = dalloc(x, &x->d_cext, (size_t)x->P * x->K)))
+  const size_t recs = (size_t)x->S * x->P * rec_words(x->K);  // per round parity
+  if ((st = dalloc(x, &x->d_srec, 2 * recs)) || (st = dalloc(x, &x->d_frec, 2 * (size_t)x->P * rec_words(x->K))) ||
+      (st = dalloc(x, &x->d_crow, 2 * (size_t)x->P * x->K)) || (st = dalloc(x, &x->d_cext, 2 * (size_t)x->P * x->K)))
     return st;
   if ((st = xfer_sync(x))) return st;  // all initialisation is stream-ordered
   *out = c.release();
@@ -934,11 +1001,12 @@ void ks_close(ks_ctx *c) {
   if (!c) return;
   (void)hipSetDevice(c->cfg.device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->rstream) (void)hipStreamSynchronize(c->rstream);
   if (c->comm) ncclCommDestroy(c->comm);
   void *bufs[] = {c->t.acpu, c->t.amem, c->t.rcpu, c->t.rmem, c->t.zcpu, c->t.zmem, c->t.apods,
                   c->t.npods, c->t.hard, c->t.prefer, c->t.lab, c->t.num, c->d_shards, c->d_slot_pos,
                   c->d_start, c->d_norm, c->d_brec, c->d_srec, c->d_frec, c->d_counters, c->d_crow,
-                  c->d_cext};
+                  c->d_cext, c->d_pipe, c->d_carry};
   for (void *b : bufs)
     if (b) (void)hipFree(b);
   if (c->h_start) (void)hipHostFree(c->h_start);
@@ -947,6 +1015,11 @@ void ks_close(ks_ctx *c) {
   for (auto &pr : c->ev_sweep) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
   for (auto &pr : c->ev_resolve) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
   for (auto e : c->ev_pool) (void)hipEventDestroy(e);
+  for (int q = 0; q < 2; ++q) {
+    if (c->ev_sw[q]) (void)hipEventDestroy(c->ev_sw[q]);
+    if (c->ev_res[q]) (void)hipEventDestroy(c->ev_res[q]);
+  }
+  if (c->rstream) (void)hipStreamDestroy(c->rstream);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -1169,16 +1242,17 @@ ks_status ks_batch_run(ks_ctx *c, ks_batch *b) {
   HIPC(c, hipMemsetAsync(c->d_start, 0, 4, c->stream));
   uint32_t host_start = 0;
   while (host_start < b->n) {
-    // every round resolves at least one pod; assume full windows and check
+    // Assume full rounds (an early stop costs the speculated round after it)
+    // and check; each pipeline run resolves at least one pod.
     const uint32_t remaining = b->n - host_start;
     uint32_t rounds = (remaining + c->P - 1) / c->P;
     rounds = std::min<uint32_t>(rounds, 64);
     for (uint32_t r = 0; r < rounds; ++r) {
-      ks_status st = enqueue_round(c, b, host_start + r * c->P);
+      ks_status st = enqueue_round(c, b, r);
       if (st) return st;
     }
-    HIPC(c, hipMemcpyAsync(c->h_start, c->d_start, 4, hipMemcpyDeviceToHost, c->stream));
-    HIPC(c, hipStreamSynchronize(c->stream));
+    ks_status st = drain_rounds(c, rounds);
+    if (st) return st;
     if (*c->h_start <= host_start) return c->fail(KS_ERR_DEVICE, "no progress in scheduling rounds");
     host_start = *c->h_start;
   }

@@ -379,7 +379,7 @@ __device__ __forceinline__ PodDev load_pod(const PodDev *pods, uint32_t i) {
 // Per pod with PF_TT / PF_NA: max raw score over feasible nodes -> atomicMax.
 template <int NPL>
 __global__ __launch_bounds__(SWEEP_THREADS) void prescore_kernel(RoundArgs a) {
-  const uint32_t start = uniform_u32(*a.d_start);
+  const uint32_t start = uniform_u32(*a.sstart);
   const uint32_t sh = blockIdx.z;
   const Shard s = a.shards[a.shard0 + sh];
   const uint32_t kw = blockIdx.x * (SWEEP_THREADS / WAVE) + threadIdx.x / WAVE;  // kernel wave
@@ -431,7 +431,7 @@ __global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
   __shared__ uint64_t s_keys[MAX_PG][NW][3];
   __shared__ uint32_t s_cnt[MAX_PG][NW][NFILT + 3];
 
-  const uint32_t start = uniform_u32(*a.d_start);
+  const uint32_t start = uniform_u32(*a.sstart);
   const uint32_t sh = blockIdx.z;
   const Shard s = a.shards[a.shard0 + sh];
   const uint32_t wid = threadIdx.x / WAVE;
@@ -675,7 +675,7 @@ __global__ __launch_bounds__(256) void merge_kernel(RoundArgs a) {
   __shared__ uint64_t s_scr[16];
   __shared__ uint32_t s_u32[16];
   __shared__ uint32_t s_cnt;
-  const uint32_t start = uniform_u32(*a.d_start);
+  const uint32_t start = uniform_u32(*a.sstart);
   const uint32_t r = blockIdx.x;
   if (start + r >= a.npods || r >= a.P) return;
   const uint32_t sh = blockIdx.y;
@@ -710,7 +710,7 @@ __global__ __launch_bounds__(256) void merge_shards_kernel(RoundArgs a) {
   __shared__ uint64_t s_scr[16];
   __shared__ uint32_t s_u32[16];
   __shared__ uint32_t s_cnt;
-  const uint32_t start = uniform_u32(*a.d_start);
+  const uint32_t start = uniform_u32(*a.sstart);
   const uint32_t r = blockIdx.x;
   if (start + r >= a.npods || r >= a.P) return;
   const uint32_t W = rec_words(a.K);
@@ -740,7 +740,7 @@ __global__ __launch_bounds__(256) void merge_shards_kernel(RoundArgs a) {
 // copy the node's S0 row (and label / taint columns) next to the key.
 template <bool EXT>
 __global__ __launch_bounds__(256) void gather_cand_kernel(RoundArgs a) {
-  const uint32_t start = uniform_u32(*a.d_start);
+  const uint32_t start = uniform_u32(*a.sstart);
   const uint32_t r = blockIdx.x;
   if (start + r >= a.npods || r >= a.P) return;
   const uint64_t *rec = a.frec + (size_t)r * rec_words(a.K);
@@ -826,14 +826,19 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
   __shared__ PodDev s_pod[MAX_P];
   __shared__ ShardRecHdr s_hdr[MAX_P];
   __shared__ uint32_t s_norm[MAX_P][2];
-  // modified nodes: S0 row, live requested state, binary64 constants, ext columns
-  __shared__ uint32_t s_mslot[MAX_P], s_mpos[MAX_P];
-  __shared__ int64_t s_acpu[MAX_P], s_amem[MAX_P];
-  __shared__ int64_t s_rc0[MAX_P], s_rm0[MAX_P], s_zc0[MAX_P], s_zm0[MAX_P];
-  __shared__ int64_t s_rc[MAX_P], s_rm[MAX_P], s_zc[MAX_P], s_zm[MAX_P];
-  __shared__ double s_dcpu[MAX_P], s_dmem[MAX_P], s_icpu[MAX_P], s_imem[MAX_P];
-  __shared__ int32_t s_apods[MAX_P], s_np0[MAX_P], s_np[MAX_P];
-  __shared__ uint64_t s_ext[EXT ? MAX_P : 1][2 + LW + NNUM];
+  // modified nodes (carried from the previous round first, then this round's):
+  // the row the sweep saw (S0: only its filter inputs), the live state,
+  // binary64 constants, ext columns; carried entries also keep their state at
+  // the start of this round (the row the next round's sweep sees)
+  __shared__ uint32_t s_mslot[MAX_MOD], s_mpos[MAX_MOD];
+  __shared__ int64_t s_acpu[MAX_MOD], s_amem[MAX_MOD];
+  __shared__ int64_t s_rc0[MAX_MOD], s_rm0[MAX_MOD];
+  __shared__ int64_t s_rc[MAX_MOD], s_rm[MAX_MOD], s_zc[MAX_MOD], s_zm[MAX_MOD];
+  __shared__ double s_dcpu[MAX_MOD], s_dmem[MAX_MOD], s_icpu[MAX_MOD], s_imem[MAX_MOD];
+  __shared__ int32_t s_apods[MAX_MOD], s_np0[MAX_MOD], s_np[MAX_MOD];
+  __shared__ int64_t s_rcm[MAX_P], s_rmm[MAX_P];
+  __shared__ int32_t s_npm[MAX_P];
+  __shared__ uint64_t s_ext[EXT ? MAX_MOD : 1][2 + LW + NNUM];
   __shared__ uint32_t s_hkey[RHASH];
   __shared__ uint16_t s_hval[RHASH];
   // per-wave partials (entries of waves that had no work keep identities)
@@ -844,28 +849,68 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
   __shared__ uint32_t s_wany[RNW];
   __shared__ uint32_t s_nmod;
   __shared__ uint32_t s_stop;
+  __shared__ uint32_t s_cout;
 
   const uint32_t tid = threadIdx.x, lane = tid % WAVE, wid = tid / WAVE;
-  const uint32_t start = uniform_u32(*a.d_start);
-  if (start >= a.npods) return;
+  const uint32_t start = uniform_u32(*a.act);
+  // The lists were swept for the pods from *sstart (speculatively); if the
+  // previous round stopped early they belong to other pods: resolve nothing.
+  if (start >= a.npods || uniform_u32(*a.sstart) != start) {
+    if (tid == 0) {
+      *a.act_next = start;
+      *a.d_start = start;
+      *a.carry_out_n = 0;
+      if (start < a.npods) a.counters[3] += 1;  // wasted (speculated) round
+    }
+    return;
+  }
   const uint32_t nround = min(a.P, a.npods - start);
+  const uint32_t nseed = a.first ? 0u : uniform_u32(*a.carry_in_n);
   const uint32_t RW = rec_words(a.K);
   const bool list_role = tid < RES_LIST_THREADS;
   // ---- stage the round
+  for (uint32_t i = tid; i < RHASH; i += RESOLVE_THREADS) s_hkey[i] = 0;
+  __syncthreads();
+  // carried nodes: modified by the previous round, which this round's sweep did not see
+  for (uint32_t m = tid; m < nseed; m += RESOLVE_THREADS) {
+    const CarryRec &c = a.carry_in[m];
+    s_mslot[m] = c.slot;
+    s_mpos[m] = c.pos;
+    s_acpu[m] = c.acpu;
+    s_amem[m] = c.amem;
+    s_rc0[m] = c.rc0;
+    s_rm0[m] = c.rm0;
+    s_np0[m] = c.np0;
+    s_rc[m] = s_rcm[m] = c.rc;
+    s_rm[m] = s_rmm[m] = c.rm;
+    s_zc[m] = c.zc;
+    s_zm[m] = c.zm;
+    s_np[m] = s_npm[m] = c.np;
+    s_apods[m] = c.apods;
+    const double dc = (double)c.acpu, dm = (double)c.amem;
+    s_dcpu[m] = dc;
+    s_dmem[m] = dm;
+    s_icpu[m] = c.acpu ? 1.0 / dc : 1.0;
+    s_imem[m] = c.amem ? 1.0 / dm : 1.0;
+    if (EXT)
+      for (int q = 0; q < 2 + LW + NNUM; ++q) s_ext[m][q] = c.ext[q];
+    uint32_t h = rhash(c.slot);
+    while (atomicCAS(&s_hkey[h], 0u, c.slot + 1) != 0u) h = (h + 1) & (RHASH - 1);
+    s_hval[h] = (uint16_t)m;
+  }
   for (uint32_t i = tid; i < nround; i += RESOLVE_THREADS) {
     s_pod[i] = a.pods[start + i];
     s_hdr[i] = *(const ShardRecHdr *)(a.frec + (size_t)i * RW);
     s_norm[i][0] = a.norm_max[2 * i];
     s_norm[i][1] = a.norm_max[2 * i + 1];
   }
-  for (uint32_t i = tid; i < RHASH; i += RESOLVE_THREADS) s_hkey[i] = 0;
   if (tid < RNW) {
     s_wkey[tid] = 0;
     s_widx[tid] = 0xFFFFFFFFu;
     s_wlk[tid] = 0;
     s_wany[tid] = 0;
   }
-  if (tid == 0) { s_nmod = 0; s_stop = nround; }
+  if (tid == 0) { s_nmod = nseed; s_stop = nround; s_cout = 0; }
   // prefetch pod 0's candidates (list thread t holds entry t, its key and S0
   // row): independent loads of the gathered candidate rows, consumed one pod later
   uint64_t ck = 0;
@@ -1063,8 +1108,6 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
         s_amem[m] = crow.amem;
         s_rc0[m] = crow.rc;
         s_rm0[m] = crow.rm;
-        s_zc0[m] = crow.zc;
-        s_zm0[m] = crow.zm;
         s_apods[m] = crow.apods;
         s_np0[m] = crow.np;
         s_rc[m] = crow.rc + p.req_cpu;
@@ -1101,25 +1144,75 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
     if (EXT) cext = next_ext;
   }
   __syncthreads();
-  // write back live rows of modified nodes and advance the queue
+  // hand the nodes this round modified to the next round and the write-back
+  // (every commit adds a pod, so "modified this round" is a pod-count change)
   const uint32_t nmod = s_nmod;
   for (uint32_t i = tid; i < nmod; i += RESOLVE_THREADS) {
-    const uint32_t pos = s_mpos[i];
-    a.t.rcpu[pos] = s_rc[i];
-    a.t.rmem[pos] = s_rm[i];
-    a.t.zcpu[pos] = s_zc[i];
-    a.t.zmem[pos] = s_zm[i];
-    a.t.npods[pos] = s_np[i];
+    const bool carried = i < nseed;
+    const int32_t npm = carried ? s_npm[i] : s_np0[i];
+    if (s_np[i] == npm) continue;
+    const uint32_t o = atomicAdd(&s_cout, 1u);
+    CarryRec c;
+    c.acpu = s_acpu[i];
+    c.amem = s_amem[i];
+    c.rc0 = carried ? s_rcm[i] : s_rc0[i];
+    c.rm0 = carried ? s_rmm[i] : s_rm0[i];
+    c.np0 = npm;
+    c.rc = s_rc[i];
+    c.rm = s_rm[i];
+    c.zc = s_zc[i];
+    c.zm = s_zm[i];
+    c.np = s_np[i];
+    c.slot = s_mslot[i];
+    c.pos = s_mpos[i];
+    c.apods = s_apods[i];
+    c._pad = 0;
+    for (int q = 0; q < 2 + LW + NNUM; ++q) c.ext[q] = EXT ? s_ext[i][q] : 0ull;
+    a.carry_out[o] = c;
   }
+  __syncthreads();
 #ifdef KS_STAMPS
   if (tid == 0)
     for (int i = 0; i < 8; ++i) atomicAdd((unsigned long long *)&a.counters[8 + i], (unsigned long long)stamp_acc[i]);
 #endif
   if (tid == 0) {
+    *a.carry_out_n = s_cout;
+    *a.act_next = start + s_stop;
     *a.d_start = start + s_stop;
     a.counters[0] += 1;                                   // rounds
     a.counters[1] += s_stop;                              // pods resolved
-    a.counters[2] += nround;                              // pods swept
+  }
+}
+
+// ============================================================ pipeline
+// Speculative start of round k's sweep, issued once round k-2 is resolved
+// (round k-1 may still be resolving): if round k-1's lists were swept for the
+// right pods, assume it resolves all of them; otherwise round k-1 resolves
+// nothing and round k restarts at its actual start.
+__global__ void advance_kernel(RoundArgs a) {
+  uint32_t s;
+  if (a.first) {
+    s = *a.d_start;
+    *a.act = s;
+  } else {
+    const uint32_t ps = *a.prev_sstart, pa = *a.prev_act;
+    s = ps == pa ? ps + a.P : pa;
+  }
+  *a.sstart = s;
+  if (s < a.npods) a.counters[2] += min(a.P, a.npods - s);  // pods swept
+}
+
+// Land a resolved round's modified rows in the table (before the sweep that
+// must see them; never while a sweep that must not see them runs).
+__global__ void writeback_kernel(NodeTable t, const CarryRec *carry, const uint32_t *n) {
+  const uint32_t cnt = *n;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += gridDim.x * blockDim.x) {
+    const CarryRec &c = carry[i];
+    t.rcpu[c.pos] = c.rc;
+    t.rmem[c.pos] = c.rm;
+    t.zcpu[c.pos] = c.zc;
+    t.zmem[c.pos] = c.zm;
+    t.npods[c.pos] = c.np;
   }
 }
 
@@ -1281,6 +1374,16 @@ hipError_t launch_merge_shards(const RoundArgs &a, hipStream_t st) {
 hipError_t launch_gather_cand(const RoundArgs &a, bool ext, hipStream_t st) {
   if (ext) gather_cand_kernel<true><<<a.P, 256, 0, st>>>(a);
   else gather_cand_kernel<false><<<a.P, 256, 0, st>>>(a);
+  return hipGetLastError();
+}
+
+hipError_t launch_advance(const RoundArgs &a, hipStream_t st) {
+  advance_kernel<<<1, 1, 0, st>>>(a);
+  return hipGetLastError();
+}
+
+hipError_t launch_writeback(const NodeTable &t, const CarryRec *carry, const uint32_t *n, hipStream_t st) {
+  writeback_kernel<<<2, 256, 0, st>>>(t, carry, n);
   return hipGetLastError();
 }
 

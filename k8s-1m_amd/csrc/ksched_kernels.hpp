@@ -9,6 +9,7 @@ namespace ks {
 
 constexpr int MAX_PG = 64;    // pods per sweep block (LDS wave records)
 constexpr int MAX_P = 256;    // pods per round (resolve stages the round in LDS)
+constexpr int MAX_MOD = 2 * MAX_P;  // modified nodes a resolve tracks (carried + its own)
 
 struct RoundArgs {
   NodeTable t;
@@ -26,7 +27,18 @@ struct RoundArgs {
   uint32_t lnpl;              // layout nodes per lane (positions of committed slots)
   const PodDev *pods;
   const uint64_t *clauses;
-  uint32_t *d_start;          // next unresolved pod of the batch (device-driven rounds)
+  uint32_t *d_start;          // next unresolved pod of the batch (latest, for the host)
+  // Two-stage pipeline (sweep k+1 overlaps resolve k), slots indexed by round parity:
+  uint32_t *sstart;           // this round's sweep start (speculative)
+  const uint32_t *prev_sstart;  // previous round's sweep start
+  uint32_t *act;              // this round's actual start (written by the previous resolve)
+  uint32_t *act_next;         // next round's actual start (written by this resolve)
+  const uint32_t *prev_act;   // previous round's actual start
+  const CarryRec *carry_in;   // nodes the previous round's resolve modified
+  const uint32_t *carry_in_n;
+  CarryRec *carry_out;        // nodes this round's resolve modifies
+  uint32_t *carry_out_n;
+  uint32_t first;             // first round of a pipeline run (no previous round)
   uint32_t *norm_max;         // [P][2] max raw TaintToleration / NodeAffinity (atomicMax, all shards)
   BlockRec *brec;             // [local shards][P][bstride]
   uint64_t *srec;             // [S][P][rec_words(K)]
@@ -35,7 +47,7 @@ struct RoundArgs {
   CandRow *crow;              // [P][K] S0 rows of the final candidates
   CandExt *cext;              // [P][K] their label / taint columns (EXT batches)
   const uint32_t *slot_pos;   // slot -> position
-  uint64_t *counters;         // [0] rounds, [1] pods resolved
+  uint64_t *counters;         // [0] rounds, [1] pods resolved, [2] pods swept, [3] wasted rounds
   Weights w;
 };
 
@@ -58,6 +70,8 @@ hipError_t launch_merge(const RoundArgs &a, uint32_t nshards, hipStream_t st);
 hipError_t launch_merge_shards(const RoundArgs &a, hipStream_t st);
 hipError_t launch_gather_cand(const RoundArgs &a, bool ext, hipStream_t st);
 hipError_t launch_resolve(const RoundArgs &a, bool ext, hipStream_t st);
+hipError_t launch_advance(const RoundArgs &a, hipStream_t st);
+hipError_t launch_writeback(const NodeTable &t, const CarryRec *carry, const uint32_t *n, hipStream_t st);
 hipError_t launch_scatter_rows(const NodeTable &t, const uint32_t *pos, const int64_t *core, const uint64_t *ext,
                                uint32_t n, uint32_t flags, hipStream_t st);
 hipError_t launch_apply_deltas(const NodeTable &t, const uint32_t *pos, const int64_t *delta, uint32_t n,
