@@ -23,7 +23,8 @@ b = s.prepare(ps.pods, npods)
 s.run(b)
 k = (C.c_uint64 * 16)()
 assert s.lib.ks_debug_counters(s.ctx, k) == 0
-names = ["top->modified", "modified eval", "list check", "wave partials", "barrier1", "decide", "commit", "barrier2"]
+# wave 0 is a list-role wave: stamp 2 (rescoring, waves 4-7) stays 0 for it
+names = ["loop top", "pod+prefetch+list", "(rescore)", "wave partials", "barrier1 wait", "decide", "commit", "barrier2 wait"]
 tot = sum(k[8:16])
 pods = k[1]
 print(f"lib={os.environ.get('KSCHED_LIB_DIR', 'default')} rounds={k[0]} pods={pods}")
