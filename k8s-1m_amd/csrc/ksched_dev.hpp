@@ -68,7 +68,8 @@ enum PodFlags : uint32_t {
 struct alignas(16) PodDev {
   int64_t req_cpu, req_mem;  // PodRequests (Fit filter, BalancedAllocation)
   int64_t nz_cpu, nz_mem;    // PodRequests with non-missing defaults (LeastAllocated)
-  double req_cpu_d, req_mem_d, nz_cpu_d, nz_mem_d;  // the same, exact in binary64 (< 2^46)
+  double req_cpu_d, req_mem_d;  // the same, exact in binary64 (< 2^46)
+  double nz100_cpu, nz100_mem;  // non-zero requests x 100, exact (< 2^53)
   uint64_t tol_hard;         // hard-taint bits tolerated (+ UNSCHED_BIT)
   uint64_t tol_prefer;       // prefer-taint bits tolerated by "" / PreferNoSchedule tolerations
   uint32_t flags;

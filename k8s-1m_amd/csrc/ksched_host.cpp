@@ -22,6 +22,7 @@
 #include <memory>
 #include <string>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "ksched.h"
@@ -34,7 +35,8 @@ namespace {
 
 constexpr int64_t kDefaultMilliCPURequest = 100;             // schedutil.DefaultMilliCPURequest
 constexpr int64_t kDefaultMemoryRequest = 200ll * 1024 * 1024;  // schedutil.DefaultMemoryRequest
-constexpr int64_t kMaxExact = 1ll << 46;  // alloc bound for exact binary64 LeastAllocated
+constexpr int64_t kMaxExact = 1ll << 46;  // pod request bound: exact binary64 sums
+constexpr int64_t kMaxAlloc = 1ll << 44;  // node allocatable bound: exact truncated LeastAllocated
 
 std::string str(const char *p) { return p ? std::string(p) : std::string(); }
 
@@ -565,8 +567,8 @@ ks_status compile_pod(ks_ctx *c, const ks_pod &p, PodDev &d, ClauseBuf &cl) {
     return c->fail(KS_ERR_RANGE, "pod %s requests outside [0, 2^46)", str(p.name).c_str());
   d.req_cpu_d = (double)d.req_cpu;
   d.req_mem_d = (double)d.req_mem;
-  d.nz_cpu_d = (double)d.nz_cpu;
-  d.nz_mem_d = (double)d.nz_mem;
+  d.nz100_cpu = (double)d.nz_cpu * 100.0;
+  d.nz100_mem = (double)d.nz_mem * 100.0;
   // tolerations -> dictionary masks
   std::vector<Tol> tols, tols_prefer;
   for (uint32_t i = 0; i < p.n_tolerations; ++i) {
@@ -1034,13 +1036,34 @@ ks_status ks_nodes_upsert(ks_ctx *c, const ks_node *nodes, const uint32_t *slots
   std::vector<uint64_t> ext;
   std::unordered_map<uint32_t, uint32_t> row_of;  // slot -> row in the upload
   bool grew = false;
+  // Validate the whole call first so that a rejected call changes nothing.
+  {
+    std::unordered_set<uint32_t> in_call(slots, slots + n);
+    std::unordered_map<std::string, uint32_t> call_names;
+    for (uint32_t i = 0; i < n; ++i) {
+      const ks_node &s = nodes[i];
+      const uint32_t slot = slots[i];
+      if (slot >= c->cap) return c->fail(KS_ERR_NOT_FOUND, "slot %u >= capacity %u", slot, c->cap);
+      if (s.alloc_milli_cpu < 0 || s.alloc_milli_cpu >= kMaxAlloc || s.alloc_memory < 0 ||
+          s.alloc_memory >= kMaxAlloc || s.alloc_pods < 0 || s.alloc_pods > INT32_MAX - 1)
+        return c->fail(KS_ERR_RANGE, "node %s allocatable outside the exact range", str(s.name).c_str());
+      // node names are unique (metadata.name matchFields resolve a name to one slot)
+      const std::string nm = str(s.name);
+      auto ci = call_names.emplace(nm, slot);
+      if (!ci.second && ci.first->second != slot)
+        return c->fail(KS_ERR_INVALID, "node name %s given to slots %u and %u", nm.c_str(), ci.first->second, slot);
+      const int64_t nid = c->lookup(s.name);
+      if (nid >= 0) {
+        auto it = c->name_slot.find((uint32_t)nid);
+        if (it != c->name_slot.end() && it->second != slot && c->nodes[it->second].present &&
+            !in_call.count(it->second))
+          return c->fail(KS_ERR_INVALID, "node name %s already names slot %u", nm.c_str(), it->second);
+      }
+    }
+  }
   for (uint32_t i = 0; i < n; ++i) {
     const ks_node &s = nodes[i];
     const uint32_t slot = slots[i];
-    if (slot >= c->cap) return c->fail(KS_ERR_NOT_FOUND, "slot %u >= capacity %u", slot, c->cap);
-    if (s.alloc_milli_cpu < 0 || s.alloc_milli_cpu >= kMaxExact || s.alloc_memory < 0 ||
-        s.alloc_memory >= kMaxExact || s.alloc_pods < 0 || s.alloc_pods > INT32_MAX - 1)
-      return c->fail(KS_ERR_RANGE, "node %s allocatable outside the exact range", str(s.name).c_str());
     HostNode &h = c->nodes[slot];
     const bool is_new = !h.present;
     if (!is_new) c->name_slot.erase(h.name);  // key_nodes entries are re-validated lazily

@@ -133,33 +133,48 @@ __device__ __forceinline__ int32_t wave_sum_i32_dpp(int32_t v) {
 // Node resource state held in registers for the whole pod loop.
 // Every resource quantity is an integer of magnitude < 2^53, so it is held as an
 // exact binary64 and the sums / differences below are exact too: no int64
-// arithmetic or int->float conversion per (pod, node) evaluation.
+// arithmetic or int->float conversion per (pod, node) evaluation.  A resource
+// with zero allocatable gets inv = 0, which makes both scores' terms for it
+// vanish; lashift / bamul then give upstream's weight-sum and fraction-count
+// rules without a per-evaluation branch.
 struct NodeRegs {
-  double free_cpu, free_mem;    // Allocatable - Requested           (Fit)
-  double rcpu, rmem;            // Requested                         (BalancedAllocation)
-  double lfree_cpu, lfree_mem;  // Allocatable - NonZeroRequested    (LeastAllocated)
+  double free_cpu, free_mem;    // Allocatable - Requested                 (Fit)
+  double rcpu, rmem;            // Requested                               (BalancedAllocation)
+  double lf100_cpu, lf100_mem;  // (Allocatable - NonZeroRequested) * 100  (LeastAllocated)
   double acpu_d, amem_d;        // Allocatable
-  double inv_cpu, inv_mem;      // RN(1 / Allocatable)
+  double inv_cpu, inv_mem;      // RN(1 / Allocatable), 0 when Allocatable == 0
+  double bamul;                 // 0.5 with two non-zero allocatables, else 0 (std = 0)
   uint32_t slot;
   uint32_t bits;                // 1 valid, 2 pods fit, 4 cpu alloc != 0, 8 mem alloc != 0
+  uint32_t lashift;             // 1 with two non-zero allocatables (score / weightSum 2), else 0
 };
 
-__device__ __forceinline__ NodeRegs make_regs(int64_t acpu, int64_t amem, int64_t rc, int64_t rm, int64_t zc,
-                                              int64_t zm, int32_t apods, int32_t np, uint32_t slot) {
+__device__ __forceinline__ NodeRegs make_regs_inv(int64_t acpu, int64_t amem, int64_t rc, int64_t rm, int64_t zc,
+                                                  int64_t zm, int32_t apods, int32_t np, uint32_t slot,
+                                                  double inv_cpu, double inv_mem) {
   NodeRegs r;
   r.slot = slot;
   r.free_cpu = (double)(acpu - rc);
   r.free_mem = (double)(amem - rm);
   r.rcpu = (double)rc;
   r.rmem = (double)rm;
-  r.lfree_cpu = (double)(acpu - zc);
-  r.lfree_mem = (double)(amem - zm);
+  r.lf100_cpu = (double)(acpu - zc) * 100.0;  // exact for a non-negative value (< 2^51)
+  r.lf100_mem = (double)(amem - zm) * 100.0;
   r.acpu_d = (double)acpu;
   r.amem_d = (double)amem;
-  r.inv_cpu = acpu ? 1.0 / r.acpu_d : 1.0;
-  r.inv_mem = amem ? 1.0 / r.amem_d : 1.0;
+  r.inv_cpu = acpu ? inv_cpu : 0.0;
+  r.inv_mem = amem ? inv_mem : 0.0;
+  const bool both = acpu && amem;
+  r.bamul = both ? 0.5 : 0.0;
+  r.lashift = both ? 1u : 0u;
   r.bits = 1u | ((int64_t)np + 1 <= (int64_t)apods ? 2u : 0u) | (acpu ? 4u : 0u) | (amem ? 8u : 0u);
   return r;
+}
+
+__device__ __forceinline__ NodeRegs make_regs(int64_t acpu, int64_t amem, int64_t rc, int64_t rm, int64_t zc,
+                                              int64_t zm, int32_t apods, int32_t np, uint32_t slot) {
+  return make_regs_inv(acpu, amem, rc, rm, zc, zm, apods, np, slot, acpu ? 1.0 / (double)acpu : 0.0,
+                       amem ? 1.0 / (double)amem : 0.0);
 }
 
 struct NodeExt {
@@ -170,13 +185,15 @@ struct NodeExt {
 
 __device__ __forceinline__ void load_core(const NodeTable &t, uint32_t pos, uint32_t slot, bool in_range,
                                           NodeRegs &r) {
-  r.slot = slot;
-  r.bits = 0;
   int32_t ap = in_range ? t.apods[pos] : -1;
-  if (ap < 0) {
-    r.free_cpu = r.free_mem = r.rcpu = r.rmem = r.lfree_cpu = r.lfree_mem = 0;
+  if (ap < 0) {  // empty slot: benign finite values, never feasible
+    r.free_cpu = r.free_mem = r.rcpu = r.rmem = r.lf100_cpu = r.lf100_mem = 0;
     r.acpu_d = r.amem_d = 1.0;
-    r.inv_cpu = r.inv_mem = 1.0;
+    r.inv_cpu = r.inv_mem = 0.0;
+    r.bamul = 0.0;
+    r.lashift = 0;
+    r.slot = slot;
+    r.bits = 0;
     return;
   }
   r = make_regs(t.acpu[pos], t.amem[pos], t.rcpu[pos], t.rmem[pos], t.zcpu[pos], t.zmem[pos], ap, t.npods[pos], slot);
@@ -291,23 +308,24 @@ __device__ __forceinline__ int filter(const PodDev &p, const uint64_t *clauses, 
   return fail ? 4 : ST_FEASIBLE;
 }
 
-// leastRequestedScore((cap - lfree) + pod_nz, cap) given lfree = cap - NonZeroRequested.
-__device__ __forceinline__ int32_t least_requested(double lfree, double pod_nz, double cap_d, double inv) {
-  const double rem = lfree - pod_nz;  // capacity - requested (exact)
-  if (rem < 0.0) return 0;            // requested > capacity
-  const double x = rem * 100.0;       // exact (< 2^53)
-  double q = floor(x * inv);             // within one of the true quotient
-  const double r = __builtin_fma(-q, cap_d, x);  // exact remainder x - q*cap
-  q += (r >= cap_d) ? 1.0 : 0.0;
-  q -= (r < 0.0) ? 1.0 : 0.0;
-  return (int32_t)q;  // in [0, 100]
+// leastRequestedScore(requested, capacity) = (capacity - requested) * 100 / capacity
+// (int64 truncation; 0 when requested > capacity) from x = max(lf100 - nz100, 0)
+// = max(capacity - requested, 0) * 100, exact.  With y = RN(1 / capacity),
+// fma(x, y, 2^-45) lies within 1.9e-14 of x / capacity + 2^-45 and the exact
+// quotient's fractional part is 0 or in [1/capacity, 1 - 1/capacity]; for
+// capacity < 2^44 (ks_nodes_upsert enforces it) 2^-45 is above the error and
+// 1/capacity above both, so truncation gives the exact floor: no remainder
+// correction.  Proof in DESIGN.md §4; checked by tools/markstein_check.cpp.
+constexpr double LA_EPS = 0x1p-45;
+__device__ __forceinline__ int32_t least_requested(double lf100, double pod_nz100, double inv) {
+  const double x = fmax(lf100 - pod_nz100, 0.0);
+  return (int32_t)__builtin_fma(x, inv, LA_EPS);  // x >= 0: truncation == floor; inv == 0 -> 0
 }
 
 __device__ __forceinline__ int32_t score_la(const PodDev &p, const NodeRegs &r) {
-  int32_t s = 0, w = 0;
-  if (r.bits & 4u) { s += least_requested(r.lfree_cpu, p.nz_cpu_d, r.acpu_d, r.inv_cpu); w += 1; }
-  if (r.bits & 8u) { s += least_requested(r.lfree_mem, p.nz_mem_d, r.amem_d, r.inv_mem); w += 1; }
-  return w == 2 ? (s >> 1) : s;  // nodeScore / weightSum (w in {0,1,2}, s >= 0)
+  // nodeScore / weightSum: a zero-allocatable resource adds 0 and is not counted
+  return (least_requested(r.lf100_cpu, p.nz100_cpu, r.inv_cpu) + least_requested(r.lf100_mem, p.nz100_mem, r.inv_mem)) >>
+         r.lashift;
 }
 
 // RN(a / b) from y = RN(1 / b): q0 = RN(a y) is within one ulp of a/b, the
@@ -321,19 +339,12 @@ __device__ __forceinline__ double div_rn(double a, double b, double y) {
 }
 
 __device__ __forceinline__ int32_t score_ba(const PodDev &p, const NodeRegs &r) {
-  double f0 = 0.0, f1 = 0.0;
-  const bool c = r.bits & 4u, m = r.bits & 8u;
-  if (c) {
-    f0 = div_rn(r.rcpu + p.req_cpu_d, r.acpu_d, r.inv_cpu);  // exact numerator
-    if (f0 > 1) f0 = 1;
-  }
-  if (m) {
-    f1 = div_rn(r.rmem + p.req_mem_d, r.amem_d, r.inv_mem);
-    if (f1 > 1) f1 = 1;
-  }
-  double sd = 0.0;
-  if (c && m) sd = fabs((f0 - f1) / 2);
-  return (int32_t)((1 - sd) * 100.0);  // in [0, 100]
+  // fraction = min(1, requested / allocatable) as an IEEE binary64 quotient
+  // (exact numerator); std = |(f0 - f1) / 2| with two fractions, else 0
+  const double f0 = fmin(div_rn(r.rcpu + p.req_cpu_d, r.acpu_d, r.inv_cpu), 1.0);
+  const double f1 = fmin(div_rn(r.rmem + p.req_mem_d, r.amem_d, r.inv_mem), 1.0);
+  const double sd = fabs((f0 - f1) * r.bamul);
+  return (int32_t)((1.0 - sd) * 100.0);  // in [0, 100]
 }
 
 __device__ __forceinline__ int64_t taint_raw(const PodDev &p, const NodeExt &e) {
@@ -469,17 +480,15 @@ __global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
       constexpr int j = J;
       constexpr int je = EXT ? j : 0;
       const bool valid = nr[j].bits & 1u;
-      int st = ST_EMPTY;
-      uint32_t sc = 0;
+      // branch-free: every lane scores its node (empty slots hold benign
+      // values) and the feasibility mask selects
+      const int st = valid ? filter<EXT>(p, a.clauses, nr[j], ne[je]) : ST_EMPTY;
+      const bool feasible = st == ST_FEASIBLE;
+      const uint32_t tot = (uint32_t)total_score<EXT>(p, a.clauses, nr[j], ne[je], a.w, tt_max, na_max) + 1u;
+      const uint32_t sc = feasible ? tot : 0u;
       bool at_tt = false, at_na = false;
-      if (valid) {
-        st = filter<EXT>(p, a.clauses, nr[j], ne[je]);
-        if (st == ST_FEASIBLE) {
-          sc = (uint32_t)(total_score<EXT>(p, a.clauses, nr[j], ne[je], a.w, tt_max, na_max) + 1);
-          if (EXT && (p.flags & PF_TT)) at_tt = taint_raw(p, ne[je]) == tt_max;
-          if (EXT && (p.flags & PF_NA)) at_na = preferred_raw(p, a.clauses, ne[je], nr[j].slot) == na_max;
-        }
-      }
+      if (EXT && (p.flags & PF_TT)) at_tt = feasible && taint_raw(p, ne[je]) == tt_max;
+      if (EXT && (p.flags & PF_NA)) at_na = feasible && preferred_raw(p, a.clauses, ne[je], nr[j].slot) == na_max;
       // running top-2 as value selects (a branchy form sinks into a scratch store)
       const bool gt1 = sc > bs, gt2 = sc > ss;
       ss = gt1 ? bs : (gt2 ? sc : ss);
@@ -989,24 +998,12 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
         const uint32_t slot = s_mslot[m];
         const int64_t acpu = s_acpu[m], amem = s_amem[m];
         const int32_t ap = s_apods[m];
-        NodeRegs ri;
-        ri.slot = slot;
-        ri.rcpu = (double)s_rc[m];
-        ri.rmem = (double)s_rm[m];
-        ri.free_cpu = (double)(acpu - s_rc[m]);
-        ri.free_mem = (double)(amem - s_rm[m]);
-        ri.lfree_cpu = (double)(acpu - s_zc[m]);
-        ri.lfree_mem = (double)(amem - s_zm[m]);
-        ri.acpu_d = s_dcpu[m];
-        ri.amem_d = s_dmem[m];
-        ri.inv_cpu = s_icpu[m];
-        ri.inv_mem = s_imem[m];
-        const uint32_t base = 1u | (acpu ? 4u : 0u) | (amem ? 8u : 0u);
-        ri.bits = base | ((int64_t)s_np[m] + 1 <= (int64_t)ap ? 2u : 0u);
+        NodeRegs ri = make_regs_inv(acpu, amem, s_rc[m], s_rm[m], s_zc[m], s_zm[m], ap, s_np[m], slot, s_icpu[m],
+                                    s_imem[m]);
         NodeRegs r0 = ri;  // S0 row: only its filter status is needed
         r0.free_cpu = (double)(acpu - s_rc0[m]);
         r0.free_mem = (double)(amem - s_rm0[m]);
-        r0.bits = base | ((int64_t)s_np0[m] + 1 <= (int64_t)ap ? 2u : 0u);
+        r0.bits = (ri.bits & ~2u) | ((int64_t)s_np0[m] + 1 <= (int64_t)ap ? 2u : 0u);
         const int st0 = filter<EXT>(p, a.clauses, r0, e);
         const int sti = filter<EXT>(p, a.clauses, ri, e);
         if (sti == ST_FEASIBLE) {

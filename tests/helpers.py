@@ -31,3 +31,16 @@ def scores_array(scores):
     return np.array([(s.status, s.least_allocated, s.balanced_allocation, s.taint_raw, s.taint_score,
                       s.affinity_raw, s.affinity_score, s.image_locality, s.total_score) for s in scores],
                     dtype=np.int64)
+
+
+STATE_DT = np.dtype([("alloc_cpu", "<i8"), ("alloc_mem", "<i8"), ("req_cpu", "<i8"), ("req_mem", "<i8"),
+                     ("nz_cpu", "<i8"), ("nz_mem", "<i8"), ("alloc_pods", "<i4"), ("pod_count", "<i4")])
+
+
+def states_np(fn, ctx, n):
+    """All n slots' ks_node_state via ks_node_states / oracle_node_states(ctx, slots, n, out), as numpy."""
+    slots = np.arange(n, dtype=np.uint32)
+    out = (_abi.KsNodeState * max(1, n))()
+    st = fn(ctx, slots.ctypes.data_as(C.POINTER(C.c_uint32)), n, out)
+    assert st == 0, f"node_states failed ({st})"
+    return np.frombuffer(C.string_at(C.addressof(out), n * C.sizeof(_abi.KsNodeState)), dtype=STATE_DT).copy()

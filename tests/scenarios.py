@@ -180,6 +180,22 @@ def ties_lowest_slot():
     return nodes, pods, exp
 
 
+@scenario
+def extreme_allocatable():
+    # capacities at the exact-arithmetic limit (allocatable < 2^44), tiny and zero
+    # capacities (a zero-allocatable resource is skipped by both scorers), and
+    # requests that make (cap - req) * 100 / cap an exact integer
+    big = (1 << 44) - 1
+    nodes = [node("max", cpu=big, mem=big, pods=110), node("tiny", cpu=1, mem=1, pods=110),
+             node("nocpu", cpu=0, mem=64 * Gi, pods=110), node("nomem", cpu=32000, mem=0, pods=110),
+             node("none", cpu=0, mem=0, pods=110), node("odd", cpu=99991, mem=3 * Gi + 7, pods=110)]
+    pods = [pod("be"), pod("zero", cpu=0, mem=0), pod("exact", cpu=320, mem=Gi),
+            pod("half-max", cpu=big // 2, mem=big // 2 + 1), pod("p1", cpu=1, mem=1),
+            pod("p3", cpu=99991 // 100, mem=(3 * Gi + 7) // 100), pod("cpu-only", cpu=1600)]
+    pods += [pod(f"f{i}", cpu=37 * i + 1, mem=(i + 1) * 64 * 1024 * 1024) for i in range(24)]
+    return nodes, pods, []
+
+
 def check(results, exp):
     """results: structured numpy array (tests.helpers.RES_DT)."""
     for i, e in enumerate(exp):

@@ -48,3 +48,34 @@ def test_scenario_plugin_scores(name):
             out = (_abi.KsNodeScore * n)()
             assert s.lib.ks_plugin_scores(s.ctx, p, out) == 0
             assert np.array_equal(scores_array(out), scores_array(o.plugin_scores(p))), (name, j)
+
+
+def test_allocatable_range_enforced():
+    # the exact truncated LeastAllocated needs allocatable < 2^44
+    from scenarios import node
+
+    a = Arena()
+    for cpu, mem, ok in [((1 << 44) - 1, (1 << 44) - 1, True), (1 << 44, 1, False), (1, 1 << 44, False)]:
+        na, n = nodes_array([node("x", cpu=cpu, mem=mem)], a)
+        with Scheduler(1) as s:
+            st = s.lib.ks_nodes_upsert(s.ctx, na, (C.c_uint32 * 1)(0), 1)
+            assert (st == 0) == ok, (cpu, mem, st)
+            if not ok:
+                assert st == _abi.KS_ERR_RANGE if hasattr(_abi, "KS_ERR_RANGE") else st == 5
+
+
+def test_upsert_rejects_duplicate_names_atomically():
+    # metadata.name is unique; a rejected call leaves the cache unchanged
+    from scenarios import node
+
+    a = Arena()
+    na, n = nodes_array([node("a"), node("b")], a)
+    with Scheduler(4) as s:
+        assert s.lib.ks_nodes_upsert(s.ctx, na, (C.c_uint32 * 2)(0, 1), 2) == 0
+        dup, _ = nodes_array([node("c", cpu=1000), node("a", cpu=1000)], a)
+        assert s.lib.ks_nodes_upsert(s.ctx, dup, (C.c_uint32 * 2)(2, 3), 2) == 1  # KS_ERR_INVALID
+        st = s.node_states([0, 1, 2, 3])
+        assert [x.pod_count for x in st] == [0, 0, -1, -1]
+        same, _ = nodes_array([node("a", cpu=1000)], a)  # an update keeps the name on its slot
+        assert s.lib.ks_nodes_upsert(s.ctx, same, (C.c_uint32 * 1)(0), 1) == 0
+        assert s.node_states([0])[0].alloc_milli_cpu == 1000
