@@ -127,19 +127,19 @@ __host__ __device__ inline uint32_t rec_words(uint32_t k) { return REC_HDR_WORDS
 // the resolve's per-pod prefetch is one independent load per thread.
 struct alignas(16) CandRow {
   int64_t acpu, amem, rc, rm, zc, zm;
+  double inv_cpu, inv_mem;  // RN(1 / allocatable), 0 for a zero allocatable (off the resolve's critical path)
   int32_t apods, np;
   uint32_t pos, _pad;
 };
-static_assert(sizeof(CandRow) == 64, "CandRow layout");
+static_assert(sizeof(CandRow) == 80, "CandRow layout");
 struct alignas(16) CandExt {
   uint64_t w[2 + LW + NNUM];  // hard, prefer, lab[LW], num[NNUM]
 };
 static_assert(sizeof(CandExt) == 64, "CandExt layout");
 
-// Normalising-plugin maxima over feasible nodes: (max raw, #feasible at max).
-// A node modified by round k's resolve, handed to round k+1's resolve (its
-// sweep ran concurrently with round k and saw the table before round k) and to
-// the write-back that lands round k in the table before sweep k+2.
+// A node modified by round k's resolve, handed to round k+1's patch (its sweep
+// ran concurrently with round k and saw the table before round k) and to the
+// write-back that lands round k in the table before sweep k+2.
 struct alignas(16) CarryRec {
   int64_t acpu, amem;
   int64_t rc0, rm0;          // Requested as sweep k+1 saw it (start of round k)

@@ -834,6 +834,13 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k) {
   }
   if (c->S > 1) HIPC(c, launch_merge_shards(a, c->stream));
   HIPC(c, launch_gather_cand(a, b->ext, c->stream));
+  if (k > 0) {
+    // merge round k-1's commits into the lists: once resolve k-1 is done, on the
+    // main stream (the sweeps of rounds k and k+1 are not running then, so the
+    // patch has the whole GPU), before the write-back of round k-1
+    HIPC(c, hipStreamWaitEvent(c->stream, c->ev_res[pq], 0));
+    HIPC(c, launch_patch(a, b->ext, c->stream));
+  }
   HIPC(c, hipEventRecord(c->ev_sw[q], c->stream));
   HIPC(c, hipStreamWaitEvent(c->rstream, c->ev_sw[q], 0));
   if (c->timing) {

@@ -766,6 +766,8 @@ __global__ __launch_bounds__(256) void gather_cand_kernel(RoundArgs a) {
     w.zm = a.t.zmem[pos];
     w.apods = a.t.apods[pos];
     w.np = a.t.npods[pos];
+    w.inv_cpu = w.acpu ? 1.0 / (double)w.acpu : 0.0;
+    w.inv_mem = w.amem ? 1.0 / (double)w.amem : 0.0;
     w.pos = pos;
     w._pad = 0;
     a.crow[(size_t)r * a.K + t] = w;
@@ -782,25 +784,242 @@ __global__ __launch_bounds__(256) void gather_cand_kernel(RoundArgs a) {
   }
 }
 
+// ================================================================== patch
+// Round k's lists were swept while round k-1 was still resolving, so they miss
+// round k-1's commits.  Before resolve k, one block per pod re-evaluates the
+// nodes round k-1 modified (the carry) under their live rows: list entries of
+// those nodes are dropped, their live keys are inserted in key order where they
+// exceed the list bound (truncating at K raises the bound), and the feasible /
+// per-plugin failure / normaliser-at-max counts are corrected by their status
+// change.  Afterwards a pod's list, bound and counts are exact for the state
+// resolve k starts from, so the resolve re-scores only its own commits.
+constexpr int PATCH_THREADS = 256;
+constexpr int PHASH = 1024;
+static_assert(PATCH_THREADS >= MAX_P && PATCH_THREADS >= MAX_K, "one thread per carried node / list entry");
+
+__device__ __forceinline__ uint32_t rhash(uint32_t x) { return (x * 2654435761u) >> 22; }  // 10 bits
+
+// #entries of the descending array v[0..n) that are > x
+__device__ __forceinline__ uint32_t count_greater(const uint64_t *v, uint32_t n, uint64_t x) {
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (v[mid] > x) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ void ext_from_words(const uint64_t *w, NodeExt &e) {
+  e.hard = w[0];
+  e.prefer = w[1];
+#pragma unroll
+  for (int q = 0; q < LW; ++q) e.lab[q] = w[2 + q];
+#pragma unroll
+  for (int q = 0; q < NNUM; ++q) e.num[q] = (int64_t)w[2 + LW + q];
+}
+
+// Status change of one node between the row the counts were taken on (st0)
+// and its live row (st1), as count corrections: d[0] feasible lost,
+// d[1 + q] first failures gained at plugin q, d[6] / d[7] normaliser-at-max lost.
+template <bool EXT>
+__device__ __forceinline__ void status_delta(const PodDev &p, const uint64_t *clauses, int st0, int st1,
+                                            const NodeExt &e, uint32_t slot, int64_t tt_max, int64_t na_max,
+                                            int32_t *d) {
+  d[0] += (st0 == ST_FEASIBLE) - (st1 == ST_FEASIBLE);
+#pragma unroll
+  for (int q = 0; q < NFILT; ++q) d[1 + q] += (st1 == q) - (st0 == q);
+  if (EXT && (p.flags & PF_TT)) {
+    const int at = taint_raw(p, e) == tt_max;
+    d[6] += (st0 == ST_FEASIBLE) * at - (st1 == ST_FEASIBLE) * at;
+  }
+  if (EXT && (p.flags & PF_NA)) {
+    const int at = preferred_raw(p, clauses, e, slot) == na_max;
+    d[7] += (st0 == ST_FEASIBLE) * at - (st1 == ST_FEASIBLE) * at;
+  }
+}
+
+template <bool EXT>
+__global__ __launch_bounds__(PATCH_THREADS) void patch_kernel(RoundArgs a) {
+  constexpr int NW = PATCH_THREADS / WAVE;
+  __shared__ uint32_t s_hkey[PHASH];
+  __shared__ uint64_t s_k1[MAX_P];    // carried nodes' live keys (0: infeasible)
+  __shared__ uint64_t s_ckey[MAX_P];  // those above the bound, descending
+  __shared__ uint64_t s_lkey[MAX_K];  // surviving list keys, compacted (descending)
+  __shared__ uint32_t s_wl[NW], s_wc[NW];
+  __shared__ int32_t s_wd[NW][NFILT + 3];
+  __shared__ uint64_t s_wdrop[NW];
+
+  const uint32_t tid = threadIdx.x, lane = tid % WAVE, wid = tid / WAVE;
+  const uint32_t start = uniform_u32(*a.act);
+  const uint32_t r = blockIdx.x;
+  if (a.first || start >= a.npods || uniform_u32(*a.sstart) != start || start + r >= a.npods) return;
+  const uint32_t nc = uniform_u32(*a.carry_in_n);
+  if (nc == 0) return;
+  const PodDev p = load_pod(a.pods, start + r);
+  uint64_t *rec = a.frec + (size_t)r * rec_words(a.K);
+  ShardRecHdr *hdr = (ShardRecHdr *)rec;
+  const uint64_t bound = hdr->bound;
+  const uint32_t nk = hdr->nkeys;
+  int64_t tt_max = 0, na_max = 0;
+  if (EXT) {
+    tt_max = a.norm_max[2 * r];
+    na_max = a.norm_max[2 * r + 1];
+  }
+  for (uint32_t i = tid; i < PHASH; i += PATCH_THREADS) s_hkey[i] = 0;
+  __syncthreads();
+
+  // (1) carried node tid: its row at the sweep (rc0 / rm0 / np0) and live
+  int32_t d[NFILT + 3] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint64_t k1 = 0;
+  CarryRec cr;
+  CandRow crow_c;
+  NodeExt ce;
+  if (tid < nc) {
+    cr = a.carry_in[tid];
+    if (EXT) ext_from_words(cr.ext, ce);
+    crow_c.acpu = cr.acpu;
+    crow_c.amem = cr.amem;
+    crow_c.rc = cr.rc;
+    crow_c.rm = cr.rm;
+    crow_c.zc = cr.zc;
+    crow_c.zm = cr.zm;
+    crow_c.inv_cpu = cr.acpu ? 1.0 / (double)cr.acpu : 0.0;
+    crow_c.inv_mem = cr.amem ? 1.0 / (double)cr.amem : 0.0;
+    crow_c.apods = cr.apods;
+    crow_c.np = cr.np;
+    crow_c.pos = cr.pos;
+    crow_c._pad = 0;
+    const NodeRegs r1 = make_regs_inv(cr.acpu, cr.amem, cr.rc, cr.rm, cr.zc, cr.zm, cr.apods, cr.np, cr.slot,
+                                      crow_c.inv_cpu, crow_c.inv_mem);
+    NodeRegs r0 = r1;
+    r0.free_cpu = (double)(cr.acpu - cr.rc0);
+    r0.free_mem = (double)(cr.amem - cr.rm0);
+    r0.bits = (r1.bits & ~2u) | ((int64_t)cr.np0 + 1 <= (int64_t)cr.apods ? 2u : 0u);
+    const int st0 = filter<EXT>(p, a.clauses, r0, ce);
+    const int st1 = filter<EXT>(p, a.clauses, r1, ce);
+    if (st1 == ST_FEASIBLE) k1 = pack_key(total_score<EXT>(p, a.clauses, r1, ce, a.w, tt_max, na_max), cr.slot);
+    if (st0 != st1) status_delta<EXT>(p, a.clauses, st0, st1, ce, cr.slot, tt_max, na_max, d);
+    uint32_t h = rhash(cr.slot);
+    while (atomicCAS(&s_hkey[h], 0u, cr.slot + 1) != 0u) h = (h + 1) & (PHASH - 1);
+  }
+  if (tid < MAX_P) s_k1[tid] = k1;
+  if (__ballot(d[0] | d[1] | d[2] | d[3] | d[4] | d[5] | d[6] | d[7]) != 0) {
+#pragma unroll
+    for (int q = 0; q < NFILT + 3; ++q) d[q] = wave_sum_i32_dpp(d[q]);
+  }
+  if (lane == 0)
+    for (int q = 0; q < NFILT + 3; ++q) s_wd[wid][q] = d[q];
+  __syncthreads();
+
+  // (2) list entry tid survives unless its node is carried; compaction keeps key order
+  uint64_t lk = 0;
+  bool keep = false;
+  CandRow lrow;
+  CandExt lext;
+  if (tid < nk) {
+    lk = rec[REC_HDR_WORDS + tid];
+    const uint32_t slot = 0xFFFFFFFFu - (uint32_t)lk;
+    uint32_t h = rhash(slot);
+    keep = true;
+    while (s_hkey[h] != 0) {
+      if (s_hkey[h] == slot + 1) { keep = false; break; }
+      h = (h + 1) & (PHASH - 1);
+    }
+    if (keep) {
+      lrow = a.crow[(size_t)r * a.K + tid];
+      if (EXT) lext = a.cext[(size_t)r * a.K + tid];
+    }
+  }
+  const bool cin = k1 > bound;  // carried keys the bound does not cover must be listed
+  const uint64_t kb = __ballot(keep), cb = __ballot(cin);
+  const uint64_t lt = (1ull << lane) - 1ull;
+  if (lane == 0) {
+    s_wl[wid] = (uint32_t)__popcll(kb);
+    s_wc[wid] = (uint32_t)__popcll(cb);
+  }
+  __syncthreads();
+  uint32_t li = (uint32_t)__popcll(kb & lt), nsurv = 0, ncl = 0;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    li += (uint32_t)w < wid ? s_wl[w] : 0u;
+    nsurv += s_wl[w];
+    ncl += s_wc[w];
+  }
+  uint32_t crank = 0;
+  if (cin) {
+    for (uint32_t c = 0; c < nc; ++c) crank += s_k1[c] > k1;  // > k1 implies above the bound
+    s_ckey[crank] = k1;
+  }
+  if (keep) s_lkey[li] = lk;
+  __syncthreads();
+
+  // (3) merged positions; what falls off the end raises the bound
+  uint32_t pos_l = 0xFFFFFFFFu, pos_c = 0xFFFFFFFFu;
+  uint64_t drop = 0;
+  if (keep) {
+    pos_l = li + count_greater(s_ckey, ncl, lk);
+    if (pos_l >= a.K) drop = lk;
+  }
+  if (cin) {
+    pos_c = crank + count_greater(s_lkey, nsurv, k1);
+    if (pos_c >= a.K) drop = max(drop, k1);
+  }
+  drop = wave_max_u64_dpp(drop);
+  if (lane == 0) s_wdrop[wid] = drop;
+  __syncthreads();  // every old key / row of this record has been read: rewrite in place
+  if (keep && pos_l < a.K) {
+    rec[REC_HDR_WORDS + pos_l] = lk;
+    a.crow[(size_t)r * a.K + pos_l] = lrow;
+    if (EXT) a.cext[(size_t)r * a.K + pos_l] = lext;
+  }
+  if (cin && pos_c < a.K) {
+    rec[REC_HDR_WORDS + pos_c] = k1;
+    a.crow[(size_t)r * a.K + pos_c] = crow_c;
+    if (EXT) {
+      CandExt x;
+      for (int q = 0; q < 2 + LW + NNUM; ++q) x.w[q] = cr.ext[q];
+      a.cext[(size_t)r * a.K + pos_c] = x;
+    }
+  }
+  if (tid == 0) {
+    uint64_t nb = bound;
+    int32_t sum[NFILT + 3] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int w = 0; w < NW; ++w) {
+      nb = max(nb, s_wdrop[w]);
+      for (int q = 0; q < NFILT + 3; ++q) sum[q] += s_wd[w][q];
+    }
+    hdr->bound = nb;
+    hdr->nkeys = min(a.K, nsurv + ncl);
+    hdr->feasible -= (uint32_t)sum[0];
+    for (int q = 0; q < NFILT; ++q) hdr->fails[q] += (uint32_t)sum[1 + q];
+    hdr->tt_cnt -= (uint32_t)sum[6];
+    hdr->na_cnt -= (uint32_t)sum[7];
+  }
+}
+
 // ================================================================= resolve
-// One workgroup walks the round's pods in queue order:
-// pod i's winner is the best of (a) its first listed candidate that no pod
-// < i modified (its key is unchanged: same row, same normalisation max) and
-// (b) every modified node re-scored against the live row.  If neither is
-// provably the maximum (every listed candidate modified and the best
-// modified key not above the list bound), or a normalising plugin's max may
-// have moved, the round ends before pod i and the next sweep restarts there.
+// One workgroup walks the round's pods in queue order.
+// The patched lists are exact for the round's start state, so pod i's winner is
+// the best of (a) its first listed candidate that no pod < i modified (its key
+// is unchanged: same row, same normalisation max) and (b) every node a pod < i
+// modified, re-scored against its live row.  If neither is provably the
+// maximum (every listed candidate modified and the best modified key not above
+// the list bound), or a normalising plugin's max may have moved, the round
+// ends before pod i and the next sweep restarts there.
 //
-// Latency design: every pod descriptor / record header of the round is
-// staged in LDS up front; the next pod's candidate keys and their S0 rows are
-// prefetched into registers while the current pod resolves; modified rows
-// (S0 and live) live in LDS; the decision is recomputed by every thread from
-// the per-wave partials, so each pod costs two barriers.
+// Latency design: pod descriptors / record headers of the round are staged in
+// LDS; the next pod's candidate keys and rows are prefetched into registers
+// while the current pod resolves; list threads (waves 0-3) hold one listed
+// candidate each, rescoring threads (waves 4-7) one modified node each, in
+// registers (the node that joins the modified set is handed over through LDS);
+// every thread recomputes the decision from the per-wave partials, so each
+// pod costs two barriers.
 constexpr int RESOLVE_THREADS = 512;
 constexpr int RNW = RESOLVE_THREADS / WAVE;
 constexpr int RHASH = 1024;
-
-__device__ __forceinline__ uint32_t rhash(uint32_t x) { return (x * 2654435761u) >> 22; }  // 10 bits
+constexpr int RES_LIST_THREADS = RESOLVE_THREADS / 2;
+static_assert(RES_LIST_THREADS >= MAX_K && RESOLVE_THREADS - RES_LIST_THREADS >= MAX_P, "resolve roles");
 
 // Workgroup barrier for LDS hand-offs only: __syncthreads() also drains vmcnt,
 // which would expose the next pod's prefetch latency on every iteration.
@@ -817,48 +1036,28 @@ __device__ __forceinline__ void lds_barrier() {
     uint64_t t_;                                                                         \
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");            \
     __builtin_amdgcn_sched_barrier(0);                                                   \
-    if (tid == 0) { stamp_acc[i] += t_ - stamp_last; }                                   \
+    if (tid == STAMP_TID) { stamp_acc[i] += t_ - stamp_last; }                           \
     stamp_last = t_;                                                                     \
   } while (0)
 #else
 #define STAMP(i) do {} while (0)
 #endif
 
-// Roles: waves 0-3 own the listed candidates (thread t = list entry t, K <= 256),
-// waves 4-7 re-score the modified nodes (m = tid - 256), so the two halves of a
-// pod's work run side by side on different SIMDs.
-constexpr int RES_LIST_THREADS = RESOLVE_THREADS / 2;
-
 template <bool EXT>
 __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
-  // round inputs
   __shared__ PodDev s_pod[MAX_P];
   __shared__ ShardRecHdr s_hdr[MAX_P];
   __shared__ uint32_t s_norm[MAX_P][2];
-  // modified nodes (carried from the previous round first, then this round's):
-  // the row the sweep saw (S0: only its filter inputs), the live state,
-  // binary64 constants, ext columns; carried entries also keep their state at
-  // the start of this round (the row the next round's sweep sees)
-  __shared__ uint32_t s_mslot[MAX_MOD], s_mpos[MAX_MOD];
-  __shared__ int64_t s_acpu[MAX_MOD], s_amem[MAX_MOD];
-  __shared__ int64_t s_rc0[MAX_MOD], s_rm0[MAX_MOD];
-  __shared__ int64_t s_rc[MAX_MOD], s_rm[MAX_MOD], s_zc[MAX_MOD], s_zm[MAX_MOD];
-  __shared__ double s_dcpu[MAX_MOD], s_dmem[MAX_MOD], s_icpu[MAX_MOD], s_imem[MAX_MOD];
-  __shared__ int32_t s_apods[MAX_MOD], s_np0[MAX_MOD], s_np[MAX_MOD];
-  __shared__ int64_t s_rcm[MAX_P], s_rmm[MAX_P];
-  __shared__ int32_t s_npm[MAX_P];
-  __shared__ uint64_t s_ext[EXT ? MAX_MOD : 1][2 + LW + NNUM];
-  __shared__ uint32_t s_hkey[RHASH];
-  __shared__ uint16_t s_hval[RHASH];
+  __shared__ uint32_t s_hkey[RHASH];   // slots modified this round (+1), linear probing
+  __shared__ CandRow s_new;            // row of the node joining the modified set
+  __shared__ CandExt s_newx;
   // per-wave partials (entries of waves that had no work keep identities)
-  __shared__ uint64_t s_wkey[RNW];      // best modified key
-  __shared__ uint32_t s_widx[RNW];      // first unmodified list index
-  __shared__ uint64_t s_wlk[RNW];       // its key
+  __shared__ uint64_t s_wkey[RNW];     // best modified key
+  __shared__ uint32_t s_widx[RNW];     // first unmodified list index
+  __shared__ uint64_t s_wlk[RNW];      // its key
   __shared__ int32_t s_wd[RNW][NFILT + 3];
   __shared__ uint32_t s_wany[RNW];
-  __shared__ uint32_t s_nmod;
   __shared__ uint32_t s_stop;
-  __shared__ uint32_t s_cout;
 
   const uint32_t tid = threadIdx.x, lane = tid % WAVE, wid = tid / WAVE;
   const uint32_t start = uniform_u32(*a.act);
@@ -874,39 +1073,11 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
     return;
   }
   const uint32_t nround = min(a.P, a.npods - start);
-  const uint32_t nseed = a.first ? 0u : uniform_u32(*a.carry_in_n);
   const uint32_t RW = rec_words(a.K);
   const bool list_role = tid < RES_LIST_THREADS;
+  const uint32_t mj = tid - RES_LIST_THREADS;  // rescoring role: owned modified node
   // ---- stage the round
   for (uint32_t i = tid; i < RHASH; i += RESOLVE_THREADS) s_hkey[i] = 0;
-  __syncthreads();
-  // carried nodes: modified by the previous round, which this round's sweep did not see
-  for (uint32_t m = tid; m < nseed; m += RESOLVE_THREADS) {
-    const CarryRec &c = a.carry_in[m];
-    s_mslot[m] = c.slot;
-    s_mpos[m] = c.pos;
-    s_acpu[m] = c.acpu;
-    s_amem[m] = c.amem;
-    s_rc0[m] = c.rc0;
-    s_rm0[m] = c.rm0;
-    s_np0[m] = c.np0;
-    s_rc[m] = s_rcm[m] = c.rc;
-    s_rm[m] = s_rmm[m] = c.rm;
-    s_zc[m] = c.zc;
-    s_zm[m] = c.zm;
-    s_np[m] = s_npm[m] = c.np;
-    s_apods[m] = c.apods;
-    const double dc = (double)c.acpu, dm = (double)c.amem;
-    s_dcpu[m] = dc;
-    s_dmem[m] = dm;
-    s_icpu[m] = c.acpu ? 1.0 / dc : 1.0;
-    s_imem[m] = c.amem ? 1.0 / dm : 1.0;
-    if (EXT)
-      for (int q = 0; q < 2 + LW + NNUM; ++q) s_ext[m][q] = c.ext[q];
-    uint32_t h = rhash(c.slot);
-    while (atomicCAS(&s_hkey[h], 0u, c.slot + 1) != 0u) h = (h + 1) & (RHASH - 1);
-    s_hval[h] = (uint16_t)m;
-  }
   for (uint32_t i = tid; i < nround; i += RESOLVE_THREADS) {
     s_pod[i] = a.pods[start + i];
     s_hdr[i] = *(const ShardRecHdr *)(a.frec + (size_t)i * RW);
@@ -919,9 +1090,9 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
     s_wlk[tid] = 0;
     s_wany[tid] = 0;
   }
-  if (tid == 0) { s_nmod = nseed; s_stop = nround; s_cout = 0; }
-  // prefetch pod 0's candidates (list thread t holds entry t, its key and S0
-  // row): independent loads of the gathered candidate rows, consumed one pod later
+  if (tid == 0) s_stop = nround;
+  // prefetch pod 0's candidates (list thread t holds entry t, its key and row):
+  // independent loads of the gathered candidate rows, consumed one pod later
   uint64_t ck = 0;
   CandRow crow{};
   CandExt cext{};
@@ -934,8 +1105,19 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
     if (!on) k = 0;
   };
   prefetch(0, ck, crow, cext);
+  // rescoring role state: modified node mj, in registers
+  bool mine = false;
+  NodeRegs mr{};             // live row
+  double m_f0c = 0, m_f0m = 0;  // round-start free cpu / memory (filter of the listed row)
+  uint32_t m_bits0 = 0;
+  NodeExt me{};
+  int64_t m_acpu = 0, m_amem = 0, m_rc0 = 0, m_rm0 = 0, m_rc = 0, m_rm = 0, m_zc = 0, m_zm = 0;
+  int32_t m_apods = 0, m_np0 = 0, m_np = 0;
+  uint32_t m_pos = 0;
+  uint32_t nmod = 0;  // uniform
   __syncthreads();
 #ifdef KS_STAMPS
+  constexpr uint32_t STAMP_TID = KS_STAMPS;
   uint64_t stamp_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, stamp_last = 0;
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(stamp_last)::"memory");
 #endif
@@ -955,10 +1137,9 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
     CandRow nrow;
     CandExt next_ext;
     prefetch(r + 1, nk, nrow, next_ext);
-    const uint32_t nmod = s_nmod;
 
     if (list_role) {
-      // (b) is my listed candidate unmodified by the pods before this one?
+      // (a) is my listed candidate unmodified by the pods before this one?
       bool unmod = false;
       if (ck != 0 && tid < hdr.nkeys) {
         const uint32_t slot = 0xFFFFFFFFu - (uint32_t)ck;
@@ -981,44 +1162,21 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
         }
       }
     } else {
-      // (a) re-score modified nodes: S0 row vs live row, both from LDS
+      // (b) my modified node re-scored: round-start row vs live row
       uint64_t mkey = 0;
       int32_t d[NFILT + 3] = {0, 0, 0, 0, 0, 0, 0, 0};
       bool dany = false;
-      for (uint32_t m = tid - RES_LIST_THREADS; m < nmod; m += RESOLVE_THREADS - RES_LIST_THREADS) {
-        NodeExt e;
-        if (EXT) {
-          e.hard = s_ext[m][0];
-          e.prefer = s_ext[m][1];
-#pragma unroll
-          for (int q = 0; q < LW; ++q) e.lab[q] = s_ext[m][2 + q];
-#pragma unroll
-          for (int q = 0; q < NNUM; ++q) e.num[q] = (int64_t)s_ext[m][2 + LW + q];
-        }
-        const uint32_t slot = s_mslot[m];
-        const int64_t acpu = s_acpu[m], amem = s_amem[m];
-        const int32_t ap = s_apods[m];
-        NodeRegs ri = make_regs_inv(acpu, amem, s_rc[m], s_rm[m], s_zc[m], s_zm[m], ap, s_np[m], slot, s_icpu[m],
-                                    s_imem[m]);
-        NodeRegs r0 = ri;  // S0 row: only its filter status is needed
-        r0.free_cpu = (double)(acpu - s_rc0[m]);
-        r0.free_mem = (double)(amem - s_rm0[m]);
-        r0.bits = (ri.bits & ~2u) | ((int64_t)s_np0[m] + 1 <= (int64_t)ap ? 2u : 0u);
-        const int st0 = filter<EXT>(p, a.clauses, r0, e);
-        const int sti = filter<EXT>(p, a.clauses, ri, e);
-        if (sti == ST_FEASIBLE) {
-          const uint64_t k = pack_key(total_score<EXT>(p, a.clauses, ri, e, a.w, tt_max, na_max), slot);
-          mkey = k > mkey ? k : mkey;
-        }
+      if (mine) {
+        NodeRegs r0 = mr;
+        r0.free_cpu = m_f0c;
+        r0.free_mem = m_f0m;
+        r0.bits = m_bits0;
+        const int st0 = filter<EXT>(p, a.clauses, r0, me);
+        const int sti = filter<EXT>(p, a.clauses, mr, me);
+        if (sti == ST_FEASIBLE) mkey = pack_key(total_score<EXT>(p, a.clauses, mr, me, a.w, tt_max, na_max), mr.slot);
         if (st0 != sti) {
           dany = true;
-          d[0] += (st0 == ST_FEASIBLE) - (sti == ST_FEASIBLE);
-#pragma unroll
-          for (int q = 0; q < NFILT; ++q) d[1 + q] += (sti == q) - (st0 == q);
-          if (EXT && st0 == ST_FEASIBLE) {
-            if (p.flags & PF_TT) d[6] += taint_raw(p, e) == tt_max;
-            if (p.flags & PF_NA) d[7] += preferred_raw(p, a.clauses, e, slot) == na_max;
-          }
+          status_delta<EXT>(p, a.clauses, st0, sti, me, mr.slot, tt_max, na_max, d);
         }
       }
       STAMP(2);
@@ -1089,91 +1247,105 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
       res.flags = (win && feasible == 1) ? 1u : 0u;
       ((DevResult *)a.results)[pi] = res;
     }
-    // commit (AssumePod -> NodeInfo.AddPod on the live row): exactly one thread
-    if (win) {
-      if (win == ku && fu != 0xFFFFFFFFu && tid == fu) {
-        // a listed, unmodified node enters the modified set with its prefetched S0 row
-        const uint32_t slot = 0xFFFFFFFFu - (uint32_t)ck;
-        const uint32_t m = nmod;
-        uint32_t h = rhash(slot);
+    // commit (AssumePod -> NodeInfo.AddPod on the live row)
+    const uint32_t wslot = 0xFFFFFFFFu - (uint32_t)win;
+    const bool joins = win != 0 && fu != 0xFFFFFFFFu && win == ku;  // a listed, unmodified node
+    if (joins) {
+      if (tid == fu) {  // hand its row to the rescoring thread that will own it
+        uint32_t h = rhash(wslot);
         while (s_hkey[h] != 0) h = (h + 1) & (RHASH - 1);
-        s_hkey[h] = slot + 1;
-        s_hval[h] = (uint16_t)m;
-        s_mslot[m] = slot;
-        s_mpos[m] = crow.pos;
-        s_acpu[m] = crow.acpu;
-        s_amem[m] = crow.amem;
-        s_rc0[m] = crow.rc;
-        s_rm0[m] = crow.rm;
-        s_apods[m] = crow.apods;
-        s_np0[m] = crow.np;
-        s_rc[m] = crow.rc + p.req_cpu;
-        s_rm[m] = crow.rm + p.req_mem;
-        s_zc[m] = crow.zc + p.nz_cpu;
-        s_zm[m] = crow.zm + p.nz_mem;
-        s_np[m] = crow.np + 1;
-        const double dc = (double)crow.acpu, dm = (double)crow.amem;
-        s_dcpu[m] = dc;
-        s_dmem[m] = dm;
-        s_icpu[m] = crow.acpu ? 1.0 / dc : 1.0;
-        s_imem[m] = crow.amem ? 1.0 / dm : 1.0;
+        s_hkey[h] = wslot + 1;
+        // field-wise: a whole-struct copy would route the prefetched row through scratch
+        s_new.acpu = crow.acpu;
+        s_new.amem = crow.amem;
+        s_new.rc = crow.rc;
+        s_new.rm = crow.rm;
+        s_new.zc = crow.zc;
+        s_new.zm = crow.zm;
+        s_new.inv_cpu = crow.inv_cpu;
+        s_new.inv_mem = crow.inv_mem;
+        s_new.apods = crow.apods;
+        s_new.np = crow.np;
+        s_new.pos = crow.pos;
         if (EXT)
-          for (int q = 0; q < 2 + LW + NNUM; ++q) s_ext[m][q] = cext.w[q];
-        s_nmod = m + 1;
-      } else if (win == bm && win != ku && !list_role) {
-        const uint32_t target = 0xFFFFFFFFu - (uint32_t)win;
-        for (uint32_t m = tid - RES_LIST_THREADS; m < nmod; m += RESOLVE_THREADS - RES_LIST_THREADS) {
-          if (s_mslot[m] == target) {
-            s_rc[m] += p.req_cpu;
-            s_rm[m] += p.req_mem;
-            s_zc[m] += p.nz_cpu;
-            s_zm[m] += p.nz_mem;
-            s_np[m] += 1;
-          }
-        }
+#pragma unroll
+          for (int q = 0; q < 2 + LW + NNUM; ++q) s_newx.w[q] = cext.w[q];
       }
+    } else if (win != 0 && mine && mr.slot == wslot) {
+      m_rc += p.req_cpu;
+      m_rm += p.req_mem;
+      m_zc += p.nz_cpu;
+      m_zm += p.nz_mem;
+      m_np += 1;
+      mr.free_cpu -= p.req_cpu_d;  // exact integer arithmetic in binary64
+      mr.free_mem -= p.req_mem_d;
+      mr.rcpu += p.req_cpu_d;
+      mr.rmem += p.req_mem_d;
+      mr.lf100_cpu -= p.nz100_cpu;
+      mr.lf100_mem -= p.nz100_mem;
+      mr.bits = (mr.bits & ~2u) | ((int64_t)m_np + 1 <= (int64_t)m_apods ? 2u : 0u);
     }
     STAMP(6);
     lds_barrier();
     STAMP(7);
+    if (joins) {
+      if (!list_role && mj == nmod) {
+        const CandRow &w = s_new;
+        m_acpu = w.acpu;
+        m_amem = w.amem;
+        m_rc0 = w.rc;
+        m_rm0 = w.rm;
+        m_np0 = w.np;
+        m_apods = w.apods;
+        m_pos = w.pos;
+        m_rc = w.rc + p.req_cpu;
+        m_rm = w.rm + p.req_mem;
+        m_zc = w.zc + p.nz_cpu;
+        m_zm = w.zm + p.nz_mem;
+        m_np = w.np + 1;
+        mr = make_regs_inv(m_acpu, m_amem, m_rc, m_rm, m_zc, m_zm, m_apods, m_np, wslot, w.inv_cpu, w.inv_mem);
+        m_f0c = (double)(m_acpu - m_rc0);
+        m_f0m = (double)(m_amem - m_rm0);
+        m_bits0 = (mr.bits & ~2u) | ((int64_t)m_np0 + 1 <= (int64_t)m_apods ? 2u : 0u);
+        if (EXT) ext_from_words(s_newx.w, me);
+        mine = true;
+      }
+      ++nmod;
+    }
     ck = nk;
     crow = nrow;
     if (EXT) cext = next_ext;
   }
-  __syncthreads();
-  // hand the nodes this round modified to the next round and the write-back
-  // (every commit adds a pod, so "modified this round" is a pod-count change)
-  const uint32_t nmod = s_nmod;
-  for (uint32_t i = tid; i < nmod; i += RESOLVE_THREADS) {
-    const bool carried = i < nseed;
-    const int32_t npm = carried ? s_npm[i] : s_np0[i];
-    if (s_np[i] == npm) continue;
-    const uint32_t o = atomicAdd(&s_cout, 1u);
+  // hand the nodes this round modified to the next round's patch and the write-back
+  if (mine) {
     CarryRec c;
-    c.acpu = s_acpu[i];
-    c.amem = s_amem[i];
-    c.rc0 = carried ? s_rcm[i] : s_rc0[i];
-    c.rm0 = carried ? s_rmm[i] : s_rm0[i];
-    c.np0 = npm;
-    c.rc = s_rc[i];
-    c.rm = s_rm[i];
-    c.zc = s_zc[i];
-    c.zm = s_zm[i];
-    c.np = s_np[i];
-    c.slot = s_mslot[i];
-    c.pos = s_mpos[i];
-    c.apods = s_apods[i];
+    c.acpu = m_acpu;
+    c.amem = m_amem;
+    c.rc0 = m_rc0;
+    c.rm0 = m_rm0;
+    c.np0 = m_np0;
+    c.rc = m_rc;
+    c.rm = m_rm;
+    c.zc = m_zc;
+    c.zm = m_zm;
+    c.np = m_np;
+    c.slot = mr.slot;
+    c.pos = m_pos;
+    c.apods = m_apods;
     c._pad = 0;
-    for (int q = 0; q < 2 + LW + NNUM; ++q) c.ext[q] = EXT ? s_ext[i][q] : 0ull;
-    a.carry_out[o] = c;
+    c.ext[0] = me.hard;
+    c.ext[1] = me.prefer;
+    for (int q = 0; q < LW; ++q) c.ext[2 + q] = me.lab[q];
+    for (int q = 0; q < NNUM; ++q) c.ext[2 + LW + q] = (uint64_t)me.num[q];
+    a.carry_out[mj] = c;
   }
   __syncthreads();
 #ifdef KS_STAMPS
-  if (tid == 0)
+  if (tid == STAMP_TID)
     for (int i = 0; i < 8; ++i) atomicAdd((unsigned long long *)&a.counters[8 + i], (unsigned long long)stamp_acc[i]);
 #endif
   if (tid == 0) {
-    *a.carry_out_n = s_cout;
+    *a.carry_out_n = nmod;
     *a.act_next = start + s_stop;
     *a.d_start = start + s_stop;
     a.counters[0] += 1;                                   // rounds
@@ -1381,6 +1553,12 @@ hipError_t launch_advance(const RoundArgs &a, hipStream_t st) {
 
 hipError_t launch_writeback(const NodeTable &t, const CarryRec *carry, const uint32_t *n, hipStream_t st) {
   writeback_kernel<<<2, 256, 0, st>>>(t, carry, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_patch(const RoundArgs &a, bool ext, hipStream_t st) {
+  if (ext) patch_kernel<true><<<a.P, PATCH_THREADS, 0, st>>>(a);
+  else patch_kernel<false><<<a.P, PATCH_THREADS, 0, st>>>(a);
   return hipGetLastError();
 }
 

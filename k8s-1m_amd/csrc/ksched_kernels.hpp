@@ -9,7 +9,7 @@ namespace ks {
 
 constexpr int MAX_PG = 64;    // pods per sweep block (LDS wave records)
 constexpr int MAX_P = 256;    // pods per round (resolve stages the round in LDS)
-constexpr int MAX_MOD = 2 * MAX_P;  // modified nodes a resolve tracks (carried + its own)
+constexpr int MAX_K = 256;    // candidates per pod record (one list thread each in the resolve)
 
 struct RoundArgs {
   NodeTable t;
@@ -34,7 +34,7 @@ struct RoundArgs {
   uint32_t *act;              // this round's actual start (written by the previous resolve)
   uint32_t *act_next;         // next round's actual start (written by this resolve)
   const uint32_t *prev_act;   // previous round's actual start
-  const CarryRec *carry_in;   // nodes the previous round's resolve modified
+  const CarryRec *carry_in;   // nodes the previous round's resolve modified (merged by the patch)
   const uint32_t *carry_in_n;
   CarryRec *carry_out;        // nodes this round's resolve modifies
   uint32_t *carry_out_n;
@@ -69,6 +69,7 @@ hipError_t launch_sweep(const RoundArgs &a, bool ext, uint32_t nblocks, uint32_t
 hipError_t launch_merge(const RoundArgs &a, uint32_t nshards, hipStream_t st);
 hipError_t launch_merge_shards(const RoundArgs &a, hipStream_t st);
 hipError_t launch_gather_cand(const RoundArgs &a, bool ext, hipStream_t st);
+hipError_t launch_patch(const RoundArgs &a, bool ext, hipStream_t st);
 hipError_t launch_resolve(const RoundArgs &a, bool ext, hipStream_t st);
 hipError_t launch_advance(const RoundArgs &a, hipStream_t st);
 hipError_t launch_writeback(const NodeTable &t, const CarryRec *carry, const uint32_t *n, hipStream_t st);
