@@ -75,6 +75,8 @@ def main():
                       topk=args.topk, nodes_per_lane=args.nodes_per_lane, world_size=world, rank=rank)
     if world > 1:
         sched.comm_init(exchange_unique_id(rank, world))
+        if rank == 0:  # ncclCommInitRank returned: every rank has read the id
+            uid_path(world).unlink(missing_ok=True)
 
     nodes = synth.nodes(kind, args.nodes, 1)
     slots = synth.slot_array(args.nodes)
@@ -184,6 +186,7 @@ def main():
             "resolve_ms_total": round(st.resolve_ms, 3),
             "scheduled_fraction": round(scheduled / pods_timed, 4),
             "speculated_rounds_wasted": int(dbg[3]),  # since open (warmup included)
+            "pods_reswept_wrong_norm_guess": int(dbg[4]),  # since open (warmup included)
             "node_evals_per_s": round(value * args.nodes, 1),
             "setup_s": round(setup_s, 2),
         },
@@ -195,13 +198,20 @@ def main():
         print(json.dumps(line), flush=True)
 
 
+def uid_path(world: int) -> Path:
+    # Every local rank of one launch is a child of the same torchrun agent, so
+    # the agent's pid (+ its restart count) names this launch alone: a file
+    # left by an earlier launch on the same port is never read.
+    key = "_".join([os.environ.get("TORCHELASTIC_RUN_ID", "run"), os.environ.get("MASTER_PORT", "0"),
+                    str(os.getppid()), os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")]).replace("/", "_")
+    return Path(os.environ.get("TMPDIR", "/tmp")) / f"ksched_uid_{key}_w{world}.bin"
+
+
 def exchange_unique_id(rank: int, world: int) -> bytes:
     """Rank 0 publishes the RCCL unique id in a file every local rank reads."""
     from ksched import Scheduler
 
-    key = "_".join([os.environ.get("TORCHELASTIC_RUN_ID", "run"), os.environ.get("MASTER_ADDR", "127.0.0.1"),
-                    os.environ.get("MASTER_PORT", "0")]).replace("/", "_")
-    path = Path(os.environ.get("TMPDIR", "/tmp")) / f"ksched_uid_{key}.bin"
+    path = uid_path(world)
     if rank == 0:
         tmp = path.with_suffix(".tmp")
         tmp.write_bytes(Scheduler.comm_unique_id())

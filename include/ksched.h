@@ -300,8 +300,10 @@ typedef struct {
 } ks_stats;
 ks_status ks_get_stats(ks_ctx *ctx, ks_stats *out);
 ks_status ks_reset_stats(ks_ctx *ctx);
-/* Raw device counters: [0] rounds [1] pods resolved [2] pods swept,
- * [8..15] resolve phase cycle sums (diagnostic KS_STAMPS build only). */
+/* Raw device counters: [0] rounds [1] pods resolved [2] pods swept
+ * [3] speculated rounds wasted [4] pods re-swept because their guessed
+ * normalising maxima were wrong, [8..15] resolve phase cycle sums
+ * (diagnostic KS_STAMPS build only). */
 ks_status ks_debug_counters(ks_ctx *ctx, uint64_t out[16]);
 /* 1 = time every sweep/resolve launch with HIP events (adds syncs), 0 = off. */
 ks_status ks_set_timing(ks_ctx *ctx, int32_t enabled);

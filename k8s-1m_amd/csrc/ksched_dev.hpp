@@ -77,7 +77,11 @@ struct alignas(16) PodDev {
   uint32_t req_off, req_len; // required program (clauses) in the clause buffer
   uint32_t pref_off, pref_len;
   uint32_t n_req_terms;      // OR terms after the mandatory nodeSelector group
-  uint32_t _pad[5];
+  // Normalising-plugin maxima the sweep scores with (PF_TT / PF_NA): the host's
+  // guess of max raw over feasible nodes.  The merge measures the true maxima;
+  // pods whose guess was wrong are re-swept with them (norm_check, fix sweep).
+  uint32_t tt_guess, na_guess;
+  uint32_t _pad[3];
 };
 static_assert(sizeof(PodDev) == 128, "PodDev layout");
 
@@ -105,9 +109,18 @@ struct alignas(16) BlockRec {
   uint64_t bound;             // every feasible node of the block not listed has key <= bound
   uint32_t feasible;
   uint32_t fails[NFILT];
-  uint32_t tt_cnt, na_cnt;    // feasible nodes whose raw normalising score equals the max
+  uint32_t tt_cnt, na_cnt;    // feasible nodes whose raw normalising score equals the max used
+  uint32_t tt_max, na_max;    // max raw TaintToleration / NodeAffinity score over the feasible nodes
 };
 static_assert(sizeof(BlockRec) == 80, "BlockRec layout");
+
+// Per pod of a round after the merge (max over blocks and shards, then RCCL
+// all-reduce(max) across ranks): the measured normalising maxima and whether
+// any node is feasible.  norm_check turns it into norm_max and the fix flags.
+struct PodStat {
+  uint32_t tt_max, na_max, any_feasible, _pad;
+};
+static_assert(sizeof(PodStat) == 16, "PodStat layout");
 
 // Per (pod-in-round, shard): sorted candidate prefix.  Stored as a fixed
 // header followed by K keys (stride rec_words(K) u64).
@@ -150,13 +163,6 @@ struct alignas(16) CarryRec {
   uint64_t ext[2 + LW + NNUM];  // hard, prefer, label words, numeric labels (EXT batches)
 };
 static_assert(sizeof(CarryRec) == 160, "CarryRec layout");
-
-struct alignas(16) NormRec {
-  int64_t tt_max, na_max;
-  uint32_t tt_cnt, na_cnt;
-  uint32_t _pad[2];
-};
-static_assert(sizeof(NormRec) == 32, "NormRec layout");
 
 // Device copy of ks_result (identical layout).
 struct DevResult {

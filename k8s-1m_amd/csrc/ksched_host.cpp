@@ -170,7 +170,9 @@ struct ks_ctx {
   uint32_t *d_slot_pos = nullptr;
   uint32_t *d_start = nullptr;
   uint32_t *h_start = nullptr;  // pinned
-  uint32_t *d_norm = nullptr;
+  uint32_t *d_norm = nullptr;     // [2][P][2] by round parity
+  PodStat *d_pstat = nullptr;     // [P]
+  uint32_t *d_fix = nullptr;      // [P] flags + [MAX_P / MAX_PG] group flags
   BlockRec *d_brec = nullptr;
   size_t brec_bytes = 0;
   uint64_t *d_srec = nullptr, *d_frec = nullptr;
@@ -191,6 +193,7 @@ struct ks_ctx {
   std::map<std::pair<uint32_t, uint32_t>, uint32_t> prefer_dict;
   std::vector<std::pair<uint32_t, uint32_t>> prefer_list;
   uint64_t hard_in_use = 0, prefer_in_use = 0;
+  std::unordered_map<uint64_t, uint32_t> prefer_masks;  // prefer-taint word -> present nodes with it
   std::map<std::pair<uint32_t, uint32_t>, uint32_t> pair_bit;
   std::unordered_map<uint32_t, uint32_t> key_bit;
   std::unordered_map<uint32_t, NumCol> num_col;
@@ -553,6 +556,19 @@ bool compile_term(ks_ctx *c, const ks_term &t, uint32_t term, int32_t weight, Cl
   return true;
 }
 
+// Reference count of the non-zero prefer-taint words of present nodes (the
+// TaintToleration max guess of compile_pod).
+void prefer_mask_ref(ks_ctx *c, uint64_t mask, int delta) {
+  if (!mask) return;
+  auto it = c->prefer_masks.find(mask);
+  if (delta > 0) {
+    if (it == c->prefer_masks.end()) c->prefer_masks.emplace(mask, 1u);
+    else it->second++;
+  } else if (it != c->prefer_masks.end() && --it->second == 0) {
+    c->prefer_masks.erase(it);
+  }
+}
+
 ks_status compile_pod(ks_ctx *c, const ks_pod &p, PodDev &d, ClauseBuf &cl) {
   std::memset(&d, 0, sizeof d);
   ks_status st;
@@ -586,7 +602,18 @@ ks_status compile_pod(ks_ctx *c, const ks_pod &p, PodDev &d, ClauseBuf &cl) {
   for (size_t b = 0; b < c->prefer_list.size(); ++b)
     if (tolerates(c, tols_prefer, c->prefer_list[b].first, c->prefer_list[b].second, KS_EFFECT_PREFER_NO_SCHEDULE))
       d.tol_prefer |= 1ull << b;
-  if (c->prefer_in_use & ~d.tol_prefer) d.flags |= PF_TT;
+  if (c->prefer_in_use & ~d.tol_prefer) {
+    d.flags |= PF_TT;
+    // guess of max raw over feasible nodes: the max over the prefer-taint words
+    // present in the cluster (exact unless no feasible node carries the worst one)
+    uint32_t g = 0;
+    if (c->prefer_masks.size() <= 256) {
+      for (const auto &kv : c->prefer_masks) g = std::max<uint32_t>(g, (uint32_t)__builtin_popcountll(kv.first & ~d.tol_prefer));
+    } else {
+      g = (uint32_t)__builtin_popcountll(c->prefer_in_use & ~d.tol_prefer);
+    }
+    d.tt_guess = g;
+  }
   // spec.nodeName
   d.name_slot = -1;
   if (p.node_name && p.node_name[0]) {
@@ -647,6 +674,7 @@ ks_status compile_pod(ks_ctx *c, const ks_pod &p, PodDev &d, ClauseBuf &cl) {
       }
       if (cl.w.size() == mark) cl.add(CK_ANY, nt + 1, t.weight, nullptr, 0);  // unreachable (non-empty)
       ++nt;
+      d.na_guess += (uint32_t)t.weight;  // guess of max raw: every term matches some feasible node
     }
     if (nt) d.flags |= PF_NA;
   }
@@ -788,6 +816,10 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k) {
   a.carry_out_n = c->d_pipe + 4 + q;
   a.first = k == 0;
   a.norm_max = c->d_norm + (size_t)q * 2 * c->P;
+  a.pstat = b->norm ? c->d_pstat : nullptr;
+  a.fix_flag = c->d_fix;
+  a.fix_group = c->d_fix + MAX_P;
+  a.fix = 0;
   a.brec = c->d_brec;
   a.srec = c->d_srec + (size_t)q * c->S * c->P * RW;
   a.frec = c->S == 1 ? a.srec : c->d_frec + (size_t)q * c->P * RW;
@@ -811,11 +843,7 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k) {
     HIPC(c, launch_writeback(c->t, c->d_carry + (size_t)q * MAX_P, c->d_pipe + 4 + q, c->stream));
   }
   HIPC(c, launch_advance(a, c->stream));
-  if (b->norm) {
-    HIPC(c, hipMemsetAsync(a.norm_max, 0, (size_t)2 * c->P * 4, c->stream));
-    HIPC(c, launch_prescore(a, bmax, groups, nloc, c->stream));
-    if (multi) NCCLC(c, ncclAllReduce(a.norm_max, a.norm_max, 2 * c->P, ncclUint32, ncclMax, c->comm, c->stream));
-  }
+  if (b->norm) HIPC(c, hipMemsetAsync(c->d_pstat, 0, (size_t)c->P * sizeof(PodStat), c->stream));
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (c->timing) {
     e0 = get_event(c);
@@ -828,6 +856,18 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k) {
     c->ev_sweep.emplace_back(e0, e1);
   }
   HIPC(c, launch_merge(a, nloc, c->stream));
+  if (b->norm) {
+    // the sweep scored normalising plugins with each pod's guessed maxima:
+    // measure (all ranks), flag the wrong guesses, re-sweep + re-merge those pods
+    if (multi)
+      NCCLC(c, ncclAllReduce(c->d_pstat, c->d_pstat, 4 * c->P, ncclUint32, ncclMax, c->comm, c->stream));
+    HIPC(c, launch_norm_check(a, c->stream));
+    RoundArgs f = a;
+    f.fix = 1;
+    f.pg = MAX_PG;
+    HIPC(c, launch_sweep(f, true, bmax, (c->P + MAX_PG - 1) / MAX_PG, nloc, c->stream));
+    HIPC(c, launch_merge(f, nloc, c->stream));
+  }
   if (multi) {
     const size_t words = (size_t)c->P * RW;
     NCCLC(c, ncclAllGather(a.srec + (size_t)c->cfg.rank * words, a.srec, words * 8, ncclUint8, c->comm, c->stream));
@@ -983,6 +1023,7 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
   HIPC(x, hipMemsetAsync(t.apods, 0xFF, (size_t)x->npos * 4, x->stream));  // every position empty
   if ((st = dalloc(x, &x->d_shards, x->S)) || (st = dalloc(x, &x->d_slot_pos, x->cap)) ||
       (st = dalloc(x, &x->d_start, 1)) || (st = dalloc(x, &x->d_norm, 2 * 2 * (size_t)x->P)) ||
+      (st = dalloc(x, &x->d_pstat, (size_t)x->P)) || (st = dalloc(x, &x->d_fix, MAX_P + MAX_P / MAX_PG)) ||
       (st = dalloc(x, &x->d_pipe, 8)) || (st = dalloc(x, &x->d_carry, 2 * (size_t)MAX_P)) ||
       (st = dalloc(x, &x->d_counters, 16)))
     return st;
@@ -1014,8 +1055,8 @@ void ks_close(ks_ctx *c) {
   if (c->comm) ncclCommDestroy(c->comm);
   void *bufs[] = {c->t.acpu, c->t.amem, c->t.rcpu, c->t.rmem, c->t.zcpu, c->t.zmem, c->t.apods,
                   c->t.npods, c->t.hard, c->t.prefer, c->t.lab, c->t.num, c->d_shards, c->d_slot_pos,
-                  c->d_start, c->d_norm, c->d_brec, c->d_srec, c->d_frec, c->d_counters, c->d_crow,
-                  c->d_cext, c->d_pipe, c->d_carry};
+                  c->d_start, c->d_norm, c->d_pstat, c->d_fix, c->d_brec, c->d_srec, c->d_frec,
+                  c->d_counters, c->d_crow, c->d_cext, c->d_pipe, c->d_carry};
   for (void *b : bufs)
     if (b) (void)hipFree(b);
   if (c->h_start) (void)hipHostFree(c->h_start);
@@ -1089,6 +1130,7 @@ ks_status ks_nodes_upsert(ks_ctx *c, const ks_node *nodes, const uint32_t *slots
       c->key_nodes[key].push_back(slot);
     }
     h.hard = h.unschedulable ? UNSCHED_BIT : 0;
+    if (!is_new) prefer_mask_ref(c, h.prefer, -1);
     h.prefer = 0;
     for (uint32_t k = 0; k < s.n_taints; ++k) {
       const ks_taint &tt = s.taints[k];
@@ -1127,6 +1169,7 @@ ks_status ks_nodes_upsert(ks_ctx *c, const ks_node *nodes, const uint32_t *slots
     if ((h.hard & ~c->hard_in_use) || (h.prefer & ~c->prefer_in_use)) grew = true;
     c->hard_in_use |= h.hard;
     c->prefer_in_use |= h.prefer;
+    prefer_mask_ref(c, h.prefer, +1);
     node_ext_bits(c, h);
     auto ins = row_of.emplace(slot, (uint32_t)pos.size());
     const uint32_t row = ins.first->second;
@@ -1172,6 +1215,7 @@ ks_status ks_nodes_delete(ks_ctx *c, const uint32_t *slots, uint32_t n) {
       return c->fail(KS_ERR_NOT_FOUND, "slot %u not present", slots[i]);
     HostNode &h = c->nodes[slots[i]];
     c->name_slot.erase(h.name);
+    prefer_mask_ref(c, h.prefer, -1);
     h = HostNode();
     c->n_present--;
     pos[i] = c->slot_pos[slots[i]];

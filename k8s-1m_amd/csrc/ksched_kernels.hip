@@ -3,11 +3,11 @@
 // One scheduling ROUND evaluates a window of P pending pods against the node
 // snapshot and then commits them in queue order:
 //
-//   prescore  (only pods with an active normalising plugin) per-pod max raw
-//             TaintToleration / NodeAffinity score over feasible nodes
 //   sweep     Filter + Score of every (pod, node) pair; per pod and block the
 //             best BLOCK_KEYS packed keys plus a bound      -> BlockRec
 //   merge     per pod: blocks -> sorted candidate prefix    -> shard record
+//   [normalising plugins: RCCL all-reduce(max) of the measured maxima,
+//    norm_check, FIX-mode sweep + merge of the pods scored with a wrong guess]
 //   [RCCL all-gather of shard records across GPUs]
 //   merge_shards  per pod: shards -> final candidate prefix
 //   resolve   one workgroup walks the window in order; pod i's winner is the
@@ -386,52 +386,14 @@ __device__ __forceinline__ PodDev load_pod(const PodDev *pods, uint32_t i) {
   return pods[i];
 }
 
-// ================================================================= prescore
-// Per pod with PF_TT / PF_NA: max raw score over feasible nodes -> atomicMax.
-template <int NPL>
-__global__ __launch_bounds__(SWEEP_THREADS) void prescore_kernel(RoundArgs a) {
-  const uint32_t start = uniform_u32(*a.sstart);
-  const uint32_t sh = blockIdx.z;
-  const Shard s = a.shards[a.shard0 + sh];
-  const uint32_t kw = blockIdx.x * (SWEEP_THREADS / WAVE) + threadIdx.x / WAVE;  // kernel wave
-  if (kw >= s.waves * a.sub) return;
-  const uint32_t lane = threadIdx.x % WAVE;
-  const uint32_t lwave = kw / a.sub, j0 = (kw % a.sub) * NPL;  // layout wave / first step
-  const uint32_t p0 = start + blockIdx.y * a.pg;
-  const uint32_t p1 = min(min(p0 + a.pg, start + a.P), a.npods);
-  if (p0 >= p1) return;
-
-  NodeRegs nr[NPL];
-  NodeExt ne[NPL];
-  static_for<NPL>([&](auto J) {
-    constexpr int j = J;
-    const uint32_t l = (j0 + (uint32_t)j) * WAVE * s.waves + lane * s.waves + lwave;
-    const uint32_t pos = s.base + kw * WAVE * NPL + (uint32_t)j * WAVE + lane;
-    load_core(a.t, pos, s.lo + l, l < s.count, nr[j]);
-    load_ext(a.t, pos, nr[j].bits & 1u, ne[j]);
-  });
-  for (uint32_t pi = p0; pi < p1; ++pi) {
-    const PodDev p = load_pod(a.pods, pi);
-    if (!(p.flags & (PF_TT | PF_NA))) continue;
-    int64_t tmax = 0, nmax = 0;
-    static_for<NPL>([&](auto J) {
-      constexpr int j = J;
-      if (!(nr[j].bits & 1u)) return;
-      if (filter<true>(p, a.clauses, nr[j], ne[j]) != ST_FEASIBLE) return;
-      if (p.flags & PF_TT) tmax = max(tmax, taint_raw(p, ne[j]));
-      if (p.flags & PF_NA) nmax = max(nmax, preferred_raw(p, a.clauses, ne[j], nr[j].slot));
-    });
-    tmax = (int64_t)wave_max_u64((uint64_t)tmax);
-    nmax = (int64_t)wave_max_u64((uint64_t)nmax);
-    if (lane == 0) {
-      const uint32_t r = pi - start;
-      if (tmax) atomicMax(&a.norm_max[2 * r + 0], (uint32_t)tmax);
-      if (nmax) atomicMax(&a.norm_max[2 * r + 1], (uint32_t)nmax);
-    }
-  }
-}
-
 // =================================================================== sweep
+// Normalising plugins (TaintToleration with PreferNoSchedule taints, NodeAffinity
+// preferred terms) score against max raw over the feasible nodes, which is
+// only known after the sweep.  The sweep scores with the pod's guess of it
+// (PodDev::tt_guess / na_guess) and measures the true maxima on the way; the
+// merge reduces them and norm_check flags the pods whose guess was wrong,
+// which a second, FIX-mode launch re-sweeps with the measured maxima.  With a
+// right guess (the usual case) one pass over the nodes suffices.
 // grid: x = block within shard, y = pod group, z = local shard.
 constexpr uint32_t KEY32_POS_BITS = 9, KEY32_POS_MASK = (1u << KEY32_POS_BITS) - 1;
 
@@ -440,7 +402,9 @@ __global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
   static_assert(NPL * WAVE <= (1 << KEY32_POS_BITS), "wave-local key position field");
   constexpr int NW = SWEEP_THREADS / WAVE;
   __shared__ uint64_t s_keys[MAX_PG][NW][3];
-  __shared__ uint32_t s_cnt[MAX_PG][NW][NFILT + 3];
+  // per pod and wave: feasible, first failures per plugin, #at max (tt, na), max raw (tt, na)
+  constexpr int NCNT = NFILT + 5;
+  __shared__ uint32_t s_cnt[MAX_PG][NW][NCNT];
 
   const uint32_t start = uniform_u32(*a.sstart);
   const uint32_t sh = blockIdx.z;
@@ -453,6 +417,9 @@ __global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
   const uint32_t p0 = start + blockIdx.y * a.pg;
   const uint32_t p1 = min(min(p0 + a.pg, start + a.P), a.npods);
   if (p0 >= p1 || blockIdx.x * NW >= kwaves) return;
+  // FIX mode: only the pods norm_check flagged (pod groups of MAX_PG)
+  const bool fix = EXT && a.fix;
+  if (fix && uniform_u32(a.fix_group[blockIdx.y]) == 0) return;
 
   NodeRegs nr[NPL];
   NodeExt ne[EXT ? NPL : 1];
@@ -465,17 +432,19 @@ __global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
   });
 
   for (uint32_t pi = p0; pi < p1; ++pi) {
-    const PodDev p = load_pod(a.pods, pi);
     const uint32_t r = pi - start;
+    if (fix && uniform_u32(a.fix_flag[r]) == 0) continue;
+    const PodDev p = load_pod(a.pods, pi);
     int64_t tt_max = 0, na_max = 0;
     if (EXT && (p.flags & (PF_TT | PF_NA))) {
-      tt_max = a.norm_max[2 * r + 0];
-      na_max = a.norm_max[2 * r + 1];
+      tt_max = fix ? a.norm_max[2 * r + 0] : p.tt_guess;
+      na_max = fix ? a.norm_max[2 * r + 1] : p.na_guess;
     }
     // lane top-2 as (TotalScore + 1, step): steps run in slot order, so an
     // equal score never displaces an earlier step (lowest slot wins ties)
     uint32_t bs = 0, bj = 0, ss = 0, sj = 0;
     uint32_t feas = 0, f0 = 0, f1 = 0, f2 = 0, f3 = 0, f4 = 0, ttc = 0, nac = 0;
+    uint32_t tmx = 0, nmx = 0;  // max raw over this lane's feasible nodes
     static_for<NPL>([&](auto J) {
       constexpr int j = J;
       constexpr int je = EXT ? j : 0;
@@ -487,8 +456,16 @@ __global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
       const uint32_t tot = (uint32_t)total_score<EXT>(p, a.clauses, nr[j], ne[je], a.w, tt_max, na_max) + 1u;
       const uint32_t sc = feasible ? tot : 0u;
       bool at_tt = false, at_na = false;
-      if (EXT && (p.flags & PF_TT)) at_tt = feasible && taint_raw(p, ne[je]) == tt_max;
-      if (EXT && (p.flags & PF_NA)) at_na = feasible && preferred_raw(p, a.clauses, ne[je], nr[j].slot) == na_max;
+      if (EXT && (p.flags & PF_TT)) {
+        const uint32_t raw = (uint32_t)taint_raw(p, ne[je]);
+        at_tt = feasible && raw == (uint32_t)tt_max;
+        tmx = max(tmx, feasible ? raw : 0u);
+      }
+      if (EXT && (p.flags & PF_NA)) {
+        const uint32_t raw = (uint32_t)preferred_raw(p, a.clauses, ne[je], nr[j].slot);
+        at_na = feasible && raw == (uint32_t)na_max;
+        nmx = max(nmx, feasible ? raw : 0u);
+      }
       // running top-2 as value selects (a branchy form sinks into a scratch store)
       const bool gt1 = sc > bs, gt2 = sc > ss;
       ss = gt1 ? bs : (gt2 ? sc : ss);
@@ -509,6 +486,8 @@ __global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
         nac += popc_ballot(at_na);
       }
     });
+    if (EXT && (p.flags & PF_TT)) tmx = wave_max_u32_dpp(tmx);
+    if (EXT && (p.flags & PF_NA)) nmx = wave_max_u32_dpp(nmx);
     // Wave-local 32-bit keys (score + 1) << 9 | ~(step * 64 + lane): within a
     // wave slot order is (step, lane) order, so these sort like packed keys.
     const uint32_t best = bs ? (bs << KEY32_POS_BITS) | (KEY32_POS_MASK - (bj * WAVE + lane)) : 0u;
@@ -551,12 +530,15 @@ __global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
       s_cnt[pl][wid][5] = f4;
       s_cnt[pl][wid][6] = ttc;
       s_cnt[pl][wid][7] = nac;
+      s_cnt[pl][wid][8] = tmx;
+      s_cnt[pl][wid][9] = nmx;
     }
   }
   __syncthreads();
   // Block list per pod: top BLOCK_KEYS of the 4 wave lists above every bound.
   const uint32_t npl = p1 - p0;
   for (uint32_t pl = threadIdx.x; pl < npl; pl += blockDim.x) {
+    if (fix && a.fix_flag[p0 + pl - start] == 0) continue;
     uint64_t k[2 * NW];
     uint64_t bound = 0;
     const uint32_t nwaves = min((uint32_t)NW, kwaves - blockIdx.x * NW);
@@ -576,12 +558,18 @@ __global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
     for (int i = 0; i < BLOCK_KEYS; ++i) br.keys[i] = (i < (int)nk && k[i] > bound) ? k[i] : 0ull;
     br.bound = bound;
     uint32_t cnt[NFILT + 3] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (uint32_t w = 0; w < nwaves; ++w)
+    uint32_t tmx = 0, nmx = 0;
+    for (uint32_t w = 0; w < nwaves; ++w) {
       for (int q = 0; q < NFILT + 3; ++q) cnt[q] += s_cnt[pl][w][q];
+      tmx = max(tmx, s_cnt[pl][w][8]);
+      nmx = max(nmx, s_cnt[pl][w][9]);
+    }
     br.feasible = cnt[0];
     for (int q = 0; q < NFILT; ++q) br.fails[q] = cnt[1 + q];
     br.tt_cnt = cnt[6];
     br.na_cnt = cnt[7];
+    br.tt_max = tmx;
+    br.na_max = nmx;
     const uint32_t r = p0 + pl - start;
     a.brec[((size_t)sh * a.P + r) * a.bstride + blockIdx.x] = br;
   }
@@ -687,6 +675,7 @@ __global__ __launch_bounds__(256) void merge_kernel(RoundArgs a) {
   const uint32_t start = uniform_u32(*a.sstart);
   const uint32_t r = blockIdx.x;
   if (start + r >= a.npods || r >= a.P) return;
+  if (a.fix && a.fix_flag[r] == 0) return;  // FIX mode: re-merge the re-swept pods only
   const uint32_t sh = blockIdx.y;
   const Shard s = a.shards[a.shard0 + sh];
   const uint32_t nb = (s.waves * a.sub + 3) / 4;
@@ -694,23 +683,68 @@ __global__ __launch_bounds__(256) void merge_kernel(RoundArgs a) {
   uint64_t *out = a.srec + ((size_t)(a.shard0 + sh) * a.P + r) * rec_words(a.K);
   merge_lists(&br[0].keys[0], sizeof(BlockRec) / 8, &br[0].bound, sizeof(BlockRec) / 8, nb, BLOCK_KEYS, a.K,
               out, s_sort, s_scr, &s_cnt, s_u32);
-  // counts
+  // counts, and the normalising maxima measured by the sweep
   uint32_t c[NFILT + 3];
   for (int q = 0; q < NFILT + 3; ++q) c[q] = 0;
+  uint32_t tmx = 0, nmx = 0;
   for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) {
     c[0] += br[i].feasible;
     for (int q = 0; q < NFILT; ++q) c[1 + q] += br[i].fails[q];
     c[6] += br[i].tt_cnt;
     c[7] += br[i].na_cnt;
+    tmx = max(tmx, br[i].tt_max);
+    nmx = max(nmx, br[i].na_max);
   }
   for (int q = 0; q < NFILT + 3; ++q) c[q] = block_sum_u32(c[q], s_u32);
+  const bool stat = a.pstat != nullptr && !a.fix;
+  if (stat) {
+    tmx = (uint32_t)block_max_u64(tmx, s_scr);
+    nmx = (uint32_t)block_max_u64(nmx, s_scr);
+  }
   if (threadIdx.x == 0) {
     ShardRecHdr *h = (ShardRecHdr *)out;
     h->feasible = c[0];
     for (int q = 0; q < NFILT; ++q) h->fails[q] = c[1 + q];
     h->tt_cnt = c[6];
     h->na_cnt = c[7];
+    if (stat) {  // across local shards (atomics) and ranks (RCCL all-reduce max)
+      PodStat *ps = a.pstat + r;
+      if (tmx) atomicMax(&ps->tt_max, tmx);
+      if (nmx) atomicMax(&ps->na_max, nmx);
+      if (c[0]) atomicMax(&ps->any_feasible, 1u);
+    }
   }
+}
+
+// One block: per pod of the round, the normalising maxima the rest of the
+// round uses (measured when some node is feasible, else the guess, which is
+// then unused) and whether the sweep's guess was wrong (FIX flags, per pod
+// and per MAX_PG-pod group; counters[4] counts re-swept pods).
+__global__ __launch_bounds__(MAX_P) void norm_check_kernel(RoundArgs a) {
+  __shared__ uint32_t s_any[MAX_P / MAX_PG];
+  const uint32_t start = uniform_u32(*a.sstart);
+  const uint32_t r = threadIdx.x;
+  if (r < MAX_P / MAX_PG) s_any[r] = 0;
+  __syncthreads();
+  bool wrong = false;
+  if (r < a.P && start + r < a.npods) {
+    const PodDev &p = a.pods[start + r];
+    const PodStat st = a.pstat[r];
+    uint32_t tt = p.tt_guess, na = p.na_guess;
+    if (st.any_feasible) {
+      wrong = ((p.flags & PF_TT) && st.tt_max != tt) || ((p.flags & PF_NA) && st.na_max != na);
+      tt = st.tt_max;
+      na = st.na_max;
+    }
+    a.norm_max[2 * r] = tt;
+    a.norm_max[2 * r + 1] = na;
+    a.fix_flag[r] = wrong ? 1u : 0u;
+    if (wrong) atomicOr(&s_any[r / MAX_PG], 1u);
+  }
+  const uint32_t nw = popc_ballot(wrong);
+  if (nw && threadIdx.x % WAVE == 0) atomicAdd((unsigned long long *)&a.counters[4], (unsigned long long)nw);
+  __syncthreads();
+  if (r < MAX_P / MAX_PG) a.fix_group[r] = s_any[r];
 }
 
 // grid: x = pod in round.  Shard records -> final record.
@@ -1506,12 +1540,8 @@ __global__ void dump_scores_kernel(DumpArgs a) {
     if (e_ != hipSuccess) return e_;         \
   } while (0)
 
-hipError_t launch_prescore(const RoundArgs &a, uint32_t nblocks, uint32_t ngroups, uint32_t nshards,
-                           hipStream_t st) {
-  dim3 g(nblocks, ngroups, nshards);
-  if (a.npl == 2) prescore_kernel<2><<<g, SWEEP_THREADS, 0, st>>>(a);
-  else if (a.npl == 4) prescore_kernel<4><<<g, SWEEP_THREADS, 0, st>>>(a);
-  else prescore_kernel<8><<<g, SWEEP_THREADS, 0, st>>>(a);
+hipError_t launch_norm_check(const RoundArgs &a, hipStream_t st) {
+  norm_check_kernel<<<1, MAX_P, 0, st>>>(a);
   return hipGetLastError();
 }
 

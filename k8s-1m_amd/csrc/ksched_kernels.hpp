@@ -16,7 +16,7 @@ struct RoundArgs {
   const Shard *shards;        // geometry of every shard, device memory (global ids)
   uint32_t total_shards;      // S
   uint32_t shard0;            // first global shard handled by this launch (grid.z / grid.y)
-  uint32_t npl;               // nodes per lane of the sweep / prescore kernel
+  uint32_t npl;               // nodes per lane of the sweep kernel
   uint32_t sub;               // layout nodes-per-lane / kernel nodes-per-lane
   uint32_t P;                 // pods per round
   uint32_t pg;                // pods per sweep block
@@ -39,7 +39,11 @@ struct RoundArgs {
   CarryRec *carry_out;        // nodes this round's resolve modifies
   uint32_t *carry_out_n;
   uint32_t first;             // first round of a pipeline run (no previous round)
-  uint32_t *norm_max;         // [P][2] max raw TaintToleration / NodeAffinity (atomicMax, all shards)
+  uint32_t *norm_max;         // [P][2] max raw TaintToleration / NodeAffinity over feasible nodes (norm_check)
+  PodStat *pstat;             // [P] measured maxima (merge, all shards); nullptr: no normalising pod
+  uint32_t *fix_flag;         // [P] the pod's guessed maxima were wrong: re-swept in FIX mode
+  uint32_t *fix_group;        // [P / MAX_PG] any flagged pod in the group
+  uint32_t fix;               // FIX-mode launch of sweep / merge
   BlockRec *brec;             // [local shards][P][bstride]
   uint64_t *srec;             // [S][P][rec_words(K)]
   uint64_t *frec;             // [P][rec_words(K)] (== srec when S == 1)
@@ -62,8 +66,7 @@ struct DumpArgs {
   Weights w;
 };
 
-hipError_t launch_prescore(const RoundArgs &a, uint32_t nblocks, uint32_t ngroups, uint32_t nshards,
-                           hipStream_t st);
+hipError_t launch_norm_check(const RoundArgs &a, hipStream_t st);
 hipError_t launch_sweep(const RoundArgs &a, bool ext, uint32_t nblocks, uint32_t ngroups, uint32_t nshards,
                         hipStream_t st);
 hipError_t launch_merge(const RoundArgs &a, uint32_t nshards, hipStream_t st);

@@ -71,6 +71,31 @@ def prefer_taints_normalize():
 
 
 @scenario
+def normalizer_guess_wrong():
+    # The sweep scores normalising plugins with a guessed max raw (the worst
+    # prefer-taint word present / the sum of preferred weights); here the node
+    # carrying the worst word is infeasible and the preferred terms exclude
+    # each other, so the measured max differs and the pods are re-swept.
+    p = lambda k: Taint(k, "true", "PreferNoSchedule")  # noqa: E731
+    T = lambda *reqs: Term(list(reqs))  # noqa: E731
+    nodes = [node("two", taints=[p("s"), p("t"), Taint("h", "", "NoSchedule")], labels={"zone": "z0"}),
+             node("one", taints=[p("s")], labels={"zone": "z1"}), node("zero", labels={"zone": "z2"}),
+             node("full", pods=0, taints=[p("s"), p("t")])]
+    pods = [
+        pod("x", cpu=1000, mem=Gi),                                               # guess 2, max 1 -> zero
+        pod("tol-h", cpu=1000, mem=Gi, tolerations=[Toleration("h", "Exists", "", "NoSchedule")]),  # max 2
+        pod("pref", cpu=1000, mem=Gi, tolerations=[Toleration("s", "Exists", "", "PreferNoSchedule")],
+            preferred=[Pref(10, T(Req("zone", "In", ["z1"]))), Pref(20, T(Req("zone", "In", ["z2"])))]),
+        pod("pref-one-feasible", cpu=1000, mem=Gi, node_selector={"zone": "z1"},
+            preferred=[Pref(10, T(Req("zone", "In", ["z1"]))), Pref(20, T(Req("zone", "In", ["z2"])))]),
+        pod("none-feasible", cpu=10 ** 9, mem=Gi),
+    ]
+    exp = [dict(node=2, feasible=2), dict(node=2, feasible=3), dict(node=2, feasible=2),
+           dict(node=1, feasible=1, single=True), dict(status=1, node=None, feasible=0)]
+    return nodes, pods, exp
+
+
+@scenario
 def unschedulable_nodes():
     nodes = [node("cordoned", unschedulable=True), node("ok")]
     pods = [pod("x"), pod("tol", tolerations=[Toleration("node.kubernetes.io/unschedulable", "Exists", "",

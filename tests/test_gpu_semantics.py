@@ -79,3 +79,24 @@ def test_upsert_rejects_duplicate_names_atomically():
         same, _ = nodes_array([node("a", cpu=1000)], a)  # an update keeps the name on its slot
         assert s.lib.ks_nodes_upsert(s.ctx, same, (C.c_uint32 * 1)(0), 1) == 0
         assert s.node_states([0])[0].alloc_milli_cpu == 1000
+
+
+def test_wrong_normaliser_guess_is_reswept():
+    # normalizer_guess_wrong: pods x, pref and pref-one-feasible are scored with a
+    # wrong guessed max first; the FIX-mode sweep must run for exactly those
+    nodes, pods, exp = SCENARIOS["normalizer_guess_wrong"]()
+    a = Arena()
+    na, n = nodes_array(nodes, a)
+    pa, m = pods_array(pods, a)
+    slots = (C.c_uint32 * n)(*range(n))
+    o = pyoracle.Oracle(n)
+    o.upsert(na, slots, n)
+    want = o.schedule(pa, m)
+    with Scheduler(n) as s:
+        s.upsert_nodes_raw(na, slots, n)
+        got = s.schedule_raw(pa, m)
+        dbg = (C.c_uint64 * 16)()
+        assert s.lib.ks_debug_counters(s.ctx, dbg) == 0
+    assert_results_equal(got, want, m, "normalizer_guess_wrong")
+    check(res_array(got, m), exp)
+    assert dbg[4] == 3, list(dbg)
