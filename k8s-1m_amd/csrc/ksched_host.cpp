@@ -1039,7 +1039,9 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
   x->brec_bytes = (size_t)nloc * x->P * bmax * sizeof(BlockRec);
   if ((st = dalloc(x, (uint8_t **)&x->d_brec, x->brec_bytes))) return st;
   const size_t recs = (size_t)x->S * x->P * rec_words(x->K);  // per round parity
-  if ((st = dalloc(x, &x->d_srec, 2 * recs)) || (st = dalloc(x, &x->d_frec, 2 * (size_t)x->P * rec_words(x->K))) ||
+  // +2 words: the resolve's 16-byte key DMA may read 8 bytes past the last record
+  if ((st = dalloc(x, &x->d_srec, 2 * recs + 2)) ||
+      (st = dalloc(x, &x->d_frec, 2 * (size_t)x->P * rec_words(x->K) + 2)) ||
       (st = dalloc(x, &x->d_crow, 2 * (size_t)x->P * x->K)) || (st = dalloc(x, &x->d_cext, 2 * (size_t)x->P * x->K)))
     return st;
   if ((st = xfer_sync(x))) return st;  // all initialisation is stream-ordered

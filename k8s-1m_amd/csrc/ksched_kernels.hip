@@ -1037,44 +1037,123 @@ __global__ __launch_bounds__(PATCH_THREADS) void patch_kernel(RoundArgs a) {
 // The patched lists are exact for the round's start state, so pod i's winner is
 // the best of (a) its first listed candidate that no pod < i modified (its key
 // is unchanged: same row, same normalisation max) and (b) every node a pod < i
-// modified, re-scored against its live row.  If neither is provably the
-// maximum (every listed candidate modified and the best modified key not above
-// the list bound), or a normalising plugin's max may have moved, the round
-// ends before pod i and the next sweep restarts there.
+// modified (the set M_i), re-scored against its live row.  If neither is
+// provably the maximum (every listed candidate modified and the best modified
+// key not above the list bound), or a normalising plugin's max may have moved,
+// the round ends before pod i and the next sweep restarts there.
 //
-// Latency design: pod descriptors / record headers of the round are staged in
-// LDS; the next pod's candidate keys and rows are prefetched into registers
-// while the current pod resolves; list threads (waves 0-3) hold one listed
-// candidate each, rescoring threads (waves 4-7) one modified node each, in
-// registers (the node that joins the modified set is handed over through LDS);
-// every thread recomputes the decision from the per-wave partials, so each
-// pod costs two barriers.
-constexpr int RESOLVE_THREADS = 512;
-constexpr int RNW = RESOLVE_THREADS / WAVE;
+// Software pipeline, one barrier per pod.  M_{i+1} = M_i + {w_i} and pod i
+// changes the state of its winner w_i only, so everything pod i+1 needs except
+// w_i's new values is computed while pod i is being decided:
+//   list waves  (0-3)  pod i+3's first four listed candidates not in M_i; at
+//                      most three of them (w_i .. w_{i+2}) are modified by pod
+//                      i+3.  Keys and the chosen rows move global -> LDS by
+//                      LDS-DMA (global_load_lds) issued three iterations before
+//                      they are read, so the loop never waits on global memory
+//                      (the next round's sweep keeps the caches cold)
+//   owner waves (4-7)  one node of M_i per thread (its state lives in LDS):
+//                      its key for pod i+1 and its filter-status change since
+//                      the round start; per wave the best two keys and the
+//                      summed status changes
+//   eval wave   (8)    every node that can win pod i (the candidates above and
+//                      w_{i-1}) committed: its key and status change for pod
+//                      i+1, speculatively, one candidate per lane
+//   decider     (9)    pod i from those partials, with the entries of the last
+//                      winners replaced by the eval wave's values for w_{i-1}
+// The per-pod critical path is the decider's LDS round trip, a few wave
+// reductions and the decision; re-scoring runs beside it on the other waves.
+constexpr int RES_LIST_WAVES = 4;
+constexpr int RES_OWN_WAVES = 4;
+constexpr int RES_EVAL_WAVE = RES_LIST_WAVES + RES_OWN_WAVES;
+constexpr int RES_DEC_WAVE = RES_EVAL_WAVE + 1;
+constexpr int RESOLVE_THREADS = (RES_DEC_WAVE + 1) * WAVE;
 constexpr int RHASH = 1024;
-constexpr int RES_LIST_THREADS = RESOLVE_THREADS / 2;
-static_assert(RES_LIST_THREADS >= MAX_K && RESOLVE_THREADS - RES_LIST_THREADS >= MAX_P, "resolve roles");
+constexpr int LSEL = 4;                                   // listed candidates kept per list wave
+constexpr int LAHEAD = 3;                                 // list waves select pod i + LAHEAD in iteration i
+constexpr int KAHEAD = 3;                                 // ... with keys fetched LAHEAD iterations before
+constexpr int KSLOTS = 8, RSLOTS = 4;                     // key / row staging slots (by pod mod)
+static_assert(LSEL > LAHEAD, "a selection LAHEAD pods ahead must survive the LAHEAD commits before it is used");
+typedef __attribute__((address_space(1))) void gvoid_t;  // global_load_lds operands
+typedef __attribute__((address_space(3))) void lvoid_t;
+static_assert(KSLOTS >= LAHEAD + KAHEAD + 1 && RSLOTS >= LAHEAD + 1, "staging depth");
+constexpr int NCAND_OWN = 2 * RES_OWN_WAVES;              // lanes [0, 8): owner waves' best two
+constexpr int NCAND_LIST = LSEL * RES_LIST_WAVES;         // lanes [8, 24): list waves' first four
+constexpr int CAND_PREV = NCAND_OWN + NCAND_LIST;         // lane 24: the previous pod's winner
+constexpr int NCAND = CAND_PREV + 1;
+constexpr int DSUM_LANE = 32;                             // decider lanes summing status changes
+constexpr uint32_t NONE32 = 0xFFFFFFFFu;
+static_assert(RES_LIST_WAVES * WAVE >= MAX_K && RES_OWN_WAVES * WAVE >= MAX_P, "resolve roles");
+static_assert(DSUM_LANE >= NCAND && DSUM_LANE + NFILT + 3 <= WAVE, "decider lanes");
+
+// A node as the resolve carries it: allocatable, the round-start filter inputs
+// (the listed row), the live state and the reciprocals.
+struct alignas(16) RNode {
+  int64_t acpu, amem;
+  int64_t rc0, rm0;        // Requested at the round start
+  int64_t rc, rm, zc, zm;  // live Requested / NonZeroRequested
+  double inv_cpu, inv_mem;
+  int32_t apods, np0, np;
+  uint32_t slot, pos, _pad;
+};
+
+__device__ __forceinline__ NodeRegs rnode_regs(const RNode &n) {
+  return make_regs_inv(n.acpu, n.amem, n.rc, n.rm, n.zc, n.zm, n.apods, n.np, n.slot, n.inv_cpu, n.inv_mem);
+}
+
+// the node with its round-start Requested / pod count (only the filter reads these)
+__device__ __forceinline__ NodeRegs rnode_regs0(const RNode &n, const NodeRegs &live) {
+  NodeRegs r = live;
+  r.free_cpu = (double)(n.acpu - n.rc0);
+  r.free_mem = (double)(n.amem - n.rm0);
+  r.bits = (live.bits & ~2u) | ((int64_t)n.np0 + 1 <= (int64_t)n.apods ? 2u : 0u);
+  return r;
+}
+
+__device__ __forceinline__ RNode rnode_from_row(const CandRow &w, uint32_t slot) {
+  RNode n;
+  n.acpu = w.acpu;
+  n.amem = w.amem;
+  n.rc0 = n.rc = w.rc;
+  n.rm0 = n.rm = w.rm;
+  n.zc = w.zc;
+  n.zm = w.zm;
+  n.inv_cpu = w.inv_cpu;
+  n.inv_mem = w.inv_mem;
+  n.apods = w.apods;
+  n.np0 = n.np = w.np;
+  n.slot = slot;
+  n.pos = w.pos;
+  n._pad = 0;
+  return n;
+}
+
+// NodeInfo.AddPod on the live state (AssumePod)
+__device__ __forceinline__ void rnode_add(RNode &n, const PodDev &p) {
+  n.rc += p.req_cpu;
+  n.rm += p.req_mem;
+  n.zc += p.nz_cpu;
+  n.zm += p.nz_mem;
+  n.np += 1;
+}
 
 // Workgroup barrier for LDS hand-offs only: __syncthreads() also drains vmcnt,
-// which would expose the next pod's prefetch latency on every iteration.
+// which would expose the list prefetch latency on every iteration.
 __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-// Diagnostic build (-DKS_STAMPS): wave 0 accumulates s_memtime per phase into
-// a.counters[8..15]; never compiled into the measured library.
+__device__ __forceinline__ uint32_t wave_min_u32_dpp(uint32_t v) { return ~wave_max_u32_dpp(~v); }
+
+// Diagnostic build (-DKS_STAMPS): the first lane of the decider, eval, first
+// owner and first list wave accumulate s_memtime of their work and of their
+// barrier wait into a.counters[8..15]; never compiled into the measured library.
 #ifdef KS_STAMPS
-#define STAMP(i)                                                                         \
-  do {                                                                                   \
-    __builtin_amdgcn_sched_barrier(0);                                                   \
-    uint64_t t_;                                                                         \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");            \
-    __builtin_amdgcn_sched_barrier(0);                                                   \
-    if (tid == STAMP_TID) { stamp_acc[i] += t_ - stamp_last; }                           \
-    stamp_last = t_;                                                                     \
+#define STAMP_NOW(t_)                                                         \
+  do {                                                                        \
+    __builtin_amdgcn_sched_barrier(0);                                        \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+    __builtin_amdgcn_sched_barrier(0);                                        \
   } while (0)
-#else
-#define STAMP(i) do {} while (0)
 #endif
 
 template <bool EXT>
@@ -1082,16 +1161,32 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
   __shared__ PodDev s_pod[MAX_P];
   __shared__ ShardRecHdr s_hdr[MAX_P];
   __shared__ uint32_t s_norm[MAX_P][2];
-  __shared__ uint32_t s_hkey[RHASH];   // slots modified this round (+1), linear probing
-  __shared__ CandRow s_new;            // row of the node joining the modified set
-  __shared__ CandExt s_newx;
-  // per-wave partials (entries of waves that had no work keep identities)
-  __shared__ uint64_t s_wkey[RNW];     // best modified key
-  __shared__ uint32_t s_widx[RNW];     // first unmodified list index
-  __shared__ uint64_t s_wlk[RNW];      // its key
-  __shared__ int32_t s_wd[RNW][NFILT + 3];
-  __shared__ uint32_t s_wany[RNW];
-  __shared__ uint32_t s_stop;
+  __shared__ uint32_t s_hkey[RHASH];  // slots modified this round (+1), linear probing
+  // the modified nodes (owner thread m owns entry m)
+  __shared__ RNode s_mod[MAX_P];
+  __shared__ CandExt s_modx[EXT ? MAX_P : 1];
+  // owner waves' partials for pod i (written in iteration i-1), by parity of i
+  __shared__ uint64_t s_okey[2][NCAND_OWN];  // best two keys per wave, 0 = none
+  __shared__ uint32_t s_oidx[2][NCAND_OWN];  // their owner indices
+  __shared__ int32_t s_dsum[2][RES_OWN_WAVES][NFILT + 3];
+  // list staging (LDS-DMA targets): listed keys by pod mod KSLOTS; the chosen
+  // rows by pod mod RSLOTS as [list wave][16-byte piece][candidate]
+  constexpr int RPIECES = (sizeof(CandRow) + (EXT ? sizeof(CandExt) : 0)) / 16;
+  __shared__ uint64_t s_keys[KSLOTS][MAX_K];
+  __shared__ uint4 s_lrowb[RSLOTS][RES_LIST_WAVES][RPIECES][LSEL];
+  // list waves' candidates for pod i (chosen in iteration i - LAHEAD), by i mod RSLOTS
+  __shared__ uint64_t s_lkey[RSLOTS][NCAND_LIST];
+  __shared__ uint32_t s_lidx[RSLOTS][NCAND_LIST];  // list index, NONE32 = none
+  // eval wave: each candidate of pod i committed, for pod i+1 (by parity of i)
+  __shared__ RNode s_post[2][NCAND];
+  __shared__ CandExt s_postx[EXT ? 2 : 1][EXT ? NCAND : 1];
+  __shared__ uint64_t s_ekey[2][NCAND];
+  __shared__ int32_t s_edd[2][NCAND][NFILT + 3];
+  // decider -> everyone: pod i's commit {valid, candidate lane, joins, owner index}
+  __shared__ uint32_t s_pend[2][4];
+  __shared__ uint32_t s_done, s_stop_at;
+  // results of the round, written out after the loop (no global stores inside it)
+  __shared__ DevResult s_res[MAX_P];
 
   const uint32_t tid = threadIdx.x, lane = tid % WAVE, wid = tid / WAVE;
   const uint32_t start = uniform_u32(*a.act);
@@ -1108,8 +1203,10 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
   }
   const uint32_t nround = min(a.P, a.npods - start);
   const uint32_t RW = rec_words(a.K);
-  const bool list_role = tid < RES_LIST_THREADS;
-  const uint32_t mj = tid - RES_LIST_THREADS;  // rescoring role: owned modified node
+  const bool is_list = wid < RES_LIST_WAVES;
+  const bool is_owner = wid >= RES_LIST_WAVES && wid < RES_EVAL_WAVE;
+  const uint32_t ow = wid - RES_LIST_WAVES;         // owner wave
+  const uint32_t mj = tid - RES_LIST_WAVES * WAVE;  // owner thread: owned modified node
   // ---- stage the round
   for (uint32_t i = tid; i < RHASH; i += RESOLVE_THREADS) s_hkey[i] = 0;
   for (uint32_t i = tid; i < nround; i += RESOLVE_THREADS) {
@@ -1118,272 +1215,441 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
     s_norm[i][0] = a.norm_max[2 * i];
     s_norm[i][1] = a.norm_max[2 * i + 1];
   }
-  if (tid < RNW) {
-    s_wkey[tid] = 0;
-    s_widx[tid] = 0xFFFFFFFFu;
-    s_wlk[tid] = 0;
-    s_wany[tid] = 0;
+  if (tid == 0) {
+    s_pend[1][0] = 0;  // "pod -1" committed nothing
+    s_done = 0;
   }
-  if (tid == 0) s_stop = nround;
-  // prefetch pod 0's candidates (list thread t holds entry t, its key and row):
-  // independent loads of the gathered candidate rows, consumed one pod later
-  uint64_t ck = 0;
-  CandRow crow{};
-  CandExt cext{};
-  auto prefetch = [&](uint32_t r, uint64_t &k, CandRow &w, CandExt &x) {
-    const bool on = r < nround && tid < a.K && list_role;
-    const uint32_t rr = on ? r : 0, tt = on ? tid : 0;
-    k = a.frec[(size_t)rr * RW + REC_HDR_WORDS + tt];
-    w = a.crow[(size_t)rr * a.K + tt];
-    if (EXT) x = a.cext[(size_t)rr * a.K + tt];
-    if (!on) k = 0;
+
+  // ---- list waves (LDS-DMA pipeline).  Per iteration a list wave issues
+  // LIST_DMA global_load_lds instructions (the chosen rows' pieces, one key
+  // block) and, before the barrier, waits until those of two iterations ago
+  // have landed; every LDS read of a DMA target in this wave is inline asm,
+  // which hipcc does not tie to the DMA (it would drain the pipeline).
+  constexpr uint32_t LIST_DMA = RPIECES + 1;
+  constexpr int32_t LIST_WAIT = 2 * LIST_DMA;  // vmcnt(N): expcnt / lgkmcnt fields at their max
+  static_assert(LIST_WAIT < 64, "vmcnt field");
+  const uint32_t lw = wid;
+  auto dma_keys = [&](uint32_t pod) {  // keys of list entries [64 lw, 64 lw + 64) of pod -> s_keys
+    const uint32_t p = min(pod, nround - 1);
+    if (lane < 32) {  // entries past K: any in-record address (never read back)
+      const uint32_t e = 64 * lw + 2 * lane;
+      const uint64_t *src = a.frec + (size_t)p * RW + REC_HDR_WORDS + (e < a.K ? e : 0u);
+      __builtin_amdgcn_global_load_lds((gvoid_t *)src, (lvoid_t *)&s_keys[pod % KSLOTS][64 * lw], 16, 0, 0);
+    }
   };
-  prefetch(0, ck, crow, cext);
-  // rescoring role state: modified node mj, in registers
-  bool mine = false;
-  NodeRegs mr{};             // live row
-  double m_f0c = 0, m_f0m = 0;  // round-start free cpu / memory (filter of the listed row)
-  uint32_t m_bits0 = 0;
-  NodeExt me{};
-  int64_t m_acpu = 0, m_amem = 0, m_rc0 = 0, m_rm0 = 0, m_rc = 0, m_rm = 0, m_zc = 0, m_zm = 0;
-  int32_t m_apods = 0, m_np0 = 0, m_np = 0;
-  uint32_t m_pos = 0;
-  uint32_t nmod = 0;  // uniform
+  auto lds_key = [&](uint32_t slot, uint32_t t) -> uint64_t {
+    uint64_t v;
+    const uint32_t addr = (uint32_t)(uintptr_t)(lvoid_t *)&s_keys[slot][t];
+    asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(addr) : "memory");
+    return v;
+  };
+  // pod's first LSEL entries (per list wave) not in the modified-slot hash:
+  // keys / indices to s_lkey / s_lidx, rows by DMA
+  auto list_select = [&](uint32_t pod) {
+    const bool real = pod < nround;
+    const uint32_t p = real ? pod : nround - 1;
+    const uint64_t k = lds_key(pod % KSLOTS, tid);
+    const uint32_t nk = s_hdr[p].nkeys;
+    bool unmod = false;
+    const uint32_t slot = 0xFFFFFFFFu - (uint32_t)k;
+    if (real && k != 0 && tid < nk) {
+      uint32_t h = rhash(slot);
+      unmod = true;
+      while (s_hkey[h] != 0) {
+        if (s_hkey[h] == slot + 1) { unmod = false; break; }
+        h = (h + 1) & (RHASH - 1);
+      }
+    }
+    const uint64_t ub = __ballot(unmod);
+    const uint32_t nsel = min((uint32_t)__popcll(ub), (uint32_t)LSEL);
+    // lane c < LSEL takes the c-th unmodified entry
+    uint64_t m = ub;
+    for (uint32_t j = 0; j < lane && j < (uint32_t)LSEL; ++j) m &= m - 1;
+    const uint32_t te = m ? (uint32_t)__builtin_ctzll(m) : 0u;
+    const uint64_t tk = (uint64_t)__shfl((long long)k, (int)te, WAVE);
+    if (lane < (uint32_t)LSEL) {
+      const uint32_t t = 64 * lw + te;
+      const uint4 *row = (const uint4 *)(a.crow + (size_t)p * a.K + (lane < nsel ? t : 0u));
+#pragma unroll
+      for (int j = 0; j < (int)(sizeof(CandRow) / 16); ++j)
+        __builtin_amdgcn_global_load_lds((gvoid_t *)(row + j), (lvoid_t *)&s_lrowb[pod % RSLOTS][lw][j][0], 16, 0, 0);
+      if constexpr (EXT) {
+        const uint4 *x = (const uint4 *)(a.cext + (size_t)p * a.K + (lane < nsel ? t : 0u));
+#pragma unroll
+        for (int j = 0; j < (int)(sizeof(CandExt) / 16); ++j)
+          __builtin_amdgcn_global_load_lds((gvoid_t *)(x + j),
+                                           (lvoid_t *)&s_lrowb[pod % RSLOTS][lw][sizeof(CandRow) / 16 + j][0], 16, 0,
+                                           0);
+      }
+      if (real) {
+        s_lkey[pod % RSLOTS][LSEL * lw + lane] = lane < nsel ? tk : 0ull;
+        s_lidx[pod % RSLOTS][LSEL * lw + lane] = lane < nsel ? t : NONE32;
+      }
+    }
+  };
+  auto list_wait = [&]() {  // DMA of two iterations ago landed
+    __builtin_amdgcn_s_waitcnt((LIST_WAIT & 0xF) | ((LIST_WAIT >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+  };
+  __syncthreads();  // staged headers, cleared hash
+  if (is_list) {
+    // prologue: keys of pods [0, LAHEAD + KAHEAD), then pods [0, LAHEAD) selected (nothing modified yet)
+    for (uint32_t p = 0; p < (uint32_t)(LAHEAD + KAHEAD); ++p) dma_keys(p);
+    __builtin_amdgcn_s_waitcnt(0);
+    for (uint32_t p = 0; p < (uint32_t)LAHEAD; ++p) list_select(p);
+    __builtin_amdgcn_s_waitcnt(0);
+  }
   __syncthreads();
+  if (is_owner && lane == 0) {
+    s_okey[0][2 * ow] = s_okey[0][2 * ow + 1] = 0;
+    for (int q = 0; q < NFILT + 3; ++q) s_dsum[0][ow][q] = 0;
+  }
+
+  // owner thread: does it own modified node mj
+  bool mine = false;
+  // decider state (wave-uniform): the last two commits, modified count, stop point
+  uint32_t pvalid = 0, pcand = 0, pslot = NONE32, p2slot = NONE32, p3slot = NONE32, powner = 0, nmod = 0,
+           stop_at = nround;
+  // the decider is the per-pod critical path, the eval wave next: issue priority
+  if (wid == RES_DEC_WAVE) __builtin_amdgcn_s_setprio(3);
+  else if (wid == RES_EVAL_WAVE) __builtin_amdgcn_s_setprio(2);
 #ifdef KS_STAMPS
-  constexpr uint32_t STAMP_TID = KS_STAMPS;
-  uint64_t stamp_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, stamp_last = 0;
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(stamp_last)::"memory");
+  const bool stamper = lane == 0 && (wid == RES_DEC_WAVE || wid == RES_EVAL_WAVE);
+  const uint32_t sidx = wid == RES_DEC_WAVE ? 0 : 2;
+  uint64_t st_work = 0, st_wait = 0, t0, t1, t2, ts, sub[4] = {0, 0, 0, 0};
 #endif
+  lds_barrier();
 
-  for (uint32_t r = 0; r < nround; ++r) {
-    STAMP(0);
-    const PodDev p = s_pod[r];
-    const ShardRecHdr hdr = s_hdr[r];
-    const uint32_t pi = start + r;
-    int64_t tt_max = 0, na_max = 0;
-    if (EXT) {
-      tt_max = s_norm[r][0];
-      na_max = s_norm[r][1];
-    }
-    // next pod's candidates: issued now, consumed next iteration
-    uint64_t nk;
-    CandRow nrow;
-    CandExt next_ext;
-    prefetch(r + 1, nk, nrow, next_ext);
-
-    if (list_role) {
-      // (a) is my listed candidate unmodified by the pods before this one?
-      bool unmod = false;
-      if (ck != 0 && tid < hdr.nkeys) {
-        const uint32_t slot = 0xFFFFFFFFu - (uint32_t)ck;
-        uint32_t h = rhash(slot);
-        unmod = true;
-        while (s_hkey[h] != 0) {
-          if (s_hkey[h] == slot + 1) { unmod = false; break; }
-          h = (h + 1) & (RHASH - 1);
+  auto iteration = [&](uint32_t r) -> bool {
+    const uint32_t buf = r & 1u, nb = buf ^ 1u;
+#ifdef KS_STAMPS
+    STAMP_NOW(t0);
+#endif
+    if (wid == RES_DEC_WAVE) {
+      // ------------------------------------------------------------- decider
+      if (r >= nround) {
+        if (lane == 0) {
+          s_pend[buf][0] = 0;
+          s_done = 1;
         }
-      }
-      STAMP(1);
-      const uint64_t ub = __ballot(unmod);
-      if (lane == 0) {
-        if (ub) {
-          const uint32_t first = (uint32_t)__builtin_ctzll(ub);
-          s_widx[wid] = wid * WAVE + first;
-          s_wlk[wid] = readlane64(ck, (int)first);
+      } else {
+        const uint32_t b4 = r % RSLOTS;
+        const uint32_t pflags = uniform_u32(s_pod[r].flags);
+        // lanes 0-7: owner candidates, 8-23: listed candidates, 24: the previous
+        // winner committed; lanes 32-39: status-change sums per count
+        uint64_t vkey = 0;
+        uint32_t vslot = NONE32, vidx = NONE32;
+        int32_t vd = 0;
+        if (lane < (uint32_t)NCAND_OWN) {
+          vkey = s_okey[buf][lane];
+          vidx = s_oidx[buf][lane];
+          vslot = vkey ? s_mod[vidx].slot : NONE32;
+        } else if (lane < (uint32_t)CAND_PREV) {
+          vkey = s_lkey[b4][lane - NCAND_OWN];
+          vidx = s_lidx[b4][lane - NCAND_OWN];
+          vslot = 0xFFFFFFFFu - (uint32_t)vkey;
+        } else if (lane == (uint32_t)CAND_PREV) {
+          if (pvalid) {
+            vkey = s_ekey[nb][pcand];
+            vslot = pslot;
+          }
+        } else if (lane >= (uint32_t)DSUM_LANE && lane < (uint32_t)DSUM_LANE + NFILT + 3) {
+          const uint32_t q = lane - DSUM_LANE;
+#pragma unroll
+          for (int w = 0; w < RES_OWN_WAVES; ++w) vd += s_dsum[buf][w][q];
+          if (pvalid) vd += s_edd[nb][pcand][q];
+        }
+        const ShardRecHdr &hd = s_hdr[r];
+#ifdef KS_STAMPS
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        STAMP_NOW(ts);
+        sub[0] += ts - t0;
+        t2 = ts;
+#endif
+        const uint32_t h_feasible = uniform_u32(hd.feasible);
+        const uint32_t h_tt = uniform_u32(hd.tt_cnt), h_na = uniform_u32(hd.na_cnt);
+        const uint64_t h_bound = ((uint64_t)uniform_u32((uint32_t)(hd.bound >> 32)) << 32) |
+                                 uniform_u32((uint32_t)hd.bound);
+        // entries computed before the last winners' commits are stale: drop them
+        const bool is_own = lane < (uint32_t)NCAND_OWN;
+        const bool is_lst = lane >= (uint32_t)NCAND_OWN && lane < (uint32_t)CAND_PREV;
+        const uint64_t mk = ((is_own && vkey && vslot != pslot) || lane == (uint32_t)CAND_PREV) ? vkey : 0ull;
+        const uint64_t bm = wave_max_u64_dpp(mk);
+        const bool lok = is_lst && vidx != NONE32 && vslot != pslot && vslot != p2slot && vslot != p3slot;
+        const uint32_t fu = wave_min_u32_dpp(lok ? vidx : NONE32);
+        uint64_t ku = 0;
+        uint32_t ulane = 0;
+        if (fu != NONE32) {
+          ulane = (uint32_t)__builtin_ctzll(__ballot(lok && vidx == fu));
+          ku = readlane64(vkey, (int)ulane);
+        }
+        int32_t sum[NFILT + 3];
+#pragma unroll
+        for (int q = 0; q < NFILT + 3; ++q) sum[q] = __builtin_amdgcn_readlane(vd, DSUM_LANE + q);
+        const uint32_t feasible = h_feasible - (uint32_t)sum[0];
+#ifdef KS_STAMPS
+        STAMP_NOW(ts);
+        sub[1] += ts - t2;
+        t2 = ts;
+#endif
+        int32_t status = 0;
+        bool stop = false;
+        uint64_t win = 0;
+        if (feasible == 0) {
+          status = 1;  // KS_POD_UNSCHEDULABLE
+        } else if ((pflags & PF_PREF_ERR) && feasible >= 2) {
+          status = 2;  // KS_POD_ERROR (NodeAffinity PreScore)
+        } else if ((EXT && (pflags & PF_TT) && h_tt - (uint32_t)sum[6] == 0) ||
+                   (EXT && (pflags & PF_NA) && h_na - (uint32_t)sum[7] == 0)) {
+          stop = true;  // a normaliser's max may have moved: re-sweep from this pod
+        } else if (fu != NONE32) {
+          win = ku > bm ? ku : bm;
+        } else if (bm > h_bound) {
+          win = bm;
         } else {
-          s_widx[wid] = 0xFFFFFFFFu;
+          stop = true;  // candidates exhausted
+        }
+        if (stop) {
+          stop_at = r;
+          if (lane == 0) {
+            s_pend[buf][0] = 0;
+            s_done = 1;
+          }
+        } else {
+          if (lane == 0) {
+            DevResult *res = &s_res[r];
+            res->node_index = win ? (int32_t)(0xFFFFFFFFu - (uint32_t)win) : -1;
+            res->status = status;
+            res->total_score = win ? (int64_t)(win >> 32) - 1 : 0;
+            res->feasible_nodes = feasible;
+            res->evaluated_nodes = a.evaluated;
+#pragma unroll
+            for (int q = 0; q < NFILT; ++q) res->fail_counts[q] = hd.fails[q] + (uint32_t)sum[1 + q];
+            res->flags = (win && feasible == 1) ? 1u : 0u;
+          }
+#ifdef KS_STAMPS
+          STAMP_NOW(ts);
+          sub[2] += ts - t2;
+          t2 = ts;
+#endif
+          // commit (AssumePod -> NodeInfo.AddPod): the eval wave holds the
+          // committed state of every candidate; record which one won
+          uint32_t cand = 0, join = 0, oidx = 0;
+          p3slot = p2slot;
+          p2slot = pslot;
+          if (win) {
+            join = (fu != NONE32 && win == ku) ? 1u : 0u;
+            cand = join ? ulane : (uint32_t)__builtin_ctzll(__ballot(mk == win));
+            const uint32_t wslot = 0xFFFFFFFFu - (uint32_t)win;
+            if (join) {
+              oidx = nmod++;
+              if (lane == 0) {
+                uint32_t h = rhash(wslot);
+                while (atomicCAS(&s_hkey[h], 0u, wslot + 1) != 0u) h = (h + 1) & (RHASH - 1);
+              }
+            } else {
+              oidx = cand == (uint32_t)CAND_PREV ? powner : (uint32_t)__builtin_amdgcn_readlane((int)vidx, (int)cand);
+            }
+            pslot = wslot;
+            powner = oidx;
+          } else {
+            pslot = NONE32;
+          }
+          pvalid = win ? 1u : 0u;
+          pcand = cand;
+          if (lane == 0) {
+            s_pend[buf][0] = pvalid;
+            s_pend[buf][1] = cand;
+            s_pend[buf][2] = join;
+            s_pend[buf][3] = oidx;
+          }
+#ifdef KS_STAMPS
+          STAMP_NOW(ts);
+          sub[3] += ts - t2;
+#endif
         }
       }
-    } else {
-      // (b) my modified node re-scored: round-start row vs live row
-      uint64_t mkey = 0;
-      int32_t d[NFILT + 3] = {0, 0, 0, 0, 0, 0, 0, 0};
-      bool dany = false;
-      if (mine) {
-        NodeRegs r0 = mr;
-        r0.free_cpu = m_f0c;
-        r0.free_mem = m_f0m;
-        r0.bits = m_bits0;
-        const int st0 = filter<EXT>(p, a.clauses, r0, me);
-        const int sti = filter<EXT>(p, a.clauses, mr, me);
-        if (sti == ST_FEASIBLE) mkey = pack_key(total_score<EXT>(p, a.clauses, mr, me, a.w, tt_max, na_max), mr.slot);
-        if (st0 != sti) {
-          dany = true;
-          status_delta<EXT>(p, a.clauses, st0, sti, me, mr.slot, tt_max, na_max, d);
+    } else if (wid == RES_EVAL_WAVE) {
+      // ---------------------------------------------------------- eval wave
+      // every candidate of pod r committed (the owners take the winner's from
+      // here), evaluated against pod r+1
+      if (r < nround) {
+        const uint32_t b4 = r % RSLOTS;
+        RNode pre{};
+        CandExt px{};
+        bool on = false;
+        if (lane < (uint32_t)NCAND_OWN) {
+          on = s_okey[buf][lane] != 0;
+          if (on) {
+            const uint32_t m = s_oidx[buf][lane];
+            pre = s_mod[m];
+            if (EXT) px = s_modx[m];
+          }
+        } else if (lane < (uint32_t)CAND_PREV) {
+          const uint32_t c = lane - NCAND_OWN, cw = c / LSEL, ck = c % LSEL;
+          on = s_lidx[b4][c] != NONE32;
+          if (on) {
+            CandRow w;
+            uint4 *wp = (uint4 *)&w;
+#pragma unroll
+            for (int j = 0; j < (int)(sizeof(CandRow) / 16); ++j) wp[j] = s_lrowb[b4][cw][j][ck];
+            pre = rnode_from_row(w, 0xFFFFFFFFu - (uint32_t)s_lkey[b4][c]);
+            if constexpr (EXT) {
+              uint4 *xp = (uint4 *)&px;
+#pragma unroll
+              for (int j = 0; j < (int)(sizeof(CandExt) / 16); ++j) xp[j] = s_lrowb[b4][cw][sizeof(CandRow) / 16 + j][ck];
+            }
+          }
+        } else if (lane == (uint32_t)CAND_PREV) {
+          const uint32_t pv = s_pend[nb][0], pc = s_pend[nb][1];  // pod r-1's commit
+          on = pv != 0;
+          if (on) {
+            pre = s_post[nb][pc];
+            if (EXT) px = s_postx[nb][pc];
+          }
+        }
+        RNode post = pre;
+        if (on) {
+          rnode_add(post, s_pod[r]);
+          s_post[buf][lane] = post;
+          if (EXT) s_postx[buf][lane] = px;
+        }
+        if (on && r + 1 < nround) {
+          const PodDev &p1 = s_pod[r + 1];
+          int64_t tt_max = 0, na_max = 0;
+          if (EXT) {
+            tt_max = s_norm[r + 1][0];
+            na_max = s_norm[r + 1][1];
+          }
+          NodeExt e{};
+          if (EXT) ext_from_words(px.w, e);
+          const NodeRegs g0 = rnode_regs(pre), g1 = rnode_regs(post);
+          const int st0 = filter<EXT>(p1, a.clauses, g0, e);
+          const int st1 = filter<EXT>(p1, a.clauses, g1, e);
+          uint64_t key = 0;
+          if (st1 == ST_FEASIBLE) key = pack_key(total_score<EXT>(p1, a.clauses, g1, e, a.w, tt_max, na_max), post.slot);
+          int32_t d[NFILT + 3] = {0, 0, 0, 0, 0, 0, 0, 0};
+          if (st0 != st1) status_delta<EXT>(p1, a.clauses, st0, st1, e, post.slot, tt_max, na_max, d);
+          s_ekey[buf][lane] = key;
+#pragma unroll
+          for (int q = 0; q < NFILT + 3; ++q) s_edd[buf][lane][q] = d[q];
         }
       }
-      STAMP(2);
-      const uint64_t wmkey = wave_max_u64_dpp(mkey);
-      const bool wdany = __ballot(dany) != 0;
-      if (wdany) {
-#pragma unroll
-        for (int q = 0; q < NFILT + 3; ++q) d[q] = wave_sum_i32_dpp(d[q]);
-      }
-      if (lane == 0) {
-        s_wkey[wid] = wmkey;
-        s_wany[wid] = wdany;
-        if (wdany)
-          for (int q = 0; q < NFILT + 3; ++q) s_wd[wid][q] = d[q];
-      }
-    }
-    STAMP(3);
-    lds_barrier();
-    STAMP(4);
-    // every wave combines the 8 partials in lanes 0-7 (identical decision everywhere)
-    const uint32_t l8 = lane & 7;
-    const uint64_t bm = readlane64(max8_u64(s_wkey[l8]), 0);
-    const uint32_t wi = s_widx[l8];
-    const uint32_t fu = (uint32_t)__builtin_amdgcn_readlane((int)min8_u32(wi), 0);
-    uint64_t ku = 0;
-    if (fu != 0xFFFFFFFFu) {
-      const uint64_t hit = __ballot(lane < 8 && wi == fu);
-      ku = readlane64(s_wlk[l8], (int)__builtin_ctzll(hit));
-    }
-    int32_t sum[NFILT + 3] = {0, 0, 0, 0, 0, 0, 0, 0};
-    const bool any = __ballot(lane < 8 && s_wany[l8] != 0) != 0;
-    if (any) {
-      const bool on = s_wany[l8] != 0;
-#pragma unroll
-      for (int q = 0; q < NFILT + 3; ++q) sum[q] = __builtin_amdgcn_readlane(sum8_i32(on ? s_wd[l8][q] : 0), 0);
-    }
-    const uint32_t feasible = hdr.feasible - (uint32_t)sum[0];
-    int32_t status = 0;
-    bool stop = false;
-    uint64_t win = 0;
-    if (feasible == 0) {
-      status = 1;  // KS_POD_UNSCHEDULABLE
-    } else if ((p.flags & PF_PREF_ERR) && feasible >= 2) {
-      status = 2;  // KS_POD_ERROR (NodeAffinity PreScore)
-    } else if ((EXT && (p.flags & PF_TT) && hdr.tt_cnt - (uint32_t)sum[6] == 0) ||
-               (EXT && (p.flags & PF_NA) && hdr.na_cnt - (uint32_t)sum[7] == 0)) {
-      stop = true;  // a normaliser's max may have moved: re-sweep from this pod
-    } else if (fu != 0xFFFFFFFFu) {
-      win = ku > bm ? ku : bm;
-    } else if (bm > hdr.bound) {
-      win = bm;
-    } else {
-      stop = true;  // candidates exhausted
-    }
-    if (stop) {
-      if (tid == 0) s_stop = r;
-      break;  // uniform
-    }
-    STAMP(5);
-    if (tid == 0) {
-      DevResult res;
-      res.node_index = win ? (int32_t)(0xFFFFFFFFu - (uint32_t)win) : -1;
-      res.status = status;
-      res.total_score = win ? (int64_t)(win >> 32) - 1 : 0;
-      res.feasible_nodes = feasible;
-      res.evaluated_nodes = a.evaluated;
-      for (int q = 0; q < NFILT; ++q) res.fail_counts[q] = hdr.fails[q] + (uint32_t)sum[1 + q];
-      res.flags = (win && feasible == 1) ? 1u : 0u;
-      ((DevResult *)a.results)[pi] = res;
-    }
-    // commit (AssumePod -> NodeInfo.AddPod on the live row)
-    const uint32_t wslot = 0xFFFFFFFFu - (uint32_t)win;
-    const bool joins = win != 0 && fu != 0xFFFFFFFFu && win == ku;  // a listed, unmodified node
-    if (joins) {
-      if (tid == fu) {  // hand its row to the rescoring thread that will own it
-        uint32_t h = rhash(wslot);
-        while (s_hkey[h] != 0) h = (h + 1) & (RHASH - 1);
-        s_hkey[h] = wslot + 1;
-        // field-wise: a whole-struct copy would route the prefetched row through scratch
-        s_new.acpu = crow.acpu;
-        s_new.amem = crow.amem;
-        s_new.rc = crow.rc;
-        s_new.rm = crow.rm;
-        s_new.zc = crow.zc;
-        s_new.zm = crow.zm;
-        s_new.inv_cpu = crow.inv_cpu;
-        s_new.inv_mem = crow.inv_mem;
-        s_new.apods = crow.apods;
-        s_new.np = crow.np;
-        s_new.pos = crow.pos;
-        if (EXT)
-#pragma unroll
-          for (int q = 0; q < 2 + LW + NNUM; ++q) s_newx.w[q] = cext.w[q];
-      }
-    } else if (win != 0 && mine && mr.slot == wslot) {
-      m_rc += p.req_cpu;
-      m_rm += p.req_mem;
-      m_zc += p.nz_cpu;
-      m_zm += p.nz_mem;
-      m_np += 1;
-      mr.free_cpu -= p.req_cpu_d;  // exact integer arithmetic in binary64
-      mr.free_mem -= p.req_mem_d;
-      mr.rcpu += p.req_cpu_d;
-      mr.rmem += p.req_mem_d;
-      mr.lf100_cpu -= p.nz100_cpu;
-      mr.lf100_mem -= p.nz100_mem;
-      mr.bits = (mr.bits & ~2u) | ((int64_t)m_np + 1 <= (int64_t)m_apods ? 2u : 0u);
-    }
-    STAMP(6);
-    lds_barrier();
-    STAMP(7);
-    if (joins) {
-      if (!list_role && mj == nmod) {
-        const CandRow &w = s_new;
-        m_acpu = w.acpu;
-        m_amem = w.amem;
-        m_rc0 = w.rc;
-        m_rm0 = w.rm;
-        m_np0 = w.np;
-        m_apods = w.apods;
-        m_pos = w.pos;
-        m_rc = w.rc + p.req_cpu;
-        m_rm = w.rm + p.req_mem;
-        m_zc = w.zc + p.nz_cpu;
-        m_zm = w.zm + p.nz_mem;
-        m_np = w.np + 1;
-        mr = make_regs_inv(m_acpu, m_amem, m_rc, m_rm, m_zc, m_zm, m_apods, m_np, wslot, w.inv_cpu, w.inv_mem);
-        m_f0c = (double)(m_acpu - m_rc0);
-        m_f0m = (double)(m_amem - m_rm0);
-        m_bits0 = (mr.bits & ~2u) | ((int64_t)m_np0 + 1 <= (int64_t)m_apods ? 2u : 0u);
-        if (EXT) ext_from_words(s_newx.w, me);
+    } else if (is_owner) {
+      // ------------------------------------------------------- owner waves
+      if (r >= 1 && s_pend[nb][0] && s_pend[nb][3] == mj) {  // apply pod r-1's commit
+        const uint32_t pc = s_pend[nb][1];
+        s_mod[mj] = s_post[nb][pc];
+        if (EXT && s_pend[nb][2]) s_modx[mj] = s_postx[nb][pc];
         mine = true;
       }
-      ++nmod;
+      if (r + 1 < nround && __ballot(mine) != 0) {
+        uint64_t key = 0;
+        int32_t d[NFILT + 3] = {0, 0, 0, 0, 0, 0, 0, 0};
+        bool dany = false;
+        if (mine) {
+          const RNode nd = s_mod[mj];
+          const PodDev &p1 = s_pod[r + 1];
+          int64_t tt_max = 0, na_max = 0;
+          if (EXT) {
+            tt_max = s_norm[r + 1][0];
+            na_max = s_norm[r + 1][1];
+          }
+          NodeExt e{};
+          if (EXT) ext_from_words(s_modx[mj].w, e);
+          const NodeRegs g = rnode_regs(nd), g0 = rnode_regs0(nd, g);
+          const int st0 = filter<EXT>(p1, a.clauses, g0, e);
+          const int st = filter<EXT>(p1, a.clauses, g, e);
+          if (st == ST_FEASIBLE) key = pack_key(total_score<EXT>(p1, a.clauses, g, e, a.w, tt_max, na_max), nd.slot);
+          if (st0 != st) {
+            dany = true;
+            status_delta<EXT>(p1, a.clauses, st0, st, e, nd.slot, tt_max, na_max, d);
+          }
+        }
+        const uint64_t k1 = wave_max_u64_dpp(key);
+        const uint64_t k2 = wave_max_u64_dpp(key == k1 ? 0ull : key);
+        if (k1 != 0 && key == k1) s_oidx[nb][2 * ow] = mj;
+        if (k2 != 0 && key == k2) s_oidx[nb][2 * ow + 1] = mj;
+        const bool wdany = __ballot(dany) != 0;
+        if (wdany) {
+#pragma unroll
+          for (int q = 0; q < NFILT + 3; ++q) d[q] = wave_sum_i32_dpp(d[q]);
+        }
+        if (lane == 0) {
+          s_okey[nb][2 * ow] = k1;
+          s_okey[nb][2 * ow + 1] = k2;
+#pragma unroll
+          for (int q = 0; q < NFILT + 3; ++q) s_dsum[nb][ow][q] = wdany ? d[q] : 0;
+        }
+      } else if (r + 1 < nround && lane == 0) {
+        s_okey[nb][2 * ow] = s_okey[nb][2 * ow + 1] = 0;
+#pragma unroll
+        for (int q = 0; q < NFILT + 3; ++q) s_dsum[nb][ow][q] = 0;
+      }
+    } else {
+      // -------------------------------------------------------- list waves
+      list_select(r + LAHEAD);
+      dma_keys(r + LAHEAD + KAHEAD);
+      list_wait();
     }
-    ck = nk;
-    crow = nrow;
-    if (EXT) cext = next_ext;
-  }
+#ifdef KS_STAMPS
+    STAMP_NOW(t1);
+#endif
+    lds_barrier();
+#ifdef KS_STAMPS
+    STAMP_NOW(t2);
+    st_work += t1 - t0;
+    st_wait += t2 - t1;
+#endif
+    return s_done != 0;
+  };
+
+  for (uint32_t r = 0;; ++r)
+    if (iteration(r)) break;
+  if (is_list) __builtin_amdgcn_s_waitcnt(0);  // no DMA outlives the block
   // hand the nodes this round modified to the next round's patch and the write-back
-  if (mine) {
+  if (is_owner && mine) {
+    const RNode nd = s_mod[mj];
     CarryRec c;
-    c.acpu = m_acpu;
-    c.amem = m_amem;
-    c.rc0 = m_rc0;
-    c.rm0 = m_rm0;
-    c.np0 = m_np0;
-    c.rc = m_rc;
-    c.rm = m_rm;
-    c.zc = m_zc;
-    c.zm = m_zm;
-    c.np = m_np;
-    c.slot = mr.slot;
-    c.pos = m_pos;
-    c.apods = m_apods;
+    c.acpu = nd.acpu;
+    c.amem = nd.amem;
+    c.rc0 = nd.rc0;
+    c.rm0 = nd.rm0;
+    c.np0 = nd.np0;
+    c.rc = nd.rc;
+    c.rm = nd.rm;
+    c.zc = nd.zc;
+    c.zm = nd.zm;
+    c.np = nd.np;
+    c.slot = nd.slot;
+    c.pos = nd.pos;
+    c.apods = nd.apods;
     c._pad = 0;
-    c.ext[0] = me.hard;
-    c.ext[1] = me.prefer;
-    for (int q = 0; q < LW; ++q) c.ext[2 + q] = me.lab[q];
-    for (int q = 0; q < NNUM; ++q) c.ext[2 + LW + q] = (uint64_t)me.num[q];
+#pragma unroll
+    for (int q = 0; q < 2 + LW + NNUM; ++q) c.ext[q] = EXT ? s_modx[mj].w[q] : 0ull;
     a.carry_out[mj] = c;
   }
-  __syncthreads();
 #ifdef KS_STAMPS
-  if (tid == STAMP_TID)
-    for (int i = 0; i < 8; ++i) atomicAdd((unsigned long long *)&a.counters[8 + i], (unsigned long long)stamp_acc[i]);
+  if (stamper) {
+    atomicAdd((unsigned long long *)&a.counters[8 + sidx], (unsigned long long)st_work);
+    atomicAdd((unsigned long long *)&a.counters[9 + sidx], (unsigned long long)st_wait);
+    if (wid == RES_DEC_WAVE)
+      for (int i = 0; i < 4; ++i) atomicAdd((unsigned long long *)&a.counters[12 + i], (unsigned long long)sub[i]);
+  }
 #endif
-  if (tid == 0) {
+  if (wid == RES_DEC_WAVE && lane == 0) s_stop_at = stop_at;
+  __syncthreads();
+  {
+    const uint32_t nres = s_stop_at;
+    const uint32_t *src = (const uint32_t *)s_res;
+    uint32_t *dst = (uint32_t *)((DevResult *)a.results + start);
+    for (uint32_t i = tid; i < nres * (uint32_t)(sizeof(DevResult) / 4); i += RESOLVE_THREADS) dst[i] = src[i];
+  }
+  if (wid == RES_DEC_WAVE && lane == 0) {
     *a.carry_out_n = nmod;
-    *a.act_next = start + s_stop;
-    *a.d_start = start + s_stop;
-    a.counters[0] += 1;                                   // rounds
-    a.counters[1] += s_stop;                              // pods resolved
+    *a.act_next = start + stop_at;
+    *a.d_start = start + stop_at;
+    a.counters[0] += 1;        // rounds
+    a.counters[1] += stop_at;  // pods resolved
   }
 }
 

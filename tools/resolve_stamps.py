@@ -1,7 +1,7 @@
 """Per-phase cycle breakdown of the resolve kernel (diagnostic KS_STAMPS build).
 
 KSCHED_LIB_DIR=k8s-1m_amd/ksched/lib/stamps python tools/resolve_stamps.py [nodes] [pods]
-Shares of wave 0's cycles per pod; the stamps' own cost inflates absolute times.
+Per-role work / barrier-wait cycles per pod; the stamps' own cost inflates absolute times.
 """
 import ctypes as C
 import os
@@ -23,11 +23,11 @@ b = s.prepare(ps.pods, npods)
 s.run(b)
 k = (C.c_uint64 * 16)()
 assert s.lib.ks_debug_counters(s.ctx, k) == 0
-# wave 0 is a list-role wave: stamp 2 (rescoring, waves 4-7) stays 0 for it
-names = ["loop top", "pod+prefetch+list", "(rescore)", "wave partials", "barrier1 wait", "decide", "commit", "barrier2 wait"]
-tot = sum(k[8:16])
-pods = k[1]
-print(f"lib={os.environ.get('KSCHED_LIB_DIR', 'default')} rounds={k[0]} pods={pods}")
-for i, nm in enumerate(names):
-    print(f"  {nm:15s} {k[8 + i] / max(1, pods):10.0f} cyc/pod  {100 * k[8 + i] / max(1, tot):5.1f}%")
-print(f"  total {tot / max(1, pods):.0f} cyc/pod")
+# decider and eval wave: cycles of work and barrier wait per iteration (pod);
+# decider sub-phases: LDS loads, reductions, decision + result, commit
+pods = max(1, k[1])
+print(f"lib={os.environ.get('KSCHED_LIB_DIR', 'default')} rounds={k[0]} pods={k[1]}")
+for i, nm in enumerate(["decider", "eval"]):
+    print(f"  {nm:9s} work {k[8 + 2 * i] / pods:8.0f} cyc/pod   wait {k[9 + 2 * i] / pods:8.0f} cyc/pod")
+for i, nm in enumerate(["loads", "reductions", "decision", "commit"]):
+    print(f"    decider {nm:11s} {k[12 + i] / pods:8.0f} cyc/pod")
