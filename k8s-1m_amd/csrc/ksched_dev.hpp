@@ -136,11 +136,15 @@ static_assert(sizeof(ShardRecHdr) == 48, "ShardRecHdr layout");
 constexpr uint32_t REC_HDR_WORDS = 6;
 __host__ __device__ inline uint32_t rec_words(uint32_t k) { return REC_HDR_WORDS + k; }
 
-// S0 row of a listed candidate, gathered next to its key after the merge so
-// the resolve's per-pod prefetch is one independent load per thread.
+// S0 row of a listed candidate, gathered next to its key after the merge, in
+// the form the resolve computes in: every resource quantity is an integer
+// below 2^53 held as an exact binary64, so commits are exact additions and no
+// int64 -> binary64 conversion sits on the resolve's per-pod critical path.
 struct alignas(16) CandRow {
-  int64_t acpu, amem, rc, rm, zc, zm;
-  double inv_cpu, inv_mem;  // RN(1 / allocatable), 0 for a zero allocatable (off the resolve's critical path)
+  double acpu, amem;        // Allocatable (< 2^44)
+  double inv_cpu, inv_mem;  // RN(1 / Allocatable), 0 for a zero allocatable
+  double rc, rm;            // Requested
+  double zc100, zm100;      // NonZeroRequested x 100 (< 2^51)
   int32_t apods, np;
   uint32_t pos, _pad;
 };

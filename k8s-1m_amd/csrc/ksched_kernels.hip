@@ -779,6 +779,24 @@ __global__ __launch_bounds__(256) void merge_shards_kernel(RoundArgs a) {
 }
 
 // ============================================================ gather rows
+__device__ __forceinline__ CandRow cand_row(int64_t acpu, int64_t amem, int64_t rc, int64_t rm, int64_t zc, int64_t zm,
+                                            int32_t apods, int32_t np, uint32_t pos) {
+  CandRow w;
+  w.acpu = (double)acpu;
+  w.amem = (double)amem;
+  w.inv_cpu = acpu ? 1.0 / w.acpu : 0.0;
+  w.inv_mem = amem ? 1.0 / w.amem : 0.0;
+  w.rc = (double)rc;
+  w.rm = (double)rm;
+  w.zc100 = (double)zc * 100.0;  // exact: < 2^51
+  w.zm100 = (double)zm * 100.0;
+  w.apods = apods;
+  w.np = np;
+  w.pos = pos;
+  w._pad = 0;
+  return w;
+}
+
 // grid: x = pod in round.  For every listed candidate of the final record,
 // copy the node's S0 row (and label / taint columns) next to the key.
 template <bool EXT>
@@ -791,20 +809,8 @@ __global__ __launch_bounds__(256) void gather_cand_kernel(RoundArgs a) {
   for (uint32_t t = threadIdx.x; t < nk; t += blockDim.x) {
     const uint64_t k = rec[REC_HDR_WORDS + t];
     const uint32_t pos = a.slot_pos[0xFFFFFFFFu - (uint32_t)k];
-    CandRow w;
-    w.acpu = a.t.acpu[pos];
-    w.amem = a.t.amem[pos];
-    w.rc = a.t.rcpu[pos];
-    w.rm = a.t.rmem[pos];
-    w.zc = a.t.zcpu[pos];
-    w.zm = a.t.zmem[pos];
-    w.apods = a.t.apods[pos];
-    w.np = a.t.npods[pos];
-    w.inv_cpu = w.acpu ? 1.0 / (double)w.acpu : 0.0;
-    w.inv_mem = w.amem ? 1.0 / (double)w.amem : 0.0;
-    w.pos = pos;
-    w._pad = 0;
-    a.crow[(size_t)r * a.K + t] = w;
+    a.crow[(size_t)r * a.K + t] = cand_row(a.t.acpu[pos], a.t.amem[pos], a.t.rcpu[pos], a.t.rmem[pos], a.t.zcpu[pos],
+                                           a.t.zmem[pos], a.t.apods[pos], a.t.npods[pos], pos);
     if (EXT) {
       CandExt x;
       x.w[0] = a.t.hard[pos];
@@ -912,18 +918,7 @@ __global__ __launch_bounds__(PATCH_THREADS) void patch_kernel(RoundArgs a) {
   if (tid < nc) {
     cr = a.carry_in[tid];
     if (EXT) ext_from_words(cr.ext, ce);
-    crow_c.acpu = cr.acpu;
-    crow_c.amem = cr.amem;
-    crow_c.rc = cr.rc;
-    crow_c.rm = cr.rm;
-    crow_c.zc = cr.zc;
-    crow_c.zm = cr.zm;
-    crow_c.inv_cpu = cr.acpu ? 1.0 / (double)cr.acpu : 0.0;
-    crow_c.inv_mem = cr.amem ? 1.0 / (double)cr.amem : 0.0;
-    crow_c.apods = cr.apods;
-    crow_c.np = cr.np;
-    crow_c.pos = cr.pos;
-    crow_c._pad = 0;
+    crow_c = cand_row(cr.acpu, cr.amem, cr.rc, cr.rm, cr.zc, cr.zm, cr.apods, cr.np, cr.pos);
     const NodeRegs r1 = make_regs_inv(cr.acpu, cr.amem, cr.rc, cr.rm, cr.zc, cr.zm, cr.apods, cr.np, cr.slot,
                                       crow_c.inv_cpu, crow_c.inv_mem);
     NodeRegs r0 = r1;
@@ -1051,17 +1046,18 @@ __global__ __launch_bounds__(PATCH_THREADS) void patch_kernel(RoundArgs a) {
 //                      LDS-DMA (global_load_lds) issued three iterations before
 //                      they are read, so the loop never waits on global memory
 //                      (the next round's sweep keeps the caches cold)
-//   owner waves (4-7)  one node of M_i per thread (its state lives in LDS):
-//                      its key for pod i+1 and its filter-status change since
-//                      the round start; per wave the best two keys and the
-//                      summed status changes
+//   owner waves (4-7)  one node of M_i per thread, in registers: its key for
+//                      pod i+1 and its filter-status change since the round
+//                      start; per wave the best two (key, node) and the summed
+//                      status changes
 //   eval wave   (8)    every node that can win pod i (the candidates above and
 //                      w_{i-1}) committed: its key and status change for pod
 //                      i+1, speculatively, one candidate per lane
-//   decider     (9)    pod i from those partials, with the entries of the last
-//                      winners replaced by the eval wave's values for w_{i-1}
-// The per-pod critical path is the decider's LDS round trip, a few wave
-// reductions and the decision; re-scoring runs beside it on the other waves.
+//   decider     (9)    pod i from those partials, the last winners' stale
+//                      entries replaced by the eval wave's values for w_{i-1}
+// Node state is exact binary64 throughout (CandRow), so a re-score is a short
+// dependent chain; every role reads its inputs for a pod in one batch of LDS
+// loads.
 constexpr int RES_LIST_WAVES = 4;
 constexpr int RES_OWN_WAVES = 4;
 constexpr int RES_EVAL_WAVE = RES_LIST_WAVES + RES_OWN_WAVES;
@@ -1070,83 +1066,116 @@ constexpr int RESOLVE_THREADS = (RES_DEC_WAVE + 1) * WAVE;
 constexpr int RHASH = 1024;
 constexpr int LSEL = 4;                                   // listed candidates kept per list wave
 constexpr int LAHEAD = 3;                                 // list waves select pod i + LAHEAD in iteration i
-constexpr int KAHEAD = 3;                                 // ... with keys fetched LAHEAD iterations before
+constexpr int KAHEAD = 3;                                 // ... with keys fetched KAHEAD iterations before
 constexpr int KSLOTS = 8, RSLOTS = 4;                     // key / row staging slots (by pod mod)
 static_assert(LSEL > LAHEAD, "a selection LAHEAD pods ahead must survive the LAHEAD commits before it is used");
+static_assert(KSLOTS >= LAHEAD + KAHEAD + 1 && RSLOTS >= LAHEAD + 1, "staging depth");
 typedef __attribute__((address_space(1))) void gvoid_t;  // global_load_lds operands
 typedef __attribute__((address_space(3))) void lvoid_t;
-static_assert(KSLOTS >= LAHEAD + KAHEAD + 1 && RSLOTS >= LAHEAD + 1, "staging depth");
 constexpr int NCAND_OWN = 2 * RES_OWN_WAVES;              // lanes [0, 8): owner waves' best two
 constexpr int NCAND_LIST = LSEL * RES_LIST_WAVES;         // lanes [8, 24): list waves' first four
 constexpr int CAND_PREV = NCAND_OWN + NCAND_LIST;         // lane 24: the previous pod's winner
 constexpr int NCAND = CAND_PREV + 1;
 constexpr int DSUM_LANE = 32;                             // decider lanes summing status changes
 constexpr uint32_t NONE32 = 0xFFFFFFFFu;
+constexpr int ROW_PIECES = sizeof(CandRow) / 16;
+constexpr int EXT_PIECES = sizeof(CandExt) / 16;
 static_assert(RES_LIST_WAVES * WAVE >= MAX_K && RES_OWN_WAVES * WAVE >= MAX_P, "resolve roles");
 static_assert(DSUM_LANE >= NCAND && DSUM_LANE + NFILT + 3 <= WAVE, "decider lanes");
 
-// A node as the resolve carries it: allocatable, the round-start filter inputs
-// (the listed row), the live state and the reciprocals.
+// A node as the resolve carries it: its row (live state) and the round-start
+// Requested / pod count its listed key was computed from.
 struct alignas(16) RNode {
-  int64_t acpu, amem;
-  int64_t rc0, rm0;        // Requested at the round start
-  int64_t rc, rm, zc, zm;  // live Requested / NonZeroRequested
-  double inv_cpu, inv_mem;
-  int32_t apods, np0, np;
-  uint32_t slot, pos, _pad;
+  CandRow row;       // live
+  double rc0, rm0;   // Requested at the round start
+  int32_t np0;
+  uint32_t slot;
+  uint32_t _pad[2];
 };
-
-__device__ __forceinline__ NodeRegs rnode_regs(const RNode &n) {
-  return make_regs_inv(n.acpu, n.amem, n.rc, n.rm, n.zc, n.zm, n.apods, n.np, n.slot, n.inv_cpu, n.inv_mem);
-}
-
-// the node with its round-start Requested / pod count (only the filter reads these)
-__device__ __forceinline__ NodeRegs rnode_regs0(const RNode &n, const NodeRegs &live) {
-  NodeRegs r = live;
-  r.free_cpu = (double)(n.acpu - n.rc0);
-  r.free_mem = (double)(n.amem - n.rm0);
-  r.bits = (live.bits & ~2u) | ((int64_t)n.np0 + 1 <= (int64_t)n.apods ? 2u : 0u);
-  return r;
-}
+static_assert(sizeof(RNode) == 112, "RNode layout");
 
 __device__ __forceinline__ RNode rnode_from_row(const CandRow &w, uint32_t slot) {
   RNode n;
-  n.acpu = w.acpu;
-  n.amem = w.amem;
-  n.rc0 = n.rc = w.rc;
-  n.rm0 = n.rm = w.rm;
-  n.zc = w.zc;
-  n.zm = w.zm;
-  n.inv_cpu = w.inv_cpu;
-  n.inv_mem = w.inv_mem;
-  n.apods = w.apods;
-  n.np0 = n.np = w.np;
+  n.row = w;
+  n.rc0 = w.rc;
+  n.rm0 = w.rm;
+  n.np0 = w.np;
   n.slot = slot;
-  n.pos = w.pos;
-  n._pad = 0;
+  n._pad[0] = n._pad[1] = 0;
   return n;
 }
 
-// NodeInfo.AddPod on the live state (AssumePod)
+// NodeInfo.AddPod on the live state (AssumePod): exact binary64 additions
 __device__ __forceinline__ void rnode_add(RNode &n, const PodDev &p) {
-  n.rc += p.req_cpu;
-  n.rm += p.req_mem;
-  n.zc += p.nz_cpu;
-  n.zm += p.nz_mem;
-  n.np += 1;
+  n.row.rc += p.req_cpu_d;
+  n.row.rm += p.req_mem_d;
+  n.row.zc100 += p.nz100_cpu;
+  n.row.zm100 += p.nz100_mem;
+  n.row.np += 1;
+}
+
+// NodeRegs of the node with Requested (rc, rm) and pod count np: no int64 ->
+// binary64 conversion, every value exact (allocatable < 2^44).
+__device__ __forceinline__ NodeRegs rnode_regs(const RNode &n, double rc, double rm, int32_t np) {
+  const CandRow &w = n.row;
+  NodeRegs r;
+  r.slot = n.slot;
+  r.free_cpu = w.acpu - rc;
+  r.free_mem = w.amem - rm;
+  r.rcpu = rc;
+  r.rmem = rm;
+  r.lf100_cpu = w.acpu * 100.0 - w.zc100;
+  r.lf100_mem = w.amem * 100.0 - w.zm100;
+  r.acpu_d = w.acpu;
+  r.amem_d = w.amem;
+  r.inv_cpu = w.inv_cpu;
+  r.inv_mem = w.inv_mem;
+  const bool ac = w.acpu != 0.0, am = w.amem != 0.0;
+  r.bamul = (ac && am) ? 0.5 : 0.0;
+  r.lashift = (ac && am) ? 1u : 0u;
+  r.bits = 1u | (np + 1 <= w.apods ? 2u : 0u) | (ac ? 4u : 0u) | (am ? 8u : 0u);
+  return r;
+}
+
+// Carry record (the next round's patch and the write-back) of a modified node.
+__device__ __forceinline__ CarryRec rnode_carry(const RNode &n, const CandExt &x, bool ext) {
+  const CandRow &w = n.row;
+  CarryRec c;
+  c.acpu = (int64_t)w.acpu;
+  c.amem = (int64_t)w.amem;
+  c.rc0 = (int64_t)n.rc0;
+  c.rm0 = (int64_t)n.rm0;
+  c.np0 = n.np0;
+  c.rc = (int64_t)w.rc;
+  c.rm = (int64_t)w.rm;
+  c.zc = (int64_t)(w.zc100 / 100.0);  // exact: zc100 is 100 zc
+  c.zm = (int64_t)(w.zm100 / 100.0);
+  c.np = w.np;
+  c.slot = n.slot;
+  c.pos = w.pos;
+  c.apods = w.apods;
+  c._pad = 0;
+#pragma unroll
+  for (int q = 0; q < 2 + LW + NNUM; ++q) c.ext[q] = ext ? x.w[q] : 0ull;
+  return c;
 }
 
 // Workgroup barrier for LDS hand-offs only: __syncthreads() also drains vmcnt,
-// which would expose the list prefetch latency on every iteration.
+// which would drain the list waves' LDS-DMA pipeline on every iteration.
 __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-__device__ __forceinline__ uint32_t wave_min_u32_dpp(uint32_t v) { return ~wave_max_u32_dpp(~v); }
-
-// Diagnostic build (-DKS_STAMPS): the first lane of the decider, eval, first
-// owner and first list wave accumulate s_memtime of their work and of their
-// barrier wait into a.counters[8..15]; never compiled into the measured library.
+// Diagnostic build (-DKS_STAMPS): the first lane of the decider and the eval
+// wave accumulate s_memtime of their work and barrier wait, and the decider of
+// its phases, into a.counters[8..15]; never compiled into the measured library.
+// Timing experiments only (-DKS_EXPT=mask): skip the list (1), owner (2) or
+// eval (4) waves' work; results are then wrong.
+#ifdef KS_EXPT
+#define ROLE_ON(b) ((KS_EXPT & (b)) == 0)
+#else
+#define ROLE_ON(b) true
+#endif
 #ifdef KS_STAMPS
 #define STAMP_NOW(t_)                                                         \
   do {                                                                        \
@@ -1162,18 +1191,17 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
   __shared__ ShardRecHdr s_hdr[MAX_P];
   __shared__ uint32_t s_norm[MAX_P][2];
   __shared__ uint32_t s_hkey[RHASH];  // slots modified this round (+1), linear probing
-  // the modified nodes (owner thread m owns entry m)
-  __shared__ RNode s_mod[MAX_P];
-  __shared__ CandExt s_modx[EXT ? MAX_P : 1];
+  __shared__ CandExt s_modx[EXT ? MAX_P : 1];  // label / taint words of the modified nodes
   // owner waves' partials for pod i (written in iteration i-1), by parity of i
-  __shared__ uint64_t s_okey[2][NCAND_OWN];  // best two keys per wave, 0 = none
+  __shared__ RNode s_ocand[2][NCAND_OWN];   // best two nodes per wave
+  __shared__ CandExt s_ocandx[EXT ? 2 : 1][EXT ? NCAND_OWN : 1];
+  __shared__ uint64_t s_okey[2][NCAND_OWN];  // their keys for pod i, 0 = none
   __shared__ uint32_t s_oidx[2][NCAND_OWN];  // their owner indices
   __shared__ int32_t s_dsum[2][RES_OWN_WAVES][NFILT + 3];
   // list staging (LDS-DMA targets): listed keys by pod mod KSLOTS; the chosen
   // rows by pod mod RSLOTS as [list wave][16-byte piece][candidate]
-  constexpr int RPIECES = (sizeof(CandRow) + (EXT ? sizeof(CandExt) : 0)) / 16;
   __shared__ uint64_t s_keys[KSLOTS][MAX_K];
-  __shared__ uint4 s_lrowb[RSLOTS][RES_LIST_WAVES][RPIECES][LSEL];
+  __shared__ uint4 s_lrowb[RSLOTS][RES_LIST_WAVES][ROW_PIECES + (EXT ? EXT_PIECES : 0)][LSEL];
   // list waves' candidates for pod i (chosen in iteration i - LAHEAD), by i mod RSLOTS
   __shared__ uint64_t s_lkey[RSLOTS][NCAND_LIST];
   __shared__ uint32_t s_lidx[RSLOTS][NCAND_LIST];  // list index, NONE32 = none
@@ -1215,17 +1243,15 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
     s_norm[i][0] = a.norm_max[2 * i];
     s_norm[i][1] = a.norm_max[2 * i + 1];
   }
-  if (tid == 0) {
-    s_pend[1][0] = 0;  // "pod -1" committed nothing
-    s_done = 0;
-  }
+  if (tid < 4) s_pend[1][tid] = 0;  // "pod -1" committed nothing
+  if (tid == 0) s_done = 0;
 
   // ---- list waves (LDS-DMA pipeline).  Per iteration a list wave issues
   // LIST_DMA global_load_lds instructions (the chosen rows' pieces, one key
   // block) and, before the barrier, waits until those of two iterations ago
   // have landed; every LDS read of a DMA target in this wave is inline asm,
   // which hipcc does not tie to the DMA (it would drain the pipeline).
-  constexpr uint32_t LIST_DMA = RPIECES + 1;
+  constexpr uint32_t LIST_DMA = ROW_PIECES + (EXT ? EXT_PIECES : 0) + 1;
   constexpr int32_t LIST_WAIT = 2 * LIST_DMA;  // vmcnt(N): expcnt / lgkmcnt fields at their max
   static_assert(LIST_WAIT < 64, "vmcnt field");
   const uint32_t lw = wid;
@@ -1271,15 +1297,14 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
       const uint32_t t = 64 * lw + te;
       const uint4 *row = (const uint4 *)(a.crow + (size_t)p * a.K + (lane < nsel ? t : 0u));
 #pragma unroll
-      for (int j = 0; j < (int)(sizeof(CandRow) / 16); ++j)
+      for (int j = 0; j < ROW_PIECES; ++j)
         __builtin_amdgcn_global_load_lds((gvoid_t *)(row + j), (lvoid_t *)&s_lrowb[pod % RSLOTS][lw][j][0], 16, 0, 0);
       if constexpr (EXT) {
         const uint4 *x = (const uint4 *)(a.cext + (size_t)p * a.K + (lane < nsel ? t : 0u));
 #pragma unroll
-        for (int j = 0; j < (int)(sizeof(CandExt) / 16); ++j)
-          __builtin_amdgcn_global_load_lds((gvoid_t *)(x + j),
-                                           (lvoid_t *)&s_lrowb[pod % RSLOTS][lw][sizeof(CandRow) / 16 + j][0], 16, 0,
-                                           0);
+        for (int j = 0; j < EXT_PIECES; ++j)
+          __builtin_amdgcn_global_load_lds((gvoid_t *)(x + j), (lvoid_t *)&s_lrowb[pod % RSLOTS][lw][ROW_PIECES + j][0],
+                                           16, 0, 0);
       }
       if (real) {
         s_lkey[pod % RSLOTS][LSEL * lw + lane] = lane < nsel ? tk : 0ull;
@@ -1304,9 +1329,10 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
     for (int q = 0; q < NFILT + 3; ++q) s_dsum[0][ow][q] = 0;
   }
 
-  // owner thread: does it own modified node mj
+  // owner thread: the modified node it owns (live state, in registers)
   bool mine = false;
-  // decider state (wave-uniform): the last two commits, modified count, stop point
+  RNode own{};
+  // decider state (wave-uniform): the last three commits, modified count, stop point
   uint32_t pvalid = 0, pcand = 0, pslot = NONE32, p2slot = NONE32, p3slot = NONE32, powner = 0, nmod = 0,
            stop_at = nround;
   // the decider is the per-pod critical path, the eval wave next: issue priority
@@ -1333,60 +1359,47 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
         }
       } else {
         const uint32_t b4 = r % RSLOTS;
-        const uint32_t pflags = uniform_u32(s_pod[r].flags);
-        // lanes 0-7: owner candidates, 8-23: listed candidates, 24: the previous
-        // winner committed; lanes 32-39: status-change sums per count
-        uint64_t vkey = 0;
-        uint32_t vslot = NONE32, vidx = NONE32;
-        int32_t vd = 0;
-        if (lane < (uint32_t)NCAND_OWN) {
-          vkey = s_okey[buf][lane];
-          vidx = s_oidx[buf][lane];
-          vslot = vkey ? s_mod[vidx].slot : NONE32;
-        } else if (lane < (uint32_t)CAND_PREV) {
-          vkey = s_lkey[b4][lane - NCAND_OWN];
-          vidx = s_lidx[b4][lane - NCAND_OWN];
-          vslot = 0xFFFFFFFFu - (uint32_t)vkey;
-        } else if (lane == (uint32_t)CAND_PREV) {
-          if (pvalid) {
-            vkey = s_ekey[nb][pcand];
-            vslot = pslot;
-          }
-        } else if (lane >= (uint32_t)DSUM_LANE && lane < (uint32_t)DSUM_LANE + NFILT + 3) {
-          const uint32_t q = lane - DSUM_LANE;
-#pragma unroll
-          for (int w = 0; w < RES_OWN_WAVES; ++w) vd += s_dsum[buf][w][q];
-          if (pvalid) vd += s_edd[nb][pcand][q];
-        }
+        // One batch of independent LDS loads.  Lanes 0-7: owner candidates,
+        // 8-23: listed candidates, 24: the previous winner committed (its key
+        // for this pod); lanes 32-39: the status-change sums per count; lanes
+        // 33-37 also their header failure counts.
+        const bool is_own = lane < (uint32_t)NCAND_OWN;
+        const bool is_lst = lane >= (uint32_t)NCAND_OWN && lane < (uint32_t)CAND_PREV;
+        const bool is_prev = lane == (uint32_t)CAND_PREV;
+        const uint32_t lo = is_own ? lane : 0u, ll = is_lst ? lane - NCAND_OWN : 0u;
+        const uint64_t *kp = is_own ? &s_okey[buf][lo] : is_prev ? &s_ekey[nb][pcand] : &s_lkey[b4][ll];
+        const uint32_t *ip = is_own ? &s_oidx[buf][lo] : &s_lidx[b4][ll];
+        const uint32_t q = (lane - DSUM_LANE) & 7u;
+        const uint64_t rkey = *kp;
+        const uint32_t vidx = *ip;
+        const uint32_t oslot = s_ocand[buf][lo].slot;
+        int32_t vd = s_dsum[buf][0][q] + s_dsum[buf][1][q] + s_dsum[buf][2][q] + s_dsum[buf][3][q] +
+                     (pvalid ? s_edd[nb][pcand][q] : 0);
         const ShardRecHdr &hd = s_hdr[r];
-#ifdef KS_STAMPS
+        const uint32_t hfail = hd.fails[(lane - DSUM_LANE - 1) % NFILT];
+        const uint32_t pflags = uniform_u32(s_pod[r].flags);
+        const uint32_t h_feasible = uniform_u32(hd.feasible);
+        const uint32_t h_tt = uniform_u32(hd.tt_cnt), h_na = uniform_u32(hd.na_cnt);
+        const uint64_t h_bound = ((uint64_t)uniform_u32((uint32_t)(hd.bound >> 32)) << 32) |
+                                 uniform_u32((uint32_t)hd.bound);
+#if KS_STAMPS == 1
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         STAMP_NOW(ts);
         sub[0] += ts - t0;
         t2 = ts;
 #endif
-        const uint32_t h_feasible = uniform_u32(hd.feasible);
-        const uint32_t h_tt = uniform_u32(hd.tt_cnt), h_na = uniform_u32(hd.na_cnt);
-        const uint64_t h_bound = ((uint64_t)uniform_u32((uint32_t)(hd.bound >> 32)) << 32) |
-                                 uniform_u32((uint32_t)hd.bound);
+        const uint64_t vkey = (is_prev && !pvalid) ? 0ull : rkey;
+        const uint32_t vslot = is_own ? oslot : is_prev ? pslot : 0xFFFFFFFFu - (uint32_t)vkey;
         // entries computed before the last winners' commits are stale: drop them
-        const bool is_own = lane < (uint32_t)NCAND_OWN;
-        const bool is_lst = lane >= (uint32_t)NCAND_OWN && lane < (uint32_t)CAND_PREV;
-        const uint64_t mk = ((is_own && vkey && vslot != pslot) || lane == (uint32_t)CAND_PREV) ? vkey : 0ull;
+        const uint64_t mk = ((is_own && vkey && vslot != pslot) || is_prev) ? vkey : 0ull;
         const uint64_t bm = wave_max_u64_dpp(mk);
         const bool lok = is_lst && vidx != NONE32 && vslot != pslot && vslot != p2slot && vslot != p3slot;
-        const uint32_t fu = wave_min_u32_dpp(lok ? vidx : NONE32);
-        uint64_t ku = 0;
-        uint32_t ulane = 0;
-        if (fu != NONE32) {
-          ulane = (uint32_t)__builtin_ctzll(__ballot(lok && vidx == fu));
-          ku = readlane64(vkey, (int)ulane);
-        }
-        int32_t sum[NFILT + 3];
-#pragma unroll
-        for (int q = 0; q < NFILT + 3; ++q) sum[q] = __builtin_amdgcn_readlane(vd, DSUM_LANE + q);
-        const uint32_t feasible = h_feasible - (uint32_t)sum[0];
-#ifdef KS_STAMPS
+        const uint64_t lb = __ballot(lok);  // listed candidates are in list order by lane
+        const uint32_t ulane = lb ? (uint32_t)__builtin_ctzll(lb) : 0u;
+        const uint64_t ku = lb ? readlane64(vkey, (int)ulane) : 0ull;
+        const int32_t s0 = __builtin_amdgcn_readlane(vd, DSUM_LANE);
+        const uint32_t feasible = h_feasible - (uint32_t)s0;
+#if KS_STAMPS == 1
         STAMP_NOW(ts);
         sub[1] += ts - t2;
         t2 = ts;
@@ -1398,10 +1411,10 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
           status = 1;  // KS_POD_UNSCHEDULABLE
         } else if ((pflags & PF_PREF_ERR) && feasible >= 2) {
           status = 2;  // KS_POD_ERROR (NodeAffinity PreScore)
-        } else if ((EXT && (pflags & PF_TT) && h_tt - (uint32_t)sum[6] == 0) ||
-                   (EXT && (pflags & PF_NA) && h_na - (uint32_t)sum[7] == 0)) {
+        } else if ((EXT && (pflags & PF_TT) && h_tt - (uint32_t)__builtin_amdgcn_readlane(vd, DSUM_LANE + 6) == 0) ||
+                   (EXT && (pflags & PF_NA) && h_na - (uint32_t)__builtin_amdgcn_readlane(vd, DSUM_LANE + 7) == 0)) {
           stop = true;  // a normaliser's max may have moved: re-sweep from this pod
-        } else if (fu != NONE32) {
+        } else if (lb) {
           win = ku > bm ? ku : bm;
         } else if (bm > h_bound) {
           win = bm;
@@ -1415,18 +1428,18 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
             s_done = 1;
           }
         } else {
+          DevResult *res = &s_res[r];
           if (lane == 0) {
-            DevResult *res = &s_res[r];
             res->node_index = win ? (int32_t)(0xFFFFFFFFu - (uint32_t)win) : -1;
             res->status = status;
             res->total_score = win ? (int64_t)(win >> 32) - 1 : 0;
             res->feasible_nodes = feasible;
             res->evaluated_nodes = a.evaluated;
-#pragma unroll
-            for (int q = 0; q < NFILT; ++q) res->fail_counts[q] = hd.fails[q] + (uint32_t)sum[1 + q];
             res->flags = (win && feasible == 1) ? 1u : 0u;
           }
-#ifdef KS_STAMPS
+          if (lane > (uint32_t)DSUM_LANE && lane <= (uint32_t)DSUM_LANE + NFILT)
+            res->fail_counts[lane - DSUM_LANE - 1] = hfail + (uint32_t)vd;
+#if KS_STAMPS == 1
           STAMP_NOW(ts);
           sub[2] += ts - t2;
           t2 = ts;
@@ -1437,7 +1450,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
           p3slot = p2slot;
           p2slot = pslot;
           if (win) {
-            join = (fu != NONE32 && win == ku) ? 1u : 0u;
+            join = (lb && win == ku) ? 1u : 0u;
             cand = join ? ulane : (uint32_t)__builtin_ctzll(__ballot(mk == win));
             const uint32_t wslot = 0xFFFFFFFFu - (uint32_t)win;
             if (join) {
@@ -1462,58 +1475,77 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
             s_pend[buf][2] = join;
             s_pend[buf][3] = oidx;
           }
-#ifdef KS_STAMPS
+#if KS_STAMPS == 1
           STAMP_NOW(ts);
           sub[3] += ts - t2;
 #endif
         }
       }
     } else if (wid == RES_EVAL_WAVE) {
+      if (ROLE_ON(4)) {
       // ---------------------------------------------------------- eval wave
       // every candidate of pod r committed (the owners take the winner's from
       // here), evaluated against pod r+1
       if (r < nround) {
         const uint32_t b4 = r % RSLOTS;
-        RNode pre{};
+        const bool is_own = lane < (uint32_t)NCAND_OWN;
+        const bool is_lst = lane >= (uint32_t)NCAND_OWN && lane < (uint32_t)CAND_PREV;
+        const bool is_prev = lane == (uint32_t)CAND_PREV;
+        const uint32_t lo = is_own ? lane : 0u, c = is_lst ? lane - NCAND_OWN : 0u;
+        const uint32_t cw = c / LSEL, ck = c % LSEL;
+        const uint32_t pv = s_pend[nb][0], pc = min(s_pend[nb][1], (uint32_t)NCAND - 1);  // pod r-1's commit
+#if KS_STAMPS == 2
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        STAMP_NOW(ts);
+        sub[0] += ts - t0;
+        t2 = ts;
+#endif
+        // one batch: the candidate's row (owner: published node; listed: DMA
+        // pieces; previous winner: its committed node), round-start fields
+        const uint4 *rp = is_own ? (const uint4 *)&s_ocand[buf][lo]
+                                 : is_prev ? (const uint4 *)&s_post[nb][pc] : &s_lrowb[b4][cw][0][ck];
+        const uint32_t rstride = (is_own || is_prev) ? 1u : (uint32_t)LSEL;
+        RNode pre;
+        uint4 *pp = (uint4 *)&pre;
+#pragma unroll
+        for (int j = 0; j < ROW_PIECES; ++j) pp[j] = rp[j * rstride];
+        const uint4 tail = is_lst ? make_uint4(0, 0, 0, 0) : rp[ROW_PIECES];  // rc0, rm0
+        const uint4 tail2 = is_lst ? make_uint4(0, 0, 0, 0) : rp[ROW_PIECES + 1];  // np0, slot
         CandExt px{};
-        bool on = false;
-        if (lane < (uint32_t)NCAND_OWN) {
-          on = s_okey[buf][lane] != 0;
-          if (on) {
-            const uint32_t m = s_oidx[buf][lane];
-            pre = s_mod[m];
-            if (EXT) px = s_modx[m];
-          }
-        } else if (lane < (uint32_t)CAND_PREV) {
-          const uint32_t c = lane - NCAND_OWN, cw = c / LSEL, ck = c % LSEL;
-          on = s_lidx[b4][c] != NONE32;
-          if (on) {
-            CandRow w;
-            uint4 *wp = (uint4 *)&w;
+        if constexpr (EXT) {
+          const uint4 *xp = is_own ? (const uint4 *)&s_ocandx[buf][lo]
+                                   : is_prev ? (const uint4 *)&s_postx[nb][pc] : &s_lrowb[b4][cw][ROW_PIECES][ck];
+          uint4 *xo = (uint4 *)&px;
 #pragma unroll
-            for (int j = 0; j < (int)(sizeof(CandRow) / 16); ++j) wp[j] = s_lrowb[b4][cw][j][ck];
-            pre = rnode_from_row(w, 0xFFFFFFFFu - (uint32_t)s_lkey[b4][c]);
-            if constexpr (EXT) {
-              uint4 *xp = (uint4 *)&px;
-#pragma unroll
-              for (int j = 0; j < (int)(sizeof(CandExt) / 16); ++j) xp[j] = s_lrowb[b4][cw][sizeof(CandRow) / 16 + j][ck];
-            }
-          }
-        } else if (lane == (uint32_t)CAND_PREV) {
-          const uint32_t pv = s_pend[nb][0], pc = s_pend[nb][1];  // pod r-1's commit
-          on = pv != 0;
-          if (on) {
-            pre = s_post[nb][pc];
-            if (EXT) px = s_postx[nb][pc];
-          }
+          for (int j = 0; j < EXT_PIECES; ++j) xo[j] = xp[j * rstride];
         }
+        const uint64_t lkey = s_lkey[b4][c];
+        const bool on = is_own ? s_okey[buf][lo] != 0 : is_lst ? s_lidx[b4][c] != NONE32 : (is_prev && pv != 0);
+        if (is_lst) {
+          pre.rc0 = pre.row.rc;
+          pre.rm0 = pre.row.rm;
+          pre.np0 = pre.row.np;
+          pre.slot = 0xFFFFFFFFu - (uint32_t)lkey;
+        } else {
+          pre.rc0 = __builtin_bit_cast(double, ((uint64_t)tail.y << 32) | tail.x);
+          pre.rm0 = __builtin_bit_cast(double, ((uint64_t)tail.w << 32) | tail.z);
+          pre.np0 = (int32_t)tail2.x;
+          pre.slot = tail2.y;
+        }
+        pre._pad[0] = pre._pad[1] = 0;
+#if KS_STAMPS == 2
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        STAMP_NOW(ts);
+        sub[1] += ts - t2;
+        t2 = ts;
+#endif
         RNode post = pre;
-        if (on) {
-          rnode_add(post, s_pod[r]);
+        rnode_add(post, s_pod[r]);
+        if (on && lane < (uint32_t)NCAND) {
           s_post[buf][lane] = post;
           if (EXT) s_postx[buf][lane] = px;
         }
-        if (on && r + 1 < nround) {
+        if (on && lane < (uint32_t)NCAND && r + 1 < nround) {
           const PodDev &p1 = s_pod[r + 1];
           int64_t tt_max = 0, na_max = 0;
           if (EXT) {
@@ -1522,7 +1554,8 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
           }
           NodeExt e{};
           if (EXT) ext_from_words(px.w, e);
-          const NodeRegs g0 = rnode_regs(pre), g1 = rnode_regs(post);
+          const NodeRegs g0 = rnode_regs(pre, pre.row.rc, pre.row.rm, pre.row.np);
+          const NodeRegs g1 = rnode_regs(post, post.row.rc, post.row.rm, post.row.np);
           const int st0 = filter<EXT>(p1, a.clauses, g0, e);
           const int st1 = filter<EXT>(p1, a.clauses, g1, e);
           uint64_t key = 0;
@@ -1531,14 +1564,21 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
           if (st0 != st1) status_delta<EXT>(p1, a.clauses, st0, st1, e, post.slot, tt_max, na_max, d);
           s_ekey[buf][lane] = key;
 #pragma unroll
-          for (int q = 0; q < NFILT + 3; ++q) s_edd[buf][lane][q] = d[q];
+          for (int qq = 0; qq < NFILT + 3; ++qq) s_edd[buf][lane][qq] = d[qq];
         }
+#if KS_STAMPS == 2
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        STAMP_NOW(ts);
+        sub[2] += ts - t2;
+#endif
+      }
       }
     } else if (is_owner) {
+      if (ROLE_ON(2)) {
       // ------------------------------------------------------- owner waves
       if (r >= 1 && s_pend[nb][0] && s_pend[nb][3] == mj) {  // apply pod r-1's commit
         const uint32_t pc = s_pend[nb][1];
-        s_mod[mj] = s_post[nb][pc];
+        own = s_post[nb][pc];
         if (EXT && s_pend[nb][2]) s_modx[mj] = s_postx[nb][pc];
         mine = true;
       }
@@ -1546,8 +1586,8 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
         uint64_t key = 0;
         int32_t d[NFILT + 3] = {0, 0, 0, 0, 0, 0, 0, 0};
         bool dany = false;
+        CandExt ox{};
         if (mine) {
-          const RNode nd = s_mod[mj];
           const PodDev &p1 = s_pod[r + 1];
           int64_t tt_max = 0, na_max = 0;
           if (EXT) {
@@ -1555,41 +1595,53 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
             na_max = s_norm[r + 1][1];
           }
           NodeExt e{};
-          if (EXT) ext_from_words(s_modx[mj].w, e);
-          const NodeRegs g = rnode_regs(nd), g0 = rnode_regs0(nd, g);
+          if (EXT) {
+            ox = s_modx[mj];
+            ext_from_words(ox.w, e);
+          }
+          const NodeRegs g = rnode_regs(own, own.row.rc, own.row.rm, own.row.np);
+          const NodeRegs g0 = rnode_regs(own, own.rc0, own.rm0, own.np0);
           const int st0 = filter<EXT>(p1, a.clauses, g0, e);
           const int st = filter<EXT>(p1, a.clauses, g, e);
-          if (st == ST_FEASIBLE) key = pack_key(total_score<EXT>(p1, a.clauses, g, e, a.w, tt_max, na_max), nd.slot);
+          if (st == ST_FEASIBLE) key = pack_key(total_score<EXT>(p1, a.clauses, g, e, a.w, tt_max, na_max), own.slot);
           if (st0 != st) {
             dany = true;
-            status_delta<EXT>(p1, a.clauses, st0, st, e, nd.slot, tt_max, na_max, d);
+            status_delta<EXT>(p1, a.clauses, st0, st, e, own.slot, tt_max, na_max, d);
           }
         }
         const uint64_t k1 = wave_max_u64_dpp(key);
         const uint64_t k2 = wave_max_u64_dpp(key == k1 ? 0ull : key);
-        if (k1 != 0 && key == k1) s_oidx[nb][2 * ow] = mj;
-        if (k2 != 0 && key == k2) s_oidx[nb][2 * ow + 1] = mj;
+        // the holders publish their node for the decider and the eval wave
+        if (key != 0 && (key == k1 || key == k2)) {
+          const uint32_t c = 2 * ow + (key == k1 ? 0u : 1u);
+          s_ocand[nb][c] = own;
+          if (EXT) s_ocandx[nb][c] = ox;
+          s_oidx[nb][c] = mj;
+        }
         const bool wdany = __ballot(dany) != 0;
         if (wdany) {
 #pragma unroll
-          for (int q = 0; q < NFILT + 3; ++q) d[q] = wave_sum_i32_dpp(d[q]);
+          for (int qq = 0; qq < NFILT + 3; ++qq) d[qq] = wave_sum_i32_dpp(d[qq]);
         }
         if (lane == 0) {
           s_okey[nb][2 * ow] = k1;
           s_okey[nb][2 * ow + 1] = k2;
 #pragma unroll
-          for (int q = 0; q < NFILT + 3; ++q) s_dsum[nb][ow][q] = wdany ? d[q] : 0;
+          for (int qq = 0; qq < NFILT + 3; ++qq) s_dsum[nb][ow][qq] = wdany ? d[qq] : 0;
         }
       } else if (r + 1 < nround && lane == 0) {
         s_okey[nb][2 * ow] = s_okey[nb][2 * ow + 1] = 0;
 #pragma unroll
-        for (int q = 0; q < NFILT + 3; ++q) s_dsum[nb][ow][q] = 0;
+        for (int qq = 0; qq < NFILT + 3; ++qq) s_dsum[nb][ow][qq] = 0;
+      }
       }
     } else {
       // -------------------------------------------------------- list waves
+      if (ROLE_ON(1)) {
       list_select(r + LAHEAD);
       dma_keys(r + LAHEAD + KAHEAD);
       list_wait();
+      }
     }
 #ifdef KS_STAMPS
     STAMP_NOW(t1);
@@ -1607,32 +1659,16 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
     if (iteration(r)) break;
   if (is_list) __builtin_amdgcn_s_waitcnt(0);  // no DMA outlives the block
   // hand the nodes this round modified to the next round's patch and the write-back
-  if (is_owner && mine) {
-    const RNode nd = s_mod[mj];
-    CarryRec c;
-    c.acpu = nd.acpu;
-    c.amem = nd.amem;
-    c.rc0 = nd.rc0;
-    c.rm0 = nd.rm0;
-    c.np0 = nd.np0;
-    c.rc = nd.rc;
-    c.rm = nd.rm;
-    c.zc = nd.zc;
-    c.zm = nd.zm;
-    c.np = nd.np;
-    c.slot = nd.slot;
-    c.pos = nd.pos;
-    c.apods = nd.apods;
-    c._pad = 0;
-#pragma unroll
-    for (int q = 0; q < 2 + LW + NNUM; ++q) c.ext[q] = EXT ? s_modx[mj].w[q] : 0ull;
-    a.carry_out[mj] = c;
+  if (is_owner && mine && ROLE_ON(7)) {
+    CandExt ox{};
+    if (EXT) ox = s_modx[mj];
+    a.carry_out[mj] = rnode_carry(own, ox, EXT);
   }
 #ifdef KS_STAMPS
   if (stamper) {
     atomicAdd((unsigned long long *)&a.counters[8 + sidx], (unsigned long long)st_work);
     atomicAdd((unsigned long long *)&a.counters[9 + sidx], (unsigned long long)st_wait);
-    if (wid == RES_DEC_WAVE)
+    if (wid == (KS_STAMPS == 2 ? RES_EVAL_WAVE : RES_DEC_WAVE))
       for (int i = 0; i < 4; ++i) atomicAdd((unsigned long long *)&a.counters[12 + i], (unsigned long long)sub[i]);
   }
 #endif
@@ -1645,6 +1681,9 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
     for (uint32_t i = tid; i < nres * (uint32_t)(sizeof(DevResult) / 4); i += RESOLVE_THREADS) dst[i] = src[i];
   }
   if (wid == RES_DEC_WAVE && lane == 0) {
+#ifdef KS_EXPT
+    nmod = 0;  // timing experiment: never write back garbage rows
+#endif
     *a.carry_out_n = nmod;
     *a.act_next = start + stop_at;
     *a.d_start = start + stop_at;
