@@ -431,6 +431,17 @@ __global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
     if constexpr (EXT) load_ext(a.t, pos, nr[j].bits & 1u, ne[j]);
   });
 
+  // per node, pod-independent: pod-count fit (also false for empty slots), and
+  // the wave-local key position ~(step * 64 + lane)
+  bool podfit[NPL];
+  uint32_t vcount = 0;  // valid nodes of the wave
+  static_for<NPL>([&](auto J) {
+    constexpr int j = J;
+    podfit[j] = nr[j].bits & 2u;
+    vcount += popc_ballot(nr[j].bits & 1u);
+  });
+  const uint32_t kpos0 = KEY32_POS_MASK - lane;
+
   for (uint32_t pi = p0; pi < p1; ++pi) {
     const uint32_t r = pi - start;
     if (fix && uniform_u32(a.fix_flag[r]) == 0) continue;
@@ -440,58 +451,70 @@ __global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
       tt_max = fix ? a.norm_max[2 * r + 0] : p.tt_guess;
       na_max = fix ? a.norm_max[2 * r + 1] : p.na_guess;
     }
-    // lane top-2 as (TotalScore + 1, step): steps run in slot order, so an
-    // equal score never displaces an earlier step (lowest slot wins ties)
-    uint32_t bs = 0, bj = 0, ss = 0, sj = 0;
+    // lane top-2 of wave-local 32-bit keys (TotalScore + 1) << 9 | ~(step * 64 + lane):
+    // within a wave slot order is (step, lane) order, so these sort like packed keys
+    uint32_t b1 = 0, b2 = 0;
     uint32_t feas = 0, f0 = 0, f1 = 0, f2 = 0, f3 = 0, f4 = 0, ttc = 0, nac = 0;
     uint32_t tmx = 0, nmx = 0;  // max raw over this lane's feasible nodes
-    static_for<NPL>([&](auto J) {
-      constexpr int j = J;
-      constexpr int je = EXT ? j : 0;
-      const bool valid = nr[j].bits & 1u;
-      // branch-free: every lane scores its node (empty slots hold benign
-      // values) and the feasibility mask selects
-      const int st = valid ? filter<EXT>(p, a.clauses, nr[j], ne[je]) : ST_EMPTY;
-      const bool feasible = st == ST_FEASIBLE;
-      const uint32_t tot = (uint32_t)total_score<EXT>(p, a.clauses, nr[j], ne[je], a.w, tt_max, na_max) + 1u;
-      const uint32_t sc = feasible ? tot : 0u;
-      bool at_tt = false, at_na = false;
-      if (EXT && (p.flags & PF_TT)) {
-        const uint32_t raw = (uint32_t)taint_raw(p, ne[je]);
-        at_tt = feasible && raw == (uint32_t)tt_max;
-        tmx = max(tmx, feasible ? raw : 0u);
-      }
-      if (EXT && (p.flags & PF_NA)) {
-        const uint32_t raw = (uint32_t)preferred_raw(p, a.clauses, ne[je], nr[j].slot);
-        at_na = feasible && raw == (uint32_t)na_max;
-        nmx = max(nmx, feasible ? raw : 0u);
-      }
-      // running top-2 as value selects (a branchy form sinks into a scratch store)
-      const bool gt1 = sc > bs, gt2 = sc > ss;
-      ss = gt1 ? bs : (gt2 ? sc : ss);
-      sj = gt1 ? bj : (gt2 ? (uint32_t)j : sj);
-      bs = gt1 ? sc : bs;
-      bj = gt1 ? (uint32_t)j : bj;
-      const uint64_t fb = __ballot(st == ST_FEASIBLE), vb = __ballot(valid);
-      feas += (uint32_t)__popcll(fb);
-      if (fb != vb) {  // some node failed a filter: per-plugin diagnosis counts
-        f0 += popc_ballot(st == 0);
-        f1 += popc_ballot(st == 1);
-        f2 += popc_ballot(st == 2);
-        f3 += popc_ballot(st == 3);
-        f4 += popc_ballot(st == 4);
-      }
-      if (EXT && (p.flags & (PF_TT | PF_NA))) {
-        ttc += popc_ballot(at_tt);
-        nac += popc_ballot(at_na);
-      }
-    });
+    if constexpr (!EXT) {
+      // Resource-only pods: only NodeResourcesFit can fail (a batch without
+      // PF_EXT pods tolerates every hard taint and names no node).  A zero
+      // request skips its check (fitsRequest), encoded as a -inf request.
+      const double rq_c = ((p.flags & PF_HAS_REQ) && p.req_cpu > 0) ? p.req_cpu_d : -__builtin_inf();
+      const double rq_m = ((p.flags & PF_HAS_REQ) && p.req_mem > 0) ? p.req_mem_d : -__builtin_inf();
+      const uint32_t cplus = (uint32_t)(a.w.tt * 100) + 1u;  // TaintToleration 100 (no prefer taints) + 1
+      static_for<NPL>([&](auto J) {
+        constexpr int j = J;
+        const bool feasible = podfit[j] && !(rq_c > nr[j].free_cpu) && !(rq_m > nr[j].free_mem);
+        const uint32_t tot1 = (uint32_t)__umul24((uint32_t)a.w.fit, (uint32_t)score_la(p, nr[j])) +
+                              (uint32_t)__umul24((uint32_t)a.w.ba, (uint32_t)score_ba(p, nr[j])) + cplus;
+        const uint32_t key = feasible ? (tot1 << KEY32_POS_BITS) | (kpos0 - (uint32_t)j * WAVE) : 0u;
+        b2 = max(b2, min(b1, key));
+        b1 = max(b1, key);
+        feas += popc_ballot(feasible);
+      });
+      f4 = vcount - feas;
+    } else {
+      static_for<NPL>([&](auto J) {
+        constexpr int j = J;
+        const bool valid = nr[j].bits & 1u;
+        // branch-free: every lane scores its node (empty slots hold benign
+        // values) and the feasibility mask selects
+        const int st = valid ? filter<EXT>(p, a.clauses, nr[j], ne[j]) : ST_EMPTY;
+        const bool feasible = st == ST_FEASIBLE;
+        const uint32_t tot1 = (uint32_t)total_score<EXT>(p, a.clauses, nr[j], ne[j], a.w, tt_max, na_max) + 1u;
+        const uint32_t key = feasible ? (tot1 << KEY32_POS_BITS) | (kpos0 - (uint32_t)j * WAVE) : 0u;
+        bool at_tt = false, at_na = false;
+        if (p.flags & PF_TT) {
+          const uint32_t raw = (uint32_t)taint_raw(p, ne[j]);
+          at_tt = feasible && raw == (uint32_t)tt_max;
+          tmx = max(tmx, feasible ? raw : 0u);
+        }
+        if (p.flags & PF_NA) {
+          const uint32_t raw = (uint32_t)preferred_raw(p, a.clauses, ne[j], nr[j].slot);
+          at_na = feasible && raw == (uint32_t)na_max;
+          nmx = max(nmx, feasible ? raw : 0u);
+        }
+        b2 = max(b2, min(b1, key));
+        b1 = max(b1, key);
+        const uint64_t fb = __ballot(feasible), vb = __ballot(valid);
+        feas += (uint32_t)__popcll(fb);
+        if (fb != vb) {  // some node failed a filter: per-plugin diagnosis counts
+          f0 += popc_ballot(st == 0);
+          f1 += popc_ballot(st == 1);
+          f2 += popc_ballot(st == 2);
+          f3 += popc_ballot(st == 3);
+          f4 += popc_ballot(st == 4);
+        }
+        if (p.flags & (PF_TT | PF_NA)) {
+          ttc += popc_ballot(at_tt);
+          nac += popc_ballot(at_na);
+        }
+      });
+    }
     if (EXT && (p.flags & PF_TT)) tmx = wave_max_u32_dpp(tmx);
     if (EXT && (p.flags & PF_NA)) nmx = wave_max_u32_dpp(nmx);
-    // Wave-local 32-bit keys (score + 1) << 9 | ~(step * 64 + lane): within a
-    // wave slot order is (step, lane) order, so these sort like packed keys.
-    const uint32_t best = bs ? (bs << KEY32_POS_BITS) | (KEY32_POS_MASK - (bj * WAVE + lane)) : 0u;
-    const uint32_t second = ss ? (ss << KEY32_POS_BITS) | (KEY32_POS_MASK - (sj * WAVE + lane)) : 0u;
+    const uint32_t best = b1, second = b2;
     // Wave list: the lane bests above every lane's second best (top 2) + bound,
     // DPP reductions, skipping those the candidate count makes unnecessary.
     uint32_t bound32 = wave_max_u32_dpp(second);
