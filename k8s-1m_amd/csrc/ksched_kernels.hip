@@ -1101,6 +1101,7 @@ constexpr int CAND_PREV = NCAND_OWN + NCAND_LIST;         // lane 24: the previo
 constexpr int NCAND = CAND_PREV + 1;
 constexpr int DSUM_LANE = 32;                             // decider lanes summing status changes
 constexpr uint32_t NONE32 = 0xFFFFFFFFu;
+constexpr int KS_PLUGIN_FIT_IDX = 4;  // filter status of NodeResourcesFit (KS_PLUGIN_FIT)
 constexpr int ROW_PIECES = sizeof(CandRow) / 16;
 constexpr int EXT_PIECES = sizeof(CandExt) / 16;
 static_assert(RES_LIST_WAVES * WAVE >= MAX_K && RES_OWN_WAVES * WAVE >= MAX_P, "resolve roles");
@@ -1207,6 +1208,54 @@ __device__ __forceinline__ void lds_barrier() {
     __builtin_amdgcn_sched_barrier(0);                                        \
   } while (0)
 #endif
+
+// Wave-uniform copy of an LDS object into scalar registers: one lane reads it
+// (a 64-lane broadcast read would cost the LDS 64x the bytes), readfirstlane
+// hands every dword to the SALU / VALU-operand side.
+template <class T>
+__device__ __forceinline__ T lds_uniform(const T &src, uint32_t lane) {
+  static_assert(sizeof(T) % 4 == 0, "dword object");
+  constexpr int N = sizeof(T) / 4;
+  uint32_t tmp[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) tmp[i] = 0;
+  if (lane == 0) {
+    const uint32_t *sp = (const uint32_t *)&src;
+#pragma unroll
+    for (int i = 0; i < N; ++i) tmp[i] = sp[i];
+  }
+  T out;
+  uint32_t *o = (uint32_t *)&out;
+#pragma unroll
+  for (int i = 0; i < N; ++i) o[i] = __builtin_amdgcn_readfirstlane(tmp[i]);
+  return out;
+}
+
+// Resource-only pods (batches without PF_EXT pods: only NodeResourcesFit can
+// fail, TaintToleration is the constant 100, NodeAffinity is skipped): the
+// resolve's straight-line evaluation of one node, same arithmetic as filter /
+// total_score.  A zero request skips its Fit check, encoded as a -inf request.
+struct PodQ {
+  double rq_c, rq_m;  // Fit: request or -inf
+  int32_t wf, wb, cplus;
+};
+__device__ __forceinline__ PodQ pod_q(const PodDev &p, const Weights &w) {
+  PodQ q;
+  q.rq_c = ((p.flags & PF_HAS_REQ) && p.req_cpu > 0) ? p.req_cpu_d : -__builtin_inf();
+  q.rq_m = ((p.flags & PF_HAS_REQ) && p.req_mem > 0) ? p.req_mem_d : -__builtin_inf();
+  q.wf = w.fit;
+  q.wb = w.ba;
+  q.cplus = w.tt * 100;
+  return q;
+}
+__device__ __forceinline__ bool fit_q(const PodQ &q, const NodeRegs &g) {
+  return (g.bits & 2u) && !(q.rq_c > g.free_cpu) && !(q.rq_m > g.free_mem);
+}
+__device__ __forceinline__ uint64_t key_q(const PodDev &p, const PodQ &q, const NodeRegs &g) {
+  const int32_t t = (int32_t)__umul24((uint32_t)q.wf, (uint32_t)score_la(p, g)) +
+                    (int32_t)__umul24((uint32_t)q.wb, (uint32_t)score_ba(p, g)) + q.cplus;
+  return pack_key(t, g.slot);
+}
 
 template <bool EXT>
 __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
@@ -1563,31 +1612,50 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
         t2 = ts;
 #endif
         RNode post = pre;
-        rnode_add(post, s_pod[r]);
+        rnode_add(post, lds_uniform(s_pod[r], lane));
         if (on && lane < (uint32_t)NCAND) {
           s_post[buf][lane] = post;
           if (EXT) s_postx[buf][lane] = px;
         }
-        if (on && lane < (uint32_t)NCAND && r + 1 < nround) {
-          const PodDev &p1 = s_pod[r + 1];
-          int64_t tt_max = 0, na_max = 0;
-          if (EXT) {
-            tt_max = s_norm[r + 1][0];
-            na_max = s_norm[r + 1][1];
-          }
-          NodeExt e{};
-          if (EXT) ext_from_words(px.w, e);
+        if constexpr (!EXT) {
+          // straight-line for every lane (no branch keeps the pod loads from
+          // being hoisted into the candidate batch); stores predicated
+          const PodDev p1 = lds_uniform(s_pod[min(r + 1, nround - 1)], lane);
+          const PodQ q1 = pod_q(p1, a.w);
           const NodeRegs g0 = rnode_regs(pre, pre.row.rc, pre.row.rm, pre.row.np);
           const NodeRegs g1 = rnode_regs(post, post.row.rc, post.row.rm, post.row.np);
-          const int st0 = filter<EXT>(p1, a.clauses, g0, e);
-          const int st1 = filter<EXT>(p1, a.clauses, g1, e);
-          uint64_t key = 0;
-          if (st1 == ST_FEASIBLE) key = pack_key(total_score<EXT>(p1, a.clauses, g1, e, a.w, tt_max, na_max), post.slot);
-          int32_t d[NFILT + 3] = {0, 0, 0, 0, 0, 0, 0, 0};
-          if (st0 != st1) status_delta<EXT>(p1, a.clauses, st0, st1, e, post.slot, tt_max, na_max, d);
-          s_ekey[buf][lane] = key;
+          const bool f0 = fit_q(q1, g0), f1 = fit_q(q1, g1);
+          const uint64_t key = f1 ? key_q(p1, q1, g1) : 0ull;
+          if (on && lane < (uint32_t)NCAND && r + 1 < nround) {
+            s_ekey[buf][lane] = key;
+            // a commit only adds: feasible -> Fit failure is the only change
+            const int32_t lost = (f0 && !f1) ? 1 : 0;
+            s_edd[buf][lane][0] = lost;
 #pragma unroll
-          for (int qq = 0; qq < NFILT + 3; ++qq) s_edd[buf][lane][qq] = d[qq];
+            for (int qq = 1; qq < NFILT + 3; ++qq) s_edd[buf][lane][qq] = qq == 1 + KS_PLUGIN_FIT_IDX ? lost : 0;
+          }
+        } else if (r + 1 < nround) {
+          const PodDev p1 = lds_uniform(s_pod[r + 1], lane);  // every lane
+          if (on && lane < (uint32_t)NCAND) {
+            int64_t tt_max = 0, na_max = 0;
+            if (EXT) {
+              tt_max = s_norm[r + 1][0];
+              na_max = s_norm[r + 1][1];
+            }
+            NodeExt e{};
+            if (EXT) ext_from_words(px.w, e);
+            const NodeRegs g0 = rnode_regs(pre, pre.row.rc, pre.row.rm, pre.row.np);
+            const NodeRegs g1 = rnode_regs(post, post.row.rc, post.row.rm, post.row.np);
+            const int st0 = filter<EXT>(p1, a.clauses, g0, e);
+            const int st1 = filter<EXT>(p1, a.clauses, g1, e);
+            uint64_t key = 0;
+            if (st1 == ST_FEASIBLE) key = pack_key(total_score<EXT>(p1, a.clauses, g1, e, a.w, tt_max, na_max), post.slot);
+            int32_t d[NFILT + 3] = {0, 0, 0, 0, 0, 0, 0, 0};
+            if (st0 != st1) status_delta<EXT>(p1, a.clauses, st0, st1, e, post.slot, tt_max, na_max, d);
+            s_ekey[buf][lane] = key;
+#pragma unroll
+            for (int qq = 0; qq < NFILT + 3; ++qq) s_edd[buf][lane][qq] = d[qq];
+          }
         }
 #if KS_STAMPS == 2
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1610,8 +1678,18 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
         int32_t d[NFILT + 3] = {0, 0, 0, 0, 0, 0, 0, 0};
         bool dany = false;
         CandExt ox{};
-        if (mine) {
-          const PodDev &p1 = s_pod[r + 1];
+        if constexpr (!EXT) {
+          const PodDev p1 = lds_uniform(s_pod[r + 1], lane);
+          const PodQ q1 = pod_q(p1, a.w);
+          const NodeRegs g = rnode_regs(own, own.row.rc, own.row.rm, own.row.np);
+          const NodeRegs g0 = rnode_regs(own, own.rc0, own.rm0, own.np0);
+          const bool f0 = fit_q(q1, g0), f = fit_q(q1, g);
+          key = (mine && f) ? key_q(p1, q1, g) : 0ull;
+          dany = mine && f0 && !f;
+          d[0] = dany ? 1 : 0;
+          d[1 + KS_PLUGIN_FIT_IDX] = dany ? 1 : 0;
+        } else {
+          const PodDev p1 = lds_uniform(s_pod[r + 1], lane);
           int64_t tt_max = 0, na_max = 0;
           if (EXT) {
             tt_max = s_norm[r + 1][0];
@@ -1624,12 +1702,14 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
           }
           const NodeRegs g = rnode_regs(own, own.row.rc, own.row.rm, own.row.np);
           const NodeRegs g0 = rnode_regs(own, own.rc0, own.rm0, own.np0);
-          const int st0 = filter<EXT>(p1, a.clauses, g0, e);
-          const int st = filter<EXT>(p1, a.clauses, g, e);
-          if (st == ST_FEASIBLE) key = pack_key(total_score<EXT>(p1, a.clauses, g, e, a.w, tt_max, na_max), own.slot);
-          if (st0 != st) {
-            dany = true;
-            status_delta<EXT>(p1, a.clauses, st0, st, e, own.slot, tt_max, na_max, d);
+          if (mine) {  // p1 above is read by every lane (lds_uniform)
+            const int st0 = filter<EXT>(p1, a.clauses, g0, e);
+            const int st = filter<EXT>(p1, a.clauses, g, e);
+            if (st == ST_FEASIBLE) key = pack_key(total_score<EXT>(p1, a.clauses, g, e, a.w, tt_max, na_max), own.slot);
+            if (st0 != st) {
+              dany = true;
+              status_delta<EXT>(p1, a.clauses, st0, st, e, own.slot, tt_max, na_max, d);
+            }
           }
         }
         const uint64_t k1 = wave_max_u64_dpp(key);
