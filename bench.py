@@ -33,6 +33,10 @@ sys.path.insert(0, str(ROOT / "k8s-1m_amd"))
 
 B_NODE = 56  # algorithmic bytes per (pod, node) evaluation, resource-only
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+# VALU issue peak in lane-ops/s: 256 CUs x 4 SIMD-32 x 32 lanes x 2.4 GHz
+# (MI355X_MICROARCH.md: a wave64 VALU instruction issues over 2 cycles; 32-bit
+# rate -- binary64 instructions take twice as long, so the sweep's mix peaks lower)
+VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
 
 
 def parse():
@@ -176,6 +180,9 @@ def main():
                                "per launch at the default config; L2 memory-side bytes (Infinity-Cache hits "
                                "included)") if traffic else None,
             "valu_lane_ops_per_eval": pmc.get("valu_lane_ops_per_eval"),
+            # the sweep re-reads each node row once per pod group, not once per
+            # pod, so its HBM fraction exceeds 1; the binding resource is VALU issue
+            "valu": valu_roofline(pmc, evals_per_launch, sweep_avg_ms),
         },
         "cpu_baseline": cpu,
         "extra": {
@@ -196,6 +203,16 @@ def main():
     sched.close()
     if rank == 0:
         print(json.dumps(line), flush=True)
+
+
+def valu_roofline(pmc, evals_per_launch, sweep_avg_ms):
+    ops = pmc.get("valu_lane_ops_per_eval")
+    if not ops or not sweep_avg_ms:
+        return None
+    achieved = ops * evals_per_launch / (sweep_avg_ms * 1e-3) / 1e12
+    return {"achieved": round(achieved, 2), "peak": round(VALU_PEAK_TOPS, 2), "unit": "T lane-ops/s",
+            "frac": round(achieved / VALU_PEAK_TOPS, 4),
+            "source": "SQ_INSTS_VALU x 64 per evaluation from the PMC file; 32-bit issue-rate peak"}
 
 
 def uid_path(world: int) -> Path:
