@@ -1090,9 +1090,9 @@ constexpr int RHASH = 1024;
 constexpr int LSEL = 4;                                   // listed candidates kept per list wave
 constexpr int LAHEAD = 3;                                 // list waves select pod i + LAHEAD in iteration i
 constexpr int KAHEAD = 3;                                 // ... with keys fetched KAHEAD iterations before
-constexpr int KSLOTS = 8, RSLOTS = 4;                     // key / row staging slots (by pod mod)
+constexpr int KSLOTS = 8, RSLOTS = 8;                     // key / row staging slots (by pod mod)
 static_assert(LSEL > LAHEAD, "a selection LAHEAD pods ahead must survive the LAHEAD commits before it is used");
-static_assert(KSLOTS >= LAHEAD + KAHEAD + 1 && RSLOTS >= LAHEAD + 1, "staging depth");
+static_assert(KSLOTS >= LAHEAD + KAHEAD + 1 && RSLOTS >= LAHEAD + 2, "staging depth (rows live until the owners apply)");
 typedef __attribute__((address_space(1))) void gvoid_t;  // global_load_lds operands
 typedef __attribute__((address_space(3))) void lvoid_t;
 constexpr int NCAND_OWN = 2 * RES_OWN_WAVES;              // lanes [0, 8): owner waves' best two
@@ -1277,7 +1277,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
   // list waves' candidates for pod i (chosen in iteration i - LAHEAD), by i mod RSLOTS
   __shared__ uint64_t s_lkey[RSLOTS][NCAND_LIST];
   __shared__ uint32_t s_lidx[RSLOTS][NCAND_LIST];  // list index, NONE32 = none
-  // eval wave: each candidate of pod i committed, for pod i+1 (by parity of i)
+  // eval wave: each candidate of pod i committed, its key / status change for pod i+1 (by parity of i)
   __shared__ RNode s_post[2][NCAND];
   __shared__ CandExt s_postx[EXT ? 2 : 1][EXT ? NCAND : 1];
   __shared__ uint64_t s_ekey[2][NCAND];
@@ -1565,33 +1565,33 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
         const bool is_prev = lane == (uint32_t)CAND_PREV;
         const uint32_t lo = is_own ? lane : 0u, c = is_lst ? lane - NCAND_OWN : 0u;
         const uint32_t cw = c / LSEL, ck = c % LSEL;
-        const uint32_t pv = s_pend[nb][0], pc = min(s_pend[nb][1], (uint32_t)NCAND - 1);  // pod r-1's commit
+        // one batch: the candidate's row (owner: published node; listed: DMA
+        // pieces) and round-start fields, independent of the last commit; the
+        // previous winner (lane 24) follows once the commit record is in
+        const uint4 *rp = is_own ? (const uint4 *)&s_ocand[buf][lo] : &s_lrowb[b4][cw][0][ck];
+        const uint32_t rstride = is_own ? 1u : (uint32_t)LSEL;
+        RNode pre;
+        uint4 *pp = (uint4 *)&pre;
+#pragma unroll
+        for (int j = 0; j < ROW_PIECES; ++j) pp[j] = rp[j * rstride];
+        const uint4 tail = is_own ? rp[ROW_PIECES] : make_uint4(0, 0, 0, 0);       // rc0, rm0
+        const uint4 tail2 = is_own ? rp[ROW_PIECES + 1] : make_uint4(0, 0, 0, 0);  // np0, slot
+        CandExt px{};
+        if constexpr (EXT) {
+          const uint4 *xp = is_own ? (const uint4 *)&s_ocandx[buf][lo] : &s_lrowb[b4][cw][ROW_PIECES][ck];
+          uint4 *xo = (uint4 *)&px;
+#pragma unroll
+          for (int j = 0; j < EXT_PIECES; ++j) xo[j] = xp[j * rstride];
+        }
+        const uint64_t lkey = s_lkey[b4][c];
+        const uint32_t pv = uniform_u32(s_pend[nb][0]);
+        const uint32_t pc = min(uniform_u32(s_pend[nb][1]), (uint32_t)NCAND - 1);  // pod r-1's commit
 #if KS_STAMPS == 2
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         STAMP_NOW(ts);
         sub[0] += ts - t0;
         t2 = ts;
 #endif
-        // one batch: the candidate's row (owner: published node; listed: DMA
-        // pieces; previous winner: its committed node), round-start fields
-        const uint4 *rp = is_own ? (const uint4 *)&s_ocand[buf][lo]
-                                 : is_prev ? (const uint4 *)&s_post[nb][pc] : &s_lrowb[b4][cw][0][ck];
-        const uint32_t rstride = (is_own || is_prev) ? 1u : (uint32_t)LSEL;
-        RNode pre;
-        uint4 *pp = (uint4 *)&pre;
-#pragma unroll
-        for (int j = 0; j < ROW_PIECES; ++j) pp[j] = rp[j * rstride];
-        const uint4 tail = is_lst ? make_uint4(0, 0, 0, 0) : rp[ROW_PIECES];  // rc0, rm0
-        const uint4 tail2 = is_lst ? make_uint4(0, 0, 0, 0) : rp[ROW_PIECES + 1];  // np0, slot
-        CandExt px{};
-        if constexpr (EXT) {
-          const uint4 *xp = is_own ? (const uint4 *)&s_ocandx[buf][lo]
-                                   : is_prev ? (const uint4 *)&s_postx[nb][pc] : &s_lrowb[b4][cw][ROW_PIECES][ck];
-          uint4 *xo = (uint4 *)&px;
-#pragma unroll
-          for (int j = 0; j < EXT_PIECES; ++j) xo[j] = xp[j * rstride];
-        }
-        const uint64_t lkey = s_lkey[b4][c];
         const bool on = is_own ? s_okey[buf][lo] != 0 : is_lst ? s_lidx[b4][c] != NONE32 : (is_prev && pv != 0);
         if (is_lst) {
           pre.rc0 = pre.row.rc;
@@ -1605,6 +1605,10 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
           pre.slot = tail2.y;
         }
         pre._pad[0] = pre._pad[1] = 0;
+        if (is_prev && pv) {  // the previous winner: its committed node, from the last iteration
+          pre = s_post[nb][pc];
+          if (EXT) px = s_postx[nb][pc];
+        }
 #if KS_STAMPS == 2
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         STAMP_NOW(ts);
@@ -1613,7 +1617,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
 #endif
         RNode post = pre;
         rnode_add(post, lds_uniform(s_pod[r], lane));
-        if (on && lane < (uint32_t)NCAND) {
+        if (on && lane < (uint32_t)NCAND) {  // lane 24 of the next iteration reads the winner's
           s_post[buf][lane] = post;
           if (EXT) s_postx[buf][lane] = px;
         }
@@ -1667,11 +1671,29 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
     } else if (is_owner) {
       if (ROLE_ON(2)) {
       // ------------------------------------------------------- owner waves
-      if (r >= 1 && s_pend[nb][0] && s_pend[nb][3] == mj) {  // apply pod r-1's commit
-        const uint32_t pc = s_pend[nb][1];
-        own = s_post[nb][pc];
-        if (EXT && s_pend[nb][2]) s_modx[mj] = s_postx[nb][pc];
-        mine = true;
+      if (r >= 1) {  // apply pod r-1's commit: its winner's owner adds the pod
+        const uint32_t pv = uniform_u32(s_pend[nb][0]), pc = uniform_u32(s_pend[nb][1]);
+        const uint32_t pj = uniform_u32(s_pend[nb][2]), po = uniform_u32(s_pend[nb][3]);
+        const PodDev pp = lds_uniform(s_pod[r - 1], lane);  // every lane (readfirstlane)
+        if (pv && po == mj) {
+          if (pj) {  // a listed node joins: its row (DMA-staged for pod r-1, still resident)
+            const uint32_t b8 = (r - 1) % RSLOTS, c = pc - NCAND_OWN, cw = c / LSEL, ck = c % LSEL;
+            CandRow w;
+            uint4 *wp = (uint4 *)&w;
+#pragma unroll
+            for (int j = 0; j < ROW_PIECES; ++j) wp[j] = s_lrowb[b8][cw][j][ck];
+            own = rnode_from_row(w, 0xFFFFFFFFu - (uint32_t)s_lkey[b8][c]);
+            if constexpr (EXT) {
+              CandExt x;
+              uint4 *xp = (uint4 *)&x;
+#pragma unroll
+              for (int j = 0; j < EXT_PIECES; ++j) xp[j] = s_lrowb[b8][cw][ROW_PIECES + j][ck];
+              s_modx[mj] = x;
+            }
+            mine = true;
+          }
+          rnode_add(own, pp);
+        }
       }
       if (r + 1 < nround && __ballot(mine) != 0) {
         uint64_t key = 0;
