@@ -724,7 +724,14 @@ uint32_t blocks_per_shard(const Shard &s, uint32_t sub) { return (s.waves * sub 
 
 // Sweep / prescore kernel width: fewer nodes per lane when label/taint
 // columns are held too (register budget).
-uint32_t kernel_npl(const ks_ctx *c, bool ext) { return ext ? std::min<uint32_t>(c->npl, 2) : c->npl; }
+uint32_t kernel_npl(const ks_ctx *c, bool ext) {
+  static const uint32_t ext_npl = [] {  // KS_EXT_NPL: geometry experiments only
+    const char *e = std::getenv("KS_EXT_NPL");
+    const int v = e ? std::atoi(e) : 2;
+    return (uint32_t)(v == 4 || v == 8 ? v : 2);
+  }();
+  return ext ? std::min<uint32_t>(c->npl, ext_npl) : c->npl;
+}
 
 hipEvent_t get_event(ks_ctx *c) {
   if (!c->ev_pool.empty()) {

@@ -199,6 +199,7 @@ __device__ __forceinline__ void load_core(const NodeTable &t, uint32_t pos, uint
   r = make_regs(t.acpu[pos], t.amem[pos], t.rcpu[pos], t.rmem[pos], t.zcpu[pos], t.zmem[pos], ap, t.npods[pos], slot);
 }
 
+template <int LWU = LW>
 __device__ __forceinline__ void load_ext(const NodeTable &t, uint32_t pos, bool valid, NodeExt &e) {
   if (!valid) {
     e.hard = e.prefer = 0;
@@ -211,7 +212,7 @@ __device__ __forceinline__ void load_ext(const NodeTable &t, uint32_t pos, bool 
   e.hard = t.hard[pos];
   e.prefer = t.prefer[pos];
 #pragma unroll
-  for (int k = 0; k < LW; ++k) e.lab[k] = k < (int)t.lw ? t.lab[(size_t)k * t.npos + pos] : 0ull;
+  for (int k = 0; k < LW; ++k) e.lab[k] = (k < LWU && k < (int)t.lw) ? t.lab[(size_t)k * t.npos + pos] : 0ull;
 #pragma unroll
   for (int k = 0; k < NNUM; ++k) e.num[k] = t.num[(size_t)k * t.npos + pos];
 }
@@ -386,6 +387,99 @@ __device__ __forceinline__ PodDev load_pod(const PodDev *pods, uint32_t i) {
   return pods[i];
 }
 
+
+// ------------------------------------------------ sweep: EXT pods, NPL nodes
+// The sweep evaluates a pod's label programs clause-outer, node-inner: each
+// clause's words are read once per pod (scalar loads) and applied to the
+// lane's NPL nodes.  Label words beyond the dictionary's (LWU, a template parameter) are not
+// read: straight-line AND / OR over the words in use, no per-word branches.
+template <int NPL, int LWU>
+__device__ __forceinline__ void clause_pass_n(const uint64_t *c, const NodeExt (&e)[NPL], const NodeRegs (&nr)[NPL],
+                                              bool (&pass)[NPL]) {
+  const uint64_t w0 = c[0];
+  const uint32_t kind = (uint32_t)w0 & 0xFF;
+  uint64_t m[LWU];
+#pragma unroll
+  for (int k = 0; k < LWU; ++k) m[k] = c[1 + k];
+  const int64_t x = (int64_t)c[5];
+  const bool col1 = (w0 >> 8) & 1u;
+  static_for<NPL>([&](auto J) {
+    constexpr int j = J;
+    uint64_t acc = 0;
+#pragma unroll
+    for (int k = 0; k < LWU; ++k) acc |= e[j].lab[k] & m[k];
+    const bool any = acc != 0;
+    bool ok;
+    switch (kind) {
+      case CK_ANY: ok = any; break;
+      case CK_NONE: ok = !any; break;
+      case CK_GT: ok = any && (col1 ? e[j].num[1] : e[j].num[0]) > x; break;
+      case CK_LT: ok = any && (col1 ? e[j].num[1] : e[j].num[0]) < x; break;
+      case CK_NAME_EQ: ok = (int64_t)nr[j].slot == x; break;
+      case CK_NAME_NE: ok = (int64_t)nr[j].slot != x; break;
+      default: ok = false; break;
+    }
+    pass[j] = ok;
+  });
+}
+
+// required_match for NPL nodes at once
+template <int NPL, int LWU>
+__device__ __forceinline__ void required_match_n(const PodDev &p, const uint64_t *clauses, const NodeExt (&e)[NPL],
+                                                 const NodeRegs (&nr)[NPL], bool (&out)[NPL]) {
+  bool sel[NPL], any[NPL], cur[NPL];
+  static_for<NPL>([&](auto J) { sel[J] = true; any[J] = false; cur[J] = true; });
+  uint32_t curterm = 0;
+  const uint64_t *c = clauses + (size_t)p.req_off * CLAUSE_WORDS;
+  for (uint32_t k = 0; k < p.req_len; ++k, c += CLAUSE_WORDS) {
+    const uint32_t term = uniform_u32(((uint32_t)c[0] >> 16) & 0xFFFF);
+    if (term != curterm) {
+      if (curterm >= 1) static_for<NPL>([&](auto J) { any[J] |= cur[J]; });
+      static_for<NPL>([&](auto J) { cur[J] = true; });
+      curterm = term;
+    }
+    bool pass[NPL];
+    clause_pass_n<NPL, LWU>(c, e, nr, pass);
+    if (term == 0) static_for<NPL>([&](auto J) { sel[J] &= pass[J]; });
+    else static_for<NPL>([&](auto J) { cur[J] &= pass[J]; });
+  }
+  if (curterm >= 1) static_for<NPL>([&](auto J) { any[J] |= cur[J]; });
+  static_for<NPL>([&](auto J) { out[J] = sel[J] && (p.n_req_terms == 0 || any[J]); });
+}
+
+// preferred_raw for NPL nodes at once
+template <int NPL, int LWU>
+__device__ __forceinline__ void preferred_raw_n(const PodDev &p, const uint64_t *clauses, const NodeExt (&e)[NPL],
+                                                const NodeRegs (&nr)[NPL], uint32_t (&raw)[NPL]) {
+  bool cur[NPL];
+  static_for<NPL>([&](auto J) { raw[J] = 0u; cur[J] = true; });
+  uint32_t curterm = 0, wcur = 0;
+  const uint64_t *c = clauses + (size_t)p.pref_off * CLAUSE_WORDS;
+  for (uint32_t k = 0; k < p.pref_len; ++k, c += CLAUSE_WORDS) {
+    const uint32_t term = uniform_u32(((uint32_t)c[0] >> 16) & 0xFFFF);
+    if (term != curterm) {
+      if (curterm >= 1) static_for<NPL>([&](auto J) { raw[J] += cur[J] ? wcur : 0u; });
+      static_for<NPL>([&](auto J) { cur[J] = true; });
+      curterm = term;
+      wcur = uniform_u32((uint32_t)(c[0] >> 32));
+    }
+    bool pass[NPL];
+    clause_pass_n<NPL, LWU>(c, e, nr, pass);
+    static_for<NPL>([&](auto J) { cur[J] &= pass[J]; });
+  }
+  if (curterm >= 1) static_for<NPL>([&](auto J) { raw[J] += cur[J] ? wcur : 0u; });
+}
+
+// DefaultNormalizeScore's floor(100 * raw / max) for 0 <= raw <= max < 2^25
+// from inv = RN(1 / max) (0 for max == 0, giving 0): the product is within
+// 2^-44 of the quotient (<= 100), whose fractional part is 0 or >= 2^-25, so
+// 2^-40 lifts exact quotients above the rounding error without reaching the
+// next integer: truncation is the exact floor.
+constexpr double NORM_EPS = 0x1p-40;
+__device__ __forceinline__ uint32_t normalize_inv(uint32_t raw, double inv) {
+  return (uint32_t)__builtin_fma((double)(100u * raw), inv, NORM_EPS);
+}
+
 // =================================================================== sweep
 // Normalising plugins (TaintToleration with PreferNoSchedule taints, NodeAffinity
 // preferred terms) score against max raw over the feasible nodes, which is
@@ -397,7 +491,7 @@ __device__ __forceinline__ PodDev load_pod(const PodDev *pods, uint32_t i) {
 // grid: x = block within shard, y = pod group, z = local shard.
 constexpr uint32_t KEY32_POS_BITS = 9, KEY32_POS_MASK = (1u << KEY32_POS_BITS) - 1;
 
-template <int NPL, bool EXT>
+template <int NPL, bool EXT, int LWU = LW>
 __global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
   static_assert(NPL * WAVE <= (1 << KEY32_POS_BITS), "wave-local key position field");
   constexpr int NW = SWEEP_THREADS / WAVE;
@@ -428,7 +522,7 @@ __global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
     const uint32_t l = (j0 + (uint32_t)j) * WAVE * s.waves + lane * s.waves + lwave;
     const uint32_t pos = s.base + kw * WAVE * NPL + (uint32_t)j * WAVE + lane;
     load_core(a.t, pos, s.lo + l, kw < kwaves && l < s.count, nr[j]);
-    if constexpr (EXT) load_ext(a.t, pos, nr[j].bits & 1u, ne[j]);
+    if constexpr (EXT) load_ext<LWU>(a.t, pos, nr[j].bits & 1u, ne[j]);
   });
 
   // per node, pod-independent: pod-count fit (also false for empty slots), and
@@ -446,10 +540,10 @@ __global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
     const uint32_t r = pi - start;
     if (fix && uniform_u32(a.fix_flag[r]) == 0) continue;
     const PodDev p = load_pod(a.pods, pi);
-    int64_t tt_max = 0, na_max = 0;
+    uint32_t tt_max = 0, na_max = 0;
     if (EXT && (p.flags & (PF_TT | PF_NA))) {
-      tt_max = fix ? a.norm_max[2 * r + 0] : p.tt_guess;
-      na_max = fix ? a.norm_max[2 * r + 1] : p.na_guess;
+      tt_max = uniform_u32(fix ? a.norm_max[2 * r + 0] : p.tt_guess);
+      na_max = uniform_u32(fix ? a.norm_max[2 * r + 1] : p.na_guess);
     }
     // lane top-2 of wave-local 32-bit keys (TotalScore + 1) << 9 | ~(step * 64 + lane):
     // within a wave slot order is (step, lane) order, so these sort like packed keys
@@ -475,26 +569,57 @@ __global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
       });
       f4 = vcount - feas;
     } else {
+      // label programs once per pod for the lane's NPL nodes
+      bool aff[NPL];
+      uint32_t praw[NPL];
+      static_for<NPL>([&](auto J) { aff[J] = true; praw[J] = 0u; });
+      if (p.flags & PF_AFF) required_match_n<NPL, LWU>(p, a.clauses, ne, nr, aff);
+      if (p.flags & PF_NA) preferred_raw_n<NPL, LWU>(p, a.clauses, ne, nr, praw);
+      const double inv_tt = tt_max ? 1.0 / (double)tt_max : 0.0;
+      const double inv_na = na_max ? 1.0 / (double)na_max : 0.0;
+      const double rq_c = ((p.flags & PF_HAS_REQ) && p.req_cpu > 0) ? p.req_cpu_d : -__builtin_inf();
+      const double rq_m = ((p.flags & PF_HAS_REQ) && p.req_mem > 0) ? p.req_mem_d : -__builtin_inf();
+      const bool ext = p.flags & PF_EXT;
+      const bool named = p.name_slot != -1;
       static_for<NPL>([&](auto J) {
         constexpr int j = J;
         const bool valid = nr[j].bits & 1u;
-        // branch-free: every lane scores its node (empty slots hold benign
-        // values) and the feasibility mask selects
-        const int st = valid ? filter<EXT>(p, a.clauses, nr[j], ne[j]) : ST_EMPTY;
+        // filter chain in profile order (NodeUnschedulable, NodeName,
+        // TaintToleration, NodeAffinity, NodeResourcesFit), branch-free:
+        // every lane scores its node and the feasibility mask selects
+        int st = ST_FEASIBLE;
+        const bool fitfail = !podfit[j] || (rq_c > nr[j].free_cpu) || (rq_m > nr[j].free_mem);
+        if (fitfail) st = 4;
+        if (ext) {
+          const uint64_t untol = ne[j].hard & ~p.tol_hard;
+          if (!aff[j]) st = 3;
+          if (untol) st = 2;
+          if (named && (int64_t)nr[j].slot != (int64_t)p.name_slot) st = 1;
+          if (untol & UNSCHED_BIT) st = 0;
+        }
+        if (!valid) st = ST_EMPTY;
         const bool feasible = st == ST_FEASIBLE;
-        const uint32_t tot1 = (uint32_t)total_score<EXT>(p, a.clauses, nr[j], ne[j], a.w, tt_max, na_max) + 1u;
-        const uint32_t key = feasible ? (tot1 << KEY32_POS_BITS) | (kpos0 - (uint32_t)j * WAVE) : 0u;
+        uint32_t tot1 = (uint32_t)__umul24((uint32_t)a.w.fit, (uint32_t)score_la(p, nr[j])) +
+                        (uint32_t)__umul24((uint32_t)a.w.ba, (uint32_t)score_ba(p, nr[j])) + 1u;
+        uint32_t tts = 100u;
         bool at_tt = false, at_na = false;
         if (p.flags & PF_TT) {
-          const uint32_t raw = (uint32_t)taint_raw(p, ne[j]);
-          at_tt = feasible && raw == (uint32_t)tt_max;
+          const uint32_t raw = (uint32_t)__popcll(ne[j].prefer & ~p.tol_prefer);
+          tts = 100u - normalize_inv(raw, inv_tt);
+          at_tt = feasible && raw == tt_max;
           tmx = max(tmx, feasible ? raw : 0u);
         }
-        if (p.flags & PF_NA) {
-          const uint32_t raw = (uint32_t)preferred_raw(p, a.clauses, ne[j], nr[j].slot);
-          at_na = feasible && raw == (uint32_t)na_max;
-          nmx = max(nmx, feasible ? raw : 0u);
+        tot1 += (uint32_t)__umul24((uint32_t)a.w.tt, tts);
+        if (p.flags & PF_HAS_PREF) {
+          uint32_t nas = 0u;
+          if (p.flags & PF_NA) {
+            nas = normalize_inv(praw[j], inv_na);
+            at_na = feasible && praw[j] == na_max;
+            nmx = max(nmx, feasible ? praw[j] : 0u);
+          }
+          tot1 += (uint32_t)__umul24((uint32_t)a.w.na, nas);
         }
+        const uint32_t key = feasible ? (tot1 << KEY32_POS_BITS) | (kpos0 - (uint32_t)j * WAVE) : 0u;
         b2 = max(b2, min(b1, key));
         b1 = max(b1, key);
         const uint64_t fb = __ballot(feasible), vb = __ballot(valid);
@@ -1979,9 +2104,19 @@ hipError_t launch_sweep(const RoundArgs &a, bool ext, uint32_t nblocks, uint32_t
                         hipStream_t st) {
   dim3 g(nblocks, ngroups, nshards);
   if (ext) {
-    if (a.npl == 2) sweep_kernel<2, true><<<g, SWEEP_THREADS, 0, st>>>(a);
-    else if (a.npl == 4) sweep_kernel<4, true><<<g, SWEEP_THREADS, 0, st>>>(a);
-    else sweep_kernel<8, true><<<g, SWEEP_THREADS, 0, st>>>(a);
+    // label words in use (dictionary size): 1, 2 or 4 words per node are read
+    const int lwu = a.t.lw <= 1 ? 1 : a.t.lw <= 2 ? 2 : 4;
+    if (a.npl == 2) {
+      if (lwu == 1) sweep_kernel<2, true, 1><<<g, SWEEP_THREADS, 0, st>>>(a);
+      else if (lwu == 2) sweep_kernel<2, true, 2><<<g, SWEEP_THREADS, 0, st>>>(a);
+      else sweep_kernel<2, true, 4><<<g, SWEEP_THREADS, 0, st>>>(a);
+    } else if (a.npl == 4) {
+      if (lwu == 1) sweep_kernel<4, true, 1><<<g, SWEEP_THREADS, 0, st>>>(a);
+      else if (lwu == 2) sweep_kernel<4, true, 2><<<g, SWEEP_THREADS, 0, st>>>(a);
+      else sweep_kernel<4, true, 4><<<g, SWEEP_THREADS, 0, st>>>(a);
+    } else {
+      sweep_kernel<8, true, 4><<<g, SWEEP_THREADS, 0, st>>>(a);
+    }
   } else {
     if (a.npl == 2) sweep_kernel<2, false><<<g, SWEEP_THREADS, 0, st>>>(a);
     else if (a.npl == 4) sweep_kernel<4, false><<<g, SWEEP_THREADS, 0, st>>>(a);
