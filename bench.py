@@ -17,6 +17,14 @@ is compiled and uploaded by ks_batch_prepare beforehand).  With --gpus N the
 node slots are sharded across N ranks (one process per GPU, RCCL candidate
 all-gather); every rank schedules the same pods, so `value` is the job's
 pods/s (strong scaling: the cluster is fixed at 1M nodes).
+
+--kind labeled is configs[3] (C4: label bitsets, nodeSelector / required and
+preferred NodeAffinity, NoSchedule / NoExecute / PreferNoSchedule taints).
+--workload c5 is configs[4] (C5): a step is one burst (default 100k pods)
+scheduled to completion followed by the seeded watch-event log (5 % of the
+bound pods deleted, 0.1 % node updates, 0.01 % node deletes + adds) applied
+to the device cache through the C ABI; the timed region holds both, the
+host-side generation and marshalling of the log do not (ksched/stream.py).
 """
 from __future__ import annotations
 
@@ -32,6 +40,7 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "k8s-1m_amd"))
 
 B_NODE = 56  # algorithmic bytes per (pod, node) evaluation, resource-only
+B_NODE_LABELED = 96  # ... with label / taint bitsets (C4)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # VALU issue peak in lane-ops/s: 256 CUs x 4 SIMD-32 x 32 lanes x 2.4 GHz
 # (MI355X_MICROARCH.md: a wave64 VALU instruction issues over 2 cycles; 32-bit
@@ -50,6 +59,9 @@ def parse():
     ap.add_argument("--topk", type=int, default=0)
     ap.add_argument("--nodes-per-lane", type=int, default=4)
     ap.add_argument("--kind", default="hetero", choices=["hetero", "kwok", "labeled"])
+    ap.add_argument("--workload", default="batch", choices=["batch", "c5"],
+                    help="batch: one batch of --batch pods per step; c5: one burst + its event log per step")
+    ap.add_argument("--burst", type=int, default=100_000, help="pods per burst (--workload c5)")
     ap.add_argument("--prefill", type=float, default=0.5)
     ap.add_argument("--cpu-pods", type=int, default=40, help="oracle sample size (pods), single thread")
     ap.add_argument("--cpu-threads", type=int, default=16, help="oracle threads for cpu_baseline (box CPU share)")
@@ -82,6 +94,8 @@ def main():
         if rank == 0:  # ncclCommInitRank returned: every rank has read the id
             uid_path(world).unlink(missing_ok=True)
 
+    if args.workload == "c5":
+        return run_c5(args, kind, sched, world, rank, t_setup)
     nodes = synth.nodes(kind, args.nodes, 1)
     slots = synth.slot_array(args.nodes)
     sched.upsert_nodes_raw(nodes.nodes, slots, args.nodes)
@@ -117,10 +131,6 @@ def main():
     sched.set_timing(False)
     if world > 1:
         elapsed = sched.allreduce_max([elapsed])[0]
-    st = sched.stats()
-    dbg = (C.c_uint64 * 16)()
-    sched.lib.ks_debug_counters(sched.ctx, dbg)
-
     # scheduled fraction of the timed pods (sanity for the reader)
     scheduled = 0
     for b in range(args.warmup, n_batches):
@@ -128,19 +138,108 @@ def main():
         scheduled += int((r["status"] == 0).sum())
 
     pods_timed = args.steps * args.batch
-    value = pods_timed / elapsed
-    nodes_local = args.nodes // world
-    sweep_avg_ms = st.sweep_ms / max(1, st.sweep_launches)
-    evals_per_launch = st.sweep_evals / max(1, st.sweep_launches)
-    achieved = B_NODE * evals_per_launch / (sweep_avg_ms * 1e-3) / 1e9 if st.sweep_launches else None
-    traffic, pmc = None, {}
-    if args.pmc_file and Path(args.pmc_file).exists():
-        pmc = json.loads(Path(args.pmc_file).read_text())
-        traffic = pmc.get("hbm_bytes_per_sweep_launch")
-
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_pods > 0:
         cpu = cpu_baseline(args, kind, nodes, slots, pre, pods)
+    line = report(args, sched, world, pods_timed, elapsed, scheduled, setup_s, cpu)
+    for b in batches:
+        sched.free(b)
+    sched.close()
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+
+
+def run_c5(args, kind, sched, world, rank, t_setup):
+    """configs[4] (C5): bursts scheduled to completion, each followed by its
+    watch-event log applied through ks_pods_remove / ks_nodes_upsert /
+    ks_nodes_delete.  Timed per step: the burst's ks_batch_run plus the log's
+    ABI calls; the log's generation (which needs the burst's bindings) and its
+    marshalling to ABI structs run outside the timed region."""
+    from ksched.framework import results_to_arrays
+    from ksched.stream import BurstStream, GpuTarget
+
+    n_bursts = args.warmup + args.steps
+    stream = BurstStream(kind, args.nodes, n_bursts, args.burst, prefill=3)
+    target = GpuTarget(sched)
+    stream.setup([target])
+    setup_s = time.time() - t_setup
+
+    def barrier():
+        if world > 1:
+            sched.allreduce_max([0.0])
+
+    t_run = t_ev = 0.0
+    scheduled = n_events = 0
+    for b in range(n_bursts):
+        timed = b >= args.warmup
+        if b == args.warmup:
+            sched.reset_stats()
+            sched.set_timing(True)
+        arr, m = stream.burst_pods(b)
+        batch = sched.prepare(arr, m)
+        barrier()
+        t0 = time.perf_counter()
+        sched.run(batch)  # returns after the scheduler stream has drained
+        barrier()
+        dt = time.perf_counter() - t0
+        res = sched.results(batch, m)
+        if timed:
+            t_run += dt
+            r = results_to_arrays(res, m)
+            scheduled += int((r["status"] == 0).sum())
+        stream.record(b, res)
+        sched.free(batch)
+        ops = stream.marshal(stream.make_events())  # the API server's side, untimed
+        barrier()
+        t0 = time.perf_counter()
+        stream.apply_marshalled(ops, [target])  # each ABI call returns with its device work done
+        barrier()
+        dt = time.perf_counter() - t0
+        if timed:
+            t_ev += dt
+            n_events += sum(o[3] for o in ops)
+    sched.set_timing(False)
+    elapsed = t_run + t_ev
+    if world > 1:
+        elapsed = sched.allreduce_max([elapsed])[0]
+    pods_timed = args.steps * args.burst
+    c5 = {"burst_ms_mean": round(1e3 * t_run / args.steps, 3), "events_ms_mean": round(1e3 * t_ev / args.steps, 3),
+          "events_per_burst": round(n_events / args.steps, 1),
+          "events_per_s": round(n_events / t_ev, 1) if t_ev else None,
+          "bound_pods_after": int(len(stream.bound_pod))}
+    line = report(args, sched, world, pods_timed, elapsed, scheduled, setup_s, None, c5=c5)
+    sched.close()
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+
+
+WORKLOADS = {
+    "hetero": "C3: {n} heterogeneous kwok-shaped nodes, prefill<{f:.0%} cpu, resource-only pods; "
+              "Fit+LeastAllocated+BalancedAllocation+TaintToleration, pct=100, in-order commit",
+    "kwok": "C1 shape at scale: {n} homogeneous kwok nodes, prefill<{f:.0%} cpu, resource-only pods; "
+            "Fit+LeastAllocated+BalancedAllocation+TaintToleration, pct=100, in-order commit",
+    "labeled": "C4: {n} nodes with label bitsets and NoSchedule/NoExecute/PreferNoSchedule taints, "
+               "prefill<{f:.0%} cpu; pods with nodeSelector / required + preferred NodeAffinity / "
+               "tolerations; all default Filter + Score plugins incl. TaintToleration and NodeAffinity "
+               "normalisation, pct=100, in-order commit",
+}
+
+
+def report(args, sched, world, pods_timed, elapsed, scheduled, setup_s, cpu, c5=None):
+    st = sched.stats()
+    dbg = (C.c_uint64 * 16)()
+    sched.lib.ks_debug_counters(sched.ctx, dbg)
+    value = pods_timed / elapsed
+    labeled = args.kind == "labeled"
+    b_node = B_NODE_LABELED if labeled else B_NODE
+    sweep_avg_ms = st.sweep_ms / max(1, st.sweep_launches)
+    evals_per_launch = st.sweep_evals / max(1, st.sweep_launches)
+    achieved = b_node * evals_per_launch / (sweep_avg_ms * 1e-3) / 1e9 if st.sweep_launches else None
+    traffic, pmc = None, {}
+    # the PMC file was measured on the default (C3) workload: used for C3 lines only
+    if args.pmc_file and Path(args.pmc_file).exists() and args.kind == "hetero" and args.workload == "batch":
+        pmc = json.loads(Path(args.pmc_file).read_text())
+        traffic = pmc.get("hbm_bytes_per_sweep_launch")
 
     line = {
         "metric": "pods scheduled/sec at 1M nodes (1/2/4/8 GPU) + % of HBM roofline",
@@ -156,10 +255,9 @@ def main():
         "dtype": "int64+f64",
         "data": "synthetic (seeded kwok-shaped cluster and pod stream, libksynth)",
         "config": {
-            "workload": f"C3: {args.nodes} {args.kind} nodes, prefill<{args.prefill:.0%} cpu, resource-only pods; "
-                        "Fit+LeastAllocated+BalancedAllocation+TaintToleration, pct=100, in-order commit",
+            "workload": WORKLOADS[args.kind].format(n=args.nodes, f=args.prefill),
             "nodes": args.nodes,
-            "pods_per_step": args.batch,
+            "pods_per_step": args.burst if c5 else args.batch,
             "pods_per_round": args.pods_per_round,
             "topk": args.topk or args.pods_per_round,
             "parallelism": f"node-sharded x{world} (RCCL all-gather)" if world > 1 else "1 GPU",
@@ -173,7 +271,7 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
             "traffic": traffic,
             "kernel": "ks::sweep_kernel",
-            "bytes_per_eval": B_NODE,
+            "bytes_per_eval": b_node,
             "evals_per_launch": int(evals_per_launch),
             "avg_launch_ms": round(sweep_avg_ms, 4),
             "traffic_source": (f"profiles/{Path(args.pmc_file).name} ({pmc.get('tag')}): 2 x FETCH_SIZE + WRITE_SIZE "
@@ -198,11 +296,16 @@ def main():
             "setup_s": round(setup_s, 2),
         },
     }
-    for b in batches:
-        sched.free(b)
-    sched.close()
-    if rank == 0:
-        print(json.dumps(line), flush=True)
+    if c5:
+        line["config"]["workload"] = (
+            f"C5: {args.nodes} heterogeneous nodes, prefill<50% cpu; bursts of {args.burst} resource-only pods, "
+            "each followed by its watch-event log (5% bound-pod deletes, 0.1% node updates, 0.01% node "
+            "deletes + adds) applied to the device cache; pct=100, in-order commit")
+        line["config"]["bursts_timed"] = args.steps
+        line["extra"].update(c5)
+    return line
+
+
 
 
 def valu_roofline(pmc, evals_per_launch, sweep_avg_ms):

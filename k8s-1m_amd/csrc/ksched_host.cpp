@@ -148,6 +148,7 @@ struct ks_batch {
   uint32_t dict_version = 0;
   bool ext = false, norm = false;
   PodDev *d_pods = nullptr;
+  double *d_pinv = nullptr;  // [n][2] reciprocals of the normalising guesses
   uint64_t *d_clauses = nullptr;
   DevResult *d_results = nullptr;
   std::vector<ks_result> host_status;  // compile-time errors (none so far)
@@ -171,6 +172,7 @@ struct ks_ctx {
   uint32_t *d_start = nullptr;
   uint32_t *h_start = nullptr;  // pinned
   uint32_t *d_norm = nullptr;     // [2][P][2] by round parity
+  double *d_norm_inv = nullptr;   // [2][P][2] by round parity
   PodStat *d_pstat = nullptr;     // [P]
   uint32_t *d_fix = nullptr;      // [P] flags + [MAX_P / MAX_PG] group flags
   BlockRec *d_brec = nullptr;
@@ -823,6 +825,8 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k) {
   a.carry_out_n = c->d_pipe + 4 + q;
   a.first = k == 0;
   a.norm_max = c->d_norm + (size_t)q * 2 * c->P;
+  a.norm_inv = c->d_norm_inv + (size_t)q * 2 * c->P;
+  a.guess_inv = b->d_pinv;
   a.pstat = b->norm ? c->d_pstat : nullptr;
   a.fix_flag = c->d_fix;
   a.fix_group = c->d_fix + MAX_P;
@@ -1030,6 +1034,7 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
   HIPC(x, hipMemsetAsync(t.apods, 0xFF, (size_t)x->npos * 4, x->stream));  // every position empty
   if ((st = dalloc(x, &x->d_shards, x->S)) || (st = dalloc(x, &x->d_slot_pos, x->cap)) ||
       (st = dalloc(x, &x->d_start, 1)) || (st = dalloc(x, &x->d_norm, 2 * 2 * (size_t)x->P)) ||
+      (st = dalloc(x, &x->d_norm_inv, 2 * 2 * (size_t)x->P)) ||
       (st = dalloc(x, &x->d_pstat, (size_t)x->P)) || (st = dalloc(x, &x->d_fix, MAX_P + MAX_P / MAX_PG)) ||
       (st = dalloc(x, &x->d_pipe, 8)) || (st = dalloc(x, &x->d_carry, 2 * (size_t)MAX_P)) ||
       (st = dalloc(x, &x->d_counters, 16)))
@@ -1064,7 +1069,7 @@ void ks_close(ks_ctx *c) {
   if (c->comm) ncclCommDestroy(c->comm);
   void *bufs[] = {c->t.acpu, c->t.amem, c->t.rcpu, c->t.rmem, c->t.zcpu, c->t.zmem, c->t.apods,
                   c->t.npods, c->t.hard, c->t.prefer, c->t.lab, c->t.num, c->d_shards, c->d_slot_pos,
-                  c->d_start, c->d_norm, c->d_pstat, c->d_fix, c->d_brec, c->d_srec, c->d_frec,
+                  c->d_start, c->d_norm, c->d_norm_inv, c->d_pstat, c->d_fix, c->d_brec, c->d_srec, c->d_frec,
                   c->d_counters, c->d_crow, c->d_cext, c->d_pipe, c->d_carry};
   for (void *b : bufs)
     if (b) (void)hipFree(b);
@@ -1301,10 +1306,17 @@ ks_status ks_batch_prepare(ks_ctx *c, const ks_pod *pods, uint32_t n, ks_batch *
   b->dict_version = c->dict_version;
   if (cl.w.empty()) cl.add(CK_FALSE, 0, 0, nullptr, 0);
   HIPC(c, hipMalloc((void **)&b->d_pods, dev.size() * sizeof(PodDev)));
+  std::vector<double> pinv(2 * dev.size(), 0.0);
+  for (size_t i = 0; i < dev.size(); ++i) {
+    pinv[2 * i] = dev[i].tt_guess ? 1.0 / (double)dev[i].tt_guess : 0.0;
+    pinv[2 * i + 1] = dev[i].na_guess ? 1.0 / (double)dev[i].na_guess : 0.0;
+  }
+  HIPC(c, hipMalloc((void **)&b->d_pinv, pinv.size() * sizeof(double)));
   HIPC(c, hipMalloc((void **)&b->d_clauses, cl.w.size() * 8));
   HIPC(c, hipMalloc((void **)&b->d_results, std::max<uint32_t>(n, 1) * sizeof(DevResult)));
-  const size_t bytes = dev.size() * sizeof(PodDev) + cl.w.size() * 8 + 1024;
+  const size_t bytes = dev.size() * sizeof(PodDev) + pinv.size() * sizeof(double) + cl.w.size() * 8 + 1024;
   if ((st = xfer_begin(c, bytes, 0)) || (st = h2d(c, b->d_pods, dev.data(), dev.size() * sizeof(PodDev))) ||
+      (st = h2d(c, b->d_pinv, pinv.data(), pinv.size() * sizeof(double))) ||
       (st = h2d(c, b->d_clauses, cl.w.data(), cl.w.size() * 8)))
     return st;
   HIPC(c, hipMemsetAsync(b->d_results, 0, std::max<uint32_t>(n, 1) * sizeof(DevResult), c->stream));
@@ -1364,6 +1376,7 @@ void ks_batch_free(ks_ctx *c, ks_batch *b) {
   if (!b) return;
   if (c) (void)hipSetDevice(c->cfg.device);
   if (b->d_pods) (void)hipFree(b->d_pods);
+  if (b->d_pinv) (void)hipFree(b->d_pinv);
   if (b->d_clauses) (void)hipFree(b->d_clauses);
   if (b->d_results) (void)hipFree(b->d_results);
   delete b;

@@ -403,24 +403,30 @@ __device__ __forceinline__ void clause_pass_n(const uint64_t *c, const NodeExt (
   for (int k = 0; k < LWU; ++k) m[k] = c[1 + k];
   const int64_t x = (int64_t)c[5];
   const bool col1 = (w0 >> 8) & 1u;
-  static_for<NPL>([&](auto J) {
-    constexpr int j = J;
+  auto any = [&](const NodeExt &n) {
     uint64_t acc = 0;
 #pragma unroll
-    for (int k = 0; k < LWU; ++k) acc |= e[j].lab[k] & m[k];
-    const bool any = acc != 0;
-    bool ok;
-    switch (kind) {
-      case CK_ANY: ok = any; break;
-      case CK_NONE: ok = !any; break;
-      case CK_GT: ok = any && (col1 ? e[j].num[1] : e[j].num[0]) > x; break;
-      case CK_LT: ok = any && (col1 ? e[j].num[1] : e[j].num[0]) < x; break;
-      case CK_NAME_EQ: ok = (int64_t)nr[j].slot == x; break;
-      case CK_NAME_NE: ok = (int64_t)nr[j].slot != x; break;
-      default: ok = false; break;
-    }
-    pass[j] = ok;
-  });
+    for (int k = 0; k < LWU; ++k) acc |= n.lab[k] & m[k];
+    return acc != 0;
+  };
+  // one wave-uniform branch per clause, the node loop inside each case
+  if (kind == CK_ANY) {
+    static_for<NPL>([&](auto J) { pass[J] = any(e[J]); });
+  } else if (kind == CK_NONE) {
+    static_for<NPL>([&](auto J) { pass[J] = !any(e[J]); });
+  } else if (kind == CK_GT || kind == CK_LT) {
+    const bool gt = kind == CK_GT;
+    static_for<NPL>([&](auto J) {
+      const int64_t v = col1 ? e[J].num[1] : e[J].num[0];
+      pass[J] = any(e[J]) && (gt ? v > x : v < x);
+    });
+  } else if (kind == CK_NAME_EQ) {
+    static_for<NPL>([&](auto J) { pass[J] = (int64_t)nr[J].slot == x; });
+  } else if (kind == CK_NAME_NE) {
+    static_for<NPL>([&](auto J) { pass[J] = (int64_t)nr[J].slot != x; });
+  } else {
+    static_for<NPL>([&](auto J) { pass[J] = false; });
+  }
 }
 
 // required_match for NPL nodes at once
@@ -550,6 +556,7 @@ __global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
     uint32_t b1 = 0, b2 = 0;
     uint32_t feas = 0, f0 = 0, f1 = 0, f2 = 0, f3 = 0, f4 = 0, ttc = 0, nac = 0;
     uint32_t tmx = 0, nmx = 0;  // max raw over this lane's feasible nodes
+    bool over = false;          // a feasible node's raw score exceeds the max used
     if constexpr (!EXT) {
       // Resource-only pods: only NodeResourcesFit can fail (a batch without
       // PF_EXT pods tolerates every hard taint and names no node).  A zero
@@ -575,8 +582,9 @@ __global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
       static_for<NPL>([&](auto J) { aff[J] = true; praw[J] = 0u; });
       if (p.flags & PF_AFF) required_match_n<NPL, LWU>(p, a.clauses, ne, nr, aff);
       if (p.flags & PF_NA) preferred_raw_n<NPL, LWU>(p, a.clauses, ne, nr, praw);
-      const double inv_tt = tt_max ? 1.0 / (double)tt_max : 0.0;
-      const double inv_na = na_max ? 1.0 / (double)na_max : 0.0;
+      const double *ip = fix ? a.norm_inv + 2 * r : a.guess_inv + 2 * (size_t)pi;  // RN(1 / max)
+      const double inv_tt = (p.flags & PF_TT) ? ip[0] : 0.0;
+      const double inv_na = (p.flags & PF_NA) ? ip[1] : 0.0;
       const double rq_c = ((p.flags & PF_HAS_REQ) && p.req_cpu > 0) ? p.req_cpu_d : -__builtin_inf();
       const double rq_m = ((p.flags & PF_HAS_REQ) && p.req_mem > 0) ? p.req_mem_d : -__builtin_inf();
       const bool ext = p.flags & PF_EXT;
@@ -607,6 +615,7 @@ __global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
           const uint32_t raw = (uint32_t)__popcll(ne[j].prefer & ~p.tol_prefer);
           tts = 100u - normalize_inv(raw, inv_tt);
           at_tt = feasible && raw == tt_max;
+          over |= feasible && raw > tt_max;
           tmx = max(tmx, feasible ? raw : 0u);
         }
         tot1 += (uint32_t)__umul24((uint32_t)a.w.tt, tts);
@@ -615,6 +624,7 @@ __global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
           if (p.flags & PF_NA) {
             nas = normalize_inv(praw[j], inv_na);
             at_na = feasible && praw[j] == na_max;
+            over |= feasible && praw[j] > na_max;
             nmx = max(nmx, feasible ? praw[j] : 0u);
           }
           tot1 += (uint32_t)__umul24((uint32_t)a.w.na, nas);
@@ -637,8 +647,13 @@ __global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
         }
       });
     }
-    if (EXT && (p.flags & PF_TT)) tmx = wave_max_u32_dpp(tmx);
-    if (EXT && (p.flags & PF_NA)) nmx = wave_max_u32_dpp(nmx);
+    if (EXT && (p.flags & (PF_TT | PF_NA))) {
+      // the wave's max raw is the max used when some feasible node reaches it
+      // and none exceeds it (the usual case): reduce only otherwise
+      const bool exceeded = __ballot(over) != 0;
+      if (p.flags & PF_TT) tmx = (!exceeded && ttc) ? tt_max : wave_max_u32_dpp(tmx);
+      if (p.flags & PF_NA) nmx = (!exceeded && nac) ? na_max : wave_max_u32_dpp(nmx);
+    }
     const uint32_t best = b1, second = b2;
     // Wave list: the lane bests above every lane's second best (top 2) + bound,
     // DPP reductions, skipping those the candidate count makes unnecessary.
@@ -886,6 +901,8 @@ __global__ __launch_bounds__(MAX_P) void norm_check_kernel(RoundArgs a) {
     }
     a.norm_max[2 * r] = tt;
     a.norm_max[2 * r + 1] = na;
+    a.norm_inv[2 * r] = tt ? 1.0 / (double)tt : 0.0;
+    a.norm_inv[2 * r + 1] = na ? 1.0 / (double)na : 0.0;
     a.fix_flag[r] = wrong ? 1u : 0u;
     if (wrong) atomicOr(&s_any[r / MAX_PG], 1u);
   }

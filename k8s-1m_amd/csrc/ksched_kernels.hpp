@@ -40,6 +40,8 @@ struct RoundArgs {
   uint32_t *carry_out_n;
   uint32_t first;             // first round of a pipeline run (no previous round)
   uint32_t *norm_max;         // [P][2] max raw TaintToleration / NodeAffinity over feasible nodes (norm_check)
+  double *norm_inv;           // [P][2] RN(1 / norm_max), 0 for 0 (norm_check; FIX-mode sweep)
+  const double *guess_inv;    // [npods][2] RN(1 / tt_guess), RN(1 / na_guess) (host)
   PodStat *pstat;             // [P] measured maxima (merge, all shards); nullptr: no normalising pod
   uint32_t *fix_flag;         // [P] the pod's guessed maxima were wrong: re-swept in FIX mode
   uint32_t *fix_group;        // [P / MAX_PG] any flagged pod in the group
