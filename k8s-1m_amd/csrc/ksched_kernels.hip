@@ -739,17 +739,17 @@ __global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
 }
 
 // =================================================================== merge
-// Bitonic sort (descending) of s[0..m) in LDS, m a power of two.
+// Bitonic sort (descending) of s[0..m) in LDS, m a power of two: every
+// thread takes whole compare-exchange pairs (p -> i, i + j), so a pass over m
+// keys is m / 2 exchanges spread over the block, one barrier per pass.
 __device__ void bitonic_desc(uint64_t *s, uint32_t m) {
   for (uint32_t k = 2; k <= m; k <<= 1) {
     for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-      for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
-        const uint32_t ixj = i ^ j;
-        if (ixj > i) {
-          const uint64_t x = s[i], y = s[ixj];
-          const bool desc = (i & k) == 0;
-          if (desc ? (x < y) : (x > y)) { s[i] = y; s[ixj] = x; }
-        }
+      for (uint32_t p = threadIdx.x; p < m / 2; p += blockDim.x) {
+        const uint32_t i = ((p & ~(j - 1)) << 1) | (p & (j - 1));
+        const uint64_t x = s[i], y = s[i + j];
+        const bool desc = (i & k) == 0;
+        if (desc ? (x < y) : (x > y)) { s[i] = y; s[i + j] = x; }
       }
       __syncthreads();
     }
@@ -830,11 +830,13 @@ __device__ void merge_lists(const uint64_t *keys, size_t list_stride, const uint
 }
 
 // grid: x = pod in round, y = local shard.  Blocks -> shard record.
-__global__ __launch_bounds__(256) void merge_kernel(RoundArgs a) {
+constexpr int MERGE_THREADS = 1024;
+__global__ __launch_bounds__(MERGE_THREADS) void merge_kernel(RoundArgs a) {
   __shared__ uint64_t s_sort[MERGE_CAP];
   __shared__ uint64_t s_scr[16];
   __shared__ uint32_t s_u32[16];
   __shared__ uint32_t s_cnt;
+  __shared__ uint32_t s_wc[MERGE_THREADS / WAVE][NFILT + 5];
   const uint32_t start = uniform_u32(*a.sstart);
   const uint32_t r = blockIdx.x;
   if (start + r >= a.npods || r >= a.P) return;
@@ -846,8 +848,9 @@ __global__ __launch_bounds__(256) void merge_kernel(RoundArgs a) {
   uint64_t *out = a.srec + ((size_t)(a.shard0 + sh) * a.P + r) * rec_words(a.K);
   merge_lists(&br[0].keys[0], sizeof(BlockRec) / 8, &br[0].bound, sizeof(BlockRec) / 8, nb, BLOCK_KEYS, a.K,
               out, s_sort, s_scr, &s_cnt, s_u32);
-  // counts, and the normalising maxima measured by the sweep
-  uint32_t c[NFILT + 3];
+  // counts, and the normalising maxima measured by the sweep: per wave by DPP,
+  // then one barrier and thread 0 over the waves
+  int32_t c[NFILT + 3];
   for (int q = 0; q < NFILT + 3; ++q) c[q] = 0;
   uint32_t tmx = 0, nmx = 0;
   for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) {
@@ -858,23 +861,34 @@ __global__ __launch_bounds__(256) void merge_kernel(RoundArgs a) {
     tmx = max(tmx, br[i].tt_max);
     nmx = max(nmx, br[i].na_max);
   }
-  for (int q = 0; q < NFILT + 3; ++q) c[q] = block_sum_u32(c[q], s_u32);
-  const bool stat = a.pstat != nullptr && !a.fix;
-  if (stat) {
-    tmx = (uint32_t)block_max_u64(tmx, s_scr);
-    nmx = (uint32_t)block_max_u64(nmx, s_scr);
+  const uint32_t wid = threadIdx.x / WAVE;
+#pragma unroll
+  for (int q = 0; q < NFILT + 3; ++q) c[q] = wave_sum_i32_dpp(c[q]);
+  tmx = wave_max_u32_dpp(tmx);
+  nmx = wave_max_u32_dpp(nmx);
+  if (threadIdx.x % WAVE == 0) {
+    for (int q = 0; q < NFILT + 3; ++q) s_wc[wid][q] = (uint32_t)c[q];
+    s_wc[wid][NFILT + 3] = tmx;
+    s_wc[wid][NFILT + 4] = nmx;
   }
+  __syncthreads();
   if (threadIdx.x == 0) {
+    uint32_t t[NFILT + 5] = {};
+    for (uint32_t w = 0; w < blockDim.x / WAVE; ++w) {
+      for (int q = 0; q < NFILT + 3; ++q) t[q] += s_wc[w][q];
+      t[NFILT + 3] = max(t[NFILT + 3], s_wc[w][NFILT + 3]);
+      t[NFILT + 4] = max(t[NFILT + 4], s_wc[w][NFILT + 4]);
+    }
     ShardRecHdr *h = (ShardRecHdr *)out;
-    h->feasible = c[0];
-    for (int q = 0; q < NFILT; ++q) h->fails[q] = c[1 + q];
-    h->tt_cnt = c[6];
-    h->na_cnt = c[7];
-    if (stat) {  // across local shards (atomics) and ranks (RCCL all-reduce max)
+    h->feasible = t[0];
+    for (int q = 0; q < NFILT; ++q) h->fails[q] = t[1 + q];
+    h->tt_cnt = t[6];
+    h->na_cnt = t[7];
+    if (a.pstat != nullptr && !a.fix) {  // across local shards (atomics) and ranks (RCCL all-reduce max)
       PodStat *ps = a.pstat + r;
-      if (tmx) atomicMax(&ps->tt_max, tmx);
-      if (nmx) atomicMax(&ps->na_max, nmx);
-      if (c[0]) atomicMax(&ps->any_feasible, 1u);
+      if (t[NFILT + 3]) atomicMax(&ps->tt_max, t[NFILT + 3]);
+      if (t[NFILT + 4]) atomicMax(&ps->na_max, t[NFILT + 4]);
+      if (t[0]) atomicMax(&ps->any_feasible, 1u);
     }
   }
 }
@@ -2143,7 +2157,7 @@ hipError_t launch_sweep(const RoundArgs &a, bool ext, uint32_t nblocks, uint32_t
 }
 
 hipError_t launch_merge(const RoundArgs &a, uint32_t nshards, hipStream_t st) {
-  merge_kernel<<<dim3(a.P, nshards), 256, 0, st>>>(a);
+  merge_kernel<<<dim3(a.P, nshards), MERGE_THREADS, 0, st>>>(a);
   return hipGetLastError();
 }
 

@@ -221,6 +221,31 @@ def extreme_allocatable():
     return nodes, pods, []
 
 
+@scenario
+def wide_label_dictionary():
+    # ~200 label-pair bits: the label programs span all four 64-bit words of a
+    # node's bitset (the widest EXT sweep variant), in required and preferred terms
+    vals = [f"r{v}" for v in range(200)]
+    racks = ["r0", "r40", "r80", "r120", "r160", "r199"]
+    nodes = [node(f"n{i}", labels={"rack": racks[i], "row": f"w{i}"}) for i in range(6)]
+    T = lambda *reqs: Term(list(reqs))  # noqa: E731
+    pods = [
+        pod("in-many", required_terms=[T(Req("rack", "In", vals))]),                          # all
+        pod("in-high", required_terms=[T(Req("rack", "In", vals[120:]))]),                    # 3, 4, 5
+        pod("notin-high", required_terms=[T(Req("rack", "NotIn", vals[160:]))]),              # 0-3
+        pod("sel-r199", node_selector={"rack": "r199"}),                                       # 5
+        pod("r80-or-w5", required_terms=[T(Req("rack", "In", ["r80"])), T(Req("row", "In", ["w5"]))]),  # 2, 5
+        pod("row-and-notin-low", required_terms=[T(Req("row", "Exists"), Req("rack", "NotIn", vals[:120]))]),
+        pod("pref-r199", preferred=[Pref(50, T(Req("rack", "In", ["r199"])))]),               # 5 (normalised)
+    ]
+    # best-effort pods keep LeastAllocated at 99 for a node's first three, so
+    # ties fall to the lowest feasible slot
+    exp = [dict(node=0, feasible=6), dict(node=3, feasible=3, fails={AFFINITY: 3}), dict(node=0, feasible=4),
+           dict(node=5, feasible=1, fails={AFFINITY: 5}), dict(node=2, feasible=2), dict(node=3, feasible=3),
+           dict(node=5, feasible=6)]
+    return nodes, pods, exp
+
+
 def check(results, exp):
     """results: structured numpy array (tests.helpers.RES_DT)."""
     for i, e in enumerate(exp):
