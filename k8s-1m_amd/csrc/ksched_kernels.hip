@@ -1241,7 +1241,8 @@ constexpr int RES_LIST_WAVES = 4;
 constexpr int RES_OWN_WAVES = 4;
 constexpr int RES_EVAL_WAVE = RES_LIST_WAVES + RES_OWN_WAVES;
 constexpr int RES_DEC_WAVE = RES_EVAL_WAVE + 1;
-constexpr int RESOLVE_THREADS = (RES_DEC_WAVE + 1) * WAVE;
+constexpr int RES_PREV_WAVE = RES_DEC_WAVE + 1;
+constexpr int RESOLVE_THREADS = (RES_PREV_WAVE + 1) * WAVE;
 constexpr int RHASH = 1024;
 constexpr int LSEL = 4;                                   // listed candidates kept per list wave
 constexpr int LAHEAD = 3;                                 // list waves select pod i + LAHEAD in iteration i
@@ -1253,7 +1254,7 @@ typedef __attribute__((address_space(1))) void gvoid_t;  // global_load_lds oper
 typedef __attribute__((address_space(3))) void lvoid_t;
 constexpr int NCAND_OWN = 2 * RES_OWN_WAVES;              // lanes [0, 8): owner waves' best two
 constexpr int NCAND_LIST = LSEL * RES_LIST_WAVES;         // lanes [8, 24): list waves' first four
-constexpr int CAND_PREV = NCAND_OWN + NCAND_LIST;         // lane 24: the previous pod's winner
+constexpr int CAND_PREV = NCAND_OWN + NCAND_LIST;         // candidate 24: the previous pod's winner (prev wave)
 constexpr int NCAND = CAND_PREV + 1;
 constexpr int DSUM_LANE = 32;                             // decider lanes summing status changes
 constexpr uint32_t NONE32 = 0xFFFFFFFFu;
@@ -1565,7 +1566,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
            stop_at = nround;
   // the decider is the per-pod critical path, the eval wave next: issue priority
   if (wid == RES_DEC_WAVE) __builtin_amdgcn_s_setprio(3);
-  else if (wid == RES_EVAL_WAVE) __builtin_amdgcn_s_setprio(2);
+  else if (wid == RES_EVAL_WAVE || wid == RES_PREV_WAVE) __builtin_amdgcn_s_setprio(2);
 #ifdef KS_STAMPS
   const bool stamper = lane == 0 && (wid == RES_DEC_WAVE || wid == RES_EVAL_WAVE);
   const uint32_t sidx = wid == RES_DEC_WAVE ? 0 : 2;
@@ -1709,46 +1710,60 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
 #endif
         }
       }
-    } else if (wid == RES_EVAL_WAVE) {
+    } else if (wid == RES_EVAL_WAVE || wid == RES_PREV_WAVE) {
       if (ROLE_ON(4)) {
-      // ---------------------------------------------------------- eval wave
-      // every candidate of pod r committed (the owners take the winner's from
-      // here), evaluated against pod r+1
+      // ------------------------------------------------ eval and prev waves
+      // every candidate of pod r committed, evaluated against pod r+1: the
+      // eval wave takes the owner and listed candidates (one per lane) and
+      // never waits for pod r-1's decision; the prev wave's first lane takes
+      // the previous winner, whose state is the eval output for pod r-1
       if (r < nround) {
+        const bool prevw = wid == RES_PREV_WAVE;
         const uint32_t b4 = r % RSLOTS;
-        const bool is_own = lane < (uint32_t)NCAND_OWN;
-        const bool is_lst = lane >= (uint32_t)NCAND_OWN && lane < (uint32_t)CAND_PREV;
-        const bool is_prev = lane == (uint32_t)CAND_PREV;
-        const uint32_t lo = is_own ? lane : 0u, c = is_lst ? lane - NCAND_OWN : 0u;
+        const uint32_t cl = prevw ? (lane == 0 ? (uint32_t)CAND_PREV : (uint32_t)NCAND)
+                                  : (lane < (uint32_t)CAND_PREV ? lane : (uint32_t)NCAND);  // candidate, NCAND = none
+        const bool is_own = cl < (uint32_t)NCAND_OWN;
+        const bool is_lst = cl >= (uint32_t)NCAND_OWN && cl < (uint32_t)CAND_PREV;
+        const bool is_prev = cl == (uint32_t)CAND_PREV;
+        const uint32_t lo = is_own ? cl : 0u, c = is_lst ? cl - NCAND_OWN : 0u;
         const uint32_t cw = c / LSEL, ck = c % LSEL;
         // one batch: the candidate's row (owner: published node; listed: DMA
-        // pieces) and round-start fields, independent of the last commit; the
-        // previous winner (lane 24) follows once the commit record is in
-        const uint4 *rp = is_own ? (const uint4 *)&s_ocand[buf][lo] : &s_lrowb[b4][cw][0][ck];
-        const uint32_t rstride = is_own ? 1u : (uint32_t)LSEL;
-        RNode pre;
-        uint4 *pp = (uint4 *)&pre;
-#pragma unroll
-        for (int j = 0; j < ROW_PIECES; ++j) pp[j] = rp[j * rstride];
-        const uint4 tail = is_own ? rp[ROW_PIECES] : make_uint4(0, 0, 0, 0);       // rc0, rm0
-        const uint4 tail2 = is_own ? rp[ROW_PIECES + 1] : make_uint4(0, 0, 0, 0);  // np0, slot
+        // pieces) and round-start fields
+        RNode pre{};
         CandExt px{};
-        if constexpr (EXT) {
-          const uint4 *xp = is_own ? (const uint4 *)&s_ocandx[buf][lo] : &s_lrowb[b4][cw][ROW_PIECES][ck];
-          uint4 *xo = (uint4 *)&px;
+        uint4 tail = make_uint4(0, 0, 0, 0), tail2 = make_uint4(0, 0, 0, 0);  // owners: rc0, rm0 / np0, slot
+        uint64_t lkey = 0;
+        uint32_t pv = 0, pc = 0;  // pod r-1's commit (prev wave only)
+        bool on = false;
+        if (!prevw) {
+          const uint4 *rp = is_own ? (const uint4 *)&s_ocand[buf][lo] : &s_lrowb[b4][cw][0][ck];
+          const uint32_t rstride = is_own ? 1u : (uint32_t)LSEL;
+          uint4 *pp = (uint4 *)&pre;
 #pragma unroll
-          for (int j = 0; j < EXT_PIECES; ++j) xo[j] = xp[j * rstride];
+          for (int j = 0; j < ROW_PIECES; ++j) pp[j] = rp[j * rstride];
+          if (is_own) {
+            tail = rp[ROW_PIECES];
+            tail2 = rp[ROW_PIECES + 1];
+          }
+          if constexpr (EXT) {
+            const uint4 *xp = is_own ? (const uint4 *)&s_ocandx[buf][lo] : &s_lrowb[b4][cw][ROW_PIECES][ck];
+            uint4 *xo = (uint4 *)&px;
+#pragma unroll
+            for (int j = 0; j < EXT_PIECES; ++j) xo[j] = xp[j * rstride];
+          }
+          lkey = s_lkey[b4][c];
+          on = is_own ? s_okey[buf][lo] != 0 : is_lst && s_lidx[b4][c] != NONE32;
+        } else {
+          pv = uniform_u32(s_pend[nb][0]);
+          pc = min(uniform_u32(s_pend[nb][1]), (uint32_t)NCAND - 1);
+          on = is_prev && pv != 0;
         }
-        const uint64_t lkey = s_lkey[b4][c];
-        const uint32_t pv = uniform_u32(s_pend[nb][0]);
-        const uint32_t pc = min(uniform_u32(s_pend[nb][1]), (uint32_t)NCAND - 1);  // pod r-1's commit
 #if KS_STAMPS == 2
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         STAMP_NOW(ts);
         sub[0] += ts - t0;
         t2 = ts;
 #endif
-        const bool on = is_own ? s_okey[buf][lo] != 0 : is_lst ? s_lidx[b4][c] != NONE32 : (is_prev && pv != 0);
         if (is_lst) {
           pre.rc0 = pre.row.rc;
           pre.rm0 = pre.row.rm;
@@ -1773,9 +1788,9 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
 #endif
         RNode post = pre;
         rnode_add(post, lds_uniform(s_pod[r], lane));
-        if (on && lane < (uint32_t)NCAND) {  // lane 24 of the next iteration reads the winner's
-          s_post[buf][lane] = post;
-          if (EXT) s_postx[buf][lane] = px;
+        if (on && cl < (uint32_t)NCAND) {  // the prev wave of the next iteration reads the winner's
+          s_post[buf][cl] = post;
+          if (EXT) s_postx[buf][cl] = px;
         }
         if constexpr (!EXT) {
           // straight-line for every lane (no branch keeps the pod loads from
@@ -1786,17 +1801,17 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
           const NodeRegs g1 = rnode_regs(post, post.row.rc, post.row.rm, post.row.np);
           const bool f0 = fit_q(q1, g0), f1 = fit_q(q1, g1);
           const uint64_t key = f1 ? key_q(p1, q1, g1) : 0ull;
-          if (on && lane < (uint32_t)NCAND && r + 1 < nround) {
-            s_ekey[buf][lane] = key;
+          if (on && cl < (uint32_t)NCAND && r + 1 < nround) {
+            s_ekey[buf][cl] = key;
             // a commit only adds: feasible -> Fit failure is the only change
             const int32_t lost = (f0 && !f1) ? 1 : 0;
-            s_edd[buf][lane][0] = lost;
+            s_edd[buf][cl][0] = lost;
 #pragma unroll
-            for (int qq = 1; qq < NFILT + 3; ++qq) s_edd[buf][lane][qq] = qq == 1 + KS_PLUGIN_FIT_IDX ? lost : 0;
+            for (int qq = 1; qq < NFILT + 3; ++qq) s_edd[buf][cl][qq] = qq == 1 + KS_PLUGIN_FIT_IDX ? lost : 0;
           }
         } else if (r + 1 < nround) {
           const PodDev p1 = lds_uniform(s_pod[r + 1], lane);  // every lane
-          if (on && lane < (uint32_t)NCAND) {
+          if (on && cl < (uint32_t)NCAND) {
             int64_t tt_max = 0, na_max = 0;
             if (EXT) {
               tt_max = s_norm[r + 1][0];
@@ -1812,9 +1827,9 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
             if (st1 == ST_FEASIBLE) key = pack_key(total_score<EXT>(p1, a.clauses, g1, e, a.w, tt_max, na_max), post.slot);
             int32_t d[NFILT + 3] = {0, 0, 0, 0, 0, 0, 0, 0};
             if (st0 != st1) status_delta<EXT>(p1, a.clauses, st0, st1, e, post.slot, tt_max, na_max, d);
-            s_ekey[buf][lane] = key;
+            s_ekey[buf][cl] = key;
 #pragma unroll
-            for (int qq = 0; qq < NFILT + 3; ++qq) s_edd[buf][lane][qq] = d[qq];
+            for (int qq = 0; qq < NFILT + 3; ++qq) s_edd[buf][cl][qq] = d[qq];
           }
         }
 #if KS_STAMPS == 2
