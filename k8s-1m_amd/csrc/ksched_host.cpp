@@ -159,7 +159,9 @@ struct ks_ctx {
   std::string err;
   hipStream_t stream = nullptr;   // table updates, prescore / sweep / merge / gather, RCCL
   hipStream_t rstream = nullptr;  // resolve (overlaps the next round's sweep)
+  hipStream_t sstream = nullptr;  // merge .. patch (overlap the next round's sweep)
   hipEvent_t ev_sw[2] = {nullptr, nullptr}, ev_res[2] = {nullptr, nullptr};  // by round parity
+  hipEvent_t ev_swept[2] = {nullptr, nullptr}, ev_fixed[2] = {nullptr, nullptr};
   // geometry
   uint32_t cap = 0, S = 1, npl = 8, P = 256, K = 256;
   std::vector<Shard> shards;
@@ -175,8 +177,8 @@ struct ks_ctx {
   double *d_norm_inv = nullptr;   // [2][P][2] by round parity
   PodStat *d_pstat = nullptr;     // [P]
   uint32_t *d_fix = nullptr;      // [P] flags + [MAX_P / MAX_PG] group flags
-  BlockRec *d_brec = nullptr;
-  size_t brec_bytes = 0;
+  BlockRec *d_brec = nullptr;     // [2][...] by round parity (merge k reads while sweep k+1 writes)
+  size_t brec_bytes = 0;          // per parity
   uint64_t *d_srec = nullptr, *d_frec = nullptr;
   uint64_t *d_counters = nullptr;
   CandRow *d_crow = nullptr;
@@ -770,9 +772,12 @@ ks_status collect_timing(ks_ctx *c) {
 
 // One device-driven round (all kernels read the queue head from d_start).
 // Round k of a pipeline run (k = 0 starts it: the table holds every previous
-// round).  Stream order, with sweep k+1 overlapping resolve k:
-//   stream : [wait resolve k-2, write-back k-2] advance k, prescore k, sweep k,
-//            merge k, (RCCL), merge_shards k, gather k, record ev_sw[k]
+// round).  Stream order, with sweep k+1 overlapping merge .. patch k and resolve k:
+//   stream : [wait resolve k-2 (and FIX sweep k-1), write-back k-2] advance k,
+//            sweep k, record ev_swept[k]
+//   sstream: wait ev_swept[k], merge k, [norm_check, FIX sweep + merge k],
+//            (RCCL), merge_shards k, gather k, [wait resolve k-1, patch k],
+//            record ev_sw[k]
 //   rstream: wait ev_sw[k], resolve k, record ev_res[k]
 ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k) {
   // RCCL path whenever a communicator exists (also a 1-rank one: exercised by tests)
@@ -831,7 +836,7 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k) {
   a.fix_flag = c->d_fix;
   a.fix_group = c->d_fix + MAX_P;
   a.fix = 0;
-  a.brec = c->d_brec;
+  a.brec = c->d_brec + (size_t)q * (c->brec_bytes / sizeof(BlockRec));
   a.srec = c->d_srec + (size_t)q * c->S * c->P * RW;
   a.frec = c->S == 1 ? a.srec : c->d_frec + (size_t)q * c->P * RW;
   a.results = b->d_results;
@@ -851,10 +856,10 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k) {
   // split into `sub` consecutive kernel waves; slots follow from the layout.
   if (k >= 2) {  // round k-2 lands in the table before sweep k (sweep k-1 has finished reading it)
     HIPC(c, hipStreamWaitEvent(c->stream, c->ev_res[q], 0));
+    if (b->norm) HIPC(c, hipStreamWaitEvent(c->stream, c->ev_fixed[pq], 0));  // ... and so has FIX sweep k-1
     HIPC(c, launch_writeback(c->t, c->d_carry + (size_t)q * MAX_P, c->d_pipe + 4 + q, c->stream));
   }
   HIPC(c, launch_advance(a, c->stream));
-  if (b->norm) HIPC(c, hipMemsetAsync(c->d_pstat, 0, (size_t)c->P * sizeof(PodStat), c->stream));
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (c->timing) {
     e0 = get_event(c);
@@ -866,33 +871,39 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k) {
     HIPC(c, hipEventRecord(e1, c->stream));
     c->ev_sweep.emplace_back(e0, e1);
   }
-  HIPC(c, launch_merge(a, nloc, c->stream));
+  // merge .. patch on the side stream, overlapping sweep k+1 (block records
+  // by parity; gather k may read the table while the write-back of round k-1
+  // lands: only rows of round k-1's nodes change, and patch k replaces those)
+  HIPC(c, hipEventRecord(c->ev_swept[q], c->stream));
+  hipStream_t ss = c->sstream;
+  HIPC(c, hipStreamWaitEvent(ss, c->ev_swept[q], 0));
+  if (b->norm) HIPC(c, hipMemsetAsync(c->d_pstat, 0, (size_t)c->P * sizeof(PodStat), ss));
+  HIPC(c, launch_merge(a, nloc, ss));
   if (b->norm) {
     // the sweep scored normalising plugins with each pod's guessed maxima:
     // measure (all ranks), flag the wrong guesses, re-sweep + re-merge those pods
     if (multi)
-      NCCLC(c, ncclAllReduce(c->d_pstat, c->d_pstat, 4 * c->P, ncclUint32, ncclMax, c->comm, c->stream));
-    HIPC(c, launch_norm_check(a, c->stream));
+      NCCLC(c, ncclAllReduce(c->d_pstat, c->d_pstat, 4 * c->P, ncclUint32, ncclMax, c->comm, ss));
+    HIPC(c, launch_norm_check(a, ss));
     RoundArgs f = a;
     f.fix = 1;
     f.pg = MAX_PG;
-    HIPC(c, launch_sweep(f, true, bmax, (c->P + MAX_PG - 1) / MAX_PG, nloc, c->stream));
-    HIPC(c, launch_merge(f, nloc, c->stream));
+    HIPC(c, launch_sweep(f, true, bmax, (c->P + MAX_PG - 1) / MAX_PG, nloc, ss));
+    HIPC(c, hipEventRecord(c->ev_fixed[q], ss));  // the FIX sweep reads the table as sweep k did
+    HIPC(c, launch_merge(f, nloc, ss));
   }
   if (multi) {
     const size_t words = (size_t)c->P * RW;
-    NCCLC(c, ncclAllGather(a.srec + (size_t)c->cfg.rank * words, a.srec, words * 8, ncclUint8, c->comm, c->stream));
+    NCCLC(c, ncclAllGather(a.srec + (size_t)c->cfg.rank * words, a.srec, words * 8, ncclUint8, c->comm, ss));
   }
-  if (c->S > 1) HIPC(c, launch_merge_shards(a, c->stream));
-  HIPC(c, launch_gather_cand(a, b->ext, c->stream));
+  if (c->S > 1) HIPC(c, launch_merge_shards(a, ss));
+  HIPC(c, launch_gather_cand(a, b->ext, ss));
   if (k > 0) {
-    // merge round k-1's commits into the lists: once resolve k-1 is done, on the
-    // main stream (the sweeps of rounds k and k+1 are not running then, so the
-    // patch has the whole GPU), before the write-back of round k-1
-    HIPC(c, hipStreamWaitEvent(c->stream, c->ev_res[pq], 0));
-    HIPC(c, launch_patch(a, b->ext, c->stream));
+    // merge round k-1's commits into the lists once resolve k-1 is done
+    HIPC(c, hipStreamWaitEvent(ss, c->ev_res[pq], 0));
+    HIPC(c, launch_patch(a, b->ext, ss));
   }
-  HIPC(c, hipEventRecord(c->ev_sw[q], c->stream));
+  HIPC(c, hipEventRecord(c->ev_sw[q], ss));
   HIPC(c, hipStreamWaitEvent(c->rstream, c->ev_sw[q], 0));
   if (c->timing) {
     e0 = get_event(c);
@@ -975,11 +986,12 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
   if (hipSetDevice(cfg->device) != hipSuccess) return KS_ERR_DEVICE;
   ks_ctx *x = c.get();
   {
-    // Resolve runs on a high-priority stream.  KS_RESOLVE_CUS=n instead
-    // reserves n CUs for it (masking the main stream off them); measured 5 %
-    // slower at 1M nodes (the sweep loses a CU), so it is off by default.
+    // Resolve runs on a high-priority stream on KS_RESOLVE_CUS (default 1) CUs
+    // of its own: the main and side streams are masked off them, so a resolve
+    // launch never waits for a CU to drain the next round's sweep blocks (the
+    // sweep loses 1/256 of the chip, measured ~4 % slower).  0: no mask.
     const char *e = std::getenv("KS_RESOLVE_CUS");
-    const int nres = e ? std::max(0, std::atoi(e)) : 0;
+    const int nres = e ? std::max(0, std::atoi(e)) : 1;
     hipDeviceProp_t prop{};
     HIPC(x, hipGetDeviceProperties(&prop, cfg->device));
     const int ncu = prop.multiProcessorCount;
@@ -988,15 +1000,19 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
       for (int i = 0; i < ncu; ++i) (i >= ncu - nres ? res_mask : main_mask)[i / 32] |= 1u << (i % 32);
       HIPC(x, hipExtStreamCreateWithCUMask(&x->stream, (uint32_t)main_mask.size(), main_mask.data()));
       HIPC(x, hipExtStreamCreateWithCUMask(&x->rstream, (uint32_t)res_mask.size(), res_mask.data()));
+      HIPC(x, hipExtStreamCreateWithCUMask(&x->sstream, (uint32_t)main_mask.size(), main_mask.data()));
     } else {
       int lo = 0, hi = 0;
       HIPC(x, hipStreamCreateWithFlags(&x->stream, hipStreamNonBlocking));
       HIPC(x, hipDeviceGetStreamPriorityRange(&lo, &hi));
       HIPC(x, hipStreamCreateWithPriority(&x->rstream, hipStreamNonBlocking, hi));
+      HIPC(x, hipStreamCreateWithPriority(&x->sstream, hipStreamNonBlocking, hi));
     }
     for (int q = 0; q < 2; ++q) {
       HIPC(x, hipEventCreateWithFlags(&x->ev_sw[q], hipEventDisableTiming));
       HIPC(x, hipEventCreateWithFlags(&x->ev_res[q], hipEventDisableTiming));
+      HIPC(x, hipEventCreateWithFlags(&x->ev_swept[q], hipEventDisableTiming));
+      HIPC(x, hipEventCreateWithFlags(&x->ev_fixed[q], hipEventDisableTiming));
     }
   }
   // shard geometry: contiguous slot ranges; waves rounded to a multiple of 4
@@ -1049,7 +1065,7 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
   for (auto &sh : x->shards) bmax = std::max(bmax, blocks_per_shard(sh, x->npl / std::min<uint32_t>(x->npl, 2)));
   const uint32_t nloc = world > 1 ? 1 : x->S;
   x->brec_bytes = (size_t)nloc * x->P * bmax * sizeof(BlockRec);
-  if ((st = dalloc(x, (uint8_t **)&x->d_brec, x->brec_bytes))) return st;
+  if ((st = dalloc(x, (uint8_t **)&x->d_brec, 2 * x->brec_bytes))) return st;
   const size_t recs = (size_t)x->S * x->P * rec_words(x->K);  // per round parity
   // +2 words: the resolve's 16-byte key DMA may read 8 bytes past the last record
   if ((st = dalloc(x, &x->d_srec, 2 * recs + 2)) ||
@@ -1066,6 +1082,7 @@ void ks_close(ks_ctx *c) {
   (void)hipSetDevice(c->cfg.device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->rstream) (void)hipStreamSynchronize(c->rstream);
+  if (c->sstream) (void)hipStreamSynchronize(c->sstream);
   if (c->comm) ncclCommDestroy(c->comm);
   void *bufs[] = {c->t.acpu, c->t.amem, c->t.rcpu, c->t.rmem, c->t.zcpu, c->t.zmem, c->t.apods,
                   c->t.npods, c->t.hard, c->t.prefer, c->t.lab, c->t.num, c->d_shards, c->d_slot_pos,
@@ -1082,8 +1099,11 @@ void ks_close(ks_ctx *c) {
   for (int q = 0; q < 2; ++q) {
     if (c->ev_sw[q]) (void)hipEventDestroy(c->ev_sw[q]);
     if (c->ev_res[q]) (void)hipEventDestroy(c->ev_res[q]);
+    if (c->ev_swept[q]) (void)hipEventDestroy(c->ev_swept[q]);
+    if (c->ev_fixed[q]) (void)hipEventDestroy(c->ev_fixed[q]);
   }
   if (c->rstream) (void)hipStreamDestroy(c->rstream);
+  if (c->sstream) (void)hipStreamDestroy(c->sstream);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
