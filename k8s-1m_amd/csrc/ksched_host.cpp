@@ -162,6 +162,12 @@ struct ks_ctx {
   hipStream_t sstream = nullptr;  // merge .. patch (overlap the next round's sweep)
   hipEvent_t ev_sw[2] = {nullptr, nullptr}, ev_res[2] = {nullptr, nullptr};  // by round parity
   hipEvent_t ev_swept[2] = {nullptr, nullptr}, ev_fixed[2] = {nullptr, nullptr};
+  // cross-stream hand-offs as stream memory operations (write / wait-value on
+  // monotone round numbers): [0] swept, [1] side done, [2] resolved, [3] fixed
+  uint32_t *d_flags = nullptr;
+  uint32_t round_seq = 0;         // rounds enqueued since open
+  uint32_t seq_of[2] = {0, 0};    // round number by parity
+  bool value_sync = true;
   // geometry
   uint32_t cap = 0, S = 1, npl = 8, P = 256, K = 256;
   std::vector<Shard> shards;
@@ -770,6 +776,19 @@ ks_status collect_timing(ks_ctx *c) {
   return KS_OK;
 }
 
+// Cross-stream hand-off: `st` signals round number `seq` on flag f (and the
+// event, which drain_rounds waits on); `wt` waits for it.
+static ks_status hand_signal(ks_ctx *c, hipStream_t st, int f, hipEvent_t ev, uint32_t seq) {
+  HIPC(c, hipEventRecord(ev, st));
+  if (c->value_sync) HIPC(c, hipStreamWriteValue32(st, c->d_flags + f, seq, 0));
+  return KS_OK;
+}
+static ks_status hand_wait(ks_ctx *c, hipStream_t wt, int f, hipEvent_t ev, uint32_t seq) {
+  if (c->value_sync) HIPC(c, hipStreamWaitValue32(wt, c->d_flags + f, seq, hipStreamWaitValueGte, 0xFFFFFFFFu));
+  else HIPC(c, hipStreamWaitEvent(wt, ev, 0));
+  return KS_OK;
+}
+
 // One device-driven round (all kernels read the queue head from d_start).
 // Round k of a pipeline run (k = 0 starts it: the table holds every previous
 // round).  Stream order, with sweep k+1 overlapping merge .. patch k and resolve k:
@@ -785,6 +804,7 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k) {
   const uint32_t nloc = multi ? 1 : c->S;
   const uint32_t shard0 = multi ? c->cfg.rank : 0;
   const uint32_t knpl = kernel_npl(c, b->ext);
+  ks_status st = KS_OK;
   const uint32_t sub = c->npl / knpl;
   uint32_t bmax = 0;
   for (uint32_t q = 0; q < nloc; ++q) bmax = std::max(bmax, blocks_per_shard(c->shards[shard0 + q], sub));
@@ -855,8 +875,8 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k) {
   // equals the layout position when the layout's npl-step block of a wave is
   // split into `sub` consecutive kernel waves; slots follow from the layout.
   if (k >= 2) {  // round k-2 lands in the table before sweep k (sweep k-1 has finished reading it)
-    HIPC(c, hipStreamWaitEvent(c->stream, c->ev_res[q], 0));
-    if (b->norm) HIPC(c, hipStreamWaitEvent(c->stream, c->ev_fixed[pq], 0));  // ... and so has FIX sweep k-1
+    if ((st = hand_wait(c, c->stream, 2, c->ev_res[q], c->seq_of[q]))) return st;
+    if (b->norm && (st = hand_wait(c, c->stream, 3, c->ev_fixed[pq], c->seq_of[pq]))) return st;  // ... and so has FIX sweep k-1
     HIPC(c, launch_writeback(c->t, c->d_carry + (size_t)q * MAX_P, c->d_pipe + 4 + q, c->stream));
   }
   HIPC(c, launch_advance(a, c->stream));
@@ -874,9 +894,10 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k) {
   // merge .. patch on the side stream, overlapping sweep k+1 (block records
   // by parity; gather k may read the table while the write-back of round k-1
   // lands: only rows of round k-1's nodes change, and patch k replaces those)
-  HIPC(c, hipEventRecord(c->ev_swept[q], c->stream));
+  const uint32_t seq = ++c->round_seq;
+  c->seq_of[q] = seq;
   hipStream_t ss = c->sstream;
-  HIPC(c, hipStreamWaitEvent(ss, c->ev_swept[q], 0));
+  if ((st = hand_signal(c, c->stream, 0, c->ev_swept[q], seq)) || (st = hand_wait(c, ss, 0, c->ev_swept[q], seq))) return st;
   if (b->norm) HIPC(c, hipMemsetAsync(c->d_pstat, 0, (size_t)c->P * sizeof(PodStat), ss));
   HIPC(c, launch_merge(a, nloc, ss));
   if (b->norm) {
@@ -889,7 +910,7 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k) {
     f.fix = 1;
     f.pg = MAX_PG;
     HIPC(c, launch_sweep(f, true, bmax, (c->P + MAX_PG - 1) / MAX_PG, nloc, ss));
-    HIPC(c, hipEventRecord(c->ev_fixed[q], ss));  // the FIX sweep reads the table as sweep k did
+    if ((st = hand_signal(c, ss, 3, c->ev_fixed[q], seq))) return st;  // the FIX sweep reads the table as sweep k did
     HIPC(c, launch_merge(f, nloc, ss));
   }
   if (multi) {
@@ -900,11 +921,10 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k) {
   HIPC(c, launch_gather_cand(a, b->ext, ss));
   if (k > 0) {
     // merge round k-1's commits into the lists once resolve k-1 is done
-    HIPC(c, hipStreamWaitEvent(ss, c->ev_res[pq], 0));
+    if ((st = hand_wait(c, ss, 2, c->ev_res[pq], seq - 1))) return st;
     HIPC(c, launch_patch(a, b->ext, ss));
   }
-  HIPC(c, hipEventRecord(c->ev_sw[q], ss));
-  HIPC(c, hipStreamWaitEvent(c->rstream, c->ev_sw[q], 0));
+  if ((st = hand_signal(c, ss, 1, c->ev_sw[q], seq)) || (st = hand_wait(c, c->rstream, 1, c->ev_sw[q], seq))) return st;
   if (c->timing) {
     e0 = get_event(c);
     e1 = get_event(c);
@@ -915,7 +935,7 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k) {
     HIPC(c, hipEventRecord(e1, c->rstream));
     c->ev_resolve.emplace_back(e0, e1);
   }
-  HIPC(c, hipEventRecord(c->ev_res[q], c->rstream));
+  if ((st = hand_signal(c, c->rstream, 2, c->ev_res[q], seq))) return st;
   return KS_OK;
 }
 
@@ -1008,6 +1028,12 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
       HIPC(x, hipStreamCreateWithPriority(&x->rstream, hipStreamNonBlocking, hi));
       HIPC(x, hipStreamCreateWithPriority(&x->sstream, hipStreamNonBlocking, hi));
     }
+    {  // KS_VALUE_SYNC=0: cross-stream hand-offs by event waits instead
+      int can = 0;
+      (void)hipDeviceGetAttribute(&can, hipDeviceAttributeCanUseStreamWaitValue, cfg->device);
+      const char *v = std::getenv("KS_VALUE_SYNC");
+      x->value_sync = can != 0 && (v ? std::atoi(v) != 0 : true);
+    }
     for (int q = 0; q < 2; ++q) {
       HIPC(x, hipEventCreateWithFlags(&x->ev_sw[q], hipEventDisableTiming));
       HIPC(x, hipEventCreateWithFlags(&x->ev_res[q], hipEventDisableTiming));
@@ -1052,7 +1078,7 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
       (st = dalloc(x, &x->d_start, 1)) || (st = dalloc(x, &x->d_norm, 2 * 2 * (size_t)x->P)) ||
       (st = dalloc(x, &x->d_norm_inv, 2 * 2 * (size_t)x->P)) ||
       (st = dalloc(x, &x->d_pstat, (size_t)x->P)) || (st = dalloc(x, &x->d_fix, MAX_P + MAX_P / MAX_PG)) ||
-      (st = dalloc(x, &x->d_pipe, 8)) || (st = dalloc(x, &x->d_carry, 2 * (size_t)MAX_P)) ||
+      (st = dalloc(x, &x->d_pipe, 8)) || (st = dalloc(x, &x->d_flags, 4)) || (st = dalloc(x, &x->d_carry, 2 * (size_t)MAX_P)) ||
       (st = dalloc(x, &x->d_counters, 16)))
     return st;
   if ((st = xfer_begin(x, x->S * sizeof(Shard) + (size_t)x->cap * 4 + 1024, 0)) ||
@@ -1087,7 +1113,7 @@ void ks_close(ks_ctx *c) {
   void *bufs[] = {c->t.acpu, c->t.amem, c->t.rcpu, c->t.rmem, c->t.zcpu, c->t.zmem, c->t.apods,
                   c->t.npods, c->t.hard, c->t.prefer, c->t.lab, c->t.num, c->d_shards, c->d_slot_pos,
                   c->d_start, c->d_norm, c->d_norm_inv, c->d_pstat, c->d_fix, c->d_brec, c->d_srec, c->d_frec,
-                  c->d_counters, c->d_crow, c->d_cext, c->d_pipe, c->d_carry};
+                  c->d_counters, c->d_crow, c->d_cext, c->d_pipe, c->d_carry, c->d_flags};
   for (void *b : bufs)
     if (b) (void)hipFree(b);
   if (c->h_start) (void)hipHostFree(c->h_start);
