@@ -930,12 +930,18 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k) {
     e1 = get_event(c);
     HIPC(c, hipEventRecord(e0, c->rstream));
   }
-  HIPC(c, launch_resolve(a, b->ext, c->rstream));
+  {
+    RoundArgs ra = a;
+    ra.flag_res = c->value_sync ? c->d_flags + 2 : nullptr;
+    ra.seq = seq;
+    HIPC(c, launch_resolve(ra, b->ext, c->rstream));
+  }
   if (c->timing) {
     HIPC(c, hipEventRecord(e1, c->rstream));
     c->ev_resolve.emplace_back(e0, e1);
   }
-  if ((st = hand_signal(c, c->rstream, 2, c->ev_res[q], seq))) return st;
+  // the resolve kernel stores `seq` in flag 2 itself (no stream write operation after it)
+  HIPC(c, hipEventRecord(c->ev_res[q], c->rstream));
   return KS_OK;
 }
 

@@ -1414,6 +1414,14 @@ __device__ __forceinline__ uint64_t key_q(const PodDev &p, const PodQ &q, const 
   return pack_key(t, g.slot);
 }
 
+// Kernel-side completion signal for a stream wait-value (release at system
+// scope, like the stream write operation it replaces).
+__device__ __forceinline__ void signal_done(uint32_t *flag, uint32_t seq) {
+  if (flag == nullptr) return;
+  __threadfence_system();
+  __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 template <bool EXT>
 __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
   __shared__ PodDev s_pod[MAX_P];
@@ -1455,6 +1463,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
       *a.d_start = start;
       *a.carry_out_n = 0;
       if (start < a.npods) a.counters[3] += 1;  // wasted (speculated) round
+      signal_done(a.flag_res, a.seq);
     }
     return;
   }
@@ -1986,6 +1995,10 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
     a.counters[0] += 1;        // rounds
     a.counters[1] += stop_at;  // pods resolved
   }
+  // the streams waiting for this round (write-back, patch) poll the flag:
+  // every thread's global stores are ordered before the signal
+  __syncthreads();
+  if (tid == 0) signal_done(a.flag_res, a.seq);
 }
 
 // ============================================================ pipeline

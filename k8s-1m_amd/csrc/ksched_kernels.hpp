@@ -46,6 +46,8 @@ struct RoundArgs {
   uint32_t *fix_flag;         // [P] the pod's guessed maxima were wrong: re-swept in FIX mode
   uint32_t *fix_group;        // [P / MAX_PG] any flagged pod in the group
   uint32_t fix;               // FIX-mode launch of sweep / merge
+  uint32_t *flag_res;         // resolve: round number `seq` stored here when done (null: the host signals)
+  uint32_t seq;
   BlockRec *brec;             // [local shards][P][bstride]
   uint64_t *srec;             // [S][P][rec_words(K)]
   uint64_t *frec;             // [P][rec_words(K)] (== srec when S == 1)
