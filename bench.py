@@ -151,10 +151,10 @@ def main():
 
 def run_c5(args, kind, sched, world, rank, t_setup):
     """configs[4] (C5): bursts scheduled to completion, each followed by its
-    watch-event log applied through ks_pods_remove / ks_nodes_upsert /
-    ks_nodes_delete.  Timed per step: the burst's ks_batch_run plus the log's
-    ABI calls; the log's generation (which needs the burst's bindings) and its
-    marshalling to ABI structs run outside the timed region."""
+    watch-event log applied in order through ks_events_apply.  Timed per step:
+    the burst's ks_batch_run plus the log's ks_events_apply call; the log's
+    generation (which needs the burst's bindings) and its marshalling to ABI
+    structs run outside the timed region."""
     from ksched.framework import results_to_arrays
     from ksched.stream import BurstStream, GpuTarget
 
@@ -189,15 +189,17 @@ def run_c5(args, kind, sched, world, rank, t_setup):
             scheduled += int((r["status"] == 0).sum())
         stream.record(b, res)
         sched.free(batch)
-        ops = stream.marshal(stream.make_events())  # the API server's side, untimed
+        # the API server's side (log generation, ABI structs) is untimed
+        ev, ne, keep = stream.event_log(stream.marshal(stream.make_events()))
         barrier()
         t0 = time.perf_counter()
-        stream.apply_marshalled(ops, [target])  # each ABI call returns with its device work done
+        target.apply_events(ev, ne)  # ks_events_apply: the ordered log, device work done on return
         barrier()
         dt = time.perf_counter() - t0
+        del keep
         if timed:
             t_ev += dt
-            n_events += sum(o[3] for o in ops)
+            n_events += ne
     sched.set_timing(False)
     elapsed = t_run + t_ev
     if world > 1:

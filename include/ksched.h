@@ -259,6 +259,30 @@ ks_status ks_nodes_delete(ks_ctx *ctx, const uint32_t *slots, uint32_t n);
 ks_status ks_pods_add(ks_ctx *ctx, const ks_pod *pods, const uint32_t *slots, uint32_t n);
 ks_status ks_pods_remove(ks_ctx *ctx, const ks_pod *pods, const uint32_t *slots, uint32_t n);
 
+/* One informer event of an ordered log (the delta feed of SURVEY §8(f) F2:
+ * upstream internal/cache AddPod / RemovePod / AddNode / UpdateNode /
+ * RemoveNode as the reference's informers deliver them, scheduler.go:200-228).
+ * kind selects the payload: pod (KS_EV_POD_*) or node (KS_EV_NODE_UPSERT);
+ * slot is the node slot the event applies to. */
+enum {
+  KS_EV_POD_ADD = 0,     /* NodeInfo.AddPod: a pod bound (or assumed) on slot */
+  KS_EV_POD_REMOVE = 1,  /* NodeInfo.RemovePod: a pod deleted from slot */
+  KS_EV_NODE_UPSERT = 2, /* AddNode / UpdateNode (keeps the slot's pods) */
+  KS_EV_NODE_DELETE = 3, /* RemoveNode (its pods leave with it) */
+};
+typedef struct {
+  int32_t kind;
+  uint32_t slot;
+  const ks_pod *pod;   /* KS_EV_POD_ADD / KS_EV_POD_REMOVE */
+  const ks_node *node; /* KS_EV_NODE_UPSERT */
+} ks_event;
+
+/* Apply an event log in order: the state afterwards equals applying each
+ * event alone, one after the other.  Consecutive events of one kind go to the
+ * device as one batch (pod deltas commute; upserts of one slot keep the last
+ * state).  On error the events before the failing run are applied. */
+ks_status ks_events_apply(ks_ctx *ctx, const ks_event *events, uint32_t n);
+
 /* schedulePod for a stream of pods, in order: each pod is scheduled against
  * the cache as left by the previous one (AssumePod commit), exactly as
  * sequential ScheduleOne calls.  out[i] receives pod i's result. */

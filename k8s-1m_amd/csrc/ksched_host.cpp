@@ -1338,6 +1338,43 @@ ks_status ks_pods_remove(ks_ctx *c, const ks_pod *pods, const uint32_t *slots, u
   return pods_delta(c, pods, slots, n, -1);
 }
 
+ks_status ks_events_apply(ks_ctx *c, const ks_event *ev, uint32_t n) {
+  if (!c || (n && !ev)) return KS_ERR_INVALID;
+  std::vector<ks_pod> pods;
+  std::vector<ks_node> nodes;
+  std::vector<uint32_t> slots;
+  for (uint32_t i = 0; i < n;) {
+    const int32_t kind = ev[i].kind;
+    if (kind < KS_EV_POD_ADD || kind > KS_EV_NODE_DELETE)
+      return c->fail(KS_ERR_INVALID, "event %u: unknown kind %d", i, kind);
+    uint32_t j = i;
+    pods.clear();
+    nodes.clear();
+    slots.clear();
+    for (; j < n && ev[j].kind == kind; ++j) {
+      slots.push_back(ev[j].slot);
+      if (kind == KS_EV_POD_ADD || kind == KS_EV_POD_REMOVE) {
+        if (!ev[j].pod) return c->fail(KS_ERR_INVALID, "event %u: no pod", j);
+        pods.push_back(*ev[j].pod);
+      } else if (kind == KS_EV_NODE_UPSERT) {
+        if (!ev[j].node) return c->fail(KS_ERR_INVALID, "event %u: no node", j);
+        nodes.push_back(*ev[j].node);
+      }
+    }
+    const uint32_t m = j - i;
+    ks_status st = KS_OK;
+    switch (kind) {
+      case KS_EV_POD_ADD: st = ks_pods_add(c, pods.data(), slots.data(), m); break;
+      case KS_EV_POD_REMOVE: st = ks_pods_remove(c, pods.data(), slots.data(), m); break;
+      case KS_EV_NODE_UPSERT: st = ks_nodes_upsert(c, nodes.data(), slots.data(), m); break;
+      default: st = ks_nodes_delete(c, slots.data(), m); break;
+    }
+    if (st) return st;
+    i = j;
+  }
+  return KS_OK;
+}
+
 ks_status ks_batch_prepare(ks_ctx *c, const ks_pod *pods, uint32_t n, ks_batch **out) {
   if (!c || !out || (n && !pods)) return KS_ERR_INVALID;
   *out = nullptr;

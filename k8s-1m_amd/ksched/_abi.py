@@ -103,6 +103,15 @@ class KsPod(C.Structure):
 NUM_FILTER_PLUGINS = 5
 
 
+class KsEvent(C.Structure):
+    _fields_ = [
+        ("kind", C.c_int32),
+        ("slot", C.c_uint32),
+        ("pod", C.POINTER(KsPod)),
+        ("node", C.POINTER(KsNode)),
+    ]
+
+
 class KsResult(C.Structure):
     _fields_ = [
         ("node_index", C.c_int32),
@@ -177,20 +186,20 @@ class KsStats(C.Structure):
 # sizes from the C headers (checked in tests/test_abi.py against offsetof via the compiler)
 EXPECTED_SIZES = {
     "ks_label": 16, "ks_taint": 24, "ks_toleration": 24, "ks_node": 64, "ks_container": 24,
-    "ks_requirement": 24, "ks_term": 24, "ks_preferred_term": 32, "ks_pod": 128, "ks_result": 48,
+    "ks_requirement": 24, "ks_term": 24, "ks_preferred_term": 32, "ks_pod": 128, "ks_event": 24, "ks_result": 48,
     "ks_node_score": 40, "ks_node_state": 56, "ks_config": 56, "ks_stats": 64,
 }
 STRUCTS = {
     "ks_label": KsLabel, "ks_taint": KsTaint, "ks_toleration": KsToleration, "ks_node": KsNode,
     "ks_container": KsContainer, "ks_requirement": KsRequirement, "ks_term": KsTerm,
-    "ks_preferred_term": KsPreferredTerm, "ks_pod": KsPod, "ks_result": KsResult,
+    "ks_preferred_term": KsPreferredTerm, "ks_pod": KsPod, "ks_event": KsEvent, "ks_result": KsResult,
     "ks_node_score": KsNodeScore, "ks_node_state": KsNodeState, "ks_config": KsConfig,
     "ks_stats": KsStats,
 }
 
 KSCHED_SYMBOLS = [
     "ks_config_default", "ks_open", "ks_close", "ks_last_error", "ks_abi_version", "ks_nodes_upsert",
-    "ks_nodes_delete", "ks_pods_add", "ks_pods_remove", "ks_schedule", "ks_batch_prepare", "ks_batch_run",
+    "ks_nodes_delete", "ks_pods_add", "ks_pods_remove", "ks_events_apply", "ks_schedule", "ks_batch_prepare", "ks_batch_run",
     "ks_batch_results", "ks_batch_free", "ks_plugin_scores", "ks_node_states", "ks_comm_unique_id",
     "ks_comm_init", "ks_comm_allreduce_max", "ks_get_stats", "ks_reset_stats", "ks_set_timing",
     "ks_debug_counters",
@@ -240,6 +249,7 @@ def ksched_lib() -> C.CDLL:
     L.ks_nodes_delete.argtypes = [vp, P(C.c_uint32), C.c_uint32]
     L.ks_pods_add.argtypes = [vp, P(KsPod), P(C.c_uint32), C.c_uint32]
     L.ks_pods_remove.argtypes = [vp, P(KsPod), P(C.c_uint32), C.c_uint32]
+    L.ks_events_apply.argtypes = [vp, P(KsEvent), C.c_uint32]
     L.ks_schedule.argtypes = [vp, P(KsPod), C.c_uint32, P(KsResult)]
     L.ks_batch_prepare.argtypes = [vp, P(KsPod), C.c_uint32, P(vp)]
     L.ks_batch_run.argtypes = [vp, vp]

@@ -76,6 +76,9 @@ class GpuTarget:
     def remove_pods(self, arr, slots, n):
         self._ok(self.s.lib.ks_pods_remove(self.s.ctx, arr, slots, n))
 
+    def apply_events(self, ev, n):
+        self._ok(self.s.lib.ks_events_apply(self.s.ctx, ev, n))
+
     def schedule(self, arr, n):
         return self.s.schedule_raw(arr, n)
 
@@ -204,6 +207,28 @@ class BurstStream:
             else:
                 raise ValueError(op)
         return out
+
+    @staticmethod
+    def event_log(ops):
+        """The marshalled log as one ks_event array for ks_events_apply (the
+        ordered delta feed): (array, count, keep-alive of the payloads)."""
+        n = sum(o[3] for o in ops)
+        ev = (_abi.KsEvent * max(1, n))()
+        kinds = {"remove_pods": 1, "update_nodes": 2, "add_nodes": 2, "delete_nodes": 3}
+        i = 0
+        for op, arr, sl, m in ops:
+            k = kinds[op]
+            T = _abi.KsPod if k == 1 else _abi.KsNode
+            for j in range(m):
+                e = ev[i]
+                e.kind = k
+                e.slot = sl[j]
+                if k == 1:
+                    e.pod = C.cast(C.addressof(arr) + j * C.sizeof(T), C.POINTER(T))
+                elif k == 2:
+                    e.node = C.cast(C.addressof(arr) + j * C.sizeof(T), C.POINTER(T))
+                i += 1
+        return ev, n, ops
 
     @staticmethod
     def apply_marshalled(ops, targets):

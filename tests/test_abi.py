@@ -53,11 +53,12 @@ C_PROBE = r"""
 #define O(t, f) printf(#t "." #f " %zu\n", offsetof(t, f));
 int main(void) {
   S(ks_label) S(ks_taint) S(ks_toleration) S(ks_node) S(ks_container) S(ks_requirement) S(ks_term)
-  S(ks_preferred_term) S(ks_pod) S(ks_result) S(ks_node_score) S(ks_node_state) S(ks_config) S(ks_stats)
+  S(ks_preferred_term) S(ks_pod) S(ks_event) S(ks_result) S(ks_node_score) S(ks_node_state) S(ks_config) S(ks_stats)
   O(ks_node, labels) O(ks_node, n_labels) O(ks_node, unschedulable)
   O(ks_pod, node_name) O(ks_pod, overhead_milli_cpu) O(ks_pod, n_containers) O(ks_pod, has_required)
   O(ks_pod, has_preferred) O(ks_pod, has_overhead)
   O(ks_result, total_score) O(ks_result, fail_counts) O(ks_result, flags)
+  O(ks_event, pod) O(ks_event, node)
   O(ks_node_score, total_score) O(ks_config, weight_fit) O(ks_config, weight_image)
   O(ks_stats, sweep_ms) O(ks_stats, resolve_launches)
   return 0;

@@ -71,6 +71,32 @@ def test_c5_1m_incremental_equals_rebuild():
     s.close()
 
 
+def test_event_log_equals_separate_calls():
+    # ks_events_apply (one ordered log per burst) leaves the same cache as the
+    # per-kind calls, burst after burst, and later bursts schedule identically
+    n, bursts, burst = 100_000, 3, 20_000
+    st = BurstStream(synth.HETERO, n, bursts + 1, burst, rates=Rates(0.05, 0.01, 0.002))
+    a, b = Scheduler(n), Scheduler(n)
+    ga, gb = GpuTarget(a), GpuTarget(b)
+    st.setup([ga, gb])
+    for k in range(bursts):
+        arr, m = st.burst_pods(k)
+        ra, rb = ga.schedule(arr, m), gb.schedule(arr, m)
+        assert_results_equal(ra, rb, m, f"burst {k}")
+        st.record(k, ra)
+        ops = st.marshal(st.make_events())
+        st.apply_marshalled(ops, [ga])
+        ev, ne, keep = st.event_log(ops)
+        assert ne > 0
+        gb.apply_events(ev, ne)
+    sa = states_np(a.lib.ks_node_states, a.ctx, n)
+    assert np.array_equal(sa, states_np(b.lib.ks_node_states, b.ctx, n))
+    arr, m = st.burst_pods(bursts)
+    assert_results_equal(a.schedule_raw(arr, m), b.schedule_raw(arr, m), m, "after the logs")
+    a.close()
+    b.close()
+
+
 def test_c2_batched_equals_sequential():
     # configs[1] shape (100k nodes): the in-order batched commit (P = 256) equals
     # one-pod-at-a-time scheduling (P = 1) on the same device, for 20k pods,
