@@ -395,37 +395,40 @@ __device__ __forceinline__ PodDev load_pod(const PodDev *pods, uint32_t i) {
 // read: straight-line AND / OR over the words in use, no per-word branches.
 template <int NPL, int LWU>
 __device__ __forceinline__ void clause_pass_n(const uint64_t *c, const NodeExt (&e)[NPL], const NodeRegs (&nr)[NPL],
-                                              bool (&pass)[NPL]) {
+                                              uint32_t (&pass)[NPL]) {
+  // Results are 0 / 1 in vector registers (not lane masks): the term
+  // bookkeeping below is then plain VALU and-or, with no exec-mask merging of
+  // booleans across the clause loop's uniform branches.
   const uint64_t w0 = c[0];
-  const uint32_t kind = (uint32_t)w0 & 0xFF;
+  const uint32_t kind = uniform_u32((uint32_t)w0 & 0xFF);
   uint64_t m[LWU];
 #pragma unroll
   for (int k = 0; k < LWU; ++k) m[k] = c[1 + k];
-  const int64_t x = (int64_t)c[5];
-  const bool col1 = (w0 >> 8) & 1u;
-  auto any = [&](const NodeExt &n) {
+  static_for<NPL>([&](auto J) {
+    constexpr int j = J;
     uint64_t acc = 0;
 #pragma unroll
-    for (int k = 0; k < LWU; ++k) acc |= n.lab[k] & m[k];
-    return acc != 0;
-  };
-  // one wave-uniform branch per clause, the node loop inside each case
-  if (kind == CK_ANY) {
-    static_for<NPL>([&](auto J) { pass[J] = any(e[J]); });
-  } else if (kind == CK_NONE) {
-    static_for<NPL>([&](auto J) { pass[J] = !any(e[J]); });
-  } else if (kind == CK_GT || kind == CK_LT) {
-    const bool gt = kind == CK_GT;
+    for (int k = 0; k < LWU; ++k) acc |= e[j].lab[k] & m[k];
+    pass[j] = acc != 0 ? 1u : 0u;
+  });
+  if (kind == CK_NONE) {
+    static_for<NPL>([&](auto J) { pass[J] ^= 1u; });
+  } else if (kind != CK_ANY) {  // rare kinds
+    const int64_t x = (int64_t)c[5];
+    const bool col1 = (w0 >> 8) & 1u;
     static_for<NPL>([&](auto J) {
-      const int64_t v = col1 ? e[J].num[1] : e[J].num[0];
-      pass[J] = any(e[J]) && (gt ? v > x : v < x);
+      constexpr int j = J;
+      const int64_t v = col1 ? e[j].num[1] : e[j].num[0];
+      bool ok;
+      switch (kind) {
+        case CK_GT: ok = pass[j] && v > x; break;
+        case CK_LT: ok = pass[j] && v < x; break;
+        case CK_NAME_EQ: ok = (int64_t)nr[j].slot == x; break;
+        case CK_NAME_NE: ok = (int64_t)nr[j].slot != x; break;
+        default: ok = false; break;
+      }
+      pass[j] = ok ? 1u : 0u;
     });
-  } else if (kind == CK_NAME_EQ) {
-    static_for<NPL>([&](auto J) { pass[J] = (int64_t)nr[J].slot == x; });
-  } else if (kind == CK_NAME_NE) {
-    static_for<NPL>([&](auto J) { pass[J] = (int64_t)nr[J].slot != x; });
-  } else {
-    static_for<NPL>([&](auto J) { pass[J] = false; });
   }
 }
 
@@ -433,47 +436,54 @@ __device__ __forceinline__ void clause_pass_n(const uint64_t *c, const NodeExt (
 template <int NPL, int LWU>
 __device__ __forceinline__ void required_match_n(const PodDev &p, const uint64_t *clauses, const NodeExt (&e)[NPL],
                                                  const NodeRegs (&nr)[NPL], bool (&out)[NPL]) {
-  bool sel[NPL], any[NPL], cur[NPL];
-  static_for<NPL>([&](auto J) { sel[J] = true; any[J] = false; cur[J] = true; });
+  uint32_t sel[NPL], any[NPL], cur[NPL];
+  static_for<NPL>([&](auto J) { sel[J] = 1u; any[J] = 0u; cur[J] = 1u; });
   uint32_t curterm = 0;
   const uint64_t *c = clauses + (size_t)p.req_off * CLAUSE_WORDS;
   for (uint32_t k = 0; k < p.req_len; ++k, c += CLAUSE_WORDS) {
     const uint32_t term = uniform_u32(((uint32_t)c[0] >> 16) & 0xFFFF);
-    if (term != curterm) {
-      if (curterm >= 1) static_for<NPL>([&](auto J) { any[J] |= cur[J]; });
-      static_for<NPL>([&](auto J) { cur[J] = true; });
-      curterm = term;
-    }
-    bool pass[NPL];
+    // a new term closes the previous one (terms >= 1 are OR-ed) and restarts
+    const uint32_t close = (term != curterm && curterm >= 1) ? 1u : 0u;
+    const uint32_t open = term != curterm ? 1u : 0u;
+    curterm = term;
+    uint32_t pass[NPL];
     clause_pass_n<NPL, LWU>(c, e, nr, pass);
-    if (term == 0) static_for<NPL>([&](auto J) { sel[J] &= pass[J]; });
-    else static_for<NPL>([&](auto J) { cur[J] &= pass[J]; });
+    const uint32_t in_sel = term == 0 ? 1u : 0u;  // term 0: the nodeSelector group (AND)
+    static_for<NPL>([&](auto J) {
+      any[J] |= cur[J] & close;
+      cur[J] |= open;
+      sel[J] &= pass[J] | (in_sel ^ 1u);
+      cur[J] &= pass[J] | in_sel;
+    });
   }
-  if (curterm >= 1) static_for<NPL>([&](auto J) { any[J] |= cur[J]; });
-  static_for<NPL>([&](auto J) { out[J] = sel[J] && (p.n_req_terms == 0 || any[J]); });
+  const uint32_t last = curterm >= 1 ? 1u : 0u;
+  const bool noterms = p.n_req_terms == 0;
+  static_for<NPL>([&](auto J) { out[J] = sel[J] && (noterms || ((any[J] | (cur[J] & last)) != 0)); });
 }
 
 // preferred_raw for NPL nodes at once
 template <int NPL, int LWU>
 __device__ __forceinline__ void preferred_raw_n(const PodDev &p, const uint64_t *clauses, const NodeExt (&e)[NPL],
                                                 const NodeRegs (&nr)[NPL], uint32_t (&raw)[NPL]) {
-  bool cur[NPL];
-  static_for<NPL>([&](auto J) { raw[J] = 0u; cur[J] = true; });
+  uint32_t cur[NPL];
+  static_for<NPL>([&](auto J) { raw[J] = 0u; cur[J] = 1u; });
   uint32_t curterm = 0, wcur = 0;
   const uint64_t *c = clauses + (size_t)p.pref_off * CLAUSE_WORDS;
   for (uint32_t k = 0; k < p.pref_len; ++k, c += CLAUSE_WORDS) {
     const uint32_t term = uniform_u32(((uint32_t)c[0] >> 16) & 0xFFFF);
-    if (term != curterm) {
-      if (curterm >= 1) static_for<NPL>([&](auto J) { raw[J] += cur[J] ? wcur : 0u; });
-      static_for<NPL>([&](auto J) { cur[J] = true; });
-      curterm = term;
-      wcur = uniform_u32((uint32_t)(c[0] >> 32));
-    }
-    bool pass[NPL];
+    const uint32_t wclose = (term != curterm && curterm >= 1) ? wcur : 0u;  // weight of the term closed here
+    const uint32_t open = term != curterm ? 1u : 0u;
+    if (term != curterm) wcur = uniform_u32((uint32_t)(c[0] >> 32));
+    curterm = term;
+    uint32_t pass[NPL];
     clause_pass_n<NPL, LWU>(c, e, nr, pass);
-    static_for<NPL>([&](auto J) { cur[J] &= pass[J]; });
+    static_for<NPL>([&](auto J) {
+      raw[J] += cur[J] * wclose;
+      cur[J] = (cur[J] | open) & pass[J];
+    });
   }
-  if (curterm >= 1) static_for<NPL>([&](auto J) { raw[J] += cur[J] ? wcur : 0u; });
+  const uint32_t wlast = curterm >= 1 ? wcur : 0u;
+  static_for<NPL>([&](auto J) { raw[J] += cur[J] * wlast; });
 }
 
 // DefaultNormalizeScore's floor(100 * raw / max) for 0 <= raw <= max < 2^25
