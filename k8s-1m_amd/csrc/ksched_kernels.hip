@@ -1239,11 +1239,13 @@ __global__ __launch_bounds__(PATCH_THREADS) void patch_kernel(RoundArgs a) {
 //                      pod i+1 and its filter-status change since the round
 //                      start; per wave the best two (key, node) and the summed
 //                      status changes
-//   eval wave   (8)    every node that can win pod i (the candidates above and
-//                      w_{i-1}) committed: its key and status change for pod
-//                      i+1, speculatively, one candidate per lane
+//   eval wave   (8)    every owner / listed candidate of pod i committed: its
+//                      key and status change for pod i+1, speculatively, one
+//                      candidate per lane (independent of pod i-1's decision)
 //   decider     (9)    pod i from those partials, the last winners' stale
-//                      entries replaced by the eval wave's values for w_{i-1}
+//                      entries replaced by the prev wave's values for w_{i-1}
+//   prev wave   (10)   w_{i-1} (state: the eval output for pod i-1) committed
+//                      with pod i and evaluated against pod i+1
 // Node state is exact binary64 throughout (CandRow), so a re-score is a short
 // dependent chain; every role reads its inputs for a pod in one batch of LDS
 // loads.
