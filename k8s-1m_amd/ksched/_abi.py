@@ -101,6 +101,9 @@ class KsPod(C.Structure):
 
 
 NUM_FILTER_PLUGINS = 5
+# ks_status codes and ks_event kinds (include/ksched.h)
+KS_OK, KS_ERR_INVALID = 0, 1
+KS_EV_POD_ADD, KS_EV_POD_REMOVE, KS_EV_NODE_UPSERT, KS_EV_NODE_DELETE = 0, 1, 2, 3
 
 
 class KsEvent(C.Structure):

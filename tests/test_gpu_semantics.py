@@ -6,7 +6,7 @@ import numpy as np
 import pytest
 
 import pyoracle
-from helpers import assert_results_equal, res_array, scores_array
+from helpers import assert_results_equal, res_array, scores_array, states_np
 from ksched import Scheduler, _abi
 from ksched.objects import Arena, nodes_array, pods_array
 from scenarios import SCENARIOS, check
@@ -100,3 +100,51 @@ def test_wrong_normaliser_guess_is_reswept():
     assert_results_equal(got, want, m, "normalizer_guess_wrong")
     check(res_array(got, m), exp)
     assert dbg[4] == 3, list(dbg)
+
+
+def test_event_log_mixed_kinds_in_order():
+    # one ks_events_apply log mixing every kind, with order dependence (a pod
+    # added to a node that is deleted, re-added and updated in the same log)
+    # equals the oracle applying the same events one call at a time
+    from scenarios import node, pod
+
+    Gi = 1 << 30
+    a = Arena()
+    na, n = nodes_array([node(f"n{i}") for i in range(6)], a)
+    fresh, _ = nodes_array([node("new2", cpu=8000, mem=16 * Gi), node("n3", cpu=64000, pods=110)], a)
+    pa, _ = pods_array([pod("p1", cpu=1500, mem=2 * Gi), pod("p2", cpu=300), pod("be")], a)
+    slots = (C.c_uint32 * n)(*range(n))
+    o = pyoracle.Oracle(n)
+    o.upsert(na, slots, n)
+    log = [  # (kind, slot, pod index, node index)
+        (_abi.KS_EV_POD_ADD, 1, 0, None), (_abi.KS_EV_POD_ADD, 2, 1, None), (_abi.KS_EV_POD_ADD, 2, 2, None),
+        (_abi.KS_EV_NODE_DELETE, 2, None, None), (_abi.KS_EV_NODE_UPSERT, 2, None, 0),
+        (_abi.KS_EV_POD_ADD, 2, 0, None), (_abi.KS_EV_POD_REMOVE, 1, 0, None),
+        (_abi.KS_EV_NODE_UPSERT, 3, None, 1), (_abi.KS_EV_POD_ADD, 3, 2, None), (_abi.KS_EV_POD_ADD, 3, 2, None),
+    ]
+    ev = (_abi.KsEvent * len(log))()
+    for i, (k, sl, pi, ni) in enumerate(log):
+        ev[i].kind, ev[i].slot = k, sl
+        if pi is not None:
+            ev[i].pod = C.pointer(pa[pi])
+        if ni is not None:
+            ev[i].node = C.pointer(fresh[ni])
+        one = (C.c_uint32 * 1)(sl)
+        if k == _abi.KS_EV_POD_ADD:
+            o.add_pods(C.pointer(pa[pi]), one, 1)
+        elif k == _abi.KS_EV_POD_REMOVE:
+            o.remove_pods(C.pointer(pa[pi]), one, 1)
+        elif k == _abi.KS_EV_NODE_UPSERT:
+            o.upsert(C.pointer(fresh[ni]), one, 1)
+        else:
+            o.delete(one, 1)
+    with Scheduler(n) as s:
+        s.upsert_nodes_raw(na, slots, n)
+        assert s.lib.ks_events_apply(s.ctx, ev, len(log)) == 0, s.lib.ks_last_error(s.ctx)
+        got = states_np(s.lib.ks_node_states, s.ctx, n)
+        want = states_np(o.L.oracle_node_states, o.o, n)
+        assert np.array_equal(got, want), (got, want)
+        bad = (_abi.KsEvent * 1)()
+        bad[0].kind = 7
+        assert s.lib.ks_events_apply(s.ctx, bad, 1) == _abi.KS_ERR_INVALID
+        assert b"unknown kind" in s.lib.ks_last_error(s.ctx)
