@@ -1595,12 +1595,14 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
 #endif
   lds_barrier();
 
-  auto iteration = [&](uint32_t r) -> bool {
+  // ROLE: 0 decider, 1 eval / prev, 2 owner, 3 list (one loop per role below)
+  auto iteration = [&](uint32_t r, auto role) __attribute__((always_inline)) -> bool {
+    constexpr int ROLE = decltype(role)::value;
     const uint32_t buf = r & 1u, nb = buf ^ 1u;
 #ifdef KS_STAMPS
     STAMP_NOW(t0);
 #endif
-    if (wid == RES_DEC_WAVE) {
+    if constexpr (ROLE == 0) {
       // ------------------------------------------------------------- decider
       if (r >= nround) {
         if (lane == 0) {
@@ -1731,7 +1733,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
 #endif
         }
       }
-    } else if (wid == RES_EVAL_WAVE || wid == RES_PREV_WAVE) {
+    } else if constexpr (ROLE == 1) {
       if (ROLE_ON(4)) {
       // ------------------------------------------------ eval and prev waves
       // every candidate of pod r committed, evaluated against pod r+1: the
@@ -1860,7 +1862,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
 #endif
       }
       }
-    } else if (is_owner) {
+    } else if constexpr (ROLE == 2) {
       if (ROLE_ON(2)) {
       // ------------------------------------------------------- owner waves
       if (r >= 1) {  // apply pod r-1's commit: its winner's owner adds the pod
@@ -1972,8 +1974,22 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
     return s_done != 0;
   };
 
-  for (uint32_t r = 0;; ++r)
-    if (iteration(r)) break;
+  // One loop per role (the barrier counts waves, not program locations): each
+  // copy of the inlined iteration keeps only its own role's state live, so no
+  // wave pays the phi moves of the other roles' registers at the loop latch.
+  if (wid == RES_DEC_WAVE) {
+    for (uint32_t r = 0;; ++r)
+      if (iteration(r, std::integral_constant<int, 0>{})) break;
+  } else if (wid == RES_EVAL_WAVE || wid == RES_PREV_WAVE) {
+    for (uint32_t r = 0;; ++r)
+      if (iteration(r, std::integral_constant<int, 1>{})) break;
+  } else if (is_owner) {
+    for (uint32_t r = 0;; ++r)
+      if (iteration(r, std::integral_constant<int, 2>{})) break;
+  } else {
+    for (uint32_t r = 0;; ++r)
+      if (iteration(r, std::integral_constant<int, 3>{})) break;
+  }
   if (is_list) __builtin_amdgcn_s_waitcnt(0);  // no DMA outlives the block
   // hand the nodes this round modified to the next round's patch and the write-back
   if (is_owner && mine && ROLE_ON(7)) {
