@@ -1254,7 +1254,28 @@ constexpr int RES_OWN_WAVES = 4;
 constexpr int RES_EVAL_WAVE = RES_LIST_WAVES + RES_OWN_WAVES;
 constexpr int RES_DEC_WAVE = RES_EVAL_WAVE + 1;
 constexpr int RES_PREV_WAVE = RES_DEC_WAVE + 1;
-constexpr int RESOLVE_THREADS = (RES_PREV_WAVE + 1) * WAVE;
+constexpr int RES_IDLE = 15;                              // a wave with no role: barriers only
+// Hardware wave h of a workgroup runs on SIMD h % 4 (round-robin dispatch onto
+// the reserved CU).  KS_RES_LAYOUT 1 (default): 16 waves, the decider alone on
+// its SIMD, the eval and prev waves on another, list and owner waves on the
+// last two; 0: 11 waves, roles in wave order (3 per SIMD, the decider with a
+// list and an owner wave).
+#ifndef KS_RES_LAYOUT
+#define KS_RES_LAYOUT 1
+#endif
+#if KS_RES_LAYOUT == 1
+constexpr int RES_HW_WAVES = 16;
+__device__ __forceinline__ uint32_t res_role(uint32_t hw) {
+  // SIMD 0: eval, prev | 1: decider | 2: list 0, owner 0, list 2, owner 2 | 3: list 1, owner 1, list 3, owner 3
+  constexpr uint8_t tab[16] = {RES_EVAL_WAVE, RES_DEC_WAVE, 0, 1, RES_PREV_WAVE, RES_IDLE, 4, 5,
+                               RES_IDLE,      RES_IDLE,     2, 3, RES_IDLE,      RES_IDLE, 6, 7};
+  return tab[hw & 15];
+}
+#else
+constexpr int RES_HW_WAVES = RES_PREV_WAVE + 1;
+__device__ __forceinline__ uint32_t res_role(uint32_t hw) { return hw; }
+#endif
+constexpr int RESOLVE_THREADS = RES_HW_WAVES * WAVE;
 constexpr int RHASH = 1024;
 constexpr int LSEL = 4;                                   // listed candidates kept per list wave
 constexpr int LAHEAD = 3;                                 // list waves select pod i + LAHEAD in iteration i
@@ -1465,7 +1486,10 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
   // results of the round, written out after the loop (no global stores inside it)
   __shared__ DevResult s_res[MAX_P];
 
-  const uint32_t tid = threadIdx.x, lane = tid % WAVE, wid = tid / WAVE;
+  // tid: hardware thread (staging loops); wid / rtid: the wave's role and the
+  // thread's index in role order (list entry, owned node)
+  const uint32_t tid = threadIdx.x, lane = tid % WAVE;
+  const uint32_t wid = __builtin_amdgcn_readfirstlane(res_role(tid / WAVE)), rtid = wid * WAVE + lane;
   const uint32_t start = uniform_u32(*a.act);
   // The lists were swept for the pods from *sstart (speculatively); if the
   // previous round stopped early they belong to other pods: resolve nothing.
@@ -1484,7 +1508,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
   const bool is_list = wid < RES_LIST_WAVES;
   const bool is_owner = wid >= RES_LIST_WAVES && wid < RES_EVAL_WAVE;
   const uint32_t ow = wid - RES_LIST_WAVES;         // owner wave
-  const uint32_t mj = tid - RES_LIST_WAVES * WAVE;  // owner thread: owned modified node
+  const uint32_t mj = rtid - RES_LIST_WAVES * WAVE;  // owner thread: owned modified node
   // ---- stage the round
   for (uint32_t i = tid; i < RHASH; i += RESOLVE_THREADS) s_hkey[i] = 0;
   for (uint32_t i = tid; i < nround; i += RESOLVE_THREADS) {
@@ -1524,11 +1548,11 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
   auto list_select = [&](uint32_t pod) {
     const bool real = pod < nround;
     const uint32_t p = real ? pod : nround - 1;
-    const uint64_t k = lds_key(pod % KSLOTS, tid);
+    const uint64_t k = lds_key(pod % KSLOTS, rtid);
     const uint32_t nk = s_hdr[p].nkeys;
     bool unmod = false;
     const uint32_t slot = 0xFFFFFFFFu - (uint32_t)k;
-    if (real && k != 0 && tid < nk) {
+    if (real && k != 0 && rtid < nk) {
       uint32_t h = rhash(slot);
       unmod = true;
       while (s_hkey[h] != 0) {
@@ -1986,6 +2010,11 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
   } else if (is_owner) {
     for (uint32_t r = 0;; ++r)
       if (iteration(r, std::integral_constant<int, 2>{})) break;
+  } else if (wid == RES_IDLE) {
+    for (;;) {
+      lds_barrier();
+      if (s_done != 0) break;
+    }
   } else {
     for (uint32_t r = 0;; ++r)
       if (iteration(r, std::integral_constant<int, 3>{})) break;
