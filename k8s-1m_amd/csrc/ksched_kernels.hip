@@ -1550,17 +1550,18 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
     const uint32_t p = real ? pod : nround - 1;
     const uint64_t k = lds_key(pod % KSLOTS, rtid);
     const uint32_t nk = s_hdr[p].nkeys;
-    bool unmod = false;
+    bool unmod = false, hempty = false;
     const uint32_t slot = 0xFFFFFFFFu - (uint32_t)k;
     if (real && k != 0 && rtid < nk) {
       uint32_t h = rhash(slot);
       unmod = true;
+      hempty = s_hkey[h] == 0;
       while (s_hkey[h] != 0) {
         if (s_hkey[h] == slot + 1) { unmod = false; break; }
         h = (h + 1) & (RHASH - 1);
       }
     }
-    const uint64_t ub = __ballot(unmod);
+    const uint64_t ub = __ballot(unmod), hb = __ballot(hempty);
     const uint32_t nsel = min((uint32_t)__popcll(ub), (uint32_t)LSEL);
     // lane c < LSEL takes the c-th unmodified entry
     uint64_t m = ub;
@@ -1582,7 +1583,8 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
       }
       if (real) {
         s_lkey[pod % RSLOTS][LSEL * lw + lane] = lane < nsel ? tk : 0ull;
-        s_lidx[pod % RSLOTS][LSEL * lw + lane] = lane < nsel ? t : NONE32;
+        // bit 16: the entry's home hash bucket was empty when selected
+        s_lidx[pod % RSLOTS][LSEL * lw + lane] = lane < nsel ? t | (uint32_t)((hb >> te) & 1u) << 16 : NONE32;
       }
     }
   };
@@ -1606,15 +1608,26 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
   // owner thread: the modified node it owns (live state, in registers)
   bool mine = false;
   RNode own{};
+  // rank of the owned slot among its wave's owned slots (0 = lowest): owner
+  // reductions run on 32-bit keys (score + 1) << 6 | (63 - rank), which order
+  // like the packed 64-bit keys within one wave
+  uint32_t srank = 0;
   // decider state (wave-uniform): the last three commits, modified count, stop point
   uint32_t pvalid = 0, pcand = 0, pslot = NONE32, p2slot = NONE32, p3slot = NONE32, powner = 0, nmod = 0,
            stop_at = nround;
+  // hash buckets the last three pods' joins were inserted at (NONE32: no insert)
+  uint32_t pb1 = NONE32, pb2 = NONE32, pb3 = NONE32;
   // the decider is the per-pod critical path, the eval wave next: issue priority
   if (wid == RES_DEC_WAVE) __builtin_amdgcn_s_setprio(3);
   else if (wid == RES_EVAL_WAVE || wid == RES_PREV_WAVE) __builtin_amdgcn_s_setprio(2);
 #ifdef KS_STAMPS
+#if KS_STAMPS == 3  // list wave 0 and owner wave 0 in the decider / eval counters
+  const bool stamper = lane == 0 && (wid == 0 || wid == RES_LIST_WAVES);
+  const uint32_t sidx = wid == 0 ? 0 : 2;
+#else
   const bool stamper = lane == 0 && (wid == RES_DEC_WAVE || wid == RES_EVAL_WAVE);
   const uint32_t sidx = wid == RES_DEC_WAVE ? 0 : 2;
+#endif
   uint64_t st_work = 0, st_wait = 0, t0, t1, t2, ts, sub[4] = {0, 0, 0, 0};
 #endif
   lds_barrier();
@@ -1668,7 +1681,9 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
         const uint32_t vslot = is_own ? oslot : is_prev ? pslot : 0xFFFFFFFFu - (uint32_t)vkey;
         // entries computed before the last winners' commits are stale: drop them
         const uint64_t mk = ((is_own && vkey && vslot != pslot) || is_prev) ? vkey : 0ull;
-        const uint64_t bm = wave_max_u64_dpp(mk);
+        // nonzero only in lanes [0, 8) (owners) and CAND_PREV
+        static_assert(NCAND_OWN == 8, "owner candidates fill one 8-lane DPP group");
+        const uint64_t bm = max64(readlane64(max8_u64(mk), 0), readlane64(mk, CAND_PREV));
         const bool lok = is_lst && vidx != NONE32 && vslot != pslot && vslot != p2slot && vslot != p3slot;
         const uint64_t lb = __ballot(lok);  // listed candidates are in list order by lane
         const uint32_t ulane = lb ? (uint32_t)__builtin_ctzll(lb) : 0u;
@@ -1731,17 +1746,36 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
             const uint32_t wslot = 0xFFFFFFFFu - (uint32_t)win;
             if (join) {
               oidx = nmod++;
-              if (lane == 0) {
-                uint32_t h = rhash(wslot);
-                while (atomicCAS(&s_hkey[h], 0u, wslot + 1) != 0u) h = (h + 1) & (RHASH - 1);
+              // The home bucket was empty at selection (LAHEAD pods ago); only
+              // the last three joins can have filled it since: then a plain
+              // store, else probe with compare-and-swap.
+              const uint32_t home = rhash(wslot);
+              const bool hfree = ((uint32_t)__builtin_amdgcn_readlane((int)vidx, (int)ulane) >> 16 & 1u) &&
+                                 home != pb1 && home != pb2 && home != pb3;
+              uint32_t h = home;
+              if (hfree) {
+                if (lane == 0) s_hkey[home] = wslot + 1;
+              } else {
+                if (lane == 0)
+                  while (atomicCAS(&s_hkey[h], 0u, wslot + 1) != 0u) h = (h + 1) & (RHASH - 1);
+                h = __builtin_amdgcn_readfirstlane(h);
               }
+              pb3 = pb2;
+              pb2 = pb1;
+              pb1 = h;
             } else {
               oidx = cand == (uint32_t)CAND_PREV ? powner : (uint32_t)__builtin_amdgcn_readlane((int)vidx, (int)cand);
+              pb3 = pb2;
+              pb2 = pb1;
+              pb1 = NONE32;
             }
             pslot = wslot;
             powner = oidx;
           } else {
             pslot = NONE32;
+            pb3 = pb2;
+            pb2 = pb1;
+            pb1 = NONE32;
           }
           pvalid = win ? 1u : 0u;
           pcand = cand;
@@ -1893,6 +1927,12 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
         const uint32_t pv = uniform_u32(s_pend[nb][0]), pc = uniform_u32(s_pend[nb][1]);
         const uint32_t pj = uniform_u32(s_pend[nb][2]), po = uniform_u32(s_pend[nb][3]);
         const PodDev pp = lds_uniform(s_pod[r - 1], lane);  // every lane (readfirstlane)
+        if (pv && pj && po / WAVE == ow) {  // a listed node joins this wave: re-rank
+          const uint32_t js = 0xFFFFFFFFu - (uint32_t)s_lkey[(r - 1) % RSLOTS][pc - NCAND_OWN];
+          const uint32_t below = (uint32_t)__popcll(__ballot(mine && own.slot < js));
+          if (mine && own.slot > js) ++srank;
+          if (po == mj) srank = below;
+        }
         if (pv && po == mj) {
           if (pj) {  // a listed node joins: its row (DMA-staged for pod r-1, still resident)
             const uint32_t b8 = (r - 1) % RSLOTS, c = pc - NCAND_OWN, cw = c / LSEL, ck = c % LSEL;
@@ -1926,8 +1966,10 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
           const bool f0 = fit_q(q1, g0), f = fit_q(q1, g);
           key = (mine && f) ? key_q(p1, q1, g) : 0ull;
           dany = mine && f0 && !f;
-          d[0] = dany ? 1 : 0;
-          d[1 + KS_PLUGIN_FIT_IDX] = dany ? 1 : 0;
+          // a commit only adds: Fit failures are the only status change
+          const int32_t nlost = (int32_t)__popcll(__ballot(dany));
+          d[0] = nlost;
+          d[1 + KS_PLUGIN_FIT_IDX] = nlost;
         } else {
           const PodDev p1 = lds_uniform(s_pod[r + 1], lane);
           int64_t tt_max = 0, na_max = 0;
@@ -1952,23 +1994,26 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
             }
           }
         }
-        const uint64_t k1 = wave_max_u64_dpp(key);
-        const uint64_t k2 = wave_max_u64_dpp(key == k1 ? 0ull : key);
-        // the holders publish their node for the decider and the eval wave
-        if (key != 0 && (key == k1 || key == k2)) {
-          const uint32_t c = 2 * ow + (key == k1 ? 0u : 1u);
+        // total + 1 < 2^24 (weights capped at 10000), rank < 64
+        const uint32_t key32 = key ? (uint32_t)(key >> 32) << 6 | (63u - srank) : 0u;
+        const uint32_t k1 = wave_max_u32_dpp(key32);
+        const uint32_t k2 = wave_max_u32_dpp(key32 == k1 ? 0u : key32);
+        // the holders publish their node and packed key for the decider and the eval wave
+        if (key32 != 0 && (key32 == k1 || key32 == k2)) {
+          const uint32_t c = 2 * ow + (key32 == k1 ? 0u : 1u);
           s_ocand[nb][c] = own;
           if (EXT) s_ocandx[nb][c] = ox;
           s_oidx[nb][c] = mj;
+          s_okey[nb][c] = key;
         }
         const bool wdany = __ballot(dany) != 0;
-        if (wdany) {
+        if (EXT && wdany) {
 #pragma unroll
           for (int qq = 0; qq < NFILT + 3; ++qq) d[qq] = wave_sum_i32_dpp(d[qq]);
         }
         if (lane == 0) {
-          s_okey[nb][2 * ow] = k1;
-          s_okey[nb][2 * ow + 1] = k2;
+          if (k1 == 0) s_okey[nb][2 * ow] = 0;
+          if (k2 == 0) s_okey[nb][2 * ow + 1] = 0;
 #pragma unroll
           for (int qq = 0; qq < NFILT + 3; ++qq) s_dsum[nb][ow][qq] = wdany ? d[qq] : 0;
         }
@@ -1982,8 +2027,20 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
       // -------------------------------------------------------- list waves
       if (ROLE_ON(1)) {
       list_select(r + LAHEAD);
+#if KS_STAMPS == 3
+      STAMP_NOW(ts);
+      sub[0] += ts - t0;
+#endif
       dma_keys(r + LAHEAD + KAHEAD);
+#if KS_STAMPS == 3
+      STAMP_NOW(t2);
+      sub[1] += t2 - ts;
+#endif
       list_wait();
+#if KS_STAMPS == 3
+      STAMP_NOW(ts);
+      sub[2] += ts - t2;
+#endif
       }
     }
 #ifdef KS_STAMPS
@@ -2030,7 +2087,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
   if (stamper) {
     atomicAdd((unsigned long long *)&a.counters[8 + sidx], (unsigned long long)st_work);
     atomicAdd((unsigned long long *)&a.counters[9 + sidx], (unsigned long long)st_wait);
-    if (wid == (KS_STAMPS == 2 ? RES_EVAL_WAVE : RES_DEC_WAVE))
+    if (wid == (KS_STAMPS == 3 ? 0u : KS_STAMPS == 2 ? (uint32_t)RES_EVAL_WAVE : (uint32_t)RES_DEC_WAVE))
       for (int i = 0; i < 4; ++i) atomicAdd((unsigned long long *)&a.counters[12 + i], (unsigned long long)sub[i]);
   }
 #endif
