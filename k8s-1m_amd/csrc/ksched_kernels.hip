@@ -1261,9 +1261,17 @@ constexpr int RES_IDLE = 15;                              // a wave with no role
 // last two; 0: 11 waves, roles in wave order (3 per SIMD, the decider with a
 // list and an owner wave).
 #ifndef KS_RES_LAYOUT
-#define KS_RES_LAYOUT 1
+#define KS_RES_LAYOUT 2
 #endif
-#if KS_RES_LAYOUT == 1
+#if KS_RES_LAYOUT == 2
+constexpr int RES_HW_WAVES = 16;
+__device__ __forceinline__ uint32_t res_role(uint32_t hw) {
+  // SIMD 0: eval, prev, owner 2 | 1: decider, owner 3 | 2: list 0, owner 0, list 2 | 3: list 1, owner 1, list 3
+  constexpr uint8_t tab[16] = {RES_EVAL_WAVE, RES_DEC_WAVE, 0, 1, RES_PREV_WAVE, RES_IDLE, 4, 5,
+                               6,             7,            2, 3, RES_IDLE,      RES_IDLE, RES_IDLE, RES_IDLE};
+  return tab[hw & 15];
+}
+#elif KS_RES_LAYOUT == 1
 constexpr int RES_HW_WAVES = 16;
 __device__ __forceinline__ uint32_t res_role(uint32_t hw) {
   // SIMD 0: eval, prev | 1: decider | 2: list 0, owner 0, list 2, owner 2 | 3: list 1, owner 1, list 3, owner 3
@@ -1621,7 +1629,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
   if (wid == RES_DEC_WAVE) __builtin_amdgcn_s_setprio(3);
   else if (wid == RES_EVAL_WAVE || wid == RES_PREV_WAVE) __builtin_amdgcn_s_setprio(2);
 #ifdef KS_STAMPS
-#if KS_STAMPS == 3  // list wave 0 and owner wave 0 in the decider / eval counters
+#if KS_STAMPS >= 3  // list wave 0 and owner wave 0 in the decider / eval counters
   const bool stamper = lane == 0 && (wid == 0 || wid == RES_LIST_WAVES);
   const uint32_t sidx = wid == 0 ? 0 : 2;
 #else
@@ -1953,6 +1961,10 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
           rnode_add(own, pp);
         }
       }
+#if KS_STAMPS == 3
+      STAMP_NOW(t2);
+      sub[0] += t2 - t0;
+#endif
       if (r + 1 < nround && __ballot(mine) != 0) {
         uint64_t key = 0;
         int32_t d[NFILT + 3] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1994,10 +2006,20 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
             }
           }
         }
+#if KS_STAMPS == 3
+        STAMP_NOW(ts);
+        sub[1] += ts - t2;
+        t2 = ts;
+#endif
         // total + 1 < 2^24 (weights capped at 10000), rank < 64
         const uint32_t key32 = key ? (uint32_t)(key >> 32) << 6 | (63u - srank) : 0u;
         const uint32_t k1 = wave_max_u32_dpp(key32);
         const uint32_t k2 = wave_max_u32_dpp(key32 == k1 ? 0u : key32);
+#if KS_STAMPS == 3
+        STAMP_NOW(ts);
+        sub[2] += ts - t2;
+        t2 = ts;
+#endif
         // the holders publish their node and packed key for the decider and the eval wave
         if (key32 != 0 && (key32 == k1 || key32 == k2)) {
           const uint32_t c = 2 * ow + (key32 == k1 ? 0u : 1u);
@@ -2027,17 +2049,17 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
       // -------------------------------------------------------- list waves
       if (ROLE_ON(1)) {
       list_select(r + LAHEAD);
-#if KS_STAMPS == 3
+#if KS_STAMPS == 4
       STAMP_NOW(ts);
       sub[0] += ts - t0;
 #endif
       dma_keys(r + LAHEAD + KAHEAD);
-#if KS_STAMPS == 3
+#if KS_STAMPS == 4
       STAMP_NOW(t2);
       sub[1] += t2 - ts;
 #endif
       list_wait();
-#if KS_STAMPS == 3
+#if KS_STAMPS == 4
       STAMP_NOW(ts);
       sub[2] += ts - t2;
 #endif
@@ -2087,7 +2109,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
   if (stamper) {
     atomicAdd((unsigned long long *)&a.counters[8 + sidx], (unsigned long long)st_work);
     atomicAdd((unsigned long long *)&a.counters[9 + sidx], (unsigned long long)st_wait);
-    if (wid == (KS_STAMPS == 3 ? 0u : KS_STAMPS == 2 ? (uint32_t)RES_EVAL_WAVE : (uint32_t)RES_DEC_WAVE))
+    if (wid == (KS_STAMPS == 4 ? 0u : KS_STAMPS == 3 ? (uint32_t)RES_LIST_WAVES : KS_STAMPS == 2 ? (uint32_t)RES_EVAL_WAVE : (uint32_t)RES_DEC_WAVE))
       for (int i = 0; i < 4; ++i) atomicAdd((unsigned long long *)&a.counters[12 + i], (unsigned long long)sub[i]);
   }
 #endif
