@@ -11,7 +11,7 @@ Score = LeastAllocated + BalancedAllocation + TaintToleration (+ NodeAffinity
 skipped, ImageLocality 0), percentageOfNodesToScore = 100, deterministic
 lowest-slot tie-break, sequential-equivalent in-order commit.
 
-A "step" schedules one batch of pods (default 8192) to completion against the
+A "step" schedules one batch of pods (default 32768) to completion against the
 live cluster; inputs are resident in HBM before the timed region (the batch
 is compiled and uploaded by ks_batch_prepare beforehand).  With --gpus N the
 node slots are sharded across N ranks (one process per GPU, RCCL candidate
@@ -54,7 +54,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--nodes", type=int, default=1_000_000)
-    ap.add_argument("--batch", type=int, default=8192, help="pods per step")
+    ap.add_argument("--batch", type=int, default=32768,
+                    help="pods per step (each batch refills the round pipeline once)")
     ap.add_argument("--pods-per-round", type=int, default=256)
     ap.add_argument("--topk", type=int, default=0)
     ap.add_argument("--nodes-per-lane", type=int, default=4)

@@ -8,7 +8,7 @@ TAG=${1:-r1}
 timeout -k 10 300 python -u bench.py --kind labeled --no-cpu-baseline > gpurun_out/bench_c4_$TAG.json 2> gpurun_out/bench_c4_$TAG.err
 rc=$?; echo "c4 rc=$rc"; cat gpurun_out/bench_c4_$TAG.json; tail -3 gpurun_out/bench_c4_$TAG.err
 if [ $rc -ne 0 ]; then exit $rc; fi
-timeout -k 10 300 python -u bench.py --nodes 100000 --steps 10 --no-cpu-baseline > gpurun_out/bench_c2_$TAG.json 2> gpurun_out/bench_c2_$TAG.err
+timeout -k 10 300 python -u bench.py --nodes 100000 --batch 20000 --steps 5 --no-cpu-baseline > gpurun_out/bench_c2_$TAG.json 2> gpurun_out/bench_c2_$TAG.err
 rc=$?; echo "c2 rc=$rc"; cat gpurun_out/bench_c2_$TAG.json; tail -3 gpurun_out/bench_c2_$TAG.err
 if [ $rc -ne 0 ]; then exit $rc; fi
 timeout -k 10 300 python -u bench.py --kind kwok --prefill 0 --no-cpu-baseline > gpurun_out/bench_kwok_$TAG.json 2> gpurun_out/bench_kwok_$TAG.err
