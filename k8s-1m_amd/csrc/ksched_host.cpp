@@ -776,11 +776,13 @@ ks_status collect_timing(ks_ctx *c) {
   return KS_OK;
 }
 
-// Cross-stream hand-off: `st` signals round number `seq` on flag f (and the
-// event, which drain_rounds waits on); `wt` waits for it.
+// Cross-stream hand-off: `st` signals round number `seq` on flag f (or by the
+// event, KS_VALUE_SYNC=0); `wt` waits for it.
 static ks_status hand_signal(ks_ctx *c, hipStream_t st, int f, hipEvent_t ev, uint32_t seq) {
-  HIPC(c, hipEventRecord(ev, st));
+  // with value hand-offs the event is not waited on (drain_rounds waits on
+  // ev_res only): skip its marker packet
   if (c->value_sync) HIPC(c, hipStreamWriteValue32(st, c->d_flags + f, seq, 0));
+  else HIPC(c, hipEventRecord(ev, st));
   return KS_OK;
 }
 static ks_status hand_wait(ks_ctx *c, hipStream_t wt, int f, hipEvent_t ev, uint32_t seq) {
@@ -799,6 +801,13 @@ static ks_status hand_wait(ks_ctx *c, hipStream_t wt, int f, hipEvent_t ev, uint
 //            record ev_sw[k]
 //   rstream: wait ev_sw[k], resolve k, record ev_res[k]
 ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k) {
+  // Timing events cost the main stream ~10 us of dispatch per sweep, so only
+  // every KS_TIMING_EVERY-th round (default 8) is timed.
+  static const uint32_t timing_every = [] {
+    const char *e = std::getenv("KS_TIMING_EVERY");
+    return e ? (uint32_t)std::max(1, std::atoi(e)) : 8u;
+  }();
+  const bool tm = c->timing && (c->round_seq + 1) % timing_every == 0;
   // RCCL path whenever a communicator exists (also a 1-rank one: exercised by tests)
   const bool multi = c->comm != nullptr;
   const uint32_t nloc = multi ? 1 : c->S;
@@ -881,13 +890,13 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k) {
   }
   HIPC(c, launch_advance(a, c->stream));
   hipEvent_t e0 = nullptr, e1 = nullptr;
-  if (c->timing) {
+  if (tm) {
     e0 = get_event(c);
     e1 = get_event(c);
     HIPC(c, hipEventRecord(e0, c->stream));
   }
   HIPC(c, launch_sweep(a, b->ext, bmax, groups, nloc, c->stream));
-  if (c->timing) {
+  if (tm) {
     HIPC(c, hipEventRecord(e1, c->stream));
     c->ev_sweep.emplace_back(e0, e1);
   }
@@ -925,7 +934,7 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k) {
     HIPC(c, launch_patch(a, b->ext, ss));
   }
   if ((st = hand_signal(c, ss, 1, c->ev_sw[q], seq)) || (st = hand_wait(c, c->rstream, 1, c->ev_sw[q], seq))) return st;
-  if (c->timing) {
+  if (tm) {
     e0 = get_event(c);
     e1 = get_event(c);
     HIPC(c, hipEventRecord(e0, c->rstream));
@@ -936,7 +945,7 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k) {
     ra.seq = seq;
     HIPC(c, launch_resolve(ra, b->ext, c->rstream));
   }
-  if (c->timing) {
+  if (tm) {
     HIPC(c, hipEventRecord(e1, c->rstream));
     c->ev_resolve.emplace_back(e0, e1);
   }
@@ -1021,12 +1030,22 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
     hipDeviceProp_t prop{};
     HIPC(x, hipGetDeviceProperties(&prop, cfg->device));
     const int ncu = prop.multiProcessorCount;
-    if (nres > 0 && nres < ncu) {
-      std::vector<uint32_t> main_mask((ncu + 31) / 32, 0u), res_mask((ncu + 31) / 32, 0u);
-      for (int i = 0; i < ncu; ++i) (i >= ncu - nres ? res_mask : main_mask)[i / 32] |= 1u << (i % 32);
+    // KS_SIDE_CUS (default 0): CUs the main stream (sweeps) leaves to the side
+    // stream, so merge / gather / patch blocks start without waiting for sweep
+    // blocks to drain
+    const char *es = std::getenv("KS_SIDE_CUS");
+    const int nside = es ? std::max(0, std::atoi(es)) : 0;
+    if (nres > 0 && nres + nside < ncu) {
+      std::vector<uint32_t> main_mask((ncu + 31) / 32, 0u), side_mask((ncu + 31) / 32, 0u),
+          res_mask((ncu + 31) / 32, 0u);
+      for (int i = 0; i < ncu; ++i) {
+        if (i >= ncu - nres) res_mask[i / 32] |= 1u << (i % 32);
+        else side_mask[i / 32] |= 1u << (i % 32);
+        if (i < ncu - nres - nside) main_mask[i / 32] |= 1u << (i % 32);
+      }
       HIPC(x, hipExtStreamCreateWithCUMask(&x->stream, (uint32_t)main_mask.size(), main_mask.data()));
       HIPC(x, hipExtStreamCreateWithCUMask(&x->rstream, (uint32_t)res_mask.size(), res_mask.data()));
-      HIPC(x, hipExtStreamCreateWithCUMask(&x->sstream, (uint32_t)main_mask.size(), main_mask.data()));
+      HIPC(x, hipExtStreamCreateWithCUMask(&x->sstream, (uint32_t)side_mask.size(), side_mask.data()));
     } else {
       int lo = 0, hi = 0;
       HIPC(x, hipStreamCreateWithFlags(&x->stream, hipStreamNonBlocking));
