@@ -886,9 +886,10 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k) {
   if (k >= 2) {  // round k-2 lands in the table before sweep k (sweep k-1 has finished reading it)
     if ((st = hand_wait(c, c->stream, 2, c->ev_res[q], c->seq_of[q]))) return st;
     if (b->norm && (st = hand_wait(c, c->stream, 3, c->ev_fixed[pq], c->seq_of[pq]))) return st;  // ... and so has FIX sweep k-1
-    HIPC(c, launch_writeback(c->t, c->d_carry + (size_t)q * MAX_P, c->d_pipe + 4 + q, c->stream));
+    HIPC(c, launch_advance_writeback(a, c->d_carry + (size_t)q * MAX_P, c->d_pipe + 4 + q, c->stream));
+  } else {
+    HIPC(c, launch_advance(a, c->stream));
   }
-  HIPC(c, launch_advance(a, c->stream));
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (tm) {
     e0 = get_event(c);

@@ -2142,7 +2142,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
 // (round k-1 may still be resolving): if round k-1's lists were swept for the
 // right pods, assume it resolves all of them; otherwise round k-1 resolves
 // nothing and round k restarts at its actual start.
-__global__ void advance_kernel(RoundArgs a) {
+__device__ __forceinline__ void advance_kernel_body(const RoundArgs &a) {
   uint32_t s;
   if (a.first) {
     s = *a.d_start;
@@ -2153,6 +2153,21 @@ __global__ void advance_kernel(RoundArgs a) {
   }
   *a.sstart = s;
   if (s < a.npods) a.counters[2] += min(a.P, a.npods - s);  // pods swept
+}
+__global__ void advance_kernel(RoundArgs a) { advance_kernel_body(a); }
+
+// advance + write-back in one dispatch (the main stream's per-round prologue)
+__global__ void advance_writeback_kernel(RoundArgs a, NodeTable t, const CarryRec *carry, const uint32_t *n) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) advance_kernel_body(a);
+  const uint32_t cnt = *n;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += gridDim.x * blockDim.x) {
+    const CarryRec &c = carry[i];
+    t.rcpu[c.pos] = c.rc;
+    t.rmem[c.pos] = c.rm;
+    t.zcpu[c.pos] = c.zc;
+    t.zmem[c.pos] = c.zm;
+    t.npods[c.pos] = c.np;
+  }
 }
 
 // Land a resolved round's modified rows in the table (before the sweep that
@@ -2338,6 +2353,11 @@ hipError_t launch_gather_cand(const RoundArgs &a, bool ext, hipStream_t st) {
 
 hipError_t launch_advance(const RoundArgs &a, hipStream_t st) {
   advance_kernel<<<1, 1, 0, st>>>(a);
+  return hipGetLastError();
+}
+
+hipError_t launch_advance_writeback(const RoundArgs &a, const CarryRec *carry, const uint32_t *n, hipStream_t st) {
+  advance_writeback_kernel<<<2, 256, 0, st>>>(a, a.t, carry, n);
   return hipGetLastError();
 }
 
