@@ -1,6 +1,6 @@
 """Per-phase cycle breakdown of the resolve kernel (diagnostic KS_STAMPS build).
 
-KSCHED_LIB_DIR=k8s-1m_amd/ksched/lib/stamps python tools/resolve_stamps.py [nodes] [pods]
+KSCHED_LIB_DIR=k8s-1m_amd/ksched/lib/stamps python tools/resolve_stamps.py [nodes] [pods] [hetero|labeled]
 Per-role work / barrier-wait cycles per pod; the stamps' own cost inflates absolute times.
 """
 import ctypes as C
@@ -12,7 +12,7 @@ from ksched import Scheduler, synth  # noqa: E402
 
 nodes = int(sys.argv[1]) if len(sys.argv) > 1 else 200000
 npods = int(sys.argv[2]) if len(sys.argv) > 2 else 8192
-kind = synth.HETERO
+kind = {"hetero": synth.HETERO, "labeled": synth.LABELED}[sys.argv[3] if len(sys.argv) > 3 else "hetero"]
 s = Scheduler(nodes, pods_per_round=256)
 ns = synth.nodes(kind, nodes, 1)
 s.upsert_nodes_raw(ns.nodes, synth.slot_array(nodes), nodes)
