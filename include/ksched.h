@@ -329,7 +329,8 @@ ks_status ks_reset_stats(ks_ctx *ctx);
  * normalising maxima were wrong, [8..15] resolve phase cycle sums
  * (diagnostic KS_STAMPS build only). */
 ks_status ks_debug_counters(ks_ctx *ctx, uint64_t out[16]);
-/* 1 = time every sweep/resolve launch with HIP events (adds syncs), 0 = off. */
+/* 1 = time sweep / resolve launches with HIP events (every KS_TIMING_EVERY-th
+ * round, default 8; sweep_evals counts the timed launches' share), 0 = off. */
 ks_status ks_set_timing(ks_ctx *ctx, int32_t enabled);
 
 #ifdef __cplusplus

@@ -219,6 +219,7 @@ struct ks_ctx {
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_sweep, ev_resolve;
   std::vector<hipEvent_t> ev_pool;
   uint64_t counters_base[4] = {0, 0, 0, 0};  // device counters at the last ks_reset_stats
+  uint64_t sweeps_issued = 0;                // main sweep launches since then (timed or not)
   // Host<->device transfers of one ABI call: a pinned host staging buffer and a
   // device scratch buffer, both bump-allocated and reset at xfer_sync (no
   // pageable hipMemcpyAsync anywhere).
@@ -897,6 +898,7 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k) {
     HIPC(c, hipEventRecord(e0, c->stream));
   }
   HIPC(c, launch_sweep(a, b->ext, bmax, groups, nloc, c->stream));
+  ++c->sweeps_issued;
   if (tm) {
     HIPC(c, hipEventRecord(e1, c->stream));
     c->ev_sweep.emplace_back(e0, e1);
@@ -1634,7 +1636,12 @@ ks_status ks_get_stats(ks_ctx *c, ks_stats *out) {
     const Shard &sh = c->shards[q];
     for (uint32_t l = 0; l < sh.count; ++l) local += c->nodes[sh.lo + l].present;
   }
-  out->sweep_evals = (k[2] - c->counters_base[2]) * local;
+  // evaluations by the timed launches: all evaluations apportioned by launch
+  // count (every launch but a batch's last sweeps P pods)
+  const uint64_t all_evals = (k[2] - c->counters_base[2]) * local;
+  out->sweep_evals = c->sweeps_issued ? (uint64_t)((double)all_evals * (double)c->stats.sweep_launches /
+                                                   (double)c->sweeps_issued)
+                                      : 0;
   out->rounds = k[0] - c->counters_base[0];
   out->pods_resolved = k[1] - c->counters_base[1];
   return KS_OK;
@@ -1643,6 +1650,7 @@ ks_status ks_get_stats(ks_ctx *c, ks_stats *out) {
 ks_status ks_reset_stats(ks_ctx *c) {
   if (!c) return KS_ERR_INVALID;
   c->stats = ks_stats{};
+  c->sweeps_issued = 0;
   return read_counters(c, c->counters_base);
 }
 
