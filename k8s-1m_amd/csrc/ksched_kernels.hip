@@ -1627,7 +1627,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
   uint32_t pb1 = NONE32, pb2 = NONE32, pb3 = NONE32;
   // the decider is the per-pod critical path, the eval wave next: issue priority
 #ifndef KS_OWNER_PRIO
-#define KS_OWNER_PRIO 2
+#define KS_OWNER_PRIO 3
 #endif
   if (wid == RES_DEC_WAVE) __builtin_amdgcn_s_setprio(3);
   else if (wid == RES_EVAL_WAVE || wid == RES_PREV_WAVE) __builtin_amdgcn_s_setprio(2);
