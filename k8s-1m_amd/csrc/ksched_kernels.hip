@@ -1626,11 +1626,14 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
   // hash buckets the last three pods' joins were inserted at (NONE32: no insert)
   uint32_t pb1 = NONE32, pb2 = NONE32, pb3 = NONE32;
   // the decider is the per-pod critical path, the eval wave next: issue priority
+#ifndef KS_EVAL_PRIO
+#define KS_EVAL_PRIO 2
+#endif
 #ifndef KS_OWNER_PRIO
 #define KS_OWNER_PRIO 3
 #endif
   if (wid == RES_DEC_WAVE) __builtin_amdgcn_s_setprio(3);
-  else if (wid == RES_EVAL_WAVE || wid == RES_PREV_WAVE) __builtin_amdgcn_s_setprio(2);
+  else if (wid == RES_EVAL_WAVE || wid == RES_PREV_WAVE) __builtin_amdgcn_s_setprio(KS_EVAL_PRIO);
   else if (is_owner) __builtin_amdgcn_s_setprio(KS_OWNER_PRIO);  // owners: the longest chain per pod
 #ifdef KS_STAMPS
 #if KS_STAMPS >= 3  // list wave 0 and owner wave 0 in the decider / eval counters
