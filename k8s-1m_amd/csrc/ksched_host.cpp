@@ -182,7 +182,7 @@ struct ks_ctx {
   uint32_t *d_norm = nullptr;     // [2][P][2] by round parity
   double *d_norm_inv = nullptr;   // [2][P][2] by round parity
   PodStat *d_pstat = nullptr;     // [P]
-  uint32_t *d_fix = nullptr;      // [P] flags + [MAX_P / MAX_PG] group flags
+  uint32_t *d_fix = nullptr;      // [P] flags + [MAX_P / MAX_PG] group flags + [MAX_P] compacted list
   BlockRec *d_brec = nullptr;     // [2][...] by round parity (merge k reads while sweep k+1 writes)
   size_t brec_bytes = 0;          // per parity
   uint64_t *d_srec = nullptr, *d_frec = nullptr;
@@ -865,6 +865,7 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k) {
   a.pstat = b->norm ? c->d_pstat : nullptr;
   a.fix_flag = c->d_fix;
   a.fix_group = c->d_fix + MAX_P;
+  a.fix_list = c->d_fix + MAX_P + MAX_P / MAX_PG;
   a.fix = 0;
   a.brec = c->d_brec + (size_t)q * (c->brec_bytes / sizeof(BlockRec));
   a.srec = c->d_srec + (size_t)q * c->S * c->P * RW;
@@ -1105,7 +1106,7 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
   if ((st = dalloc(x, &x->d_shards, x->S)) || (st = dalloc(x, &x->d_slot_pos, x->cap)) ||
       (st = dalloc(x, &x->d_start, 1)) || (st = dalloc(x, &x->d_norm, 2 * 2 * (size_t)x->P)) ||
       (st = dalloc(x, &x->d_norm_inv, 2 * 2 * (size_t)x->P)) ||
-      (st = dalloc(x, &x->d_pstat, (size_t)x->P)) || (st = dalloc(x, &x->d_fix, MAX_P + MAX_P / MAX_PG)) ||
+      (st = dalloc(x, &x->d_pstat, (size_t)x->P)) || (st = dalloc(x, &x->d_fix, 2 * MAX_P + MAX_P / MAX_PG)) ||
       (st = dalloc(x, &x->d_pipe, 8)) || (st = dalloc(x, &x->d_flags, 4)) || (st = dalloc(x, &x->d_carry, 2 * (size_t)MAX_P)) ||
       (st = dalloc(x, &x->d_counters, 16)))
     return st;

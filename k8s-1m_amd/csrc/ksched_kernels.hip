@@ -552,9 +552,11 @@ __global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
   });
   const uint32_t kpos0 = KEY32_POS_MASK - lane;
 
-  for (uint32_t pi = p0; pi < p1; ++pi) {
-    const uint32_t r = pi - start;
-    if (fix && uniform_u32(a.fix_flag[r]) == 0) continue;
+  for (uint32_t it = p0; it < p1; ++it) {
+    // FIX mode: slice entry it - start of the compacted flagged-pod list
+    const uint32_t r = fix ? uniform_u32(a.fix_list[it - start]) : it - start;
+    if (fix && r == FIX_NONE) continue;
+    const uint32_t pi = start + r;
     const PodDev p = load_pod(a.pods, pi);
     uint32_t tt_max = 0, na_max = 0;
     if (EXT && (p.flags & (PF_TT | PF_NA))) {
@@ -691,7 +693,7 @@ __global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
         return ((uint64_t)(k >> KEY32_POS_BITS) << 32) | (uint64_t)(0xFFFFFFFFu - slot);
       };
       const uint64_t k1 = widen(c1), k2 = widen(c2), bound = widen(bound32);
-      const uint32_t pl = pi - p0;
+      const uint32_t pl = it - p0;
       s_keys[pl][wid][0] = k1;
       s_keys[pl][wid][1] = k2;
       s_keys[pl][wid][2] = bound;
@@ -711,7 +713,8 @@ __global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
   // Block list per pod: top BLOCK_KEYS of the 4 wave lists above every bound.
   const uint32_t npl = p1 - p0;
   for (uint32_t pl = threadIdx.x; pl < npl; pl += blockDim.x) {
-    if (fix && a.fix_flag[p0 + pl - start] == 0) continue;
+    const uint32_t r = fix ? a.fix_list[p0 + pl - start] : p0 + pl - start;
+    if (fix && r == FIX_NONE) continue;
     uint64_t k[2 * NW];
     uint64_t bound = 0;
     const uint32_t nwaves = min((uint32_t)NW, kwaves - blockIdx.x * NW);
@@ -743,7 +746,6 @@ __global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
     br.na_cnt = cnt[7];
     br.tt_max = tmx;
     br.na_max = nmx;
-    const uint32_t r = p0 + pl - start;
     a.brec[((size_t)sh * a.P + r) * a.bstride + blockIdx.x] = br;
   }
 }
@@ -908,11 +910,9 @@ __global__ __launch_bounds__(MERGE_THREADS) void merge_kernel(RoundArgs a) {
 // then unused) and whether the sweep's guess was wrong (FIX flags, per pod
 // and per MAX_PG-pod group; counters[4] counts re-swept pods).
 __global__ __launch_bounds__(MAX_P) void norm_check_kernel(RoundArgs a) {
-  __shared__ uint32_t s_any[MAX_P / MAX_PG];
+  __shared__ uint32_t s_wn[MAX_P / WAVE];
   const uint32_t start = uniform_u32(*a.sstart);
   const uint32_t r = threadIdx.x;
-  if (r < MAX_P / MAX_PG) s_any[r] = 0;
-  __syncthreads();
   bool wrong = false;
   if (r < a.P && start + r < a.npods) {
     const PodDev &p = a.pods[start + r];
@@ -928,12 +928,25 @@ __global__ __launch_bounds__(MAX_P) void norm_check_kernel(RoundArgs a) {
     a.norm_inv[2 * r] = tt ? 1.0 / (double)tt : 0.0;
     a.norm_inv[2 * r + 1] = na ? 1.0 / (double)na : 0.0;
     a.fix_flag[r] = wrong ? 1u : 0u;
-    if (wrong) atomicOr(&s_any[r / MAX_PG], 1u);
   }
-  const uint32_t nw = popc_ballot(wrong);
-  if (nw && threadIdx.x % WAVE == 0) atomicAdd((unsigned long long *)&a.counters[4], (unsigned long long)nw);
+  // compacted list of the flagged pods (round order): the FIX sweep runs
+  // ceil(count / MAX_PG) pod groups, so node rows are re-read once per 64
+  // flagged pods rather than once per 64-pod slice holding one
+  const uint64_t wb = __ballot(wrong);
+  const uint32_t nw = (uint32_t)__popcll(wb);
+  const uint32_t wid = threadIdx.x / WAVE, lane = threadIdx.x % WAVE;
+  if (lane == 0) s_wn[wid] = nw;
+  if (nw && lane == 0) atomicAdd((unsigned long long *)&a.counters[4], (unsigned long long)nw);
   __syncthreads();
-  if (r < MAX_P / MAX_PG) a.fix_group[r] = s_any[r];
+  uint32_t idx = (uint32_t)__popcll(wb & ((1ull << lane) - 1ull)), total = 0;
+#pragma unroll
+  for (int w = 0; w < MAX_P / WAVE; ++w) {
+    idx += (uint32_t)w < wid ? s_wn[w] : 0u;
+    total += s_wn[w];
+  }
+  if (wrong) a.fix_list[idx] = r;
+  if (r >= total) a.fix_list[r] = FIX_NONE;
+  if (r < MAX_P / MAX_PG) a.fix_group[r] = r * MAX_PG < total ? 1u : 0u;
 }
 
 // grid: x = pod in round.  Shard records -> final record.

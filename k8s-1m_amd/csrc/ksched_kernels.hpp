@@ -10,6 +10,7 @@ namespace ks {
 constexpr int MAX_PG = 64;    // pods per sweep block (LDS wave records)
 constexpr int MAX_P = 256;    // pods per round (resolve stages the round in LDS)
 constexpr int MAX_K = 256;    // candidates per pod record (one list thread each in the resolve)
+constexpr uint32_t FIX_NONE = 0xFFFFFFFFu;  // fix_list tail
 
 struct RoundArgs {
   NodeTable t;
@@ -44,7 +45,8 @@ struct RoundArgs {
   const double *guess_inv;    // [npods][2] RN(1 / tt_guess), RN(1 / na_guess) (host)
   PodStat *pstat;             // [P] measured maxima (merge, all shards); nullptr: no normalising pod
   uint32_t *fix_flag;         // [P] the pod's guessed maxima were wrong: re-swept in FIX mode
-  uint32_t *fix_group;        // [P / MAX_PG] any flagged pod in the group
+  uint32_t *fix_group;        // [P / MAX_PG] FIX-mode pod group g holds flagged pods (g * MAX_PG < count)
+  uint32_t *fix_list;         // [P] flagged pods of the round in order, then FIX_NONE
   uint32_t fix;               // FIX-mode launch of sweep / merge
   uint32_t *flag_res;         // resolve: round number `seq` stored here when done (null: the host signals)
   uint32_t seq;
