@@ -885,9 +885,19 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k) {
   // The kernels address positions as base + wave*64*knpl + j*64 + lane, which
   // equals the layout position when the layout's npl-step block of a wave is
   // split into `sub` consecutive kernel waves; slots follow from the layout.
+  // KS_EARLY_FIX (default 1, one rank): the sweep measures the normaliser
+  // maxima itself and norm_check + the FIX sweep follow it on the main
+  // stream, so sweep k+1 no longer waits for the side stream's merge k; the
+  // merge then reads the FIX records of the flagged pods directly
+  static const bool early_env = [] {
+    const char *e = std::getenv("KS_EARLY_FIX");
+    return e ? std::atoi(e) != 0 : true;
+  }();
+  const bool early = b->norm && !multi && early_env;
+  a.pstat_sweep = early ? 1u : 0u;
   if (k >= 2) {  // round k-2 lands in the table before sweep k (sweep k-1 has finished reading it)
     if ((st = hand_wait(c, c->stream, 2, c->ev_res[q], c->seq_of[q]))) return st;
-    if (b->norm && (st = hand_wait(c, c->stream, 3, c->ev_fixed[pq], c->seq_of[pq]))) return st;  // ... and so has FIX sweep k-1
+    if (b->norm && !early && (st = hand_wait(c, c->stream, 3, c->ev_fixed[pq], c->seq_of[pq]))) return st;  // ... and so has FIX sweep k-1
     HIPC(c, launch_advance_writeback(a, c->d_carry + (size_t)q * MAX_P, c->d_pipe + 4 + q, c->stream));
   } else {
     HIPC(c, launch_advance(a, c->stream));
@@ -898,6 +908,7 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k) {
     e1 = get_event(c);
     HIPC(c, hipEventRecord(e0, c->stream));
   }
+  if (early) HIPC(c, hipMemsetAsync(c->d_pstat, 0, (size_t)c->P * sizeof(PodStat), c->stream));
   HIPC(c, launch_sweep(a, b->ext, bmax, groups, nloc, c->stream));
   ++c->sweeps_issued;
   if (tm) {
@@ -910,10 +921,17 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k) {
   const uint32_t seq = ++c->round_seq;
   c->seq_of[q] = seq;
   hipStream_t ss = c->sstream;
+  if (early) {
+    HIPC(c, launch_norm_check(a, c->stream));
+    RoundArgs f = a;
+    f.fix = 1;
+    f.pg = MAX_PG;
+    HIPC(c, launch_sweep(f, true, bmax, (c->P + MAX_PG - 1) / MAX_PG, nloc, c->stream));
+  }
   if ((st = hand_signal(c, c->stream, 0, c->ev_swept[q], seq)) || (st = hand_wait(c, ss, 0, c->ev_swept[q], seq))) return st;
-  if (b->norm) HIPC(c, hipMemsetAsync(c->d_pstat, 0, (size_t)c->P * sizeof(PodStat), ss));
+  if (b->norm && !early) HIPC(c, hipMemsetAsync(c->d_pstat, 0, (size_t)c->P * sizeof(PodStat), ss));
   HIPC(c, launch_merge(a, nloc, ss));
-  if (b->norm) {
+  if (b->norm && !early) {
     // the sweep scored normalising plugins with each pod's guessed maxima:
     // measure (all ranks), flag the wrong guesses, re-sweep + re-merge those pods
     if (multi)

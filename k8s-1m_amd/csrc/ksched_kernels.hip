@@ -746,6 +746,18 @@ __global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
     br.na_cnt = cnt[7];
     br.tt_max = tmx;
     br.na_max = nmx;
+    if (EXT && a.pstat_sweep && !fix) {
+      // measured normaliser maxima straight from the sweep, so norm_check and
+      // the FIX sweep follow it on its own stream; the coherent pre-check keeps
+      // the atomics to the few blocks that raise a maximum
+      PodStat *ps = a.pstat + r;
+      if (tmx && tmx > __hip_atomic_load(&ps->tt_max, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        atomicMax(&ps->tt_max, tmx);
+      if (nmx && nmx > __hip_atomic_load(&ps->na_max, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        atomicMax(&ps->na_max, nmx);
+      if (cnt[0] && __hip_atomic_load(&ps->any_feasible, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
+        atomicMax(&ps->any_feasible, 1u);
+    }
     a.brec[((size_t)sh * a.P + r) * a.bstride + blockIdx.x] = br;
   }
 }
@@ -896,7 +908,7 @@ __global__ __launch_bounds__(MERGE_THREADS) void merge_kernel(RoundArgs a) {
     for (int q = 0; q < NFILT; ++q) h->fails[q] = t[1 + q];
     h->tt_cnt = t[6];
     h->na_cnt = t[7];
-    if (a.pstat != nullptr && !a.fix) {  // across local shards (atomics) and ranks (RCCL all-reduce max)
+    if (a.pstat != nullptr && !a.fix && !a.pstat_sweep) {  // across local shards (atomics) and ranks (RCCL all-reduce max)
       PodStat *ps = a.pstat + r;
       if (t[NFILT + 3]) atomicMax(&ps->tt_max, t[NFILT + 3]);
       if (t[NFILT + 4]) atomicMax(&ps->na_max, t[NFILT + 4]);

@@ -48,6 +48,7 @@ struct RoundArgs {
   uint32_t *fix_group;        // [P / MAX_PG] FIX-mode pod group g holds flagged pods (g * MAX_PG < count)
   uint32_t *fix_list;         // [P] flagged pods of the round in order, then FIX_NONE
   uint32_t fix;               // FIX-mode launch of sweep / merge
+  uint32_t pstat_sweep;       // the sweep (not the merge) folds its maxima into pstat (one rank)
   uint32_t *flag_res;         // resolve: round number `seq` stored here when done (null: the host signals)
   uint32_t seq;
   BlockRec *brec;             // [local shards][P][bstride]
