@@ -746,17 +746,16 @@ __global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
     br.na_cnt = cnt[7];
     br.tt_max = tmx;
     br.na_max = nmx;
-    if (EXT && a.pstat_sweep && !fix) {
+    if (EXT && a.pstat_sweep && !fix && cnt[0]) {
       // measured normaliser maxima straight from the sweep, so norm_check and
-      // the FIX sweep follow it on its own stream; the coherent pre-check keeps
-      // the atomics to the few blocks that raise a maximum
-      PodStat *ps = a.pstat + r;
-      if (tmx && tmx > __hip_atomic_load(&ps->tt_max, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-        atomicMax(&ps->tt_max, tmx);
-      if (nmx && nmx > __hip_atomic_load(&ps->na_max, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-        atomicMax(&ps->na_max, nmx);
-      if (cnt[0] && __hip_atomic_load(&ps->any_feasible, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u)
-        atomicMax(&ps->any_feasible, 1u);
+      // the FIX sweep follow it on its own stream.  Blocks with a feasible node
+      // raise tt_max / na_max to max raw + 1 (0: no feasible node anywhere);
+      // one coherent 64-bit pre-check keeps the atomics to the few blocks that
+      // raise a maximum
+      uint32_t *pm = &a.pstat[r].tt_max;  // tt_max, na_max adjacent (8-B aligned)
+      const uint64_t cur = __hip_atomic_load((uint64_t *)pm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (tmx + 1u > (uint32_t)cur) atomicMax(pm, tmx + 1u);
+      if (nmx + 1u > (uint32_t)(cur >> 32)) atomicMax(pm + 1, nmx + 1u);
     }
     a.brec[((size_t)sh * a.P + r) * a.bstride + blockIdx.x] = br;
   }
@@ -928,7 +927,12 @@ __global__ __launch_bounds__(MAX_P) void norm_check_kernel(RoundArgs a) {
   bool wrong = false;
   if (r < a.P && start + r < a.npods) {
     const PodDev &p = a.pods[start + r];
-    const PodStat st = a.pstat[r];
+    PodStat st = a.pstat[r];
+    if (a.pstat_sweep) {  // sweep encoding: max raw + 1 over blocks with a feasible node
+      st.any_feasible = st.tt_max != 0u;
+      st.tt_max = st.tt_max ? st.tt_max - 1u : 0u;
+      st.na_max = st.na_max ? st.na_max - 1u : 0u;
+    }
     uint32_t tt = p.tt_guess, na = p.na_guess;
     if (st.any_feasible) {
       wrong = ((p.flags & PF_TT) && st.tt_max != tt) || ((p.flags & PF_NA) && st.na_max != na);
