@@ -168,6 +168,11 @@ struct ks_ctx {
   uint32_t round_seq = 0;         // rounds enqueued since open
   uint32_t seq_of[2] = {0, 0};    // round number by parity
   bool value_sync = true;
+  // Tuning switches, read from the environment once per context in ks_open
+  // (KS_EARLY_FIX, KS_TIMING_EVERY, KS_SWEEP_BLOCKS, KS_EXT_NPL), so one
+  // process can open contexts with different settings (tests do).
+  bool early_fix = true;
+  uint32_t timing_every = 8, sweep_blocks = 8192, ext_npl = 2;
   // geometry
   uint32_t cap = 0, S = 1, npl = 8, P = 256, K = 256;
   std::vector<Shard> shards;
@@ -736,12 +741,7 @@ uint32_t blocks_per_shard(const Shard &s, uint32_t sub) { return (s.waves * sub 
 // Sweep / prescore kernel width: fewer nodes per lane when label/taint
 // columns are held too (register budget).
 uint32_t kernel_npl(const ks_ctx *c, bool ext) {
-  static const uint32_t ext_npl = [] {  // KS_EXT_NPL: geometry experiments only
-    const char *e = std::getenv("KS_EXT_NPL");
-    const int v = e ? std::atoi(e) : 2;
-    return (uint32_t)(v == 4 || v == 8 ? v : 2);
-  }();
-  return ext ? std::min<uint32_t>(c->npl, ext_npl) : c->npl;
+  return ext ? std::min<uint32_t>(c->npl, c->ext_npl) : c->npl;
 }
 
 hipEvent_t get_event(ks_ctx *c) {
@@ -804,11 +804,7 @@ static ks_status hand_wait(ks_ctx *c, hipStream_t wt, int f, hipEvent_t ev, uint
 ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k) {
   // Timing events cost the main stream ~10 us of dispatch per sweep, so only
   // every KS_TIMING_EVERY-th round (default 8) is timed.
-  static const uint32_t timing_every = [] {
-    const char *e = std::getenv("KS_TIMING_EVERY");
-    return e ? (uint32_t)std::max(1, std::atoi(e)) : 8u;
-  }();
-  const bool tm = c->timing && (c->round_seq + 1) % timing_every == 0;
+  const bool tm = c->timing && (c->round_seq + 1) % c->timing_every == 0;
   // RCCL path whenever a communicator exists (also a 1-rank one: exercised by tests)
   const bool multi = c->comm != nullptr;
   const uint32_t nloc = multi ? 1 : c->S;
@@ -819,10 +815,7 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k) {
   uint32_t bmax = 0;
   for (uint32_t q = 0; q < nloc; ++q) bmax = std::max(bmax, blocks_per_shard(c->shards[shard0 + q], sub));
   // pods per block: enough (block, pod-group) pairs to fill 256 CUs x 8 waves
-  static const uint32_t want = [] {  // target (block, pod-group) pairs; KS_SWEEP_BLOCKS overrides
-    const char *e = std::getenv("KS_SWEEP_BLOCKS");
-    return e ? (uint32_t)std::max(1, std::atoi(e)) : 8192u;
-  }();
+  const uint32_t want = c->sweep_blocks;
   const uint32_t total_blocks = bmax * nloc;
   uint32_t groups = (want + total_blocks - 1) / total_blocks;
   groups = std::max<uint32_t>(1, std::min(groups, c->P));
@@ -889,11 +882,7 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k) {
   // maxima itself and norm_check + the FIX sweep follow it on the main
   // stream, so sweep k+1 no longer waits for the side stream's merge k; the
   // merge then reads the FIX records of the flagged pods directly
-  static const bool early_env = [] {
-    const char *e = std::getenv("KS_EARLY_FIX");
-    return e ? std::atoi(e) != 0 : true;
-  }();
-  const bool early = b->norm && !multi && early_env;
+  const bool early = b->norm && !multi && c->early_fix;
   a.pstat_sweep = early ? 1u : 0u;
   if (k >= 2) {  // round k-2 lands in the table before sweep k (sweep k-1 has finished reading it)
     if ((st = hand_wait(c, c->stream, 2, c->ev_res[q], c->seq_of[q]))) return st;
@@ -1042,6 +1031,17 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
   if (cfg->device < 0 || cfg->device >= ndev) return KS_ERR_DEVICE;
   if (hipSetDevice(cfg->device) != hipSuccess) return KS_ERR_DEVICE;
   ks_ctx *x = c.get();
+  {
+    auto env_u = [](const char *name, int dflt) {
+      const char *e = std::getenv(name);
+      return e ? std::atoi(e) : dflt;
+    };
+    x->early_fix = env_u("KS_EARLY_FIX", 1) != 0;
+    x->timing_every = (uint32_t)std::max(1, env_u("KS_TIMING_EVERY", 8));
+    x->sweep_blocks = (uint32_t)std::max(1, env_u("KS_SWEEP_BLOCKS", 8192));
+    const int en = env_u("KS_EXT_NPL", 2);  // geometry experiments only
+    x->ext_npl = (uint32_t)(en == 4 || en == 8 ? en : 2);
+  }
   {
     // Resolve runs on a high-priority stream on KS_RESOLVE_CUS (default 1) CUs
     // of its own: the main and side streams are masked off them, so a resolve

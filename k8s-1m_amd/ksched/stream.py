@@ -1,6 +1,6 @@
 """C5 driver: a bursty pod stream with a seeded event log
 between bursts, applied identically to any number of targets (libksched
-contexts and/or oracles).
+contexts here; tests/stream.py adds the checker's target).
 
 Between bursts, in log order (the informer events the reference's cache would
 see, dist-scheduler/cmd/dist-scheduler/scheduler.go:200-228 -> upstream
@@ -32,29 +32,6 @@ class Rates:
     pod_delete: float = 0.05
     node_update: float = 0.001
     node_delete: float = 0.0001
-
-
-class OracleTarget:
-    def __init__(self, o):
-        self.o = o
-
-    def upsert(self, arr, slots, n):
-        self.o.upsert(arr, slots, n)
-
-    def delete(self, slots, n):
-        self.o.delete(slots, n)
-
-    def add_pods(self, arr, slots, n):
-        self.o.add_pods(arr, slots, n)
-
-    def remove_pods(self, arr, slots, n):
-        self.o.remove_pods(arr, slots, n)
-
-    def schedule(self, arr, n):
-        return self.o.schedule(arr, n)
-
-    def states(self, slots):
-        return self.o.node_states(slots)
 
 
 class GpuTarget:

@@ -1,0 +1,143 @@
+"""Parity at BASELINE.json's full sizes, on the exact paths the bench lines run.
+
+A 1M-node oracle cannot schedule a 32,768-pod batch in test time (~20 pods/s
+on 16 threads), so these tests use a REPLAY check: libksched schedules the
+whole batch through the default configuration (P = K = 256, 4 nodes per lane,
+pipelined rounds, early FIX for normalising plugins); the oracle then replays
+the GPU's own decisions (NodeInfo.AddPod at the chosen slot) up to each check
+window and schedules the window's pods itself.  Every window's results must be
+bit-identical (node, TotalScore, feasible / evaluated counts, Diagnosis), so
+each window proves the GPU's decisions correct given the state the GPU had
+reached; windows sit in the first round, mid-batch at offsets that are not
+round-aligned (pipelined rounds, patched lists, carried commits), and at the
+end of the batch.  After the last window the oracle replays the remaining
+decisions and the two node tables must be equal (commit bookkeeping of every
+pod).
+
+Workloads: C3 (1M heterogeneous, prefilled), C4 (1M labeled: EXT sweep, 2 nodes
+per lane, early FIX with wrongly guessed normalisers asserted to occur), the
+reference's own kwok shape with request-less pods (kwok/make_nodes/main.go:
+126-181, kwok/make_pods/main.go:118-148), and the kwok line's C1-shaped pods.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+import pyoracle
+from helpers import assert_results_equal, res_array, states_np
+from ksched import Scheduler, _abi, synth
+
+pytestmark = pytest.mark.gpu
+
+N = 1_000_000
+BATCH = 32_768
+WLEN = 32
+WINDOWS = (0, 5_003, 16_411, BATCH - WLEN)
+ORACLE_THREADS = 16  # the GPU box's CPU share
+
+
+def pod_subset(pods_ptr, idx):
+    """Contiguous ks_pod array of pods_ptr[idx] (the structs keep their pointers)."""
+    out = (_abi.KsPod * max(1, len(idx)))()
+    for j, i in enumerate(idx):
+        out[j] = pods_ptr[int(i)]
+    return out
+
+
+def u32(a):
+    a = np.ascontiguousarray(a, dtype=np.uint32)
+    return (C.c_uint32 * max(1, len(a)))(*a.tolist())
+
+
+def replay_check(o, pods, got, m, windows=WINDOWS, wlen=WLEN):
+    """Replay the GPU's decisions into oracle `o` and check each window (see module doc)."""
+    r = res_array(got, m)
+    pos = 0
+    checked = 0
+    for w in sorted(windows):
+        assert w >= pos
+        idx = np.nonzero(r["status"][pos:w] == 0)[0] + pos
+        if len(idx):
+            o.add_pods(pod_subset(pods.pods, idx), u32(r["node_index"][idx]), len(idx))
+        want = o.schedule(pods.pods_at(w), wlen)  # commits the window in the oracle
+        sub = (_abi.KsResult * wlen).from_buffer_copy(
+            C.string_at(C.addressof(got) + w * C.sizeof(_abi.KsResult), wlen * C.sizeof(_abi.KsResult)))
+        assert_results_equal(sub, want, wlen, f"window at pod {w}")
+        checked += wlen
+        pos = w + wlen
+    idx = np.nonzero(r["status"][pos:m] == 0)[0] + pos
+    if len(idx):
+        o.add_pods(pod_subset(pods.pods, idx), u32(r["node_index"][idx]), len(idx))
+    return checked
+
+
+def run_fullsize(kind, pods, prefill, *, env=None, **cfg):
+    nodes = synth.nodes(kind, N, 1)
+    slots = synth.slot_array(N)
+    pf = synth.prefill(kind, N, 1, 3, 0.5) if prefill else None
+    old = {k: os.environ.get(k) for k in (env or {})}
+    os.environ.update(env or {})
+    try:
+        s = Scheduler(N, **cfg)  # switches are read when the context opens
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    s.upsert_nodes_raw(nodes.nodes, slots, N)
+    if pf is not None:
+        assert s.lib.ks_pods_add(s.ctx, pf.pods, pf.slot_ptr, pf.n_pods) == 0
+    b = s.prepare(pods.pods, BATCH)
+    s.run(b)
+    got = s.results(b, BATCH)
+    s.free(b)
+    dbg = (C.c_uint64 * 16)()
+    assert s.lib.ks_debug_counters(s.ctx, dbg) == 0
+    o = pyoracle.Oracle(N, threads=ORACLE_THREADS)
+    o.upsert(nodes.nodes, slots, N)
+    if pf is not None:
+        o.add_pods(pf.pods, pf.slot_ptr, pf.n_pods)
+    replay_check(o, pods, got, BATCH)
+    sg = states_np(s.lib.ks_node_states, s.ctx, N)
+    sw = states_np(o.L.oracle_node_states, o.o, N)
+    assert np.array_equal(sg, sw), "node tables differ after replaying every decision"
+    s.close()
+    o.close()
+    return res_array(got, BATCH), list(dbg)
+
+
+def test_c3_hetero_1m_replay():
+    r, dbg = run_fullsize(synth.HETERO, synth.pods(synth.HETERO, BATCH, 2), prefill=True)
+    assert (r["status"] == 0).all()
+    assert dbg[0] >= BATCH // 256  # rounds
+
+
+def test_c4_labeled_1m_replay_early_fix():
+    # the C4 bench path: EXT sweep (2 nodes per lane), early FIX, compacted FIX list
+    r, dbg = run_fullsize(synth.LABELED, synth.pods(synth.LABELED, BATCH, 2), prefill=True)
+    assert dbg[4] > 0, "no pod was re-swept with a measured normaliser (FIX path not exercised)"
+    assert (r["status"] == 1).any() and (r["status"] == 0).mean() > 0.9
+
+
+def test_c4_labeled_1m_replay_merge_fix():
+    # the same with the FIX sweep behind the merge (the multi-rank order, one rank)
+    r, dbg = run_fullsize(synth.LABELED, synth.pods(synth.LABELED, BATCH, 5), prefill=True,
+                          env={"KS_EARLY_FIX": "0"})
+    assert dbg[4] > 0
+
+
+def test_kwok_1m_requestless_replay():
+    # the reference's published workload shape: identical kwok nodes, busybox
+    # pods with no requests (non-zero defaults 100m / 200Mi for LeastAllocated)
+    r, dbg = run_fullsize(synth.KWOK, synth.besteffort_pods(BATCH), prefill=False)
+    assert (r["status"] == 0).all()
+    # identical nodes: ties everywhere, lowest slot wins; 3 pods per node before LeastAllocated drops
+    assert r["node_index"][:6].tolist() == [0, 0, 0, 1, 1, 1]
+
+
+def test_kwok_1m_c1_pods_replay():
+    r, dbg = run_fullsize(synth.KWOK, synth.pods(synth.KWOK, BATCH, 2), prefill=False)
+    assert (r["status"] == 0).all()

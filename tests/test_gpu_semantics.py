@@ -148,3 +148,47 @@ def test_event_log_mixed_kinds_in_order():
         bad[0].kind = 7
         assert s.lib.ks_events_apply(s.ctx, bad, 1) == _abi.KS_ERR_INVALID
         assert b"unknown kind" in s.lib.ks_last_error(s.ctx)
+
+
+@pytest.mark.parametrize("early", ["1", "0"])
+def test_fix_list_spans_several_groups(early, monkeypatch):
+    # More than 128 pods of one 256-pod round carry a preferred term no node
+    # matches: their guessed NodeAffinity max (the term weight) is wrong (the
+    # measured max is 0), so the compacted FIX list spans 3+ groups of MAX_PG.
+    # Interleaved with pods whose guess is right, and with a PreferNoSchedule
+    # taint so TaintToleration normalises too.  KS_EARLY_FIX=0 runs the FIX
+    # sweep behind the merge (the multi-rank order) on one rank.
+    from ksched.objects import NodeSelectorRequirement as R, NodeSelectorTerm as T, \
+        PreferredSchedulingTerm as PT, Taint
+    from scenarios import node, pod
+
+    monkeypatch.setenv("KS_EARLY_FIX", early)
+    Gi = 1 << 30
+    nodes = [node(f"n{i}", cpu=(8 + 8 * (i % 5)) * 1000, mem=(32 << (i % 4)) * Gi,
+                  labels={"zone": f"z{i % 3}", "disk": "ssd" if i % 4 == 0 else "hdd"},
+                  taints=[Taint("spot", "true", "PreferNoSchedule")] if i % 7 == 0 else [])
+             for i in range(300)]
+    pods = []
+    flagged = 0
+    for j in range(600):
+        if j % 5 != 0:  # preferred term matching nothing: guess = weight, true max = 0
+            pref = [PT(1 + j % 90, T([R("gpu", "Exists")]))]
+            flagged += 1
+        else:  # matches some feasible node: the guess (sum of weights) is right
+            pref = [PT(10, T([R("disk", "In", ["ssd"])]))]
+        pods.append(pod(f"p{j}", cpu=100 + 37 * (j % 23), mem=(1 + j % 7) * Gi // 4, preferred=pref))
+    a = Arena()
+    na, n = nodes_array(nodes, a)
+    pa, m = pods_array(pods, a)
+    slots = (C.c_uint32 * n)(*range(n))
+    o = pyoracle.Oracle(n)
+    o.upsert(na, slots, n)
+    want = o.schedule(pa, m)
+    with Scheduler(n, pods_per_round=256) as s:
+        s.upsert_nodes_raw(na, slots, n)
+        got = s.schedule_raw(pa, m)
+        dbg = (C.c_uint64 * 16)()
+        assert s.lib.ks_debug_counters(s.ctx, dbg) == 0
+    assert_results_equal(got, want, m, f"fix groups (early={early})")
+    # every flagged pod is re-swept at least once (a pod of a stopped round may be re-swept again)
+    assert dbg[4] >= flagged, (list(dbg), flagged)
