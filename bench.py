@@ -1,37 +1,57 @@
 #!/usr/bin/env python3
 """bench.py — pods scheduled/sec at 1M nodes (BASELINE.json metric) on MI355X.
 
-Workload (BASELINE.json configs[2], "C3" of SURVEY.md §8(d)): a 1,000,000-node
-kwok-shaped heterogeneous cluster (cpu 8-96 cores, memory 32-512 Gi, 32/110
-pods, kwok NoSchedule taint; every node pre-filled with seeded pods to a
-random 0-50% of its CPU), and a stream of resource-only pods (cpu 50-4000m,
-memory 64Mi x 1..256, 10% best-effort, kwok tolerations).  Filter =
-NodeUnschedulable/NodeName/TaintToleration/NodeAffinity/NodeResourcesFit,
-Score = LeastAllocated + BalancedAllocation + TaintToleration (+ NodeAffinity
-skipped, ImageLocality 0), percentageOfNodesToScore = 100, deterministic
-lowest-slot tie-break, sequential-equivalent in-order commit.
+Workload (default: BASELINE.json configs[2], "C3" of SURVEY.md §8(d)): a
+1,000,000-node kwok-shaped heterogeneous cluster (cpu 8-96 cores, memory
+32-512 Gi, 32/110 pods, kwok NoSchedule taint; every node pre-filled with
+seeded pods to a random 0-50% of its CPU), and a stream of resource-only pods
+(cpu 50-4000m, memory 64Mi x 1..256, 10% best-effort, kwok tolerations).
+Filter = NodeUnschedulable/NodeName/TaintToleration/NodeAffinity/
+NodeResourcesFit, Score = LeastAllocated + BalancedAllocation +
+TaintToleration (+ NodeAffinity skipped, ImageLocality 0),
+percentageOfNodesToScore = 100, deterministic lowest-slot tie-break,
+sequential-equivalent in-order commit.
 
 A "step" schedules one batch of pods (default 32768) to completion against the
-live cluster; inputs are resident in HBM before the timed region (the batch
-is compiled and uploaded by ks_batch_prepare beforehand).  With --gpus N the
-node slots are sharded across N ranks (one process per GPU, RCCL candidate
-all-gather); every rank schedules the same pods, so `value` is the job's
-pods/s (strong scaling: the cluster is fixed at 1M nodes).
+live cluster.  `value` times ks_batch_run only: the batch was compiled and
+uploaded by ks_batch_prepare before the timed region (inputs resident in
+HBM).  Beside it the line reports:
 
---kind labeled is configs[3] (C4: label bitsets, nodeSelector / required and
-preferred NodeAffinity, NoSchedule / NoExecute / PreferNoSchedule taints).
---workload c5 is configs[4] (C5): a step is one burst (default 100k pods)
-scheduled to completion followed by the seeded watch-event log (5 % of the
-bound pods deleted, 0.1 % node updates, 0.01 % node deletes + adds) applied
-to the device cache through the C ABI; the timed region holds both, the
-host-side generation and marshalling of the log do not (ksched/stream.py).
+* value_end_to_end: the same steps through the whole boundary (pod compile +
+  H2D + run + D2H of the results), pipelined with ks_batch_submit /
+  ks_batch_wait so that compiling batch k+1 overlaps running batch k;
+* latency: per-call wall time of ks_schedule (compile + upload + run +
+  results) for 1-, 16- and 256-pod batches (p50 / p99), next to the
+  reference's ScheduleOne latency (~560 us per pod per shard, README.adoc:786);
+* roofline: the sweep kernel's VALU issue fraction (its binding resource) from
+  the PMC file measured for this exact configuration and kernel source
+  (profiles/pmc/<key>.json, tools/pmc.sh), with the measured HBM traffic and
+  its fraction of 8 TB/s beside it;
+* cpu_baseline: the C++ oracle (a restatement of upstream kube-scheduler) on a
+  bounded prefix of the same stream, on the box's CPU share.
+
+--gpus N: one process per GPU.  Launched by torchrun (WORLD_SIZE set) each
+rank runs directly; otherwise bench.py starts the N rank processes itself
+(children get RANK / LOCAL_RANK / WORLD_SIZE; nothing touches the GPU before
+they start).  Node slots are sharded across ranks (RCCL candidate
+all-gather); every rank schedules the same pods, so `value` is the job's pods/s
+(strong scaling: the cluster is fixed at 1M nodes).
+
+--kind labeled is configs[3] (C4).  --kind kwok is the reference's own node
+shape (kwok/make_nodes/main.go:126-181), with --pods besteffort its request-less
+busybox pods (kwok/make_pods/main.go:118-148).  --workload c5 is configs[4]:
+a step is one burst (default 100k pods) scheduled to completion followed by
+the seeded watch-event log applied through ks_events_apply.
 """
 from __future__ import annotations
 
 import argparse
 import ctypes as C
+import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -39,13 +59,17 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "k8s-1m_amd"))
 
-B_NODE = 56  # algorithmic bytes per (pod, node) evaluation, resource-only
+B_NODE = 56  # node-row bytes per (pod, node) evaluation, resource-only
 B_NODE_LABELED = 96  # ... with label / taint bitsets (C4)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-# VALU issue peak in lane-ops/s: 256 CUs x 4 SIMD-32 x 32 lanes x 2.4 GHz
-# (MI355X_MICROARCH.md: a wave64 VALU instruction issues over 2 cycles; 32-bit
-# rate -- binary64 instructions take twice as long, so the sweep's mix peaks lower)
-VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
+# VALU issue peak: 256 CUs x 4 SIMDs x one wave64 instruction per 2 cycles x
+# 2.4 GHz (MI355X_MICROARCH.md: "issues each VALU instruction over 2 cycles";
+# max clock 2400 MHz) = 1.229e12 wave-instructions/s = 78.6e12 lane-ops/s.
+# binary64 instructions occupy the SIMD twice as long, so a mix with f64 peaks lower.
+VALU_PEAK_WAVE_INSTR = 256 * 4 * 0.5 * 2.4e9
+REF_SCHEDULE_ONE_US = 560.0  # README.adoc:786 (per pod per shard, ~195 nodes evaluated)
+KERNEL_SOURCES = ["k8s-1m_amd/csrc/ksched_kernels.hip", "k8s-1m_amd/csrc/ksched_dev.hpp",
+                  "k8s-1m_amd/csrc/ksched_kernels.hpp", "k8s-1m_amd/Makefile"]
 
 
 def parse():
@@ -60,22 +84,85 @@ def parse():
     ap.add_argument("--topk", type=int, default=0)
     ap.add_argument("--nodes-per-lane", type=int, default=4)
     ap.add_argument("--kind", default="hetero", choices=["hetero", "kwok", "labeled"])
+    ap.add_argument("--pods", default="default", choices=["default", "besteffort"],
+                    help="besteffort: request-less pods (kwok/make_pods/main.go:118-148)")
     ap.add_argument("--workload", default="batch", choices=["batch", "c5"],
                     help="batch: one batch of --batch pods per step; c5: one burst + its event log per step")
     ap.add_argument("--burst", type=int, default=100_000, help="pods per burst (--workload c5)")
-    ap.add_argument("--prefill", type=float, default=0.5)
-    ap.add_argument("--cpu-pods", type=int, default=40, help="oracle sample size (pods), single thread")
-    ap.add_argument("--cpu-threads", type=int, default=16, help="oracle threads for cpu_baseline (box CPU share)")
-    ap.add_argument("--cpu-pods-mt", type=int, default=240, help="oracle sample size (pods), multi-thread")
+    ap.add_argument("--prefill", type=float, default=None, help="max prefill fraction (default 0.5, kwok 0)")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (compile + H2D + run + D2H) pass")
+    ap.add_argument("--latency-calls", type=int, default=100, help="ks_schedule calls per latency batch size (0: skip)")
+    ap.add_argument("--cpu-pods", type=int, default=24, help="oracle sample (pods), single thread")
+    ap.add_argument("--cpu-pods-mt", type=int, default=400, help="oracle sample (pods), multi-thread")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--pmc-file", default=os.environ.get("KS_PMC_FILE", str(ROOT / "profiles" / "pmc_sweep.json")),
-                    help="JSON with measured L2-fabric bytes per sweep launch (tools/pmc.sh + tools/pmc_summary.py)")
-    return ap.parse_args()
+    ap.add_argument("--pmc-dir", default=str(ROOT / "profiles" / "pmc"),
+                    help="per-configuration PMC summaries (tools/pmc.sh + tools/pmc_summary.py)")
+    a = ap.parse_args()
+    if a.prefill is None:
+        a.prefill = 0.0 if a.kind == "kwok" else 0.5
+    return a
+
+
+# ------------------------------------------------------------------ launch
+
+def spawn_ranks(args) -> int:
+    """--gpus N without a launcher: start the N rank processes (before any GPU call)."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve())] + sys.argv[1:], env=env))
+    rc = 0
+    try:
+        for p in procs:
+            rc = max(rc, p.wait())
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    return rc
+
+
+def uid_path(world: int) -> Path:
+    # Every local rank of one launch is a child of the same parent (the torchrun
+    # agent, or bench.py's own spawner), so the parent's pid (+ its restart
+    # count) names this launch alone: a file left by an earlier launch is never read.
+    key = "_".join([os.environ.get("TORCHELASTIC_RUN_ID", "run"), os.environ.get("MASTER_PORT", "0"),
+                    str(os.getppid()), os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")]).replace("/", "_")
+    return Path(os.environ.get("TMPDIR", "/tmp")) / f"ksched_uid_{key}_w{world}.bin"
+
+
+def exchange_unique_id(rank: int, world: int) -> bytes:
+    """Rank 0 publishes the RCCL unique id in a file every local rank reads."""
+    from ksched import Scheduler
+
+    path = uid_path(world)
+    if rank == 0:
+        tmp = path.with_suffix(".tmp")
+        tmp.write_bytes(Scheduler.comm_unique_id())
+        os.replace(tmp, path)
+        return path.read_bytes()
+    deadline = time.time() + 300
+    while time.time() < deadline:
+        if path.exists():
+            data = path.read_bytes()
+            if len(data) == 128:
+                return data
+        time.sleep(0.05)
+    raise TimeoutError(f"rank {rank}: no RCCL unique id at {path}")
 
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     # No torch in this process: torch bundles its own libamdhip64 / librccl
@@ -84,7 +171,6 @@ def main():
     # ranks rendezvous through a file on the node (RCCL unique id) and use the
     # scheduler's own RCCL communicator for barriers and the max-over-ranks time.
     from ksched import Scheduler, synth
-    from ksched.framework import results_to_arrays
 
     kind = {"hetero": synth.HETERO, "kwok": synth.KWOK, "labeled": synth.LABELED}[args.kind]
     t_setup = time.time()
@@ -94,9 +180,23 @@ def main():
         sched.comm_init(exchange_unique_id(rank, world))
         if rank == 0:  # ncclCommInitRank returned: every rank has read the id
             uid_path(world).unlink(missing_ok=True)
-
     if args.workload == "c5":
         return run_c5(args, kind, sched, world, rank, t_setup)
+    return run_batches(args, kind, sched, world, rank, t_setup)
+
+
+def pod_stream(args, kind, n, seed):
+    from ksched import synth
+
+    if args.pods == "besteffort":
+        return synth.besteffort_pods(n)
+    return synth.pods(kind, n, seed)
+
+
+def run_batches(args, kind, sched, world, rank, t_setup):
+    from ksched import synth
+    from ksched.framework import results_to_arrays
+
     nodes = synth.nodes(kind, args.nodes, 1)
     slots = synth.slot_array(args.nodes)
     sched.upsert_nodes_raw(nodes.nodes, slots, args.nodes)
@@ -106,48 +206,126 @@ def main():
         assert sched.lib.ks_pods_add(sched.ctx, pre.pods, pre.slot_ptr, pre.n_pods) == 0, \
             sched.lib.ks_last_error(sched.ctx)
     n_batches = args.warmup + args.steps
-    pods = synth.pods(kind, n_batches * args.batch, 2)
+    pods = pod_stream(args, kind, n_batches * args.batch, 2)
+    t0 = time.perf_counter()
     batches = [sched.prepare(pods.pods_at(b * args.batch), args.batch) for b in range(n_batches)]
+    prepare_s = time.perf_counter() - t0
     setup_s = time.time() - t_setup
 
     def barrier():
         if world > 1:
             sched.allreduce_max([0.0])  # RCCL all-reduce on the scheduler's stream
 
-    def sync():
-        pass  # ks_batch_run returns after hipStreamSynchronize on the scheduler stream
-
     for b in range(args.warmup):
         sched.run(batches[b])
     sched.reset_stats()
     sched.set_timing(True)
     barrier()
-    sync()
     t0 = time.perf_counter()
     for b in range(args.warmup, n_batches):
-        sched.run(batches[b])
-    sync()
+        sched.run(batches[b])  # returns after hipStreamSynchronize on the scheduler stream
     barrier()
     elapsed = time.perf_counter() - t0
     sched.set_timing(False)
     if world > 1:
         elapsed = sched.allreduce_max([elapsed])[0]
-    # scheduled fraction of the timed pods (sanity for the reader)
+    st = sched.stats()
+    dbg = (C.c_uint64 * 16)()
+    sched.lib.ks_debug_counters(sched.ctx, dbg)
     scheduled = 0
     for b in range(args.warmup, n_batches):
         r = results_to_arrays(sched.results(batches[b], args.batch), args.batch)
         scheduled += int((r["status"] == 0).sum())
-
-    pods_timed = args.steps * args.batch
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_pods > 0:
-        cpu = cpu_baseline(args, kind, nodes, slots, pre, pods)
-    line = report(args, sched, world, pods_timed, elapsed, scheduled, setup_s, cpu)
     for b in batches:
         sched.free(b)
+    pods_timed = args.steps * args.batch
+
+    e2e = None if args.no_e2e else end_to_end(args, kind, sched, world, barrier)
+    lat = latency(args, kind, sched, world) if args.latency_calls > 0 else None
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_pods > 0:
+        cpu = cpu_baseline(args, nodes, slots, pre, pods)
+    line = report(args, sched, st, dbg, world, pods_timed, elapsed, scheduled, setup_s, cpu)
+    line["extra"]["prepare_us_per_pod"] = round(1e6 * prepare_s / (n_batches * args.batch), 3)
+    if e2e:
+        line["value_end_to_end"] = e2e.pop("value")
+        line["end_to_end"] = e2e
+    if lat:
+        line["latency"] = lat
     sched.close()
     if rank == 0:
         print(json.dumps(line), flush=True)
+
+
+def end_to_end(args, kind, sched, world, barrier):
+    """The timed steps again through the whole boundary: compile + H2D
+    (ks_batch_prepare), run, D2H (the run copies results into the batch's
+    pinned buffer; ks_batch_results reads them), with batch k+1 compiled on
+    the host while batch k runs (ks_batch_submit / ks_batch_wait)."""
+    n = args.steps
+    pods = pod_stream(args, kind, n * args.batch, 7)
+    lib, ctx = sched.lib, sched.ctx
+    from ksched import _abi
+
+    out = (_abi.KsResult * args.batch)()
+    barrier()
+    t0 = time.perf_counter()
+    cur = sched.prepare(pods.pods_at(0), args.batch)
+    assert lib.ks_batch_submit(ctx, cur) == 0
+    compile_s = 0.0
+    for k in range(n):
+        nxt = None
+        if k + 1 < n:
+            tc = time.perf_counter()
+            nxt = sched.prepare(pods.pods_at((k + 1) * args.batch), args.batch)
+            compile_s += time.perf_counter() - tc
+            assert lib.ks_batch_submit(ctx, nxt) == 0
+        assert lib.ks_batch_wait(ctx, cur) == 0, lib.ks_last_error(ctx)
+        assert lib.ks_batch_results(ctx, cur, out) == 0
+        sched.free(cur)
+        cur = nxt
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        elapsed = sched.allreduce_max([elapsed])[0]
+    return {"value": round(n * args.batch / elapsed, 1), "unit": "pods/s", "steps": n,
+            "ms_per_step": round(1e3 * elapsed / n, 3),
+            "host_compile_ms_per_step": round(1e3 * compile_s / max(1, n - 1), 3),
+            "what": "ks_batch_prepare (compile + H2D) + ks_batch_submit/wait (run + D2H) + ks_batch_results, "
+                    "batch k+1 compiled while batch k runs; fresh pods (seed 7) against the live cluster"}
+
+
+def latency(args, kind, sched, world):
+    """Per-call wall time of ks_schedule (compile + upload + run + results) on
+    the live cluster, for 1-, 16- and 256-pod batches."""
+    import numpy as np
+
+    from ksched import _abi
+
+    res = {}
+    seed = 100
+    for size in (1, 16, 256):
+        calls = max(5, args.latency_calls if size < 256 else args.latency_calls // 2)
+        pods = pod_stream(args, kind, size * (calls + 3), seed)
+        seed += 1
+        out = (_abi.KsResult * size)()
+        ts = []
+        for c in range(calls + 3):  # 3 untimed calls warm the batch pool
+            t0 = time.perf_counter()
+            st = sched.lib.ks_schedule(sched.ctx, pods.pods_at(c * size), size, out)
+            dt = time.perf_counter() - t0
+            assert st == 0, sched.lib.ks_last_error(sched.ctx)
+            if c >= 3:
+                ts.append(dt)
+        a = np.array(ts) * 1e6
+        res[f"batch_{size}"] = {"calls": calls, "p50_us": round(float(np.percentile(a, 50)), 1),
+                                "p99_us": round(float(np.percentile(a, 99)), 1),
+                                "per_pod_p50_us": round(float(np.percentile(a, 50)) / size, 2)}
+    res["reference_schedule_one_us"] = REF_SCHEDULE_ONE_US
+    res["what"] = ("ks_schedule wall time per call (pod compile + H2D + every round + D2H), "
+                   f"{args.nodes} nodes, {world} GPU(s); reference: ScheduleOne per pod per shard "
+                   "(~3.9k nodes, ~195 evaluated), README.adoc:786")
+    return res
 
 
 def run_c5(args, kind, sched, world, rank, t_setup):
@@ -205,45 +383,100 @@ def run_c5(args, kind, sched, world, rank, t_setup):
     elapsed = t_run + t_ev
     if world > 1:
         elapsed = sched.allreduce_max([elapsed])[0]
+    st = sched.stats()
+    dbg = (C.c_uint64 * 16)()
+    sched.lib.ks_debug_counters(sched.ctx, dbg)
     pods_timed = args.steps * args.burst
     c5 = {"burst_ms_mean": round(1e3 * t_run / args.steps, 3), "events_ms_mean": round(1e3 * t_ev / args.steps, 3),
           "events_per_burst": round(n_events / args.steps, 1),
           "events_per_s": round(n_events / t_ev, 1) if t_ev else None,
           "bound_pods_after": int(len(stream.bound_pod))}
-    line = report(args, sched, world, pods_timed, elapsed, scheduled, setup_s, None, c5=c5)
+    line = report(args, sched, st, dbg, world, pods_timed, elapsed, scheduled, setup_s, None, c5=c5)
     sched.close()
     if rank == 0:
         print(json.dumps(line), flush=True)
 
 
-WORKLOADS = {
-    "hetero": "C3: {n} heterogeneous kwok-shaped nodes, prefill<{f:.0%} cpu, resource-only pods; "
-              "Fit+LeastAllocated+BalancedAllocation+TaintToleration, pct=100, in-order commit",
-    "kwok": "C1 shape at scale: {n} homogeneous kwok nodes, prefill<{f:.0%} cpu, resource-only pods; "
-            "Fit+LeastAllocated+BalancedAllocation+TaintToleration, pct=100, in-order commit",
-    "labeled": "C4: {n} nodes with label bitsets and NoSchedule/NoExecute/PreferNoSchedule taints, "
-               "prefill<{f:.0%} cpu; pods with nodeSelector / required + preferred NodeAffinity / "
-               "tolerations; all default Filter + Score plugins incl. TaintToleration and NodeAffinity "
-               "normalisation, pct=100, in-order commit",
-}
+# ------------------------------------------------------------------ report
+
+def workload_name(args) -> str:
+    n, f = args.nodes, args.prefill
+    if args.workload == "c5":
+        return (f"C5: {n} heterogeneous nodes, prefill<50% cpu; bursts of {args.burst} resource-only pods, "
+                "each followed by its watch-event log (5% bound-pod deletes, 0.1% node updates, 0.01% node "
+                "deletes + adds) applied to the device cache; pct=100, in-order commit")
+    pods = ("request-less busybox pods (kwok/make_pods)" if args.pods == "besteffort"
+            else "resource-only pods (cpu 50-4000m, mem 64Mi x 1..256, 10% best-effort)")
+    if args.kind == "hetero":
+        cfg = "C2" if n <= 100_000 else "C3"
+        return (f"{cfg}: {n} heterogeneous kwok-shaped nodes, prefill<{f:.0%} cpu, {pods}; "
+                "Fit+LeastAllocated+BalancedAllocation+TaintToleration, pct=100, in-order commit")
+    if args.kind == "kwok":
+        return (f"kwok: {n} identical kwok nodes (kwok/make_nodes), prefill<{f:.0%} cpu, {pods}; "
+                "Fit+LeastAllocated+BalancedAllocation+TaintToleration, pct=100, in-order commit")
+    return (f"C4: {n} nodes with label bitsets and NoSchedule/NoExecute/PreferNoSchedule taints, "
+            f"prefill<{f:.0%} cpu; pods with nodeSelector / required + preferred NodeAffinity / "
+            "tolerations; all default Filter + Score plugins incl. TaintToleration and NodeAffinity "
+            "normalisation, pct=100, in-order commit")
 
 
-def report(args, sched, world, pods_timed, elapsed, scheduled, setup_s, cpu, c5=None):
-    st = sched.stats()
-    dbg = (C.c_uint64 * 16)()
-    sched.lib.ks_debug_counters(sched.ctx, dbg)
-    value = pods_timed / elapsed
+def pmc_key(args, world) -> str:
+    """Name of the PMC summary measured for exactly this configuration."""
+    pods = "-be" if args.pods == "besteffort" else ""
+    return (f"{args.workload}_{args.kind}{pods}_n{args.nodes}_P{args.pods_per_round}_K{args.topk or args.pods_per_round}"
+            f"_npl{args.nodes_per_lane}_w{world}")
+
+
+def kernel_src_hash() -> str:
+    h = hashlib.sha256()
+    for f in KERNEL_SOURCES:
+        h.update((ROOT / f).read_bytes())
+    return h.hexdigest()[:16]
+
+
+def roofline(args, st, world):
     labeled = args.kind == "labeled"
-    b_node = B_NODE_LABELED if labeled else B_NODE
     sweep_avg_ms = st.sweep_ms / max(1, st.sweep_launches)
     evals_per_launch = st.sweep_evals / max(1, st.sweep_launches)
-    achieved = b_node * evals_per_launch / (sweep_avg_ms * 1e-3) / 1e9 if st.sweep_launches else None
-    traffic, pmc = None, {}
-    # the PMC file was measured on the default (C3) workload: used for C3 lines only
-    if args.pmc_file and Path(args.pmc_file).exists() and args.kind == "hetero" and args.workload == "batch":
-        pmc = json.loads(Path(args.pmc_file).read_text())
-        traffic = pmc.get("hbm_bytes_per_sweep_launch")
+    launch_s = sweep_avg_ms * 1e-3
+    key = pmc_key(args, world)
+    src = kernel_src_hash()
+    path = Path(args.pmc_dir) / f"{key}.json"
+    pmc = json.loads(path.read_text()) if path.exists() else {}
+    fresh = bool(pmc) and pmc.get("kernel_src") == src
+    r = {"bound": "valu", "achieved": None, "peak": round(VALU_PEAK_WAVE_INSTR * 64 / 1e12, 2),
+         "unit": "T VALU lane-ops/s", "frac": None, "traffic": None,
+         "kernel": pmc.get("sweep_kernel", "ks::sweep_kernel"), "avg_launch_ms": round(sweep_avg_ms, 4),
+         "evals_per_launch": int(evals_per_launch),
+         "pmc": f"profiles/pmc/{key}.json" + ("" if fresh else (" (stale: kernel source changed)" if pmc else
+                                                                 " (missing)")),
+         "kernel_src": src}
+    if fresh and st.sweep_launches:
+        wi = pmc["valu_wave_instr_per_eval"] * evals_per_launch  # wave instructions per launch
+        r["achieved"] = round(wi * 64 / launch_s / 1e12, 2)
+        r["frac"] = round(wi / launch_s / VALU_PEAK_WAVE_INSTR, 4)
+        r["valu_lane_ops_per_eval"] = round(pmc["valu_wave_instr_per_eval"] * 64, 2)
+        if pmc.get("valu_busy") is not None:
+            r["valu_busy"] = pmc["valu_busy"]  # SQ_ACTIVE_INST_VALU share of SIMD cycles (f64 counted at its cost)
+        if pmc.get("hbm_bytes_per_eval") is not None:
+            traffic = pmc["hbm_bytes_per_eval"] * evals_per_launch
+            r["traffic"] = int(traffic)
+            r["hbm"] = {"achieved": round(traffic / launch_s / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(traffic / launch_s / 1e9 / HBM_PEAK_GBS, 4),
+                        "what": "2 x FETCH_SIZE + WRITE_SIZE per sweep launch (L2 memory-side bytes, "
+                                "Infinity-Cache hits included: an upper bound on HBM traffic)"}
+        if pmc.get("lds_bank_conflict_ratio") is not None:
+            r["lds_bank_conflict_ratio"] = pmc["lds_bank_conflict_ratio"]
+    # compulsory node-table bytes: every launch needs each local node row once
+    b_node = B_NODE_LABELED if labeled else B_NODE
+    local_nodes = args.nodes / world
+    r["compulsory_bytes_per_launch"] = int(b_node * local_nodes)
+    r["compulsory_hbm_frac"] = round(b_node * local_nodes / launch_s / 1e9 / HBM_PEAK_GBS, 4) if launch_s else None
+    return r
 
+
+def report(args, sched, st, dbg, world, pods_timed, elapsed, scheduled, setup_s, cpu, c5=None):
+    value = pods_timed / elapsed
     line = {
         "metric": "pods scheduled/sec at 1M nodes (1/2/4/8 GPU) + % of HBM roofline",
         "value": round(value, 1),
@@ -258,7 +491,7 @@ def report(args, sched, world, pods_timed, elapsed, scheduled, setup_s, cpu, c5=
         "dtype": "int64+f64",
         "data": "synthetic (seeded kwok-shaped cluster and pod stream, libksynth)",
         "config": {
-            "workload": WORKLOADS[args.kind].format(n=args.nodes, f=args.prefill),
+            "workload": workload_name(args),
             "nodes": args.nodes,
             "pods_per_step": args.burst if c5 else args.batch,
             "pods_per_round": args.pods_per_round,
@@ -266,25 +499,7 @@ def report(args, sched, world, pods_timed, elapsed, scheduled, setup_s, cpu, c5=
             "parallelism": f"node-sharded x{world} (RCCL all-gather)" if world > 1 else "1 GPU",
             "node_evals_per_pod": args.nodes,
         },
-        "roofline": {
-            "bound": "hbm",
-            "achieved": round(achieved, 1) if achieved else None,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-            "traffic": traffic,
-            "kernel": "ks::sweep_kernel",
-            "bytes_per_eval": b_node,
-            "evals_per_launch": int(evals_per_launch),
-            "avg_launch_ms": round(sweep_avg_ms, 4),
-            "traffic_source": (f"profiles/{Path(args.pmc_file).name} ({pmc.get('tag')}): 2 x FETCH_SIZE + WRITE_SIZE "
-                               "per launch at the default config; L2 memory-side bytes (Infinity-Cache hits "
-                               "included)") if traffic else None,
-            "valu_lane_ops_per_eval": pmc.get("valu_lane_ops_per_eval"),
-            # the sweep re-reads each node row once per pod group, not once per
-            # pod, so its HBM fraction exceeds 1; the binding resource is VALU issue
-            "valu": valu_roofline(pmc, evals_per_launch, sweep_avg_ms),
-        },
+        "roofline": roofline(args, st, world),
         "cpu_baseline": cpu,
         "extra": {
             "rounds": int(st.rounds),
@@ -297,91 +512,50 @@ def report(args, sched, world, pods_timed, elapsed, scheduled, setup_s, cpu, c5=
             "pods_reswept_wrong_norm_guess": int(dbg[4]),  # since open (warmup included)
             "node_evals_per_s": round(value * args.nodes, 1),
             "setup_s": round(setup_s, 2),
+            "pmc_key": pmc_key(args, world),
         },
     }
     if c5:
-        line["config"]["workload"] = (
-            f"C5: {args.nodes} heterogeneous nodes, prefill<50% cpu; bursts of {args.burst} resource-only pods, "
-            "each followed by its watch-event log (5% bound-pod deletes, 0.1% node updates, 0.01% node "
-            "deletes + adds) applied to the device cache; pct=100, in-order commit")
         line["config"]["bursts_timed"] = args.steps
         line["extra"].update(c5)
     return line
 
 
+def cpu_threads() -> int:
+    """The CPU share this process may use: OMP_NUM_THREADS (16 per GPU on the
+    box), else the affinity mask."""
+    aff = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(aff, int(omp))) if omp and omp.isdigit() else aff
 
 
-def valu_roofline(pmc, evals_per_launch, sweep_avg_ms):
-    ops = pmc.get("valu_lane_ops_per_eval")
-    if not ops or not sweep_avg_ms:
-        return None
-    achieved = ops * evals_per_launch / (sweep_avg_ms * 1e-3) / 1e12
-    return {"achieved": round(achieved, 2), "peak": round(VALU_PEAK_TOPS, 2), "unit": "T lane-ops/s",
-            "frac": round(achieved / VALU_PEAK_TOPS, 4),
-            "source": "SQ_INSTS_VALU x 64 per evaluation from the PMC file; 32-bit issue-rate peak"}
-
-
-def uid_path(world: int) -> Path:
-    # Every local rank of one launch is a child of the same torchrun agent, so
-    # the agent's pid (+ its restart count) names this launch alone: a file
-    # left by an earlier launch on the same port is never read.
-    key = "_".join([os.environ.get("TORCHELASTIC_RUN_ID", "run"), os.environ.get("MASTER_PORT", "0"),
-                    str(os.getppid()), os.environ.get("TORCHELASTIC_RESTART_COUNT", "0")]).replace("/", "_")
-    return Path(os.environ.get("TMPDIR", "/tmp")) / f"ksched_uid_{key}_w{world}.bin"
-
-
-def exchange_unique_id(rank: int, world: int) -> bytes:
-    """Rank 0 publishes the RCCL unique id in a file every local rank reads."""
-    from ksched import Scheduler
-
-    path = uid_path(world)
-    if rank == 0:
-        tmp = path.with_suffix(".tmp")
-        tmp.write_bytes(Scheduler.comm_unique_id())
-        os.replace(tmp, path)
-        return path.read_bytes()
-    deadline = time.time() + 300
-    while time.time() < deadline:
-        if path.exists():
-            data = path.read_bytes()
-            if len(data) == 128:
-                return data
-        time.sleep(0.05)
-    raise TimeoutError(f"rank {rank}: no RCCL unique id at {path}")
-
-
-def cpu_baseline(args, kind, nodes, slots, pre, pods):
+def cpu_baseline(args, nodes, slots, pre, pods):
     """The CPU oracle (oracle/oracle.cpp, C++ restatement of upstream v1.31.3) on
-    the same cluster, timed on a bounded pod sample, one host thread."""
+    the same cluster and stream prefix: single thread, and the box's CPU
+    share with parallelize.Until chunking."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import pyoracle
 
-    o = pyoracle.Oracle(args.nodes)
-    o.upsert(nodes.nodes, slots, args.nodes)
-    if pre is not None:
-        o.add_pods(pre.pods, pre.slot_ptr, pre.n_pods)
-    # single thread: the first cpu_pods pods of the stream
+    def timed(threads, n):
+        o = pyoracle.Oracle(args.nodes, threads=threads)
+        o.upsert(nodes.nodes, slots, args.nodes)
+        if pre is not None:
+            o.add_pods(pre.pods, pre.slot_ptr, pre.n_pods)
+        t0 = time.perf_counter()
+        o.schedule(pods.pods, n)
+        dt = time.perf_counter() - t0
+        o.close()
+        return dt
+
     n1 = args.cpu_pods
-    t0 = time.perf_counter()
-    o.schedule(pods.pods, n1)
-    dt1 = time.perf_counter() - t0
-    o.close()
-    # threads with parallelize.Until's chunking (oracle.cpp), on a fresh replica
-    nt, n = max(1, args.cpu_threads), args.cpu_pods_mt
-    o = pyoracle.Oracle(args.nodes, threads=nt)
-    o.upsert(nodes.nodes, slots, args.nodes)
-    if pre is not None:
-        o.add_pods(pre.pods, pre.slot_ptr, pre.n_pods)
-    t0 = time.perf_counter()
-    o.schedule(pods.pods, n)
-    dt = time.perf_counter() - t0
-    o.close()
+    dt1 = timed(1, n1)
+    nt, n = cpu_threads(), args.cpu_pods_mt
+    dt = timed(nt, n)
     return {"value": round(n / dt, 2), "unit": "pods/s", "cores": nt, "kind": "port",
-            "sample": f"first {n} pods of the stream on the same {args.nodes}-node prefilled cluster "
-                      f"({n * args.nodes:.2e} node evaluations, {dt:.1f} s), {nt} threads "
-                      "(parallelize.Until chunking)",
-            "single_thread": {"value": round(n1 / dt1, 2), "cores": 1,
-                              "sample": f"first {n1} pods, {dt1:.1f} s"}}
+            "sample": f"first {n} pods of the stream on the same {args.nodes}-node cluster "
+                      f"({n * args.nodes:.2e} node evaluations, {dt:.1f} s), {nt} threads = the process's CPU "
+                      "share (OMP_NUM_THREADS / affinity), parallelize.Until chunking",
+            "single_thread": {"value": round(n1 / dt1, 2), "cores": 1, "sample": f"first {n1} pods, {dt1:.1f} s"}}
 
 
 if __name__ == "__main__":

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define KSCHED_ABI_VERSION 1
+#define KSCHED_ABI_VERSION 2
 
 /* ---------------------------------------------------------------- status */
 typedef int32_t ks_status;
@@ -84,7 +84,10 @@ typedef struct {
   int32_t effect;    /* KS_EFFECT_* ; KS_EFFECT_ALL = "" (all effects) */
 } ks_toleration;
 
-/* v1.Node (name, labels, spec.taints, spec.unschedulable, status.allocatable) */
+/* v1.Node (name, labels, spec.taints, spec.unschedulable, status.allocatable,
+ * status.images).  images lists every name of every status.images entry
+ * (ContainerImage.Names, flattened); upstream's cache keys ImageStates by
+ * those names (internal/cache/cache.go#addNodeImageStates). */
 typedef struct {
   const char *name;
   int64_t alloc_milli_cpu;
@@ -95,7 +98,8 @@ typedef struct {
   uint32_t n_labels;
   uint32_t n_taints;
   uint32_t unschedulable;
-  uint32_t _pad;
+  uint32_t n_images;
+  const char *const *images;
 } ks_node;
 
 /* One container's resources.requests.  A resource that is ABSENT from the
@@ -107,6 +111,7 @@ typedef struct {
   int64_t memory;
   uint32_t flags;          /* KS_REQ_* presence bits; HAS_OTHER = any other resource (unsupported) */
   uint32_t restart_always; /* init containers only: restartPolicy: Always (sidecar) */
+  const char *image;       /* container image (NULL / "" = none); ImageLocality precondition */
 } ks_container;
 
 /* v1.NodeSelectorOperator */
@@ -140,6 +145,28 @@ typedef struct {
   int32_t _pad;
 } ks_preferred_term;
 
+/* Pod features whose plugins ksched does not model.
+ * The caller sets the bit when the pod carries the feature; a pod with any
+ * bit set is refused with KS_ERR_UNSUPPORTED (ks_pods_check names it) and
+ * the shim falls back to upstream schedulePod for it.  The
+ * default profile's plugins that read them: */
+enum {
+  KS_UNMODELLED_HOST_PORTS = 1u,       /* NodePorts: a container port with hostPort != 0             */
+  KS_UNMODELLED_TOPOLOGY_SPREAD = 2u,  /* PodTopologySpread: topologySpreadConstraints, or the
+                                          system-default constraints apply (the pod is selected by a
+                                          Service or owned by a ReplicaSet / StatefulSet /
+                                          ReplicationController)                                    */
+  KS_UNMODELLED_POD_AFFINITY = 4u,     /* InterPodAffinity: podAffinity / podAntiAffinity terms.  On
+                                          a pod bound through ks_pods_add / KS_EV_POD_ADD it makes
+                                          every later batch refuse until that pod is removed
+                                          (existing pods' terms filter and score the incoming pod) */
+  KS_UNMODELLED_VOLUMES = 8u,          /* VolumeBinding / VolumeRestrictions / VolumeZone /
+                                          NodeVolumeLimits: PVC, ephemeral or CSI volumes           */
+  KS_UNMODELLED_NOMINATED_NODE = 16u,  /* status.nominatedNodeName (evaluateNominatedNode)          */
+  KS_UNMODELLED_RESOURCE_CLAIMS = 32u, /* DynamicResources: spec.resourceClaims                     */
+  KS_UNMODELLED_ALL = 63u
+};
+
 /* v1.Pod restricted to scheduling-relevant fields. */
 typedef struct {
   const char *ns;
@@ -162,7 +189,7 @@ typedef struct {
   uint32_t n_preferred;
   uint32_t has_preferred; /* PreferredDuringSchedulingIgnoredDuringExecution != nil */
   uint32_t has_overhead;
-  uint32_t _pad;
+  uint32_t unmodelled;    /* KS_UNMODELLED_* bits */
 } ks_pod;
 
 /* ------------------------------------------------------------- outputs */
@@ -184,6 +211,13 @@ enum {
 
 enum { KS_RESULT_SINGLE_FEASIBLE = 1u /* upstream returns without scoring */ };
 
+/* fail_counts[KS_FAIL_PREFILTER_RESULT]: nodes outside NodeAffinity's
+ * PreFilterResult (required terms that all name nodes by matchFields
+ * metadata.name In), which upstream v1.31 records as
+ * UnschedulableAndUnresolvable "node is filtered out by the prefilter result"
+ * without running any Filter plugin on them (schedule_one.go#findNodesThatFitPod). */
+enum { KS_FAIL_PREFILTER_RESULT = KS_NUM_FILTER_PLUGINS, KS_NUM_FAIL_COUNTS = KS_NUM_FILTER_PLUGINS + 1 };
+
 /* ScheduleResult{SuggestedHost, EvaluatedNodes, FeasibleNodes} or FitError. */
 typedef struct {
   int32_t node_index;     /* chosen node slot, -1 if none                        */
@@ -191,8 +225,10 @@ typedef struct {
   int64_t total_score;    /* TotalScore of the chosen node (NodePluginScores)    */
   uint32_t feasible_nodes;
   uint32_t evaluated_nodes;
-  uint32_t fail_counts[KS_NUM_FILTER_PLUGINS]; /* nodes rejected first by each filter plugin */
+  uint32_t fail_counts[KS_NUM_FAIL_COUNTS]; /* nodes rejected first by each filter plugin, then
+                                               nodes excluded by the PreFilterResult */
   uint32_t flags;         /* KS_RESULT_*                                         */
+  uint32_t _pad;
 } ks_result;
 
 /* Per-node plugin scores of one pod (parity dump; NodePluginScores analogue). */
@@ -233,7 +269,13 @@ typedef struct {
   int32_t weight_taint;      /* TaintToleration                                 */
   int32_t weight_affinity;   /* NodeAffinity                                    */
   int32_t weight_image;      /* ImageLocality                                   */
-  uint32_t _pad;
+  /* KubeSchedulerProfile.percentageOfNodesToScore.  100 (the default here and
+   * the reference's dist-scheduler/deployment.yaml:95) scores every node; any
+   * other value (0 = upstream's adaptive 50 - N/125, the published run's 5 at
+   * terraform/kubernetes/dist-scheduler.tf:562) makes ks_open return
+   * KS_ERR_UNSUPPORTED: upstream's early stop is order- and parallelism-
+   * dependent (schedule_one.go#numFeasibleNodesToFind / findNodesThatPassFilters). */
+  int32_t percentage_of_nodes_to_score;
 } ks_config;
 
 typedef struct ks_ctx ks_ctx;
@@ -288,12 +330,33 @@ ks_status ks_events_apply(ks_ctx *ctx, const ks_event *events, uint32_t n);
  * sequential ScheduleOne calls.  out[i] receives pod i's result. */
 ks_status ks_schedule(ks_ctx *ctx, const ks_pod *pods, uint32_t n, ks_result *out);
 
+/* Per-pod admission check without scheduling: status[i] = KS_OK, or the
+ * ks_status ks_batch_prepare would fail pod i with (KS_ERR_UNSUPPORTED for a
+ * KS_UNMODELLED_* feature, an unsupported resource or a container image some
+ * node reports; KS_ERR_RANGE; KS_ERR_CAPACITY).  Returns KS_OK when every pod
+ * passes, else the first failing pod's status (ks_last_error names it).  The
+ * shim splits a batch at refused pods and hands those to upstream schedulePod. */
+ks_status ks_pods_check(ks_ctx *ctx, const ks_pod *pods, uint32_t n, ks_status *status);
+
 /* Split form of ks_schedule: compile + upload once (prepare), then run with
- * all inputs resident in HBM (the timed hot path), then fetch results. */
+ * all inputs resident in HBM (the timed hot path), then fetch results.
+ * Batch buffers come from a per-context pool (no device allocation per batch
+ * once the pool holds a batch of that size; ks_batch_free returns them). */
 ks_status ks_batch_prepare(ks_ctx *ctx, const ks_pod *pods, uint32_t n, ks_batch **out);
 ks_status ks_batch_run(ks_ctx *ctx, ks_batch *batch);
 ks_status ks_batch_results(ks_ctx *ctx, const ks_batch *batch, ks_result *out);
 void ks_batch_free(ks_ctx *ctx, ks_batch *batch);
+
+/* Asynchronous run: ks_batch_submit queues a prepared batch on the context's
+ * worker thread (batches run in submission order, each against the cache the
+ * previous one left) and returns at once; ks_batch_wait blocks until that
+ * batch has run and returns its run status.  While batches are in flight the
+ * caller may ks_batch_prepare (compile + upload on a stream of its own, so
+ * compiling batch k+1 overlaps running batch k), ks_batch_results of a waited
+ * batch, and ks_batch_free; every other call on the context first waits for
+ * all submitted batches. */
+ks_status ks_batch_submit(ks_ctx *ctx, ks_batch *batch);
+ks_status ks_batch_wait(ks_ctx *ctx, ks_batch *batch);
 
 /* Per-plugin scores of `pod` on every node slot against the current cache
  * (out has node_capacity entries).  Parity dump of NodePluginScores. */

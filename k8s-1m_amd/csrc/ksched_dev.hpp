@@ -20,6 +20,9 @@ constexpr uint64_t UNSCHED_BIT = 1ull << 63;  // hard-taint word: spec.unschedul
 // Filter status codes (first failing plugin); FEASIBLE = passed every filter.
 constexpr int ST_FEASIBLE = -1;
 constexpr int ST_EMPTY = -2;
+// Outside NodeAffinity's PreFilterResult: no Filter plugin runs on the node
+// and no plugin is blamed (counted in ks_result.fail_counts[5] by the host).
+constexpr int ST_PREFILTERED = 5;
 
 // ---------------------------------------------------------- node table (SoA)
 // Columns are indexed by POSITION, not slot: a shard's slots are permuted so
@@ -63,6 +66,8 @@ enum PodFlags : uint32_t {
   PF_HAS_PREF = 16u,  // preferredDuringScheduling != nil (NodeAffinity not skipped)
   PF_PREF_ERR = 32u,  // preferred terms failed to parse: PreScore error with >= 2 feasible
   PF_AFF = 64u,       // required program present (nodeSelector and/or required terms)
+  PF_PREFILTER = 128u,   // NodeAffinity PreFilterResult: only nodes passing the prefilter program are evaluated
+  PF_NA_CONFLICT = 256u, // NodeAffinity PreFilter rejects (conflicting metadata.name terms): every node fails NodeAffinity
 };
 
 struct alignas(16) PodDev {
@@ -81,7 +86,10 @@ struct alignas(16) PodDev {
   // guess of max raw over feasible nodes.  The merge measures the true maxima;
   // pods whose guess was wrong are re-swept with them (norm_check, fix sweep).
   uint32_t tt_guess, na_guess;
-  uint32_t _pad[3];
+  // NodeAffinity PreFilterResult (PF_PREFILTER): one CK_NAME_EQ clause per
+  // named node, OR-ed; prefilter_out = present nodes outside it (host count)
+  uint32_t pre_off, pre_len;
+  uint32_t prefilter_out;
 };
 static_assert(sizeof(PodDev) == 128, "PodDev layout");
 
@@ -176,9 +184,11 @@ struct DevResult {
   uint32_t feasible_nodes;
   uint32_t evaluated_nodes;
   uint32_t fail_counts[NFILT];
+  uint32_t prefiltered;  // ks_result.fail_counts[KS_FAIL_PREFILTER_RESULT]
   uint32_t flags;
+  uint32_t _pad;
 };
-static_assert(sizeof(DevResult) == 48, "DevResult layout");
+static_assert(sizeof(DevResult) == 56, "DevResult layout");
 
 struct Weights {
   int32_t fit, ba, tt, na, il;

@@ -17,8 +17,13 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
+#include <condition_variable>
 #include <cstring>
+#include <deque>
 #include <map>
+#include <mutex>
+#include <set>
+#include <thread>
 #include <memory>
 #include <string>
 #include <unordered_map>
@@ -107,6 +112,25 @@ bool parse_int64(const std::string &s, int64_t *out) {  // strconv.ParseInt(s, 1
   return true;
 }
 
+// imagelocality#normalizedImageName: a name without a tag gets ":latest".
+std::string normalized_image(const char *p) {
+  std::string n = str(p);
+  const size_t colon = n.rfind(':'), slash = n.rfind('/');
+  const long lc = colon == std::string::npos ? -1 : (long)colon, ls = slash == std::string::npos ? -1 : (long)slash;
+  if (lc <= ls) n += ":latest";
+  return n;
+}
+
+const char *unmodelled_name(uint32_t bits) {
+  if (bits & KS_UNMODELLED_HOST_PORTS) return "host ports (NodePorts)";
+  if (bits & KS_UNMODELLED_TOPOLOGY_SPREAD) return "topology spread constraints (PodTopologySpread)";
+  if (bits & KS_UNMODELLED_POD_AFFINITY) return "pod (anti-)affinity (InterPodAffinity)";
+  if (bits & KS_UNMODELLED_VOLUMES) return "volumes (VolumeBinding / VolumeRestrictions / VolumeZone / NodeVolumeLimits)";
+  if (bits & KS_UNMODELLED_NOMINATED_NODE) return "a nominated node";
+  if (bits & KS_UNMODELLED_RESOURCE_CLAIMS) return "resource claims (DynamicResources)";
+  return "an unknown feature bit";
+}
+
 // ------------------------------------------------------------ host types
 
 struct Tol {
@@ -124,6 +148,7 @@ struct HostNode {
   uint64_t hard = 0, prefer = 0;
   uint64_t lab[LW] = {};
   int64_t num[NNUM] = {};
+  std::vector<std::string> images;  // normalised image names
 };
 
 struct TaintKey {
@@ -146,12 +171,28 @@ struct NumCol {
 struct ks_batch {
   uint32_t n = 0;
   uint32_t dict_version = 0;
+  uint32_t names_version = 0;  // 0: no pod of the batch resolved a node name
   bool ext = false, norm = false;
+  // pooled device buffers (capacities in pods / clause words) and the pinned
+  // host copy of the results, filled at the end of the run
+  uint32_t cap_pods = 0;
+  size_t cap_words = 0;
   PodDev *d_pods = nullptr;
   double *d_pinv = nullptr;  // [n][2] reciprocals of the normalising guesses
   uint64_t *d_clauses = nullptr;
   DevResult *d_results = nullptr;
-  std::vector<ks_result> host_status;  // compile-time errors (none so far)
+  DevResult *h_results = nullptr;
+  // pinned host copies of the compiled batch: uploaded by ks_batch_prepare
+  // when nothing is in flight, else by the run itself (uploaded = false)
+  PodDev *h_pods = nullptr;
+  double *h_pinv = nullptr;
+  uint64_t *h_clauses = nullptr;
+  size_t n_words = 0;
+  bool uploaded = false;
+  // asynchronous run state (ks_batch_submit / ks_batch_wait)
+  bool queued = false, done = false;
+  ks_status run_status = KS_OK;
+  std::string run_err;
 };
 
 struct ks_ctx {
@@ -214,8 +255,14 @@ struct ks_ctx {
   std::unordered_map<uint32_t, NumCol> num_col;
   uint32_t next_bit = 0, next_num = 0;
   std::unordered_map<uint32_t, std::vector<uint32_t>> key_nodes;  // key id -> slots having it
-  uint32_t dict_version = 1;
+  bool compile_used_names = false;  // set by compile_pod when a pod resolved a node name to a slot
+  uint32_t dict_version = 1;   // taint dictionary / node image set (compiled masks and checks)
+  uint32_t names_version = 1;  // node name -> slot map (compiled NodeName / metadata.name slots)
   std::vector<uint32_t> dirty_ext;
+  // normalised image name -> present nodes reporting it (ImageLocality precondition)
+  std::unordered_map<std::string, uint32_t> images;
+  // bound pods carrying pod (anti-)affinity terms (InterPodAffinity precondition)
+  int64_t affinity_pods = 0;
   // comm
   ncclComm_t comm = nullptr;
   // stats
@@ -227,14 +274,38 @@ struct ks_ctx {
   uint64_t sweeps_issued = 0;                // main sweep launches since then (timed or not)
   // Host<->device transfers of one ABI call: a pinned host staging buffer and a
   // device scratch buffer, both bump-allocated and reset at xfer_sync (no
-  // pageable hipMemcpyAsync anywhere).
-  uint8_t *pin = nullptr, *dscr = nullptr;
-  size_t pin_cap = 0, pin_used = 0, dscr_cap = 0, dscr_used = 0;
-  struct Pending {
-    void *dst;
-    size_t off, bytes;
+  // pageable hipMemcpyAsync anywhere), on `stream`.  No fourth stream: the
+  // box gives a process 4 hardware queues (GPU_MAX_HW_QUEUES), and a stream
+  // sharing the resolve's queue serialises resolve k behind sweep k+1.
+  struct Xfer {
+    hipStream_t st = nullptr;
+    uint8_t *pin = nullptr, *dscr = nullptr;
+    size_t pin_cap = 0, pin_used = 0, dscr_cap = 0, dscr_used = 0;
+    struct Pending {
+      void *dst;
+      size_t off, bytes;
+    };
+    std::vector<Pending> d2h_pending;
   };
-  std::vector<Pending> d2h_pending;
+  Xfer xm;
+  // device buffers replaced while work may be in flight: freed at ks_close
+  // (hipFree synchronises the whole device)
+  std::vector<void *> graveyard;
+  std::vector<void *> pinned_graveyard;
+  // batch pool (ks_batch_free returns batches here; buffers are reused)
+  std::mutex pool_mu;
+  std::vector<ks_batch *> pool;
+  std::vector<ks_batch *> all_batches;
+  // host dictionaries / node mirror: ks_batch_prepare vs the worker's reads of t.lw
+  std::mutex mu;
+  std::mutex err_mu;
+  // asynchronous runs (ks_batch_submit / ks_batch_wait)
+  std::thread worker;
+  std::mutex qmu;
+  std::condition_variable qcv, dcv;
+  std::deque<ks_batch *> queue;
+  uint32_t inflight = 0;
+  bool stop = false;
 
   uint32_t intern(const char *p) {
     std::string s = str(p);
@@ -255,6 +326,7 @@ struct ks_ctx {
     va_start(ap, fmt);
     std::vsnprintf(buf, sizeof buf, fmt, ap);
     va_end(ap);
+    std::lock_guard<std::mutex> g(err_mu);
     err = buf;
     return st;
   }
@@ -280,62 +352,72 @@ namespace {
 
 inline size_t xround(size_t b) { return (b + 255) & ~(size_t)255; }
 
-ks_status xfer_sync(ks_ctx *c) {
-  HIPC(c, hipStreamSynchronize(c->stream));
-  for (auto &p : c->d2h_pending) std::memcpy(p.dst, c->pin + p.off, p.bytes);
-  c->d2h_pending.clear();
-  c->pin_used = c->dscr_used = 0;
+using Xfer = ks_ctx::Xfer;
+
+ks_status xfer_sync(ks_ctx *c, Xfer &x) {
+  HIPC(c, hipStreamSynchronize(x.st));
+  for (auto &p : x.d2h_pending) std::memcpy(p.dst, x.pin + p.off, p.bytes);
+  x.d2h_pending.clear();
+  x.pin_used = x.dscr_used = 0;
   return KS_OK;
 }
+ks_status xfer_sync(ks_ctx *c) { return xfer_sync(c, c->xm); }
 
 // Start an ABI call's transfers: completes earlier work, then guarantees
 // pin_bytes of staging and dev_bytes of device scratch (each segment is
-// rounded to 256 B: callers include that slack).
-ks_status xfer_begin(ks_ctx *c, size_t pin_bytes, size_t dev_bytes) {
-  ks_status st = xfer_sync(c);
+// rounded to 256 B: callers include that slack).  Outgrown buffers are
+// retired to the graveyard (freed at ks_close: hipFree would wait for the
+// whole device, including batches running on the other streams).
+ks_status xfer_begin(ks_ctx *c, Xfer &x, size_t pin_bytes, size_t dev_bytes) {
+  ks_status st = xfer_sync(c, x);
   if (st) return st;
-  if (pin_bytes > c->pin_cap) {
-    if (c->pin) HIPC(c, hipHostFree(c->pin));
-    c->pin = nullptr;
-    c->pin_cap = std::max<size_t>(pin_bytes, std::max<size_t>(2 * c->pin_cap, 1 << 20));
-    HIPC(c, hipHostMalloc((void **)&c->pin, c->pin_cap, hipHostMallocDefault));
+  if (pin_bytes > x.pin_cap) {
+    if (x.pin) c->pinned_graveyard.push_back(x.pin);
+    x.pin = nullptr;
+    x.pin_cap = std::max<size_t>(pin_bytes, std::max<size_t>(2 * x.pin_cap, 1 << 20));
+    HIPC(c, hipHostMalloc((void **)&x.pin, x.pin_cap, hipHostMallocDefault));
   }
-  if (dev_bytes > c->dscr_cap) {
-    if (c->dscr) HIPC(c, hipFree(c->dscr));
-    c->dscr = nullptr;
-    c->dscr_cap = std::max<size_t>(dev_bytes, std::max<size_t>(2 * c->dscr_cap, 1 << 20));
-    HIPC(c, hipMalloc((void **)&c->dscr, c->dscr_cap));
+  if (dev_bytes > x.dscr_cap) {
+    if (x.dscr) c->graveyard.push_back(x.dscr);
+    x.dscr = nullptr;
+    x.dscr_cap = std::max<size_t>(dev_bytes, std::max<size_t>(2 * x.dscr_cap, 1 << 20));
+    HIPC(c, hipMalloc((void **)&x.dscr, x.dscr_cap));
   }
   return KS_OK;
 }
+ks_status xfer_begin(ks_ctx *c, size_t pin_bytes, size_t dev_bytes) { return xfer_begin(c, c->xm, pin_bytes, dev_bytes); }
 
 template <class T>
-T *dscratch(ks_ctx *c, size_t count) {
+T *dscratch(Xfer &x, size_t count) {
   const size_t b = xround(std::max<size_t>(count, 1) * sizeof(T));
-  if (c->dscr_used + b > c->dscr_cap) return nullptr;
-  T *p = (T *)(c->dscr + c->dscr_used);
-  c->dscr_used += b;
+  if (x.dscr_used + b > x.dscr_cap) return nullptr;
+  T *p = (T *)(x.dscr + x.dscr_used);
+  x.dscr_used += b;
   return p;
 }
+template <class T>
+T *dscratch(ks_ctx *c, size_t count) { return dscratch<T>(c->xm, count); }
 
-ks_status h2d(ks_ctx *c, void *dst, const void *src, size_t bytes) {
+ks_status h2d(ks_ctx *c, Xfer &x, void *dst, const void *src, size_t bytes) {
   if (!bytes) return KS_OK;
   const size_t b = xround(bytes);
-  if (c->pin_used + b > c->pin_cap) return c->fail(KS_ERR_INVALID, "staging overflow (h2d %zu)", bytes);
-  std::memcpy(c->pin + c->pin_used, src, bytes);
-  HIPC(c, hipMemcpyAsync(dst, c->pin + c->pin_used, bytes, hipMemcpyHostToDevice, c->stream));
-  c->pin_used += b;
+  if (x.pin_used + b > x.pin_cap) return c->fail(KS_ERR_INVALID, "staging overflow (h2d %zu)", bytes);
+  std::memcpy(x.pin + x.pin_used, src, bytes);
+  HIPC(c, hipMemcpyAsync(dst, x.pin + x.pin_used, bytes, hipMemcpyHostToDevice, x.st));
+  x.pin_used += b;
   return KS_OK;
 }
+ks_status h2d(ks_ctx *c, void *dst, const void *src, size_t bytes) { return h2d(c, c->xm, dst, src, bytes); }
 
 // Completed (copied to dst) at the next xfer_sync.
 ks_status d2h(ks_ctx *c, void *dst, const void *src, size_t bytes) {
+  Xfer &x = c->xm;
   if (!bytes) return KS_OK;
   const size_t b = xround(bytes);
-  if (c->pin_used + b > c->pin_cap) return c->fail(KS_ERR_INVALID, "staging overflow (d2h %zu)", bytes);
-  HIPC(c, hipMemcpyAsync(c->pin + c->pin_used, src, bytes, hipMemcpyDeviceToHost, c->stream));
-  c->d2h_pending.push_back({dst, c->pin_used, bytes});
-  c->pin_used += b;
+  if (x.pin_used + b > x.pin_cap) return c->fail(KS_ERR_INVALID, "staging overflow (d2h %zu)", bytes);
+  HIPC(c, hipMemcpyAsync(x.pin + x.pin_used, src, bytes, hipMemcpyDeviceToHost, x.st));
+  x.d2h_pending.push_back({dst, x.pin_used, bytes});
+  x.pin_used += b;
   return KS_OK;
 }
 
@@ -566,6 +648,7 @@ bool compile_term(ks_ctx *c, const ks_term &t, uint32_t term, int32_t weight, Cl
       if (it != c->name_slot.end()) slot = it->second;
     }
     tmp.add(e.op == KS_OP_IN ? CK_NAME_EQ : CK_NAME_NE, term, weight, nullptr, (uint64_t)slot);
+    c->compile_used_names = true;
   }
   if (!ok) return false;
   out.w.insert(out.w.end(), tmp.w.begin(), tmp.w.end());
@@ -585,9 +668,80 @@ void prefer_mask_ref(ks_ctx *c, uint64_t mask, int delta) {
   }
 }
 
+// NodeAffinity.PreFilter's PreFilterResult (upstream v1.31
+// plugins/nodeaffinity/node_affinity.go#PreFilter), from the RAW required
+// terms (parse errors and empty terms included, as upstream): when every term
+// has matchFields metadata.name In requirements, the candidate nodes are the
+// union over terms of the intersection of each term's name sets.  Returns
+// false when some term names no node (all nodes eligible); *names = the union.
+bool prefilter_names(const ks_pod &p, std::vector<std::string> *names) {
+  if (!p.has_required || p.n_required_terms == 0) return false;
+  std::vector<std::string> uni;
+  for (uint32_t i = 0; i < p.n_required_terms; ++i) {
+    const ks_term &t = p.required_terms[i];
+    bool have = false;
+    std::vector<std::string> inter;
+    for (uint32_t k = 0; k < t.n_fields; ++k) {
+      const ks_requirement &r = t.match_fields[k];
+      if (str(r.key) != "metadata.name" || r.op != KS_OP_IN) continue;
+      std::vector<std::string> vs;
+      for (uint32_t v = 0; v < r.n_values; ++v) vs.push_back(str(r.values[v]));
+      std::sort(vs.begin(), vs.end());
+      vs.erase(std::unique(vs.begin(), vs.end()), vs.end());
+      if (!have) {
+        inter = vs;
+        have = true;
+      } else {
+        std::vector<std::string> x;
+        std::set_intersection(inter.begin(), inter.end(), vs.begin(), vs.end(), std::back_inserter(x));
+        inter.swap(x);
+      }
+    }
+    if (!have) return false;  // this term does not restrict node names
+    uni.insert(uni.end(), inter.begin(), inter.end());
+  }
+  std::sort(uni.begin(), uni.end());
+  uni.erase(std::unique(uni.begin(), uni.end()), uni.end());
+  *names = std::move(uni);
+  return true;
+}
+
+// Preconditions of the modelled plugin set: a pod the
+// default profile would filter or score with a plugin ksched does not model is
+// refused, never scheduled approximately.
+ks_status check_modelled(ks_ctx *c, const ks_pod &p) {
+  if (p.unmodelled)
+    return c->fail(KS_ERR_UNSUPPORTED, "pod %s/%s carries %s", str(p.ns).c_str(), str(p.name).c_str(),
+                   unmodelled_name(p.unmodelled));
+  if (c->affinity_pods > 0)
+    return c->fail(KS_ERR_UNSUPPORTED,
+                   "%lld bound pod(s) carry pod (anti-)affinity terms: InterPodAffinity filters and scores every "
+                   "incoming pod", (long long)c->affinity_pods);
+  // ImageLocality scores 0 on every node only when no node reports one of the
+  // pod's images (its per-node NumNodes snapshots make any other case
+  // history-dependent: framework/types.go#ImageStateSummary.Snapshot)
+  if (!c->images.empty()) {
+    auto check = [&](const ks_container *cs, uint32_t n) -> ks_status {
+      for (uint32_t i = 0; i < n; ++i) {
+        if (!cs[i].image || !cs[i].image[0]) continue;
+        auto it = c->images.find(normalized_image(cs[i].image));
+        if (it != c->images.end())
+          return c->fail(KS_ERR_UNSUPPORTED, "pod %s/%s: image %s is present on %u node(s) (ImageLocality)",
+                         str(p.ns).c_str(), str(p.name).c_str(), it->first.c_str(), it->second);
+      }
+      return KS_OK;
+    };
+    ks_status st;
+    if ((st = check(p.containers, p.n_containers)) || (st = check(p.init_containers, p.n_init_containers)))
+      return st;
+  }
+  return KS_OK;
+}
+
 ks_status compile_pod(ks_ctx *c, const ks_pod &p, PodDev &d, ClauseBuf &cl) {
   std::memset(&d, 0, sizeof d);
   ks_status st;
+  if ((st = check_modelled(c, p))) return st;
   if ((st = pod_requests(p, false, &d.req_cpu, &d.req_mem)) ||
       (st = pod_requests(p, true, &d.nz_cpu, &d.nz_mem)))
     return c->fail(st, "pod %s/%s requests a resource other than cpu/memory", str(p.ns).c_str(),
@@ -639,6 +793,7 @@ ks_status compile_pod(ks_ctx *c, const ks_pod &p, PodDev &d, ClauseBuf &cl) {
       auto it = c->name_slot.find((uint32_t)nid);
       if (it != c->name_slot.end()) d.name_slot = (int32_t)it->second;
     }
+    c->compile_used_names = true;
   }
   // required: nodeSelector (term 0) + RequiredDuringScheduling terms (1..)
   d.req_off = cl.count();
@@ -669,6 +824,29 @@ ks_status compile_pod(ks_ctx *c, const ks_pod &p, PodDev &d, ClauseBuf &cl) {
     d.n_req_terms = nt;
   }
   d.req_len = cl.count() - d.req_off;
+  {
+    std::vector<std::string> names;
+    if (prefilter_names(p, &names)) {
+      if (names.empty()) {
+        d.flags |= PF_NA_CONFLICT;  // UnschedulableAndUnresolvable (errReasonConflict) at PreFilter
+      } else {
+        d.flags |= PF_PREFILTER;
+        d.pre_off = cl.count();
+        uint32_t found = 0;
+        for (auto &nm : names) {
+          auto id = c->str_ids.find(nm);
+          if (id == c->str_ids.end()) continue;
+          auto it = c->name_slot.find(id->second);
+          if (it == c->name_slot.end()) continue;  // PreFilterResult names a node the snapshot lacks
+          cl.add(CK_NAME_EQ, 1, 0, nullptr, (uint64_t)it->second);
+          ++found;
+        }
+        d.pre_len = cl.count() - d.pre_off;
+        d.prefilter_out = c->n_present - found;
+      }
+      c->compile_used_names = true;
+    }
+  }
   if (p.n_node_selector || p.has_required) d.flags |= PF_AFF;
   // preferred terms
   d.pref_off = cl.count();
@@ -700,9 +878,29 @@ ks_status compile_pod(ks_ctx *c, const ks_pod &p, PodDev &d, ClauseBuf &cl) {
   return KS_OK;
 }
 
+// Node image set (ImageLocality precondition): reference counts of present
+// nodes per normalised image name.  Returns true when a name is new.
+bool node_images_ref(ks_ctx *c, HostNode &h, int delta) {
+  bool grew = false;
+  for (auto &nm : h.images) {
+    auto it = c->images.find(nm);
+    if (delta > 0) {
+      if (it == c->images.end()) {
+        c->images.emplace(nm, 1u);
+        grew = true;
+      } else {
+        it->second++;
+      }
+    } else if (it != c->images.end() && --it->second == 0) {
+      c->images.erase(it);
+    }
+  }
+  return grew;
+}
+
 // --------------------------------------------------------------- devices
 
-ks_status upload_dirty_ext(ks_ctx *c) {
+ks_status upload_dirty_ext(ks_ctx *c, Xfer &x) {
   if (c->dirty_ext.empty()) return KS_OK;
   std::sort(c->dirty_ext.begin(), c->dirty_ext.end());
   c->dirty_ext.erase(std::unique(c->dirty_ext.begin(), c->dirty_ext.end()), c->dirty_ext.end());
@@ -718,13 +916,13 @@ ks_status upload_dirty_ext(ks_ctx *c) {
     for (int k = 0; k < LW; ++k) e[2 + k] = h.lab[k];
     for (int k = 0; k < NNUM; ++k) e[2 + LW + k] = (uint64_t)h.num[k];
   }
-  ks_status st = xfer_begin(c, n * 4 + ext.size() * 8 + 1024, n * 4 + ext.size() * 8 + 1024);
+  ks_status st = xfer_begin(c, x, n * 4 + ext.size() * 8 + 1024, n * 4 + ext.size() * 8 + 1024);
   if (st) return st;
-  uint32_t *d_pos = dscratch<uint32_t>(c, n);
-  uint64_t *d_ext = dscratch<uint64_t>(c, ext.size());
-  if ((st = h2d(c, d_pos, pos.data(), n * 4)) || (st = h2d(c, d_ext, ext.data(), ext.size() * 8))) return st;
-  HIPC(c, launch_scatter_rows(c->t, d_pos, nullptr, d_ext, n, 2u, c->stream));
-  if ((st = xfer_sync(c))) return st;
+  uint32_t *d_pos = dscratch<uint32_t>(x, n);
+  uint64_t *d_ext = dscratch<uint64_t>(x, ext.size());
+  if ((st = h2d(c, x, d_pos, pos.data(), n * 4)) || (st = h2d(c, x, d_ext, ext.data(), ext.size() * 8))) return st;
+  HIPC(c, launch_scatter_rows(c->t, d_pos, nullptr, d_ext, n, 2u, x.st));
+  if ((st = xfer_sync(c, x))) return st;
   c->dirty_ext.clear();
   return KS_OK;
 }
@@ -824,7 +1022,10 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k) {
   groups = (c->P + pg - 1) / pg;
 
   RoundArgs a{};
-  a.t = c->t;
+  {
+    std::lock_guard<std::mutex> g(c->mu);  // ks_batch_prepare may widen t.lw concurrently
+    a.t = c->t;
+  }
   a.shards = c->d_shards;
   a.total_shards = c->S;
   a.shard0 = shard0;
@@ -967,14 +1168,160 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k) {
 
 // End of a pipeline run of `rounds` rounds: land the last two rounds in the
 // table and wait for everything.
-ks_status drain_rounds(ks_ctx *c, uint32_t rounds) {
+ks_status drain_rounds(ks_ctx *c, uint32_t rounds, void *h_res, const void *d_res, size_t res_bytes) {
   for (uint32_t k = rounds >= 2 ? rounds - 2 : 0; k < rounds; ++k) {
     const uint32_t q = k & 1u;
     HIPC(c, hipStreamWaitEvent(c->stream, c->ev_res[q], 0));
     HIPC(c, launch_writeback(c->t, c->d_carry + (size_t)q * MAX_P, c->d_pipe + 4 + q, c->stream));
   }
+  if (res_bytes) HIPC(c, hipMemcpyAsync(h_res, d_res, res_bytes, hipMemcpyDeviceToHost, c->stream));
   HIPC(c, hipMemcpyAsync(c->h_start, c->d_start, 4, hipMemcpyDeviceToHost, c->stream));
   HIPC(c, hipStreamSynchronize(c->stream));
+  return KS_OK;
+}
+
+// ------------------------------------------------------------- batches
+
+// A pooled batch with room for n pods and `words` clause words: device
+// buffers are allocated only when no pooled batch is large enough, and
+// outgrown clause buffers are retired to the graveyard.
+ks_status batch_acquire(ks_ctx *c, uint32_t n, size_t words, ks_batch **out) {
+  const uint32_t need = std::max<uint32_t>(n, 1);
+  ks_batch *b = nullptr;
+  {
+    std::lock_guard<std::mutex> g(c->pool_mu);
+    size_t bi = SIZE_MAX;
+    for (size_t i = 0; i < c->pool.size(); ++i)
+      if (c->pool[i]->cap_pods >= need && (bi == SIZE_MAX || c->pool[i]->cap_pods < c->pool[bi]->cap_pods)) bi = i;
+    if (bi != SIZE_MAX) {
+      b = c->pool[bi];
+      c->pool.erase(c->pool.begin() + (long)bi);
+    }
+  }
+  if (!b) {
+    b = new ks_batch();
+    {
+      std::lock_guard<std::mutex> g(c->pool_mu);
+      c->all_batches.push_back(b);
+    }
+    HIPC(c, hipMalloc((void **)&b->d_pods, (size_t)need * sizeof(PodDev)));
+    HIPC(c, hipMalloc((void **)&b->d_pinv, (size_t)need * 2 * sizeof(double)));
+    HIPC(c, hipMalloc((void **)&b->d_results, (size_t)need * sizeof(DevResult)));
+    HIPC(c, hipHostMalloc((void **)&b->h_results, (size_t)need * sizeof(DevResult), hipHostMallocDefault));
+    HIPC(c, hipHostMalloc((void **)&b->h_pods, (size_t)need * sizeof(PodDev), hipHostMallocDefault));
+    HIPC(c, hipHostMalloc((void **)&b->h_pinv, (size_t)need * 2 * sizeof(double), hipHostMallocDefault));
+    b->cap_pods = need;
+  }
+  if (words > b->cap_words) {
+    if (b->d_clauses) c->graveyard.push_back(b->d_clauses);
+    if (b->h_clauses) c->pinned_graveyard.push_back(b->h_clauses);
+    b->d_clauses = nullptr;
+    b->h_clauses = nullptr;
+    b->cap_words = std::max<size_t>(words, std::max<size_t>(2 * b->cap_words, 4096));
+    HIPC(c, hipMalloc((void **)&b->d_clauses, b->cap_words * 8));
+    HIPC(c, hipHostMalloc((void **)&b->h_clauses, b->cap_words * 8, hipHostMallocDefault));
+  }
+  b->n = 0;
+  b->queued = b->done = false;
+  b->run_status = KS_OK;
+  b->run_err.clear();
+  *out = b;
+  return KS_OK;
+}
+
+void batch_release(ks_ctx *c, ks_batch *b) {
+  std::lock_guard<std::mutex> g(c->pool_mu);
+  b->queued = b->done = false;
+  c->pool.push_back(b);
+}
+
+// Compiled batch (pinned host copies) -> device, on the scheduler stream.
+ks_status upload_batch(ks_ctx *c, ks_batch *b) {
+  const size_t np = std::max<uint32_t>(b->n, 1);
+  HIPC(c, hipMemcpyAsync(b->d_pods, b->h_pods, np * sizeof(PodDev), hipMemcpyHostToDevice, c->stream));
+  HIPC(c, hipMemcpyAsync(b->d_pinv, b->h_pinv, np * 2 * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  HIPC(c, hipMemcpyAsync(b->d_clauses, b->h_clauses, b->n_words * 8, hipMemcpyHostToDevice, c->stream));
+  HIPC(c, hipMemsetAsync(b->d_results, 0, np * sizeof(DevResult), c->stream));
+  b->uploaded = true;
+  return KS_OK;
+}
+
+// Run a prepared batch to completion on the scheduler streams; the results
+// land in the batch's pinned host buffer.
+ks_status run_batch(ks_ctx *c, ks_batch *b) {
+  if (b->dict_version != c->dict_version)
+    return c->fail(KS_ERR_STALE, "batch compiled against taint dictionary / node image set v%u, cache is at v%u",
+                   b->dict_version, c->dict_version);
+  if (b->names_version && b->names_version != c->names_version)
+    return c->fail(KS_ERR_STALE, "batch resolved node names before the node set changed");
+  if (c->cfg.world_size > 1 && !c->comm) return c->fail(KS_ERR_COMM, "world_size > 1 but ks_comm_init not called");
+  if (c->comm && c->S != c->cfg.world_size)
+    return c->fail(KS_ERR_INVALID, "RCCL sharding needs one shard per rank (virtual_shards must be 1)");
+  HIPC(c, hipSetDevice(c->cfg.device));
+  ks_status st0;
+  {
+    // label words of nodes that gained dictionary bits since the last upload
+    // (bits of this batch or a later-prepared one: a superset is harmless)
+    std::lock_guard<std::mutex> g(c->mu);
+    if ((st0 = upload_dirty_ext(c, c->xm))) return st0;
+  }
+  if (!b->uploaded && (st0 = upload_batch(c, b))) return st0;
+  HIPC(c, hipMemsetAsync(c->d_start, 0, 4, c->stream));
+  uint32_t host_start = 0;
+  while (host_start < b->n) {
+    // Assume full rounds (an early stop costs the speculated round after it)
+    // and check; each pipeline run resolves at least one pod.
+    const uint32_t remaining = b->n - host_start;
+    uint32_t rounds = (remaining + c->P - 1) / c->P;
+    rounds = std::min<uint32_t>(rounds, 64);
+    for (uint32_t r = 0; r < rounds; ++r) {
+      ks_status st = enqueue_round(c, b, r);
+      if (st) return st;
+    }
+    // results of every pod this pipeline run can resolve, behind its last round
+    const uint32_t hi = std::min<uint32_t>(b->n, host_start + rounds * c->P);
+    ks_status st = drain_rounds(c, rounds, b->h_results + host_start, b->d_results + host_start,
+                                (size_t)(hi - host_start) * sizeof(DevResult));
+    if (st) return st;
+    if (*c->h_start <= host_start) return c->fail(KS_ERR_DEVICE, "no progress in scheduling rounds");
+    host_start = *c->h_start;
+  }
+  if (c->timing) {
+    ks_status st = collect_timing(c);
+    if (st) return st;
+  }
+  return KS_OK;
+}
+
+void worker_main(ks_ctx *c) {
+  (void)hipSetDevice(c->cfg.device);
+  std::unique_lock<std::mutex> lk(c->qmu);
+  for (;;) {
+    c->qcv.wait(lk, [&] { return c->stop || !c->queue.empty(); });
+    if (c->queue.empty()) return;  // stop requested, nothing queued
+    ks_batch *b = c->queue.front();
+    c->queue.pop_front();
+    lk.unlock();
+    const ks_status st = run_batch(c, b);
+    std::string e;
+    if (st) {
+      std::lock_guard<std::mutex> g(c->err_mu);
+      e = c->err;
+    }
+    lk.lock();
+    b->run_status = st;
+    b->run_err = e;
+    b->done = true;
+    c->inflight--;
+    c->dcv.notify_all();
+  }
+}
+
+// Every ABI call except prepare / submit / wait / results / free first lets
+// the submitted batches finish (they own the scheduler streams and the table).
+ks_status drain_async(ks_ctx *c) {
+  std::unique_lock<std::mutex> lk(c->qmu);
+  c->dcv.wait(lk, [&] { return c->inflight == 0; });
   return KS_OK;
 }
 
@@ -999,6 +1346,7 @@ void ks_config_default(ks_config *cfg) {
   cfg->weight_taint = 3;
   cfg->weight_affinity = 2;
   cfg->weight_image = 1;
+  cfg->percentage_of_nodes_to_score = 100;
 }
 
 int32_t ks_abi_version(void) { return KSCHED_ABI_VERSION; }
@@ -1026,6 +1374,9 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
   // weights are small non-negative integers (the kernels add them in 32 bits)
   for (int32_t w : {cfg->weight_fit, cfg->weight_balanced, cfg->weight_taint, cfg->weight_affinity, cfg->weight_image})
     if (w < 0 || w > 10000) return KS_ERR_INVALID;
+  // percentageOfNodesToScore (ksched.h): only 100 (every node) is modelled
+  if (cfg->percentage_of_nodes_to_score < 0 || cfg->percentage_of_nodes_to_score > 100) return KS_ERR_INVALID;
+  if (cfg->percentage_of_nodes_to_score != 100) return KS_ERR_UNSUPPORTED;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return KS_ERR_DEVICE;
   if (cfg->device < 0 || cfg->device >= ndev) return KS_ERR_DEVICE;
@@ -1075,6 +1426,7 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
       HIPC(x, hipStreamCreateWithPriority(&x->rstream, hipStreamNonBlocking, hi));
       HIPC(x, hipStreamCreateWithPriority(&x->sstream, hipStreamNonBlocking, hi));
     }
+    x->xm.st = x->stream;
     {  // KS_VALUE_SYNC=0: cross-stream hand-offs by event waits instead
       int can = 0;
       (void)hipDeviceGetAttribute(&can, hipDeviceAttributeCanUseStreamWaitValue, cfg->device);
@@ -1152,6 +1504,13 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
 
 void ks_close(ks_ctx *c) {
   if (!c) return;
+  drain_async(c);
+  {
+    std::lock_guard<std::mutex> g(c->qmu);
+    c->stop = true;
+    c->qcv.notify_all();
+  }
+  if (c->worker.joinable()) c->worker.join();
   (void)hipSetDevice(c->cfg.device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->rstream) (void)hipStreamSynchronize(c->rstream);
@@ -1164,8 +1523,17 @@ void ks_close(ks_ctx *c) {
   for (void *b : bufs)
     if (b) (void)hipFree(b);
   if (c->h_start) (void)hipHostFree(c->h_start);
-  if (c->pin) (void)hipHostFree(c->pin);
-  if (c->dscr) (void)hipFree(c->dscr);
+  if (c->xm.pin) (void)hipHostFree(c->xm.pin);
+  if (c->xm.dscr) (void)hipFree(c->xm.dscr);
+  for (void *g : c->graveyard) (void)hipFree(g);
+  for (void *g : c->pinned_graveyard) (void)hipHostFree(g);
+  for (ks_batch *b : c->all_batches) {
+    for (void *p : {(void *)b->d_pods, (void *)b->d_pinv, (void *)b->d_clauses, (void *)b->d_results})
+      if (p) (void)hipFree(p);
+    for (void *p : {(void *)b->h_results, (void *)b->h_pods, (void *)b->h_pinv, (void *)b->h_clauses})
+      if (p) (void)hipHostFree(p);
+    delete b;
+  }
   for (auto &pr : c->ev_sweep) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
   for (auto &pr : c->ev_resolve) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
   for (auto e : c->ev_pool) (void)hipEventDestroy(e);
@@ -1183,6 +1551,7 @@ void ks_close(ks_ctx *c) {
 
 ks_status ks_nodes_upsert(ks_ctx *c, const ks_node *nodes, const uint32_t *slots, uint32_t n) {
   if (!c || (n && (!nodes || !slots))) return KS_ERR_INVALID;
+  if (ks_status dst_ = drain_async(c)) return dst_;
   HIPC(c, hipSetDevice(c->cfg.device));
   // Events are applied in order; a slot named twice in one call ends in its
   // last state (one device row per distinct slot, so the scatter is race-free).
@@ -1221,11 +1590,23 @@ ks_status ks_nodes_upsert(ks_ctx *c, const ks_node *nodes, const uint32_t *slots
     const uint32_t slot = slots[i];
     HostNode &h = c->nodes[slot];
     const bool is_new = !h.present;
-    if (!is_new) c->name_slot.erase(h.name);  // key_nodes entries are re-validated lazily
-    else c->n_present++;
+    const uint32_t nid = c->intern(s.name);
+    if (is_new || h.name != nid) c->names_version++;
+    if (!is_new) {
+      c->name_slot.erase(h.name);  // key_nodes entries are re-validated lazily
+      node_images_ref(c, h, -1);
+    } else {
+      c->n_present++;
+    }
     h.present = true;
-    h.name = c->intern(s.name);
+    h.name = nid;
     c->name_slot[h.name] = slot;
+    h.images.clear();
+    for (uint32_t k = 0; k < s.n_images; ++k)
+      if (s.images && s.images[k] && s.images[k][0]) h.images.push_back(normalized_image(s.images[k]));
+    std::sort(h.images.begin(), h.images.end());
+    h.images.erase(std::unique(h.images.begin(), h.images.end()), h.images.end());
+    if (node_images_ref(c, h, +1)) grew = true;  // a prepared pod's image may now be present
     h.acpu = s.alloc_milli_cpu;
     h.amem = s.alloc_memory;
     h.apods = s.alloc_pods;
@@ -1314,6 +1695,7 @@ ks_status ks_nodes_upsert(ks_ctx *c, const ks_node *nodes, const uint32_t *slots
 
 ks_status ks_nodes_delete(ks_ctx *c, const uint32_t *slots, uint32_t n) {
   if (!c || (n && !slots)) return KS_ERR_INVALID;
+  if (ks_status dst_ = drain_async(c)) return dst_;
   HIPC(c, hipSetDevice(c->cfg.device));
   std::vector<uint32_t> pos(n);
   std::vector<int64_t> core((size_t)n * 8, 0);
@@ -1322,7 +1704,9 @@ ks_status ks_nodes_delete(ks_ctx *c, const uint32_t *slots, uint32_t n) {
       return c->fail(KS_ERR_NOT_FOUND, "slot %u not present", slots[i]);
     HostNode &h = c->nodes[slots[i]];
     c->name_slot.erase(h.name);
+    c->names_version++;
     prefer_mask_ref(c, h.prefer, -1);
+    node_images_ref(c, h, -1);
     h = HostNode();
     c->n_present--;
     pos[i] = c->slot_pos[slots[i]];
@@ -1343,10 +1727,12 @@ ks_status ks_nodes_delete(ks_ctx *c, const uint32_t *slots, uint32_t n) {
 
 static ks_status pods_delta(ks_ctx *c, const ks_pod *pods, const uint32_t *slots, uint32_t n, int sign) {
   if (!c || (n && (!pods || !slots))) return KS_ERR_INVALID;
+  if (ks_status dst_ = drain_async(c)) return dst_;
   if (!n) return KS_OK;
   HIPC(c, hipSetDevice(c->cfg.device));
   std::vector<uint32_t> pos(n);
   std::vector<int64_t> d((size_t)n * 5);
+  int64_t aff = 0;
   for (uint32_t i = 0; i < n; ++i) {
     if (slots[i] >= c->cap || !c->nodes[slots[i]].present)
       return c->fail(KS_ERR_NOT_FOUND, "slot %u not present", slots[i]);
@@ -1354,6 +1740,7 @@ static ks_status pods_delta(ks_ctx *c, const ks_pod *pods, const uint32_t *slots
     ks_status st;
     if ((st = pod_requests(pods[i], false, &rc, &rm)) || (st = pod_requests(pods[i], true, &zc, &zm)))
       return c->fail(st, "pod requests a resource other than cpu/memory");
+    if (pods[i].unmodelled & KS_UNMODELLED_POD_AFFINITY) aff += sign;
     pos[i] = c->slot_pos[slots[i]];
     int64_t *x = &d[(size_t)i * 5];
     x[0] = sign * rc;
@@ -1369,6 +1756,7 @@ static ks_status pods_delta(ks_ctx *c, const ks_pod *pods, const uint32_t *slots
   int64_t *d_d = dscratch<int64_t>(c, d.size());
   if ((st = h2d(c, d_pos, pos.data(), (size_t)n * 4)) || (st = h2d(c, d_d, d.data(), d.size() * 8))) return st;
   HIPC(c, launch_apply_deltas(c->t, d_pos, d_d, n, c->stream));
+  c->affinity_pods += aff;
   return xfer_sync(c);
 }
 
@@ -1416,100 +1804,142 @@ ks_status ks_events_apply(ks_ctx *c, const ks_event *ev, uint32_t n) {
   return KS_OK;
 }
 
+ks_status ks_pods_check(ks_ctx *c, const ks_pod *pods, uint32_t n, ks_status *status) {
+  if (!c || (n && (!pods || !status))) return KS_ERR_INVALID;
+  std::lock_guard<std::mutex> g(c->mu);
+  ks_status first = KS_OK;
+  std::string first_err;
+  for (uint32_t i = 0; i < n; ++i) {
+    PodDev d;
+    ClauseBuf cl;
+    status[i] = compile_pod(c, pods[i], d, cl);
+    if (status[i] && !first) {
+      first = status[i];
+      std::lock_guard<std::mutex> ge(c->err_mu);
+      first_err = "pod " + std::to_string(i) + ": " + c->err;
+    }
+  }
+  if (first) c->fail(first, "%s", first_err.c_str());
+  return first;
+}
+
 ks_status ks_batch_prepare(ks_ctx *c, const ks_pod *pods, uint32_t n, ks_batch **out) {
   if (!c || !out || (n && !pods)) return KS_ERR_INVALID;
   *out = nullptr;
   HIPC(c, hipSetDevice(c->cfg.device));
-  auto b = std::make_unique<ks_batch>();
-  b->n = n;
   std::vector<PodDev> dev(std::max<uint32_t>(n, 1));
   ClauseBuf cl;
-  for (uint32_t i = 0; i < n; ++i) {
-    ks_status st = compile_pod(c, pods[i], dev[i], cl);
-    if (st) return st;
-    if (dev[i].flags & PF_EXT) b->ext = true;
-    if (dev[i].flags & (PF_TT | PF_NA)) b->norm = true;
+  bool ext = false, norm = false;
+  uint32_t dict_v, names_v;
+  ks_status st;
+  {
+    // compile against the host dictionaries (the worker reads t.lw and the
+    // dirty label rows under mu)
+    std::lock_guard<std::mutex> g(c->mu);
+    c->compile_used_names = false;
+    for (uint32_t i = 0; i < n; ++i) {
+      if ((st = compile_pod(c, pods[i], dev[i], cl))) return st;
+      if (dev[i].flags & PF_EXT) ext = true;
+      if (dev[i].flags & (PF_TT | PF_NA)) norm = true;
+    }
+    dict_v = c->dict_version;
+    names_v = c->compile_used_names ? c->names_version : 0;
   }
-  if (b->norm) b->ext = true;
-  ks_status st = upload_dirty_ext(c);
-  if (st) return st;
-  b->dict_version = c->dict_version;
+  if (norm) ext = true;
   if (cl.w.empty()) cl.add(CK_FALSE, 0, 0, nullptr, 0);
-  HIPC(c, hipMalloc((void **)&b->d_pods, dev.size() * sizeof(PodDev)));
-  std::vector<double> pinv(2 * dev.size(), 0.0);
+  ks_batch *b = nullptr;
+  if ((st = batch_acquire(c, n, cl.w.size(), &b))) return st;
+  b->n = n;
+  b->ext = ext;
+  b->norm = norm;
+  b->dict_version = dict_v;
+  b->names_version = names_v;
+  b->n_words = cl.w.size();
+  std::memcpy(b->h_pods, dev.data(), dev.size() * sizeof(PodDev));
   for (size_t i = 0; i < dev.size(); ++i) {
-    pinv[2 * i] = dev[i].tt_guess ? 1.0 / (double)dev[i].tt_guess : 0.0;
-    pinv[2 * i + 1] = dev[i].na_guess ? 1.0 / (double)dev[i].na_guess : 0.0;
+    b->h_pinv[2 * i] = dev[i].tt_guess ? 1.0 / (double)dev[i].tt_guess : 0.0;
+    b->h_pinv[2 * i + 1] = dev[i].na_guess ? 1.0 / (double)dev[i].na_guess : 0.0;
   }
-  HIPC(c, hipMalloc((void **)&b->d_pinv, pinv.size() * sizeof(double)));
-  HIPC(c, hipMalloc((void **)&b->d_clauses, cl.w.size() * 8));
-  HIPC(c, hipMalloc((void **)&b->d_results, std::max<uint32_t>(n, 1) * sizeof(DevResult)));
-  const size_t bytes = dev.size() * sizeof(PodDev) + pinv.size() * sizeof(double) + cl.w.size() * 8 + 1024;
-  if ((st = xfer_begin(c, bytes, 0)) || (st = h2d(c, b->d_pods, dev.data(), dev.size() * sizeof(PodDev))) ||
-      (st = h2d(c, b->d_pinv, pinv.data(), pinv.size() * sizeof(double))) ||
-      (st = h2d(c, b->d_clauses, cl.w.data(), cl.w.size() * 8)))
-    return st;
-  HIPC(c, hipMemsetAsync(b->d_results, 0, std::max<uint32_t>(n, 1) * sizeof(DevResult), c->stream));
-  if ((st = xfer_sync(c))) return st;
-  *out = b.release();
+  std::memcpy(b->h_clauses, cl.w.data(), cl.w.size() * 8);
+  b->uploaded = false;
+  bool idle;
+  {
+    std::lock_guard<std::mutex> g(c->qmu);
+    idle = c->inflight == 0;
+  }
+  if (idle) {
+    // nothing in flight: upload now, so the run starts with every input
+    // resident in HBM (the scheduler stream is ours until ks_batch_submit)
+    {
+      std::lock_guard<std::mutex> g(c->mu);
+      if ((st = upload_dirty_ext(c, c->xm))) {
+        batch_release(c, b);
+        return st;
+      }
+    }
+    if ((st = upload_batch(c, b)) || (st = xfer_sync(c))) {
+      batch_release(c, b);
+      return st;
+    }
+  }
+  *out = b;
   return KS_OK;
 }
 
 ks_status ks_batch_run(ks_ctx *c, ks_batch *b) {
   if (!c || !b) return KS_ERR_INVALID;
-  if (b->dict_version != c->dict_version)
-    return c->fail(KS_ERR_STALE, "batch compiled against taint dictionary v%u, cache is at v%u", b->dict_version,
-                   c->dict_version);
-  if (c->cfg.world_size > 1 && !c->comm) return c->fail(KS_ERR_COMM, "world_size > 1 but ks_comm_init not called");
-  if (c->comm && c->S != c->cfg.world_size)
-    return c->fail(KS_ERR_INVALID, "RCCL sharding needs one shard per rank (virtual_shards must be 1)");
-  HIPC(c, hipSetDevice(c->cfg.device));
-  HIPC(c, hipMemsetAsync(c->d_start, 0, 4, c->stream));
-  uint32_t host_start = 0;
-  while (host_start < b->n) {
-    // Assume full rounds (an early stop costs the speculated round after it)
-    // and check; each pipeline run resolves at least one pod.
-    const uint32_t remaining = b->n - host_start;
-    uint32_t rounds = (remaining + c->P - 1) / c->P;
-    rounds = std::min<uint32_t>(rounds, 64);
-    for (uint32_t r = 0; r < rounds; ++r) {
-      ks_status st = enqueue_round(c, b, r);
-      if (st) return st;
-    }
-    ks_status st = drain_rounds(c, rounds);
-    if (st) return st;
-    if (*c->h_start <= host_start) return c->fail(KS_ERR_DEVICE, "no progress in scheduling rounds");
-    host_start = *c->h_start;
-  }
-  if (c->timing) {
-    ks_status st = collect_timing(c);
-    if (st) return st;
-  }
+  ks_status st = drain_async(c);
+  if (st) return st;
+  return run_batch(c, b);
+}
+
+ks_status ks_batch_submit(ks_ctx *c, ks_batch *b) {
+  if (!c || !b) return KS_ERR_INVALID;
+  std::lock_guard<std::mutex> g(c->qmu);
+  if (b->queued && !b->done) return c->fail(KS_ERR_INVALID, "batch already submitted");
+  if (!c->worker.joinable()) c->worker = std::thread(worker_main, c);
+  b->queued = true;
+  b->done = false;
+  b->run_status = KS_OK;
+  b->run_err.clear();
+  c->queue.push_back(b);
+  c->inflight++;
+  c->qcv.notify_one();
   return KS_OK;
+}
+
+ks_status ks_batch_wait(ks_ctx *c, ks_batch *b) {
+  if (!c || !b) return KS_ERR_INVALID;
+  std::unique_lock<std::mutex> lk(c->qmu);
+  if (!b->queued) return c->fail(KS_ERR_INVALID, "batch was not submitted");
+  c->dcv.wait(lk, [&] { return b->done; });
+  if (b->run_status) c->fail(b->run_status, "%s", b->run_err.c_str());
+  return b->run_status;
 }
 
 ks_status ks_batch_results(ks_ctx *c, const ks_batch *b, ks_result *out) {
   if (!c || !b || (b->n && !out)) return KS_ERR_INVALID;
   static_assert(sizeof(ks_result) == sizeof(DevResult), "result layout");
-  HIPC(c, hipSetDevice(c->cfg.device));
-  const size_t bytes = (size_t)b->n * sizeof(DevResult) + 1024;
-  ks_status st;
-  if ((st = xfer_begin(c, bytes, 0)) || (st = d2h(c, out, b->d_results, (size_t)b->n * sizeof(DevResult))) ||
-      (st = xfer_sync(c)))
-    return st;
-  for (uint32_t i = 0; i < b->n; ++i)
-    if (out[i].status == KS_POD_SCHEDULED) c->stats.pods_scheduled++;
+  {
+    std::lock_guard<std::mutex> g(c->qmu);
+    if (b->queued && !b->done) return c->fail(KS_ERR_INVALID, "batch still running (ks_batch_wait first)");
+  }
+  // the run copied the results into the batch's pinned buffer
+  std::memcpy(out, b->h_results, (size_t)b->n * sizeof(DevResult));
+  uint64_t sched = 0;
+  for (uint32_t i = 0; i < b->n; ++i) sched += out[i].status == KS_POD_SCHEDULED;
+  c->stats.pods_scheduled += sched;
   return KS_OK;
 }
 
 void ks_batch_free(ks_ctx *c, ks_batch *b) {
   if (!b) return;
-  if (c) (void)hipSetDevice(c->cfg.device);
-  if (b->d_pods) (void)hipFree(b->d_pods);
-  if (b->d_pinv) (void)hipFree(b->d_pinv);
-  if (b->d_clauses) (void)hipFree(b->d_clauses);
-  if (b->d_results) (void)hipFree(b->d_results);
-  delete b;
+  if (!c) return;  // pooled buffers belong to the context (ks_close frees them)
+  {
+    std::unique_lock<std::mutex> lk(c->qmu);
+    if (b->queued) c->dcv.wait(lk, [&] { return b->done; });
+  }
+  batch_release(c, b);
 }
 
 ks_status ks_schedule(ks_ctx *c, const ks_pod *pods, uint32_t n, ks_result *out) {
@@ -1524,12 +1954,16 @@ ks_status ks_schedule(ks_ctx *c, const ks_pod *pods, uint32_t n, ks_result *out)
 
 ks_status ks_plugin_scores(ks_ctx *c, const ks_pod *pod, ks_node_score *out) {
   if (!c || !pod || !out) return KS_ERR_INVALID;
+  if (ks_status dst_ = drain_async(c)) return dst_;
   HIPC(c, hipSetDevice(c->cfg.device));
   PodDev d;
   ClauseBuf cl;
-  ks_status st = compile_pod(c, *pod, d, cl);
-  if (st) return st;
-  if ((st = upload_dirty_ext(c))) return st;
+  ks_status st;
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    if ((st = compile_pod(c, *pod, d, cl))) return st;
+    if ((st = upload_dirty_ext(c, c->xm))) return st;
+  }
   if (cl.w.empty()) cl.add(CK_FALSE, 0, 0, nullptr, 0);
   DumpArgs a{};
   a.t = c->t;
@@ -1571,6 +2005,7 @@ ks_status ks_plugin_scores(ks_ctx *c, const ks_pod *pod, ks_node_score *out) {
 
 ks_status ks_node_states(ks_ctx *c, const uint32_t *slots, uint32_t n, ks_node_state *out) {
   if (!c || (n && (!slots || !out))) return KS_ERR_INVALID;
+  if (ks_status dst_ = drain_async(c)) return dst_;
   if (!n) return KS_OK;
   HIPC(c, hipSetDevice(c->cfg.device));
   std::vector<uint32_t> pos(n);
@@ -1614,6 +2049,7 @@ ks_status ks_comm_unique_id(uint8_t out[KS_COMM_ID_BYTES]) {
 
 ks_status ks_comm_init(ks_ctx *c, const uint8_t id[KS_COMM_ID_BYTES]) {
   if (!c || !id) return KS_ERR_INVALID;
+  if (ks_status dst_ = drain_async(c)) return dst_;
   HIPC(c, hipSetDevice(c->cfg.device));
   ncclUniqueId uid;
   std::memcpy(&uid, id, sizeof uid);
@@ -1623,6 +2059,7 @@ ks_status ks_comm_init(ks_ctx *c, const uint8_t id[KS_COMM_ID_BYTES]) {
 
 ks_status ks_comm_allreduce_max(ks_ctx *c, double *values, uint32_t n) {
   if (!c || (n && !values)) return KS_ERR_INVALID;
+  if (ks_status dst_ = drain_async(c)) return dst_;
   if (!c->comm) return c->fail(KS_ERR_COMM, "ks_comm_init not called");
   HIPC(c, hipSetDevice(c->cfg.device));
   ks_status st = xfer_begin(c, 2 * (size_t)n * 8 + 1024, (size_t)n * 8 + 1024);
@@ -1643,6 +2080,7 @@ static ks_status read_counters(ks_ctx *c, uint64_t out[4]) {
 
 ks_status ks_get_stats(ks_ctx *c, ks_stats *out) {
   if (!c || !out) return KS_ERR_INVALID;
+  if (ks_status dst_ = drain_async(c)) return dst_;
   uint64_t k[4];
   ks_status st = read_counters(c, k);
   if (st) return st;
@@ -1668,6 +2106,7 @@ ks_status ks_get_stats(ks_ctx *c, ks_stats *out) {
 
 ks_status ks_reset_stats(ks_ctx *c) {
   if (!c) return KS_ERR_INVALID;
+  if (ks_status dst_ = drain_async(c)) return dst_;
   c->stats = ks_stats{};
   c->sweeps_issued = 0;
   return read_counters(c, c->counters_base);
@@ -1675,6 +2114,7 @@ ks_status ks_reset_stats(ks_ctx *c) {
 
 ks_status ks_debug_counters(ks_ctx *c, uint64_t out[16]) {
   if (!c || !out) return KS_ERR_INVALID;
+  if (ks_status dst_ = drain_async(c)) return dst_;
   HIPC(c, hipSetDevice(c->cfg.device));
   ks_status st;
   if ((st = xfer_begin(c, 1024, 0)) || (st = d2h(c, out, c->d_counters, 16 * sizeof(uint64_t)))) return st;
@@ -1683,6 +2123,7 @@ ks_status ks_debug_counters(ks_ctx *c, uint64_t out[16]) {
 
 ks_status ks_set_timing(ks_ctx *c, int32_t enabled) {
   if (!c) return KS_ERR_INVALID;
+  if (ks_status dst_ = drain_async(c)) return dst_;
   c->timing = enabled != 0;
   return KS_OK;
 }

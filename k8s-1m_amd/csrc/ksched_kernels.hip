@@ -289,11 +289,25 @@ __device__ __forceinline__ int64_t preferred_raw(const PodDev &p, const uint64_t
   return raw;
 }
 
-// Filter chain in default-profile order; returns ST_FEASIBLE or KS_PLUGIN_*.
+// NodeAffinity PreFilterResult: the node is one of the named ones (one
+// CK_NAME_EQ clause per named node in the pod's prefilter program).
+__device__ __forceinline__ bool prefilter_match(const PodDev &p, const uint64_t *clauses, uint32_t slot) {
+  const uint64_t *c = clauses + (size_t)p.pre_off * CLAUSE_WORDS;
+  bool any = false;
+  for (uint32_t k = 0; k < p.pre_len; ++k, c += CLAUSE_WORDS) any |= (int64_t)slot == (int64_t)c[5];
+  return any;
+}
+
+// Filter chain in default-profile order; returns ST_FEASIBLE, KS_PLUGIN_* or
+// ST_PREFILTERED.  NodeAffinity's PreFilter runs before any Filter: a
+// conflicting name set fails every node at NodeAffinity, a PreFilterResult
+// leaves the nodes outside it unevaluated (schedule_one.go#findNodesThatFitPod).
 template <bool EXT>
 __device__ __forceinline__ int filter(const PodDev &p, const uint64_t *clauses, const NodeRegs &r,
                                       const NodeExt &e) {
   if (EXT && (p.flags & PF_EXT)) {
+    if (p.flags & PF_NA_CONFLICT) return 3;
+    if ((p.flags & PF_PREFILTER) && !prefilter_match(p, clauses, r.slot)) return ST_PREFILTERED;
     const uint64_t untol = e.hard & ~p.tol_hard;
     if (untol & UNSCHED_BIT) return 0;                              // NodeUnschedulable
     if (p.name_slot != -1 && (int64_t)r.slot != (int64_t)p.name_slot) return 1;  // NodeName
@@ -589,10 +603,19 @@ __global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
       f4 = vcount - feas;
     } else {
       // label programs once per pod for the lane's NPL nodes
-      bool aff[NPL];
+      bool aff[NPL], pre[NPL];
       uint32_t praw[NPL];
-      static_for<NPL>([&](auto J) { aff[J] = true; praw[J] = 0u; });
+      static_for<NPL>([&](auto J) { aff[J] = true; pre[J] = true; praw[J] = 0u; });
       if (p.flags & PF_AFF) required_match_n<NPL, LWU>(p, a.clauses, ne, nr, aff);
+      if (p.flags & PF_PREFILTER) {  // rare: pods naming their nodes by metadata.name
+        static_for<NPL>([&](auto J) { pre[J] = false; });
+        const uint64_t *c = a.clauses + (size_t)p.pre_off * CLAUSE_WORDS;
+        for (uint32_t k = 0; k < p.pre_len; ++k, c += CLAUSE_WORDS) {
+          const int64_t x = (int64_t)c[5];
+          static_for<NPL>([&](auto J) { pre[J] |= (int64_t)nr[J].slot == x; });
+        }
+      }
+      const bool conflict = p.flags & PF_NA_CONFLICT;
       if (p.flags & PF_NA) preferred_raw_n<NPL, LWU>(p, a.clauses, ne, nr, praw);
       const double *ip = fix ? a.norm_inv + 2 * r : a.guess_inv + 2 * (size_t)pi;  // RN(1 / max)
       const double inv_tt = (p.flags & PF_TT) ? ip[0] : 0.0;
@@ -616,6 +639,8 @@ __global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
           if (untol) st = 2;
           if (named && (int64_t)nr[j].slot != (int64_t)p.name_slot) st = 1;
           if (untol & UNSCHED_BIT) st = 0;
+          if (conflict) st = 3;
+          if (!pre[j]) st = ST_PREFILTERED;  // not evaluated, no plugin blamed
         }
         if (!valid) st = ST_EMPTY;
         const bool feasible = st == ST_FEASIBLE;
@@ -1771,6 +1796,8 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
             res->feasible_nodes = feasible;
             res->evaluated_nodes = a.evaluated;
             res->flags = (win && feasible == 1) ? 1u : 0u;
+            res->prefiltered = s_pod[r].prefilter_out;
+            res->_pad = 0;
           }
           if (lane > (uint32_t)DSUM_LANE && lane <= (uint32_t)DSUM_LANE + NFILT)
             res->fail_counts[lane - DSUM_LANE - 1] = hfail + (uint32_t)vd;

@@ -39,7 +39,8 @@ class KsNode(C.Structure):
         ("n_labels", C.c_uint32),
         ("n_taints", C.c_uint32),
         ("unschedulable", C.c_uint32),
-        ("_pad", C.c_uint32),
+        ("n_images", C.c_uint32),
+        ("images", C.POINTER(c_char_p)),
     ]
 
 
@@ -49,6 +50,7 @@ class KsContainer(C.Structure):
         ("memory", C.c_int64),
         ("flags", C.c_uint32),
         ("restart_always", C.c_uint32),
+        ("image", c_char_p),
     ]
 
 
@@ -96,13 +98,18 @@ class KsPod(C.Structure):
         ("n_preferred", C.c_uint32),
         ("has_preferred", C.c_uint32),
         ("has_overhead", C.c_uint32),
-        ("_pad", C.c_uint32),
+        ("unmodelled", C.c_uint32),
     ]
 
 
 NUM_FILTER_PLUGINS = 5
+NUM_FAIL_COUNTS = 6  # + KS_FAIL_PREFILTER_RESULT
 # ks_status codes and ks_event kinds (include/ksched.h)
-KS_OK, KS_ERR_INVALID = 0, 1
+KS_OK, KS_ERR_INVALID, KS_ERR_DEVICE, KS_ERR_CAPACITY, KS_ERR_UNSUPPORTED, KS_ERR_RANGE = 0, 1, 2, 3, 4, 5
+KS_ERR_NOT_FOUND, KS_ERR_COMM, KS_ERR_STALE = 6, 7, 8
+# KS_UNMODELLED_* pod feature bits
+UNMODELLED = {"host_ports": 1, "topology_spread": 2, "pod_affinity": 4, "volumes": 8, "nominated_node": 16,
+              "resource_claims": 32}
 KS_EV_POD_ADD, KS_EV_POD_REMOVE, KS_EV_NODE_UPSERT, KS_EV_NODE_DELETE = 0, 1, 2, 3
 
 
@@ -122,8 +129,9 @@ class KsResult(C.Structure):
         ("total_score", C.c_int64),
         ("feasible_nodes", C.c_uint32),
         ("evaluated_nodes", C.c_uint32),
-        ("fail_counts", C.c_uint32 * NUM_FILTER_PLUGINS),
+        ("fail_counts", C.c_uint32 * NUM_FAIL_COUNTS),
         ("flags", C.c_uint32),
+        ("_pad", C.c_uint32),
     ]
 
 
@@ -169,7 +177,7 @@ class KsConfig(C.Structure):
         ("weight_taint", C.c_int32),
         ("weight_affinity", C.c_int32),
         ("weight_image", C.c_int32),
-        ("_pad", C.c_uint32),
+        ("percentage_of_nodes_to_score", C.c_int32),
     ]
 
 
@@ -188,8 +196,8 @@ class KsStats(C.Structure):
 
 # sizes from the C headers (checked in tests/test_abi.py against offsetof via the compiler)
 EXPECTED_SIZES = {
-    "ks_label": 16, "ks_taint": 24, "ks_toleration": 24, "ks_node": 64, "ks_container": 24,
-    "ks_requirement": 24, "ks_term": 24, "ks_preferred_term": 32, "ks_pod": 128, "ks_event": 24, "ks_result": 48,
+    "ks_label": 16, "ks_taint": 24, "ks_toleration": 24, "ks_node": 72, "ks_container": 32,
+    "ks_requirement": 24, "ks_term": 24, "ks_preferred_term": 32, "ks_pod": 128, "ks_event": 24, "ks_result": 56,
     "ks_node_score": 40, "ks_node_state": 56, "ks_config": 56, "ks_stats": 64,
 }
 STRUCTS = {
@@ -203,7 +211,7 @@ STRUCTS = {
 KSCHED_SYMBOLS = [
     "ks_config_default", "ks_open", "ks_close", "ks_last_error", "ks_abi_version", "ks_nodes_upsert",
     "ks_nodes_delete", "ks_pods_add", "ks_pods_remove", "ks_events_apply", "ks_schedule", "ks_batch_prepare", "ks_batch_run",
-    "ks_batch_results", "ks_batch_free", "ks_plugin_scores", "ks_node_states", "ks_comm_unique_id",
+    "ks_batch_results", "ks_batch_free", "ks_batch_submit", "ks_batch_wait", "ks_pods_check", "ks_plugin_scores", "ks_node_states", "ks_comm_unique_id",
     "ks_comm_init", "ks_comm_allreduce_max", "ks_get_stats", "ks_reset_stats", "ks_set_timing",
     "ks_debug_counters",
 ]
@@ -259,6 +267,9 @@ def ksched_lib() -> C.CDLL:
     L.ks_batch_results.argtypes = [vp, vp, P(KsResult)]
     L.ks_batch_free.argtypes = [vp, vp]
     L.ks_batch_free.restype = None
+    L.ks_batch_submit.argtypes = [vp, vp]
+    L.ks_batch_wait.argtypes = [vp, vp]
+    L.ks_pods_check.argtypes = [vp, P(KsPod), C.c_uint32, P(C.c_int32)]
     L.ks_plugin_scores.argtypes = [vp, P(KsPod), P(KsNodeScore)]
     L.ks_node_states.argtypes = [vp, P(C.c_uint32), C.c_uint32, P(KsNodeState)]
     L.ks_comm_unique_id.argtypes = [P(C.c_uint8)]

@@ -314,5 +314,5 @@ def results_to_arrays(raw, n: int):
 
     buf = np.frombuffer(C.string_at(C.addressof(raw), n * C.sizeof(_abi.KsResult)), dtype=np.uint8)
     dt = np.dtype([("node_index", "<i4"), ("status", "<i4"), ("total_score", "<i8"), ("feasible", "<u4"),
-                   ("evaluated", "<u4"), ("fail", "<u4", (5,)), ("flags", "<u4")])
+                   ("evaluated", "<u4"), ("fail", "<u4", (6,)), ("flags", "<u4"), ("_pad", "<u4")])
     return buf.view(dt)

@@ -38,6 +38,7 @@ class Container:
     # resources.requests; an absent key is a MISSING request (not zero)
     requests: Dict[str, int] = field(default_factory=dict)
     restart_policy_always: bool = False  # init containers: sidecar
+    image: str = ""
 
 
 @dataclass
@@ -66,6 +67,7 @@ class Node:
     labels: Dict[str, str] = field(default_factory=dict)
     taints: List[Taint] = field(default_factory=list)
     unschedulable: bool = False
+    images: List[str] = field(default_factory=list)  # status.images[].names, flattened
 
 
 @dataclass
@@ -83,6 +85,8 @@ class Pod:
     preferred: Optional[List[PreferredSchedulingTerm]] = None
     node_name: str = ""
     overhead: Optional[Dict[str, int]] = None
+    # features whose plugins ksched does not model (ksched.h KS_UNMODELLED_*): names from _abi.UNMODELLED
+    unmodelled: List[str] = field(default_factory=list)
 
 
 class Arena:
@@ -104,7 +108,7 @@ class Arena:
         return C.cast(arr, C.POINTER(ctype)), len(items)
 
 
-def _container(c: Container) -> _abi.KsContainer:
+def _container(c: Container, a: "Arena") -> _abi.KsContainer:
     flags = 0
     for k in c.requests:
         if k == "cpu":
@@ -114,7 +118,7 @@ def _container(c: Container) -> _abi.KsContainer:
         else:
             flags |= REQ_HAS_OTHER
     return _abi.KsContainer(c.requests.get("cpu", 0), c.requests.get("memory", 0), flags,
-                            1 if c.restart_policy_always else 0)
+                            1 if c.restart_policy_always else 0, a.s(c.image) if c.image else None)
 
 
 def _requirement(r: NodeSelectorRequirement, a: Arena) -> _abi.KsRequirement:
@@ -132,14 +136,15 @@ def node_to_c(n: Node, a: Arena) -> _abi.KsNode:
     labels, nl = a.array(_abi.KsLabel, [_abi.KsLabel(a.s(k), a.s(v)) for k, v in n.labels.items()])
     taints, nt = a.array(
         _abi.KsTaint, [_abi.KsTaint(a.s(t.key), a.s(t.value), EFFECTS.get(t.effect, 9), 0) for t in n.taints])
+    images, ni = a.array(C.c_char_p, [a.s(i) for i in n.images])
     al = n.allocatable
     return _abi.KsNode(a.s(n.name), al.get("cpu", 0), al.get("memory", 0), al.get("pods", 0), labels, taints,
-                       nl, nt, 1 if n.unschedulable else 0, 0)
+                       nl, nt, 1 if n.unschedulable else 0, ni, images)
 
 
 def pod_to_c(p: Pod, a: Arena) -> _abi.KsPod:
-    cs, ncs = a.array(_abi.KsContainer, [_container(c) for c in p.containers])
-    ics, nics = a.array(_abi.KsContainer, [_container(c) for c in p.init_containers])
+    cs, ncs = a.array(_abi.KsContainer, [_container(c, a) for c in p.containers])
+    ics, nics = a.array(_abi.KsContainer, [_container(c, a) for c in p.init_containers])
     tols, ntol = a.array(_abi.KsToleration, [
         _abi.KsToleration(a.s(t.key), a.s(t.value), TOL_OPS.get(t.operator, 2), EFFECTS.get(t.effect, 9))
         for t in p.tolerations])
@@ -152,7 +157,7 @@ def pod_to_c(p: Pod, a: Arena) -> _abi.KsPod:
         a.s(p.namespace), a.s(p.name), cs, ics, tols, sel, req, pref, a.s(p.node_name),
         ov.get("cpu", 0), ov.get("memory", 0), ncs, nics, ntol, nsel, nreq,
         0 if p.required_terms is None else 1, npref, 0 if p.preferred is None else 1,
-        0 if p.overhead is None else 1, 0)
+        0 if p.overhead is None else 1, sum(_abi.UNMODELLED[u] for u in p.unmodelled))
 
 
 def nodes_array(nodes: List[Node], a: Arena):

@@ -304,6 +304,10 @@ struct PodState {
   std::vector<Requirement> node_selector;
   bool has_required = false;
   std::vector<NodeSelectorTerm> required;  // non-empty terms only
+  // NodeAffinity PreFilter: PreFilterResult.NodeNames (prefilter) or a
+  // conflicting name set (conflict: UnschedulableAndUnresolvable)
+  bool prefilter = false, conflict = false;
+  std::vector<std::string> prefilter_names;  // sorted
   // NodeAffinity PreScore: PreferredSchedulingTerms
   bool has_preferred = false;
   bool preferred_error = false;
@@ -376,6 +380,45 @@ PodState compile_pod(const ks_pod &p) {
     if (is_empty_term(p.required_terms[i])) continue;  // NewLazyErrorNodeSelector
     st.required.push_back(newNodeSelectorTerm(p.required_terms[i]));
   }
+  // nodeaffinity#PreFilter: when every required term carries matchFields
+  // metadata.name In requirements, PreFilterResult.NodeNames = the union over
+  // terms of the intersection of each term's value sets (raw values, before
+  // any parsing); an empty union rejects the pod (errReasonConflict).
+  if (st.has_required && p.n_required_terms > 0) {
+    bool all = true;
+    std::vector<std::string> uni;
+    for (uint32_t i = 0; i < p.n_required_terms && all; ++i) {
+      const ks_term &t = p.required_terms[i];
+      bool have = false;
+      std::vector<std::string> term_names;
+      for (uint32_t k = 0; k < t.n_fields; ++k) {
+        const ks_requirement &r = t.match_fields[k];
+        if (S(r.key) != "metadata.name" || r.op != KS_OP_IN) continue;
+        std::vector<std::string> vs;
+        for (uint32_t v = 0; v < r.n_values; ++v) vs.push_back(S(r.values[v]));
+        if (!have) {
+          term_names = vs;
+          have = true;
+        } else {  // sets.Intersection
+          std::vector<std::string> keep;
+          for (auto &x : term_names)
+            if (std::find(vs.begin(), vs.end(), x) != vs.end()) keep.push_back(x);
+          term_names = keep;
+        }
+      }
+      if (!have) all = false;  // "all nodes are eligible because the terms are ORed"
+      else uni.insert(uni.end(), term_names.begin(), term_names.end());
+    }
+    if (all) {
+      std::sort(uni.begin(), uni.end());
+      uni.erase(std::unique(uni.begin(), uni.end()), uni.end());
+      if (uni.empty()) st.conflict = true;
+      else {
+        st.prefilter = true;
+        st.prefilter_names = uni;
+      }
+    }
+  }
   st.has_preferred = p.has_preferred != 0;
   for (uint32_t i = 0; i < p.n_preferred; ++i) {
     const ks_preferred_term &t = p.preferred[i];
@@ -393,6 +436,13 @@ PodState compile_pod(const ks_pod &p) {
 // non-success status).
 
 int Filter(const PodState &st, const Node &n) {
+  // PreFilter outcome (schedule_one.go#findNodesThatFitPod): a rejecting
+  // NodeAffinity PreFilter gives every node its status; nodes outside the
+  // PreFilterResult get UnschedulableAndUnresolvable with no plugin and no
+  // Filter runs on them (KS_FAIL_PREFILTER_RESULT)
+  if (st.conflict) return KS_PLUGIN_NODE_AFFINITY;
+  if (st.prefilter && !std::binary_search(st.prefilter_names.begin(), st.prefilter_names.end(), n.name))
+    return KS_FAIL_PREFILTER_RESULT;
   // nodeunschedulable#Filter
   if (n.unschedulable &&
       !TolerationsTolerateTaint(st.tolerations,

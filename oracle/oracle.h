@@ -51,7 +51,7 @@ int32_t oracle_node_states(oracle *o, const uint32_t *slots, uint32_t n, ks_node
  * shard's feasible nodes given the global maxima.  commit: AssumePod. */
 typedef struct {
   uint32_t feasible;
-  uint32_t fail_counts[KS_NUM_FILTER_PLUGINS];
+  uint32_t fail_counts[KS_NUM_FAIL_COUNTS]; /* + KS_FAIL_PREFILTER_RESULT */
   int64_t taint_max, affinity_max;
   uint32_t taint_count, affinity_count;
   int32_t error; /* 1 if the pod's PreScore would fail (preferred-term parse error) */

@@ -20,7 +20,7 @@ LIB = ROOT / "oracle" / "_build" / "liboracle.so"
 class ShardPrescore(C.Structure):
     _fields_ = [
         ("feasible", C.c_uint32),
-        ("fail_counts", C.c_uint32 * 5),
+        ("fail_counts", C.c_uint32 * 6),
         ("taint_max", C.c_int64),
         ("affinity_max", C.c_int64),
         ("taint_count", C.c_uint32),

@@ -6,7 +6,7 @@ import numpy as np
 from ksched import _abi
 
 RES_DT = np.dtype([("node_index", "<i4"), ("status", "<i4"), ("total_score", "<i8"), ("feasible", "<u4"),
-                   ("evaluated", "<u4"), ("fail", "<u4", (5,)), ("flags", "<u4")])
+                   ("evaluated", "<u4"), ("fail", "<u4", (6,)), ("flags", "<u4"), ("_pad", "<u4")])
 
 
 def res_array(raw, n):

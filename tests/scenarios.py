@@ -6,7 +6,7 @@ from ksched.objects import (Container, Node, NodeSelectorRequirement as Req, Nod
                             PreferredSchedulingTerm as Pref, Taint, Toleration)
 
 Gi = 1 << 30
-UNSCHED, NAME, TAINT, AFFINITY, FIT = range(5)
+UNSCHED, NAME, TAINT, AFFINITY, FIT, PREFILTER = range(6)
 
 
 def node(name, cpu=32000, mem=256 * Gi, pods=32, labels=None, taints=None, unschedulable=False):
@@ -243,6 +243,48 @@ def wide_label_dictionary():
     exp = [dict(node=0, feasible=6), dict(node=3, feasible=3, fails={AFFINITY: 3}), dict(node=0, feasible=4),
            dict(node=5, feasible=1, fails={AFFINITY: 5}), dict(node=2, feasible=2), dict(node=3, feasible=3),
            dict(node=5, feasible=6)]
+    return nodes, pods, exp
+
+
+@scenario
+def prefilter_result():
+    # NodeAffinity.PreFilter (upstream v1.31 nodeaffinity#PreFilter) with required
+    # terms that all name nodes via matchFields metadata.name In: only the union of
+    # the per-term name intersections is evaluated; every other node is
+    # UnschedulableAndUnresolvable "filtered out by the prefilter result" with no
+    # plugin blamed (fail_counts[5]); an empty union rejects every node at
+    # NodeAffinity.  The PreFilter reads RAW values: a name-In requirement with two
+    # values puts both names in the result, although Filter rejects that term
+    # (parse error: one value required).
+    nodes = [node(f"n{i}", taints=[Taint("t", "", "NoSchedule")] if i == 3 else [],
+                  unschedulable=(i == 4), labels={"zone": "a" if i % 2 else "b"}) for i in range(8)]
+    F = lambda *names: Req("metadata.name", "In", list(names))  # noqa: E731
+    pods = [
+        pod("one", required_terms=[Term(match_fields=[F("n2")])]),
+        pod("two-terms", required_terms=[Term(match_fields=[F("n5")]), Term(match_fields=[F("n1")])]),
+        # tainted / unschedulable named nodes fail their Filter plugins; the rest are prefiltered
+        pod("named-bad", required_terms=[Term(match_fields=[F("n3")]), Term(match_fields=[F("n4")])]),
+        pod("conflict", required_terms=[Term(match_fields=[F("n1"), F("n2")])]),
+        pod("absent", required_terms=[Term(match_fields=[F("nope")])]),
+        # one term without a name field: every node stays eligible (no PreFilterResult)
+        pod("mixed", required_terms=[Term(match_fields=[F("n6")]),
+                                     Term(match_expressions=[Req("zone", "In", ["a"])])]),
+        # two values: PreFilterResult {n6, n7}; the term itself never matches (parse error)
+        pod("two-values", required_terms=[Term(match_fields=[F("n6", "n7")])]),
+        # intersection within a term, label expression on top
+        pod("intersect", required_terms=[Term(match_expressions=[Req("zone", "In", ["a"])],
+                                              match_fields=[F("n7"), F("n7")])]),
+    ]
+    exp = [
+        dict(node=2, feasible=1, fails={PREFILTER: 7}, single=True),
+        dict(node=1, feasible=2, fails={PREFILTER: 6}),
+        dict(node=None, status=1, feasible=0, fails={TAINT: 1, UNSCHED: 1, PREFILTER: 6}),
+        dict(node=None, status=1, feasible=0, fails={AFFINITY: 8, PREFILTER: 0}),
+        dict(node=None, status=1, feasible=0, fails={PREFILTER: 8}),
+        dict(node=1, fails={PREFILTER: 0}),
+        dict(node=None, status=1, feasible=0, fails={AFFINITY: 2, PREFILTER: 6}),
+        dict(node=7, feasible=1, fails={PREFILTER: 7}),
+    ]
     return nodes, pods, exp
 
 

@@ -28,7 +28,7 @@ def test_libksched_exports_every_declared_symbol():
     lib = _abi.ksched_lib()
     for name in declared("ksched.h", "ks_"):
         assert hasattr(lib, name), name
-    assert lib.ks_abi_version() == 1
+    assert lib.ks_abi_version() == 2
 
 
 def test_libksynth_exports_every_declared_symbol():

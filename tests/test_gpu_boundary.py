@@ -1,0 +1,182 @@
+"""The drop-in boundary's admission rules and its asynchronous form (ABI v2).
+
+* Pods carrying a feature whose plugin ksched does not model are refused with
+  KS_ERR_UNSUPPORTED (ks_pods_check names each, ks_batch_prepare fails), never
+  scheduled approximately: host ports (NodePorts), topology spread
+  (PodTopologySpread), pod (anti-)affinity (InterPodAffinity), volumes, a
+  nominated node, resource claims; a container image some node reports
+  (ImageLocality); any batch while a bound pod carries pod (anti-)affinity;
+  percentageOfNodesToScore != 100 at ks_open.
+* A batch that resolved node names goes stale when the node set changes.
+* ks_batch_submit / ks_batch_wait give the results of sequential ks_batch_run
+  calls, with the next batch compiled while the previous one runs.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import pyoracle
+from helpers import assert_results_equal, res_array
+from ksched import Scheduler, _abi, synth
+from ksched.objects import Arena, NodeSelectorRequirement as R, NodeSelectorTerm as T, nodes_array, pods_array
+from scenarios import node, pod
+
+pytestmark = pytest.mark.gpu
+
+
+def small_cluster(s, n=8, images=None):
+    a = Arena()
+    nodes = [node(f"n{i}") for i in range(n)]
+    if images:
+        for i, im in images.items():
+            nodes[i].images = list(im)
+    na, _ = nodes_array(nodes, a)
+    assert s.lib.ks_nodes_upsert(s.ctx, na, (C.c_uint32 * n)(*range(n)), n) == 0
+    return a
+
+
+@pytest.mark.parametrize("feature", sorted(_abi.UNMODELLED))
+def test_unmodelled_feature_is_refused(feature):
+    with Scheduler(8) as s:
+        a = small_cluster(s)
+        pods = [pod("ok", cpu=100), pod("x", cpu=100, unmodelled=[feature]), pod("ok2")]
+        pa, m = pods_array(pods, a)
+        st = (C.c_int32 * m)()
+        assert s.lib.ks_pods_check(s.ctx, pa, m, st) == _abi.KS_ERR_UNSUPPORTED
+        assert list(st) == [0, _abi.KS_ERR_UNSUPPORTED, 0]
+        assert b"pod 1" in s.lib.ks_last_error(s.ctx)
+        out = (_abi.KsResult * m)()
+        assert s.lib.ks_schedule(s.ctx, pa, m, out) == _abi.KS_ERR_UNSUPPORTED
+        # nothing was committed by the refused call
+        assert all(x.pod_count == 0 for x in s.node_states(list(range(8))))
+
+
+def test_image_on_a_node_is_refused():
+    with Scheduler(8) as s:
+        # node 3 reports "busybox" (normalised to busybox:latest) and a tagged image
+        a = small_cluster(s, images={3: ["busybox", "registry.k8s.io/pause:3.9"]})
+        from ksched.objects import Container, Pod
+        ok = Pod("ok", containers=[Container({"cpu": 100}, image="nginx:1.25")])
+        tag = Pod("tag", containers=[Container({"cpu": 100}, image="busybox:latest")])
+        init = Pod("init", init_containers=[Container(image="registry.k8s.io/pause:3.9")],
+                   containers=[Container(image="alpine")])
+        pa, m = pods_array([ok, tag, init], a)
+        st = (C.c_int32 * m)()
+        assert s.lib.ks_pods_check(s.ctx, pa, m, st) == _abi.KS_ERR_UNSUPPORTED
+        assert list(st) == [0, _abi.KS_ERR_UNSUPPORTED, _abi.KS_ERR_UNSUPPORTED]
+        # once the node is gone (deleted), nobody reports the image: admitted
+        assert s.lib.ks_nodes_delete(s.ctx, (C.c_uint32 * 1)(3), 1) == 0
+        assert s.lib.ks_pods_check(s.ctx, pa, m, st) == 0
+
+
+def test_bound_pod_with_pod_affinity_blocks_batches_until_removed():
+    with Scheduler(8) as s:
+        a = small_cluster(s)
+        bound, _ = pods_array([pod("anti", cpu=100, unmodelled=["pod_affinity"])], a)
+        pa, m = pods_array([pod("p", cpu=100)], a)
+        st = (C.c_int32 * 1)()
+        assert s.lib.ks_pods_check(s.ctx, pa, 1, st) == 0
+        assert s.lib.ks_pods_add(s.ctx, bound, (C.c_uint32 * 1)(2), 1) == 0
+        assert s.lib.ks_pods_check(s.ctx, pa, 1, st) == _abi.KS_ERR_UNSUPPORTED
+        assert b"InterPodAffinity" in s.lib.ks_last_error(s.ctx)
+        assert s.lib.ks_pods_remove(s.ctx, bound, (C.c_uint32 * 1)(2), 1) == 0
+        assert s.lib.ks_pods_check(s.ctx, pa, 1, st) == 0
+
+
+@pytest.mark.parametrize("pct,status", [(100, 0), (5, _abi.KS_ERR_UNSUPPORTED), (0, _abi.KS_ERR_UNSUPPORTED),
+                                        (101, _abi.KS_ERR_INVALID)])
+def test_percentage_of_nodes_to_score(pct, status):
+    lib = _abi.ksched_lib()
+    cfg = _abi.KsConfig()
+    lib.ks_config_default(C.byref(cfg))
+    assert cfg.percentage_of_nodes_to_score == 100
+    cfg.node_capacity = 16
+    cfg.percentage_of_nodes_to_score = pct
+    ctx = C.c_void_p()
+    assert lib.ks_open(C.byref(cfg), C.byref(ctx)) == status
+    if status == 0:
+        lib.ks_close(ctx)
+
+
+def test_batch_naming_nodes_goes_stale_when_nodes_change():
+    with Scheduler(16) as s:
+        a = small_cluster(s)
+        named, _ = pods_array([pod("by-name", cpu=100, node_name="n3")], a)
+        plain, _ = pods_array([pod("plain", cpu=100)], a)
+        b1, b2 = s.prepare(named, 1), s.prepare(plain, 1)
+        na, _ = nodes_array([node("n8")], a)
+        assert s.lib.ks_nodes_upsert(s.ctx, na, (C.c_uint32 * 1)(8), 1) == 0  # a new node name
+        assert s.lib.ks_batch_run(s.ctx, b1) == _abi.KS_ERR_STALE
+        assert s.lib.ks_batch_run(s.ctx, b2) == 0  # no name resolved: still valid
+        s.free(b1)
+        s.free(b2)
+
+
+def test_prefilter_counts_nodes_outside_the_result():
+    with Scheduler(8) as s:
+        a = small_cluster(s)
+        p = pod("named", cpu=100, required_terms=[T(match_fields=[R("metadata.name", "In", ["n5", "zz"])])])
+        pa, _ = pods_array([p], a)
+        r = res_array(s.schedule_raw(pa, 1), 1)[0]
+        # both values enter the PreFilterResult; Filter rejects the two-value
+        # term (parse error), so n5 fails NodeAffinity and 7 nodes are prefiltered
+        assert r["status"] == 1 and list(r["fail"]) == [0, 0, 0, 1, 0, 7]
+
+
+def test_async_submit_equals_sequential_runs():
+    n, per, nb = 20_000, 3_000, 5
+    nodes = synth.nodes(synth.LABELED, n, 1)
+    pf = synth.prefill(synth.LABELED, n, 1, 3, 0.5)
+    pods = synth.pods(synth.LABELED, per * nb, 2)
+    out = []
+    for mode in ("sync", "async"):
+        s = Scheduler(n)
+        s.upsert_nodes_raw(nodes.nodes, synth.slot_array(n), n)
+        assert s.lib.ks_pods_add(s.ctx, pf.pods, pf.slot_ptr, pf.n_pods) == 0
+        res = []
+        if mode == "sync":
+            for k in range(nb):
+                b = s.prepare(pods.pods_at(k * per), per)
+                s.run(b)
+                res.append(res_array(s.results(b, per), per))
+                s.free(b)
+        else:
+            # compile batch k+1 while batch k runs; two in flight at a time
+            b = s.prepare(pods.pods_at(0), per)
+            assert s.lib.ks_batch_submit(s.ctx, b) == 0
+            for k in range(nb):
+                nxt = None
+                if k + 1 < nb:
+                    nxt = s.prepare(pods.pods_at((k + 1) * per), per)
+                    assert s.lib.ks_batch_submit(s.ctx, nxt) == 0
+                assert s.lib.ks_batch_wait(s.ctx, b) == 0, s.lib.ks_last_error(s.ctx)
+                res.append(res_array(s.results(b, per), per))
+                s.free(b)
+                b = nxt
+        out.append(np.concatenate(res))
+        s.close()
+    assert np.array_equal(out[0], out[1])
+    # and the oracle agrees on the first batch
+    o = pyoracle.Oracle(n, threads=16)
+    o.upsert(nodes.nodes, synth.slot_array(n), n)
+    o.add_pods(pf.pods, pf.slot_ptr, pf.n_pods)
+    want = res_array(o.schedule(pods.pods, 600), 600)
+    assert np.array_equal(out[1][:600], want)
+
+
+def test_batch_pool_reuses_buffers_and_results_survive_other_runs():
+    with Scheduler(64) as s:
+        a = small_cluster(s, n=64)
+        pa, m = pods_array([pod(f"p{i}", cpu=100 + i) for i in range(40)], a)
+        b1 = s.prepare(pa, m)
+        s.run(b1)
+        r1 = res_array(s.results(b1, m), m)
+        b2 = s.prepare(pa, 20)  # a second batch while b1 is held
+        s.run(b2)
+        assert np.array_equal(res_array(s.results(b1, m), m), r1)  # b1's results unchanged
+        s.free(b2)
+        b3 = s.prepare(pa, 10)  # reuses b2's buffers
+        assert b3.value == b2.value
+        s.free(b3)
+        s.free(b1)

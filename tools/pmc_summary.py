@@ -1,87 +1,120 @@
 #!/usr/bin/env python3
-"""Summarise the rocprofv3 --pmc passes of tools/pmc.sh into profiles/<tag>_pmc.json.
+"""Summarise the rocprofv3 --pmc passes of tools/pmc.sh into profiles/pmc/<key>.json.
 
-    python tools/pmc_summary.py gpurun_out/pmc_r1e --tag r1e --out profiles/pmc_sweep.json
+    python tools/pmc_summary.py gpurun_out/pmc_r2c3 --tag r2c3 --out-dir profiles/pmc
 
-Per kernel (averaged over its dispatches): every collected counter, plus for
-the sweep kernel the quantities bench.py's roofline reports:
+<key> is the bench configuration (bench.py's extra.pmc_key, read from the
+passes' own bench lines), and the file records the kernel-source hash it was
+measured on (bench.py's roofline ignores a summary whose hash differs).
 
-* ``hbm_bytes_per_sweep_launch`` = 2 x FETCH_SIZE x 1024 + WRITE_SIZE x 1024.
-  FETCH_SIZE / WRITE_SIZE are in KB.  The x2 is MI355X_MICROARCH.md's gfx950
-  correction (FETCH_SIZE tallies 128-B fabric reads at 64 B); the sweep's
-  loads are 8-B and 4-B per lane, outside the guide's calibrated 16-B case, so
-  the script also checks it against the kernel's own known read volume
-  (pod groups x node-table bytes), see ``fetch_calibration``.  These are L2
-  memory-side bytes: Infinity-Cache hits are counted, so the figure is an
-  upper bound on true HBM traffic (the 56 MB node table stays L3-resident).
-* ``valu_lane_ops_per_eval`` = SQ_INSTS_VALU x 64 / evaluations per launch.
-* ``lds_bank_conflict_ratio`` = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE.
+Main sweep dispatches only: the sweep kernel's dispatches with the largest
+grid (FIX-mode re-sweeps of flagged pods use the same kernel on a smaller
+grid).  Per evaluation (pod x node, evaluations per launch from the bench line):
+
+* ``valu_wave_instr_per_eval`` = SQ_INSTS_VALU / evaluations (x 64 = lane-ops);
+* ``hbm_bytes_per_eval`` = (2 x FETCH_SIZE + WRITE_SIZE) x 1024 / evaluations:
+  FETCH_SIZE / WRITE_SIZE are in KB; the x2 is MI355X_MICROARCH.md's gfx950
+  correction (FETCH_SIZE tallies 128-B fabric reads at 64 B).  These are L2
+  memory-side bytes (Infinity-Cache hits counted): an upper bound on HBM bytes;
+* ``valu_busy`` = SQ_ACTIVE_INST_VALU x 4 / (SQ_BUSY_CYCLES x 4 SIMDs ... ) is
+  reported as SQ_ACTIVE_INST_VALU / (GRBM_GUI_ACTIVE / 8 XCDs x 256 CUs x 4 SIMDs / 4)
+  (quad-cycles of VALU execution per SIMD quad-cycle);
+* ``lds_bank_conflict_ratio`` = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE;
 * ``clock_ghz`` = GRBM_GUI_ACTIVE / 8 XCDs / kernel duration.
 """
 import argparse
 import csv
+import hashlib
 import json
 from collections import defaultdict
 from pathlib import Path
 
+ROOT = Path(__file__).resolve().parent.parent
 SWEEP = "sweep_kernel"
+KERNEL_SOURCES = ["k8s-1m_amd/csrc/ksched_kernels.hip", "k8s-1m_amd/csrc/ksched_dev.hpp",
+                  "k8s-1m_amd/csrc/ksched_kernels.hpp", "k8s-1m_amd/Makefile"]
+
+
+def kernel_src_hash() -> str:
+    h = hashlib.sha256()
+    for f in KERNEL_SOURCES:
+        h.update((ROOT / f).read_bytes())
+    return h.hexdigest()[:16]
 
 
 def load(dirpath: Path):
-    per = defaultdict(lambda: defaultdict(list))  # kernel -> counter -> values
-    dur = defaultdict(list)
+    """kernel -> grid -> counter -> [values]; kernel -> grid -> [durations ms]."""
+    per = defaultdict(lambda: defaultdict(lambda: defaultdict(list)))
+    dur = defaultdict(lambda: defaultdict(list))
     for f in sorted(dirpath.rglob("*counter_collection.csv")):
         seen = set()
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                k = row["Kernel_Name"]
-                per[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
-                key = (row["Dispatch_Id"], k)
+                k, g = row["Kernel_Name"], int(row["Grid_Size"])
+                per[k][g][row["Counter_Name"]].append(float(row["Counter_Value"]))
+                key = (f, row["Dispatch_Id"])
                 if key not in seen:
                     seen.add(key)
-                    dur[k].append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-6)
+                    dur[k][g].append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-6)
     return per, dur
+
+
+def bench_line(dirpath: Path):
+    for f in sorted(dirpath.glob("p*.json")):
+        for ln in f.read_text().splitlines():
+            ln = ln.strip()
+            if ln.startswith("{"):
+                return json.loads(ln)
+    raise SystemExit(f"no bench line under {dirpath}")
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
     ap.add_argument("--tag", required=True)
-    ap.add_argument("--out", required=True)
-    ap.add_argument("--evals-per-launch", type=float, default=256 * 1_000_000,
-                    help="(pod, node) evaluations per sweep launch of the profiled bench")
-    ap.add_argument("--table-bytes", type=float, default=56 * 1_000_000, help="node-table bytes one pod group reads")
-    ap.add_argument("--pod-groups", type=int, default=9, help="pod groups per sweep launch (host geometry)")
+    ap.add_argument("--out-dir", required=True)
     a = ap.parse_args()
-    per, dur = load(Path(a.dir))
+    d = Path(a.dir)
+    line = bench_line(d)
+    key = line["extra"]["pmc_key"]
+    evals = line["roofline"]["evals_per_launch"]
+    per, dur = load(d)
     kernels = {}
-    for k, ctrs in per.items():
+    for k, grids in per.items():
         name = k.split("(")[0]
+        g = max(grids)  # the largest grid of this kernel
+        ctrs = grids[g]
         kernels[name] = {c: sum(v) / len(v) for c, v in ctrs.items()}
+        kernels[name]["grid"] = g
         kernels[name]["dispatches"] = max(len(v) for v in ctrs.values())
-        d = dur.get(k, [])
-        kernels[name]["avg_ms_under_pmc"] = sum(d) / len(d) if d else None
+        ds = dur[k][g]
+        kernels[name]["avg_ms_under_pmc"] = sum(ds) / len(ds) if ds else None
+    out = {"tag": a.tag, "key": key, "kernel_src": kernel_src_hash(), "evals_per_launch": evals,
+           "workload": line["config"]["workload"],
+           "source": f"rocprofv3 --pmc passes (tools/pmc.sh), {a.dir}", "kernels": kernels}
     sweep = {n: v for n, v in kernels.items() if SWEEP in n}
-    out = {"tag": a.tag, "source": f"rocprofv3 --pmc passes (tools/pmc.sh), {a.dir}", "kernels": kernels}
     if sweep:
         name, s = max(sweep.items(), key=lambda kv: kv[1].get("dispatches", 0))
-        fetch = s.get("FETCH_SIZE")
-        write = s.get("WRITE_SIZE")
-        if fetch is not None and write is not None:
-            out["hbm_bytes_per_sweep_launch"] = round(2 * fetch * 1024 + write * 1024)
-            out["fetch_calibration"] = {
-                "expected_read_bytes": a.pod_groups * a.table_bytes,
-                "fetch_size_x2_bytes": 2 * fetch * 1024,
-                "ratio": round(2 * fetch * 1024 / (a.pod_groups * a.table_bytes), 4),
-            }
+        out["sweep_kernel"] = name
         if "SQ_INSTS_VALU" in s:
-            out["valu_lane_ops_per_eval"] = round(s["SQ_INSTS_VALU"] * 64 / a.evals_per_launch, 2)
+            out["valu_wave_instr_per_eval"] = s["SQ_INSTS_VALU"] / evals
+            out["valu_lane_ops_per_eval"] = round(s["SQ_INSTS_VALU"] * 64 / evals, 2)
+        if "SQ_INSTS_SALU" in s:
+            out["salu_instr_per_valu_instr"] = round(s["SQ_INSTS_SALU"] / max(1.0, s.get("SQ_INSTS_VALU", 0)), 4)
+        if "FETCH_SIZE" in s and "WRITE_SIZE" in s:
+            b = 2 * s["FETCH_SIZE"] * 1024 + s["WRITE_SIZE"] * 1024
+            out["hbm_bytes_per_launch"] = round(b)
+            out["hbm_bytes_per_eval"] = b / evals
         if "SQ_LDS_BANK_CONFLICT" in s and s.get("SQ_LDS_IDX_ACTIVE"):
             out["lds_bank_conflict_ratio"] = round(s["SQ_LDS_BANK_CONFLICT"] / s["SQ_LDS_IDX_ACTIVE"], 5)
         if "GRBM_GUI_ACTIVE" in s and s.get("avg_ms_under_pmc"):
             out["clock_ghz"] = round(s["GRBM_GUI_ACTIVE"] / 8 / (s["avg_ms_under_pmc"] * 1e-3) / 1e9, 3)
-        out["sweep_kernel"] = name
-    Path(a.out).write_text(json.dumps(out, indent=1, sort_keys=True) + "\n")
+        if "SQ_ACTIVE_INST_VALU" in s and s.get("GRBM_GUI_ACTIVE"):
+            simd_quads = s["GRBM_GUI_ACTIVE"] / 8 * 256 * 4 / 4
+            out["valu_busy"] = round(s["SQ_ACTIVE_INST_VALU"] / simd_quads, 4)
+    od = Path(a.out_dir)
+    od.mkdir(parents=True, exist_ok=True)
+    (od / f"{key}.json").write_text(json.dumps(out, indent=1, sort_keys=True) + "\n")
     print(json.dumps({k: v for k, v in out.items() if k != "kernels"}, indent=1))
 
 
