@@ -456,6 +456,11 @@ def roofline(args, st, world):
         r["achieved"] = round(wi * 64 / launch_s / 1e12, 2)
         r["frac"] = round(wi / launch_s / VALU_PEAK_WAVE_INSTR, 4)
         r["valu_lane_ops_per_eval"] = round(pmc["valu_wave_instr_per_eval"] * 64, 2)
+        if pmc.get("valu_issue_cycles_per_eval") is not None:
+            # the same against SIMD cycles with binary64 instructions at their half rate
+            cyc = pmc["valu_issue_cycles_per_eval"] * evals_per_launch
+            r["valu_mix_frac"] = round(cyc / (launch_s * 2.4e9 * 1024), 4)
+            r["valu_f64_share"] = pmc.get("valu_f64_share")
         if pmc.get("valu_busy") is not None:
             r["valu_busy"] = pmc["valu_busy"]  # SQ_ACTIVE_INST_VALU share of SIMD cycles (f64 counted at its cost)
         if pmc.get("hbm_bytes_per_eval") is not None:

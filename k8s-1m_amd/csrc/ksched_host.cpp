@@ -1365,7 +1365,7 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
   c->P = cfg->pods_per_round ? cfg->pods_per_round : 256;
   if (c->P > (uint32_t)MAX_P) return KS_ERR_INVALID;
   c->K = cfg->topk ? cfg->topk : c->P;
-  if (c->K > 256) return KS_ERR_INVALID;  // resolve: one listed candidate per list thread
+  if (c->K > (uint32_t)MAX_K) return KS_ERR_INVALID;  // resolve: two listed candidates per list-wave lane
   const uint32_t world = cfg->world_size ? cfg->world_size : 1;
   c->cfg.world_size = world;
   if (cfg->rank >= world) return KS_ERR_INVALID;

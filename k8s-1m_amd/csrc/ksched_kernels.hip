@@ -1076,7 +1076,7 @@ __global__ __launch_bounds__(256) void gather_cand_kernel(RoundArgs a) {
 // per-plugin failure / normaliser-at-max counts are corrected by their status
 // change.  Afterwards a pod's list, bound and counts are exact for the state
 // resolve k starts from, so the resolve re-scores only its own commits.
-constexpr int PATCH_THREADS = 256;
+constexpr int PATCH_THREADS = 512;
 constexpr int PHASH = 1024;
 static_assert(PATCH_THREADS >= MAX_P && PATCH_THREADS >= MAX_K, "one thread per carried node / list entry");
 
@@ -1356,7 +1356,8 @@ constexpr uint32_t NONE32 = 0xFFFFFFFFu;
 constexpr int KS_PLUGIN_FIT_IDX = 4;  // filter status of NodeResourcesFit (KS_PLUGIN_FIT)
 constexpr int ROW_PIECES = sizeof(CandRow) / 16;
 constexpr int EXT_PIECES = sizeof(CandExt) / 16;
-static_assert(RES_LIST_WAVES * WAVE >= MAX_K && RES_OWN_WAVES * WAVE >= MAX_P, "resolve roles");
+static_assert(2 * RES_LIST_WAVES * WAVE >= MAX_K && RES_OWN_WAVES * WAVE >= MAX_P, "resolve roles");
+constexpr int LIST_SPAN = 2 * WAVE;  // list entries per list wave: lane l holds entries l and l + 64
 static_assert(DSUM_LANE >= NCAND && DSUM_LANE + NFILT + 3 <= WAVE, "decider lanes");
 
 // A node as the resolve carries it: its row (live state) and the round-start
@@ -1591,13 +1592,13 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
   constexpr int32_t LIST_WAIT = 2 * LIST_DMA;  // vmcnt(N): expcnt / lgkmcnt fields at their max
   static_assert(LIST_WAIT < 64, "vmcnt field");
   const uint32_t lw = wid;
-  auto dma_keys = [&](uint32_t pod) {  // keys of list entries [64 lw, 64 lw + 64) of pod -> s_keys
+  auto dma_keys = [&](uint32_t pod) {  // keys of list entries [128 lw, 128 lw + 128) of pod -> s_keys
     const uint32_t p = min(pod, nround - 1);
-    if (lane < 32) {  // entries past K: any in-record address (never read back)
-      const uint32_t e = 64 * lw + 2 * lane;
-      const uint64_t *src = a.frec + (size_t)p * RW + REC_HDR_WORDS + (e < a.K ? e : 0u);
-      __builtin_amdgcn_global_load_lds((gvoid_t *)src, (lvoid_t *)&s_keys[pod % KSLOTS][64 * lw], 16, 0, 0);
-    }
+    // every wave issues it (list_wait counts LIST_DMA loads per iteration);
+    // entries past K: any in-record address (never read back)
+    const uint32_t e = LIST_SPAN * lw + 2 * lane;
+    const uint64_t *src = a.frec + (size_t)p * RW + REC_HDR_WORDS + (e < a.K ? e : 0u);
+    __builtin_amdgcn_global_load_lds((gvoid_t *)src, (lvoid_t *)&s_keys[pod % KSLOTS][LIST_SPAN * lw], 16, 0, 0);
   };
   auto lds_key = [&](uint32_t slot, uint32_t t) -> uint64_t {
     uint64_t v;
@@ -1610,28 +1611,44 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
   auto list_select = [&](uint32_t pod) {
     const bool real = pod < nround;
     const uint32_t p = real ? pod : nround - 1;
-    const uint64_t k = lds_key(pod % KSLOTS, rtid);
     const uint32_t nk = s_hdr[p].nkeys;
-    bool unmod = false, hempty = false;
-    const uint32_t slot = 0xFFFFFFFFu - (uint32_t)k;
-    if (real && k != 0 && rtid < nk) {
-      uint32_t h = rhash(slot);
-      unmod = true;
-      hempty = s_hkey[h] == 0;
-      while (s_hkey[h] != 0) {
-        if (s_hkey[h] == slot + 1) { unmod = false; break; }
-        h = (h + 1) & (RHASH - 1);
+    // lane l checks entries e0 = 128 lw + l and e1 = e0 + 64 against the
+    // modified-slot hash; list order within the wave is e0's 64, then e1's
+    const uint32_t e0 = LIST_SPAN * lw + lane, e1 = e0 + WAVE;
+    const uint64_t k0 = e0 < a.K ? lds_key(pod % KSLOTS, e0) : 0ull;
+    const uint64_t k1 = e1 < a.K ? lds_key(pod % KSLOTS, e1) : 0ull;
+    auto probe = [&](uint64_t k, uint32_t e, bool &unmod, bool &hempty) {
+      unmod = hempty = false;
+      const uint32_t slot = 0xFFFFFFFFu - (uint32_t)k;
+      if (real && k != 0 && e < nk) {
+        uint32_t h = rhash(slot);
+        unmod = true;
+        hempty = s_hkey[h] == 0;
+        while (s_hkey[h] != 0) {
+          if (s_hkey[h] == slot + 1) { unmod = false; break; }
+          h = (h + 1) & (RHASH - 1);
+        }
       }
-    }
-    const uint64_t ub = __ballot(unmod), hb = __ballot(hempty);
-    const uint32_t nsel = min((uint32_t)__popcll(ub), (uint32_t)LSEL);
-    // lane c < LSEL takes the c-th unmodified entry
-    uint64_t m = ub;
-    for (uint32_t j = 0; j < lane && j < (uint32_t)LSEL; ++j) m &= m - 1;
-    const uint32_t te = m ? (uint32_t)__builtin_ctzll(m) : 0u;
-    const uint64_t tk = (uint64_t)__shfl((long long)k, (int)te, WAVE);
+    };
+    bool u0, h0, u1 = false, h1 = false;
+    probe(k0, e0, u0, h0);
+    if (LIST_SPAN * lw + WAVE < nk) probe(k1, e1, u1, h1);  // wave-uniform: second half only when listed
+    const uint64_t ub0 = __ballot(u0), hb0 = __ballot(h0), ub1 = __ballot(u1), hb1 = __ballot(h1);
+    const uint32_t n0 = (uint32_t)__popcll(ub0);
+    const uint32_t nsel = min(n0 + (uint32_t)__popcll(ub1), (uint32_t)LSEL);
+    // lane c < LSEL takes the c-th unmodified entry of the wave's 128
+    const bool second = lane >= n0;
+    uint64_t m = second ? ub1 : ub0;
+    const uint32_t skip = second ? lane - n0 : lane;
+    for (uint32_t j = 0; j < skip && j < (uint32_t)LSEL; ++j) m &= m - 1;
+    const uint32_t tb = m ? (uint32_t)__builtin_ctzll(m) : 0u;
+    const uint64_t tk0 = (uint64_t)__shfl((long long)k0, (int)tb, WAVE);
+    const uint64_t tk1 = (uint64_t)__shfl((long long)k1, (int)tb, WAVE);
+    const uint64_t tk = second ? tk1 : tk0;
+    const uint32_t te = tb + (second ? (uint32_t)WAVE : 0u);
+    const uint64_t hb = second ? hb1 : hb0;
     if (lane < (uint32_t)LSEL) {
-      const uint32_t t = 64 * lw + te;
+      const uint32_t t = LIST_SPAN * lw + te;
       const uint4 *row = (const uint4 *)(a.crow + (size_t)p * a.K + (lane < nsel ? t : 0u));
 #pragma unroll
       for (int j = 0; j < ROW_PIECES; ++j)
@@ -1646,7 +1663,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
       if (real) {
         s_lkey[pod % RSLOTS][LSEL * lw + lane] = lane < nsel ? tk : 0ull;
         // bit 16: the entry's home hash bucket was empty when selected
-        s_lidx[pod % RSLOTS][LSEL * lw + lane] = lane < nsel ? t | (uint32_t)((hb >> te) & 1u) << 16 : NONE32;
+        s_lidx[pod % RSLOTS][LSEL * lw + lane] = lane < nsel ? t | (uint32_t)((hb >> tb) & 1u) << 16 : NONE32;
       }
     }
   };

@@ -9,7 +9,7 @@ namespace ks {
 
 constexpr int MAX_PG = 64;    // pods per sweep block (LDS wave records)
 constexpr int MAX_P = 256;    // pods per round (resolve stages the round in LDS)
-constexpr int MAX_K = 256;    // candidates per pod record (one list thread each in the resolve)
+constexpr int MAX_K = 512;    // candidates per pod record (two list entries per list-wave lane in the resolve)
 constexpr uint32_t FIX_NONE = 0xFFFFFFFFu;  // fix_list tail
 
 struct RoundArgs {

@@ -141,3 +141,11 @@ def test_kwok_1m_requestless_replay():
 def test_kwok_1m_c1_pods_replay():
     r, dbg = run_fullsize(synth.KWOK, synth.pods(synth.KWOK, BATCH, 2), prefill=False)
     assert (r["status"] == 0).all()
+
+
+def test_kwok_1m_c1_pods_k512_replay():
+    # the kwok bench geometry: 512 candidates per pod, so a round's lists
+    # survive the previous round's commits to identical nodes
+    r, dbg = run_fullsize(synth.KWOK, synth.pods(synth.KWOK, BATCH, 2), prefill=False, topk=512)
+    assert (r["status"] == 0).all()
+    assert dbg[3] * 20 < dbg[0], f"wasted speculative rounds {dbg[3]} of {dbg[0]}"

@@ -66,12 +66,20 @@ def test_labeled_taints_affinity():
     s.close()
 
 
-@pytest.mark.parametrize("P,K", [(16, 4), (64, 8), (1, 1), (256, 256), (200, 256)])
+@pytest.mark.parametrize("P,K", [(16, 4), (64, 8), (1, 1), (256, 256), (200, 256), (256, 512), (128, 300)])
 def test_round_shapes(P, K):
     # tiny candidate lists force early round ends; results must not change
     s, o, got, want, sg, sw, _ = run_both(synth.HETERO, 1500, synth.HETERO, 2000, prefill=7,
                                           pods_per_round=P, topk=K)
     check(got, want, 2000, sg, sw, f"P={P} K={K}")
+    s.close()
+
+
+@pytest.mark.parametrize("K", [256, 512])
+def test_labeled_long_lists(K):
+    # EXT resolve with both halves of every list wave's 128 entries in use
+    s, o, got, want, sg, sw, _ = run_both(synth.LABELED, 2500, synth.LABELED, 2500, seeds=(14, 15), topk=K)
+    check(got, want, 2500, sg, sw, f"labeled K={K}")
     s.close()
 
 

@@ -109,6 +109,17 @@ def main():
             out["lds_bank_conflict_ratio"] = round(s["SQ_LDS_BANK_CONFLICT"] / s["SQ_LDS_IDX_ACTIVE"], 5)
         if "GRBM_GUI_ACTIVE" in s and s.get("avg_ms_under_pmc"):
             out["clock_ghz"] = round(s["GRBM_GUI_ACTIVE"] / 8 / (s["avg_ms_under_pmc"] * 1e-3) / 1e9, 3)
+        f64 = [s.get(c) for c in ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64",
+                                  "SQ_INSTS_VALU_TRANS_F64")]
+        if all(v is not None for v in f64) and s.get("SQ_INSTS_VALU"):
+            n64 = sum(f64)
+            out["valu_f64_share"] = round(n64 / s["SQ_INSTS_VALU"], 4)
+            # SIMD issue cycles per wave instruction: 2 (32 lanes/cycle), 4 for
+            # binary64 (half rate: MI355X FP64 vector peak is half the FP32 one)
+            out["valu_issue_cycles_per_eval"] = (2 * (s["SQ_INSTS_VALU"] - n64) + 4 * n64) / evals
+            for c in ("SQ_INSTS_VALU_INT32", "SQ_INSTS_VALU_INT64", "SQ_INSTS_VALU_CVT"):
+                if c in s:
+                    out[c.lower() + "_share"] = round(s[c] / s["SQ_INSTS_VALU"], 4)
         if "SQ_ACTIVE_INST_VALU" in s and s.get("GRBM_GUI_ACTIVE"):
             simd_quads = s["GRBM_GUI_ACTIVE"] / 8 * 256 * 4 / 4
             out["valu_busy"] = round(s["SQ_ACTIVE_INST_VALU"] / simd_quads, 4)
