@@ -62,11 +62,13 @@ sys.path.insert(0, str(ROOT / "k8s-1m_amd"))
 B_NODE = 56  # node-row bytes per (pod, node) evaluation, resource-only
 B_NODE_LABELED = 96  # ... with label / taint bitsets (C4)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-# VALU issue peak: 256 CUs x 4 SIMDs x one wave64 instruction per 2 cycles x
-# 2.4 GHz (MI355X_MICROARCH.md: "issues each VALU instruction over 2 cycles";
-# max clock 2400 MHz) = 1.229e12 wave-instructions/s = 78.6e12 lane-ops/s.
-# binary64 instructions occupy the SIMD twice as long, so a mix with f64 peaks lower.
-VALU_PEAK_WAVE_INSTR = 256 * 4 * 0.5 * 2.4e9
+# VALU issue peak: a wave64 VALU instruction occupies a 16-lane SIMD for 4
+# cycles (MI355X FP64 vector peak 78.6 TFLOP/s = 256 CUs x 4 SIMDs x 16 lanes
+# x 2 FLOP x 2.4 GHz; only packed FP32 doubles that), and the sweep's PMC pass
+# measures SQ_ACTIVE_INST_VALU (quad-cycles) / SQ_INSTS_VALU = 1.06, i.e. 4.25
+# cycles per instruction: 256 x 4 SIMDs x 2.4 GHz / 4 = 6.14e11 wave64
+# instructions/s = 39.3e12 lane-ops/s.
+VALU_PEAK_WAVE_INSTR = 256 * 4 * 2.4e9 / 4
 REF_SCHEDULE_ONE_US = 560.0  # README.adoc:786 (per pod per shard, ~195 nodes evaluated)
 KERNEL_SOURCES = ["k8s-1m_amd/csrc/ksched_kernels.hip", "k8s-1m_amd/csrc/ksched_dev.hpp",
                   "k8s-1m_amd/csrc/ksched_kernels.hpp", "k8s-1m_amd/Makefile"]
@@ -456,13 +458,11 @@ def roofline(args, st, world):
         r["achieved"] = round(wi * 64 / launch_s / 1e12, 2)
         r["frac"] = round(wi / launch_s / VALU_PEAK_WAVE_INSTR, 4)
         r["valu_lane_ops_per_eval"] = round(pmc["valu_wave_instr_per_eval"] * 64, 2)
-        if pmc.get("valu_issue_cycles_per_eval") is not None:
-            # the same against SIMD cycles with binary64 instructions at their half rate
-            cyc = pmc["valu_issue_cycles_per_eval"] * evals_per_launch
-            r["valu_mix_frac"] = round(cyc / (launch_s * 2.4e9 * 1024), 4)
-            r["valu_f64_share"] = pmc.get("valu_f64_share")
+        for k in ("valu_cycles_per_instr", "valu_f64_share", "clock_ghz"):
+            if pmc.get(k) is not None:
+                r[k] = pmc[k]
         if pmc.get("valu_busy") is not None:
-            r["valu_busy"] = pmc["valu_busy"]  # SQ_ACTIVE_INST_VALU share of SIMD cycles (f64 counted at its cost)
+            r["valu_busy"] = pmc["valu_busy"]  # SQ_ACTIVE_INST_VALU share of SIMD quad-cycles
         if pmc.get("hbm_bytes_per_eval") is not None:
             traffic = pmc["hbm_bytes_per_eval"] * evals_per_launch
             r["traffic"] = int(traffic)

@@ -79,36 +79,40 @@ struct alignas(16) PodDev {
   uint64_t tol_prefer;       // prefer-taint bits tolerated by "" / PreferNoSchedule tolerations
   uint32_t flags;
   int32_t name_slot;         // spec.nodeName: -1 unset, -2 names no node, else slot
-  uint32_t req_off, req_len; // required program (clauses) in the clause buffer
-  uint32_t pref_off, pref_len;
-  uint32_t n_req_terms;      // OR terms after the mandatory nodeSelector group
+  uint32_t req_off, req_len; // required program: word offset in the label-program buffer, terms (OR)
+  uint32_t pref_off, pref_len;  // preferred program: word offset, terms (weighted sum)
+  uint32_t n_req_terms;      // required terms emitted (diagnostic)
   // Normalising-plugin maxima the sweep scores with (PF_TT / PF_NA): the host's
   // guess of max raw over feasible nodes.  The merge measures the true maxima;
   // pods whose guess was wrong are re-swept with them (norm_check, fix sweep).
   uint32_t tt_guess, na_guess;
-  // NodeAffinity PreFilterResult (PF_PREFILTER): one CK_NAME_EQ clause per
-  // named node, OR-ed; prefilter_out = present nodes outside it (host count)
+  // NodeAffinity PreFilterResult (PF_PREFILTER): pre_len slot words at
+  // pre_off; prefilter_out = present nodes outside it (host count)
   uint32_t pre_off, pre_len;
   uint32_t prefilter_out;
 };
 static_assert(sizeof(PodDev) == 128, "PodDev layout");
 
-// A clause is one label-selector requirement, 6 x u64:
-//   w0 = kind | num_col << 8 | term << 16 | (uint64)weight << 32
-//   w1..w4 = LW mask words (ANY / NONE: the pair / key bits; GT / LT: the
-//            key's numeric-valid bit), w5 = GT / LT operand or NAME_* slot.
-// term 0 = nodeSelector (AND); terms >= 1 = required terms (OR of ANDs) or,
-// in the preferred program, preferred terms (sum of weights of matching terms).
-enum ClauseKind : uint32_t {
-  CK_ANY = 0,     // In / Exists: any mask bit present
-  CK_NONE = 1,    // NotIn / DoesNotExist: no mask bit present
-  CK_GT = 2,      // numeric label > value
-  CK_LT = 3,      // numeric label < value
-  CK_NAME_EQ = 4, // metadata.name In  (w5 = slot, or -1 = no such node)
-  CK_NAME_NE = 5, // metadata.name NotIn
-  CK_FALSE = 6,   // term with parse errors: never matches
-};
-constexpr int CLAUSE_WORDS = 6;
+// Label programs.  A pod's required node affinity is an OR of TERMS and its
+// preferred affinity a weighted sum of TERMS; each term is compiled on the
+// host from one NodeSelectorTerm (the pod's nodeSelector merged into every
+// required term), as fixed-form masks over the node's label bitset:
+//   w0         n_groups | n_num << 8 | n_name << 16 | (uint64)weight << 32
+//   must[LW]   bits the node must carry (In with one value, Exists, the
+//              nodeSelector's pairs, the numeric-valid bit of a Gt / Lt key)
+//   mf[LW]     must | forbid (NotIn values, DoesNotExist keys): the node
+//              passes the pair / key requirements iff (lab & mf) == must
+//   groups     n_groups x LW words (In with several values): lab & g != 0
+//   num        n_num x 2 words: col | op << 8 (TO_GT / TO_LT), int64 operand
+//   name       n_name x 2 words: TO_NAME_IN / TO_NAME_NOT_IN, slot
+//              (matchFields metadata.name; -1 = the name is no node's)
+// The PreFilterResult program (PF_PREFILTER) is a plain list of slots.
+constexpr int TERM_HDR_WORDS = 1 + 2 * LW;
+enum TermOp : uint32_t { TO_GT = 0, TO_LT = 1, TO_NAME_IN = 0, TO_NAME_NOT_IN = 1 };
+__host__ __device__ inline uint32_t term_words(uint64_t w0) {
+  const uint32_t ng = (uint32_t)w0 & 0xFF, nn = ((uint32_t)w0 >> 8) & 0xFF, nm = ((uint32_t)w0 >> 16) & 0xFF;
+  return TERM_HDR_WORDS + ng * LW + 2 * (nn + nm);
+}
 
 // ----------------------------------------------------------- round records
 // Per (pod-in-round, sweep block): best keys of the block + bound + counts.

@@ -14,6 +14,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <array>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -566,31 +567,47 @@ ks_status pod_requests(const ks_pod &p, bool non_missing, int64_t *cpu, int64_t 
   return KS_OK;
 }
 
-struct ClauseBuf {
+// Label-program words of one batch (ksched_dev.hpp: terms, PreFilterResult slots).
+struct ProgBuf {
   std::vector<uint64_t> w;
-  uint32_t count() const { return (uint32_t)(w.size() / CLAUSE_WORDS); }
-  void add(uint32_t kind, uint32_t term, int32_t weight, const uint64_t mask[LW], uint64_t operand,
-           uint32_t col = 0) {
-    w.push_back((uint64_t)kind | ((uint64_t)col << 8) | ((uint64_t)term << 16) | ((uint64_t)(uint32_t)weight << 32));
-    for (int k = 0; k < LW; ++k) w.push_back(mask ? mask[k] : 0);
-    w.push_back(operand);
-  }
+  uint32_t size() const { return (uint32_t)w.size(); }
 };
 
 inline void set_bit(uint64_t m[LW], uint32_t b) { m[b >> 6] |= 1ull << (b & 63); }
 
-// newNodeSelectorTerm -> clauses.  Returns false on a parse error (the term
+// One NodeSelectorTerm as fixed-form masks (ksched_dev.hpp).
+struct TermBuild {
+  uint64_t must[LW] = {}, forbid[LW] = {};
+  std::vector<std::array<uint64_t, LW>> groups;
+  std::vector<std::pair<uint64_t, uint64_t>> nums, names;
+  // a pair / key both required and forbidden: the term matches no node
+  bool contradictory() const {
+    for (int k = 0; k < LW; ++k)
+      if (must[k] & forbid[k]) return true;
+    return false;
+  }
+  void emit(ProgBuf &out, int32_t weight) const {
+    out.w.push_back((uint64_t)groups.size() | ((uint64_t)nums.size() << 8) | ((uint64_t)names.size() << 16) |
+                    ((uint64_t)(uint32_t)weight << 32));
+    for (int k = 0; k < LW; ++k) out.w.push_back(must[k]);
+    for (int k = 0; k < LW; ++k) out.w.push_back(must[k] | forbid[k]);
+    for (auto &g : groups) out.w.insert(out.w.end(), g.begin(), g.end());
+    for (auto &x : nums) { out.w.push_back(x.first); out.w.push_back(x.second); }
+    for (auto &x : names) { out.w.push_back(x.first); out.w.push_back(x.second); }
+  }
+};
+
+// newNodeSelectorTerm -> TermBuild.  Returns false on a parse error (the term
 // then matches nothing in a required selector; a preferred term's PreScore
 // fails).  Capacity / unsupported errors propagate through *st.
-bool compile_term(ks_ctx *c, const ks_term &t, uint32_t term, int32_t weight, ClauseBuf &out, ks_status *st) {
-  ClauseBuf tmp;
-  bool ok = true;
-  for (uint32_t i = 0; i < t.n_expressions && ok; ++i) {
+bool compile_term(ks_ctx *c, const ks_term &t, TermBuild &tb, ks_status *st) {
+  for (uint32_t i = 0; i < t.n_expressions; ++i) {
     const ks_requirement &e = t.match_expressions[i];
     const std::string key = str(e.key);
     std::vector<std::string> vals;
     for (uint32_t k = 0; k < e.n_values; ++k) vals.push_back(str(e.values[k]));
     // labels.NewRequirement validation
+    bool ok;
     switch (e.op) {
       case KS_OP_IN:
       case KS_OP_NOT_IN: ok = !vals.empty(); break;
@@ -606,52 +623,58 @@ bool compile_term(ks_ctx *c, const ks_term &t, uint32_t term, int32_t weight, Cl
     }
     for (auto &v : vals) ok = ok && label_value_ok(v);
     ok = ok && qualified_name_ok(key);
-    if (!ok) break;
+    if (!ok) return false;
     const uint32_t kid = c->intern(e.key);
-    uint64_t mask[LW] = {};
     uint32_t bit;
     switch (e.op) {
-      case KS_OP_IN:
-      case KS_OP_NOT_IN:
+      case KS_OP_IN: {  // one value: a required pair; several: any of the pairs
+        std::array<uint64_t, LW> g{};
         for (auto &v : vals) {
           if ((*st = get_pair_bit(c, kid, c->intern(v.c_str()), &bit))) return false;
-          set_bit(mask, bit);
+          set_bit(g.data(), bit);
         }
-        tmp.add(e.op == KS_OP_IN ? CK_ANY : CK_NONE, term, weight, mask, 0);
+        int nb = 0;
+        for (int k = 0; k < LW; ++k) nb += __builtin_popcountll(g[k]);
+        if (nb == 1) {
+          for (int k = 0; k < LW; ++k) tb.must[k] |= g[k];
+        } else {
+          tb.groups.push_back(g);
+        }
+        break;
+      }
+      case KS_OP_NOT_IN:  // no listed pair (true when the key is absent)
+        for (auto &v : vals) {
+          if ((*st = get_pair_bit(c, kid, c->intern(v.c_str()), &bit))) return false;
+          set_bit(tb.forbid, bit);
+        }
         break;
       case KS_OP_EXISTS:
       case KS_OP_DOES_NOT_EXIST:
         if ((*st = get_key_bit(c, kid, &bit))) return false;
-        set_bit(mask, bit);
-        tmp.add(e.op == KS_OP_EXISTS ? CK_ANY : CK_NONE, term, weight, mask, 0);
+        set_bit(e.op == KS_OP_EXISTS ? tb.must : tb.forbid, bit);
         break;
-      default: {  // Gt / Lt
+      default: {  // Gt / Lt: the label parses as an int64 (valid bit) and compares
         NumCol nc;
         if ((*st = get_num_col(c, kid, &nc))) return false;
-        set_bit(mask, nc.valid_bit);
+        set_bit(tb.must, nc.valid_bit);
         int64_t x = 0;
         parse_int64(vals[0], &x);
-        tmp.add(e.op == KS_OP_GT ? CK_GT : CK_LT, term, weight, mask, (uint64_t)x, nc.col);
+        tb.nums.emplace_back((uint64_t)nc.col | ((uint64_t)(e.op == KS_OP_GT ? TO_GT : TO_LT) << 8), (uint64_t)x);
       }
     }
   }
-  for (uint32_t i = 0; i < t.n_fields && ok; ++i) {  // nodeSelectorRequirementsAsFieldSelector
+  for (uint32_t i = 0; i < t.n_fields; ++i) {  // nodeSelectorRequirementsAsFieldSelector
     const ks_requirement &e = t.match_fields[i];
-    if (str(e.key) != "metadata.name" || e.n_values != 1 || (e.op != KS_OP_IN && e.op != KS_OP_NOT_IN)) {
-      ok = false;
-      break;
-    }
+    if (str(e.key) != "metadata.name" || e.n_values != 1 || (e.op != KS_OP_IN && e.op != KS_OP_NOT_IN)) return false;
     const int32_t nid = c->lookup(e.values[0]);
     int64_t slot = -1;
     if (nid >= 0) {
       auto it = c->name_slot.find((uint32_t)nid);
       if (it != c->name_slot.end()) slot = it->second;
     }
-    tmp.add(e.op == KS_OP_IN ? CK_NAME_EQ : CK_NAME_NE, term, weight, nullptr, (uint64_t)slot);
+    tb.names.emplace_back(e.op == KS_OP_IN ? TO_NAME_IN : TO_NAME_NOT_IN, (uint64_t)slot);
     c->compile_used_names = true;
   }
-  if (!ok) return false;
-  out.w.insert(out.w.end(), tmp.w.begin(), tmp.w.end());
   return true;
 }
 
@@ -738,7 +761,7 @@ ks_status check_modelled(ks_ctx *c, const ks_pod &p) {
   return KS_OK;
 }
 
-ks_status compile_pod(ks_ctx *c, const ks_pod &p, PodDev &d, ClauseBuf &cl) {
+ks_status compile_pod(ks_ctx *c, const ks_pod &p, PodDev &d, ProgBuf &cl) {
   std::memset(&d, 0, sizeof d);
   ks_status st;
   if ((st = check_modelled(c, p))) return st;
@@ -795,35 +818,37 @@ ks_status compile_pod(ks_ctx *c, const ks_pod &p, PodDev &d, ClauseBuf &cl) {
     }
     c->compile_used_names = true;
   }
-  // required: nodeSelector (term 0) + RequiredDuringScheduling terms (1..)
-  d.req_off = cl.count();
+  // required: OR of the RequiredDuringScheduling terms, the nodeSelector's
+  // pairs merged into each (RequiredNodeAffinity.Match: selector AND terms);
+  // no usable term (all empty / parse errors / contradictory) matches nothing
+  TermBuild sel;
   for (uint32_t i = 0; i < p.n_node_selector; ++i) {
-    uint64_t mask[LW] = {};
     uint32_t bit;
     if ((st = get_pair_bit(c, c->intern(p.node_selector[i].key), c->intern(p.node_selector[i].value), &bit)))
       return st;
-    set_bit(mask, bit);
-    cl.add(CK_ANY, 0, 0, mask, 0);
+    set_bit(sel.must, bit);
   }
+  d.req_off = cl.size();
   if (p.has_required) {
-    uint32_t nt = 0;
     for (uint32_t i = 0; i < p.n_required_terms; ++i) {
       const ks_term &t = p.required_terms[i];
       if (t.n_expressions == 0 && t.n_fields == 0) continue;  // empty term selects nothing: skipped
-      ++nt;
+      TermBuild tb;
       st = KS_OK;
-      if (!compile_term(c, t, nt, 0, cl, &st)) {
+      if (!compile_term(c, t, tb, &st)) {
         if (st) return st;
-        cl.add(CK_FALSE, nt, 0, nullptr, 0);  // parse error: term never matches
+        continue;  // parse error: the term never matches
       }
+      for (int k = 0; k < LW; ++k) tb.must[k] |= sel.must[k];
+      if (tb.contradictory()) continue;
+      tb.emit(cl, 0);
+      d.req_len++;
     }
-    if (nt == 0) {  // no usable term: nothing matches
-      cl.add(CK_FALSE, 1, 0, nullptr, 0);
-      nt = 1;
-    }
-    d.n_req_terms = nt;
+  } else if (p.n_node_selector) {
+    sel.emit(cl, 0);
+    d.req_len = 1;
   }
-  d.req_len = cl.count() - d.req_off;
+  d.n_req_terms = d.req_len;
   {
     std::vector<std::string> names;
     if (prefilter_names(p, &names)) {
@@ -831,48 +856,44 @@ ks_status compile_pod(ks_ctx *c, const ks_pod &p, PodDev &d, ClauseBuf &cl) {
         d.flags |= PF_NA_CONFLICT;  // UnschedulableAndUnresolvable (errReasonConflict) at PreFilter
       } else {
         d.flags |= PF_PREFILTER;
-        d.pre_off = cl.count();
-        uint32_t found = 0;
+        d.pre_off = cl.size();
         for (auto &nm : names) {
           auto id = c->str_ids.find(nm);
           if (id == c->str_ids.end()) continue;
           auto it = c->name_slot.find(id->second);
           if (it == c->name_slot.end()) continue;  // PreFilterResult names a node the snapshot lacks
-          cl.add(CK_NAME_EQ, 1, 0, nullptr, (uint64_t)it->second);
-          ++found;
+          cl.w.push_back((uint64_t)it->second);
         }
-        d.pre_len = cl.count() - d.pre_off;
-        d.prefilter_out = c->n_present - found;
+        d.pre_len = cl.size() - d.pre_off;
+        d.prefilter_out = c->n_present - d.pre_len;
       }
       c->compile_used_names = true;
     }
   }
   if (p.n_node_selector || p.has_required) d.flags |= PF_AFF;
-  // preferred terms
-  d.pref_off = cl.count();
+  // preferred terms: Σ weight of the matching ones
+  d.pref_off = cl.size();
   if (p.has_preferred) {
     d.flags |= PF_HAS_PREF;
-    uint32_t nt = 0;
     for (uint32_t i = 0; i < p.n_preferred; ++i) {
       const ks_preferred_term &t = p.preferred[i];
       if (t.weight == 0 || (t.preference.n_expressions == 0 && t.preference.n_fields == 0)) continue;
       if (t.weight < 0 || t.weight > 100)
         return c->fail(KS_ERR_UNSUPPORTED, "preferred term weight %d outside 1..100", t.weight);
+      TermBuild tb;
       st = KS_OK;
-      const uint32_t mark = (uint32_t)cl.w.size();
-      if (!compile_term(c, t.preference, nt + 1, t.weight, cl, &st)) {
+      if (!compile_term(c, t.preference, tb, &st)) {
         if (st) return st;
-        cl.w.resize(mark);
         d.flags |= PF_PREF_ERR;
         continue;
       }
-      if (cl.w.size() == mark) cl.add(CK_ANY, nt + 1, t.weight, nullptr, 0);  // unreachable (non-empty)
-      ++nt;
+      if (tb.contradictory()) continue;  // matches no node: adds 0 everywhere
+      tb.emit(cl, t.weight);
+      d.pref_len++;
       d.na_guess += (uint32_t)t.weight;  // guess of max raw: every term matches some feasible node
     }
-    if (nt) d.flags |= PF_NA;
+    if (d.pref_len) d.flags |= PF_NA;
   }
-  d.pref_len = cl.count() - d.pref_off;
   if ((c->hard_in_use & ~d.tol_hard) || d.name_slot != -1 || (d.flags & (PF_AFF | PF_TT | PF_NA)))
     d.flags |= PF_EXT;
   return KS_OK;
@@ -1811,7 +1832,7 @@ ks_status ks_pods_check(ks_ctx *c, const ks_pod *pods, uint32_t n, ks_status *st
   std::string first_err;
   for (uint32_t i = 0; i < n; ++i) {
     PodDev d;
-    ClauseBuf cl;
+    ProgBuf cl;
     status[i] = compile_pod(c, pods[i], d, cl);
     if (status[i] && !first) {
       first = status[i];
@@ -1828,7 +1849,7 @@ ks_status ks_batch_prepare(ks_ctx *c, const ks_pod *pods, uint32_t n, ks_batch *
   *out = nullptr;
   HIPC(c, hipSetDevice(c->cfg.device));
   std::vector<PodDev> dev(std::max<uint32_t>(n, 1));
-  ClauseBuf cl;
+  ProgBuf cl;
   bool ext = false, norm = false;
   uint32_t dict_v, names_v;
   ks_status st;
@@ -1846,7 +1867,7 @@ ks_status ks_batch_prepare(ks_ctx *c, const ks_pod *pods, uint32_t n, ks_batch *
     names_v = c->compile_used_names ? c->names_version : 0;
   }
   if (norm) ext = true;
-  if (cl.w.empty()) cl.add(CK_FALSE, 0, 0, nullptr, 0);
+  if (cl.w.empty()) cl.w.push_back(0);
   ks_batch *b = nullptr;
   if ((st = batch_acquire(c, n, cl.w.size(), &b))) return st;
   b->n = n;
@@ -1957,14 +1978,14 @@ ks_status ks_plugin_scores(ks_ctx *c, const ks_pod *pod, ks_node_score *out) {
   if (ks_status dst_ = drain_async(c)) return dst_;
   HIPC(c, hipSetDevice(c->cfg.device));
   PodDev d;
-  ClauseBuf cl;
+  ProgBuf cl;
   ks_status st;
   {
     std::lock_guard<std::mutex> g(c->mu);
     if ((st = compile_pod(c, *pod, d, cl))) return st;
     if ((st = upload_dirty_ext(c, c->xm))) return st;
   }
-  if (cl.w.empty()) cl.add(CK_FALSE, 0, 0, nullptr, 0);
+  if (cl.w.empty()) cl.w.push_back(0);
   DumpArgs a{};
   a.t = c->t;
   a.nslots = c->cap;

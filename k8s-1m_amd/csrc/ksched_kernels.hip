@@ -217,84 +217,64 @@ __device__ __forceinline__ void load_ext(const NodeTable &t, uint32_t pos, bool 
   for (int k = 0; k < NNUM; ++k) e.num[k] = t.num[(size_t)k * t.npos + pos];
 }
 
-// One label-selector requirement (clause) against one node.  The node's
-// label words / numeric values are passed as scalars so that no runtime index
-// into the per-node register arrays can form (it would demote them to scratch).
-__device__ __forceinline__ bool clause_pass(const uint64_t *c, uint64_t l0, uint64_t l1, uint64_t l2, uint64_t l3,
-                                            int64_t n0, int64_t n1, uint32_t slot) {
-  const uint32_t kind = (uint32_t)c[0] & 0xFF;
-  const uint64_t any = (l0 & c[1]) | (l1 & c[2]) | (l2 & c[3]) | (l3 & c[4]);
-  switch (kind) {
-    case CK_ANY: return any != 0;
-    case CK_NONE: return any == 0;
-    case CK_GT:
-    case CK_LT: {
-      // mask words hold the key's numeric-valid bit; c[5] the operand
-      const bool col1 = (c[0] >> 8) & 1u;
-      const int64_t v = col1 ? n1 : n0;
-      const int64_t x = (int64_t)c[5];
-      return any != 0 && (kind == CK_GT ? v > x : v < x);
-    }
-    case CK_NAME_EQ: return (int64_t)slot == (int64_t)c[5];
-    case CK_NAME_NE: return (int64_t)slot != (int64_t)c[5];
-    default: return false;
+// One label-program term (ksched_dev.hpp) against one node: fixed-form mask
+// tests, then the rare Gt / Lt and metadata.name entries.
+__device__ __forceinline__ bool term_pass(const uint64_t *t, const NodeExt &e, uint32_t slot) {
+  const uint64_t w0 = t[0];
+  const uint32_t ng = (uint32_t)w0 & 0xFF, nn = ((uint32_t)w0 >> 8) & 0xFF, nm = ((uint32_t)w0 >> 16) & 0xFF;
+  uint64_t diff = 0;
+#pragma unroll
+  for (int k = 0; k < LW; ++k) diff |= (e.lab[k] & t[1 + LW + k]) ^ t[1 + k];
+  bool ok = diff == 0;
+  const uint64_t *g = t + TERM_HDR_WORDS;
+  for (uint32_t i = 0; i < ng; ++i, g += LW) {
+    uint64_t any = 0;
+#pragma unroll
+    for (int k = 0; k < LW; ++k) any |= e.lab[k] & g[k];
+    ok &= any != 0;
   }
+  for (uint32_t i = 0; i < nn; ++i, g += 2) {
+    const int64_t v = (g[0] & 0xFF) ? e.num[1] : e.num[0];
+    const int64_t x = (int64_t)g[1];
+    ok &= ((g[0] >> 8) & 0xFF) == TO_GT ? v > x : v < x;
+  }
+  for (uint32_t i = 0; i < nm; ++i, g += 2) {
+    const bool eq = (int64_t)slot == (int64_t)g[1];
+    ok &= g[0] == TO_NAME_IN ? eq : !eq;
+  }
+  return ok;
 }
 
-__device__ __forceinline__ bool clause_pass(const uint64_t *c, const NodeExt &e, uint32_t slot) {
-  return clause_pass(c, e.lab[0], e.lab[1], e.lab[2], e.lab[3], e.num[0], e.num[1], slot);
-}
-
-// RequiredNodeAffinity.Match: nodeSelector group (term 0) AND (no required
-// terms OR any required term whose clauses all pass).
-__device__ __forceinline__ bool required_match(const PodDev &p, const uint64_t *clauses, const NodeExt &e,
+// RequiredNodeAffinity.Match: any required term (the nodeSelector is merged
+// into each; PF_AFF with no term matches nothing).
+__device__ __forceinline__ bool required_match(const PodDev &p, const uint64_t *prog, const NodeExt &e,
                                                uint32_t slot) {
-  bool sel = true, any = false, cur = true;
-  uint32_t curterm = 0;
-  const uint64_t *c = clauses + (size_t)p.req_off * CLAUSE_WORDS;
-  for (uint32_t k = 0; k < p.req_len; ++k, c += CLAUSE_WORDS) {
-    const uint32_t term = ((uint32_t)c[0] >> 16) & 0xFFFF;
-    if (term != curterm) {
-      if (curterm >= 1) any |= cur;
-      cur = true;
-      curterm = term;
-    }
-    const bool pass = clause_pass(c, e, slot);
-    if (term == 0) sel &= pass;
-    else cur &= pass;
+  const uint64_t *t = prog + p.req_off;
+  bool any = false;
+  for (uint32_t k = 0; k < p.req_len; ++k) {
+    any |= term_pass(t, e, slot);
+    t += term_words(t[0]);
   }
-  if (curterm >= 1) any |= cur;
-  return sel && (p.n_req_terms == 0 || any);
+  return any;
 }
 
 // PreferredSchedulingTerms.Score: Σ weight of matching preferred terms.
-__device__ __forceinline__ int64_t preferred_raw(const PodDev &p, const uint64_t *clauses, const NodeExt &e,
+__device__ __forceinline__ int64_t preferred_raw(const PodDev &p, const uint64_t *prog, const NodeExt &e,
                                                  uint32_t slot) {
+  const uint64_t *t = prog + p.pref_off;
   int64_t raw = 0;
-  bool cur = true;
-  uint32_t curterm = 0;
-  int64_t wcur = 0;
-  const uint64_t *c = clauses + (size_t)p.pref_off * CLAUSE_WORDS;
-  for (uint32_t k = 0; k < p.pref_len; ++k, c += CLAUSE_WORDS) {
-    const uint32_t term = ((uint32_t)c[0] >> 16) & 0xFFFF;
-    if (term != curterm) {
-      if (curterm >= 1 && cur) raw += wcur;
-      cur = true;
-      curterm = term;
-      wcur = (int64_t)(int32_t)(c[0] >> 32);
-    }
-    cur &= clause_pass(c, e, slot);
+  for (uint32_t k = 0; k < p.pref_len; ++k) {
+    if (term_pass(t, e, slot)) raw += (int64_t)(uint32_t)(t[0] >> 32);
+    t += term_words(t[0]);
   }
-  if (curterm >= 1 && cur) raw += wcur;
   return raw;
 }
 
-// NodeAffinity PreFilterResult: the node is one of the named ones (one
-// CK_NAME_EQ clause per named node in the pod's prefilter program).
-__device__ __forceinline__ bool prefilter_match(const PodDev &p, const uint64_t *clauses, uint32_t slot) {
-  const uint64_t *c = clauses + (size_t)p.pre_off * CLAUSE_WORDS;
+// NodeAffinity PreFilterResult: the node is one of the named ones (the
+// pod's prefilter program lists their slots).
+__device__ __forceinline__ bool prefilter_match(const PodDev &p, const uint64_t *prog, uint32_t slot) {
   bool any = false;
-  for (uint32_t k = 0; k < p.pre_len; ++k, c += CLAUSE_WORDS) any |= (int64_t)slot == (int64_t)c[5];
+  for (uint32_t k = 0; k < p.pre_len; ++k) any |= (uint64_t)slot == prog[p.pre_off + k];
   return any;
 }
 
@@ -403,101 +383,90 @@ __device__ __forceinline__ PodDev load_pod(const PodDev *pods, uint32_t i) {
 
 
 // ------------------------------------------------ sweep: EXT pods, NPL nodes
-// The sweep evaluates a pod's label programs clause-outer, node-inner: each
-// clause's words are read once per pod (scalar loads) and applied to the
-// lane's NPL nodes.  Label words beyond the dictionary's (LWU, a template parameter) are not
-// read: straight-line AND / OR over the words in use, no per-word branches.
+// The sweep evaluates a pod's label programs term-outer, node-inner: each
+// term's words are read once per pod (scalar loads) and applied to the
+// lane's NPL nodes.  Label words beyond the dictionary's (LWU, a template
+// parameter) are not read: straight-line AND / XOR / OR over the words in
+// use, no per-word branches.  Results are 0 / 1 vector values.
 template <int NPL, int LWU>
-__device__ __forceinline__ void clause_pass_n(const uint64_t *c, const NodeExt (&e)[NPL], const NodeRegs (&nr)[NPL],
-                                              uint32_t (&pass)[NPL]) {
-  // Results are 0 / 1 in vector registers (not lane masks): the term
-  // bookkeeping below is then plain VALU and-or, with no exec-mask merging of
-  // booleans across the clause loop's uniform branches.
-  const uint64_t w0 = c[0];
-  const uint32_t kind = uniform_u32((uint32_t)w0 & 0xFF);
-  uint64_t m[LWU];
+__device__ __forceinline__ const uint64_t *term_pass_n(const uint64_t *t, const NodeExt (&e)[NPL],
+                                                       const NodeRegs (&nr)[NPL], uint32_t (&ok)[NPL]) {
+  const uint64_t w0 = t[0];
+  const uint32_t ng = uniform_u32((uint32_t)w0 & 0xFF), nn = uniform_u32(((uint32_t)w0 >> 8) & 0xFF),
+                 nm = uniform_u32(((uint32_t)w0 >> 16) & 0xFF);
+  uint64_t must[LWU], mf[LWU];
 #pragma unroll
-  for (int k = 0; k < LWU; ++k) m[k] = c[1 + k];
+  for (int k = 0; k < LWU; ++k) {
+    must[k] = t[1 + k];
+    mf[k] = t[1 + LW + k];
+  }
   static_for<NPL>([&](auto J) {
     constexpr int j = J;
-    uint64_t acc = 0;
+    uint64_t diff = 0;
 #pragma unroll
-    for (int k = 0; k < LWU; ++k) acc |= e[j].lab[k] & m[k];
-    pass[j] = acc != 0 ? 1u : 0u;
+    for (int k = 0; k < LWU; ++k) diff |= (e[j].lab[k] & mf[k]) ^ must[k];
+    ok[j] = diff == 0 ? 1u : 0u;
   });
-  if (kind == CK_NONE) {
-    static_for<NPL>([&](auto J) { pass[J] ^= 1u; });
-  } else if (kind != CK_ANY) {  // rare kinds
-    const int64_t x = (int64_t)c[5];
-    const bool col1 = (w0 >> 8) & 1u;
+  const uint64_t *g = t + TERM_HDR_WORDS;
+  for (uint32_t i = 0; i < ng; ++i, g += LW) {
+    uint64_t gm[LWU];
+#pragma unroll
+    for (int k = 0; k < LWU; ++k) gm[k] = g[k];
+    static_for<NPL>([&](auto J) {
+      constexpr int j = J;
+      uint64_t any = 0;
+#pragma unroll
+      for (int k = 0; k < LWU; ++k) any |= e[j].lab[k] & gm[k];
+      ok[j] &= any != 0 ? 1u : 0u;
+    });
+  }
+  for (uint32_t i = 0; i < nn; ++i, g += 2) {  // rare: Gt / Lt
+    const bool col1 = g[0] & 0xFF, gt = ((g[0] >> 8) & 0xFF) == TO_GT;
+    const int64_t x = (int64_t)g[1];
     static_for<NPL>([&](auto J) {
       constexpr int j = J;
       const int64_t v = col1 ? e[j].num[1] : e[j].num[0];
-      bool ok;
-      switch (kind) {
-        case CK_GT: ok = pass[j] && v > x; break;
-        case CK_LT: ok = pass[j] && v < x; break;
-        case CK_NAME_EQ: ok = (int64_t)nr[j].slot == x; break;
-        case CK_NAME_NE: ok = (int64_t)nr[j].slot != x; break;
-        default: ok = false; break;
-      }
-      pass[j] = ok ? 1u : 0u;
+      ok[j] &= (gt ? v > x : v < x) ? 1u : 0u;
     });
   }
+  for (uint32_t i = 0; i < nm; ++i, g += 2) {  // rare: metadata.name
+    const bool in = g[0] == TO_NAME_IN;
+    const int64_t x = (int64_t)g[1];
+    static_for<NPL>([&](auto J) {
+      constexpr int j = J;
+      ok[j] &= (((int64_t)nr[j].slot == x) == in) ? 1u : 0u;
+    });
+  }
+  return g;
 }
 
 // required_match for NPL nodes at once
 template <int NPL, int LWU>
-__device__ __forceinline__ void required_match_n(const PodDev &p, const uint64_t *clauses, const NodeExt (&e)[NPL],
+__device__ __forceinline__ void required_match_n(const PodDev &p, const uint64_t *prog, const NodeExt (&e)[NPL],
                                                  const NodeRegs (&nr)[NPL], bool (&out)[NPL]) {
-  uint32_t sel[NPL], any[NPL], cur[NPL];
-  static_for<NPL>([&](auto J) { sel[J] = 1u; any[J] = 0u; cur[J] = 1u; });
-  uint32_t curterm = 0;
-  const uint64_t *c = clauses + (size_t)p.req_off * CLAUSE_WORDS;
-  for (uint32_t k = 0; k < p.req_len; ++k, c += CLAUSE_WORDS) {
-    const uint32_t term = uniform_u32(((uint32_t)c[0] >> 16) & 0xFFFF);
-    // a new term closes the previous one (terms >= 1 are OR-ed) and restarts
-    const uint32_t close = (term != curterm && curterm >= 1) ? 1u : 0u;
-    const uint32_t open = term != curterm ? 1u : 0u;
-    curterm = term;
-    uint32_t pass[NPL];
-    clause_pass_n<NPL, LWU>(c, e, nr, pass);
-    const uint32_t in_sel = term == 0 ? 1u : 0u;  // term 0: the nodeSelector group (AND)
-    static_for<NPL>([&](auto J) {
-      any[J] |= cur[J] & close;
-      cur[J] |= open;
-      sel[J] &= pass[J] | (in_sel ^ 1u);
-      cur[J] &= pass[J] | in_sel;
-    });
+  uint32_t any[NPL];
+  static_for<NPL>([&](auto J) { any[J] = 0u; });
+  const uint64_t *t = prog + p.req_off;
+  for (uint32_t k = 0; k < p.req_len; ++k) {
+    uint32_t ok[NPL];
+    t = term_pass_n<NPL, LWU>(t, e, nr, ok);
+    static_for<NPL>([&](auto J) { any[J] |= ok[J]; });
   }
-  const uint32_t last = curterm >= 1 ? 1u : 0u;
-  const bool noterms = p.n_req_terms == 0;
-  static_for<NPL>([&](auto J) { out[J] = sel[J] && (noterms || ((any[J] | (cur[J] & last)) != 0)); });
+  static_for<NPL>([&](auto J) { out[J] = any[J] != 0u; });
 }
 
 // preferred_raw for NPL nodes at once
 template <int NPL, int LWU>
-__device__ __forceinline__ void preferred_raw_n(const PodDev &p, const uint64_t *clauses, const NodeExt (&e)[NPL],
+__device__ __forceinline__ void preferred_raw_n(const PodDev &p, const uint64_t *prog, const NodeExt (&e)[NPL],
                                                 const NodeRegs (&nr)[NPL], uint32_t (&raw)[NPL]) {
-  uint32_t cur[NPL];
-  static_for<NPL>([&](auto J) { raw[J] = 0u; cur[J] = 1u; });
-  uint32_t curterm = 0, wcur = 0;
-  const uint64_t *c = clauses + (size_t)p.pref_off * CLAUSE_WORDS;
-  for (uint32_t k = 0; k < p.pref_len; ++k, c += CLAUSE_WORDS) {
-    const uint32_t term = uniform_u32(((uint32_t)c[0] >> 16) & 0xFFFF);
-    const uint32_t wclose = (term != curterm && curterm >= 1) ? wcur : 0u;  // weight of the term closed here
-    const uint32_t open = term != curterm ? 1u : 0u;
-    if (term != curterm) wcur = uniform_u32((uint32_t)(c[0] >> 32));
-    curterm = term;
-    uint32_t pass[NPL];
-    clause_pass_n<NPL, LWU>(c, e, nr, pass);
-    static_for<NPL>([&](auto J) {
-      raw[J] += cur[J] * wclose;
-      cur[J] = (cur[J] | open) & pass[J];
-    });
+  static_for<NPL>([&](auto J) { raw[J] = 0u; });
+  const uint64_t *t = prog + p.pref_off;
+  for (uint32_t k = 0; k < p.pref_len; ++k) {
+    const uint32_t w = uniform_u32((uint32_t)(t[0] >> 32));
+    uint32_t ok[NPL];
+    t = term_pass_n<NPL, LWU>(t, e, nr, ok);
+    static_for<NPL>([&](auto J) { raw[J] += ok[J] * w; });
   }
-  const uint32_t wlast = curterm >= 1 ? wcur : 0u;
-  static_for<NPL>([&](auto J) { raw[J] += cur[J] * wlast; });
 }
 
 // DefaultNormalizeScore's floor(100 * raw / max) for 0 <= raw <= max < 2^25
@@ -509,6 +478,15 @@ constexpr double NORM_EPS = 0x1p-40;
 __device__ __forceinline__ uint32_t normalize_inv(uint32_t raw, double inv) {
   return (uint32_t)__builtin_fma((double)(100u * raw), inv, NORM_EPS);
 }
+
+// Timing ablations (-DKS_ABL=mask, diagnostic builds only; results are then
+// wrong): skip the EXT sweep's label programs (1), per-plugin failure counts
+// (2), TaintToleration normalisation (4), BalancedAllocation (8).
+#ifdef KS_ABL
+#define ABL_ON(b) ((KS_ABL & (b)) == 0)
+#else
+#define ABL_ON(b) true
+#endif
 
 // =================================================================== sweep
 // Normalising plugins (TaintToleration with PreferNoSchedule taints, NodeAffinity
@@ -606,17 +584,16 @@ __global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
       bool aff[NPL], pre[NPL];
       uint32_t praw[NPL];
       static_for<NPL>([&](auto J) { aff[J] = true; pre[J] = true; praw[J] = 0u; });
-      if (p.flags & PF_AFF) required_match_n<NPL, LWU>(p, a.clauses, ne, nr, aff);
+      if (ABL_ON(1) && (p.flags & PF_AFF)) required_match_n<NPL, LWU>(p, a.clauses, ne, nr, aff);
       if (p.flags & PF_PREFILTER) {  // rare: pods naming their nodes by metadata.name
         static_for<NPL>([&](auto J) { pre[J] = false; });
-        const uint64_t *c = a.clauses + (size_t)p.pre_off * CLAUSE_WORDS;
-        for (uint32_t k = 0; k < p.pre_len; ++k, c += CLAUSE_WORDS) {
-          const int64_t x = (int64_t)c[5];
-          static_for<NPL>([&](auto J) { pre[J] |= (int64_t)nr[J].slot == x; });
+        for (uint32_t k = 0; k < p.pre_len; ++k) {
+          const uint64_t x = a.clauses[p.pre_off + k];
+          static_for<NPL>([&](auto J) { pre[J] |= (uint64_t)nr[J].slot == x; });
         }
       }
       const bool conflict = p.flags & PF_NA_CONFLICT;
-      if (p.flags & PF_NA) preferred_raw_n<NPL, LWU>(p, a.clauses, ne, nr, praw);
+      if (ABL_ON(1) && (p.flags & PF_NA)) preferred_raw_n<NPL, LWU>(p, a.clauses, ne, nr, praw);
       const double *ip = fix ? a.norm_inv + 2 * r : a.guess_inv + 2 * (size_t)pi;  // RN(1 / max)
       const double inv_tt = (p.flags & PF_TT) ? ip[0] : 0.0;
       const double inv_na = (p.flags & PF_NA) ? ip[1] : 0.0;
@@ -645,12 +622,12 @@ __global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
         if (!valid) st = ST_EMPTY;
         const bool feasible = st == ST_FEASIBLE;
         uint32_t tot1 = (uint32_t)__umul24((uint32_t)a.w.fit, (uint32_t)score_la(p, nr[j])) +
-                        (uint32_t)__umul24((uint32_t)a.w.ba, (uint32_t)score_ba(p, nr[j])) + 1u;
+                        (uint32_t)__umul24((uint32_t)a.w.ba, ABL_ON(8) ? (uint32_t)score_ba(p, nr[j]) : 50u) + 1u;
         uint32_t tts = 100u;
         bool at_tt = false, at_na = false;
         if (p.flags & PF_TT) {
           const uint32_t raw = (uint32_t)__popcll(ne[j].prefer & ~p.tol_prefer);
-          tts = 100u - normalize_inv(raw, inv_tt);
+          tts = ABL_ON(4) ? 100u - normalize_inv(raw, inv_tt) : 100u;
           at_tt = feasible && raw == tt_max;
           over |= feasible && raw > tt_max;
           tmx = max(tmx, feasible ? raw : 0u);
@@ -671,7 +648,7 @@ __global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
         b1 = max(b1, key);
         const uint64_t fb = __ballot(feasible), vb = __ballot(valid);
         feas += (uint32_t)__popcll(fb);
-        if (fb != vb) {  // some node failed a filter: per-plugin diagnosis counts
+        if (ABL_ON(2) && fb != vb) {  // some node failed a filter: per-plugin diagnosis counts
           f0 += popc_ballot(st == 0);
           f1 += popc_ballot(st == 1);
           f2 += popc_ballot(st == 2);
@@ -1076,9 +1053,11 @@ __global__ __launch_bounds__(256) void gather_cand_kernel(RoundArgs a) {
 // per-plugin failure / normaliser-at-max counts are corrected by their status
 // change.  Afterwards a pod's list, bound and counts are exact for the state
 // resolve k starts from, so the resolve re-scores only its own commits.
-constexpr int PATCH_THREADS = 512;
+// One thread per carried node and per list entry: 256 threads for K <= 256,
+// 512 for longer lists (a 512-thread launch of the EXT variant costs 4x the
+// time per round on C4, so it is only used when needed).
 constexpr int PHASH = 1024;
-static_assert(PATCH_THREADS >= MAX_P && PATCH_THREADS >= MAX_K, "one thread per carried node / list entry");
+static_assert(2 * MAX_P >= MAX_K, "patch thread counts");
 
 __device__ __forceinline__ uint32_t rhash(uint32_t x) { return (x * 2654435761u) >> 22; }  // 10 bits
 
@@ -1122,8 +1101,9 @@ __device__ __forceinline__ void status_delta(const PodDev &p, const uint64_t *cl
   }
 }
 
-template <bool EXT>
+template <bool EXT, int PATCH_THREADS>
 __global__ __launch_bounds__(PATCH_THREADS) void patch_kernel(RoundArgs a) {
+  static_assert(PATCH_THREADS >= MAX_P, "one thread per carried node");
   constexpr int NW = PATCH_THREADS / WAVE;
   __shared__ uint32_t s_hkey[PHASH];
   __shared__ uint64_t s_k1[MAX_P];    // carried nodes' live keys (0: infeasible)
@@ -2447,8 +2427,13 @@ hipError_t launch_writeback(const NodeTable &t, const CarryRec *carry, const uin
 }
 
 hipError_t launch_patch(const RoundArgs &a, bool ext, hipStream_t st) {
-  if (ext) patch_kernel<true><<<a.P, PATCH_THREADS, 0, st>>>(a);
-  else patch_kernel<false><<<a.P, PATCH_THREADS, 0, st>>>(a);
+  if (a.K <= (uint32_t)MAX_P) {
+    if (ext) patch_kernel<true, MAX_P><<<a.P, MAX_P, 0, st>>>(a);
+    else patch_kernel<false, MAX_P><<<a.P, MAX_P, 0, st>>>(a);
+  } else {
+    if (ext) patch_kernel<true, MAX_K><<<a.P, MAX_K, 0, st>>>(a);
+    else patch_kernel<false, MAX_K><<<a.P, MAX_K, 0, st>>>(a);
+  }
   return hipGetLastError();
 }
 

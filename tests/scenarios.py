@@ -288,6 +288,20 @@ def prefilter_result():
     return nodes, pods, exp
 
 
+@scenario
+def ba_float_boundary():
+    # a 21760m / explicit-0-memory pod on an empty 32-core
+    # node has BalancedAllocation (1 - 0.34) * 100 = 65.99999999999999 -> 65 in
+    # Go's float64 (66 in exact arithmetic).  Node 0 (40 cores / 64 Gi, first
+    # filled to 5250m / 2 Gi by pod 0) then totals 431 = node 1's; the tie
+    # goes to slot 0.  A score off by one at node 1 would pick node 1: this pins
+    # the sweep's binary32 fast path's hand-off to binary64 next to integers.
+    nodes = [node("b", cpu=40000, mem=64 * Gi), node("a", cpu=32000, mem=256 * Gi)]
+    pods = [pod("fill", cpu=5250, mem=2 * Gi), pod("kat", cpu=21760, mem=0)]
+    exp = [dict(node=0, feasible=2), dict(node=0, feasible=2, score=431)]
+    return nodes, pods, exp
+
+
 def check(results, exp):
     """results: structured numpy array (tests.helpers.RES_DT)."""
     for i, e in enumerate(exp):
@@ -302,5 +316,7 @@ def check(results, exp):
             assert r["feasible"] == e["feasible"], (i, r, e)
         for k, v in e.get("fails", {}).items():
             assert r["fail"][k] == v, (i, k, r, e)
+        if "score" in e:
+            assert r["total_score"] == e["score"], (i, r, e)
         if e.get("single"):
             assert r["flags"] & 1, (i, r)

@@ -98,7 +98,7 @@ def test_open_without_device_fails_cleanly():
 def test_invalid_configs_rejected():
     lib = _abi.ksched_lib()
     for field, value in (("node_capacity", 0), ("nodes_per_lane", 3), ("pods_per_round", 100000),
-                         ("topk", 300), ("world_size", 2)):
+                         ("topk", 513), ("world_size", 2)):
         cfg = _abi.KsConfig()
         lib.ks_config_default(C.byref(cfg))
         setattr(cfg, field, value)

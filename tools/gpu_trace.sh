@@ -1,8 +1,17 @@
 #!/bin/bash
-# Kernel trace of a short bench (args after the tag are passed to bench.py).
+# Kernel trace + stats of one bench configuration: tools/gpu_trace.sh TAG [bench args...]
 export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"
-TAG=$1; shift
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/trace_$TAG" -o run --output-format csv -- python3 "$R/bench.py" --no-cpu-baseline "$@" > gpurun_out/trace_$TAG.json 2> gpurun_out/trace_$TAG.err
-rc=$?; echo "trace rc=$rc"; cat gpurun_out/trace_$TAG.json; exit $rc
+TAG=$1
+shift
+mkdir -p gpurun_out/$TAG
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/$TAG/trace" -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-e2e --latency-calls 0 "$@" > gpurun_out/$TAG/bench.json 2> gpurun_out/$TAG/bench.err || exit $?
+python3 - "$R/gpurun_out/$TAG" <<'PY'
+import csv, json, sys
+d = sys.argv[1]
+b = json.load(open(d + "/bench.json"))
+print("value", b["value"], "sweep_ms", b["roofline"]["avg_launch_ms"], "resolve_ms", b["extra"]["resolve_ms_per_round"])
+for r in list(csv.DictReader(open(d + "/trace/run_kernel_stats.csv")))[:12]:
+    print(r["Name"][:70].ljust(70), r["Calls"], round(float(r["AverageNs"]) / 1e3, 1), "us")
+PY

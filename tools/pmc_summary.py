@@ -16,9 +16,10 @@ grid).  Per evaluation (pod x node, evaluations per launch from the bench line):
   FETCH_SIZE / WRITE_SIZE are in KB; the x2 is MI355X_MICROARCH.md's gfx950
   correction (FETCH_SIZE tallies 128-B fabric reads at 64 B).  These are L2
   memory-side bytes (Infinity-Cache hits counted): an upper bound on HBM bytes;
-* ``valu_busy`` = SQ_ACTIVE_INST_VALU x 4 / (SQ_BUSY_CYCLES x 4 SIMDs ... ) is
-  reported as SQ_ACTIVE_INST_VALU / (GRBM_GUI_ACTIVE / 8 XCDs x 256 CUs x 4 SIMDs / 4)
-  (quad-cycles of VALU execution per SIMD quad-cycle);
+* ``valu_cycles_per_instr`` = 4 x SQ_ACTIVE_INST_VALU / SQ_INSTS_VALU: cycles a
+  wave64 VALU instruction occupies its SIMD (the counter is in quad-cycles);
+* ``valu_busy`` = SQ_ACTIVE_INST_VALU / (GRBM_GUI_ACTIVE / 8 XCDs x 256 CUs x 4
+  SIMDs / 4): the share of SIMD quad-cycles executing VALU;
 * ``lds_bank_conflict_ratio`` = SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE;
 * ``clock_ghz`` = GRBM_GUI_ACTIVE / 8 XCDs / kernel duration.
 """
@@ -114,12 +115,12 @@ def main():
         if all(v is not None for v in f64) and s.get("SQ_INSTS_VALU"):
             n64 = sum(f64)
             out["valu_f64_share"] = round(n64 / s["SQ_INSTS_VALU"], 4)
-            # SIMD issue cycles per wave instruction: 2 (32 lanes/cycle), 4 for
-            # binary64 (half rate: MI355X FP64 vector peak is half the FP32 one)
-            out["valu_issue_cycles_per_eval"] = (2 * (s["SQ_INSTS_VALU"] - n64) + 4 * n64) / evals
             for c in ("SQ_INSTS_VALU_INT32", "SQ_INSTS_VALU_INT64", "SQ_INSTS_VALU_CVT"):
                 if c in s:
                     out[c.lower() + "_share"] = round(s[c] / s["SQ_INSTS_VALU"], 4)
+        if "SQ_ACTIVE_INST_VALU" in s and s.get("SQ_INSTS_VALU"):
+            # cycles a wave64 VALU instruction occupies its SIMD (quad-cycle counter x 4)
+            out["valu_cycles_per_instr"] = round(4 * s["SQ_ACTIVE_INST_VALU"] / s["SQ_INSTS_VALU"], 3)
         if "SQ_ACTIVE_INST_VALU" in s and s.get("GRBM_GUI_ACTIVE"):
             simd_quads = s["GRBM_GUI_ACTIVE"] / 8 * 256 * 4 / 4
             out["valu_busy"] = round(s["SQ_ACTIVE_INST_VALU"] / simd_quads, 4)
