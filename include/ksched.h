@@ -387,10 +387,11 @@ typedef struct {
 } ks_stats;
 ks_status ks_get_stats(ks_ctx *ctx, ks_stats *out);
 ks_status ks_reset_stats(ks_ctx *ctx);
-/* Raw device counters: [0] rounds [1] pods resolved [2] pods swept
+/* Raw counters: [0] rounds [1] pods resolved [2] pods swept
  * [3] speculated rounds wasted [4] pods re-swept because their guessed
- * normalising maxima were wrong, [8..15] resolve phase cycle sums
- * (diagnostic KS_STAMPS build only). */
+ * normalising maxima were wrong, [5] label-dictionary reclaims, [6] taint
+ * dictionary rebuilds, [8..15] resolve phase cycle sums (diagnostic
+ * KS_STAMPS build only). */
 ks_status ks_debug_counters(ks_ctx *ctx, uint64_t out[16]);
 /* 1 = time sweep / resolve launches with HIP events (every KS_TIMING_EVERY-th
  * round, default 8; sweep_evals counts the timed launches' share), 0 = off. */

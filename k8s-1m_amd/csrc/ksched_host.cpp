@@ -150,6 +150,9 @@ struct HostNode {
   uint64_t lab[LW] = {};
   int64_t num[NNUM] = {};
   std::vector<std::string> images;  // normalised image names
+  // taints as interned ids (the taint dictionaries are rebuilt from these)
+  std::vector<std::array<uint32_t, 3>> hard_taints;            // key, value, effect
+  std::vector<std::pair<uint32_t, uint32_t>> prefer_taints;    // key, value
 };
 
 struct TaintKey {
@@ -255,6 +258,7 @@ struct ks_ctx {
   std::unordered_map<uint32_t, uint32_t> key_bit;
   std::unordered_map<uint32_t, NumCol> num_col;
   uint32_t next_bit = 0, next_num = 0;
+  uint64_t label_resets = 0, taint_rebuilds = 0;  // dictionary capacity reclaims (diagnostics)
   std::unordered_map<uint32_t, std::vector<uint32_t>> key_nodes;  // key id -> slots having it
   bool compile_used_names = false;  // set by compile_pod when a pod resolved a node name to a slot
   uint32_t dict_version = 1;   // taint dictionary / node image set (compiled masks and checks)
@@ -506,6 +510,32 @@ ks_status get_num_col(ks_ctx *c, uint32_t key, NumCol *out) {
   mark_key_nodes_dirty(c, key);
   *out = nc;
   return KS_OK;
+}
+
+// Label dictionary reclaim.  Bits are pod-driven and only grow; when a batch
+// cannot get the bits its label programs need, the dictionary restarts empty:
+// every present node's label words are re-encoded (zero until the batch's
+// own requirements allocate bits again, which re-encodes the nodes carrying
+// those keys) and prepared batches turn stale (dict_version).  The caller
+// has drained the submitted batches (their programs test the old bits).
+void reset_label_dict(ks_ctx *c) {
+  c->pair_bit.clear();
+  c->key_bit.clear();
+  c->num_col.clear();
+  c->next_bit = c->next_num = 0;
+  for (uint32_t s = 0; s < c->cap; ++s) {
+    HostNode &h = c->nodes[s];
+    if (!h.present) continue;
+    bool any = false;
+    for (int k = 0; k < LW; ++k) any |= h.lab[k] != 0;
+    for (int k = 0; k < NNUM; ++k) any |= h.num[k] != 0;
+    if (!any) continue;
+    std::memset(h.lab, 0, sizeof h.lab);
+    std::memset(h.num, 0, sizeof h.num);
+    c->dirty_ext.push_back(s);
+  }
+  c->dict_version++;
+  c->label_resets++;
 }
 
 // ------------------------------------------------------------ pod compile
@@ -896,6 +926,74 @@ ks_status compile_pod(ks_ctx *c, const ks_pod &p, PodDev &d, ProgBuf &cl) {
   }
   if ((c->hard_in_use & ~d.tol_hard) || d.name_slot != -1 || (d.flags & (PF_AFF | PF_TT | PF_NA)))
     d.flags |= PF_EXT;
+  return KS_OK;
+}
+
+// Taint dictionaries (hard: NoSchedule / NoExecute, prefer: PreferNoSchedule)
+// for one node from its stored taint ids.  Returns KS_ERR_CAPACITY when a new
+// taint finds the dictionary full (63 hard taints + the unschedulable bit, 64
+// prefer taints); *grew when a taint was new.
+ks_status encode_taints(ks_ctx *c, HostNode &h, bool *grew) {
+  h.hard = h.unschedulable ? UNSCHED_BIT : 0;
+  h.prefer = 0;
+  for (auto &t : h.hard_taints) {
+    TaintKey tk{t[0], t[1], (int32_t)t[2]};
+    auto it = c->hard_dict.find(tk);
+    uint32_t b;
+    if (it == c->hard_dict.end()) {
+      if (c->hard_list.size() >= 63) return KS_ERR_CAPACITY;
+      b = (uint32_t)c->hard_list.size();
+      c->hard_dict.emplace(tk, b);
+      c->hard_list.push_back(tk);
+      *grew = true;
+    } else {
+      b = it->second;
+    }
+    h.hard |= 1ull << b;
+  }
+  for (auto &pk : h.prefer_taints) {
+    auto it = c->prefer_dict.find(pk);
+    uint32_t b;
+    if (it == c->prefer_dict.end()) {
+      if (c->prefer_list.size() >= 64) return KS_ERR_CAPACITY;
+      b = (uint32_t)c->prefer_list.size();
+      c->prefer_dict.emplace(pk, b);
+      c->prefer_list.push_back(pk);
+      *grew = true;
+    } else {
+      b = it->second;
+    }
+    h.prefer |= 1ull << b;
+  }
+  return KS_OK;
+}
+
+// Taint dictionary reclaim: rebuilt from the taints present nodes carry now
+// (deleted / updated nodes' taints drop out); every present node's taint
+// words are re-encoded and prepared batches turn stale.  KS_ERR_CAPACITY when
+// the present nodes alone carry more distinct taints than the words hold.
+ks_status rebuild_taint_dicts(ks_ctx *c) {
+  c->hard_dict.clear();
+  c->hard_list.clear();
+  c->prefer_dict.clear();
+  c->prefer_list.clear();
+  c->prefer_masks.clear();
+  c->hard_in_use = c->prefer_in_use = 0;
+  bool grew = false;
+  ks_status st = KS_OK;
+  for (uint32_t s = 0; s < c->cap; ++s) {
+    HostNode &h = c->nodes[s];
+    if (!h.present) continue;
+    if (!st) st = encode_taints(c, h, &grew);
+    if (st) h.hard = h.prefer = 0;  // keep the mirror consistent; the call fails
+    c->hard_in_use |= h.hard;
+    c->prefer_in_use |= h.prefer;
+    prefer_mask_ref(c, h.prefer, +1);
+    c->dirty_ext.push_back(s);
+  }
+  c->dict_version++;
+  c->taint_rebuilds++;
+  if (st) return c->fail(st, "present nodes carry more than 63 hard / 64 PreferNoSchedule distinct taints");
   return KS_OK;
 }
 
@@ -1638,47 +1736,29 @@ ks_status ks_nodes_upsert(ks_ctx *c, const ks_node *nodes, const uint32_t *slots
       h.labels.emplace_back(key, c->intern(s.labels[k].value));
       c->key_nodes[key].push_back(slot);
     }
-    h.hard = h.unschedulable ? UNSCHED_BIT : 0;
     if (!is_new) prefer_mask_ref(c, h.prefer, -1);
-    h.prefer = 0;
+    h.hard_taints.clear();
+    h.prefer_taints.clear();
     for (uint32_t k = 0; k < s.n_taints; ++k) {
       const ks_taint &tt = s.taints[k];
       const uint32_t key = c->intern(tt.key), val = c->intern(tt.value);
-      if (tt.effect == KS_EFFECT_NO_SCHEDULE || tt.effect == KS_EFFECT_NO_EXECUTE) {
-        TaintKey tk{key, val, tt.effect};
-        auto it = c->hard_dict.find(tk);
-        uint32_t b;
-        if (it == c->hard_dict.end()) {
-          if (c->hard_list.size() >= 63) return c->fail(KS_ERR_CAPACITY, "more than 63 distinct hard taints");
-          b = (uint32_t)c->hard_list.size();
-          c->hard_dict.emplace(tk, b);
-          c->hard_list.push_back(tk);
-          grew = true;
-        } else {
-          b = it->second;
-        }
-        h.hard |= 1ull << b;
-      } else if (tt.effect == KS_EFFECT_PREFER_NO_SCHEDULE) {
-        auto pk = std::make_pair(key, val);
-        auto it = c->prefer_dict.find(pk);
-        uint32_t b;
-        if (it == c->prefer_dict.end()) {
-          if (c->prefer_list.size() >= 64) return c->fail(KS_ERR_CAPACITY, "more than 64 distinct prefer taints");
-          b = (uint32_t)c->prefer_list.size();
-          c->prefer_dict.emplace(pk, b);
-          c->prefer_list.push_back(pk);
-          grew = true;
-        } else {
-          b = it->second;
-        }
-        h.prefer |= 1ull << b;
-      }
+      if (tt.effect == KS_EFFECT_NO_SCHEDULE || tt.effect == KS_EFFECT_NO_EXECUTE)
+        h.hard_taints.push_back({key, val, (uint32_t)tt.effect});
+      else if (tt.effect == KS_EFFECT_PREFER_NO_SCHEDULE)
+        h.prefer_taints.emplace_back(key, val);
       // other effects are ignored by both TaintToleration filters and scores
+    }
+    bool rebuilt = false;
+    if (encode_taints(c, h, &grew) == KS_ERR_CAPACITY) {
+      // dictionary full of taints no present node may carry any more: rebuild
+      // it from the present nodes (this one included) and re-encode them all
+      if (ks_status st = rebuild_taint_dicts(c)) return st;
+      grew = rebuilt = true;
     }
     if ((h.hard & ~c->hard_in_use) || (h.prefer & ~c->prefer_in_use)) grew = true;
     c->hard_in_use |= h.hard;
     c->prefer_in_use |= h.prefer;
-    prefer_mask_ref(c, h.prefer, +1);
+    if (!rebuilt) prefer_mask_ref(c, h.prefer, +1);  // (the rebuild counted it)
     node_ext_bits(c, h);
     auto ins = row_of.emplace(slot, (uint32_t)pos.size());
     const uint32_t row = ins.first->second;
@@ -1825,15 +1905,33 @@ ks_status ks_events_apply(ks_ctx *c, const ks_event *ev, uint32_t n) {
   return KS_OK;
 }
 
+// Compile a batch's pods into dev / cl under c->mu.  When the label
+// dictionary runs out of bits, reclaim it once (reset_label_dict, after the
+// submitted batches drained) and compile the batch again from its first pod.
+static ks_status compile_batch(ks_ctx *c, const ks_pod *pods, uint32_t n, PodDev *dev, ProgBuf &cl,
+                               std::unique_lock<std::mutex> &lk) {
+  for (int attempt = 0;; ++attempt) {
+    cl.w.clear();
+    c->compile_used_names = false;
+    ks_status st = KS_OK;
+    for (uint32_t i = 0; i < n && !st; ++i) st = compile_pod(c, pods[i], dev[i], cl);
+    if (st != KS_ERR_CAPACITY || attempt > 0 || c->next_bit == 0) return st;
+    lk.unlock();
+    drain_async(c);
+    lk.lock();
+    reset_label_dict(c);
+  }
+}
+
 ks_status ks_pods_check(ks_ctx *c, const ks_pod *pods, uint32_t n, ks_status *status) {
   if (!c || (n && (!pods || !status))) return KS_ERR_INVALID;
-  std::lock_guard<std::mutex> g(c->mu);
+  std::unique_lock<std::mutex> g(c->mu);
   ks_status first = KS_OK;
   std::string first_err;
   for (uint32_t i = 0; i < n; ++i) {
     PodDev d;
     ProgBuf cl;
-    status[i] = compile_pod(c, pods[i], d, cl);
+    status[i] = compile_batch(c, &pods[i], 1, &d, cl, g);
     if (status[i] && !first) {
       first = status[i];
       std::lock_guard<std::mutex> ge(c->err_mu);
@@ -1856,10 +1954,9 @@ ks_status ks_batch_prepare(ks_ctx *c, const ks_pod *pods, uint32_t n, ks_batch *
   {
     // compile against the host dictionaries (the worker reads t.lw and the
     // dirty label rows under mu)
-    std::lock_guard<std::mutex> g(c->mu);
-    c->compile_used_names = false;
+    std::unique_lock<std::mutex> g(c->mu);
+    if ((st = compile_batch(c, pods, n, dev.data(), cl, g))) return st;
     for (uint32_t i = 0; i < n; ++i) {
-      if ((st = compile_pod(c, pods[i], dev[i], cl))) return st;
       if (dev[i].flags & PF_EXT) ext = true;
       if (dev[i].flags & (PF_TT | PF_NA)) norm = true;
     }
@@ -1981,8 +2078,8 @@ ks_status ks_plugin_scores(ks_ctx *c, const ks_pod *pod, ks_node_score *out) {
   ProgBuf cl;
   ks_status st;
   {
-    std::lock_guard<std::mutex> g(c->mu);
-    if ((st = compile_pod(c, *pod, d, cl))) return st;
+    std::unique_lock<std::mutex> g(c->mu);
+    if ((st = compile_batch(c, pod, 1, &d, cl, g))) return st;
     if ((st = upload_dirty_ext(c, c->xm))) return st;
   }
   if (cl.w.empty()) cl.w.push_back(0);
@@ -2138,8 +2235,12 @@ ks_status ks_debug_counters(ks_ctx *c, uint64_t out[16]) {
   if (ks_status dst_ = drain_async(c)) return dst_;
   HIPC(c, hipSetDevice(c->cfg.device));
   ks_status st;
-  if ((st = xfer_begin(c, 1024, 0)) || (st = d2h(c, out, c->d_counters, 16 * sizeof(uint64_t)))) return st;
-  return xfer_sync(c);
+  if ((st = xfer_begin(c, 1024, 0)) || (st = d2h(c, out, c->d_counters, 16 * sizeof(uint64_t))) ||
+      (st = xfer_sync(c)))
+    return st;
+  out[5] = c->label_resets;
+  out[6] = c->taint_rebuilds;
+  return KS_OK;
 }
 
 ks_status ks_set_timing(ks_ctx *c, int32_t enabled) {

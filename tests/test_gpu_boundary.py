@@ -180,3 +180,54 @@ def test_batch_pool_reuses_buffers_and_results_survive_other_runs():
         assert b3.value == b2.value
         s.free(b3)
         s.free(b1)
+
+
+def test_label_dictionary_reclaim_streams_beyond_256_bits():
+    # Batches over time use 480 distinct nodeSelector pairs (the label words
+    # hold 256 bits): the dictionary restarts empty when a batch cannot get
+    # its bits, nodes are re-encoded, and every batch still equals the oracle
+    from ksched.objects import Taint
+    n = 1200
+    nodes = [node(f"n{i}", cpu=8000 + 1000 * (i % 9), labels={"k": f"v{i % 480}", "z": f"z{i % 7}"},
+                  taints=[Taint("t", "x", "NoSchedule")] if i % 11 == 0 else [])
+             for i in range(n)]
+    a = Arena()
+    na, _ = nodes_array(nodes, a)
+    slots = (C.c_uint32 * n)(*range(n))
+    o = pyoracle.Oracle(n)
+    o.upsert(na, slots, n)
+    with Scheduler(n) as s:
+        s.upsert_nodes_raw(na, slots, n)
+        for b in range(8):
+            pods = [pod(f"p{b}-{j}", cpu=100 + j, node_selector={"k": f"v{(b * 60 + j) % 480}"},
+                        required_terms=[T([R("z", "NotIn", [f"z{(b + j) % 7}"])])] if j % 3 == 0 else None)
+                    for j in range(60)]
+            pa, m = pods_array(pods, a)
+            assert_results_equal(s.schedule_raw(pa, m), o.schedule(pa, m), m, f"batch {b}")
+        dbg = (C.c_uint64 * 16)()
+        assert s.lib.ks_debug_counters(s.ctx, dbg) == 0
+        assert dbg[5] >= 1, list(dbg)  # the label dictionary was reclaimed
+
+
+def test_taint_dictionary_rebuild_after_churn():
+    # 100 distinct NoSchedule taints over the cluster's life, at most 12 live:
+    # the 64-bit taint words are rebuilt from the present nodes
+    from ksched.objects import Taint, Toleration
+    n = 40
+    a = Arena()
+    o = pyoracle.Oracle(n)
+    with Scheduler(n) as s:
+        slots = (C.c_uint32 * n)(*range(n))
+        for gen in range(10):
+            nodes = [node(f"n{i}", taints=[Taint(f"t{gen * 10 + i % 12}", "", "NoSchedule")] if i % 3 else [])
+                     for i in range(n)]
+            na, _ = nodes_array(nodes, a)
+            assert s.lib.ks_nodes_upsert(s.ctx, na, slots, n) == 0, s.lib.ks_last_error(s.ctx)
+            o.upsert(na, slots, n)
+            pods = [pod(f"p{gen}-{j}", cpu=200, tolerations=[Toleration(f"t{gen * 10 + j % 12}", "Exists")])
+                    for j in range(30)]
+            pa, m = pods_array(pods, a)
+            assert_results_equal(s.schedule_raw(pa, m), o.schedule(pa, m), m, f"generation {gen}")
+        dbg = (C.c_uint64 * 16)()
+        assert s.lib.ks_debug_counters(s.ctx, dbg) == 0
+        assert dbg[6] >= 1, list(dbg)
