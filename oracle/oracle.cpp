@@ -563,6 +563,7 @@ struct oracle {
     int status;
     int64_t la, ba, tt_raw, na_raw;
   };
+  std::vector<Eval> ev;  // per-node scratch, reused across pods
 
   Eval eval(const PodState &st, const Node &n) const {
     Eval e{};
@@ -626,25 +627,43 @@ struct oracle {
     r.node_index = -1;
     PodState st = compile_pod(p);
     const uint32_t N = (uint32_t)nodes.size();
-    std::vector<Eval> ev(N);
-    for_nodes(0, N, [&](uint32_t a, uint32_t b, int) {
-      for (uint32_t i = a; i < b; ++i)
-        if (nodes[i].present) ev[i] = eval(st, nodes[i]);
+    ev.resize(N);
+    // Filter + raw scores in parallel (findNodesThatPassFilters / RunScorePlugins
+    // both fan out with parallelize.Until); counts and normaliser maxima are
+    // order-independent reductions, combined from per-thread partials.
+    struct Part {
+      uint32_t evaluated = 0, feasible = 0, only = 0;
+      uint32_t fail[KS_NUM_FAIL_COUNTS] = {};
+      int64_t tt_max = 0, na_max = 0;
+      uint64_t best = 0;
+    };
+    std::vector<Part> part(threads < 1 ? 1 : threads);
+    for_nodes(0, N, [&](uint32_t a, uint32_t b, int t) {
+      Part &q = part[t];
+      for (uint32_t i = a; i < b; ++i) {
+        if (!nodes[i].present) continue;
+        ev[i] = eval(st, nodes[i]);
+        ++q.evaluated;
+        if (ev[i].status >= 0) {
+          q.fail[ev[i].status]++;
+          continue;
+        }
+        ++q.feasible;
+        q.only = i;
+        q.tt_max = std::max(q.tt_max, ev[i].tt_raw);
+        q.na_max = std::max(q.na_max, ev[i].na_raw);
+      }
     });
     uint32_t evaluated = 0, feasible = 0;
     int64_t tt_max = 0, na_max = 0;
     uint32_t only = 0;
-    for (uint32_t i = 0; i < N; ++i) {
-      if (!nodes[i].present) continue;
-      ++evaluated;
-      if (ev[i].status >= 0) {
-        r.fail_counts[ev[i].status]++;
-        continue;
-      }
-      ++feasible;
-      only = i;
-      tt_max = std::max(tt_max, ev[i].tt_raw);
-      na_max = std::max(na_max, ev[i].na_raw);
+    for (const Part &q : part) {
+      evaluated += q.evaluated;
+      feasible += q.feasible;
+      if (q.feasible) only = q.only;
+      for (int k = 0; k < KS_NUM_FAIL_COUNTS; ++k) r.fail_counts[k] += q.fail[k];
+      tt_max = std::max(tt_max, q.tt_max);
+      na_max = std::max(na_max, q.na_max);
     }
     r.evaluated_nodes = evaluated;
     r.feasible_nodes = feasible;
@@ -665,12 +684,16 @@ struct oracle {
       r.status = KS_POD_ERROR;
       return r;
     }
+    for_nodes(0, N, [&](uint32_t a, uint32_t b, int t) {
+      uint64_t &best = part[t].best;
+      for (uint32_t i = a; i < b; ++i) {
+        if (!nodes[i].present || ev[i].status >= 0) continue;
+        uint64_t k = PackKey(total(st, ev[i], tt_max, na_max), i);
+        if (k > best) best = k;  // max TotalScore, tie -> lowest slot
+      }
+    });
     uint64_t best = 0;
-    for (uint32_t i = 0; i < N; ++i) {
-      if (!nodes[i].present || ev[i].status >= 0) continue;
-      uint64_t k = PackKey(total(st, ev[i], tt_max, na_max), i);
-      if (k > best) best = k;  // max TotalScore, tie -> lowest slot
-    }
+    for (const Part &q : part) best = std::max(best, q.best);
     r.node_index = (int32_t)(0xFFFFFFFFu - (uint32_t)best);
     r.total_score = (int64_t)(best >> 32) - 1;
     r.status = KS_POD_SCHEDULED;
