@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define KSCHED_ABI_VERSION 2
+#define KSCHED_ABI_VERSION 3
 
 /* ---------------------------------------------------------------- status */
 typedef int32_t ks_status;
@@ -145,6 +145,41 @@ typedef struct {
   int32_t _pad;
 } ks_preferred_term;
 
+/* metav1.LabelSelector (labels.Selector after LabelSelectorAsSelector): every
+ * match_labels pair and every expression (KS_OP_IN / NOT_IN / EXISTS /
+ * DOES_NOT_EXIST) must hold.  is_nil = 1: the selector field is nil, which
+ * selects no pod. */
+typedef struct {
+  const ks_label *match_labels;
+  const ks_requirement *match_expressions;
+  uint32_t n_match_labels;
+  uint32_t n_match_expressions;
+  uint32_t is_nil;
+  uint32_t _pad;
+} ks_label_selector;
+
+/* v1.UnsatisfiableConstraintAction and v1.NodeInclusionPolicy */
+enum { KS_DO_NOT_SCHEDULE = 0, KS_SCHEDULE_ANYWAY = 1 };
+enum { KS_INCLUSION_DEFAULT = 0 /* field nil */, KS_INCLUSION_HONOR = 1, KS_INCLUSION_IGNORE = 2 };
+
+/* v1.TopologySpreadConstraint (PodTopologySpread plugin, upstream
+ * pkg/scheduler/framework/plugins/podtopologyspread).  Defaults of nil
+ * fields as upstream's filterTopologySpreadConstraints: min_domains 0 = 1,
+ * node_affinity_policy Honor, node_taints_policy Ignore.  match_label_keys
+ * are merged into the selector with the incoming pod's values
+ * (MatchLabelKeysInPodTopologySpread, on by default in v1.31). */
+typedef struct {
+  const char *topology_key;
+  ks_label_selector selector;
+  const char *const *match_label_keys;
+  uint32_t n_match_label_keys;
+  int32_t max_skew;
+  int32_t when_unsatisfiable;   /* KS_DO_NOT_SCHEDULE / KS_SCHEDULE_ANYWAY   */
+  int32_t min_domains;          /* 0 = nil                                   */
+  int32_t node_affinity_policy; /* KS_INCLUSION_*                            */
+  int32_t node_taints_policy;   /* KS_INCLUSION_*                            */
+} ks_spread_constraint;
+
 /* Pod features whose plugins ksched does not model.
  * The caller sets the bit when the pod carries the feature; a pod with any
  * bit set is refused with KS_ERR_UNSUPPORTED (ks_pods_check names it) and
@@ -152,10 +187,9 @@ typedef struct {
  * default profile's plugins that read them: */
 enum {
   KS_UNMODELLED_HOST_PORTS = 1u,       /* NodePorts: a container port with hostPort != 0             */
-  KS_UNMODELLED_TOPOLOGY_SPREAD = 2u,  /* PodTopologySpread: topologySpreadConstraints, or the
-                                          system-default constraints apply (the pod is selected by a
-                                          Service or owned by a ReplicaSet / StatefulSet /
-                                          ReplicationController)                                    */
+  KS_UNMODELLED_TOPOLOGY_SPREAD = 2u,  /* PodTopologySpread constraints the caller could not express
+                                          as ks_pod.spread (ksched models the plugin itself: pass the
+                                          pod's constraints, or its system-default ones, there)      */
   KS_UNMODELLED_POD_AFFINITY = 4u,     /* InterPodAffinity: podAffinity / podAntiAffinity terms.  On
                                           a pod bound through ks_pods_add / KS_EV_POD_ADD it makes
                                           every later batch refuse until that pod is removed
@@ -190,6 +224,23 @@ typedef struct {
   uint32_t has_preferred; /* PreferredDuringSchedulingIgnoredDuringExecution != nil */
   uint32_t has_overhead;
   uint32_t unmodelled;    /* KS_UNMODELLED_* bits */
+  /* PodTopologySpread inputs.  labels / ns of a pod bound through ks_pods_add,
+   * KS_EV_POD_ADD or a batch are what later pods' spread selectors count
+   * (countPodsMatchSelector: same namespace, selector match).  spread holds
+   * the pod's topologySpreadConstraints; when it has none and upstream's
+   * system defaulting applies (the pod is selected by a Service or owned by a
+   * ReplicaSet / StatefulSet / ReplicationController: helper.DefaultSelector
+   * is non-empty), the caller passes the two system-default constraints
+   * (kubernetes.io/hostname maxSkew 3, topology.kubernetes.io/zone maxSkew 5,
+   * ScheduleAnyway, selector = DefaultSelector) and sets spread_defaulted = 1,
+   * which makes PreScore keep nodes lacking a topology key
+   * (requireAllTopologies = false). */
+  const ks_label *labels;              /* metadata.labels */
+  const ks_spread_constraint *spread;
+  uint32_t n_labels;
+  uint32_t n_spread;
+  uint32_t spread_defaulted;
+  uint32_t _pad2;
 } ks_pod;
 
 /* ------------------------------------------------------------- outputs */
@@ -200,7 +251,8 @@ enum {
   KS_PLUGIN_TAINT_TOLERATION = 2,
   KS_PLUGIN_NODE_AFFINITY = 3,
   KS_PLUGIN_NODE_RESOURCES_FIT = 4,
-  KS_NUM_FILTER_PLUGINS = 5
+  KS_PLUGIN_POD_TOPOLOGY_SPREAD = 5,
+  KS_NUM_FILTER_PLUGINS = 6
 };
 
 enum {
@@ -228,7 +280,6 @@ typedef struct {
   uint32_t fail_counts[KS_NUM_FAIL_COUNTS]; /* nodes rejected first by each filter plugin, then
                                                nodes excluded by the PreFilterResult */
   uint32_t flags;         /* KS_RESULT_*                                         */
-  uint32_t _pad;
 } ks_result;
 
 /* Per-node plugin scores of one pod (parity dump; NodePluginScores analogue). */
@@ -241,6 +292,8 @@ typedef struct {
   int32_t affinity_raw;         /* NodeAffinity raw                      */
   int32_t affinity_score;       /* NodeAffinity normalized               */
   int32_t image_locality;       /* ImageLocality (0: nodes report no images) */
+  int32_t spread_raw;           /* PodTopologySpread raw (0 when its PreScore skips) */
+  int32_t spread_score;         /* PodTopologySpread normalized          */
   int64_t total_score;          /* Σ weight × score over non-skipped plugins */
 } ks_node_score;
 
@@ -269,6 +322,7 @@ typedef struct {
   int32_t weight_taint;      /* TaintToleration                                 */
   int32_t weight_affinity;   /* NodeAffinity                                    */
   int32_t weight_image;      /* ImageLocality                                   */
+  /* (weight_topology_spread: after percentage_of_nodes_to_score) */
   /* KubeSchedulerProfile.percentageOfNodesToScore.  100 (the default here and
    * the reference's dist-scheduler/deployment.yaml:95) scores every node; any
    * other value (0 = upstream's adaptive 50 - N/125, the published run's 5 at
@@ -276,6 +330,7 @@ typedef struct {
    * KS_ERR_UNSUPPORTED: upstream's early stop is order- and parallelism-
    * dependent (schedule_one.go#numFeasibleNodesToFind / findNodesThatPassFilters). */
   int32_t percentage_of_nodes_to_score;
+  int32_t weight_topology_spread; /* PodTopologySpread (default profile: 2)     */
 } ks_config;
 
 typedef struct ks_ctx ks_ctx;

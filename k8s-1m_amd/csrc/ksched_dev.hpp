@@ -9,7 +9,8 @@ namespace ks {
 // ------------------------------------------------------------------ limits
 constexpr int LW = 4;           // label bitset words per node (256 dictionary bits)
 constexpr int NNUM = 2;         // numeric label columns (Gt / Lt operands)
-constexpr int NFILT = 5;        // filter plugins (KS_PLUGIN_*)
+constexpr int NFILT = 5;        // filter plugins of the round kernels (KS_PLUGIN_* 0..4)
+constexpr int PLUGIN_SPREAD = 5;  // KS_PLUGIN_POD_TOPOLOGY_SPREAD (spread path only)
 constexpr int WAVE = 64;
 constexpr int SWEEP_THREADS = 256;
 constexpr int BLOCK_KEYS = 4;   // candidates kept per sweep block and pod
@@ -21,8 +22,8 @@ constexpr uint64_t UNSCHED_BIT = 1ull << 63;  // hard-taint word: spec.unschedul
 constexpr int ST_FEASIBLE = -1;
 constexpr int ST_EMPTY = -2;
 // Outside NodeAffinity's PreFilterResult: no Filter plugin runs on the node
-// and no plugin is blamed (counted in ks_result.fail_counts[5] by the host).
-constexpr int ST_PREFILTERED = 5;
+// and no plugin is blamed (ks_result.fail_counts[KS_FAIL_PREFILTER_RESULT]).
+constexpr int ST_PREFILTERED = 6;
 
 // ---------------------------------------------------------- node table (SoA)
 // Columns are indexed by POSITION, not slot: a shard's slots are permuted so
@@ -68,7 +69,10 @@ enum PodFlags : uint32_t {
   PF_AFF = 64u,       // required program present (nodeSelector and/or required terms)
   PF_PREFILTER = 128u,   // NodeAffinity PreFilterResult: only nodes passing the prefilter program are evaluated
   PF_NA_CONFLICT = 256u, // NodeAffinity PreFilter rejects (conflicting metadata.name terms): every node fails NodeAffinity
+  PF_SPREAD = 512u,      // PodTopologySpread constraints: scheduled by the spread path (ksched_spread.hip)
+  PF_SPREAD_ALLKEYS = 1024u,  // PreScore requireAllTopologies (the pod's own constraints, not system defaults)
 };
+constexpr uint32_t PF_NSPREAD_SHIFT = 24;  // flags >> 24: number of SpreadDev records at spread_off
 
 struct alignas(16) PodDev {
   int64_t req_cpu, req_mem;  // PodRequests (Fit filter, BalancedAllocation)
@@ -81,7 +85,7 @@ struct alignas(16) PodDev {
   int32_t name_slot;         // spec.nodeName: -1 unset, -2 names no node, else slot
   uint32_t req_off, req_len; // required program: word offset in the label-program buffer, terms (OR)
   uint32_t pref_off, pref_len;  // preferred program: word offset, terms (weighted sum)
-  uint32_t n_req_terms;      // required terms emitted (diagnostic)
+  uint32_t spread_off;       // word offset of the pod's SpreadDev records in the label-program buffer
   // Normalising-plugin maxima the sweep scores with (PF_TT / PF_NA): the host's
   // guess of max raw over feasible nodes.  The merge measures the true maxima;
   // pods whose guess was wrong are re-swept with them (norm_check, fix sweep).
@@ -113,6 +117,43 @@ __host__ __device__ inline uint32_t term_words(uint64_t w0) {
   const uint32_t ng = (uint32_t)w0 & 0xFF, nn = ((uint32_t)w0 >> 8) & 0xFF, nm = ((uint32_t)w0 >> 16) & 0xFF;
   return TERM_HDR_WORDS + ng * LW + 2 * (nn + nm);
 }
+
+// PodTopologySpread (ksched_spread.hip).  A pod's constraints, compiled on the
+// host: the topology key's domain-id column, the selector's class column
+// (matching bound pods per node), and the constraint's parameters.
+constexpr int MAX_SPREAD = 8;        // constraints per pod
+constexpr int MAX_TOPO_KEYS = 16;    // topology-key domain columns
+constexpr int MAX_CLASSES = 64;      // selector-class count columns
+constexpr uint32_t DOM_NONE = 0xFFFFFFFFu;  // node lacks the topology key
+constexpr uint32_t CLS_NONE = 0xFFFFFFFFu;  // Empty() / Nothing() selector: counts are 0
+enum SpreadFlags : uint32_t {
+  SP_SCORE = 1u,   // ScheduleAnyway (Score); else DoNotSchedule (Filter)
+  SP_AFF = 2u,     // nodeAffinityPolicy Honor
+  SP_TAINT = 4u,   // nodeTaintsPolicy Honor
+  SP_SELF = 8u,    // the selector matches the incoming pod's own labels
+  SP_HOST = 16u,   // topologyKey == kubernetes.io/hostname (Score counts per node)
+};
+struct alignas(16) SpreadDev {
+  uint32_t key;        // topology-key column
+  uint32_t cls;        // selector-class column or CLS_NONE
+  int32_t max_skew, min_domains;
+  uint32_t flags;      // SP_*
+  uint32_t _pad[3];
+};
+static_assert(sizeof(SpreadDev) == 32, "SpreadDev layout");
+constexpr uint32_t SPREAD_WORDS = sizeof(SpreadDev) / 8;
+
+// Per-pod accumulators of the spread path (reset by its commit kernel).
+struct SpreadAcc {
+  uint32_t fail[NFILT + 1];            // first failures per plugin (+ PodTopologySpread)
+  uint32_t feasible, ignored;          // feasible nodes; feasible nodes PreScore ignores
+  uint32_t tt_max, na_max;             // max raw TaintToleration / NodeAffinity over feasible nodes
+  uint32_t min_match[MAX_SPREAD];      // Filter: min matching pods over eligible domains
+  uint32_t ndomains[MAX_SPREAD];       // Filter: eligible domains
+  uint32_t topo_size[MAX_SPREAD];      // Score: domains of non-ignored feasible nodes
+  uint64_t pts_min, pts_max;           // Score: raw PodTopologySpread min / max over non-ignored feasible nodes
+  uint64_t best;                       // packed key of the winner
+};
 
 // ----------------------------------------------------------- round records
 // Per (pod-in-round, sweep block): best keys of the block + bound + counts.
@@ -188,9 +229,9 @@ struct DevResult {
   uint32_t feasible_nodes;
   uint32_t evaluated_nodes;
   uint32_t fail_counts[NFILT];
+  uint32_t spread_fail;  // ks_result.fail_counts[KS_PLUGIN_POD_TOPOLOGY_SPREAD]
   uint32_t prefiltered;  // ks_result.fail_counts[KS_FAIL_PREFILTER_RESULT]
   uint32_t flags;
-  uint32_t _pad;
 };
 static_assert(sizeof(DevResult) == 56, "DevResult layout");
 

@@ -153,6 +153,36 @@ struct HostNode {
   // taints as interned ids (the taint dictionaries are rebuilt from these)
   std::vector<std::array<uint32_t, 3>> hard_taints;            // key, value, effect
   std::vector<std::pair<uint32_t, uint32_t>> prefer_taints;    // key, value
+  // NodeInfo.Pods as interned (namespace, labels) sets, one entry per bound pod
+  // (PodTopologySpread counts them through selector classes)
+  std::vector<uint32_t> pod_sets;
+};
+
+// PodTopologySpread host state.  A bound pod's (namespace, labels) is interned
+// as a label set; a spread constraint's (namespace, selector) is a selector
+// CLASS with a device column of matching bound pods per node; a topology key
+// has a device column of per-node domain ids (value -> id, "" = 0).
+struct LabelSet {
+  uint32_t ns;
+  std::vector<std::pair<uint32_t, uint32_t>> labels;  // sorted (key id, value id)
+};
+struct SelReq {
+  uint32_t key;
+  int32_t op;                   // KS_OP_IN / NOT_IN / EXISTS / DOES_NOT_EXIST
+  std::vector<uint32_t> vals;   // sorted value ids
+};
+struct SpreadClass {
+  bool live = false;
+  uint32_t ns = 0;
+  std::vector<SelReq> reqs;
+  std::string canon;
+  uint32_t refs = 0;            // prepared batches using the class
+  uint64_t last_use = 0;
+};
+struct TopoKey {
+  uint32_t key = 0;
+  std::unordered_map<uint32_t, uint32_t> dom;  // value id -> domain id ("" -> 0)
+  uint32_t ndom = 1;
 };
 
 struct TaintKey {
@@ -193,6 +223,15 @@ struct ks_batch {
   uint64_t *h_clauses = nullptr;
   size_t n_words = 0;
   bool uploaded = false;
+  // PodTopologySpread: per-pod label-set ids (bound pods are recorded at the
+  // end of the run), spread-path flags (1 spread pod, 2 DoNotSchedule
+  // constraints, 4 ScheduleAnyway constraints), the selector classes the
+  // batch references, and the pods' class masks (computed at run time)
+  std::vector<uint32_t> set_ids;
+  std::vector<uint8_t> spread;
+  bool any_spread = false;
+  std::vector<uint32_t> class_refs;
+  uint64_t *d_cmask = nullptr, *h_cmask = nullptr;
   // asynchronous run state (ks_batch_submit / ks_batch_wait)
   bool queued = false, done = false;
   ks_status run_status = KS_OK;
@@ -268,6 +307,23 @@ struct ks_ctx {
   std::unordered_map<std::string, uint32_t> images;
   // bound pods carrying pod (anti-)affinity terms (InterPodAffinity precondition)
   int64_t affinity_pods = 0;
+  // PodTopologySpread (ksched_spread.hip; device columns allocated on first use)
+  std::map<std::pair<uint32_t, std::vector<std::pair<uint32_t, uint32_t>>>, uint32_t> set_ids;
+  std::vector<LabelSet> label_sets;
+  SpreadClass classes[MAX_CLASSES];
+  std::unordered_map<std::string, uint32_t> class_of;  // canonical selector -> class
+  uint64_t class_seq = 0;
+  std::vector<TopoKey> topo;                            // topology-key columns
+  std::unordered_map<uint32_t, uint32_t> topo_of;       // key id -> column
+  uint32_t *d_dom = nullptr;       // [MAX_TOPO_KEYS][npos]
+  uint32_t *d_cnt = nullptr;       // [MAX_CLASSES][npos]
+  uint32_t *d_pos_slot = nullptr;  // [npos]
+  uint32_t *d_dcnt = nullptr, *d_dflag = nullptr;  // [MAX_SPREAD][dom_cap]
+  uint32_t dom_cap = 0;
+  SpreadAcc *d_acc = nullptr;
+  int8_t *d_sst = nullptr;
+  int64_t *d_sraw = nullptr;
+  uint32_t *h_seg = nullptr;       // pinned: start pod of a round-kernel segment
   // comm
   ncclComm_t comm = nullptr;
   // stats
@@ -791,7 +847,11 @@ ks_status check_modelled(ks_ctx *c, const ks_pod &p) {
   return KS_OK;
 }
 
-ks_status compile_pod(ks_ctx *c, const ks_pod &p, PodDev &d, ProgBuf &cl) {
+ks_status spread_compile(ks_ctx *c, const ks_pod &p, PodDev &d, ProgBuf &cl, bool create,
+                         std::vector<uint32_t> *refs);
+
+ks_status compile_pod(ks_ctx *c, const ks_pod &p, PodDev &d, ProgBuf &cl, bool create_spread = false,
+                      std::vector<uint32_t> *class_refs = nullptr) {
   std::memset(&d, 0, sizeof d);
   ks_status st;
   if ((st = check_modelled(c, p))) return st;
@@ -878,7 +938,7 @@ ks_status compile_pod(ks_ctx *c, const ks_pod &p, PodDev &d, ProgBuf &cl) {
     sel.emit(cl, 0);
     d.req_len = 1;
   }
-  d.n_req_terms = d.req_len;
+  d.spread_off = 0;
   {
     std::vector<std::string> names;
     if (prefilter_names(p, &names)) {
@@ -926,6 +986,7 @@ ks_status compile_pod(ks_ctx *c, const ks_pod &p, PodDev &d, ProgBuf &cl) {
   }
   if ((c->hard_in_use & ~d.tol_hard) || d.name_slot != -1 || (d.flags & (PF_AFF | PF_TT | PF_NA)))
     d.flags |= PF_EXT;
+  if (p.n_spread) return spread_compile(c, p, d, cl, create_spread, class_refs);
   return KS_OK;
 }
 
@@ -1061,6 +1122,387 @@ uint32_t kernel_npl(const ks_ctx *c, bool ext) {
   return ext ? std::min<uint32_t>(c->npl, c->ext_npl) : c->npl;
 }
 
+
+// ====================================================== PodTopologySpread
+// Host side of the spread path (ksched_spread.hip): label sets of bound pods,
+// selector classes, topology-key domain columns, and the compilation of a
+// pod's constraints (upstream podtopologyspread/common.go
+// #filterTopologySpreadConstraints, LabelSelectorAsSelector,
+// mergeLabelSetWithSelector).
+
+// Interned (namespace, labels) of a pod.
+uint32_t intern_set(ks_ctx *c, const ks_pod &p) {
+  std::vector<std::pair<uint32_t, uint32_t>> l;
+  l.reserve(p.n_labels);
+  for (uint32_t k = 0; k < p.n_labels; ++k) l.emplace_back(c->intern(p.labels[k].key), c->intern(p.labels[k].value));
+  std::sort(l.begin(), l.end());
+  auto key = std::make_pair(c->intern(p.ns), std::move(l));
+  auto it = c->set_ids.find(key);
+  if (it != c->set_ids.end()) return it->second;
+  const uint32_t id = (uint32_t)c->label_sets.size();
+  c->label_sets.push_back(LabelSet{key.first, key.second});
+  c->set_ids.emplace(std::move(key), id);
+  return id;
+}
+
+// labels.Selector.Matches over sorted (key, value) ids.
+bool reqs_match(const std::vector<SelReq> &reqs, const std::vector<std::pair<uint32_t, uint32_t>> &labels) {
+  for (const SelReq &r : reqs) {
+    auto it = std::lower_bound(labels.begin(), labels.end(), std::make_pair(r.key, 0u));
+    const bool has = it != labels.end() && it->first == r.key;
+    const bool in = has && std::binary_search(r.vals.begin(), r.vals.end(), it->second);
+    switch (r.op) {
+      case KS_OP_IN: if (!in) return false; break;
+      case KS_OP_NOT_IN: if (in) return false; break;
+      case KS_OP_EXISTS: if (!has) return false; break;
+      default: if (has) return false; break;  // DoesNotExist
+    }
+  }
+  return true;
+}
+
+bool class_matches(const ks_ctx *c, const SpreadClass &k, uint32_t set) {
+  const LabelSet &ls = c->label_sets[set];
+  return ls.ns == k.ns && reqs_match(k.reqs, ls.labels);
+}
+
+ks_status spread_scratch(ks_ctx *c, uint32_t need) {
+  if (need <= c->dom_cap) return KS_OK;
+  // callers have drained every submitted batch (hipFree waits for the device)
+  HIPC(c, hipStreamSynchronize(c->stream));
+  if (c->d_dcnt) (void)hipFree(c->d_dcnt);
+  if (c->d_dflag) (void)hipFree(c->d_dflag);
+  c->d_dcnt = c->d_dflag = nullptr;
+  const uint32_t cap = std::max<uint32_t>({need, 2 * c->dom_cap, 1024});
+  ks_status st;
+  if ((st = dalloc(c, &c->d_dcnt, (size_t)MAX_SPREAD * cap)) || (st = dalloc(c, &c->d_dflag, (size_t)MAX_SPREAD * cap)))
+    return st;
+  c->dom_cap = cap;
+  return KS_OK;
+}
+
+ks_status spread_alloc(ks_ctx *c) {
+  if (c->d_dom) return KS_OK;
+  ks_status st;
+  // domain columns then class columns, one allocation (one index space for scatters)
+  if ((st = dalloc(c, &c->d_dom, (size_t)(MAX_TOPO_KEYS + MAX_CLASSES) * c->npos)) || (st = dalloc(c, &c->d_pos_slot, c->npos)) ||
+      (st = dalloc(c, &c->d_acc, 1)) || (st = dalloc(c, &c->d_sst, c->npos)) || (st = dalloc(c, &c->d_sraw, c->npos)))
+    return st;
+  c->d_cnt = c->d_dom + (size_t)MAX_TOPO_KEYS * c->npos;
+  HIPC(c, hipMemsetAsync(c->d_dom, 0xFF, (size_t)MAX_TOPO_KEYS * c->npos * 4, c->stream));
+  std::vector<uint32_t> ps(c->npos, SLOT_NONE);
+  for (uint32_t sl = 0; sl < c->cap; ++sl) ps[c->slot_pos[sl]] = sl;
+  SpreadAcc acc{};
+  for (int k = 0; k < MAX_SPREAD; ++k) acc.min_match[k] = 0xFFFFFFFFu;
+  acc.pts_min = ~0ull;
+  if ((st = xfer_begin(c, (size_t)c->npos * 4 + sizeof acc + 1024, 0)) ||
+      (st = h2d(c, c->d_pos_slot, ps.data(), (size_t)c->npos * 4)) || (st = h2d(c, c->d_acc, &acc, sizeof acc)) ||
+      (st = xfer_sync(c)))
+    return st;
+  return spread_scratch(c, 1024);
+}
+
+// Domain id of a node for one topology key (DOM_NONE: no such label; the value
+// "" is domain 0); new values get the next id.
+uint32_t node_domain(TopoKey &k, const HostNode &h) {
+  for (auto &kv : h.labels) {
+    if (kv.first != k.key) continue;
+    if (kv.second == 0) return 0;
+    auto it = k.dom.find(kv.second);
+    if (it != k.dom.end()) return it->second;
+    const uint32_t id = k.ndom++;
+    k.dom.emplace(kv.second, id);
+    return id;
+  }
+  return DOM_NONE;
+}
+
+// (Re)build topology-key column `ti` from the present nodes.
+ks_status topo_build(ks_ctx *c, uint32_t ti) {
+  TopoKey &k = c->topo[ti];
+  k.dom.clear();
+  k.ndom = 1;
+  std::vector<uint32_t> col(c->npos, DOM_NONE);
+  for (uint32_t sl = 0; sl < c->cap; ++sl)
+    if (c->nodes[sl].present) col[c->slot_pos[sl]] = node_domain(k, c->nodes[sl]);
+  ks_status st;
+  if ((st = spread_scratch(c, k.ndom)) || (st = xfer_begin(c, (size_t)c->npos * 4 + 1024, 0)) ||
+      (st = h2d(c, c->d_dom + (size_t)ti * c->npos, col.data(), (size_t)c->npos * 4)) || (st = xfer_sync(c)))
+    return st;
+  return KS_OK;
+}
+
+// Column of a topology key (created when `create`; the caller has drained).
+ks_status topo_column(ks_ctx *c, uint32_t key, bool create, uint32_t *out) {
+  auto it = c->topo_of.find(key);
+  if (it != c->topo_of.end()) {
+    *out = it->second;
+    return KS_OK;
+  }
+  if (!create) {
+    *out = 0;
+    return KS_OK;
+  }
+  if (c->topo.size() >= (size_t)MAX_TOPO_KEYS)
+    return c->fail(KS_ERR_CAPACITY, "more than %d topology keys in spread constraints", MAX_TOPO_KEYS);
+  ks_status st;
+  if ((st = spread_alloc(c))) return st;
+  const uint32_t ti = (uint32_t)c->topo.size();
+  c->topo.emplace_back();
+  c->topo.back().key = key;
+  c->topo_of.emplace(key, ti);
+  if ((st = topo_build(c, ti))) return st;
+  *out = ti;
+  return KS_OK;
+}
+
+// Selector class of (namespace, requirements): its column counts the bound
+// pods of every node that the selector matches (created when `create`, from
+// the host's records of bound pods; the caller has drained).
+ks_status class_get(ks_ctx *c, uint32_t ns, std::vector<SelReq> &&reqs, bool create, uint32_t *out) {
+  std::string canon = std::to_string(ns);
+  for (auto &r : reqs) {
+    canon += '|' + std::to_string(r.key) + ':' + std::to_string(r.op);
+    for (uint32_t v : r.vals) canon += ',' + std::to_string(v);
+  }
+  auto it = c->class_of.find(canon);
+  if (it != c->class_of.end()) {
+    *out = it->second;
+    c->classes[it->second].last_use = ++c->class_seq;
+    return KS_OK;
+  }
+  if (!create) {
+    *out = CLS_NONE;
+    return KS_OK;
+  }
+  ks_status st;
+  if ((st = spread_alloc(c))) return st;
+  int slot = -1;
+  for (int k = 0; k < MAX_CLASSES && slot < 0; ++k)
+    if (!c->classes[k].live) slot = k;
+  if (slot < 0) {  // evict the least recently used class no prepared batch references
+    uint64_t best = UINT64_MAX;
+    for (int k = 0; k < MAX_CLASSES; ++k)
+      if (c->classes[k].refs == 0 && c->classes[k].last_use < best) {
+        best = c->classes[k].last_use;
+        slot = k;
+      }
+    if (slot < 0)
+      return c->fail(KS_ERR_CAPACITY, "%d spread selector classes referenced by prepared batches", MAX_CLASSES);
+    c->class_of.erase(c->classes[slot].canon);
+  }
+  SpreadClass &k = c->classes[slot];
+  k = SpreadClass{};
+  k.live = true;
+  k.ns = ns;
+  k.reqs = std::move(reqs);
+  k.canon = canon;
+  k.last_use = ++c->class_seq;
+  c->class_of.emplace(canon, (uint32_t)slot);
+  std::vector<int8_t> match(c->label_sets.size(), -1);
+  std::vector<uint32_t> col(c->npos, 0);
+  for (uint32_t sl = 0; sl < c->cap; ++sl) {
+    const HostNode &h = c->nodes[sl];
+    if (!h.present) continue;
+    uint32_t n = 0;
+    for (uint32_t set : h.pod_sets) {
+      if (match[set] < 0) match[set] = class_matches(c, k, set) ? 1 : 0;
+      n += (uint32_t)match[set];
+    }
+    col[c->slot_pos[sl]] = n;
+  }
+  if ((st = xfer_begin(c, (size_t)c->npos * 4 + 1024, 0)) ||
+      (st = h2d(c, c->d_cnt + (size_t)slot * c->npos, col.data(), (size_t)c->npos * 4)) || (st = xfer_sync(c)))
+    return st;
+  *out = (uint32_t)slot;
+  return KS_OK;
+}
+
+// metav1.LabelSelectorAsSelector: false on a parse error.
+bool parse_label_selector(ks_ctx *c, const ks_label_selector &ls, std::vector<SelReq> *reqs) {
+  auto add = [&](const char *key, int32_t op, const char *const *vals, uint32_t nv) {
+    const std::string k = str(key);
+    if (!qualified_name_ok(k)) return false;
+    if ((op == KS_OP_IN || op == KS_OP_NOT_IN) && nv == 0) return false;
+    if ((op == KS_OP_EXISTS || op == KS_OP_DOES_NOT_EXIST) && nv != 0) return false;
+    SelReq r{c->intern(key), op, {}};
+    for (uint32_t i = 0; i < nv; ++i) {
+      if (!label_value_ok(str(vals[i]))) return false;
+      r.vals.push_back(c->intern(vals[i]));
+    }
+    std::sort(r.vals.begin(), r.vals.end());
+    r.vals.erase(std::unique(r.vals.begin(), r.vals.end()), r.vals.end());
+    reqs->push_back(std::move(r));
+    return true;
+  };
+  for (uint32_t i = 0; i < ls.n_match_labels; ++i) {
+    const char *v = ls.match_labels[i].value;
+    if (!add(ls.match_labels[i].key, KS_OP_IN, &v, 1)) return false;  // selection.Equals
+  }
+  for (uint32_t i = 0; i < ls.n_match_expressions; ++i) {
+    const ks_requirement &e = ls.match_expressions[i];
+    if (e.op != KS_OP_IN && e.op != KS_OP_NOT_IN && e.op != KS_OP_EXISTS && e.op != KS_OP_DOES_NOT_EXIST)
+      return false;  // "is not a valid label selector operator"
+    if (!add(e.key, e.op, e.values, e.n_values)) return false;
+  }
+  return true;
+}
+
+// A pod's spread constraints -> SpreadDev records in the program buffer.
+// Invalid constraints (the apiserver would reject them; upstream's PreFilter /
+// PreScore would return an Error) are refused with KS_ERR_UNSUPPORTED, so
+// the shim hands the pod to upstream.  Without `create` (ks_pods_check) only
+// validates.
+ks_status spread_compile(ks_ctx *c, const ks_pod &p, PodDev &d, ProgBuf &cl, bool create,
+                         std::vector<uint32_t> *refs) {
+  const std::string pn = str(p.ns) + "/" + str(p.name);
+  if (c->cfg.world_size > 1)
+    return c->fail(KS_ERR_UNSUPPORTED, "pod %s: topology spread constraints need a single-rank context", pn.c_str());
+  if (p.n_spread > (uint32_t)MAX_SPREAD)
+    return c->fail(KS_ERR_UNSUPPORTED, "pod %s: more than %d topology spread constraints", pn.c_str(), MAX_SPREAD);
+  std::vector<std::pair<uint32_t, uint32_t>> own;  // the pod's labels (selfMatch)
+  for (uint32_t k = 0; k < p.n_labels; ++k) own.emplace_back(c->intern(p.labels[k].key), c->intern(p.labels[k].value));
+  std::sort(own.begin(), own.end());
+  const uint32_t host_key = c->intern("kubernetes.io/hostname");
+  std::vector<SpreadDev> recs;
+  std::set<std::pair<uint32_t, int32_t>> seen;
+  bool any_filter = false, any_score = false;
+  for (uint32_t i = 0; i < p.n_spread; ++i) {
+    const ks_spread_constraint &sc = p.spread[i];
+    const uint32_t key = c->intern(sc.topology_key);
+    if (!sc.topology_key || !sc.topology_key[0] || sc.max_skew < 1 ||
+        (sc.when_unsatisfiable != KS_DO_NOT_SCHEDULE && sc.when_unsatisfiable != KS_SCHEDULE_ANYWAY) ||
+        sc.min_domains < 0 || (sc.min_domains > 0 && sc.when_unsatisfiable != KS_DO_NOT_SCHEDULE) ||
+        sc.node_affinity_policy < 0 || sc.node_affinity_policy > 2 || sc.node_taints_policy < 0 ||
+        sc.node_taints_policy > 2 || !seen.emplace(key, sc.when_unsatisfiable).second)
+      return c->fail(KS_ERR_UNSUPPORTED, "pod %s: topology spread constraint %u is invalid", pn.c_str(), i);
+    SpreadDev r{};
+    r.max_skew = sc.max_skew;
+    r.min_domains = sc.min_domains ? sc.min_domains : 1;
+    const bool score = sc.when_unsatisfiable == KS_SCHEDULE_ANYWAY;
+    r.flags = (score ? SP_SCORE : 0u) | (key == host_key ? SP_HOST : 0u) |
+              (sc.node_affinity_policy != KS_INCLUSION_IGNORE ? SP_AFF : 0u) |
+              (sc.node_taints_policy == KS_INCLUSION_HONOR ? SP_TAINT : 0u);
+    (score ? any_score : any_filter) = true;
+    // selector (+ matchLabelKeys with the pod's own values; Nothing() stays Nothing())
+    std::vector<SelReq> reqs;
+    const bool nothing = sc.selector.is_nil != 0;
+    if (!nothing && !parse_label_selector(c, sc.selector, &reqs))
+      return c->fail(KS_ERR_UNSUPPORTED, "pod %s: topology spread constraint %u has an invalid label selector",
+                     pn.c_str(), i);
+    if (!nothing) {
+      for (uint32_t k = 0; k < sc.n_match_label_keys; ++k) {
+        const uint32_t mk = c->intern(sc.match_label_keys[k]);
+        auto it = std::lower_bound(own.begin(), own.end(), std::make_pair(mk, 0u));
+        if (it != own.end() && it->first == mk) reqs.push_back(SelReq{mk, KS_OP_IN, {it->second}});
+      }
+      std::sort(reqs.begin(), reqs.end(), [](const SelReq &a, const SelReq &b) {
+        return std::tie(a.key, a.op, a.vals) < std::tie(b.key, b.op, b.vals);
+      });
+      reqs.erase(std::unique(reqs.begin(), reqs.end(),
+                             [](const SelReq &a, const SelReq &b) {
+                               return a.key == b.key && a.op == b.op && a.vals == b.vals;
+                             }),
+                 reqs.end());
+    }
+    if (!nothing && reqs_match(reqs, own)) r.flags |= SP_SELF;
+    r.cls = CLS_NONE;  // Nothing() matches no pod; Empty() counts 0 (countPodsMatchSelector)
+    ks_status st;
+    if (!nothing && !reqs.empty()) {
+      if ((st = class_get(c, c->intern(p.ns), std::move(reqs), create, &r.cls))) return st;
+      if (create && refs) refs->push_back(r.cls);
+    }
+    if ((st = topo_column(c, key, create, &r.key))) return st;
+    recs.push_back(r);
+  }
+  if (!create) return KS_OK;
+  if (cl.w.size() & 1) cl.w.push_back(0);  // SpreadDev is 16-byte aligned
+  d.spread_off = (uint32_t)cl.w.size();
+  for (const SpreadDev &r : recs) {
+    uint64_t w[SPREAD_WORDS];
+    std::memcpy(w, &r, sizeof r);
+    cl.w.insert(cl.w.end(), w, w + SPREAD_WORDS);
+  }
+  d.flags |= PF_SPREAD | (p.n_spread << PF_NSPREAD_SHIFT) | (p.spread_defaulted ? 0u : PF_SPREAD_ALLKEYS);
+  (void)any_filter;
+  (void)any_score;
+  return KS_OK;
+}
+
+// Device deltas of the selector-class columns for pods bound / removed on
+// slots (sign +1 / -1), and the host records.
+ks_status spread_pods_delta(ks_ctx *c, const ks_pod *pods, const uint32_t *slots, uint32_t n, int sign) {
+  std::vector<uint64_t> idx;
+  std::vector<int32_t> dv;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t set = intern_set(c, pods[i]);
+    HostNode &h = c->nodes[slots[i]];
+    if (sign > 0) {
+      h.pod_sets.push_back(set);
+    } else {
+      auto it = std::find(h.pod_sets.begin(), h.pod_sets.end(), set);
+      if (it == h.pod_sets.end()) continue;  // never bound here: no count to remove
+      h.pod_sets.erase(it);
+    }
+    for (int k = 0; k < MAX_CLASSES; ++k)
+      if (c->classes[k].live && class_matches(c, c->classes[k], set)) {
+        idx.push_back((uint64_t)k * c->npos + c->slot_pos[slots[i]]);
+        dv.push_back(sign);
+      }
+  }
+  if (idx.empty()) return KS_OK;
+  const size_t bytes = idx.size() * 12 + 1024;
+  ks_status st = xfer_begin(c, bytes, bytes);
+  if (st) return st;
+  uint64_t *d_idx = dscratch<uint64_t>(c, idx.size());
+  int32_t *d_dv = dscratch<int32_t>(c, dv.size());
+  if ((st = h2d(c, d_idx, idx.data(), idx.size() * 8)) || (st = h2d(c, d_dv, dv.data(), dv.size() * 4))) return st;
+  HIPC(c, launch_add_u32(c->d_cnt, d_idx, d_dv, (uint32_t)idx.size(), c->stream));
+  return xfer_sync(c);
+}
+
+// Topology-key and class columns of nodes upserted (their labels may have
+// changed; their bound pods stay) or deleted (pods leave with the node).
+ks_status spread_nodes_changed(ks_ctx *c, const uint32_t *slots, uint32_t n, bool deleted) {
+  if (!c->d_dom || !n) return KS_OK;
+  std::vector<uint64_t> idx;
+  std::vector<uint32_t> val;
+  std::vector<uint32_t> rebuild;
+  for (uint32_t ti = 0; ti < c->topo.size(); ++ti) {
+    TopoKey &k = c->topo[ti];
+    for (uint32_t i = 0; i < n; ++i) {
+      idx.push_back((uint64_t)ti * c->npos + c->slot_pos[slots[i]]);
+      val.push_back(deleted ? DOM_NONE : node_domain(k, c->nodes[slots[i]]));
+    }
+    if (k.ndom > 2 * c->cap + 1024) rebuild.push_back(ti);  // churned values: renumber
+  }
+  if (deleted)
+    for (int k = 0; k < MAX_CLASSES; ++k)
+      if (c->classes[k].live)
+        for (uint32_t i = 0; i < n; ++i) {
+          idx.push_back((uint64_t)c->npos * MAX_TOPO_KEYS + (uint64_t)k * c->npos + c->slot_pos[slots[i]]);
+          val.push_back(0);
+        }
+  ks_status st;
+  uint32_t need = 0;
+  for (auto &k : c->topo) need = std::max(need, k.ndom);
+  if ((st = spread_scratch(c, need))) return st;
+  if (!idx.empty()) {
+    const size_t bytes = idx.size() * 12 + 1024;
+    if ((st = xfer_begin(c, bytes, bytes))) return st;
+    uint64_t *d_idx = dscratch<uint64_t>(c, idx.size());
+    uint32_t *d_val = dscratch<uint32_t>(c, val.size());
+    if ((st = h2d(c, d_idx, idx.data(), idx.size() * 8)) || (st = h2d(c, d_val, val.data(), val.size() * 4)))
+      return st;
+    // one index space: topology columns, then (offset by MAX_TOPO_KEYS columns) class columns
+    HIPC(c, launch_scatter_u32(c->d_dom, d_idx, d_val, (uint32_t)idx.size(), c->stream));
+    if ((st = xfer_sync(c))) return st;
+  }
+  for (uint32_t ti : rebuild)
+    if ((st = topo_build(c, ti))) return st;
+  return KS_OK;
+}
+
 hipEvent_t get_event(ks_ctx *c) {
   if (!c->ev_pool.empty()) {
     hipEvent_t e = c->ev_pool.back();
@@ -1118,7 +1560,7 @@ static ks_status hand_wait(ks_ctx *c, hipStream_t wt, int f, hipEvent_t ev, uint
 //            (RCCL), merge_shards k, gather k, [wait resolve k-1, patch k],
 //            record ev_sw[k]
 //   rstream: wait ev_sw[k], resolve k, record ev_res[k]
-ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k) {
+ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k, uint32_t end) {
   // Timing events cost the main stream ~10 us of dispatch per sweep, so only
   // every KS_TIMING_EVERY-th round (default 8) is timed.
   const bool tm = c->timing && (c->round_seq + 1) % c->timing_every == 0;
@@ -1154,7 +1596,7 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k) {
   a.P = c->P;
   a.pg = pg;
   a.K = c->K;
-  a.npods = b->n;
+  a.npods = end;  // the segment ends here (pods after it go to the spread path)
   a.bstride = bmax;
   a.evaluated = c->n_present;
   a.pods = b->d_pods;
@@ -1329,6 +1771,8 @@ ks_status batch_acquire(ks_ctx *c, uint32_t n, size_t words, ks_batch **out) {
     HIPC(c, hipHostMalloc((void **)&b->h_results, (size_t)need * sizeof(DevResult), hipHostMallocDefault));
     HIPC(c, hipHostMalloc((void **)&b->h_pods, (size_t)need * sizeof(PodDev), hipHostMallocDefault));
     HIPC(c, hipHostMalloc((void **)&b->h_pinv, (size_t)need * 2 * sizeof(double), hipHostMallocDefault));
+    HIPC(c, hipMalloc((void **)&b->d_cmask, (size_t)need * 8));
+    HIPC(c, hipHostMalloc((void **)&b->h_cmask, (size_t)need * 8, hipHostMallocDefault));
     b->cap_pods = need;
   }
   if (words > b->cap_words) {
@@ -1385,25 +1829,101 @@ ks_status run_batch(ks_ctx *c, ks_batch *b) {
     if ((st0 = upload_dirty_ext(c, c->xm))) return st0;
   }
   if (!b->uploaded && (st0 = upload_batch(c, b))) return st0;
-  HIPC(c, hipMemsetAsync(c->d_start, 0, 4, c->stream));
-  uint32_t host_start = 0;
-  while (host_start < b->n) {
-    // Assume full rounds (an early stop costs the speculated round after it)
-    // and check; each pipeline run resolves at least one pod.
-    const uint32_t remaining = b->n - host_start;
-    uint32_t rounds = (remaining + c->P - 1) / c->P;
-    rounds = std::min<uint32_t>(rounds, 64);
-    for (uint32_t r = 0; r < rounds; ++r) {
-      ks_status st = enqueue_round(c, b, r);
-      if (st) return st;
+  if (b->any_spread && c->comm)
+    return c->fail(KS_ERR_UNSUPPORTED, "topology spread pods need a single-rank context");
+  // Selector classes each pod matches, against the classes live now: the
+  // spread path's commits and the round kernels' (class_commit) count them.
+  bool classes = false;
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    for (int k = 0; k < MAX_CLASSES; ++k) classes |= c->classes[k].live;
+    if (classes || b->any_spread) {
+      std::vector<uint64_t> memo(c->label_sets.size(), ~0ull);
+      for (uint32_t i = 0; i < b->n; ++i) {
+        const uint32_t set = b->set_ids[i];
+        if (memo[set] == ~0ull) {
+          uint64_t m = 0;
+          for (int k = 0; k < MAX_CLASSES; ++k)
+            if (c->classes[k].live && class_matches(c, c->classes[k], set)) m |= 1ull << k;
+          memo[set] = m;
+        }
+        b->h_cmask[i] = memo[set];
+      }
     }
-    // results of every pod this pipeline run can resolve, behind its last round
-    const uint32_t hi = std::min<uint32_t>(b->n, host_start + rounds * c->P);
-    ks_status st = drain_rounds(c, rounds, b->h_results + host_start, b->d_results + host_start,
-                                (size_t)(hi - host_start) * sizeof(DevResult));
-    if (st) return st;
-    if (*c->h_start <= host_start) return c->fail(KS_ERR_DEVICE, "no progress in scheduling rounds");
-    host_start = *c->h_start;
+  }
+  if (classes || b->any_spread)
+    HIPC(c, hipMemcpyAsync(b->d_cmask, b->h_cmask, (size_t)std::max<uint32_t>(b->n, 1) * 8, hipMemcpyHostToDevice,
+                           c->stream));
+  // Segments in queue order: runs of pods without spread constraints through
+  // the pipelined rounds, spread pods one at a time through ksched_spread.hip.
+  for (uint32_t lo = 0; lo < b->n;) {
+    uint32_t hi = lo;
+    if (b->any_spread && b->spread[lo]) {
+      SpreadArgs sa{};
+      {
+        std::lock_guard<std::mutex> g(c->mu);
+        sa.t = c->t;
+        for (uint32_t k = 0; k < c->topo.size(); ++k) sa.ndom[k] = c->topo[k].ndom;
+      }
+      sa.pos_slot = c->d_pos_slot;
+      sa.slot_pos = c->d_slot_pos;
+      sa.npos = c->npos;
+      sa.pods = b->d_pods;
+      sa.clauses = b->d_clauses;
+      sa.cmask = b->d_cmask;
+      sa.dom = c->d_dom;
+      sa.cnt = c->d_cnt;
+      sa.dcnt = c->d_dcnt;
+      sa.dflag = c->d_dflag;
+      sa.dom_cap = c->dom_cap;
+      sa.acc = c->d_acc;
+      sa.st = c->d_sst;
+      sa.raw = c->d_sraw;
+      sa.results = b->d_results;
+      sa.counters = c->d_counters;
+      sa.w = Weights{c->cfg.weight_fit, c->cfg.weight_balanced, c->cfg.weight_taint, c->cfg.weight_affinity,
+                     c->cfg.weight_image};
+      sa.w_pts = c->cfg.weight_topology_spread;
+      sa.evaluated = c->n_present;
+      for (; hi < b->n && b->spread[hi]; ++hi) {
+        sa.pod = hi;
+        HIPC(c, launch_spread_pod(sa, (b->spread[hi] & 2) != 0, (b->spread[hi] & 4) != 0, c->stream));
+      }
+      HIPC(c, hipMemcpyAsync(b->h_results + lo, b->d_results + lo, (size_t)(hi - lo) * sizeof(DevResult),
+                             hipMemcpyDeviceToHost, c->stream));
+    } else {
+      while (hi < b->n && !(b->any_spread && b->spread[hi])) ++hi;
+      *c->h_seg = lo;
+      HIPC(c, hipMemcpyAsync(c->d_start, c->h_seg, 4, hipMemcpyHostToDevice, c->stream));
+      uint32_t host_start = lo;
+      while (host_start < hi) {
+        // Assume full rounds (an early stop costs the speculated round after it)
+        // and check; each pipeline run resolves at least one pod.
+        uint32_t rounds = (hi - host_start + c->P - 1) / c->P;
+        rounds = std::min<uint32_t>(rounds, 64);
+        for (uint32_t r = 0; r < rounds; ++r) {
+          ks_status st = enqueue_round(c, b, r, hi);
+          if (st) return st;
+        }
+        // results of every pod this pipeline run can resolve, behind its last round
+        const uint32_t top = std::min<uint32_t>(hi, host_start + rounds * c->P);
+        ks_status st = drain_rounds(c, rounds, b->h_results + host_start, b->d_results + host_start,
+                                    (size_t)(top - host_start) * sizeof(DevResult));
+        if (st) return st;
+        if (*c->h_start <= host_start) return c->fail(KS_ERR_DEVICE, "no progress in scheduling rounds");
+        host_start = *c->h_start;
+      }
+      if (classes)
+        HIPC(c, launch_class_commit(b->d_results, b->d_cmask, c->d_slot_pos, c->d_cnt, c->npos, lo, hi, c->stream));
+    }
+    lo = hi;
+  }
+  HIPC(c, hipStreamSynchronize(c->stream));
+  {
+    // NodeInfo.Pods of the nodes this batch bound pods to (later selector classes count them)
+    std::lock_guard<std::mutex> g(c->mu);
+    for (uint32_t i = 0; i < b->n; ++i)
+      if (b->h_results[i].status == KS_POD_SCHEDULED) c->nodes[b->h_results[i].node_index].pod_sets.push_back(b->set_ids[i]);
   }
   if (c->timing) {
     ks_status st = collect_timing(c);
@@ -1465,6 +1985,7 @@ void ks_config_default(ks_config *cfg) {
   cfg->weight_taint = 3;
   cfg->weight_affinity = 2;
   cfg->weight_image = 1;
+  cfg->weight_topology_spread = 2;
   cfg->percentage_of_nodes_to_score = 100;
 }
 
@@ -1491,7 +2012,8 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
   c->S = world > 1 ? world : std::max<uint32_t>(1, cfg->virtual_shards);
   if (c->S > (uint32_t)MAX_SHARDS) return KS_ERR_INVALID;
   // weights are small non-negative integers (the kernels add them in 32 bits)
-  for (int32_t w : {cfg->weight_fit, cfg->weight_balanced, cfg->weight_taint, cfg->weight_affinity, cfg->weight_image})
+  for (int32_t w : {cfg->weight_fit, cfg->weight_balanced, cfg->weight_taint, cfg->weight_affinity, cfg->weight_image,
+                    cfg->weight_topology_spread})
     if (w < 0 || w > 10000) return KS_ERR_INVALID;
   // percentageOfNodesToScore (ksched.h): only 100 (every node) is modelled
   if (cfg->percentage_of_nodes_to_score < 0 || cfg->percentage_of_nodes_to_score > 100) return KS_ERR_INVALID;
@@ -1604,6 +2126,7 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
       (st = h2d(x, x->d_slot_pos, x->slot_pos.data(), (size_t)x->cap * 4)))
     return st;
   HIPC(x, hipHostMalloc((void **)&x->h_start, 4, hipHostMallocDefault));
+  HIPC(x, hipHostMalloc((void **)&x->h_seg, 4, hipHostMallocDefault));
   // round records: blocks of the widest kernel (npl 2 -> sub = npl / 2)
   uint32_t bmax = 0;
   for (auto &sh : x->shards) bmax = std::max(bmax, blocks_per_shard(sh, x->npl / std::min<uint32_t>(x->npl, 2)));
@@ -1638,18 +2161,22 @@ void ks_close(ks_ctx *c) {
   void *bufs[] = {c->t.acpu, c->t.amem, c->t.rcpu, c->t.rmem, c->t.zcpu, c->t.zmem, c->t.apods,
                   c->t.npods, c->t.hard, c->t.prefer, c->t.lab, c->t.num, c->d_shards, c->d_slot_pos,
                   c->d_start, c->d_norm, c->d_norm_inv, c->d_pstat, c->d_fix, c->d_brec, c->d_srec, c->d_frec,
-                  c->d_counters, c->d_crow, c->d_cext, c->d_pipe, c->d_carry, c->d_flags};
+                  c->d_counters, c->d_crow, c->d_cext, c->d_pipe, c->d_carry, c->d_flags, c->d_dom,
+                  c->d_pos_slot, c->d_dcnt, c->d_dflag, c->d_acc, c->d_sst, c->d_sraw};
   for (void *b : bufs)
     if (b) (void)hipFree(b);
   if (c->h_start) (void)hipHostFree(c->h_start);
+  if (c->h_seg) (void)hipHostFree(c->h_seg);
   if (c->xm.pin) (void)hipHostFree(c->xm.pin);
   if (c->xm.dscr) (void)hipFree(c->xm.dscr);
   for (void *g : c->graveyard) (void)hipFree(g);
   for (void *g : c->pinned_graveyard) (void)hipHostFree(g);
   for (ks_batch *b : c->all_batches) {
-    for (void *p : {(void *)b->d_pods, (void *)b->d_pinv, (void *)b->d_clauses, (void *)b->d_results})
+    for (void *p : {(void *)b->d_pods, (void *)b->d_pinv, (void *)b->d_clauses, (void *)b->d_results,
+                    (void *)b->d_cmask})
       if (p) (void)hipFree(p);
-    for (void *p : {(void *)b->h_results, (void *)b->h_pods, (void *)b->h_pinv, (void *)b->h_clauses})
+    for (void *p : {(void *)b->h_results, (void *)b->h_pods, (void *)b->h_pinv, (void *)b->h_clauses,
+                    (void *)b->h_cmask})
       if (p) (void)hipHostFree(p);
     delete b;
   }
@@ -1791,7 +2318,11 @@ ks_status ks_nodes_upsert(ks_ctx *c, const ks_node *nodes, const uint32_t *slots
       (st = h2d(c, d_ext, ext.data(), ext.size() * 8)))
     return st;
   HIPC(c, launch_scatter_rows(c->t, d_pos, d_core, d_ext, n, 1u, c->stream));
-  return xfer_sync(c);
+  if ((st = xfer_sync(c))) return st;
+  std::vector<uint32_t> changed;
+  changed.reserve(row_of.size());
+  for (auto &kv : row_of) changed.push_back(kv.first);
+  return spread_nodes_changed(c, changed.data(), (uint32_t)changed.size(), false);
 }
 
 ks_status ks_nodes_delete(ks_ctx *c, const uint32_t *slots, uint32_t n) {
@@ -1823,7 +2354,8 @@ ks_status ks_nodes_delete(ks_ctx *c, const uint32_t *slots, uint32_t n) {
   if ((st = h2d(c, d_pos, pos.data(), (size_t)n * 4)) || (st = h2d(c, d_core, core.data(), core.size() * 8)))
     return st;
   HIPC(c, launch_scatter_rows(c->t, d_pos, d_core, nullptr, n, 0u, c->stream));
-  return xfer_sync(c);
+  if ((st = xfer_sync(c))) return st;
+  return spread_nodes_changed(c, slots, n, true);
 }
 
 static ks_status pods_delta(ks_ctx *c, const ks_pod *pods, const uint32_t *slots, uint32_t n, int sign) {
@@ -1858,7 +2390,8 @@ static ks_status pods_delta(ks_ctx *c, const ks_pod *pods, const uint32_t *slots
   if ((st = h2d(c, d_pos, pos.data(), (size_t)n * 4)) || (st = h2d(c, d_d, d.data(), d.size() * 8))) return st;
   HIPC(c, launch_apply_deltas(c->t, d_pos, d_d, n, c->stream));
   c->affinity_pods += aff;
-  return xfer_sync(c);
+  if ((st = xfer_sync(c))) return st;
+  return spread_pods_delta(c, pods, slots, n, sign);
 }
 
 ks_status ks_pods_add(ks_ctx *c, const ks_pod *pods, const uint32_t *slots, uint32_t n) {
@@ -1909,12 +2442,14 @@ ks_status ks_events_apply(ks_ctx *c, const ks_event *ev, uint32_t n) {
 // dictionary runs out of bits, reclaim it once (reset_label_dict, after the
 // submitted batches drained) and compile the batch again from its first pod.
 static ks_status compile_batch(ks_ctx *c, const ks_pod *pods, uint32_t n, PodDev *dev, ProgBuf &cl,
-                               std::unique_lock<std::mutex> &lk) {
+                               std::unique_lock<std::mutex> &lk, bool create_spread = false,
+                               std::vector<uint32_t> *class_refs = nullptr) {
   for (int attempt = 0;; ++attempt) {
     cl.w.clear();
     c->compile_used_names = false;
+    if (class_refs) class_refs->clear();
     ks_status st = KS_OK;
-    for (uint32_t i = 0; i < n && !st; ++i) st = compile_pod(c, pods[i], dev[i], cl);
+    for (uint32_t i = 0; i < n && !st; ++i) st = compile_pod(c, pods[i], dev[i], cl, create_spread, class_refs);
     if (st != KS_ERR_CAPACITY || attempt > 0 || c->next_bit == 0) return st;
     lk.unlock();
     drain_async(c);
@@ -1951,15 +2486,24 @@ ks_status ks_batch_prepare(ks_ctx *c, const ks_pod *pods, uint32_t n, ks_batch *
   bool ext = false, norm = false;
   uint32_t dict_v, names_v;
   ks_status st;
+  // Spread pods may create topology / selector-class columns, computed from the
+  // host's records of bound pods: let every submitted batch finish first.
+  bool any_spread = false;
+  for (uint32_t i = 0; i < n && !any_spread; ++i) any_spread = pods[i].n_spread != 0;
+  if (any_spread) drain_async(c);
+  std::vector<uint32_t> set_ids(n), refs;
   {
     // compile against the host dictionaries (the worker reads t.lw and the
     // dirty label rows under mu)
     std::unique_lock<std::mutex> g(c->mu);
-    if ((st = compile_batch(c, pods, n, dev.data(), cl, g))) return st;
+    if ((st = compile_batch(c, pods, n, dev.data(), cl, g, true, &refs))) return st;
     for (uint32_t i = 0; i < n; ++i) {
+      if (dev[i].flags & PF_SPREAD) continue;  // the spread path evaluates it
       if (dev[i].flags & PF_EXT) ext = true;
       if (dev[i].flags & (PF_TT | PF_NA)) norm = true;
     }
+    for (uint32_t i = 0; i < n; ++i) set_ids[i] = intern_set(c, pods[i]);
+    for (uint32_t k : refs) c->classes[k].refs++;
     dict_v = c->dict_version;
     names_v = c->compile_used_names ? c->names_version : 0;
   }
@@ -1973,6 +2517,18 @@ ks_status ks_batch_prepare(ks_ctx *c, const ks_pod *pods, uint32_t n, ks_batch *
   b->dict_version = dict_v;
   b->names_version = names_v;
   b->n_words = cl.w.size();
+  b->set_ids = std::move(set_ids);
+  b->class_refs = std::move(refs);
+  b->spread.assign(n, 0);
+  b->any_spread = false;
+  for (uint32_t i = 0; i < n; ++i) {
+    if (!(dev[i].flags & PF_SPREAD)) continue;
+    const SpreadDev *sd = reinterpret_cast<const SpreadDev *>(cl.w.data() + dev[i].spread_off);
+    uint8_t f = 1;
+    for (uint32_t k = 0; k < (dev[i].flags >> PF_NSPREAD_SHIFT); ++k) f |= (sd[k].flags & SP_SCORE) ? 4 : 2;
+    b->spread[i] = f;
+    b->any_spread = true;
+  }
   std::memcpy(b->h_pods, dev.data(), dev.size() * sizeof(PodDev));
   for (size_t i = 0; i < dev.size(); ++i) {
     b->h_pinv[2 * i] = dev[i].tt_guess ? 1.0 / (double)dev[i].tt_guess : 0.0;
@@ -2057,6 +2613,12 @@ void ks_batch_free(ks_ctx *c, ks_batch *b) {
     std::unique_lock<std::mutex> lk(c->qmu);
     if (b->queued) c->dcv.wait(lk, [&] { return b->done; });
   }
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    for (uint32_t k : b->class_refs)
+      if (c->classes[k].refs) c->classes[k].refs--;
+    b->class_refs.clear();
+  }
   batch_release(c, b);
 }
 
@@ -2070,6 +2632,81 @@ ks_status ks_schedule(ks_ctx *c, const ks_pod *pods, uint32_t n, ks_result *out)
   return st;
 }
 
+}  // extern "C"
+
+namespace {
+
+// SpreadArgs of the context's columns and scratch (the batch fields are the caller's).
+SpreadArgs spread_args(ks_ctx *c) {
+  SpreadArgs sa{};
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    sa.t = c->t;
+    for (uint32_t k = 0; k < c->topo.size(); ++k) sa.ndom[k] = c->topo[k].ndom;
+  }
+  sa.pos_slot = c->d_pos_slot;
+  sa.slot_pos = c->d_slot_pos;
+  sa.npos = c->npos;
+  sa.dom = c->d_dom;
+  sa.cnt = c->d_cnt;
+  sa.dcnt = c->d_dcnt;
+  sa.dflag = c->d_dflag;
+  sa.dom_cap = c->dom_cap;
+  sa.acc = c->d_acc;
+  sa.st = c->d_sst;
+  sa.raw = c->d_sraw;
+  sa.counters = c->d_counters;
+  sa.w = Weights{c->cfg.weight_fit, c->cfg.weight_balanced, c->cfg.weight_taint, c->cfg.weight_affinity,
+                 c->cfg.weight_image};
+  sa.w_pts = c->cfg.weight_topology_spread;
+  sa.evaluated = c->n_present;
+  return sa;
+}
+
+// ks_plugin_scores of a pod with spread constraints: the spread chain in dump mode.
+ks_status spread_plugin_scores(ks_ctx *c, const PodDev &d, const ProgBuf &cl, ks_node_score *out) {
+  std::vector<int32_t> raw((size_t)c->cap * SPREAD_DUMP_WORDS);
+  const size_t bytes = sizeof(PodDev) + cl.w.size() * 8 + raw.size() * 4 + 2048;
+  ks_status st;
+  if ((st = xfer_begin(c, bytes, bytes))) return st;
+  PodDev *d_pod = dscratch<PodDev>(c, 1);
+  uint64_t *d_cl = dscratch<uint64_t>(c, cl.w.size());
+  int32_t *d_out = dscratch<int32_t>(c, raw.size());
+  if ((st = h2d(c, d_pod, &d, sizeof d)) || (st = h2d(c, d_cl, cl.w.data(), cl.w.size() * 8))) return st;
+  SpreadArgs sa = spread_args(c);
+  sa.pods = d_pod;
+  sa.clauses = d_cl;
+  sa.pod = 0;
+  sa.dump = d_out;
+  sa.no_commit = 1;
+  bool has_filter = false, has_score = false;
+  const SpreadDev *sd = reinterpret_cast<const SpreadDev *>(cl.w.data() + d.spread_off);
+  for (uint32_t k = 0; k < (d.flags >> PF_NSPREAD_SHIFT); ++k) ((sd[k].flags & SP_SCORE) ? has_score : has_filter) = true;
+  HIPC(c, launch_spread_pod(sa, has_filter, has_score, c->stream));
+  if ((st = d2h(c, raw.data(), d_out, raw.size() * 4)) || (st = xfer_sync(c))) return st;
+  for (uint32_t i = 0; i < c->cap; ++i) {
+    const int32_t *o = &raw[(size_t)i * SPREAD_DUMP_WORDS];
+    ks_node_score s{};
+    s.status = o[0];
+    s.least_allocated = o[1];
+    s.balanced_allocation = o[2];
+    s.taint_raw = o[3];
+    s.taint_score = o[4];
+    s.affinity_raw = o[5];
+    s.affinity_score = o[6];
+    s.image_locality = o[7];
+    s.spread_raw = o[8];
+    s.spread_score = o[9];
+    s.total_score = (int64_t)(((uint64_t)(uint32_t)o[11] << 32) | (uint32_t)o[10]);
+    out[i] = s;
+  }
+  return KS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
 ks_status ks_plugin_scores(ks_ctx *c, const ks_pod *pod, ks_node_score *out) {
   if (!c || !pod || !out) return KS_ERR_INVALID;
   if (ks_status dst_ = drain_async(c)) return dst_;
@@ -2079,10 +2716,11 @@ ks_status ks_plugin_scores(ks_ctx *c, const ks_pod *pod, ks_node_score *out) {
   ks_status st;
   {
     std::unique_lock<std::mutex> g(c->mu);
-    if ((st = compile_batch(c, pod, 1, &d, cl, g))) return st;
+    if ((st = compile_batch(c, pod, 1, &d, cl, g, true))) return st;
     if ((st = upload_dirty_ext(c, c->xm))) return st;
   }
   if (cl.w.empty()) cl.w.push_back(0);
+  if (d.flags & PF_SPREAD) return spread_plugin_scores(c, d, cl, out);
   DumpArgs a{};
   a.t = c->t;
   a.nslots = c->cap;
@@ -2115,6 +2753,8 @@ ks_status ks_plugin_scores(ks_ctx *c, const ks_pod *pod, ks_node_score *out) {
     s.affinity_raw = o[5];
     s.affinity_score = o[6];
     s.image_locality = o[7];
+    s.spread_raw = 0;
+    s.spread_score = 0;
     s.total_score = (int64_t)(((uint64_t)(uint32_t)o[9] << 32) | (uint32_t)o[8]);
     out[i] = s;
   }

@@ -73,6 +73,43 @@ struct DumpArgs {
   Weights w;
 };
 
+// PodTopologySpread path (ksched_spread.hip): one pod per launch chain.
+constexpr uint32_t SLOT_NONE = 0xFFFFFFFFu;  // position holding no slot (shard padding)
+constexpr int SPREAD_DUMP_WORDS = 12;  // status, la, ba, tt raw/score, na raw/score, il, pts raw/score, total lo/hi
+struct SpreadArgs {
+  NodeTable t;
+  const uint32_t *pos_slot;   // position -> slot (SLOT_NONE: padding)
+  const uint32_t *slot_pos;   // slot -> position
+  uint32_t npos;
+  uint32_t pod;               // index of the pod in the batch
+  const PodDev *pods;
+  const uint64_t *clauses;    // label programs + SpreadDev records
+  const uint64_t *cmask;      // [npods] selector classes each pod of the batch matches
+  const uint32_t *dom;        // [MAX_TOPO_KEYS][npos] domain id per position (DOM_NONE: key absent)
+  uint32_t *cnt;              // [MAX_CLASSES][npos] matching bound pods per position
+  uint32_t *dcnt;             // [MAX_SPREAD][dom_cap] per-constraint domain counts (zero between pods)
+  uint32_t *dflag;            // [MAX_SPREAD][dom_cap] bit 0 Filter-eligible domain, bit 1 Score domain
+  uint32_t dom_cap;
+  uint32_t ndom[MAX_TOPO_KEYS];  // domain ids of every topology-key column (at launch)
+  SpreadAcc *acc;
+  int8_t *st;                 // [npos] status of every position for this pod
+  int64_t *raw;               // [npos] PodTopologySpread raw score
+  DevResult *results;
+  int32_t *dump;              // ks_plugin_scores: [slots][SPREAD_DUMP_WORDS] (null: schedule)
+  uint32_t no_commit;         // dump / reset: no result, no AssumePod
+  uint64_t *counters;
+  Weights w;
+  int32_t w_pts;
+  uint32_t evaluated;         // present nodes
+};
+
+hipError_t launch_spread_pod(const SpreadArgs &a, bool has_filter, bool has_score, hipStream_t st);
+hipError_t launch_spread_reset(const SpreadArgs &a, hipStream_t st);
+hipError_t launch_class_commit(const DevResult *res, const uint64_t *cmask, const uint32_t *slot_pos, uint32_t *cnt,
+                               uint32_t npos, uint32_t lo, uint32_t hi, hipStream_t st);
+hipError_t launch_scatter_u32(uint32_t *col, const uint64_t *idx, const uint32_t *val, uint32_t n, hipStream_t st);
+hipError_t launch_add_u32(uint32_t *col, const uint64_t *idx, const int32_t *delta, uint32_t n, hipStream_t st);
+
 hipError_t launch_norm_check(const RoundArgs &a, hipStream_t st);
 hipError_t launch_sweep(const RoundArgs &a, bool ext, uint32_t nblocks, uint32_t ngroups, uint32_t nshards,
                         hipStream_t st);

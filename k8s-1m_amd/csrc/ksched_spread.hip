@@ -1,0 +1,581 @@
+// ksched_spread.hip — gfx950 kernels of the PodTopologySpread path.
+//
+// A pod with topology spread constraints depends on counts aggregated over
+// whole topology domains (every node of a zone shares its zone's count), so a
+// commit changes the score of every node in the committed node's domain: the
+// round kernels' premise (a commit changes only its own node) does not hold.
+// Such pods are scheduled one at a time, in queue order, by this chain of
+// node-parallel passes over the same SoA node table (upstream v1.31.3
+// pkg/scheduler/framework/plugins/podtopologyspread, restated in oracle.cpp):
+//
+//   spread_prep    PreFilter (filtering.go#calPreFilterState) and the
+//                  PreScore counts (scoring.go#PreScore): matching bound pods
+//                  of every eligible node summed per topology domain
+//   spread_min     criticalPaths[0] / TpKeyToDomainsNum per DoNotSchedule
+//                  constraint
+//   spread_filter  the whole filter chain + PodTopologySpread.Filter; Score
+//                  domains of the filtered nodes; normaliser maxima
+//   spread_score   Score: Σ cnt·log(size+2) + (maxSkew-1), math.Round; min/max
+//   spread_select  total score of every feasible node, NormalizeScore,
+//                  packed-key argmax; clears the domain scratch
+//   spread_commit  the result and AssumePod (resources, pod count, the bound
+//                  pod's selector-class counts)
+//
+// Domain counts are aggregated per block in LDS for low-cardinality keys
+// (zones), with global atomics only for high-cardinality ones (hostnames).
+#include <hip/hip_runtime.h>
+
+#include "ksched_dev.hpp"
+#include "ksched_eval.hpp"
+#include "ksched_kernels.hpp"
+
+namespace ks {
+
+namespace {
+
+constexpr int SP_THREADS = 256;
+constexpr uint32_t SP_LDS = 4096;     // LDS domain-histogram entries per block
+constexpr uint32_t SP_LDS_DOM = 1024; // keys with at most this many domains aggregate in LDS
+constexpr uint32_t SP_OFF_NONE = 0xFFFFFFFFu;
+constexpr int8_t SST_FEASIBLE = -1, SST_EMPTY = -2, SST_IGNORED = -3;  // per-position status
+
+__device__ __forceinline__ const SpreadDev *spread_recs(const SpreadArgs &a, const PodDev &p) {
+  return reinterpret_cast<const SpreadDev *>(a.clauses + p.spread_off);
+}
+__device__ __forceinline__ uint32_t spread_count(const PodDev &p) { return p.flags >> PF_NSPREAD_SHIFT; }
+
+// Go math.Log (log.go, fdlibm e_log.c; the amd64 assembly performs the same
+// operations) for a finite x >= 2, one rounding per operation.
+__device__ double go_log(double x) {
+  const double Ln2Hi = 6.93147180369123816490e-01, Ln2Lo = 1.90821492927058770002e-10;
+  const double L1 = 6.666666666666735130e-01, L2 = 3.999999999940941908e-01, L3 = 2.857142874366239149e-01,
+               L4 = 2.222219843214978396e-01, L5 = 1.818357216161805012e-01, L6 = 1.531383769920937332e-01,
+               L7 = 1.479819860511658591e-01;
+  // Frexp: x = f1 * 2^ki, f1 in [0.5, 1)
+  const uint64_t b = (uint64_t)__double_as_longlong(x);
+  int ki = (int)((b >> 52) & 0x7FF) - 1022;
+  double f1 = __longlong_as_double((long long)((b & 0x800FFFFFFFFFFFFFull) | (1022ull << 52)));
+  if (f1 < 0.70710678118654752440) {  // Sqrt2 / 2
+    f1 *= 2;
+    ki--;
+  }
+  const double f = f1 - 1;
+  const double k = (double)ki;
+  const double s = f / (2 + f);
+  const double s2 = s * s;
+  const double s4 = s2 * s2;
+  const double t1 = s2 * (L1 + s4 * (L3 + s4 * (L5 + s4 * L7)));
+  const double t2 = s4 * (L2 + s4 * (L4 + s4 * L6));
+  const double R = t1 + t2;
+  const double hfsq = 0.5 * f * f;
+  return k * Ln2Hi - ((hfsq - (s * (hfsq + R) + k * Ln2Lo)) - f);
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = max(v, __shfl_xor(v, o));
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_min(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = min(v, __shfl_xor(v, o));
+  return v;
+}
+__device__ __forceinline__ uint64_t wave_max64(uint64_t v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const uint64_t w = __shfl_xor(v, o);
+    v = w > v ? w : v;
+  }
+  return v;
+}
+__device__ __forceinline__ uint64_t wave_min64(uint64_t v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const uint64_t w = __shfl_xor(v, o);
+    v = w < v ? w : v;
+  }
+  return v;
+}
+
+// LDS segments of the low-cardinality constraints (thread 0; caller syncs).
+__device__ void lds_segments(const SpreadArgs &a, const SpreadDev *sd, uint32_t n, uint32_t *off) {
+  uint32_t o = 0;
+  for (uint32_t c = 0; c < n; ++c) {
+    const uint32_t nd = a.ndom[sd[c].key];
+    const bool small = nd <= SP_LDS_DOM && o + nd <= SP_LDS;
+    off[c] = small ? o : SP_OFF_NONE;
+    if (small) o += nd;
+  }
+}
+
+__device__ __forceinline__ uint32_t grid_threads() { return gridDim.x * blockDim.x; }
+
+}  // namespace
+
+// ------------------------------------------------------------------ prep
+// Per DoNotSchedule constraint c: dcnt[c][d] = matching pods on the eligible
+// nodes of domain d (the node has every DoNotSchedule key and passes the
+// constraint's inclusion policies), dflag[c][d] bit 0 = d has an eligible
+// node.  Per ScheduleAnyway constraint (not kubernetes.io/hostname): dcnt over
+// the nodes PreScore counts (requireAllTopologies, inclusion policies; a node
+// lacking the key belongs to the "" domain, id 0, when it is not required).
+__global__ __launch_bounds__(SP_THREADS) void spread_prep_kernel(SpreadArgs a) {
+  __shared__ uint32_t s_h[SP_LDS];
+  __shared__ uint32_t s_off[MAX_SPREAD];
+  const PodDev p = a.pods[a.pod];
+  const SpreadDev *sd = spread_recs(a, p);
+  const uint32_t n = spread_count(p);
+  if (threadIdx.x == 0) lds_segments(a, sd, n, s_off);
+  for (uint32_t i = threadIdx.x; i < SP_LDS; i += SP_THREADS) s_h[i] = 0;
+  __syncthreads();
+  const bool allkeys = p.flags & PF_SPREAD_ALLKEYS;
+  for (uint32_t pos = blockIdx.x * SP_THREADS + threadIdx.x; pos < a.npos; pos += grid_threads()) {
+    const uint32_t slot = a.pos_slot[pos];
+    if (slot == SLOT_NONE || a.t.apods[pos] < 0) continue;
+    NodeExt e;
+    load_ext(a.t, pos, true, e);
+    const bool aff_ok = !(p.flags & PF_AFF) || required_match(p, a.clauses, e, slot);
+    const bool taint_ok = (e.hard & ~p.tol_hard & ~UNSCHED_BIT) == 0;
+    bool all_f = true, all_s = true;
+    for (uint32_t c = 0; c < n; ++c) {
+      if (a.dom[(size_t)sd[c].key * a.npos + pos] != DOM_NONE) continue;
+      if (sd[c].flags & SP_SCORE) all_s = false;
+      else all_f = false;
+    }
+    for (uint32_t c = 0; c < n; ++c) {
+      const SpreadDev &s = sd[c];
+      const bool score = s.flags & SP_SCORE;
+      if (score ? ((s.flags & SP_HOST) || (allkeys && !all_s)) : !all_f) continue;
+      if (((s.flags & SP_AFF) && !aff_ok) || ((s.flags & SP_TAINT) && !taint_ok)) continue;
+      uint32_t d = a.dom[(size_t)s.key * a.npos + pos];
+      if (d == DOM_NONE) d = 0;  // Score without requireAllTopologies: the "" value
+      const uint32_t k = s.cls == CLS_NONE ? 0u : a.cnt[(size_t)s.cls * a.npos + pos];
+      if (s_off[c] != SP_OFF_NONE) {
+        if (k) atomicAdd(&s_h[s_off[c] + d], k);
+        if (!score) atomicOr(&s_h[s_off[c] + d], 0x80000000u);
+      } else {
+        if (k) atomicAdd(&a.dcnt[(size_t)c * a.dom_cap + d], k);
+        if (!score) atomicOr(&a.dflag[(size_t)c * a.dom_cap + d], 1u);
+      }
+    }
+  }
+  __syncthreads();
+  for (uint32_t c = 0; c < n; ++c) {
+    if (s_off[c] == SP_OFF_NONE) continue;
+    for (uint32_t d = threadIdx.x; d < a.ndom[sd[c].key]; d += SP_THREADS) {
+      const uint32_t v = s_h[s_off[c] + d];
+      if (v & 0x7FFFFFFFu) atomicAdd(&a.dcnt[(size_t)c * a.dom_cap + d], v & 0x7FFFFFFFu);
+      if (v >> 31) atomicOr(&a.dflag[(size_t)c * a.dom_cap + d], 1u);
+    }
+  }
+}
+
+// ------------------------------------------------------------------- min
+// criticalPaths[0].MatchNum (min over the eligible domains) and the number of
+// eligible domains of every DoNotSchedule constraint.
+__global__ __launch_bounds__(SP_THREADS) void spread_min_kernel(SpreadArgs a) {
+  __shared__ uint32_t s_r[SP_THREADS / WAVE][2];
+  const PodDev p = a.pods[a.pod];
+  const SpreadDev *sd = spread_recs(a, p);
+  const uint32_t n = spread_count(p);
+  const uint32_t lane = threadIdx.x % WAVE, wid = threadIdx.x / WAVE;
+  for (uint32_t c = 0; c < n; ++c) {
+    if (sd[c].flags & SP_SCORE) continue;
+    uint32_t mn = 0xFFFFFFFFu, cnt = 0;
+    for (uint32_t d = blockIdx.x * SP_THREADS + threadIdx.x; d < a.ndom[sd[c].key]; d += grid_threads()) {
+      if (!(a.dflag[(size_t)c * a.dom_cap + d] & 1u)) continue;
+      mn = min(mn, a.dcnt[(size_t)c * a.dom_cap + d]);
+      ++cnt;
+    }
+    mn = wave_min(mn);
+    cnt = wave_sum(cnt);
+    if (lane == 0) {
+      s_r[wid][0] = mn;
+      s_r[wid][1] = cnt;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int w = 1; w < SP_THREADS / WAVE; ++w) {
+        mn = min(mn, s_r[w][0]);
+        cnt += s_r[w][1];
+      }
+      if (cnt) {
+        atomicMin(&a.acc->min_match[c], mn);
+        atomicAdd(&a.acc->ndomains[c], cnt);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------- filter
+// Filter chain in default-profile order, PodTopologySpread last
+// (filtering.go#Filter: node without the key -> UnschedulableAndUnresolvable;
+// matchNum + selfMatch - minMatchNum > maxSkew -> Unschedulable).  Feasible
+// nodes: normaliser maxima, PreScore's ignored nodes and the Score domains of
+// the rest (topoSize).
+__global__ __launch_bounds__(SP_THREADS) void spread_filter_kernel(SpreadArgs a) {
+  __shared__ uint32_t s_seen[SP_LDS / 32];
+  __shared__ uint32_t s_off[MAX_SPREAD];
+  __shared__ uint32_t s_red[SP_THREADS / WAVE][NFILT + 5];
+  const PodDev p = a.pods[a.pod];
+  const SpreadDev *sd = spread_recs(a, p);
+  const uint32_t n = spread_count(p);
+  if (threadIdx.x == 0) lds_segments(a, sd, n, s_off);
+  for (uint32_t i = threadIdx.x; i < SP_LDS / 32; i += SP_THREADS) s_seen[i] = 0;
+  __syncthreads();
+  const bool allkeys = p.flags & PF_SPREAD_ALLKEYS;
+  const uint32_t lane = threadIdx.x % WAVE, wid = threadIdx.x / WAVE;
+  uint32_t fails[NFILT + 1] = {0, 0, 0, 0, 0, 0};
+  uint32_t feasible = 0, ignored = 0, tt_max = 0, na_max = 0;
+  for (uint32_t pos = blockIdx.x * SP_THREADS + threadIdx.x; pos < a.npos; pos += grid_threads()) {
+    const uint32_t slot = a.pos_slot[pos];
+    if (slot == SLOT_NONE) continue;
+    NodeRegs r;
+    load_core(a.t, pos, slot, true, r);
+    if (!(r.bits & 1u)) {
+      a.st[pos] = SST_EMPTY;
+      continue;
+    }
+    NodeExt e;
+    load_ext(a.t, pos, true, e);
+    int s = filter<true>(p, a.clauses, r, e);
+    if (s == ST_FEASIBLE) {
+      for (uint32_t c = 0; c < n; ++c) {
+        const SpreadDev &q = sd[c];
+        if (q.flags & SP_SCORE) continue;
+        const uint32_t d = a.dom[(size_t)q.key * a.npos + pos];
+        if (d == DOM_NONE) {
+          s = PLUGIN_SPREAD;  // ErrReasonNodeLabelNotMatch
+          break;
+        }
+        const uint32_t minm = a.acc->ndomains[c] < (uint32_t)q.min_domains ? 0u : a.acc->min_match[c];
+        const int64_t skew = (int64_t)a.dcnt[(size_t)c * a.dom_cap + d] + ((q.flags & SP_SELF) ? 1 : 0) - (int64_t)minm;
+        if (skew > (int64_t)q.max_skew) {
+          s = PLUGIN_SPREAD;  // ErrReasonConstraintsNotMatch
+          break;
+        }
+      }
+    }
+    int8_t out = (int8_t)s;
+    if (s == ST_FEASIBLE) {
+      ++feasible;
+      if (p.flags & PF_TT) tt_max = max(tt_max, (uint32_t)taint_raw(p, e));
+      if (p.flags & PF_NA) na_max = max(na_max, (uint32_t)preferred_raw(p, a.clauses, e, slot));
+      // PreScore (initPreScoreState): with requireAllTopologies a node lacking
+      // a ScheduleAnyway key is ignored; the others' domains make topoSize
+      bool all_s = true;
+      for (uint32_t c = 0; c < n; ++c)
+        if ((sd[c].flags & SP_SCORE) && a.dom[(size_t)sd[c].key * a.npos + pos] == DOM_NONE) all_s = false;
+      if (allkeys && !all_s) {
+        ++ignored;
+        out = SST_IGNORED;
+      } else {
+        for (uint32_t c = 0; c < n; ++c) {
+          const SpreadDev &q = sd[c];
+          if (!(q.flags & SP_SCORE) || (q.flags & SP_HOST)) continue;
+          uint32_t d = a.dom[(size_t)q.key * a.npos + pos];
+          if (d == DOM_NONE) d = 0;
+          if (s_off[c] != SP_OFF_NONE) {
+            const uint32_t bit = s_off[c] + d;
+            if (atomicOr(&s_seen[bit >> 5], 1u << (bit & 31)) & (1u << (bit & 31))) continue;
+          }
+          if (!(atomicOr(&a.dflag[(size_t)c * a.dom_cap + d], 2u) & 2u)) atomicAdd(&a.acc->topo_size[c], 1u);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q <= NFILT; ++q) fails[q] += s == q ? 1u : 0u;  // ST_PREFILTERED: no plugin
+    }
+    a.st[pos] = out;
+  }
+  // block reduction: counts, maxima
+  uint32_t v[NFILT + 5];
+#pragma unroll
+  for (int q = 0; q <= NFILT; ++q) v[q] = wave_sum(fails[q]);
+  v[NFILT + 1] = wave_sum(feasible);
+  v[NFILT + 2] = wave_sum(ignored);
+  v[NFILT + 3] = wave_max(tt_max);
+  v[NFILT + 4] = wave_max(na_max);
+  if (lane == 0)
+    for (int q = 0; q < NFILT + 5; ++q) s_red[wid][q] = v[q];
+  __syncthreads();
+  if (threadIdx.x < NFILT + 5) {
+    const int q = threadIdx.x;
+    uint32_t t = s_red[0][q];
+    for (int w = 1; w < SP_THREADS / WAVE; ++w) t = q >= NFILT + 3 ? max(t, s_red[w][q]) : t + s_red[w][q];
+    if (t) {
+      if (q <= NFILT) atomicAdd(&a.acc->fail[q], t);
+      else if (q == NFILT + 1) atomicAdd(&a.acc->feasible, t);
+      else if (q == NFILT + 2) atomicAdd(&a.acc->ignored, t);
+      else if (q == NFILT + 3) atomicMax(&a.acc->tt_max, t);
+      else atomicMax(&a.acc->na_max, t);
+    }
+  }
+}
+
+// ----------------------------------------------------------------- score
+// scoring.go#Score: Σ over the ScheduleAnyway constraints whose key the node
+// has of float64(cnt) * log(size + 2) + float64(maxSkew - 1), rounded
+// (math.Round); cnt = matching pods of the node's domain (of the node itself
+// for kubernetes.io/hostname); size = Score domains (filtered nodes minus
+// ignored ones for hostname).
+__global__ __launch_bounds__(SP_THREADS) void spread_score_kernel(SpreadArgs a) {
+  __shared__ double s_w[MAX_SPREAD];
+  __shared__ uint64_t s_r[SP_THREADS / WAVE][2];
+  const PodDev p = a.pods[a.pod];
+  const SpreadDev *sd = spread_recs(a, p);
+  const uint32_t n = spread_count(p);
+  if (threadIdx.x < n) {
+    const SpreadDev &q = sd[threadIdx.x];
+    const uint32_t sz = (q.flags & SP_HOST) ? a.acc->feasible - a.acc->ignored : a.acc->topo_size[threadIdx.x];
+    s_w[threadIdx.x] = go_log((double)sz + 2.0);  // topologyNormalizingWeight
+  }
+  __syncthreads();
+  uint64_t mn = ~0ull, mx = 0;
+  for (uint32_t pos = blockIdx.x * SP_THREADS + threadIdx.x; pos < a.npos; pos += grid_threads()) {
+    if (a.st[pos] != SST_FEASIBLE) continue;
+    double score = 0;
+    for (uint32_t c = 0; c < n; ++c) {
+      const SpreadDev &q = sd[c];
+      if (!(q.flags & SP_SCORE)) continue;
+      const uint32_t d = a.dom[(size_t)q.key * a.npos + pos];
+      if (d == DOM_NONE) continue;  // the node lacks the key: no term
+      uint32_t cnt;
+      if (q.flags & SP_HOST) cnt = q.cls == CLS_NONE ? 0u : a.cnt[(size_t)q.cls * a.npos + pos];
+      else cnt = a.dcnt[(size_t)c * a.dom_cap + d];
+      score += (double)cnt * s_w[c] + (double)(q.max_skew - 1);  // scoreForCount
+    }
+    const int64_t raw = (int64_t)round(score);
+    a.raw[pos] = raw;
+    mn = min(mn, (uint64_t)raw);
+    mx = max(mx, (uint64_t)raw);
+  }
+  mn = wave_min64(mn);
+  mx = wave_max64(mx);
+  const uint32_t lane = threadIdx.x % WAVE, wid = threadIdx.x / WAVE;
+  if (lane == 0) {
+    s_r[wid][0] = mn;
+    s_r[wid][1] = mx;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < SP_THREADS / WAVE; ++w) {
+      mn = min(mn, s_r[w][0]);
+      mx = max(mx, s_r[w][1]);
+    }
+    if (mn != ~0ull) atomicMin((unsigned long long *)&a.acc->pts_min, (unsigned long long)mn);
+    if (mx) atomicMax((unsigned long long *)&a.acc->pts_max, (unsigned long long)mx);
+  }
+}
+
+// ---------------------------------------------------------------- select
+// TotalScore of every feasible node (PodTopologySpread NormalizeScore:
+// ignored -> 0, max 0 -> 100, else 100 (max + min - s) / max), the packed-key
+// argmax; ks_plugin_scores writes the per-node plugin scores instead.  The
+// domain scratch is cleared for the next pod (its last reader was the score
+// pass).
+__global__ __launch_bounds__(SP_THREADS) void spread_select_kernel(SpreadArgs a) {
+  __shared__ uint64_t s_r[SP_THREADS / WAVE];
+  const PodDev p = a.pods[a.pod];
+  const SpreadDev *sd = spread_recs(a, p);
+  const uint32_t n = spread_count(p);
+  bool has_score = false;
+  for (uint32_t c = 0; c < n; ++c) has_score |= (sd[c].flags & SP_SCORE) != 0;
+  const int64_t tt_max = a.acc->tt_max, na_max = a.acc->na_max;
+  const int64_t pmin = (int64_t)a.acc->pts_min, pmax = (int64_t)a.acc->pts_max;
+  uint64_t best = 0;
+  for (uint32_t pos = blockIdx.x * SP_THREADS + threadIdx.x; pos < a.npos; pos += grid_threads()) {
+    const int8_t s = a.st[pos];
+    const uint32_t slot = a.pos_slot[pos];
+    if (s != SST_FEASIBLE && s != SST_IGNORED) {
+      if (a.dump && slot != SLOT_NONE) {
+        int32_t *o = a.dump + (size_t)slot * SPREAD_DUMP_WORDS;
+        for (int q = 0; q < SPREAD_DUMP_WORDS; ++q) o[q] = 0;
+        o[0] = s == SST_EMPTY ? ST_EMPTY : s;
+      }
+      continue;
+    }
+    NodeRegs r;
+    load_core(a.t, pos, slot, true, r);
+    NodeExt e;
+    load_ext(a.t, pos, true, e);
+    int64_t raw = 0, norm = 0;
+    if (has_score) {
+      if (s == SST_IGNORED) norm = 0;
+      else {
+        raw = a.raw[pos];
+        norm = pmax == 0 ? 100 : 100 * (pmax + pmin - raw) / pmax;
+      }
+    }
+    const int64_t total = (int64_t)total_score<true>(p, a.clauses, r, e, a.w, tt_max, na_max) +
+                          (has_score ? (int64_t)a.w_pts * norm : 0);
+    if (a.dump) {
+      int32_t *o = a.dump + (size_t)slot * SPREAD_DUMP_WORDS;
+      o[0] = ST_FEASIBLE;
+      o[1] = score_la(p, r);
+      o[2] = score_ba(p, r);
+      const int64_t tr = (p.flags & PF_TT) ? taint_raw(p, e) : 0;
+      o[3] = (int32_t)tr;
+      o[4] = (int32_t)normalize(tr, (p.flags & PF_TT) ? tt_max : 0, true);
+      const int64_t nr = (p.flags & PF_NA) ? preferred_raw(p, a.clauses, e, slot) : 0;
+      o[5] = (int32_t)nr;
+      o[6] = (p.flags & PF_HAS_PREF) ? (int32_t)normalize(nr, (p.flags & PF_NA) ? na_max : 0, false) : 0;
+      o[7] = 0;
+      o[8] = (int32_t)raw;
+      o[9] = (int32_t)norm;
+      o[10] = (int32_t)(total & 0xFFFFFFFF);
+      o[11] = (int32_t)(total >> 32);
+    }
+    const uint64_t k = pack_key(total, slot);
+    best = k > best ? k : best;
+  }
+  best = wave_max64(best);
+  if (threadIdx.x % WAVE == 0) s_r[threadIdx.x / WAVE] = best;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < SP_THREADS / WAVE; ++w) best = s_r[w] > best ? s_r[w] : best;
+    if (best) atomicMax((unsigned long long *)&a.acc->best, (unsigned long long)best);
+  }
+  // clear the domain scratch of this pod's constraints
+  for (uint32_t c = 0; c < n; ++c)
+    for (uint32_t d = blockIdx.x * SP_THREADS + threadIdx.x; d < a.ndom[sd[c].key]; d += grid_threads()) {
+      a.dcnt[(size_t)c * a.dom_cap + d] = 0;
+      a.dflag[(size_t)c * a.dom_cap + d] = 0;
+    }
+}
+
+// ---------------------------------------------------------------- commit
+// One thread: the pod's result (ScheduleResult / FitError / Error as the round
+// kernels report them), AssumePod on the winner (Requested, NonZeroRequested,
+// pod count, and +1 in every selector-class column the pod matches), and the
+// accumulators reset for the next pod.
+__global__ void spread_commit_kernel(SpreadArgs a) {
+  if (threadIdx.x != 0) return;
+  const PodDev p = a.pods[a.pod];
+  SpreadAcc &acc = *a.acc;
+  DevResult r;
+  r.node_index = -1;
+  r.status = 1;  // KS_POD_UNSCHEDULABLE
+  r.total_score = 0;
+  r.feasible_nodes = acc.feasible;
+  r.evaluated_nodes = a.evaluated;
+  for (int q = 0; q < NFILT; ++q) r.fail_counts[q] = acc.fail[q];
+  r.spread_fail = acc.fail[PLUGIN_SPREAD];
+  r.prefiltered = p.prefilter_out;
+  r.flags = 0;
+  if (acc.feasible > 0) {
+    if ((p.flags & PF_PREF_ERR) && acc.feasible >= 2) {
+      r.status = 2;  // KS_POD_ERROR (NodeAffinity PreScore)
+    } else if (acc.best == 0) {
+      r.status = 2;  // no key although a node passed the filters: never expected, never committed
+    } else {
+      const uint64_t win = acc.best;
+      const uint32_t slot = 0xFFFFFFFFu - (uint32_t)win;
+      r.node_index = (int32_t)slot;
+      r.status = 0;
+      r.total_score = (int64_t)(win >> 32) - 1;
+      r.flags = acc.feasible == 1 ? 1u : 0u;  // KS_RESULT_SINGLE_FEASIBLE
+      if (!a.no_commit) {
+        const uint32_t pos = a.slot_pos[slot];
+        a.t.rcpu[pos] += p.req_cpu;
+        a.t.rmem[pos] += p.req_mem;
+        a.t.zcpu[pos] += p.nz_cpu;
+        a.t.zmem[pos] += p.nz_mem;
+        a.t.npods[pos] += 1;
+        uint64_t m = a.cmask[a.pod];
+        while (m) {
+          const uint32_t cls = (uint32_t)__builtin_ctzll(m);
+          m &= m - 1;
+          a.cnt[(size_t)cls * a.npos + pos] += 1;
+        }
+        a.counters[1] += 1;  // pods resolved
+      }
+    }
+  } else if (!a.no_commit) {
+    a.counters[1] += 1;
+  }
+  if (!a.no_commit) a.results[a.pod] = r;
+  for (int q = 0; q <= NFILT; ++q) acc.fail[q] = 0;
+  acc.feasible = acc.ignored = acc.tt_max = acc.na_max = 0;
+  for (int c = 0; c < MAX_SPREAD; ++c) {
+    acc.min_match[c] = 0xFFFFFFFFu;
+    acc.ndomains[c] = 0;
+    acc.topo_size[c] = 0;
+  }
+  acc.pts_min = ~0ull;
+  acc.pts_max = 0;
+  acc.best = 0;
+}
+
+// Selector-class counts of the pods a round-kernel segment [lo, hi) bound.
+__global__ void class_commit_kernel(const DevResult *res, const uint64_t *cmask, const uint32_t *slot_pos,
+                                    uint32_t *cnt, uint32_t npos, uint32_t lo, uint32_t hi) {
+  const uint32_t i = lo + blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= hi) return;
+  uint64_t m = cmask[i];
+  if (!m || res[i].status != 0) return;
+  const uint32_t pos = slot_pos[res[i].node_index];
+  while (m) {
+    const uint32_t cls = (uint32_t)__builtin_ctzll(m);
+    m &= m - 1;
+    atomicAdd(&cnt[(size_t)cls * npos + pos], 1u);
+  }
+}
+
+// col[idx[i]] = val[i] / col[idx[i]] += delta[i] (domain and class columns).
+__global__ void scatter_u32_kernel(uint32_t *col, const uint64_t *idx, const uint32_t *val, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) col[idx[i]] = val[i];
+}
+__global__ void add_u32_kernel(uint32_t *col, const uint64_t *idx, const int32_t *delta, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) atomicAdd(&col[idx[i]], (uint32_t)delta[i]);
+}
+
+// ------------------------------------------------------------- launchers
+
+hipError_t launch_spread_pod(const SpreadArgs &a, bool has_filter, bool has_score, hipStream_t st) {
+  const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((a.npos + SP_THREADS - 1) / SP_THREADS, 2048));
+  spread_prep_kernel<<<blocks, SP_THREADS, 0, st>>>(a);
+  if (has_filter) spread_min_kernel<<<blocks, SP_THREADS, 0, st>>>(a);
+  spread_filter_kernel<<<blocks, SP_THREADS, 0, st>>>(a);
+  if (has_score) spread_score_kernel<<<blocks, SP_THREADS, 0, st>>>(a);
+  spread_select_kernel<<<blocks, SP_THREADS, 0, st>>>(a);
+  spread_commit_kernel<<<1, WAVE, 0, st>>>(a);
+  return hipGetLastError();
+}
+
+hipError_t launch_spread_reset(const SpreadArgs &a, hipStream_t st) {
+  SpreadArgs z = a;
+  z.no_commit = 1;  // reset only: no result, no commit
+  spread_commit_kernel<<<1, WAVE, 0, st>>>(z);
+  return hipGetLastError();
+}
+
+hipError_t launch_class_commit(const DevResult *res, const uint64_t *cmask, const uint32_t *slot_pos, uint32_t *cnt,
+                               uint32_t npos, uint32_t lo, uint32_t hi, hipStream_t st) {
+  if (hi <= lo) return hipSuccess;
+  class_commit_kernel<<<(hi - lo + 255) / 256, 256, 0, st>>>(res, cmask, slot_pos, cnt, npos, lo, hi);
+  return hipGetLastError();
+}
+
+hipError_t launch_scatter_u32(uint32_t *col, const uint64_t *idx, const uint32_t *val, uint32_t n, hipStream_t st) {
+  if (!n) return hipSuccess;
+  scatter_u32_kernel<<<(n + 255) / 256, 256, 0, st>>>(col, idx, val, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_add_u32(uint32_t *col, const uint64_t *idx, const int32_t *delta, uint32_t n, hipStream_t st) {
+  if (!n) return hipSuccess;
+  add_u32_kernel<<<(n + 255) / 256, 256, 0, st>>>(col, idx, delta, n);
+  return hipGetLastError();
+}
+
+}  // namespace ks

@@ -76,6 +76,31 @@ class KsPreferredTerm(C.Structure):
     _fields_ = [("preference", KsTerm), ("weight", C.c_int32), ("_pad", C.c_int32)]
 
 
+class KsLabelSelector(C.Structure):
+    _fields_ = [
+        ("match_labels", C.POINTER(KsLabel)),
+        ("match_expressions", C.POINTER(KsRequirement)),
+        ("n_match_labels", C.c_uint32),
+        ("n_match_expressions", C.c_uint32),
+        ("is_nil", C.c_uint32),
+        ("_pad", C.c_uint32),
+    ]
+
+
+class KsSpreadConstraint(C.Structure):
+    _fields_ = [
+        ("topology_key", c_char_p),
+        ("selector", KsLabelSelector),
+        ("match_label_keys", C.POINTER(c_char_p)),
+        ("n_match_label_keys", C.c_uint32),
+        ("max_skew", C.c_int32),
+        ("when_unsatisfiable", C.c_int32),
+        ("min_domains", C.c_int32),
+        ("node_affinity_policy", C.c_int32),
+        ("node_taints_policy", C.c_int32),
+    ]
+
+
 class KsPod(C.Structure):
     _fields_ = [
         ("ns", c_char_p),
@@ -99,11 +124,17 @@ class KsPod(C.Structure):
         ("has_preferred", C.c_uint32),
         ("has_overhead", C.c_uint32),
         ("unmodelled", C.c_uint32),
+        ("labels", C.POINTER(KsLabel)),
+        ("spread", C.POINTER(KsSpreadConstraint)),
+        ("n_labels", C.c_uint32),
+        ("n_spread", C.c_uint32),
+        ("spread_defaulted", C.c_uint32),
+        ("_pad2", C.c_uint32),
     ]
 
 
-NUM_FILTER_PLUGINS = 5
-NUM_FAIL_COUNTS = 6  # + KS_FAIL_PREFILTER_RESULT
+NUM_FILTER_PLUGINS = 6
+NUM_FAIL_COUNTS = 7  # + KS_FAIL_PREFILTER_RESULT
 # ks_status codes and ks_event kinds (include/ksched.h)
 KS_OK, KS_ERR_INVALID, KS_ERR_DEVICE, KS_ERR_CAPACITY, KS_ERR_UNSUPPORTED, KS_ERR_RANGE = 0, 1, 2, 3, 4, 5
 KS_ERR_NOT_FOUND, KS_ERR_COMM, KS_ERR_STALE = 6, 7, 8
@@ -131,7 +162,6 @@ class KsResult(C.Structure):
         ("evaluated_nodes", C.c_uint32),
         ("fail_counts", C.c_uint32 * NUM_FAIL_COUNTS),
         ("flags", C.c_uint32),
-        ("_pad", C.c_uint32),
     ]
 
 
@@ -145,6 +175,8 @@ class KsNodeScore(C.Structure):
         ("affinity_raw", C.c_int32),
         ("affinity_score", C.c_int32),
         ("image_locality", C.c_int32),
+        ("spread_raw", C.c_int32),
+        ("spread_score", C.c_int32),
         ("total_score", C.c_int64),
     ]
 
@@ -178,6 +210,7 @@ class KsConfig(C.Structure):
         ("weight_affinity", C.c_int32),
         ("weight_image", C.c_int32),
         ("percentage_of_nodes_to_score", C.c_int32),
+        ("weight_topology_spread", C.c_int32),
     ]
 
 
@@ -197,15 +230,16 @@ class KsStats(C.Structure):
 # sizes from the C headers (checked in tests/test_abi.py against offsetof via the compiler)
 EXPECTED_SIZES = {
     "ks_label": 16, "ks_taint": 24, "ks_toleration": 24, "ks_node": 72, "ks_container": 32,
-    "ks_requirement": 24, "ks_term": 24, "ks_preferred_term": 32, "ks_pod": 128, "ks_event": 24, "ks_result": 56,
-    "ks_node_score": 40, "ks_node_state": 56, "ks_config": 56, "ks_stats": 64,
+    "ks_requirement": 24, "ks_term": 24, "ks_preferred_term": 32, "ks_pod": 160, "ks_event": 24, "ks_result": 56,
+    "ks_node_score": 48, "ks_node_state": 56, "ks_config": 60, "ks_stats": 64, "ks_label_selector": 32,
+    "ks_spread_constraint": 72,
 }
 STRUCTS = {
     "ks_label": KsLabel, "ks_taint": KsTaint, "ks_toleration": KsToleration, "ks_node": KsNode,
     "ks_container": KsContainer, "ks_requirement": KsRequirement, "ks_term": KsTerm,
     "ks_preferred_term": KsPreferredTerm, "ks_pod": KsPod, "ks_event": KsEvent, "ks_result": KsResult,
     "ks_node_score": KsNodeScore, "ks_node_state": KsNodeState, "ks_config": KsConfig,
-    "ks_stats": KsStats,
+    "ks_stats": KsStats, "ks_label_selector": KsLabelSelector, "ks_spread_constraint": KsSpreadConstraint,
 }
 
 KSCHED_SYMBOLS = [

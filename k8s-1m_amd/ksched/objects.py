@@ -61,6 +61,39 @@ class PreferredSchedulingTerm:
 
 
 @dataclass
+class LabelSelectorRequirement:
+    key: str
+    operator: str  # In / NotIn / Exists / DoesNotExist
+    values: List[str] = field(default_factory=list)
+
+
+@dataclass
+class LabelSelector:
+    match_labels: Dict[str, str] = field(default_factory=dict)
+    match_expressions: List[LabelSelectorRequirement] = field(default_factory=list)
+
+
+@dataclass
+class TopologySpreadConstraint:
+    max_skew: int
+    topology_key: str
+    when_unsatisfiable: str = "DoNotSchedule"  # or "ScheduleAnyway"
+    label_selector: Optional[LabelSelector] = None  # None = nil (selects no pod)
+    min_domains: Optional[int] = None
+    node_affinity_policy: Optional[str] = None  # "Honor" / "Ignore" (None = Honor)
+    node_taints_policy: Optional[str] = None    # "Honor" / "Ignore" (None = Ignore)
+    match_label_keys: List[str] = field(default_factory=list)
+
+
+# PodTopologySpread's system-default constraints (upstream
+# podtopologyspread.systemDefaultConstraints), applied with the pod's
+# DefaultSelector when it has no constraints of its own.
+def system_default_spread(selector: LabelSelector) -> List[TopologySpreadConstraint]:
+    return [TopologySpreadConstraint(3, "kubernetes.io/hostname", "ScheduleAnyway", selector),
+            TopologySpreadConstraint(5, "topology.kubernetes.io/zone", "ScheduleAnyway", selector)]
+
+
+@dataclass
 class Node:
     name: str
     allocatable: Dict[str, int]  # {"cpu": millicores, "memory": bytes, "pods": count}
@@ -87,6 +120,9 @@ class Pod:
     overhead: Optional[Dict[str, int]] = None
     # features whose plugins ksched does not model (ksched.h KS_UNMODELLED_*): names from _abi.UNMODELLED
     unmodelled: List[str] = field(default_factory=list)
+    labels: Dict[str, str] = field(default_factory=dict)
+    topology_spread: List[TopologySpreadConstraint] = field(default_factory=list)
+    spread_defaulted: bool = False  # topology_spread holds the system defaults (see ksched.h ks_pod)
 
 
 class Arena:
@@ -132,6 +168,27 @@ def _term(t: NodeSelectorTerm, a: Arena) -> _abi.KsTerm:
     return _abi.KsTerm(ex, fl, nx, nf)
 
 
+WHEN = {"DoNotSchedule": 0, "ScheduleAnyway": 1}
+POLICY = {None: 0, "Honor": 1, "Ignore": 2}
+
+
+def _selector(sel: Optional[LabelSelector], a: Arena) -> _abi.KsLabelSelector:
+    if sel is None:
+        return _abi.KsLabelSelector(None, None, 0, 0, 1, 0)
+    ml, nml = a.array(_abi.KsLabel, [_abi.KsLabel(a.s(k), a.s(v)) for k, v in sel.match_labels.items()])
+    ex, nex = a.array(_abi.KsRequirement, [
+        _abi.KsRequirement(a.s(r.key), *a.array(C.c_char_p, [a.s(v) for v in r.values]), SEL_OPS.get(r.operator, 6))
+        for r in sel.match_expressions])
+    return _abi.KsLabelSelector(ml, ex, nml, nex, 0, 0)
+
+
+def _spread(c: TopologySpreadConstraint, a: Arena) -> _abi.KsSpreadConstraint:
+    keys, nk = a.array(C.c_char_p, [a.s(k) for k in c.match_label_keys])
+    return _abi.KsSpreadConstraint(a.s(c.topology_key), _selector(c.label_selector, a), keys, nk, c.max_skew,
+                                   WHEN.get(c.when_unsatisfiable, 9), c.min_domains or 0,
+                                   POLICY.get(c.node_affinity_policy, 9), POLICY.get(c.node_taints_policy, 9))
+
+
 def node_to_c(n: Node, a: Arena) -> _abi.KsNode:
     labels, nl = a.array(_abi.KsLabel, [_abi.KsLabel(a.s(k), a.s(v)) for k, v in n.labels.items()])
     taints, nt = a.array(
@@ -153,11 +210,14 @@ def pod_to_c(p: Pod, a: Arena) -> _abi.KsPod:
     pref, npref = a.array(_abi.KsPreferredTerm, [
         _abi.KsPreferredTerm(_term(t.preference, a), t.weight, 0) for t in (p.preferred or [])])
     ov = p.overhead or {}
+    labels, nlab = a.array(_abi.KsLabel, [_abi.KsLabel(a.s(k), a.s(v)) for k, v in p.labels.items()])
+    spread, nsp = a.array(_abi.KsSpreadConstraint, [_spread(c, a) for c in p.topology_spread])
     return _abi.KsPod(
         a.s(p.namespace), a.s(p.name), cs, ics, tols, sel, req, pref, a.s(p.node_name),
         ov.get("cpu", 0), ov.get("memory", 0), ncs, nics, ntol, nsel, nreq,
         0 if p.required_terms is None else 1, npref, 0 if p.preferred is None else 1,
-        0 if p.overhead is None else 1, sum(_abi.UNMODELLED[u] for u in p.unmodelled))
+        0 if p.overhead is None else 1, sum(_abi.UNMODELLED[u] for u in p.unmodelled),
+        labels, spread, nlab, nsp, 1 if p.spread_defaulted else 0, 0)
 
 
 def nodes_array(nodes: List[Node], a: Arena):

@@ -53,6 +53,13 @@ struct Node {
   // NodeInfo.Requested / NonZeroRequested / len(Pods)
   int64_t req_cpu = 0, req_mem = 0, nz_cpu = 0, nz_mem = 0;
   int64_t pods = 0;
+  // NodeInfo.Pods' namespace and labels (PodTopologySpread counts them)
+  struct PodRec {
+    std::string ns;
+    std::map<std::string, std::string> labels;
+    bool operator==(const PodRec &o) const { return ns == o.ns && labels == o.labels; }
+  };
+  std::vector<PodRec> pod_recs;
 };
 
 // k8s.io/api/core/v1/toleration.go#ToleratesTaint
@@ -169,6 +176,9 @@ bool NewRequirement(const std::string &key, SelOp op, const std::vector<std::str
     case SEL_EXISTS:
     case SEL_DOES_NOT_EXIST:
       if (!vals.empty()) ok = false;
+      break;
+    case SEL_EQUALS:
+      if (vals.size() != 1) ok = false;
       break;
     case SEL_GT:
     case SEL_LT:
@@ -288,6 +298,63 @@ NodeSelectorTerm newNodeSelectorTerm(const ks_term &t) {
   return out;
 }
 
+// ------------------------------------------------------ labels.Selector
+
+// apimachinery/pkg/labels: the internalSelector of LabelSelectorAsSelector
+// (Everything() = no requirement, Nothing() = nil LabelSelector).
+struct Selector {
+  bool nothing = false;
+  std::vector<Requirement> reqs;
+  bool Empty() const { return !nothing && reqs.empty(); }
+  bool Match(const std::map<std::string, std::string> &ls) const {
+    if (nothing) return false;
+    for (auto &r : reqs)
+      if (!Matches(r, ls)) return false;
+    return true;
+  }
+};
+
+// metav1.LabelSelectorAsSelector; false on a parse error.
+bool LabelSelectorAsSelector(const ks_label_selector &ls, Selector *out) {
+  *out = Selector{};
+  if (ls.is_nil) {
+    out->nothing = true;
+    return true;
+  }
+  for (uint32_t i = 0; i < ls.n_match_labels; ++i) {
+    Requirement r;
+    if (!NewRequirement(S(ls.match_labels[i].key), SEL_EQUALS, {S(ls.match_labels[i].value)}, &r)) return false;
+    out->reqs.push_back(r);
+  }
+  for (uint32_t i = 0; i < ls.n_match_expressions; ++i) {
+    const ks_requirement &e = ls.match_expressions[i];
+    SelOp op;
+    switch (e.op) {
+      case KS_OP_IN: op = SEL_IN; break;
+      case KS_OP_NOT_IN: op = SEL_NOT_IN; break;
+      case KS_OP_EXISTS: op = SEL_EXISTS; break;
+      case KS_OP_DOES_NOT_EXIST: op = SEL_DOES_NOT_EXIST; break;
+      default: return false;  // "is not a valid label selector operator"
+    }
+    std::vector<std::string> vals;
+    for (uint32_t k = 0; k < e.n_values; ++k) vals.push_back(S(e.values[k]));
+    Requirement r;
+    if (!NewRequirement(S(e.key), op, vals, &r)) return false;
+    out->reqs.push_back(r);
+  }
+  return true;
+}
+
+// podtopologyspread/common.go: one constraint after filterTopologySpreadConstraints.
+struct SpreadConstraint {
+  int32_t max_skew = 1;
+  std::string key;
+  Selector sel;
+  int32_t min_domains = 1;
+  bool aff_honor = true, taint_honor = false;
+  bool hostname = false;  // topologyKey == v1.LabelHostname (scoring counts per node)
+};
+
 // ------------------------------------------------------------ pod state
 
 struct PodState {
@@ -312,6 +379,13 @@ struct PodState {
   bool has_preferred = false;
   bool preferred_error = false;
   std::vector<std::pair<int64_t, NodeSelectorTerm>> preferred;
+  // PodTopologySpread: DoNotSchedule (Filter) and ScheduleAnyway (Score)
+  // constraints; requireAllTopologies = !spread_defaulted
+  std::string ns;
+  std::map<std::string, std::string> labels;
+  std::vector<SpreadConstraint> spread_filter, spread_score;
+  bool spread_defaulted = false;
+  bool spread_error = false;  // a selector failed to parse (the product refuses the pod)
 };
 
 // upstream:pkg/api/v1/resource/helpers.go#PodRequests for cpu/memory.
@@ -419,6 +493,30 @@ PodState compile_pod(const ks_pod &p) {
       }
     }
   }
+  st.ns = S(p.ns);
+  for (uint32_t i = 0; i < p.n_labels; ++i) st.labels[S(p.labels[i].key)] = S(p.labels[i].value);
+  // podtopologyspread/common.go#filterTopologySpreadConstraints, per action
+  st.spread_defaulted = p.spread_defaulted != 0;
+  for (uint32_t i = 0; i < p.n_spread; ++i) {
+    const ks_spread_constraint &c = p.spread[i];
+    SpreadConstraint sc;
+    sc.max_skew = c.max_skew;
+    sc.key = S(c.topology_key);
+    sc.hostname = sc.key == "kubernetes.io/hostname";
+    if (!LabelSelectorAsSelector(c.selector, &sc.sel)) st.spread_error = true;
+    // MatchLabelKeys: the incoming pod's values merged into the selector
+    // (mergeLabelSetWithSelector: a Nothing() selector stays Nothing())
+    std::vector<Requirement> extra;
+    for (uint32_t k = 0; k < c.n_match_label_keys; ++k) {
+      auto it = st.labels.find(S(c.match_label_keys[k]));
+      if (it != st.labels.end()) extra.push_back(Requirement{it->first, SEL_EQUALS, {it->second}});
+    }
+    if (!extra.empty() && !sc.sel.nothing) sc.sel.reqs.insert(sc.sel.reqs.begin(), extra.begin(), extra.end());
+    if (c.min_domains != 0) sc.min_domains = c.min_domains;
+    if (c.node_affinity_policy != KS_INCLUSION_DEFAULT) sc.aff_honor = c.node_affinity_policy == KS_INCLUSION_HONOR;
+    if (c.node_taints_policy != KS_INCLUSION_DEFAULT) sc.taint_honor = c.node_taints_policy == KS_INCLUSION_HONOR;
+    (c.when_unsatisfiable == KS_DO_NOT_SCHEDULE ? st.spread_filter : st.spread_score).push_back(sc);
+  }
   st.has_preferred = p.has_preferred != 0;
   for (uint32_t i = 0; i < p.n_preferred; ++i) {
     const ks_preferred_term &t = p.preferred[i];
@@ -428,6 +526,28 @@ PodState compile_pod(const ks_pod &p) {
     else st.preferred.emplace_back((int64_t)t.weight, term);
   }
   return st;
+}
+
+// nodeaffinity.GetRequiredNodeAffinity(pod).Match(node), parse errors ignored
+bool RequiredMatch(const PodState &st, const Node &n) {
+  if (st.affinity_skip) return true;
+  for (auto &r : st.node_selector)
+    if (!Matches(r, n.labels)) return false;
+  if (st.has_required) {
+    for (auto &t : st.required)
+      if (t.match(n)) return true;
+    return false;
+  }
+  return true;
+}
+
+// v1helper.FindMatchingUntoleratedTaint(taints, tolerations, DoNotScheduleTaintsFilterFunc)
+bool HasUntoleratedDoNotSchedule(const PodState &st, const Node &n) {
+  for (auto &t : n.taints) {
+    if (t.effect != KS_EFFECT_NO_SCHEDULE && t.effect != KS_EFFECT_NO_EXECUTE) continue;
+    if (!TolerationsTolerateTaint(st.tolerations, t)) return true;
+  }
+  return false;
 }
 
 // -------------------------------------------------------------- filters
@@ -456,16 +576,7 @@ int Filter(const PodState &st, const Node &n) {
     if (!TolerationsTolerateTaint(st.tolerations, t)) return KS_PLUGIN_TAINT_TOLERATION;
   }
   // nodeaffinity#Filter: RequiredNodeAffinity.Match (parse errors ignored)
-  if (!st.affinity_skip) {
-    for (auto &r : st.node_selector)
-      if (!Matches(r, n.labels)) return KS_PLUGIN_NODE_AFFINITY;
-    if (st.has_required) {
-      bool any = false;
-      for (auto &t : st.required)
-        if (t.match(n)) { any = true; break; }
-      if (!any) return KS_PLUGIN_NODE_AFFINITY;
-    }
-  }
+  if (!RequiredMatch(st, n)) return KS_PLUGIN_NODE_AFFINITY;
   // noderesources/fit.go#fitsRequest
   bool fail = false;
   if (n.pods + 1 > n.alloc_pods) fail = true;
@@ -546,6 +657,101 @@ int64_t Normalize(int64_t score, int64_t maxCount, bool reverse) {
   return reverse ? kMaxNodeScore - s : s;
 }
 
+// Go math.Log (pure-Go log.go, the fdlibm e_log.c algorithm; the amd64
+// assembly version performs the same operations), no FMA contraction.
+double GoLog(double x) {
+  const double Ln2Hi = 6.93147180369123816490e-01, Ln2Lo = 1.90821492927058770002e-10;
+  const double L1 = 6.666666666666735130e-01, L2 = 3.999999999940941908e-01, L3 = 2.857142874366239149e-01,
+               L4 = 2.222219843214978396e-01, L5 = 1.818357216161805012e-01, L6 = 1.531383769920937332e-01,
+               L7 = 1.479819860511658591e-01;
+  if (std::isnan(x) || std::isinf(x)) return x;
+  if (x < 0) return std::nan("");
+  if (x == 0) return -INFINITY;
+  int ki;
+  double f1 = std::frexp(x, &ki);
+  if (f1 < 0.70710678118654752440 /* Sqrt2/2 */) {
+    f1 *= 2;
+    ki--;
+  }
+  const double f = f1 - 1;
+  const double k = (double)ki;
+  const double s = f / (2 + f);
+  const double s2 = s * s;
+  const double s4 = s2 * s2;
+  const double t1 = s2 * (L1 + s4 * (L3 + s4 * (L5 + s4 * L7)));
+  const double t2 = s4 * (L2 + s4 * (L4 + s4 * L6));
+  const double R = t1 + t2;
+  const double hfsq = 0.5 * f * f;
+  return k * Ln2Hi - ((hfsq - (s * (hfsq + R) + k * Ln2Lo)) - f);
+}
+
+// podtopologyspread/common.go#countPodsMatchSelector
+int64_t CountPodsMatchSelector(const Node &n, const Selector &sel, const std::string &ns) {
+  if (sel.Empty()) return 0;
+  int64_t c = 0;
+  for (auto &r : n.pod_recs)
+    if (r.ns == ns && sel.Match(r.labels)) ++c;
+  return c;
+}
+
+// common.go#nodeLabelsMatchSpreadConstraints
+bool HasAllKeys(const Node &n, const std::vector<SpreadConstraint> &cs) {
+  for (auto &c : cs)
+    if (!n.labels.count(c.key)) return false;
+  return true;
+}
+
+// topologySpreadConstraint.matchNodeInclusionPolicies
+bool MatchInclusion(const SpreadConstraint &c, const PodState &st, const Node &n) {
+  if (c.aff_honor && !RequiredMatch(st, n)) return false;
+  if (c.taint_honor && HasUntoleratedDoNotSchedule(st, n)) return false;
+  return true;
+}
+
+// filtering.go#calPreFilterState: matching pods per topology value of every
+// DoNotSchedule constraint over all nodes, and the global minimum
+// (criticalPaths[0], 0 when fewer domains than minDomains).
+struct SpreadFilterState {
+  std::vector<std::map<std::string, int64_t>> counts;
+  std::vector<int64_t> min_match;
+};
+
+SpreadFilterState SpreadPreFilter(const PodState &st, const std::vector<Node> &nodes) {
+  SpreadFilterState s;
+  const size_t nc = st.spread_filter.size();
+  s.counts.resize(nc);
+  s.min_match.assign(nc, 0);
+  for (auto &n : nodes) {
+    if (!n.present || !HasAllKeys(n, st.spread_filter)) continue;
+    for (size_t i = 0; i < nc; ++i) {
+      const SpreadConstraint &c = st.spread_filter[i];
+      if (!MatchInclusion(c, st, n)) continue;
+      s.counts[i][n.labels.at(c.key)] += CountPodsMatchSelector(n, c.sel, st.ns);
+    }
+  }
+  for (size_t i = 0; i < nc; ++i) {
+    int64_t m = INT32_MAX;  // newCriticalPaths: MatchNum = math.MaxInt32
+    for (auto &kv : s.counts[i]) m = std::min(m, kv.second);
+    if ((int64_t)s.counts[i].size() < st.spread_filter[i].min_domains) m = 0;  // minMatchNum
+    s.min_match[i] = m;
+  }
+  return s;
+}
+
+// filtering.go#Filter: 'existing matching num' + 'self-match' - 'global min' <= maxSkew
+bool SpreadFilter(const PodState &st, const SpreadFilterState &s, const Node &n) {
+  for (size_t i = 0; i < st.spread_filter.size(); ++i) {
+    const SpreadConstraint &c = st.spread_filter[i];
+    auto it = n.labels.find(c.key);
+    if (it == n.labels.end()) return false;  // ErrReasonNodeLabelNotMatch
+    const int64_t self = c.sel.Match(st.labels) ? 1 : 0;
+    auto m = s.counts[i].find(it->second);
+    const int64_t match = m == s.counts[i].end() ? 0 : m->second;
+    if (match + self - s.min_match[i] > (int64_t)c.max_skew) return false;  // ErrReasonConstraintsNotMatch
+  }
+  return true;
+}
+
 inline uint64_t PackKey(int64_t total, uint32_t slot) {
   return ((uint64_t)(total + 1) << 32) | (uint64_t)(0xFFFFFFFFu - slot);
 }
@@ -556,18 +762,22 @@ inline uint64_t PackKey(int64_t total, uint32_t slot) {
 
 struct oracle {
   std::vector<Node> nodes;
-  int64_t w_fit, w_ba, w_tt, w_na, w_il;
+  int64_t w_fit, w_ba, w_tt, w_na, w_il, w_pts = 2;
   int threads = 1;
 
   struct Eval {
     int status;
     int64_t la, ba, tt_raw, na_raw;
+    int64_t pts_raw, pts;  // PodTopologySpread raw / normalized (ScheduleAnyway constraints)
   };
   std::vector<Eval> ev;  // per-node scratch, reused across pods
 
-  Eval eval(const PodState &st, const Node &n) const {
+  Eval eval(const PodState &st, const Node &n, const SpreadFilterState *sf = nullptr) const {
     Eval e{};
     e.status = Filter(st, n);
+    // PodTopologySpread.Filter follows NodeResourcesFit in the default profile
+    if (e.status < 0 && sf && !st.spread_filter.empty() && !SpreadFilter(st, *sf, n))
+      e.status = KS_PLUGIN_POD_TOPOLOGY_SPREAD;
     if (e.status >= 0) return e;
     e.la = LeastAllocated(n.alloc_cpu, n.alloc_mem, n.nz_cpu, n.nz_mem, st.nz_cpu, st.nz_mem);
     e.ba = BalancedAllocation(n.alloc_cpu, n.alloc_mem, n.req_cpu, n.req_mem, st.req_cpu, st.req_mem);
@@ -582,10 +792,20 @@ struct oracle {
     // preferred terms (PreScore Skip) and contributes nothing either way.
     int64_t t = w_fit * e.la + w_ba * e.ba + w_tt * Normalize(e.tt_raw, tt_max, true) + w_il * 0;
     if (st.has_preferred) t += w_na * Normalize(e.na_raw, na_max, false);
+    if (!st.spread_score.empty()) t += w_pts * e.pts;  // PreScore Skip without ScheduleAnyway constraints
     return t;
   }
 
   void add_pod(Node &n, const ks_pod &p, int sign) {
+    Node::PodRec rec;
+    rec.ns = S(p.ns);
+    for (uint32_t k = 0; k < p.n_labels; ++k) rec.labels[S(p.labels[k].key)] = S(p.labels[k].value);
+    if (sign > 0) {
+      n.pod_recs.push_back(std::move(rec));
+    } else {
+      auto it = std::find(n.pod_recs.begin(), n.pod_recs.end(), rec);
+      if (it != n.pod_recs.end()) n.pod_recs.erase(it);
+    }
     // framework/types.go#NodeInfo.update via calculateResource
     int64_t rc, rm, zc, zm;
     bool other = false;
@@ -621,6 +841,74 @@ struct oracle {
     for (auto &w : ws) w.join();
   }
 
+  // PodTopologySpread PreScore / Score / NormalizeScore (scoring.go) over the
+  // feasible nodes (ev[i].status < 0): fills ev[i].pts_raw / ev[i].pts.
+  void spread_score(const PodState &st, std::vector<Eval> &ev) const {
+    const auto &cs = st.spread_score;
+    if (cs.empty()) return;
+    const bool requireAll = !st.spread_defaulted;
+    const uint32_t N = (uint32_t)nodes.size();
+    const size_t nc = cs.size();
+    std::vector<char> ignored(N, 0);
+    int64_t n_filtered = 0, n_ignored = 0;
+    // initPreScoreState: topology values of the filtered (feasible) nodes
+    std::vector<std::map<std::string, int64_t>> counts(nc);
+    for (uint32_t i = 0; i < N; ++i) {
+      if (!nodes[i].present || ev[i].status >= 0) continue;
+      ++n_filtered;
+      if (requireAll && !HasAllKeys(nodes[i], cs)) {
+        ignored[i] = 1;
+        ++n_ignored;
+        continue;
+      }
+      for (size_t c = 0; c < nc; ++c) {
+        if (cs[c].hostname) continue;
+        auto it = nodes[i].labels.find(cs[c].key);
+        counts[c].emplace(it == nodes[i].labels.end() ? std::string() : it->second, 0);
+      }
+    }
+    std::vector<double> weight(nc);
+    for (size_t c = 0; c < nc; ++c) {
+      const int64_t sz = cs[c].hostname ? n_filtered - n_ignored : (int64_t)counts[c].size();
+      weight[c] = GoLog((double)(sz + 2));  // topologyNormalizingWeight
+    }
+    // PreScore processAllNode: matching pods of every node in a filtered domain
+    for (uint32_t i = 0; i < N; ++i) {
+      const Node &n = nodes[i];
+      if (!n.present) continue;
+      if (requireAll && !HasAllKeys(n, cs)) continue;
+      for (size_t c = 0; c < nc; ++c) {
+        if (cs[c].hostname || !MatchInclusion(cs[c], st, n)) continue;
+        auto it = n.labels.find(cs[c].key);
+        auto d = counts[c].find(it == n.labels.end() ? std::string() : it->second);
+        if (d == counts[c].end()) continue;
+        d->second += CountPodsMatchSelector(n, cs[c].sel, st.ns);
+      }
+    }
+    // Score: Σ cnt * weight + (maxSkew - 1), math.Round; NormalizeScore: min / max
+    int64_t mn = INT64_MAX, mx = 0;
+    for (uint32_t i = 0; i < N; ++i) {
+      if (!nodes[i].present || ev[i].status >= 0 || ignored[i]) continue;
+      const Node &n = nodes[i];
+      double score = 0;
+      for (size_t c = 0; c < nc; ++c) {
+        auto it = n.labels.find(cs[c].key);
+        if (it == n.labels.end()) continue;
+        const int64_t cnt = cs[c].hostname ? CountPodsMatchSelector(n, cs[c].sel, st.ns) : counts[c].at(it->second);
+        score += (double)cnt * weight[c] + (double)(cs[c].max_skew - 1);  // scoreForCount
+      }
+      ev[i].pts_raw = (int64_t)std::round(score);
+      mn = std::min(mn, ev[i].pts_raw);
+      mx = std::max(mx, ev[i].pts_raw);
+    }
+    for (uint32_t i = 0; i < N; ++i) {
+      if (!nodes[i].present || ev[i].status >= 0) continue;
+      if (ignored[i]) ev[i].pts = 0;
+      else if (mx == 0) ev[i].pts = kMaxNodeScore;
+      else ev[i].pts = kMaxNodeScore * (mx + mn - ev[i].pts_raw) / mx;
+    }
+  }
+
   // schedulePod (schedule_one.go): findNodesThatFitPod -> prioritizeNodes -> selectHost.
   ks_result schedule_one(const ks_pod &p) {
     ks_result r{};
@@ -628,6 +916,8 @@ struct oracle {
     PodState st = compile_pod(p);
     const uint32_t N = (uint32_t)nodes.size();
     ev.resize(N);
+    SpreadFilterState sf;
+    if (!st.spread_filter.empty()) sf = SpreadPreFilter(st, nodes);
     // Filter + raw scores in parallel (findNodesThatPassFilters / RunScorePlugins
     // both fan out with parallelize.Until); counts and normaliser maxima are
     // order-independent reductions, combined from per-thread partials.
@@ -642,7 +932,7 @@ struct oracle {
       Part &q = part[t];
       for (uint32_t i = a; i < b; ++i) {
         if (!nodes[i].present) continue;
-        ev[i] = eval(st, nodes[i]);
+        ev[i] = eval(st, nodes[i], &sf);
         ++q.evaluated;
         if (ev[i].status >= 0) {
           q.fail[ev[i].status]++;
@@ -674,6 +964,7 @@ struct oracle {
     if (feasible == 1) {
       // "When only one node after predicate, just use it." No scoring upstream;
       // the build still reports that node's TotalScore.
+      spread_score(st, ev);
       r.flags |= KS_RESULT_SINGLE_FEASIBLE;
       r.node_index = (int32_t)only;
       r.total_score = total(st, ev[only], tt_max, na_max);
@@ -684,6 +975,7 @@ struct oracle {
       r.status = KS_POD_ERROR;
       return r;
     }
+    spread_score(st, ev);
     for_nodes(0, N, [&](uint32_t a, uint32_t b, int t) {
       uint64_t &best = part[t].best;
       for (uint32_t i = a; i < b; ++i) {
@@ -715,6 +1007,8 @@ oracle *oracle_new(uint32_t cap, int32_t w_fit, int32_t w_ba, int32_t w_tt, int3
 }
 void oracle_free(oracle *o) { delete o; }
 void oracle_set_threads(oracle *o, int32_t t) { o->threads = t < 1 ? 1 : t; }
+void oracle_set_weight_spread(oracle *o, int32_t w) { o->w_pts = w; }
+double oracle_go_log(double x) { return GoLog(x); }
 
 int32_t oracle_nodes_upsert(oracle *o, const ks_node *nodes, const uint32_t *slots, uint32_t n) {
   for (uint32_t i = 0; i < n; ++i) {
@@ -775,9 +1069,14 @@ int32_t oracle_plugin_scores(oracle *o, const ks_pod *pod, ks_node_score *out) {
   const uint32_t N = (uint32_t)o->nodes.size();
   std::vector<oracle::Eval> ev(N);
   int64_t tt_max = 0, na_max = 0;
+  SpreadFilterState sf;
+  if (!st.spread_filter.empty()) sf = SpreadPreFilter(st, o->nodes);
   for (uint32_t i = 0; i < N; ++i) {
-    if (!o->nodes[i].present) continue;
-    ev[i] = o->eval(st, o->nodes[i]);
+    if (!o->nodes[i].present) {
+      ev[i].status = -2;
+      continue;
+    }
+    ev[i] = o->eval(st, o->nodes[i], &sf);
     if (ev[i].status < 0) {
       tt_max = std::max(tt_max, ev[i].tt_raw);
       na_max = std::max(na_max, ev[i].na_raw);
@@ -785,6 +1084,7 @@ int32_t oracle_plugin_scores(oracle *o, const ks_pod *pod, ks_node_score *out) {
   }
   for (uint32_t i = 0; i < N; ++i) {
     ks_node_score s{};
+    if (i == 0) o->spread_score(st, ev);  // PodTopologySpread over the feasible set
     if (!o->nodes[i].present) {
       s.status = -2;
     } else if (ev[i].status >= 0) {
@@ -798,6 +1098,8 @@ int32_t oracle_plugin_scores(oracle *o, const ks_pod *pod, ks_node_score *out) {
       s.affinity_raw = (int32_t)ev[i].na_raw;
       s.affinity_score = st.has_preferred ? (int32_t)Normalize(ev[i].na_raw, na_max, false) : 0;
       s.image_locality = 0;
+      s.spread_raw = (int32_t)ev[i].pts_raw;
+      s.spread_score = st.spread_score.empty() ? 0 : (int32_t)ev[i].pts;
       s.total_score = o->total(st, ev[i], tt_max, na_max);
     }
     out[i] = s;

@@ -32,6 +32,8 @@ oracle *oracle_new(uint32_t node_capacity, int32_t w_fit, int32_t w_balanced, in
 void oracle_free(oracle *o);
 /* Worker threads for the per-pod node loop (parallelize.Until chunking). */
 void oracle_set_threads(oracle *o, int32_t threads);
+/* PodTopologySpread score weight (default 2, the default profile's). */
+void oracle_set_weight_spread(oracle *o, int32_t w);
 
 int32_t oracle_nodes_upsert(oracle *o, const ks_node *nodes, const uint32_t *slots, uint32_t n);
 int32_t oracle_nodes_delete(oracle *o, const uint32_t *slots, uint32_t n);
@@ -64,6 +66,7 @@ uint64_t oracle_shard_best(oracle *o, const ks_pod *pod, uint32_t lo, uint32_t h
 int32_t oracle_commit(oracle *o, const ks_pod *pod, uint32_t slot);
 
 /* Scalar plugin arithmetic for known-answer tests. */
+double oracle_go_log(double x); /* Go math.Log (topologyNormalizingWeight) */
 int64_t oracle_least_allocated(int64_t alloc_cpu, int64_t alloc_mem, int64_t node_nz_cpu,
                                int64_t node_nz_mem, int64_t pod_nz_cpu, int64_t pod_nz_mem);
 int64_t oracle_balanced_allocation(int64_t alloc_cpu, int64_t alloc_mem, int64_t node_req_cpu,

@@ -20,7 +20,7 @@ LIB = ROOT / "oracle" / "_build" / "liboracle.so"
 class ShardPrescore(C.Structure):
     _fields_ = [
         ("feasible", C.c_uint32),
-        ("fail_counts", C.c_uint32 * 6),
+        ("fail_counts", C.c_uint32 * 7),
         ("taint_max", C.c_int64),
         ("affinity_max", C.c_int64),
         ("taint_count", C.c_uint32),
@@ -47,6 +47,8 @@ def lib() -> C.CDLL:
     L.oracle_free.restype = None
     L.oracle_set_threads.argtypes = [vp, C.c_int32]
     L.oracle_set_threads.restype = None
+    L.oracle_set_weight_spread.argtypes = [vp, C.c_int32]
+    L.oracle_set_weight_spread.restype = None
     L.oracle_nodes_upsert.argtypes = [vp, P(_abi.KsNode), P(C.c_uint32), C.c_uint32]
     L.oracle_nodes_delete.argtypes = [vp, P(C.c_uint32), C.c_uint32]
     L.oracle_pods_add.argtypes = [vp, P(_abi.KsPod), P(C.c_uint32), C.c_uint32]
@@ -61,15 +63,19 @@ def lib() -> C.CDLL:
     for f in ("oracle_least_allocated", "oracle_balanced_allocation"):
         getattr(L, f).argtypes = [C.c_int64] * 6
         getattr(L, f).restype = C.c_int64
+    L.oracle_go_log.argtypes = [C.c_double]
+    L.oracle_go_log.restype = C.c_double
     L.oracle_pod_requests.argtypes = [P(_abi.KsPod), P(C.c_int64)]
     _lib = L
     return L
 
 
 class Oracle:
-    def __init__(self, capacity: int, weights=(1, 1, 3, 2, 1), threads: int = 1):
+    def __init__(self, capacity: int, weights=(1, 1, 3, 2, 1, 2), threads: int = 1):
         self.L = lib()
-        self.o = self.L.oracle_new(capacity, *weights)
+        self.o = self.L.oracle_new(capacity, *weights[:5])
+        if len(weights) > 5:
+            self.L.oracle_set_weight_spread(self.o, weights[5])
         self.capacity = capacity
         if threads > 1:
             self.L.oracle_set_threads(self.o, threads)

@@ -28,7 +28,7 @@ def test_libksched_exports_every_declared_symbol():
     lib = _abi.ksched_lib()
     for name in declared("ksched.h", "ks_"):
         assert hasattr(lib, name), name
-    assert lib.ks_abi_version() == 2
+    assert lib.ks_abi_version() == 3
 
 
 def test_libksynth_exports_every_declared_symbol():
@@ -54,6 +54,9 @@ C_PROBE = r"""
 int main(void) {
   S(ks_label) S(ks_taint) S(ks_toleration) S(ks_node) S(ks_container) S(ks_requirement) S(ks_term)
   S(ks_preferred_term) S(ks_pod) S(ks_event) S(ks_result) S(ks_node_score) S(ks_node_state) S(ks_config) S(ks_stats)
+  S(ks_label_selector) S(ks_spread_constraint)
+  O(ks_pod, labels) O(ks_pod, spread) O(ks_pod, spread_defaulted) O(ks_spread_constraint, max_skew)
+  O(ks_spread_constraint, node_taints_policy) O(ks_node_score, spread_score) O(ks_config, weight_topology_spread)
   O(ks_node, labels) O(ks_node, n_labels) O(ks_node, unschedulable)
   O(ks_pod, node_name) O(ks_pod, overhead_milli_cpu) O(ks_pod, n_containers) O(ks_pod, has_required)
   O(ks_pod, has_preferred) O(ks_pod, has_overhead)

@@ -135,4 +135,4 @@ def test_pod_requests_other_resource_flagged():
 
 def test_struct_layout_consistency():
     # pyoracle reuses the ksched ctypes structs: layout mirrors the header
-    assert C.sizeof(_abi.KsPod) == 128 and C.sizeof(_abi.KsNode) == 72 and C.sizeof(_abi.KsResult) == 56
+    assert C.sizeof(_abi.KsPod) == 160 and C.sizeof(_abi.KsNode) == 72 and C.sizeof(_abi.KsResult) == 56
