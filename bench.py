@@ -61,6 +61,13 @@ sys.path.insert(0, str(ROOT / "k8s-1m_amd"))
 
 B_NODE = 56  # node-row bytes per (pod, node) evaluation, resource-only
 B_NODE_LABELED = 96  # ... with label / taint bitsets (C4)
+# PodTopologySpread path: node-table bytes the kernel chain reads / writes per
+# (pod, node): prep 52 (slot, apods, taint / label / numeric
+# words, 2 domain ids, 1 class count), filter 101 (slot, 56-B resource row,
+# 32-B label / taint words, 2 domain ids, status), score 21 (status, domain
+# ids, class count, raw score), select 101 (status, slot, resource row,
+# label / taint words, raw score)
+B_SPREAD_NODE = 275
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # VALU issue peak: a wave64 VALU instruction occupies a 16-lane SIMD for 4
 # cycles (MI355X FP64 vector peak 78.6 TFLOP/s = 256 CUs x 4 SIMDs x 16 lanes
@@ -85,9 +92,11 @@ def parse():
     ap.add_argument("--pods-per-round", type=int, default=256)
     ap.add_argument("--topk", type=int, default=0)
     ap.add_argument("--nodes-per-lane", type=int, default=4)
-    ap.add_argument("--kind", default="hetero", choices=["hetero", "kwok", "labeled"])
-    ap.add_argument("--pods", default="default", choices=["default", "besteffort"],
-                    help="besteffort: request-less pods (kwok/make_pods/main.go:118-148)")
+    ap.add_argument("--kind", default="hetero", choices=["hetero", "kwok", "labeled", "zoned"])
+    ap.add_argument("--pods", default="default", choices=["default", "besteffort", "spread"],
+                    help="besteffort: request-less pods (kwok/make_pods/main.go:118-148); spread: "
+                         "deployment pods with PodTopologySpread constraints (use with --kind zoned)")
+    ap.add_argument("--apps", type=int, default=64, help="deployments of the --pods spread stream")
     ap.add_argument("--workload", default="batch", choices=["batch", "c5"],
                     help="batch: one batch of --batch pods per step; c5: one burst + its event log per step")
     ap.add_argument("--burst", type=int, default=100_000, help="pods per burst (--workload c5)")
@@ -102,6 +111,12 @@ def parse():
     a = ap.parse_args()
     if a.prefill is None:
         a.prefill = 0.0 if a.kind == "kwok" else 0.5
+    if a.pods == "spread":  # one pod at a time through the spread path: smaller steps and CPU samples
+        if a.batch == 32768:
+            a.batch = 2048
+        a.cpu_pods = min(a.cpu_pods, 4)
+        a.cpu_pods_mt = min(a.cpu_pods_mt, 16)
+        a.latency_calls = min(a.latency_calls, 10)
     return a
 
 
@@ -174,7 +189,7 @@ def main():
     # scheduler's own RCCL communicator for barriers and the max-over-ranks time.
     from ksched import Scheduler, synth
 
-    kind = {"hetero": synth.HETERO, "kwok": synth.KWOK, "labeled": synth.LABELED}[args.kind]
+    kind = {"hetero": synth.HETERO, "kwok": synth.KWOK, "labeled": synth.LABELED, "zoned": synth.ZONED}[args.kind]
     t_setup = time.time()
     sched = Scheduler(args.nodes, device=local_rank if world > 1 else 0, pods_per_round=args.pods_per_round,
                       topk=args.topk, nodes_per_lane=args.nodes_per_lane, world_size=world, rank=rank)
@@ -192,6 +207,8 @@ def pod_stream(args, kind, n, seed):
 
     if args.pods == "besteffort":
         return synth.besteffort_pods(n)
+    if args.pods == "spread":
+        return synth.spread_pods(n, args.apps, seed)
     return synth.pods(kind, n, seed)
 
 
@@ -407,6 +424,12 @@ def workload_name(args) -> str:
         return (f"C5: {n} heterogeneous nodes, prefill<50% cpu; bursts of {args.burst} resource-only pods, "
                 "each followed by its watch-event log (5% bound-pod deletes, 0.1% node updates, 0.01% node "
                 "deletes + adds) applied to the device cache; pct=100, in-order commit")
+    if args.pods == "spread":
+        return (f"spread: {n} heterogeneous nodes in 32 zones, prefill<{f:.0%} cpu (pods of 64 apps); "
+                f"pods of {args.apps} deployments with PodTopologySpread (half the system defaults: hostname "
+                "maxSkew 3 + zone maxSkew 5 ScheduleAnyway; half zone maxSkew 1 DoNotSchedule + hostname "
+                "maxSkew 1 ScheduleAnyway), every default Filter / Score plugin, pct=100, one pod at a time "
+                "(spread path)")
     pods = ("request-less busybox pods (kwok/make_pods)" if args.pods == "besteffort"
             else "resource-only pods (cpu 50-4000m, mem 64Mi x 1..256, 10% best-effort)")
     if args.kind == "hetero":
@@ -424,7 +447,7 @@ def workload_name(args) -> str:
 
 def pmc_key(args, world) -> str:
     """Name of the PMC summary measured for exactly this configuration."""
-    pods = "-be" if args.pods == "besteffort" else ""
+    pods = {"besteffort": "-be", "spread": "-spread"}.get(args.pods, "")
     return (f"{args.workload}_{args.kind}{pods}_n{args.nodes}_P{args.pods_per_round}_K{args.topk or args.pods_per_round}"
             f"_npl{args.nodes_per_lane}_w{world}")
 
@@ -436,7 +459,23 @@ def kernel_src_hash() -> str:
     return h.hexdigest()[:16]
 
 
+def roofline_spread(args, st):
+    """The spread path: HBM-bound node passes (B_SPREAD_NODE bytes per node per
+    pod), timed per pod with HIP events around the whole kernel chain."""
+    ms = st.spread_ms / max(1, st.spread_pods_timed)
+    traffic = B_SPREAD_NODE * args.nodes
+    ach = traffic / (ms * 1e-3) / 1e9 if ms else None
+    return {"bound": "hbm", "achieved": round(ach, 1) if ach else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None, "traffic": None,
+            "kernel": "ks::spread_* chain (prep, min, filter, score, select, commit)",
+            "ms_per_pod": round(ms, 4), "pods_timed": int(st.spread_pods_timed),
+            "algorithmic_bytes_per_pod": traffic,
+            "what": "B_SPREAD_NODE x nodes per pod / chain time (HIP events on every 8th pod)"}
+
+
 def roofline(args, st, world):
+    if args.pods == "spread":
+        return roofline_spread(args, st)
     labeled = args.kind == "labeled"
     sweep_avg_ms = st.sweep_ms / max(1, st.sweep_launches)
     evals_per_launch = st.sweep_evals / max(1, st.sweep_launches)
@@ -512,6 +551,7 @@ def report(args, sched, st, dbg, world, pods_timed, elapsed, scheduled, setup_s,
             "resolve_ms_per_round": round(st.resolve_ms / max(1, st.resolve_launches), 4),
             "sweep_ms_total": round(st.sweep_ms, 3),
             "resolve_ms_total": round(st.resolve_ms, 3),
+            "spread_pods": int(st.spread_pods),
             "scheduled_fraction": round(scheduled / pods_timed, 4),
             "speculated_rounds_wasted": int(dbg[3]),  # since open (warmup included)
             "pods_reswept_wrong_norm_guess": int(dbg[4]),  # since open (warmup included)

@@ -439,6 +439,9 @@ typedef struct {
   uint64_t sweep_evals;     /* Σ (pod, node) evaluations by timed sweeps   */
   double resolve_ms;        /* Σ device time of resolve launches           */
   uint64_t resolve_launches;
+  double spread_ms;         /* Σ device time of timed spread-path pods (whole kernel chain) */
+  uint64_t spread_pods_timed;
+  uint64_t spread_pods;     /* pods scheduled by the spread path           */
 } ks_stats;
 ks_status ks_get_stats(ks_ctx *ctx, ks_stats *out);
 ks_status ks_reset_stats(ks_ctx *ctx);

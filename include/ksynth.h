@@ -23,7 +23,9 @@ extern "C" {
 enum {
   KSYNTH_KWOK = 1,   /* C1: homogeneous kwok nodes                        */
   KSYNTH_HETERO = 2, /* C2/C3: heterogeneous shapes (+ prefill separately) */
-  KSYNTH_LABELED = 4 /* C4: C2 shapes + zone/instance-type/pool/feature/gpu labels and taints */
+  KSYNTH_LABELED = 4, /* C4: C2 shapes + zone/instance-type/pool/feature/gpu labels and taints */
+  KSYNTH_ZONED = 8    /* C2 shapes + topology.kubernetes.io/zone (32 zones); prefill pods carry
+                         app labels (PodTopologySpread workloads) */
 };
 
 typedef struct ksynth ksynth; /* owns every array and string it returns */
@@ -40,6 +42,13 @@ ksynth *ksynth_prefill(int32_t kind, uint32_t n_nodes, uint64_t nodes_seed, uint
                        double max_fill);
 /* Pods that request nothing (kwok/make_pods/main.go:138-148 best-effort busybox). */
 ksynth *ksynth_besteffort_pods(uint32_t n);
+/* Deployment-shaped pods with topology spread constraints: pod j belongs to
+ * app-k (k drawn from n_apps), labels {app: app-k}, C1 requests, kwok
+ * tolerations; half carry PodTopologySpread's system defaults (hostname
+ * maxSkew 3 + zone maxSkew 5, ScheduleAnyway, spread_defaulted), half their
+ * own [zone maxSkew 1 DoNotSchedule, hostname maxSkew 1 ScheduleAnyway], all
+ * selecting app=app-k. */
+ksynth *ksynth_spread_pods(uint32_t n, uint32_t n_apps, uint64_t seed);
 
 const ks_node *ksynth_node_array(const ksynth *s, uint32_t *n);
 const ks_pod *ksynth_pod_array(const ksynth *s, uint32_t *n);

@@ -144,15 +144,23 @@ static_assert(sizeof(SpreadDev) == 32, "SpreadDev layout");
 constexpr uint32_t SPREAD_WORDS = sizeof(SpreadDev) / 8;
 
 // Per-pod accumulators of the spread path (reset by its commit kernel).
-struct SpreadAcc {
+// Blocks add into ACC_SHARDS copies (block b -> copy b % ACC_SHARDS) and
+// readers combine the copies: hundreds of blocks' atomics on ONE address
+// serialise in L2 (~20 ns each: 2048 blocks cost +30 us per pass).
+constexpr int SPREAD_MAX_BLOCKS = 256;
+constexpr int ACC_SHARDS = 16;
+struct SpreadAccShard {
   uint32_t fail[NFILT + 1];            // first failures per plugin (+ PodTopologySpread)
   uint32_t feasible, ignored;          // feasible nodes; feasible nodes PreScore ignores
   uint32_t tt_max, na_max;             // max raw TaintToleration / NodeAffinity over feasible nodes
+  uint64_t pts_min, pts_max;           // raw PodTopologySpread min / max over non-ignored feasible nodes
+  uint64_t best;                       // packed key of the winner
+};
+struct SpreadAcc {
   uint32_t min_match[MAX_SPREAD];      // Filter: min matching pods over eligible domains
   uint32_t ndomains[MAX_SPREAD];       // Filter: eligible domains
   uint32_t topo_size[MAX_SPREAD];      // Score: domains of non-ignored feasible nodes
-  uint64_t pts_min, pts_max;           // Score: raw PodTopologySpread min / max over non-ignored feasible nodes
-  uint64_t best;                       // packed key of the winner
+  SpreadAccShard sh[ACC_SHARDS];
 };
 
 // ----------------------------------------------------------- round records

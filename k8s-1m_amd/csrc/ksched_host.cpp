@@ -323,16 +323,18 @@ struct ks_ctx {
   SpreadAcc *d_acc = nullptr;
   int8_t *d_sst = nullptr;
   int64_t *d_sraw = nullptr;
+  uint64_t *d_spart = nullptr;
   uint32_t *h_seg = nullptr;       // pinned: start pod of a round-kernel segment
   // comm
   ncclComm_t comm = nullptr;
   // stats
   ks_stats stats{};
   bool timing = false;
-  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_sweep, ev_resolve;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_sweep, ev_resolve, ev_spread;
   std::vector<hipEvent_t> ev_pool;
   uint64_t counters_base[4] = {0, 0, 0, 0};  // device counters at the last ks_reset_stats
   uint64_t sweeps_issued = 0;                // main sweep launches since then (timed or not)
+  uint64_t spread_seq = 0;                   // spread-path pods issued (timing sample)
   // Host<->device transfers of one ABI call: a pinned host staging buffer and a
   // device scratch buffer, both bump-allocated and reset at xfer_sync (no
   // pageable hipMemcpyAsync anywhere), on `stream`.  No fourth stream: the
@@ -1186,7 +1188,8 @@ ks_status spread_alloc(ks_ctx *c) {
   ks_status st;
   // domain columns then class columns, one allocation (one index space for scatters)
   if ((st = dalloc(c, &c->d_dom, (size_t)(MAX_TOPO_KEYS + MAX_CLASSES) * c->npos)) || (st = dalloc(c, &c->d_pos_slot, c->npos)) ||
-      (st = dalloc(c, &c->d_acc, 1)) || (st = dalloc(c, &c->d_sst, c->npos)) || (st = dalloc(c, &c->d_sraw, c->npos)))
+      (st = dalloc(c, &c->d_acc, 1)) || (st = dalloc(c, &c->d_sst, c->npos)) || (st = dalloc(c, &c->d_sraw, c->npos)) ||
+      (st = dalloc(c, &c->d_spart, c->npos)))
     return st;
   c->d_cnt = c->d_dom + (size_t)MAX_TOPO_KEYS * c->npos;
   HIPC(c, hipMemsetAsync(c->d_dom, 0xFF, (size_t)MAX_TOPO_KEYS * c->npos * 4, c->stream));
@@ -1194,7 +1197,7 @@ ks_status spread_alloc(ks_ctx *c) {
   for (uint32_t sl = 0; sl < c->cap; ++sl) ps[c->slot_pos[sl]] = sl;
   SpreadAcc acc{};
   for (int k = 0; k < MAX_SPREAD; ++k) acc.min_match[k] = 0xFFFFFFFFu;
-  acc.pts_min = ~0ull;
+  for (int k = 0; k < ACC_SHARDS; ++k) acc.sh[k].pts_min = ~0ull;
   if ((st = xfer_begin(c, (size_t)c->npos * 4 + sizeof acc + 1024, 0)) ||
       (st = h2d(c, c->d_pos_slot, ps.data(), (size_t)c->npos * 4)) || (st = h2d(c, c->d_acc, &acc, sizeof acc)) ||
       (st = xfer_sync(c)))
@@ -1531,8 +1534,17 @@ ks_status collect_timing(ks_ctx *c) {
     c->ev_pool.push_back(pr.first);
     c->ev_pool.push_back(pr.second);
   }
+  for (auto &pr : c->ev_spread) {
+    float ms = 0;
+    HIPC(c, hipEventElapsedTime(&ms, pr.first, pr.second));
+    c->stats.spread_ms += ms;
+    c->stats.spread_pods_timed++;
+    c->ev_pool.push_back(pr.first);
+    c->ev_pool.push_back(pr.second);
+  }
   c->ev_sweep.clear();
   c->ev_resolve.clear();
+  c->ev_spread.clear();
   return KS_OK;
 }
 
@@ -1879,6 +1891,7 @@ ks_status run_batch(ks_ctx *c, ks_batch *b) {
       sa.acc = c->d_acc;
       sa.st = c->d_sst;
       sa.raw = c->d_sraw;
+      sa.part = c->d_spart;
       sa.results = b->d_results;
       sa.counters = c->d_counters;
       sa.w = Weights{c->cfg.weight_fit, c->cfg.weight_balanced, c->cfg.weight_taint, c->cfg.weight_affinity,
@@ -1887,7 +1900,20 @@ ks_status run_batch(ks_ctx *c, ks_batch *b) {
       sa.evaluated = c->n_present;
       for (; hi < b->n && b->spread[hi]; ++hi) {
         sa.pod = hi;
+        // timing events on every KS_TIMING_EVERY-th spread pod
+        const bool tm = c->timing && ++c->spread_seq % c->timing_every == 0;
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        if (tm) {
+          e0 = get_event(c);
+          e1 = get_event(c);
+          HIPC(c, hipEventRecord(e0, c->stream));
+        }
         HIPC(c, launch_spread_pod(sa, (b->spread[hi] & 2) != 0, (b->spread[hi] & 4) != 0, c->stream));
+        if (tm) {
+          HIPC(c, hipEventRecord(e1, c->stream));
+          c->ev_spread.emplace_back(e0, e1);
+        }
+        c->stats.spread_pods++;
       }
       HIPC(c, hipMemcpyAsync(b->h_results + lo, b->d_results + lo, (size_t)(hi - lo) * sizeof(DevResult),
                              hipMemcpyDeviceToHost, c->stream));
@@ -2162,7 +2188,7 @@ void ks_close(ks_ctx *c) {
                   c->t.npods, c->t.hard, c->t.prefer, c->t.lab, c->t.num, c->d_shards, c->d_slot_pos,
                   c->d_start, c->d_norm, c->d_norm_inv, c->d_pstat, c->d_fix, c->d_brec, c->d_srec, c->d_frec,
                   c->d_counters, c->d_crow, c->d_cext, c->d_pipe, c->d_carry, c->d_flags, c->d_dom,
-                  c->d_pos_slot, c->d_dcnt, c->d_dflag, c->d_acc, c->d_sst, c->d_sraw};
+                  c->d_pos_slot, c->d_dcnt, c->d_dflag, c->d_acc, c->d_sst, c->d_sraw, c->d_spart};
   for (void *b : bufs)
     if (b) (void)hipFree(b);
   if (c->h_start) (void)hipHostFree(c->h_start);
@@ -2182,6 +2208,7 @@ void ks_close(ks_ctx *c) {
   }
   for (auto &pr : c->ev_sweep) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
   for (auto &pr : c->ev_resolve) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
+  for (auto &pr : c->ev_spread) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
   for (auto e : c->ev_pool) (void)hipEventDestroy(e);
   for (int q = 0; q < 2; ++q) {
     if (c->ev_sw[q]) (void)hipEventDestroy(c->ev_sw[q]);
@@ -2655,6 +2682,7 @@ SpreadArgs spread_args(ks_ctx *c) {
   sa.acc = c->d_acc;
   sa.st = c->d_sst;
   sa.raw = c->d_sraw;
+  sa.part = c->d_spart;
   sa.counters = c->d_counters;
   sa.w = Weights{c->cfg.weight_fit, c->cfg.weight_balanced, c->cfg.weight_taint, c->cfg.weight_affinity,
                  c->cfg.weight_image};

@@ -94,6 +94,7 @@ struct SpreadArgs {
   SpreadAcc *acc;
   int8_t *st;                 // [npos] status of every position for this pod
   int64_t *raw;               // [npos] PodTopologySpread raw score
+  uint64_t *part;             // [npos] normalisation-free score parts of feasible nodes (filter -> select)
   DevResult *results;
   int32_t *dump;              // ks_plugin_scores: [slots][SPREAD_DUMP_WORDS] (null: schedule)
   uint32_t no_commit;         // dump / reset: no result, no AssumePod

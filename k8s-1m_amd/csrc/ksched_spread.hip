@@ -33,7 +33,7 @@ namespace ks {
 
 namespace {
 
-constexpr int SP_THREADS = 256;
+constexpr int SP_THREADS = 1024;  // few fat blocks (at most SPREAD_MAX_BLOCKS): one partial record each
 constexpr uint32_t SP_LDS = 4096;     // LDS domain-histogram entries per block
 constexpr uint32_t SP_LDS_DOM = 1024; // keys with at most this many domains aggregate in LDS
 constexpr uint32_t SP_OFF_NONE = 0xFFFFFFFFu;
@@ -116,15 +116,39 @@ __device__ void lds_segments(const SpreadArgs &a, const SpreadDev *sd, uint32_t 
 
 __device__ __forceinline__ uint32_t grid_threads() { return gridDim.x * blockDim.x; }
 
+// Totals of the accumulator copies (ACC_SHARDS) written by the previous passes.
+struct Totals {
+  uint32_t fail[NFILT + 1];
+  uint32_t feasible, ignored, tt_max, na_max;
+  uint64_t pts_min, pts_max, best;
+};
+__device__ __forceinline__ Totals acc_totals(const SpreadAcc *acc) {
+  Totals t{};
+  t.pts_min = ~0ull;
+  for (int k = 0; k < ACC_SHARDS; ++k) {
+    const SpreadAccShard &q = acc->sh[k];
+    for (int f = 0; f <= NFILT; ++f) t.fail[f] += q.fail[f];
+    t.feasible += q.feasible;
+    t.ignored += q.ignored;
+    t.tt_max = max(t.tt_max, q.tt_max);
+    t.na_max = max(t.na_max, q.na_max);
+    t.pts_min = min(t.pts_min, q.pts_min);
+    t.pts_max = max(t.pts_max, q.pts_max);
+    t.best = max(t.best, q.best);
+  }
+  return t;
+}
+__device__ __forceinline__ SpreadAccShard &acc_shard(const SpreadArgs &a) { return a.acc->sh[blockIdx.x % ACC_SHARDS]; }
+
 }  // namespace
 
 // ------------------------------------------------------------------ prep
 // Per DoNotSchedule constraint c: dcnt[c][d] = matching pods on the eligible
 // nodes of domain d (the node has every DoNotSchedule key and passes the
 // constraint's inclusion policies), dflag[c][d] bit 0 = d has an eligible
-// node.  Per ScheduleAnyway constraint (not kubernetes.io/hostname): dcnt over
-// the nodes PreScore counts (requireAllTopologies, inclusion policies; a node
-// lacking the key belongs to the "" domain, id 0, when it is not required).
+// node.  (The ScheduleAnyway counts are taken by the filter pass, which
+// visits every node anyway.)  Launched only for pods with DoNotSchedule
+// constraints.
 __global__ __launch_bounds__(SP_THREADS) void spread_prep_kernel(SpreadArgs a) {
   __shared__ uint32_t s_h[SP_LDS];
   __shared__ uint32_t s_off[MAX_SPREAD];
@@ -134,34 +158,35 @@ __global__ __launch_bounds__(SP_THREADS) void spread_prep_kernel(SpreadArgs a) {
   if (threadIdx.x == 0) lds_segments(a, sd, n, s_off);
   for (uint32_t i = threadIdx.x; i < SP_LDS; i += SP_THREADS) s_h[i] = 0;
   __syncthreads();
-  const bool allkeys = p.flags & PF_SPREAD_ALLKEYS;
+  bool aff_needed = false, taint_needed = false;
+  for (uint32_t c = 0; c < n; ++c) {
+    if (sd[c].flags & SP_SCORE) continue;
+    aff_needed |= (sd[c].flags & SP_AFF) && (p.flags & PF_AFF);
+    taint_needed |= (sd[c].flags & SP_TAINT) != 0;
+  }
   for (uint32_t pos = blockIdx.x * SP_THREADS + threadIdx.x; pos < a.npos; pos += grid_threads()) {
     const uint32_t slot = a.pos_slot[pos];
     if (slot == SLOT_NONE || a.t.apods[pos] < 0) continue;
     NodeExt e;
-    load_ext(a.t, pos, true, e);
-    const bool aff_ok = !(p.flags & PF_AFF) || required_match(p, a.clauses, e, slot);
-    const bool taint_ok = (e.hard & ~p.tol_hard & ~UNSCHED_BIT) == 0;
-    bool all_f = true, all_s = true;
-    for (uint32_t c = 0; c < n; ++c) {
-      if (a.dom[(size_t)sd[c].key * a.npos + pos] != DOM_NONE) continue;
-      if (sd[c].flags & SP_SCORE) all_s = false;
-      else all_f = false;
-    }
+    if (aff_needed || taint_needed) load_ext(a.t, pos, true, e);
+    const bool aff_ok = !aff_needed || required_match(p, a.clauses, e, slot);
+    const bool taint_ok = !taint_needed || (e.hard & ~p.tol_hard & ~UNSCHED_BIT) == 0;
+    bool all_f = true;
+    for (uint32_t c = 0; c < n; ++c)
+      if (!(sd[c].flags & SP_SCORE) && a.dom[(size_t)sd[c].key * a.npos + pos] == DOM_NONE) all_f = false;
+    if (!all_f) continue;
     for (uint32_t c = 0; c < n; ++c) {
       const SpreadDev &s = sd[c];
-      const bool score = s.flags & SP_SCORE;
-      if (score ? ((s.flags & SP_HOST) || (allkeys && !all_s)) : !all_f) continue;
-      if (((s.flags & SP_AFF) && !aff_ok) || ((s.flags & SP_TAINT) && !taint_ok)) continue;
-      uint32_t d = a.dom[(size_t)s.key * a.npos + pos];
-      if (d == DOM_NONE) d = 0;  // Score without requireAllTopologies: the "" value
+      if ((s.flags & SP_SCORE) || ((s.flags & SP_AFF) && !aff_ok) || ((s.flags & SP_TAINT) && !taint_ok)) continue;
+      const uint32_t d = a.dom[(size_t)s.key * a.npos + pos];
       const uint32_t k = s.cls == CLS_NONE ? 0u : a.cnt[(size_t)s.cls * a.npos + pos];
       if (s_off[c] != SP_OFF_NONE) {
-        if (k) atomicAdd(&s_h[s_off[c] + d], k);
-        if (!score) atomicOr(&s_h[s_off[c] + d], 0x80000000u);
+        const uint32_t e = s_off[c] + d;
+        if (k) atomicAdd(&s_h[e], k);
+        if (!(s_h[e] >> 31)) atomicOr(&s_h[e], 0x80000000u);
       } else {
         if (k) atomicAdd(&a.dcnt[(size_t)c * a.dom_cap + d], k);
-        if (!score) atomicOr(&a.dflag[(size_t)c * a.dom_cap + d], 1u);
+        if (!(a.dflag[(size_t)c * a.dom_cap + d] & 1u)) atomicOr(&a.dflag[(size_t)c * a.dom_cap + d], 1u);
       }
     }
   }
@@ -217,11 +242,22 @@ __global__ __launch_bounds__(SP_THREADS) void spread_min_kernel(SpreadArgs a) {
 // ---------------------------------------------------------------- filter
 // Filter chain in default-profile order, PodTopologySpread last
 // (filtering.go#Filter: node without the key -> UnschedulableAndUnresolvable;
-// matchNum + selfMatch - minMatchNum > maxSkew -> Unschedulable).  Feasible
-// nodes: normaliser maxima, PreScore's ignored nodes and the Score domains of
-// the rest (topoSize).
+// matchNum + selfMatch - minMatchNum > maxSkew -> Unschedulable).  Every
+// node: PreScore's ScheduleAnyway counts (dcnt over the nodes PreScore
+// counts: requireAllTopologies, inclusion policies; a node lacking the key
+// belongs to the "" domain, id 0, when it is not required).  Feasible nodes:
+// normaliser maxima, PreScore's ignored nodes, the Score domains of the rest
+// (topoSize), and the node's normalisation-free score parts packed for the
+// select pass (Σ weight x LeastAllocated / BalancedAllocation, raw
+// TaintToleration, raw NodeAffinity), so that it reads 8 bytes per node
+// instead of the resource and label rows.
+__device__ __forceinline__ uint64_t pack_part(uint32_t base, uint32_t tt_raw, uint32_t na_raw) {
+  return (uint64_t)base | ((uint64_t)(tt_raw & 0xFFu) << 32) | ((uint64_t)(na_raw & 0xFFFFFFu) << 40);
+}
+
 __global__ __launch_bounds__(SP_THREADS) void spread_filter_kernel(SpreadArgs a) {
   __shared__ uint32_t s_seen[SP_LDS / 32];
+  __shared__ uint32_t s_h[SP_LDS];
   __shared__ uint32_t s_off[MAX_SPREAD];
   __shared__ uint32_t s_red[SP_THREADS / WAVE][NFILT + 5];
   const PodDev p = a.pods[a.pod];
@@ -229,7 +265,15 @@ __global__ __launch_bounds__(SP_THREADS) void spread_filter_kernel(SpreadArgs a)
   const uint32_t n = spread_count(p);
   if (threadIdx.x == 0) lds_segments(a, sd, n, s_off);
   for (uint32_t i = threadIdx.x; i < SP_LDS / 32; i += SP_THREADS) s_seen[i] = 0;
+  for (uint32_t i = threadIdx.x; i < SP_LDS; i += SP_THREADS) s_h[i] = 0;
   __syncthreads();
+  bool any_s = false, aff_needed = false, taint_needed = false;
+  for (uint32_t c = 0; c < n; ++c) {
+    if (!(sd[c].flags & SP_SCORE)) continue;
+    any_s |= !(sd[c].flags & SP_HOST);
+    aff_needed |= (sd[c].flags & SP_AFF) != 0;
+    taint_needed |= (sd[c].flags & SP_TAINT) != 0;
+  }
   const bool allkeys = p.flags & PF_SPREAD_ALLKEYS;
   const uint32_t lane = threadIdx.x % WAVE, wid = threadIdx.x / WAVE;
   uint32_t fails[NFILT + 1] = {0, 0, 0, 0, 0, 0};
@@ -245,6 +289,26 @@ __global__ __launch_bounds__(SP_THREADS) void spread_filter_kernel(SpreadArgs a)
     }
     NodeExt e;
     load_ext(a.t, pos, true, e);
+    bool all_s = true;
+    for (uint32_t c = 0; c < n; ++c)
+      if ((sd[c].flags & SP_SCORE) && a.dom[(size_t)sd[c].key * a.npos + pos] == DOM_NONE) all_s = false;
+    if (any_s && (!allkeys || all_s)) {
+      // PreScore counts (scoring.go#PreScore processAllNode) of this node
+      const bool aff_ok = !aff_needed || !(p.flags & PF_AFF) || required_match(p, a.clauses, e, slot);
+      const bool taint_ok = !taint_needed || (e.hard & ~p.tol_hard & ~UNSCHED_BIT) == 0;
+      for (uint32_t c = 0; c < n; ++c) {
+        const SpreadDev &q = sd[c];
+        if (!(q.flags & SP_SCORE) || (q.flags & SP_HOST) || ((q.flags & SP_AFF) && !aff_ok) ||
+            ((q.flags & SP_TAINT) && !taint_ok))
+          continue;
+        uint32_t d = a.dom[(size_t)q.key * a.npos + pos];
+        if (d == DOM_NONE) d = 0;
+        const uint32_t k = q.cls == CLS_NONE ? 0u : a.cnt[(size_t)q.cls * a.npos + pos];
+        if (!k) continue;
+        if (s_off[c] != SP_OFF_NONE) atomicAdd(&s_h[s_off[c] + d], k);
+        else atomicAdd(&a.dcnt[(size_t)c * a.dom_cap + d], k);
+      }
+    }
     int s = filter<true>(p, a.clauses, r, e);
     if (s == ST_FEASIBLE) {
       for (uint32_t c = 0; c < n; ++c) {
@@ -266,13 +330,14 @@ __global__ __launch_bounds__(SP_THREADS) void spread_filter_kernel(SpreadArgs a)
     int8_t out = (int8_t)s;
     if (s == ST_FEASIBLE) {
       ++feasible;
-      if (p.flags & PF_TT) tt_max = max(tt_max, (uint32_t)taint_raw(p, e));
-      if (p.flags & PF_NA) na_max = max(na_max, (uint32_t)preferred_raw(p, a.clauses, e, slot));
+      const uint32_t tr = (p.flags & PF_TT) ? (uint32_t)taint_raw(p, e) : 0u;
+      const uint32_t nr = (p.flags & PF_NA) ? (uint32_t)preferred_raw(p, a.clauses, e, slot) : 0u;
+      tt_max = max(tt_max, tr);
+      na_max = max(na_max, nr);
+      a.part[pos] = pack_part((uint32_t)a.w.fit * (uint32_t)score_la(p, r) + (uint32_t)a.w.ba * (uint32_t)score_ba(p, r),
+                              tr, nr);
       // PreScore (initPreScoreState): with requireAllTopologies a node lacking
       // a ScheduleAnyway key is ignored; the others' domains make topoSize
-      bool all_s = true;
-      for (uint32_t c = 0; c < n; ++c)
-        if ((sd[c].flags & SP_SCORE) && a.dom[(size_t)sd[c].key * a.npos + pos] == DOM_NONE) all_s = false;
       if (allkeys && !all_s) {
         ++ignored;
         out = SST_IGNORED;
@@ -283,8 +348,10 @@ __global__ __launch_bounds__(SP_THREADS) void spread_filter_kernel(SpreadArgs a)
           uint32_t d = a.dom[(size_t)q.key * a.npos + pos];
           if (d == DOM_NONE) d = 0;
           if (s_off[c] != SP_OFF_NONE) {
-            const uint32_t bit = s_off[c] + d;
-            if (atomicOr(&s_seen[bit >> 5], 1u << (bit & 31)) & (1u << (bit & 31))) continue;
+            const uint32_t bit = s_off[c] + d, m = 1u << (bit & 31);
+            if ((s_seen[bit >> 5] & m) || (atomicOr(&s_seen[bit >> 5], m) & m)) continue;
+          } else if (a.dflag[(size_t)c * a.dom_cap + d] & 2u) {
+            continue;
           }
           if (!(atomicOr(&a.dflag[(size_t)c * a.dom_cap + d], 2u) & 2u)) atomicAdd(&a.acc->topo_size[c], 1u);
         }
@@ -306,16 +373,25 @@ __global__ __launch_bounds__(SP_THREADS) void spread_filter_kernel(SpreadArgs a)
   if (lane == 0)
     for (int q = 0; q < NFILT + 5; ++q) s_red[wid][q] = v[q];
   __syncthreads();
+  // flush the block's ScheduleAnyway domain counts
+  for (uint32_t c = 0; c < n; ++c) {
+    if (s_off[c] == SP_OFF_NONE || !(sd[c].flags & SP_SCORE)) continue;
+    for (uint32_t d = threadIdx.x; d < a.ndom[sd[c].key]; d += SP_THREADS) {
+      const uint32_t v = s_h[s_off[c] + d];
+      if (v) atomicAdd(&a.dcnt[(size_t)c * a.dom_cap + d], v);
+    }
+  }
   if (threadIdx.x < NFILT + 5) {
     const int q = threadIdx.x;
     uint32_t t = s_red[0][q];
     for (int w = 1; w < SP_THREADS / WAVE; ++w) t = q >= NFILT + 3 ? max(t, s_red[w][q]) : t + s_red[w][q];
+    SpreadAccShard &bp = acc_shard(a);
     if (t) {
-      if (q <= NFILT) atomicAdd(&a.acc->fail[q], t);
-      else if (q == NFILT + 1) atomicAdd(&a.acc->feasible, t);
-      else if (q == NFILT + 2) atomicAdd(&a.acc->ignored, t);
-      else if (q == NFILT + 3) atomicMax(&a.acc->tt_max, t);
-      else atomicMax(&a.acc->na_max, t);
+      if (q <= NFILT) atomicAdd(&bp.fail[q], t);
+      else if (q == NFILT + 1) atomicAdd(&bp.feasible, t);
+      else if (q == NFILT + 2) atomicAdd(&bp.ignored, t);
+      else if (q == NFILT + 3) atomicMax(&bp.tt_max, t);
+      else atomicMax(&bp.na_max, t);
     }
   }
 }
@@ -333,8 +409,9 @@ __global__ __launch_bounds__(SP_THREADS) void spread_score_kernel(SpreadArgs a) 
   const SpreadDev *sd = spread_recs(a, p);
   const uint32_t n = spread_count(p);
   if (threadIdx.x < n) {
+    const Totals tot = acc_totals(a.acc);
     const SpreadDev &q = sd[threadIdx.x];
-    const uint32_t sz = (q.flags & SP_HOST) ? a.acc->feasible - a.acc->ignored : a.acc->topo_size[threadIdx.x];
+    const uint32_t sz = (q.flags & SP_HOST) ? tot.feasible - tot.ignored : a.acc->topo_size[threadIdx.x];
     s_w[threadIdx.x] = go_log((double)sz + 2.0);  // topologyNormalizingWeight
   }
   __syncthreads();
@@ -370,8 +447,8 @@ __global__ __launch_bounds__(SP_THREADS) void spread_score_kernel(SpreadArgs a) 
       mn = min(mn, s_r[w][0]);
       mx = max(mx, s_r[w][1]);
     }
-    if (mn != ~0ull) atomicMin((unsigned long long *)&a.acc->pts_min, (unsigned long long)mn);
-    if (mx) atomicMax((unsigned long long *)&a.acc->pts_max, (unsigned long long)mx);
+    if (mn != ~0ull) atomicMin((unsigned long long *)&acc_shard(a).pts_min, (unsigned long long)mn);
+    if (mx) atomicMax((unsigned long long *)&acc_shard(a).pts_max, (unsigned long long)mx);
   }
 }
 
@@ -388,8 +465,9 @@ __global__ __launch_bounds__(SP_THREADS) void spread_select_kernel(SpreadArgs a)
   const uint32_t n = spread_count(p);
   bool has_score = false;
   for (uint32_t c = 0; c < n; ++c) has_score |= (sd[c].flags & SP_SCORE) != 0;
-  const int64_t tt_max = a.acc->tt_max, na_max = a.acc->na_max;
-  const int64_t pmin = (int64_t)a.acc->pts_min, pmax = (int64_t)a.acc->pts_max;
+  const Totals tot = acc_totals(a.acc);
+  const int64_t tt_max = tot.tt_max, na_max = tot.na_max;
+  const int64_t pmin = (int64_t)tot.pts_min, pmax = (int64_t)tot.pts_max;
   uint64_t best = 0;
   for (uint32_t pos = blockIdx.x * SP_THREADS + threadIdx.x; pos < a.npos; pos += grid_threads()) {
     const int8_t s = a.st[pos];
@@ -402,10 +480,6 @@ __global__ __launch_bounds__(SP_THREADS) void spread_select_kernel(SpreadArgs a)
       }
       continue;
     }
-    NodeRegs r;
-    load_core(a.t, pos, slot, true, r);
-    NodeExt e;
-    load_ext(a.t, pos, true, e);
     int64_t raw = 0, norm = 0;
     if (has_score) {
       if (s == SST_IGNORED) norm = 0;
@@ -414,9 +488,23 @@ __global__ __launch_bounds__(SP_THREADS) void spread_select_kernel(SpreadArgs a)
         norm = pmax == 0 ? 100 : 100 * (pmax + pmin - raw) / pmax;
       }
     }
-    const int64_t total = (int64_t)total_score<true>(p, a.clauses, r, e, a.w, tt_max, na_max) +
-                          (has_score ? (int64_t)a.w_pts * norm : 0);
+    // total_score<true> from the packed parts (same terms, same order)
+    const uint64_t pk = a.part[pos];
+    int64_t total = (int64_t)(uint32_t)pk;
+    int64_t tt = 100;
+    if (p.flags & PF_TT) tt = normalize((int64_t)((pk >> 32) & 0xFF), tt_max, true);
+    total += (int64_t)a.w.tt * tt;
+    if (p.flags & PF_HAS_PREF) {
+      int64_t na = 0;
+      if (p.flags & PF_NA) na = normalize((int64_t)(pk >> 40), na_max, false);
+      total += (int64_t)a.w.na * na;
+    }
+    if (has_score) total += (int64_t)a.w_pts * norm;
     if (a.dump) {
+      NodeRegs r;
+      load_core(a.t, pos, slot, true, r);
+      NodeExt e;
+      load_ext(a.t, pos, true, e);
       int32_t *o = a.dump + (size_t)slot * SPREAD_DUMP_WORDS;
       o[0] = ST_FEASIBLE;
       o[1] = score_la(p, r);
@@ -441,10 +529,12 @@ __global__ __launch_bounds__(SP_THREADS) void spread_select_kernel(SpreadArgs a)
   __syncthreads();
   if (threadIdx.x == 0) {
     for (int w = 1; w < SP_THREADS / WAVE; ++w) best = s_r[w] > best ? s_r[w] : best;
-    if (best) atomicMax((unsigned long long *)&a.acc->best, (unsigned long long)best);
+    if (best) atomicMax((unsigned long long *)&acc_shard(a).best, (unsigned long long)best);
   }
-  // clear the domain scratch of this pod's constraints
+  // clear the domain scratch of this pod's constraints (a ScheduleAnyway
+  // kubernetes.io/hostname constraint counts per node and never used it)
   for (uint32_t c = 0; c < n; ++c)
+    if ((sd[c].flags & (SP_SCORE | SP_HOST)) != (SP_SCORE | SP_HOST))
     for (uint32_t d = blockIdx.x * SP_THREADS + threadIdx.x; d < a.ndom[sd[c].key]; d += grid_threads()) {
       a.dcnt[(size_t)c * a.dom_cap + d] = 0;
       a.dflag[(size_t)c * a.dom_cap + d] = 0;
@@ -458,30 +548,31 @@ __global__ __launch_bounds__(SP_THREADS) void spread_select_kernel(SpreadArgs a)
 // accumulators reset for the next pod.
 __global__ void spread_commit_kernel(SpreadArgs a) {
   if (threadIdx.x != 0) return;
+  const Totals tot = acc_totals(a.acc);
   const PodDev p = a.pods[a.pod];
   SpreadAcc &acc = *a.acc;
   DevResult r;
   r.node_index = -1;
   r.status = 1;  // KS_POD_UNSCHEDULABLE
   r.total_score = 0;
-  r.feasible_nodes = acc.feasible;
+  r.feasible_nodes = tot.feasible;
   r.evaluated_nodes = a.evaluated;
-  for (int q = 0; q < NFILT; ++q) r.fail_counts[q] = acc.fail[q];
-  r.spread_fail = acc.fail[PLUGIN_SPREAD];
+  for (int q = 0; q < NFILT; ++q) r.fail_counts[q] = tot.fail[q];
+  r.spread_fail = tot.fail[PLUGIN_SPREAD];
   r.prefiltered = p.prefilter_out;
   r.flags = 0;
-  if (acc.feasible > 0) {
-    if ((p.flags & PF_PREF_ERR) && acc.feasible >= 2) {
+  if (tot.feasible > 0) {
+    if ((p.flags & PF_PREF_ERR) && tot.feasible >= 2) {
       r.status = 2;  // KS_POD_ERROR (NodeAffinity PreScore)
-    } else if (acc.best == 0) {
+    } else if (tot.best == 0) {
       r.status = 2;  // no key although a node passed the filters: never expected, never committed
     } else {
-      const uint64_t win = acc.best;
+      const uint64_t win = tot.best;
       const uint32_t slot = 0xFFFFFFFFu - (uint32_t)win;
       r.node_index = (int32_t)slot;
       r.status = 0;
       r.total_score = (int64_t)(win >> 32) - 1;
-      r.flags = acc.feasible == 1 ? 1u : 0u;  // KS_RESULT_SINGLE_FEASIBLE
+      r.flags = tot.feasible == 1 ? 1u : 0u;  // KS_RESULT_SINGLE_FEASIBLE
       if (!a.no_commit) {
         const uint32_t pos = a.slot_pos[slot];
         a.t.rcpu[pos] += p.req_cpu;
@@ -502,16 +593,19 @@ __global__ void spread_commit_kernel(SpreadArgs a) {
     a.counters[1] += 1;
   }
   if (!a.no_commit) a.results[a.pod] = r;
-  for (int q = 0; q <= NFILT; ++q) acc.fail[q] = 0;
-  acc.feasible = acc.ignored = acc.tt_max = acc.na_max = 0;
   for (int c = 0; c < MAX_SPREAD; ++c) {
     acc.min_match[c] = 0xFFFFFFFFu;
     acc.ndomains[c] = 0;
     acc.topo_size[c] = 0;
   }
-  acc.pts_min = ~0ull;
-  acc.pts_max = 0;
-  acc.best = 0;
+  for (int k = 0; k < ACC_SHARDS; ++k) {
+    SpreadAccShard &q = acc.sh[k];
+    for (int f = 0; f <= NFILT; ++f) q.fail[f] = 0;
+    q.feasible = q.ignored = q.tt_max = q.na_max = 0;
+    q.pts_min = ~0ull;
+    q.pts_max = 0;
+    q.best = 0;
+  }
 }
 
 // Selector-class counts of the pods a round-kernel segment [lo, hi) bound.
@@ -541,10 +635,14 @@ __global__ void add_u32_kernel(uint32_t *col, const uint64_t *idx, const int32_t
 
 // ------------------------------------------------------------- launchers
 
-hipError_t launch_spread_pod(const SpreadArgs &a, bool has_filter, bool has_score, hipStream_t st) {
-  const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((a.npos + SP_THREADS - 1) / SP_THREADS, 2048));
-  spread_prep_kernel<<<blocks, SP_THREADS, 0, st>>>(a);
-  if (has_filter) spread_min_kernel<<<blocks, SP_THREADS, 0, st>>>(a);
+hipError_t launch_spread_pod(const SpreadArgs &args, bool has_filter, bool has_score, hipStream_t st) {
+  const uint32_t blocks =
+      std::max<uint32_t>(1, std::min<uint32_t>((args.npos + SP_THREADS - 1) / SP_THREADS, SPREAD_MAX_BLOCKS));
+  const SpreadArgs &a = args;
+  if (has_filter) {
+    spread_prep_kernel<<<blocks, SP_THREADS, 0, st>>>(a);
+    spread_min_kernel<<<blocks, SP_THREADS, 0, st>>>(a);
+  }
   spread_filter_kernel<<<blocks, SP_THREADS, 0, st>>>(a);
   if (has_score) spread_score_kernel<<<blocks, SP_THREADS, 0, st>>>(a);
   spread_select_kernel<<<blocks, SP_THREADS, 0, st>>>(a);

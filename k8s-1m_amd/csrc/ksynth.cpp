@@ -64,6 +64,7 @@ struct ksynth {
   std::vector<ks_term> terms;
   std::vector<ks_preferred_term> prefs;
   std::vector<const char *> values;
+  std::vector<ks_spread_constraint> spread;
   std::deque<std::string> strings;
   std::unordered_map<std::string, const char *> interned;
 
@@ -144,6 +145,11 @@ extern "C" ksynth *ksynth_nodes(int32_t kind, uint32_t n, uint64_t seed) {
     nd.taints = s->taints.data() + s->taints.size();
     ksynth::push(s->taints, ks_taint{s->intern("kwok.x-k8s.io/node"), s->intern("fake"),
                                      KS_EFFECT_NO_SCHEDULE, 0});
+    if (kind == KSYNTH_ZONED) {
+      Rng r(seed, i, 2);
+      ksynth::push(s->labels, ks_label{s->intern("topology.kubernetes.io/zone"),
+                                       s->intern("zone-" + std::to_string(r.below(32)))});
+    }
     if (kind == KSYNTH_LABELED) {
       Rng r(seed, i, 2);
       auto lab = [&](const std::string &k, const std::string &v) {
@@ -187,7 +193,8 @@ void reserve_pods(ksynth *s, size_t n) {
   s->terms.reserve(n * 4);
   s->prefs.reserve(n * 2);
   s->values.reserve(n * 16);
-  s->labels.reserve(n);
+  s->labels.reserve(n * 2);
+  s->spread.reserve(n * 2);
 }
 
 // Resource requests of the C1 stream: cpu in {50..4000 step 50}m,
@@ -352,6 +359,52 @@ extern "C" ksynth *ksynth_besteffort_pods(uint32_t n) {
   return s;
 }
 
+extern "C" ksynth *ksynth_spread_pods(uint32_t n, uint32_t n_apps, uint64_t seed) {
+  auto *s = new ksynth();
+  reserve_pods(s, n);
+  if (n_apps == 0) n_apps = 1;
+  for (uint32_t j = 0; j < n; ++j) {
+    Rng r(seed, j, 6);
+    ks_pod p = base_pod(s, j, "spread-");
+    ks_container c;
+    draw_requests(r, c);
+    p.containers = ksynth::push(s->containers, c);
+    p.n_containers = 1;
+    p.tolerations = s->tolerations.data() + s->tolerations.size();
+    kwok_tolerations(s);
+    p.n_tolerations = 3;
+    const std::string app = "app-" + std::to_string(r.below(n_apps));
+    const ks_label *lab = ksynth::push(s->labels, ks_label{s->intern("app"), s->intern(app)});
+    p.labels = lab;
+    p.n_labels = 1;
+    ks_spread_constraint a{}, b{};
+    a.selector.match_labels = lab;
+    a.selector.n_match_labels = 1;
+    b.selector = a.selector;
+    if (r.chance(0.5)) {  // system defaults (podtopologyspread systemDefaultConstraints)
+      a.topology_key = s->intern("kubernetes.io/hostname");
+      a.max_skew = 3;
+      a.when_unsatisfiable = KS_SCHEDULE_ANYWAY;
+      b.topology_key = s->intern("topology.kubernetes.io/zone");
+      b.max_skew = 5;
+      b.when_unsatisfiable = KS_SCHEDULE_ANYWAY;
+      p.spread_defaulted = 1;
+    } else {
+      a.topology_key = s->intern("topology.kubernetes.io/zone");
+      a.max_skew = 1;
+      a.when_unsatisfiable = KS_DO_NOT_SCHEDULE;
+      b.topology_key = s->intern("kubernetes.io/hostname");
+      b.max_skew = 1;
+      b.when_unsatisfiable = KS_SCHEDULE_ANYWAY;
+    }
+    p.spread = ksynth::push(s->spread, a);
+    ksynth::push(s->spread, b);
+    p.n_spread = 2;
+    s->pods.push_back(p);
+  }
+  return s;
+}
+
 extern "C" ksynth *ksynth_prefill(int32_t kind, uint32_t n_nodes, uint64_t nodes_seed,
                                   uint64_t seed, double max_fill) {
   auto *s = new ksynth();
@@ -382,6 +435,10 @@ extern "C" ksynth *ksynth_prefill(int32_t kind, uint32_t n_nodes, uint64_t nodes
   reserve_pods(s, reqs.size());
   for (size_t j = 0; j < reqs.size(); ++j) {
     ks_pod p = base_pod(s, (uint32_t)j, "prefill-");
+    if (kind == KSYNTH_ZONED) {  // bound pods of 64 apps (spread selectors count them)
+      p.labels = ksynth::push(s->labels, ks_label{s->intern("app"), s->intern("app-" + std::to_string(j % 64))});
+      p.n_labels = 1;
+    }
     p.containers = ksynth::push(s->containers, reqs[j]);
     p.n_containers = 1;
     p.tolerations = s->tolerations.data() + s->tolerations.size();

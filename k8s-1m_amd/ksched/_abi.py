@@ -224,6 +224,9 @@ class KsStats(C.Structure):
         ("sweep_evals", C.c_uint64),
         ("resolve_ms", C.c_double),
         ("resolve_launches", C.c_uint64),
+        ("spread_ms", C.c_double),
+        ("spread_pods_timed", C.c_uint64),
+        ("spread_pods", C.c_uint64),
     ]
 
 
@@ -231,7 +234,7 @@ class KsStats(C.Structure):
 EXPECTED_SIZES = {
     "ks_label": 16, "ks_taint": 24, "ks_toleration": 24, "ks_node": 72, "ks_container": 32,
     "ks_requirement": 24, "ks_term": 24, "ks_preferred_term": 32, "ks_pod": 160, "ks_event": 24, "ks_result": 56,
-    "ks_node_score": 48, "ks_node_state": 56, "ks_config": 60, "ks_stats": 64, "ks_label_selector": 32,
+    "ks_node_score": 48, "ks_node_state": 56, "ks_config": 60, "ks_stats": 88, "ks_label_selector": 32,
     "ks_spread_constraint": 72,
 }
 STRUCTS = {
@@ -250,7 +253,7 @@ KSCHED_SYMBOLS = [
     "ks_debug_counters",
 ]
 KSYNTH_SYMBOLS = [
-    "ksynth_nodes", "ksynth_pods", "ksynth_prefill", "ksynth_besteffort_pods", "ksynth_node_array",
+    "ksynth_nodes", "ksynth_pods", "ksynth_prefill", "ksynth_besteffort_pods", "ksynth_spread_pods", "ksynth_node_array",
     "ksynth_pod_array", "ksynth_slots", "ksynth_free", "ksynth_fnv64",
 ]
 
@@ -336,6 +339,8 @@ def ksynth_lib() -> C.CDLL:
     L.ksynth_prefill.restype = vp
     L.ksynth_besteffort_pods.argtypes = [C.c_uint32]
     L.ksynth_besteffort_pods.restype = vp
+    L.ksynth_spread_pods.argtypes = [C.c_uint32, C.c_uint32, C.c_uint64]
+    L.ksynth_spread_pods.restype = vp
     L.ksynth_node_array.argtypes = [vp, P(C.c_uint32)]
     L.ksynth_node_array.restype = P(KsNode)
     L.ksynth_pod_array.argtypes = [vp, P(C.c_uint32)]

@@ -5,7 +5,7 @@ import ctypes as C
 
 from . import _abi
 
-KWOK, HETERO, LABELED = 1, 2, 4
+KWOK, HETERO, LABELED, ZONED = 1, 2, 4, 8
 
 
 class Synth:
@@ -55,6 +55,10 @@ def prefill(kind: int, n_nodes: int, nodes_seed: int, seed: int, max_fill: float
 
 def besteffort_pods(n: int) -> Synth:
     return Synth(_abi.ksynth_lib().ksynth_besteffort_pods(n))
+
+
+def spread_pods(n: int, n_apps: int, seed: int) -> Synth:
+    return Synth(_abi.ksynth_lib().ksynth_spread_pods(n, n_apps, seed))
 
 
 def slot_array(n: int, start: int = 0):

@@ -149,3 +149,62 @@ def test_kwok_1m_c1_pods_k512_replay():
     r, dbg = run_fullsize(synth.KWOK, synth.pods(synth.KWOK, BATCH, 2), prefill=False, topk=512)
     assert (r["status"] == 0).all()
     assert dbg[3] * 20 < dbg[0], f"wasted speculative rounds {dbg[3]} of {dbg[0]}"
+
+
+class MixedStream:
+    """A ks_pod array interleaving two synthetic streams in blocks (pods_at / pods like synth.Synth)."""
+
+    def __init__(self, a, b, block):
+        self.keep = (a, b)
+        out = []
+        ia = ib = 0
+        while ia < a.n_pods or ib < b.n_pods:
+            for _ in range(block):
+                if ia < a.n_pods:
+                    out.append(a.pods[ia])
+                    ia += 1
+            for _ in range(block):
+                if ib < b.n_pods:
+                    out.append(b.pods[ib])
+                    ib += 1
+        self.n_pods = len(out)
+        self.arr = (_abi.KsPod * self.n_pods)(*out)
+        self.pods = C.cast(self.arr, C.POINTER(_abi.KsPod))
+
+    def pods_at(self, start):
+        return C.cast(C.addressof(self.arr) + start * C.sizeof(_abi.KsPod), C.POINTER(_abi.KsPod))
+
+
+def test_spread_1m_replay():
+    # the spread bench's cluster (1M nodes in 32 zones, prefill pods of 64 apps)
+    # with deployment pods carrying PodTopologySpread constraints interleaved
+    # with plain pods: spread path and round kernels alternate, class counts
+    # follow both; the oracle replays every decision and checks three windows
+    n_pods = 3072
+    nodes = synth.nodes(synth.ZONED, N, 1)
+    slots = synth.slot_array(N)
+    pf = synth.prefill(synth.ZONED, N, 1, 3, 0.5)
+    spread, plain = synth.spread_pods(n_pods // 2, 64, 5), synth.pods(synth.HETERO, n_pods // 2, 6)
+    mixed = MixedStream(plain, spread, 128)
+    s = Scheduler(N)
+    s.upsert_nodes_raw(nodes.nodes, slots, N)
+    assert s.lib.ks_pods_add(s.ctx, pf.pods, pf.slot_ptr, pf.n_pods) == 0
+    b = s.prepare(mixed.pods, n_pods)
+    s.run(b)
+    got = s.results(b, n_pods)
+    s.free(b)
+    st = _abi.KsStats()
+    assert s.lib.ks_get_stats(s.ctx, C.byref(st)) == 0
+    assert st.spread_pods == n_pods // 2
+    o = pyoracle.Oracle(N, threads=ORACLE_THREADS)
+    o.upsert(nodes.nodes, slots, N)
+    o.add_pods(pf.pods, pf.slot_ptr, pf.n_pods)
+    # windows straddle a plain -> spread boundary, sit inside a spread run, and end the batch
+    replay_check(o, mixed, got, n_pods, windows=(124, 1400, n_pods - 6), wlen=6)
+    sg = states_np(s.lib.ks_node_states, s.ctx, N)
+    sw = states_np(o.L.oracle_node_states, o.o, N)
+    assert np.array_equal(sg, sw), "node tables differ after replaying every decision"
+    r = res_array(got, n_pods)
+    assert (r["status"] == 0).mean() > 0.9
+    s.close()
+    o.close()

@@ -11,7 +11,7 @@ python3 - "$R/gpurun_out/$TAG" <<'PY'
 import csv, json, sys
 d = sys.argv[1]
 b = json.load(open(d + "/bench.json"))
-print("value", b["value"], "sweep_ms", b["roofline"]["avg_launch_ms"], "resolve_ms", b["extra"]["resolve_ms_per_round"])
+print("value", b["value"], "roofline", json.dumps({k: b["roofline"].get(k) for k in ("avg_launch_ms", "ms_per_pod", "frac")}), "resolve_ms", b["extra"]["resolve_ms_per_round"])
 for r in list(csv.DictReader(open(d + "/trace/run_kernel_stats.csv")))[:12]:
     print(r["Name"][:70].ljust(70), r["Calls"], round(float(r["AverageNs"]) / 1e3, 1), "us")
 PY
