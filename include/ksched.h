@@ -84,10 +84,27 @@ typedef struct {
   int32_t effect;    /* KS_EFFECT_* ; KS_EFFECT_ALL = "" (all effects) */
 } ks_toleration;
 
+/* A resource quantity other than cpu / memory / pods: ephemeral-storage
+ * (bytes) or a scalar resource (extended "vendor.example/x", hugepages-*,
+ * attachable-volumes-*, kubernetes.io/-prefixed), as Quantity.Value().  Other
+ * names are ignored, as upstream's framework.Resource ignores them. */
+typedef struct {
+  const char *name;
+  int64_t value;
+} ks_resource;
+
+/* One name of a status.images entry with the entry's sizeBytes (an entry with
+ * several names appears once per name). */
+typedef struct {
+  const char *name;
+  int64_t size_bytes;
+} ks_image;
+
 /* v1.Node (name, labels, spec.taints, spec.unschedulable, status.allocatable,
- * status.images).  images lists every name of every status.images entry
- * (ContainerImage.Names, flattened); upstream's cache keys ImageStates by
- * those names (internal/cache/cache.go#addNodeImageStates). */
+ * status.images).  images: every name of every status.images entry; upstream's
+ * cache keys ImageStates by those names (internal/cache/cache.go
+ * #addNodeImageStates: the size is the first reporting node's, the node count
+ * the number of nodes reporting the name). */
 typedef struct {
   const char *name;
   int64_t alloc_milli_cpu;
@@ -99,7 +116,10 @@ typedef struct {
   uint32_t n_taints;
   uint32_t unschedulable;
   uint32_t n_images;
-  const char *const *images;
+  const ks_image *images;
+  const ks_resource *extended;  /* status.allocatable beyond cpu / memory / pods */
+  uint32_t n_extended;
+  uint32_t _pad;
 } ks_node;
 
 /* One container's resources.requests.  A resource that is ABSENT from the
@@ -109,9 +129,13 @@ enum { KS_REQ_HAS_CPU = 1u, KS_REQ_HAS_MEMORY = 2u, KS_REQ_HAS_OTHER = 4u };
 typedef struct {
   int64_t milli_cpu;
   int64_t memory;
-  uint32_t flags;          /* KS_REQ_* presence bits; HAS_OTHER = any other resource (unsupported) */
+  uint32_t flags;          /* KS_REQ_* presence bits; HAS_OTHER = a request the caller cannot
+                              express in `extended` (refused) */
   uint32_t restart_always; /* init containers only: restartPolicy: Always (sidecar) */
-  const char *image;       /* container image (NULL / "" = none); ImageLocality precondition */
+  const char *image;       /* container image (NULL / "" = none): ImageLocality */
+  const ks_resource *extended;  /* requests beyond cpu / memory (ephemeral-storage, scalar) */
+  uint32_t n_extended;
+  uint32_t _pad;
 } ks_container;
 
 /* v1.NodeSelectorOperator */

@@ -69,10 +69,10 @@ enum PodFlags : uint32_t {
   PF_AFF = 64u,       // required program present (nodeSelector and/or required terms)
   PF_PREFILTER = 128u,   // NodeAffinity PreFilterResult: only nodes passing the prefilter program are evaluated
   PF_NA_CONFLICT = 256u, // NodeAffinity PreFilter rejects (conflicting metadata.name terms): every node fails NodeAffinity
-  PF_SPREAD = 512u,      // PodTopologySpread constraints: scheduled by the spread path (ksched_spread.hip)
+  PF_SOLO = 512u,        // scheduled one at a time by the spread path (ksched_spread.hip): topology
+                         // spread constraints, extended resources or ImageLocality; SoloHdr at solo_off
   PF_SPREAD_ALLKEYS = 1024u,  // PreScore requireAllTopologies (the pod's own constraints, not system defaults)
 };
-constexpr uint32_t PF_NSPREAD_SHIFT = 24;  // flags >> 24: number of SpreadDev records at spread_off
 
 struct alignas(16) PodDev {
   int64_t req_cpu, req_mem;  // PodRequests (Fit filter, BalancedAllocation)
@@ -85,7 +85,7 @@ struct alignas(16) PodDev {
   int32_t name_slot;         // spec.nodeName: -1 unset, -2 names no node, else slot
   uint32_t req_off, req_len; // required program: word offset in the label-program buffer, terms (OR)
   uint32_t pref_off, pref_len;  // preferred program: word offset, terms (weighted sum)
-  uint32_t spread_off;       // word offset of the pod's SpreadDev records in the label-program buffer
+  uint32_t solo_off;         // PF_SOLO: word offset of the pod's SoloHdr in the label-program buffer
   // Normalising-plugin maxima the sweep scores with (PF_TT / PF_NA): the host's
   // guess of max raw over feasible nodes.  The merge measures the true maxima;
   // pods whose guess was wrong are re-swept with them (norm_check, fix sweep).
@@ -142,6 +142,28 @@ struct alignas(16) SpreadDev {
 };
 static_assert(sizeof(SpreadDev) == 32, "SpreadDev layout");
 constexpr uint32_t SPREAD_WORDS = sizeof(SpreadDev) / 8;
+
+// A one-pod-path program (16-byte aligned in the label-program buffer):
+//   SoloHdr, n_spread SpreadDev, n_xres XResDev, n_img ImageDev.
+struct alignas(16) SoloHdr {
+  uint32_t n_spread, n_xres, n_img;
+  uint32_t n_containers;  // ImageLocality: len(initContainers) + len(containers)
+};
+// NodeResourcesFit for an extended resource (ephemeral-storage or a scalar
+// resource): the pod's request and the resource's column.
+constexpr int MAX_XRES = 8;
+struct alignas(16) XResDev {
+  uint32_t col, _pad;
+  int64_t req;
+};
+// ImageLocality: one container image present on some node: the label bit of
+// the node-side "image present" key and scaledImageScore (size x NumNodes /
+// totalNumNodes, host-computed).
+struct alignas(16) ImageDev {
+  uint32_t bit, _pad;
+  int64_t scaled;
+};
+static_assert(sizeof(SoloHdr) == 16 && sizeof(XResDev) == 16 && sizeof(ImageDev) == 16, "solo program layout");
 
 // Per-pod accumulators of the spread path (reset by its commit kernel).
 // Blocks add into ACC_SHARDS copies (block b -> copy b % ACC_SHARDS) and

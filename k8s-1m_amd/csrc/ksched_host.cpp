@@ -21,6 +21,7 @@
 #include <condition_variable>
 #include <cstring>
 #include <deque>
+#include <functional>
 #include <map>
 #include <mutex>
 #include <set>
@@ -149,7 +150,7 @@ struct HostNode {
   uint64_t hard = 0, prefer = 0;
   uint64_t lab[LW] = {};
   int64_t num[NNUM] = {};
-  std::vector<std::string> images;  // normalised image names
+  std::vector<std::pair<std::string, int64_t>> images;  // status.images names (as reported) and sizes
   // taints as interned ids (the taint dictionaries are rebuilt from these)
   std::vector<std::array<uint32_t, 3>> hard_taints;            // key, value, effect
   std::vector<std::pair<uint32_t, uint32_t>> prefer_taints;    // key, value
@@ -303,8 +304,17 @@ struct ks_ctx {
   uint32_t dict_version = 1;   // taint dictionary / node image set (compiled masks and checks)
   uint32_t names_version = 1;  // node name -> slot map (compiled NodeName / metadata.name slots)
   std::vector<uint32_t> dirty_ext;
-  // normalised image name -> present nodes reporting it (ImageLocality precondition)
-  std::unordered_map<std::string, uint32_t> images;
+  // ImageLocality: image name (as nodes report it) -> present nodes reporting
+  // it and the size the first of them reported (upstream cache imageStates)
+  struct ImageState {
+    uint32_t nodes = 0;
+    int64_t size = 0;
+  };
+  std::unordered_map<std::string, ImageState> images;
+  // extended resources (ephemeral-storage, scalar resources): name id -> column
+  std::unordered_map<uint32_t, uint32_t> xres_of;
+  std::vector<uint32_t> xres_names;
+  int64_t *d_xalloc = nullptr, *d_xreq = nullptr;  // [MAX_XRES][npos], one allocation
   // bound pods carrying pod (anti-)affinity terms (InterPodAffinity precondition)
   int64_t affinity_pods = 0;
   // PodTopologySpread (ksched_spread.hip; device columns allocated on first use)
@@ -828,29 +838,11 @@ ks_status check_modelled(ks_ctx *c, const ks_pod &p) {
     return c->fail(KS_ERR_UNSUPPORTED,
                    "%lld bound pod(s) carry pod (anti-)affinity terms: InterPodAffinity filters and scores every "
                    "incoming pod", (long long)c->affinity_pods);
-  // ImageLocality scores 0 on every node only when no node reports one of the
-  // pod's images (its per-node NumNodes snapshots make any other case
-  // history-dependent: framework/types.go#ImageStateSummary.Snapshot)
-  if (!c->images.empty()) {
-    auto check = [&](const ks_container *cs, uint32_t n) -> ks_status {
-      for (uint32_t i = 0; i < n; ++i) {
-        if (!cs[i].image || !cs[i].image[0]) continue;
-        auto it = c->images.find(normalized_image(cs[i].image));
-        if (it != c->images.end())
-          return c->fail(KS_ERR_UNSUPPORTED, "pod %s/%s: image %s is present on %u node(s) (ImageLocality)",
-                         str(p.ns).c_str(), str(p.name).c_str(), it->first.c_str(), it->second);
-      }
-      return KS_OK;
-    };
-    ks_status st;
-    if ((st = check(p.containers, p.n_containers)) || (st = check(p.init_containers, p.n_init_containers)))
-      return st;
-  }
   return KS_OK;
 }
 
-ks_status spread_compile(ks_ctx *c, const ks_pod &p, PodDev &d, ProgBuf &cl, bool create,
-                         std::vector<uint32_t> *refs);
+ks_status solo_compile(ks_ctx *c, const ks_pod &p, PodDev &d, ProgBuf &cl, bool create,
+                       std::vector<uint32_t> *refs);
 
 ks_status compile_pod(ks_ctx *c, const ks_pod &p, PodDev &d, ProgBuf &cl, bool create_spread = false,
                       std::vector<uint32_t> *class_refs = nullptr) {
@@ -940,7 +932,7 @@ ks_status compile_pod(ks_ctx *c, const ks_pod &p, PodDev &d, ProgBuf &cl, bool c
     sel.emit(cl, 0);
     d.req_len = 1;
   }
-  d.spread_off = 0;
+  d.solo_off = 0;
   {
     std::vector<std::string> names;
     if (prefilter_names(p, &names)) {
@@ -988,8 +980,7 @@ ks_status compile_pod(ks_ctx *c, const ks_pod &p, PodDev &d, ProgBuf &cl, bool c
   }
   if ((c->hard_in_use & ~d.tol_hard) || d.name_slot != -1 || (d.flags & (PF_AFF | PF_TT | PF_NA)))
     d.flags |= PF_EXT;
-  if (p.n_spread) return spread_compile(c, p, d, cl, create_spread, class_refs);
-  return KS_OK;
+  return solo_compile(c, p, d, cl, create_spread, class_refs);
 }
 
 // Taint dictionaries (hard: NoSchedule / NoExecute, prefer: PreferNoSchedule)
@@ -1064,20 +1055,123 @@ ks_status rebuild_taint_dicts(ks_ctx *c) {
 // nodes per normalised image name.  Returns true when a name is new.
 bool node_images_ref(ks_ctx *c, HostNode &h, int delta) {
   bool grew = false;
-  for (auto &nm : h.images) {
-    auto it = c->images.find(nm);
+  for (auto &im : h.images) {
+    auto it = c->images.find(im.first);
     if (delta > 0) {
-      if (it == c->images.end()) {
-        c->images.emplace(nm, 1u);
+      if (it == c->images.end()) {  // addNodeImageStates: the first reporter's size
+        c->images.emplace(im.first, ks_ctx::ImageState{1u, im.second});
         grew = true;
       } else {
-        it->second++;
+        it->second.nodes++;
       }
-    } else if (it != c->images.end() && --it->second == 0) {
-      c->images.erase(it);
+    } else if (it != c->images.end() && --it->second.nodes == 0) {
+      c->images.erase(it);  // removeNodeImageStates: the last node reporting it left
     }
   }
   return grew;
+}
+
+// Node-side "image present" key of ImageLocality (a label key no real label can have).
+std::string image_key(const std::string &name) { return std::string("\x01image\x01") + name; }
+
+// schedutil.IsScalarResourceName || ephemeral-storage (framework.Resource fields
+// beyond cpu / memory / pods); other names are ignored upstream.
+bool xres_name_ok(const std::string &n) {
+  if (n == "ephemeral-storage") return true;
+  if (n.rfind("hugepages-", 0) == 0 || n.rfind("attachable-volumes-", 0) == 0) return true;
+  if (n.find("kubernetes.io/") != std::string::npos) return true;  // IsPrefixedNativeResource
+  if (n.find('/') == std::string::npos) return false;               // IsNativeResource
+  if (n.rfind("requests.", 0) == 0) return false;
+  return qualified_name_ok("requests." + n);                        // IsExtendedResourceName
+}
+
+// Column of an extended resource (created on first sight, at most MAX_XRES).
+ks_status xres_column(ks_ctx *c, uint32_t name, bool create, uint32_t *out) {
+  auto it = c->xres_of.find(name);
+  if (it != c->xres_of.end()) {
+    *out = it->second;
+    return KS_OK;
+  }
+  if (!create) {
+    *out = UINT32_MAX;
+    return KS_OK;
+  }
+  if (c->xres_names.size() >= (size_t)MAX_XRES)
+    return c->fail(KS_ERR_UNSUPPORTED, "more than %d extended resource names (%s)", MAX_XRES, c->strs[name].c_str());
+  if (!c->d_xalloc) {
+    const size_t n = (size_t)MAX_XRES * c->npos;
+    HIPC(c, hipMalloc((void **)&c->d_xalloc, 2 * n * 8));
+    HIPC(c, hipMemsetAsync(c->d_xalloc, 0, 2 * n * 8, c->stream));
+    c->d_xreq = c->d_xalloc + n;
+  }
+  *out = (uint32_t)c->xres_names.size();
+  c->xres_of.emplace(name, *out);
+  c->xres_names.push_back(name);
+  return KS_OK;
+}
+
+// col[idx] = val (add: col[idx] += val) over the extended-resource columns
+// (d_xalloc, then d_xreq at MAX_XRES * npos).
+ks_status xres_scatter(ks_ctx *c, const std::vector<uint64_t> &idx, const std::vector<int64_t> &val, bool add) {
+  if (idx.empty()) return KS_OK;
+  const size_t bytes = idx.size() * 16 + 1024;
+  ks_status st = xfer_begin(c, bytes, bytes);
+  if (st) return st;
+  uint64_t *d_idx = dscratch<uint64_t>(c, idx.size());
+  int64_t *d_val = dscratch<int64_t>(c, val.size());
+  if ((st = h2d(c, d_idx, idx.data(), idx.size() * 8)) || (st = h2d(c, d_val, val.data(), val.size() * 8))) return st;
+  HIPC(c, launch_scatter_i64(c->d_xalloc, d_idx, d_val, (uint32_t)idx.size(), add, c->stream));
+  return xfer_sync(c);
+}
+
+// PodRequests for the extended resources (resourcehelper.PodRequests: the
+// containers' sum, init containers' max with sidecars) as (column, value) with
+// value > 0.  KS_REQ_HAS_OTHER (a request the caller could not express) is
+// refused; names framework.Resource ignores are skipped.
+ks_status pod_xrequests(ks_ctx *c, const ks_pod &p, bool create, std::vector<std::pair<uint32_t, int64_t>> *out) {
+  out->clear();
+  bool any = false;
+  auto scan = [&](const ks_container *cs, uint32_t n) {
+    for (uint32_t i = 0; i < n; ++i) any |= cs[i].n_extended != 0;
+  };
+  scan(p.containers, p.n_containers);
+  scan(p.init_containers, p.n_init_containers);
+  if (!any) return KS_OK;
+  std::map<uint32_t, int64_t> sum, side, init;  // by column
+  auto each = [&](const ks_container &k, const std::function<ks_status(uint32_t, int64_t)> &f) -> ks_status {
+    for (uint32_t j = 0; j < k.n_extended; ++j) {
+      const std::string nm = str(k.extended[j].name);
+      if (!xres_name_ok(nm)) continue;
+      if (k.extended[j].value < 0 || k.extended[j].value >= kMaxExact)
+        return c->fail(KS_ERR_RANGE, "pod %s: %s request outside [0, 2^46)", str(p.name).c_str(), nm.c_str());
+      uint32_t col;
+      if (ks_status st = xres_column(c, c->intern(nm.c_str()), create, &col)) return st;
+      if (col == UINT32_MAX) continue;  // ks_pods_check: no column yet (validation only)
+      if (ks_status st = f(col, k.extended[j].value)) return st;
+    }
+    return KS_OK;
+  };
+  for (uint32_t i = 0; i < p.n_containers; ++i)
+    if (ks_status st = each(p.containers[i], [&](uint32_t col, int64_t v) { sum[col] += v; return KS_OK; }))
+      return st;
+  for (uint32_t i = 0; i < p.n_init_containers; ++i) {
+    const ks_container &k = p.init_containers[i];
+    std::map<uint32_t, int64_t> use;
+    ks_status st;
+    if (k.restart_always) {
+      st = each(k, [&](uint32_t col, int64_t v) { sum[col] += v; side[col] += v; return KS_OK; });
+      use = side;
+    } else {
+      use = side;
+      st = each(k, [&](uint32_t col, int64_t v) { use[col] += v; return KS_OK; });
+    }
+    if (st) return st;
+    for (auto &kv : use) init[kv.first] = std::max(init[kv.first], kv.second);
+  }
+  for (auto &kv : init) sum[kv.first] = std::max(sum[kv.first], kv.second);
+  for (auto &kv : sum)
+    if (kv.second > 0) out->emplace_back(kv.first, kv.second);
+  return KS_OK;
 }
 
 // --------------------------------------------------------------- devices
@@ -1351,16 +1445,62 @@ bool parse_label_selector(ks_ctx *c, const ks_label_selector &ls, std::vector<Se
   return true;
 }
 
-// A pod's spread constraints -> SpreadDev records in the program buffer.
-// Invalid constraints (the apiserver would reject them; upstream's PreFilter /
-// PreScore would return an Error) are refused with KS_ERR_UNSUPPORTED, so
-// the shim hands the pod to upstream.  Without `create` (ks_pods_check) only
-// validates.
-ks_status spread_compile(ks_ctx *c, const ks_pod &p, PodDev &d, ProgBuf &cl, bool create,
-                         std::vector<uint32_t> *refs) {
+// Whether compiling the pod may create one-pod-path state (columns, label
+// bits, device buffers): ks_batch_prepare drains the submitted batches first.
+bool may_need_solo(const ks_ctx *c, const ks_pod &p) {
+  if (p.n_spread) return true;
+  for (uint32_t i = 0; i < p.n_containers; ++i)
+    if (p.containers[i].n_extended || (!c->images.empty() && p.containers[i].image && p.containers[i].image[0]))
+      return true;
+  for (uint32_t i = 0; i < p.n_init_containers; ++i)
+    if (p.init_containers[i].n_extended ||
+        (!c->images.empty() && p.init_containers[i].image && p.init_containers[i].image[0]))
+      return true;
+  return false;
+}
+
+// The one-pod-path program of a pod (ksched_dev.hpp SoloHdr): its spread
+// constraints (SpreadDev), extended-resource requests (XResDev) and the
+// ImageLocality terms of its images present on some node (ImageDev).  Pods
+// with none of them stay on the round kernels.  Invalid constraints (the
+// apiserver would reject them; upstream's PreFilter / PreScore would return
+// an Error) are refused with KS_ERR_UNSUPPORTED, so the shim hands the pod to
+// upstream.  Without `create` (ks_pods_check) only validates.
+ks_status solo_compile(ks_ctx *c, const ks_pod &p, PodDev &d, ProgBuf &cl, bool create,
+                       std::vector<uint32_t> *refs) {
   const std::string pn = str(p.ns) + "/" + str(p.name);
+  ks_status st;
+  std::vector<std::pair<uint32_t, int64_t>> xr;
+  if ((st = pod_xrequests(c, p, create, &xr))) return st;
+  // imagelocality#sumImageScores: every init and regular container whose
+  // (normalised) image some node reports adds scaledImageScore
+  std::vector<ImageDev> imgs;
+  if (!c->images.empty()) {
+    auto scan = [&](const ks_container *cs, uint32_t n) -> ks_status {
+      for (uint32_t i = 0; i < n; ++i) {
+        if (!cs[i].image || !cs[i].image[0]) continue;
+        const std::string nm = normalized_image(cs[i].image);
+        auto it = c->images.find(nm);
+        if (it == c->images.end()) continue;
+        ImageDev g{};
+        if (create) {
+          if (ks_status e = get_key_bit(c, c->intern(image_key(nm).c_str()), &g.bit)) return e;
+        }
+        // scaledImageScore: int64(float64(size) * (float64(numNodes) / float64(totalNumNodes)))
+        g.scaled = (int64_t)((double)it->second.size * ((double)it->second.nodes / (double)c->n_present));
+        imgs.push_back(g);
+      }
+      return KS_OK;
+    };
+    if ((st = scan(p.init_containers, p.n_init_containers)) || (st = scan(p.containers, p.n_containers))) return st;
+    if (!imgs.empty()) c->compile_used_names = true;  // the node count enters the scores
+  }
+  if (!p.n_spread && xr.empty() && imgs.empty()) return KS_OK;
   if (c->cfg.world_size > 1)
-    return c->fail(KS_ERR_UNSUPPORTED, "pod %s: topology spread constraints need a single-rank context", pn.c_str());
+    return c->fail(KS_ERR_UNSUPPORTED,
+                   "pod %s: spread constraints, extended resources and present images need a single-rank context",
+                   pn.c_str());
+  if (create && (st = spread_alloc(c))) return st;
   if (p.n_spread > (uint32_t)MAX_SPREAD)
     return c->fail(KS_ERR_UNSUPPORTED, "pod %s: more than %d topology spread constraints", pn.c_str(), MAX_SPREAD);
   std::vector<std::pair<uint32_t, uint32_t>> own;  // the pod's labels (selfMatch)
@@ -1410,7 +1550,6 @@ ks_status spread_compile(ks_ctx *c, const ks_pod &p, PodDev &d, ProgBuf &cl, boo
     }
     if (!nothing && reqs_match(reqs, own)) r.flags |= SP_SELF;
     r.cls = CLS_NONE;  // Nothing() matches no pod; Empty() counts 0 (countPodsMatchSelector)
-    ks_status st;
     if (!nothing && !reqs.empty()) {
       if ((st = class_get(c, c->intern(p.ns), std::move(reqs), create, &r.cls))) return st;
       if (create && refs) refs->push_back(r.cls);
@@ -1419,14 +1558,23 @@ ks_status spread_compile(ks_ctx *c, const ks_pod &p, PodDev &d, ProgBuf &cl, boo
     recs.push_back(r);
   }
   if (!create) return KS_OK;
-  if (cl.w.size() & 1) cl.w.push_back(0);  // SpreadDev is 16-byte aligned
-  d.spread_off = (uint32_t)cl.w.size();
-  for (const SpreadDev &r : recs) {
-    uint64_t w[SPREAD_WORDS];
-    std::memcpy(w, &r, sizeof r);
-    cl.w.insert(cl.w.end(), w, w + SPREAD_WORDS);
+  if (cl.w.size() & 1) cl.w.push_back(0);  // the records are 16-byte aligned
+  d.solo_off = (uint32_t)cl.w.size();
+  auto emit = [&](const void *rec, size_t bytes) {
+    const size_t w0 = cl.w.size();
+    cl.w.resize(w0 + bytes / 8);
+    std::memcpy(cl.w.data() + w0, rec, bytes);
+  };
+  const SoloHdr hdr{(uint32_t)recs.size(), (uint32_t)xr.size(), (uint32_t)imgs.size(),
+                    p.n_init_containers + p.n_containers};
+  emit(&hdr, sizeof hdr);
+  for (const SpreadDev &r : recs) emit(&r, sizeof r);
+  for (auto &x : xr) {
+    const XResDev r{x.first, 0, x.second};
+    emit(&r, sizeof r);
   }
-  d.flags |= PF_SPREAD | (p.n_spread << PF_NSPREAD_SHIFT) | (p.spread_defaulted ? 0u : PF_SPREAD_ALLKEYS);
+  for (const ImageDev &g : imgs) emit(&g, sizeof g);
+  d.flags |= PF_SOLO | (p.n_spread && !p.spread_defaulted ? PF_SPREAD_ALLKEYS : 0u);
   (void)any_filter;
   (void)any_score;
   return KS_OK;
@@ -1885,6 +2033,8 @@ ks_status run_batch(ks_ctx *c, ks_batch *b) {
       sa.cmask = b->d_cmask;
       sa.dom = c->d_dom;
       sa.cnt = c->d_cnt;
+      sa.xalloc = c->d_xalloc;
+      sa.xreq = c->d_xreq;
       sa.dcnt = c->d_dcnt;
       sa.dflag = c->d_dflag;
       sa.dom_cap = c->dom_cap;
@@ -2188,7 +2338,8 @@ void ks_close(ks_ctx *c) {
                   c->t.npods, c->t.hard, c->t.prefer, c->t.lab, c->t.num, c->d_shards, c->d_slot_pos,
                   c->d_start, c->d_norm, c->d_norm_inv, c->d_pstat, c->d_fix, c->d_brec, c->d_srec, c->d_frec,
                   c->d_counters, c->d_crow, c->d_cext, c->d_pipe, c->d_carry, c->d_flags, c->d_dom,
-                  c->d_pos_slot, c->d_dcnt, c->d_dflag, c->d_acc, c->d_sst, c->d_sraw, c->d_spart};
+                  c->d_pos_slot, c->d_dcnt, c->d_dflag, c->d_acc, c->d_sst, c->d_sraw, c->d_spart,
+                  c->d_xalloc};
   for (void *b : bufs)
     if (b) (void)hipFree(b);
   if (c->h_start) (void)hipHostFree(c->h_start);
@@ -2223,6 +2374,7 @@ void ks_close(ks_ctx *c) {
 }
 
 ks_status ks_nodes_upsert(ks_ctx *c, const ks_node *nodes, const uint32_t *slots, uint32_t n) {
+  const uint32_t nodes_n = n;
   if (!c || (n && (!nodes || !slots))) return KS_ERR_INVALID;
   if (ks_status dst_ = drain_async(c)) return dst_;
   HIPC(c, hipSetDevice(c->cfg.device));
@@ -2274,12 +2426,19 @@ ks_status ks_nodes_upsert(ks_ctx *c, const ks_node *nodes, const uint32_t *slots
     h.present = true;
     h.name = nid;
     c->name_slot[h.name] = slot;
-    h.images.clear();
-    for (uint32_t k = 0; k < s.n_images; ++k)
-      if (s.images && s.images[k] && s.images[k][0]) h.images.push_back(normalized_image(s.images[k]));
-    std::sort(h.images.begin(), h.images.end());
-    h.images.erase(std::unique(h.images.begin(), h.images.end()), h.images.end());
-    if (node_images_ref(c, h, +1)) grew = true;  // a prepared pod's image may now be present
+    std::vector<std::pair<std::string, int64_t>> old_images;
+    old_images.swap(h.images);
+    {
+      // one entry per name, the first occurrence's size (addNodeImageStates)
+      std::unordered_set<std::string> seen;
+      for (uint32_t k = 0; k < s.n_images; ++k)
+        if (s.images && s.images[k].name && s.images[k].name[0] && seen.insert(str(s.images[k].name)).second)
+          h.images.emplace_back(str(s.images[k].name), s.images[k].size_bytes);
+      std::sort(h.images.begin(), h.images.end());
+    }
+    node_images_ref(c, h, +1);
+    // prepared pods' ImageLocality terms (sizes, node counts) may have changed
+    if (h.images != old_images || (is_new && !h.images.empty())) grew = true;
     h.acpu = s.alloc_milli_cpu;
     h.amem = s.alloc_memory;
     h.apods = s.alloc_pods;
@@ -2288,6 +2447,11 @@ ks_status ks_nodes_upsert(ks_ctx *c, const ks_node *nodes, const uint32_t *slots
     for (uint32_t k = 0; k < s.n_labels; ++k) {
       const uint32_t key = c->intern(s.labels[k].key);
       h.labels.emplace_back(key, c->intern(s.labels[k].value));
+      c->key_nodes[key].push_back(slot);
+    }
+    for (auto &im : h.images) {  // ImageLocality: "image present" keys in the label bitset
+      const uint32_t key = c->intern(image_key(im.first).c_str());
+      h.labels.emplace_back(key, 0u);
       c->key_nodes[key].push_back(slot);
     }
     if (!is_new) prefer_mask_ref(c, h.prefer, -1);
@@ -2349,6 +2513,45 @@ ks_status ks_nodes_upsert(ks_ctx *c, const ks_node *nodes, const uint32_t *slots
   std::vector<uint32_t> changed;
   changed.reserve(row_of.size());
   for (auto &kv : row_of) changed.push_back(kv.first);
+  // extended allocatable (ephemeral-storage, scalar resources): columns for
+  // every name first, then every column's value of every upserted node; a new
+  // node's Requested starts at 0
+  std::unordered_map<uint32_t, uint32_t> last;  // slot -> index of its last state in the call
+  for (uint32_t i = 0; i < nodes_n; ++i) last[slots[i]] = i;
+  for (uint32_t i = 0; i < nodes_n; ++i)
+    for (uint32_t k = 0; k < nodes[i].n_extended; ++k) {
+      const std::string nm = str(nodes[i].extended[k].name);
+      if (!xres_name_ok(nm)) continue;
+      uint32_t col;
+      if ((st = xres_column(c, c->intern(nm.c_str()), true, &col)) == KS_ERR_UNSUPPORTED) continue;  // ignored
+      if (st) return st;
+    }
+  if (!c->xres_names.empty()) {
+    std::vector<uint64_t> idx;
+    std::vector<int64_t> val;
+    const uint64_t nx = (uint64_t)MAX_XRES * c->npos;
+    for (auto &kv : last) {
+      const ks_node &nd = nodes[kv.second];
+      const uint64_t pos = c->slot_pos[kv.first];
+      std::vector<int64_t> a(c->xres_names.size(), 0);
+      for (uint32_t k = 0; k < nd.n_extended; ++k) {
+        auto it = c->xres_of.find((uint32_t)c->lookup(nd.extended[k].name));
+        if (nd.extended[k].name && it != c->xres_of.end() && xres_name_ok(str(nd.extended[k].name)))
+          a[it->second] = nd.extended[k].value;
+      }
+      for (uint32_t col = 0; col < a.size(); ++col) {
+        if (a[col] < 0 || a[col] >= kMaxAlloc)
+          return c->fail(KS_ERR_RANGE, "node %s extended allocatable outside the exact range", str(nd.name).c_str());
+        idx.push_back(col * (uint64_t)c->npos + pos);
+        val.push_back(a[col]);
+        if (core[(size_t)row_of[kv.first] * 8 + 3]) {  // new node: Requested = 0
+          idx.push_back(nx + col * (uint64_t)c->npos + pos);
+          val.push_back(0);
+        }
+      }
+    }
+    if ((st = xres_scatter(c, idx, val, false))) return st;
+  }
   return spread_nodes_changed(c, changed.data(), (uint32_t)changed.size(), false);
 }
 
@@ -2382,6 +2585,19 @@ ks_status ks_nodes_delete(ks_ctx *c, const uint32_t *slots, uint32_t n) {
     return st;
   HIPC(c, launch_scatter_rows(c->t, d_pos, d_core, nullptr, n, 0u, c->stream));
   if ((st = xfer_sync(c))) return st;
+  if (!c->xres_names.empty()) {  // extended Allocatable / Requested leave with the node
+    std::vector<uint64_t> idx;
+    std::vector<int64_t> val;
+    const uint64_t nx = (uint64_t)MAX_XRES * c->npos;
+    for (uint32_t i = 0; i < n; ++i)
+      for (uint32_t col = 0; col < c->xres_names.size(); ++col) {
+        idx.push_back(col * (uint64_t)c->npos + pos[i]);
+        idx.push_back(nx + col * (uint64_t)c->npos + pos[i]);
+        val.push_back(0);
+        val.push_back(0);
+      }
+    if ((st = xres_scatter(c, idx, val, false))) return st;
+  }
   return spread_nodes_changed(c, slots, n, true);
 }
 
@@ -2393,13 +2609,22 @@ static ks_status pods_delta(ks_ctx *c, const ks_pod *pods, const uint32_t *slots
   std::vector<uint32_t> pos(n);
   std::vector<int64_t> d((size_t)n * 5);
   int64_t aff = 0;
+  // NodeInfo.Requested of the extended resources (validated before any device work)
+  std::vector<uint64_t> xidx;
+  std::vector<int64_t> xval;
+  std::vector<std::pair<uint32_t, int64_t>> xr;
   for (uint32_t i = 0; i < n; ++i) {
     if (slots[i] >= c->cap || !c->nodes[slots[i]].present)
       return c->fail(KS_ERR_NOT_FOUND, "slot %u not present", slots[i]);
     int64_t rc, rm, zc, zm;
     ks_status st;
     if ((st = pod_requests(pods[i], false, &rc, &rm)) || (st = pod_requests(pods[i], true, &zc, &zm)))
-      return c->fail(st, "pod requests a resource other than cpu/memory");
+      return c->fail(st, "pod requests a resource it cannot express (KS_REQ_HAS_OTHER)");
+    if ((st = pod_xrequests(c, pods[i], true, &xr))) return st;
+    for (auto &x : xr) {
+      xidx.push_back((uint64_t)MAX_XRES * c->npos + x.first * (uint64_t)c->npos + c->slot_pos[slots[i]]);
+      xval.push_back(sign * x.second);
+    }
     if (pods[i].unmodelled & KS_UNMODELLED_POD_AFFINITY) aff += sign;
     pos[i] = c->slot_pos[slots[i]];
     int64_t *x = &d[(size_t)i * 5];
@@ -2418,6 +2643,7 @@ static ks_status pods_delta(ks_ctx *c, const ks_pod *pods, const uint32_t *slots
   HIPC(c, launch_apply_deltas(c->t, d_pos, d_d, n, c->stream));
   c->affinity_pods += aff;
   if ((st = xfer_sync(c))) return st;
+  if ((st = xres_scatter(c, xidx, xval, true))) return st;
   return spread_pods_delta(c, pods, slots, n, sign);
 }
 
@@ -2515,9 +2741,12 @@ ks_status ks_batch_prepare(ks_ctx *c, const ks_pod *pods, uint32_t n, ks_batch *
   ks_status st;
   // Spread pods may create topology / selector-class columns, computed from the
   // host's records of bound pods: let every submitted batch finish first.
-  bool any_spread = false;
-  for (uint32_t i = 0; i < n && !any_spread; ++i) any_spread = pods[i].n_spread != 0;
-  if (any_spread) drain_async(c);
+  bool any_solo = false;
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    for (uint32_t i = 0; i < n && !any_solo; ++i) any_solo = may_need_solo(c, pods[i]);
+  }
+  if (any_solo) drain_async(c);
   std::vector<uint32_t> set_ids(n), refs;
   {
     // compile against the host dictionaries (the worker reads t.lw and the
@@ -2525,7 +2754,7 @@ ks_status ks_batch_prepare(ks_ctx *c, const ks_pod *pods, uint32_t n, ks_batch *
     std::unique_lock<std::mutex> g(c->mu);
     if ((st = compile_batch(c, pods, n, dev.data(), cl, g, true, &refs))) return st;
     for (uint32_t i = 0; i < n; ++i) {
-      if (dev[i].flags & PF_SPREAD) continue;  // the spread path evaluates it
+      if (dev[i].flags & PF_SOLO) continue;  // the one-pod path evaluates it
       if (dev[i].flags & PF_EXT) ext = true;
       if (dev[i].flags & (PF_TT | PF_NA)) norm = true;
     }
@@ -2549,10 +2778,11 @@ ks_status ks_batch_prepare(ks_ctx *c, const ks_pod *pods, uint32_t n, ks_batch *
   b->spread.assign(n, 0);
   b->any_spread = false;
   for (uint32_t i = 0; i < n; ++i) {
-    if (!(dev[i].flags & PF_SPREAD)) continue;
-    const SpreadDev *sd = reinterpret_cast<const SpreadDev *>(cl.w.data() + dev[i].spread_off);
+    if (!(dev[i].flags & PF_SOLO)) continue;
+    const SoloHdr *hd = reinterpret_cast<const SoloHdr *>(cl.w.data() + dev[i].solo_off);
+    const SpreadDev *sd = reinterpret_cast<const SpreadDev *>(hd + 1);
     uint8_t f = 1;
-    for (uint32_t k = 0; k < (dev[i].flags >> PF_NSPREAD_SHIFT); ++k) f |= (sd[k].flags & SP_SCORE) ? 4 : 2;
+    for (uint32_t k = 0; k < hd->n_spread; ++k) f |= (sd[k].flags & SP_SCORE) ? 4 : 2;
     b->spread[i] = f;
     b->any_spread = true;
   }
@@ -2676,6 +2906,8 @@ SpreadArgs spread_args(ks_ctx *c) {
   sa.npos = c->npos;
   sa.dom = c->d_dom;
   sa.cnt = c->d_cnt;
+  sa.xalloc = c->d_xalloc;
+  sa.xreq = c->d_xreq;
   sa.dcnt = c->d_dcnt;
   sa.dflag = c->d_dflag;
   sa.dom_cap = c->dom_cap;
@@ -2708,8 +2940,9 @@ ks_status spread_plugin_scores(ks_ctx *c, const PodDev &d, const ProgBuf &cl, ks
   sa.dump = d_out;
   sa.no_commit = 1;
   bool has_filter = false, has_score = false;
-  const SpreadDev *sd = reinterpret_cast<const SpreadDev *>(cl.w.data() + d.spread_off);
-  for (uint32_t k = 0; k < (d.flags >> PF_NSPREAD_SHIFT); ++k) ((sd[k].flags & SP_SCORE) ? has_score : has_filter) = true;
+  const SoloHdr *hd = reinterpret_cast<const SoloHdr *>(cl.w.data() + d.solo_off);
+  const SpreadDev *sd = reinterpret_cast<const SpreadDev *>(hd + 1);
+  for (uint32_t k = 0; k < hd->n_spread; ++k) ((sd[k].flags & SP_SCORE) ? has_score : has_filter) = true;
   HIPC(c, launch_spread_pod(sa, has_filter, has_score, c->stream));
   if ((st = d2h(c, raw.data(), d_out, raw.size() * 4)) || (st = xfer_sync(c))) return st;
   for (uint32_t i = 0; i < c->cap; ++i) {
@@ -2748,7 +2981,7 @@ ks_status ks_plugin_scores(ks_ctx *c, const ks_pod *pod, ks_node_score *out) {
     if ((st = upload_dirty_ext(c, c->xm))) return st;
   }
   if (cl.w.empty()) cl.w.push_back(0);
-  if (d.flags & PF_SPREAD) return spread_plugin_scores(c, d, cl, out);
+  if (d.flags & PF_SOLO) return spread_plugin_scores(c, d, cl, out);
   DumpArgs a{};
   a.t = c->t;
   a.nslots = c->cap;

@@ -87,6 +87,7 @@ struct SpreadArgs {
   const uint64_t *cmask;      // [npods] selector classes each pod of the batch matches
   const uint32_t *dom;        // [MAX_TOPO_KEYS][npos] domain id per position (DOM_NONE: key absent)
   uint32_t *cnt;              // [MAX_CLASSES][npos] matching bound pods per position
+  int64_t *xalloc, *xreq;     // [MAX_XRES][npos] extended resources: Allocatable, Requested
   uint32_t *dcnt;             // [MAX_SPREAD][dom_cap] per-constraint domain counts (zero between pods)
   uint32_t *dflag;            // [MAX_SPREAD][dom_cap] bit 0 Filter-eligible domain, bit 1 Score domain
   uint32_t dom_cap;
@@ -110,6 +111,8 @@ hipError_t launch_class_commit(const DevResult *res, const uint64_t *cmask, cons
                                uint32_t npos, uint32_t lo, uint32_t hi, hipStream_t st);
 hipError_t launch_scatter_u32(uint32_t *col, const uint64_t *idx, const uint32_t *val, uint32_t n, hipStream_t st);
 hipError_t launch_add_u32(uint32_t *col, const uint64_t *idx, const int32_t *delta, uint32_t n, hipStream_t st);
+hipError_t launch_scatter_i64(int64_t *col, const uint64_t *idx, const int64_t *val, uint32_t n, bool add,
+                              hipStream_t st);
 
 hipError_t launch_norm_check(const RoundArgs &a, hipStream_t st);
 hipError_t launch_sweep(const RoundArgs &a, bool ext, uint32_t nblocks, uint32_t ngroups, uint32_t nshards,

@@ -39,10 +39,34 @@ constexpr uint32_t SP_LDS_DOM = 1024; // keys with at most this many domains agg
 constexpr uint32_t SP_OFF_NONE = 0xFFFFFFFFu;
 constexpr int8_t SST_FEASIBLE = -1, SST_EMPTY = -2, SST_IGNORED = -3;  // per-position status
 
-__device__ __forceinline__ const SpreadDev *spread_recs(const SpreadArgs &a, const PodDev &p) {
-  return reinterpret_cast<const SpreadDev *>(a.clauses + p.spread_off);
+// The pod's one-pod-path program (ksched_dev.hpp SoloHdr): SpreadDev, XResDev, ImageDev records.
+__device__ __forceinline__ const SoloHdr &solo_hdr(const SpreadArgs &a, const PodDev &p) {
+  return *reinterpret_cast<const SoloHdr *>(a.clauses + p.solo_off);
 }
-__device__ __forceinline__ uint32_t spread_count(const PodDev &p) { return p.flags >> PF_NSPREAD_SHIFT; }
+__device__ __forceinline__ const SpreadDev *spread_recs(const SpreadArgs &a, const PodDev &p) {
+  return reinterpret_cast<const SpreadDev *>(&solo_hdr(a, p) + 1);
+}
+__device__ __forceinline__ uint32_t spread_count(const SpreadArgs &a, const PodDev &p) { return solo_hdr(a, p).n_spread; }
+__device__ __forceinline__ const XResDev *xres_recs(const SpreadArgs &a, const PodDev &p) {
+  return reinterpret_cast<const XResDev *>(spread_recs(a, p) + solo_hdr(a, p).n_spread);
+}
+__device__ __forceinline__ const ImageDev *image_recs(const SpreadArgs &a, const PodDev &p) {
+  return reinterpret_cast<const ImageDev *>(xres_recs(a, p) + solo_hdr(a, p).n_xres);
+}
+
+// imagelocality#calculatePriority over sumImageScores of the node (label bits
+// of the "image present" keys); 0 without present images.
+__device__ __forceinline__ int64_t image_score(const SpreadArgs &a, const PodDev &p, const NodeExt &e) {
+  const SoloHdr &h = solo_hdr(a, p);
+  if (!h.n_img) return 0;
+  const ImageDev *g = image_recs(a, p);
+  int64_t sum = 0;
+  for (uint32_t k = 0; k < h.n_img; ++k)
+    if ((e.lab[g[k].bit >> 6] >> (g[k].bit & 63)) & 1ull) sum += g[k].scaled;
+  const int64_t mb = 1024 * 1024, min_t = 23 * mb, max_t = 1000 * mb * (int64_t)h.n_containers;
+  sum = sum < min_t ? min_t : (sum > max_t ? max_t : sum);
+  return 100 * (sum - min_t) / (max_t - min_t);
+}
 
 // Go math.Log (log.go, fdlibm e_log.c; the amd64 assembly performs the same
 // operations) for a finite x >= 2, one rounding per operation.
@@ -154,7 +178,7 @@ __global__ __launch_bounds__(SP_THREADS) void spread_prep_kernel(SpreadArgs a) {
   __shared__ uint32_t s_off[MAX_SPREAD];
   const PodDev p = a.pods[a.pod];
   const SpreadDev *sd = spread_recs(a, p);
-  const uint32_t n = spread_count(p);
+  const uint32_t n = spread_count(a, p);
   if (threadIdx.x == 0) lds_segments(a, sd, n, s_off);
   for (uint32_t i = threadIdx.x; i < SP_LDS; i += SP_THREADS) s_h[i] = 0;
   __syncthreads();
@@ -208,7 +232,7 @@ __global__ __launch_bounds__(SP_THREADS) void spread_min_kernel(SpreadArgs a) {
   __shared__ uint32_t s_r[SP_THREADS / WAVE][2];
   const PodDev p = a.pods[a.pod];
   const SpreadDev *sd = spread_recs(a, p);
-  const uint32_t n = spread_count(p);
+  const uint32_t n = spread_count(a, p);
   const uint32_t lane = threadIdx.x % WAVE, wid = threadIdx.x / WAVE;
   for (uint32_t c = 0; c < n; ++c) {
     if (sd[c].flags & SP_SCORE) continue;
@@ -262,11 +286,12 @@ __global__ __launch_bounds__(SP_THREADS) void spread_filter_kernel(SpreadArgs a)
   __shared__ uint32_t s_red[SP_THREADS / WAVE][NFILT + 5];
   const PodDev p = a.pods[a.pod];
   const SpreadDev *sd = spread_recs(a, p);
-  const uint32_t n = spread_count(p);
+  const uint32_t n = spread_count(a, p);
   if (threadIdx.x == 0) lds_segments(a, sd, n, s_off);
   for (uint32_t i = threadIdx.x; i < SP_LDS / 32; i += SP_THREADS) s_seen[i] = 0;
   for (uint32_t i = threadIdx.x; i < SP_LDS; i += SP_THREADS) s_h[i] = 0;
   __syncthreads();
+  const uint32_t n_xres = solo_hdr(a, p).n_xres;
   bool any_s = false, aff_needed = false, taint_needed = false;
   for (uint32_t c = 0; c < n; ++c) {
     if (!(sd[c].flags & SP_SCORE)) continue;
@@ -311,6 +336,14 @@ __global__ __launch_bounds__(SP_THREADS) void spread_filter_kernel(SpreadArgs a)
     }
     int s = filter<true>(p, a.clauses, r, e);
     if (s == ST_FEASIBLE) {
+      // NodeResourcesFit (fitsRequest) for ephemeral-storage / scalar resources
+      const XResDev *xr = xres_recs(a, p);
+      for (uint32_t k = 0; k < n_xres; ++k) {
+        const size_t ix = (size_t)xr[k].col * a.npos + pos;
+        if (xr[k].req > a.xalloc[ix] - a.xreq[ix]) s = 4;  // KS_PLUGIN_NODE_RESOURCES_FIT
+      }
+    }
+    if (s == ST_FEASIBLE) {
       for (uint32_t c = 0; c < n; ++c) {
         const SpreadDev &q = sd[c];
         if (q.flags & SP_SCORE) continue;
@@ -334,7 +367,8 @@ __global__ __launch_bounds__(SP_THREADS) void spread_filter_kernel(SpreadArgs a)
       const uint32_t nr = (p.flags & PF_NA) ? (uint32_t)preferred_raw(p, a.clauses, e, slot) : 0u;
       tt_max = max(tt_max, tr);
       na_max = max(na_max, nr);
-      a.part[pos] = pack_part((uint32_t)a.w.fit * (uint32_t)score_la(p, r) + (uint32_t)a.w.ba * (uint32_t)score_ba(p, r),
+      a.part[pos] = pack_part((uint32_t)a.w.fit * (uint32_t)score_la(p, r) + (uint32_t)a.w.ba * (uint32_t)score_ba(p, r) +
+                                  (uint32_t)a.w.il * (uint32_t)image_score(a, p, e),
                               tr, nr);
       // PreScore (initPreScoreState): with requireAllTopologies a node lacking
       // a ScheduleAnyway key is ignored; the others' domains make topoSize
@@ -407,7 +441,7 @@ __global__ __launch_bounds__(SP_THREADS) void spread_score_kernel(SpreadArgs a) 
   __shared__ uint64_t s_r[SP_THREADS / WAVE][2];
   const PodDev p = a.pods[a.pod];
   const SpreadDev *sd = spread_recs(a, p);
-  const uint32_t n = spread_count(p);
+  const uint32_t n = spread_count(a, p);
   if (threadIdx.x < n) {
     const Totals tot = acc_totals(a.acc);
     const SpreadDev &q = sd[threadIdx.x];
@@ -462,7 +496,7 @@ __global__ __launch_bounds__(SP_THREADS) void spread_select_kernel(SpreadArgs a)
   __shared__ uint64_t s_r[SP_THREADS / WAVE];
   const PodDev p = a.pods[a.pod];
   const SpreadDev *sd = spread_recs(a, p);
-  const uint32_t n = spread_count(p);
+  const uint32_t n = spread_count(a, p);
   bool has_score = false;
   for (uint32_t c = 0; c < n; ++c) has_score |= (sd[c].flags & SP_SCORE) != 0;
   const Totals tot = acc_totals(a.acc);
@@ -515,7 +549,7 @@ __global__ __launch_bounds__(SP_THREADS) void spread_select_kernel(SpreadArgs a)
       const int64_t nr = (p.flags & PF_NA) ? preferred_raw(p, a.clauses, e, slot) : 0;
       o[5] = (int32_t)nr;
       o[6] = (p.flags & PF_HAS_PREF) ? (int32_t)normalize(nr, (p.flags & PF_NA) ? na_max : 0, false) : 0;
-      o[7] = 0;
+      o[7] = (int32_t)image_score(a, p, e);
       o[8] = (int32_t)raw;
       o[9] = (int32_t)norm;
       o[10] = (int32_t)(total & 0xFFFFFFFF);
@@ -580,6 +614,8 @@ __global__ void spread_commit_kernel(SpreadArgs a) {
         a.t.zcpu[pos] += p.nz_cpu;
         a.t.zmem[pos] += p.nz_mem;
         a.t.npods[pos] += 1;
+        const XResDev *xr = xres_recs(a, p);
+        for (uint32_t k = 0; k < solo_hdr(a, p).n_xres; ++k) a.xreq[(size_t)xr[k].col * a.npos + pos] += xr[k].req;
         uint64_t m = a.cmask[a.pod];
         while (m) {
           const uint32_t cls = (uint32_t)__builtin_ctzll(m);
@@ -632,6 +668,12 @@ __global__ void add_u32_kernel(uint32_t *col, const uint64_t *idx, const int32_t
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) atomicAdd(&col[idx[i]], (uint32_t)delta[i]);
 }
+__global__ void scatter_i64_kernel(int64_t *col, const uint64_t *idx, const int64_t *val, uint32_t n, uint32_t add) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (add) atomicAdd((unsigned long long *)&col[idx[i]], (unsigned long long)val[i]);
+  else col[idx[i]] = val[i];
+}
 
 // ------------------------------------------------------------- launchers
 
@@ -667,6 +709,13 @@ hipError_t launch_class_commit(const DevResult *res, const uint64_t *cmask, cons
 hipError_t launch_scatter_u32(uint32_t *col, const uint64_t *idx, const uint32_t *val, uint32_t n, hipStream_t st) {
   if (!n) return hipSuccess;
   scatter_u32_kernel<<<(n + 255) / 256, 256, 0, st>>>(col, idx, val, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_scatter_i64(int64_t *col, const uint64_t *idx, const int64_t *val, uint32_t n, bool add,
+                              hipStream_t st) {
+  if (!n) return hipSuccess;
+  scatter_i64_kernel<<<(n + 255) / 256, 256, 0, st>>>(col, idx, val, n, add ? 1u : 0u);
   return hipGetLastError();
 }
 

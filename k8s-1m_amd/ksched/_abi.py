@@ -28,6 +28,14 @@ class KsToleration(C.Structure):
     _fields_ = [("key", c_char_p), ("value", c_char_p), ("op", C.c_int32), ("effect", C.c_int32)]
 
 
+class KsResource(C.Structure):
+    _fields_ = [("name", c_char_p), ("value", C.c_int64)]
+
+
+class KsImage(C.Structure):
+    _fields_ = [("name", c_char_p), ("size_bytes", C.c_int64)]
+
+
 class KsNode(C.Structure):
     _fields_ = [
         ("name", c_char_p),
@@ -40,7 +48,10 @@ class KsNode(C.Structure):
         ("n_taints", C.c_uint32),
         ("unschedulable", C.c_uint32),
         ("n_images", C.c_uint32),
-        ("images", C.POINTER(c_char_p)),
+        ("images", C.POINTER(KsImage)),
+        ("extended", C.POINTER(KsResource)),
+        ("n_extended", C.c_uint32),
+        ("_pad", C.c_uint32),
     ]
 
 
@@ -51,6 +62,9 @@ class KsContainer(C.Structure):
         ("flags", C.c_uint32),
         ("restart_always", C.c_uint32),
         ("image", c_char_p),
+        ("extended", C.POINTER(KsResource)),
+        ("n_extended", C.c_uint32),
+        ("_pad", C.c_uint32),
     ]
 
 
@@ -232,7 +246,8 @@ class KsStats(C.Structure):
 
 # sizes from the C headers (checked in tests/test_abi.py against offsetof via the compiler)
 EXPECTED_SIZES = {
-    "ks_label": 16, "ks_taint": 24, "ks_toleration": 24, "ks_node": 72, "ks_container": 32,
+    "ks_label": 16, "ks_taint": 24, "ks_toleration": 24, "ks_node": 88, "ks_container": 48,
+    "ks_resource": 16, "ks_image": 16,
     "ks_requirement": 24, "ks_term": 24, "ks_preferred_term": 32, "ks_pod": 160, "ks_event": 24, "ks_result": 56,
     "ks_node_score": 48, "ks_node_state": 56, "ks_config": 60, "ks_stats": 88, "ks_label_selector": 32,
     "ks_spread_constraint": 72,
@@ -243,6 +258,7 @@ STRUCTS = {
     "ks_preferred_term": KsPreferredTerm, "ks_pod": KsPod, "ks_event": KsEvent, "ks_result": KsResult,
     "ks_node_score": KsNodeScore, "ks_node_state": KsNodeState, "ks_config": KsConfig,
     "ks_stats": KsStats, "ks_label_selector": KsLabelSelector, "ks_spread_constraint": KsSpreadConstraint,
+    "ks_resource": KsResource, "ks_image": KsImage,
 }
 
 KSCHED_SYMBOLS = [

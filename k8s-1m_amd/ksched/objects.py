@@ -8,7 +8,7 @@ from __future__ import annotations
 
 import ctypes as C
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional
+from typing import Dict, List, Optional, Tuple
 
 from . import _abi
 
@@ -35,7 +35,9 @@ class Toleration:
 
 @dataclass
 class Container:
-    # resources.requests; an absent key is a MISSING request (not zero)
+    # resources.requests; an absent key is a MISSING request (not zero); names
+    # other than cpu / memory go to ks_container.extended (ephemeral-storage,
+    # scalar resources; canonical integers)
     requests: Dict[str, int] = field(default_factory=dict)
     restart_policy_always: bool = False  # init containers: sidecar
     image: str = ""
@@ -100,7 +102,9 @@ class Node:
     labels: Dict[str, str] = field(default_factory=dict)
     taints: List[Taint] = field(default_factory=list)
     unschedulable: bool = False
-    images: List[str] = field(default_factory=list)  # status.images[].names, flattened
+    # status.images: (name, sizeBytes) per name, flattened
+    images: List[Tuple[str, int]] = field(default_factory=list)
+    extended: Dict[str, int] = field(default_factory=dict)  # status.allocatable beyond cpu / memory / pods
 
 
 @dataclass
@@ -146,15 +150,17 @@ class Arena:
 
 def _container(c: Container, a: "Arena") -> _abi.KsContainer:
     flags = 0
-    for k in c.requests:
+    ext = []
+    for k, v in c.requests.items():
         if k == "cpu":
             flags |= REQ_HAS_CPU
         elif k == "memory":
             flags |= REQ_HAS_MEMORY
         else:
-            flags |= REQ_HAS_OTHER
+            ext.append(_abi.KsResource(a.s(k), v))
+    xs, nx = a.array(_abi.KsResource, ext)
     return _abi.KsContainer(c.requests.get("cpu", 0), c.requests.get("memory", 0), flags,
-                            1 if c.restart_policy_always else 0, a.s(c.image) if c.image else None)
+                            1 if c.restart_policy_always else 0, a.s(c.image) if c.image else None, xs, nx, 0)
 
 
 def _requirement(r: NodeSelectorRequirement, a: Arena) -> _abi.KsRequirement:
@@ -193,10 +199,11 @@ def node_to_c(n: Node, a: Arena) -> _abi.KsNode:
     labels, nl = a.array(_abi.KsLabel, [_abi.KsLabel(a.s(k), a.s(v)) for k, v in n.labels.items()])
     taints, nt = a.array(
         _abi.KsTaint, [_abi.KsTaint(a.s(t.key), a.s(t.value), EFFECTS.get(t.effect, 9), 0) for t in n.taints])
-    images, ni = a.array(C.c_char_p, [a.s(i) for i in n.images])
+    images, ni = a.array(_abi.KsImage, [_abi.KsImage(a.s(nm), size) for nm, size in n.images])
+    ext, nx = a.array(_abi.KsResource, [_abi.KsResource(a.s(k), v) for k, v in n.extended.items()])
     al = n.allocatable
     return _abi.KsNode(a.s(n.name), al.get("cpu", 0), al.get("memory", 0), al.get("pods", 0), labels, taints,
-                       nl, nt, 1 if n.unschedulable else 0, ni, images)
+                       nl, nt, 1 if n.unschedulable else 0, ni, images, ext, nx, 0)
 
 
 def pod_to_c(p: Pod, a: Arena) -> _abi.KsPod:

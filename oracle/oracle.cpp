@@ -19,6 +19,7 @@
 #include <cstring>
 #include <functional>
 #include <map>
+#include <set>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -53,6 +54,11 @@ struct Node {
   // NodeInfo.Requested / NonZeroRequested / len(Pods)
   int64_t req_cpu = 0, req_mem = 0, nz_cpu = 0, nz_mem = 0;
   int64_t pods = 0;
+  // framework.Resource beyond cpu / memory / pods: ephemeral-storage and scalar
+  // resources (Allocatable, Requested)
+  std::map<std::string, int64_t> xalloc, xreq;
+  // status.images names (as reported) -> the entry's size (first occurrence)
+  std::vector<std::pair<std::string, int64_t>> images;
   // NodeInfo.Pods' namespace and labels (PodTopologySpread counts them)
   struct PodRec {
     std::string ns;
@@ -386,7 +392,64 @@ struct PodState {
   std::vector<SpreadConstraint> spread_filter, spread_score;
   bool spread_defaulted = false;
   bool spread_error = false;  // a selector failed to parse (the product refuses the pod)
+  // NodeResourcesFit beyond cpu / memory; ImageLocality inputs
+  std::map<std::string, int64_t> xreq;
+  std::vector<std::string> images;  // normalised, init containers then containers ("" = none)
+  int64_t n_containers = 0;
 };
+
+// v1helper.IsScalarResourceName (extended, hugepages-, attachable-volumes-,
+// kubernetes.io/-prefixed native) or ephemeral-storage: the resources
+// framework.Resource keeps beyond cpu / memory / pods.
+bool ExtendedResourceName(const std::string &n) {
+  if (n == "ephemeral-storage") return true;
+  if (n.rfind("hugepages-", 0) == 0 || n.rfind("attachable-volumes-", 0) == 0) return true;
+  const bool prefixed_native = n.find("kubernetes.io/") != std::string::npos;
+  if (prefixed_native) return true;
+  if (n.find('/') == std::string::npos) return false;  // native, not scalar
+  if (n.rfind("requests.", 0) == 0) return false;
+  return IsQualifiedName("requests." + n);  // IsExtendedResourceName
+}
+
+// PodRequests for the extended resources: containers' sum, init containers'
+// max with sidecars (the same rules as cpu / memory).
+std::map<std::string, int64_t> PodXRequests(const ks_pod &p) {
+  auto get = [](const ks_container &c) {
+    std::map<std::string, int64_t> r;
+    for (uint32_t k = 0; k < c.n_extended; ++k) {
+      const std::string nm = S(c.extended[k].name);
+      if (ExtendedResourceName(nm)) r[nm] += c.extended[k].value;
+    }
+    return r;
+  };
+  std::map<std::string, int64_t> sum, side, init;
+  for (uint32_t i = 0; i < p.n_containers; ++i)
+    for (auto &kv : get(p.containers[i])) sum[kv.first] += kv.second;
+  for (uint32_t i = 0; i < p.n_init_containers; ++i) {
+    auto r = get(p.init_containers[i]);
+    std::map<std::string, int64_t> use;
+    if (p.init_containers[i].restart_always) {
+      for (auto &kv : r) {
+        sum[kv.first] += kv.second;
+        side[kv.first] += kv.second;
+      }
+      use = side;
+    } else {
+      use = side;
+      for (auto &kv : r) use[kv.first] += kv.second;
+    }
+    for (auto &kv : use) init[kv.first] = std::max(init[kv.first], kv.second);
+  }
+  for (auto &kv : init) sum[kv.first] = std::max(sum[kv.first], kv.second);
+  return sum;
+}
+
+// imagelocality#normalizedImageName
+std::string NormalizedImageName(const std::string &name) {
+  const size_t c = name.rfind(':'), sl = name.rfind('/');
+  const long lc = c == std::string::npos ? -1 : (long)c, ls = sl == std::string::npos ? -1 : (long)sl;
+  return lc <= ls ? name + ":latest" : name;
+}
 
 // upstream:pkg/api/v1/resource/helpers.go#PodRequests for cpu/memory.
 void PodRequests(const ks_pod &p, bool non_missing, int64_t *cpu, int64_t *mem, bool *other) {
@@ -493,6 +556,14 @@ PodState compile_pod(const ks_pod &p) {
       }
     }
   }
+  st.xreq = PodXRequests(p);
+  for (uint32_t i = 0; i < p.n_init_containers; ++i)
+    st.images.push_back(p.init_containers[i].image && p.init_containers[i].image[0]
+                            ? NormalizedImageName(S(p.init_containers[i].image)) : std::string());
+  for (uint32_t i = 0; i < p.n_containers; ++i)
+    st.images.push_back(p.containers[i].image && p.containers[i].image[0]
+                            ? NormalizedImageName(S(p.containers[i].image)) : std::string());
+  st.n_containers = (int64_t)p.n_init_containers + p.n_containers;
   st.ns = S(p.ns);
   for (uint32_t i = 0; i < p.n_labels; ++i) st.labels[S(p.labels[i].key)] = S(p.labels[i].value);
   // podtopologyspread/common.go#filterTopologySpreadConstraints, per action
@@ -580,9 +651,17 @@ int Filter(const PodState &st, const Node &n) {
   // noderesources/fit.go#fitsRequest
   bool fail = false;
   if (n.pods + 1 > n.alloc_pods) fail = true;
-  if (!(st.req_cpu == 0 && st.req_mem == 0 && !st.req_other)) {
+  if (!(st.req_cpu == 0 && st.req_mem == 0 && !st.req_other && st.xreq.empty())) {
     if (st.req_cpu > 0 && st.req_cpu > n.alloc_cpu - n.req_cpu) fail = true;
     if (st.req_mem > 0 && st.req_mem > n.alloc_mem - n.req_mem) fail = true;
+    // ephemeral-storage (> 0) and every scalar resource (rQuant == 0 skipped)
+    for (auto &kv : st.xreq) {
+      if (kv.second == 0) continue;
+      auto a = n.xalloc.find(kv.first);
+      auto r = n.xreq.find(kv.first);
+      const int64_t alloc = a == n.xalloc.end() ? 0 : a->second, req = r == n.xreq.end() ? 0 : r->second;
+      if (kv.second > alloc - req) fail = true;
+    }
   }
   if (fail) return KS_PLUGIN_NODE_RESOURCES_FIT;
   return -1;
@@ -762,6 +841,42 @@ inline uint64_t PackKey(int64_t total, uint32_t slot) {
 
 struct oracle {
   std::vector<Node> nodes;
+  // cache imageStates: name -> (size of the first reporter, nodes reporting it)
+  struct ImageState {
+    int64_t size = 0;
+    int64_t nodes = 0;
+  };
+  std::map<std::string, ImageState> image_states;
+  int64_t n_present = 0;
+
+  void images_ref(const Node &n, int sign) {
+    for (auto &im : n.images) {
+      auto it = image_states.find(im.first);
+      if (sign > 0) {
+        if (it == image_states.end()) image_states.emplace(im.first, ImageState{im.second, 1});
+        else it->second.nodes++;
+      } else if (it != image_states.end() && --it->second.nodes == 0) {
+        image_states.erase(it);
+      }
+    }
+  }
+
+  // imagelocality Score: calculatePriority(sumImageScores, #containers)
+  int64_t ImageLocality(const PodState &st, const Node &n) const {
+    int64_t sum = 0;
+    for (auto &nm : st.images) {
+      if (nm.empty()) continue;
+      bool on = false;
+      for (auto &im : n.images) on |= im.first == nm;
+      if (!on) continue;
+      const ImageState &s = image_states.at(nm);
+      sum += (int64_t)((double)s.size * ((double)s.nodes / (double)n_present));  // scaledImageScore
+    }
+    const int64_t mb = 1024 * 1024, minT = 23 * mb, maxT = 1000 * mb * st.n_containers;
+    if (sum < minT) sum = minT;
+    else if (sum > maxT) sum = maxT;
+    return kMaxNodeScore * (sum - minT) / (maxT - minT);
+  }
   int64_t w_fit, w_ba, w_tt, w_na, w_il, w_pts = 2;
   int threads = 1;
 
@@ -769,6 +884,7 @@ struct oracle {
     int status;
     int64_t la, ba, tt_raw, na_raw;
     int64_t pts_raw, pts;  // PodTopologySpread raw / normalized (ScheduleAnyway constraints)
+    int64_t il;            // ImageLocality
   };
   std::vector<Eval> ev;  // per-node scratch, reused across pods
 
@@ -783,6 +899,7 @@ struct oracle {
     e.ba = BalancedAllocation(n.alloc_cpu, n.alloc_mem, n.req_cpu, n.req_mem, st.req_cpu, st.req_mem);
     e.tt_raw = TaintRaw(st, n);
     e.na_raw = st.has_preferred ? AffinityRaw(st, n) : 0;
+    e.il = ImageLocality(st, n);
     return e;
   }
 
@@ -790,7 +907,7 @@ struct oracle {
     // frameworkImpl.RunScorePlugins: Σ weight × normalized score.  ImageLocality
     // scores 0 (nodes report no images); NodeAffinity is skipped without
     // preferred terms (PreScore Skip) and contributes nothing either way.
-    int64_t t = w_fit * e.la + w_ba * e.ba + w_tt * Normalize(e.tt_raw, tt_max, true) + w_il * 0;
+    int64_t t = w_fit * e.la + w_ba * e.ba + w_tt * Normalize(e.tt_raw, tt_max, true) + w_il * e.il;
     if (st.has_preferred) t += w_na * Normalize(e.na_raw, na_max, false);
     if (!st.spread_score.empty()) t += w_pts * e.pts;  // PreScore Skip without ScheduleAnyway constraints
     return t;
@@ -813,6 +930,7 @@ struct oracle {
     PodRequests(p, true, &zc, &zm, &other);
     n.req_cpu += sign * rc;
     n.req_mem += sign * rm;
+    for (auto &kv : PodXRequests(p)) n.xreq[kv.first] += sign * kv.second;
     n.nz_cpu += sign * zc;
     n.nz_mem += sign * zm;
     n.pods += sign;
@@ -1015,8 +1133,24 @@ int32_t oracle_nodes_upsert(oracle *o, const ks_node *nodes, const uint32_t *slo
     if (slots[i] >= o->nodes.size()) return KS_ERR_NOT_FOUND;
     Node &d = o->nodes[slots[i]];
     const ks_node &s = nodes[i];
-    if (!d.present) d = Node();
+    if (!d.present) {
+      d = Node();
+      o->n_present++;
+    } else {
+      o->images_ref(d, -1);  // UpdateNode: removeNodeImageStates, then add
+    }
     d.present = true;
+    d.images.clear();
+    {
+      std::set<std::string> seen;
+      for (uint32_t k = 0; k < s.n_images; ++k)
+        if (s.images[k].name && s.images[k].name[0] && seen.insert(S(s.images[k].name)).second)
+          d.images.emplace_back(S(s.images[k].name), s.images[k].size_bytes);
+    }
+    o->images_ref(d, +1);
+    d.xalloc.clear();
+    for (uint32_t k = 0; k < s.n_extended; ++k)
+      if (ExtendedResourceName(S(s.extended[k].name))) d.xalloc[S(s.extended[k].name)] = s.extended[k].value;
     d.name = S(s.name);
     d.alloc_cpu = s.alloc_milli_cpu;
     d.alloc_mem = s.alloc_memory;
@@ -1034,6 +1168,10 @@ int32_t oracle_nodes_upsert(oracle *o, const ks_node *nodes, const uint32_t *slo
 int32_t oracle_nodes_delete(oracle *o, const uint32_t *slots, uint32_t n) {
   for (uint32_t i = 0; i < n; ++i) {
     if (slots[i] >= o->nodes.size()) return KS_ERR_NOT_FOUND;
+    if (o->nodes[slots[i]].present) {
+      o->images_ref(o->nodes[slots[i]], -1);
+      o->n_present--;
+    }
     o->nodes[slots[i]] = Node();
   }
   return KS_OK;
@@ -1097,7 +1235,7 @@ int32_t oracle_plugin_scores(oracle *o, const ks_pod *pod, ks_node_score *out) {
       s.taint_score = (int32_t)Normalize(ev[i].tt_raw, tt_max, true);
       s.affinity_raw = (int32_t)ev[i].na_raw;
       s.affinity_score = st.has_preferred ? (int32_t)Normalize(ev[i].na_raw, na_max, false) : 0;
-      s.image_locality = 0;
+      s.image_locality = (int32_t)ev[i].il;
       s.spread_raw = (int32_t)ev[i].pts_raw;
       s.spread_score = st.spread_score.empty() ? 0 : (int32_t)ev[i].pts;
       s.total_score = o->total(st, ev[i], tt_max, na_max);

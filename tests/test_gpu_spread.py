@@ -254,3 +254,85 @@ def test_spread_1k_nodes_many_pods_same_deployment():
     assert (r["status"] == 0).all()
     x.states_equal("replicas")
     x.close()
+
+
+# ------------------------------------------- extended resources, ImageLocality
+
+@pytest.mark.parametrize("name", sorted(__import__("solo_cases").CASES))
+@pytest.mark.parametrize("P", [256, 2])
+def test_solo_case_gpu(name, P):
+    from solo_cases import CASES as SOLO
+    nodes, bound, pods, exp, dumps = SOLO[name]()
+    x = Pair(len(nodes), pods_per_round=P)
+    x.upsert(nodes, list(range(len(nodes))))
+    x.add([p for p, _ in bound], [s for _, s in bound])
+    for j, p in enumerate(pods):
+        if j in dumps:
+            out = x.dump_equal(p, f"{name} dump {j}")
+            assert [out[i].image_locality for i in range(len(nodes))] == dumps[j]
+    r = x.schedule(pods, name)
+    check(r, exp)
+    x.states_equal(name)
+    x.close()
+
+
+IMAGES = [(f"reg.example/app{i}:v{i % 3}", (20 + 97 * i) << 20) for i in range(12)]
+XRES = ["nvidia.com/gpu", "ephemeral-storage", "hugepages-2Mi", "example.com/nic"]
+
+
+def rand_res_nodes(rng, n, slot0=0):
+    out = rand_nodes(rng, n, 6, slot0)
+    for nd in out:
+        if rng.random() < 0.5:
+            nd.extended["nvidia.com/gpu"] = rng.choice([1, 2, 4, 8])
+        if rng.random() < 0.6:
+            nd.extended["ephemeral-storage"] = rng.choice([50, 100, 200]) * Gi
+        if rng.random() < 0.2:
+            nd.extended["hugepages-2Mi"] = rng.choice([256, 1024]) * Mi
+        if rng.random() < 0.1:
+            nd.extended["example.com/nic"] = rng.randint(1, 4)
+        nd.images = rng.sample(IMAGES, rng.randint(0, 5))
+    return out
+
+
+def rand_res_pod(rng, j):
+    p = rand_pod(rng, j, spread_frac=0.25)
+    c = p.containers[0]
+    if rng.random() < 0.3:
+        c.requests["nvidia.com/gpu"] = rng.choice([0, 1, 2, 4])
+    if rng.random() < 0.3:
+        c.requests["ephemeral-storage"] = rng.choice([1, 10, 40]) * Gi
+    if rng.random() < 0.05:
+        c.requests["hugepages-2Mi"] = 256 * Mi
+    if rng.random() < 0.05:
+        c.requests["example.com/nic"] = 1
+    if rng.random() < 0.5:
+        c.image = rng.choice(IMAGES)[0] if rng.random() < 0.8 else "unknown/img"
+    if rng.random() < 0.1:
+        p.init_containers = [Container({"nvidia.com/gpu": rng.choice([1, 8])}, image=rng.choice(IMAGES)[0])]
+    return p
+
+
+@pytest.mark.parametrize("seed,n,P", [(21, 400, 256), (22, 1500, 64)])
+def test_resources_images_random_stream(seed, n, P):
+    rng = random.Random(seed)
+    x = Pair(n, pods_per_round=P)
+    x.upsert(rand_res_nodes(rng, n), list(range(n)))
+    pre = [rand_res_pod(rng, 50_000 + j) for j in range(n // 3)]
+    for p in pre:
+        p.topology_spread = []
+    live = [(p, rng.randrange(n)) for p in pre]
+    x.add([p for p, _ in live], [s for _, s in live])
+    for b in range(3):
+        pods = [rand_res_pod(rng, b * 1000 + j) for j in range(150)]
+        x.schedule(pods, f"seed {seed} batch {b}")
+        x.states_equal(f"seed {seed} batch {b}")
+        rng.shuffle(live)
+        gone, live = live[:5], live[5:]
+        x.add([p for p, _ in gone], [s for _, s in gone], sign=-1)
+        slots = rng.sample(range(n), 3)
+        live = [(p, s) for p, s in live if s != slots[1]]
+        x.upsert(rand_res_nodes(rng, 3, slot0=n + 10 * b), slots)  # new images / allocatable
+        x.delete([slots[1]])
+        x.dump_equal(rand_res_pod(rng, 90_000 + b), f"seed {seed} dump {b}")
+    x.close()

@@ -129,10 +129,13 @@ def test_pod_requests_init_sidecar_overhead():
     assert (rc, rm) == (max(350, 1000, 50, 450) + 7, max(80, 5, 50, 150) + 3)
 
 
-def test_pod_requests_other_resource_flagged():
-    assert requests(Pod("p", containers=[Container({"nvidia.com/gpu": 1})]))[0] == 4
+def test_pod_requests_extended_resources_pass_through():
+    # extended / scalar requests travel in ks_container.extended (KS_REQ_HAS_OTHER only
+    # for requests the caller cannot express); cpu / memory are unaffected
+    st, (rc, rm, zc, zm) = requests(Pod("p", containers=[Container({"nvidia.com/gpu": 1, "cpu": 5})]))
+    assert st == 0 and (rc, zc) == (5, 5)
 
 
 def test_struct_layout_consistency():
     # pyoracle reuses the ksched ctypes structs: layout mirrors the header
-    assert C.sizeof(_abi.KsPod) == 160 and C.sizeof(_abi.KsNode) == 72 and C.sizeof(_abi.KsResult) == 56
+    assert C.sizeof(_abi.KsPod) == 160 and C.sizeof(_abi.KsNode) == 88 and C.sizeof(_abi.KsResult) == 56

@@ -75,3 +75,19 @@ def test_go_log_restatement():
         assert L.oracle_go_log(x) == go_log(x), x
     assert go_log(2.0) == 0.6931471805599453 and go_log(10.0) == 2.302585092994046
     assert sum(go_log(float(x)) != math.log(x) for x in range(2, 10_000)) > 0  # really not libm
+
+
+@pytest.mark.parametrize("name", sorted(__import__("solo_cases").CASES))
+def test_solo_case(name):
+    from solo_cases import CASES as SOLO
+    nodes, bound, pods, exp, dumps = SOLO[name]()
+    a = Arena()
+    o = build_oracle(nodes, bound, a)
+    pa, m = pods_array(pods, a)
+    out = []
+    for j in range(m):
+        if j in dumps:
+            sc = o.plugin_scores(pod_ptr(pa, j))
+            assert [sc[i].image_locality for i in range(len(nodes))] == dumps[j], (name, j)
+        out.append(res_array(o.schedule(pod_ptr(pa, j), 1), 1)[0])
+    check(np.array(out), exp)
