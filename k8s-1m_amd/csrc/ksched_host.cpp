@@ -320,6 +320,10 @@ struct ks_ctx {
   // PodTopologySpread (ksched_spread.hip; device columns allocated on first use)
   std::map<std::pair<uint32_t, std::vector<std::pair<uint32_t, uint32_t>>>, uint32_t> set_ids;
   std::vector<LabelSet> label_sets;
+  std::unordered_map<std::string, uint32_t> empty_set_of_ns;  // label-less pods: namespace -> set id
+  // (slot, set) of pods the batches bound, appended at the end of each run and
+  // applied to HostNode::pod_sets only when a reader needs them (flush_bound)
+  std::vector<std::pair<uint32_t, uint32_t>> pending_bound;
   SpreadClass classes[MAX_CLASSES];
   std::unordered_map<std::string, uint32_t> class_of;  // canonical selector -> class
   uint64_t class_seq = 0;
@@ -1228,6 +1232,10 @@ uint32_t kernel_npl(const ks_ctx *c, bool ext) {
 
 // Interned (namespace, labels) of a pod.
 uint32_t intern_set(ks_ctx *c, const ks_pod &p) {
+  if (p.n_labels == 0) {  // the common case: one lookup by namespace
+    auto it = c->empty_set_of_ns.find(str(p.ns));
+    if (it != c->empty_set_of_ns.end()) return it->second;
+  }
   std::vector<std::pair<uint32_t, uint32_t>> l;
   l.reserve(p.n_labels);
   for (uint32_t k = 0; k < p.n_labels; ++k) l.emplace_back(c->intern(p.labels[k].key), c->intern(p.labels[k].value));
@@ -1238,7 +1246,15 @@ uint32_t intern_set(ks_ctx *c, const ks_pod &p) {
   const uint32_t id = (uint32_t)c->label_sets.size();
   c->label_sets.push_back(LabelSet{key.first, key.second});
   c->set_ids.emplace(std::move(key), id);
+  if (p.n_labels == 0) c->empty_set_of_ns.emplace(str(p.ns), id);
   return id;
+}
+
+// Apply the pending records of batch-bound pods to the nodes (before a
+// reader: class creation, pod removal, node deletion).
+void flush_bound(ks_ctx *c) {
+  for (auto &b : c->pending_bound) c->nodes[b.first].pod_sets.push_back(b.second);
+  c->pending_bound.clear();
 }
 
 // labels.Selector.Matches over sorted (key, value) ids.
@@ -1374,6 +1390,7 @@ ks_status class_get(ks_ctx *c, uint32_t ns, std::vector<SelReq> &&reqs, bool cre
   }
   ks_status st;
   if ((st = spread_alloc(c))) return st;
+  flush_bound(c);  // the column counts every bound pod
   int slot = -1;
   for (int k = 0; k < MAX_CLASSES && slot < 0; ++k)
     if (!c->classes[k].live) slot = k;
@@ -1585,6 +1602,7 @@ ks_status solo_compile(ks_ctx *c, const ks_pod &p, PodDev &d, ProgBuf &cl, bool 
 ks_status spread_pods_delta(ks_ctx *c, const ks_pod *pods, const uint32_t *slots, uint32_t n, int sign) {
   std::vector<uint64_t> idx;
   std::vector<int32_t> dv;
+  if (sign < 0) flush_bound(c);
   for (uint32_t i = 0; i < n; ++i) {
     const uint32_t set = intern_set(c, pods[i]);
     HostNode &h = c->nodes[slots[i]];
@@ -2096,10 +2114,13 @@ ks_status run_batch(ks_ctx *c, ks_batch *b) {
   }
   HIPC(c, hipStreamSynchronize(c->stream));
   {
-    // NodeInfo.Pods of the nodes this batch bound pods to (later selector classes count them)
+    // NodeInfo.Pods of the nodes this batch bound pods to (later selector
+    // classes count them): appended to a log, applied when read
     std::lock_guard<std::mutex> g(c->mu);
+    if (c->pending_bound.size() > (1u << 24)) flush_bound(c);
     for (uint32_t i = 0; i < b->n; ++i)
-      if (b->h_results[i].status == KS_POD_SCHEDULED) c->nodes[b->h_results[i].node_index].pod_sets.push_back(b->set_ids[i]);
+      if (b->h_results[i].status == KS_POD_SCHEDULED)
+        c->pending_bound.emplace_back((uint32_t)b->h_results[i].node_index, b->set_ids[i]);
   }
   if (c->timing) {
     ks_status st = collect_timing(c);
@@ -2559,6 +2580,7 @@ ks_status ks_nodes_delete(ks_ctx *c, const uint32_t *slots, uint32_t n) {
   if (!c || (n && !slots)) return KS_ERR_INVALID;
   if (ks_status dst_ = drain_async(c)) return dst_;
   HIPC(c, hipSetDevice(c->cfg.device));
+  flush_bound(c);  // the deleted nodes' records go with them
   std::vector<uint32_t> pos(n);
   std::vector<int64_t> core((size_t)n * 8, 0);
   for (uint32_t i = 0; i < n; ++i) {
