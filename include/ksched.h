@@ -204,6 +204,29 @@ typedef struct {
   int32_t node_taints_policy;   /* KS_INCLUSION_*                            */
 } ks_spread_constraint;
 
+/* v1.PodAffinityTerm / WeightedPodAffinityTerm (InterPodAffinity plugin,
+ * upstream pkg/scheduler/framework/plugins/interpodaffinity).  namespaces
+ * empty and namespace_selector nil = the pod's own namespace.  A
+ * namespace_selector is matched against the labels of a pod's namespace,
+ * which every ks_pod carries (namespace_labels).  matchLabelKeys /
+ * mismatchLabelKeys are merged into labelSelector by the apiserver (v1.31). */
+enum {
+  KS_POD_AFFINITY_REQUIRED = 0,       /* podAffinity.requiredDuringScheduling...      */
+  KS_POD_ANTI_AFFINITY_REQUIRED = 1,  /* podAntiAffinity.requiredDuringScheduling...  */
+  KS_POD_AFFINITY_PREFERRED = 2,      /* podAffinity.preferredDuringScheduling...     */
+  KS_POD_ANTI_AFFINITY_PREFERRED = 3  /* podAntiAffinity.preferredDuringScheduling... */
+};
+typedef struct {
+  ks_label_selector selector;            /* labelSelector (is_nil: matches no pod)  */
+  ks_label_selector namespace_selector;  /* is_nil: the field is not set            */
+  const char *const *namespaces;
+  const char *topology_key;
+  uint32_t n_namespaces;
+  int32_t kind;                          /* KS_POD_*AFFINITY_*                      */
+  int32_t weight;                        /* preferred terms: 1..100                 */
+  int32_t _pad;
+} ks_pod_affinity_term;
+
 /* Pod features whose plugins ksched does not model.
  * The caller sets the bit when the pod carries the feature; a pod with any
  * bit set is refused with KS_ERR_UNSUPPORTED (ks_pods_check names it) and
@@ -214,10 +237,11 @@ enum {
   KS_UNMODELLED_TOPOLOGY_SPREAD = 2u,  /* PodTopologySpread constraints the caller could not express
                                           as ks_pod.spread (ksched models the plugin itself: pass the
                                           pod's constraints, or its system-default ones, there)      */
-  KS_UNMODELLED_POD_AFFINITY = 4u,     /* InterPodAffinity: podAffinity / podAntiAffinity terms.  On
-                                          a pod bound through ks_pods_add / KS_EV_POD_ADD it makes
-                                          every later batch refuse until that pod is removed
-                                          (existing pods' terms filter and score the incoming pod) */
+  KS_UNMODELLED_POD_AFFINITY = 4u,     /* InterPodAffinity terms the caller could not express as
+                                          ks_pod.affinity_terms.  On a pod bound through ks_pods_add /
+                                          KS_EV_POD_ADD it makes every later batch refuse until that
+                                          pod is removed (existing pods' terms filter and score the
+                                          incoming pod)                                             */
   KS_UNMODELLED_VOLUMES = 8u,          /* VolumeBinding / VolumeRestrictions / VolumeZone /
                                           NodeVolumeLimits: PVC, ephemeral or CSI volumes           */
   KS_UNMODELLED_NOMINATED_NODE = 16u,  /* status.nominatedNodeName (evaluateNominatedNode)          */
@@ -265,6 +289,12 @@ typedef struct {
   uint32_t n_spread;
   uint32_t spread_defaulted;
   uint32_t _pad2;
+  /* InterPodAffinity: the pod's pod (anti-)affinity terms, and the labels of
+   * its namespace (namespace selectors of other pods' terms match them). */
+  const ks_pod_affinity_term *affinity_terms;
+  const ks_label *namespace_labels;
+  uint32_t n_affinity_terms;
+  uint32_t n_namespace_labels;
 } ks_pod;
 
 /* ------------------------------------------------------------- outputs */
@@ -276,7 +306,8 @@ enum {
   KS_PLUGIN_NODE_AFFINITY = 3,
   KS_PLUGIN_NODE_RESOURCES_FIT = 4,
   KS_PLUGIN_POD_TOPOLOGY_SPREAD = 5,
-  KS_NUM_FILTER_PLUGINS = 6
+  KS_PLUGIN_INTER_POD_AFFINITY = 6,
+  KS_NUM_FILTER_PLUGINS = 7
 };
 
 enum {
@@ -304,6 +335,7 @@ typedef struct {
   uint32_t fail_counts[KS_NUM_FAIL_COUNTS]; /* nodes rejected first by each filter plugin, then
                                                nodes excluded by the PreFilterResult */
   uint32_t flags;         /* KS_RESULT_*                                         */
+  uint32_t _pad;
 } ks_result;
 
 /* Per-node plugin scores of one pod (parity dump; NodePluginScores analogue). */
@@ -318,6 +350,8 @@ typedef struct {
   int32_t image_locality;       /* ImageLocality (0: nodes report no images) */
   int32_t spread_raw;           /* PodTopologySpread raw (0 when its PreScore skips) */
   int32_t spread_score;         /* PodTopologySpread normalized          */
+  int32_t affinity_pod_raw;     /* InterPodAffinity raw (0 when its PreScore skips) */
+  int32_t affinity_pod_score;   /* InterPodAffinity normalized           */
   int64_t total_score;          /* Σ weight × score over non-skipped plugins */
 } ks_node_score;
 
@@ -355,6 +389,8 @@ typedef struct {
    * dependent (schedule_one.go#numFeasibleNodesToFind / findNodesThatPassFilters). */
   int32_t percentage_of_nodes_to_score;
   int32_t weight_topology_spread; /* PodTopologySpread (default profile: 2)     */
+  int32_t weight_inter_pod_affinity; /* InterPodAffinity (default profile: 2)    */
+  int32_t hard_pod_affinity_weight;  /* InterPodAffinityArgs.hardPodAffinityWeight (1) */
 } ks_config;
 
 typedef struct ks_ctx ks_ctx;

@@ -10,7 +10,8 @@ namespace ks {
 constexpr int LW = 4;           // label bitset words per node (256 dictionary bits)
 constexpr int NNUM = 2;         // numeric label columns (Gt / Lt operands)
 constexpr int NFILT = 5;        // filter plugins of the round kernels (KS_PLUGIN_* 0..4)
-constexpr int PLUGIN_SPREAD = 5;  // KS_PLUGIN_POD_TOPOLOGY_SPREAD (spread path only)
+constexpr int PLUGIN_SPREAD = 5;  // KS_PLUGIN_POD_TOPOLOGY_SPREAD (one-pod path only)
+constexpr int PLUGIN_IPA = 6;     // KS_PLUGIN_INTER_POD_AFFINITY (one-pod path only)
 constexpr int WAVE = 64;
 constexpr int SWEEP_THREADS = 256;
 constexpr int BLOCK_KEYS = 4;   // candidates kept per sweep block and pod
@@ -23,7 +24,7 @@ constexpr int ST_FEASIBLE = -1;
 constexpr int ST_EMPTY = -2;
 // Outside NodeAffinity's PreFilterResult: no Filter plugin runs on the node
 // and no plugin is blamed (ks_result.fail_counts[KS_FAIL_PREFILTER_RESULT]).
-constexpr int ST_PREFILTERED = 6;
+constexpr int ST_PREFILTERED = 7;
 
 // ---------------------------------------------------------- node table (SoA)
 // Columns are indexed by POSITION, not slot: a shard's slots are permuted so
@@ -260,10 +261,12 @@ struct DevResult {
   uint32_t evaluated_nodes;
   uint32_t fail_counts[NFILT];
   uint32_t spread_fail;  // ks_result.fail_counts[KS_PLUGIN_POD_TOPOLOGY_SPREAD]
+  uint32_t ipa_fail;     // ks_result.fail_counts[KS_PLUGIN_INTER_POD_AFFINITY]
   uint32_t prefiltered;  // ks_result.fail_counts[KS_FAIL_PREFILTER_RESULT]
   uint32_t flags;
+  uint32_t _pad;
 };
-static_assert(sizeof(DevResult) == 56, "DevResult layout");
+static_assert(sizeof(DevResult) == 64, "DevResult layout");
 
 struct Weights {
   int32_t fit, ba, tt, na, il;

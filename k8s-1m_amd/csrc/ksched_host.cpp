@@ -835,6 +835,9 @@ bool prefilter_names(const ks_pod &p, std::vector<std::string> *names) {
 // default profile would filter or score with a plugin ksched does not model is
 // refused, never scheduled approximately.
 ks_status check_modelled(ks_ctx *c, const ks_pod &p) {
+  if (p.n_affinity_terms)
+    return c->fail(KS_ERR_UNSUPPORTED, "pod %s/%s carries pod (anti-)affinity terms (InterPodAffinity)",
+                   str(p.ns).c_str(), str(p.name).c_str());
   if (p.unmodelled)
     return c->fail(KS_ERR_UNSUPPORTED, "pod %s/%s carries %s", str(p.ns).c_str(), str(p.name).c_str(),
                    unmodelled_name(p.unmodelled));
@@ -2183,6 +2186,8 @@ void ks_config_default(ks_config *cfg) {
   cfg->weight_affinity = 2;
   cfg->weight_image = 1;
   cfg->weight_topology_spread = 2;
+  cfg->weight_inter_pod_affinity = 2;
+  cfg->hard_pod_affinity_weight = 1;
   cfg->percentage_of_nodes_to_score = 100;
 }
 
@@ -2210,7 +2215,7 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
   if (c->S > (uint32_t)MAX_SHARDS) return KS_ERR_INVALID;
   // weights are small non-negative integers (the kernels add them in 32 bits)
   for (int32_t w : {cfg->weight_fit, cfg->weight_balanced, cfg->weight_taint, cfg->weight_affinity, cfg->weight_image,
-                    cfg->weight_topology_spread})
+                    cfg->weight_topology_spread, cfg->weight_inter_pod_affinity, cfg->hard_pod_affinity_weight})
     if (w < 0 || w > 10000) return KS_ERR_INVALID;
   // percentageOfNodesToScore (ksched.h): only 100 (every node) is modelled
   if (cfg->percentage_of_nodes_to_score < 0 || cfg->percentage_of_nodes_to_score > 100) return KS_ERR_INVALID;
@@ -3038,6 +3043,8 @@ ks_status ks_plugin_scores(ks_ctx *c, const ks_pod *pod, ks_node_score *out) {
     s.image_locality = o[7];
     s.spread_raw = 0;
     s.spread_score = 0;
+    s.affinity_pod_raw = 0;
+    s.affinity_pod_score = 0;
     s.total_score = (int64_t)(((uint64_t)(uint32_t)o[9] << 32) | (uint32_t)o[8]);
     out[i] = s;
   }

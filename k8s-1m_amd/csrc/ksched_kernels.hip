@@ -1551,6 +1551,8 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
             res->flags = (win && feasible == 1) ? 1u : 0u;
             res->prefiltered = s_pod[r].prefilter_out;
             res->spread_fail = 0;
+            res->ipa_fail = 0;
+            res->_pad = 0;
           }
           if (lane > (uint32_t)DSUM_LANE && lane <= (uint32_t)DSUM_LANE + NFILT)
             res->fail_counts[lane - DSUM_LANE - 1] = hfail + (uint32_t)vd;

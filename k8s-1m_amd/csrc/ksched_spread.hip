@@ -593,6 +593,8 @@ __global__ void spread_commit_kernel(SpreadArgs a) {
   r.evaluated_nodes = a.evaluated;
   for (int q = 0; q < NFILT; ++q) r.fail_counts[q] = tot.fail[q];
   r.spread_fail = tot.fail[PLUGIN_SPREAD];
+  r.ipa_fail = 0;
+  r._pad = 0;
   r.prefiltered = p.prefilter_out;
   r.flags = 0;
   if (tot.feasible > 0) {

@@ -115,6 +115,19 @@ class KsSpreadConstraint(C.Structure):
     ]
 
 
+class KsPodAffinityTerm(C.Structure):
+    _fields_ = [
+        ("selector", KsLabelSelector),
+        ("namespace_selector", KsLabelSelector),
+        ("namespaces", C.POINTER(c_char_p)),
+        ("topology_key", c_char_p),
+        ("n_namespaces", C.c_uint32),
+        ("kind", C.c_int32),
+        ("weight", C.c_int32),
+        ("_pad", C.c_int32),
+    ]
+
+
 class KsPod(C.Structure):
     _fields_ = [
         ("ns", c_char_p),
@@ -144,11 +157,15 @@ class KsPod(C.Structure):
         ("n_spread", C.c_uint32),
         ("spread_defaulted", C.c_uint32),
         ("_pad2", C.c_uint32),
+        ("affinity_terms", C.POINTER(KsPodAffinityTerm)),
+        ("namespace_labels", C.POINTER(KsLabel)),
+        ("n_affinity_terms", C.c_uint32),
+        ("n_namespace_labels", C.c_uint32),
     ]
 
 
-NUM_FILTER_PLUGINS = 6
-NUM_FAIL_COUNTS = 7  # + KS_FAIL_PREFILTER_RESULT
+NUM_FILTER_PLUGINS = 7
+NUM_FAIL_COUNTS = 8  # + KS_FAIL_PREFILTER_RESULT
 # ks_status codes and ks_event kinds (include/ksched.h)
 KS_OK, KS_ERR_INVALID, KS_ERR_DEVICE, KS_ERR_CAPACITY, KS_ERR_UNSUPPORTED, KS_ERR_RANGE = 0, 1, 2, 3, 4, 5
 KS_ERR_NOT_FOUND, KS_ERR_COMM, KS_ERR_STALE = 6, 7, 8
@@ -176,6 +193,7 @@ class KsResult(C.Structure):
         ("evaluated_nodes", C.c_uint32),
         ("fail_counts", C.c_uint32 * NUM_FAIL_COUNTS),
         ("flags", C.c_uint32),
+        ("_pad", C.c_uint32),
     ]
 
 
@@ -191,6 +209,8 @@ class KsNodeScore(C.Structure):
         ("image_locality", C.c_int32),
         ("spread_raw", C.c_int32),
         ("spread_score", C.c_int32),
+        ("affinity_pod_raw", C.c_int32),
+        ("affinity_pod_score", C.c_int32),
         ("total_score", C.c_int64),
     ]
 
@@ -225,6 +245,8 @@ class KsConfig(C.Structure):
         ("weight_image", C.c_int32),
         ("percentage_of_nodes_to_score", C.c_int32),
         ("weight_topology_spread", C.c_int32),
+        ("weight_inter_pod_affinity", C.c_int32),
+        ("hard_pod_affinity_weight", C.c_int32),
     ]
 
 
@@ -248,8 +270,8 @@ class KsStats(C.Structure):
 EXPECTED_SIZES = {
     "ks_label": 16, "ks_taint": 24, "ks_toleration": 24, "ks_node": 88, "ks_container": 48,
     "ks_resource": 16, "ks_image": 16,
-    "ks_requirement": 24, "ks_term": 24, "ks_preferred_term": 32, "ks_pod": 160, "ks_event": 24, "ks_result": 56,
-    "ks_node_score": 48, "ks_node_state": 56, "ks_config": 60, "ks_stats": 88, "ks_label_selector": 32,
+    "ks_requirement": 24, "ks_term": 24, "ks_preferred_term": 32, "ks_pod": 184, "ks_event": 24, "ks_result": 64,
+    "ks_node_score": 56, "ks_node_state": 56, "ks_config": 68, "ks_pod_affinity_term": 96, "ks_stats": 88, "ks_label_selector": 32,
     "ks_spread_constraint": 72,
 }
 STRUCTS = {
@@ -258,7 +280,7 @@ STRUCTS = {
     "ks_preferred_term": KsPreferredTerm, "ks_pod": KsPod, "ks_event": KsEvent, "ks_result": KsResult,
     "ks_node_score": KsNodeScore, "ks_node_state": KsNodeState, "ks_config": KsConfig,
     "ks_stats": KsStats, "ks_label_selector": KsLabelSelector, "ks_spread_constraint": KsSpreadConstraint,
-    "ks_resource": KsResource, "ks_image": KsImage,
+    "ks_resource": KsResource, "ks_image": KsImage, "ks_pod_affinity_term": KsPodAffinityTerm,
 }
 
 KSCHED_SYMBOLS = [

@@ -28,7 +28,7 @@ from . import _abi
 from .objects import Arena, Node, Pod, nodes_array, pods_array
 
 FILTER_PLUGINS = ["NodeUnschedulable", "NodeName", "TaintToleration", "NodeAffinity", "NodeResourcesFit",
-                  "PodTopologySpread"]
+                  "PodTopologySpread", "InterPodAffinity"]
 NODE_PLUGIN_SCORES_STATE_KEY = "NodePluginScores"  # fork: framework.NodePluginScoresStateKey
 DEFAULT_WEIGHTS = {  # apis/config/v1 default plugin weights (v1.31)
     "NodeResourcesFit": 1,
@@ -37,6 +37,7 @@ DEFAULT_WEIGHTS = {  # apis/config/v1 default plugin weights (v1.31)
     "NodeAffinity": 2,
     "ImageLocality": 1,
     "PodTopologySpread": 2,
+    "InterPodAffinity": 2,
 }
 
 
@@ -135,6 +136,8 @@ class Scheduler:
         cfg.weight_affinity = w["NodeAffinity"]
         cfg.weight_image = w["ImageLocality"]
         cfg.weight_topology_spread = w["PodTopologySpread"]
+        cfg.weight_inter_pod_affinity = w["InterPodAffinity"]
+        cfg.hard_pod_affinity_weight = 1
         self.weights = w
         self.capacity = node_capacity
         self.ctx = C.c_void_p()
@@ -220,7 +223,7 @@ class Scheduler:
                 out.append(ScheduleResult(self.names.get(r.node_index, str(r.node_index)), r.evaluated_nodes,
                                           r.feasible_nodes, r.node_index, r.total_score, bool(r.flags & 1)))
             elif r.status == 1:
-                counts = {FILTER_PLUGINS[k]: int(r.fail_counts[k]) for k in range(6) if r.fail_counts[k]}
+                counts = {FILTER_PLUGINS[k]: int(r.fail_counts[k]) for k in range(7) if r.fail_counts[k]}
                 out.append(FitError(f"pod#{i}", r.evaluated_nodes, Diagnosis(counts, set(counts))))
             else:
                 out.append(FrameworkError(f"pod#{i}: plugin Error status"))
@@ -317,5 +320,5 @@ def results_to_arrays(raw, n: int):
 
     buf = np.frombuffer(C.string_at(C.addressof(raw), n * C.sizeof(_abi.KsResult)), dtype=np.uint8)
     dt = np.dtype([("node_index", "<i4"), ("status", "<i4"), ("total_score", "<i8"), ("feasible", "<u4"),
-                   ("evaluated", "<u4"), ("fail", "<u4", (7,)), ("flags", "<u4")])
+                   ("evaluated", "<u4"), ("fail", "<u4", (8,)), ("flags", "<u4"), ("_pad", "<u4")])
     return buf.view(dt)

@@ -87,6 +87,19 @@ class TopologySpreadConstraint:
     match_label_keys: List[str] = field(default_factory=list)
 
 
+@dataclass
+class PodAffinityTerm:
+    topology_key: str
+    label_selector: Optional[LabelSelector] = None  # None = nil (matches no pod)
+    namespaces: List[str] = field(default_factory=list)
+    namespace_selector: Optional[LabelSelector] = None  # None = not set
+    kind: str = "affinity"  # affinity / anti-affinity (required) or preferred-affinity / preferred-anti-affinity
+    weight: int = 0  # preferred terms
+
+
+AFF_KINDS = {"affinity": 0, "anti-affinity": 1, "preferred-affinity": 2, "preferred-anti-affinity": 3}
+
+
 # PodTopologySpread's system-default constraints (upstream
 # podtopologyspread.systemDefaultConstraints), applied with the pod's
 # DefaultSelector when it has no constraints of its own.
@@ -127,6 +140,8 @@ class Pod:
     labels: Dict[str, str] = field(default_factory=dict)
     topology_spread: List[TopologySpreadConstraint] = field(default_factory=list)
     spread_defaulted: bool = False  # topology_spread holds the system defaults (see ksched.h ks_pod)
+    affinity_terms: List[PodAffinityTerm] = field(default_factory=list)
+    namespace_labels: Dict[str, str] = field(default_factory=dict)
 
 
 class Arena:
@@ -195,6 +210,12 @@ def _spread(c: TopologySpreadConstraint, a: Arena) -> _abi.KsSpreadConstraint:
                                    POLICY.get(c.node_affinity_policy, 9), POLICY.get(c.node_taints_policy, 9))
 
 
+def _aff_term(t: PodAffinityTerm, a: Arena) -> _abi.KsPodAffinityTerm:
+    ns, nns = a.array(C.c_char_p, [a.s(x) for x in t.namespaces])
+    return _abi.KsPodAffinityTerm(_selector(t.label_selector, a), _selector(t.namespace_selector, a), ns,
+                                  a.s(t.topology_key), nns, AFF_KINDS.get(t.kind, 9), t.weight, 0)
+
+
 def node_to_c(n: Node, a: Arena) -> _abi.KsNode:
     labels, nl = a.array(_abi.KsLabel, [_abi.KsLabel(a.s(k), a.s(v)) for k, v in n.labels.items()])
     taints, nt = a.array(
@@ -219,12 +240,14 @@ def pod_to_c(p: Pod, a: Arena) -> _abi.KsPod:
     ov = p.overhead or {}
     labels, nlab = a.array(_abi.KsLabel, [_abi.KsLabel(a.s(k), a.s(v)) for k, v in p.labels.items()])
     spread, nsp = a.array(_abi.KsSpreadConstraint, [_spread(c, a) for c in p.topology_spread])
+    terms, nterm = a.array(_abi.KsPodAffinityTerm, [_aff_term(t, a) for t in p.affinity_terms])
+    nsl, nnsl = a.array(_abi.KsLabel, [_abi.KsLabel(a.s(k), a.s(v)) for k, v in p.namespace_labels.items()])
     return _abi.KsPod(
         a.s(p.namespace), a.s(p.name), cs, ics, tols, sel, req, pref, a.s(p.node_name),
         ov.get("cpu", 0), ov.get("memory", 0), ncs, nics, ntol, nsel, nreq,
         0 if p.required_terms is None else 1, npref, 0 if p.preferred is None else 1,
         0 if p.overhead is None else 1, sum(_abi.UNMODELLED[u] for u in p.unmodelled),
-        labels, spread, nlab, nsp, 1 if p.spread_defaulted else 0, 0)
+        labels, spread, nlab, nsp, 1 if p.spread_defaulted else 0, 0, terms, nsl, nterm, nnsl)
 
 
 def nodes_array(nodes: List[Node], a: Arena):

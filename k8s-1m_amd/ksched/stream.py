@@ -120,7 +120,7 @@ class BurstStream:
     def record(self, b, results):
         """Bind the scheduled pods of burst b (AssumePod -> bound)."""
         r = np.frombuffer(C.string_at(C.addressof(results), self.burst * C.sizeof(_abi.KsResult)),
-                          dtype=np.dtype([("node_index", "<i4"), ("status", "<i4"), ("rest", "V48")]))
+                          dtype=np.dtype([("node_index", "<i4"), ("status", "<i4"), ("rest", f"V{C.sizeof(_abi.KsResult) - 8}")]))
         ok = np.nonzero(r["status"] == 0)[0]
         self.bound_pod = np.concatenate([self.bound_pod, b * self.burst + ok])
         self.bound_slot = np.concatenate([self.bound_slot, r["node_index"][ok].astype(np.int64)])

@@ -44,6 +44,8 @@ struct Toleration {
   int32_t op, effect;
 };
 
+struct AffTerm;  // interpodaffinity term of a bound pod (defined below)
+
 struct Node {
   bool present = false;
   std::string name;
@@ -62,8 +64,10 @@ struct Node {
   // NodeInfo.Pods' namespace and labels (PodTopologySpread counts them)
   struct PodRec {
     std::string ns;
-    std::map<std::string, std::string> labels;
-    bool operator==(const PodRec &o) const { return ns == o.ns && labels == o.labels; }
+    std::map<std::string, std::string> labels, ns_labels;
+    std::vector<AffTerm> terms;  // the pod's pod (anti-)affinity terms
+    std::string key;             // identity for RemovePod
+    bool operator==(const PodRec &o) const { return key == o.key; }
   };
   std::vector<PodRec> pod_recs;
 };
@@ -361,6 +365,36 @@ struct SpreadConstraint {
   bool hostname = false;  // topologyKey == v1.LabelHostname (scoring counts per node)
 };
 
+// interpodaffinity: framework.AffinityTerm (framework/types.go#newAffinityTerm)
+struct AffTerm {
+  int32_t kind = 0;    // KS_POD_*AFFINITY_*
+  int64_t weight = 0;  // preferred terms
+  std::set<std::string> namespaces;
+  Selector ns_sel;     // NamespaceSelector (nil -> Nothing())
+  Selector sel;
+  std::string key;
+  // AffinityTerm.Matches(pod, nsLabels): namespace listed or selected, then the selector
+  bool Matches(const std::string &ns, const std::map<std::string, std::string> &labels,
+               const std::map<std::string, std::string> &ns_labels) const {
+    if (!namespaces.count(ns) && !ns_sel.Match(ns_labels)) return false;
+    return sel.Match(labels);
+  }
+};
+
+// newAffinityTerm for one of pod p's terms; false on a selector parse error.
+bool NewAffinityTerm(const ks_pod &p, const ks_pod_affinity_term &t, AffTerm *out) {
+  AffTerm a;
+  a.kind = t.kind;
+  a.weight = t.weight;
+  a.key = S(t.topology_key);
+  for (uint32_t i = 0; i < t.n_namespaces; ++i) a.namespaces.insert(S(t.namespaces[i]));
+  if (a.namespaces.empty() && t.namespace_selector.is_nil) a.namespaces.insert(S(p.ns));
+  if (!LabelSelectorAsSelector(t.selector, &a.sel) || !LabelSelectorAsSelector(t.namespace_selector, &a.ns_sel))
+    return false;
+  *out = a;
+  return true;
+}
+
 // ------------------------------------------------------------ pod state
 
 struct PodState {
@@ -396,6 +430,10 @@ struct PodState {
   std::map<std::string, int64_t> xreq;
   std::vector<std::string> images;  // normalised, init containers then containers ("" = none)
   int64_t n_containers = 0;
+  // InterPodAffinity: the pod's terms by kind, its namespace's labels
+  std::vector<AffTerm> ipa[4];
+  std::map<std::string, std::string> ns_labels;
+  bool ipa_error = false;  // a term's selector failed to parse (the product refuses the pod)
 };
 
 // v1helper.IsScalarResourceName (extended, hugepages-, attachable-volumes-,
@@ -564,6 +602,13 @@ PodState compile_pod(const ks_pod &p) {
     st.images.push_back(p.containers[i].image && p.containers[i].image[0]
                             ? NormalizedImageName(S(p.containers[i].image)) : std::string());
   st.n_containers = (int64_t)p.n_init_containers + p.n_containers;
+  for (uint32_t i = 0; i < p.n_namespace_labels; ++i)
+    st.ns_labels[S(p.namespace_labels[i].key)] = S(p.namespace_labels[i].value);
+  for (uint32_t i = 0; i < p.n_affinity_terms; ++i) {
+    AffTerm a;
+    if (!NewAffinityTerm(p, p.affinity_terms[i], &a) || a.kind < 0 || a.kind > 3) st.ipa_error = true;
+    else st.ipa[a.kind].push_back(a);
+  }
   st.ns = S(p.ns);
   for (uint32_t i = 0; i < p.n_labels; ++i) st.labels[S(p.labels[i].key)] = S(p.labels[i].value);
   // podtopologyspread/common.go#filterTopologySpreadConstraints, per action
@@ -831,6 +876,76 @@ bool SpreadFilter(const PodState &st, const SpreadFilterState &s, const Node &n)
   return true;
 }
 
+// interpodaffinity/filtering.go#PreFilter: existingAntiAffinityCounts (the
+// existing pods' required anti-affinity terms the incoming pod matches),
+// affinityCounts (existing pods matching ALL the incoming pod's required
+// affinity terms, per term's topology pair) and antiAffinityCounts.
+using TopoPair = std::pair<std::string, std::string>;
+struct IpaFilterState {
+  bool active = false;
+  std::map<TopoPair, int64_t> existing_anti, aff, anti;
+};
+
+IpaFilterState IpaPreFilter(const PodState &st, const std::vector<Node> &nodes) {
+  IpaFilterState s;
+  const auto &req_aff = st.ipa[KS_POD_AFFINITY_REQUIRED], &req_anti = st.ipa[KS_POD_ANTI_AFFINITY_REQUIRED];
+  for (auto &n : nodes) {
+    if (!n.present) continue;
+    for (auto &e : n.pod_recs) {
+      for (auto &t : e.terms) {  // updateWithAntiAffinityTerms(existing terms, incoming pod)
+        if (t.kind != KS_POD_ANTI_AFFINITY_REQUIRED || !t.Matches(st.ns, st.labels, st.ns_labels)) continue;
+        auto it = n.labels.find(t.key);
+        if (it != n.labels.end()) s.existing_anti[{t.key, it->second}] += 1;
+      }
+      bool all = !req_aff.empty();  // podMatchesAllAffinityTerms (merged namespaces)
+      for (auto &t : req_aff) all = all && t.Matches(e.ns, e.labels, e.ns_labels);
+      if (all)
+        for (auto &t : req_aff) {
+          auto it = n.labels.find(t.key);
+          if (it != n.labels.end()) s.aff[{t.key, it->second}] += 1;
+        }
+      for (auto &t : req_anti) {
+        if (!t.Matches(e.ns, e.labels, e.ns_labels)) continue;
+        auto it = n.labels.find(t.key);
+        if (it != n.labels.end()) s.anti[{t.key, it->second}] += 1;
+      }
+    }
+  }
+  s.active = !(s.existing_anti.empty() && req_aff.empty() && req_anti.empty());  // else PreFilter Skip
+  return s;
+}
+
+// filtering.go#Filter: satisfyPodAffinity, satisfyPodAntiAffinity, satisfyExistingPodsAntiAffinity
+bool IpaFilter(const PodState &st, const IpaFilterState &s, const Node &n) {
+  const auto &req_aff = st.ipa[KS_POD_AFFINITY_REQUIRED];
+  bool exist = true;
+  for (auto &t : req_aff) {
+    auto it = n.labels.find(t.key);
+    if (it == n.labels.end()) return false;  // all topology labels must exist on the node
+    auto c = s.aff.find({t.key, it->second});
+    if (c == s.aff.end() || c->second <= 0) exist = false;
+  }
+  if (!exist) {
+    // the first pod of a series with affinity to itself
+    bool self = !req_aff.empty();
+    for (auto &t : req_aff) self = self && t.Matches(st.ns, st.labels, st.ns_labels);
+    if (!(s.aff.empty() && self)) return false;
+  }
+  if (!s.anti.empty())
+    for (auto &t : st.ipa[KS_POD_ANTI_AFFINITY_REQUIRED]) {
+      auto it = n.labels.find(t.key);
+      if (it == n.labels.end()) continue;
+      auto c = s.anti.find({t.key, it->second});
+      if (c != s.anti.end() && c->second > 0) return false;
+    }
+  if (!s.existing_anti.empty())
+    for (auto &kv : n.labels) {
+      auto c = s.existing_anti.find({kv.first, kv.second});
+      if (c != s.existing_anti.end() && c->second > 0) return false;
+    }
+  return true;
+}
+
 inline uint64_t PackKey(int64_t total, uint32_t slot) {
   return ((uint64_t)(total + 1) << 32) | (uint64_t)(0xFFFFFFFFu - slot);
 }
@@ -877,7 +992,7 @@ struct oracle {
     else if (sum > maxT) sum = maxT;
     return kMaxNodeScore * (sum - minT) / (maxT - minT);
   }
-  int64_t w_fit, w_ba, w_tt, w_na, w_il, w_pts = 2;
+  int64_t w_fit, w_ba, w_tt, w_na, w_il, w_pts = 2, w_ipa = 2, hard_weight = 1;
   int threads = 1;
 
   struct Eval {
@@ -885,15 +1000,18 @@ struct oracle {
     int64_t la, ba, tt_raw, na_raw;
     int64_t pts_raw, pts;  // PodTopologySpread raw / normalized (ScheduleAnyway constraints)
     int64_t il;            // ImageLocality
+    int64_t ipa_raw, ipa;  // InterPodAffinity raw / normalized
   };
   std::vector<Eval> ev;  // per-node scratch, reused across pods
 
-  Eval eval(const PodState &st, const Node &n, const SpreadFilterState *sf = nullptr) const {
+  Eval eval(const PodState &st, const Node &n, const SpreadFilterState *sf = nullptr,
+            const IpaFilterState *af = nullptr) const {
     Eval e{};
     e.status = Filter(st, n);
     // PodTopologySpread.Filter follows NodeResourcesFit in the default profile
     if (e.status < 0 && sf && !st.spread_filter.empty() && !SpreadFilter(st, *sf, n))
       e.status = KS_PLUGIN_POD_TOPOLOGY_SPREAD;
+    if (e.status < 0 && af && af->active && !IpaFilter(st, *af, n)) e.status = KS_PLUGIN_INTER_POD_AFFINITY;
     if (e.status >= 0) return e;
     e.la = LeastAllocated(n.alloc_cpu, n.alloc_mem, n.nz_cpu, n.nz_mem, st.nz_cpu, st.nz_mem);
     e.ba = BalancedAllocation(n.alloc_cpu, n.alloc_mem, n.req_cpu, n.req_mem, st.req_cpu, st.req_mem);
@@ -910,6 +1028,7 @@ struct oracle {
     int64_t t = w_fit * e.la + w_ba * e.ba + w_tt * Normalize(e.tt_raw, tt_max, true) + w_il * e.il;
     if (st.has_preferred) t += w_na * Normalize(e.na_raw, na_max, false);
     if (!st.spread_score.empty()) t += w_pts * e.pts;  // PreScore Skip without ScheduleAnyway constraints
+    t += w_ipa * e.ipa;  // 0 when its PreScore skips (no topology score at all)
     return t;
   }
 
@@ -917,6 +1036,14 @@ struct oracle {
     Node::PodRec rec;
     rec.ns = S(p.ns);
     for (uint32_t k = 0; k < p.n_labels; ++k) rec.labels[S(p.labels[k].key)] = S(p.labels[k].value);
+    for (uint32_t k = 0; k < p.n_namespace_labels; ++k)
+      rec.ns_labels[S(p.namespace_labels[k].key)] = S(p.namespace_labels[k].value);
+    rec.key = rec.ns + "\x01" + S(p.name);
+    for (auto &kv : rec.labels) rec.key += "\x01" + kv.first + "=" + kv.second;
+    for (uint32_t k = 0; k < p.n_affinity_terms; ++k) {
+      AffTerm a;
+      if (NewAffinityTerm(p, p.affinity_terms[k], &a)) rec.terms.push_back(a);
+    }
     if (sign > 0) {
       n.pod_recs.push_back(std::move(rec));
     } else {
@@ -1027,6 +1154,58 @@ struct oracle {
     }
   }
 
+  // InterPodAffinity PreScore / Score / NormalizeScore (scoring.go) over the
+  // feasible nodes: topologyScore[key][value] from the incoming pod's
+  // preferred terms against existing pods and the existing pods' required
+  // (hardPodAffinityWeight) and preferred terms against the incoming pod;
+  // min-max normalised in float64.  Fills ev[i].ipa_raw / ev[i].ipa.
+  void ipa_score(const PodState &st, std::vector<Eval> &ev) const {
+    std::map<std::string, std::map<std::string, int64_t>> ts;
+    const uint32_t N = (uint32_t)nodes.size();
+    for (uint32_t i = 0; i < N; ++i) {
+      const Node &n = nodes[i];
+      if (!n.present || n.labels.empty()) continue;
+      auto add = [&](const AffTerm &t, int64_t w) {
+        auto it = n.labels.find(t.key);
+        if (it != n.labels.end()) ts[t.key][it->second] += w;
+      };
+      for (auto &e : n.pod_recs) {
+        for (auto &t : st.ipa[KS_POD_AFFINITY_PREFERRED])
+          if (t.Matches(e.ns, e.labels, e.ns_labels)) add(t, t.weight);
+        for (auto &t : st.ipa[KS_POD_ANTI_AFFINITY_PREFERRED])
+          if (t.Matches(e.ns, e.labels, e.ns_labels)) add(t, -t.weight);
+        for (auto &t : e.terms) {
+          if (!t.Matches(st.ns, st.labels, st.ns_labels)) continue;
+          if (t.kind == KS_POD_AFFINITY_REQUIRED && hard_weight > 0) add(t, hard_weight);
+          else if (t.kind == KS_POD_AFFINITY_PREFERRED) add(t, t.weight);
+          else if (t.kind == KS_POD_ANTI_AFFINITY_PREFERRED) add(t, -t.weight);
+        }
+      }
+    }
+    if (ts.empty()) return;  // PreScore Skip: every score stays 0
+    int64_t mn = INT64_MAX, mx = INT64_MIN;
+    for (uint32_t i = 0; i < N; ++i) {
+      if (!nodes[i].present || ev[i].status >= 0) continue;
+      int64_t sc = 0;
+      for (auto &kv : ts) {
+        auto it = nodes[i].labels.find(kv.first);
+        if (it == nodes[i].labels.end()) continue;
+        auto v = kv.second.find(it->second);
+        if (v != kv.second.end()) sc += v->second;
+      }
+      ev[i].ipa_raw = sc;
+      mn = std::min(mn, sc);
+      mx = std::max(mx, sc);
+    }
+    const int64_t diff = mx - mn;
+    for (uint32_t i = 0; i < N; ++i) {
+      if (!nodes[i].present || ev[i].status >= 0) continue;
+      double f = 0;
+      if (diff > 0) f = (double)kMaxNodeScore * ((double)(ev[i].ipa_raw - mn) / (double)diff);
+      ev[i].ipa = (int64_t)f;
+    }
+  }
+
   // schedulePod (schedule_one.go): findNodesThatFitPod -> prioritizeNodes -> selectHost.
   ks_result schedule_one(const ks_pod &p) {
     ks_result r{};
@@ -1036,6 +1215,7 @@ struct oracle {
     ev.resize(N);
     SpreadFilterState sf;
     if (!st.spread_filter.empty()) sf = SpreadPreFilter(st, nodes);
+    const IpaFilterState af = IpaPreFilter(st, nodes);
     // Filter + raw scores in parallel (findNodesThatPassFilters / RunScorePlugins
     // both fan out with parallelize.Until); counts and normaliser maxima are
     // order-independent reductions, combined from per-thread partials.
@@ -1050,7 +1230,7 @@ struct oracle {
       Part &q = part[t];
       for (uint32_t i = a; i < b; ++i) {
         if (!nodes[i].present) continue;
-        ev[i] = eval(st, nodes[i], &sf);
+        ev[i] = eval(st, nodes[i], &sf, &af);
         ++q.evaluated;
         if (ev[i].status >= 0) {
           q.fail[ev[i].status]++;
@@ -1083,6 +1263,7 @@ struct oracle {
       // "When only one node after predicate, just use it." No scoring upstream;
       // the build still reports that node's TotalScore.
       spread_score(st, ev);
+      ipa_score(st, ev);
       r.flags |= KS_RESULT_SINGLE_FEASIBLE;
       r.node_index = (int32_t)only;
       r.total_score = total(st, ev[only], tt_max, na_max);
@@ -1094,6 +1275,7 @@ struct oracle {
       return r;
     }
     spread_score(st, ev);
+    ipa_score(st, ev);
     for_nodes(0, N, [&](uint32_t a, uint32_t b, int t) {
       uint64_t &best = part[t].best;
       for (uint32_t i = a; i < b; ++i) {
@@ -1126,6 +1308,10 @@ oracle *oracle_new(uint32_t cap, int32_t w_fit, int32_t w_ba, int32_t w_tt, int3
 void oracle_free(oracle *o) { delete o; }
 void oracle_set_threads(oracle *o, int32_t t) { o->threads = t < 1 ? 1 : t; }
 void oracle_set_weight_spread(oracle *o, int32_t w) { o->w_pts = w; }
+void oracle_set_weight_inter_pod_affinity(oracle *o, int32_t w, int32_t hard) {
+  o->w_ipa = w;
+  o->hard_weight = hard;
+}
 double oracle_go_log(double x) { return GoLog(x); }
 
 int32_t oracle_nodes_upsert(oracle *o, const ks_node *nodes, const uint32_t *slots, uint32_t n) {
@@ -1209,12 +1395,13 @@ int32_t oracle_plugin_scores(oracle *o, const ks_pod *pod, ks_node_score *out) {
   int64_t tt_max = 0, na_max = 0;
   SpreadFilterState sf;
   if (!st.spread_filter.empty()) sf = SpreadPreFilter(st, o->nodes);
+  const IpaFilterState af = IpaPreFilter(st, o->nodes);
   for (uint32_t i = 0; i < N; ++i) {
     if (!o->nodes[i].present) {
       ev[i].status = -2;
       continue;
     }
-    ev[i] = o->eval(st, o->nodes[i], &sf);
+    ev[i] = o->eval(st, o->nodes[i], &sf, &af);
     if (ev[i].status < 0) {
       tt_max = std::max(tt_max, ev[i].tt_raw);
       na_max = std::max(na_max, ev[i].na_raw);
@@ -1222,7 +1409,10 @@ int32_t oracle_plugin_scores(oracle *o, const ks_pod *pod, ks_node_score *out) {
   }
   for (uint32_t i = 0; i < N; ++i) {
     ks_node_score s{};
-    if (i == 0) o->spread_score(st, ev);  // PodTopologySpread over the feasible set
+    if (i == 0) {  // PodTopologySpread and InterPodAffinity over the feasible set
+      o->spread_score(st, ev);
+      o->ipa_score(st, ev);
+    }
     if (!o->nodes[i].present) {
       s.status = -2;
     } else if (ev[i].status >= 0) {
@@ -1238,6 +1428,8 @@ int32_t oracle_plugin_scores(oracle *o, const ks_pod *pod, ks_node_score *out) {
       s.image_locality = (int32_t)ev[i].il;
       s.spread_raw = (int32_t)ev[i].pts_raw;
       s.spread_score = st.spread_score.empty() ? 0 : (int32_t)ev[i].pts;
+      s.affinity_pod_raw = (int32_t)ev[i].ipa_raw;
+      s.affinity_pod_score = (int32_t)ev[i].ipa;
       s.total_score = o->total(st, ev[i], tt_max, na_max);
     }
     out[i] = s;

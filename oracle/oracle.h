@@ -34,6 +34,8 @@ void oracle_free(oracle *o);
 void oracle_set_threads(oracle *o, int32_t threads);
 /* PodTopologySpread score weight (default 2, the default profile's). */
 void oracle_set_weight_spread(oracle *o, int32_t w);
+/* InterPodAffinity score weight (2) and hardPodAffinityWeight (1). */
+void oracle_set_weight_inter_pod_affinity(oracle *o, int32_t w, int32_t hard);
 
 int32_t oracle_nodes_upsert(oracle *o, const ks_node *nodes, const uint32_t *slots, uint32_t n);
 int32_t oracle_nodes_delete(oracle *o, const uint32_t *slots, uint32_t n);

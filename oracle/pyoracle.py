@@ -20,7 +20,7 @@ LIB = ROOT / "oracle" / "_build" / "liboracle.so"
 class ShardPrescore(C.Structure):
     _fields_ = [
         ("feasible", C.c_uint32),
-        ("fail_counts", C.c_uint32 * 7),
+        ("fail_counts", C.c_uint32 * 8),
         ("taint_max", C.c_int64),
         ("affinity_max", C.c_int64),
         ("taint_count", C.c_uint32),
@@ -49,6 +49,8 @@ def lib() -> C.CDLL:
     L.oracle_set_threads.restype = None
     L.oracle_set_weight_spread.argtypes = [vp, C.c_int32]
     L.oracle_set_weight_spread.restype = None
+    L.oracle_set_weight_inter_pod_affinity.argtypes = [vp, C.c_int32, C.c_int32]
+    L.oracle_set_weight_inter_pod_affinity.restype = None
     L.oracle_nodes_upsert.argtypes = [vp, P(_abi.KsNode), P(C.c_uint32), C.c_uint32]
     L.oracle_nodes_delete.argtypes = [vp, P(C.c_uint32), C.c_uint32]
     L.oracle_pods_add.argtypes = [vp, P(_abi.KsPod), P(C.c_uint32), C.c_uint32]

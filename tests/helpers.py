@@ -6,7 +6,7 @@ import numpy as np
 from ksched import _abi
 
 RES_DT = np.dtype([("node_index", "<i4"), ("status", "<i4"), ("total_score", "<i8"), ("feasible", "<u4"),
-                   ("evaluated", "<u4"), ("fail", "<u4", (7,)), ("flags", "<u4")])
+                   ("evaluated", "<u4"), ("fail", "<u4", (8,)), ("flags", "<u4"), ("_pad", "<u4")])
 
 
 def res_array(raw, n):
@@ -30,7 +30,7 @@ def state_array(states):
 def scores_array(scores):
     return np.array([(s.status, s.least_allocated, s.balanced_allocation, s.taint_raw, s.taint_score,
                       s.affinity_raw, s.affinity_score, s.image_locality, s.spread_raw, s.spread_score,
-                      s.total_score) for s in scores],
+                      s.affinity_pod_raw, s.affinity_pod_score, s.total_score) for s in scores],
                     dtype=np.int64)
 
 

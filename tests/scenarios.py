@@ -6,7 +6,7 @@ from ksched.objects import (Container, Node, NodeSelectorRequirement as Req, Nod
                             PreferredSchedulingTerm as Pref, Taint, Toleration)
 
 Gi = 1 << 30
-UNSCHED, NAME, TAINT, AFFINITY, FIT, SPREAD, PREFILTER = range(7)
+UNSCHED, NAME, TAINT, AFFINITY, FIT, SPREAD, POD_AFFINITY, PREFILTER = range(8)
 
 
 def node(name, cpu=32000, mem=256 * Gi, pods=32, labels=None, taints=None, unschedulable=False):
@@ -252,7 +252,7 @@ def prefilter_result():
     # terms that all name nodes via matchFields metadata.name In: only the union of
     # the per-term name intersections is evaluated; every other node is
     # UnschedulableAndUnresolvable "filtered out by the prefilter result" with no
-    # plugin blamed (fail_counts[6]); an empty union rejects every node at
+    # plugin blamed (fail_counts[7]); an empty union rejects every node at
     # NodeAffinity.  The PreFilter reads RAW values: a name-In requirement with two
     # values puts both names in the result, although Filter rejects that term
     # (parse error: one value required).

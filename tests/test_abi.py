@@ -54,7 +54,9 @@ C_PROBE = r"""
 int main(void) {
   S(ks_label) S(ks_taint) S(ks_toleration) S(ks_node) S(ks_container) S(ks_requirement) S(ks_term)
   S(ks_preferred_term) S(ks_pod) S(ks_event) S(ks_result) S(ks_node_score) S(ks_node_state) S(ks_config) S(ks_stats)
-  S(ks_label_selector) S(ks_spread_constraint) S(ks_resource) S(ks_image)
+  S(ks_label_selector) S(ks_spread_constraint) S(ks_resource) S(ks_image) S(ks_pod_affinity_term)
+  O(ks_pod, affinity_terms) O(ks_pod, n_namespace_labels) O(ks_pod_affinity_term, kind) O(ks_pod_affinity_term, weight)
+  O(ks_config, hard_pod_affinity_weight) O(ks_node_score, affinity_pod_score) O(ks_result, flags)
   O(ks_node, extended) O(ks_node, n_extended) O(ks_container, extended) O(ks_container, n_extended)
   O(ks_pod, labels) O(ks_pod, spread) O(ks_pod, spread_defaulted) O(ks_spread_constraint, max_skew)
   O(ks_spread_constraint, node_taints_policy) O(ks_node_score, spread_score) O(ks_config, weight_topology_spread)

@@ -53,10 +53,10 @@ def rank_main(rank, world, port, kind, q):
         dist.all_reduce(maxima, op=dist.ReduceOp.MAX)
         feasible = int(counts[0])
         if feasible == 0:
-            out.append((-1, 1, 0, feasible, list(map(int, counts[1:8]))))
+            out.append((-1, 1, 0, feasible, list(map(int, counts[1:9]))))
             continue
-        if int(counts[8]) and feasible >= 2:
-            out.append((-1, 2, 0, feasible, list(map(int, counts[1:8]))))
+        if int(counts[9]) and feasible >= 2:
+            out.append((-1, 2, 0, feasible, list(map(int, counts[1:9]))))
             continue
         key = torch.tensor([o.shard_best(p, lo, hi, int(maxima[0]), int(maxima[1]))], dtype=torch.int64)
         keys = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
@@ -64,7 +64,7 @@ def rank_main(rank, world, port, kind, q):
         best = max(int(k) & 0xFFFFFFFFFFFFFFFF for k in keys)
         slot = 0xFFFFFFFF - (best & 0xFFFFFFFF)
         o.commit(p, slot)  # identical on every replica
-        out.append((slot, 0, (best >> 32) - 1, feasible, list(map(int, counts[1:8]))))
+        out.append((slot, 0, (best >> 32) - 1, feasible, list(map(int, counts[1:9]))))
     if rank == 0:
         q.put(out)
     dist.barrier()

@@ -113,7 +113,7 @@ def test_prefilter_counts_nodes_outside_the_result():
         r = res_array(s.schedule_raw(pa, 1), 1)[0]
         # both values enter the PreFilterResult; Filter rejects the two-value
         # term (parse error), so n5 fails NodeAffinity and 7 nodes are prefiltered
-        assert r["status"] == 1 and list(r["fail"]) == [0, 0, 0, 1, 0, 0, 7]
+        assert r["status"] == 1 and list(r["fail"]) == [0, 0, 0, 1, 0, 0, 0, 7]
 
 
 def test_async_submit_equals_sequential_runs():

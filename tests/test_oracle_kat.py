@@ -138,4 +138,4 @@ def test_pod_requests_extended_resources_pass_through():
 
 def test_struct_layout_consistency():
     # pyoracle reuses the ksched ctypes structs: layout mirrors the header
-    assert C.sizeof(_abi.KsPod) == 160 and C.sizeof(_abi.KsNode) == 88 and C.sizeof(_abi.KsResult) == 56
+    assert C.sizeof(_abi.KsPod) == 184 and C.sizeof(_abi.KsNode) == 88 and C.sizeof(_abi.KsResult) == 64
