@@ -91,3 +91,20 @@ def test_solo_case(name):
             assert [sc[i].image_locality for i in range(len(nodes))] == dumps[j], (name, j)
         out.append(res_array(o.schedule(pod_ptr(pa, j), 1), 1)[0])
     check(np.array(out), exp)
+
+
+@pytest.mark.parametrize("name", sorted(__import__("ipa_cases").CASES))
+def test_ipa_case(name):
+    from ipa_cases import CASES as IPA
+    nodes, bound, pods, exp, dumps = IPA[name]()
+    a = Arena()
+    o = build_oracle(nodes, bound, a)
+    pa, m = pods_array(pods, a)
+    out = []
+    for j in range(m):
+        if j in dumps:
+            sc = o.plugin_scores(pod_ptr(pa, j))
+            got = [(sc[i].affinity_pod_raw, sc[i].affinity_pod_score) for i in range(len(nodes))]
+            assert got == dumps[j], (name, j, got)
+        out.append(res_array(o.schedule(pod_ptr(pa, j), 1), 1)[0])
+    check(np.array(out), exp)
