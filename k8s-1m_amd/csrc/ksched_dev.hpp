@@ -124,7 +124,8 @@ __host__ __device__ inline uint32_t term_words(uint64_t w0) {
 // (matching bound pods per node), and the constraint's parameters.
 constexpr int MAX_SPREAD = 8;        // constraints per pod
 constexpr int MAX_TOPO_KEYS = 16;    // topology-key domain columns
-constexpr int MAX_CLASSES = 64;      // selector-class count columns
+constexpr int MAX_CLASSES = 128;     // selector-class count columns
+constexpr int CMASK_WORDS = MAX_CLASSES / 64;  // per-pod class bitmask words
 constexpr uint32_t DOM_NONE = 0xFFFFFFFFu;  // node lacks the topology key
 constexpr uint32_t CLS_NONE = 0xFFFFFFFFu;  // Empty() / Nothing() selector: counts are 0
 enum SpreadFlags : uint32_t {
@@ -145,10 +146,38 @@ static_assert(sizeof(SpreadDev) == 32, "SpreadDev layout");
 constexpr uint32_t SPREAD_WORDS = sizeof(SpreadDev) / 8;
 
 // A one-pod-path program (16-byte aligned in the label-program buffer):
-//   SoloHdr, n_spread SpreadDev, n_xres XResDev, n_img ImageDev.
+//   SoloHdr, n_spread SpreadDev, n_xres XResDev, n_img ImageDev, n_aff AffDev.
 struct alignas(16) SoloHdr {
   uint32_t n_spread, n_xres, n_img;
   uint32_t n_containers;  // ImageLocality: len(initContainers) + len(containers)
+  uint32_t n_aff;         // InterPodAffinity records
+  uint32_t aff_flags;     // AFF_SELF
+  uint32_t _pad[2];
+};
+// InterPodAffinity (interpodaffinity/filtering.go, scoring.go): one record per
+// (term, count column) the pod's cycle reads.  Counts are summed per topology
+// domain of the record's key over every node (PreFilter / PreScore maps keyed
+// by topology pair); the count column is a selector-class column (the incoming
+// pod's terms against bound pods) or a term-class column (bound pods' terms
+// that match the incoming pod: per node, the carriers of a required term, the
+// summed weights of the carriers of a preferred one).
+constexpr int MAX_AFF = 64;             // records per pod
+constexpr int MAX_TERM_CLASSES = 1024;  // term-class columns (allocated as they are needed)
+enum AffKind : uint32_t {
+  AF_REQ_AFF = 0,     // required affinity term; column: pods matching ALL such terms (affinityCounts)
+  AF_REQ_ANTI = 1,    // required anti-affinity term (antiAffinityCounts)
+  AF_EXIST_ANTI = 2,  // a bound pod's required anti-affinity term (existingAntiAffinityCounts)
+  AF_SCORE = 3,       // topologyScore: weight x count
+  AF_OWN = 4,         // a term class of the pod's own terms: +weight on commit
+  AF_KIND = 15u,
+  AF_TERM = 16u,      // the column is a term-class column
+};
+constexpr uint32_t AFF_SELF = 1u;  // the pod matches all its required affinity terms
+struct alignas(16) AffDev {
+  uint32_t key;    // topology-key column
+  uint32_t col;    // class column
+  uint32_t kind;   // AffKind | AF_TERM
+  int32_t weight;  // AF_SCORE: multiplier of the domain sum; AF_OWN: the column unit
 };
 // NodeResourcesFit for an extended resource (ephemeral-storage or a scalar
 // resource): the pod's request and the resource's column.
@@ -164,7 +193,8 @@ struct alignas(16) ImageDev {
   uint32_t bit, _pad;
   int64_t scaled;
 };
-static_assert(sizeof(SoloHdr) == 16 && sizeof(XResDev) == 16 && sizeof(ImageDev) == 16, "solo program layout");
+static_assert(sizeof(SoloHdr) == 32 && sizeof(XResDev) == 16 && sizeof(ImageDev) == 16 && sizeof(AffDev) == 16,
+              "solo program layout");
 
 // Per-pod accumulators of the spread path (reset by its commit kernel).
 // Blocks add into ACC_SHARDS copies (block b -> copy b % ACC_SHARDS) and
@@ -173,16 +203,20 @@ static_assert(sizeof(SoloHdr) == 16 && sizeof(XResDev) == 16 && sizeof(ImageDev)
 constexpr int SPREAD_MAX_BLOCKS = 256;
 constexpr int ACC_SHARDS = 16;
 struct SpreadAccShard {
-  uint32_t fail[NFILT + 1];            // first failures per plugin (+ PodTopologySpread)
+  uint32_t fail[NFILT + 2];            // first failures per plugin (+ PodTopologySpread, InterPodAffinity)
   uint32_t feasible, ignored;          // feasible nodes; feasible nodes PreScore ignores
   uint32_t tt_max, na_max;             // max raw TaintToleration / NodeAffinity over feasible nodes
   uint64_t pts_min, pts_max;           // raw PodTopologySpread min / max over non-ignored feasible nodes
+  uint64_t ipa_min, ipa_max;           // raw InterPodAffinity min / max over feasible nodes (biased 2^63)
   uint64_t best;                       // packed key of the winner
 };
 struct SpreadAcc {
   uint32_t min_match[MAX_SPREAD];      // Filter: min matching pods over eligible domains
   uint32_t ndomains[MAX_SPREAD];       // Filter: eligible domains
   uint32_t topo_size[MAX_SPREAD];      // Score: domains of non-ignored feasible nodes
+  uint32_t aff_any;                    // InterPodAffinity: affinityCounts non-empty
+  uint32_t score_any;                  // InterPodAffinity: topologyScore non-empty (else PreScore Skip)
+  uint32_t _pad[2];
   SpreadAccShard sh[ACC_SHARDS];
 };
 

@@ -165,20 +165,49 @@ struct HostNode {
 // has a device column of per-node domain ids (value -> id, "" = 0).
 struct LabelSet {
   uint32_t ns;
-  std::vector<std::pair<uint32_t, uint32_t>> labels;  // sorted (key id, value id)
+  std::vector<std::pair<uint32_t, uint32_t>> labels;     // sorted (key id, value id)
+  std::vector<std::pair<uint32_t, uint32_t>> ns_labels;  // the namespace's labels, sorted
+  // InterPodAffinity term classes of the pod's own terms, with the unit the
+  // pod adds to the class column (the weight of a preferred term, else 1)
+  std::vector<std::pair<uint32_t, uint32_t>> terms;
+  std::string key;              // set_of_key entry (sets with namespace labels or terms)
 };
 struct SelReq {
   uint32_t key;
   int32_t op;                   // KS_OP_IN / NOT_IN / EXISTS / DOES_NOT_EXIST
   std::vector<uint32_t> vals;   // sorted value ids
 };
+// One conjunct of a pod matcher (framework.AffinityTerm.Matches): the pod's
+// namespace listed or selected by the namespace selector, and its labels
+// selected.  A spread constraint's selector is {own namespace, selector}.
+struct Clause {
+  std::vector<uint32_t> nss;    // sorted namespace ids
+  bool ns_sel_set = false;      // namespaceSelector set (else Nothing())
+  std::vector<SelReq> ns_sel;
+  bool sel_nothing = false;     // labelSelector nil: matches no pod
+  std::vector<SelReq> sel;
+};
 struct SpreadClass {
   bool live = false;
-  uint32_t ns = 0;
-  std::vector<SelReq> reqs;
+  std::vector<Clause> clauses;  // all must match
   std::string canon;
   uint32_t refs = 0;            // prepared batches using the class
   uint64_t last_use = 0;
+};
+// A pod (anti-)affinity term some bound pod carries (InterPodAffinity's
+// existing-pod side): device column = bound pods carrying it, per node
+// (MAX_TERM_CLASSES columns, ksched_dev.hpp).
+struct TermClass {
+  bool live = false;
+  int32_t kind = 0;
+  uint32_t key = 0;             // topology key id
+  Clause clause;
+  std::string canon;
+  int64_t bound = 0;            // bound pods carrying the term (the column's sum)
+  uint32_t refs = 0;            // prepared batches holding pods that carry it
+  // pods matching the term take the one-pod path while some bound or
+  // prepared pod carries it
+  bool active() const { return live && (bound > 0 || refs > 0); }
 };
 struct TopoKey {
   uint32_t key = 0;
@@ -232,6 +261,7 @@ struct ks_batch {
   std::vector<uint8_t> spread;
   bool any_spread = false;
   std::vector<uint32_t> class_refs;
+  std::vector<uint32_t> term_refs;  // term classes of the batch's pods' own terms (one per pod and term)
   uint64_t *d_cmask = nullptr, *h_cmask = nullptr;
   // asynchronous run state (ks_batch_submit / ks_batch_wait)
   bool queued = false, done = false;
@@ -321,6 +351,14 @@ struct ks_ctx {
   std::map<std::pair<uint32_t, std::vector<std::pair<uint32_t, uint32_t>>>, uint32_t> set_ids;
   std::vector<LabelSet> label_sets;
   std::unordered_map<std::string, uint32_t> empty_set_of_ns;  // label-less pods: namespace -> set id
+  std::unordered_map<std::string, uint32_t> set_of_key;       // pods with terms / namespace labels
+  TermClass terms[MAX_TERM_CLASSES];
+  uint32_t n_terms = 0;
+  std::unordered_map<std::string, uint32_t> term_of;         // canonical term -> class
+  uint32_t *d_tcnt = nullptr;                                // [tcnt_cap][npos]
+  uint32_t tcnt_cap = 0;
+  uint32_t *d_adcnt = nullptr;                               // [MAX_AFF][dom_cap] affinity domain counts
+  int64_t *d_sraw2 = nullptr;                                // [npos] InterPodAffinity raw score
   // (slot, set) of pods the batches bound, appended at the end of each run and
   // applied to HostNode::pod_sets only when a reader needs them (flush_bound)
   std::vector<std::pair<uint32_t, uint32_t>> pending_bound;
@@ -835,9 +873,6 @@ bool prefilter_names(const ks_pod &p, std::vector<std::string> *names) {
 // default profile would filter or score with a plugin ksched does not model is
 // refused, never scheduled approximately.
 ks_status check_modelled(ks_ctx *c, const ks_pod &p) {
-  if (p.n_affinity_terms)
-    return c->fail(KS_ERR_UNSUPPORTED, "pod %s/%s carries pod (anti-)affinity terms (InterPodAffinity)",
-                   str(p.ns).c_str(), str(p.name).c_str());
   if (p.unmodelled)
     return c->fail(KS_ERR_UNSUPPORTED, "pod %s/%s carries %s", str(p.ns).c_str(), str(p.name).c_str(),
                    unmodelled_name(p.unmodelled));
@@ -1233,24 +1268,74 @@ uint32_t kernel_npl(const ks_ctx *c, bool ext) {
 // #filterTopologySpreadConstraints, LabelSelectorAsSelector,
 // mergeLabelSetWithSelector).
 
-// Interned (namespace, labels) of a pod.
-uint32_t intern_set(ks_ctx *c, const ks_pod &p) {
-  if (p.n_labels == 0) {  // the common case: one lookup by namespace
+ks_status term_get(ks_ctx *c, const ks_pod &p, const ks_pod_affinity_term &t, bool create, uint32_t *out);
+bool term_valid(const ks_pod_affinity_term &t);
+
+void term_activate(ks_ctx *c, uint32_t tc, int64_t bound_delta, int32_t refs_delta);
+
+// Interned (namespace, labels, namespace labels, own affinity terms) of a
+// pod; creates the term classes of its terms (invalid terms are dropped, as
+// the oracle's cache does) and holds each (a reference in `hold`, released by
+// the caller) so that no later term class creation reuses its slot.
+ks_status intern_set(ks_ctx *c, const ks_pod &p, uint32_t *out, std::vector<uint32_t> *hold) {
+  const bool plain = p.n_namespace_labels == 0 && p.n_affinity_terms == 0;
+  if (plain && p.n_labels == 0) {  // the common case: one lookup by namespace
     auto it = c->empty_set_of_ns.find(str(p.ns));
-    if (it != c->empty_set_of_ns.end()) return it->second;
+    if (it != c->empty_set_of_ns.end()) {
+      *out = it->second;
+      return KS_OK;
+    }
   }
   std::vector<std::pair<uint32_t, uint32_t>> l;
   l.reserve(p.n_labels);
   for (uint32_t k = 0; k < p.n_labels; ++k) l.emplace_back(c->intern(p.labels[k].key), c->intern(p.labels[k].value));
   std::sort(l.begin(), l.end());
-  auto key = std::make_pair(c->intern(p.ns), std::move(l));
-  auto it = c->set_ids.find(key);
-  if (it != c->set_ids.end()) return it->second;
+  const uint32_t ns = c->intern(p.ns);
+  if (plain) {
+    auto key = std::make_pair(ns, std::move(l));
+    auto it = c->set_ids.find(key);
+    if (it != c->set_ids.end()) {
+      *out = it->second;
+      return KS_OK;
+    }
+    const uint32_t id = (uint32_t)c->label_sets.size();
+    c->label_sets.push_back(LabelSet{key.first, key.second, {}, {}, {}});
+    c->set_ids.emplace(std::move(key), id);
+    if (p.n_labels == 0) c->empty_set_of_ns.emplace(str(p.ns), id);
+    *out = id;
+    return KS_OK;
+  }
+  std::vector<std::pair<uint32_t, uint32_t>> nl;
+  for (uint32_t k = 0; k < p.n_namespace_labels; ++k)
+    nl.emplace_back(c->intern(p.namespace_labels[k].key), c->intern(p.namespace_labels[k].value));
+  std::sort(nl.begin(), nl.end());
+  std::vector<std::pair<uint32_t, uint32_t>> terms;
+  for (uint32_t k = 0; k < p.n_affinity_terms; ++k) {
+    uint32_t t;
+    if (!term_valid(p.affinity_terms[k])) continue;
+    const ks_status st = term_get(c, p, p.affinity_terms[k], true, &t);
+    if (st == KS_ERR_UNSUPPORTED) continue;  // selector parse error
+    if (st) return st;
+    term_activate(c, t, 0, +1);
+    hold->push_back(t);
+    terms.emplace_back(t, p.affinity_terms[k].kind >= KS_POD_AFFINITY_PREFERRED ? (uint32_t)p.affinity_terms[k].weight : 1u);
+  }
+  std::string key = std::to_string(ns);
+  for (auto &kv : l) key += '|' + std::to_string(kv.first) + '=' + std::to_string(kv.second);
+  key += "#";
+  for (auto &kv : nl) key += '|' + std::to_string(kv.first) + '=' + std::to_string(kv.second);
+  key += "#";
+  for (auto &t : terms) key += ',' + std::to_string(t.first) + '*' + std::to_string(t.second);
+  auto it = c->set_of_key.find(key);
+  if (it != c->set_of_key.end()) {
+    *out = it->second;
+    return KS_OK;  // same term classes: held above
+  }
   const uint32_t id = (uint32_t)c->label_sets.size();
-  c->label_sets.push_back(LabelSet{key.first, key.second});
-  c->set_ids.emplace(std::move(key), id);
-  if (p.n_labels == 0) c->empty_set_of_ns.emplace(str(p.ns), id);
-  return id;
+  c->label_sets.push_back(LabelSet{ns, std::move(l), std::move(nl), std::move(terms), key});
+  c->set_of_key.emplace(std::move(key), id);
+  *out = id;
+  return KS_OK;
 }
 
 // Apply the pending records of batch-bound pods to the nodes (before a
@@ -1276,9 +1361,41 @@ bool reqs_match(const std::vector<SelReq> &reqs, const std::vector<std::pair<uin
   return true;
 }
 
+// framework.AffinityTerm.Matches (namespace listed or selected, then the
+// selector) of one clause.
+bool clause_match(const Clause &k, uint32_t ns, const std::vector<std::pair<uint32_t, uint32_t>> &labels,
+                  const std::vector<std::pair<uint32_t, uint32_t>> &ns_labels) {
+  if (!std::binary_search(k.nss.begin(), k.nss.end(), ns) && !(k.ns_sel_set && reqs_match(k.ns_sel, ns_labels)))
+    return false;
+  return !k.sel_nothing && reqs_match(k.sel, labels);
+}
+
+void reqs_canon(std::string &s, const std::vector<SelReq> &reqs) {
+  for (auto &r : reqs) {
+    s += '|' + std::to_string(r.key) + ':' + std::to_string(r.op);
+    for (uint32_t v : r.vals) s += ',' + std::to_string(v);
+  }
+}
+std::string clause_canon(const Clause &k) {
+  std::string s = "N";
+  for (uint32_t n : k.nss) s += ',' + std::to_string(n);
+  if (k.ns_sel_set) {
+    s += "S";
+    reqs_canon(s, k.ns_sel);
+  }
+  if (k.sel_nothing) s += "L-";
+  else {
+    s += "L";
+    reqs_canon(s, k.sel);
+  }
+  return s;
+}
+
 bool class_matches(const ks_ctx *c, const SpreadClass &k, uint32_t set) {
   const LabelSet &ls = c->label_sets[set];
-  return ls.ns == k.ns && reqs_match(k.reqs, ls.labels);
+  for (const Clause &cl : k.clauses)
+    if (!clause_match(cl, ls.ns, ls.labels, ls.ns_labels)) return false;
+  return true;
 }
 
 ks_status spread_scratch(ks_ctx *c, uint32_t need) {
@@ -1287,10 +1404,12 @@ ks_status spread_scratch(ks_ctx *c, uint32_t need) {
   HIPC(c, hipStreamSynchronize(c->stream));
   if (c->d_dcnt) (void)hipFree(c->d_dcnt);
   if (c->d_dflag) (void)hipFree(c->d_dflag);
-  c->d_dcnt = c->d_dflag = nullptr;
+  if (c->d_adcnt) (void)hipFree(c->d_adcnt);
+  c->d_dcnt = c->d_dflag = c->d_adcnt = nullptr;
   const uint32_t cap = std::max<uint32_t>({need, 2 * c->dom_cap, 1024});
   ks_status st;
-  if ((st = dalloc(c, &c->d_dcnt, (size_t)MAX_SPREAD * cap)) || (st = dalloc(c, &c->d_dflag, (size_t)MAX_SPREAD * cap)))
+  if ((st = dalloc(c, &c->d_dcnt, (size_t)MAX_SPREAD * cap)) || (st = dalloc(c, &c->d_dflag, (size_t)MAX_SPREAD * cap)) ||
+      (st = dalloc(c, &c->d_adcnt, (size_t)MAX_AFF * cap)))
     return st;
   c->dom_cap = cap;
   return KS_OK;
@@ -1302,7 +1421,7 @@ ks_status spread_alloc(ks_ctx *c) {
   // domain columns then class columns, one allocation (one index space for scatters)
   if ((st = dalloc(c, &c->d_dom, (size_t)(MAX_TOPO_KEYS + MAX_CLASSES) * c->npos)) || (st = dalloc(c, &c->d_pos_slot, c->npos)) ||
       (st = dalloc(c, &c->d_acc, 1)) || (st = dalloc(c, &c->d_sst, c->npos)) || (st = dalloc(c, &c->d_sraw, c->npos)) ||
-      (st = dalloc(c, &c->d_spart, c->npos)))
+      (st = dalloc(c, &c->d_spart, c->npos)) || (st = dalloc(c, &c->d_sraw2, c->npos)))
     return st;
   c->d_cnt = c->d_dom + (size_t)MAX_TOPO_KEYS * c->npos;
   HIPC(c, hipMemsetAsync(c->d_dom, 0xFF, (size_t)MAX_TOPO_KEYS * c->npos * 4, c->stream));
@@ -1310,7 +1429,7 @@ ks_status spread_alloc(ks_ctx *c) {
   for (uint32_t sl = 0; sl < c->cap; ++sl) ps[c->slot_pos[sl]] = sl;
   SpreadAcc acc{};
   for (int k = 0; k < MAX_SPREAD; ++k) acc.min_match[k] = 0xFFFFFFFFu;
-  for (int k = 0; k < ACC_SHARDS; ++k) acc.sh[k].pts_min = ~0ull;
+  for (int k = 0; k < ACC_SHARDS; ++k) acc.sh[k].pts_min = acc.sh[k].ipa_min = ~0ull;
   if ((st = xfer_begin(c, (size_t)c->npos * 4 + sizeof acc + 1024, 0)) ||
       (st = h2d(c, c->d_pos_slot, ps.data(), (size_t)c->npos * 4)) || (st = h2d(c, c->d_acc, &acc, sizeof acc)) ||
       (st = xfer_sync(c)))
@@ -1375,12 +1494,9 @@ ks_status topo_column(ks_ctx *c, uint32_t key, bool create, uint32_t *out) {
 // Selector class of (namespace, requirements): its column counts the bound
 // pods of every node that the selector matches (created when `create`, from
 // the host's records of bound pods; the caller has drained).
-ks_status class_get(ks_ctx *c, uint32_t ns, std::vector<SelReq> &&reqs, bool create, uint32_t *out) {
-  std::string canon = std::to_string(ns);
-  for (auto &r : reqs) {
-    canon += '|' + std::to_string(r.key) + ':' + std::to_string(r.op);
-    for (uint32_t v : r.vals) canon += ',' + std::to_string(v);
-  }
+ks_status class_get(ks_ctx *c, std::vector<Clause> &&clauses, bool create, uint32_t *out) {
+  std::string canon;
+  for (const Clause &k : clauses) canon += clause_canon(k) + ';';
   auto it = c->class_of.find(canon);
   if (it != c->class_of.end()) {
     *out = it->second;
@@ -1411,8 +1527,7 @@ ks_status class_get(ks_ctx *c, uint32_t ns, std::vector<SelReq> &&reqs, bool cre
   SpreadClass &k = c->classes[slot];
   k = SpreadClass{};
   k.live = true;
-  k.ns = ns;
-  k.reqs = std::move(reqs);
+  k.clauses = std::move(clauses);
   k.canon = canon;
   k.last_use = ++c->class_seq;
   c->class_of.emplace(canon, (uint32_t)slot);
@@ -1433,6 +1548,20 @@ ks_status class_get(ks_ctx *c, uint32_t ns, std::vector<SelReq> &&reqs, bool cre
     return st;
   *out = (uint32_t)slot;
   return KS_OK;
+}
+
+// A prepared batch's hold on a selector class (no eviction until ks_batch_free);
+// taken as soon as the class is looked up, so that later pods of the same
+// batch cannot evict it.
+void class_hold(ks_ctx *c, std::vector<uint32_t> *refs, uint32_t k) {
+  if (k == CLS_NONE) return;
+  refs->push_back(k);
+  c->classes[k].refs++;
+}
+void class_release(ks_ctx *c, std::vector<uint32_t> *refs) {
+  for (uint32_t k : *refs)
+    if (c->classes[k].refs) c->classes[k].refs--;
+  refs->clear();
 }
 
 // metav1.LabelSelectorAsSelector: false on a parse error.
@@ -1462,13 +1591,149 @@ bool parse_label_selector(ks_ctx *c, const ks_label_selector &ls, std::vector<Se
       return false;  // "is not a valid label selector operator"
     if (!add(e.key, e.op, e.values, e.n_values)) return false;
   }
+  std::sort(reqs->begin(), reqs->end(), [](const SelReq &a, const SelReq &b) {
+    return std::tie(a.key, a.op, a.vals) < std::tie(b.key, b.op, b.vals);
+  });
+  reqs->erase(std::unique(reqs->begin(), reqs->end(),
+                          [](const SelReq &a, const SelReq &b) {
+                            return a.key == b.key && a.op == b.op && a.vals == b.vals;
+                          }),
+              reqs->end());
   return true;
+}
+
+// framework/types.go#newAffinityTerm of one of pod p's terms: namespaces
+// listed, else the pod's own when the namespace selector is nil; nil
+// selectors are Nothing().  False on a parse error or an invalid term (the
+// apiserver would reject it).
+bool term_clause(ks_ctx *c, const ks_pod &p, const ks_pod_affinity_term &t, Clause *out) {
+  Clause k;
+  for (uint32_t i = 0; i < t.n_namespaces; ++i) k.nss.push_back(c->intern(t.namespaces[i]));
+  if (k.nss.empty() && t.namespace_selector.is_nil) k.nss.push_back(c->intern(p.ns));
+  std::sort(k.nss.begin(), k.nss.end());
+  k.nss.erase(std::unique(k.nss.begin(), k.nss.end()), k.nss.end());
+  k.ns_sel_set = !t.namespace_selector.is_nil;
+  if (k.ns_sel_set && !parse_label_selector(c, t.namespace_selector, &k.ns_sel)) return false;
+  k.sel_nothing = t.selector.is_nil != 0;
+  if (!k.sel_nothing && !parse_label_selector(c, t.selector, &k.sel)) return false;
+  *out = std::move(k);
+  return true;
+}
+
+bool term_valid(const ks_pod_affinity_term &t) {
+  if (!t.topology_key || !t.topology_key[0] || t.kind < KS_POD_AFFINITY_REQUIRED || t.kind > KS_POD_ANTI_AFFINITY_PREFERRED)
+    return false;
+  if (t.kind >= KS_POD_AFFINITY_PREFERRED && (t.weight < 1 || t.weight > 100)) return false;
+  return true;
+}
+
+// Term class of one of a bound (or to-be-bound) pod's terms, created when
+// `create` (its column starts at zero: no pod carrying it is bound yet).
+// Classes no pod carries (bound or prepared) are reused when the table is full.
+ks_status term_get(ks_ctx *c, const ks_pod &p, const ks_pod_affinity_term &t, bool create, uint32_t *out) {
+  Clause k;
+  if (!term_valid(t) || !term_clause(c, p, t, &k))
+    return c->fail(KS_ERR_UNSUPPORTED, "pod %s/%s: invalid pod (anti-)affinity term", str(p.ns).c_str(),
+                   str(p.name).c_str());
+  const uint32_t key = c->intern(t.topology_key);
+  // preferred terms of any weight share a class: its column sums the weights
+  const std::string canon = std::to_string(t.kind) + '/' + std::to_string(key) + '/' + clause_canon(k);
+  auto it = c->term_of.find(canon);
+  if (it != c->term_of.end()) {
+    *out = it->second;
+    return KS_OK;
+  }
+  if (!create) {
+    *out = UINT32_MAX;
+    return KS_OK;
+  }
+  int slot = -1;
+  for (int i = 0; i < MAX_TERM_CLASSES && slot < 0; ++i)
+    if (!c->terms[i].live) slot = i;
+  for (int i = 0; i < MAX_TERM_CLASSES && slot < 0; ++i)
+    if (c->terms[i].bound == 0 && c->terms[i].refs == 0) {
+      slot = i;
+      c->term_of.erase(c->terms[i].canon);
+      // label sets of pods carrying the old term (none bound or prepared) are
+      // retired: a new such pod interns a fresh set
+      for (LabelSet &ls : c->label_sets)
+        if (std::any_of(ls.terms.begin(), ls.terms.end(), [&](const std::pair<uint32_t, uint32_t> &x) {
+              return x.first == (uint32_t)i;
+            })) {
+          c->set_of_key.erase(ls.key);
+          ls.terms.clear();
+          ls.key.clear();
+        }
+    }
+  if (slot < 0) return c->fail(KS_ERR_CAPACITY, "more than %d distinct pod (anti-)affinity terms", MAX_TERM_CLASSES);
+  ks_status st;
+  if ((st = spread_alloc(c))) return st;
+  if ((uint32_t)slot >= c->tcnt_cap) {  // grow the columns (callers have drained)
+    const uint32_t cap = std::min<uint32_t>(MAX_TERM_CLASSES, std::max<uint32_t>({16, 2 * c->tcnt_cap, (uint32_t)slot + 1}));
+    uint32_t *nt = nullptr;
+    if ((st = dalloc(c, &nt, (size_t)cap * c->npos))) return st;
+    if (c->d_tcnt) {
+      HIPC(c, hipMemcpyAsync(nt, c->d_tcnt, (size_t)c->tcnt_cap * c->npos * 4, hipMemcpyDeviceToDevice, c->stream));
+      HIPC(c, hipStreamSynchronize(c->stream));
+      (void)hipFree(c->d_tcnt);
+    }
+    c->d_tcnt = nt;
+    c->tcnt_cap = cap;
+  }
+  uint32_t col;
+  if ((st = topo_column(c, key, true, &col))) return st;
+  TermClass &tc = c->terms[slot];
+  tc = TermClass{};
+  tc.live = true;
+  tc.kind = t.kind;
+  tc.key = key;
+  tc.clause = std::move(k);
+  tc.canon = canon;
+  c->term_of.emplace(canon, (uint32_t)slot);
+  c->n_terms = std::max<uint32_t>(c->n_terms, (uint32_t)slot + 1);
+  *out = (uint32_t)slot;
+  return KS_OK;
+}
+
+// A term class gains its first carrier: pods compiled before saw no such term
+// (prepared batches go stale).
+void term_activate(ks_ctx *c, uint32_t tc, int64_t bound_delta, int32_t refs_delta) {
+  TermClass &t = c->terms[tc];
+  const bool was = t.active();
+  t.bound += bound_delta;
+  t.refs += refs_delta;
+  if (!was && t.active()) c->dict_version++;
+}
+
+// Interned, sorted labels and namespace labels of a pod.
+void pod_label_ids(ks_ctx *c, const ks_pod &p, std::vector<std::pair<uint32_t, uint32_t>> *l,
+                   std::vector<std::pair<uint32_t, uint32_t>> *nl) {
+  for (uint32_t k = 0; k < p.n_labels; ++k) l->emplace_back(c->intern(p.labels[k].key), c->intern(p.labels[k].value));
+  for (uint32_t k = 0; k < p.n_namespace_labels; ++k)
+    nl->emplace_back(c->intern(p.namespace_labels[k].key), c->intern(p.namespace_labels[k].value));
+  std::sort(l->begin(), l->end());
+  std::sort(nl->begin(), nl->end());
+}
+
+// Whether some bound (or prepared) pod's term selects the pod: InterPodAffinity
+// then filters (existing anti-affinity) or scores it.
+bool matched_by_terms(ks_ctx *c, const ks_pod &p) {
+  bool any = false;
+  for (uint32_t t = 0; t < c->n_terms && !any; ++t) any = c->terms[t].active();
+  if (!any) return false;
+  std::vector<std::pair<uint32_t, uint32_t>> l, nl;
+  pod_label_ids(c, p, &l, &nl);
+  const uint32_t ns = c->intern(p.ns);
+  for (uint32_t t = 0; t < c->n_terms; ++t)
+    if (c->terms[t].active() && clause_match(c->terms[t].clause, ns, l, nl)) return true;
+  return false;
 }
 
 // Whether compiling the pod may create one-pod-path state (columns, label
 // bits, device buffers): ks_batch_prepare drains the submitted batches first.
-bool may_need_solo(const ks_ctx *c, const ks_pod &p) {
-  if (p.n_spread) return true;
+bool may_need_solo(ks_ctx *c, const ks_pod &p) {
+  if (p.n_spread || p.n_affinity_terms) return true;
+  if (matched_by_terms(c, p)) return true;
   for (uint32_t i = 0; i < p.n_containers; ++i)
     if (p.containers[i].n_extended || (!c->images.empty() && p.containers[i].image && p.containers[i].image[0]))
       return true;
@@ -1477,6 +1742,89 @@ bool may_need_solo(const ks_ctx *c, const ks_pod &p) {
         (!c->images.empty() && p.init_containers[i].image && p.init_containers[i].image[0]))
       return true;
   return false;
+}
+
+// InterPodAffinity records of a pod (ksched_dev.hpp AffDev): its own required
+// affinity terms (one selector class of all of them: affinityCounts counts
+// pods matching every term), required anti-affinity and preferred terms (one
+// class each), the bound pods' term classes that match it (existing
+// anti-affinity; hardPodAffinityWeight x required and weighted preferred
+// terms for the score), and its own term classes (counted on commit).
+ks_status ipa_compile(ks_ctx *c, const ks_pod &p, bool create, std::vector<uint32_t> *refs, std::vector<AffDev> *out,
+                      uint32_t *flags) {
+  const std::string pn = str(p.ns) + "/" + str(p.name);
+  ks_status st;
+  std::vector<std::pair<uint32_t, uint32_t>> l, nl;
+  pod_label_ids(c, p, &l, &nl);
+  const uint32_t ns = c->intern(p.ns);
+  std::vector<Clause> req_aff;
+  std::vector<uint32_t> req_keys;
+  for (uint32_t k = 0; k < p.n_affinity_terms; ++k) {
+    const ks_pod_affinity_term &t = p.affinity_terms[k];
+    Clause cl;
+    if (!term_valid(t) || !term_clause(c, p, t, &cl))
+      return c->fail(KS_ERR_UNSUPPORTED, "pod %s: pod (anti-)affinity term %u is invalid", pn.c_str(), k);
+    uint32_t kc;
+    if ((st = topo_column(c, c->intern(t.topology_key), create, &kc))) return st;
+    if (t.kind == KS_POD_AFFINITY_REQUIRED) {
+      req_aff.push_back(std::move(cl));
+      req_keys.push_back(kc);
+      continue;
+    }
+    std::vector<Clause> one(1, std::move(cl));
+    uint32_t col;
+    if ((st = class_get(c, std::move(one), create, &col))) return st;
+    if (create && refs) class_hold(c, refs, col);
+    const int32_t w = t.kind == KS_POD_AFFINITY_PREFERRED ? t.weight : -t.weight;
+    out->push_back(AffDev{kc, col, t.kind == KS_POD_ANTI_AFFINITY_REQUIRED ? (uint32_t)AF_REQ_ANTI : (uint32_t)AF_SCORE,
+                          t.kind == KS_POD_ANTI_AFFINITY_REQUIRED ? 0 : w});
+  }
+  if (!req_aff.empty()) {
+    bool self = true;  // podMatchesAllAffinityTerms(terms, pod)
+    for (const Clause &cl : req_aff) self = self && clause_match(cl, ns, l, nl);
+    if (self) *flags |= AFF_SELF;
+    uint32_t col;
+    if ((st = class_get(c, std::move(req_aff), create, &col))) return st;
+    if (create && refs) class_hold(c, refs, col);
+    for (uint32_t kc : req_keys) out->push_back(AffDev{kc, col, AF_REQ_AFF, 0});
+  }
+  for (uint32_t t = 0; t < c->n_terms; ++t) {
+    const TermClass &tc = c->terms[t];
+    if (!tc.active() || !clause_match(tc.clause, ns, l, nl)) continue;
+    uint32_t kc;
+    if ((st = topo_column(c, tc.key, create, &kc))) return st;
+    if (tc.kind == KS_POD_ANTI_AFFINITY_REQUIRED) out->push_back(AffDev{kc, t, AF_EXIST_ANTI | AF_TERM, 0});
+    else if (tc.kind == KS_POD_AFFINITY_REQUIRED) {
+      if (c->cfg.hard_pod_affinity_weight > 0)
+        out->push_back(AffDev{kc, t, AF_SCORE | AF_TERM, c->cfg.hard_pod_affinity_weight});
+    } else {
+      out->push_back(AffDev{kc, t, AF_SCORE | AF_TERM, tc.kind == KS_POD_AFFINITY_PREFERRED ? 1 : -1});
+    }
+  }
+  if (create)  // the pod's own term classes (ks_batch_prepare interned them)
+    for (uint32_t k = 0; k < p.n_affinity_terms; ++k) {
+      uint32_t t;
+      if ((st = term_get(c, p, p.affinity_terms[k], false, &t))) return st;
+      const ks_pod_affinity_term &tm = p.affinity_terms[k];
+      if (t != UINT32_MAX)
+        out->push_back(AffDev{0, t, AF_OWN | AF_TERM, tm.kind >= KS_POD_AFFINITY_PREFERRED ? tm.weight : 1});
+    }
+  if (out->size() > (size_t)MAX_AFF)
+    return c->fail(KS_ERR_UNSUPPORTED, "pod %s: more than %d pod (anti-)affinity records (own and matching terms)",
+                   pn.c_str(), MAX_AFF);
+  return KS_OK;
+}
+
+// Passes of the spread chain a one-pod program needs (SpreadLaunch).
+uint32_t solo_passes(const SoloHdr *hd) {
+  const SpreadDev *sd = reinterpret_cast<const SpreadDev *>(hd + 1);
+  uint32_t f = 0;
+  for (uint32_t k = 0; k < hd->n_spread; ++k) f |= (sd[k].flags & SP_SCORE) ? SPL_SCORE : (SPL_PREP | SPL_MIN);
+  const AffDev *ad = reinterpret_cast<const AffDev *>(reinterpret_cast<const uint8_t *>(sd + hd->n_spread) +
+                                                      hd->n_xres * sizeof(XResDev) + hd->n_img * sizeof(ImageDev));
+  for (uint32_t k = 0; k < hd->n_aff; ++k)
+    if ((ad[k].kind & AF_KIND) != AF_OWN) f |= SPL_PREP;
+  return f;
 }
 
 // The one-pod-path program of a pod (ksched_dev.hpp SoloHdr): its spread
@@ -1515,10 +1863,16 @@ ks_status solo_compile(ks_ctx *c, const ks_pod &p, PodDev &d, ProgBuf &cl, bool 
     if ((st = scan(p.init_containers, p.n_init_containers)) || (st = scan(p.containers, p.n_containers))) return st;
     if (!imgs.empty()) c->compile_used_names = true;  // the node count enters the scores
   }
-  if (!p.n_spread && xr.empty() && imgs.empty()) return KS_OK;
+  std::vector<AffDev> aff;
+  uint32_t aff_flags = 0;
+  if (p.n_affinity_terms || c->n_terms) {
+    if ((st = ipa_compile(c, p, create, refs, &aff, &aff_flags))) return st;
+  }
+  if (!p.n_spread && xr.empty() && imgs.empty() && aff.empty()) return KS_OK;
   if (c->cfg.world_size > 1)
     return c->fail(KS_ERR_UNSUPPORTED,
-                   "pod %s: spread constraints, extended resources and present images need a single-rank context",
+                   "pod %s: spread constraints, pod affinity, extended resources and present images need a "
+                   "single-rank context",
                    pn.c_str());
   if (create && (st = spread_alloc(c))) return st;
   if (p.n_spread > (uint32_t)MAX_SPREAD)
@@ -1571,8 +1925,11 @@ ks_status solo_compile(ks_ctx *c, const ks_pod &p, PodDev &d, ProgBuf &cl, bool 
     if (!nothing && reqs_match(reqs, own)) r.flags |= SP_SELF;
     r.cls = CLS_NONE;  // Nothing() matches no pod; Empty() counts 0 (countPodsMatchSelector)
     if (!nothing && !reqs.empty()) {
-      if ((st = class_get(c, c->intern(p.ns), std::move(reqs), create, &r.cls))) return st;
-      if (create && refs) refs->push_back(r.cls);
+      std::vector<Clause> cls(1);
+      cls[0].nss = {c->intern(p.ns)};
+      cls[0].sel = std::move(reqs);
+      if ((st = class_get(c, std::move(cls), create, &r.cls))) return st;
+      if (create && refs) class_hold(c, refs, r.cls);
     }
     if ((st = topo_column(c, key, create, &r.key))) return st;
     recs.push_back(r);
@@ -1586,7 +1943,7 @@ ks_status solo_compile(ks_ctx *c, const ks_pod &p, PodDev &d, ProgBuf &cl, bool 
     std::memcpy(cl.w.data() + w0, rec, bytes);
   };
   const SoloHdr hdr{(uint32_t)recs.size(), (uint32_t)xr.size(), (uint32_t)imgs.size(),
-                    p.n_init_containers + p.n_containers};
+                    p.n_init_containers + p.n_containers, (uint32_t)aff.size(), aff_flags, {0, 0}};
   emit(&hdr, sizeof hdr);
   for (const SpreadDev &r : recs) emit(&r, sizeof r);
   for (auto &x : xr) {
@@ -1594,20 +1951,21 @@ ks_status solo_compile(ks_ctx *c, const ks_pod &p, PodDev &d, ProgBuf &cl, bool 
     emit(&r, sizeof r);
   }
   for (const ImageDev &g : imgs) emit(&g, sizeof g);
+  for (const AffDev &r : aff) emit(&r, sizeof r);
   d.flags |= PF_SOLO | (p.n_spread && !p.spread_defaulted ? PF_SPREAD_ALLKEYS : 0u);
   (void)any_filter;
   (void)any_score;
   return KS_OK;
 }
 
-// Device deltas of the selector-class columns for pods bound / removed on
-// slots (sign +1 / -1), and the host records.
-ks_status spread_pods_delta(ks_ctx *c, const ks_pod *pods, const uint32_t *slots, uint32_t n, int sign) {
-  std::vector<uint64_t> idx;
-  std::vector<int32_t> dv;
+// Device deltas of the selector-class and term-class columns for pods bound /
+// removed on slots (sign +1 / -1), and the host records.
+ks_status spread_pods_delta(ks_ctx *c, const uint32_t *sets, const uint32_t *slots, uint32_t n, int sign) {
+  std::vector<uint64_t> idx, tidx;
+  std::vector<int32_t> dv, tdv;
   if (sign < 0) flush_bound(c);
   for (uint32_t i = 0; i < n; ++i) {
-    const uint32_t set = intern_set(c, pods[i]);
+    const uint32_t set = sets[i];
     HostNode &h = c->nodes[slots[i]];
     if (sign > 0) {
       h.pod_sets.push_back(set);
@@ -1616,21 +1974,32 @@ ks_status spread_pods_delta(ks_ctx *c, const ks_pod *pods, const uint32_t *slots
       if (it == h.pod_sets.end()) continue;  // never bound here: no count to remove
       h.pod_sets.erase(it);
     }
+    const uint32_t pos = c->slot_pos[slots[i]];
     for (int k = 0; k < MAX_CLASSES; ++k)
       if (c->classes[k].live && class_matches(c, c->classes[k], set)) {
-        idx.push_back((uint64_t)k * c->npos + c->slot_pos[slots[i]]);
+        idx.push_back((uint64_t)k * c->npos + pos);
         dv.push_back(sign);
       }
+    for (auto &t : c->label_sets[set].terms) {
+      term_activate(c, t.first, sign, 0);
+      tidx.push_back((uint64_t)t.first * c->npos + pos);
+      tdv.push_back(sign * (int32_t)t.second);
+    }
   }
-  if (idx.empty()) return KS_OK;
-  const size_t bytes = idx.size() * 12 + 1024;
-  ks_status st = xfer_begin(c, bytes, bytes);
-  if (st) return st;
-  uint64_t *d_idx = dscratch<uint64_t>(c, idx.size());
-  int32_t *d_dv = dscratch<int32_t>(c, dv.size());
-  if ((st = h2d(c, d_idx, idx.data(), idx.size() * 8)) || (st = h2d(c, d_dv, dv.data(), dv.size() * 4))) return st;
-  HIPC(c, launch_add_u32(c->d_cnt, d_idx, d_dv, (uint32_t)idx.size(), c->stream));
-  return xfer_sync(c);
+  for (int pass = 0; pass < 2; ++pass) {
+    auto &ix = pass ? tidx : idx;
+    auto &dx = pass ? tdv : dv;
+    if (ix.empty()) continue;
+    const size_t bytes = ix.size() * 12 + 1024;
+    ks_status st = xfer_begin(c, bytes, bytes);
+    if (st) return st;
+    uint64_t *d_idx = dscratch<uint64_t>(c, ix.size());
+    int32_t *d_dv = dscratch<int32_t>(c, dx.size());
+    if ((st = h2d(c, d_idx, ix.data(), ix.size() * 8)) || (st = h2d(c, d_dv, dx.data(), dx.size() * 4))) return st;
+    HIPC(c, launch_add_u32(pass ? c->d_tcnt : c->d_cnt, d_idx, d_dv, (uint32_t)ix.size(), c->stream));
+    if ((st = xfer_sync(c))) return st;
+  }
+  return KS_OK;
 }
 
 // Topology-key and class columns of nodes upserted (their labels may have
@@ -1669,6 +2038,26 @@ ks_status spread_nodes_changed(ks_ctx *c, const uint32_t *slots, uint32_t n, boo
     // one index space: topology columns, then (offset by MAX_TOPO_KEYS columns) class columns
     HIPC(c, launch_scatter_u32(c->d_dom, d_idx, d_val, (uint32_t)idx.size(), c->stream));
     if ((st = xfer_sync(c))) return st;
+  }
+  if (deleted && c->d_tcnt && c->n_terms) {
+    idx.clear();
+    val.clear();
+    for (uint32_t t = 0; t < c->n_terms; ++t)
+      if (c->terms[t].live)
+        for (uint32_t i = 0; i < n; ++i) {
+          idx.push_back((uint64_t)t * c->npos + c->slot_pos[slots[i]]);
+          val.push_back(0);
+        }
+    if (!idx.empty()) {
+      const size_t bytes = idx.size() * 12 + 1024;
+      if ((st = xfer_begin(c, bytes, bytes))) return st;
+      uint64_t *d_idx = dscratch<uint64_t>(c, idx.size());
+      uint32_t *d_val = dscratch<uint32_t>(c, val.size());
+      if ((st = h2d(c, d_idx, idx.data(), idx.size() * 8)) || (st = h2d(c, d_val, val.data(), val.size() * 4)))
+        return st;
+      HIPC(c, launch_scatter_u32(c->d_tcnt, d_idx, d_val, (uint32_t)idx.size(), c->stream));
+      if ((st = xfer_sync(c))) return st;
+    }
   }
   for (uint32_t ti : rebuild)
     if ((st = topo_build(c, ti))) return st;
@@ -1952,8 +2341,8 @@ ks_status batch_acquire(ks_ctx *c, uint32_t n, size_t words, ks_batch **out) {
     HIPC(c, hipHostMalloc((void **)&b->h_results, (size_t)need * sizeof(DevResult), hipHostMallocDefault));
     HIPC(c, hipHostMalloc((void **)&b->h_pods, (size_t)need * sizeof(PodDev), hipHostMallocDefault));
     HIPC(c, hipHostMalloc((void **)&b->h_pinv, (size_t)need * 2 * sizeof(double), hipHostMallocDefault));
-    HIPC(c, hipMalloc((void **)&b->d_cmask, (size_t)need * 8));
-    HIPC(c, hipHostMalloc((void **)&b->h_cmask, (size_t)need * 8, hipHostMallocDefault));
+    HIPC(c, hipMalloc((void **)&b->d_cmask, (size_t)need * 8 * CMASK_WORDS));
+    HIPC(c, hipHostMalloc((void **)&b->h_cmask, (size_t)need * 8 * CMASK_WORDS, hipHostMallocDefault));
     b->cap_pods = need;
   }
   if (words > b->cap_words) {
@@ -2019,21 +2408,23 @@ ks_status run_batch(ks_ctx *c, ks_batch *b) {
     std::lock_guard<std::mutex> g(c->mu);
     for (int k = 0; k < MAX_CLASSES; ++k) classes |= c->classes[k].live;
     if (classes || b->any_spread) {
-      std::vector<uint64_t> memo(c->label_sets.size(), ~0ull);
+      std::vector<int32_t> memo(c->label_sets.size(), -1);  // set -> first pod index with it
       for (uint32_t i = 0; i < b->n; ++i) {
         const uint32_t set = b->set_ids[i];
-        if (memo[set] == ~0ull) {
-          uint64_t m = 0;
-          for (int k = 0; k < MAX_CLASSES; ++k)
-            if (c->classes[k].live && class_matches(c, c->classes[k], set)) m |= 1ull << k;
-          memo[set] = m;
+        uint64_t *m = b->h_cmask + (size_t)i * CMASK_WORDS;
+        if (memo[set] >= 0) {
+          std::memcpy(m, b->h_cmask + (size_t)memo[set] * CMASK_WORDS, 8 * CMASK_WORDS);
+          continue;
         }
-        b->h_cmask[i] = memo[set];
+        for (int w = 0; w < CMASK_WORDS; ++w) m[w] = 0;
+        for (int k = 0; k < MAX_CLASSES; ++k)
+          if (c->classes[k].live && class_matches(c, c->classes[k], set)) m[k / 64] |= 1ull << (k % 64);
+        memo[set] = (int32_t)i;
       }
     }
   }
   if (classes || b->any_spread)
-    HIPC(c, hipMemcpyAsync(b->d_cmask, b->h_cmask, (size_t)std::max<uint32_t>(b->n, 1) * 8, hipMemcpyHostToDevice,
+    HIPC(c, hipMemcpyAsync(b->d_cmask, b->h_cmask, (size_t)std::max<uint32_t>(b->n, 1) * 8 * CMASK_WORDS, hipMemcpyHostToDevice,
                            c->stream));
   // Segments in queue order: runs of pods without spread constraints through
   // the pipelined rounds, spread pods one at a time through ksched_spread.hip.
@@ -2058,6 +2449,9 @@ ks_status run_batch(ks_ctx *c, ks_batch *b) {
       sa.xreq = c->d_xreq;
       sa.dcnt = c->d_dcnt;
       sa.dflag = c->d_dflag;
+      sa.tcnt = c->d_tcnt;
+      sa.adcnt = c->d_adcnt;
+      sa.ipa_raw = c->d_sraw2;
       sa.dom_cap = c->dom_cap;
       sa.acc = c->d_acc;
       sa.st = c->d_sst;
@@ -2068,6 +2462,7 @@ ks_status run_batch(ks_ctx *c, ks_batch *b) {
       sa.w = Weights{c->cfg.weight_fit, c->cfg.weight_balanced, c->cfg.weight_taint, c->cfg.weight_affinity,
                      c->cfg.weight_image};
       sa.w_pts = c->cfg.weight_topology_spread;
+      sa.w_ipa = c->cfg.weight_inter_pod_affinity;
       sa.evaluated = c->n_present;
       for (; hi < b->n && b->spread[hi]; ++hi) {
         sa.pod = hi;
@@ -2079,7 +2474,7 @@ ks_status run_batch(ks_ctx *c, ks_batch *b) {
           e1 = get_event(c);
           HIPC(c, hipEventRecord(e0, c->stream));
         }
-        HIPC(c, launch_spread_pod(sa, (b->spread[hi] & 2) != 0, (b->spread[hi] & 4) != 0, c->stream));
+        HIPC(c, launch_spread_pod(sa, b->spread[hi] & 0x7Fu, c->stream));
         if (tm) {
           HIPC(c, hipEventRecord(e1, c->stream));
           c->ev_spread.emplace_back(e0, e1);
@@ -2122,8 +2517,10 @@ ks_status run_batch(ks_ctx *c, ks_batch *b) {
     std::lock_guard<std::mutex> g(c->mu);
     if (c->pending_bound.size() > (1u << 24)) flush_bound(c);
     for (uint32_t i = 0; i < b->n; ++i)
-      if (b->h_results[i].status == KS_POD_SCHEDULED)
+      if (b->h_results[i].status == KS_POD_SCHEDULED) {
         c->pending_bound.emplace_back((uint32_t)b->h_results[i].node_index, b->set_ids[i]);
+        for (auto &t : c->label_sets[b->set_ids[i]].terms) c->terms[t.first].bound++;  // the commit counted it
+      }
   }
   if (c->timing) {
     ks_status st = collect_timing(c);
@@ -2365,7 +2762,7 @@ void ks_close(ks_ctx *c) {
                   c->d_start, c->d_norm, c->d_norm_inv, c->d_pstat, c->d_fix, c->d_brec, c->d_srec, c->d_frec,
                   c->d_counters, c->d_crow, c->d_cext, c->d_pipe, c->d_carry, c->d_flags, c->d_dom,
                   c->d_pos_slot, c->d_dcnt, c->d_dflag, c->d_acc, c->d_sst, c->d_sraw, c->d_spart,
-                  c->d_xalloc};
+                  c->d_xalloc, c->d_tcnt, c->d_adcnt, c->d_sraw2};
   for (void *b : bufs)
     if (b) (void)hipFree(b);
   if (c->h_start) (void)hipHostFree(c->h_start);
@@ -2592,6 +2989,8 @@ ks_status ks_nodes_delete(ks_ctx *c, const uint32_t *slots, uint32_t n) {
     if (slots[i] >= c->cap || !c->nodes[slots[i]].present)
       return c->fail(KS_ERR_NOT_FOUND, "slot %u not present", slots[i]);
     HostNode &h = c->nodes[slots[i]];
+    for (uint32_t set : h.pod_sets)
+      for (auto &t : c->label_sets[set].terms) c->terms[t.first].bound--;
     c->name_slot.erase(h.name);
     c->names_version++;
     prefer_mask_ref(c, h.prefer, -1);
@@ -2640,11 +3039,21 @@ static ks_status pods_delta(ks_ctx *c, const ks_pod *pods, const uint32_t *slots
   std::vector<uint64_t> xidx;
   std::vector<int64_t> xval;
   std::vector<std::pair<uint32_t, int64_t>> xr;
+  std::vector<uint32_t> sets(n);
+  // term classes held until the bound counts are applied (released on every return)
+  struct Hold {
+    ks_ctx *c;
+    std::vector<uint32_t> v;
+    ~Hold() {
+      for (uint32_t t : v) term_activate(c, t, 0, -1);
+    }
+  } hold{c, {}};
   for (uint32_t i = 0; i < n; ++i) {
     if (slots[i] >= c->cap || !c->nodes[slots[i]].present)
       return c->fail(KS_ERR_NOT_FOUND, "slot %u not present", slots[i]);
     int64_t rc, rm, zc, zm;
     ks_status st;
+    if ((st = intern_set(c, pods[i], &sets[i], &hold.v))) return st;
     if ((st = pod_requests(pods[i], false, &rc, &rm)) || (st = pod_requests(pods[i], true, &zc, &zm)))
       return c->fail(st, "pod requests a resource it cannot express (KS_REQ_HAS_OTHER)");
     if ((st = pod_xrequests(c, pods[i], true, &xr))) return st;
@@ -2671,7 +3080,7 @@ static ks_status pods_delta(ks_ctx *c, const ks_pod *pods, const uint32_t *slots
   c->affinity_pods += aff;
   if ((st = xfer_sync(c))) return st;
   if ((st = xres_scatter(c, xidx, xval, true))) return st;
-  return spread_pods_delta(c, pods, slots, n, sign);
+  return spread_pods_delta(c, sets.data(), slots, n, sign);
 }
 
 ks_status ks_pods_add(ks_ctx *c, const ks_pod *pods, const uint32_t *slots, uint32_t n) {
@@ -2727,9 +3136,10 @@ static ks_status compile_batch(ks_ctx *c, const ks_pod *pods, uint32_t n, PodDev
   for (int attempt = 0;; ++attempt) {
     cl.w.clear();
     c->compile_used_names = false;
-    if (class_refs) class_refs->clear();
+    if (class_refs) class_release(c, class_refs);
     ks_status st = KS_OK;
     for (uint32_t i = 0; i < n && !st; ++i) st = compile_pod(c, pods[i], dev[i], cl, create_spread, class_refs);
+    if (st && class_refs) class_release(c, class_refs);
     if (st != KS_ERR_CAPACITY || attempt > 0 || c->next_bit == 0) return st;
     lk.unlock();
     drain_async(c);
@@ -2774,26 +3184,40 @@ ks_status ks_batch_prepare(ks_ctx *c, const ks_pod *pods, uint32_t n, ks_batch *
     for (uint32_t i = 0; i < n && !any_solo; ++i) any_solo = may_need_solo(c, pods[i]);
   }
   if (any_solo) drain_async(c);
-  std::vector<uint32_t> set_ids(n), refs;
+  std::vector<uint32_t> set_ids(n), refs, term_refs;
   {
     // compile against the host dictionaries (the worker reads t.lw and the
     // dirty label rows under mu)
     std::unique_lock<std::mutex> g(c->mu);
-    if ((st = compile_batch(c, pods, n, dev.data(), cl, g, true, &refs))) return st;
+    // label sets first: they create the term classes of the pods' own terms,
+    // which every later pod of the batch that they select must see
+    st = KS_OK;
+    for (uint32_t i = 0; i < n && !st; ++i) st = intern_set(c, pods[i], &set_ids[i], &term_refs);
+    if (st) {
+      for (uint32_t t : term_refs) term_activate(c, t, 0, -1);
+      return st;
+    }
+    if ((st = compile_batch(c, pods, n, dev.data(), cl, g, true, &refs))) {
+      for (uint32_t t : term_refs) term_activate(c, t, 0, -1);
+      return st;
+    }
     for (uint32_t i = 0; i < n; ++i) {
       if (dev[i].flags & PF_SOLO) continue;  // the one-pod path evaluates it
       if (dev[i].flags & PF_EXT) ext = true;
       if (dev[i].flags & (PF_TT | PF_NA)) norm = true;
     }
-    for (uint32_t i = 0; i < n; ++i) set_ids[i] = intern_set(c, pods[i]);
-    for (uint32_t k : refs) c->classes[k].refs++;
     dict_v = c->dict_version;
     names_v = c->compile_used_names ? c->names_version : 0;
   }
   if (norm) ext = true;
   if (cl.w.empty()) cl.w.push_back(0);
   ks_batch *b = nullptr;
-  if ((st = batch_acquire(c, n, cl.w.size(), &b))) return st;
+  if ((st = batch_acquire(c, n, cl.w.size(), &b))) {
+    std::lock_guard<std::mutex> g(c->mu);
+    class_release(c, &refs);
+    for (uint32_t t : term_refs) term_activate(c, t, 0, -1);
+    return st;
+  }
   b->n = n;
   b->ext = ext;
   b->norm = norm;
@@ -2802,15 +3226,13 @@ ks_status ks_batch_prepare(ks_ctx *c, const ks_pod *pods, uint32_t n, ks_batch *
   b->n_words = cl.w.size();
   b->set_ids = std::move(set_ids);
   b->class_refs = std::move(refs);
+  b->term_refs = std::move(term_refs);
   b->spread.assign(n, 0);
   b->any_spread = false;
   for (uint32_t i = 0; i < n; ++i) {
     if (!(dev[i].flags & PF_SOLO)) continue;
     const SoloHdr *hd = reinterpret_cast<const SoloHdr *>(cl.w.data() + dev[i].solo_off);
-    const SpreadDev *sd = reinterpret_cast<const SpreadDev *>(hd + 1);
-    uint8_t f = 1;
-    for (uint32_t k = 0; k < hd->n_spread; ++k) f |= (sd[k].flags & SP_SCORE) ? 4 : 2;
-    b->spread[i] = f;
+    b->spread[i] = (uint8_t)(0x80u | solo_passes(hd));
     b->any_spread = true;
   }
   std::memcpy(b->h_pods, dev.data(), dev.size() * sizeof(PodDev));
@@ -2899,9 +3321,9 @@ void ks_batch_free(ks_ctx *c, ks_batch *b) {
   }
   {
     std::lock_guard<std::mutex> g(c->mu);
-    for (uint32_t k : b->class_refs)
-      if (c->classes[k].refs) c->classes[k].refs--;
-    b->class_refs.clear();
+    class_release(c, &b->class_refs);
+    for (uint32_t t : b->term_refs) term_activate(c, t, 0, -1);
+    b->term_refs.clear();
   }
   batch_release(c, b);
 }
@@ -2937,6 +3359,9 @@ SpreadArgs spread_args(ks_ctx *c) {
   sa.xreq = c->d_xreq;
   sa.dcnt = c->d_dcnt;
   sa.dflag = c->d_dflag;
+  sa.tcnt = c->d_tcnt;
+  sa.adcnt = c->d_adcnt;
+  sa.ipa_raw = c->d_sraw2;
   sa.dom_cap = c->dom_cap;
   sa.acc = c->d_acc;
   sa.st = c->d_sst;
@@ -2946,6 +3371,7 @@ SpreadArgs spread_args(ks_ctx *c) {
   sa.w = Weights{c->cfg.weight_fit, c->cfg.weight_balanced, c->cfg.weight_taint, c->cfg.weight_affinity,
                  c->cfg.weight_image};
   sa.w_pts = c->cfg.weight_topology_spread;
+  sa.w_ipa = c->cfg.weight_inter_pod_affinity;
   sa.evaluated = c->n_present;
   return sa;
 }
@@ -2966,11 +3392,8 @@ ks_status spread_plugin_scores(ks_ctx *c, const PodDev &d, const ProgBuf &cl, ks
   sa.pod = 0;
   sa.dump = d_out;
   sa.no_commit = 1;
-  bool has_filter = false, has_score = false;
   const SoloHdr *hd = reinterpret_cast<const SoloHdr *>(cl.w.data() + d.solo_off);
-  const SpreadDev *sd = reinterpret_cast<const SpreadDev *>(hd + 1);
-  for (uint32_t k = 0; k < hd->n_spread; ++k) ((sd[k].flags & SP_SCORE) ? has_score : has_filter) = true;
-  HIPC(c, launch_spread_pod(sa, has_filter, has_score, c->stream));
+  HIPC(c, launch_spread_pod(sa, solo_passes(hd), c->stream));
   if ((st = d2h(c, raw.data(), d_out, raw.size() * 4)) || (st = xfer_sync(c))) return st;
   for (uint32_t i = 0; i < c->cap; ++i) {
     const int32_t *o = &raw[(size_t)i * SPREAD_DUMP_WORDS];
@@ -2986,6 +3409,8 @@ ks_status spread_plugin_scores(ks_ctx *c, const PodDev &d, const ProgBuf &cl, ks
     s.spread_raw = o[8];
     s.spread_score = o[9];
     s.total_score = (int64_t)(((uint64_t)(uint32_t)o[11] << 32) | (uint32_t)o[10]);
+    s.affinity_pod_raw = o[12];
+    s.affinity_pod_score = o[13];
     out[i] = s;
   }
   return KS_OK;

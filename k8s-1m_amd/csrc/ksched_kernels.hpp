@@ -75,7 +75,11 @@ struct DumpArgs {
 
 // PodTopologySpread path (ksched_spread.hip): one pod per launch chain.
 constexpr uint32_t SLOT_NONE = 0xFFFFFFFFu;  // position holding no slot (shard padding)
-constexpr int SPREAD_DUMP_WORDS = 12;  // status, la, ba, tt raw/score, na raw/score, il, pts raw/score, total lo/hi
+// status, la, ba, tt raw/score, na raw/score, il, pts raw/score, total lo/hi, ipa raw/score
+constexpr int SPREAD_DUMP_WORDS = 14;
+// launch_spread_pod passes: prep (PodTopologySpread DoNotSchedule counts,
+// InterPodAffinity domain counts), min (criticalPaths), score (ScheduleAnyway)
+enum SpreadLaunch : uint32_t { SPL_PREP = 1u, SPL_MIN = 2u, SPL_SCORE = 4u };
 struct SpreadArgs {
   NodeTable t;
   const uint32_t *pos_slot;   // position -> slot (SLOT_NONE: padding)
@@ -84,12 +88,15 @@ struct SpreadArgs {
   uint32_t pod;               // index of the pod in the batch
   const PodDev *pods;
   const uint64_t *clauses;    // label programs + SpreadDev records
-  const uint64_t *cmask;      // [npods] selector classes each pod of the batch matches
+  const uint64_t *cmask;      // [npods][CMASK_WORDS] selector classes each pod of the batch matches
   const uint32_t *dom;        // [MAX_TOPO_KEYS][npos] domain id per position (DOM_NONE: key absent)
   uint32_t *cnt;              // [MAX_CLASSES][npos] matching bound pods per position
   int64_t *xalloc, *xreq;     // [MAX_XRES][npos] extended resources: Allocatable, Requested
   uint32_t *dcnt;             // [MAX_SPREAD][dom_cap] per-constraint domain counts (zero between pods)
   uint32_t *dflag;            // [MAX_SPREAD][dom_cap] bit 0 Filter-eligible domain, bit 1 Score domain
+  uint32_t *tcnt;             // [MAX_TERM_CLASSES][npos] bound pods carrying each term class
+  uint32_t *adcnt;            // [MAX_AFF][dom_cap] InterPodAffinity domain counts per record (zero between pods)
+  int64_t *ipa_raw;           // [npos] InterPodAffinity raw score (filter -> select)
   uint32_t dom_cap;
   uint32_t ndom[MAX_TOPO_KEYS];  // domain ids of every topology-key column (at launch)
   SpreadAcc *acc;
@@ -101,11 +108,11 @@ struct SpreadArgs {
   uint32_t no_commit;         // dump / reset: no result, no AssumePod
   uint64_t *counters;
   Weights w;
-  int32_t w_pts;
+  int32_t w_pts, w_ipa;
   uint32_t evaluated;         // present nodes
 };
 
-hipError_t launch_spread_pod(const SpreadArgs &a, bool has_filter, bool has_score, hipStream_t st);
+hipError_t launch_spread_pod(const SpreadArgs &a, uint32_t passes, hipStream_t st);
 hipError_t launch_spread_reset(const SpreadArgs &a, hipStream_t st);
 hipError_t launch_class_commit(const DevResult *res, const uint64_t *cmask, const uint32_t *slot_pos, uint32_t *cnt,
                                uint32_t npos, uint32_t lo, uint32_t hi, hipStream_t st);

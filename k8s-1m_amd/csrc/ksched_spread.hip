@@ -19,7 +19,15 @@
 //   spread_select  total score of every feasible node, NormalizeScore,
 //                  packed-key argmax; clears the domain scratch
 //   spread_commit  the result and AssumePod (resources, pod count, the bound
-//                  pod's selector-class counts)
+//                  pod's selector-class and term-class counts)
+//
+// InterPodAffinity (interpodaffinity/filtering.go, scoring.go) rides the same
+// chain: spread_prep sums each AffDev record's count column per topology
+// domain over every node (PreFilter's affinity / anti-affinity /
+// existing-anti-affinity counts, PreScore's topologyScore), spread_filter
+// checks them (satisfyPodAffinity, satisfyPodAntiAffinity,
+// satisfyExistingPodsAntiAffinity) and takes the raw score, spread_select
+// normalises it (float64 min-max, as NormalizeScore).
 //
 // Domain counts are aggregated per block in LDS for low-cardinality keys
 // (zones), with global atomics only for high-cardinality ones (hostnames).
@@ -52,6 +60,48 @@ __device__ __forceinline__ const XResDev *xres_recs(const SpreadArgs &a, const P
 }
 __device__ __forceinline__ const ImageDev *image_recs(const SpreadArgs &a, const PodDev &p) {
   return reinterpret_cast<const ImageDev *>(xres_recs(a, p) + solo_hdr(a, p).n_xres);
+}
+__device__ __forceinline__ const AffDev *aff_recs(const SpreadArgs &a, const PodDev &p) {
+  return reinterpret_cast<const AffDev *>(image_recs(a, p) + solo_hdr(a, p).n_img);
+}
+// Count column of an InterPodAffinity record at a position.
+__device__ __forceinline__ uint32_t aff_count(const SpreadArgs &a, const AffDev &r, uint32_t pos) {
+  return ((r.kind & AF_TERM) ? a.tcnt : a.cnt)[(size_t)r.col * a.npos + pos];
+}
+constexpr uint64_t IPA_BIAS = 1ull << 63;  // signed raw scores as unsigned min / max keys
+
+// interpodaffinity Filter over the prefilter domain counts: every required
+// affinity key present and its domain holding a pod that matches all the
+// required affinity terms (unless no such pod exists anywhere and the pod
+// matches its own terms), no required anti-affinity match in the node's
+// domains, no bound pod's required anti-affinity term matching the pod there.
+__device__ __forceinline__ bool ipa_fits(const SpreadArgs &a, const AffDev *ad, uint32_t na, uint32_t pos,
+                                         bool first_ok) {
+  bool has_req = false, exist = true;
+  for (uint32_t r = 0; r < na; ++r) {
+    const uint32_t kind = ad[r].kind & AF_KIND;
+    if (kind > AF_EXIST_ANTI) continue;
+    const uint32_t d = a.dom[(size_t)ad[r].key * a.npos + pos];
+    if (kind == AF_REQ_AFF) {
+      has_req = true;
+      if (d == DOM_NONE) return false;  // all topology labels must exist on the node
+      if (!a.adcnt[(size_t)r * a.dom_cap + d]) exist = false;
+    } else if (d != DOM_NONE && a.adcnt[(size_t)r * a.dom_cap + d]) {
+      return false;
+    }
+  }
+  return !has_req || exist || first_ok;
+}
+
+// interpodaffinity Score: Σ topologyScore[key][node's value].
+__device__ __forceinline__ int64_t ipa_raw_score(const SpreadArgs &a, const AffDev *ad, uint32_t na, uint32_t pos) {
+  int64_t raw = 0;
+  for (uint32_t r = 0; r < na; ++r) {
+    if ((ad[r].kind & AF_KIND) != AF_SCORE) continue;
+    const uint32_t d = a.dom[(size_t)ad[r].key * a.npos + pos];
+    if (d != DOM_NONE) raw += (int64_t)ad[r].weight * (int64_t)a.adcnt[(size_t)r * a.dom_cap + d];
+  }
+  return raw;
 }
 
 // imagelocality#calculatePriority over sumImageScores of the node (label bits
@@ -127,13 +177,21 @@ __device__ __forceinline__ uint64_t wave_min64(uint64_t v) {
   return v;
 }
 
-// LDS segments of the low-cardinality constraints (thread 0; caller syncs).
-__device__ void lds_segments(const SpreadArgs &a, const SpreadDev *sd, uint32_t n, uint32_t *off) {
+// LDS segments of the low-cardinality constraints (thread 0; caller syncs);
+// with `aoff`, then of the InterPodAffinity records the prep pass sums.
+__device__ void lds_segments(const SpreadArgs &a, const SpreadDev *sd, uint32_t n, uint32_t *off,
+                             const AffDev *ad = nullptr, uint32_t na = 0, uint32_t *aoff = nullptr) {
   uint32_t o = 0;
   for (uint32_t c = 0; c < n; ++c) {
     const uint32_t nd = a.ndom[sd[c].key];
     const bool small = nd <= SP_LDS_DOM && o + nd <= SP_LDS;
     off[c] = small ? o : SP_OFF_NONE;
+    if (small) o += nd;
+  }
+  for (uint32_t r = 0; r < na; ++r) {
+    const uint32_t nd = a.ndom[ad[r].key];
+    const bool small = (ad[r].kind & AF_KIND) != AF_OWN && nd <= SP_LDS_DOM && o + nd <= SP_LDS;
+    aoff[r] = small ? o : SP_OFF_NONE;
     if (small) o += nd;
   }
 }
@@ -142,16 +200,18 @@ __device__ __forceinline__ uint32_t grid_threads() { return gridDim.x * blockDim
 
 // Totals of the accumulator copies (ACC_SHARDS) written by the previous passes.
 struct Totals {
-  uint32_t fail[NFILT + 1];
+  uint32_t fail[NFILT + 2];
   uint32_t feasible, ignored, tt_max, na_max;
-  uint64_t pts_min, pts_max, best;
+  uint64_t pts_min, pts_max, ipa_min, ipa_max, best;
 };
 __device__ __forceinline__ Totals acc_totals(const SpreadAcc *acc) {
   Totals t{};
-  t.pts_min = ~0ull;
+  t.pts_min = t.ipa_min = ~0ull;
   for (int k = 0; k < ACC_SHARDS; ++k) {
     const SpreadAccShard &q = acc->sh[k];
-    for (int f = 0; f <= NFILT; ++f) t.fail[f] += q.fail[f];
+    for (int f = 0; f < NFILT + 2; ++f) t.fail[f] += q.fail[f];
+    t.ipa_min = min(t.ipa_min, q.ipa_min);
+    t.ipa_max = max(t.ipa_max, q.ipa_max);
     t.feasible += q.feasible;
     t.ignored += q.ignored;
     t.tt_max = max(t.tt_max, q.tt_max);
@@ -172,14 +232,19 @@ __device__ __forceinline__ SpreadAccShard &acc_shard(const SpreadArgs &a) { retu
 // constraint's inclusion policies), dflag[c][d] bit 0 = d has an eligible
 // node.  (The ScheduleAnyway counts are taken by the filter pass, which
 // visits every node anyway.)  Launched only for pods with DoNotSchedule
-// constraints.
+// constraints.  InterPodAffinity: adcnt[r][d] = Σ count column of record r
+// over every node of domain d (any node: upstream's PreFilter / PreScore walk
+// all nodes), aff_any / score_any = some affinityCounts / topologyScore entry.
 __global__ __launch_bounds__(SP_THREADS) void spread_prep_kernel(SpreadArgs a) {
   __shared__ uint32_t s_h[SP_LDS];
   __shared__ uint32_t s_off[MAX_SPREAD];
+  __shared__ uint32_t s_aoff[MAX_AFF];
   const PodDev p = a.pods[a.pod];
   const SpreadDev *sd = spread_recs(a, p);
   const uint32_t n = spread_count(a, p);
-  if (threadIdx.x == 0) lds_segments(a, sd, n, s_off);
+  const AffDev *ad = aff_recs(a, p);
+  const uint32_t na = solo_hdr(a, p).n_aff;
+  if (threadIdx.x == 0) lds_segments(a, sd, n, s_off, ad, na, s_aoff);
   for (uint32_t i = threadIdx.x; i < SP_LDS; i += SP_THREADS) s_h[i] = 0;
   __syncthreads();
   bool aff_needed = false, taint_needed = false;
@@ -188,9 +253,23 @@ __global__ __launch_bounds__(SP_THREADS) void spread_prep_kernel(SpreadArgs a) {
     aff_needed |= (sd[c].flags & SP_AFF) && (p.flags & PF_AFF);
     taint_needed |= (sd[c].flags & SP_TAINT) != 0;
   }
+  bool any_aff = false, any_score = false;
   for (uint32_t pos = blockIdx.x * SP_THREADS + threadIdx.x; pos < a.npos; pos += grid_threads()) {
     const uint32_t slot = a.pos_slot[pos];
     if (slot == SLOT_NONE || a.t.apods[pos] < 0) continue;
+    for (uint32_t r = 0; r < na; ++r) {
+      const AffDev &q = ad[r];
+      const uint32_t kind = q.kind & AF_KIND;
+      if (kind == AF_OWN) continue;
+      const uint32_t v = aff_count(a, q, pos);
+      if (!v) continue;
+      const uint32_t d = a.dom[(size_t)q.key * a.npos + pos];
+      if (d == DOM_NONE) continue;  // no topology pair for this node
+      any_aff |= kind == AF_REQ_AFF;
+      any_score |= kind == AF_SCORE;
+      if (s_aoff[r] != SP_OFF_NONE) atomicAdd(&s_h[s_aoff[r] + d], v);
+      else atomicAdd(&a.adcnt[(size_t)r * a.dom_cap + d], v);
+    }
     NodeExt e;
     if (aff_needed || taint_needed) load_ext(a.t, pos, true, e);
     const bool aff_ok = !aff_needed || required_match(p, a.clauses, e, slot);
@@ -214,13 +293,25 @@ __global__ __launch_bounds__(SP_THREADS) void spread_prep_kernel(SpreadArgs a) {
       }
     }
   }
-  __syncthreads();
+  const int blk_aff = __syncthreads_or(any_aff ? 1 : 0);
+  const int blk_score = __syncthreads_or(any_score ? 1 : 0);
+  if (threadIdx.x == 0) {
+    if (blk_aff) atomicOr(&a.acc->aff_any, 1u);
+    if (blk_score) atomicOr(&a.acc->score_any, 1u);
+  }
   for (uint32_t c = 0; c < n; ++c) {
     if (s_off[c] == SP_OFF_NONE) continue;
     for (uint32_t d = threadIdx.x; d < a.ndom[sd[c].key]; d += SP_THREADS) {
       const uint32_t v = s_h[s_off[c] + d];
       if (v & 0x7FFFFFFFu) atomicAdd(&a.dcnt[(size_t)c * a.dom_cap + d], v & 0x7FFFFFFFu);
       if (v >> 31) atomicOr(&a.dflag[(size_t)c * a.dom_cap + d], 1u);
+    }
+  }
+  for (uint32_t r = 0; r < na; ++r) {
+    if (s_aoff[r] == SP_OFF_NONE) continue;
+    for (uint32_t d = threadIdx.x; d < a.ndom[ad[r].key]; d += SP_THREADS) {
+      const uint32_t v = s_h[s_aoff[r] + d];
+      if (v) atomicAdd(&a.adcnt[(size_t)r * a.dom_cap + d], v);
     }
   }
 }
@@ -279,11 +370,16 @@ __device__ __forceinline__ uint64_t pack_part(uint32_t base, uint32_t tt_raw, ui
   return (uint64_t)base | ((uint64_t)(tt_raw & 0xFFu) << 32) | ((uint64_t)(na_raw & 0xFFFFFFu) << 40);
 }
 
+// Block-reduction slots of the filter pass: first failures per plugin, then
+// feasible / ignored counts and the normaliser maxima.
+constexpr int RF = NFILT + 2, R_FEAS = RF, R_IGN = RF + 1, R_TT = RF + 2, R_NA = RF + 3, R_N = RF + 4;
+
 __global__ __launch_bounds__(SP_THREADS) void spread_filter_kernel(SpreadArgs a) {
   __shared__ uint32_t s_seen[SP_LDS / 32];
   __shared__ uint32_t s_h[SP_LDS];
   __shared__ uint32_t s_off[MAX_SPREAD];
-  __shared__ uint32_t s_red[SP_THREADS / WAVE][NFILT + 5];
+  __shared__ uint32_t s_red[SP_THREADS / WAVE][R_N];
+  __shared__ uint64_t s_r64[SP_THREADS / WAVE][2];
   const PodDev p = a.pods[a.pod];
   const SpreadDev *sd = spread_recs(a, p);
   const uint32_t n = spread_count(a, p);
@@ -292,6 +388,12 @@ __global__ __launch_bounds__(SP_THREADS) void spread_filter_kernel(SpreadArgs a)
   for (uint32_t i = threadIdx.x; i < SP_LDS; i += SP_THREADS) s_h[i] = 0;
   __syncthreads();
   const uint32_t n_xres = solo_hdr(a, p).n_xres;
+  const AffDev *ad = aff_recs(a, p);
+  const uint32_t na = solo_hdr(a, p).n_aff;
+  bool ipa_filter = false;
+  for (uint32_t r = 0; r < na; ++r) ipa_filter |= (ad[r].kind & AF_KIND) <= AF_EXIST_ANTI;
+  const bool ipa_first_ok = !a.acc->aff_any && (solo_hdr(a, p).aff_flags & AFF_SELF);
+  const bool ipa_score = a.acc->score_any != 0;
   bool any_s = false, aff_needed = false, taint_needed = false;
   for (uint32_t c = 0; c < n; ++c) {
     if (!(sd[c].flags & SP_SCORE)) continue;
@@ -301,8 +403,9 @@ __global__ __launch_bounds__(SP_THREADS) void spread_filter_kernel(SpreadArgs a)
   }
   const bool allkeys = p.flags & PF_SPREAD_ALLKEYS;
   const uint32_t lane = threadIdx.x % WAVE, wid = threadIdx.x / WAVE;
-  uint32_t fails[NFILT + 1] = {0, 0, 0, 0, 0, 0};
+  uint32_t fails[RF] = {0, 0, 0, 0, 0, 0, 0};
   uint32_t feasible = 0, ignored = 0, tt_max = 0, na_max = 0;
+  uint64_t ipa_mn = ~0ull, ipa_mx = 0;
   for (uint32_t pos = blockIdx.x * SP_THREADS + threadIdx.x; pos < a.npos; pos += grid_threads()) {
     const uint32_t slot = a.pos_slot[pos];
     if (slot == SLOT_NONE) continue;
@@ -360,6 +463,7 @@ __global__ __launch_bounds__(SP_THREADS) void spread_filter_kernel(SpreadArgs a)
         }
       }
     }
+    if (s == ST_FEASIBLE && ipa_filter && !ipa_fits(a, ad, na, pos, ipa_first_ok)) s = PLUGIN_IPA;
     int8_t out = (int8_t)s;
     if (s == ST_FEASIBLE) {
       ++feasible;
@@ -370,6 +474,13 @@ __global__ __launch_bounds__(SP_THREADS) void spread_filter_kernel(SpreadArgs a)
       a.part[pos] = pack_part((uint32_t)a.w.fit * (uint32_t)score_la(p, r) + (uint32_t)a.w.ba * (uint32_t)score_ba(p, r) +
                                   (uint32_t)a.w.il * (uint32_t)image_score(a, p, e),
                               tr, nr);
+      if (ipa_score) {
+        const int64_t raw = ipa_raw_score(a, ad, na, pos);
+        a.ipa_raw[pos] = raw;
+        const uint64_t k = (uint64_t)raw + IPA_BIAS;
+        ipa_mn = min(ipa_mn, k);
+        ipa_mx = max(ipa_mx, k);
+      }
       // PreScore (initPreScoreState): with requireAllTopologies a node lacking
       // a ScheduleAnyway key is ignored; the others' domains make topoSize
       if (allkeys && !all_s) {
@@ -392,20 +503,25 @@ __global__ __launch_bounds__(SP_THREADS) void spread_filter_kernel(SpreadArgs a)
       }
     } else {
 #pragma unroll
-      for (int q = 0; q <= NFILT; ++q) fails[q] += s == q ? 1u : 0u;  // ST_PREFILTERED: no plugin
+      for (int q = 0; q < RF; ++q) fails[q] += s == q ? 1u : 0u;  // ST_PREFILTERED: no plugin
     }
     a.st[pos] = out;
   }
   // block reduction: counts, maxima
-  uint32_t v[NFILT + 5];
+  uint32_t v[R_N];
 #pragma unroll
-  for (int q = 0; q <= NFILT; ++q) v[q] = wave_sum(fails[q]);
-  v[NFILT + 1] = wave_sum(feasible);
-  v[NFILT + 2] = wave_sum(ignored);
-  v[NFILT + 3] = wave_max(tt_max);
-  v[NFILT + 4] = wave_max(na_max);
-  if (lane == 0)
-    for (int q = 0; q < NFILT + 5; ++q) s_red[wid][q] = v[q];
+  for (int q = 0; q < RF; ++q) v[q] = wave_sum(fails[q]);
+  v[R_FEAS] = wave_sum(feasible);
+  v[R_IGN] = wave_sum(ignored);
+  v[R_TT] = wave_max(tt_max);
+  v[R_NA] = wave_max(na_max);
+  ipa_mn = wave_min64(ipa_mn);
+  ipa_mx = wave_max64(ipa_mx);
+  if (lane == 0) {
+    for (int q = 0; q < R_N; ++q) s_red[wid][q] = v[q];
+    s_r64[wid][0] = ipa_mn;
+    s_r64[wid][1] = ipa_mx;
+  }
   __syncthreads();
   // flush the block's ScheduleAnyway domain counts
   for (uint32_t c = 0; c < n; ++c) {
@@ -415,18 +531,27 @@ __global__ __launch_bounds__(SP_THREADS) void spread_filter_kernel(SpreadArgs a)
       if (v) atomicAdd(&a.dcnt[(size_t)c * a.dom_cap + d], v);
     }
   }
-  if (threadIdx.x < NFILT + 5) {
+  if (threadIdx.x < R_N) {
     const int q = threadIdx.x;
     uint32_t t = s_red[0][q];
-    for (int w = 1; w < SP_THREADS / WAVE; ++w) t = q >= NFILT + 3 ? max(t, s_red[w][q]) : t + s_red[w][q];
+    for (int w = 1; w < SP_THREADS / WAVE; ++w) t = q >= R_TT ? max(t, s_red[w][q]) : t + s_red[w][q];
     SpreadAccShard &bp = acc_shard(a);
     if (t) {
-      if (q <= NFILT) atomicAdd(&bp.fail[q], t);
-      else if (q == NFILT + 1) atomicAdd(&bp.feasible, t);
-      else if (q == NFILT + 2) atomicAdd(&bp.ignored, t);
-      else if (q == NFILT + 3) atomicMax(&bp.tt_max, t);
+      if (q < RF) atomicAdd(&bp.fail[q], t);
+      else if (q == R_FEAS) atomicAdd(&bp.feasible, t);
+      else if (q == R_IGN) atomicAdd(&bp.ignored, t);
+      else if (q == R_TT) atomicMax(&bp.tt_max, t);
       else atomicMax(&bp.na_max, t);
     }
+  } else if (threadIdx.x == R_N && ipa_score) {
+    uint64_t mn = s_r64[0][0], mx = s_r64[0][1];
+    for (int w = 1; w < SP_THREADS / WAVE; ++w) {
+      mn = min(mn, s_r64[w][0]);
+      mx = max(mx, s_r64[w][1]);
+    }
+    SpreadAccShard &bp = acc_shard(a);
+    if (mn != ~0ull) atomicMin((unsigned long long *)&bp.ipa_min, (unsigned long long)mn);
+    if (mx) atomicMax((unsigned long long *)&bp.ipa_max, (unsigned long long)mx);
   }
 }
 
@@ -502,6 +627,8 @@ __global__ __launch_bounds__(SP_THREADS) void spread_select_kernel(SpreadArgs a)
   const Totals tot = acc_totals(a.acc);
   const int64_t tt_max = tot.tt_max, na_max = tot.na_max;
   const int64_t pmin = (int64_t)tot.pts_min, pmax = (int64_t)tot.pts_max;
+  const bool ipa_on = a.acc->score_any != 0;
+  const int64_t imin = (int64_t)(tot.ipa_min - IPA_BIAS), idiff = (int64_t)(tot.ipa_max - tot.ipa_min);
   uint64_t best = 0;
   for (uint32_t pos = blockIdx.x * SP_THREADS + threadIdx.x; pos < a.npos; pos += grid_threads()) {
     const int8_t s = a.st[pos];
@@ -534,6 +661,13 @@ __global__ __launch_bounds__(SP_THREADS) void spread_select_kernel(SpreadArgs a)
       total += (int64_t)a.w.na * na;
     }
     if (has_score) total += (int64_t)a.w_pts * norm;
+    // InterPodAffinity NormalizeScore: int64(MaxNodeScore * float64(s - min) / float64(max - min))
+    int64_t ipa_raw = 0, ipa = 0;
+    if (ipa_on) {
+      ipa_raw = a.ipa_raw[pos];
+      if (idiff > 0) ipa = (int64_t)(100.0 * ((double)(ipa_raw - imin) / (double)idiff));
+    }
+    total += (int64_t)a.w_ipa * ipa;
     if (a.dump) {
       NodeRegs r;
       load_core(a.t, pos, slot, true, r);
@@ -554,6 +688,8 @@ __global__ __launch_bounds__(SP_THREADS) void spread_select_kernel(SpreadArgs a)
       o[9] = (int32_t)norm;
       o[10] = (int32_t)(total & 0xFFFFFFFF);
       o[11] = (int32_t)(total >> 32);
+      o[12] = (int32_t)ipa_raw;
+      o[13] = (int32_t)ipa;
     }
     const uint64_t k = pack_key(total, slot);
     best = k > best ? k : best;
@@ -573,6 +709,11 @@ __global__ __launch_bounds__(SP_THREADS) void spread_select_kernel(SpreadArgs a)
       a.dcnt[(size_t)c * a.dom_cap + d] = 0;
       a.dflag[(size_t)c * a.dom_cap + d] = 0;
     }
+  const AffDev *ad = aff_recs(a, p);
+  for (uint32_t r = 0; r < solo_hdr(a, p).n_aff; ++r)
+    if ((ad[r].kind & AF_KIND) != AF_OWN)
+      for (uint32_t d = blockIdx.x * SP_THREADS + threadIdx.x; d < a.ndom[ad[r].key]; d += grid_threads())
+        a.adcnt[(size_t)r * a.dom_cap + d] = 0;
 }
 
 // ---------------------------------------------------------------- commit
@@ -593,7 +734,7 @@ __global__ void spread_commit_kernel(SpreadArgs a) {
   r.evaluated_nodes = a.evaluated;
   for (int q = 0; q < NFILT; ++q) r.fail_counts[q] = tot.fail[q];
   r.spread_fail = tot.fail[PLUGIN_SPREAD];
-  r.ipa_fail = 0;
+  r.ipa_fail = tot.fail[PLUGIN_IPA];
   r._pad = 0;
   r.prefiltered = p.prefilter_out;
   r.flags = 0;
@@ -618,12 +759,17 @@ __global__ void spread_commit_kernel(SpreadArgs a) {
         a.t.npods[pos] += 1;
         const XResDev *xr = xres_recs(a, p);
         for (uint32_t k = 0; k < solo_hdr(a, p).n_xres; ++k) a.xreq[(size_t)xr[k].col * a.npos + pos] += xr[k].req;
-        uint64_t m = a.cmask[a.pod];
-        while (m) {
-          const uint32_t cls = (uint32_t)__builtin_ctzll(m);
-          m &= m - 1;
-          a.cnt[(size_t)cls * a.npos + pos] += 1;
+        for (int w = 0; w < CMASK_WORDS; ++w) {
+          uint64_t m = a.cmask[(size_t)a.pod * CMASK_WORDS + w];
+          while (m) {
+            const uint32_t cls = 64 * w + (uint32_t)__builtin_ctzll(m);
+            m &= m - 1;
+            a.cnt[(size_t)cls * a.npos + pos] += 1;
+          }
         }
+        const AffDev *ad = aff_recs(a, p);
+        for (uint32_t k = 0; k < solo_hdr(a, p).n_aff; ++k)
+          if ((ad[k].kind & AF_KIND) == AF_OWN) a.tcnt[(size_t)ad[k].col * a.npos + pos] += (uint32_t)ad[k].weight;
         a.counters[1] += 1;  // pods resolved
       }
     }
@@ -636,12 +782,13 @@ __global__ void spread_commit_kernel(SpreadArgs a) {
     acc.ndomains[c] = 0;
     acc.topo_size[c] = 0;
   }
+  acc.aff_any = acc.score_any = 0;
   for (int k = 0; k < ACC_SHARDS; ++k) {
     SpreadAccShard &q = acc.sh[k];
-    for (int f = 0; f <= NFILT; ++f) q.fail[f] = 0;
+    for (int f = 0; f < NFILT + 2; ++f) q.fail[f] = 0;
     q.feasible = q.ignored = q.tt_max = q.na_max = 0;
-    q.pts_min = ~0ull;
-    q.pts_max = 0;
+    q.pts_min = q.ipa_min = ~0ull;
+    q.pts_max = q.ipa_max = 0;
     q.best = 0;
   }
 }
@@ -651,13 +798,15 @@ __global__ void class_commit_kernel(const DevResult *res, const uint64_t *cmask,
                                     uint32_t *cnt, uint32_t npos, uint32_t lo, uint32_t hi) {
   const uint32_t i = lo + blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= hi) return;
-  uint64_t m = cmask[i];
-  if (!m || res[i].status != 0) return;
+  if (res[i].status != 0) return;
   const uint32_t pos = slot_pos[res[i].node_index];
-  while (m) {
-    const uint32_t cls = (uint32_t)__builtin_ctzll(m);
-    m &= m - 1;
-    atomicAdd(&cnt[(size_t)cls * npos + pos], 1u);
+  for (int w = 0; w < CMASK_WORDS; ++w) {
+    uint64_t m = cmask[(size_t)i * CMASK_WORDS + w];
+    while (m) {
+      const uint32_t cls = 64 * w + (uint32_t)__builtin_ctzll(m);
+      m &= m - 1;
+      atomicAdd(&cnt[(size_t)cls * npos + pos], 1u);
+    }
   }
 }
 
@@ -679,16 +828,14 @@ __global__ void scatter_i64_kernel(int64_t *col, const uint64_t *idx, const int6
 
 // ------------------------------------------------------------- launchers
 
-hipError_t launch_spread_pod(const SpreadArgs &args, bool has_filter, bool has_score, hipStream_t st) {
+hipError_t launch_spread_pod(const SpreadArgs &args, uint32_t passes, hipStream_t st) {
   const uint32_t blocks =
       std::max<uint32_t>(1, std::min<uint32_t>((args.npos + SP_THREADS - 1) / SP_THREADS, SPREAD_MAX_BLOCKS));
   const SpreadArgs &a = args;
-  if (has_filter) {
-    spread_prep_kernel<<<blocks, SP_THREADS, 0, st>>>(a);
-    spread_min_kernel<<<blocks, SP_THREADS, 0, st>>>(a);
-  }
+  if (passes & SPL_PREP) spread_prep_kernel<<<blocks, SP_THREADS, 0, st>>>(a);
+  if (passes & SPL_MIN) spread_min_kernel<<<blocks, SP_THREADS, 0, st>>>(a);
   spread_filter_kernel<<<blocks, SP_THREADS, 0, st>>>(a);
-  if (has_score) spread_score_kernel<<<blocks, SP_THREADS, 0, st>>>(a);
+  if (passes & SPL_SCORE) spread_score_kernel<<<blocks, SP_THREADS, 0, st>>>(a);
   spread_select_kernel<<<blocks, SP_THREADS, 0, st>>>(a);
   spread_commit_kernel<<<1, WAVE, 0, st>>>(a);
   return hipGetLastError();

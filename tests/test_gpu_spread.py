@@ -336,3 +336,123 @@ def test_resources_images_random_stream(seed, n, P):
         x.delete([slots[1]])
         x.dump_equal(rand_res_pod(rng, 90_000 + b), f"seed {seed} dump {b}")
     x.close()
+
+
+# ------------------------------------------------------------ InterPodAffinity
+
+@pytest.mark.parametrize("name", sorted(__import__("ipa_cases").CASES))
+@pytest.mark.parametrize("P", [256, 2])
+def test_ipa_case_gpu(name, P):
+    from ipa_cases import CASES as IPA
+    nodes, bound, pods, exp, dumps = IPA[name]()
+    x = Pair(len(nodes), pods_per_round=P)
+    x.upsert(nodes, list(range(len(nodes))))
+    x.add([p for p, _ in bound], [s for _, s in bound])
+    for j, p in enumerate(pods):
+        if j in dumps:
+            out = x.dump_equal(p, f"{name} dump {j}")
+            assert [(out[i].affinity_pod_raw, out[i].affinity_pod_score) for i in range(len(nodes))] == dumps[j]
+    r = x.schedule(pods, name)
+    check(r, exp)
+    x.states_equal(name)
+    x.close()
+
+
+def rand_term(rng, kinds=("affinity", "anti-affinity", "preferred-affinity", "preferred-anti-affinity")):
+    from ksched.objects import PodAffinityTerm
+    kind = rng.choice(kinds)
+    r = rng.random()
+    ns, nsel = [], None
+    if r < 0.15:
+        ns = rng.sample(NSS, rng.randint(1, 2))
+    elif r < 0.25:
+        nsel = LabelSelector({"team": "blue"}) if rng.random() < 0.7 else LabelSelector()
+    sel = rand_selector(rng) if rng.random() < 0.5 else LabelSelector({"app": rng.choice(APPS)})
+    return PodAffinityTerm(rng.choice([ZONE, HOST, "rack"]), sel, ns, nsel, kind,
+                           rng.randint(1, 100) if kind.startswith("preferred") else 0)
+
+
+def rand_ipa_pod(rng, j, frac=0.5, spread_frac=0.2):
+    p = rand_pod(rng, j, spread_frac=spread_frac)
+    if p.namespace == "other":
+        p.namespace_labels = {"team": "blue"}
+    if rng.random() < frac:
+        p.affinity_terms = [rand_term(rng) for _ in range(rng.randint(1, 3))]
+    return p
+
+
+@pytest.mark.parametrize("seed,n,zones,P", [(31, 300, 3, 256), (32, 1200, 10, 64), (33, 600, 4, 2)])
+def test_ipa_random_stream(seed, n, zones, P):
+    rng = random.Random(seed)
+    x = Pair(n, pods_per_round=P)
+    x.upsert(rand_nodes(rng, n, zones), list(range(n)))
+    pre = [rand_ipa_pod(rng, 10_000 + j, frac=0.15, spread_frac=0.0) for j in range(n // 3)]
+    for p in pre:
+        # bound pods: anti-affinity only in rare, narrow terms so most incoming pods stay schedulable
+        p.affinity_terms = [t for t in p.affinity_terms if t.kind != "anti-affinity" or rng.random() < 0.3]
+    live = [(p, rng.randrange(n)) for p in pre]
+    x.add([p for p, _ in live], [s for _, s in live])
+    for b in range(4):
+        pods = [rand_ipa_pod(rng, b * 1000 + j, frac=0.3) for j in range(100)]
+        x.schedule(pods, f"seed {seed} batch {b}")
+        x.states_equal(f"seed {seed} batch {b}")
+        rng.shuffle(live)
+        gone, live = live[:6], live[6:]
+        x.add([p for p, _ in gone], [s for _, s in gone], sign=-1)
+        slots = rng.sample(range(n), 3)
+        live = [(p, s) for p, s in live if s != slots[0]]
+        x.upsert(rand_nodes(rng, 3, zones, slot0=n + 10 * b), slots)
+        x.delete([slots[0]])
+        x.upsert(rand_nodes(rng, 1, zones, slot0=n + 10 * b + 5), [slots[0]])
+        extra = [rand_ipa_pod(rng, 70_000 + 10 * b + k, frac=0.8, spread_frac=0.0) for k in range(3)]
+        es = [rng.randrange(n) for _ in extra]
+        x.add(extra, es)  # new term classes between batches
+        live += list(zip(extra, es))
+        x.dump_equal(rand_ipa_pod(rng, 99_000 + b, frac=1.0), f"seed {seed} dump {b}")
+        x.dump_equal(rand_ipa_pod(rng, 98_000 + b, frac=0.0, spread_frac=0.0), f"seed {seed} plain dump {b}")
+    x.close()
+
+
+def test_ipa_deployment_anti_affinity_replicas():
+    # a deployment with hostname anti-affinity to itself and zone preferred
+    # affinity: every replica lands on a fresh node until none is left
+    rng = random.Random(41)
+    n = 300
+    x = Pair(n)
+    x.upsert(rand_nodes(rng, n, 6, nozone=0.0), list(range(n)))
+    from ksched.objects import PodAffinityTerm as T
+    sel = LabelSelector({"app": "web"})
+    terms = [T(HOST, sel, kind="anti-affinity"), T(ZONE, sel, kind="preferred-affinity", weight=10)]
+    pods = [Pod(f"r{j}", containers=[Container({"cpu": 100, "memory": 64 * Mi})], labels={"app": "web"},
+                affinity_terms=terms) for j in range(n + 20)]
+    r = x.schedule(pods, "replicas")
+    ok = r["status"] == 0
+    assert ok[:n - 30].all() and not ok[n:].any()
+    assert len(set(r["node_index"][ok].tolist())) == int(ok.sum())  # one per node
+    x.states_equal("replicas")
+    x.close()
+
+
+def test_ipa_refusals():
+    from ksched.objects import PodAffinityTerm as T
+    s = Scheduler(8)
+    a = Arena()
+    na, k = nodes_array([Node("n", {"cpu": 1000, "memory": Gi, "pods": 8}, {ZONE: "a"})], a)
+    s.upsert_nodes_raw(na, u32([0]), k)
+    bad = [
+        [T("", LabelSelector({"app": "x"}))],                                       # empty topology key
+        [T(ZONE, LabelSelector({"bad key!": "x"}))],                                 # selector parse error
+        [T(ZONE, LabelSelector({"app": "x"}), kind="preferred-affinity", weight=0)],  # weight out of range
+        [T(ZONE, LabelSelector({"app": "x"}), namespace_selector=LabelSelector(
+            match_expressions=[LabelSelectorRequirement("a", "In")]))],              # namespace selector error
+        [T(ZONE, LabelSelector({"app": f"x{i}"}), kind="anti-affinity") for i in range(70)],  # > MAX_AFF
+    ]
+    pods = [Pod(f"p{i}", affinity_terms=t) for i, t in enumerate(bad)]
+    pa, m = pods_array(pods, a)
+    st = (C.c_int32 * m)()
+    s.lib.ks_pods_check(s.ctx, pa, m, st)
+    assert list(st) == [_abi.KS_ERR_UNSUPPORTED] * m
+    ok = Pod("fine", affinity_terms=[T(ZONE, LabelSelector({"app": "x"}), kind="anti-affinity")])
+    pa, m = pods_array([ok], a)
+    assert s.lib.ks_pods_check(s.ctx, pa, 1, st) == 0
+    s.close()
