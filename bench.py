@@ -68,6 +68,11 @@ B_NODE_LABELED = 96  # ... with label / taint bitsets (C4)
 # ids, class count, raw score), select 101 (status, slot, resource row,
 # label / taint words, raw score)
 B_SPREAD_NODE = 275
+# InterPodAffinity pods of --pods affinity on the same chain: prep 32 (slot,
+# apods, domain id + count column of 3 records), filter 133 (slot, 56-B
+# resource row, 32-B label / taint words, 3 domain ids + domain sums, status,
+# packed parts, raw score), select 21 (status, slot, packed parts, raw score)
+B_AFF_NODE = 186
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # VALU issue peak: a wave64 VALU instruction occupies a 16-lane SIMD for 4
 # cycles (MI355X FP64 vector peak 78.6 TFLOP/s = 256 CUs x 4 SIMDs x 16 lanes
@@ -93,7 +98,7 @@ def parse():
     ap.add_argument("--topk", type=int, default=0)
     ap.add_argument("--nodes-per-lane", type=int, default=4)
     ap.add_argument("--kind", default="hetero", choices=["hetero", "kwok", "labeled", "zoned"])
-    ap.add_argument("--pods", default="default", choices=["default", "besteffort", "spread"],
+    ap.add_argument("--pods", default="default", choices=["default", "besteffort", "spread", "affinity"],
                     help="besteffort: request-less pods (kwok/make_pods/main.go:118-148); spread: "
                          "deployment pods with PodTopologySpread constraints (use with --kind zoned)")
     ap.add_argument("--apps", type=int, default=64, help="deployments of the --pods spread stream")
@@ -111,7 +116,7 @@ def parse():
     a = ap.parse_args()
     if a.prefill is None:
         a.prefill = 0.0 if a.kind == "kwok" else 0.5
-    if a.pods == "spread":  # one pod at a time through the spread path: smaller steps and CPU samples
+    if a.pods in ("spread", "affinity"):  # one pod at a time (spread path): smaller steps and CPU samples
         if a.batch == 32768:
             a.batch = 2048
         a.cpu_pods = min(a.cpu_pods, 4)
@@ -209,6 +214,8 @@ def pod_stream(args, kind, n, seed):
         return synth.besteffort_pods(n)
     if args.pods == "spread":
         return synth.spread_pods(n, args.apps, seed)
+    if args.pods == "affinity":
+        return synth.affinity_pods(n, args.apps, seed)
     return synth.pods(kind, n, seed)
 
 
@@ -430,6 +437,12 @@ def workload_name(args) -> str:
                 "maxSkew 3 + zone maxSkew 5 ScheduleAnyway; half zone maxSkew 1 DoNotSchedule + hostname "
                 "maxSkew 1 ScheduleAnyway), every default Filter / Score plugin, pct=100, one pod at a time "
                 "(spread path)")
+    if args.pods == "affinity":
+        return (f"affinity: {n} heterogeneous nodes in 32 zones, prefill<{f:.0%} cpu (pods of 64 apps); "
+                f"pods of {args.apps} deployments with InterPodAffinity terms (half required hostname "
+                "anti-affinity + preferred zone affinity (50) to the own app, half preferred hostname "
+                "anti-affinity (100) + required zone affinity to the next app), every default Filter / "
+                "Score plugin, pct=100, one pod at a time (spread path)")
     pods = ("request-less busybox pods (kwok/make_pods)" if args.pods == "besteffort"
             else "resource-only pods (cpu 50-4000m, mem 64Mi x 1..256, 10% best-effort)")
     if args.kind == "hetero":
@@ -447,7 +460,7 @@ def workload_name(args) -> str:
 
 def pmc_key(args, world) -> str:
     """Name of the PMC summary measured for exactly this configuration."""
-    pods = {"besteffort": "-be", "spread": "-spread"}.get(args.pods, "")
+    pods = {"besteffort": "-be", "spread": "-spread", "affinity": "-affinity"}.get(args.pods, "")
     return (f"{args.workload}_{args.kind}{pods}_n{args.nodes}_P{args.pods_per_round}_K{args.topk or args.pods_per_round}"
             f"_npl{args.nodes_per_lane}_w{world}")
 
@@ -463,18 +476,20 @@ def roofline_spread(args, st):
     """The spread path: HBM-bound node passes (B_SPREAD_NODE bytes per node per
     pod), timed per pod with HIP events around the whole kernel chain."""
     ms = st.spread_ms / max(1, st.spread_pods_timed)
-    traffic = B_SPREAD_NODE * args.nodes
+    b_node = B_AFF_NODE if args.pods == "affinity" else B_SPREAD_NODE
+    traffic = b_node * args.nodes
     ach = traffic / (ms * 1e-3) / 1e9 if ms else None
     return {"bound": "hbm", "achieved": round(ach, 1) if ach else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(ach / HBM_PEAK_GBS, 4) if ach else None, "traffic": None,
             "kernel": "ks::spread_* chain (prep, min, filter, score, select, commit)",
             "ms_per_pod": round(ms, 4), "pods_timed": int(st.spread_pods_timed),
             "algorithmic_bytes_per_pod": traffic,
-            "what": "B_SPREAD_NODE x nodes per pod / chain time (HIP events on every 8th pod)"}
+            "what": f"{'B_AFF_NODE' if args.pods == 'affinity' else 'B_SPREAD_NODE'} x nodes per pod / chain "
+                    "time (HIP events on every 8th pod)"}
 
 
 def roofline(args, st, world):
-    if args.pods == "spread":
+    if args.pods in ("spread", "affinity"):
         return roofline_spread(args, st)
     labeled = args.kind == "labeled"
     sweep_avg_ms = st.sweep_ms / max(1, st.sweep_launches)

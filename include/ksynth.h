@@ -49,6 +49,10 @@ ksynth *ksynth_besteffort_pods(uint32_t n);
  * own [zone maxSkew 1 DoNotSchedule, hostname maxSkew 1 ScheduleAnyway], all
  * selecting app=app-k. */
 ksynth *ksynth_spread_pods(uint32_t n, uint32_t n_apps, uint64_t seed);
+// InterPodAffinity deployment pods (ksynth.cpp): alternately required hostname
+// anti-affinity + preferred zone affinity to the own app, and preferred
+// hostname anti-affinity + required zone affinity to the next app.
+ksynth *ksynth_affinity_pods(uint32_t n, uint32_t n_apps, uint64_t seed);
 
 const ks_node *ksynth_node_array(const ksynth *s, uint32_t *n);
 const ks_pod *ksynth_pod_array(const ksynth *s, uint32_t *n);

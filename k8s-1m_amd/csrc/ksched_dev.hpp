@@ -171,6 +171,8 @@ enum AffKind : uint32_t {
   AF_OWN = 4,         // a term class of the pod's own terms: +weight on commit
   AF_KIND = 15u,
   AF_TERM = 16u,      // the column is a term-class column
+  AF_NODE = 32u,      // every domain of the key holds one node (hostnames): the domain sum is the
+                      // node's own count, read in place (no prep pass, no scattered domain sums)
 };
 constexpr uint32_t AFF_SELF = 1u;  // the pod matches all its required affinity terms
 struct alignas(16) AffDev {
@@ -193,6 +195,7 @@ struct alignas(16) ImageDev {
   uint32_t bit, _pad;
   int64_t scaled;
 };
+constexpr int MAX_IMG = 32;  // ImageDev records per pod (containers whose image some node reports)
 static_assert(sizeof(SoloHdr) == 32 && sizeof(XResDev) == 16 && sizeof(ImageDev) == 16 && sizeof(AffDev) == 16,
               "solo program layout");
 

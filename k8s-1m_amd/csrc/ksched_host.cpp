@@ -213,6 +213,21 @@ struct TopoKey {
   uint32_t key = 0;
   std::unordered_map<uint32_t, uint32_t> dom;  // value id -> domain id ("" -> 0)
   uint32_t ndom = 1;
+  // nodes per domain: while no domain holds two nodes (hostnames), a domain
+  // sum is the node's own count (InterPodAffinity's per-node records, AF_NODE)
+  std::vector<uint32_t> slot_dom;   // [cap] domain of each slot (DOM_NONE: absent / no key)
+  std::vector<uint32_t> dom_nodes;  // [ndom]
+  uint32_t shared = 0;              // domains holding two or more nodes
+  void place(uint32_t slot, uint32_t d) {
+    const uint32_t o = slot_dom[slot];
+    if (o == d) return;
+    if (o != DOM_NONE && --dom_nodes[o] == 1) --shared;
+    if (d != DOM_NONE) {
+      if (d >= dom_nodes.size()) dom_nodes.resize((size_t)d + 1, 0);
+      if (++dom_nodes[d] == 2) ++shared;
+    }
+    slot_dom[slot] = d;
+  }
 };
 
 struct TaintKey {
@@ -1457,9 +1472,15 @@ ks_status topo_build(ks_ctx *c, uint32_t ti) {
   TopoKey &k = c->topo[ti];
   k.dom.clear();
   k.ndom = 1;
+  k.slot_dom.assign(c->cap, DOM_NONE);
+  k.dom_nodes.clear();
+  k.shared = 0;
   std::vector<uint32_t> col(c->npos, DOM_NONE);
   for (uint32_t sl = 0; sl < c->cap; ++sl)
-    if (c->nodes[sl].present) col[c->slot_pos[sl]] = node_domain(k, c->nodes[sl]);
+    if (c->nodes[sl].present) {
+      col[c->slot_pos[sl]] = node_domain(k, c->nodes[sl]);
+      k.place(sl, col[c->slot_pos[sl]]);
+    }
   ks_status st;
   if ((st = spread_scratch(c, k.ndom)) || (st = xfer_begin(c, (size_t)c->npos * 4 + 1024, 0)) ||
       (st = h2d(c, c->d_dom + (size_t)ti * c->npos, col.data(), (size_t)c->npos * 4)) || (st = xfer_sync(c)))
@@ -1812,6 +1833,12 @@ ks_status ipa_compile(ks_ctx *c, const ks_pod &p, bool create, std::vector<uint3
   if (out->size() > (size_t)MAX_AFF)
     return c->fail(KS_ERR_UNSUPPORTED, "pod %s: more than %d pod (anti-)affinity records (own and matching terms)",
                    pn.c_str(), MAX_AFF);
+  if (create)  // keys whose every domain is one node (hostnames): per-node records
+    for (AffDev &r : *out) {
+      const uint32_t kind = r.kind & AF_KIND;
+      if (kind != AF_REQ_AFF && kind != AF_OWN && r.key < c->topo.size() && c->topo[r.key].shared == 0)
+        r.kind |= AF_NODE;
+    }
   return KS_OK;
 }
 
@@ -1823,7 +1850,7 @@ uint32_t solo_passes(const SoloHdr *hd) {
   const AffDev *ad = reinterpret_cast<const AffDev *>(reinterpret_cast<const uint8_t *>(sd + hd->n_spread) +
                                                       hd->n_xres * sizeof(XResDev) + hd->n_img * sizeof(ImageDev));
   for (uint32_t k = 0; k < hd->n_aff; ++k)
-    if ((ad[k].kind & AF_KIND) != AF_OWN) f |= SPL_PREP;
+    if ((ad[k].kind & AF_KIND) != AF_OWN && !(ad[k].kind & AF_NODE)) f |= SPL_PREP;
   return f;
 }
 
@@ -1861,6 +1888,9 @@ ks_status solo_compile(ks_ctx *c, const ks_pod &p, PodDev &d, ProgBuf &cl, bool 
       return KS_OK;
     };
     if ((st = scan(p.init_containers, p.n_init_containers)) || (st = scan(p.containers, p.n_containers))) return st;
+    if (imgs.size() > (size_t)MAX_IMG)
+      return c->fail(KS_ERR_UNSUPPORTED, "pod %s: more than %d containers with images present on nodes", pn.c_str(),
+                     MAX_IMG);
     if (!imgs.empty()) c->compile_used_names = true;  // the node count enters the scores
   }
   std::vector<AffDev> aff;
@@ -2011,10 +2041,13 @@ ks_status spread_nodes_changed(ks_ctx *c, const uint32_t *slots, uint32_t n, boo
   std::vector<uint32_t> rebuild;
   for (uint32_t ti = 0; ti < c->topo.size(); ++ti) {
     TopoKey &k = c->topo[ti];
+    const bool unique = k.shared == 0;
     for (uint32_t i = 0; i < n; ++i) {
       idx.push_back((uint64_t)ti * c->npos + c->slot_pos[slots[i]]);
       val.push_back(deleted ? DOM_NONE : node_domain(k, c->nodes[slots[i]]));
+      k.place(slots[i], val.back());
     }
+    if (unique && k.shared) c->dict_version++;  // prepared per-node records no longer hold
     if (k.ndom > 2 * c->cap + 1024) rebuild.push_back(ti);  // churned values: renumber
   }
   if (deleted)

@@ -75,6 +75,11 @@ constexpr uint64_t IPA_BIAS = 1ull << 63;  // signed raw scores as unsigned min 
 // required affinity terms (unless no such pod exists anywhere and the pod
 // matches its own terms), no required anti-affinity match in the node's
 // domains, no bound pod's required anti-affinity term matching the pod there.
+// Domain sum of record r at a position whose domain is d (!= DOM_NONE).
+__device__ __forceinline__ uint32_t aff_sum(const SpreadArgs &a, const AffDev &q, uint32_t r, uint32_t pos, uint32_t d) {
+  return (q.kind & AF_NODE) ? aff_count(a, q, pos) : a.adcnt[(size_t)r * a.dom_cap + d];
+}
+
 __device__ __forceinline__ bool ipa_fits(const SpreadArgs &a, const AffDev *ad, uint32_t na, uint32_t pos,
                                          bool first_ok) {
   bool has_req = false, exist = true;
@@ -85,8 +90,8 @@ __device__ __forceinline__ bool ipa_fits(const SpreadArgs &a, const AffDev *ad, 
     if (kind == AF_REQ_AFF) {
       has_req = true;
       if (d == DOM_NONE) return false;  // all topology labels must exist on the node
-      if (!a.adcnt[(size_t)r * a.dom_cap + d]) exist = false;
-    } else if (d != DOM_NONE && a.adcnt[(size_t)r * a.dom_cap + d]) {
+      if (!aff_sum(a, ad[r], r, pos, d)) exist = false;
+    } else if (d != DOM_NONE && aff_sum(a, ad[r], r, pos, d)) {
       return false;
     }
   }
@@ -99,20 +104,46 @@ __device__ __forceinline__ int64_t ipa_raw_score(const SpreadArgs &a, const AffD
   for (uint32_t r = 0; r < na; ++r) {
     if ((ad[r].kind & AF_KIND) != AF_SCORE) continue;
     const uint32_t d = a.dom[(size_t)ad[r].key * a.npos + pos];
-    if (d != DOM_NONE) raw += (int64_t)ad[r].weight * (int64_t)a.adcnt[(size_t)r * a.dom_cap + d];
+    if (d != DOM_NONE) raw += (int64_t)ad[r].weight * (int64_t)aff_sum(a, ad[r], r, pos, d);
   }
   return raw;
 }
 
+// The pod's program staged in LDS by the node-parallel passes: read in every
+// node iteration, records in global memory would be re-fetched after each of
+// the iteration's stores (the compiler cannot rule out aliasing).
+struct SoloLds {
+  SoloHdr h;
+  SpreadDev sd[MAX_SPREAD];
+  XResDev xr[MAX_XRES];
+  ImageDev img[MAX_IMG];
+  AffDev ad[MAX_AFF];
+};
+__device__ __forceinline__ void stage_solo(const SpreadArgs &a, const PodDev &p, SoloLds &s) {
+  const SoloHdr &h = solo_hdr(a, p);
+  const uint32_t t = threadIdx.x;
+  if (t == 0) s.h = h;
+  if (t < h.n_spread) s.sd[t] = spread_recs(a, p)[t];
+  if (t < h.n_xres) s.xr[t] = xres_recs(a, p)[t];
+  if (t < h.n_img) s.img[t] = image_recs(a, p)[t];
+  if (t < h.n_aff) s.ad[t] = aff_recs(a, p)[t];
+}
+
 // imagelocality#calculatePriority over sumImageScores of the node (label bits
 // of the "image present" keys); 0 without present images.
-__device__ __forceinline__ int64_t image_score(const SpreadArgs &a, const PodDev &p, const NodeExt &e) {
-  const SoloHdr &h = solo_hdr(a, p);
+__device__ __forceinline__ int64_t image_score(const SoloLds &sl, const NodeExt &e) {
+  const SoloHdr &h = sl.h;
   if (!h.n_img) return 0;
-  const ImageDev *g = image_recs(a, p);
+  const ImageDev *g = sl.img;
   int64_t sum = 0;
-  for (uint32_t k = 0; k < h.n_img; ++k)
-    if ((e.lab[g[k].bit >> 6] >> (g[k].bit & 63)) & 1ull) sum += g[k].scaled;
+  for (uint32_t k = 0; k < h.n_img; ++k) {
+    // the label word by a select chain: a dynamic index would put e.lab in scratch
+    const uint32_t wi = g[k].bit >> 6;
+    uint64_t w = 0;
+#pragma unroll
+    for (int q = 0; q < LW; ++q) w = (uint32_t)q == wi ? e.lab[q] : w;
+    if ((w >> (g[k].bit & 63)) & 1ull) sum += g[k].scaled;
+  }
   const int64_t mb = 1024 * 1024, min_t = 23 * mb, max_t = 1000 * mb * (int64_t)h.n_containers;
   sum = sum < min_t ? min_t : (sum > max_t ? max_t : sum);
   return 100 * (sum - min_t) / (max_t - min_t);
@@ -190,7 +221,8 @@ __device__ void lds_segments(const SpreadArgs &a, const SpreadDev *sd, uint32_t 
   }
   for (uint32_t r = 0; r < na; ++r) {
     const uint32_t nd = a.ndom[ad[r].key];
-    const bool small = (ad[r].kind & AF_KIND) != AF_OWN && nd <= SP_LDS_DOM && o + nd <= SP_LDS;
+    const bool small = (ad[r].kind & AF_KIND) != AF_OWN && !(ad[r].kind & AF_NODE) && nd <= SP_LDS_DOM &&
+                       o + nd <= SP_LDS;
     aoff[r] = small ? o : SP_OFF_NONE;
     if (small) o += nd;
   }
@@ -239,13 +271,16 @@ __global__ __launch_bounds__(SP_THREADS) void spread_prep_kernel(SpreadArgs a) {
   __shared__ uint32_t s_h[SP_LDS];
   __shared__ uint32_t s_off[MAX_SPREAD];
   __shared__ uint32_t s_aoff[MAX_AFF];
+  __shared__ SoloLds s_solo;
   const PodDev p = a.pods[a.pod];
-  const SpreadDev *sd = spread_recs(a, p);
-  const uint32_t n = spread_count(a, p);
-  const AffDev *ad = aff_recs(a, p);
-  const uint32_t na = solo_hdr(a, p).n_aff;
-  if (threadIdx.x == 0) lds_segments(a, sd, n, s_off, ad, na, s_aoff);
+  stage_solo(a, p, s_solo);
   for (uint32_t i = threadIdx.x; i < SP_LDS; i += SP_THREADS) s_h[i] = 0;
+  __syncthreads();
+  const SpreadDev *sd = s_solo.sd;
+  const uint32_t n = s_solo.h.n_spread;
+  const AffDev *ad = s_solo.ad;
+  const uint32_t na = s_solo.h.n_aff;
+  if (threadIdx.x == 0) lds_segments(a, sd, n, s_off, ad, na, s_aoff);
   __syncthreads();
   bool aff_needed = false, taint_needed = false;
   for (uint32_t c = 0; c < n; ++c) {
@@ -260,7 +295,7 @@ __global__ __launch_bounds__(SP_THREADS) void spread_prep_kernel(SpreadArgs a) {
     for (uint32_t r = 0; r < na; ++r) {
       const AffDev &q = ad[r];
       const uint32_t kind = q.kind & AF_KIND;
-      if (kind == AF_OWN) continue;
+      if (kind == AF_OWN || (q.kind & AF_NODE)) continue;  // per-node records: read in place
       const uint32_t v = aff_count(a, q, pos);
       if (!v) continue;
       const uint32_t d = a.dom[(size_t)q.key * a.npos + pos];
@@ -380,20 +415,29 @@ __global__ __launch_bounds__(SP_THREADS) void spread_filter_kernel(SpreadArgs a)
   __shared__ uint32_t s_off[MAX_SPREAD];
   __shared__ uint32_t s_red[SP_THREADS / WAVE][R_N];
   __shared__ uint64_t s_r64[SP_THREADS / WAVE][2];
+  __shared__ SoloLds s_solo;
   const PodDev p = a.pods[a.pod];
-  const SpreadDev *sd = spread_recs(a, p);
-  const uint32_t n = spread_count(a, p);
-  if (threadIdx.x == 0) lds_segments(a, sd, n, s_off);
+  stage_solo(a, p, s_solo);
   for (uint32_t i = threadIdx.x; i < SP_LDS / 32; i += SP_THREADS) s_seen[i] = 0;
   for (uint32_t i = threadIdx.x; i < SP_LDS; i += SP_THREADS) s_h[i] = 0;
   __syncthreads();
-  const uint32_t n_xres = solo_hdr(a, p).n_xres;
-  const AffDev *ad = aff_recs(a, p);
-  const uint32_t na = solo_hdr(a, p).n_aff;
+  const SpreadDev *sd = s_solo.sd;
+  const uint32_t n = s_solo.h.n_spread;
+  if (threadIdx.x == 0) lds_segments(a, sd, n, s_off);
+  __syncthreads();
+  const uint32_t n_xres = s_solo.h.n_xres;
+  const AffDev *ad = s_solo.ad;
+  const uint32_t na = s_solo.h.n_aff;
   bool ipa_filter = false;
   for (uint32_t r = 0; r < na; ++r) ipa_filter |= (ad[r].kind & AF_KIND) <= AF_EXIST_ANTI;
-  const bool ipa_first_ok = !a.acc->aff_any && (solo_hdr(a, p).aff_flags & AFF_SELF);
-  const bool ipa_score = a.acc->score_any != 0;
+  const bool ipa_first_ok = !a.acc->aff_any && (s_solo.h.aff_flags & AFF_SELF);
+  bool ipa_score = false, node_score = false;  // topologyScore records; per-node ones
+  for (uint32_t r = 0; r < na; ++r)
+    if ((ad[r].kind & AF_KIND) == AF_SCORE) {
+      ipa_score = true;
+      node_score |= (ad[r].kind & AF_NODE) != 0;
+    }
+  bool score_any = false;  // topologyScore entries of the per-node records
   bool any_s = false, aff_needed = false, taint_needed = false;
   for (uint32_t c = 0; c < n; ++c) {
     if (!(sd[c].flags & SP_SCORE)) continue;
@@ -415,6 +459,11 @@ __global__ __launch_bounds__(SP_THREADS) void spread_filter_kernel(SpreadArgs a)
       a.st[pos] = SST_EMPTY;
       continue;
     }
+    if (node_score)
+      for (uint32_t q = 0; q < na; ++q)
+        if ((ad[q].kind & (AF_KIND | AF_NODE)) == (AF_SCORE | AF_NODE) && aff_count(a, ad[q], pos) &&
+            a.dom[(size_t)ad[q].key * a.npos + pos] != DOM_NONE)
+          score_any = true;
     NodeExt e;
     load_ext(a.t, pos, true, e);
     bool all_s = true;
@@ -440,7 +489,7 @@ __global__ __launch_bounds__(SP_THREADS) void spread_filter_kernel(SpreadArgs a)
     int s = filter<true>(p, a.clauses, r, e);
     if (s == ST_FEASIBLE) {
       // NodeResourcesFit (fitsRequest) for ephemeral-storage / scalar resources
-      const XResDev *xr = xres_recs(a, p);
+      const XResDev *xr = s_solo.xr;
       for (uint32_t k = 0; k < n_xres; ++k) {
         const size_t ix = (size_t)xr[k].col * a.npos + pos;
         if (xr[k].req > a.xalloc[ix] - a.xreq[ix]) s = 4;  // KS_PLUGIN_NODE_RESOURCES_FIT
@@ -472,7 +521,7 @@ __global__ __launch_bounds__(SP_THREADS) void spread_filter_kernel(SpreadArgs a)
       tt_max = max(tt_max, tr);
       na_max = max(na_max, nr);
       a.part[pos] = pack_part((uint32_t)a.w.fit * (uint32_t)score_la(p, r) + (uint32_t)a.w.ba * (uint32_t)score_ba(p, r) +
-                                  (uint32_t)a.w.il * (uint32_t)image_score(a, p, e),
+                                  (uint32_t)a.w.il * (uint32_t)image_score(s_solo, e),
                               tr, nr);
       if (ipa_score) {
         const int64_t raw = ipa_raw_score(a, ad, na, pos);
@@ -517,7 +566,9 @@ __global__ __launch_bounds__(SP_THREADS) void spread_filter_kernel(SpreadArgs a)
   v[R_NA] = wave_max(na_max);
   ipa_mn = wave_min64(ipa_mn);
   ipa_mx = wave_max64(ipa_mx);
+  if (__syncthreads_or(score_any ? 1 : 0) && threadIdx.x == 0) atomicOr(&a.acc->score_any, 1u);
   if (lane == 0) {
+#pragma unroll
     for (int q = 0; q < R_N; ++q) s_red[wid][q] = v[q];
     s_r64[wid][0] = ipa_mn;
     s_r64[wid][1] = ipa_mx;
@@ -564,9 +615,12 @@ __global__ __launch_bounds__(SP_THREADS) void spread_filter_kernel(SpreadArgs a)
 __global__ __launch_bounds__(SP_THREADS) void spread_score_kernel(SpreadArgs a) {
   __shared__ double s_w[MAX_SPREAD];
   __shared__ uint64_t s_r[SP_THREADS / WAVE][2];
+  __shared__ SpreadDev s_sd[MAX_SPREAD];
   const PodDev p = a.pods[a.pod];
-  const SpreadDev *sd = spread_recs(a, p);
   const uint32_t n = spread_count(a, p);
+  if (threadIdx.x < n) s_sd[threadIdx.x] = spread_recs(a, p)[threadIdx.x];
+  const SpreadDev *sd = s_sd;
+  __syncthreads();
   if (threadIdx.x < n) {
     const Totals tot = acc_totals(a.acc);
     const SpreadDev &q = sd[threadIdx.x];
@@ -619,9 +673,12 @@ __global__ __launch_bounds__(SP_THREADS) void spread_score_kernel(SpreadArgs a) 
 // pass).
 __global__ __launch_bounds__(SP_THREADS) void spread_select_kernel(SpreadArgs a) {
   __shared__ uint64_t s_r[SP_THREADS / WAVE];
+  __shared__ SoloLds s_solo;
   const PodDev p = a.pods[a.pod];
-  const SpreadDev *sd = spread_recs(a, p);
-  const uint32_t n = spread_count(a, p);
+  stage_solo(a, p, s_solo);
+  __syncthreads();
+  const SpreadDev *sd = s_solo.sd;
+  const uint32_t n = s_solo.h.n_spread;
   bool has_score = false;
   for (uint32_t c = 0; c < n; ++c) has_score |= (sd[c].flags & SP_SCORE) != 0;
   const Totals tot = acc_totals(a.acc);
@@ -683,7 +740,7 @@ __global__ __launch_bounds__(SP_THREADS) void spread_select_kernel(SpreadArgs a)
       const int64_t nr = (p.flags & PF_NA) ? preferred_raw(p, a.clauses, e, slot) : 0;
       o[5] = (int32_t)nr;
       o[6] = (p.flags & PF_HAS_PREF) ? (int32_t)normalize(nr, (p.flags & PF_NA) ? na_max : 0, false) : 0;
-      o[7] = (int32_t)image_score(a, p, e);
+      o[7] = (int32_t)image_score(s_solo, e);
       o[8] = (int32_t)raw;
       o[9] = (int32_t)norm;
       o[10] = (int32_t)(total & 0xFFFFFFFF);
@@ -709,9 +766,9 @@ __global__ __launch_bounds__(SP_THREADS) void spread_select_kernel(SpreadArgs a)
       a.dcnt[(size_t)c * a.dom_cap + d] = 0;
       a.dflag[(size_t)c * a.dom_cap + d] = 0;
     }
-  const AffDev *ad = aff_recs(a, p);
-  for (uint32_t r = 0; r < solo_hdr(a, p).n_aff; ++r)
-    if ((ad[r].kind & AF_KIND) != AF_OWN)
+  const AffDev *ad = s_solo.ad;
+  for (uint32_t r = 0; r < s_solo.h.n_aff; ++r)
+    if ((ad[r].kind & AF_KIND) != AF_OWN && !(ad[r].kind & AF_NODE))
       for (uint32_t d = blockIdx.x * SP_THREADS + threadIdx.x; d < a.ndom[ad[r].key]; d += grid_threads())
         a.adcnt[(size_t)r * a.dom_cap + d] = 0;
 }
@@ -829,8 +886,13 @@ __global__ void scatter_i64_kernel(int64_t *col, const uint64_t *idx, const int6
 // ------------------------------------------------------------- launchers
 
 hipError_t launch_spread_pod(const SpreadArgs &args, uint32_t passes, hipStream_t st) {
-  const uint32_t blocks =
-      std::max<uint32_t>(1, std::min<uint32_t>((args.npos + SP_THREADS - 1) / SP_THREADS, SPREAD_MAX_BLOCKS));
+  // KS_SPREAD_BLOCKS (diagnostic): the node passes' block cap
+  static const uint32_t cap = [] {
+    const char *e = getenv("KS_SPREAD_BLOCKS");
+    const long v = e ? atol(e) : 0;
+    return v > 0 && v <= 4096 ? (uint32_t)v : (uint32_t)SPREAD_MAX_BLOCKS;
+  }();
+  const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((args.npos + SP_THREADS - 1) / SP_THREADS, cap));
   const SpreadArgs &a = args;
   if (passes & SPL_PREP) spread_prep_kernel<<<blocks, SP_THREADS, 0, st>>>(a);
   if (passes & SPL_MIN) spread_min_kernel<<<blocks, SP_THREADS, 0, st>>>(a);

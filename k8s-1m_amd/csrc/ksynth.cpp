@@ -65,6 +65,7 @@ struct ksynth {
   std::vector<ks_preferred_term> prefs;
   std::vector<const char *> values;
   std::vector<ks_spread_constraint> spread;
+  std::vector<ks_pod_affinity_term> affinity;
   std::deque<std::string> strings;
   std::unordered_map<std::string, const char *> interned;
 
@@ -195,6 +196,7 @@ void reserve_pods(ksynth *s, size_t n) {
   s->values.reserve(n * 16);
   s->labels.reserve(n * 2);
   s->spread.reserve(n * 2);
+  s->affinity.reserve(n * 2);
 }
 
 // Resource requests of the C1 stream: cpu in {50..4000 step 50}m,
@@ -400,6 +402,59 @@ extern "C" ksynth *ksynth_spread_pods(uint32_t n, uint32_t n_apps, uint64_t seed
     p.spread = ksynth::push(s->spread, a);
     ksynth::push(s->spread, b);
     p.n_spread = 2;
+    s->pods.push_back(p);
+  }
+  return s;
+}
+
+// Deployment pods with pod (anti-)affinity (InterPodAffinity, the one-pod
+// path): app-k pods with, alternately, required hostname anti-affinity to
+// their own app + preferred zone affinity to it (weight 50), and preferred
+// hostname anti-affinity to their own app (weight 100) + required zone
+// affinity to app-(k+1) (the zoned prefill holds pods of every app).
+extern "C" ksynth *ksynth_affinity_pods(uint32_t n, uint32_t n_apps, uint64_t seed) {
+  auto *s = new ksynth();
+  reserve_pods(s, n);
+  if (n_apps == 0) n_apps = 1;
+  for (uint32_t j = 0; j < n; ++j) {
+    Rng r(seed, j, 7);
+    ks_pod p = base_pod(s, j, "aff-");
+    ks_container c;
+    draw_requests(r, c);
+    p.containers = ksynth::push(s->containers, c);
+    p.n_containers = 1;
+    p.tolerations = s->tolerations.data() + s->tolerations.size();
+    kwok_tolerations(s);
+    p.n_tolerations = 3;
+    const uint32_t k = r.below(n_apps);
+    const ks_label *own = ksynth::push(s->labels, ks_label{s->intern("app"), s->intern("app-" + std::to_string(k))});
+    const ks_label *next =
+        ksynth::push(s->labels, ks_label{s->intern("app"), s->intern("app-" + std::to_string((k + 1) % n_apps))});
+    p.labels = own;
+    p.n_labels = 1;
+    ks_pod_affinity_term a{}, b{};
+    a.namespace_selector.is_nil = b.namespace_selector.is_nil = 1;
+    a.selector.match_labels = own;
+    a.selector.n_match_labels = 1;
+    if (j % 2 == 0) {
+      a.topology_key = s->intern("kubernetes.io/hostname");
+      a.kind = KS_POD_ANTI_AFFINITY_REQUIRED;
+      b.selector = a.selector;
+      b.topology_key = s->intern("topology.kubernetes.io/zone");
+      b.kind = KS_POD_AFFINITY_PREFERRED;
+      b.weight = 50;
+    } else {
+      a.topology_key = s->intern("kubernetes.io/hostname");
+      a.kind = KS_POD_ANTI_AFFINITY_PREFERRED;
+      a.weight = 100;
+      b.selector.match_labels = next;
+      b.selector.n_match_labels = 1;
+      b.topology_key = s->intern("topology.kubernetes.io/zone");
+      b.kind = KS_POD_AFFINITY_REQUIRED;
+    }
+    p.affinity_terms = ksynth::push(s->affinity, a);
+    ksynth::push(s->affinity, b);
+    p.n_affinity_terms = 2;
     s->pods.push_back(p);
   }
   return s;

@@ -61,6 +61,10 @@ def spread_pods(n: int, n_apps: int, seed: int) -> Synth:
     return Synth(_abi.ksynth_lib().ksynth_spread_pods(n, n_apps, seed))
 
 
+def affinity_pods(n: int, n_apps: int, seed: int) -> Synth:
+    return Synth(_abi.ksynth_lib().ksynth_affinity_pods(n, n_apps, seed))
+
+
 def slot_array(n: int, start: int = 0):
     return (C.c_uint32 * n)(*range(start, start + n))
 

@@ -208,3 +208,37 @@ def test_spread_1m_replay():
     assert (r["status"] == 0).mean() > 0.9
     s.close()
     o.close()
+
+
+def test_affinity_1m_replay():
+    # the affinity bench's cluster with InterPodAffinity deployment pods
+    # interleaved with plain pods: term classes of the batch's own pods
+    # (required hostname anti-affinity) are counted by the commits and read by
+    # later pods; the oracle replays every decision and checks three windows
+    n_pods = 2048
+    nodes = synth.nodes(synth.ZONED, N, 1)
+    slots = synth.slot_array(N)
+    pf = synth.prefill(synth.ZONED, N, 1, 3, 0.5)
+    aff, plain = synth.affinity_pods(n_pods // 2, 16, 7), synth.pods(synth.HETERO, n_pods // 2, 8)
+    mixed = MixedStream(plain, aff, 128)
+    s = Scheduler(N)
+    s.upsert_nodes_raw(nodes.nodes, slots, N)
+    assert s.lib.ks_pods_add(s.ctx, pf.pods, pf.slot_ptr, pf.n_pods) == 0
+    b = s.prepare(mixed.pods, n_pods)
+    s.run(b)
+    got = s.results(b, n_pods)
+    s.free(b)
+    st = _abi.KsStats()
+    assert s.lib.ks_get_stats(s.ctx, C.byref(st)) == 0
+    assert st.spread_pods == n_pods // 2
+    o = pyoracle.Oracle(N, threads=ORACLE_THREADS)
+    o.upsert(nodes.nodes, slots, N)
+    o.add_pods(pf.pods, pf.slot_ptr, pf.n_pods)
+    replay_check(o, mixed, got, n_pods, windows=(124, 900, n_pods - 6), wlen=6)
+    sg = states_np(s.lib.ks_node_states, s.ctx, N)
+    sw = states_np(o.L.oracle_node_states, o.o, N)
+    assert np.array_equal(sg, sw), "node tables differ after replaying every decision"
+    r = res_array(got, n_pods)
+    assert (r["status"] == 0).mean() > 0.9
+    s.close()
+    o.close()

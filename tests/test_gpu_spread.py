@@ -456,3 +456,28 @@ def test_ipa_refusals():
     pa, m = pods_array([ok], a)
     assert s.lib.ks_pods_check(s.ctx, pa, 1, st) == 0
     s.close()
+
+
+def test_ipa_shared_hostname_values():
+    # two nodes carrying the same hostname label value form one topology
+    # domain: per-node counts no longer stand for domain sums (AF_NODE off),
+    # before and after the relabel that makes the values shared
+    from ksched.objects import PodAffinityTerm as T
+    rng = random.Random(51)
+    n = 64
+    x = Pair(n)
+    nodes = rand_nodes(rng, n, 4, nozone=0.0)
+    x.upsert(nodes, list(range(n)))
+    sel = LabelSelector({"app": "web"})
+    anti = [T(HOST, sel, kind="anti-affinity"), T(HOST, sel, kind="preferred-anti-affinity", weight=7)]
+    mk = lambda j: Pod(f"w{j}", containers=[Container({"cpu": 100})], labels={"app": "web"}, affinity_terms=anti)
+    x.schedule([mk(j) for j in range(20)], "unique hostnames")
+    x.states_equal("unique")
+    dup = rand_nodes(rng, 2, 4, slot0=1000, nozone=0.0)
+    for d in dup:
+        d.labels[HOST] = "shared"
+    x.upsert(dup, [40, 41])
+    x.schedule([mk(100 + j) for j in range(40)], "shared hostname")
+    x.states_equal("shared")
+    x.dump_equal(mk(999), "shared dump")
+    x.close()

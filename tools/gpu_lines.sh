@@ -19,6 +19,7 @@ if [ -n "$ONLY" ]; then
     case $l in
       c3) run c3 || exit $? ;;
       spread) run spread --kind zoned --pods spread --latency-calls 0 || exit $? ;;
+      affinity) run affinity --kind zoned --pods affinity --latency-calls 0 || exit $? ;;
       c4) run c4 --kind labeled --no-cpu-baseline --latency-calls 0 || exit $? ;;
     esac
   done
@@ -30,4 +31,5 @@ run c2 --nodes 100000 --batch 20000 --steps 5 --no-cpu-baseline --latency-calls 
 run kwok --kind kwok --topk 512 --no-cpu-baseline --latency-calls 0 && \
 run kwokbe --kind kwok --pods besteffort --no-cpu-baseline --latency-calls 0 && \
 run c5 --workload c5 --steps 5 --warmup 1 && \
-run spread --kind zoned --pods spread --latency-calls 0
+run spread --kind zoned --pods spread --latency-calls 0 && \
+run affinity --kind zoned --pods affinity --latency-calls 0
