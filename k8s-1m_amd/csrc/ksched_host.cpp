@@ -299,9 +299,11 @@ struct ks_ctx {
   uint32_t seq_of[2] = {0, 0};    // round number by parity
   bool value_sync = true;
   // Tuning switches, read from the environment once per context in ks_open
-  // (KS_EARLY_FIX, KS_TIMING_EVERY, KS_SWEEP_BLOCKS, KS_EXT_NPL), so one
-  // process can open contexts with different settings (tests do).
+  // (KS_EARLY_FIX, KS_TIMING_EVERY, KS_SWEEP_BLOCKS, KS_EXT_NPL,
+  // KS_TUPLE_GUESS), so one process can open contexts with different settings
+  // (tests do).
   bool early_fix = true;
+  bool tuple_guess = true;  // normaliser guesses over node tuples (refine_guesses)
   uint32_t timing_every = 8, sweep_blocks = 8192, ext_npl = 2;
   // geometry
   uint32_t cap = 0, S = 1, npl = 8, P = 256, K = 256;
@@ -347,6 +349,16 @@ struct ks_ctx {
   std::unordered_map<uint32_t, std::vector<uint32_t>> key_nodes;  // key id -> slots having it
   bool compile_used_names = false;  // set by compile_pod when a pod resolved a node name to a slot
   uint32_t dict_version = 1;   // taint dictionary / node image set (compiled masks and checks)
+  // Normaliser guesses (PodDev::tt_guess / na_guess): the distinct (label
+  // words, numeric labels, taint words) of the present nodes, rebuilt when a
+  // node's words change (tuple_version), and per (required, preferred
+  // program, tolerations) the max raw over the tuples a node could pass with
+  struct NodeTuple {
+    uint64_t w[LW + NNUM + 2];  // lab, num, hard, prefer
+  };
+  uint64_t tuple_version = 0, tuples_for = ~0ull;
+  std::vector<NodeTuple> tuples;
+  std::unordered_map<std::string, std::pair<uint32_t, uint32_t>> guess_memo;
   uint32_t names_version = 1;  // node name -> slot map (compiled NodeName / metadata.name slots)
   std::vector<uint32_t> dirty_ext;
   // ImageLocality: image name (as nodes report it) -> present nodes reporting
@@ -572,6 +584,7 @@ void node_ext_bits(ks_ctx *c, HostNode &n) {
   }
   std::memcpy(n.lab, lab, sizeof lab);
   std::memcpy(n.num, num, sizeof num);
+  c->tuple_version++;
 }
 
 ks_status alloc_bit(ks_ctx *c, uint32_t *bit) {
@@ -661,6 +674,7 @@ void reset_label_dict(ks_ctx *c) {
   }
   c->dict_version++;
   c->label_resets++;
+  c->tuple_version++;
 }
 
 // ------------------------------------------------------------ pod compile
@@ -900,6 +914,7 @@ ks_status check_modelled(ks_ctx *c, const ks_pod &p) {
 
 ks_status solo_compile(ks_ctx *c, const ks_pod &p, PodDev &d, ProgBuf &cl, bool create,
                        std::vector<uint32_t> *refs);
+void refine_guesses(ks_ctx *c, PodDev &d, const ProgBuf &cl);
 
 ks_status compile_pod(ks_ctx *c, const ks_pod &p, PodDev &d, ProgBuf &cl, bool create_spread = false,
                       std::vector<uint32_t> *class_refs = nullptr) {
@@ -1037,7 +1052,106 @@ ks_status compile_pod(ks_ctx *c, const ks_pod &p, PodDev &d, ProgBuf &cl, bool c
   }
   if ((c->hard_in_use & ~d.tol_hard) || d.name_slot != -1 || (d.flags & (PF_AFF | PF_TT | PF_NA)))
     d.flags |= PF_EXT;
+  refine_guesses(c, d, cl);
   return solo_compile(c, p, d, cl, create_spread, class_refs);
+}
+
+// One label-program term (ksched_dev.hpp) against a node tuple; false in
+// *known for metadata.name entries (a per-node property).
+bool tuple_term(const uint64_t *t, const ks_ctx::NodeTuple &x, bool *known) {
+  const uint64_t w0 = t[0];
+  const uint32_t ng = (uint32_t)w0 & 0xFF, nn = ((uint32_t)w0 >> 8) & 0xFF, nm = ((uint32_t)w0 >> 16) & 0xFF;
+  if (nm) *known = false;
+  bool ok = true;
+  for (int k = 0; k < LW; ++k) ok &= ((x.w[k] & t[1 + LW + k]) ^ t[1 + k]) == 0;
+  const uint64_t *g = t + TERM_HDR_WORDS;
+  for (uint32_t i = 0; i < ng; ++i, g += LW) {
+    uint64_t any = 0;
+    for (int k = 0; k < LW; ++k) any |= x.w[k] & g[k];
+    ok &= any != 0;
+  }
+  for (uint32_t i = 0; i < nn; ++i, g += 2) {
+    const int64_t v = (int64_t)x.w[LW + ((g[0] & 0xFF) ? 1 : 0)];
+    const int64_t o = (int64_t)g[1];
+    ok &= ((g[0] >> 8) & 0xFF) == TO_GT ? v > o : v < o;
+  }
+  return ok;
+}
+
+// Normaliser guesses of a compiled pod: max raw TaintToleration / NodeAffinity
+// over the node tuples that pass the pod's label and taint filters (every
+// node of such a tuple fails only on resources, so with many nodes per tuple
+// the guess is the measured max).  Memoised per program; name-based terms
+// keep the caller's guesses.
+void refine_guesses(ks_ctx *c, PodDev &d, const ProgBuf &cl) {
+  if (!c->tuple_guess || !(d.flags & (PF_TT | PF_NA)) || (d.flags & (PF_PREFILTER | PF_NA_CONFLICT)) ||
+      d.name_slot != -1)
+    return;
+  if (c->tuples_for != c->tuple_version) {
+    struct H {
+      size_t operator()(const ks_ctx::NodeTuple &x) const {
+        uint64_t h = 1469598103934665603ull;
+        for (uint64_t v : x.w) h = (h ^ v) * 1099511628211ull;
+        return (size_t)h;
+      }
+    };
+    struct E {
+      bool operator()(const ks_ctx::NodeTuple &a, const ks_ctx::NodeTuple &b) const {
+        return std::memcmp(a.w, b.w, sizeof a.w) == 0;
+      }
+    };
+    std::unordered_set<ks_ctx::NodeTuple, H, E> seen;
+    for (uint32_t sl = 0; sl < c->cap && seen.size() <= 4096; ++sl) {  // past 4096: simple guesses
+      const HostNode &h = c->nodes[sl];
+      if (!h.present) continue;
+      ks_ctx::NodeTuple x;
+      std::memcpy(x.w, h.lab, sizeof h.lab);
+      std::memcpy(x.w + LW, h.num, sizeof h.num);
+      x.w[LW + NNUM] = h.hard;
+      x.w[LW + NNUM + 1] = h.prefer;
+      seen.insert(x);
+    }
+    c->tuples.assign(seen.begin(), seen.end());
+    c->guess_memo.clear();
+    c->tuples_for = c->tuple_version;
+  }
+  if (c->tuples.size() > 4096) return;  // too many distinct tuples: keep the simple guesses
+  const uint64_t *req = cl.w.data() + d.req_off, *pref = cl.w.data() + d.pref_off;
+  size_t req_words = 0, pref_words = 0;
+  for (uint32_t k = 0; k < d.req_len; ++k) req_words += term_words(req[req_words]);
+  for (uint32_t k = 0; k < d.pref_len; ++k) pref_words += term_words(pref[pref_words]);
+  std::string key((const char *)&d.tol_hard, 8);
+  key.append((const char *)&d.tol_prefer, 8);
+  const uint32_t f = d.flags & (PF_AFF | PF_TT | PF_NA);
+  key.append((const char *)&f, 4);
+  key.append((const char *)&d.req_len, 4);
+  key.append((const char *)req, req_words * 8);
+  key.append((const char *)pref, pref_words * 8);
+  auto it = c->guess_memo.find(key);
+  if (it == c->guess_memo.end()) {
+    uint32_t tt = 0, na = 0;
+    bool known = true, any = false;
+    for (const ks_ctx::NodeTuple &x : c->tuples) {
+      if (x.w[LW + NNUM] & ~d.tol_hard) continue;  // a hard taint (or unschedulable) the pod does not tolerate
+      if (d.flags & PF_AFF) {
+        bool m = false;
+        const uint64_t *t = req;
+        for (uint32_t k = 0; k < d.req_len; ++k, t += term_words(t[0])) m |= tuple_term(t, x, &known);
+        if (!m) continue;
+      }
+      any = true;
+      tt = std::max<uint32_t>(tt, (uint32_t)__builtin_popcountll(x.w[LW + NNUM + 1] & ~d.tol_prefer));
+      uint32_t raw = 0;
+      const uint64_t *t = pref;
+      for (uint32_t k = 0; k < d.pref_len; ++k, t += term_words(t[0]))
+        if (tuple_term(t, x, &known)) raw += (uint32_t)(t[0] >> 32);
+      na = std::max(na, raw);
+    }
+    if (!known || !any) return;
+    it = c->guess_memo.emplace(std::move(key), std::make_pair(tt, na)).first;
+  }
+  if (d.flags & PF_TT) d.tt_guess = it->second.first;
+  if (d.flags & PF_NA) d.na_guess = it->second.second;
 }
 
 // Taint dictionaries (hard: NoSchedule / NoExecute, prefer: PreferNoSchedule)
@@ -1045,6 +1159,7 @@ ks_status compile_pod(ks_ctx *c, const ks_pod &p, PodDev &d, ProgBuf &cl, bool c
 // taint finds the dictionary full (63 hard taints + the unschedulable bit, 64
 // prefer taints); *grew when a taint was new.
 ks_status encode_taints(ks_ctx *c, HostNode &h, bool *grew) {
+  c->tuple_version++;
   h.hard = h.unschedulable ? UNSCHED_BIT : 0;
   h.prefer = 0;
   for (auto &t : h.hard_taints) {
@@ -2661,6 +2776,7 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
       return e ? std::atoi(e) : dflt;
     };
     x->early_fix = env_u("KS_EARLY_FIX", 1) != 0;
+    x->tuple_guess = env_u("KS_TUPLE_GUESS", 1) != 0;
     x->timing_every = (uint32_t)std::max(1, env_u("KS_TIMING_EVERY", 8));
     x->sweep_blocks = (uint32_t)std::max(1, env_u("KS_SWEEP_BLOCKS", 8192));
     const int en = env_u("KS_EXT_NPL", 2);  // geometry experiments only
@@ -2833,6 +2949,7 @@ ks_status ks_nodes_upsert(ks_ctx *c, const ks_node *nodes, const uint32_t *slots
   const uint32_t nodes_n = n;
   if (!c || (n && (!nodes || !slots))) return KS_ERR_INVALID;
   if (ks_status dst_ = drain_async(c)) return dst_;
+  c->tuple_version++;
   HIPC(c, hipSetDevice(c->cfg.device));
   // Events are applied in order; a slot named twice in one call ends in its
   // last state (one device row per distinct slot, so the scatter is race-free).
@@ -3014,6 +3131,7 @@ ks_status ks_nodes_upsert(ks_ctx *c, const ks_node *nodes, const uint32_t *slots
 ks_status ks_nodes_delete(ks_ctx *c, const uint32_t *slots, uint32_t n) {
   if (!c || (n && !slots)) return KS_ERR_INVALID;
   if (ks_status dst_ = drain_async(c)) return dst_;
+  c->tuple_version++;
   HIPC(c, hipSetDevice(c->cfg.device));
   flush_bound(c);  // the deleted nodes' records go with them
   std::vector<uint32_t> pos(n);

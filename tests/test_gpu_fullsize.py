@@ -117,7 +117,8 @@ def test_c3_hetero_1m_replay():
 
 def test_c4_labeled_1m_replay_early_fix():
     # the C4 bench path: EXT sweep (2 nodes per lane), early FIX, compacted FIX list
-    r, dbg = run_fullsize(synth.LABELED, synth.pods(synth.LABELED, BATCH, 2), prefill=True)
+    r, dbg = run_fullsize(synth.LABELED, synth.pods(synth.LABELED, BATCH, 2), prefill=True,
+                          env={"KS_TUPLE_GUESS": "0"})  # simple guesses: the FIX path runs often
     assert dbg[4] > 0, "no pod was re-swept with a measured normaliser (FIX path not exercised)"
     assert (r["status"] == 1).any() and (r["status"] == 0).mean() > 0.9
 
@@ -125,8 +126,14 @@ def test_c4_labeled_1m_replay_early_fix():
 def test_c4_labeled_1m_replay_merge_fix():
     # the same with the FIX sweep behind the merge (the multi-rank order, one rank)
     r, dbg = run_fullsize(synth.LABELED, synth.pods(synth.LABELED, BATCH, 5), prefill=True,
-                          env={"KS_EARLY_FIX": "0"})
+                          env={"KS_EARLY_FIX": "0", "KS_TUPLE_GUESS": "0"})
     assert dbg[4] > 0
+
+
+def test_c4_labeled_1m_replay_tuple_guess():
+    # the default (node-tuple normaliser guesses): the bench configuration
+    r, dbg = run_fullsize(synth.LABELED, synth.pods(synth.LABELED, BATCH, 7), prefill=True)
+    assert (r["status"] == 0).mean() > 0.9
 
 
 def test_kwok_1m_requestless_replay():

@@ -81,9 +81,16 @@ def test_upsert_rejects_duplicate_names_atomically():
         assert s.node_states([0])[0].alloc_milli_cpu == 1000
 
 
-def test_wrong_normaliser_guess_is_reswept():
-    # normalizer_guess_wrong: pods x, pref and pref-one-feasible are scored with a
-    # wrong guessed max first; the FIX-mode sweep must run for exactly those
+@pytest.mark.parametrize("tuple_guess,fixes", [("0", 3), ("1", 2)])
+def test_wrong_normaliser_guess_is_reswept(tuple_guess, fixes, monkeypatch):
+    # normalizer_guess_wrong: with the simple guesses (worst prefer-taint word,
+    # sum of preferred weights) pods x, pref and pref-one-feasible are scored
+    # with a wrong max first and the FIX-mode sweep must run for exactly those;
+    # the node-tuple guesses (KS_TUPLE_GUESS, default) get pref-one-feasible's
+    # NodeAffinity max and pref's right (the tuples a pod's label / taint
+    # filters pass), and x and pref stay wrong (their worst node fails on
+    # resources, which tuples do not see)
+    monkeypatch.setenv("KS_TUPLE_GUESS", tuple_guess)
     nodes, pods, exp = SCENARIOS["normalizer_guess_wrong"]()
     a = Arena()
     na, n = nodes_array(nodes, a)
@@ -99,7 +106,7 @@ def test_wrong_normaliser_guess_is_reswept():
         assert s.lib.ks_debug_counters(s.ctx, dbg) == 0
     assert_results_equal(got, want, m, "normalizer_guess_wrong")
     check(res_array(got, m), exp)
-    assert dbg[4] == 3, list(dbg)
+    assert dbg[4] == fixes, list(dbg)
 
 
 def test_event_log_mixed_kinds_in_order():
@@ -163,6 +170,7 @@ def test_fix_list_spans_several_groups(early, monkeypatch):
     from scenarios import node, pod
 
     monkeypatch.setenv("KS_EARLY_FIX", early)
+    monkeypatch.setenv("KS_TUPLE_GUESS", "0")  # simple guesses: every no-match term is guessed wrong
     Gi = 1 << 30
     nodes = [node(f"n{i}", cpu=(8 + 8 * (i % 5)) * 1000, mem=(32 << (i % 4)) * Gi,
                   labels={"zone": f"z{i % 3}", "disk": "ssd" if i % 4 == 0 else "hdd"},
