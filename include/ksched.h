@@ -486,6 +486,12 @@ ks_status ks_node_states(ks_ctx *ctx, const uint32_t *slots, uint32_t n, ks_node
 #define KS_COMM_ID_BYTES 128
 ks_status ks_comm_unique_id(uint8_t out[KS_COMM_ID_BYTES]);
 ks_status ks_comm_init(ks_ctx *ctx, const uint8_t id[KS_COMM_ID_BYTES]);
+/* In-process communicator: ctxs[r] (world_size n, rank r) are contexts of
+ * this process -- one device or several -- each then driven by its own host
+ * thread; the collectives above run as device copies ordered by stream events
+ * instead of RCCL (which refuses two ranks on one GPU).  It exists so the
+ * multi-rank path can be tested on one GPU; a deployment uses ks_comm_init. */
+ks_status ks_comm_init_local(ks_ctx *const *ctxs, uint32_t n);
 /* Element-wise max of n doubles over all ranks (in place); also a barrier. */
 ks_status ks_comm_allreduce_max(ks_ctx *ctx, double *values, uint32_t n);
 

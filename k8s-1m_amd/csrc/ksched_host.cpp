@@ -15,6 +15,7 @@
 
 #include <algorithm>
 #include <array>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -284,6 +285,45 @@ struct ks_batch {
   std::string run_err;
 };
 
+// In-process communicator (ks_comm_init_local): the ranks are contexts of one
+// process -- on one device or several -- each driven by its own host thread.
+// A collective is a host rendezvous exchanging (event, device pointer) pairs,
+// device-to-device copies ordered by stream waits on the peers' events, and a
+// second rendezvous whose events hold every rank's stream until all peers have
+// read its buffers: the ordering an RCCL collective gives, without RCCL (which
+// refuses two ranks on one GPU).  Test plumbing for the multi-rank path.
+struct LocalGroup {
+  struct Post {
+    hipEvent_t ev = nullptr;
+    const void *ptr = nullptr;
+    std::vector<double> vals;
+  };
+  explicit LocalGroup(uint32_t n) : world(n), posts(n), snap(n) {}
+  uint32_t world;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<Post> posts, snap;
+  uint32_t arrived = 0;
+  uint64_t gen = 0;
+  // Post this rank's entry and wait for every rank's; false after 300 s (a
+  // peer failed and will never arrive).
+  bool exchange(uint32_t rank, Post p, std::vector<Post> &out) {
+    std::unique_lock<std::mutex> g(mu);
+    posts[rank] = std::move(p);
+    const uint64_t my = gen;
+    if (++arrived == world) {
+      snap = posts;
+      arrived = 0;
+      ++gen;
+      cv.notify_all();
+    } else if (!cv.wait_for(g, std::chrono::seconds(300), [&] { return gen != my; })) {
+      return false;
+    }
+    out = snap;
+    return true;
+  }
+};
+
 struct ks_ctx {
   ks_config cfg{};
   std::string err;
@@ -404,8 +444,12 @@ struct ks_ctx {
   int64_t *d_sraw = nullptr;
   uint64_t *d_spart = nullptr;
   uint32_t *h_seg = nullptr;       // pinned: start pod of a round-kernel segment
-  // comm
+  // comm: RCCL, or an in-process group of contexts (tests of the multi-rank path on one GPU)
   ncclComm_t comm = nullptr;
+  std::shared_ptr<LocalGroup> lgroup;
+  hipEvent_t lg_ev[2] = {nullptr, nullptr};  // posted / finished
+  uint32_t *d_lgstage = nullptr;             // all-reduce input as peers read it
+  bool has_comm() const { return comm != nullptr || lgroup != nullptr; }
   // stats
   ks_stats stats{};
   bool timing = false;
@@ -2269,6 +2313,67 @@ static ks_status hand_wait(ks_ctx *c, hipStream_t wt, int f, hipEvent_t ev, uint
   return KS_OK;
 }
 
+// ------------------------------------------------------------- collectives
+// RCCL when ks_comm_init made a communicator, else the in-process group.
+
+ks_status lg_exchange(ks_ctx *c, LocalGroup::Post p, std::vector<LocalGroup::Post> &out) {
+  if (!c->lgroup->exchange(c->cfg.rank, std::move(p), out))
+    return c->fail(KS_ERR_COMM, "in-process communicator: a peer rank did not arrive within 300 s");
+  return KS_OK;
+}
+
+// Second rendezvous of a local collective: the stream continues only once
+// every peer's copies out of this rank's buffers are done.
+ks_status lg_finish(ks_ctx *c, hipStream_t st) {
+  HIPC(c, hipEventRecord(c->lg_ev[1], st));
+  std::vector<LocalGroup::Post> ps;
+  ks_status e = lg_exchange(c, {c->lg_ev[1], nullptr, {}}, ps);
+  if (e) return e;
+  for (uint32_t j = 0; j < c->lgroup->world; ++j)
+    if (j != c->cfg.rank) HIPC(c, hipStreamWaitEvent(st, ps[j].ev, 0));
+  return KS_OK;
+}
+
+// In place: rank r's slice [r * bytes, (r + 1) * bytes) of buf -> every rank's buf.
+ks_status coll_allgather(ks_ctx *c, void *buf, size_t bytes, hipStream_t st) {
+  const uint32_t r = c->cfg.rank;
+  if (c->comm) {
+    NCCLC(c, ncclAllGather((uint8_t *)buf + (size_t)r * bytes, buf, bytes, ncclUint8, c->comm, st));
+    return KS_OK;
+  }
+  HIPC(c, hipEventRecord(c->lg_ev[0], st));
+  std::vector<LocalGroup::Post> ps;
+  ks_status e = lg_exchange(c, {c->lg_ev[0], buf, {}}, ps);
+  if (e) return e;
+  for (uint32_t j = 0; j < c->lgroup->world; ++j) {
+    if (j == r) continue;
+    HIPC(c, hipStreamWaitEvent(st, ps[j].ev, 0));
+    HIPC(c, hipMemcpyAsync((uint8_t *)buf + (size_t)j * bytes, (const uint8_t *)ps[j].ptr + (size_t)j * bytes, bytes,
+                           hipMemcpyDeviceToDevice, st));
+  }
+  return lg_finish(c, st);
+}
+
+// In place: element-wise max of n uint32 over all ranks.
+ks_status coll_allreduce_max_u32(ks_ctx *c, uint32_t *buf, size_t n, hipStream_t st) {
+  if (c->comm) {
+    NCCLC(c, ncclAllReduce(buf, buf, n, ncclUint32, ncclMax, c->comm, st));
+    return KS_OK;
+  }
+  if (n > 4 * (size_t)MAX_P) return c->fail(KS_ERR_INVALID, "in-process all-reduce of %zu words", n);
+  HIPC(c, hipMemcpyAsync(c->d_lgstage, buf, n * 4, hipMemcpyDeviceToDevice, st));
+  HIPC(c, hipEventRecord(c->lg_ev[0], st));
+  std::vector<LocalGroup::Post> ps;
+  ks_status e = lg_exchange(c, {c->lg_ev[0], c->d_lgstage, {}}, ps);
+  if (e) return e;
+  for (uint32_t j = 0; j < c->lgroup->world; ++j) {
+    if (j == c->cfg.rank) continue;
+    HIPC(c, hipStreamWaitEvent(st, ps[j].ev, 0));
+    HIPC(c, launch_umax_u32(buf, (const uint32_t *)ps[j].ptr, (uint32_t)n, st));
+  }
+  return lg_finish(c, st);
+}
+
 // One device-driven round (all kernels read the queue head from d_start).
 // Round k of a pipeline run (k = 0 starts it: the table holds every previous
 // round).  Stream order, with sweep k+1 overlapping merge .. patch k and resolve k:
@@ -2282,8 +2387,8 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k, uint32_t end) {
   // Timing events cost the main stream ~10 us of dispatch per sweep, so only
   // every KS_TIMING_EVERY-th round (default 8) is timed.
   const bool tm = c->timing && (c->round_seq + 1) % c->timing_every == 0;
-  // RCCL path whenever a communicator exists (also a 1-rank one: exercised by tests)
-  const bool multi = c->comm != nullptr;
+  // multi-rank path whenever a communicator exists (also a 1-rank one: exercised by tests)
+  const bool multi = c->has_comm();
   const uint32_t nloc = multi ? 1 : c->S;
   const uint32_t shard0 = multi ? c->cfg.rank : 0;
   const uint32_t knpl = kernel_npl(c, b->ext);
@@ -2403,8 +2508,7 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k, uint32_t end) {
   if (b->norm && !early) {
     // the sweep scored normalising plugins with each pod's guessed maxima:
     // measure (all ranks), flag the wrong guesses, re-sweep + re-merge those pods
-    if (multi)
-      NCCLC(c, ncclAllReduce(c->d_pstat, c->d_pstat, 4 * c->P, ncclUint32, ncclMax, c->comm, ss));
+    if (multi && (st = coll_allreduce_max_u32(c, (uint32_t *)c->d_pstat, 4 * (size_t)c->P, ss))) return st;
     HIPC(c, launch_norm_check(a, ss));
     RoundArgs f = a;
     f.fix = 1;
@@ -2415,7 +2519,7 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k, uint32_t end) {
   }
   if (multi) {
     const size_t words = (size_t)c->P * RW;
-    NCCLC(c, ncclAllGather(a.srec + (size_t)c->cfg.rank * words, a.srec, words * 8, ncclUint8, c->comm, ss));
+    if ((st = coll_allgather(c, a.srec, words * 8, ss))) return st;
   }
   if (c->S > 1) HIPC(c, launch_merge_shards(a, ss));
   HIPC(c, launch_gather_cand(a, b->ext, ss));
@@ -2535,8 +2639,8 @@ ks_status run_batch(ks_ctx *c, ks_batch *b) {
                    b->dict_version, c->dict_version);
   if (b->names_version && b->names_version != c->names_version)
     return c->fail(KS_ERR_STALE, "batch resolved node names before the node set changed");
-  if (c->cfg.world_size > 1 && !c->comm) return c->fail(KS_ERR_COMM, "world_size > 1 but ks_comm_init not called");
-  if (c->comm && c->S != c->cfg.world_size)
+  if (c->cfg.world_size > 1 && !c->has_comm()) return c->fail(KS_ERR_COMM, "world_size > 1 but ks_comm_init not called");
+  if (c->has_comm() && c->S != c->cfg.world_size)
     return c->fail(KS_ERR_INVALID, "RCCL sharding needs one shard per rank (virtual_shards must be 1)");
   HIPC(c, hipSetDevice(c->cfg.device));
   ks_status st0;
@@ -2547,7 +2651,7 @@ ks_status run_batch(ks_ctx *c, ks_batch *b) {
     if ((st0 = upload_dirty_ext(c, c->xm))) return st0;
   }
   if (!b->uploaded && (st0 = upload_batch(c, b))) return st0;
-  if (b->any_spread && c->comm)
+  if (b->any_spread && c->has_comm())
     return c->fail(KS_ERR_UNSUPPORTED, "topology spread pods need a single-rank context");
   // Selector classes each pod matches, against the classes live now: the
   // spread path's commits and the round kernels' (class_commit) count them.
@@ -2906,6 +3010,9 @@ void ks_close(ks_ctx *c) {
   if (c->rstream) (void)hipStreamSynchronize(c->rstream);
   if (c->sstream) (void)hipStreamSynchronize(c->sstream);
   if (c->comm) ncclCommDestroy(c->comm);
+  for (auto &e : c->lg_ev)
+    if (e) (void)hipEventDestroy(e);
+  if (c->d_lgstage) (void)hipFree(c->d_lgstage);
   void *bufs[] = {c->t.acpu, c->t.amem, c->t.rcpu, c->t.rmem, c->t.zcpu, c->t.zmem, c->t.apods,
                   c->t.npods, c->t.hard, c->t.prefer, c->t.lab, c->t.num, c->d_shards, c->d_slot_pos,
                   c->d_start, c->d_norm, c->d_norm_inv, c->d_pstat, c->d_fix, c->d_brec, c->d_srec, c->d_frec,
@@ -3673,6 +3780,7 @@ ks_status ks_comm_unique_id(uint8_t out[KS_COMM_ID_BYTES]) {
 
 ks_status ks_comm_init(ks_ctx *c, const uint8_t id[KS_COMM_ID_BYTES]) {
   if (!c || !id) return KS_ERR_INVALID;
+  if (c->has_comm()) return c->fail(KS_ERR_INVALID, "the context already has a communicator");
   if (ks_status dst_ = drain_async(c)) return dst_;
   HIPC(c, hipSetDevice(c->cfg.device));
   ncclUniqueId uid;
@@ -3681,11 +3789,42 @@ ks_status ks_comm_init(ks_ctx *c, const uint8_t id[KS_COMM_ID_BYTES]) {
   return KS_OK;
 }
 
+ks_status ks_comm_init_local(ks_ctx *const *ctxs, uint32_t n) {
+  if (!ctxs || n == 0 || n > (uint32_t)MAX_SHARDS) return KS_ERR_INVALID;
+  for (uint32_t r = 0; r < n; ++r) {
+    ks_ctx *c = ctxs[r];
+    if (!c) return KS_ERR_INVALID;
+    if (c->cfg.world_size != n || c->cfg.rank != r)
+      return c->fail(KS_ERR_INVALID, "context %u: world_size %u rank %u, expected %u / %u", r, c->cfg.world_size,
+                     c->cfg.rank, n, r);
+    if (c->has_comm()) return c->fail(KS_ERR_INVALID, "context %u already has a communicator", r);
+  }
+  auto g = std::make_shared<LocalGroup>(n);
+  for (uint32_t r = 0; r < n; ++r) {
+    ks_ctx *c = ctxs[r];
+    if (ks_status dst_ = drain_async(c)) return dst_;
+    HIPC(c, hipSetDevice(c->cfg.device));
+    for (auto &e : c->lg_ev) HIPC(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIPC(c, hipMalloc((void **)&c->d_lgstage, 4 * (size_t)MAX_P * sizeof(uint32_t)));
+    c->lgroup = g;
+  }
+  return KS_OK;
+}
+
 ks_status ks_comm_allreduce_max(ks_ctx *c, double *values, uint32_t n) {
   if (!c || (n && !values)) return KS_ERR_INVALID;
   if (ks_status dst_ = drain_async(c)) return dst_;
-  if (!c->comm) return c->fail(KS_ERR_COMM, "ks_comm_init not called");
+  if (!c->has_comm()) return c->fail(KS_ERR_COMM, "ks_comm_init not called");
   HIPC(c, hipSetDevice(c->cfg.device));
+  if (c->lgroup) {  // host values: a rendezvous after this rank's queued work has finished
+    HIPC(c, hipStreamSynchronize(c->stream));
+    std::vector<LocalGroup::Post> ps;
+    ks_status e = lg_exchange(c, {nullptr, nullptr, std::vector<double>(values, values + n)}, ps);
+    if (e) return e;
+    for (const auto &p : ps)
+      for (uint32_t i = 0; i < n && i < p.vals.size(); ++i) values[i] = std::max(values[i], p.vals[i]);
+    return KS_OK;
+  }
   ks_status st = xfer_begin(c, 2 * (size_t)n * 8 + 1024, (size_t)n * 8 + 1024);
   if (st) return st;
   double *d = dscratch<double>(c, n);
@@ -3710,7 +3849,7 @@ ks_status ks_get_stats(ks_ctx *c, ks_stats *out) {
   if (st) return st;
   *out = c->stats;
   // (pod, node) evaluations of this rank's sweeps: pods swept x present local nodes
-  const bool multi = c->comm != nullptr;
+  const bool multi = c->has_comm();
   uint64_t local = 0;
   for (uint32_t q = 0; q < c->S; ++q) {
     if (multi && q != c->cfg.rank) continue;

@@ -118,6 +118,7 @@ hipError_t launch_class_commit(const DevResult *res, const uint64_t *cmask, cons
                                uint32_t npos, uint32_t lo, uint32_t hi, hipStream_t st);
 hipError_t launch_scatter_u32(uint32_t *col, const uint64_t *idx, const uint32_t *val, uint32_t n, hipStream_t st);
 hipError_t launch_add_u32(uint32_t *col, const uint64_t *idx, const int32_t *delta, uint32_t n, hipStream_t st);
+hipError_t launch_umax_u32(uint32_t *dst, const uint32_t *src, uint32_t n, hipStream_t st);
 hipError_t launch_scatter_i64(int64_t *col, const uint64_t *idx, const int64_t *val, uint32_t n, bool add,
                               hipStream_t st);
 

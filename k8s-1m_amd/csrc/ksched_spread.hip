@@ -876,6 +876,11 @@ __global__ void add_u32_kernel(uint32_t *col, const uint64_t *idx, const int32_t
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) atomicAdd(&col[idx[i]], (uint32_t)delta[i]);
 }
+// dst[i] = max(dst[i], src[i]) (the in-process communicator's all-reduce(max))
+__global__ void umax_u32_kernel(uint32_t *dst, const uint32_t *src, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = max(dst[i], src[i]);
+}
 __global__ void scatter_i64_kernel(int64_t *col, const uint64_t *idx, const int64_t *val, uint32_t n, uint32_t add) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -933,6 +938,12 @@ hipError_t launch_scatter_i64(int64_t *col, const uint64_t *idx, const int64_t *
 hipError_t launch_add_u32(uint32_t *col, const uint64_t *idx, const int32_t *delta, uint32_t n, hipStream_t st) {
   if (!n) return hipSuccess;
   add_u32_kernel<<<(n + 255) / 256, 256, 0, st>>>(col, idx, delta, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_umax_u32(uint32_t *dst, const uint32_t *src, uint32_t n, hipStream_t st) {
+  if (!n) return hipSuccess;
+  umax_u32_kernel<<<(n + 255) / 256, 256, 0, st>>>(dst, src, n);
   return hipGetLastError();
 }
 

@@ -286,7 +286,7 @@ STRUCTS = {
 KSCHED_SYMBOLS = [
     "ks_config_default", "ks_open", "ks_close", "ks_last_error", "ks_abi_version", "ks_nodes_upsert",
     "ks_nodes_delete", "ks_pods_add", "ks_pods_remove", "ks_events_apply", "ks_schedule", "ks_batch_prepare", "ks_batch_run",
-    "ks_batch_results", "ks_batch_free", "ks_batch_submit", "ks_batch_wait", "ks_pods_check", "ks_plugin_scores", "ks_node_states", "ks_comm_unique_id",
+    "ks_batch_results", "ks_batch_free", "ks_batch_submit", "ks_batch_wait", "ks_pods_check", "ks_plugin_scores", "ks_node_states", "ks_comm_unique_id", "ks_comm_init_local",
     "ks_comm_init", "ks_comm_allreduce_max", "ks_get_stats", "ks_reset_stats", "ks_set_timing",
     "ks_debug_counters",
 ]
@@ -349,6 +349,7 @@ def ksched_lib() -> C.CDLL:
     L.ks_node_states.argtypes = [vp, P(C.c_uint32), C.c_uint32, P(KsNodeState)]
     L.ks_comm_unique_id.argtypes = [P(C.c_uint8)]
     L.ks_comm_init.argtypes = [vp, P(C.c_uint8)]
+    L.ks_comm_init_local.argtypes = [P(vp), C.c_uint32]
     L.ks_comm_allreduce_max.argtypes = [vp, P(C.c_double), C.c_uint32]
     L.ks_get_stats.argtypes = [vp, P(KsStats)]
     L.ks_reset_stats.argtypes = [vp]

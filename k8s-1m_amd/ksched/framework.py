@@ -307,6 +307,17 @@ class Scheduler:
         buf = (C.c_uint8 * 128).from_buffer_copy(uid)
         self._ok(self.lib.ks_comm_init(self.ctx, buf))
 
+    @staticmethod
+    def comm_init_local(scheds: Sequence["Scheduler"]):
+        """In-process communicator over contexts of this process (rank r =
+        scheds[r]; one GPU may hold them all): the multi-rank path without
+        RCCL, for tests.  Each rank must then be driven from its own thread."""
+        lib = _abi.ksched_lib()
+        arr = (C.c_void_p * len(scheds))(*[s.ctx.value for s in scheds])
+        st = lib.ks_comm_init_local(arr, len(scheds))
+        if st != 0:
+            raise _abi.KschedError(st, lib.ks_last_error(scheds[0].ctx).decode())
+
     def allreduce_max(self, values):
         """Element-wise max over ranks (RCCL); doubles as a barrier."""
         arr = (C.c_double * max(1, len(values)))(*values)
