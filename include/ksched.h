@@ -412,6 +412,29 @@ int32_t ks_abi_version(void);
 ks_status ks_nodes_upsert(ks_ctx *ctx, const ks_node *nodes, const uint32_t *slots, uint32_t n);
 ks_status ks_nodes_delete(ks_ctx *ctx, const uint32_t *slots, uint32_t n);
 
+/* Generation-based snapshot update (upstream Cache.UpdateSnapshot,
+ * pkg/scheduler/internal/cache/cache.go; the reference's shards call it once
+ * per ScheduleOne through the fork, scheduler.go:543): the cache's NodeInfos
+ * -- all of them, or any superset of those changed since the last call --
+ * each with its NodeInfo.Generation.  An item whose generation is not above
+ * the last one applied to its slot is already in the snapshot and skipped
+ * (replayed or reordered deliveries are harmless); of several items for one
+ * slot in a call the highest generation wins.  deleted = 1 is RemoveNode
+ * (the node leaves with its pods; skipped if the slot is empty), otherwise
+ * AddNode / UpdateNode of `node` (the slot's pods stay: pods arrive through
+ * ks_pods_add / ks_pods_remove / ks_events_apply).  Deletions are applied
+ * before upserts, so a name may move to another slot within one call.
+ * *generation receives the highest generation applied so far (the snapshot's
+ * generation), *applied the number of items applied (either may be null). */
+typedef struct {
+  uint32_t slot;
+  uint32_t deleted;
+  int64_t generation;
+  const ks_node *node; /* deleted = 0 */
+} ks_node_info;
+ks_status ks_snapshot_update(ks_ctx *ctx, const ks_node_info *items, uint32_t n, int64_t *generation,
+                             uint32_t *applied);
+
 /* Pod cache events: NodeInfo.AddPod (bind / assume) and RemovePod (delete). */
 ks_status ks_pods_add(ks_ctx *ctx, const ks_pod *pods, const uint32_t *slots, uint32_t n);
 ks_status ks_pods_remove(ks_ctx *ctx, const ks_pod *pods, const uint32_t *slots, uint32_t n);

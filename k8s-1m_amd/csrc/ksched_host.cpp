@@ -372,6 +372,9 @@ struct ks_ctx {
   // host mirror / dictionaries
   std::vector<HostNode> nodes;
   uint32_t n_present = 0;
+  // ks_snapshot_update: the last NodeInfo.Generation applied per slot, and the max
+  std::vector<int64_t> slot_gen;
+  int64_t snapshot_gen = 0;
   std::unordered_map<std::string, uint32_t> str_ids{{"", 0}};
   std::vector<std::string> strs{""};
   std::unordered_map<uint32_t, uint32_t> name_slot;  // name id -> slot
@@ -3346,6 +3349,48 @@ ks_status ks_pods_add(ks_ctx *c, const ks_pod *pods, const uint32_t *slots, uint
 }
 ks_status ks_pods_remove(ks_ctx *c, const ks_pod *pods, const uint32_t *slots, uint32_t n) {
   return pods_delta(c, pods, slots, n, -1);
+}
+
+ks_status ks_snapshot_update(ks_ctx *c, const ks_node_info *items, uint32_t n, int64_t *generation,
+                             uint32_t *applied) {
+  if (!c || (n && !items)) return KS_ERR_INVALID;
+  if (c->slot_gen.size() != c->cap) c->slot_gen.assign(c->cap, INT64_MIN);
+  // newest item per slot (validated before anything changes)
+  std::unordered_map<uint32_t, uint32_t> best;
+  for (uint32_t i = 0; i < n; ++i) {
+    const ks_node_info &it = items[i];
+    if (it.slot >= c->cap) return c->fail(KS_ERR_NOT_FOUND, "item %u: slot %u >= capacity %u", i, it.slot, c->cap);
+    if (!it.deleted && !it.node) return c->fail(KS_ERR_INVALID, "item %u: no node", i);
+    if (it.generation <= c->slot_gen[it.slot]) continue;  // already in the snapshot
+    auto r = best.emplace(it.slot, i);
+    if (!r.second && items[r.first->second].generation < it.generation) r.first->second = i;
+  }
+  std::vector<uint32_t> order;
+  order.reserve(best.size());
+  for (auto &kv : best) order.push_back(kv.second);
+  std::sort(order.begin(), order.end());  // call order (deterministic)
+  std::vector<uint32_t> del;
+  std::vector<uint32_t> up_slots;
+  std::vector<ks_node> up;
+  for (uint32_t i : order) {
+    const ks_node_info &it = items[i];
+    if (it.deleted) {
+      if (c->nodes[it.slot].present) del.push_back(it.slot);
+    } else {
+      up_slots.push_back(it.slot);
+      up.push_back(*it.node);
+    }
+  }
+  ks_status st;
+  if (!del.empty() && (st = ks_nodes_delete(c, del.data(), (uint32_t)del.size()))) return st;
+  if (!up.empty() && (st = ks_nodes_upsert(c, up.data(), up_slots.data(), (uint32_t)up.size()))) return st;
+  for (uint32_t i : order) {
+    c->slot_gen[items[i].slot] = items[i].generation;
+    c->snapshot_gen = std::max(c->snapshot_gen, items[i].generation);
+  }
+  if (generation) *generation = c->snapshot_gen;
+  if (applied) *applied = (uint32_t)order.size();
+  return KS_OK;
 }
 
 ks_status ks_events_apply(ks_ctx *c, const ks_event *ev, uint32_t n) {

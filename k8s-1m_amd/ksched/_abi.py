@@ -175,6 +175,15 @@ UNMODELLED = {"host_ports": 1, "topology_spread": 2, "pod_affinity": 4, "volumes
 KS_EV_POD_ADD, KS_EV_POD_REMOVE, KS_EV_NODE_UPSERT, KS_EV_NODE_DELETE = 0, 1, 2, 3
 
 
+class KsNodeInfo(C.Structure):
+    _fields_ = [
+        ("slot", C.c_uint32),
+        ("deleted", C.c_uint32),
+        ("generation", C.c_int64),
+        ("node", C.POINTER(KsNode)),
+    ]
+
+
 class KsEvent(C.Structure):
     _fields_ = [
         ("kind", C.c_int32),
@@ -277,7 +286,7 @@ EXPECTED_SIZES = {
 STRUCTS = {
     "ks_label": KsLabel, "ks_taint": KsTaint, "ks_toleration": KsToleration, "ks_node": KsNode,
     "ks_container": KsContainer, "ks_requirement": KsRequirement, "ks_term": KsTerm,
-    "ks_preferred_term": KsPreferredTerm, "ks_pod": KsPod, "ks_event": KsEvent, "ks_result": KsResult,
+    "ks_preferred_term": KsPreferredTerm, "ks_pod": KsPod, "ks_event": KsEvent, "ks_node_info": KsNodeInfo, "ks_result": KsResult,
     "ks_node_score": KsNodeScore, "ks_node_state": KsNodeState, "ks_config": KsConfig,
     "ks_stats": KsStats, "ks_label_selector": KsLabelSelector, "ks_spread_constraint": KsSpreadConstraint,
     "ks_resource": KsResource, "ks_image": KsImage, "ks_pod_affinity_term": KsPodAffinityTerm,
@@ -286,7 +295,7 @@ STRUCTS = {
 KSCHED_SYMBOLS = [
     "ks_config_default", "ks_open", "ks_close", "ks_last_error", "ks_abi_version", "ks_nodes_upsert",
     "ks_nodes_delete", "ks_pods_add", "ks_pods_remove", "ks_events_apply", "ks_schedule", "ks_batch_prepare", "ks_batch_run",
-    "ks_batch_results", "ks_batch_free", "ks_batch_submit", "ks_batch_wait", "ks_pods_check", "ks_plugin_scores", "ks_node_states", "ks_comm_unique_id", "ks_comm_init_local",
+    "ks_batch_results", "ks_batch_free", "ks_batch_submit", "ks_batch_wait", "ks_pods_check", "ks_plugin_scores", "ks_node_states", "ks_comm_unique_id", "ks_comm_init_local", "ks_snapshot_update",
     "ks_comm_init", "ks_comm_allreduce_max", "ks_get_stats", "ks_reset_stats", "ks_set_timing",
     "ks_debug_counters",
 ]
@@ -336,6 +345,7 @@ def ksched_lib() -> C.CDLL:
     L.ks_pods_add.argtypes = [vp, P(KsPod), P(C.c_uint32), C.c_uint32]
     L.ks_pods_remove.argtypes = [vp, P(KsPod), P(C.c_uint32), C.c_uint32]
     L.ks_events_apply.argtypes = [vp, P(KsEvent), C.c_uint32]
+    L.ks_snapshot_update.argtypes = [vp, P(KsNodeInfo), C.c_uint32, P(C.c_int64), P(C.c_uint32)]
     L.ks_schedule.argtypes = [vp, P(KsPod), C.c_uint32, P(KsResult)]
     L.ks_batch_prepare.argtypes = [vp, P(KsPod), C.c_uint32, P(vp)]
     L.ks_batch_run.argtypes = [vp, vp]

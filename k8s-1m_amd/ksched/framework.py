@@ -184,6 +184,35 @@ class Scheduler:
     def upsert_nodes_raw(self, arr, slots, n: int, names: Optional[Sequence[str]] = None):
         self._ok(self.lib.ks_nodes_upsert(self.ctx, arr, slots, n))
 
+    def snapshot_update(self, items):
+        """Cache.UpdateSnapshot: items = [(slot, generation, Node or None for
+        RemoveNode)]; returns (snapshot generation, items applied)."""
+        a = Arena()
+        live = [(sl, g, nd) for sl, g, nd in items]
+        arr, _ = nodes_array([nd for _, _, nd in live if nd is not None], a) if any(
+            nd is not None for _, _, nd in live) else (None, 0)
+        infos = (_abi.KsNodeInfo * max(1, len(live)))()
+        k = 0
+        for i, (sl, g, nd) in enumerate(live):
+            infos[i].slot, infos[i].generation = sl, g
+            if nd is None:
+                infos[i].deleted = 1
+            else:
+                infos[i].node = C.pointer(arr[k])
+                k += 1
+        gen, applied = C.c_int64(), C.c_uint32()
+        self._ok(self.lib.ks_snapshot_update(self.ctx, infos, len(live), C.byref(gen), C.byref(applied)))
+        for sl, g, nd in live:
+            if nd is None:
+                old = self.names.pop(sl, None)
+                if old is not None and self.slots.get(old) == sl:
+                    self.slots.pop(old, None)
+        for sl, g, nd in live:
+            if nd is not None:
+                self.names[sl] = nd.name
+                self.slots[nd.name] = sl
+        return gen.value, applied.value
+
     def delete_nodes(self, names: Sequence[str]):
         slots = [self.slots[n] for n in names]
         sl = (C.c_uint32 * max(1, len(slots)))(*slots)

@@ -64,7 +64,7 @@ int main(void) {
   O(ks_pod, node_name) O(ks_pod, overhead_milli_cpu) O(ks_pod, n_containers) O(ks_pod, has_required)
   O(ks_pod, has_preferred) O(ks_pod, has_overhead)
   O(ks_result, total_score) O(ks_result, fail_counts) O(ks_result, flags)
-  O(ks_event, pod) O(ks_event, node)
+  O(ks_event, pod) O(ks_event, node) S(ks_node_info) O(ks_node_info, generation) O(ks_node_info, node)
   O(ks_node_score, total_score) O(ks_config, weight_fit) O(ks_config, weight_image)
   O(ks_stats, sweep_ms) O(ks_stats, resolve_launches)
   return 0;
