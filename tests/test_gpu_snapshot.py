@@ -108,10 +108,10 @@ def test_snapshot_rejects_bad_items_without_change():
     infos[0].slot, infos[0].generation, infos[0].node = 3, 5, node_ptr(ns.nodes, 3)
     infos[1].slot, infos[1].generation = 99, 6  # beyond capacity
     assert s.lib.ks_snapshot_update(s.ctx, infos, 2, None, None) != 0
-    assert s.node_states([3])[0].alloc_pods < 0  # nothing applied
+    assert s.node_states([3])[0].pod_count < 0  # nothing applied (empty slot)
     infos[1].slot, infos[1].deleted = 4, 1  # deleting an empty slot is a no-op
     g, a = C.c_int64(), C.c_uint32()
     assert s.lib.ks_snapshot_update(s.ctx, infos, 2, C.byref(g), C.byref(a)) == 0
     assert (g.value, a.value) == (6, 2)
-    assert s.node_states([3])[0].alloc_pods > 0
+    assert s.node_states([3])[0].pod_count == 0 and s.node_states([3])[0].alloc_pods > 0
     s.close()
