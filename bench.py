@@ -567,8 +567,6 @@ def report(args, sched, st, dbg, world, pods_timed, elapsed, scheduled, setup_s,
             "sweep_ms_total": round(st.sweep_ms, 3),
             "resolve_ms_total": round(st.resolve_ms, 3),
             "spread_pods": int(st.spread_pods),
-            "relayouts": int(st.relayouts),
-            "sweep_pruned_fraction": round(st.prune_pruned / st.prune_pairs, 4) if st.prune_pairs else None,
             "scheduled_fraction": round(scheduled / pods_timed, 4),
             "speculated_rounds_wasted": int(dbg[3]),  # since open (warmup included)
             "pods_reswept_wrong_norm_guess": int(dbg[4]),  # since open (warmup included)

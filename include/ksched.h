@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define KSCHED_ABI_VERSION 4
+#define KSCHED_ABI_VERSION 3
 
 /* ---------------------------------------------------------------- status */
 typedef int32_t ks_status;
@@ -531,9 +531,6 @@ typedef struct {
   double spread_ms;         /* Σ device time of timed spread-path pods (whole kernel chain) */
   uint64_t spread_pods_timed;
   uint64_t spread_pods;     /* pods scheduled by the spread path           */
-  uint64_t relayouts;       /* node-layout re-sorts for pruned sweeps (since open) */
-  uint64_t prune_pairs;     /* sampled (pod, block) pairs of pruned sweep launches */
-  uint64_t prune_pruned;    /* ... of which only Filter ran (score bound below threshold) */
 } ks_stats;
 ks_status ks_get_stats(ks_ctx *ctx, ks_stats *out);
 ks_status ks_reset_stats(ks_ctx *ctx);

@@ -350,17 +350,6 @@ struct ks_ctx {
   std::vector<Shard> shards;
   uint32_t npos = 0;
   std::vector<uint32_t> slot_pos;
-  // Pruned sweeps: KS_PRUNE (default 1), pilot blocks per
-  // shard (KS_PRUNE_PILOT, 64), threshold rank (KS_PRUNE_KT, default K / 4);
-  // the node layout is re-sorted by the LeastAllocated bound when it drifts
-  bool prune = true;
-  uint32_t prune_pilot = 64, prune_kt = 0;
-  uint32_t *d_prune_t = nullptr;  // [MAX_P]
-  bool layout_sorted = false;
-  uint64_t layout_changes = 0;    // node / pod-removal events since the last relayout
-  uint64_t relayouts = 0, batches_since_relayout = 0;
-  uint64_t prune_base[2] = {0, 0};  // device counters [5], [6] at the last relayout decision
-  double prune_fresh = -1.0;        // pruned fraction of the first batch after a relayout
   // device state
   NodeTable t{};
   Shard *d_shards = nullptr;
@@ -469,7 +458,7 @@ struct ks_ctx {
   bool timing = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_sweep, ev_resolve, ev_spread;
   std::vector<hipEvent_t> ev_pool;
-  uint64_t counters_base[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // device counters at the last ks_reset_stats
+  uint64_t counters_base[4] = {0, 0, 0, 0};  // device counters at the last ks_reset_stats
   uint64_t sweeps_issued = 0;                // main sweep launches since then (timed or not)
   uint64_t spread_seq = 0;                   // spread-path pods issued (timing sample)
   // Host<->device transfers of one ABI call: a pinned host staging buffer and a
@@ -1607,16 +1596,19 @@ ks_status spread_alloc(ks_ctx *c) {
   if (c->d_dom) return KS_OK;
   ks_status st;
   // domain columns then class columns, one allocation (one index space for scatters)
-  if ((st = dalloc(c, &c->d_dom, (size_t)(MAX_TOPO_KEYS + MAX_CLASSES) * c->npos)) ||
+  if ((st = dalloc(c, &c->d_dom, (size_t)(MAX_TOPO_KEYS + MAX_CLASSES) * c->npos)) || (st = dalloc(c, &c->d_pos_slot, c->npos)) ||
       (st = dalloc(c, &c->d_acc, 1)) || (st = dalloc(c, &c->d_sst, c->npos)) || (st = dalloc(c, &c->d_sraw, c->npos)) ||
       (st = dalloc(c, &c->d_spart, c->npos)) || (st = dalloc(c, &c->d_sraw2, c->npos)))
     return st;
   c->d_cnt = c->d_dom + (size_t)MAX_TOPO_KEYS * c->npos;
   HIPC(c, hipMemsetAsync(c->d_dom, 0xFF, (size_t)MAX_TOPO_KEYS * c->npos * 4, c->stream));
+  std::vector<uint32_t> ps(c->npos, SLOT_NONE);
+  for (uint32_t sl = 0; sl < c->cap; ++sl) ps[c->slot_pos[sl]] = sl;
   SpreadAcc acc{};
   for (int k = 0; k < MAX_SPREAD; ++k) acc.min_match[k] = 0xFFFFFFFFu;
   for (int k = 0; k < ACC_SHARDS; ++k) acc.sh[k].pts_min = acc.sh[k].ipa_min = ~0ull;
-  if ((st = xfer_begin(c, sizeof acc + 1024, 0)) || (st = h2d(c, c->d_acc, &acc, sizeof acc)) ||
+  if ((st = xfer_begin(c, (size_t)c->npos * 4 + sizeof acc + 1024, 0)) ||
+      (st = h2d(c, c->d_pos_slot, ps.data(), (size_t)c->npos * 4)) || (st = h2d(c, c->d_acc, &acc, sizeof acc)) ||
       (st = xfer_sync(c)))
     return st;
   return spread_scratch(c, 1024);
@@ -2464,9 +2456,6 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k, uint32_t end) {
   a.crow = c->d_crow + (size_t)q * c->P * c->K;
   a.cext = c->d_cext + (size_t)q * c->P * c->K;
   a.slot_pos = c->d_slot_pos;
-  a.pos_slot = c->d_pos_slot;
-  a.block0 = 0;
-  a.prune_t = nullptr;
   a.w = Weights{c->cfg.weight_fit, c->cfg.weight_balanced, c->cfg.weight_taint, c->cfg.weight_affinity,
                 c->cfg.weight_image};
   if ((size_t)nloc * c->P * bmax * sizeof(BlockRec) > c->brec_bytes)
@@ -2497,31 +2486,7 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k, uint32_t end) {
     HIPC(c, hipEventRecord(e0, c->stream));
   }
   if (early) HIPC(c, hipMemsetAsync(c->d_pstat, 0, (size_t)c->P * sizeof(PodStat), c->stream));
-  // Pruned sweep: the pilot blocks -- the best of every
-  // shard in relayout order -- are swept first; their lists bound each pod's
-  // K_T-th best key from below, and the rest of the blocks skip scoring where
-  // their TotalScore bound is below it
-  const uint32_t pilot = c->prune_pilot;
-  if (c->prune && c->layout_sorted && bmax >= 4 * pilot && pilot * nloc * BLOCK_KEYS <= 1024) {
-    const uint32_t kt = std::min(c->prune_kt ? c->prune_kt : std::max<uint32_t>(1, c->K / 4),
-                                 pilot * nloc * (uint32_t)BLOCK_KEYS);
-    auto geometry = [&](uint32_t nblk, RoundArgs &x) {  // pods per block filling the chip
-      uint32_t g = std::max<uint32_t>(1, std::min((want + nblk * nloc - 1) / (nblk * nloc), c->P));
-      x.pg = std::min<uint32_t>(std::max<uint32_t>((c->P + g - 1) / g, 1), MAX_PG);
-      return (c->P + x.pg - 1) / x.pg;
-    };
-    RoundArgs pa = a;
-    const uint32_t gp = geometry(pilot, pa);
-    HIPC(c, launch_sweep(pa, b->ext, pilot, gp, nloc, c->stream));
-    HIPC(c, launch_prune_threshold(a, pilot, nloc, kt, c->d_prune_t, c->stream));
-    RoundArgs pb = a;
-    pb.block0 = pilot;
-    pb.prune_t = c->d_prune_t;
-    const uint32_t gb = geometry(bmax - pilot, pb);
-    HIPC(c, launch_sweep(pb, b->ext, bmax - pilot, gb, nloc, c->stream));
-  } else {
-    HIPC(c, launch_sweep(a, b->ext, bmax, groups, nloc, c->stream));
-  }
+  HIPC(c, launch_sweep(a, b->ext, bmax, groups, nloc, c->stream));
   ++c->sweeps_issued;
   if (tm) {
     HIPC(c, hipEventRecord(e1, c->stream));
@@ -2669,127 +2634,6 @@ ks_status upload_batch(ks_ctx *c, ks_batch *b) {
   return KS_OK;
 }
 
-// ------------------------------------------------------------ relayout
-// Re-sort every shard's nodes by their LeastAllocated bound at zero request
-// (descending; the pruned sweep's pilot blocks are then the best nodes and
-// later blocks bound low): layout wave w of a shard takes ranks
-// [w * 64 * npl, (w + 1) * 64 * npl), its slots in ascending order over
-// (step, lane) -- the order the sweep's wave-local keys break ties in.
-// Every position-indexed device column is permuted; results never depend on
-// the layout (keys carry slots).
-ks_status relayout(ks_ctx *c) {
-  ks_status st;
-  const uint32_t cap = c->cap, npos = c->npos;
-  if ((st = xfer_begin(c, (size_t)cap + 1024, (size_t)cap + 1024))) return st;
-  uint8_t *d_ub = dscratch<uint8_t>(c, cap);
-  HIPC(c, launch_la_bound(c->t, c->d_slot_pos, d_ub, cap, c->stream));
-  std::vector<uint8_t> ub(cap);
-  if ((st = d2h(c, ub.data(), d_ub, cap)) || (st = xfer_sync(c))) return st;
-  std::vector<uint32_t> new_pos(c->slot_pos), src(npos), pos_slot(npos, SLOT_NONE);
-  for (uint32_t p = 0; p < npos; ++p) src[p] = p;
-  const uint32_t WS = WAVE * c->npl;
-  std::vector<uint32_t> order, bucket_n(256);
-  for (const Shard &sh : c->shards) {
-    // counting sort by bound, stable in slot order
-    std::fill(bucket_n.begin(), bucket_n.end(), 0u);
-    for (uint32_t l = 0; l < sh.count; ++l) bucket_n[ub[sh.lo + l]]++;
-    uint32_t acc = 0;
-    for (uint32_t v = 0; v < 256; ++v) {
-      const uint32_t n = bucket_n[v];
-      bucket_n[v] = acc;
-      acc += n;
-    }
-    order.assign(sh.count, 0);
-    for (uint32_t l = 0; l < sh.count; ++l) order[bucket_n[ub[sh.lo + l]]++] = sh.lo + l;
-    for (uint32_t i = 0; i < sh.count; i += WS) {
-      const uint32_t e = std::min(sh.count, i + WS);
-      std::sort(order.begin() + i, order.begin() + e);
-      for (uint32_t q = i; q < e; ++q) new_pos[order[q]] = sh.base + i + (q - i);
-    }
-    // padding positions of the shard keep empty rows: pair the old ones with the new ones
-    const uint32_t end = sh.base + sh.waves * WS;
-    std::vector<uint8_t> old_used(end - sh.base, 0), new_used(end - sh.base, 0);
-    for (uint32_t l = 0; l < sh.count; ++l) {
-      old_used[c->slot_pos[sh.lo + l] - sh.base] = 1;
-      new_used[new_pos[sh.lo + l] - sh.base] = 1;
-    }
-    uint32_t o = 0;
-    for (uint32_t q = 0; q < end - sh.base; ++q) {
-      if (new_used[q]) continue;
-      while (old_used[o]) ++o;
-      src[sh.base + q] = sh.base + o++;
-    }
-  }
-  for (uint32_t sl = 0; sl < cap; ++sl) {
-    src[new_pos[sl]] = c->slot_pos[sl];
-    pos_slot[new_pos[sl]] = sl;
-  }
-  // device: index, position maps, permuted columns
-  uint32_t *d_src = nullptr;
-  void *tmp = nullptr;
-  constexpr uint32_t GROUP = 8;  // columns per permute pass
-  HIPC(c, hipMalloc((void **)&d_src, (size_t)npos * 4));
-  HIPC(c, hipMalloc(&tmp, (size_t)npos * 8 * GROUP));
-  if ((st = xfer_begin(c, (size_t)npos * 8 + (size_t)cap * 4 + 1024, 0)) ||
-      (st = h2d(c, d_src, src.data(), (size_t)npos * 4)) ||
-      (st = h2d(c, c->d_pos_slot, pos_slot.data(), (size_t)npos * 4)) ||
-      (st = h2d(c, c->d_slot_pos, new_pos.data(), (size_t)cap * 4)))
-    return st;
-  auto permute = [&](void *col, uint32_t ncols, uint32_t wb) -> ks_status {
-    for (uint32_t c0 = 0; c0 < ncols; c0 += GROUP) {
-      const uint32_t nc = std::min(GROUP, ncols - c0);
-      uint8_t *base = (uint8_t *)col + (size_t)c0 * npos * wb;
-      HIPC(c, launch_permute_cols(tmp, base, d_src, npos, nc, wb, c->stream));
-      HIPC(c, hipMemcpyAsync(base, tmp, (size_t)nc * npos * wb, hipMemcpyDeviceToDevice, c->stream));
-    }
-    return KS_OK;
-  };
-  NodeTable &t = c->t;
-  for (void *col : {(void *)t.acpu, (void *)t.amem, (void *)t.rcpu, (void *)t.rmem, (void *)t.zcpu, (void *)t.zmem,
-                    (void *)t.hard, (void *)t.prefer})
-    if ((st = permute(col, 1, 8))) return st;
-  if ((st = permute(t.apods, 1, 4)) || (st = permute(t.npods, 1, 4)) || (st = permute(t.lab, LW, 8)) ||
-      (st = permute(t.num, NNUM, 8)))
-    return st;
-  if (c->d_dom && (st = permute(c->d_dom, MAX_TOPO_KEYS + MAX_CLASSES, 4))) return st;
-  if (c->d_tcnt && (st = permute(c->d_tcnt, c->tcnt_cap, 4))) return st;
-  if (c->d_xalloc && (st = permute(c->d_xalloc, 2 * MAX_XRES, 8))) return st;
-  if ((st = xfer_sync(c))) return st;
-  HIPC(c, hipFree(d_src));
-  HIPC(c, hipFree(tmp));
-  {
-    std::lock_guard<std::mutex> g(c->mu);
-    c->slot_pos.swap(new_pos);
-  }
-  c->layout_sorted = true;
-  c->layout_changes = 0;
-  c->batches_since_relayout = 0;
-  c->prune_fresh = -1.0;
-  c->relayouts++;
-  return KS_OK;
-}
-
-// Relayout policy, once per batch: the first batch, after node / pod-removal
-// events touching more than 1/64 of the nodes, or when the sampled pruned
-// fraction has fallen below 60 % of its value right after the last relayout.
-ks_status maybe_relayout(ks_ctx *c) {
-  if (!c->prune) return KS_OK;
-  uint64_t k[8];
-  ks_status st;
-  if ((st = xfer_begin(c, 1024, 0)) || (st = d2h(c, k, c->d_counters, sizeof k)) || (st = xfer_sync(c))) return st;
-  const uint64_t pruned = k[5] - c->prune_base[0], pairs = k[6] - c->prune_base[1];
-  c->prune_base[0] = k[5];
-  c->prune_base[1] = k[6];
-  bool go = !c->layout_sorted || c->layout_changes * 64 > c->n_present;
-  if (!go && pairs >= 64) {
-    const double frac = (double)pruned / (double)pairs;
-    if (c->prune_fresh < 0) c->prune_fresh = frac;
-    else if (c->batches_since_relayout >= 4 && frac < 0.6 * c->prune_fresh) go = true;
-  }
-  c->batches_since_relayout++;
-  return go ? relayout(c) : KS_OK;
-}
-
 // Run a prepared batch to completion on the scheduler streams; the results
 // land in the batch's pinned host buffer.
 ks_status run_batch(ks_ctx *c, ks_batch *b) {
@@ -2812,7 +2656,6 @@ ks_status run_batch(ks_ctx *c, ks_batch *b) {
   if (!b->uploaded && (st0 = upload_batch(c, b))) return st0;
   if (b->any_spread && c->has_comm())
     return c->fail(KS_ERR_UNSUPPORTED, "topology spread pods need a single-rank context");
-  if ((st0 = maybe_relayout(c))) return st0;
   // Selector classes each pod matches, against the classes live now: the
   // spread path's commits and the round kernels' (class_commit) count them.
   bool classes = false;
@@ -3045,9 +2888,6 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
     x->sweep_blocks = (uint32_t)std::max(1, env_u("KS_SWEEP_BLOCKS", 8192));
     const int en = env_u("KS_EXT_NPL", 2);  // geometry experiments only
     x->ext_npl = (uint32_t)(en == 4 || en == 8 ? en : 2);
-    x->prune = env_u("KS_PRUNE", 1) != 0;
-    x->prune_pilot = (uint32_t)std::max(1, std::min(256, env_u("KS_PRUNE_PILOT", 64)));
-    x->prune_kt = (uint32_t)std::max(0, env_u("KS_PRUNE_KT", 0));
   }
   {
     // Resolve runs on a high-priority stream on KS_RESOLVE_CUS (default 1) CUs
@@ -3134,15 +2974,11 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
       (st = dalloc(x, &x->d_norm_inv, 2 * 2 * (size_t)x->P)) ||
       (st = dalloc(x, &x->d_pstat, (size_t)x->P)) || (st = dalloc(x, &x->d_fix, 2 * MAX_P + MAX_P / MAX_PG)) ||
       (st = dalloc(x, &x->d_pipe, 8)) || (st = dalloc(x, &x->d_flags, 4)) || (st = dalloc(x, &x->d_carry, 2 * (size_t)MAX_P)) ||
-      (st = dalloc(x, &x->d_counters, 16)) || (st = dalloc(x, &x->d_pos_slot, x->npos)) ||
-      (st = dalloc(x, &x->d_prune_t, MAX_P)))
+      (st = dalloc(x, &x->d_counters, 16)))
     return st;
-  std::vector<uint32_t> ps(x->npos, SLOT_NONE);
-  for (uint32_t sl = 0; sl < x->cap; ++sl) ps[x->slot_pos[sl]] = sl;
-  if ((st = xfer_begin(x, x->S * sizeof(Shard) + (size_t)x->cap * 4 + (size_t)x->npos * 4 + 1024, 0)) ||
+  if ((st = xfer_begin(x, x->S * sizeof(Shard) + (size_t)x->cap * 4 + 1024, 0)) ||
       (st = h2d(x, x->d_shards, x->shards.data(), x->S * sizeof(Shard))) ||
-      (st = h2d(x, x->d_slot_pos, x->slot_pos.data(), (size_t)x->cap * 4)) ||
-      (st = h2d(x, x->d_pos_slot, ps.data(), (size_t)x->npos * 4)))
+      (st = h2d(x, x->d_slot_pos, x->slot_pos.data(), (size_t)x->cap * 4)))
     return st;
   HIPC(x, hipHostMalloc((void **)&x->h_start, 4, hipHostMallocDefault));
   HIPC(x, hipHostMalloc((void **)&x->h_seg, 4, hipHostMallocDefault));
@@ -3183,7 +3019,7 @@ void ks_close(ks_ctx *c) {
   void *bufs[] = {c->t.acpu, c->t.amem, c->t.rcpu, c->t.rmem, c->t.zcpu, c->t.zmem, c->t.apods,
                   c->t.npods, c->t.hard, c->t.prefer, c->t.lab, c->t.num, c->d_shards, c->d_slot_pos,
                   c->d_start, c->d_norm, c->d_norm_inv, c->d_pstat, c->d_fix, c->d_brec, c->d_srec, c->d_frec,
-                  c->d_counters, c->d_prune_t, c->d_crow, c->d_cext, c->d_pipe, c->d_carry, c->d_flags, c->d_dom,
+                  c->d_counters, c->d_crow, c->d_cext, c->d_pipe, c->d_carry, c->d_flags, c->d_dom,
                   c->d_pos_slot, c->d_dcnt, c->d_dflag, c->d_acc, c->d_sst, c->d_sraw, c->d_spart,
                   c->d_xalloc, c->d_tcnt, c->d_adcnt, c->d_sraw2};
   for (void *b : bufs)
@@ -3223,7 +3059,6 @@ ks_status ks_nodes_upsert(ks_ctx *c, const ks_node *nodes, const uint32_t *slots
   const uint32_t nodes_n = n;
   if (!c || (n && (!nodes || !slots))) return KS_ERR_INVALID;
   if (ks_status dst_ = drain_async(c)) return dst_;
-  c->layout_changes += n;
   c->tuple_version++;
   HIPC(c, hipSetDevice(c->cfg.device));
   // Events are applied in order; a slot named twice in one call ends in its
@@ -3406,7 +3241,6 @@ ks_status ks_nodes_upsert(ks_ctx *c, const ks_node *nodes, const uint32_t *slots
 ks_status ks_nodes_delete(ks_ctx *c, const uint32_t *slots, uint32_t n) {
   if (!c || (n && !slots)) return KS_ERR_INVALID;
   if (ks_status dst_ = drain_async(c)) return dst_;
-  c->layout_changes += n;
   c->tuple_version++;
   HIPC(c, hipSetDevice(c->cfg.device));
   flush_bound(c);  // the deleted nodes' records go with them
@@ -3514,7 +3348,6 @@ ks_status ks_pods_add(ks_ctx *c, const ks_pod *pods, const uint32_t *slots, uint
   return pods_delta(c, pods, slots, n, +1);
 }
 ks_status ks_pods_remove(ks_ctx *c, const ks_pod *pods, const uint32_t *slots, uint32_t n) {
-  if (c) c->layout_changes += n;  // freed capacity raises the nodes' score bounds
   return pods_delta(c, pods, slots, n, -1);
 }
 
@@ -4046,17 +3879,17 @@ ks_status ks_comm_allreduce_max(ks_ctx *c, double *values, uint32_t n) {
   return xfer_sync(c);
 }
 
-static ks_status read_counters(ks_ctx *c, uint64_t out[8]) {
+static ks_status read_counters(ks_ctx *c, uint64_t out[4]) {
   HIPC(c, hipSetDevice(c->cfg.device));
   ks_status st;
-  if ((st = xfer_begin(c, 1024, 0)) || (st = d2h(c, out, c->d_counters, 8 * sizeof(uint64_t)))) return st;
+  if ((st = xfer_begin(c, 1024, 0)) || (st = d2h(c, out, c->d_counters, 4 * sizeof(uint64_t)))) return st;
   return xfer_sync(c);
 }
 
 ks_status ks_get_stats(ks_ctx *c, ks_stats *out) {
   if (!c || !out) return KS_ERR_INVALID;
   if (ks_status dst_ = drain_async(c)) return dst_;
-  uint64_t k[8];
+  uint64_t k[4];
   ks_status st = read_counters(c, k);
   if (st) return st;
   *out = c->stats;
@@ -4074,9 +3907,6 @@ ks_status ks_get_stats(ks_ctx *c, ks_stats *out) {
   out->sweep_evals = c->sweeps_issued ? (uint64_t)((double)all_evals * (double)c->stats.sweep_launches /
                                                    (double)c->sweeps_issued)
                                       : 0;
-  out->relayouts = c->relayouts;
-  out->prune_pruned = k[5] - c->counters_base[5];
-  out->prune_pairs = k[6] - c->counters_base[6];
   out->rounds = k[0] - c->counters_base[0];
   out->pods_resolved = k[1] - c->counters_base[1];
   return KS_OK;

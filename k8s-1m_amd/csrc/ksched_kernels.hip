@@ -263,54 +263,31 @@ __global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
   // per pod and wave: feasible, first failures per plugin, #at max (tt, na), max raw (tt, na)
   constexpr int NCNT = NFILT + 5;
   __shared__ uint32_t s_cnt[MAX_PG][NW][NCNT];
-  __shared__ uint32_t s_ub[NW];
 
   const uint32_t start = uniform_u32(*a.sstart);
   const uint32_t sh = blockIdx.z;
   const Shard s = a.shards[a.shard0 + sh];
   const uint32_t wid = threadIdx.x / WAVE;
-  const uint32_t bx = blockIdx.x + a.block0;  // block of the shard (a pruned launch starts past the pilot blocks)
-  const uint32_t kw = bx * NW + wid;         // kernel wave
+  const uint32_t kw = blockIdx.x * NW + wid;  // kernel wave
   const uint32_t kwaves = s.waves * a.sub;
   const uint32_t lane = threadIdx.x % WAVE;
+  const uint32_t lwave = kw / a.sub, j0 = (kw % a.sub) * NPL;  // layout wave / first step
   const uint32_t p0 = start + blockIdx.y * a.pg;
   const uint32_t p1 = min(min(p0 + a.pg, start + a.P), a.npods);
-  if (p0 >= p1 || bx * NW >= kwaves) return;
+  if (p0 >= p1 || blockIdx.x * NW >= kwaves) return;
   // FIX mode: only the pods norm_check flagged (pod groups of MAX_PG)
   const bool fix = EXT && a.fix;
   if (fix && uniform_u32(a.fix_group[blockIdx.y]) == 0) return;
 
-  // Slots come from the position -> slot map (ks relayout orders a shard's
-  // nodes by their LeastAllocated bound; within a layout wave slots ascend
-  // with (step, lane), which the wave-local key order relies on).
   NodeRegs nr[NPL];
   NodeExt ne[EXT ? NPL : 1];
   static_for<NPL>([&](auto J) {
     constexpr int j = J;
+    const uint32_t l = (j0 + (uint32_t)j) * WAVE * s.waves + lane * s.waves + lwave;
     const uint32_t pos = s.base + kw * WAVE * NPL + (uint32_t)j * WAVE + lane;
-    const uint32_t slot = kw < kwaves ? a.pos_slot[pos] : SLOT_NONE;
-    load_core(a.t, pos, slot, slot != SLOT_NONE, nr[j]);
+    load_core(a.t, pos, s.lo + l, kw < kwaves && l < s.count, nr[j]);
     if constexpr (EXT) load_ext<LWU>(a.t, pos, nr[j].bits & 1u, ne[j]);
   });
-  // Pruned launch: the block's best LeastAllocated over its nodes at zero
-  // request (LA only falls as a request grows: an upper bound for every pod),
-  // so a pod whose threshold (the pilot's K_T-th best TotalScore) exceeds the
-  // block's best possible TotalScore skips scoring here: only Filter runs.
-  uint32_t ub_la = 0;
-  if (a.prune_t) {
-    uint32_t u = 0;
-    static_for<NPL>([&](auto J) {
-      constexpr int j = J;
-      const uint32_t la0 = (uint32_t)((least_requested(nr[j].lf100_cpu, 0.0, nr[j].inv_cpu) +
-                                       least_requested(nr[j].lf100_mem, 0.0, nr[j].inv_mem)) >> nr[j].lashift);
-      u = max(u, (nr[j].bits & 1u) ? la0 : 0u);
-    });
-    u = wave_max_u32_dpp(u);
-    if (lane == 0) s_ub[wid] = u;
-    __syncthreads();
-    static_for<NW>([&](auto W) { ub_la = max(ub_la, s_ub[W]); });
-  }
-  uint32_t n_pruned = 0;
 
   // per node, pod-independent: pod-count fit (also false for empty slots), and
   // the wave-local key position ~(step * 64 + lane)
@@ -329,16 +306,6 @@ __global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
     if (fix && r == FIX_NONE) continue;
     const uint32_t pi = start + r;
     const PodDev p = load_pod(a.pods, pi);
-    // TotalScore + 1 bound of this block for the pod: LA bound, BalancedAllocation,
-    // TaintToleration and NodeAffinity (normalised scores <= 100) at their maximum
-    uint32_t ub_tot1 = 0;
-    bool pruned = false;
-    if (a.prune_t) {
-      ub_tot1 = (uint32_t)__umul24((uint32_t)a.w.fit, ub_la) + (uint32_t)(a.w.ba * 100) + (uint32_t)(a.w.tt * 100) + 1u;
-      if (EXT && (p.flags & PF_HAS_PREF)) ub_tot1 += (uint32_t)(a.w.na * 100);
-      pruned = uniform_u32(a.prune_t[r]) > ub_tot1;
-      n_pruned += pruned;
-    }
     uint32_t tt_max = 0, na_max = 0;
     if (EXT && (p.flags & (PF_TT | PF_NA))) {
       tt_max = uniform_u32(fix ? a.norm_max[2 * r + 0] : p.tt_guess);
@@ -357,23 +324,16 @@ __global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
       const double rq_c = ((p.flags & PF_HAS_REQ) && p.req_cpu > 0) ? p.req_cpu_d : -__builtin_inf();
       const double rq_m = ((p.flags & PF_HAS_REQ) && p.req_mem > 0) ? p.req_mem_d : -__builtin_inf();
       const uint32_t cplus = (uint32_t)(a.w.tt * 100) + 1u;  // TaintToleration 100 (no prefer taints) + 1
-      if (pruned) {
-        static_for<NPL>([&](auto J) {
-          constexpr int j = J;
-          feas += popc_ballot(podfit[j] && !(rq_c > nr[j].free_cpu) && !(rq_m > nr[j].free_mem));
-        });
-      } else {
-        static_for<NPL>([&](auto J) {
-          constexpr int j = J;
-          const bool feasible = podfit[j] && !(rq_c > nr[j].free_cpu) && !(rq_m > nr[j].free_mem);
-          const uint32_t tot1 = (uint32_t)__umul24((uint32_t)a.w.fit, (uint32_t)score_la(p, nr[j])) +
-                                (uint32_t)__umul24((uint32_t)a.w.ba, (uint32_t)score_ba(p, nr[j])) + cplus;
-          const uint32_t key = feasible ? (tot1 << KEY32_POS_BITS) | (kpos0 - (uint32_t)j * WAVE) : 0u;
-          b2 = max(b2, min(b1, key));
-          b1 = max(b1, key);
-          feas += popc_ballot(feasible);
-        });
-      }
+      static_for<NPL>([&](auto J) {
+        constexpr int j = J;
+        const bool feasible = podfit[j] && !(rq_c > nr[j].free_cpu) && !(rq_m > nr[j].free_mem);
+        const uint32_t tot1 = (uint32_t)__umul24((uint32_t)a.w.fit, (uint32_t)score_la(p, nr[j])) +
+                              (uint32_t)__umul24((uint32_t)a.w.ba, (uint32_t)score_ba(p, nr[j])) + cplus;
+        const uint32_t key = feasible ? (tot1 << KEY32_POS_BITS) | (kpos0 - (uint32_t)j * WAVE) : 0u;
+        b2 = max(b2, min(b1, key));
+        b1 = max(b1, key);
+        feas += popc_ballot(feasible);
+      });
       f4 = vcount - feas;
     } else {
       // label programs once per pod for the lane's NPL nodes
@@ -417,15 +377,13 @@ __global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
         }
         if (!valid) st = ST_EMPTY;
         const bool feasible = st == ST_FEASIBLE;
-        uint32_t tot1 = 0;
-        if (!pruned)
-          tot1 = (uint32_t)__umul24((uint32_t)a.w.fit, (uint32_t)score_la(p, nr[j])) +
-                 (uint32_t)__umul24((uint32_t)a.w.ba, ABL_ON(8) ? (uint32_t)score_ba(p, nr[j]) : 50u) + 1u;
+        uint32_t tot1 = (uint32_t)__umul24((uint32_t)a.w.fit, (uint32_t)score_la(p, nr[j])) +
+                        (uint32_t)__umul24((uint32_t)a.w.ba, ABL_ON(8) ? (uint32_t)score_ba(p, nr[j]) : 50u) + 1u;
         uint32_t tts = 100u;
         bool at_tt = false, at_na = false;
         if (p.flags & PF_TT) {
           const uint32_t raw = (uint32_t)__popcll(ne[j].prefer & ~p.tol_prefer);
-          tts = ABL_ON(4) && !pruned ? 100u - normalize_inv(raw, inv_tt) : 100u;
+          tts = ABL_ON(4) ? 100u - normalize_inv(raw, inv_tt) : 100u;
           at_tt = feasible && raw == tt_max;
           over |= feasible && raw > tt_max;
           tmx = max(tmx, feasible ? raw : 0u);
@@ -434,14 +392,14 @@ __global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
         if (p.flags & PF_HAS_PREF) {
           uint32_t nas = 0u;
           if (p.flags & PF_NA) {
-            if (!pruned) nas = normalize_inv(praw[j], inv_na);
+            nas = normalize_inv(praw[j], inv_na);
             at_na = feasible && praw[j] == na_max;
             over |= feasible && praw[j] > na_max;
             nmx = max(nmx, feasible ? praw[j] : 0u);
           }
           tot1 += (uint32_t)__umul24((uint32_t)a.w.na, nas);
         }
-        const uint32_t key = feasible && !pruned ? (tot1 << KEY32_POS_BITS) | (kpos0 - (uint32_t)j * WAVE) : 0u;
+        const uint32_t key = feasible ? (tot1 << KEY32_POS_BITS) | (kpos0 - (uint32_t)j * WAVE) : 0u;
         b2 = max(b2, min(b1, key));
         b1 = max(b1, key);
         const uint64_t fb = __ballot(feasible), vb = __ballot(valid);
@@ -484,24 +442,15 @@ __global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
         }
       }
     }
-    // back to packed keys ((score + 1) << 32 | ~slot): the slot of wave-local
-    // position q = step * 64 + lane is that lane's nr[step].slot (keys are
-    // wave-uniform here, readlane ignores EXEC)
-    auto widen = [&](uint32_t k) -> uint64_t {
-      if (!k) return 0ull;
-      const uint32_t q = KEY32_POS_MASK - (k & KEY32_POS_MASK);
-      const uint32_t stp = q / WAVE;
-      uint32_t v = nr[0].slot;
-      static_for<NPL>([&](auto J) {
-        if ((uint32_t)J == stp) v = nr[J].slot;
-      });
-      const uint32_t slot = (uint32_t)__builtin_amdgcn_readlane((int)v, (int)(q % WAVE));
-      return ((uint64_t)(k >> KEY32_POS_BITS) << 32) | (uint64_t)(0xFFFFFFFFu - slot);
-    };
-    const uint64_t k1 = widen(c1), k2 = widen(c2);
-    // a pruned block bounds every feasible key it holds by its TotalScore bound
-    const uint64_t bound = pruned ? (feas ? ((uint64_t)ub_tot1 << 32) | 0xFFFFFFFFull : 0ull) : widen(bound32);
     if (lane == 0) {
+      // back to packed keys ((score + 1) << 32 | ~slot)
+      auto widen = [&](uint32_t k) -> uint64_t {
+        if (!k) return 0ull;
+        const uint32_t q = KEY32_POS_MASK - (k & KEY32_POS_MASK);
+        const uint32_t slot = s.lo + (j0 + q / WAVE) * WAVE * s.waves + (q % WAVE) * s.waves + lwave;
+        return ((uint64_t)(k >> KEY32_POS_BITS) << 32) | (uint64_t)(0xFFFFFFFFu - slot);
+      };
+      const uint64_t k1 = widen(c1), k2 = widen(c2), bound = widen(bound32);
       const uint32_t pl = it - p0;
       s_keys[pl][wid][0] = k1;
       s_keys[pl][wid][1] = k2;
@@ -526,7 +475,7 @@ __global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
     if (fix && r == FIX_NONE) continue;
     uint64_t k[2 * NW];
     uint64_t bound = 0;
-    const uint32_t nwaves = min((uint32_t)NW, kwaves - bx * NW);
+    const uint32_t nwaves = min((uint32_t)NW, kwaves - blockIdx.x * NW);
     static_for<NW>([&](auto W) {
       constexpr int w = W;
       const bool on = (uint32_t)w < nwaves;
@@ -566,12 +515,7 @@ __global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
       if (tmx + 1u > (uint32_t)cur) atomicMax(pm, tmx + 1u);
       if (nmx + 1u > (uint32_t)(cur >> 32)) atomicMax(pm + 1, nmx + 1u);
     }
-    a.brec[((size_t)sh * a.P + r) * a.bstride + bx] = br;
-  }
-  // sampled pruning statistics (relayout policy): every 8th block of the first pod group
-  if (a.prune_t && threadIdx.x == 0 && blockIdx.y == 0 && (bx & 7u) == 0) {
-    atomicAdd((unsigned long long *)&a.counters[5], (unsigned long long)n_pruned);
-    atomicAdd((unsigned long long *)&a.counters[6], (unsigned long long)(p1 - p0));
+    a.brec[((size_t)sh * a.P + r) * a.bstride + blockIdx.x] = br;
   }
 }
 
@@ -728,37 +672,6 @@ __global__ __launch_bounds__(MERGE_THREADS) void merge_kernel(RoundArgs a) {
       if (t[0]) atomicMax(&ps->any_feasible, 1u);
     }
   }
-}
-
-// One block per pod of the round: the pilot launch's block lists (the best
-// blocks of the relayout order) give a lower bound on the pod's kt-th best
-// key over all nodes; the pruned launch skips scoring in blocks whose
-// TotalScore bound is below it.
-constexpr uint32_t PRUNE_CAP = 1024;  // pilot keys per pod (nblk * nshards * BLOCK_KEYS)
-__global__ __launch_bounds__(256) void prune_threshold_kernel(RoundArgs a, uint32_t nblk, uint32_t nshards,
-                                                              uint32_t kt, uint32_t *out) {
-  __shared__ uint64_t s_k[PRUNE_CAP];
-  const uint32_t start = uniform_u32(*a.sstart);
-  const uint32_t r = blockIdx.x;
-  if (start + r >= a.npods) {
-    if (threadIdx.x == 0) out[r] = 0;
-    return;
-  }
-  const uint32_t per = nblk * BLOCK_KEYS;
-  const uint32_t n = min(per * nshards, PRUNE_CAP);
-  uint32_t m = 64;
-  while (m < n) m <<= 1;
-  for (uint32_t i = threadIdx.x; i < m; i += blockDim.x) {
-    uint64_t k = 0;
-    if (i < n) {
-      const uint32_t sh = i / per, b = (i % per) / BLOCK_KEYS, q = i % BLOCK_KEYS;
-      k = a.brec[((size_t)sh * a.P + r) * a.bstride + b].keys[q];
-    }
-    s_k[i] = k;
-  }
-  __syncthreads();
-  bitonic_desc(s_k, m);
-  if (threadIdx.x == 0) out[r] = kt && kt <= n ? (uint32_t)(s_k[kt - 1] >> 32) : 0u;
 }
 
 // One block: per pod of the round, the normalising maxima the rest of the
@@ -2147,27 +2060,6 @@ __global__ void gather_rows_kernel(NodeTable t, const uint32_t *pos, int64_t *ou
   o[7] = t.npods[p];
 }
 
-// Relayout order: 100 - LeastAllocated of an empty request (its upper bound
-// for every pod), 255 for an empty slot.
-__global__ void la_bound_kernel(NodeTable t, const uint32_t *slot_pos, uint8_t *out, uint32_t n) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  NodeRegs r;
-  const uint32_t p = slot_pos[i];
-  load_core(t, p, i, true, r);
-  const int32_t la0 = (least_requested(r.lf100_cpu, 0.0, r.inv_cpu) + least_requested(r.lf100_mem, 0.0, r.inv_mem)) >>
-                      r.lashift;
-  out[i] = (r.bits & 1u) ? (uint8_t)(100 - min(max(la0, 0), 100)) : (uint8_t)255;
-}
-
-template <class T>
-__global__ void permute_cols_kernel(T *dst, const T *src, const uint32_t *idx, uint32_t npos, uint32_t ncols) {
-  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= npos) return;
-  const uint32_t q = idx[p];
-  for (uint32_t c = 0; c < ncols; ++c) dst[(size_t)c * npos + p] = src[(size_t)c * npos + q];
-}
-
 // Full relabel of one label word column (dictionary growth).
 __global__ void scatter_u64_kernel(uint64_t *col, const uint32_t *pos, const uint64_t *val, uint32_t n) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2258,29 +2150,6 @@ hipError_t launch_sweep(const RoundArgs &a, bool ext, uint32_t nblocks, uint32_t
     else if (a.npl == 4) sweep_kernel<4, false><<<g, SWEEP_THREADS, 0, st>>>(a);
     else sweep_kernel<8, false><<<g, SWEEP_THREADS, 0, st>>>(a);
   }
-  return hipGetLastError();
-}
-
-hipError_t launch_prune_threshold(const RoundArgs &a, uint32_t nblk, uint32_t nshards, uint32_t kt, uint32_t *out,
-                                  hipStream_t st) {
-  prune_threshold_kernel<<<a.P, 256, 0, st>>>(a, nblk, nshards, kt, out);
-  return hipGetLastError();
-}
-
-hipError_t launch_la_bound(const NodeTable &t, const uint32_t *slot_pos, uint8_t *out, uint32_t n, hipStream_t st) {
-  if (!n) return hipSuccess;
-  la_bound_kernel<<<(n + 255) / 256, 256, 0, st>>>(t, slot_pos, out, n);
-  return hipGetLastError();
-}
-
-hipError_t launch_permute_cols(void *dst, const void *src, const uint32_t *idx, uint32_t npos, uint32_t ncols,
-                               uint32_t word_bytes, hipStream_t st) {
-  if (!npos || !ncols) return hipSuccess;
-  const dim3 g((npos + 255) / 256);
-  if (word_bytes == 8)
-    permute_cols_kernel<uint64_t><<<g, 256, 0, st>>>((uint64_t *)dst, (const uint64_t *)src, idx, npos, ncols);
-  else
-    permute_cols_kernel<uint32_t><<<g, 256, 0, st>>>((uint32_t *)dst, (const uint32_t *)src, idx, npos, ncols);
   return hipGetLastError();
 }
 

@@ -58,12 +58,8 @@ struct RoundArgs {
   CandRow *crow;              // [P][K] S0 rows of the final candidates
   CandExt *cext;              // [P][K] their label / taint columns (EXT batches)
   const uint32_t *slot_pos;   // slot -> position
-  uint64_t *counters;         // [0] rounds, [1] pods resolved, [2] pods swept, [3] wasted rounds,
-                              // [5] / [6] pruned / all (pod, block) pairs of sampled pruned-launch blocks
+  uint64_t *counters;         // [0] rounds, [1] pods resolved, [2] pods swept, [3] wasted rounds
   Weights w;
-  const uint32_t *pos_slot;   // position -> slot (SLOT_NONE: padding)
-  uint32_t block0;            // sweep: first block of the shard this launch covers
-  const uint32_t *prune_t;    // sweep: [P] TotalScore + 1 thresholds (pilot K_T-th best), null: no pruning
 };
 
 struct DumpArgs {
@@ -127,15 +123,6 @@ hipError_t launch_scatter_i64(int64_t *col, const uint64_t *idx, const int64_t *
                               hipStream_t st);
 
 hipError_t launch_norm_check(const RoundArgs &a, hipStream_t st);
-// Pruning threshold per pod of the round: the kt-th largest key of the pilot
-// blocks [0, nblk) of every local shard (TotalScore + 1; 0 with fewer keys).
-hipError_t launch_prune_threshold(const RoundArgs &a, uint32_t nblk, uint32_t nshards, uint32_t kt, uint32_t *out,
-                                  hipStream_t st);
-// Relayout: per slot 100 - LeastAllocated at zero request (255: empty slot).
-hipError_t launch_la_bound(const NodeTable &t, const uint32_t *slot_pos, uint8_t *out, uint32_t n, hipStream_t st);
-// dst[c * npos + p] = src[c * npos + idx[p]] for c < ncols (4- or 8-byte words)
-hipError_t launch_permute_cols(void *dst, const void *src, const uint32_t *idx, uint32_t npos, uint32_t ncols,
-                               uint32_t word_bytes, hipStream_t st);
 hipError_t launch_sweep(const RoundArgs &a, bool ext, uint32_t nblocks, uint32_t ngroups, uint32_t nshards,
                         hipStream_t st);
 hipError_t launch_merge(const RoundArgs &a, uint32_t nshards, hipStream_t st);

@@ -272,9 +272,6 @@ class KsStats(C.Structure):
         ("spread_ms", C.c_double),
         ("spread_pods_timed", C.c_uint64),
         ("spread_pods", C.c_uint64),
-        ("relayouts", C.c_uint64),
-        ("prune_pairs", C.c_uint64),
-        ("prune_pruned", C.c_uint64),
     ]
 
 

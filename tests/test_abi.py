@@ -28,7 +28,7 @@ def test_libksched_exports_every_declared_symbol():
     lib = _abi.ksched_lib()
     for name in declared("ksched.h", "ks_"):
         assert hasattr(lib, name), name
-    assert lib.ks_abi_version() == 4
+    assert lib.ks_abi_version() == 3
 
 
 def test_libksynth_exports_every_declared_symbol():
@@ -66,7 +66,7 @@ int main(void) {
   O(ks_result, total_score) O(ks_result, fail_counts) O(ks_result, flags)
   O(ks_event, pod) O(ks_event, node) S(ks_node_info) O(ks_node_info, generation) O(ks_node_info, node)
   O(ks_node_score, total_score) O(ks_config, weight_fit) O(ks_config, weight_image)
-  O(ks_stats, sweep_ms) O(ks_stats, resolve_launches) O(ks_stats, prune_pruned)
+  O(ks_stats, sweep_ms) O(ks_stats, resolve_launches)
   return 0;
 }
 """

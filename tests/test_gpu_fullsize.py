@@ -96,8 +96,6 @@ def run_fullsize(kind, pods, prefill, *, env=None, **cfg):
     s.free(b)
     dbg = (C.c_uint64 * 16)()
     assert s.lib.ks_debug_counters(s.ctx, dbg) == 0
-    st = s.stats()
-    dbg[5], dbg[6] = st.prune_pruned, st.prune_pairs  # (label / taint reclaims are not checked here)
     o = pyoracle.Oracle(N, threads=ORACLE_THREADS)
     o.upsert(nodes.nodes, slots, N)
     if pf is not None:
@@ -115,7 +113,6 @@ def test_c3_hetero_1m_replay():
     r, dbg = run_fullsize(synth.HETERO, synth.pods(synth.HETERO, BATCH, 2), prefill=True)
     assert (r["status"] == 0).all()
     assert dbg[0] >= BATCH // 256  # rounds
-    assert dbg[5] * 2 > dbg[6] > 0, f"pruned sweep: {dbg[5]} of {dbg[6]} sampled (pod, block) pairs pruned"
 
 
 def test_c4_labeled_1m_replay_early_fix():
@@ -137,7 +134,6 @@ def test_c4_labeled_1m_replay_tuple_guess():
     # the default (node-tuple normaliser guesses): the bench configuration
     r, dbg = run_fullsize(synth.LABELED, synth.pods(synth.LABELED, BATCH, 7), prefill=True)
     assert (r["status"] == 0).mean() > 0.9
-    assert dbg[5] > 0, "pruned EXT sweep never pruned"
 
 
 def test_kwok_1m_requestless_replay():

@@ -78,7 +78,7 @@ def test_snapshot_generations_vs_oracle(kind):
             if g <= snap_gen:
                 continue
             if v is None:
-                if o.node_states([sl])[0].pod_count >= 0:
+                if o.node_states([sl])[0].alloc_pods >= 0:
                     o.delete((C.c_uint32 * 1)(sl), 1)
             else:
                 o.upsert(node_ptr(versions[v].nodes, sl), (C.c_uint32 * 1)(sl), 1)
