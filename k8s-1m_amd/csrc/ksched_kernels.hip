@@ -1093,7 +1093,11 @@ constexpr int KS_PLUGIN_FIT_IDX = 4;  // filter status of NodeResourcesFit (KS_P
 constexpr int ROW_PIECES = sizeof(CandRow) / 16;
 constexpr int EXT_PIECES = sizeof(CandExt) / 16;
 static_assert(2 * RES_LIST_WAVES * WAVE >= MAX_K && RES_OWN_WAVES * WAVE >= MAX_P, "resolve roles");
-constexpr int LIST_SPAN = 2 * WAVE;  // list entries per list wave: lane l holds entries l and l + 64
+// list entries per list wave: 64 (lane l holds entry l) for K <= 256, 128
+// (entries l and l + 64) for longer lists -- a resolve_kernel parameter, so
+// K <= 256 rounds keep the single-probe loop (the two-entry select costs
+// ~15 % of the resolve)
+constexpr int LIST_SPAN_1 = WAVE, LIST_SPAN_2 = 2 * WAVE;
 static_assert(DSUM_LANE >= NCAND && DSUM_LANE + NFILT + 3 <= WAVE, "decider lanes");
 
 // A node as the resolve carries it: its row (live state) and the round-start
@@ -1254,8 +1258,9 @@ __device__ __forceinline__ void signal_done(uint32_t *flag, uint32_t seq) {
   __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-template <bool EXT>
+template <bool EXT, int LIST_SPAN>
 __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
+  constexpr bool TWO = LIST_SPAN == 2 * WAVE;
   __shared__ PodDev s_pod[MAX_P];
   __shared__ ShardRecHdr s_hdr[MAX_P];
   __shared__ uint32_t s_norm[MAX_P][2];
@@ -1328,13 +1333,14 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
   constexpr int32_t LIST_WAIT = 2 * LIST_DMA;  // vmcnt(N): expcnt / lgkmcnt fields at their max
   static_assert(LIST_WAIT < 64, "vmcnt field");
   const uint32_t lw = wid;
-  auto dma_keys = [&](uint32_t pod) {  // keys of list entries [128 lw, 128 lw + 128) of pod -> s_keys
+  auto dma_keys = [&](uint32_t pod) {  // keys of list entries [SPAN lw, SPAN lw + SPAN) of pod -> s_keys
     const uint32_t p = min(pod, nround - 1);
     // every wave issues it (list_wait counts LIST_DMA loads per iteration);
     // entries past K: any in-record address (never read back)
     const uint32_t e = LIST_SPAN * lw + 2 * lane;
     const uint64_t *src = a.frec + (size_t)p * RW + REC_HDR_WORDS + (e < a.K ? e : 0u);
-    __builtin_amdgcn_global_load_lds((gvoid_t *)src, (lvoid_t *)&s_keys[pod % KSLOTS][LIST_SPAN * lw], 16, 0, 0);
+    if (TWO || lane < WAVE / 2)
+      __builtin_amdgcn_global_load_lds((gvoid_t *)src, (lvoid_t *)&s_keys[pod % KSLOTS][LIST_SPAN * lw], 16, 0, 0);
   };
   auto lds_key = [&](uint32_t slot, uint32_t t) -> uint64_t {
     uint64_t v;
@@ -1352,7 +1358,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
     // modified-slot hash; list order within the wave is e0's 64, then e1's
     const uint32_t e0 = LIST_SPAN * lw + lane, e1 = e0 + WAVE;
     const uint64_t k0 = e0 < a.K ? lds_key(pod % KSLOTS, e0) : 0ull;
-    const uint64_t k1 = e1 < a.K ? lds_key(pod % KSLOTS, e1) : 0ull;
+    const uint64_t k1 = TWO && e1 < a.K ? lds_key(pod % KSLOTS, e1) : 0ull;
     auto probe = [&](uint64_t k, uint32_t e, bool &unmod, bool &hempty) {
       unmod = hempty = false;
       const uint32_t slot = 0xFFFFFFFFu - (uint32_t)k;
@@ -1368,18 +1374,19 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
     };
     bool u0, h0, u1 = false, h1 = false;
     probe(k0, e0, u0, h0);
-    if (LIST_SPAN * lw + WAVE < nk) probe(k1, e1, u1, h1);  // wave-uniform: second half only when listed
-    const uint64_t ub0 = __ballot(u0), hb0 = __ballot(h0), ub1 = __ballot(u1), hb1 = __ballot(h1);
+    if (TWO && LIST_SPAN * lw + WAVE < nk) probe(k1, e1, u1, h1);  // wave-uniform: second half only when listed
+    const uint64_t ub0 = __ballot(u0), hb0 = __ballot(h0);
+    const uint64_t ub1 = TWO ? __ballot(u1) : 0ull, hb1 = TWO ? __ballot(h1) : 0ull;
     const uint32_t n0 = (uint32_t)__popcll(ub0);
-    const uint32_t nsel = min(n0 + (uint32_t)__popcll(ub1), (uint32_t)LSEL);
-    // lane c < LSEL takes the c-th unmodified entry of the wave's 128
-    const bool second = lane >= n0;
+    const uint32_t nsel = min(n0 + (TWO ? (uint32_t)__popcll(ub1) : 0u), (uint32_t)LSEL);
+    // lane c < LSEL takes the c-th unmodified entry of the wave's span
+    const bool second = TWO && lane >= n0;
     uint64_t m = second ? ub1 : ub0;
     const uint32_t skip = second ? lane - n0 : lane;
     for (uint32_t j = 0; j < skip && j < (uint32_t)LSEL; ++j) m &= m - 1;
     const uint32_t tb = m ? (uint32_t)__builtin_ctzll(m) : 0u;
     const uint64_t tk0 = (uint64_t)__shfl((long long)k0, (int)tb, WAVE);
-    const uint64_t tk1 = (uint64_t)__shfl((long long)k1, (int)tb, WAVE);
+    const uint64_t tk1 = TWO ? (uint64_t)__shfl((long long)k1, (int)tb, WAVE) : 0ull;
     const uint64_t tk = second ? tk1 : tk0;
     const uint32_t te = tb + (second ? (uint32_t)WAVE : 0u);
     const uint64_t hb = second ? hb1 : hb0;
@@ -2196,8 +2203,13 @@ hipError_t launch_patch(const RoundArgs &a, bool ext, hipStream_t st) {
 }
 
 hipError_t launch_resolve(const RoundArgs &a, bool ext, hipStream_t st) {
-  if (ext) resolve_kernel<true><<<1, RESOLVE_THREADS, 0, st>>>(a);
-  else resolve_kernel<false><<<1, RESOLVE_THREADS, 0, st>>>(a);
+  if (a.K <= (uint32_t)(RES_LIST_WAVES * LIST_SPAN_1)) {
+    if (ext) resolve_kernel<true, LIST_SPAN_1><<<1, RESOLVE_THREADS, 0, st>>>(a);
+    else resolve_kernel<false, LIST_SPAN_1><<<1, RESOLVE_THREADS, 0, st>>>(a);
+  } else {
+    if (ext) resolve_kernel<true, LIST_SPAN_2><<<1, RESOLVE_THREADS, 0, st>>>(a);
+    else resolve_kernel<false, LIST_SPAN_2><<<1, RESOLVE_THREADS, 0, st>>>(a);
+  }
   return hipGetLastError();
 }
 
