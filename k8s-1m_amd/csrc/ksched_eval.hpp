@@ -185,6 +185,15 @@ __device__ __forceinline__ int filter(const PodDev &p, const uint64_t *clauses, 
   return fail ? 4 : ST_FEASIBLE;
 }
 
+// Plugin weight x score (both < 2^24): v_mul_u32_u24, full rate.  Written as
+// asm because the compiler turns __umul24 of these operands into
+// v_mul_lo_u32, a quarter-rate instruction (two per node in the sweep).
+__device__ __forceinline__ uint32_t wmul(uint32_t w, uint32_t x) {
+  uint32_t r;
+  asm("v_mul_u32_u24 %0, %1, %2" : "=v"(r) : "v"(w), "v"(x));
+  return r;
+}
+
 // leastRequestedScore(requested, capacity) = (capacity - requested) * 100 / capacity
 // (int64 truncation; 0 when requested > capacity) from x = max(lf100 - nz100, 0)
 // = max(capacity - requested, 0) * 100, exact.  With y = RN(1 / capacity),
@@ -241,15 +250,15 @@ template <bool EXT>
 __device__ __forceinline__ int32_t total_score(const PodDev &p, const uint64_t *clauses, const NodeRegs &r,
                                                const NodeExt &e, const Weights &w, int64_t tt_max,
                                                int64_t na_max) {
-  int32_t t = (int32_t)__umul24((uint32_t)w.fit, (uint32_t)score_la(p, r)) +
-              (int32_t)__umul24((uint32_t)w.ba, (uint32_t)score_ba(p, r));
+  int32_t t = (int32_t)wmul((uint32_t)w.fit, (uint32_t)score_la(p, r)) +
+              (int32_t)wmul((uint32_t)w.ba, (uint32_t)score_ba(p, r));
   int32_t tt = 100;
   if (EXT && (p.flags & PF_TT)) tt = (int32_t)normalize(taint_raw(p, e), tt_max, true);
   t += w.tt * tt;  // wave-uniform unless TaintToleration is normalised per node
   if (p.flags & PF_HAS_PREF) {
     int32_t na = 0;
     if (EXT && (p.flags & PF_NA)) na = (int32_t)normalize(preferred_raw(p, clauses, e, r.slot), na_max, false);
-    t += (int32_t)__umul24((uint32_t)w.na, (uint32_t)na);
+    t += (int32_t)wmul((uint32_t)w.na, (uint32_t)na);
   }
   return t;  // + w.il * 0 (ImageLocality: nodes report no images)
 }

@@ -327,8 +327,8 @@ __global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
       static_for<NPL>([&](auto J) {
         constexpr int j = J;
         const bool feasible = podfit[j] && !(rq_c > nr[j].free_cpu) && !(rq_m > nr[j].free_mem);
-        const uint32_t tot1 = (uint32_t)__umul24((uint32_t)a.w.fit, (uint32_t)score_la(p, nr[j])) +
-                              (uint32_t)__umul24((uint32_t)a.w.ba, (uint32_t)score_ba(p, nr[j])) + cplus;
+        const uint32_t tot1 = wmul((uint32_t)a.w.fit, (uint32_t)score_la(p, nr[j])) +
+                              wmul((uint32_t)a.w.ba, (uint32_t)score_ba(p, nr[j])) + cplus;
         const uint32_t key = feasible ? (tot1 << KEY32_POS_BITS) | (kpos0 - (uint32_t)j * WAVE) : 0u;
         b2 = max(b2, min(b1, key));
         b1 = max(b1, key);
@@ -377,8 +377,8 @@ __global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
         }
         if (!valid) st = ST_EMPTY;
         const bool feasible = st == ST_FEASIBLE;
-        uint32_t tot1 = (uint32_t)__umul24((uint32_t)a.w.fit, (uint32_t)score_la(p, nr[j])) +
-                        (uint32_t)__umul24((uint32_t)a.w.ba, ABL_ON(8) ? (uint32_t)score_ba(p, nr[j]) : 50u) + 1u;
+        uint32_t tot1 = wmul((uint32_t)a.w.fit, (uint32_t)score_la(p, nr[j])) +
+                        wmul((uint32_t)a.w.ba, ABL_ON(8) ? (uint32_t)score_ba(p, nr[j]) : 50u) + 1u;
         uint32_t tts = 100u;
         bool at_tt = false, at_na = false;
         if (p.flags & PF_TT) {
@@ -388,7 +388,7 @@ __global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
           over |= feasible && raw > tt_max;
           tmx = max(tmx, feasible ? raw : 0u);
         }
-        tot1 += (uint32_t)__umul24((uint32_t)a.w.tt, tts);
+        tot1 += wmul((uint32_t)a.w.tt, tts);
         if (p.flags & PF_HAS_PREF) {
           uint32_t nas = 0u;
           if (p.flags & PF_NA) {
@@ -397,7 +397,7 @@ __global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
             over |= feasible && praw[j] > na_max;
             nmx = max(nmx, feasible ? praw[j] : 0u);
           }
-          tot1 += (uint32_t)__umul24((uint32_t)a.w.na, nas);
+          tot1 += wmul((uint32_t)a.w.na, nas);
         }
         const uint32_t key = feasible ? (tot1 << KEY32_POS_BITS) | (kpos0 - (uint32_t)j * WAVE) : 0u;
         b2 = max(b2, min(b1, key));
@@ -1245,8 +1245,8 @@ __device__ __forceinline__ bool fit_q(const PodQ &q, const NodeRegs &g) {
   return (g.bits & 2u) && !(q.rq_c > g.free_cpu) && !(q.rq_m > g.free_mem);
 }
 __device__ __forceinline__ uint64_t key_q(const PodDev &p, const PodQ &q, const NodeRegs &g) {
-  const int32_t t = (int32_t)__umul24((uint32_t)q.wf, (uint32_t)score_la(p, g)) +
-                    (int32_t)__umul24((uint32_t)q.wb, (uint32_t)score_ba(p, g)) + q.cplus;
+  const int32_t t = wmul((uint32_t)q.wf, (uint32_t)score_la(p, g)) +
+                    wmul((uint32_t)q.wb, (uint32_t)score_ba(p, g)) + q.cplus;
   return pack_key(t, g.slot);
 }
 
