@@ -299,6 +299,9 @@ KSCHED_SYMBOLS = [
     "ks_comm_init", "ks_comm_allreduce_max", "ks_get_stats", "ks_reset_stats", "ks_set_timing",
     "ks_debug_counters",
 ]
+KSGATHER_SYMBOLS = [
+    "ksg_open", "ksg_close", "ksg_set_members", "ksg_record_and_wait", "ksg_pending", "ksg_fnv1_32", "ksg_target_index",
+]
 KSYNTH_SYMBOLS = [
     "ksynth_nodes", "ksynth_pods", "ksynth_prefill", "ksynth_besteffort_pods", "ksynth_spread_pods", "ksynth_affinity_pods", "ksynth_node_array",
     "ksynth_pod_array", "ksynth_slots", "ksynth_free", "ksynth_fnv64",
@@ -403,4 +406,33 @@ def ksynth_lib() -> C.CDLL:
     L.ksynth_fnv64.argtypes = [vp, C.c_uint64, C.c_uint64]
     L.ksynth_fnv64.restype = C.c_uint64
     _ksynth = L
+    return L
+
+
+_ksgather = None
+
+
+def ksgather_lib() -> C.CDLL:
+    """libksgather.so: the cross-host gather (include/ksgather.h); host code only."""
+    global _ksgather
+    if _ksgather is not None:
+        return _ksgather
+    L = _load("libksgather.so")
+    vp = C.c_void_p
+    P = C.POINTER
+    L.ksg_open.argtypes = [C.c_uint32, C.c_uint32, C.c_int32, C.c_uint64]
+    L.ksg_open.restype = vp
+    L.ksg_close.argtypes = [vp]
+    L.ksg_close.restype = None
+    L.ksg_set_members.argtypes = [vp, C.c_uint32]
+    L.ksg_set_members.restype = None
+    L.ksg_record_and_wait.argtypes = [vp, C.c_char_p, C.c_char_p, C.c_int32, C.c_char_p, C.c_uint32, P(C.c_int32)]
+    L.ksg_record_and_wait.restype = C.c_int32
+    L.ksg_pending.argtypes = [vp]
+    L.ksg_pending.restype = C.c_uint32
+    L.ksg_fnv1_32.argtypes = [C.c_char_p, C.c_uint32]
+    L.ksg_fnv1_32.restype = C.c_uint32
+    L.ksg_target_index.argtypes = [C.c_char_p, P(C.c_char_p), C.c_uint32, C.c_char_p]
+    L.ksg_target_index.restype = C.c_uint32
+    _ksgather = L
     return L

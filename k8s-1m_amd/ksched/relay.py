@@ -1,0 +1,163 @@
+"""Cross-host candidate gather over the reference's gRPC contract (SURVEY.md
+§8(f) F3: RCCL for co-located shards, gRPC ``CollectScore`` for remote hosts).
+
+Inside a host, the GPUs' shards are merged by RCCL (``Scheduler.comm_init``):
+the host's answer for a pod is one ``(node name, TotalScore)``.  Across hosts
+every member sends that score, as int32, to the pod's gatherer --
+``PodService.CollectScore(SchedulingScore) returns (ScheduleResponse)``
+(``dist-scheduler/proto/pod.proto:21-35``) -- and the gatherer's
+ScoreEvaluator answers each sender whether its node won
+(``grpc_server.go:116-127``, ``scoreevaluator.go:45-126``; here the C++
+state machine of ``libksgather.so``, include/ksgather.h).
+
+The messages are built at run time from a FileDescriptorProto equal to
+pod.proto's ``ScheduleResponse`` / ``SchedulingScore`` (same package, names,
+field numbers and types, so the bytes on the wire are the reference's); the
+``NewPod`` stream of the same service is the relay tree's pod ingress, outside
+this path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import threading
+from concurrent import futures
+from typing import Optional, Sequence, Tuple
+
+import grpc
+from google.protobuf import descriptor_pb2, descriptor_pool, message_factory
+
+from . import _abi
+
+SERVICE = "podservice.PodService"
+COLLECT_SCORE = f"/{SERVICE}/CollectScore"
+GRPC_PORT = 50051  # distpermit.go:87 (the reference hard-codes it)
+SCORE_DELAY_S = 5.0  # grpc_server.go:135
+TIE_RANDOM, TIE_LOWEST_NAME = 0, 1
+
+
+def _messages():
+    fd = descriptor_pb2.FileDescriptorProto(name="ksched_pod.proto", package="podservice", syntax="proto3")
+    m = fd.message_type.add(name="ScheduleResponse")
+    m.field.add(name="permit", number=1, type=descriptor_pb2.FieldDescriptorProto.TYPE_BOOL,
+                label=descriptor_pb2.FieldDescriptorProto.LABEL_OPTIONAL, json_name="permit")
+    m = fd.message_type.add(name="SchedulingScore")
+    for i, (name, typ) in enumerate((("podName", "TYPE_STRING"), ("namespace", "TYPE_STRING"),
+                                     ("nodeName", "TYPE_STRING"), ("score", "TYPE_INT32")), start=1):
+        m.field.add(name=name, number=i, type=getattr(descriptor_pb2.FieldDescriptorProto, typ),
+                    label=descriptor_pb2.FieldDescriptorProto.LABEL_OPTIONAL, json_name=name)
+    pool = descriptor_pool.DescriptorPool()
+    pool.Add(fd)
+    get = message_factory.GetMessageClass
+    return (get(pool.FindMessageTypeByName("podservice.ScheduleResponse")),
+            get(pool.FindMessageTypeByName("podservice.SchedulingScore")))
+
+
+ScheduleResponse, SchedulingScore = _messages()
+
+
+def host_score(result, node_names) -> Tuple[str, int]:
+    """A host's CollectScore payload for one ks_result: the chosen node's name
+    and TotalScore as int32 (distpermit.go:106), or ("", 0) when the host has
+    no feasible node (scheduler.go:397-400: score 0 = no candidate)."""
+    if result.status != 0 or result.node_index < 0:
+        return "", 0
+    return node_names[result.node_index], int(result.total_score)
+
+
+class ScoreEvaluator:
+    """ctypes handle on the gatherer state machine (ksg_record_and_wait)."""
+
+    def __init__(self, members: int, delay_s: float = SCORE_DELAY_S, tie: int = TIE_RANDOM, seed: int = 0):
+        self.lib = _abi.ksgather_lib()
+        self.h = self.lib.ksg_open(members, int(delay_s * 1000), tie, seed)
+        if not self.h:
+            raise ValueError("ksg_open: bad arguments")
+
+    def set_members(self, members: int):
+        self.lib.ksg_set_members(self.h, members)
+
+    def record_and_wait(self, key: str, node_name: str, score: int) -> Tuple[bool, str, int]:
+        """Blocks (without the GIL) until the pod fires; (permit, winner, winner score)."""
+        buf = C.create_string_buffer(512)
+        ws = C.c_int32()
+        r = self.lib.ksg_record_and_wait(self.h, key.encode(), node_name.encode(), int(score), buf, 512, C.byref(ws))
+        if r < 0:
+            raise ValueError("ksg_record_and_wait: bad arguments")
+        return r == 1, buf.value.decode(), ws.value
+
+    def pending(self) -> int:
+        return self.lib.ksg_pending(self.h)
+
+    def close(self):
+        if self.h:
+            self.lib.ksg_close(self.h)
+            self.h = None
+
+
+def target_index(key: str, members: Sequence[str], leader: Optional[str] = None) -> int:
+    """SchedulerSet.GetTargetForScoring: index into `members` of the gatherer of `key`."""
+    lib = _abi.ksgather_lib()
+    arr = (C.c_char_p * max(1, len(members)))(*[m.encode() for m in members])
+    return lib.ksg_target_index(key.encode(), arr, len(members), leader.encode() if leader else None)
+
+
+class CollectScoreServer:
+    """The gatherer side: a gRPC server exposing PodService.CollectScore."""
+
+    def __init__(self, evaluator: ScoreEvaluator, address: str = "127.0.0.1:0", workers: int = 64):
+        self.evaluator = evaluator
+        self.server = grpc.server(futures.ThreadPoolExecutor(max_workers=workers))
+        handler = grpc.unary_unary_rpc_method_handler(
+            self._collect, request_deserializer=SchedulingScore.FromString,
+            response_serializer=ScheduleResponse.SerializeToString)
+        self.server.add_generic_rpc_handlers((grpc.method_handlers_generic_handler(SERVICE, {"CollectScore": handler}),))
+        self.port = self.server.add_insecure_port(address)
+        self.address = f"{address.rsplit(':', 1)[0]}:{self.port}"
+
+    def _collect(self, req, context):
+        permit, _, _ = self.evaluator.record_and_wait(f"{req.namespace}/{req.podName}", req.nodeName, req.score)
+        return ScheduleResponse(permit=permit)
+
+    def start(self):
+        self.server.start()
+        return self
+
+    def stop(self):
+        self.server.stop(grace=None)
+
+
+class ScoreClient:
+    """The member side (distpermit.SendScore): one cached channel per gatherer."""
+
+    _lock = threading.Lock()
+    _channels: dict = {}
+    _inflight: set = set()  # fire-and-forget calls (a dropped grpc future cancels its call)
+
+    def __init__(self, address: str):
+        with ScoreClient._lock:
+            ch = ScoreClient._channels.get(address)
+            if ch is None:
+                ch = grpc.insecure_channel(address)
+                ScoreClient._channels[address] = ch
+        self.call = ch.unary_unary(COLLECT_SCORE, request_serializer=SchedulingScore.SerializeToString,
+                                   response_deserializer=ScheduleResponse.FromString)
+
+    def send_score(self, pod_name: str, namespace: str, node_name: str, score: int, timeout: float = 30.0) -> bool:
+        """The permit for node_name.  Score 0 (no candidate) is sent without
+        waiting for the answer, which is a rejection (distpermit.go:111-115)."""
+        req = SchedulingScore(podName=pod_name, namespace=namespace, nodeName=node_name, score=int(score))
+        if score == 0:
+            fut = self.call.future(req, timeout=timeout)
+            with ScoreClient._lock:
+                ScoreClient._inflight.add(fut)
+
+            def done(f):
+                with ScoreClient._lock:
+                    ScoreClient._inflight.discard(f)
+
+            fut.add_done_callback(done)
+            return False
+        try:
+            return bool(self.call(req, timeout=timeout).permit)
+        except grpc.RpcError:
+            return False  # "could not send score. Denying permit"

@@ -22,6 +22,7 @@ def declared(header: str, prefix: str):
 def test_header_symbols_match_mirror():
     assert declared("ksched.h", "ks_") == sorted(_abi.KSCHED_SYMBOLS)
     assert declared("ksynth.h", "ksynth_") == sorted(_abi.KSYNTH_SYMBOLS)
+    assert declared("ksgather.h", "ksg_") == sorted(_abi.KSGATHER_SYMBOLS)
 
 
 def test_libksched_exports_every_declared_symbol():
@@ -29,6 +30,12 @@ def test_libksched_exports_every_declared_symbol():
     for name in declared("ksched.h", "ks_"):
         assert hasattr(lib, name), name
     assert lib.ks_abi_version() == 3
+
+
+def test_libksgather_exports_every_declared_symbol():
+    lib = _abi.ksgather_lib()
+    for name in declared("ksgather.h", "ksg_"):
+        assert hasattr(lib, name), name
 
 
 def test_libksynth_exports_every_declared_symbol():

@@ -1,0 +1,140 @@
+"""F3: cross-host gather (include/ksgather.h, ksched/relay.py) on CPU.
+
+The gatherer's state machine against scoreevaluator.go's behaviour (fire when
+every member has scored or after the delay, highest score, ties among the
+first 100, late scores start a new evaluation), the member-side gatherer
+choice (FNV-1 32 over "namespace/name" modulo the sorted member list,
+schedulerset.go:107-143), and PodService.CollectScore end to end over gRPC on
+127.0.0.1 with the reference's message layout.
+"""
+import threading
+import time
+
+import pytest
+
+from ksched import relay
+
+
+def run_parallel(fns):
+    out = [None] * len(fns)
+
+    def go(i, f):
+        out[i] = f()
+
+    th = [threading.Thread(target=go, args=(i, f)) for i, f in enumerate(fns)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=30)
+    return out
+
+
+def test_fires_when_all_members_scored():
+    ev = relay.ScoreEvaluator(members=4, delay_s=30, tie=relay.TIE_LOWEST_NAME)
+    t0 = time.time()
+    res = run_parallel([lambda n=n, s=s: ev.record_and_wait("ns/p", n, s)
+                        for n, s in (("node-a", 410), ("node-b", 455), ("node-c", 0), ("node-d", 300))])
+    assert time.time() - t0 < 5  # did not wait for the delay
+    assert [r[0] for r in res] == [False, True, False, False]
+    assert all(r[1:] == ("node-b", 455) for r in res)
+    assert ev.pending() == 0
+    ev.close()
+
+
+def test_fires_after_delay_with_missing_member():
+    ev = relay.ScoreEvaluator(members=3, delay_s=0.3, tie=relay.TIE_LOWEST_NAME)
+    t0 = time.time()
+    res = run_parallel([lambda: ev.record_and_wait("ns/q", "n1", 200), lambda: ev.record_and_wait("ns/q", "n2", 350)])
+    dt = time.time() - t0
+    assert 0.25 <= dt < 3
+    assert [r[0] for r in res] == [False, True]
+    ev.close()
+
+
+def test_ties_deterministic_lowest_name():
+    ev = relay.ScoreEvaluator(members=3, delay_s=30, tie=relay.TIE_LOWEST_NAME)
+    res = run_parallel([lambda n=n: ev.record_and_wait("ns/t", n, 500) for n in ("zeta", "alpha", "mid")])
+    assert [r[0] for r in res] == [False, True, False]
+    ev.close()
+
+
+def test_ties_random_among_tied():
+    wins = {"a": 0, "b": 0, "c": 0}
+    for i in range(60):
+        ev = relay.ScoreEvaluator(members=4, delay_s=30, tie=relay.TIE_RANDOM, seed=i)
+        res = run_parallel([lambda n=n, s=s: ev.record_and_wait(f"ns/r{i}", n, s)
+                            for n, s in (("a", 7), ("b", 7), ("c", 7), ("d", 3))])
+        assert sum(r[0] for r in res) == 1 and not res[3][0]
+        wins[res[0][1]] += 1
+        ev.close()
+    assert all(v > 5 for v in wins.values()), wins
+
+
+def test_only_zero_scores_and_late_score():
+    ev = relay.ScoreEvaluator(members=2, delay_s=30, tie=relay.TIE_LOWEST_NAME)
+    res = run_parallel([lambda: ev.record_and_wait("ns/z", "", 0), lambda: ev.record_and_wait("ns/z", "", 0)])
+    assert all(r[1:] == ("", 0) for r in res)
+    # a score arriving after its pod fired starts a new evaluation (scoreevaluator.go:48-52)
+    ev.set_members(1)
+    permit, w, s = ev.record_and_wait("ns/z", "late-node", 90)
+    assert (permit, w, s) == (True, "late-node", 90)
+    ev.close()
+
+
+def test_fnv1_and_target_index():
+    lib = relay._abi.ksgather_lib()
+    # FNV-1 32 known answers (Go hash/fnv New32): "" -> offset basis, "a" -> 0x050c5d7e
+    assert lib.ksg_fnv1_32(b"", 0) == 0x811C9DC5
+    assert lib.ksg_fnv1_32(b"a", 1) == 0x050C5D7E
+    members = ["dist-scheduler-7", "dist-scheduler-relay-1", "dist-scheduler-2", "leader-0", "dist-scheduler-relay-0"]
+    order = ["leader-0", "dist-scheduler-relay-0", "dist-scheduler-relay-1", "dist-scheduler-2", "dist-scheduler-7"]
+    for key in ("default/pod-1", "ns/x", "kube-system/coredns-abc"):
+        h = lib.ksg_fnv1_32(key.encode(), len(key)) % len(members)
+        assert members[relay.target_index(key, members, "leader-0")] == order[h]
+    assert relay.target_index("ns/x", ["only"]) == 0
+
+
+class Result:  # ks_result fields host_score reads
+    def __init__(self, status, node_index, total_score):
+        self.status, self.node_index, self.total_score = status, node_index, total_score
+
+
+def test_collect_score_over_grpc():
+    ev = relay.ScoreEvaluator(members=3, delay_s=20, tie=relay.TIE_LOWEST_NAME)
+    srv = relay.CollectScoreServer(ev).start()
+    try:
+        names = ["node-%d" % i for i in range(8)]
+        hosts = [Result(0, 3, 412), Result(0, 6, 498), Result(1, -1, 0)]  # the third host has no candidate
+        payloads = [relay.host_score(r, names) for r in hosts]
+        assert payloads[2] == ("", 0)
+        cli = relay.ScoreClient(srv.address)
+        res = run_parallel([lambda n=n, s=s: cli.send_score("web-0", "default", n, s) for n, s in payloads])
+        assert res == [False, True, False]
+        # the wire bytes are pod.proto's: field numbers 1-4, int32 score
+        b = relay.SchedulingScore(podName="p", namespace="n", nodeName="x", score=7).SerializeToString()
+        assert b == b"\x0a\x01p\x12\x01n\x1a\x01x\x20\x07"
+        assert relay.ScheduleResponse(permit=True).SerializeToString() == b"\x08\x01"
+    finally:
+        srv.stop()
+        ev.close()
+
+
+@pytest.mark.parametrize("pods", [50])
+def test_many_pods_concurrently(pods):
+    ev = relay.ScoreEvaluator(members=2, delay_s=20, tie=relay.TIE_LOWEST_NAME)
+    srv = relay.CollectScoreServer(ev, workers=4 * pods).start()
+    try:
+        cli = relay.ScoreClient(srv.address)
+        fns = []
+        for p in range(pods):
+            fns.append(lambda p=p: cli.send_score(f"pod-{p}", "ns", f"a{p}", 100 + p % 3))
+            fns.append(lambda p=p: cli.send_score(f"pod-{p}", "ns", f"b{p}", 101))
+        res = run_parallel(fns)
+        for p in range(pods):
+            a, b = res[2 * p], res[2 * p + 1]
+            assert a + b == 1
+            assert a == (100 + p % 3 >= 101)  # ties: the lowest name (a...) wins
+        assert ev.pending() == 0
+    finally:
+        srv.stop()
+        ev.close()
