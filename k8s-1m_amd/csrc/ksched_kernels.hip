@@ -256,7 +256,11 @@ __device__ __forceinline__ uint32_t normalize_inv(uint32_t raw, double inv) {
 constexpr uint32_t KEY32_POS_BITS = 9, KEY32_POS_MASK = (1u << KEY32_POS_BITS) - 1;
 
 template <int NPL, bool EXT, int LWU = LW>
-__global__ __launch_bounds__(SWEEP_THREADS) void sweep_kernel(RoundArgs a) {
+// EXT with 2 nodes per lane: 5 waves per SIMD (96 VGPRs, 12 B/lane spilled at
+// 2 label words) runs the C4 sweep 5 % faster than 4 (103 VGPRs); 6 waves
+// spill 72 B, and the resource-only kernel spills 76 B at 5 (kept at 4)
+__global__ __launch_bounds__(SWEEP_THREADS) __attribute__((amdgpu_waves_per_eu(EXT && NPL == 2 ? 5 : 1)))
+void sweep_kernel(RoundArgs a) {
   static_assert(NPL * WAVE <= (1 << KEY32_POS_BITS), "wave-local key position field");
   constexpr int NW = SWEEP_THREADS / WAVE;
   __shared__ uint64_t s_keys[MAX_PG][NW][3];
