@@ -224,13 +224,18 @@ __device__ __forceinline__ double div_rn(double a, double b, double y) {
   return __builtin_fma(r, y, q0);
 }
 
-__device__ __forceinline__ int32_t score_ba(const PodDev &p, const NodeRegs &r) {
+// sc / sm: Requested + the pod's request (the sweep shares them with Fit)
+__device__ __forceinline__ int32_t score_ba_sum(double sc, double sm, const NodeRegs &r) {
   // fraction = min(1, requested / allocatable) as an IEEE binary64 quotient
   // (exact numerator); std = |(f0 - f1) / 2| with two fractions, else 0
-  const double f0 = fmin(div_rn(r.rcpu + p.req_cpu_d, r.acpu_d, r.inv_cpu), 1.0);
-  const double f1 = fmin(div_rn(r.rmem + p.req_mem_d, r.amem_d, r.inv_mem), 1.0);
+  const double f0 = fmin(div_rn(sc, r.acpu_d, r.inv_cpu), 1.0);
+  const double f1 = fmin(div_rn(sm, r.amem_d, r.inv_mem), 1.0);
   const double sd = fabs((f0 - f1) * r.bamul);
   return (int32_t)((1.0 - sd) * 100.0);  // in [0, 100]
+}
+
+__device__ __forceinline__ int32_t score_ba(const PodDev &p, const NodeRegs &r) {
+  return score_ba_sum(r.rcpu + p.req_cpu_d, r.rmem + p.req_mem_d, r);
 }
 
 __device__ __forceinline__ int64_t taint_raw(const PodDev &p, const NodeExt &e) {

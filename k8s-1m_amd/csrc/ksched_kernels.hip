@@ -256,9 +256,9 @@ __device__ __forceinline__ uint32_t normalize_inv(uint32_t raw, double inv) {
 constexpr uint32_t KEY32_POS_BITS = 9, KEY32_POS_MASK = (1u << KEY32_POS_BITS) - 1;
 
 template <int NPL, bool EXT, int LWU = LW>
-// EXT with 2 nodes per lane: 5 waves per SIMD (96 VGPRs, 12 B/lane spilled at
-// 2 label words) runs the C4 sweep 5 % faster than 4 (103 VGPRs); 6 waves
-// spill 72 B, and the resource-only kernel spills 76 B at 5 (kept at 4)
+// EXT with 2 nodes per lane: 5 waves per SIMD (91 VGPRs) runs the C4 sweep
+// 5 % faster than 4 (103 VGPRs); 6 waves spill 72 B; the resource-only
+// kernel at 5 waves spills 20 B and measured 9 % slower (kept at 4)
 __global__ __launch_bounds__(SWEEP_THREADS) __attribute__((amdgpu_waves_per_eu(EXT && NPL == 2 ? 5 : 1)))
 void sweep_kernel(RoundArgs a) {
   static_assert(NPL * WAVE <= (1 << KEY32_POS_BITS), "wave-local key position field");
@@ -357,8 +357,10 @@ void sweep_kernel(RoundArgs a) {
       const double *ip = fix ? a.norm_inv + 2 * r : a.guess_inv + 2 * (size_t)pi;  // RN(1 / max)
       const double inv_tt = (p.flags & PF_TT) ? ip[0] : 0.0;
       const double inv_na = (p.flags & PF_NA) ? ip[1] : 0.0;
-      const double rq_c = ((p.flags & PF_HAS_REQ) && p.req_cpu > 0) ? p.req_cpu_d : -__builtin_inf();
-      const double rq_m = ((p.flags & PF_HAS_REQ) && p.req_mem > 0) ? p.req_mem_d : -__builtin_inf();
+      // request > Allocatable - Requested as Requested + request > Allocatable
+      // (exact integers in binary64): the sums BalancedAllocation divides,
+      // so the free columns need no registers (96 -> 91 VGPRs, no spill at 5 waves)
+      const bool hc = (p.flags & PF_HAS_REQ) && p.req_cpu > 0, hm = (p.flags & PF_HAS_REQ) && p.req_mem > 0;
       const bool ext = p.flags & PF_EXT;
       const bool named = p.name_slot != -1;
       static_for<NPL>([&](auto J) {
@@ -368,7 +370,8 @@ void sweep_kernel(RoundArgs a) {
         // TaintToleration, NodeAffinity, NodeResourcesFit), branch-free:
         // every lane scores its node and the feasibility mask selects
         int st = ST_FEASIBLE;
-        const bool fitfail = !podfit[j] || (rq_c > nr[j].free_cpu) || (rq_m > nr[j].free_mem);
+        const double sc = nr[j].rcpu + p.req_cpu_d, sm = nr[j].rmem + p.req_mem_d;
+        const bool fitfail = !podfit[j] || (hc && sc > nr[j].acpu_d) || (hm && sm > nr[j].amem_d);
         if (fitfail) st = 4;
         if (ext) {
           const uint64_t untol = ne[j].hard & ~p.tol_hard;
@@ -382,7 +385,7 @@ void sweep_kernel(RoundArgs a) {
         if (!valid) st = ST_EMPTY;
         const bool feasible = st == ST_FEASIBLE;
         uint32_t tot1 = wmul((uint32_t)a.w.fit, (uint32_t)score_la(p, nr[j])) +
-                        wmul((uint32_t)a.w.ba, ABL_ON(8) ? (uint32_t)score_ba(p, nr[j]) : 50u) + 1u;
+                        wmul((uint32_t)a.w.ba, ABL_ON(8) ? (uint32_t)score_ba_sum(sc, sm, nr[j]) : 50u) + 1u;
         uint32_t tts = 100u;
         bool at_tt = false, at_na = false;
         if (p.flags & PF_TT) {
