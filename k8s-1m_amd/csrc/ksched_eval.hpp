@@ -194,6 +194,13 @@ __device__ __forceinline__ uint32_t wmul(uint32_t w, uint32_t x) {
   return r;
 }
 
+// w * x + y, all < 2^24 (v_mad_u32_u24, full rate)
+__device__ __forceinline__ uint32_t wmad(uint32_t w, uint32_t x, uint32_t y) {
+  uint32_t r;
+  asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(r) : "v"(w), "v"(x), "v"(y));
+  return r;
+}
+
 // leastRequestedScore(requested, capacity) = (capacity - requested) * 100 / capacity
 // (int64 truncation; 0 when requested > capacity) from x = max(lf100 - nz100, 0)
 // = max(capacity - requested, 0) * 100, exact.  With y = RN(1 / capacity),

@@ -71,8 +71,10 @@ __device__ __forceinline__ void sort8_desc(uint64_t *k) {
   cx_desc(k[1], k[2]); cx_desc(k[3], k[4]); cx_desc(k[5], k[6]);
 }
 
+// the builtin takes the compare's lane mask as is (__ballot(int) made the
+// compiler copy it into a VGPR and compare it again)
 __device__ __forceinline__ uint32_t popc_ballot(bool b) {
-  return (uint32_t)__popcll(__ballot(b));
+  return (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(b));
 }
 
 __device__ __forceinline__ uint32_t uniform_u32(uint32_t v) {
@@ -303,6 +305,13 @@ void sweep_kernel(RoundArgs a) {
     vcount += popc_ballot(nr[j].bits & 1u);
   });
   const uint32_t kpos0 = KEY32_POS_MASK - lane;
+  // resource-only batches: the pod-independent part of each node's key,
+  // (TaintToleration 100 * weight + 1) << 9 | ~(step * 64 + lane)
+  uint32_t kc[EXT ? 1 : NPL];
+  if constexpr (!EXT) {
+    const uint32_t cplus = (uint32_t)(a.w.tt * 100) + 1u;
+    static_for<NPL>([&](auto J) { kc[J] = (cplus << KEY32_POS_BITS) + (kpos0 - (uint32_t)J * WAVE); });
+  }
 
   for (uint32_t it = p0; it < p1; ++it) {
     // FIX mode: slice entry it - start of the compacted flagged-pod list
@@ -327,16 +336,17 @@ void sweep_kernel(RoundArgs a) {
       // request skips its check (fitsRequest), encoded as a -inf request.
       const double rq_c = ((p.flags & PF_HAS_REQ) && p.req_cpu > 0) ? p.req_cpu_d : -__builtin_inf();
       const double rq_m = ((p.flags & PF_HAS_REQ) && p.req_mem > 0) ? p.req_mem_d : -__builtin_inf();
-      const uint32_t cplus = (uint32_t)(a.w.tt * 100) + 1u;  // TaintToleration 100 (no prefer taints) + 1
       static_for<NPL>([&](auto J) {
         constexpr int j = J;
         const bool feasible = podfit[j] && !(rq_c > nr[j].free_cpu) && !(rq_m > nr[j].free_mem);
-        const uint32_t tot1 = wmul((uint32_t)a.w.fit, (uint32_t)score_la(p, nr[j])) +
-                              wmul((uint32_t)a.w.ba, (uint32_t)score_ba(p, nr[j])) + cplus;
-        const uint32_t key = feasible ? (tot1 << KEY32_POS_BITS) | (kpos0 - (uint32_t)j * WAVE) : 0u;
+        // key = (w_fit LA + w_ba BA) << 9 + kc[j]: one 24-bit multiply, one
+        // multiply-add and one shift-add per node
+        const uint32_t s = wmad((uint32_t)a.w.fit, (uint32_t)score_la(p, nr[j]),
+                                wmul((uint32_t)a.w.ba, (uint32_t)score_ba(p, nr[j])));
+        const uint32_t key = feasible ? (s << KEY32_POS_BITS) + kc[j] : 0u;
         b2 = max(b2, min(b1, key));
         b1 = max(b1, key);
-        feas += popc_ballot(feasible);
+        feas += popc_ballot(key != 0u);  // feasible keys are >= 1 << 9 (one compare, no bool copy)
       });
       f4 = vcount - feas;
     } else {
