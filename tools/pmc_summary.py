@@ -32,7 +32,9 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
 SWEEP = "sweep_kernel"
-KERNEL_SOURCES = ["k8s-1m_amd/csrc/ksched_kernels.hip", "k8s-1m_amd/csrc/ksched_dev.hpp",
+# the same list, in the same order, as bench.py's KERNEL_SOURCES (the bench
+# uses a summary only when the hashes agree)
+KERNEL_SOURCES = ["k8s-1m_amd/csrc/ksched_kernels.hip", "k8s-1m_amd/csrc/ksched_eval.hpp", "k8s-1m_amd/csrc/ksched_dev.hpp",
                   "k8s-1m_amd/csrc/ksched_kernels.hpp", "k8s-1m_amd/Makefile"]
 
 
