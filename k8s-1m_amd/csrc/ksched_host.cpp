@@ -345,6 +345,12 @@ struct ks_ctx {
   bool early_fix = true;
   bool tuple_guess = true;  // normaliser guesses over node tuples (refine_guesses)
   uint32_t timing_every = 8, sweep_blocks = 8192, ext_npl = 2;
+  // KS_EVENT_PROFILE=1: per event kind, runs / events / seconds of ks_events_apply (stderr at ks_close)
+  bool ev_profile = false;
+  struct EvProf {
+    uint64_t runs = 0, events = 0;
+    double s = 0;
+  } ev_prof[4];
   // geometry
   uint32_t cap = 0, S = 1, npl = 8, P = 256, K = 256;
   std::vector<Shard> shards;
@@ -431,7 +437,16 @@ struct ks_ctx {
   int64_t *d_sraw2 = nullptr;                                // [npos] InterPodAffinity raw score
   // (slot, set) of pods the batches bound, appended at the end of each run and
   // applied to HostNode::pod_sets only when a reader needs them (flush_bound)
-  std::vector<std::pair<uint32_t, uint32_t>> pending_bound;
+  // NodeInfo.Pods changes as a log of (slot, set, op): +1 bound, -1 removed,
+  // 0 node deleted.  While no selector class is live and no pod carries an
+  // affinity term nothing reads the per-node records, so pod events and node
+  // deletions only append here (no random access into 1M HostNodes per
+  // event); flush_bound replays the log in order when a reader needs them.
+  struct PodRec {
+    uint32_t slot, set;
+    int32_t op;
+  };
+  std::vector<PodRec> pending_bound;
   SpreadClass classes[MAX_CLASSES];
   std::unordered_map<std::string, uint32_t> class_of;  // canonical selector -> class
   uint64_t class_seq = 0;
@@ -1518,8 +1533,29 @@ ks_status intern_set(ks_ctx *c, const ks_pod &p, uint32_t *out, std::vector<uint
 // Apply the pending records of batch-bound pods to the nodes (before a
 // reader: class creation, pod removal, node deletion).
 void flush_bound(ks_ctx *c) {
-  for (auto &b : c->pending_bound) c->nodes[b.first].pod_sets.push_back(b.second);
+  for (auto &b : c->pending_bound) {
+    std::vector<uint32_t> &v = c->nodes[b.slot].pod_sets;
+    if (b.op > 0) {
+      v.push_back(b.set);
+    } else if (b.op < 0) {
+      auto it = std::find(v.begin(), v.end(), b.set);
+      if (it != v.end()) {  // never bound here: nothing to remove
+        *it = v.back();     // a multiset: order is immaterial
+        v.pop_back();
+      }
+    } else {
+      v.clear();
+    }
+  }
   c->pending_bound.clear();
+}
+
+// Nothing reads the per-node pod records: no live selector class, no term class.
+bool pod_records_unread(const ks_ctx *c) {
+  if (c->n_terms) return false;
+  for (int k = 0; k < MAX_CLASSES; ++k)
+    if (c->classes[k].live) return false;
+  return true;
 }
 
 // labels.Selector.Matches over sorted (key, value) ids.
@@ -2155,7 +2191,15 @@ ks_status solo_compile(ks_ctx *c, const ks_pod &p, PodDev &d, ProgBuf &cl, bool 
 ks_status spread_pods_delta(ks_ctx *c, const uint32_t *sets, const uint32_t *slots, uint32_t n, int sign) {
   std::vector<uint64_t> idx, tidx;
   std::vector<int32_t> dv, tdv;
-  if (sign < 0) flush_bound(c);
+  if (pod_records_unread(c)) {  // log only (flush_bound replays it in order)
+    for (uint32_t i = 0; i < n; ++i) c->pending_bound.push_back({slots[i], sets[i], sign});
+    return KS_OK;
+  }
+  flush_bound(c);
+  int live[MAX_CLASSES];  // live selector classes (the per-pod loop visits only these)
+  int nlive = 0;
+  for (int k = 0; k < MAX_CLASSES; ++k)
+    if (c->classes[k].live) live[nlive++] = k;
   for (uint32_t i = 0; i < n; ++i) {
     const uint32_t set = sets[i];
     HostNode &h = c->nodes[slots[i]];
@@ -2164,11 +2208,12 @@ ks_status spread_pods_delta(ks_ctx *c, const uint32_t *sets, const uint32_t *slo
     } else {
       auto it = std::find(h.pod_sets.begin(), h.pod_sets.end(), set);
       if (it == h.pod_sets.end()) continue;  // never bound here: no count to remove
-      h.pod_sets.erase(it);
+      *it = h.pod_sets.back();  // a multiset: order is immaterial
+      h.pod_sets.pop_back();
     }
     const uint32_t pos = c->slot_pos[slots[i]];
-    for (int k = 0; k < MAX_CLASSES; ++k)
-      if (c->classes[k].live && class_matches(c, c->classes[k], set)) {
+    for (int q = 0; q < nlive; ++q)
+      if (const int k = live[q]; class_matches(c, c->classes[k], set)) {
         idx.push_back((uint64_t)k * c->npos + pos);
         dv.push_back(sign);
       }
@@ -2773,7 +2818,7 @@ ks_status run_batch(ks_ctx *c, ks_batch *b) {
     if (c->pending_bound.size() > (1u << 24)) flush_bound(c);
     for (uint32_t i = 0; i < b->n; ++i)
       if (b->h_results[i].status == KS_POD_SCHEDULED) {
-        c->pending_bound.emplace_back((uint32_t)b->h_results[i].node_index, b->set_ids[i]);
+        c->pending_bound.push_back({(uint32_t)b->h_results[i].node_index, b->set_ids[i], +1});
         for (auto &t : c->label_sets[b->set_ids[i]].terms) c->terms[t.first].bound++;  // the commit counted it
       }
   }
@@ -2884,6 +2929,7 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
     };
     x->early_fix = env_u("KS_EARLY_FIX", 1) != 0;
     x->tuple_guess = env_u("KS_TUPLE_GUESS", 1) != 0;
+    x->ev_profile = env_u("KS_EVENT_PROFILE", 0) != 0;
     x->timing_every = (uint32_t)std::max(1, env_u("KS_TIMING_EVERY", 8));
     x->sweep_blocks = (uint32_t)std::max(1, env_u("KS_SWEEP_BLOCKS", 8192));
     const int en = env_u("KS_EXT_NPL", 2);  // geometry experiments only
@@ -3001,6 +3047,10 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
 
 void ks_close(ks_ctx *c) {
   if (!c) return;
+  if (c->ev_profile)
+    for (int k = 0; k < 4; ++k)
+      std::fprintf(stderr, "ksched events kind %d: %llu runs, %llu events, %.3f s\n", k,
+                   (unsigned long long)c->ev_prof[k].runs, (unsigned long long)c->ev_prof[k].events, c->ev_prof[k].s);
   drain_async(c);
   {
     std::lock_guard<std::mutex> g(c->qmu);
@@ -3243,13 +3293,17 @@ ks_status ks_nodes_delete(ks_ctx *c, const uint32_t *slots, uint32_t n) {
   if (ks_status dst_ = drain_async(c)) return dst_;
   c->tuple_version++;
   HIPC(c, hipSetDevice(c->cfg.device));
-  flush_bound(c);  // the deleted nodes' records go with them
+  // the deleted nodes' records go with them: replayed now when term counts
+  // need them, else a clear entry in the log
+  const bool unread = pod_records_unread(c);
+  if (!unread) flush_bound(c);
   std::vector<uint32_t> pos(n);
   std::vector<int64_t> core((size_t)n * 8, 0);
   for (uint32_t i = 0; i < n; ++i) {
     if (slots[i] >= c->cap || !c->nodes[slots[i]].present)
       return c->fail(KS_ERR_NOT_FOUND, "slot %u not present", slots[i]);
     HostNode &h = c->nodes[slots[i]];
+    if (unread) c->pending_bound.push_back({slots[i], 0u, 0});
     for (uint32_t set : h.pod_sets)
       for (auto &t : c->label_sets[set].terms) c->terms[t.first].bound--;
     c->name_slot.erase(h.name);
@@ -3288,7 +3342,9 @@ ks_status ks_nodes_delete(ks_ctx *c, const uint32_t *slots, uint32_t n) {
   return spread_nodes_changed(c, slots, n, true);
 }
 
-static ks_status pods_delta(ks_ctx *c, const ks_pod *pods, const uint32_t *slots, uint32_t n, int sign) {
+// pods[i] points at pod i (ks_events_apply passes its events' pointers: no
+// copy of the ks_pod structs)
+static ks_status pods_delta(ks_ctx *c, const ks_pod *const *pods, const uint32_t *slots, uint32_t n, int sign) {
   if (!c || (n && (!pods || !slots))) return KS_ERR_INVALID;
   if (ks_status dst_ = drain_async(c)) return dst_;
   if (!n) return KS_OK;
@@ -3314,15 +3370,16 @@ static ks_status pods_delta(ks_ctx *c, const ks_pod *pods, const uint32_t *slots
       return c->fail(KS_ERR_NOT_FOUND, "slot %u not present", slots[i]);
     int64_t rc, rm, zc, zm;
     ks_status st;
-    if ((st = intern_set(c, pods[i], &sets[i], &hold.v))) return st;
-    if ((st = pod_requests(pods[i], false, &rc, &rm)) || (st = pod_requests(pods[i], true, &zc, &zm)))
+    const ks_pod &pd = *pods[i];
+    if ((st = intern_set(c, pd, &sets[i], &hold.v))) return st;
+    if ((st = pod_requests(pd, false, &rc, &rm)) || (st = pod_requests(pd, true, &zc, &zm)))
       return c->fail(st, "pod requests a resource it cannot express (KS_REQ_HAS_OTHER)");
-    if ((st = pod_xrequests(c, pods[i], true, &xr))) return st;
+    if ((st = pod_xrequests(c, pd, true, &xr))) return st;
     for (auto &x : xr) {
       xidx.push_back((uint64_t)MAX_XRES * c->npos + x.first * (uint64_t)c->npos + c->slot_pos[slots[i]]);
       xval.push_back(sign * x.second);
     }
-    if (pods[i].unmodelled & KS_UNMODELLED_POD_AFFINITY) aff += sign;
+    if (pd.unmodelled & KS_UNMODELLED_POD_AFFINITY) aff += sign;
     pos[i] = c->slot_pos[slots[i]];
     int64_t *x = &d[(size_t)i * 5];
     x[0] = sign * rc;
@@ -3344,11 +3401,19 @@ static ks_status pods_delta(ks_ctx *c, const ks_pod *pods, const uint32_t *slots
   return spread_pods_delta(c, sets.data(), slots, n, sign);
 }
 
+static std::vector<const ks_pod *> pod_ptrs(const ks_pod *pods, uint32_t n) {
+  std::vector<const ks_pod *> v(n);
+  for (uint32_t i = 0; i < n; ++i) v[i] = pods + i;
+  return v;
+}
+
 ks_status ks_pods_add(ks_ctx *c, const ks_pod *pods, const uint32_t *slots, uint32_t n) {
-  return pods_delta(c, pods, slots, n, +1);
+  if (n && !pods) return KS_ERR_INVALID;
+  return pods_delta(c, pod_ptrs(pods, n).data(), slots, n, +1);
 }
 ks_status ks_pods_remove(ks_ctx *c, const ks_pod *pods, const uint32_t *slots, uint32_t n) {
-  return pods_delta(c, pods, slots, n, -1);
+  if (n && !pods) return KS_ERR_INVALID;
+  return pods_delta(c, pod_ptrs(pods, n).data(), slots, n, -1);
 }
 
 ks_status ks_snapshot_update(ks_ctx *c, const ks_node_info *items, uint32_t n, int64_t *generation,
@@ -3395,7 +3460,7 @@ ks_status ks_snapshot_update(ks_ctx *c, const ks_node_info *items, uint32_t n, i
 
 ks_status ks_events_apply(ks_ctx *c, const ks_event *ev, uint32_t n) {
   if (!c || (n && !ev)) return KS_ERR_INVALID;
-  std::vector<ks_pod> pods;
+  std::vector<const ks_pod *> pods;
   std::vector<ks_node> nodes;
   std::vector<uint32_t> slots;
   for (uint32_t i = 0; i < n;) {
@@ -3410,7 +3475,7 @@ ks_status ks_events_apply(ks_ctx *c, const ks_event *ev, uint32_t n) {
       slots.push_back(ev[j].slot);
       if (kind == KS_EV_POD_ADD || kind == KS_EV_POD_REMOVE) {
         if (!ev[j].pod) return c->fail(KS_ERR_INVALID, "event %u: no pod", j);
-        pods.push_back(*ev[j].pod);
+        pods.push_back(ev[j].pod);
       } else if (kind == KS_EV_NODE_UPSERT) {
         if (!ev[j].node) return c->fail(KS_ERR_INVALID, "event %u: no node", j);
         nodes.push_back(*ev[j].node);
@@ -3418,11 +3483,17 @@ ks_status ks_events_apply(ks_ctx *c, const ks_event *ev, uint32_t n) {
     }
     const uint32_t m = j - i;
     ks_status st = KS_OK;
+    const auto t0 = std::chrono::steady_clock::now();
     switch (kind) {
-      case KS_EV_POD_ADD: st = ks_pods_add(c, pods.data(), slots.data(), m); break;
-      case KS_EV_POD_REMOVE: st = ks_pods_remove(c, pods.data(), slots.data(), m); break;
+      case KS_EV_POD_ADD: st = pods_delta(c, pods.data(), slots.data(), m, +1); break;
+      case KS_EV_POD_REMOVE: st = pods_delta(c, pods.data(), slots.data(), m, -1); break;
       case KS_EV_NODE_UPSERT: st = ks_nodes_upsert(c, nodes.data(), slots.data(), m); break;
       default: st = ks_nodes_delete(c, slots.data(), m); break;
+    }
+    if (c->ev_profile) {
+      c->ev_prof[kind].runs++;
+      c->ev_prof[kind].events += m;
+      c->ev_prof[kind].s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     }
     if (st) return st;
     i = j;
