@@ -378,6 +378,7 @@ struct ks_ctx {
   // host mirror / dictionaries
   std::vector<HostNode> nodes;
   uint32_t n_present = 0;
+  std::vector<uint8_t> present_map;  // HostNode::present by slot, compact (pod events check it per pod)
   // ks_snapshot_update: the last NodeInfo.Generation applied per slot, and the max
   std::vector<int64_t> slot_gen;
   int64_t snapshot_gen = 0;
@@ -3002,6 +3003,7 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
   for (auto &sh : x->shards)
     for (uint32_t l = 0; l < sh.count; ++l) x->slot_pos[sh.lo + l] = shard_pos(sh, x->npl, l);
   x->nodes.resize(x->cap);
+  x->present_map.assign(x->cap, 0);
   // device table
   ks_status st;
   NodeTable &t = x->t;
@@ -3157,6 +3159,7 @@ ks_status ks_nodes_upsert(ks_ctx *c, const ks_node *nodes, const uint32_t *slots
       c->n_present++;
     }
     h.present = true;
+    c->present_map[slot] = 1;
     h.name = nid;
     c->name_slot[h.name] = slot;
     std::vector<std::pair<std::string, int64_t>> old_images;
@@ -3311,6 +3314,7 @@ ks_status ks_nodes_delete(ks_ctx *c, const uint32_t *slots, uint32_t n) {
     prefer_mask_ref(c, h.prefer, -1);
     node_images_ref(c, h, -1);
     h = HostNode();
+    c->present_map[slots[i]] = 0;
     c->n_present--;
     pos[i] = c->slot_pos[slots[i]];
     core[(size_t)i * 8 + 2] = -1;  // apods < 0: empty slot
@@ -3366,7 +3370,7 @@ static ks_status pods_delta(ks_ctx *c, const ks_pod *const *pods, const uint32_t
     }
   } hold{c, {}};
   for (uint32_t i = 0; i < n; ++i) {
-    if (slots[i] >= c->cap || !c->nodes[slots[i]].present)
+    if (slots[i] >= c->cap || !c->present_map[slots[i]])
       return c->fail(KS_ERR_NOT_FOUND, "slot %u not present", slots[i]);
     int64_t rc, rm, zc, zm;
     ks_status st;
