@@ -70,6 +70,10 @@ struct Node {
     bool operator==(const PodRec &o) const { return key == o.key; }
   };
   std::vector<PodRec> pod_recs;
+  // NodeInfo.PodsWithAffinity / PodsWithRequiredAntiAffinity sizes: upstream's
+  // HavePodsWithAffinityList / HavePodsWithRequiredAntiAffinityList restrict
+  // InterPodAffinity's scans to these nodes (same results, upstream's cost)
+  int64_t pods_with_affinity = 0, pods_with_req_anti = 0;
 };
 
 // k8s.io/api/core/v1/toleration.go#ToleratesTaint
@@ -889,9 +893,14 @@ struct IpaFilterState {
 IpaFilterState IpaPreFilter(const PodState &st, const std::vector<Node> &nodes) {
   IpaFilterState s;
   const auto &req_aff = st.ipa[KS_POD_AFFINITY_REQUIRED], &req_anti = st.ipa[KS_POD_ANTI_AFFINITY_REQUIRED];
+  // getIncomingAffinityAntiAffinityCounts visits every node only for a pod
+  // with required terms; getExistingAntiAffinityCounts only the nodes with
+  // pods carrying required anti-affinity
+  const bool incoming = !req_aff.empty() || !req_anti.empty();
   for (auto &n : nodes) {
-    if (!n.present) continue;
+    if (!n.present || (!incoming && n.pods_with_req_anti == 0)) continue;
     for (auto &e : n.pod_recs) {
+      if (!incoming && e.terms.empty()) continue;
       for (auto &t : e.terms) {  // updateWithAntiAffinityTerms(existing terms, incoming pod)
         if (t.kind != KS_POD_ANTI_AFFINITY_REQUIRED || !t.Matches(st.ns, st.labels, st.ns_labels)) continue;
         auto it = n.labels.find(t.key);
@@ -1044,11 +1053,21 @@ struct oracle {
       AffTerm a;
       if (NewAffinityTerm(p, p.affinity_terms[k], &a)) rec.terms.push_back(a);
     }
+    auto counts = [&n](const Node::PodRec &r, int64_t d) {
+      bool anti = false;
+      for (auto &t : r.terms) anti |= t.kind == KS_POD_ANTI_AFFINITY_REQUIRED;
+      n.pods_with_affinity += r.terms.empty() ? 0 : d;
+      n.pods_with_req_anti += anti ? d : 0;
+    };
     if (sign > 0) {
+      counts(rec, +1);
       n.pod_recs.push_back(std::move(rec));
     } else {
       auto it = std::find(n.pod_recs.begin(), n.pod_recs.end(), rec);
-      if (it != n.pod_recs.end()) n.pod_recs.erase(it);
+      if (it != n.pod_recs.end()) {
+        counts(*it, -1);
+        n.pod_recs.erase(it);
+      }
     }
     // framework/types.go#NodeInfo.update via calculateResource
     int64_t rc, rm, zc, zm;
@@ -1162,14 +1181,18 @@ struct oracle {
   void ipa_score(const PodState &st, std::vector<Eval> &ev) const {
     std::map<std::string, std::map<std::string, int64_t>> ts;
     const uint32_t N = (uint32_t)nodes.size();
+    // scoring.go#PreScore: without preferred terms of its own only the pods
+    // with affinity (HavePodsWithAffinityList, NodeInfo.PodsWithAffinity) count
+    const bool own = !st.ipa[KS_POD_AFFINITY_PREFERRED].empty() || !st.ipa[KS_POD_ANTI_AFFINITY_PREFERRED].empty();
     for (uint32_t i = 0; i < N; ++i) {
       const Node &n = nodes[i];
-      if (!n.present || n.labels.empty()) continue;
+      if (!n.present || n.labels.empty() || (!own && n.pods_with_affinity == 0)) continue;
       auto add = [&](const AffTerm &t, int64_t w) {
         auto it = n.labels.find(t.key);
         if (it != n.labels.end()) ts[t.key][it->second] += w;
       };
       for (auto &e : n.pod_recs) {
+        if (!own && e.terms.empty()) continue;
         for (auto &t : st.ipa[KS_POD_AFFINITY_PREFERRED])
           if (t.Matches(e.ns, e.labels, e.ns_labels)) add(t, t.weight);
         for (auto &t : st.ipa[KS_POD_ANTI_AFFINITY_PREFERRED])
