@@ -518,6 +518,17 @@ ks_status ks_comm_init_local(ks_ctx *const *ctxs, uint32_t n);
 /* Element-wise max of n doubles over all ranks (in place); also a barrier. */
 ks_status ks_comm_allreduce_max(ks_ctx *ctx, double *values, uint32_t n);
 
+/* Parity dump of the round kernels' own output: the merged candidate record
+ * of pod `pod_in_round` of the LAST batch's first round (read after
+ * ks_schedule / ks_batch_run returns; valid while that round resolved every
+ * pod it swept, i.e. for batches of at most pods_per_round pods): out[0] the
+ * bound (>= every unlisted feasible packed key), out[1] the key count, then
+ * the packed keys ((TotalScore + 1) << 32 | ~slot, descending) as the sweep
+ * computed them against the round-start state; out has room for 2 + topk
+ * words.  Lets tests compare the fused sweep's per-node scores with the
+ * oracle for every listed node, not only the chosen one. */
+ks_status ks_debug_round_record(ks_ctx *ctx, uint32_t pod_in_round, uint64_t *out);
+
 /* Counters for measurement. */
 typedef struct {
   uint64_t rounds;          /* sweep rounds issued                         */

@@ -3995,6 +3995,25 @@ ks_status ks_reset_stats(ks_ctx *c) {
   return read_counters(c, c->counters_base);
 }
 
+ks_status ks_debug_round_record(ks_ctx *c, uint32_t r, uint64_t *out) {
+  if (!c || !out) return KS_ERR_INVALID;
+  if (ks_status dst_ = drain_async(c)) return dst_;
+  if (r >= c->P) return c->fail(KS_ERR_INVALID, "pod %u of a %u-pod round", r, c->P);
+  HIPC(c, hipSetDevice(c->cfg.device));
+  const size_t RW = rec_words(c->K);
+  // round 0 = parity 0; with several shards the merged record (merge_shards)
+  const uint64_t *rec = (c->S == 1 ? c->d_srec : c->d_frec) + (size_t)r * RW;
+  std::vector<uint64_t> w(RW);
+  ks_status st;
+  if ((st = xfer_begin(c, RW * 8 + 1024, 0)) || (st = d2h(c, w.data(), rec, RW * 8)) || (st = xfer_sync(c)))
+    return st;
+  const ShardRecHdr *h = (const ShardRecHdr *)w.data();
+  out[0] = h->bound;
+  out[1] = h->nkeys;
+  for (uint32_t i = 0; i < c->K; ++i) out[2 + i] = i < h->nkeys ? w[REC_HDR_WORDS + i] : 0ull;
+  return KS_OK;
+}
+
 ks_status ks_debug_counters(ks_ctx *c, uint64_t out[16]) {
   if (!c || !out) return KS_ERR_INVALID;
   if (ks_status dst_ = drain_async(c)) return dst_;
