@@ -979,6 +979,25 @@ ks_status solo_compile(ks_ctx *c, const ks_pod &p, PodDev &d, ProgBuf &cl, bool 
                        std::vector<uint32_t> *refs);
 void refine_guesses(ks_ctx *c, PodDev &d, const ProgBuf &cl);
 
+// A preferred term no node passing the pod's nodeSelector can match (a node
+// holds one value per label key): In / NotIn / DoesNotExist on a key the
+// nodeSelector pins to another value.  Its weight never counts toward the
+// NodeAffinity max, so the normaliser guess leaves it out (a guess only has
+// to be right often: a wrong one costs a FIX re-sweep, never a wrong result).
+static bool pref_excluded_by_selector(const ks_pod &p, const ks_term &t) {
+  for (uint32_t e = 0; e < t.n_expressions; ++e) {
+    const ks_requirement &r = t.match_expressions[e];
+    for (uint32_t s = 0; s < p.n_node_selector; ++s) {
+      if (str(p.node_selector[s].key) != str(r.key)) continue;
+      const std::string v = str(p.node_selector[s].value);
+      bool in = false;
+      for (uint32_t k = 0; k < r.n_values; ++k) in |= str(r.values[k]) == v;
+      if ((r.op == KS_OP_IN && !in) || (r.op == KS_OP_NOT_IN && in) || r.op == KS_OP_DOES_NOT_EXIST) return true;
+    }
+  }
+  return false;
+}
+
 ks_status compile_pod(ks_ctx *c, const ks_pod &p, PodDev &d, ProgBuf &cl, bool create_spread = false,
                       std::vector<uint32_t> *class_refs = nullptr) {
   std::memset(&d, 0, sizeof d);
@@ -1109,7 +1128,9 @@ ks_status compile_pod(ks_ctx *c, const ks_pod &p, PodDev &d, ProgBuf &cl, bool c
       if (tb.contradictory()) continue;  // matches no node: adds 0 everywhere
       tb.emit(cl, t.weight);
       d.pref_len++;
-      d.na_guess += (uint32_t)t.weight;  // guess of max raw: every term matches some feasible node
+      // guess of max raw: every term matches some feasible node, except the
+      // ones the pod's own nodeSelector rules out
+      if (!pref_excluded_by_selector(p, t.preference)) d.na_guess += (uint32_t)t.weight;
     }
     if (d.pref_len) d.flags |= PF_NA;
   }

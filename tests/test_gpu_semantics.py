@@ -84,12 +84,14 @@ def test_upsert_rejects_duplicate_names_atomically():
 @pytest.mark.parametrize("tuple_guess,fixes", [("0", 3), ("1", 2)])
 def test_wrong_normaliser_guess_is_reswept(tuple_guess, fixes, monkeypatch):
     # normalizer_guess_wrong: with the simple guesses (worst prefer-taint word,
-    # sum of preferred weights) pods x, pref and pref-one-feasible are scored
-    # with a wrong max first and the FIX-mode sweep must run for exactly those;
-    # the node-tuple guesses (KS_TUPLE_GUESS, default) get pref-one-feasible's
-    # NodeAffinity max and pref's right (the tuples a pod's label / taint
-    # filters pass), and x and pref stay wrong (their worst node fails on
-    # resources, which tuples do not see)
+    # sum of the preferred weights the pod's nodeSelector does not rule out)
+    # pods x, pref and pref-one-feasible are scored with a wrong max first
+    # (pref-one-feasible's NodeAffinity guess is right -- its zone=z2 term is
+    # ruled out by nodeSelector zone=z1 -- but its TaintToleration guess is
+    # not) and the FIX-mode sweep must run for exactly those; the node-tuple
+    # guesses (KS_TUPLE_GUESS, default) get pref-one-feasible right, and x and
+    # pref stay wrong (their worst node fails on resources, which tuples do
+    # not see)
     monkeypatch.setenv("KS_TUPLE_GUESS", tuple_guess)
     nodes, pods, exp = SCENARIOS["normalizer_guess_wrong"]()
     a = Arena()
