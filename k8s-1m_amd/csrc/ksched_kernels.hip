@@ -77,6 +77,13 @@ __device__ __forceinline__ uint32_t popc_ballot(bool b) {
   return (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(b));
 }
 
+// v where the lane's bit of the wave mask m is set, else 0
+__device__ __forceinline__ uint32_t sel_mask(uint64_t m, uint32_t v) {
+  uint32_t r;
+  asm("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(r) : "v"(v), "s"(m));
+  return r;
+}
+
 __device__ __forceinline__ uint32_t uniform_u32(uint32_t v) {
   return __builtin_amdgcn_readfirstlane(v);
 }
@@ -298,10 +305,12 @@ void sweep_kernel(RoundArgs a) {
   // per node, pod-independent: pod-count fit (also false for empty slots), and
   // the wave-local key position ~(step * 64 + lane)
   bool podfit[NPL];
+  uint64_t podfit_m[NPL];  // as wave masks (SGPR pairs)
   uint32_t vcount = 0;  // valid nodes of the wave
   static_for<NPL>([&](auto J) {
     constexpr int j = J;
     podfit[j] = nr[j].bits & 2u;
+    podfit_m[j] = __builtin_amdgcn_ballot_w64(podfit[j]);
     vcount += popc_ballot(nr[j].bits & 1u);
   });
   const uint32_t kpos0 = KEY32_POS_MASK - lane;
@@ -338,15 +347,20 @@ void sweep_kernel(RoundArgs a) {
       const double rq_m = ((p.flags & PF_HAS_REQ) && p.req_mem > 0) ? p.req_mem_d : -__builtin_inf();
       static_for<NPL>([&](auto J) {
         constexpr int j = J;
-        const bool feasible = podfit[j] && !(rq_c > nr[j].free_cpu) && !(rq_m > nr[j].free_mem);
+        // the wave's feasibility mask, ANDed from the compares' lane masks
+        // (SALU), selects the key and is counted by s_bcnt1: a bool here
+        // made the compiler copy the mask through a VGPR per node
+        const uint64_t fm = podfit_m[j] &
+                            __builtin_amdgcn_ballot_w64(!(rq_c > nr[j].free_cpu)) &
+                            __builtin_amdgcn_ballot_w64(!(rq_m > nr[j].free_mem));
         // key = (w_fit LA + w_ba BA) << 9 + kc[j]: one 24-bit multiply, one
         // multiply-add and one shift-add per node
         const uint32_t s = wmad((uint32_t)a.w.fit, (uint32_t)score_la(p, nr[j]),
                                 wmul((uint32_t)a.w.ba, (uint32_t)score_ba(p, nr[j])));
-        const uint32_t key = feasible ? (s << KEY32_POS_BITS) + kc[j] : 0u;
+        const uint32_t key = sel_mask(fm, (s << KEY32_POS_BITS) + kc[j]);
         b2 = max(b2, min(b1, key));
         b1 = max(b1, key);
-        feas += popc_ballot(key != 0u);  // feasible keys are >= 1 << 9 (one compare, no bool copy)
+        feas += (uint32_t)__popcll(fm);
       });
       f4 = vcount - feas;
     } else {
