@@ -88,6 +88,14 @@ __device__ __forceinline__ uint32_t uniform_u32(uint32_t v) {
   return __builtin_amdgcn_readfirstlane(v);
 }
 
+// max of two wave-uniform values on the SALU (left to itself the compiler
+// moves the row maxima into VGPRs for one v_max3: three VALU per reduction)
+__device__ __forceinline__ uint32_t smax_u32(uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("s_max_u32 %0, %1, %2" : "=s"(r) : "s"(a), "s"(b) : "scc");
+  return r;
+}
+
 // DPP lane moves (no LDS): quad_perm(1,0,3,2) = 0xB1, quad_perm(2,3,0,1) = 0x4E,
 // row_half_mirror = 0x141, row_mirror = 0x140.
 template <int CTRL>
@@ -120,8 +128,8 @@ __device__ __forceinline__ uint32_t wave_max_u32_dpp(uint32_t v) {
   v = max(v, dpp32<0x4E>(v));
   v = max(v, dpp32<0x141>(v));
   v = max(v, dpp32<0x140>(v));
-  return max(max((uint32_t)__builtin_amdgcn_readlane((int)v, 0), (uint32_t)__builtin_amdgcn_readlane((int)v, 16)),
-             max((uint32_t)__builtin_amdgcn_readlane((int)v, 32), (uint32_t)__builtin_amdgcn_readlane((int)v, 48)));
+  return smax_u32(smax_u32((uint32_t)__builtin_amdgcn_readlane((int)v, 0), (uint32_t)__builtin_amdgcn_readlane((int)v, 16)),
+                  smax_u32((uint32_t)__builtin_amdgcn_readlane((int)v, 32), (uint32_t)__builtin_amdgcn_readlane((int)v, 48)));
 }
 __device__ __forceinline__ uint32_t min8_u32(uint32_t v) {
   v = min(v, dpp32<0xB1>(v));
