@@ -325,6 +325,9 @@ void sweep_kernel(RoundArgs a) {
   // resource-only batches: the pod-independent part of each node's key,
   // (TaintToleration 100 * weight + 1) << 9 | ~(step * 64 + lane)
   uint32_t kc[EXT ? 1 : NPL];
+  const uint32_t wf9 = (uint32_t)a.w.fit << KEY32_POS_BITS, wb9 = (uint32_t)a.w.ba << KEY32_POS_BITS;
+  const uint32_t wt9 = (uint32_t)a.w.tt << KEY32_POS_BITS, wn9 = (uint32_t)a.w.na << KEY32_POS_BITS;
+  const uint32_t kpos1 = (1u << KEY32_POS_BITS) + kpos0;  // the + 1 of the key, and the position
   if constexpr (!EXT) {
     const uint32_t cplus = (uint32_t)(a.w.tt * 100) + 1u;
     static_for<NPL>([&](auto J) { kc[J] = (cplus << KEY32_POS_BITS) + (kpos0 - (uint32_t)J * WAVE); });
@@ -351,8 +354,10 @@ void sweep_kernel(RoundArgs a) {
       // Resource-only pods: only NodeResourcesFit can fail (a batch without
       // PF_EXT pods tolerates every hard taint and names no node).  A zero
       // request skips its check (fitsRequest), encoded as a -inf request.
-      const double rq_c = ((p.flags & PF_HAS_REQ) && p.req_cpu > 0) ? p.req_cpu_d : -__builtin_inf();
-      const double rq_m = ((p.flags & PF_HAS_REQ) && p.req_mem > 0) ? p.req_mem_d : -__builtin_inf();
+      // (requests are >= 0, compile_pod refuses others: `!= 0` is a SALU
+      // compare where `> 0` is a 64-bit VALU one; PF_HAS_REQ is implied)
+      const double rq_c = p.req_cpu != 0 ? p.req_cpu_d : -__builtin_inf();
+      const double rq_m = p.req_mem != 0 ? p.req_mem_d : -__builtin_inf();
       static_for<NPL>([&](auto J) {
         constexpr int j = J;
         // the wave's feasibility mask, ANDed from the compares' lane masks
@@ -361,11 +366,10 @@ void sweep_kernel(RoundArgs a) {
         const uint64_t fm = podfit_m[j] &
                             __builtin_amdgcn_ballot_w64(!(rq_c > nr[j].free_cpu)) &
                             __builtin_amdgcn_ballot_w64(!(rq_m > nr[j].free_mem));
-        // key = (w_fit LA + w_ba BA) << 9 + kc[j]: one 24-bit multiply, one
-        // multiply-add and one shift-add per node
-        const uint32_t s = wmad((uint32_t)a.w.fit, (uint32_t)score_la(p, nr[j]),
-                                wmul((uint32_t)a.w.ba, (uint32_t)score_ba(p, nr[j])));
-        const uint32_t key = sel_mask(fm, (s << KEY32_POS_BITS) + kc[j]);
+        // key = (w_fit LA + w_ba BA) << 9 + kc[j]: two 24-bit multiply-adds
+        // with the weights pre-shifted (10000 << 9 < 2^24; the key < 2^31)
+        const uint32_t key = sel_mask(fm, wmad(wf9, (uint32_t)score_la(p, nr[j]),
+                                               wmad(wb9, (uint32_t)score_ba(p, nr[j]), kc[j])));
         b2 = max(b2, min(b1, key));
         b1 = max(b1, key);
         feas += (uint32_t)__popcll(fm);
@@ -392,7 +396,7 @@ void sweep_kernel(RoundArgs a) {
       // request > Allocatable - Requested as Requested + request > Allocatable
       // (exact integers in binary64): the sums BalancedAllocation divides,
       // so the free columns need no registers (96 -> 91 VGPRs, no spill at 5 waves)
-      const bool hc = (p.flags & PF_HAS_REQ) && p.req_cpu > 0, hm = (p.flags & PF_HAS_REQ) && p.req_mem > 0;
+      const bool hc = p.req_cpu != 0, hm = p.req_mem != 0;  // as rq_c / rq_m above
       const bool ext = p.flags & PF_EXT;
       const bool named = p.name_slot != -1;
       static_for<NPL>([&](auto J) {
@@ -416,8 +420,9 @@ void sweep_kernel(RoundArgs a) {
         }
         if (!valid) st = ST_EMPTY;
         const bool feasible = st == ST_FEASIBLE;
-        uint32_t tot1 = wmul((uint32_t)a.w.fit, (uint32_t)score_la(p, nr[j])) +
-                        wmul((uint32_t)a.w.ba, ABL_ON(8) ? (uint32_t)score_ba_sum(sc, sm, nr[j]) : 50u) + 1u;
+        // key = (TotalScore + 1) << 9 | position, accumulated by 24-bit
+        // multiply-adds with pre-shifted weights (10000 << 9 < 2^24; < 2^31)
+        uint32_t acc = kpos1 - (uint32_t)j * WAVE;
         uint32_t tts = 100u;
         bool at_tt = false, at_na = false;
         if (p.flags & PF_TT) {
@@ -427,18 +432,17 @@ void sweep_kernel(RoundArgs a) {
           over |= feasible && raw > tt_max;
           tmx = max(tmx, feasible ? raw : 0u);
         }
-        tot1 += wmul((uint32_t)a.w.tt, tts);
-        if (p.flags & PF_HAS_PREF) {
-          uint32_t nas = 0u;
-          if (p.flags & PF_NA) {
-            nas = normalize_inv(praw[j], inv_na);
-            at_na = feasible && praw[j] == na_max;
-            over |= feasible && praw[j] > na_max;
-            nmx = max(nmx, feasible ? praw[j] : 0u);
-          }
-          tot1 += wmul((uint32_t)a.w.na, nas);
+        acc = wmad(wt9, tts, acc);
+        if (p.flags & PF_NA) {  // (PF_HAS_PREF without PF_NA scores 0)
+          const uint32_t nas = normalize_inv(praw[j], inv_na);
+          at_na = feasible && praw[j] == na_max;
+          over |= feasible && praw[j] > na_max;
+          nmx = max(nmx, feasible ? praw[j] : 0u);
+          acc = wmad(wn9, nas, acc);
         }
-        const uint32_t key = feasible ? (tot1 << KEY32_POS_BITS) | (kpos0 - (uint32_t)j * WAVE) : 0u;
+        acc = wmad(wb9, ABL_ON(8) ? (uint32_t)score_ba_sum(sc, sm, nr[j]) : 50u, acc);
+        acc = wmad(wf9, (uint32_t)score_la(p, nr[j]), acc);
+        const uint32_t key = feasible ? acc : 0u;
         b2 = max(b2, min(b1, key));
         b1 = max(b1, key);
         const uint64_t fb = __ballot(feasible), vb = __ballot(valid);
