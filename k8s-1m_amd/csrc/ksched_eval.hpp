@@ -210,9 +210,15 @@ __device__ __forceinline__ uint32_t wmad(uint32_t w, uint32_t x, uint32_t y) {
 // 1/capacity above both, so truncation gives the exact floor: no remainder
 // correction.  Proof in DESIGN.md §4; checked by tools/markstein_check.cpp.
 constexpr double LA_EPS = 0x1p-45;
+// The max with 0 is the conversion's: x = lf100 - nz100 is a multiple of 100,
+// so a negative x gives fma <= -100 / capacity + 2^-45 < 0, which
+// v_cvt_u32_f64 clamps to 0 (an unsigned conversion of a negative double is
+// undefined in C++, hence the instruction itself).
 __device__ __forceinline__ int32_t least_requested(double lf100, double pod_nz100, double inv) {
-  const double x = fmax(lf100 - pod_nz100, 0.0);
-  return (int32_t)__builtin_fma(x, inv, LA_EPS);  // x >= 0: truncation == floor; inv == 0 -> 0
+  const double q = __builtin_fma(lf100 - pod_nz100, inv, LA_EPS);  // x >= 0: truncation == floor; inv == 0 -> 0
+  uint32_t r;
+  asm("v_cvt_u32_f64 %0, %1" : "=v"(r) : "v"(q));
+  return (int32_t)r;
 }
 
 __device__ __forceinline__ int32_t score_la(const PodDev &p, const NodeRegs &r) {
@@ -237,8 +243,10 @@ __device__ __forceinline__ int32_t score_ba_sum(double sc, double sm, const Node
   // (exact numerator); std = |(f0 - f1) / 2| with two fractions, else 0
   const double f0 = fmin(div_rn(sc, r.acpu_d, r.inv_cpu), 1.0);
   const double f1 = fmin(div_rn(sm, r.amem_d, r.inv_mem), 1.0);
-  const double sd = fabs((f0 - f1) * r.bamul);
-  return (int32_t)((1.0 - sd) * 100.0);  // in [0, 100]
+  // 1 - std in one FMA: the product |f0 - f1| * bamul (0.5 or 0) is exact,
+  // so the FMA rounds the same difference upstream's 1 - std rounds
+  const double om = __builtin_fma(-fabs(f0 - f1), r.bamul, 1.0);
+  return (int32_t)(om * 100.0);  // in [0, 100]
 }
 
 __device__ __forceinline__ int32_t score_ba(const PodDev &p, const NodeRegs &r) {
