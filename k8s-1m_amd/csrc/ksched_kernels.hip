@@ -356,20 +356,23 @@ void sweep_kernel(RoundArgs a) {
       // request skips its check (fitsRequest), encoded as a -inf request.
       // (requests are >= 0, compile_pod refuses others: `!= 0` is a SALU
       // compare where `> 0` is a 64-bit VALU one; PF_HAS_REQ is implied)
-      const double rq_c = p.req_cpu != 0 ? p.req_cpu_d : -__builtin_inf();
-      const double rq_m = p.req_mem != 0 ? p.req_mem_d : -__builtin_inf();
+      // Fit as Requested + request > Allocatable on the sums BalancedAllocation
+      // divides (exact integers in binary64), so the free columns need no
+      // registers; a zero request's check is masked off (all-ones lane mask)
+      const uint32_t zc32 = uniform_u32(p.req_cpu != 0 ? 0u : ~0u), zm32 = uniform_u32(p.req_mem != 0 ? 0u : ~0u);
+      const uint64_t zc = ((uint64_t)zc32 << 32) | zc32, zm = ((uint64_t)zm32 << 32) | zm32;  // SGPR pairs
       static_for<NPL>([&](auto J) {
         constexpr int j = J;
+        const double sc = nr[j].rcpu + p.req_cpu_d, sm = nr[j].rmem + p.req_mem_d;
         // the wave's feasibility mask, ANDed from the compares' lane masks
         // (SALU), selects the key and is counted by s_bcnt1: a bool here
         // made the compiler copy the mask through a VGPR per node
-        const uint64_t fm = podfit_m[j] &
-                            __builtin_amdgcn_ballot_w64(!(rq_c > nr[j].free_cpu)) &
-                            __builtin_amdgcn_ballot_w64(!(rq_m > nr[j].free_mem));
+        const uint64_t fm = podfit_m[j] & (zc | __builtin_amdgcn_ballot_w64(!(sc > nr[j].acpu_d))) &
+                            (zm | __builtin_amdgcn_ballot_w64(!(sm > nr[j].amem_d)));
         // key = (w_fit LA + w_ba BA) << 9 + kc[j]: two 24-bit multiply-adds
         // with the weights pre-shifted (10000 << 9 < 2^24; the key < 2^31)
         const uint32_t key = sel_mask(fm, wmad(wf9, (uint32_t)score_la(p, nr[j]),
-                                               wmad(wb9, (uint32_t)score_ba(p, nr[j]), kc[j])));
+                                               wmad(wb9, (uint32_t)score_ba_sum(sc, sm, nr[j]), kc[j])));
         b2 = max(b2, min(b1, key));
         b1 = max(b1, key);
         feas += (uint32_t)__popcll(fm);
