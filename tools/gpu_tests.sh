@@ -6,7 +6,7 @@ cd "$R"
 TAG=${1:-r2}
 SEL=${2:-}
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread $SEL > gpurun_out/tests_gpu_$TAG.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout ${PYTEST_TIMEOUT:-170} --timeout-method thread --durations=15 $SEL > gpurun_out/tests_gpu_$TAG.log 2>&1
 rc=$?; tail -5 gpurun_out/tests_gpu_$TAG.log; echo "tests rc=$rc"
 if [ $rc -ne 0 ]; then exit $rc; fi
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1
