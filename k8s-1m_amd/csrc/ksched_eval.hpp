@@ -201,6 +201,14 @@ __device__ __forceinline__ uint32_t wmad(uint32_t w, uint32_t x, uint32_t y) {
   return r;
 }
 
+// the same with a wave-uniform w read from an SGPR (VOP3 takes one): no
+// v_mov of the weight per use where VGPRs are short
+__device__ __forceinline__ uint32_t wmad_s(uint32_t w, uint32_t x, uint32_t y) {
+  uint32_t r;
+  asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(r) : "s"(w), "v"(x), "v"(y));
+  return r;
+}
+
 // leastRequestedScore(requested, capacity) = (capacity - requested) * 100 / capacity
 // (int64 truncation; 0 when requested > capacity) from x = max(lf100 - nz100, 0)
 // = max(capacity - requested, 0) * 100, exact.  With y = RN(1 / capacity),

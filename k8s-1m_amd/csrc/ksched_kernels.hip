@@ -349,7 +349,7 @@ void sweep_kernel(RoundArgs a) {
     uint32_t b1 = 0, b2 = 0;
     uint32_t feas = 0, f0 = 0, f1 = 0, f2 = 0, f3 = 0, f4 = 0, ttc = 0, nac = 0;
     uint32_t tmx = 0, nmx = 0;  // max raw over this lane's feasible nodes
-    bool over = false;          // a feasible node's raw score exceeds the max used
+    uint64_t over_m = 0;        // lanes where a feasible node's raw score exceeds the max used
     if constexpr (!EXT) {
       // Resource-only pods: only NodeResourcesFit can fail (a batch without
       // PF_EXT pods tolerates every hard taint and names no node).  A zero
@@ -371,8 +371,8 @@ void sweep_kernel(RoundArgs a) {
                             (zm | __builtin_amdgcn_ballot_w64(!(sm > nr[j].amem_d)));
         // key = (w_fit LA + w_ba BA) << 9 + kc[j]: two 24-bit multiply-adds
         // with the weights pre-shifted (10000 << 9 < 2^24; the key < 2^31)
-        const uint32_t key = sel_mask(fm, wmad(wf9, (uint32_t)score_la(p, nr[j]),
-                                               wmad(wb9, (uint32_t)score_ba_sum(sc, sm, nr[j]), kc[j])));
+        const uint32_t key = sel_mask(fm, wmad_s(wf9, (uint32_t)score_la(p, nr[j]),
+                                                 wmad_s(wb9, (uint32_t)score_ba_sum(sc, sm, nr[j]), kc[j])));
         b2 = max(b2, min(b1, key));
         b1 = max(b1, key);
         feas += (uint32_t)__popcll(fm);
@@ -423,32 +423,34 @@ void sweep_kernel(RoundArgs a) {
         }
         if (!valid) st = ST_EMPTY;
         const bool feasible = st == ST_FEASIBLE;
+        // feasibility and the normaliser tallies as wave masks (SGPR pairs):
+        // bools here are copied through VGPRs and compared again per node
+        const uint64_t fb = __builtin_amdgcn_ballot_w64(feasible);
         // key = (TotalScore + 1) << 9 | position, accumulated by 24-bit
         // multiply-adds with pre-shifted weights (10000 << 9 < 2^24; < 2^31)
         uint32_t acc = kpos1 - (uint32_t)j * WAVE;
         uint32_t tts = 100u;
-        bool at_tt = false, at_na = false;
         if (p.flags & PF_TT) {
           const uint32_t raw = (uint32_t)__popcll(ne[j].prefer & ~p.tol_prefer);
           tts = ABL_ON(4) ? 100u - normalize_inv(raw, inv_tt) : 100u;
-          at_tt = feasible && raw == tt_max;
-          over |= feasible && raw > tt_max;
+          ttc += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(raw == tt_max) & fb);
+          over_m |= __builtin_amdgcn_ballot_w64(raw > tt_max) & fb;
           tmx = max(tmx, feasible ? raw : 0u);
         }
-        acc = wmad(wt9, tts, acc);
+        acc = wmad_s(wt9, tts, acc);
         if (p.flags & PF_NA) {  // (PF_HAS_PREF without PF_NA scores 0)
           const uint32_t nas = normalize_inv(praw[j], inv_na);
-          at_na = feasible && praw[j] == na_max;
-          over |= feasible && praw[j] > na_max;
+          nac += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(praw[j] == na_max) & fb);
+          over_m |= __builtin_amdgcn_ballot_w64(praw[j] > na_max) & fb;
           nmx = max(nmx, feasible ? praw[j] : 0u);
-          acc = wmad(wn9, nas, acc);
+          acc = wmad_s(wn9, nas, acc);
         }
-        acc = wmad(wb9, ABL_ON(8) ? (uint32_t)score_ba_sum(sc, sm, nr[j]) : 50u, acc);
-        acc = wmad(wf9, (uint32_t)score_la(p, nr[j]), acc);
-        const uint32_t key = feasible ? acc : 0u;
+        acc = wmad_s(wb9, ABL_ON(8) ? (uint32_t)score_ba_sum(sc, sm, nr[j]) : 50u, acc);
+        acc = wmad_s(wf9, (uint32_t)score_la(p, nr[j]), acc);
+        const uint32_t key = sel_mask(fb, acc);
         b2 = max(b2, min(b1, key));
         b1 = max(b1, key);
-        const uint64_t fb = __ballot(feasible), vb = __ballot(valid);
+        const uint64_t vb = __builtin_amdgcn_ballot_w64(valid);
         feas += (uint32_t)__popcll(fb);
         if (ABL_ON(2) && fb != vb) {  // some node failed a filter: per-plugin diagnosis counts
           f0 += popc_ballot(st == 0);
@@ -457,16 +459,12 @@ void sweep_kernel(RoundArgs a) {
           f3 += popc_ballot(st == 3);
           f4 += popc_ballot(st == 4);
         }
-        if (p.flags & (PF_TT | PF_NA)) {
-          ttc += popc_ballot(at_tt);
-          nac += popc_ballot(at_na);
-        }
       });
     }
     if (EXT && (p.flags & (PF_TT | PF_NA))) {
       // the wave's max raw is the max used when some feasible node reaches it
       // and none exceeds it (the usual case): reduce only otherwise
-      const bool exceeded = __ballot(over) != 0;
+      const bool exceeded = over_m != 0;
       if (p.flags & PF_TT) tmx = (!exceeded && ttc) ? tt_max : wave_max_u32_dpp(tmx);
       if (p.flags & PF_NA) nmx = (!exceeded && nac) ? na_max : wave_max_u32_dpp(nmx);
     }
