@@ -551,6 +551,19 @@ ks_status ks_reset_stats(ks_ctx *ctx);
  * dictionary rebuilds, [8..15] resolve phase cycle sums (diagnostic
  * KS_STAMPS build only). */
 ks_status ks_debug_counters(ks_ctx *ctx, uint64_t out[16]);
+/* Device-stall guard.  Every wait of the library on the device is bounded
+ * (KS_SYNC_TIMEOUT_MS at ks_open, default 60000, or this call).  A stream
+ * that has not finished in time makes the call return KS_ERR_DEVICE with
+ * ks_last_error naming the unfinished streams, the hand-off flags' device
+ * values and the round numbers they were expected to reach; the context is
+ * then wedged: every later call that waits on the device fails at once, and
+ * ks_close frees nothing the device may still use. */
+ks_status ks_set_sync_timeout(ks_ctx *ctx, uint32_t ms);
+/* Fault injection for that guard (tests): the next scheduling round holds
+ * back the signal of cross-stream hand-off flag `flag` (0 sweep done, 1 side
+ * stream done, 2 round resolved, 3 FIX sweep done) by `usec` microseconds of
+ * bounded device-side waiting, then signals as usual. */
+ks_status ks_debug_stall(ks_ctx *ctx, uint32_t flag, uint32_t usec);
 /* 1 = time sweep / resolve launches with HIP events (every KS_TIMING_EVERY-th
  * round, default 8; sweep_evals counts the timed launches' share), 0 = off. */
 ks_status ks_set_timing(ks_ctx *ctx, int32_t enabled);

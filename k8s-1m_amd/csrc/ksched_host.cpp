@@ -305,10 +305,13 @@ struct LocalGroup {
   std::vector<Post> posts, snap;
   uint32_t arrived = 0;
   uint64_t gen = 0;
+  bool failed = false;  // a rendezvous timed out: the ranks no longer pair up
   // Post this rank's entry and wait for every rank's; false after 300 s (a
-  // peer failed and will never arrive).
+  // peer failed and will never arrive).  A timeout fails the group for good:
+  // the late rank's post would otherwise pair with the next collective's.
   bool exchange(uint32_t rank, Post p, std::vector<Post> &out) {
     std::unique_lock<std::mutex> g(mu);
+    if (failed) return false;
     posts[rank] = std::move(p);
     const uint64_t my = gen;
     if (++arrived == world) {
@@ -316,7 +319,9 @@ struct LocalGroup {
       arrived = 0;
       ++gen;
       cv.notify_all();
-    } else if (!cv.wait_for(g, std::chrono::seconds(300), [&] { return gen != my; })) {
+    } else if (!cv.wait_for(g, std::chrono::seconds(300), [&] { return gen != my || failed; }) || failed) {
+      failed = true;
+      cv.notify_all();
       return false;
     }
     out = snap;
@@ -338,6 +343,16 @@ struct ks_ctx {
   uint32_t round_seq = 0;         // rounds enqueued since open
   uint32_t seq_of[2] = {0, 0};    // round number by parity
   bool value_sync = true;
+  // Device-stall guard (sync_bounded): every host wait on a stream is bounded;
+  // a miss wedges the context.  flag_want[f]: the last round number enqueued
+  // to be signalled on hand-off flag f (what a finished stream leaves there)
+  uint32_t sync_timeout_ms = 60000;
+  bool wedged = false;
+  uint32_t flag_want[4] = {0, 0, 0, 0};
+  uint32_t *h_diag = nullptr;  // pinned: flags read back by the stall report
+  // ks_debug_stall: the next round holds back flag stall_flag's signal by stall_us
+  int32_t stall_flag = -1;
+  uint32_t stall_us = 0;
   // Tuning switches, read from the environment once per context in ks_open
   // (KS_EARLY_FIX, KS_TIMING_EVERY, KS_SWEEP_BLOCKS, KS_EXT_NPL,
   // KS_TUPLE_GUESS), so one process can open contexts with different settings
@@ -559,8 +574,72 @@ inline size_t xround(size_t b) { return (b + 255) & ~(size_t)255; }
 
 using Xfer = ks_ctx::Xfer;
 
+// ------------------------------------------------------------ stall guard
+
+const char *const kFlagName[4] = {"0 (sweep done: main -> side stream)", "1 (side stream done: -> resolve)",
+                                  "2 (round resolved: resolve kernel -> main / side)",
+                                  "3 (FIX sweep done: side -> main)"};
+
+// A stream missed the deadline: wedge the context and name what is stuck.
+ks_status stall_report(ks_ctx *c, hipStream_t st, const char *what, double ms) {
+  c->wedged = true;
+  std::string busy;
+  const std::pair<hipStream_t, const char *> ss[3] = {{c->stream, "main"}, {c->sstream, "side"}, {c->rstream, "resolve"}};
+  for (auto &p : ss)
+    if (p.first && hipStreamQuery(p.first) == hipErrorNotReady) busy += std::string(busy.empty() ? "" : ", ") + p.second;
+  // the flags through a stream of their own (the context's streams are stuck)
+  std::string flags = "unreadable";
+  hipStream_t d = nullptr;
+  if (c->d_flags && c->h_diag && hipStreamCreateWithFlags(&d, hipStreamNonBlocking) == hipSuccess) {
+    if (hipMemcpyAsync(c->h_diag, c->d_flags, 16, hipMemcpyDeviceToHost, d) == hipSuccess) {
+      const auto t0 = std::chrono::steady_clock::now();
+      while (hipStreamQuery(d) == hipErrorNotReady &&
+             std::chrono::steady_clock::now() - t0 < std::chrono::seconds(2))
+        std::this_thread::sleep_for(std::chrono::microseconds(200));
+      if (hipStreamQuery(d) == hipSuccess) {
+        flags.clear();
+        // the stuck hand-off: of the flags behind what was enqueued, the one
+        // at the earliest round, ties in pipeline order (sweep, FIX, side,
+        // resolve): the flags after it wait on it
+        int stuck = -1;
+        for (int f : {0, 3, 1, 2}) {
+          char b[96];
+          std::snprintf(b, sizeof b, "%sflag %d = %u (enqueued up to %u)", flags.empty() ? "" : "; ", f, c->h_diag[f],
+                        c->flag_want[f]);
+          flags += b;
+          if (c->h_diag[f] < c->flag_want[f] && (stuck < 0 || c->h_diag[f] < c->h_diag[stuck])) stuck = f;
+        }
+        flags += stuck >= 0 ? std::string("; stuck: flag ") + kFlagName[stuck] : std::string("; every flag reached");
+      }
+    }
+    (void)hipStreamDestroy(d);  // returns once the copy is done or abandoned
+  }
+  return c->fail(KS_ERR_DEVICE,
+                 "device stall: %s stream work of %s not finished after %.0f ms (round %u); unfinished streams: %s; %s",
+                 st == c->stream ? "main" : st == c->sstream ? "side" : st == c->rstream ? "resolve" : "a",
+                 what, ms, c->round_seq, busy.empty() ? "none" : busy.c_str(), flags.c_str());
+}
+
+// hipStreamSynchronize with a deadline (sync_timeout_ms): polls, yielding for
+// the first 20 ms (a drain normally ends within a few ms), then sleeping.
+ks_status sync_bounded(ks_ctx *c, hipStream_t st, const char *what) {
+  if (c->wedged) return c->fail(KS_ERR_DEVICE, "context wedged by an earlier device stall (%s)", what);
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    const hipError_t e = hipStreamQuery(st);
+    if (e == hipSuccess) return KS_OK;
+    if (e != hipErrorNotReady)
+      return c->fail(KS_ERR_DEVICE, "hipStreamQuery (%s): %s", what, hipGetErrorString(e));
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (ms > c->sync_timeout_ms) return stall_report(c, st, what, ms);
+    if (ms < 20) std::this_thread::yield();
+    else std::this_thread::sleep_for(std::chrono::microseconds(ms < 1000 ? 50 : 1000));
+  }
+}
+
 ks_status xfer_sync(ks_ctx *c, Xfer &x) {
-  HIPC(c, hipStreamSynchronize(x.st));
+  ks_status st0 = sync_bounded(c, x.st, "a host<->device transfer");
+  if (st0) return st0;
   for (auto &p : x.d2h_pending) std::memcpy(p.dst, x.pin + p.off, p.bytes);
   x.d2h_pending.clear();
   x.pin_used = x.dscr_used = 0;
@@ -1636,7 +1715,7 @@ bool class_matches(const ks_ctx *c, const SpreadClass &k, uint32_t set) {
 ks_status spread_scratch(ks_ctx *c, uint32_t need) {
   if (need <= c->dom_cap) return KS_OK;
   // callers have drained every submitted batch (hipFree waits for the device)
-  HIPC(c, hipStreamSynchronize(c->stream));
+  if (ks_status e_ = sync_bounded(c, c->stream, __func__)) return e_;
   if (c->d_dcnt) (void)hipFree(c->d_dcnt);
   if (c->d_dflag) (void)hipFree(c->d_dflag);
   if (c->d_adcnt) (void)hipFree(c->d_adcnt);
@@ -1915,7 +1994,7 @@ ks_status term_get(ks_ctx *c, const ks_pod &p, const ks_pod_affinity_term &t, bo
     if ((st = dalloc(c, &nt, (size_t)cap * c->npos))) return st;
     if (c->d_tcnt) {
       HIPC(c, hipMemcpyAsync(nt, c->d_tcnt, (size_t)c->tcnt_cap * c->npos * 4, hipMemcpyDeviceToDevice, c->stream));
-      HIPC(c, hipStreamSynchronize(c->stream));
+      if (ks_status e_ = sync_bounded(c, c->stream, __func__)) return e_;
       (void)hipFree(c->d_tcnt);
     }
     c->d_tcnt = nt;
@@ -2371,6 +2450,11 @@ ks_status collect_timing(ks_ctx *c) {
 // Cross-stream hand-off: `st` signals round number `seq` on flag f (or by the
 // event, KS_VALUE_SYNC=0); `wt` waits for it.
 static ks_status hand_signal(ks_ctx *c, hipStream_t st, int f, hipEvent_t ev, uint32_t seq) {
+  if (c->stall_flag == f) {  // ks_debug_stall
+    HIPC(c, launch_stall(c->stall_us, st));
+    c->stall_flag = -1;
+  }
+  c->flag_want[f] = seq;
   // with value hand-offs the event is not waited on (drain_rounds waits on
   // ev_res only): skip its marker packet
   if (c->value_sync) HIPC(c, hipStreamWriteValue32(st, c->d_flags + f, seq, 0));
@@ -2388,7 +2472,7 @@ static ks_status hand_wait(ks_ctx *c, hipStream_t wt, int f, hipEvent_t ev, uint
 
 ks_status lg_exchange(ks_ctx *c, LocalGroup::Post p, std::vector<LocalGroup::Post> &out) {
   if (!c->lgroup->exchange(c->cfg.rank, std::move(p), out))
-    return c->fail(KS_ERR_COMM, "in-process communicator: a peer rank did not arrive within 300 s");
+    return c->fail(KS_ERR_COMM, "in-process communicator failed: a peer rank did not arrive within 300 s");
   return KS_OK;
 }
 
@@ -2608,6 +2692,12 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k, uint32_t end) {
     RoundArgs ra = a;
     ra.flag_res = c->value_sync ? c->d_flags + 2 : nullptr;
     ra.seq = seq;
+    ra.stall_us = 0;
+    if (c->stall_flag == 2) {  // ks_debug_stall
+      ra.stall_us = c->stall_us;
+      c->stall_flag = -1;
+    }
+    c->flag_want[2] = seq;
     HIPC(c, launch_resolve(ra, b->ext, c->rstream));
   }
   if (tm) {
@@ -2629,8 +2719,7 @@ ks_status drain_rounds(ks_ctx *c, uint32_t rounds, void *h_res, const void *d_re
   }
   if (res_bytes) HIPC(c, hipMemcpyAsync(h_res, d_res, res_bytes, hipMemcpyDeviceToHost, c->stream));
   HIPC(c, hipMemcpyAsync(c->h_start, c->d_start, 4, hipMemcpyDeviceToHost, c->stream));
-  HIPC(c, hipStreamSynchronize(c->stream));
-  return KS_OK;
+  return sync_bounded(c, c->stream, "a pipeline run's drain");
 }
 
 // ------------------------------------------------------------- batches
@@ -2832,7 +2921,10 @@ ks_status run_batch(ks_ctx *c, ks_batch *b) {
     }
     lo = hi;
   }
-  HIPC(c, hipStreamSynchronize(c->stream));
+  {
+    ks_status st1 = sync_bounded(c, c->stream, "a batch run");
+    if (st1) return st1;
+  }
   {
     // NodeInfo.Pods of the nodes this batch bound pods to (later selector
     // classes count them): appended to a log, applied when read
@@ -2956,6 +3048,7 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
     x->sweep_blocks = (uint32_t)std::max(1, env_u("KS_SWEEP_BLOCKS", 8192));
     const int en = env_u("KS_EXT_NPL", 2);  // geometry experiments only
     x->ext_npl = (uint32_t)(en == 4 || en == 8 ? en : 2);
+    x->sync_timeout_ms = (uint32_t)std::max(1, env_u("KS_SYNC_TIMEOUT_MS", 60000));
   }
   {
     // Resolve runs on a high-priority stream on KS_RESOLVE_CUS (default 1) CUs
@@ -3051,6 +3144,7 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
     return st;
   HIPC(x, hipHostMalloc((void **)&x->h_start, 4, hipHostMallocDefault));
   HIPC(x, hipHostMalloc((void **)&x->h_seg, 4, hipHostMallocDefault));
+  HIPC(x, hipHostMalloc((void **)&x->h_diag, 64, hipHostMallocDefault));
   // round records: blocks of the widest kernel (npl 2 -> sub = npl / 2)
   uint32_t bmax = 0;
   for (auto &sh : x->shards) bmax = std::max(bmax, blocks_per_shard(sh, x->npl / std::min<uint32_t>(x->npl, 2)));
@@ -3082,9 +3176,19 @@ void ks_close(ks_ctx *c) {
   }
   if (c->worker.joinable()) c->worker.join();
   (void)hipSetDevice(c->cfg.device);
-  if (c->stream) (void)hipStreamSynchronize(c->stream);
-  if (c->rstream) (void)hipStreamSynchronize(c->rstream);
-  if (c->sstream) (void)hipStreamSynchronize(c->sstream);
+  // bounded (a wedged context gets one more full timeout to finish)
+  const bool was_wedged = c->wedged;
+  c->wedged = false;
+  for (hipStream_t st : {c->stream, c->rstream, c->sstream})
+    if (st && !c->wedged) (void)sync_bounded(c, st, "ks_close");
+  if (was_wedged && !c->wedged)
+    std::fprintf(stderr, "ksched: the stalled device work of a wedged context finished before ks_close\n");
+  if (c->wedged) {
+    // device work of this context may never finish: free nothing it may use
+    std::fprintf(stderr, "ksched: closing a wedged context; its device memory and streams are left allocated\n");
+    delete c;
+    return;
+  }
   if (c->comm) ncclCommDestroy(c->comm);
   for (auto &e : c->lg_ev)
     if (e) (void)hipEventDestroy(e);
@@ -3099,6 +3203,7 @@ void ks_close(ks_ctx *c) {
     if (b) (void)hipFree(b);
   if (c->h_start) (void)hipHostFree(c->h_start);
   if (c->h_seg) (void)hipHostFree(c->h_seg);
+  if (c->h_diag) (void)hipHostFree(c->h_diag);
   if (c->xm.pin) (void)hipHostFree(c->xm.pin);
   if (c->xm.dscr) (void)hipFree(c->xm.dscr);
   for (void *g : c->graveyard) (void)hipFree(g);
@@ -3958,7 +4063,7 @@ ks_status ks_comm_allreduce_max(ks_ctx *c, double *values, uint32_t n) {
   if (!c->has_comm()) return c->fail(KS_ERR_COMM, "ks_comm_init not called");
   HIPC(c, hipSetDevice(c->cfg.device));
   if (c->lgroup) {  // host values: a rendezvous after this rank's queued work has finished
-    HIPC(c, hipStreamSynchronize(c->stream));
+    if (ks_status e_ = sync_bounded(c, c->stream, __func__)) return e_;
     std::vector<LocalGroup::Post> ps;
     ks_status e = lg_exchange(c, {nullptr, nullptr, std::vector<double>(values, values + n)}, ps);
     if (e) return e;
@@ -4052,6 +4157,21 @@ ks_status ks_set_timing(ks_ctx *c, int32_t enabled) {
   if (!c) return KS_ERR_INVALID;
   if (ks_status dst_ = drain_async(c)) return dst_;
   c->timing = enabled != 0;
+  return KS_OK;
+}
+
+ks_status ks_set_sync_timeout(ks_ctx *c, uint32_t ms) {
+  if (!c || ms == 0) return KS_ERR_INVALID;
+  if (ks_status dst_ = drain_async(c)) return dst_;
+  c->sync_timeout_ms = ms;
+  return KS_OK;
+}
+
+ks_status ks_debug_stall(ks_ctx *c, uint32_t flag, uint32_t usec) {
+  if (!c || flag > 3 || usec > 600u * 1000u * 1000u) return KS_ERR_INVALID;
+  if (ks_status dst_ = drain_async(c)) return dst_;
+  c->stall_flag = (int32_t)flag;
+  c->stall_us = usec;
   return KS_OK;
 }
 

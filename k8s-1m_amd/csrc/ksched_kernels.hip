@@ -1246,6 +1246,20 @@ __device__ __forceinline__ void lds_barrier() {
   } while (0)
 #endif
 
+// KS_SINGLE_DONE (diagnostic builds only, make probe_old): the pre-fix
+// single done word, to show the race the double buffer removes
+#ifdef KS_SINGLE_DONE
+#define DONE(b) s_done[0]
+#else
+#define DONE(b) s_done[b]
+#endif
+#ifdef KS_RACE_PROBE
+__device__ __forceinline__ void race_probe_delay() {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) __builtin_amdgcn_s_sleep(127);
+}
+#endif
+
 // Wave-uniform copy of an LDS object into scalar registers: one lane reads it
 // (a 64-lane broadcast read would cost the LDS 64x the bytes), readfirstlane
 // hands every dword to the SALU / VALU-operand side.
@@ -1294,10 +1308,17 @@ __device__ __forceinline__ uint64_t key_q(const PodDev &p, const PodQ &q, const 
   return pack_key(t, g.slot);
 }
 
+// Bounded wall-clock wait (ks_debug_stall): s_memrealtime counts at 100 MHz.
+__device__ __forceinline__ void stall_for(uint32_t usec) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < 100ull * usec) __builtin_amdgcn_s_sleep(127);
+}
+
 // Kernel-side completion signal for a stream wait-value (release at system
 // scope, like the stream write operation it replaces).
-__device__ __forceinline__ void signal_done(uint32_t *flag, uint32_t seq) {
+__device__ __forceinline__ void signal_done(uint32_t *flag, uint32_t seq, uint32_t stall_us = 0) {
   if (flag == nullptr) return;
+  if (stall_us) stall_for(stall_us);
   __threadfence_system();
   __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -1330,7 +1351,12 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
   __shared__ int32_t s_edd[2][NCAND][NFILT + 3];
   // decider -> everyone: pod i's commit {valid, candidate lane, joins, owner index}
   __shared__ uint32_t s_pend[2][4];
-  __shared__ uint32_t s_done, s_stop_at;
+  // s_done[b]: set by the decider in an iteration of parity b, read by every
+  // wave after that iteration's barrier.  Double-buffered: a single word let
+  // the decider's next-iteration store (r == nround: immediately after the
+  // barrier) overtake a slow wave's read of this iteration, which then left
+  // the loop one barrier early
+  __shared__ uint32_t s_done[2], s_stop_at;
   // results of the round, written out after the loop (no global stores inside it)
   __shared__ DevResult s_res[MAX_P];
 
@@ -1347,7 +1373,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
       *a.d_start = start;
       *a.carry_out_n = 0;
       if (start < a.npods) a.counters[3] += 1;  // wasted (speculated) round
-      signal_done(a.flag_res, a.seq);
+      signal_done(a.flag_res, a.seq, a.stall_us);
     }
     return;
   }
@@ -1366,7 +1392,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
     s_norm[i][1] = a.norm_max[2 * i + 1];
   }
   if (tid < 4) s_pend[1][tid] = 0;  // "pod -1" committed nothing
-  if (tid == 0) s_done = 0;
+  if (tid < 2) s_done[tid] = 0;
 
   // ---- list waves (LDS-DMA pipeline).  Per iteration a list wave issues
   // LIST_DMA global_load_lds instructions (the chosen rows' pieces, one key
@@ -1517,7 +1543,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
       if (r >= nround) {
         if (lane == 0) {
           s_pend[buf][0] = 0;
-          s_done = 1;
+          DONE(buf) = 1;
         }
       } else {
         const uint32_t b4 = r % RSLOTS;
@@ -1589,7 +1615,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
           stop_at = r;
           if (lane == 0) {
             s_pend[buf][0] = 0;
-            s_done = 1;
+            DONE(buf) = 1;
           }
         } else {
           DevResult *res = &s_res[r];
@@ -1943,7 +1969,13 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
     st_work += t1 - t0;
     st_wait += t2 - t1;
 #endif
-    return s_done != 0;
+#ifdef KS_RACE_PROBE
+    // regression build (make probe): every wave but the decider reads the
+    // done word late in the last two iterations, so that the decider's
+    // next-iteration store lands first
+    if (ROLE != 0 && r + 2 >= nround) race_probe_delay();
+#endif
+    return DONE(buf) != 0;
   };
 
   // One loop per role (the barrier counts waves, not program locations): each
@@ -1959,9 +1991,12 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
     for (uint32_t r = 0;; ++r)
       if (iteration(r, std::integral_constant<int, 2>{})) break;
   } else if (wid == RES_IDLE) {
-    for (;;) {
+    for (uint32_t r = 0;; ++r) {
       lds_barrier();
-      if (s_done != 0) break;
+#ifdef KS_RACE_PROBE
+      if (r + 2 >= nround) race_probe_delay();
+#endif
+      if (DONE(r & 1u) != 0) break;
     }
   } else {
     for (uint32_t r = 0;; ++r)
@@ -2003,7 +2038,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
   // the streams waiting for this round (write-back, patch) poll the flag:
   // every thread's global stores are ordered before the signal
   __syncthreads();
-  if (tid == 0) signal_done(a.flag_res, a.seq);
+  if (tid == 0) signal_done(a.flag_res, a.seq, a.stall_us);
 }
 
 // ============================================================ pipeline
@@ -2289,6 +2324,14 @@ hipError_t launch_dump(const DumpArgs &a, hipStream_t st) {
   dump_max_kernel<<<g, 256, 0, st>>>(a);
   KS_CHECK(hipGetLastError());
   dump_scores_kernel<<<g, 256, 0, st>>>(a);
+  return hipGetLastError();
+}
+
+__global__ void stall_kernel(uint32_t usec) {
+  if (threadIdx.x == 0) stall_for(usec);
+}
+hipError_t launch_stall(uint32_t usec, hipStream_t st) {
+  stall_kernel<<<1, 64, 0, st>>>(usec);
   return hipGetLastError();
 }
 

@@ -51,6 +51,7 @@ struct RoundArgs {
   uint32_t pstat_sweep;       // the sweep (not the merge) folds its maxima into pstat (one rank)
   uint32_t *flag_res;         // resolve: round number `seq` stored here when done (null: the host signals)
   uint32_t seq;
+  uint32_t stall_us;          // ks_debug_stall: the resolve holds its signal back this long (0: never)
   BlockRec *brec;             // [local shards][P][bstride]
   uint64_t *srec;             // [S][P][rec_words(K)]
   uint64_t *frec;             // [P][rec_words(K)] (== srec when S == 1)
@@ -141,5 +142,7 @@ hipError_t launch_gather_rows(const NodeTable &t, const uint32_t *pos, int64_t *
 hipError_t launch_scatter_u64(uint64_t *col, const uint32_t *pos, const uint64_t *val, uint32_t n,
                               hipStream_t st);
 hipError_t launch_dump(const DumpArgs &a, hipStream_t st);
+// ks_debug_stall: one wave that waits `usec` microseconds of wall clock, then exits
+hipError_t launch_stall(uint32_t usec, hipStream_t st);
 
 }  // namespace ks
