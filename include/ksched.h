@@ -551,6 +551,13 @@ ks_status ks_reset_stats(ks_ctx *ctx);
  * dictionary rebuilds, [8..15] resolve phase cycle sums (diagnostic
  * KS_STAMPS build only). */
 ks_status ks_debug_counters(ks_ctx *ctx, uint64_t out[16]);
+/* Round marks of a finished batch (diagnostics for tests that place parity
+ * checks where the round machinery changed course): out[i] for pod i of the
+ * batch, bits KS_MARK_*.  Valid after ks_batch_run / ks_batch_wait. */
+#define KS_MARK_FIX 1u          /* re-swept with the measured normaliser maxima  */
+#define KS_MARK_ROUND_START 2u  /* first pod of a resolved round                 */
+#define KS_MARK_AFTER_WASTE 4u  /* ... whose previous speculated round was wasted */
+ks_status ks_batch_marks(ks_ctx *ctx, const ks_batch *batch, uint8_t *out);
 /* Device-stall guard.  Every wait of the library on the device is bounded
  * (KS_SYNC_TIMEOUT_MS at ks_open, default 60000, or this call).  A stream
  * that has not finished in time makes the call return KS_ERR_DEVICE with

@@ -279,6 +279,7 @@ struct ks_batch {
   std::vector<uint32_t> class_refs;
   std::vector<uint32_t> term_refs;  // term classes of the batch's pods' own terms (one per pod and term)
   uint64_t *d_cmask = nullptr, *h_cmask = nullptr;
+  uint8_t *d_marks = nullptr;  // [cap_pods rounded to 4] round marks (ks_batch_marks)
   // asynchronous run state (ks_batch_submit / ks_batch_wait)
   bool queued = false, done = false;
   ks_status run_status = KS_OK;
@@ -2578,6 +2579,7 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k, uint32_t end) {
   a.evaluated = c->n_present;
   a.pods = b->d_pods;
   a.clauses = b->d_clauses;
+  a.marks = b->d_marks;
   const uint32_t q = k & 1u, pq = q ^ 1u;
   const size_t RW = rec_words(c->K);
   a.d_start = c->d_start;
@@ -2754,6 +2756,7 @@ ks_status batch_acquire(ks_ctx *c, uint32_t n, size_t words, ks_batch **out) {
     HIPC(c, hipHostMalloc((void **)&b->h_pinv, (size_t)need * 2 * sizeof(double), hipHostMallocDefault));
     HIPC(c, hipMalloc((void **)&b->d_cmask, (size_t)need * 8 * CMASK_WORDS));
     HIPC(c, hipHostMalloc((void **)&b->h_cmask, (size_t)need * 8 * CMASK_WORDS, hipHostMallocDefault));
+    HIPC(c, hipMalloc((void **)&b->d_marks, ((size_t)need + 3) & ~(size_t)3));
     b->cap_pods = need;
   }
   if (words > b->cap_words) {
@@ -2786,6 +2789,7 @@ ks_status upload_batch(ks_ctx *c, ks_batch *b) {
   HIPC(c, hipMemcpyAsync(b->d_pinv, b->h_pinv, np * 2 * sizeof(double), hipMemcpyHostToDevice, c->stream));
   HIPC(c, hipMemcpyAsync(b->d_clauses, b->h_clauses, b->n_words * 8, hipMemcpyHostToDevice, c->stream));
   HIPC(c, hipMemsetAsync(b->d_results, 0, np * sizeof(DevResult), c->stream));
+  HIPC(c, hipMemsetAsync(b->d_marks, 0, (np + 3) & ~(size_t)3, c->stream));
   b->uploaded = true;
   return KS_OK;
 }
@@ -3210,7 +3214,7 @@ void ks_close(ks_ctx *c) {
   for (void *g : c->pinned_graveyard) (void)hipHostFree(g);
   for (ks_batch *b : c->all_batches) {
     for (void *p : {(void *)b->d_pods, (void *)b->d_pinv, (void *)b->d_clauses, (void *)b->d_results,
-                    (void *)b->d_cmask})
+                    (void *)b->d_cmask, (void *)b->d_marks})
       if (p) (void)hipFree(p);
     for (void *p : {(void *)b->h_results, (void *)b->h_pods, (void *)b->h_pinv, (void *)b->h_clauses,
                     (void *)b->h_cmask})
@@ -3814,6 +3818,19 @@ ks_status ks_batch_results(ks_ctx *c, const ks_batch *b, ks_result *out) {
   for (uint32_t i = 0; i < b->n; ++i) sched += out[i].status == KS_POD_SCHEDULED;
   c->stats.pods_scheduled += sched;
   return KS_OK;
+}
+
+ks_status ks_batch_marks(ks_ctx *c, const ks_batch *b, uint8_t *out) {
+  if (!c || !b || (b->n && !out)) return KS_ERR_INVALID;
+  {
+    std::lock_guard<std::mutex> g(c->qmu);
+    if (b->queued && !b->done) return c->fail(KS_ERR_INVALID, "batch still running (ks_batch_wait first)");
+  }
+  if (!b->n) return KS_OK;
+  ks_status st;
+  if ((st = xfer_begin(c, xround(b->n), 0))) return st;
+  if ((st = d2h(c, out, b->d_marks, b->n))) return st;
+  return xfer_sync(c);
 }
 
 void ks_batch_free(ks_ctx *c, ks_batch *b) {

@@ -722,6 +722,13 @@ __global__ __launch_bounds__(MERGE_THREADS) void merge_kernel(RoundArgs a) {
 // round uses (measured when some node is feasible, else the guess, which is
 // then unused) and whether the sweep's guess was wrong (FIX flags, per pod
 // and per MAX_PG-pod group; counters[4] counts re-swept pods).
+// Round marks (diagnostics, ks_batch_marks): byte i of a word-aligned
+// buffer, set atomically (the main stream's norm_check and the resolve stream
+// may mark pods of one word concurrently).
+__device__ __forceinline__ void mark_pod(uint8_t *marks, uint32_t i, uint8_t bit) {
+  atomicOr((uint32_t *)(marks + (i & ~3u)), (uint32_t)bit << (8u * (i & 3u)));
+}
+
 __global__ __launch_bounds__(MAX_P) void norm_check_kernel(RoundArgs a) {
   __shared__ uint32_t s_wn[MAX_P / WAVE];
   const uint32_t start = uniform_u32(*a.sstart);
@@ -746,6 +753,7 @@ __global__ __launch_bounds__(MAX_P) void norm_check_kernel(RoundArgs a) {
     a.norm_inv[2 * r] = tt ? 1.0 / (double)tt : 0.0;
     a.norm_inv[2 * r + 1] = na ? 1.0 / (double)na : 0.0;
     a.fix_flag[r] = wrong ? 1u : 0u;
+    if (wrong) mark_pod(a.marks, start + r, MARK_FIX);
   }
   // compacted list of the flagged pods (round order): the FIX sweep runs
   // ceil(count / MAX_PG) pod groups, so node rows are re-read once per 64
@@ -1372,7 +1380,10 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
       *a.act_next = start;
       *a.d_start = start;
       *a.carry_out_n = 0;
-      if (start < a.npods) a.counters[3] += 1;  // wasted (speculated) round
+      if (start < a.npods) {
+        a.counters[3] += 1;  // wasted (speculated) round
+        mark_pod(a.marks, start, MARK_AFTER_WASTE);  // the next resolved round starts here
+      }
       signal_done(a.flag_res, a.seq, a.stall_us);
     }
     return;
@@ -2030,6 +2041,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
     nmod = 0;  // timing experiment: never write back garbage rows
 #endif
     *a.carry_out_n = nmod;
+    mark_pod(a.marks, start, MARK_ROUND_START);
     *a.act_next = start + stop_at;
     *a.d_start = start + stop_at;
     a.counters[0] += 1;        // rounds

@@ -11,6 +11,11 @@ constexpr int MAX_PG = 64;    // pods per sweep block (LDS wave records)
 constexpr int MAX_P = 256;    // pods per round (resolve stages the round in LDS)
 constexpr int MAX_K = 512;    // candidates per pod record (two list entries per list-wave lane in the resolve)
 constexpr uint32_t FIX_NONE = 0xFFFFFFFFu;  // fix_list tail
+// per-pod round marks (ks_batch_marks, include/ksched.h): where the round
+// machinery changed course, for tests that place checks there
+constexpr uint8_t MARK_FIX = 1;          // re-swept with measured normaliser maxima (FIX sweep)
+constexpr uint8_t MARK_ROUND_START = 2;  // first pod of a resolved round
+constexpr uint8_t MARK_AFTER_WASTE = 4;  // ... whose previous speculated round was wasted
 
 struct RoundArgs {
   NodeTable t;
@@ -52,6 +57,7 @@ struct RoundArgs {
   uint32_t *flag_res;         // resolve: round number `seq` stored here when done (null: the host signals)
   uint32_t seq;
   uint32_t stall_us;          // ks_debug_stall: the resolve holds its signal back this long (0: never)
+  uint8_t *marks;             // [npods] per-pod round marks of the batch (ks_batch_marks): KS_MARK_*
   BlockRec *brec;             // [local shards][P][bstride]
   uint64_t *srec;             // [S][P][rec_words(K)]
   uint64_t *frec;             // [P][rec_words(K)] (== srec when S == 1)

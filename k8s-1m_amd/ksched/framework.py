@@ -307,6 +307,12 @@ class Scheduler:
         self._ok(self.lib.ks_batch_results(self.ctx, batch, raw))
         return raw
 
+    def marks(self, batch, n: int) -> bytes:
+        """Per-pod round marks of a finished batch (ks_batch_marks: KS_MARK_* bits)."""
+        out = (C.c_uint8 * max(1, n))()
+        self._ok(self.lib.ks_batch_marks(self.ctx, batch, out))
+        return bytes(out)[:n]
+
     def free(self, batch):
         self.lib.ks_batch_free(self.ctx, batch)
 

@@ -73,6 +73,30 @@ def replay_check(o, pods, got, m, windows=WINDOWS, wlen=WLEN):
     return checked
 
 
+MARK_FIX, MARK_ROUND_START, MARK_AFTER_WASTE = 1, 2, 4  # ks_batch_marks (include/ksched.h)
+
+
+def pick_windows(marks, m, wlen=WLEN, fixed=WINDOWS, per_kind=3):
+    """The fixed windows plus windows starting where the round machinery changed
+    course (ks_batch_marks): the first pods re-swept with measured normaliser
+    maxima (FIX) and the first pods of rounds that follow a wasted speculated
+    round, up to `per_kind` of each spread over the batch; non-overlapping."""
+    mk = np.frombuffer(marks, dtype=np.uint8)
+    cand = [(w, "fixed") for w in fixed]
+    for bit, what in ((MARK_FIX, "fix"), (MARK_AFTER_WASTE, "after-waste")):
+        idx = np.nonzero(mk & bit)[0]
+        idx = idx[idx + wlen <= m]
+        if len(idx):
+            for j in np.unique(np.linspace(0, len(idx) - 1, min(per_kind, len(idx))).astype(int)):
+                cand.append((int(idx[j]), what))
+    out, end = [], -1
+    for w, what in sorted(cand):
+        if w >= end:
+            out.append((w, what))
+            end = w + wlen
+    return out
+
+
 def run_fullsize(kind, pods, prefill, *, env=None, **cfg):
     nodes = synth.nodes(kind, N, 1)
     slots = synth.slot_array(N)
@@ -93,6 +117,7 @@ def run_fullsize(kind, pods, prefill, *, env=None, **cfg):
     b = s.prepare(pods.pods, BATCH)
     s.run(b)
     got = s.results(b, BATCH)
+    marks = s.marks(b, BATCH)
     s.free(b)
     dbg = (C.c_uint64 * 16)()
     assert s.lib.ks_debug_counters(s.ctx, dbg) == 0
@@ -100,7 +125,16 @@ def run_fullsize(kind, pods, prefill, *, env=None, **cfg):
     o.upsert(nodes.nodes, slots, N)
     if pf is not None:
         o.add_pods(pf.pods, pf.slot_ptr, pf.n_pods)
-    replay_check(o, pods, got, BATCH)
+    wins = pick_windows(marks, BATCH)
+    replay_check(o, pods, got, BATCH, windows=[w for w, _ in wins])
+    mk = np.frombuffer(marks, dtype=np.uint8)
+    covered = np.zeros(BATCH, dtype=bool)
+    for w, _ in wins:
+        covered[w:w + WLEN] = True
+    # a FIX re-sweep / a wasted round that happened is also checked
+    for bit in (MARK_FIX, MARK_AFTER_WASTE):
+        assert not (mk & bit).any() or (covered & ((mk & bit) != 0)).any(), f"no window on a pod marked {bit}"
+    assert (mk & MARK_ROUND_START).sum() >= BATCH // 256
     sg = states_np(s.lib.ks_node_states, s.ctx, N)
     sw = states_np(o.L.oracle_node_states, o.o, N)
     assert np.array_equal(sg, sw), "node tables differ after replaying every decision"

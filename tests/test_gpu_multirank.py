@@ -55,3 +55,26 @@ def test_short_lists_ranks():
 def test_kwok_ties_ranks():
     # identical nodes: every pod's best keys tie across both shards
     run_case(world=2, kind=1, nodes=8000, pods=6000, K=512)
+
+
+def run_full(**cfg):
+    # 8 contexts x 3 streams: hardware queues up to the box's limit
+    env = dict(os.environ, GPU_MAX_HW_QUEUES="32")
+    p = subprocess.run([sys.executable, "-u", os.path.join(HERE, "multirank_full.py"), json.dumps(cfg)],
+                       capture_output=True, text=True, timeout=600, env=env)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert p.returncode == 0 and lines, f"rc={p.returncode}\n{p.stdout[-2000:]}\n{p.stderr[-3000:]}"
+    res = json.loads(lines[-1])
+    assert res["ok"], res["error"]
+    print(res)
+    return res
+
+
+@pytest.mark.parametrize("kind", ["c3", "c4", "c5"])
+def test_fullsize_eight_ranks(kind):
+    # BASELINE.json's 1M-node configurations at the 8-GPU split (125,000 nodes
+    # per rank): every rank == rank 0 == a one-rank context == the oracle's windows
+    r = run_full(world=8, kind=kind)
+    assert r["oracle_pods_checked"] >= 4 * 32
+    if kind == "c4":
+        assert r["reswept"] > 0, "multi-rank FIX path not exercised"
