@@ -74,13 +74,16 @@ B_SPREAD_NODE = 275
 # packed parts, raw score), select 21 (status, slot, packed parts, raw score)
 B_AFF_NODE = 186
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
-# VALU issue peak: a wave64 VALU instruction occupies a 16-lane SIMD for 4
-# cycles (MI355X FP64 vector peak 78.6 TFLOP/s = 256 CUs x 4 SIMDs x 16 lanes
-# x 2 FLOP x 2.4 GHz; only packed FP32 doubles that), and the sweep's PMC pass
-# measures SQ_ACTIVE_INST_VALU (quad-cycles) / SQ_INSTS_VALU = 1.06, i.e. 4.25
-# cycles per instruction: 256 x 4 SIMDs x 2.4 GHz / 4 = 6.14e11 wave64
-# instructions/s = 39.3e12 lane-ops/s.
-VALU_PEAK_WAVE_INSTR = 256 * 4 * 2.4e9 / 4
+# VALU issue peak of the sweep: 256 CUs x 4 SIMDs x 2.4 GHz SIMD cycles per
+# second over the cycles ONE wave64 VALU instruction of the sweep's own mix
+# occupies a SIMD.  That cost is measured, not assumed: tools/valu_issue.hip
+# times every opcode of the sweep's pod loop at 4 waves per SIMD on MI355X
+# (profiles/valu_issue.jsonl: the 32-bit add / logic / move class 2.3-2.5
+# cycles, f64 arithmetic, conversions, compares, multiplies, DPP, readlane and
+# VOP3 forms 4.2-4.4) and tools/valu_mix.py weights them by each kernel's loop
+# mix (profiles/valu_mix.json: 4.08 cycles for the C3 kernel, 3.88 for C4's).
+SIMD_CYCLES_PER_S = 256 * 4 * 2.4e9
+VALU_CYCLES_FALLBACK = 4.0  # when valu_mix.json does not match the kernel sources
 REF_SCHEDULE_ONE_US = 560.0  # README.adoc:786 (per pod per shard, ~195 nodes evaluated)
 KERNEL_SOURCES = ["k8s-1m_amd/csrc/ksched_kernels.hip", "k8s-1m_amd/csrc/ksched_eval.hpp", "k8s-1m_amd/csrc/ksched_dev.hpp",
                   "k8s-1m_amd/csrc/ksched_kernels.hpp", "k8s-1m_amd/Makefile"]
@@ -500,17 +503,29 @@ def roofline(args, st, world):
     path = Path(args.pmc_dir) / f"{key}.json"
     pmc = json.loads(path.read_text()) if path.exists() else {}
     fresh = bool(pmc) and pmc.get("kernel_src") == src
-    r = {"bound": "valu", "achieved": None, "peak": round(VALU_PEAK_WAVE_INSTR * 64 / 1e12, 2),
+    kname = pmc.get("sweep_kernel", "ks::sweep_kernel")
+    # issue cycles per VALU instruction of this kernel's mix (tools/valu_mix.py)
+    mix_path = ROOT / "profiles" / "valu_mix.json"
+    mix = json.loads(mix_path.read_text()) if mix_path.exists() else {}
+    targs = kname[kname.find("<"):] if "<" in kname else ""
+    mk = mix.get("kernels", {}).get(targs) if mix.get("kernel_src") == src else None
+    cyc = mk["cycles_per_valu"] if mk else VALU_CYCLES_FALLBACK
+    peak_wi = SIMD_CYCLES_PER_S / cyc  # wave instructions per second
+    r = {"bound": "valu", "achieved": None, "peak": round(peak_wi * 64 / 1e12, 2),
          "unit": "T VALU lane-ops/s", "frac": None, "traffic": None,
-         "kernel": pmc.get("sweep_kernel", "ks::sweep_kernel"), "avg_launch_ms": round(sweep_avg_ms, 4),
+         "kernel": kname, "avg_launch_ms": round(sweep_avg_ms, 4),
          "evals_per_launch": int(evals_per_launch),
+         "issue_cycles_per_valu": cyc,
+         "issue_model": ("profiles/valu_mix.json (tools/valu_issue.hip costs x the pod loop's opcode mix, "
+                         f"{mk['measured_share']:.0%} of it measured opcodes)" if mk else
+                         "4.0 cycles per instruction (profiles/valu_mix.json missing or stale)"),
          "pmc": f"profiles/pmc/{key}.json" + ("" if fresh else (" (stale: kernel source changed)" if pmc else
                                                                  " (missing)")),
          "kernel_src": src}
     if fresh and st.sweep_launches:
         wi = pmc["valu_wave_instr_per_eval"] * evals_per_launch  # wave instructions per launch
         r["achieved"] = round(wi * 64 / launch_s / 1e12, 2)
-        r["frac"] = round(wi / launch_s / VALU_PEAK_WAVE_INSTR, 4)
+        r["frac"] = round(wi / launch_s / peak_wi, 4)
         r["valu_lane_ops_per_eval"] = round(pmc["valu_wave_instr_per_eval"] * 64, 2)
         for k in ("valu_cycles_per_instr", "valu_f64_share", "clock_ghz"):
             if pmc.get(k) is not None:
