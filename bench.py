@@ -13,13 +13,14 @@ percentageOfNodesToScore = 100, deterministic lowest-slot tie-break,
 sequential-equivalent in-order commit.
 
 A "step" schedules one batch of pods (default 32768) to completion against the
-live cluster.  `value` times ks_batch_run only: the batch was compiled and
-uploaded by ks_batch_prepare before the timed region (inputs resident in
-HBM).  Beside it the line reports:
+live cluster, through the whole boundary the cgo caller uses: `value` times
+ks_batch_prepare (pod compile + H2D), ks_batch_submit / ks_batch_wait (every
+round + D2H of the results) and ks_batch_results, pipelined so that compiling
+batch k+1 overlaps running batch k.  Beside it the line reports:
 
-* value_end_to_end: the same steps through the whole boundary (pod compile +
-  H2D + run + D2H of the results), pipelined with ks_batch_submit /
-  ks_batch_wait so that compiling batch k+1 overlaps running batch k;
+* value_inputs_resident: the same number of steps with every batch compiled
+  and uploaded before the timed region (ks_batch_run only: the device-side
+  rate with inputs resident in HBM);
 * latency: per-call wall time of ks_schedule (compile + upload + run +
   results) for 1-, 16- and 256-pod batches (p50 / p99), next to the
   reference's ScheduleOne latency (~560 us per pod per shard, README.adoc:786);
@@ -109,7 +110,8 @@ def parse():
                     help="batch: one batch of --batch pods per step; c5: one burst + its event log per step")
     ap.add_argument("--burst", type=int, default=100_000, help="pods per burst (--workload c5)")
     ap.add_argument("--prefill", type=float, default=None, help="max prefill fraction (default 0.5, kwok 0)")
-    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (compile + H2D + run + D2H) pass")
+    ap.add_argument("--no-resident", action="store_true",
+                    help="skip the secondary inputs-resident pass (batches compiled + uploaded before timing)")
     ap.add_argument("--latency-calls", type=int, default=100, help="ks_schedule calls per latency batch size (0: skip)")
     ap.add_argument("--cpu-pods", type=int, default=24, help="oracle sample (pods), single thread")
     ap.add_argument("--cpu-pods-mt", type=int, default=400, help="oracle sample (pods), multi-thread")
@@ -224,7 +226,6 @@ def pod_stream(args, kind, n, seed):
 
 def run_batches(args, kind, sched, world, rank, t_setup):
     from ksched import synth
-    from ksched.framework import results_to_arrays
 
     nodes = synth.nodes(kind, args.nodes, 1)
     slots = synth.slot_array(args.nodes)
@@ -234,51 +235,32 @@ def run_batches(args, kind, sched, world, rank, t_setup):
         pre = synth.prefill(kind, args.nodes, 1, 3, args.prefill)
         assert sched.lib.ks_pods_add(sched.ctx, pre.pods, pre.slot_ptr, pre.n_pods) == 0, \
             sched.lib.ks_last_error(sched.ctx)
-    n_batches = args.warmup + args.steps
-    pods = pod_stream(args, kind, n_batches * args.batch, 2)
-    t0 = time.perf_counter()
-    batches = [sched.prepare(pods.pods_at(b * args.batch), args.batch) for b in range(n_batches)]
-    prepare_s = time.perf_counter() - t0
-    setup_s = time.time() - t_setup
 
     def barrier():
         if world > 1:
             sched.allreduce_max([0.0])  # RCCL all-reduce on the scheduler's stream
 
-    for b in range(args.warmup):
-        sched.run(batches[b])
-    sched.reset_stats()
-    sched.set_timing(True)
-    barrier()
-    t0 = time.perf_counter()
-    for b in range(args.warmup, n_batches):
-        sched.run(batches[b])  # returns after hipStreamSynchronize on the scheduler stream
-    barrier()
-    elapsed = time.perf_counter() - t0
-    sched.set_timing(False)
-    if world > 1:
-        elapsed = sched.allreduce_max([elapsed])[0]
+    setup_s = time.time() - t_setup
+    # the headline: every step through the whole boundary (compile + H2D +
+    # run + D2H), W untimed steps first
+    e2e = end_to_end(args, kind, sched, world, barrier)
     st = sched.stats()
     dbg = (C.c_uint64 * 16)()
     sched.lib.ks_debug_counters(sched.ctx, dbg)
-    scheduled = 0
-    for b in range(args.warmup, n_batches):
-        r = results_to_arrays(sched.results(batches[b], args.batch), args.batch)
-        scheduled += int((r["status"] == 0).sum())
-    for b in batches:
-        sched.free(b)
-    pods_timed = args.steps * args.batch
-
-    e2e = None if args.no_e2e else end_to_end(args, kind, sched, world, barrier)
+    # secondary: the same number of steps with every batch compiled and
+    # uploaded before the timed region (inputs resident in HBM)
+    res = None if args.no_resident else resident(args, kind, sched, world, barrier)
     lat = latency(args, kind, sched, world) if args.latency_calls > 0 else None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_pods > 0:
-        cpu = cpu_baseline(args, nodes, slots, pre, pods)
-    line = report(args, sched, st, dbg, world, pods_timed, elapsed, scheduled, setup_s, cpu)
-    line["extra"]["prepare_us_per_pod"] = round(1e6 * prepare_s / (n_batches * args.batch), 3)
-    if e2e:
-        line["value_end_to_end"] = e2e.pop("value")
-        line["end_to_end"] = e2e
+        cpu = cpu_baseline(args, nodes, slots, pre, pod_stream(args, kind, args.cpu_pods_mt + args.cpu_pods, 7))
+    line = report(args, sched, st, dbg, world, e2e.pop("pods_timed"), e2e.pop("elapsed"), e2e.pop("scheduled"),
+                  setup_s, cpu)
+    line["extra"]["host_compile_ms_per_step"] = e2e["host_compile_ms_per_step"]
+    line["end_to_end"] = e2e
+    if res:
+        line["value_inputs_resident"] = res.pop("value")
+        line["inputs_resident"] = res
     if lat:
         line["latency"] = lat
     sched.close()
@@ -287,41 +269,83 @@ def run_batches(args, kind, sched, world, rank, t_setup):
 
 
 def end_to_end(args, kind, sched, world, barrier):
-    """The timed steps again through the whole boundary: compile + H2D
-    (ks_batch_prepare), run, D2H (the run copies results into the batch's
-    pinned buffer; ks_batch_results reads them), with batch k+1 compiled on
-    the host while batch k runs (ks_batch_submit / ks_batch_wait)."""
-    n = args.steps
-    pods = pod_stream(args, kind, n * args.batch, 7)
-    lib, ctx = sched.lib, sched.ctx
+    """The headline steps: each batch goes through the whole boundary a cgo
+    caller uses -- ks_batch_prepare (pod compile + H2D), ks_batch_submit /
+    ks_batch_wait (every round + D2H of the results), ks_batch_results -- with
+    batch k+1 compiled on the host while batch k runs.  W untimed steps, then
+    K timed steps between barriers (fresh pods, seed 7, against the live
+    cluster); HIP-event timing of the kernels covers the timed steps."""
     from ksched import _abi
+    from ksched.framework import results_to_arrays
 
+    w, n = args.warmup, args.steps
+    pods = pod_stream(args, kind, (w + n) * args.batch, 7)
+    lib, ctx = sched.lib, sched.ctx
     out = (_abi.KsResult * args.batch)()
+    scheduled = 0
+
+    def run(k0, k1, timed):
+        nonlocal scheduled
+        compile_s = 0.0
+        cur = sched.prepare(pods.pods_at(k0 * args.batch), args.batch)
+        assert lib.ks_batch_submit(ctx, cur) == 0
+        for k in range(k0, k1):
+            nxt = None
+            if k + 1 < k1:
+                tc = time.perf_counter()
+                nxt = sched.prepare(pods.pods_at((k + 1) * args.batch), args.batch)
+                compile_s += time.perf_counter() - tc
+                assert lib.ks_batch_submit(ctx, nxt) == 0
+            assert lib.ks_batch_wait(ctx, cur) == 0, lib.ks_last_error(ctx)
+            assert lib.ks_batch_results(ctx, cur, out) == 0
+            if timed:
+                scheduled += int((results_to_arrays(out, args.batch)["status"] == 0).sum())
+            sched.free(cur)
+            cur = nxt
+        return compile_s
+
+    if w:
+        run(0, w, False)
+    sched.reset_stats()
+    sched.set_timing(True)
     barrier()
     t0 = time.perf_counter()
-    cur = sched.prepare(pods.pods_at(0), args.batch)
-    assert lib.ks_batch_submit(ctx, cur) == 0
-    compile_s = 0.0
-    for k in range(n):
-        nxt = None
-        if k + 1 < n:
-            tc = time.perf_counter()
-            nxt = sched.prepare(pods.pods_at((k + 1) * args.batch), args.batch)
-            compile_s += time.perf_counter() - tc
-            assert lib.ks_batch_submit(ctx, nxt) == 0
-        assert lib.ks_batch_wait(ctx, cur) == 0, lib.ks_last_error(ctx)
-        assert lib.ks_batch_results(ctx, cur, out) == 0
-        sched.free(cur)
-        cur = nxt
+    compile_s = run(w, w + n, True)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    sched.set_timing(False)
+    if world > 1:
+        elapsed = sched.allreduce_max([elapsed])[0]
+    return {"pods_timed": n * args.batch, "elapsed": elapsed, "scheduled": scheduled,
+            "host_compile_ms_per_step": round(1e3 * compile_s / max(1, n - 1), 3),
+            "what": "value: ks_batch_prepare (compile + H2D) + ks_batch_submit/wait (run + D2H) + "
+                    "ks_batch_results per step, batch k+1 compiled while batch k runs; fresh pods (seed 7)"}
+
+
+def resident(args, kind, sched, world, barrier):
+    """The same step count with every batch compiled and uploaded before the
+    timed region (ks_batch_prepare ahead, ks_batch_run timed): the device-side
+    rate with inputs resident in HBM."""
+    n = args.steps
+    pods = pod_stream(args, kind, n * args.batch, 2)
+    t0 = time.perf_counter()
+    batches = [sched.prepare(pods.pods_at(b * args.batch), args.batch) for b in range(n)]
+    prepare_s = time.perf_counter() - t0
+    barrier()
+    t0 = time.perf_counter()
+    for b in batches:
+        sched.run(b)
     barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
         elapsed = sched.allreduce_max([elapsed])[0]
+    for b in batches:
+        sched.free(b)
     return {"value": round(n * args.batch / elapsed, 1), "unit": "pods/s", "steps": n,
             "ms_per_step": round(1e3 * elapsed / n, 3),
-            "host_compile_ms_per_step": round(1e3 * compile_s / max(1, n - 1), 3),
-            "what": "ks_batch_prepare (compile + H2D) + ks_batch_submit/wait (run + D2H) + ks_batch_results, "
-                    "batch k+1 compiled while batch k runs; fresh pods (seed 7) against the live cluster"}
+            "prepare_us_per_pod": round(1e6 * prepare_s / (n * args.batch), 3),
+            "what": "ks_batch_run only: every batch compiled + uploaded by ks_batch_prepare before the timed "
+                    "region; pods seed 2, after the headline steps"}
 
 
 def latency(args, kind, sched, world):

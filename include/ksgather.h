@@ -29,16 +29,25 @@ extern "C" {
 typedef struct ksg_evaluator ksg_evaluator;
 
 /* Ties at the highest score: the reference picks uniformly at random among
- * the first 100 tied scores in arrival order (rand.Intn); the deterministic
- * mode picks the lexicographically smallest node name among them. */
-enum { KSG_TIE_RANDOM = 0, KSG_TIE_LOWEST_NAME = 1 };
+ * the first 100 tied scores in arrival order (rand.Intn).  The deterministic
+ * modes pick among them the lexicographically smallest node name, or the
+ * lowest global node index of ksg_set_node_order -- the rule every host
+ * applies to its own nodes (lowest slot), so a multi-host run ends as one
+ * unsharded scheduler would. */
+enum { KSG_TIE_RANDOM = 0, KSG_TIE_LOWEST_NAME = 1, KSG_TIE_LOWEST_INDEX = 2 };
 
 /* members: scores that complete a pod (SchedulerSet.GetMemberCountNoRelays,
  * read when a pod's first score arrives); delay_ms: how long a pod waits for
  * missing members after its first score (the reference: 5 s,
  * grpc_server.go:135).  NULL on bad arguments. */
 ksg_evaluator *ksg_open(uint32_t members, uint32_t delay_ms, int32_t tie_mode, uint64_t seed);
+/* Fires every pending evaluation (its waiters return with the scores recorded
+ * so far), wakes ksg_next_fired, waits until no thread is inside a call on
+ * `ev`, then frees it.  Calls arriving after it started return -1. */
 void ksg_close(ksg_evaluator *ev);
+/* KSG_TIE_LOWEST_INDEX: names[i] is the node of global index i (the hosts'
+ * node slots laid end to end); a name not listed sorts after every listed one. */
+void ksg_set_node_order(ksg_evaluator *ev, const char *const *names, uint32_t n);
 /* Membership changed (relay tree): applies to pods whose first score arrives later. */
 void ksg_set_members(ksg_evaluator *ev, uint32_t members);
 
@@ -51,6 +60,19 @@ void ksg_set_members(ksg_evaluator *ev, uint32_t members);
  * won (the CollectScore permit), 0 when it did not, -1 on bad arguments. */
 int32_t ksg_record_and_wait(ksg_evaluator *ev, const char *key, const char *node_name, int32_t score,
                             char *winner, uint32_t winner_cap, int32_t *winner_score);
+
+/* Non-blocking form for event-driven servers: record the score; returns 1 / 0
+ * (permit or not) when this score fired the evaluation, 2 when it is still
+ * pending (*eval_id names the evaluation; ksg_next_fired reports it once it
+ * fires), -1 on bad arguments or after ksg_close began. */
+int32_t ksg_record(ksg_evaluator *ev, const char *key, const char *node_name, int32_t score, uint64_t *eval_id,
+                   char *winner, uint32_t winner_cap, int32_t *winner_score);
+/* Wait up to timeout_ms for the next fired evaluation that has ksg_record
+ * callers pending (firing evaluations whose delay expired meanwhile): 1 with
+ * *eval_id and its winner, 0 on timeout, -1 once ksg_close began and nothing
+ * is left to report.  One thread drives it for a whole server. */
+int32_t ksg_next_fired(ksg_evaluator *ev, uint32_t timeout_ms, uint64_t *eval_id, char *winner, uint32_t winner_cap,
+                       int32_t *winner_score);
 
 /* Pods recorded and not fired yet (diagnostics / tests). */
 uint32_t ksg_pending(ksg_evaluator *ev);

@@ -363,6 +363,10 @@ struct ks_ctx {
   uint32_t timing_every = 8, sweep_blocks = 8192, ext_npl = 2;
   // KS_EVENT_PROFILE=1: per event kind, runs / events / seconds of ks_events_apply (stderr at ks_close)
   bool ev_profile = false;
+  // KS_RUN_PROFILE=1: seconds per phase of the batch runs (stderr at ks_close):
+  // [0] waiting for `mu` at run start, [1] enqueueing rounds, [2] drains, [3] runs
+  bool run_profile = false;
+  double prof[4] = {0, 0, 0, 0};
   struct EvProf {
     uint64_t runs = 0, events = 0;
     double s = 0;
@@ -374,6 +378,7 @@ struct ks_ctx {
   std::vector<uint32_t> slot_pos;
   // device state
   NodeTable t{};
+  NodeTable run_t{};  // t as the running batch's rounds see it (run_batch)
   Shard *d_shards = nullptr;
   uint32_t *d_slot_pos = nullptr;
   uint32_t *d_start = nullptr;
@@ -2561,10 +2566,7 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k, uint32_t end) {
   groups = (c->P + pg - 1) / pg;
 
   RoundArgs a{};
-  {
-    std::lock_guard<std::mutex> g(c->mu);  // ks_batch_prepare may widen t.lw concurrently
-    a.t = c->t;
-  }
+  a.t = c->run_t;  // the table as this run sees it (run_batch), no lock per round
   a.shards = c->d_shards;
   a.total_shards = c->S;
   a.shard0 = shard0;
@@ -2807,20 +2809,21 @@ ks_status run_batch(ks_ctx *c, ks_batch *b) {
     return c->fail(KS_ERR_INVALID, "RCCL sharding needs one shard per rank (virtual_shards must be 1)");
   HIPC(c, hipSetDevice(c->cfg.device));
   ks_status st0;
-  {
-    // label words of nodes that gained dictionary bits since the last upload
-    // (bits of this batch or a later-prepared one: a superset is harmless)
-    std::lock_guard<std::mutex> g(c->mu);
-    if ((st0 = upload_dirty_ext(c, c->xm))) return st0;
-  }
-  if (!b->uploaded && (st0 = upload_batch(c, b))) return st0;
-  if (b->any_spread && c->has_comm())
-    return c->fail(KS_ERR_UNSUPPORTED, "topology spread pods need a single-rank context");
-  // Selector classes each pod matches, against the classes live now: the
-  // spread path's commits and the round kernels' (class_commit) count them.
+  // One critical section (a second one let the next batch's compile, which
+  // holds `mu` for milliseconds, stall this run between the two):
+  //  * label words of nodes that gained dictionary bits since the last upload
+  //    (bits of this batch or a later-prepared one: a superset is harmless);
+  //  * the table as the rounds read it (ks_batch_prepare of the next batch may
+  //    widen t.lw meanwhile: its label words are uploaded by its own run);
+  //  * the selector classes each pod matches, against the classes live now:
+  //    the spread path's commits and the round kernels' (class_commit) count them.
   bool classes = false;
   {
+    const auto tw = std::chrono::steady_clock::now();
     std::lock_guard<std::mutex> g(c->mu);
+    if (c->run_profile) c->prof[0] += std::chrono::duration<double>(std::chrono::steady_clock::now() - tw).count();
+    if ((st0 = upload_dirty_ext(c, c->xm))) return st0;
+    c->run_t = c->t;
     for (int k = 0; k < MAX_CLASSES; ++k) classes |= c->classes[k].live;
     if (classes || b->any_spread) {
       std::vector<int32_t> memo(c->label_sets.size(), -1);  // set -> first pod index with it
@@ -2838,6 +2841,9 @@ ks_status run_batch(ks_ctx *c, ks_batch *b) {
       }
     }
   }
+  if (!b->uploaded && (st0 = upload_batch(c, b))) return st0;
+  if (b->any_spread && c->has_comm())
+    return c->fail(KS_ERR_UNSUPPORTED, "topology spread pods need a single-rank context");
   if (classes || b->any_spread)
     HIPC(c, hipMemcpyAsync(b->d_cmask, b->h_cmask, (size_t)std::max<uint32_t>(b->n, 1) * 8 * CMASK_WORDS, hipMemcpyHostToDevice,
                            c->stream));
@@ -2908,15 +2914,21 @@ ks_status run_batch(ks_ctx *c, ks_batch *b) {
         // and check; each pipeline run resolves at least one pod.
         uint32_t rounds = (hi - host_start + c->P - 1) / c->P;
         rounds = std::min<uint32_t>(rounds, 64);
+        const auto te = std::chrono::steady_clock::now();
         for (uint32_t r = 0; r < rounds; ++r) {
           ks_status st = enqueue_round(c, b, r, hi);
           if (st) return st;
         }
+        const auto td = std::chrono::steady_clock::now();
         // results of every pod this pipeline run can resolve, behind its last round
         const uint32_t top = std::min<uint32_t>(hi, host_start + rounds * c->P);
         ks_status st = drain_rounds(c, rounds, b->h_results + host_start, b->d_results + host_start,
                                     (size_t)(top - host_start) * sizeof(DevResult));
         if (st) return st;
+        if (c->run_profile) {
+          c->prof[1] += std::chrono::duration<double>(td - te).count();
+          c->prof[2] += std::chrono::duration<double>(std::chrono::steady_clock::now() - td).count();
+        }
         if (*c->h_start <= host_start) return c->fail(KS_ERR_DEVICE, "no progress in scheduling rounds");
         host_start = *c->h_start;
       }
@@ -2944,6 +2956,7 @@ ks_status run_batch(ks_ctx *c, ks_batch *b) {
     ks_status st = collect_timing(c);
     if (st) return st;
   }
+  c->prof[3] += 1;
   return KS_OK;
 }
 
@@ -3048,6 +3061,7 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
     x->early_fix = env_u("KS_EARLY_FIX", 1) != 0;
     x->tuple_guess = env_u("KS_TUPLE_GUESS", 1) != 0;
     x->ev_profile = env_u("KS_EVENT_PROFILE", 0) != 0;
+    x->run_profile = env_u("KS_RUN_PROFILE", 0) != 0;
     x->timing_every = (uint32_t)std::max(1, env_u("KS_TIMING_EVERY", 8));
     x->sweep_blocks = (uint32_t)std::max(1, env_u("KS_SWEEP_BLOCKS", 8192));
     const int en = env_u("KS_EXT_NPL", 2);  // geometry experiments only
@@ -3168,6 +3182,9 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
 
 void ks_close(ks_ctx *c) {
   if (!c) return;
+  if (c->run_profile)
+    std::fprintf(stderr, "ksched runs: %.0f %s: lock wait %.3f s, enqueue %.3f s, drains %.3f s\n", c->prof[3],
+                 "runs", c->prof[0], c->prof[1], c->prof[2]);
   if (c->ev_profile)
     for (int k = 0; k < 4; ++k)
       std::fprintf(stderr, "ksched events kind %d: %llu runs, %llu events, %.3f s\n", k,
@@ -3426,6 +3443,16 @@ ks_status ks_nodes_delete(ks_ctx *c, const uint32_t *slots, uint32_t n) {
   if (ks_status dst_ = drain_async(c)) return dst_;
   c->tuple_version++;
   HIPC(c, hipSetDevice(c->cfg.device));
+  // every slot is checked before anything changes: a missing or repeated
+  // slot fails the call with the host mirror and the device table untouched
+  {
+    std::unordered_set<uint32_t> seen;
+    for (uint32_t i = 0; i < n; ++i) {
+      if (slots[i] >= c->cap || !c->nodes[slots[i]].present)
+        return c->fail(KS_ERR_NOT_FOUND, "slot %u not present", slots[i]);
+      if (!seen.insert(slots[i]).second) return c->fail(KS_ERR_INVALID, "slot %u deleted twice in one call", slots[i]);
+    }
+  }
   // the deleted nodes' records go with them: replayed now when term counts
   // need them, else a clear entry in the log
   const bool unread = pod_records_unread(c);
@@ -3433,8 +3460,6 @@ ks_status ks_nodes_delete(ks_ctx *c, const uint32_t *slots, uint32_t n) {
   std::vector<uint32_t> pos(n);
   std::vector<int64_t> core((size_t)n * 8, 0);
   for (uint32_t i = 0; i < n; ++i) {
-    if (slots[i] >= c->cap || !c->nodes[slots[i]].present)
-      return c->fail(KS_ERR_NOT_FOUND, "slot %u not present", slots[i]);
     HostNode &h = c->nodes[slots[i]];
     if (unread) c->pending_bound.push_back({slots[i], 0u, 0});
     for (uint32_t set : h.pod_sets)
@@ -3581,12 +3606,20 @@ ks_status ks_snapshot_update(ks_ctx *c, const ks_node_info *items, uint32_t n, i
     }
   }
   ks_status st;
-  if (!del.empty() && (st = ks_nodes_delete(c, del.data(), (uint32_t)del.size()))) return st;
-  if (!up.empty() && (st = ks_nodes_upsert(c, up.data(), up_slots.data(), (uint32_t)up.size()))) return st;
-  for (uint32_t i : order) {
-    c->slot_gen[items[i].slot] = items[i].generation;
-    c->snapshot_gen = std::max(c->snapshot_gen, items[i].generation);
+  auto record = [&](bool deleted) {
+    for (uint32_t i : order)
+      if ((items[i].deleted != 0) == deleted) {
+        c->slot_gen[items[i].slot] = items[i].generation;
+        c->snapshot_gen = std::max(c->snapshot_gen, items[i].generation);
+      }
+  };
+  if (!del.empty() && (st = ks_nodes_delete(c, del.data(), (uint32_t)del.size()))) return st;  // nothing changed
+  record(true);  // the deletions are in: a failing upsert below leaves them recorded (a retry skips them)
+  if (!up.empty() && (st = ks_nodes_upsert(c, up.data(), up_slots.data(), (uint32_t)up.size()))) {
+    std::string e = ks_last_error(c);
+    return c->fail(st, "%s (the call's %zu deletions were applied)", e.c_str(), del.size());
   }
+  record(false);
   if (generation) *generation = c->snapshot_gen;
   if (applied) *applied = (uint32_t)order.size();
   return KS_OK;

@@ -301,6 +301,7 @@ KSCHED_SYMBOLS = [
 ]
 KSGATHER_SYMBOLS = [
     "ksg_open", "ksg_close", "ksg_set_members", "ksg_record_and_wait", "ksg_pending", "ksg_fnv1_32", "ksg_target_index",
+    "ksg_record", "ksg_next_fired", "ksg_set_node_order",
 ]
 KSYNTH_SYMBOLS = [
     "ksynth_nodes", "ksynth_pods", "ksynth_prefill", "ksynth_besteffort_pods", "ksynth_spread_pods", "ksynth_affinity_pods", "ksynth_node_array",
@@ -432,6 +433,13 @@ def ksgather_lib() -> C.CDLL:
     L.ksg_set_members.restype = None
     L.ksg_record_and_wait.argtypes = [vp, C.c_char_p, C.c_char_p, C.c_int32, C.c_char_p, C.c_uint32, P(C.c_int32)]
     L.ksg_record_and_wait.restype = C.c_int32
+    L.ksg_record.argtypes = [vp, C.c_char_p, C.c_char_p, C.c_int32, P(C.c_uint64), C.c_char_p, C.c_uint32,
+                             P(C.c_int32)]
+    L.ksg_record.restype = C.c_int32
+    L.ksg_next_fired.argtypes = [vp, C.c_uint32, P(C.c_uint64), C.c_char_p, C.c_uint32, P(C.c_int32)]
+    L.ksg_next_fired.restype = C.c_int32
+    L.ksg_set_node_order.argtypes = [vp, P(C.c_char_p), C.c_uint32]
+    L.ksg_set_node_order.restype = None
     L.ksg_pending.argtypes = [vp]
     L.ksg_pending.restype = C.c_uint32
     L.ksg_fnv1_32.argtypes = [C.c_char_p, C.c_uint32]

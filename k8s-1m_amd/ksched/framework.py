@@ -146,6 +146,7 @@ class Scheduler:
             raise _abi.KschedError(st, "ks_open failed (no usable HIP device?)")
         self.names: Dict[int, str] = {}
         self.slots: Dict[str, int] = {}
+        self.slot_gen: Dict[int, int] = {}  # last NodeInfo.Generation applied per slot (snapshot_update)
 
     # ------------------------------------------------------------ lifecycle
     def close(self):
@@ -186,7 +187,13 @@ class Scheduler:
 
     def snapshot_update(self, items):
         """Cache.UpdateSnapshot: items = [(slot, generation, Node or None for
-        RemoveNode)]; returns (snapshot generation, items applied)."""
+        RemoveNode)]; returns (snapshot generation, items applied).
+
+        The slot -> name mirror follows what ks_snapshot_update applies, not
+        every item it is handed: per slot only the highest generation above
+        the slot's last applied one counts (stale or replayed items are
+        skipped), deletions go first, and an upsert that renames a slot drops
+        the old name's reverse entry."""
         a = Arena()
         live = [(sl, g, nd) for sl, g, nd in items]
         arr, _ = nodes_array([nd for _, _, nd in live if nd is not None], a) if any(
@@ -200,18 +207,41 @@ class Scheduler:
             else:
                 infos[i].node = C.pointer(arr[k])
                 k += 1
+        # the items the library will apply (its filter, restated)
+        best: Dict[int, int] = {}
+        for i, (sl, g, nd) in enumerate(live):
+            if g <= self.slot_gen.get(sl, -(1 << 63)):
+                continue
+            if sl not in best or live[best[sl]][1] < g:
+                best[sl] = i
+        order = sorted(best.values())
         gen, applied = C.c_int64(), C.c_uint32()
-        self._ok(self.lib.ks_snapshot_update(self.ctx, infos, len(live), C.byref(gen), C.byref(applied)))
-        for sl, g, nd in live:
+        try:
+            self._ok(self.lib.ks_snapshot_update(self.ctx, infos, len(live), C.byref(gen), C.byref(applied)))
+        except _abi.KschedError as e:
+            if "deletions were applied" in str(e):  # the upserts failed after the deletions went in
+                self._mirror_snapshot([i for i in order if live[i][2] is None], live)
+            raise
+        self._mirror_snapshot(order, live)
+        return gen.value, applied.value
+
+    def _mirror_snapshot(self, order, live):
+        for i in order:  # deletions first, as the library applies them
+            sl, g, nd = live[i]
             if nd is None:
                 old = self.names.pop(sl, None)
                 if old is not None and self.slots.get(old) == sl:
                     self.slots.pop(old, None)
-        for sl, g, nd in live:
+        for i in order:
+            sl, g, nd = live[i]
             if nd is not None:
+                old = self.names.get(sl)
+                if old is not None and old != nd.name and self.slots.get(old) == sl:
+                    self.slots.pop(old, None)
                 self.names[sl] = nd.name
                 self.slots[nd.name] = sl
-        return gen.value, applied.value
+        for i in order:
+            self.slot_gen[live[i][0]] = live[i][1]
 
     def delete_nodes(self, names: Sequence[str]):
         slots = [self.slots[n] for n in names]

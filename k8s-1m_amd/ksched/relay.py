@@ -18,10 +18,10 @@ this path.
 """
 from __future__ import annotations
 
+import asyncio
 import ctypes as C
 import threading
-from concurrent import futures
-from typing import Optional, Sequence, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import grpc
 from google.protobuf import descriptor_pb2, descriptor_pool, message_factory
@@ -32,7 +32,7 @@ SERVICE = "podservice.PodService"
 COLLECT_SCORE = f"/{SERVICE}/CollectScore"
 GRPC_PORT = 50051  # distpermit.go:87 (the reference hard-codes it)
 SCORE_DELAY_S = 5.0  # grpc_server.go:135
-TIE_RANDOM, TIE_LOWEST_NAME = 0, 1
+TIE_RANDOM, TIE_LOWEST_NAME, TIE_LOWEST_INDEX = 0, 1, 2  # include/ksgather.h
 
 
 def _messages():
@@ -76,6 +76,36 @@ class ScoreEvaluator:
     def set_members(self, members: int):
         self.lib.ksg_set_members(self.h, members)
 
+    def set_node_order(self, names: Sequence[str]):
+        """TIE_LOWEST_INDEX: names[i] is global node index i (the hosts' slots end to end)."""
+        arr = (C.c_char_p * max(1, len(names)))(*[n.encode() for n in names])
+        self.lib.ksg_set_node_order(self.h, arr, len(names))
+
+    def record(self, key: str, node_name: str, score: int):
+        """Non-blocking record: (True/False, winner, score) when this score fired
+        the evaluation, else ("pending", evaluation id)."""
+        buf = C.create_string_buffer(512)
+        ws, eid = C.c_int32(), C.c_uint64()
+        r = self.lib.ksg_record(self.h, key.encode(), node_name.encode(), int(score), C.byref(eid), buf, 512,
+                                C.byref(ws))
+        if r < 0:
+            raise ValueError("ksg_record: bad arguments or closed")
+        if r == 2:
+            return "pending", eid.value
+        return r == 1, buf.value.decode(), ws.value
+
+    def next_fired(self, timeout_ms: int):
+        """(evaluation id, winner, score) of the next evaluation with pending
+        records that fired, None on timeout, False once closed."""
+        buf = C.create_string_buffer(512)
+        eid, ws = C.c_uint64(), C.c_int32()
+        r = self.lib.ksg_next_fired(self.h, timeout_ms, C.byref(eid), buf, 512, C.byref(ws))
+        if r < 0:
+            return False
+        if r == 0:
+            return None
+        return eid.value, buf.value.decode(), ws.value
+
     def record_and_wait(self, key: str, node_name: str, score: int) -> Tuple[bool, str, int]:
         """Blocks (without the GIL) until the pod fires; (permit, winner, winner score)."""
         buf = C.create_string_buffer(512)
@@ -102,28 +132,84 @@ def target_index(key: str, members: Sequence[str], leader: Optional[str] = None)
 
 
 class CollectScoreServer:
-    """The gatherer side: a gRPC server exposing PodService.CollectScore."""
+    """The gatherer side: PodService.CollectScore on a grpc.aio server.
 
-    def __init__(self, evaluator: ScoreEvaluator, address: str = "127.0.0.1:0", workers: int = 64):
+    A CollectScore RPC records its score without blocking (ksg_record); the
+    RPCs of a pod that is still collecting park on asyncio futures, and ONE
+    thread (ksg_next_fired) reports every evaluation that fires -- all members
+    in, or its delay expired -- to the event loop, which answers each parked
+    sender.  In-flight pods are therefore not bounded by a thread pool (the
+    reference runs one goroutine per RPC, grpc_server.go:116-127)."""
+
+    def __init__(self, evaluator: ScoreEvaluator, address: str = "127.0.0.1:0", workers: Optional[int] = None):
+        del workers  # no per-RPC threads (kept for callers of the former thread-pool server)
         self.evaluator = evaluator
-        self.server = grpc.server(futures.ThreadPoolExecutor(max_workers=workers))
+        self._bind = address
+        self._waiting: Dict[int, List[Tuple[str, asyncio.Future]]] = {}
+        self._loop = asyncio.new_event_loop()
+        self._ready = threading.Event()
+        self._stopped = threading.Event()
+        self._thread = threading.Thread(target=self._serve, name="collect-score", daemon=True)
+        self._fired = threading.Thread(target=self._fired_loop, name="collect-score-fired", daemon=True)
+        self.port = 0
+        self.address = ""
+
+    # -- event loop thread
+    def _serve(self):
+        asyncio.set_event_loop(self._loop)
+        self._loop.run_until_complete(self._start())
+        self._ready.set()
+        self._loop.run_forever()
+
+    async def _start(self):
+        self.server = grpc.aio.server()
         handler = grpc.unary_unary_rpc_method_handler(
             self._collect, request_deserializer=SchedulingScore.FromString,
             response_serializer=ScheduleResponse.SerializeToString)
         self.server.add_generic_rpc_handlers((grpc.method_handlers_generic_handler(SERVICE, {"CollectScore": handler}),))
-        self.port = self.server.add_insecure_port(address)
-        self.address = f"{address.rsplit(':', 1)[0]}:{self.port}"
+        self.port = self.server.add_insecure_port(self._bind)
+        self.address = f"{self._bind.rsplit(':', 1)[0]}:{self.port}"
+        await self.server.start()
 
-    def _collect(self, req, context):
-        permit, _, _ = self.evaluator.record_and_wait(f"{req.namespace}/{req.podName}", req.nodeName, req.score)
-        return ScheduleResponse(permit=permit)
+    async def _collect(self, req, context):
+        r = self.evaluator.record(f"{req.namespace}/{req.podName}", req.nodeName, req.score)
+        if r[0] != "pending":
+            return ScheduleResponse(permit=r[0])
+        fut = self._loop.create_future()  # registered before the loop can run the fire report
+        self._waiting.setdefault(r[1], []).append((req.nodeName, fut))
+        return ScheduleResponse(permit=await fut)
+
+    def _resolve(self, eval_id: int, winner: str):
+        for node, fut in self._waiting.pop(eval_id, []):
+            if not fut.done():
+                fut.set_result(node == winner)
+
+    # -- the one thread that waits for evaluations to fire
+    def _fired_loop(self):
+        while not self._stopped.is_set():
+            r = self.evaluator.next_fired(200)
+            if r is False:
+                break
+            if r:
+                self._loop.call_soon_threadsafe(self._resolve, r[0], r[1])
 
     def start(self):
-        self.server.start()
+        self._thread.start()
+        self._ready.wait(30)
+        self._fired.start()
         return self
 
     def stop(self):
-        self.server.stop(grace=None)
+        """Stops serving; RPCs still parked are answered by the evaluator's
+        close (ScoreEvaluator.close fires every pending pod)."""
+        self._stopped.set()
+        fut = asyncio.run_coroutine_threadsafe(self.server.stop(grace=None), self._loop)
+        try:
+            fut.result(30)
+        finally:
+            self._loop.call_soon_threadsafe(self._loop.stop)
+            self._thread.join(30)
+            self._fired.join(30)
 
 
 class ScoreClient:

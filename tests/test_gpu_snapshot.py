@@ -115,3 +115,51 @@ def test_snapshot_rejects_bad_items_without_change():
     assert (g.value, a.value) == (6, 2)
     assert s.node_states([3])[0].pod_count == 0 and s.node_states([3])[0].alloc_pods > 0
     s.close()
+
+
+def test_scheduler_snapshot_mirror_follows_applied_items():
+    # Scheduler.snapshot_update (the framework wrapper): shuffled NodeInfo lists
+    # with stale replays, renames and tombstones; the slot <-> name mirror must
+    # follow what the library applied, so results name the right node
+    from ksched import Node, Pod
+    from ksched.objects import Container
+
+    n = 40
+    rng = random.Random(11)
+    s = Scheduler(n)
+    gen = 0
+    cache = {}    # slot -> (generation, version or None)
+    history = []  # every published (slot, generation, version)
+
+    def node(slot, ver):
+        return Node(f"node-{slot}-v{ver}", {"cpu": 4000 + 1000 * ver, "memory": 8 << 30, "pods": 110})
+
+    def publish(slot, ver):
+        nonlocal gen
+        gen += 1
+        cache[slot] = (gen, ver)
+        history.append((slot, gen, ver))
+
+    for slot in range(n):
+        publish(slot, 0)
+    try:
+        for cycle in range(8):
+            if cycle:
+                for slot in rng.sample(range(n), 12):
+                    g0, v0 = cache[slot]
+                    publish(slot, None if (v0 is not None and rng.random() < 0.3) else rng.randrange(1, 50))
+            items = [(sl, g, v) for sl, (g, v) in cache.items()] + rng.sample(history, min(len(history), 30))
+            rng.shuffle(items)
+            s.snapshot_update([(sl, g, None if v is None else node(sl, v)) for sl, g, v in items])
+            want = {sl: f"node-{sl}-v{v}" for sl, (g, v) in cache.items() if v is not None}
+            assert s.names == want, f"cycle {cycle}: slot -> name mirror"
+            assert s.slots == {nm: sl for sl, nm in want.items()}, f"cycle {cycle}: name -> slot mirror"
+            # a pod only the largest live node fits reports that node's name
+            big = max(want, key=lambda sl: (cache[sl][1], -sl))
+            cpu = 4000 + 1000 * cache[big][1] - 1
+            if sum(1 for sl in want if cache[sl][1] == cache[big][1]) == 1:
+                res = s.schedule_pods([Pod(f"p{cycle}", containers=[Container({"cpu": cpu, "memory": 1 << 20})])])[0]
+                assert res.suggested_host == want[big], (cycle, res, want[big])
+                s.remove_pods([Pod(f"p{cycle}", containers=[Container({"cpu": cpu, "memory": 1 << 20})])], [big])
+    finally:
+        s.close()

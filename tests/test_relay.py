@@ -119,10 +119,13 @@ def test_collect_score_over_grpc():
         ev.close()
 
 
-@pytest.mark.parametrize("pods", [50])
+@pytest.mark.parametrize("pods", [50, 200])
 def test_many_pods_concurrently(pods):
+    # the default server: far more pods in flight than the former thread pool's
+    # 64 workers, none of them waiting for the 20-s delay
     ev = relay.ScoreEvaluator(members=2, delay_s=20, tie=relay.TIE_LOWEST_NAME)
-    srv = relay.CollectScoreServer(ev, workers=4 * pods).start()
+    srv = relay.CollectScoreServer(ev).start()
+    t0 = time.time()
     try:
         cli = relay.ScoreClient(srv.address)
         fns = []
@@ -135,6 +138,55 @@ def test_many_pods_concurrently(pods):
             assert a + b == 1
             assert a == (100 + p % 3 >= 101)  # ties: the lowest name (a...) wins
         assert ev.pending() == 0
+        assert time.time() - t0 < 15, "pods waited for the delay: RPCs were queued"
     finally:
         srv.stop()
         ev.close()
+
+
+def test_delay_fires_pending_async_records():
+    # a member never answers: the server's fired thread fires the pod at its delay
+    ev = relay.ScoreEvaluator(members=3, delay_s=0.4, tie=relay.TIE_LOWEST_NAME)
+    srv = relay.CollectScoreServer(ev).start()
+    try:
+        cli = relay.ScoreClient(srv.address)
+        t0 = time.time()
+        res = run_parallel([lambda: cli.send_score("slow", "ns", "n1", 300), lambda: cli.send_score("slow", "ns", "n2", 200)])
+        assert res == [True, False] and 0.3 <= time.time() - t0 < 5
+    finally:
+        srv.stop()
+        ev.close()
+
+
+def test_ties_lowest_global_index():
+    # KSG_TIE_LOWEST_INDEX: ties go to the lowest global node index, the rule
+    # each host applies to its own slots, whatever the names
+    ev = relay.ScoreEvaluator(members=3, delay_s=30, tie=relay.TIE_LOWEST_INDEX)
+    ev.set_node_order(["zz-node", "mm-node", "aa-node"])
+    res = run_parallel([lambda n=n: ev.record_and_wait("ns/i", n, 500) for n in ("aa-node", "zz-node", "mm-node")])
+    assert [r[0] for r in res] == [False, True, False]
+    res = run_parallel([lambda n=n: ev.record_and_wait("ns/j", n, 500) for n in ("unlisted", "aa-node", "b")])
+    assert [r[0] for r in res] == [False, True, False]  # listed names before unlisted ones
+    ev.close()
+
+
+def test_close_releases_waiters():
+    # ksg_close fires every pending pod and frees the evaluator only after
+    # every waiter has returned (no waiter touches freed memory)
+    ev = relay.ScoreEvaluator(members=5, delay_s=60, tie=relay.TIE_LOWEST_NAME)
+    out = []
+    th = [threading.Thread(target=lambda n=n: out.append(ev.record_and_wait("ns/c", f"n{n}", 10 + n)))
+          for n in range(3)]
+    for t in th:
+        t.start()
+    deadline = time.time() + 10
+    while ev.pending() == 0 and time.time() < deadline:
+        time.sleep(0.01)
+    time.sleep(0.1)
+    t0 = time.time()
+    ev.close()
+    for t in th:
+        t.join(5)
+    assert time.time() - t0 < 5 and len(out) == 3
+    assert sorted(o[0] for o in out) == [False, False, True]
+    assert all(o[1:] == ("n2", 12) for o in out)

@@ -4,7 +4,7 @@ export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"
 TAG=${1:-abl}
-ARGS="--kind labeled --steps 3 --warmup 1 --no-cpu-baseline --no-e2e --latency-calls 0"
+ARGS="--kind labeled --steps 3 --warmup 1 --no-cpu-baseline --no-resident --latency-calls 0"
 mkdir -p gpurun_out/$TAG
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/$TAG/trace" -o run --output-format csv -- python3 bench.py $ARGS > gpurun_out/$TAG/real.json 2> gpurun_out/$TAG/real.err || exit $?
 python3 -c "import json;d=json.load(open('gpurun_out/$TAG/real.json'));print('real', d['value'], d['roofline']['avg_launch_ms'])"

@@ -27,7 +27,7 @@ for l in $LINES; do
     spread) run spread --kind zoned --pods spread --latency-calls 0 || exit $? ;;
     affinity) run affinity --kind zoned --pods affinity --latency-calls 0 || exit $? ;;
     prof)
-      timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_$TAG" -o run --output-format csv -- python3 "$R/bench.py" --steps 4 --warmup 1 --no-cpu-baseline --no-e2e --latency-calls 0 > gpurun_out/bench_prof_$TAG.json 2> gpurun_out/prof_$TAG.err
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_$TAG" -o run --output-format csv -- python3 "$R/bench.py" --steps 4 --warmup 1 --no-cpu-baseline --no-resident --latency-calls 0 > gpurun_out/bench_prof_$TAG.json 2> gpurun_out/prof_$TAG.err
       rc=$?; echo "prof rc=$rc"; [ $rc -eq 0 ] || exit $rc ;;
   esac
 done

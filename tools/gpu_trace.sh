@@ -6,7 +6,7 @@ cd "$R"
 TAG=$1
 shift
 mkdir -p gpurun_out/$TAG
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/$TAG/trace" -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-e2e --latency-calls 0 "$@" > gpurun_out/$TAG/bench.json 2> gpurun_out/$TAG/bench.err || exit $?
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/$TAG/trace" -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-resident --latency-calls 0 "$@" > gpurun_out/$TAG/bench.json 2> gpurun_out/$TAG/bench.err || exit $?
 python3 - "$R/gpurun_out/$TAG" <<'PY'
 import csv, json, sys
 d = sys.argv[1]

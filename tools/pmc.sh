@@ -9,7 +9,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"
 TAG=${1:-r2}
 shift
-ARGS="--steps 2 --warmup 1 --no-cpu-baseline --no-e2e --latency-calls 0 $*"
+ARGS="--steps 2 --warmup 1 --no-cpu-baseline --no-resident --latency-calls 0 $*"
 # Counter collection serialises dispatches; cross-stream hand-offs by stream
 # wait-value packets then stall behind it, so the PMC runs use event waits.
 export KS_VALUE_SYNC=0

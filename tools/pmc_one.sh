@@ -8,7 +8,7 @@ TAG=$1; CTRS=$2; shift 2
 export KS_VALUE_SYNC=0
 OUT="$R/gpurun_out/$TAG"
 mkdir -p "$OUT"
-timeout -s KILL 170 rocprofv3 --pmc $CTRS -d "$OUT/p" -o run --output-format csv -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-e2e --latency-calls 0 "$@" > "$OUT/bench.json" 2> "$OUT/bench.err" || { tail -5 "$OUT/bench.err"; exit 1; }
+timeout -s KILL 170 rocprofv3 --pmc $CTRS -d "$OUT/p" -o run --output-format csv -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-resident --latency-calls 0 "$@" > "$OUT/bench.json" 2> "$OUT/bench.err" || { tail -5 "$OUT/bench.err"; exit 1; }
 python3 - "$OUT" <<'PY'
 import csv, sys, collections
 from pathlib import Path
