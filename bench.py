@@ -85,6 +85,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # mix (profiles/valu_mix.json: 4.08 cycles for the C3 kernel, 3.88 for C4's).
 SIMD_CYCLES_PER_S = 256 * 4 * 2.4e9
 VALU_CYCLES_FALLBACK = 4.0  # when valu_mix.json does not match the kernel sources
+E2E_DEPTH = 2  # batches submitted ahead in the headline loop (compile of k+1 and k+2 overlaps run k)
 REF_SCHEDULE_ONE_US = 560.0  # README.adoc:786 (per pod per shard, ~195 nodes evaluated)
 KERNEL_SOURCES = ["k8s-1m_amd/csrc/ksched_kernels.hip", "k8s-1m_amd/csrc/ksched_eval.hpp", "k8s-1m_amd/csrc/ksched_dev.hpp",
                   "k8s-1m_amd/csrc/ksched_kernels.hpp", "k8s-1m_amd/Makefile"]
@@ -275,6 +276,8 @@ def end_to_end(args, kind, sched, world, barrier):
     batch k+1 compiled on the host while batch k runs.  W untimed steps, then
     K timed steps between barriers (fresh pods, seed 7, against the live
     cluster); HIP-event timing of the kernels covers the timed steps."""
+    import numpy  # noqa: F401 -- imported here, not by the first results_to_arrays inside the timed steps (~0.1 s)
+
     from ksched import _abi
     from ksched.framework import results_to_arrays
 
@@ -285,23 +288,27 @@ def end_to_end(args, kind, sched, world, barrier):
     scheduled = 0
 
     def run(k0, k1, timed):
+        # up to DEPTH batches submitted ahead of the one being waited for, so
+        # the worker always finds the next batch queued when a run ends
         nonlocal scheduled
         compile_s = 0.0
-        cur = sched.prepare(pods.pods_at(k0 * args.batch), args.batch)
-        assert lib.ks_batch_submit(ctx, cur) == 0
+        inflight = []
+        nxt = k0
         for k in range(k0, k1):
-            nxt = None
-            if k + 1 < k1:
+            while nxt < k1 and len(inflight) < E2E_DEPTH:
                 tc = time.perf_counter()
-                nxt = sched.prepare(pods.pods_at((k + 1) * args.batch), args.batch)
-                compile_s += time.perf_counter() - tc
-                assert lib.ks_batch_submit(ctx, nxt) == 0
+                b = sched.prepare(pods.pods_at(nxt * args.batch), args.batch)
+                if nxt > k0:
+                    compile_s += time.perf_counter() - tc
+                assert lib.ks_batch_submit(ctx, b) == 0
+                inflight.append(b)
+                nxt += 1
+            cur = inflight.pop(0)
             assert lib.ks_batch_wait(ctx, cur) == 0, lib.ks_last_error(ctx)
             assert lib.ks_batch_results(ctx, cur, out) == 0
             if timed:
                 scheduled += int((results_to_arrays(out, args.batch)["status"] == 0).sum())
             sched.free(cur)
-            cur = nxt
         return compile_s
 
     if w:

@@ -364,9 +364,10 @@ struct ks_ctx {
   // KS_EVENT_PROFILE=1: per event kind, runs / events / seconds of ks_events_apply (stderr at ks_close)
   bool ev_profile = false;
   // KS_RUN_PROFILE=1: seconds per phase of the batch runs (stderr at ks_close):
-  // [0] waiting for `mu` at run start, [1] enqueueing rounds, [2] drains, [3] runs
+  // [0] waiting for `mu` at run start, [1] enqueueing rounds, [2] drains, [3] runs,
+  // [4] worker runs' wall time, [5] worker idle between submitted runs, [6] worker runs
   bool run_profile = false;
-  double prof[4] = {0, 0, 0, 0};
+  double prof[7] = {0, 0, 0, 0, 0, 0, 0};
   struct EvProf {
     uint64_t runs = 0, events = 0;
     double s = 0;
@@ -2969,7 +2970,12 @@ void worker_main(ks_ctx *c) {
     ks_batch *b = c->queue.front();
     c->queue.pop_front();
     lk.unlock();
+    const auto t0 = std::chrono::steady_clock::now();
     const ks_status st = run_batch(c, b);
+    if (c->run_profile) {
+      c->prof[4] += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      c->prof[6] += 1;
+    }
     std::string e;
     if (st) {
       std::lock_guard<std::mutex> g(c->err_mu);
@@ -2981,6 +2987,12 @@ void worker_main(ks_ctx *c) {
     b->done = true;
     c->inflight--;
     c->dcv.notify_all();
+    if (c->run_profile && !c->queue.empty()) c->prof[5] += 0;  // next run already queued: no idle time
+    else if (c->run_profile) {
+      const auto ti = std::chrono::steady_clock::now();
+      c->qcv.wait(lk, [&] { return c->stop || !c->queue.empty(); });
+      if (!c->queue.empty()) c->prof[5] += std::chrono::duration<double>(std::chrono::steady_clock::now() - ti).count();
+    }
   }
 }
 
@@ -3183,8 +3195,10 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
 void ks_close(ks_ctx *c) {
   if (!c) return;
   if (c->run_profile)
-    std::fprintf(stderr, "ksched runs: %.0f %s: lock wait %.3f s, enqueue %.3f s, drains %.3f s\n", c->prof[3],
-                 "runs", c->prof[0], c->prof[1], c->prof[2]);
+    std::fprintf(stderr,
+                 "ksched runs: %.0f runs: lock wait %.3f s, enqueue %.3f s, drains %.3f s; worker: %.0f runs %.3f s, "
+                 "idle with work queued %.3f s\n",
+                 c->prof[3], c->prof[0], c->prof[1], c->prof[2], c->prof[6], c->prof[4], c->prof[5]);
   if (c->ev_profile)
     for (int k = 0; k < 4; ++k)
       std::fprintf(stderr, "ksched events kind %d: %llu runs, %llu events, %.3f s\n", k,
