@@ -101,7 +101,10 @@ def parse():
                     help="pods per step (each batch refills the round pipeline once)")
     ap.add_argument("--pods-per-round", type=int, default=256)
     ap.add_argument("--topk", type=int, default=0)
-    ap.add_argument("--nodes-per-lane", type=int, default=4)
+    ap.add_argument("--nodes-per-lane", type=int, default=None,
+                    help="default 4 on one GPU; 2 when sharded over several GPUs (twice the sweep blocks per "
+                         "shard: a shard's candidate lists hold up to 4 keys per block, and at tied top scores "
+                         "a 125k-node shard's lists ran short with 4, DESIGN §6)")
     ap.add_argument("--kind", default="hetero", choices=["hetero", "kwok", "labeled", "zoned"])
     ap.add_argument("--pods", default="default", choices=["default", "besteffort", "spread", "affinity"],
                     help="besteffort: request-less pods (kwok/make_pods/main.go:118-148); spread: "
@@ -120,6 +123,8 @@ def parse():
     ap.add_argument("--pmc-dir", default=str(ROOT / "profiles" / "pmc"),
                     help="per-configuration PMC summaries (tools/pmc.sh + tools/pmc_summary.py)")
     a = ap.parse_args()
+    if a.nodes_per_lane is None:
+        a.nodes_per_lane = 2 if a.gpus > 1 else 4
     if a.prefill is None:
         a.prefill = 0.0 if a.kind == "kwok" else 0.5
     if a.pods in ("spread", "affinity"):  # one pod at a time (spread path): smaller steps and CPU samples

@@ -2205,11 +2205,9 @@ ks_status solo_compile(ks_ctx *c, const ks_pod &p, PodDev &d, ProgBuf &cl, bool 
     if ((st = ipa_compile(c, p, create, refs, &aff, &aff_flags))) return st;
   }
   if (!p.n_spread && xr.empty() && imgs.empty() && aff.empty()) return KS_OK;
-  if (c->cfg.world_size > 1)
-    return c->fail(KS_ERR_UNSUPPORTED,
-                   "pod %s: spread constraints, pod affinity, extended resources and present images need a "
-                   "single-rank context",
-                   pn.c_str());
+  // multi-rank contexts run the one-pod path replicated: every rank holds the
+  // whole node table and every commit, so each rank's chain over
+  // all positions gives the same result with no exchange
   if (create && (st = spread_alloc(c))) return st;
   if (p.n_spread > (uint32_t)MAX_SPREAD)
     return c->fail(KS_ERR_UNSUPPORTED, "pod %s: more than %d topology spread constraints", pn.c_str(), MAX_SPREAD);
@@ -2843,8 +2841,6 @@ ks_status run_batch(ks_ctx *c, ks_batch *b) {
     }
   }
   if (!b->uploaded && (st0 = upload_batch(c, b))) return st0;
-  if (b->any_spread && c->has_comm())
-    return c->fail(KS_ERR_UNSUPPORTED, "topology spread pods need a single-rank context");
   if (classes || b->any_spread)
     HIPC(c, hipMemcpyAsync(b->d_cmask, b->h_cmask, (size_t)std::max<uint32_t>(b->n, 1) * 8 * CMASK_WORDS, hipMemcpyHostToDevice,
                            c->stream));

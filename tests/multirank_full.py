@@ -79,8 +79,8 @@ def run_ranks(ranks, pods, m):
     return out[0], marks[0]
 
 
-def one_rank(nodes, slots, pf, stream, bursts, events):
-    s = Scheduler(N)
+def one_rank(nodes, slots, pf, stream, bursts, events, npl):
+    s = Scheduler(N, nodes_per_lane=npl)
     t = GpuTarget(s)
     if stream is not None:
         stream.setup([t])
@@ -117,15 +117,28 @@ def main(cfg):
     world, kind = cfg["world"], cfg["kind"]
     t0 = time.time()
     stream = nodes = slots = pf = None
+    m = BATCH
     if kind == "c5":
         stream = BurstStream(synth.HETERO, N, 2, BATCH)  # C5 rates: 5 % pods, 0.1 % / 0.01 % nodes
+    elif kind == "spread":
+        # the spread bench's cluster (1M nodes in 32 zones, prefill pods of 64
+        # apps) with deployment pods carrying PodTopologySpread constraints
+        # interleaved with plain pods: the one-pod path replicated on every rank
+        from test_gpu_fullsize import MixedStream
+        m = 3072
+        nodes = synth.nodes(synth.ZONED, N, 1)
+        slots = synth.slot_array(N)
+        pf = synth.prefill(synth.ZONED, N, 1, 3, 0.5)
+        keep = (synth.spread_pods(m // 2, 64, 5), synth.pods(synth.HETERO, m // 2, 6))
+        pods = MixedStream(keep[1], keep[0], 128)
     else:
         k = synth.HETERO if kind == "c3" else synth.LABELED
         nodes = synth.nodes(k, N, 1)
         slots = synth.slot_array(N)
         pf = synth.prefill(k, N, 1, 3, 0.5)
         pods = synth.pods(k, BATCH, 2 if kind == "c3" else 7)
-    ranks = [Scheduler(N, world_size=world, rank=r) for r in range(world)]
+    npl = cfg.get("npl", 2)  # bench.py --gpus N > 1 lays the table out with 2 nodes per lane
+    ranks = [Scheduler(N, world_size=world, rank=r, nodes_per_lane=npl) for r in range(world)]
     Scheduler.comm_init_local(ranks)
     targets = [GpuTarget(s) for s in ranks]
     if stream is not None:
@@ -143,8 +156,8 @@ def main(cfg):
             p = StreamPods(stream, b)
             bursts.append((p, BATCH))
         else:
-            bursts.append((pods, BATCH))
-        res, mk = run_ranks(ranks, bursts[-1][0], BATCH)
+            bursts.append((pods, m))
+        res, mk = run_ranks(ranks, bursts[-1][0], m)
         got.append(res)
         marks.append(mk)
         if stream is not None and b + 1 < nb:
@@ -165,9 +178,9 @@ def main(cfg):
     run_s = time.time() - t0 - setup_s
     # one rank, same stream
     one, one_table = one_rank(nodes, slots, pf, BurstStream(synth.HETERO, N, 2, BATCH) if stream is not None else None,
-                              bursts, events)
+                              bursts, events, npl)
     for b in range(nb):
-        if not np.array_equal(one[b], res_array(got[b], BATCH)):
+        if not np.array_equal(one[b], res_array(got[b], bursts[b][1])):
             raise Fail(f"burst {b}: the one-rank context's results differ from the ranks'")
     if not np.array_equal(one_table, tables[0]):
         raise Fail("the one-rank context's node table differs from the ranks'")
@@ -181,17 +194,21 @@ def main(cfg):
         o.add_pods(pf.pods, pf.slot_ptr, pf.n_pods)
     checked, kinds = 0, set()
     for b in range(nb):
-        wins = pick_windows(marks[b], BATCH)
+        mb = bursts[b][1]
+        if kind == "spread":  # windows straddle a plain -> spread boundary, sit in a spread run, end the batch
+            wins, wlen = [(124, "fixed"), (1400, "fixed"), (mb - 6, "fixed")], 6
+        else:
+            wins, wlen = pick_windows(marks[b], mb), 32
         kinds |= {what for _, what in wins}
-        checked += replay_check(o, bursts[b][0], got[b], BATCH, windows=[w for w, _ in wins])
+        checked += replay_check(o, bursts[b][0], got[b], mb, windows=[w for w, _ in wins], wlen=wlen)
         if b < len(events):
             BurstStream.apply_marshalled(events[b][2], [ot])
     ow = states_np(o.L.oracle_node_states, o.o, N)
     if not np.array_equal(ow, tables[0]):
         raise Fail("node tables differ from the oracle's after replaying every decision")
     o.close()
-    r0 = res_array(got[0], BATCH)
-    return {"ok": True, "kind": kind, "world": world, "scheduled": int((r0["status"] == 0).sum()),
+    r0 = res_array(got[0], bursts[0][1])
+    return {"ok": True, "kind": kind, "world": world, "npl": npl, "scheduled": int((r0["status"] == 0).sum()),
             "rounds": int(dbg[0]), "reswept": int(dbg[4]), "wasted": int(dbg[3]), "oracle_pods_checked": checked,
             "window_kinds": sorted(kinds), "setup_s": round(setup_s, 1), "ranks_s": round(run_s, 1),
             "total_s": round(time.time() - t0, 1)}

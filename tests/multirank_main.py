@@ -32,7 +32,15 @@ def main(cfg):
     P, K, calls = cfg.get("P", 256), cfg.get("K", 0), cfg.get("calls", 3)
     nodes = synth.nodes(kind, n, cfg.get("node_seed", 11))
     slots = synth.slot_array(n)
-    pods = synth.pods(kind, m, cfg.get("pod_seed", 12))
+    if cfg.get("pods_kind") in ("spread", "affinity"):
+        # one-pod-path pods (PodTopologySpread / InterPodAffinity) interleaved
+        # with plain pods: run replicated on every rank over the whole table
+        from test_gpu_fullsize import MixedStream
+        gen = synth.spread_pods if cfg["pods_kind"] == "spread" else synth.affinity_pods
+        keep = (gen(m // 2, 16, cfg.get("pod_seed", 12)), synth.pods(synth.HETERO, m - m // 2, 13))
+        pods = MixedStream(keep[1], keep[0], 64)
+    else:
+        pods = synth.pods(kind, m, cfg.get("pod_seed", 12))
     pre = synth.prefill(kind, n, 1, 3, 0.5) if cfg.get("prefill") else None
     ranks = [Scheduler(n, device=0, pods_per_round=P, topk=K, world_size=world, rank=r) for r in range(world)]
     Scheduler.comm_init_local(ranks)

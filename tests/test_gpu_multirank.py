@@ -52,6 +52,15 @@ def test_short_lists_ranks():
     assert r["wasted"] >= 0
 
 
+@pytest.mark.parametrize("pods_kind", ["spread", "affinity"])
+def test_one_pod_path_ranks(pods_kind):
+    # PodTopologySpread / InterPodAffinity pods on a multi-rank context: the
+    # one-pod path runs replicated on every rank (each holds every node and
+    # commit), mixed with plain pods on the round kernels
+    r = run_case(world=3, kind=8, nodes=6000, pods=1200, prefill=True, pods_kind=pods_kind, calls=2)
+    assert r["scheduled"] > 0
+
+
 def test_kwok_ties_ranks():
     # identical nodes: every pod's best keys tie across both shards
     run_case(world=2, kind=1, nodes=8000, pods=6000, K=512)
@@ -70,11 +79,11 @@ def run_full(**cfg):
     return res
 
 
-@pytest.mark.parametrize("kind", ["c3", "c4", "c5"])
+@pytest.mark.parametrize("kind", ["c3", "c4", "c5", "spread"])
 def test_fullsize_eight_ranks(kind):
     # BASELINE.json's 1M-node configurations at the 8-GPU split (125,000 nodes
     # per rank): every rank == rank 0 == a one-rank context == the oracle's windows
     r = run_full(world=8, kind=kind)
-    assert r["oracle_pods_checked"] >= 4 * 32
+    assert r["oracle_pods_checked"] >= (18 if kind == "spread" else 4 * 32)
     if kind == "c4":
         assert r["reswept"] > 0, "multi-rank FIX path not exercised"
