@@ -26,7 +26,7 @@ batch k+1 overlaps running batch k.  Beside it the line reports:
   reference's ScheduleOne latency (~560 us per pod per shard, README.adoc:786);
 * roofline: the sweep kernel's VALU issue fraction (its binding resource) from
   the PMC file measured for this exact configuration and kernel source
-  (profiles/pmc/<key>.json, tools/pmc.sh), with the measured HBM traffic and
+  (profiles/pmc/<key>.json, tools/gpu.sh pmc), with the measured HBM traffic and
   its fraction of 8 TB/s beside it;
 * cpu_baseline: the C++ oracle (a restatement of upstream kube-scheduler) on a
   bounded prefix of the same stream, on the box's CPU share.
@@ -121,7 +121,7 @@ def parse():
     ap.add_argument("--cpu-pods-mt", type=int, default=400, help="oracle sample (pods), multi-thread")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc-dir", default=str(ROOT / "profiles" / "pmc"),
-                    help="per-configuration PMC summaries (tools/pmc.sh + tools/pmc_summary.py)")
+                    help="per-configuration PMC summaries (tools/gpu.sh pmc + tools/pmc_summary.py)")
     a = ap.parse_args()
     if a.nodes_per_lane is None:
         a.nodes_per_lane = 2 if a.gpus > 1 else 4

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarise the rocprofv3 --pmc passes of tools/pmc.sh into profiles/pmc/<key>.json.
+"""Summarise the rocprofv3 --pmc passes of tools/gpu.sh pmc into profiles/pmc/<key>.json.
 
     python tools/pmc_summary.py gpurun_out/pmc_r2c3 --tag r2c3 --out-dir profiles/pmc
 
@@ -94,7 +94,7 @@ def main():
         kernels[name]["avg_ms_under_pmc"] = sum(ds) / len(ds) if ds else None
     out = {"tag": a.tag, "key": key, "kernel_src": kernel_src_hash(), "evals_per_launch": evals,
            "workload": line["config"]["workload"],
-           "source": f"rocprofv3 --pmc passes (tools/pmc.sh), {a.dir}", "kernels": kernels}
+           "source": f"rocprofv3 --pmc passes (tools/gpu.sh pmc), {a.dir}", "kernels": kernels}
     sweep = {n: v for n, v in kernels.items() if SWEEP in n}
     if sweep:
         name, s = max(sweep.items(), key=lambda kv: kv[1].get("dispatches", 0))

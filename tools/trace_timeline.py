@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-round timeline from a rocprofv3 kernel trace (tools/gpu_trace.sh):
+"""Per-round timeline from a rocprofv3 kernel trace (tools/gpu.sh trace):
 resolve duration, resolve-to-resolve gap, and the kernels around one resolve.
 
     python tools/trace_timeline.py gpurun_out/trace_<tag>/run_kernel_trace.csv [round]
