@@ -9,6 +9,7 @@
 #   tools/gpu.sh trace TAG [bench args]       rocprofv3 --kernel-trace --stats of a short bench run
 #   tools/gpu.sh pmc TAG [bench args]         PMC passes of one configuration -> gpurun_out/pmc/<key>.json
 #   tools/gpu.sh ab TAG [bench args]          A/B: default library vs lib/alt (or ALT_ENV="VAR=value"), twice each
+#   tools/gpu.sh variants TAG [bench args]    VARIANTS="default expt2 ..." one configuration on several lib/<name> builds
 #   tools/gpu.sh stamps TAG [kind]            resolve-phase stamps (make stamps stamps2 stamps3 first)
 #   tools/gpu.sh valu                         VALU issue costs (tools/valu_issue, built by hipcc on the CPU side)
 export TMPDIR=/tmp
@@ -105,6 +106,14 @@ PY
       timeout -k 10 300 python -u bench.py --no-cpu-baseline --steps 6 --latency-calls 0 "$@" \
         > gpurun_out/ab_${TAG}_$v.json 2> gpurun_out/ab_${TAG}_$v.err || { tail -3 gpurun_out/ab_${TAG}_$v.err; exit 1; }
       summary gpurun_out/ab_${TAG}_$v.json $v
+    done ;;
+  variants)
+    # one bench configuration on several library builds: VARIANTS="default expt2 ..." (lib/<name>)
+    for v in ${VARIANTS:-default}; do
+      if [ "$v" = default ]; then unset KSCHED_LIB_DIR; else export KSCHED_LIB_DIR=k8s-1m_amd/ksched/lib/$v; fi
+      timeout -k 10 300 python -u bench.py --no-cpu-baseline --steps 4 --warmup 1 --latency-calls 0 "$@" \
+        > gpurun_out/var_${TAG}_$v.json 2> gpurun_out/var_${TAG}_$v.err || { tail -3 gpurun_out/var_${TAG}_$v.err; exit 1; }
+      summary gpurun_out/var_${TAG}_$v.json $v
     done ;;
   stamps)
     KIND=${1:-hetero}
