@@ -280,6 +280,10 @@ struct ks_batch {
   std::vector<uint32_t> term_refs;  // term classes of the batch's pods' own terms (one per pod and term)
   uint64_t *d_cmask = nullptr, *h_cmask = nullptr;
   uint8_t *d_marks = nullptr;  // [cap_pods rounded to 4] round marks (ks_batch_marks)
+  // identical pods (RoundArgs::cls): per pod the batch index of its first
+  // byte-identical descriptor; dups = some pod repeats an earlier one
+  uint32_t *d_cls = nullptr, *h_cls = nullptr;
+  bool dups = false;
   // asynchronous run state (ks_batch_submit / ks_batch_wait)
   bool queued = false, done = false;
   ks_status run_status = KS_OK;
@@ -359,6 +363,7 @@ struct ks_ctx {
   // KS_TUPLE_GUESS), so one process can open contexts with different settings
   // (tests do).
   bool early_fix = true;
+  bool dedup = true;        // KS_DEDUP: sweep identical pods of a round once (resource-only batches)
   bool tuple_guess = true;  // normaliser guesses over node tuples (refine_guesses)
   uint32_t timing_every = 8, sweep_blocks = 8192, ext_npl = 2;
   // KS_EVENT_PROFILE=1: per event kind, runs / events / seconds of ks_events_apply (stderr at ks_close)
@@ -388,6 +393,8 @@ struct ks_ctx {
   double *d_norm_inv = nullptr;   // [2][P][2] by round parity
   PodStat *d_pstat = nullptr;     // [P]
   uint32_t *d_fix = nullptr;      // [P] flags + [MAX_P / MAX_PG] group flags + [MAX_P] compacted list
+  uint32_t *d_dedup = nullptr;    // by round parity: rep [MAX_P], ulist [MAX_P], nuniq (RoundArgs::cls)
+  bool dedup_used[2] = {false, false};  // the last round of that parity read records through rep
   BlockRec *d_brec = nullptr;     // [2][...] by round parity (merge k reads while sweep k+1 writes)
   size_t brec_bytes = 0;          // per parity
   uint64_t *d_srec = nullptr, *d_frec = nullptr;
@@ -2582,6 +2589,14 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k, uint32_t end) {
   a.clauses = b->d_clauses;
   a.marks = b->d_marks;
   const uint32_t q = k & 1u, pq = q ^ 1u;
+  c->dedup_used[q] = !b->ext && b->dups && c->dedup;
+  if (c->dedup_used[q]) {
+    uint32_t *dd = c->d_dedup + (size_t)q * (2 * MAX_P + 4);
+    a.cls = b->d_cls;
+    a.rep = dd;
+    a.ulist = dd + MAX_P;
+    a.nuniq = dd + 2 * MAX_P;
+  }
   const size_t RW = rec_words(c->K);
   a.d_start = c->d_start;
   a.sstart = c->d_pipe + q;
@@ -2758,6 +2773,8 @@ ks_status batch_acquire(ks_ctx *c, uint32_t n, size_t words, ks_batch **out) {
     HIPC(c, hipMalloc((void **)&b->d_cmask, (size_t)need * 8 * CMASK_WORDS));
     HIPC(c, hipHostMalloc((void **)&b->h_cmask, (size_t)need * 8 * CMASK_WORDS, hipHostMallocDefault));
     HIPC(c, hipMalloc((void **)&b->d_marks, ((size_t)need + 3) & ~(size_t)3));
+    HIPC(c, hipMalloc((void **)&b->d_cls, (size_t)need * 4));
+    HIPC(c, hipHostMalloc((void **)&b->h_cls, (size_t)need * 4, hipHostMallocDefault));
     b->cap_pods = need;
   }
   if (words > b->cap_words) {
@@ -2784,10 +2801,41 @@ void batch_release(ks_ctx *c, ks_batch *b) {
 }
 
 // Compiled batch (pinned host copies) -> device, on the scheduler stream.
+// Identical pods of a resource-only batch (RoundArgs::cls): cls[i] = the index
+// of the first pod whose compiled descriptor is byte-identical to pod i's
+// (the sweep, Filter and Score read nothing else of a pod), i for pods of the
+// one-pod path.  Returns whether some pod repeats an earlier one.
+bool pod_classes(const PodDev *dev, uint32_t n, uint32_t *cls) {
+  std::unordered_map<uint64_t, uint32_t> first;
+  first.reserve(n);
+  bool dups = false;
+  for (uint32_t i = 0; i < n; ++i) {
+    cls[i] = i;
+    if (dev[i].flags & PF_SOLO) continue;
+    uint64_t h = 1469598103934665603ull;  // FNV-1a over the descriptor's words
+    const uint64_t *w = reinterpret_cast<const uint64_t *>(&dev[i]);
+    for (size_t q = 0; q < sizeof(PodDev) / 8; ++q) h = (h ^ w[q]) * 1099511628211ull;
+    for (;; ++h) {  // open addressing on the hash value itself (collisions probe h + 1)
+      auto it = first.find(h);
+      if (it == first.end()) {
+        first.emplace(h, i);
+        break;
+      }
+      if (std::memcmp(&dev[it->second], &dev[i], sizeof(PodDev)) == 0) {
+        cls[i] = it->second;
+        dups = true;
+        break;
+      }
+    }
+  }
+  return dups;
+}
+
 ks_status upload_batch(ks_ctx *c, ks_batch *b) {
   const size_t np = std::max<uint32_t>(b->n, 1);
   HIPC(c, hipMemcpyAsync(b->d_pods, b->h_pods, np * sizeof(PodDev), hipMemcpyHostToDevice, c->stream));
   HIPC(c, hipMemcpyAsync(b->d_pinv, b->h_pinv, np * 2 * sizeof(double), hipMemcpyHostToDevice, c->stream));
+  if (b->dups) HIPC(c, hipMemcpyAsync(b->d_cls, b->h_cls, np * 4, hipMemcpyHostToDevice, c->stream));
   HIPC(c, hipMemcpyAsync(b->d_clauses, b->h_clauses, b->n_words * 8, hipMemcpyHostToDevice, c->stream));
   HIPC(c, hipMemsetAsync(b->d_results, 0, np * sizeof(DevResult), c->stream));
   HIPC(c, hipMemsetAsync(b->d_marks, 0, (np + 3) & ~(size_t)3, c->stream));
@@ -3067,6 +3115,7 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
       return e ? std::atoi(e) : dflt;
     };
     x->early_fix = env_u("KS_EARLY_FIX", 1) != 0;
+    x->dedup = env_u("KS_DEDUP", 1) != 0;
     x->tuple_guess = env_u("KS_TUPLE_GUESS", 1) != 0;
     x->ev_profile = env_u("KS_EVENT_PROFILE", 0) != 0;
     x->run_profile = env_u("KS_RUN_PROFILE", 0) != 0;
@@ -3161,6 +3210,7 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
       (st = dalloc(x, &x->d_start, 1)) || (st = dalloc(x, &x->d_norm, 2 * 2 * (size_t)x->P)) ||
       (st = dalloc(x, &x->d_norm_inv, 2 * 2 * (size_t)x->P)) ||
       (st = dalloc(x, &x->d_pstat, (size_t)x->P)) || (st = dalloc(x, &x->d_fix, 2 * MAX_P + MAX_P / MAX_PG)) ||
+      (st = dalloc(x, &x->d_dedup, 2 * (2 * (size_t)MAX_P + 4))) ||
       (st = dalloc(x, &x->d_pipe, 8)) || (st = dalloc(x, &x->d_flags, 4)) || (st = dalloc(x, &x->d_carry, 2 * (size_t)MAX_P)) ||
       (st = dalloc(x, &x->d_counters, 16)))
     return st;
@@ -3227,7 +3277,7 @@ void ks_close(ks_ctx *c) {
   void *bufs[] = {c->t.acpu, c->t.amem, c->t.rcpu, c->t.rmem, c->t.zcpu, c->t.zmem, c->t.apods,
                   c->t.npods, c->t.hard, c->t.prefer, c->t.lab, c->t.num, c->d_shards, c->d_slot_pos,
                   c->d_start, c->d_norm, c->d_norm_inv, c->d_pstat, c->d_fix, c->d_brec, c->d_srec, c->d_frec,
-                  c->d_counters, c->d_crow, c->d_cext, c->d_pipe, c->d_carry, c->d_flags, c->d_dom,
+                  c->d_counters, c->d_crow, c->d_cext, c->d_pipe, c->d_carry, c->d_flags, c->d_dom, c->d_dedup,
                   c->d_pos_slot, c->d_dcnt, c->d_dflag, c->d_acc, c->d_sst, c->d_sraw, c->d_spart,
                   c->d_xalloc, c->d_tcnt, c->d_adcnt, c->d_sraw2};
   for (void *b : bufs)
@@ -3241,10 +3291,10 @@ void ks_close(ks_ctx *c) {
   for (void *g : c->pinned_graveyard) (void)hipHostFree(g);
   for (ks_batch *b : c->all_batches) {
     for (void *p : {(void *)b->d_pods, (void *)b->d_pinv, (void *)b->d_clauses, (void *)b->d_results,
-                    (void *)b->d_cmask, (void *)b->d_marks})
+                    (void *)b->d_cmask, (void *)b->d_marks, (void *)b->d_cls})
       if (p) (void)hipFree(p);
     for (void *p : {(void *)b->h_results, (void *)b->h_pods, (void *)b->h_pinv, (void *)b->h_clauses,
-                    (void *)b->h_cmask})
+                    (void *)b->h_cmask, (void *)b->h_cls})
       if (p) (void)hipHostFree(p);
     delete b;
   }
@@ -3787,6 +3837,7 @@ ks_status ks_batch_prepare(ks_ctx *c, const ks_pod *pods, uint32_t n, ks_batch *
     b->any_spread = true;
   }
   std::memcpy(b->h_pods, dev.data(), dev.size() * sizeof(PodDev));
+  b->dups = !ext && pod_classes(dev.data(), n, b->h_cls);
   for (size_t i = 0; i < dev.size(); ++i) {
     b->h_pinv[2 * i] = dev[i].tt_guess ? 1.0 / (double)dev[i].tt_guess : 0.0;
     b->h_pinv[2 * i + 1] = dev[i].na_guess ? 1.0 / (double)dev[i].na_guess : 0.0;
@@ -4188,9 +4239,14 @@ ks_status ks_debug_round_record(ks_ctx *c, uint32_t r, uint64_t *out) {
   HIPC(c, hipSetDevice(c->cfg.device));
   const size_t RW = rec_words(c->K);
   // round 0 = parity 0; with several shards the merged record (merge_shards)
+  ks_status st;
+  if (c->dedup_used[0]) {  // an identical pod's record serves pod r
+    uint32_t rr = r;
+    if ((st = xfer_begin(c, 1024, 0)) || (st = d2h(c, &rr, c->d_dedup + r, 4)) || (st = xfer_sync(c))) return st;
+    r = rr;
+  }
   const uint64_t *rec = (c->S == 1 ? c->d_srec : c->d_frec) + (size_t)r * RW;
   std::vector<uint64_t> w(RW);
-  ks_status st;
   if ((st = xfer_begin(c, RW * 8 + 1024, 0)) || (st = d2h(c, w.data(), rec, RW * 8)) || (st = xfer_sync(c)))
     return st;
   const ShardRecHdr *h = (const ShardRecHdr *)w.data();

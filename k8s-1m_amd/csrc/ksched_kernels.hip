@@ -294,10 +294,13 @@ void sweep_kernel(RoundArgs a) {
   const uint32_t lane = threadIdx.x % WAVE;
   const uint32_t lwave = kw / a.sub, j0 = (kw % a.sub) * NPL;  // layout wave / first step
   const uint32_t p0 = start + blockIdx.y * a.pg;
-  const uint32_t p1 = min(min(p0 + a.pg, start + a.P), a.npods);
-  if (p0 >= p1 || blockIdx.x * NW >= kwaves) return;
+  uint32_t p1 = min(min(p0 + a.pg, start + a.P), a.npods);
   // FIX mode: only the pods norm_check flagged (pod groups of MAX_PG)
   const bool fix = EXT && a.fix;
+  // identical pods: the groups walk the round's representatives (ulist)
+  const bool dedup = !EXT && a.ulist != nullptr;
+  if (dedup) p1 = min(p1, start + uniform_u32(*a.nuniq));
+  if (p0 >= p1 || blockIdx.x * NW >= kwaves) return;
   if (fix && uniform_u32(a.fix_group[blockIdx.y]) == 0) return;
 
   NodeRegs nr[NPL];
@@ -335,7 +338,7 @@ void sweep_kernel(RoundArgs a) {
 
   for (uint32_t it = p0; it < p1; ++it) {
     // FIX mode: slice entry it - start of the compacted flagged-pod list
-    const uint32_t r = fix ? uniform_u32(a.fix_list[it - start]) : it - start;
+    const uint32_t r = fix ? uniform_u32(a.fix_list[it - start]) : dedup ? uniform_u32(a.ulist[it - start]) : it - start;
     if (fix && r == FIX_NONE) continue;
     const uint32_t pi = start + r;
     const PodDev p = load_pod(a.pods, pi);
@@ -515,7 +518,7 @@ void sweep_kernel(RoundArgs a) {
   // Block list per pod: top BLOCK_KEYS of the 4 wave lists above every bound.
   const uint32_t npl = p1 - p0;
   for (uint32_t pl = threadIdx.x; pl < npl; pl += blockDim.x) {
-    const uint32_t r = fix ? a.fix_list[p0 + pl - start] : p0 + pl - start;
+    const uint32_t r = fix ? a.fix_list[p0 + pl - start] : dedup ? a.ulist[p0 + pl - start] : p0 + pl - start;
     if (fix && r == FIX_NONE) continue;
     uint64_t k[2 * NW];
     uint64_t bound = 0;
@@ -666,6 +669,7 @@ __global__ __launch_bounds__(MERGE_THREADS) void merge_kernel(RoundArgs a) {
   const uint32_t r = blockIdx.x;
   if (start + r >= a.npods || r >= a.P) return;
   if (a.fix && a.fix_flag[r] == 0) return;  // FIX mode: re-merge the re-swept pods only
+  if (a.rep != nullptr && a.rep[r] != r) return;  // an identical pod's record serves it
   const uint32_t sh = blockIdx.y;
   const Shard s = a.shards[a.shard0 + sh];
   const uint32_t nb = (s.waves * a.sub + 3) / 4;
@@ -784,6 +788,7 @@ __global__ __launch_bounds__(256) void merge_shards_kernel(RoundArgs a) {
   const uint32_t start = uniform_u32(*a.sstart);
   const uint32_t r = blockIdx.x;
   if (start + r >= a.npods || r >= a.P) return;
+  if (a.rep != nullptr && a.rep[r] != r) return;
   const uint32_t W = rec_words(a.K);
   const uint64_t *in = a.srec + (size_t)r * W;
   const size_t stride = (size_t)a.P * W;  // between shards
@@ -832,6 +837,7 @@ __global__ __launch_bounds__(256) void gather_cand_kernel(RoundArgs a) {
   const uint32_t start = uniform_u32(*a.sstart);
   const uint32_t r = blockIdx.x;
   if (start + r >= a.npods || r >= a.P) return;
+  if (a.rep != nullptr && a.rep[r] != r) return;
   const uint64_t *rec = a.frec + (size_t)r * rec_words(a.K);
   const uint32_t nk = ((const ShardRecHdr *)rec)->nkeys;
   for (uint32_t t = threadIdx.x; t < nk; t += blockDim.x) {
@@ -925,6 +931,7 @@ __global__ __launch_bounds__(PATCH_THREADS) void patch_kernel(RoundArgs a) {
   const uint32_t start = uniform_u32(*a.act);
   const uint32_t r = blockIdx.x;
   if (a.first || start >= a.npods || uniform_u32(*a.sstart) != start || start + r >= a.npods) return;
+  if (a.rep != nullptr && uniform_u32(a.rep[r]) != r) return;
   const uint32_t nc = uniform_u32(*a.carry_in_n);
   if (nc == 0) return;
   const PodDev p = load_pod(a.pods, start + r);
@@ -1336,6 +1343,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
   constexpr bool TWO = LIST_SPAN == 2 * WAVE;
   __shared__ PodDev s_pod[MAX_P];
   __shared__ ShardRecHdr s_hdr[MAX_P];
+  __shared__ uint32_t s_rep[MAX_P];  // record of each pod (an identical pod's: RoundArgs::rep)
   __shared__ uint32_t s_norm[MAX_P][2];
   __shared__ uint32_t s_hkey[RHASH];  // slots modified this round (+1), linear probing
   __shared__ CandExt s_modx[EXT ? MAX_P : 1];  // label / taint words of the modified nodes
@@ -1397,8 +1405,10 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
   // ---- stage the round
   for (uint32_t i = tid; i < RHASH; i += RESOLVE_THREADS) s_hkey[i] = 0;
   for (uint32_t i = tid; i < nround; i += RESOLVE_THREADS) {
+    const uint32_t ri = a.rep != nullptr ? a.rep[i] : i;
+    s_rep[i] = ri;
     s_pod[i] = a.pods[start + i];
-    s_hdr[i] = *(const ShardRecHdr *)(a.frec + (size_t)i * RW);
+    s_hdr[i] = *(const ShardRecHdr *)(a.frec + (size_t)ri * RW);
     s_norm[i][0] = a.norm_max[2 * i];
     s_norm[i][1] = a.norm_max[2 * i + 1];
   }
@@ -1419,7 +1429,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
     // every wave issues it (list_wait counts LIST_DMA loads per iteration);
     // entries past K: any in-record address (never read back)
     const uint32_t e = LIST_SPAN * lw + 2 * lane;
-    const uint64_t *src = a.frec + (size_t)p * RW + REC_HDR_WORDS + (e < a.K ? e : 0u);
+    const uint64_t *src = a.frec + (size_t)s_rep[p] * RW + REC_HDR_WORDS + (e < a.K ? e : 0u);
     if (TWO || lane < WAVE / 2)
       __builtin_amdgcn_global_load_lds((gvoid_t *)src, (lvoid_t *)&s_keys[pod % KSLOTS][LIST_SPAN * lw], 16, 0, 0);
   };
@@ -1473,12 +1483,13 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
     const uint64_t hb = second ? hb1 : hb0;
     if (lane < (uint32_t)LSEL) {
       const uint32_t t = LIST_SPAN * lw + te;
-      const uint4 *row = (const uint4 *)(a.crow + (size_t)p * a.K + (lane < nsel ? t : 0u));
+      const size_t rb = (size_t)s_rep[p] * a.K;
+      const uint4 *row = (const uint4 *)(a.crow + rb + (lane < nsel ? t : 0u));
 #pragma unroll
       for (int j = 0; j < ROW_PIECES; ++j)
         __builtin_amdgcn_global_load_lds((gvoid_t *)(row + j), (lvoid_t *)&s_lrowb[pod % RSLOTS][lw][j][0], 16, 0, 0);
       if constexpr (EXT) {
-        const uint4 *x = (const uint4 *)(a.cext + (size_t)p * a.K + (lane < nsel ? t : 0u));
+        const uint4 *x = (const uint4 *)(a.cext + rb + (lane < nsel ? t : 0u));
 #pragma unroll
         for (int j = 0; j < EXT_PIECES; ++j)
           __builtin_amdgcn_global_load_lds((gvoid_t *)(x + j), (lvoid_t *)&s_lrowb[pod % RSLOTS][lw][ROW_PIECES + j][0],
@@ -2070,11 +2081,68 @@ __device__ __forceinline__ void advance_kernel_body(const RoundArgs &a) {
   *a.sstart = s;
   if (s < a.npods) a.counters[2] += min(a.P, a.npods - s);  // pods swept
 }
-__global__ void advance_kernel(RoundArgs a) { advance_kernel_body(a); }
+
+// The round window's classes of identical pods (RoundArgs::cls), one block
+// of ADV_THREADS >= P threads after the advance: thread r inserts its class
+// into an LDS hash with the lowest r as value, reads back its representative,
+// and the representatives are compacted in window order (ballot prefix sums).
+constexpr int ADV_THREADS = MAX_P;
+constexpr uint32_t DHASH = 2 * MAX_P;
+__device__ void dedup_round(const RoundArgs &a, uint32_t s) {
+  __shared__ uint32_t s_k[DHASH], s_v[DHASH], s_wn[ADV_THREADS / WAVE];
+  const uint32_t t = threadIdx.x, lane = t % WAVE, wid = t / WAVE;
+  for (uint32_t i = t; i < DHASH; i += ADV_THREADS) {
+    s_k[i] = NONE32;
+    s_v[i] = NONE32;
+  }
+  __syncthreads();
+  const bool valid = t < a.P && s < a.npods && t < a.npods - s;
+  const uint32_t key = valid ? a.cls[s + t] : NONE32;
+  uint32_t h = (key * 2654435761u) >> 23;  // 9 bits
+  if (valid) {
+    for (;;) {
+      const uint32_t prev = atomicCAS(&s_k[h], NONE32, key);
+      if (prev == NONE32 || prev == key) break;
+      h = (h + 1) & (DHASH - 1);
+    }
+    atomicMin(&s_v[h], t);
+  }
+  __syncthreads();
+  const uint32_t rep = valid ? s_v[h] : t;
+  const bool u = valid && rep == t;
+  const uint64_t ub = __ballot(u);
+  if (lane == 0) s_wn[wid] = (uint32_t)__popcll(ub);
+  if (t < (uint32_t)MAX_P) a.rep[t] = rep;
+  __syncthreads();
+  uint32_t idx = (uint32_t)__popcll(ub & ((1ull << lane) - 1ull)), total = 0;
+#pragma unroll
+  for (int w = 0; w < ADV_THREADS / WAVE; ++w) {
+    idx += (uint32_t)w < wid ? s_wn[w] : 0u;
+    total += s_wn[w];
+  }
+  if (u) a.ulist[idx] = t;
+  if (t == 0) {
+    *a.nuniq = total;
+    a.counters[7] += total;  // representatives swept
+  }
+}
+
+__device__ __forceinline__ void advance_block(const RoundArgs &a) {
+  __shared__ uint32_t s_s;
+  if (threadIdx.x == 0) {
+    advance_kernel_body(a);
+    s_s = *a.sstart;
+  }
+  if (a.rep == nullptr) return;
+  __syncthreads();
+  dedup_round(a, s_s);
+}
+__global__ __launch_bounds__(ADV_THREADS) void advance_kernel(RoundArgs a) { advance_block(a); }
 
 // advance + write-back in one dispatch (the main stream's per-round prologue)
-__global__ void advance_writeback_kernel(RoundArgs a, NodeTable t, const CarryRec *carry, const uint32_t *n) {
-  if (blockIdx.x == 0 && threadIdx.x == 0) advance_kernel_body(a);
+__global__ __launch_bounds__(ADV_THREADS) void advance_writeback_kernel(RoundArgs a, NodeTable t, const CarryRec *carry,
+                                                                        const uint32_t *n) {
+  if (blockIdx.x == 0) advance_block(a);
   const uint32_t cnt = *n;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += gridDim.x * blockDim.x) {
     const CarryRec &c = carry[i];
@@ -2268,12 +2336,12 @@ hipError_t launch_gather_cand(const RoundArgs &a, bool ext, hipStream_t st) {
 }
 
 hipError_t launch_advance(const RoundArgs &a, hipStream_t st) {
-  advance_kernel<<<1, 1, 0, st>>>(a);
+  advance_kernel<<<1, ADV_THREADS, 0, st>>>(a);
   return hipGetLastError();
 }
 
 hipError_t launch_advance_writeback(const RoundArgs &a, const CarryRec *carry, const uint32_t *n, hipStream_t st) {
-  advance_writeback_kernel<<<2, 256, 0, st>>>(a, a.t, carry, n);
+  advance_writeback_kernel<<<2, ADV_THREADS, 0, st>>>(a, a.t, carry, n);
   return hipGetLastError();
 }
 

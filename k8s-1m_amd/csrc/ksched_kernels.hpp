@@ -58,6 +58,15 @@ struct RoundArgs {
   uint32_t seq;
   uint32_t stall_us;          // ks_debug_stall: the resolve holds its signal back this long (0: never)
   uint8_t *marks;             // [npods] per-pod round marks of the batch (ks_batch_marks): KS_MARK_*
+  // Identical pods (resource-only batches; null otherwise): pods of a round
+  // with byte-identical descriptors have identical lists, so only the first
+  // of each class in the round window is swept, merged, gathered and patched
+  // and the others read its record.  cls[i]: the batch index of pod i's
+  // first identical pod (host); per round (by parity), written by the
+  // advance kernel: rep[r] (the window's first pod of r's class), ulist
+  // (the representatives in window order) and nuniq (their count)
+  const uint32_t *cls;
+  uint32_t *rep, *ulist, *nuniq;
   BlockRec *brec;             // [local shards][P][bstride]
   uint64_t *srec;             // [S][P][rec_words(K)]
   uint64_t *frec;             // [P][rec_words(K)] (== srec when S == 1)
@@ -65,7 +74,8 @@ struct RoundArgs {
   CandRow *crow;              // [P][K] S0 rows of the final candidates
   CandExt *cext;              // [P][K] their label / taint columns (EXT batches)
   const uint32_t *slot_pos;   // slot -> position
-  uint64_t *counters;         // [0] rounds, [1] pods resolved, [2] pods swept, [3] wasted rounds
+  uint64_t *counters;         // [0] rounds, [1] pods resolved, [2] pods swept, [3] wasted rounds,
+                              // [4] FIX re-swept pods, [7] representatives swept (identical pods)
   Weights w;
 };
 

@@ -1,0 +1,117 @@
+"""Identical pods of a round swept once (RoundArgs::cls).
+
+Resource-only batches whose pods repeat byte-identical descriptors (the
+reference's own benchmark pods are all alike: kwok/make_pods/main.go:138-148
+creates request-less pods from one template) sweep, merge, gather and patch
+each class once per round window; every pod of the class reads that record.
+Parity: bit-exact results and node states against the CPU oracle, and against
+the same library with the deduplication switched off (KS_DEDUP=0), over
+duplicate densities from "every pod alike" to a few repeats, round geometries
+with early stops (short lists) and wasted speculative rounds, virtual shards,
+and calls split so that classes straddle round windows.
+"""
+import ctypes as C
+import os
+import random
+
+import numpy as np
+import pytest
+
+import pyoracle
+from helpers import assert_results_equal, res_array, states_np
+from ksched import Scheduler, _abi, synth
+
+pytestmark = pytest.mark.gpu
+
+
+def repeated(src, idx):
+    """A pod array whose pod j is a copy of src's pod idx[j]."""
+    arr = (_abi.KsPod * len(idx))()
+    for j, i in enumerate(idx):
+        arr[j] = src.pods[i]
+    return arr
+
+
+def run_pair(ns, n, pods, m, splits=1, dedup=True, **kw):
+    """libksched results + node states for `pods`, with or without dedup."""
+    old = os.environ.get("KS_DEDUP")
+    os.environ["KS_DEDUP"] = "1" if dedup else "0"
+    try:
+        s = Scheduler(n, **kw)
+    finally:
+        if old is None:
+            del os.environ["KS_DEDUP"]
+        else:
+            os.environ["KS_DEDUP"] = old
+    try:
+        s.upsert_nodes_raw(ns.nodes, synth.slot_array(n), n)
+        bounds = np.linspace(0, m, splits + 1).astype(int)
+        out = []
+        for b0, b1 in zip(bounds, bounds[1:]):
+            k = int(b1 - b0)
+            ptr = C.cast(C.addressof(pods) + int(b0) * C.sizeof(_abi.KsPod), C.POINTER(_abi.KsPod))
+            out.append(res_array(s.schedule_raw(ptr, k), k))
+        return np.concatenate(out), states_np(s.lib.ks_node_states, s.ctx, n)
+    finally:
+        s.close()
+
+
+def oracle_run(ns, n, pods, m):
+    o = pyoracle.Oracle(n)
+    o.upsert(ns.nodes, synth.slot_array(n), n)
+    ptr = C.cast(C.addressof(pods), C.POINTER(_abi.KsPod))
+    got = res_array(o.schedule(ptr, m), m)
+    return got, states_np(o.L.oracle_node_states, o.o, n)
+
+
+CASES = [
+    # node kind, nodes, pods, distinct shapes, P, K, virtual shards, splits
+    (synth.KWOK, 2000, 3000, 1, 256, 256, 1, 1),      # every pod alike (the published workload)
+    (synth.KWOK, 1500, 2000, 3, 64, 16, 2, 3),        # short lists: rounds stop early
+    (synth.HETERO, 3000, 2500, 8, 256, 256, 1, 2),
+    (synth.HETERO, 2048, 1800, 40, 100, 64, 3, 1),
+    (synth.HETERO, 700, 1200, 2, 256, 8, 1, 4),       # lists of 8: many wasted speculative rounds
+]
+
+
+@pytest.mark.parametrize("case", range(len(CASES)))
+def test_dedup_equals_oracle_and_undeduplicated(case):
+    kn, n, m, shapes, P, K, shards, splits = CASES[case]
+    ns = synth.nodes(kn, n, 31 + case)
+    src = synth.pods(synth.HETERO, max(shapes, 1), 41 + case)
+    r = random.Random(case)
+    idx = [r.randrange(shapes) for _ in range(m)]
+    pods = repeated(src, idx)
+    kw = dict(pods_per_round=P, topk=K, virtual_shards=shards)
+    got, gst = run_pair(ns, n, pods, m, splits, True, **kw)
+    ref, rst = run_pair(ns, n, pods, m, splits, False, **kw)
+    want, wst = oracle_run(ns, n, pods, m)
+    what = f"case {CASES[case]}"
+    assert_results_equal_np(got, want, f"{what} dedup vs oracle")
+    assert_results_equal_np(ref, want, f"{what} no dedup vs oracle")
+    assert np.array_equal(gst, wst), f"{what}: node states differ from the oracle"
+    assert np.array_equal(gst, rst), f"{what}: node states differ with / without dedup"
+
+
+def assert_results_equal_np(g, w, what):
+    if not np.array_equal(g, w):
+        bad = np.nonzero(g != w)[0]
+        i = int(bad[0])
+        raise AssertionError(f"{what}: {len(bad)}/{len(g)} results differ; first at pod {i}: got {g[i]} want {w[i]}")
+
+
+def test_besteffort_stream_vs_oracle():
+    # ksynth's request-less pods (the bench's kwok-be line) on prefilled kwok nodes
+    n, m = 4000, 6000
+    ns = synth.nodes(synth.KWOK, n, 5)
+    ps = synth.besteffort_pods(m)
+    pf = synth.prefill(synth.KWOK, n, 5, 6, 0.4)
+    o = pyoracle.Oracle(n)
+    o.upsert(ns.nodes, synth.slot_array(n), n)
+    o.add_pods(pf.pods, pf.slot_ptr, pf.n_pods)
+    with Scheduler(n) as s:
+        s.upsert_nodes_raw(ns.nodes, synth.slot_array(n), n)
+        assert s.lib.ks_pods_add(s.ctx, pf.pods, pf.slot_ptr, pf.n_pods) == 0, s.lib.ks_last_error(s.ctx)
+        assert_results_equal(s.schedule_raw(ps.pods, m), o.schedule(ps.pods, m), m, "best-effort stream")
+        assert np.array_equal(states_np(s.lib.ks_node_states, s.ctx, n),
+                              states_np(o.L.oracle_node_states, o.o, n))
