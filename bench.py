@@ -621,9 +621,9 @@ def report(args, sched, st, dbg, world, pods_timed, elapsed, scheduled, setup_s,
             "scheduled_fraction": round(scheduled / pods_timed, 4),
             "speculated_rounds_wasted": int(dbg[3]),  # since open (warmup included)
             "pods_reswept_wrong_norm_guess": int(dbg[4]),  # since open (warmup included)
-            # identical pods of a round swept once: class representatives
-            # swept / pods in the swept windows, since open (0: no duplicates or KS_DEDUP=0)
-            "sweep_representative_fraction": round(int(dbg[7]) / max(1, int(dbg[2])), 4),
+            # identical pods of a round swept once: pods swept (class
+            # representatives) / pods in the swept windows, since open
+            "sweep_representative_fraction": round(int(dbg[2]) / max(1, int(dbg[2]) + int(dbg[7])), 4),
             "node_evals_per_s": round(value * args.nodes, 1),
             "setup_s": round(setup_s, 2),
             "pmc_key": pmc_key(args, world),

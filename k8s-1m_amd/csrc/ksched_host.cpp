@@ -896,6 +896,23 @@ ks_status pod_requests(const ks_pod &p, bool non_missing, int64_t *cpu, int64_t 
 struct ProgBuf {
   std::vector<uint64_t> w;
   uint32_t size() const { return (uint32_t)w.size(); }
+  // Programs are content-addressed within a batch, so pods with identical
+  // programs get identical offsets (and byte-identical descriptors: the
+  // sweep's identical-pod classes, pod_classes).  intern(off): the words
+  // [off, size) were just appended; returns the offset of their first copy
+  // (dropping the new one), 0 for an empty program.
+  std::unordered_map<std::string, uint32_t> progs;
+  uint32_t intern(uint32_t off) {
+    if (off == size()) return 0;
+    std::string key((const char *)(w.data() + off), (size() - off) * 8);
+    auto it = progs.find(key);
+    if (it != progs.end()) {
+      w.resize(off);
+      return it->second;
+    }
+    progs.emplace(std::move(key), off);
+    return off;
+  }
 };
 
 inline void set_bit(uint64_t m[LW], uint32_t b) { m[b >> 6] |= 1ull << (b & 63); }
@@ -1179,6 +1196,7 @@ ks_status compile_pod(ks_ctx *c, const ks_pod &p, PodDev &d, ProgBuf &cl, bool c
     sel.emit(cl, 0);
     d.req_len = 1;
   }
+  d.req_off = cl.intern(d.req_off);
   d.solo_off = 0;
   {
     std::vector<std::string> names;
@@ -1196,6 +1214,7 @@ ks_status compile_pod(ks_ctx *c, const ks_pod &p, PodDev &d, ProgBuf &cl, bool c
           cl.w.push_back((uint64_t)it->second);
         }
         d.pre_len = cl.size() - d.pre_off;
+        d.pre_off = cl.intern(d.pre_off);
         d.prefilter_out = c->n_present - d.pre_len;
       }
       c->compile_used_names = true;
@@ -1227,6 +1246,7 @@ ks_status compile_pod(ks_ctx *c, const ks_pod &p, PodDev &d, ProgBuf &cl, bool c
     }
     if (d.pref_len) d.flags |= PF_NA;
   }
+  d.pref_off = cl.intern(d.pref_off);
   if ((c->hard_in_use & ~d.tol_hard) || d.name_slot != -1 || (d.flags & (PF_AFF | PF_TT | PF_NA)))
     d.flags |= PF_EXT;
   refine_guesses(c, d, cl);
@@ -2589,7 +2609,7 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k, uint32_t end) {
   a.clauses = b->d_clauses;
   a.marks = b->d_marks;
   const uint32_t q = k & 1u, pq = q ^ 1u;
-  c->dedup_used[q] = !b->ext && b->dups && c->dedup;
+  c->dedup_used[q] = b->dups && c->dedup;
   if (c->dedup_used[q]) {
     uint32_t *dd = c->d_dedup + (size_t)q * (2 * MAX_P + 4);
     a.cls = b->d_cls;
@@ -3837,7 +3857,7 @@ ks_status ks_batch_prepare(ks_ctx *c, const ks_pod *pods, uint32_t n, ks_batch *
     b->any_spread = true;
   }
   std::memcpy(b->h_pods, dev.data(), dev.size() * sizeof(PodDev));
-  b->dups = !ext && pod_classes(dev.data(), n, b->h_cls);
+  b->dups = pod_classes(dev.data(), n, b->h_cls);
   for (size_t i = 0; i < dev.size(); ++i) {
     b->h_pinv[2 * i] = dev[i].tt_guess ? 1.0 / (double)dev[i].tt_guess : 0.0;
     b->h_pinv[2 * i + 1] = dev[i].na_guess ? 1.0 / (double)dev[i].na_guess : 0.0;

@@ -298,7 +298,7 @@ void sweep_kernel(RoundArgs a) {
   // FIX mode: only the pods norm_check flagged (pod groups of MAX_PG)
   const bool fix = EXT && a.fix;
   // identical pods: the groups walk the round's representatives (ulist)
-  const bool dedup = !EXT && a.ulist != nullptr;
+  const bool dedup = !fix && a.ulist != nullptr;
   if (dedup) p1 = min(p1, start + uniform_u32(*a.nuniq));
   if (p0 >= p1 || blockIdx.x * NW >= kwaves) return;
   if (fix && uniform_u32(a.fix_group[blockIdx.y]) == 0) return;
@@ -737,10 +737,12 @@ __global__ __launch_bounds__(MAX_P) void norm_check_kernel(RoundArgs a) {
   __shared__ uint32_t s_wn[MAX_P / WAVE];
   const uint32_t start = uniform_u32(*a.sstart);
   const uint32_t r = threadIdx.x;
-  bool wrong = false;
+  bool wrong = false, listed = false;
   if (r < a.P && start + r < a.npods) {
     const PodDev &p = a.pods[start + r];
-    PodStat st = a.pstat[r];
+    // identical pods: the representative's measured maxima (only it was swept)
+    const uint32_t rr = a.rep != nullptr ? a.rep[r] : r;
+    PodStat st = a.pstat[rr];
     if (a.pstat_sweep) {  // sweep encoding: max raw + 1 over blocks with a feasible node
       st.any_feasible = st.tt_max != 0u;
       st.tt_max = st.tt_max ? st.tt_max - 1u : 0u;
@@ -758,15 +760,16 @@ __global__ __launch_bounds__(MAX_P) void norm_check_kernel(RoundArgs a) {
     a.norm_inv[2 * r + 1] = na ? 1.0 / (double)na : 0.0;
     a.fix_flag[r] = wrong ? 1u : 0u;
     if (wrong) mark_pod(a.marks, start + r, MARK_FIX);
+    listed = wrong && rr == r;  // the FIX sweep re-sweeps representatives
   }
   // compacted list of the flagged pods (round order): the FIX sweep runs
   // ceil(count / MAX_PG) pod groups, so node rows are re-read once per 64
   // flagged pods rather than once per 64-pod slice holding one
-  const uint64_t wb = __ballot(wrong);
-  const uint32_t nw = (uint32_t)__popcll(wb);
+  const uint64_t wb = __ballot(listed);
+  const uint32_t nw = (uint32_t)__popcll(wb), nwrong = (uint32_t)__popcll(__ballot(wrong));
   const uint32_t wid = threadIdx.x / WAVE, lane = threadIdx.x % WAVE;
   if (lane == 0) s_wn[wid] = nw;
-  if (nw && lane == 0) atomicAdd((unsigned long long *)&a.counters[4], (unsigned long long)nw);
+  if (nwrong && lane == 0) atomicAdd((unsigned long long *)&a.counters[4], (unsigned long long)nwrong);
   __syncthreads();
   uint32_t idx = (uint32_t)__popcll(wb & ((1ull << lane) - 1ull)), total = 0;
 #pragma unroll
@@ -774,7 +777,7 @@ __global__ __launch_bounds__(MAX_P) void norm_check_kernel(RoundArgs a) {
     idx += (uint32_t)w < wid ? s_wn[w] : 0u;
     total += s_wn[w];
   }
-  if (wrong) a.fix_list[idx] = r;
+  if (listed) a.fix_list[idx] = r;
   if (r >= total) a.fix_list[r] = FIX_NONE;
   if (r < MAX_P / MAX_PG) a.fix_group[r] = r * MAX_PG < total ? 1u : 0u;
 }
@@ -2123,7 +2126,10 @@ __device__ void dedup_round(const RoundArgs &a, uint32_t s) {
   if (u) a.ulist[idx] = t;
   if (t == 0) {
     *a.nuniq = total;
-    a.counters[7] += total;  // representatives swept
+    // counters[2] counts pods swept (the representatives), [7] the duplicates skipped
+    const uint32_t window = s < a.npods ? min(a.P, a.npods - s) : 0u;
+    a.counters[2] -= window - total;
+    a.counters[7] += window - total;
   }
 }
 

@@ -75,7 +75,8 @@ struct RoundArgs {
   CandExt *cext;              // [P][K] their label / taint columns (EXT batches)
   const uint32_t *slot_pos;   // slot -> position
   uint64_t *counters;         // [0] rounds, [1] pods resolved, [2] pods swept, [3] wasted rounds,
-                              // [4] FIX re-swept pods, [7] representatives swept (identical pods)
+                              // [4] FIX re-swept pods, [7] identical pods not swept (their class's
+                              // representative was; [2] counts representatives)
   Weights w;
 };
 

@@ -32,17 +32,20 @@ def repeated(src, idx):
     return arr
 
 
-def run_pair(ns, n, pods, m, splits=1, dedup=True, **kw):
-    """libksched results + node states for `pods`, with or without dedup."""
-    old = os.environ.get("KS_DEDUP")
-    os.environ["KS_DEDUP"] = "1" if dedup else "0"
+def run_pair(ns, n, pods, m, splits=1, dedup=True, env=None, **kw):
+    """libksched results + node states for `pods`, with or without dedup
+    (tuning switches are read from the environment when a context opens)."""
+    env = dict(env or {}, KS_DEDUP="1" if dedup else "0")
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
     try:
         s = Scheduler(n, **kw)
     finally:
-        if old is None:
-            del os.environ["KS_DEDUP"]
-        else:
-            os.environ["KS_DEDUP"] = old
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
     try:
         s.upsert_nodes_raw(ns.nodes, synth.slot_array(n), n)
         bounds = np.linspace(0, m, splits + 1).astype(int)
@@ -64,27 +67,34 @@ def oracle_run(ns, n, pods, m):
     return got, states_np(o.L.oracle_node_states, o.o, n)
 
 
+E = {"KS_TUPLE_GUESS": "0"}   # plain normaliser guesses: FIX re-sweeps happen
+M = {"KS_EARLY_FIX": "0"}     # normaliser maxima measured by the merge
 CASES = [
-    # node kind, nodes, pods, distinct shapes, P, K, virtual shards, splits
-    (synth.KWOK, 2000, 3000, 1, 256, 256, 1, 1),      # every pod alike (the published workload)
-    (synth.KWOK, 1500, 2000, 3, 64, 16, 2, 3),        # short lists: rounds stop early
-    (synth.HETERO, 3000, 2500, 8, 256, 256, 1, 2),
-    (synth.HETERO, 2048, 1800, 40, 100, 64, 3, 1),
-    (synth.HETERO, 700, 1200, 2, 256, 8, 1, 4),       # lists of 8: many wasted speculative rounds
+    # node kind, pod kind, nodes, pods, distinct shapes, P, K, virtual shards, splits, env
+    (synth.KWOK, synth.HETERO, 2000, 3000, 1, 256, 256, 1, 1, None),   # every pod alike (the published workload)
+    (synth.KWOK, synth.HETERO, 1500, 2000, 3, 64, 16, 2, 3, None),     # short lists: rounds stop early
+    (synth.HETERO, synth.HETERO, 3000, 2500, 8, 256, 256, 1, 2, None),
+    (synth.HETERO, synth.HETERO, 2048, 1800, 40, 100, 64, 3, 1, None),
+    (synth.HETERO, synth.HETERO, 700, 1200, 2, 256, 8, 1, 4, None),    # lists of 8: wasted speculative rounds
+    # labeled pods (EXT batches: taints, selectors, affinity, normalisation)
+    (synth.LABELED, synth.LABELED, 3000, 2000, 12, 256, 256, 1, 2, None),
+    (synth.LABELED, synth.LABELED, 2048, 1500, 30, 128, 64, 2, 1, E),
+    (synth.LABELED, synth.LABELED, 2500, 1500, 6, 256, 256, 1, 1, M),
+    (synth.LABELED, synth.LABELED, 1200, 1000, 4, 64, 16, 1, 3, E),
 ]
 
 
 @pytest.mark.parametrize("case", range(len(CASES)))
 def test_dedup_equals_oracle_and_undeduplicated(case):
-    kn, n, m, shapes, P, K, shards, splits = CASES[case]
+    kn, kp, n, m, shapes, P, K, shards, splits, env = CASES[case]
     ns = synth.nodes(kn, n, 31 + case)
-    src = synth.pods(synth.HETERO, max(shapes, 1), 41 + case)
+    src = synth.pods(kp, max(shapes, 1), 41 + case)
     r = random.Random(case)
     idx = [r.randrange(shapes) for _ in range(m)]
     pods = repeated(src, idx)
     kw = dict(pods_per_round=P, topk=K, virtual_shards=shards)
-    got, gst = run_pair(ns, n, pods, m, splits, True, **kw)
-    ref, rst = run_pair(ns, n, pods, m, splits, False, **kw)
+    got, gst = run_pair(ns, n, pods, m, splits, True, env, **kw)
+    ref, rst = run_pair(ns, n, pods, m, splits, False, env, **kw)
     want, wst = oracle_run(ns, n, pods, m)
     what = f"case {CASES[case]}"
     assert_results_equal_np(got, want, f"{what} dedup vs oracle")

@@ -45,9 +45,8 @@ print(sys.argv[2], d['value'], d.get('value_inputs_resident'), r.get('frac'), r.
 
 case $JOB in
   tests)
-    SEL=${1:+-k "$1"}
     timeout -k 10 1500 python -u -m pytest tests -m gpu -x -v --timeout ${PYTEST_TIMEOUT:-600} --timeout-method thread \
-      --durations=15 $SEL > gpurun_out/tests_gpu_$TAG.log 2>&1
+      --durations=15 ${1:+-k "$1"} > gpurun_out/tests_gpu_$TAG.log 2>&1
     rc=$?; tail -5 gpurun_out/tests_gpu_$TAG.log; echo "tests rc=$rc"
     [ $rc -eq 0 ] || exit $rc
     timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1
