@@ -1278,12 +1278,19 @@ __device__ __forceinline__ void race_probe_delay() {
 }
 #endif
 
-// Wave-uniform copy of an LDS object into scalar registers: one lane reads it
-// (a 64-lane broadcast read would cost the LDS 64x the bytes), readfirstlane
-// hands every dword to the SALU / VALU-operand side.
+// Wave-uniform copy of an LDS object: every lane reads it (one address: an
+// LDS broadcast, no bank conflicts).  Round 3: this replaced a copy read by
+// one lane and handed to the SALU by a readfirstlane per dword, which put
+// ~25 dependent readfirstlanes on the owner / eval waves' chains (resolve
+// 0.287 -> 0.279 ms per round on the 125k-node proxy, profiles/r3/bcast_ab/).
+// KS_POD_RFL: the old form (A/B builds only).
 template <class T>
 __device__ __forceinline__ T lds_uniform(const T &src, uint32_t lane) {
   static_assert(sizeof(T) % 4 == 0, "dword object");
+#ifndef KS_POD_RFL
+  (void)lane;
+  return src;
+#endif
   constexpr int N = sizeof(T) / 4;
   uint32_t tmp[N];
 #pragma unroll
@@ -1355,7 +1362,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
   __shared__ CandExt s_ocandx[EXT ? 2 : 1][EXT ? NCAND_OWN : 1];
   __shared__ uint64_t s_okey[2][NCAND_OWN];  // their keys for pod i, 0 = none
   __shared__ uint32_t s_oidx[2][NCAND_OWN];  // their owner indices
-  __shared__ int32_t s_dsum[2][RES_OWN_WAVES][NFILT + 3];
+  __shared__ alignas(16) int32_t s_dsum[2][RES_OWN_WAVES][NFILT + 3];
   // list staging (LDS-DMA targets): listed keys by pod mod KSLOTS; the chosen
   // rows by pod mod RSLOTS as [list wave][16-byte piece][candidate]
   __shared__ uint64_t s_keys[KSLOTS][MAX_K];
@@ -1367,9 +1374,9 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
   __shared__ RNode s_post[2][NCAND];
   __shared__ CandExt s_postx[EXT ? 2 : 1][EXT ? NCAND : 1];
   __shared__ uint64_t s_ekey[2][NCAND];
-  __shared__ int32_t s_edd[2][NCAND][NFILT + 3];
+  __shared__ alignas(16) int32_t s_edd[2][NCAND][NFILT + 3];
   // decider -> everyone: pod i's commit {valid, candidate lane, joins, owner index}
-  __shared__ uint32_t s_pend[2][4];
+  __shared__ alignas(16) uint32_t s_pend[2][4];
   // s_done[b]: set by the decider in an iteration of parity b, read by every
   // wave after that iteration's barrier.  Double-buffered: a single word let
   // the decider's next-iteration store (r == nround: immediately after the
