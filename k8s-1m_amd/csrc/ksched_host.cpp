@@ -363,7 +363,7 @@ struct ks_ctx {
   // KS_TUPLE_GUESS), so one process can open contexts with different settings
   // (tests do).
   bool early_fix = true;
-  bool dedup = true;        // KS_DEDUP: sweep identical pods of a round once (resource-only batches)
+  bool dedup = true;        // KS_DEDUP: sweep identical pods of a round once
   bool tuple_guess = true;  // normaliser guesses over node tuples (refine_guesses)
   uint32_t timing_every = 8, sweep_blocks = 8192, ext_npl = 2;
   // KS_EVENT_PROFILE=1: per event kind, runs / events / seconds of ks_events_apply (stderr at ks_close)

@@ -261,6 +261,21 @@ __device__ __forceinline__ uint32_t normalize_inv(uint32_t raw, double inv) {
 #define ABL_ON(b) true
 #endif
 
+// Bounded wall-clock wait (ks_debug_stall): s_memrealtime counts at 100 MHz.
+__device__ __forceinline__ void stall_for(uint32_t usec) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < 100ull * usec) __builtin_amdgcn_s_sleep(127);
+}
+
+// Kernel-side completion signal for a stream wait-value (release at system
+// scope, like the stream write operation it replaces).
+__device__ __forceinline__ void signal_done(uint32_t *flag, uint32_t seq, uint32_t stall_us = 0) {
+  if (flag == nullptr) return;
+  if (stall_us) stall_for(stall_us);
+  __threadfence_system();
+  __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // =================================================================== sweep
 // Normalising plugins (TaintToleration with PreferNoSchedule taints, NodeAffinity
 // preferred terms) score against max raw over the feasible nodes, which is
@@ -1333,20 +1348,6 @@ __device__ __forceinline__ uint64_t key_q(const PodDev &p, const PodQ &q, const 
   return pack_key(t, g.slot);
 }
 
-// Bounded wall-clock wait (ks_debug_stall): s_memrealtime counts at 100 MHz.
-__device__ __forceinline__ void stall_for(uint32_t usec) {
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  while (__builtin_amdgcn_s_memrealtime() - t0 < 100ull * usec) __builtin_amdgcn_s_sleep(127);
-}
-
-// Kernel-side completion signal for a stream wait-value (release at system
-// scope, like the stream write operation it replaces).
-__device__ __forceinline__ void signal_done(uint32_t *flag, uint32_t seq, uint32_t stall_us = 0) {
-  if (flag == nullptr) return;
-  if (stall_us) stall_for(stall_us);
-  __threadfence_system();
-  __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
 
 template <bool EXT, int LIST_SPAN>
 __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
@@ -1384,7 +1385,11 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
   // the loop one barrier early
   __shared__ uint32_t s_done[2], s_stop_at;
   // results of the round, written out after the loop (no global stores inside it)
-  __shared__ DevResult s_res[MAX_P];
+  // per pod: {winning key lo, hi, feasible nodes, status} (one 16-B store by
+  // the decider) and the failure counts (lanes of the decider); expanded into
+  // DevResults after the loop
+  __shared__ uint4 s_resc[MAX_P];
+  __shared__ uint32_t s_rfail[MAX_P][NFILT];
 
   // tid: hardware thread (staging loops); wid / rtid: the wave's role and the
   // thread's index in role order (list entry, owned node)
@@ -1650,21 +1655,9 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
             DONE(buf) = 1;
           }
         } else {
-          DevResult *res = &s_res[r];
-          if (lane == 0) {
-            res->node_index = win ? (int32_t)(0xFFFFFFFFu - (uint32_t)win) : -1;
-            res->status = status;
-            res->total_score = win ? (int64_t)(win >> 32) - 1 : 0;
-            res->feasible_nodes = feasible;
-            res->evaluated_nodes = a.evaluated;
-            res->flags = (win && feasible == 1) ? 1u : 0u;
-            res->prefiltered = s_pod[r].prefilter_out;
-            res->spread_fail = 0;
-            res->ipa_fail = 0;
-            res->_pad = 0;
-          }
+          if (lane == 0) s_resc[r] = make_uint4((uint32_t)win, (uint32_t)(win >> 32), feasible, (uint32_t)status);
           if (lane > (uint32_t)DSUM_LANE && lane <= (uint32_t)DSUM_LANE + NFILT)
-            res->fail_counts[lane - DSUM_LANE - 1] = hfail + (uint32_t)vd;
+            s_rfail[r][lane - DSUM_LANE - 1] = hfail + (uint32_t)vd;
 #if KS_STAMPS == 1
           STAMP_NOW(ts);
           sub[2] += ts - t2;
@@ -1714,12 +1707,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
           }
           pvalid = win ? 1u : 0u;
           pcand = cand;
-          if (lane == 0) {
-            s_pend[buf][0] = pvalid;
-            s_pend[buf][1] = cand;
-            s_pend[buf][2] = join;
-            s_pend[buf][3] = oidx;
-          }
+          if (lane == 0) *(uint4 *)&s_pend[buf][0] = make_uint4(pvalid, cand, join, oidx);
 #if KS_STAMPS == 1
           STAMP_NOW(ts);
           sub[3] += ts - t2;
@@ -2052,10 +2040,30 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
   if (wid == RES_DEC_WAVE && lane == 0) s_stop_at = stop_at;
   __syncthreads();
   {
+    // results of the round: 16 threads per pod, one dword of its DevResult each
     const uint32_t nres = s_stop_at;
-    const uint32_t *src = (const uint32_t *)s_res;
     uint32_t *dst = (uint32_t *)((DevResult *)a.results + start);
-    for (uint32_t i = tid; i < nres * (uint32_t)(sizeof(DevResult) / 4); i += RESOLVE_THREADS) dst[i] = src[i];
+    constexpr uint32_t RW32 = sizeof(DevResult) / 4;
+    for (uint32_t i = tid; i < nres * RW32; i += RESOLVE_THREADS) {
+      const uint32_t pr = i / RW32, w = i % RW32;
+      const uint4 c = s_resc[pr];
+      const uint64_t win = ((uint64_t)c.y << 32) | c.x;
+      const int64_t total = win ? (int64_t)(win >> 32) - 1 : 0;
+      uint32_t v;
+      switch (w) {
+        case 0: v = win ? 0xFFFFFFFFu - (uint32_t)win : 0xFFFFFFFFu; break;  // node_index (-1: none)
+        case 1: v = c.w; break;                                               // status
+        case 2: v = (uint32_t)total; break;                                  // total_score
+        case 3: v = (uint32_t)((uint64_t)total >> 32); break;
+        case 4: v = c.z; break;                                              // feasible_nodes
+        case 5: v = a.evaluated; break;                                      // evaluated_nodes
+        case 6: case 7: case 8: case 9: case 10: v = s_rfail[pr][w - 6]; break;  // fail_counts
+        case 13: v = s_pod[pr].prefilter_out; break;                         // prefiltered
+        case 14: v = (win && c.z == 1) ? 1u : 0u; break;                     // flags
+        default: v = 0; break;                                               // spread_fail, ipa_fail, _pad
+      }
+      dst[i] = v;
+    }
   }
   if (wid == RES_DEC_WAVE && lane == 0) {
 #ifdef KS_EXPT
