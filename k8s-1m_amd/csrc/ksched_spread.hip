@@ -46,6 +46,7 @@ constexpr uint32_t SP_LDS = 4096;     // LDS domain-histogram entries per block
 constexpr uint32_t SP_LDS_DOM = 1024; // keys with at most this many domains aggregate in LDS
 constexpr uint32_t SP_OFF_NONE = 0xFFFFFFFFu;
 constexpr int8_t SST_FEASIBLE = -1, SST_EMPTY = -2, SST_IGNORED = -3;  // per-position status
+constexpr int SP_BATCH = 4;           // positions per thread per step of the score / select passes
 
 // The pod's one-pod-path program (ksched_dev.hpp SoloHdr): SpreadDev, XResDev, ImageDev records.
 __device__ __forceinline__ const SoloHdr &solo_hdr(const SpreadArgs &a, const PodDev &p) {
@@ -446,6 +447,10 @@ __global__ __launch_bounds__(SP_THREADS) void spread_filter_kernel(SpreadArgs a)
     taint_needed |= (sd[c].flags & SP_TAINT) != 0;
   }
   const bool allkeys = p.flags & PF_SPREAD_ALLKEYS;
+  // label / taint columns (64 B per node) only for pods that read them: the
+  // EXT filter chain and normalising plugins, the spread policies' node
+  // affinity / taint checks, ImageLocality's "image present" bits
+  const bool need_ext = (p.flags & PF_EXT) || aff_needed || taint_needed || s_solo.h.n_img != 0;
   const uint32_t lane = threadIdx.x % WAVE, wid = threadIdx.x / WAVE;
   uint32_t fails[RF] = {0, 0, 0, 0, 0, 0, 0};
   uint32_t feasible = 0, ignored = 0, tt_max = 0, na_max = 0;
@@ -464,8 +469,8 @@ __global__ __launch_bounds__(SP_THREADS) void spread_filter_kernel(SpreadArgs a)
         if ((ad[q].kind & (AF_KIND | AF_NODE)) == (AF_SCORE | AF_NODE) && aff_count(a, ad[q], pos) &&
             a.dom[(size_t)ad[q].key * a.npos + pos] != DOM_NONE)
           score_any = true;
-    NodeExt e;
-    load_ext(a.t, pos, true, e);
+    NodeExt e{};
+    if (need_ext) load_ext(a.t, pos, true, e);
     bool all_s = true;
     for (uint32_t c = 0; c < n; ++c)
       if ((sd[c].flags & SP_SCORE) && a.dom[(size_t)sd[c].key * a.npos + pos] == DOM_NONE) all_s = false;
@@ -629,23 +634,44 @@ __global__ __launch_bounds__(SP_THREADS) void spread_score_kernel(SpreadArgs a) 
   }
   __syncthreads();
   uint64_t mn = ~0ull, mx = 0;
-  for (uint32_t pos = blockIdx.x * SP_THREADS + threadIdx.x; pos < a.npos; pos += grid_threads()) {
-    if (a.st[pos] != SST_FEASIBLE) continue;
-    double score = 0;
+  // SP_BATCH positions per thread per step (spans of SP_THREADS, coalesced):
+  // their loads are issued together, not one dependent chain per position
+  for (uint32_t base = blockIdx.x * SP_THREADS * SP_BATCH + threadIdx.x; base < a.npos;
+       base += grid_threads() * SP_BATCH) {
+    bool on[SP_BATCH];
+#pragma unroll
+    for (int u = 0; u < SP_BATCH; ++u) {
+      const uint32_t pos = base + u * SP_THREADS;
+      on[u] = pos < a.npos && a.st[pos] == SST_FEASIBLE;
+    }
+    double score[SP_BATCH];
+#pragma unroll
+    for (int u = 0; u < SP_BATCH; ++u) score[u] = 0;
     for (uint32_t c = 0; c < n; ++c) {
       const SpreadDev &q = sd[c];
       if (!(q.flags & SP_SCORE)) continue;
-      const uint32_t d = a.dom[(size_t)q.key * a.npos + pos];
-      if (d == DOM_NONE) continue;  // the node lacks the key: no term
-      uint32_t cnt;
-      if (q.flags & SP_HOST) cnt = q.cls == CLS_NONE ? 0u : a.cnt[(size_t)q.cls * a.npos + pos];
-      else cnt = a.dcnt[(size_t)c * a.dom_cap + d];
-      score += (double)cnt * s_w[c] + (double)(q.max_skew - 1);  // scoreForCount
+      uint32_t d[SP_BATCH], cnt[SP_BATCH];
+#pragma unroll
+      for (int u = 0; u < SP_BATCH; ++u) d[u] = on[u] ? a.dom[(size_t)q.key * a.npos + base + u * SP_THREADS] : DOM_NONE;
+#pragma unroll
+      for (int u = 0; u < SP_BATCH; ++u) {
+        cnt[u] = 0;
+        if (d[u] == DOM_NONE) continue;  // the node lacks the key: no term
+        if (q.flags & SP_HOST) cnt[u] = q.cls == CLS_NONE ? 0u : a.cnt[(size_t)q.cls * a.npos + base + u * SP_THREADS];
+        else cnt[u] = a.dcnt[(size_t)c * a.dom_cap + d[u]];
+      }
+#pragma unroll
+      for (int u = 0; u < SP_BATCH; ++u)
+        if (d[u] != DOM_NONE) score[u] += (double)cnt[u] * s_w[c] + (double)(q.max_skew - 1);  // scoreForCount
     }
-    const int64_t raw = (int64_t)round(score);
-    a.raw[pos] = raw;
-    mn = min(mn, (uint64_t)raw);
-    mx = max(mx, (uint64_t)raw);
+#pragma unroll
+    for (int u = 0; u < SP_BATCH; ++u) {
+      if (!on[u]) continue;
+      const int64_t raw = (int64_t)round(score[u]);
+      a.raw[base + u * SP_THREADS] = raw;
+      mn = min(mn, (uint64_t)raw);
+      mx = max(mx, (uint64_t)raw);
+    }
   }
   mn = wave_min64(mn);
   mx = wave_max64(mx);
@@ -687,27 +713,14 @@ __global__ __launch_bounds__(SP_THREADS) void spread_select_kernel(SpreadArgs a)
   const bool ipa_on = a.acc->score_any != 0;
   const int64_t imin = (int64_t)(tot.ipa_min - IPA_BIAS), idiff = (int64_t)(tot.ipa_max - tot.ipa_min);
   uint64_t best = 0;
-  for (uint32_t pos = blockIdx.x * SP_THREADS + threadIdx.x; pos < a.npos; pos += grid_threads()) {
-    const int8_t s = a.st[pos];
-    const uint32_t slot = a.pos_slot[pos];
-    if (s != SST_FEASIBLE && s != SST_IGNORED) {
-      if (a.dump && slot != SLOT_NONE) {
-        int32_t *o = a.dump + (size_t)slot * SPREAD_DUMP_WORDS;
-        for (int q = 0; q < SPREAD_DUMP_WORDS; ++q) o[q] = 0;
-        o[0] = s == SST_EMPTY ? ST_EMPTY : s;
-      }
-      continue;
-    }
+  // one feasible (or ignored) position: its total score, the packed key
+  auto select_one = [&](uint32_t pos, int8_t s, uint32_t slot, uint64_t pk, int64_t raw_in, int64_t ipa_in) {
     int64_t raw = 0, norm = 0;
-    if (has_score) {
-      if (s == SST_IGNORED) norm = 0;
-      else {
-        raw = a.raw[pos];
-        norm = pmax == 0 ? 100 : 100 * (pmax + pmin - raw) / pmax;
-      }
+    if (has_score && s != SST_IGNORED) {
+      raw = raw_in;
+      norm = pmax == 0 ? 100 : 100 * (pmax + pmin - raw) / pmax;
     }
     // total_score<true> from the packed parts (same terms, same order)
-    const uint64_t pk = a.part[pos];
     int64_t total = (int64_t)(uint32_t)pk;
     int64_t tt = 100;
     if (p.flags & PF_TT) tt = normalize((int64_t)((pk >> 32) & 0xFF), tt_max, true);
@@ -721,7 +734,7 @@ __global__ __launch_bounds__(SP_THREADS) void spread_select_kernel(SpreadArgs a)
     // InterPodAffinity NormalizeScore: int64(MaxNodeScore * float64(s - min) / float64(max - min))
     int64_t ipa_raw = 0, ipa = 0;
     if (ipa_on) {
-      ipa_raw = a.ipa_raw[pos];
+      ipa_raw = ipa_in;
       if (idiff > 0) ipa = (int64_t)(100.0 * ((double)(ipa_raw - imin) / (double)idiff));
     }
     total += (int64_t)a.w_ipa * ipa;
@@ -750,6 +763,40 @@ __global__ __launch_bounds__(SP_THREADS) void spread_select_kernel(SpreadArgs a)
     }
     const uint64_t k = pack_key(total, slot);
     best = k > best ? k : best;
+  };
+  // SP_BATCH positions per thread per step (spans of SP_THREADS, coalesced):
+  // their loads are issued together, not one dependent chain per position
+  for (uint32_t base = blockIdx.x * SP_THREADS * SP_BATCH + threadIdx.x; base < a.npos;
+       base += grid_threads() * SP_BATCH) {
+    int8_t sv[SP_BATCH];
+    uint32_t slv[SP_BATCH];
+    uint64_t pkv[SP_BATCH];
+    int64_t rawv[SP_BATCH], iprv[SP_BATCH];
+#pragma unroll
+    for (int u = 0; u < SP_BATCH; ++u) {
+      const uint32_t pos = base + u * SP_THREADS;
+      sv[u] = pos < a.npos ? a.st[pos] : SST_EMPTY;
+      slv[u] = pos < a.npos ? a.pos_slot[pos] : SLOT_NONE;
+    }
+#pragma unroll
+    for (int u = 0; u < SP_BATCH; ++u) {
+      const uint32_t pos = base + u * SP_THREADS;
+      const bool f = sv[u] == SST_FEASIBLE || sv[u] == SST_IGNORED;
+      pkv[u] = f ? a.part[pos] : 0ull;
+      rawv[u] = f && has_score && sv[u] == SST_FEASIBLE ? a.raw[pos] : 0;
+      iprv[u] = f && ipa_on ? a.ipa_raw[pos] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < SP_BATCH; ++u) {
+      const int8_t s = sv[u];
+      if (s == SST_FEASIBLE || s == SST_IGNORED) {
+        select_one(base + u * SP_THREADS, s, slv[u], pkv[u], rawv[u], iprv[u]);
+      } else if (a.dump && slv[u] != SLOT_NONE) {
+        int32_t *o = a.dump + (size_t)slv[u] * SPREAD_DUMP_WORDS;
+        for (int q = 0; q < SPREAD_DUMP_WORDS; ++q) o[q] = 0;
+        o[0] = s == SST_EMPTY ? ST_EMPTY : s;
+      }
+    }
   }
   best = wave_max64(best);
   if (threadIdx.x % WAVE == 0) s_r[threadIdx.x / WAVE] = best;
