@@ -3604,7 +3604,48 @@ static ks_status pods_delta(ks_ctx *c, const ks_pod *const *pods, const uint32_t
       for (uint32_t t : v) term_activate(c, t, 0, -1);
     }
   } hold{c, {}};
+  // Large logs (a burst's bound-pod deletions: ~150k pods): the per-pod work
+  // that reads only the pod and the slot maps runs on a few threads (it is
+  // memory-latency bound: scattered pod structs and slot entries).  Pods
+  // that need more (an interned label set other than a namespace's empty
+  // one, extended resources) and every error take the serial loop below,
+  // which then reproduces the first failure exactly.
+  std::vector<uint8_t> done(n, 0);
+  if (n >= 8192) {
+    const uint32_t T = std::min<uint32_t>(8, std::max(1u, std::thread::hardware_concurrency()));
+    std::vector<int64_t> affs(T, 0);
+    std::vector<std::thread> th;
+    for (uint32_t t = 0; t < T; ++t)
+      th.emplace_back([&, t] {
+        for (uint32_t i = (uint32_t)((uint64_t)n * t / T), e = (uint32_t)((uint64_t)n * (t + 1) / T); i < e; ++i) {
+          if (slots[i] >= c->cap || !c->present_map[slots[i]]) continue;
+          const ks_pod &pd = *pods[i];
+          if (pd.n_namespace_labels || pd.n_affinity_terms || pd.n_labels) continue;
+          bool ext = false;
+          for (uint32_t k = 0; k < pd.n_containers; ++k) ext |= pd.containers[k].n_extended != 0;
+          for (uint32_t k = 0; k < pd.n_init_containers; ++k) ext |= pd.init_containers[k].n_extended != 0;
+          if (ext) continue;
+          auto it = c->empty_set_of_ns.find(str(pd.ns));  // read-only here: no thread interns
+          if (it == c->empty_set_of_ns.end()) continue;
+          int64_t rc, rm, zc, zm;
+          if (pod_requests(pd, false, &rc, &rm) || pod_requests(pd, true, &zc, &zm)) continue;
+          sets[i] = it->second;
+          if (pd.unmodelled & KS_UNMODELLED_POD_AFFINITY) affs[t] += sign;
+          pos[i] = c->slot_pos[slots[i]];
+          int64_t *x = &d[(size_t)i * 5];
+          x[0] = sign * rc;
+          x[1] = sign * rm;
+          x[2] = sign * zc;
+          x[3] = sign * zm;
+          x[4] = sign;
+          done[i] = 1;
+        }
+      });
+    for (auto &t : th) t.join();
+    for (int64_t v : affs) aff += v;
+  }
   for (uint32_t i = 0; i < n; ++i) {
+    if (done[i]) continue;
     if (slots[i] >= c->cap || !c->present_map[slots[i]])
       return c->fail(KS_ERR_NOT_FOUND, "slot %u not present", slots[i]);
     int64_t rc, rm, zc, zm;
