@@ -365,7 +365,12 @@ struct ks_ctx {
   bool early_fix = true;
   bool dedup = true;        // KS_DEDUP: sweep identical pods of a round once
   bool tuple_guess = true;  // normaliser guesses over node tuples (refine_guesses)
-  uint32_t timing_every = 8, sweep_blocks = 8192, ext_npl = 2;
+  uint32_t timing_every = 8, ext_npl = 2;
+  // (block, pod group) pairs a sweep aims for: resource-only sweeps 4096
+  // (bigger pod groups amortise each block's row loads: C3 sweep 0.365 ->
+  // 0.356 ms, profiles/r3/sweep_blocks_ab/), label / taint sweeps 8192 (4096
+  // measured 2 % slower on C4); KS_SWEEP_BLOCKS sets both
+  uint32_t sweep_blocks = 4096, sweep_blocks_ext = 8192;
   // KS_EVENT_PROFILE=1: per event kind, runs / events / seconds of ks_events_apply (stderr at ks_close)
   bool ev_profile = false;
   // KS_RUN_PROFILE=1: seconds per phase of the batch runs (stderr at ks_close):
@@ -2583,7 +2588,7 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k, uint32_t end) {
   uint32_t bmax = 0;
   for (uint32_t q = 0; q < nloc; ++q) bmax = std::max(bmax, blocks_per_shard(c->shards[shard0 + q], sub));
   // pods per block: enough (block, pod-group) pairs to fill 256 CUs x 8 waves
-  const uint32_t want = c->sweep_blocks;
+  const uint32_t want = b->ext ? c->sweep_blocks_ext : c->sweep_blocks;
   const uint32_t total_blocks = bmax * nloc;
   uint32_t groups = (want + total_blocks - 1) / total_blocks;
   groups = std::max<uint32_t>(1, std::min(groups, c->P));
@@ -3140,7 +3145,7 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
     x->ev_profile = env_u("KS_EVENT_PROFILE", 0) != 0;
     x->run_profile = env_u("KS_RUN_PROFILE", 0) != 0;
     x->timing_every = (uint32_t)std::max(1, env_u("KS_TIMING_EVERY", 8));
-    x->sweep_blocks = (uint32_t)std::max(1, env_u("KS_SWEEP_BLOCKS", 8192));
+    if (std::getenv("KS_SWEEP_BLOCKS")) x->sweep_blocks = x->sweep_blocks_ext = (uint32_t)std::max(1, env_u("KS_SWEEP_BLOCKS", 8192));
     const int en = env_u("KS_EXT_NPL", 2);  // geometry experiments only
     x->ext_npl = (uint32_t)(en == 4 || en == 8 ? en : 2);
     x->sync_timeout_ms = (uint32_t)std::max(1, env_u("KS_SYNC_TIMEOUT_MS", 60000));
