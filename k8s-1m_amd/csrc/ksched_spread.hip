@@ -231,6 +231,64 @@ __device__ void lds_segments(const SpreadArgs &a, const SpreadDev *sd, uint32_t 
 
 __device__ __forceinline__ uint32_t grid_threads() { return gridDim.x * blockDim.x; }
 
+// A position's inputs of the node passes, every load issued before any branch:
+// the passes visit each position once, so the slot -> pod-count -> resource-row
+// chain of load_core (three dependent round trips through the memory system)
+// becomes one.  dm / kc: domain ids and selector-class counts of the pod's
+// first SP_PF constraints (kc only where `want_cnt`).
+constexpr int SP_PF = 4;
+struct PosIn {
+  uint32_t slot;
+  int32_t ap, np;
+  int64_t acpu, amem, rc, rm, zc, zm;
+  uint32_t dm[SP_PF], kc[SP_PF];
+};
+__device__ __forceinline__ void load_pos(const SpreadArgs &a, const SpreadDev *sd, uint32_t n, uint32_t want_cnt,
+                                         uint32_t pos, bool core, PosIn &v) {
+  v.slot = a.pos_slot[pos];
+  v.ap = a.t.apods[pos];
+  if (core) {
+    v.np = a.t.npods[pos];
+    v.acpu = a.t.acpu[pos];
+    v.amem = a.t.amem[pos];
+    v.rc = a.t.rcpu[pos];
+    v.rm = a.t.rmem[pos];
+    v.zc = a.t.zcpu[pos];
+    v.zm = a.t.zmem[pos];
+  }
+#pragma unroll
+  for (int c = 0; c < SP_PF; ++c) {
+    v.dm[c] = (uint32_t)c < n ? a.dom[(size_t)sd[c].key * a.npos + pos] : DOM_NONE;
+    v.kc[c] = (uint32_t)c < n && ((want_cnt >> c) & 1u) ? a.cnt[(size_t)sd[c].cls * a.npos + pos] : 0u;
+  }
+  // the values are needed before the first branch: no load sinks below it
+  asm volatile("" ::"v"(v.slot), "v"(v.ap), "v"(v.dm[0]), "v"(v.dm[1]), "v"(v.dm[2]), "v"(v.dm[3]), "v"(v.kc[0]),
+               "v"(v.kc[1]), "v"(v.kc[2]), "v"(v.kc[3]));
+  if (core) asm volatile("" ::"v"(v.np), "v"(v.acpu), "v"(v.amem), "v"(v.rc), "v"(v.rm), "v"(v.zc), "v"(v.zm));
+}
+// Domain id of constraint c at the position (prefetched for c < SP_PF).
+__device__ __forceinline__ uint32_t pos_dom(const SpreadArgs &a, const SpreadDev *sd, const PosIn &v, uint32_t c,
+                                            uint32_t pos) {
+  if (c >= (uint32_t)SP_PF) return a.dom[(size_t)sd[c].key * a.npos + pos];
+  uint32_t d = v.dm[0];
+#pragma unroll
+  for (int k = 1; k < SP_PF; ++k) d = c == (uint32_t)k ? v.dm[k] : d;
+  return d;
+}
+// Selector-class count of constraint c at the position (prefetched where want_cnt).
+__device__ __forceinline__ uint32_t pos_cnt(const SpreadArgs &a, const SpreadDev *sd, const PosIn &v, uint32_t c,
+                                            uint32_t pos) {
+  if (c >= (uint32_t)SP_PF) return a.cnt[(size_t)sd[c].cls * a.npos + pos];
+  uint32_t k = v.kc[0];
+#pragma unroll
+  for (int q = 1; q < SP_PF; ++q) k = c == (uint32_t)q ? v.kc[q] : k;
+  return k;
+}
+__device__ __forceinline__ void pos_regs(const SpreadArgs &a, uint32_t pos, const PosIn &v, NodeRegs &r) {
+  if (v.ap < 0) load_core(a.t, pos, v.slot, false, r);  // empty slot: load_core's benign values, no loads
+  else r = make_regs(v.acpu, v.amem, v.rc, v.rm, v.zc, v.zm, v.ap, v.np, v.slot);
+}
+
 // Totals of the accumulator copies (ACC_SHARDS) written by the previous passes.
 struct Totals {
   uint32_t fail[NFILT + 2];
@@ -289,10 +347,15 @@ __global__ __launch_bounds__(SP_THREADS) void spread_prep_kernel(SpreadArgs a) {
     aff_needed |= (sd[c].flags & SP_AFF) && (p.flags & PF_AFF);
     taint_needed |= (sd[c].flags & SP_TAINT) != 0;
   }
+  uint32_t want_cnt = 0;  // DoNotSchedule counts this pass takes per node
+  for (uint32_t c = 0; c < n && c < (uint32_t)SP_PF; ++c)
+    if (!(sd[c].flags & SP_SCORE) && sd[c].cls != CLS_NONE) want_cnt |= 1u << c;
   bool any_aff = false, any_score = false;
   for (uint32_t pos = blockIdx.x * SP_THREADS + threadIdx.x; pos < a.npos; pos += grid_threads()) {
-    const uint32_t slot = a.pos_slot[pos];
-    if (slot == SLOT_NONE || a.t.apods[pos] < 0) continue;
+    PosIn in;
+    load_pos(a, sd, n, want_cnt, pos, false, in);
+    const uint32_t slot = in.slot;
+    if (slot == SLOT_NONE || in.ap < 0) continue;
     for (uint32_t r = 0; r < na; ++r) {
       const AffDev &q = ad[r];
       const uint32_t kind = q.kind & AF_KIND;
@@ -312,13 +375,13 @@ __global__ __launch_bounds__(SP_THREADS) void spread_prep_kernel(SpreadArgs a) {
     const bool taint_ok = !taint_needed || (e.hard & ~p.tol_hard & ~UNSCHED_BIT) == 0;
     bool all_f = true;
     for (uint32_t c = 0; c < n; ++c)
-      if (!(sd[c].flags & SP_SCORE) && a.dom[(size_t)sd[c].key * a.npos + pos] == DOM_NONE) all_f = false;
+      if (!(sd[c].flags & SP_SCORE) && pos_dom(a, sd, in, c, pos) == DOM_NONE) all_f = false;
     if (!all_f) continue;
     for (uint32_t c = 0; c < n; ++c) {
       const SpreadDev &s = sd[c];
       if ((s.flags & SP_SCORE) || ((s.flags & SP_AFF) && !aff_ok) || ((s.flags & SP_TAINT) && !taint_ok)) continue;
-      const uint32_t d = a.dom[(size_t)s.key * a.npos + pos];
-      const uint32_t k = s.cls == CLS_NONE ? 0u : a.cnt[(size_t)s.cls * a.npos + pos];
+      const uint32_t d = pos_dom(a, sd, in, c, pos);
+      const uint32_t k = s.cls == CLS_NONE ? 0u : pos_cnt(a, sd, in, c, pos);
       if (s_off[c] != SP_OFF_NONE) {
         const uint32_t e = s_off[c] + d;
         if (k) atomicAdd(&s_h[e], k);
@@ -414,6 +477,7 @@ __global__ __launch_bounds__(SP_THREADS) void spread_filter_kernel(SpreadArgs a)
   __shared__ uint32_t s_seen[SP_LDS / 32];
   __shared__ uint32_t s_h[SP_LDS];
   __shared__ uint32_t s_off[MAX_SPREAD];
+  __shared__ uint32_t s_minm[MAX_SPREAD];
   __shared__ uint32_t s_red[SP_THREADS / WAVE][R_N];
   __shared__ uint64_t s_r64[SP_THREADS / WAVE][2];
   __shared__ SoloLds s_solo;
@@ -425,6 +489,22 @@ __global__ __launch_bounds__(SP_THREADS) void spread_filter_kernel(SpreadArgs a)
   const SpreadDev *sd = s_solo.sd;
   const uint32_t n = s_solo.h.n_spread;
   if (threadIdx.x == 0) lds_segments(a, sd, n, s_off);
+  __syncthreads();
+  // DoNotSchedule constraints: the prep pass's domain counts (low-cardinality
+  // keys: into their s_h segments, which only ScheduleAnyway constraints
+  // accumulate into) and minMatchNum, read per node by the skew check
+  for (uint32_t c = 0; c < n; ++c) {
+    if ((sd[c].flags & SP_SCORE) || s_off[c] == SP_OFF_NONE) continue;
+    for (uint32_t d = threadIdx.x; d < a.ndom[sd[c].key]; d += SP_THREADS)
+      s_h[s_off[c] + d] = a.dcnt[(size_t)c * a.dom_cap + d];
+  }
+  if (threadIdx.x < n && !(sd[threadIdx.x].flags & SP_SCORE)) {
+    const uint32_t c = threadIdx.x;
+    s_minm[c] = a.acc->ndomains[c] < (uint32_t)sd[c].min_domains ? 0u : a.acc->min_match[c];
+  }
+  uint32_t want_cnt = 0;  // ScheduleAnyway counts this pass takes per node
+  for (uint32_t c = 0; c < n && c < (uint32_t)SP_PF; ++c)
+    if ((sd[c].flags & (SP_SCORE | SP_HOST)) == SP_SCORE && sd[c].cls != CLS_NONE) want_cnt |= 1u << c;
   __syncthreads();
   const uint32_t n_xres = s_solo.h.n_xres;
   const AffDev *ad = s_solo.ad;
@@ -456,10 +536,12 @@ __global__ __launch_bounds__(SP_THREADS) void spread_filter_kernel(SpreadArgs a)
   uint32_t feasible = 0, ignored = 0, tt_max = 0, na_max = 0;
   uint64_t ipa_mn = ~0ull, ipa_mx = 0;
   for (uint32_t pos = blockIdx.x * SP_THREADS + threadIdx.x; pos < a.npos; pos += grid_threads()) {
-    const uint32_t slot = a.pos_slot[pos];
+    PosIn in;
+    load_pos(a, sd, n, want_cnt, pos, true, in);
+    const uint32_t slot = in.slot;
     if (slot == SLOT_NONE) continue;
     NodeRegs r;
-    load_core(a.t, pos, slot, true, r);
+    pos_regs(a, pos, in, r);
     if (!(r.bits & 1u)) {
       a.st[pos] = SST_EMPTY;
       continue;
@@ -473,7 +555,7 @@ __global__ __launch_bounds__(SP_THREADS) void spread_filter_kernel(SpreadArgs a)
     if (need_ext) load_ext(a.t, pos, true, e);
     bool all_s = true;
     for (uint32_t c = 0; c < n; ++c)
-      if ((sd[c].flags & SP_SCORE) && a.dom[(size_t)sd[c].key * a.npos + pos] == DOM_NONE) all_s = false;
+      if ((sd[c].flags & SP_SCORE) && pos_dom(a, sd, in, c, pos) == DOM_NONE) all_s = false;
     if (any_s && (!allkeys || all_s)) {
       // PreScore counts (scoring.go#PreScore processAllNode) of this node
       const bool aff_ok = !aff_needed || !(p.flags & PF_AFF) || required_match(p, a.clauses, e, slot);
@@ -483,9 +565,9 @@ __global__ __launch_bounds__(SP_THREADS) void spread_filter_kernel(SpreadArgs a)
         if (!(q.flags & SP_SCORE) || (q.flags & SP_HOST) || ((q.flags & SP_AFF) && !aff_ok) ||
             ((q.flags & SP_TAINT) && !taint_ok))
           continue;
-        uint32_t d = a.dom[(size_t)q.key * a.npos + pos];
+        uint32_t d = pos_dom(a, sd, in, c, pos);
         if (d == DOM_NONE) d = 0;
-        const uint32_t k = q.cls == CLS_NONE ? 0u : a.cnt[(size_t)q.cls * a.npos + pos];
+        const uint32_t k = q.cls == CLS_NONE ? 0u : pos_cnt(a, sd, in, c, pos);
         if (!k) continue;
         if (s_off[c] != SP_OFF_NONE) atomicAdd(&s_h[s_off[c] + d], k);
         else atomicAdd(&a.dcnt[(size_t)c * a.dom_cap + d], k);
@@ -504,13 +586,13 @@ __global__ __launch_bounds__(SP_THREADS) void spread_filter_kernel(SpreadArgs a)
       for (uint32_t c = 0; c < n; ++c) {
         const SpreadDev &q = sd[c];
         if (q.flags & SP_SCORE) continue;
-        const uint32_t d = a.dom[(size_t)q.key * a.npos + pos];
+        const uint32_t d = pos_dom(a, sd, in, c, pos);
         if (d == DOM_NONE) {
           s = PLUGIN_SPREAD;  // ErrReasonNodeLabelNotMatch
           break;
         }
-        const uint32_t minm = a.acc->ndomains[c] < (uint32_t)q.min_domains ? 0u : a.acc->min_match[c];
-        const int64_t skew = (int64_t)a.dcnt[(size_t)c * a.dom_cap + d] + ((q.flags & SP_SELF) ? 1 : 0) - (int64_t)minm;
+        const uint32_t dc = s_off[c] != SP_OFF_NONE ? s_h[s_off[c] + d] : a.dcnt[(size_t)c * a.dom_cap + d];
+        const int64_t skew = (int64_t)dc + ((q.flags & SP_SELF) ? 1 : 0) - (int64_t)s_minm[c];
         if (skew > (int64_t)q.max_skew) {
           s = PLUGIN_SPREAD;  // ErrReasonConstraintsNotMatch
           break;
@@ -544,7 +626,7 @@ __global__ __launch_bounds__(SP_THREADS) void spread_filter_kernel(SpreadArgs a)
         for (uint32_t c = 0; c < n; ++c) {
           const SpreadDev &q = sd[c];
           if (!(q.flags & SP_SCORE) || (q.flags & SP_HOST)) continue;
-          uint32_t d = a.dom[(size_t)q.key * a.npos + pos];
+          uint32_t d = pos_dom(a, sd, in, c, pos);
           if (d == DOM_NONE) d = 0;
           if (s_off[c] != SP_OFF_NONE) {
             const uint32_t bit = s_off[c] + d, m = 1u << (bit & 31);
