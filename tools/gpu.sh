@@ -8,6 +8,7 @@
 #                                             (each -> gpurun_out/bench_TAG_<line>.json)
 #   tools/gpu.sh trace TAG [bench args]       rocprofv3 --kernel-trace --stats of a short bench run
 #   tools/gpu.sh pmc TAG [bench args]         PMC passes of one configuration -> gpurun_out/pmc/<key>.json
+#   tools/gpu.sh sq TAG [bench args]          SQ counters per kernel of one short bench run
 #   tools/gpu.sh ab TAG [bench args]          A/B: default library vs lib/alt (or ALT_ENV="VAR=value"), twice each
 #   tools/gpu.sh variants TAG [bench args]    VARIANTS="default expt2 ..." one configuration on several lib/<name> builds
 #   tools/gpu.sh stamps TAG [kind]            resolve-phase stamps (make stamps stamps2 stamps3 first)
@@ -95,6 +96,17 @@ PY
       [ $rc -eq 0 ] || { tail -5 "$OUT/p$i.err"; exit $rc; }
     done
     python3 tools/pmc_summary.py "$OUT" --tag "$TAG" --out-dir "$R/gpurun_out/pmc" ;;
+  sq)
+    # SQ counters per kernel of one short bench run (e.g. the one-pod path:
+    # tools/gpu.sh sq TAG --kind zoned --pods spread --batch 128); value sync
+    # off as in pmc, small batches: per-dispatch collection slows every launch
+    export KS_VALUE_SYNC=0
+    mkdir -p gpurun_out/sq_$TAG
+    timeout -s KILL 170 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_WAVES SQ_WAVE_CYCLES \
+      SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU -d "$R/gpurun_out/sq_$TAG/p1" -o run --output-format csv -- \
+      python3 "$R/bench.py" --steps 1 --warmup 1 --no-cpu-baseline --no-resident --latency-calls 0 "$@" \
+      > gpurun_out/sq_$TAG/p1.json 2> gpurun_out/sq_$TAG/p1.err
+    rc=$?; echo "sq rc=$rc"; exit $rc ;;
   ab)
     for v in new alt new alt; do
       if [ $v = alt ]; then
