@@ -368,9 +368,10 @@ struct ks_ctx {
   uint32_t timing_every = 8, ext_npl = 2;
   // (block, pod group) pairs a sweep aims for: resource-only sweeps 4096
   // (bigger pod groups amortise each block's row loads: C3 sweep 0.365 ->
-  // 0.356 ms, profiles/r3/sweep_blocks_ab/), label / taint sweeps 8192 (4096
-  // measured 2 % slower on C4); KS_SWEEP_BLOCKS sets both
-  uint32_t sweep_blocks = 4096, sweep_blocks_ext = 8192;
+  // 0.356 ms, profiles/r3/sweep_blocks_ab/), label / taint sweeps 16384
+  // (C4 sweep 1.117 -> 1.102 ms; 4096 measured 2 % slower than 8192, 32768
+  // no better: profiles/r3/sweep_blocks_ab/c4_*); KS_SWEEP_BLOCKS sets both
+  uint32_t sweep_blocks = 4096, sweep_blocks_ext = 16384;
   // KS_EVENT_PROFILE=1: per event kind, runs / events / seconds of ks_events_apply (stderr at ks_close)
   bool ev_profile = false;
   // KS_RUN_PROFILE=1: seconds per phase of the batch runs (stderr at ks_close):
