@@ -2190,6 +2190,7 @@ uint32_t solo_passes(const SoloHdr *hd) {
                                                       hd->n_xres * sizeof(XResDev) + hd->n_img * sizeof(ImageDev));
   for (uint32_t k = 0; k < hd->n_aff; ++k)
     if ((ad[k].kind & AF_KIND) != AF_OWN && !(ad[k].kind & AF_NODE)) f |= SPL_PREP;
+  if (hd->n_aff) f |= SPL_AFF;  // the filter variant that reads the records
   return f;
 }
 

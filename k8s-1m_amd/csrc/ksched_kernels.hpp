@@ -97,7 +97,7 @@ constexpr uint32_t SLOT_NONE = 0xFFFFFFFFu;  // position holding no slot (shard 
 constexpr int SPREAD_DUMP_WORDS = 14;
 // launch_spread_pod passes: prep (PodTopologySpread DoNotSchedule counts,
 // InterPodAffinity domain counts), min (criticalPaths), score (ScheduleAnyway)
-enum SpreadLaunch : uint32_t { SPL_PREP = 1u, SPL_MIN = 2u, SPL_SCORE = 4u };
+enum SpreadLaunch : uint32_t { SPL_PREP = 1u, SPL_MIN = 2u, SPL_SCORE = 4u, SPL_AFF = 8u /* InterPodAffinity records */ };
 struct SpreadArgs {
   NodeTable t;
   const uint32_t *pos_slot;   // position -> slot (SLOT_NONE: padding)

@@ -77,22 +77,57 @@ constexpr uint64_t IPA_BIAS = 1ull << 63;  // signed raw scores as unsigned min 
 // matches its own terms), no required anti-affinity match in the node's
 // domains, no bound pod's required anti-affinity term matching the pod there.
 // Domain sum of record r at a position whose domain is d (!= DOM_NONE).
-__device__ __forceinline__ uint32_t aff_sum(const SpreadArgs &a, const AffDev &q, uint32_t r, uint32_t pos, uint32_t d) {
-  return (q.kind & AF_NODE) ? aff_count(a, q, pos) : a.adcnt[(size_t)r * a.dom_cap + d];
+// The filter pass's view of the records at one position: domain sums of the
+// low-cardinality records staged in LDS (aoff: segment per record or
+// SP_OFF_NONE), the first AF_PF records' domain ids and per-node counts
+// loaded with the position's other inputs.
+constexpr int AF_PF = 4;
+struct AffView {
+  const uint32_t *aoff, *lds;
+  uint32_t dm[AF_PF], nc[AF_PF];
+};
+__device__ __forceinline__ uint32_t aff_dom(const SpreadArgs &a, const AffDev *ad, const AffView &v, uint32_t r,
+                                            uint32_t pos) {
+  if (r >= (uint32_t)AF_PF) return a.dom[(size_t)ad[r].key * a.npos + pos];
+  uint32_t d = v.dm[0];
+#pragma unroll
+  for (int k = 1; k < AF_PF; ++k) d = r == (uint32_t)k ? v.dm[k] : d;
+  return d;
+}
+__device__ __forceinline__ uint32_t aff_sum(const SpreadArgs &a, const AffDev *ad, const AffView &v, uint32_t r,
+                                            uint32_t pos, uint32_t d) {
+  const AffDev &q = ad[r];
+  if (q.kind & AF_NODE) {
+    if (r >= (uint32_t)AF_PF) return aff_count(a, q, pos);
+    uint32_t c = v.nc[0];
+#pragma unroll
+    for (int k = 1; k < AF_PF; ++k) c = r == (uint32_t)k ? v.nc[k] : c;
+    return c;
+  }
+  const uint32_t o = v.aoff[r];
+  return o != SP_OFF_NONE ? v.lds[o + d] : a.adcnt[(size_t)r * a.dom_cap + d];
+}
+__device__ __forceinline__ void aff_prefetch(const SpreadArgs &a, const AffDev *ad, uint32_t na, uint32_t pos,
+                                             AffView &v) {
+#pragma unroll
+  for (int r = 0; r < AF_PF; ++r) {
+    v.dm[r] = (uint32_t)r < na ? a.dom[(size_t)ad[r].key * a.npos + pos] : DOM_NONE;
+    v.nc[r] = (uint32_t)r < na && (ad[r].kind & AF_NODE) ? aff_count(a, ad[r], pos) : 0u;
+  }
 }
 
-__device__ __forceinline__ bool ipa_fits(const SpreadArgs &a, const AffDev *ad, uint32_t na, uint32_t pos,
-                                         bool first_ok) {
+__device__ __forceinline__ bool ipa_fits(const SpreadArgs &a, const AffDev *ad, uint32_t na, const AffView &v,
+                                         uint32_t pos, bool first_ok) {
   bool has_req = false, exist = true;
   for (uint32_t r = 0; r < na; ++r) {
     const uint32_t kind = ad[r].kind & AF_KIND;
     if (kind > AF_EXIST_ANTI) continue;
-    const uint32_t d = a.dom[(size_t)ad[r].key * a.npos + pos];
+    const uint32_t d = aff_dom(a, ad, v, r, pos);
     if (kind == AF_REQ_AFF) {
       has_req = true;
       if (d == DOM_NONE) return false;  // all topology labels must exist on the node
-      if (!aff_sum(a, ad[r], r, pos, d)) exist = false;
-    } else if (d != DOM_NONE && aff_sum(a, ad[r], r, pos, d)) {
+      if (!aff_sum(a, ad, v, r, pos, d)) exist = false;
+    } else if (d != DOM_NONE && aff_sum(a, ad, v, r, pos, d)) {
       return false;
     }
   }
@@ -100,12 +135,13 @@ __device__ __forceinline__ bool ipa_fits(const SpreadArgs &a, const AffDev *ad, 
 }
 
 // interpodaffinity Score: Σ topologyScore[key][node's value].
-__device__ __forceinline__ int64_t ipa_raw_score(const SpreadArgs &a, const AffDev *ad, uint32_t na, uint32_t pos) {
+__device__ __forceinline__ int64_t ipa_raw_score(const SpreadArgs &a, const AffDev *ad, uint32_t na, const AffView &v,
+                                                 uint32_t pos) {
   int64_t raw = 0;
   for (uint32_t r = 0; r < na; ++r) {
     if ((ad[r].kind & AF_KIND) != AF_SCORE) continue;
-    const uint32_t d = a.dom[(size_t)ad[r].key * a.npos + pos];
-    if (d != DOM_NONE) raw += (int64_t)ad[r].weight * (int64_t)aff_sum(a, ad[r], r, pos, d);
+    const uint32_t d = aff_dom(a, ad, v, r, pos);
+    if (d != DOM_NONE) raw += (int64_t)ad[r].weight * (int64_t)aff_sum(a, ad, v, r, pos, d);
   }
   return raw;
 }
@@ -352,6 +388,15 @@ __global__ __launch_bounds__(SP_THREADS) void spread_prep_kernel(SpreadArgs a) {
     if (!(sd[c].flags & SP_SCORE) && sd[c].cls != CLS_NONE) want_cnt |= 1u << c;
   bool any_aff = false, any_score = false;
   for (uint32_t pos = blockIdx.x * SP_THREADS + threadIdx.x; pos < a.npos; pos += grid_threads()) {
+    // the first AF_PF summed records' counts and domain ids, loaded with the
+    // position's other inputs
+    uint32_t pv[AF_PF], pd[AF_PF];
+#pragma unroll
+    for (int r = 0; r < AF_PF; ++r) {
+      const bool summed = (uint32_t)r < na && (ad[r].kind & AF_KIND) != AF_OWN && !(ad[r].kind & AF_NODE);
+      pv[r] = summed ? aff_count(a, ad[r], pos) : 0u;
+      pd[r] = summed ? a.dom[(size_t)ad[r].key * a.npos + pos] : DOM_NONE;
+    }
     PosIn in;
     load_pos(a, sd, n, want_cnt, pos, false, in);
     const uint32_t slot = in.slot;
@@ -360,9 +405,15 @@ __global__ __launch_bounds__(SP_THREADS) void spread_prep_kernel(SpreadArgs a) {
       const AffDev &q = ad[r];
       const uint32_t kind = q.kind & AF_KIND;
       if (kind == AF_OWN || (q.kind & AF_NODE)) continue;  // per-node records: read in place
-      const uint32_t v = aff_count(a, q, pos);
+      uint32_t v = pv[0], d = pd[0];
+#pragma unroll
+      for (int k = 1; k < AF_PF; ++k) {
+        v = r == (uint32_t)k ? pv[k] : v;
+        d = r == (uint32_t)k ? pd[k] : d;
+      }
+      if (r >= (uint32_t)AF_PF) v = aff_count(a, q, pos);
       if (!v) continue;
-      const uint32_t d = a.dom[(size_t)q.key * a.npos + pos];
+      if (r >= (uint32_t)AF_PF) d = a.dom[(size_t)q.key * a.npos + pos];
       if (d == DOM_NONE) continue;  // no topology pair for this node
       any_aff |= kind == AF_REQ_AFF;
       any_score |= kind == AF_SCORE;
@@ -473,10 +524,14 @@ __device__ __forceinline__ uint64_t pack_part(uint32_t base, uint32_t tt_raw, ui
 // feasible / ignored counts and the normaliser maxima.
 constexpr int RF = NFILT + 2, R_FEAS = RF, R_IGN = RF + 1, R_TT = RF + 2, R_NA = RF + 3, R_N = RF + 4;
 
+// AFF: the pod has InterPodAffinity records (SPL_AFF); the variant without
+// them keeps their prefetched values out of the registers of spread pods.
+template <bool AFF>
 __global__ __launch_bounds__(SP_THREADS) void spread_filter_kernel(SpreadArgs a) {
   __shared__ uint32_t s_seen[SP_LDS / 32];
   __shared__ uint32_t s_h[SP_LDS];
   __shared__ uint32_t s_off[MAX_SPREAD];
+  __shared__ uint32_t s_aoff[MAX_AFF];
   __shared__ uint32_t s_minm[MAX_SPREAD];
   __shared__ uint32_t s_red[SP_THREADS / WAVE][R_N];
   __shared__ uint64_t s_r64[SP_THREADS / WAVE][2];
@@ -488,8 +543,15 @@ __global__ __launch_bounds__(SP_THREADS) void spread_filter_kernel(SpreadArgs a)
   __syncthreads();
   const SpreadDev *sd = s_solo.sd;
   const uint32_t n = s_solo.h.n_spread;
-  if (threadIdx.x == 0) lds_segments(a, sd, n, s_off);
+  if (threadIdx.x == 0) lds_segments(a, sd, n, s_off, s_solo.ad, AFF ? s_solo.h.n_aff : 0u, s_aoff);
   __syncthreads();
+  // InterPodAffinity domain sums of the low-cardinality records (the prep
+  // pass's), read per node by the checks and the raw score
+  for (uint32_t r = 0; r < (AFF ? s_solo.h.n_aff : 0u); ++r) {
+    if (s_aoff[r] == SP_OFF_NONE) continue;
+    for (uint32_t d = threadIdx.x; d < a.ndom[s_solo.ad[r].key]; d += SP_THREADS)
+      s_h[s_aoff[r] + d] = a.adcnt[(size_t)r * a.dom_cap + d];
+  }
   // DoNotSchedule constraints: the prep pass's domain counts (low-cardinality
   // keys: into their s_h segments, which only ScheduleAnyway constraints
   // accumulate into) and minMatchNum, read per node by the skew check
@@ -508,7 +570,7 @@ __global__ __launch_bounds__(SP_THREADS) void spread_filter_kernel(SpreadArgs a)
   __syncthreads();
   const uint32_t n_xres = s_solo.h.n_xres;
   const AffDev *ad = s_solo.ad;
-  const uint32_t na = s_solo.h.n_aff;
+  const uint32_t na = AFF ? s_solo.h.n_aff : 0u;
   bool ipa_filter = false;
   for (uint32_t r = 0; r < na; ++r) ipa_filter |= (ad[r].kind & AF_KIND) <= AF_EXIST_ANTI;
   const bool ipa_first_ok = !a.acc->aff_any && (s_solo.h.aff_flags & AFF_SELF);
@@ -537,6 +599,8 @@ __global__ __launch_bounds__(SP_THREADS) void spread_filter_kernel(SpreadArgs a)
   uint64_t ipa_mn = ~0ull, ipa_mx = 0;
   for (uint32_t pos = blockIdx.x * SP_THREADS + threadIdx.x; pos < a.npos; pos += grid_threads()) {
     PosIn in;
+    AffView av{s_aoff, s_h, {}, {}};
+    if (AFF) aff_prefetch(a, ad, na, pos, av);
     load_pos(a, sd, n, want_cnt, pos, true, in);
     const uint32_t slot = in.slot;
     if (slot == SLOT_NONE) continue;
@@ -548,8 +612,8 @@ __global__ __launch_bounds__(SP_THREADS) void spread_filter_kernel(SpreadArgs a)
     }
     if (node_score)
       for (uint32_t q = 0; q < na; ++q)
-        if ((ad[q].kind & (AF_KIND | AF_NODE)) == (AF_SCORE | AF_NODE) && aff_count(a, ad[q], pos) &&
-            a.dom[(size_t)ad[q].key * a.npos + pos] != DOM_NONE)
+        if ((ad[q].kind & (AF_KIND | AF_NODE)) == (AF_SCORE | AF_NODE) && aff_dom(a, ad, av, q, pos) != DOM_NONE &&
+            aff_sum(a, ad, av, q, pos, 0))
           score_any = true;
     NodeExt e{};
     if (need_ext) load_ext(a.t, pos, true, e);
@@ -599,7 +663,7 @@ __global__ __launch_bounds__(SP_THREADS) void spread_filter_kernel(SpreadArgs a)
         }
       }
     }
-    if (s == ST_FEASIBLE && ipa_filter && !ipa_fits(a, ad, na, pos, ipa_first_ok)) s = PLUGIN_IPA;
+    if (s == ST_FEASIBLE && ipa_filter && !ipa_fits(a, ad, na, av, pos, ipa_first_ok)) s = PLUGIN_IPA;
     int8_t out = (int8_t)s;
     if (s == ST_FEASIBLE) {
       ++feasible;
@@ -611,7 +675,7 @@ __global__ __launch_bounds__(SP_THREADS) void spread_filter_kernel(SpreadArgs a)
                                   (uint32_t)a.w.il * (uint32_t)image_score(s_solo, e),
                               tr, nr);
       if (ipa_score) {
-        const int64_t raw = ipa_raw_score(a, ad, na, pos);
+        const int64_t raw = ipa_raw_score(a, ad, na, av, pos);
         a.ipa_raw[pos] = raw;
         const uint64_t k = (uint64_t)raw + IPA_BIAS;
         ipa_mn = min(ipa_mn, k);
@@ -1030,7 +1094,8 @@ hipError_t launch_spread_pod(const SpreadArgs &args, uint32_t passes, hipStream_
   const SpreadArgs &a = args;
   if (passes & SPL_PREP) spread_prep_kernel<<<blocks, SP_THREADS, 0, st>>>(a);
   if (passes & SPL_MIN) spread_min_kernel<<<blocks, SP_THREADS, 0, st>>>(a);
-  spread_filter_kernel<<<blocks, SP_THREADS, 0, st>>>(a);
+  if (passes & SPL_AFF) spread_filter_kernel<true><<<blocks, SP_THREADS, 0, st>>>(a);
+  else spread_filter_kernel<false><<<blocks, SP_THREADS, 0, st>>>(a);
   if (passes & SPL_SCORE) spread_score_kernel<<<blocks, SP_THREADS, 0, st>>>(a);
   spread_select_kernel<<<blocks, SP_THREADS, 0, st>>>(a);
   spread_commit_kernel<<<1, WAVE, 0, st>>>(a);
