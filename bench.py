@@ -120,6 +120,10 @@ def parse():
     ap.add_argument("--cpu-pods", type=int, default=24, help="oracle sample (pods), single thread")
     ap.add_argument("--cpu-pods-mt", type=int, default=400, help="oracle sample (pods), multi-thread")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="ks_config execution option (include/ksched.h), e.g. resolve_mode=1; none changes a result")
+    ap.add_argument("--resolve-profile", action="store_true",
+                    help="phase clocks of the parallel commit during the inputs-resident pass (diagnostic)")
     ap.add_argument("--pmc-dir", default=str(ROOT / "profiles" / "pmc"),
                     help="per-configuration PMC summaries (tools/gpu.sh pmc + tools/pmc_summary.py)")
     a = ap.parse_args()
@@ -207,8 +211,9 @@ def main():
 
     kind = {"hetero": synth.HETERO, "kwok": synth.KWOK, "labeled": synth.LABELED, "zoned": synth.ZONED}[args.kind]
     t_setup = time.time()
+    options = {k: int(v) for k, v in (o.split("=", 1) for o in args.opt)}
     sched = Scheduler(args.nodes, device=local_rank if world > 1 else 0, pods_per_round=args.pods_per_round,
-                      topk=args.topk, nodes_per_lane=args.nodes_per_lane, world_size=world, rank=rank)
+                      topk=args.topk, nodes_per_lane=args.nodes_per_lane, world_size=world, rank=rank, options=options)
     if world > 1:
         sched.comm_init(exchange_unique_id(rank, world))
         if rank == 0:  # ncclCommInitRank returned: every rank has read the id
@@ -255,7 +260,22 @@ def run_batches(args, kind, sched, world, rank, t_setup):
     sched.lib.ks_debug_counters(sched.ctx, dbg)
     # secondary: the same number of steps with every batch compiled and
     # uploaded before the timed region (inputs resident in HBM)
+    if args.resolve_profile:
+        sched.lib.ks_debug_set_profile(sched.ctx, 1)
     res = None if args.no_resident else resident(args, kind, sched, world, barrier)
+    prof = None
+    if args.resolve_profile:
+        pr = (C.c_uint64 * 16)()
+        sched.lib.ks_debug_resolve_profile(sched.ctx, pr)
+        rounds = max(1, int(pr[9]))
+        names = ["stage", "gather_barrier", "proposals", "gather_w0_scan", "chunk_pairs", "gather_w0_dmawait", "commit",
+                 "rpre_update", "epilogue"]
+        prof = {"rounds": int(pr[9]), "cycles_per_round": {k: round(int(pr[i]) / rounds, 1) for i, k in enumerate(names)}}
+        prof["cycles_per_round"]["total"] = round(sum(int(pr[i]) for i in range(9)) / rounds, 1)
+        prof["dirty_recomputes_per_round"] = round(int(pr[10]) / rounds, 2)
+        prof["extra_windows_per_round"] = round(int(pr[11]) / rounds, 2)
+        prof["w0_prefetch_wait"] = round(int(pr[12]) / rounds, 1)
+        prof["w0_pre_scan"] = round(int(pr[13]) / rounds, 1)
     lat = latency(args, kind, sched, world) if args.latency_calls > 0 else None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_pods > 0:
@@ -269,6 +289,8 @@ def run_batches(args, kind, sched, world, rank, t_setup):
         line["inputs_resident"] = res
     if lat:
         line["latency"] = lat
+    if prof:
+        line["resolve_profile"] = prof
     sched.close()
     if rank == 0:
         print(json.dumps(line), flush=True)
@@ -627,6 +649,9 @@ def report(args, sched, st, dbg, world, pods_timed, elapsed, scheduled, setup_s,
             "spread_pods": int(st.spread_pods),
             "scheduled_fraction": round(scheduled / pods_timed, 4),
             "speculated_rounds_wasted": int(dbg[3]),  # since open (warmup included)
+            # parallel commit, since open: rounds it resolved and its chunk passes per round
+            "parallel_commit_rounds": int(dbg[13]),
+            "parallel_commit_passes_per_round": round(int(dbg[12]) / max(1, int(dbg[13])), 2),
             "pods_reswept_wrong_norm_guess": int(dbg[4]),  # since open (warmup included)
             # identical pods of a round swept once: pods swept (class
             # representatives) / pods in the swept windows, since open

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define KSCHED_ABI_VERSION 3
+#define KSCHED_ABI_VERSION 4
 
 /* ---------------------------------------------------------------- status */
 typedef int32_t ks_status;
@@ -391,7 +391,34 @@ typedef struct {
   int32_t weight_topology_spread; /* PodTopologySpread (default profile: 2)     */
   int32_t weight_inter_pod_affinity; /* InterPodAffinity (default profile: 2)    */
   int32_t hard_pod_affinity_weight;  /* InterPodAffinityArgs.hardPodAffinityWeight (1) */
+  /* Execution options (ks_config_default sets each default).  None of them
+   * changes a result -- every combination schedules exactly as upstream's
+   * sequential loop does (the tests pin each one); they choose how the device
+   * gets there.  ks_open reads no environment variable that selects any of
+   * this. */
+  uint32_t resolve_mode;          /* in-order commit of resource-only rounds: KS_RESOLVE_AUTO (default:
+                                     the parallel proposal / verify kernel, handing rounds where pods pile
+                                     onto the same nodes to the serial kernel), KS_RESOLVE_SERIAL,
+                                     KS_RESOLVE_PARALLEL */
+  uint32_t resolve_par_max_passes;  /* AUTO: a round taking more chunk passes than this (32) ...        */
+  uint32_t resolve_serial_rounds;   /* ... hands this many following rounds (16) to the serial kernel */
+  uint32_t dedup_identical_pods;  /* 1 (default): a round's byte-identical pods are swept once (§5.5) */
+  uint32_t early_fix;             /* 1 (default): on one rank the normaliser FIX re-sweep follows the
+                                     sweep on its stream (§5.2); 0: behind the merge (multi-rank order) */
+  uint32_t tuple_guess;           /* 1 (default): normaliser maxima guessed from node label / taint
+                                     tuples; 0: from the pod alone (more FIX re-sweeps)               */
+  uint32_t ext_nodes_per_lane;    /* nodes per lane of the label / taint sweep: 2 (default), 4 or 8  */
+  uint32_t sweep_pairs;           /* (block, pod group) pairs of a resource-only sweep (4096)        */
+  uint32_t sweep_pairs_ext;       /* ... of a label / taint sweep (16384)                            */
+  uint32_t resolve_cus;           /* CUs reserved for the resolve stream (1; 0: no CU masks)         */
+  uint32_t side_cus;              /* CUs the sweep stream leaves to the side stream (0)              */
+  uint32_t value_sync;            /* 1 (default): cross-stream hand-offs by stream wait-value packets;
+                                     0: by events (profilers that serialise dispatches)              */
+  uint32_t sync_timeout_ms;       /* bound on every host wait for device work (60000), see
+                                     ks_set_sync_timeout                                            */
 } ks_config;
+
+enum { KS_RESOLVE_AUTO = 0, KS_RESOLVE_SERIAL = 1, KS_RESOLVE_PARALLEL = 2 };
 
 typedef struct ks_ctx ks_ctx;
 typedef struct ks_batch ks_batch;
@@ -548,9 +575,16 @@ ks_status ks_reset_stats(ks_ctx *ctx);
 /* Raw counters: [0] rounds [1] pods resolved [2] pods swept
  * [3] speculated rounds wasted [4] pods re-swept because their guessed
  * normalising maxima were wrong, [5] label-dictionary reclaims, [6] taint
- * dictionary rebuilds, [8..15] resolve phase cycle sums (diagnostic
- * KS_STAMPS build only). */
+ * dictionary rebuilds, [7] identical pods not swept, [8..11] resolve phase
+ * cycle sums (diagnostic KS_STAMPS build only), [12] passes of the parallel
+ * commit, [13] rounds it resolved. */
 ks_status ks_debug_counters(ks_ctx *ctx, uint64_t out[16]);
+/* Diagnostics of the parallel commit (resource-only rounds): with the profile
+ * on, every round accumulates s_memtime cycles per phase into out[0..8]
+ * (stage, gather, proposals, base rows, chunk pairs, decisions, commit,
+ * Rpre updates, epilogue) and out[9] counts the rounds profiled. */
+ks_status ks_debug_set_profile(ks_ctx *ctx, int32_t on);
+ks_status ks_debug_resolve_profile(ks_ctx *ctx, uint64_t out[16]);
 /* Round marks of a finished batch (diagnostics for tests that place parity
  * checks where the round machinery changed course): out[i] for pod i of the
  * batch, bits KS_MARK_*.  Valid after ks_batch_run / ks_batch_wait. */
@@ -559,7 +593,7 @@ ks_status ks_debug_counters(ks_ctx *ctx, uint64_t out[16]);
 #define KS_MARK_AFTER_WASTE 4u  /* ... whose previous speculated round was wasted */
 ks_status ks_batch_marks(ks_ctx *ctx, const ks_batch *batch, uint8_t *out);
 /* Device-stall guard.  Every wait of the library on the device is bounded
- * (KS_SYNC_TIMEOUT_MS at ks_open, default 60000, or this call).  A stream
+ * (ks_config.sync_timeout_ms at ks_open, default 60000, or this call).  A stream
  * that has not finished in time makes the call return KS_ERR_DEVICE with
  * ks_last_error naming the unfinished streams, the hand-off flags' device
  * values and the round numbers they were expected to reach; the context is

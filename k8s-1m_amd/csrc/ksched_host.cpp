@@ -358,19 +358,23 @@ struct ks_ctx {
   // ks_debug_stall: the next round holds back flag stall_flag's signal by stall_us
   int32_t stall_flag = -1;
   uint32_t stall_us = 0;
-  // Tuning switches, read from the environment once per context in ks_open
-  // (KS_EARLY_FIX, KS_TIMING_EVERY, KS_SWEEP_BLOCKS, KS_EXT_NPL,
-  // KS_TUPLE_GUESS), so one process can open contexts with different settings
-  // (tests do).
+  // Execution options from ks_config (ks_open), per context, so one process
+  // can open contexts with different settings (tests do).
   bool early_fix = true;
-  bool dedup = true;        // KS_DEDUP: sweep identical pods of a round once
+  // resolve kernel of resource-only rounds (ksched_resolve.hip): KS_RESOLVE_AUTO
+  // launches the parallel commit with the serial kernel behind it as its
+  // fallback (RoundArgs::rmode, the two words at d_flags + 4)
+  uint32_t resolve_mode = KS_RESOLVE_AUTO;
+  uint32_t par_max_passes = 32, serial_rounds = 16;
+  bool res_profile = false;  // ks_debug_set_profile: phase clocks of the parallel commit
+  bool dedup = true;        // dedup_identical_pods: sweep identical pods of a round once
   bool tuple_guess = true;  // normaliser guesses over node tuples (refine_guesses)
   uint32_t timing_every = 8, ext_npl = 2;
   // (block, pod group) pairs a sweep aims for: resource-only sweeps 4096
   // (bigger pod groups amortise each block's row loads: C3 sweep 0.365 ->
   // 0.356 ms, profiles/r3/sweep_blocks_ab/), label / taint sweeps 16384
   // (C4 sweep 1.117 -> 1.102 ms; 4096 measured 2 % slower than 8192, 32768
-  // no better: profiles/r3/sweep_blocks_ab/c4_*); KS_SWEEP_BLOCKS sets both
+  // no better: profiles/r3/sweep_blocks_ab/c4_*): sweep_pairs / sweep_pairs_ext
   uint32_t sweep_blocks = 4096, sweep_blocks_ext = 16384;
   // KS_EVENT_PROFILE=1: per event kind, runs / events / seconds of ks_events_apply (stderr at ks_close)
   bool ev_profile = false;
@@ -2487,7 +2491,7 @@ ks_status collect_timing(ks_ctx *c) {
 }
 
 // Cross-stream hand-off: `st` signals round number `seq` on flag f (or by the
-// event, KS_VALUE_SYNC=0); `wt` waits for it.
+// event, value_sync = 0); `wt` waits for it.
 static ks_status hand_signal(ks_ctx *c, hipStream_t st, int f, hipEvent_t ev, uint32_t seq) {
   if (c->stall_flag == f) {  // ks_debug_stall
     HIPC(c, launch_stall(c->stall_us, st));
@@ -2662,7 +2666,7 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k, uint32_t end) {
   // The kernels address positions as base + wave*64*knpl + j*64 + lane, which
   // equals the layout position when the layout's npl-step block of a wave is
   // split into `sub` consecutive kernel waves; slots follow from the layout.
-  // KS_EARLY_FIX (default 1, one rank): the sweep measures the normaliser
+  // early_fix (default 1, one rank): the sweep measures the normaliser
   // maxima itself and norm_check + the FIX sweep follow it on the main
   // stream, so sweep k+1 no longer waits for the side stream's merge k; the
   // merge then reads the FIX records of the flagged pods directly
@@ -2743,7 +2747,19 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k, uint32_t end) {
       c->stall_flag = -1;
     }
     c->flag_want[2] = seq;
-    HIPC(c, launch_resolve(ra, b->ext, c->rstream));
+    ra.par_max_passes = c->par_max_passes;
+    ra.prof = c->res_profile ? c->d_counters + 16 : nullptr;
+    ra.serial_rounds = c->serial_rounds;
+    if (!b->ext && c->resolve_mode != KS_RESOLVE_SERIAL) {
+      // the parallel commit; under RES_AUTO the serial kernel follows and
+      // resolves the round only if the parallel one handed it over
+      ra.rmode = c->resolve_mode == KS_RESOLVE_AUTO ? c->d_flags + 4 : nullptr;
+      HIPC(c, launch_resolve_par(ra, c->rstream));
+      if (ra.rmode) HIPC(c, launch_resolve(ra, false, c->rstream));
+    } else {
+      ra.rmode = nullptr;
+      HIPC(c, launch_resolve(ra, b->ext, c->rstream));
+    }
   }
   if (tm) {
     HIPC(c, hipEventRecord(e1, c->rstream));
@@ -3100,6 +3116,19 @@ void ks_config_default(ks_config *cfg) {
   cfg->weight_inter_pod_affinity = 2;
   cfg->hard_pod_affinity_weight = 1;
   cfg->percentage_of_nodes_to_score = 100;
+  cfg->resolve_mode = KS_RESOLVE_AUTO;
+  cfg->resolve_par_max_passes = 32;
+  cfg->resolve_serial_rounds = 16;
+  cfg->dedup_identical_pods = 1;
+  cfg->early_fix = 1;
+  cfg->tuple_guess = 1;
+  cfg->ext_nodes_per_lane = 2;
+  cfg->sweep_pairs = 4096;
+  cfg->sweep_pairs_ext = 16384;
+  cfg->resolve_cus = 1;
+  cfg->side_cus = 0;
+  cfg->value_sync = 1;
+  cfg->sync_timeout_ms = 60000;
 }
 
 int32_t ks_abi_version(void) { return KSCHED_ABI_VERSION; }
@@ -3137,36 +3166,45 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
   if (hipSetDevice(cfg->device) != hipSuccess) return KS_ERR_DEVICE;
   ks_ctx *x = c.get();
   {
+    // execution options (ks_config; none changes a result)
+    if (cfg->resolve_mode > KS_RESOLVE_PARALLEL || cfg->resolve_par_max_passes == 0 ||
+        (cfg->ext_nodes_per_lane != 2 && cfg->ext_nodes_per_lane != 4 && cfg->ext_nodes_per_lane != 8) ||
+        cfg->sweep_pairs == 0 || cfg->sweep_pairs_ext == 0 || cfg->sync_timeout_ms == 0 || cfg->resolve_cus > 64 ||
+        cfg->side_cus > 64)
+      return KS_ERR_INVALID;
+    x->resolve_mode = cfg->resolve_mode;
+    x->par_max_passes = cfg->resolve_par_max_passes;
+    x->serial_rounds = cfg->resolve_serial_rounds;
+    x->dedup = cfg->dedup_identical_pods != 0;
+    x->early_fix = cfg->early_fix != 0;
+    x->tuple_guess = cfg->tuple_guess != 0;
+    x->ext_npl = cfg->ext_nodes_per_lane;
+    x->sweep_blocks = cfg->sweep_pairs;
+    x->sweep_blocks_ext = cfg->sweep_pairs_ext;
+    x->sync_timeout_ms = cfg->sync_timeout_ms;
+    // diagnostics only (stderr reports, timing sample rate): they change no
+    // scheduling decision
     auto env_u = [](const char *name, int dflt) {
       const char *e = std::getenv(name);
       return e ? std::atoi(e) : dflt;
     };
-    x->early_fix = env_u("KS_EARLY_FIX", 1) != 0;
-    x->dedup = env_u("KS_DEDUP", 1) != 0;
-    x->tuple_guess = env_u("KS_TUPLE_GUESS", 1) != 0;
     x->ev_profile = env_u("KS_EVENT_PROFILE", 0) != 0;
     x->run_profile = env_u("KS_RUN_PROFILE", 0) != 0;
     x->timing_every = (uint32_t)std::max(1, env_u("KS_TIMING_EVERY", 8));
-    if (std::getenv("KS_SWEEP_BLOCKS")) x->sweep_blocks = x->sweep_blocks_ext = (uint32_t)std::max(1, env_u("KS_SWEEP_BLOCKS", 8192));
-    const int en = env_u("KS_EXT_NPL", 2);  // geometry experiments only
-    x->ext_npl = (uint32_t)(en == 4 || en == 8 ? en : 2);
-    x->sync_timeout_ms = (uint32_t)std::max(1, env_u("KS_SYNC_TIMEOUT_MS", 60000));
   }
   {
-    // Resolve runs on a high-priority stream on KS_RESOLVE_CUS (default 1) CUs
+    // Resolve runs on a high-priority stream on resolve_cus (default 1) CUs
     // of its own: the main and side streams are masked off them, so a resolve
     // launch never waits for a CU to drain the next round's sweep blocks (the
     // sweep loses 1/256 of the chip, measured ~4 % slower).  0: no mask.
-    const char *e = std::getenv("KS_RESOLVE_CUS");
-    const int nres = e ? std::max(0, std::atoi(e)) : 1;
+    const int nres = (int)cfg->resolve_cus;
     hipDeviceProp_t prop{};
     HIPC(x, hipGetDeviceProperties(&prop, cfg->device));
     const int ncu = prop.multiProcessorCount;
-    // KS_SIDE_CUS (default 0): CUs the main stream (sweeps) leaves to the side
+    // side_cus (default 0): CUs the main stream (sweeps) leaves to the side
     // stream, so merge / gather / patch blocks start without waiting for sweep
     // blocks to drain
-    const char *es = std::getenv("KS_SIDE_CUS");
-    const int nside = es ? std::max(0, std::atoi(es)) : 0;
+    const int nside = (int)cfg->side_cus;
     if (nres > 0 && nres + nside < ncu) {
       std::vector<uint32_t> main_mask((ncu + 31) / 32, 0u), side_mask((ncu + 31) / 32, 0u),
           res_mask((ncu + 31) / 32, 0u);
@@ -3186,11 +3224,10 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
       HIPC(x, hipStreamCreateWithPriority(&x->sstream, hipStreamNonBlocking, hi));
     }
     x->xm.st = x->stream;
-    {  // KS_VALUE_SYNC=0: cross-stream hand-offs by event waits instead
+    {  // value_sync = 0: cross-stream hand-offs by event waits instead
       int can = 0;
       (void)hipDeviceGetAttribute(&can, hipDeviceAttributeCanUseStreamWaitValue, cfg->device);
-      const char *v = std::getenv("KS_VALUE_SYNC");
-      x->value_sync = can != 0 && (v ? std::atoi(v) != 0 : true);
+      x->value_sync = can != 0 && cfg->value_sync != 0;
     }
     for (int q = 0; q < 2; ++q) {
       HIPC(x, hipEventCreateWithFlags(&x->ev_sw[q], hipEventDisableTiming));
@@ -3238,8 +3275,8 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
       (st = dalloc(x, &x->d_norm_inv, 2 * 2 * (size_t)x->P)) ||
       (st = dalloc(x, &x->d_pstat, (size_t)x->P)) || (st = dalloc(x, &x->d_fix, 2 * MAX_P + MAX_P / MAX_PG)) ||
       (st = dalloc(x, &x->d_dedup, 2 * (2 * (size_t)MAX_P + 4))) ||
-      (st = dalloc(x, &x->d_pipe, 8)) || (st = dalloc(x, &x->d_flags, 4)) || (st = dalloc(x, &x->d_carry, 2 * (size_t)MAX_P)) ||
-      (st = dalloc(x, &x->d_counters, 16)))
+      (st = dalloc(x, &x->d_pipe, 8)) || (st = dalloc(x, &x->d_flags, 8)) || (st = dalloc(x, &x->d_carry, 2 * (size_t)MAX_P)) ||
+      (st = dalloc(x, &x->d_counters, 32)))
     return st;
   if ((st = xfer_begin(x, x->S * sizeof(Shard) + (size_t)x->cap * 4 + 1024, 0)) ||
       (st = h2d(x, x->d_shards, x->shards.data(), x->S * sizeof(Shard))) ||
@@ -4321,6 +4358,24 @@ ks_status ks_debug_round_record(ks_ctx *c, uint32_t r, uint64_t *out) {
   out[0] = h->bound;
   out[1] = h->nkeys;
   for (uint32_t i = 0; i < c->K; ++i) out[2 + i] = i < h->nkeys ? w[REC_HDR_WORDS + i] : 0ull;
+  return KS_OK;
+}
+
+ks_status ks_debug_set_profile(ks_ctx *c, int32_t on) {
+  if (!c) return KS_ERR_INVALID;
+  if (ks_status dst_ = drain_async(c)) return dst_;
+  c->res_profile = on != 0;
+  return KS_OK;
+}
+
+ks_status ks_debug_resolve_profile(ks_ctx *c, uint64_t out[16]) {
+  if (!c || !out) return KS_ERR_INVALID;
+  if (ks_status dst_ = drain_async(c)) return dst_;
+  HIPC(c, hipSetDevice(c->cfg.device));
+  ks_status st;
+  if ((st = xfer_begin(c, 1024, 0)) || (st = d2h(c, out, c->d_counters + 16, 16 * sizeof(uint64_t))) ||
+      (st = xfer_sync(c)))
+    return st;
   return KS_OK;
 }
 

@@ -11,6 +11,9 @@ constexpr int MAX_PG = 64;    // pods per sweep block (LDS wave records)
 constexpr int MAX_P = 256;    // pods per round (resolve stages the round in LDS)
 constexpr int MAX_K = 512;    // candidates per pod record (two list entries per list-wave lane in the resolve)
 constexpr uint32_t FIX_NONE = 0xFFFFFFFFu;  // fix_list tail
+// device counters of the parallel commit (ksched_resolve.hip): chunk passes,
+// rounds it resolved
+constexpr int CTR_PAR_PASSES = 12, CTR_PAR_ROUNDS = 13;
 // per-pod round marks (ks_batch_marks, include/ksched.h): where the round
 // machinery changed course, for tests that place checks there
 constexpr uint8_t MARK_FIX = 1;          // re-swept with measured normaliser maxima (FIX sweep)
@@ -57,6 +60,16 @@ struct RoundArgs {
   uint32_t *flag_res;         // resolve: round number `seq` stored here when done (null: the host signals)
   uint32_t seq;
   uint32_t stall_us;          // ks_debug_stall: the resolve holds its signal back this long (0: never)
+  // Resolve-kernel choice of a resource-only round (ksched_resolve.hip): both
+  // kernels are launched, resolve_par_kernel first.  rmode[0]: rounds left for
+  // the serial resolve_kernel (the parallel kernel exits at once while > 0);
+  // rmode[1]: seq of the last round the parallel kernel resolved (the serial
+  // kernel then exits at once).  A round that took more than par_max_passes
+  // passes hands the next serial_rounds rounds to the serial kernel.
+  // nullptr: only one kernel is launched and it resolves every round.
+  uint32_t *rmode;
+  uint32_t par_max_passes, serial_rounds;
+  uint64_t *prof;             // ks_debug_set_profile: resolve_par_kernel phase cycle sums (null: off)
   uint8_t *marks;             // [npods] per-pod round marks of the batch (ks_batch_marks): KS_MARK_*
   // Identical pods (resource-only batches; null otherwise): pods of a round
   // with byte-identical descriptors have identical lists, so only the first
@@ -76,7 +89,7 @@ struct RoundArgs {
   const uint32_t *slot_pos;   // slot -> position
   uint64_t *counters;         // [0] rounds, [1] pods resolved, [2] pods swept, [3] wasted rounds,
                               // [4] FIX re-swept pods, [7] identical pods not swept (their class's
-                              // representative was; [2] counts representatives)
+                              // representative was; [2] counts representatives), [CTR_PAR_*]
   Weights w;
 };
 
@@ -148,6 +161,7 @@ hipError_t launch_merge_shards(const RoundArgs &a, hipStream_t st);
 hipError_t launch_gather_cand(const RoundArgs &a, bool ext, hipStream_t st);
 hipError_t launch_patch(const RoundArgs &a, bool ext, hipStream_t st);
 hipError_t launch_resolve(const RoundArgs &a, bool ext, hipStream_t st);
+hipError_t launch_resolve_par(const RoundArgs &a, hipStream_t st);
 hipError_t launch_advance(const RoundArgs &a, hipStream_t st);
 hipError_t launch_advance_writeback(const RoundArgs &a, const CarryRec *carry, const uint32_t *n, hipStream_t st);
 hipError_t launch_writeback(const NodeTable &t, const CarryRec *carry, const uint32_t *n, hipStream_t st);

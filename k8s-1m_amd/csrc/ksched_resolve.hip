@@ -1,0 +1,717 @@
+// ksched_resolve.hip — the round's in-order commit as a parallel proposal /
+// verify over chunks of the window (resource-only rounds).
+//
+// Sequential semantics (the serial resolve_kernel in
+// ksched_kernels.hip): pod j's winner is the best of (a) its first listed
+// candidate that no earlier pod of the round took and (b) every node an
+// earlier pod took, re-scored against its state after those commits; the
+// round stops at j when neither is provably the maximum.  The serial kernel
+// walks the pods one barrier each (~1.2 us per pod).  Here the round is
+// resolved in passes over chunks of up to PCH pods:
+//
+//   fixed prefix [0, f)   exact, committed.  Its modified nodes are held in
+//                         LDS with their live rows (M); for every later pod j
+//                         Rpre[j] = max over M of j's key on the live row and
+//                         dl[j] = feasible nodes j lost to those commits are
+//                         maintained incrementally as pods are fixed
+//   A   (all waves)       each chunk pod gathers its first PNC listed entries
+//                         that are not in M and score above Rpre[j]
+//   B1  (one wave)        proposals: the serial greedy "first entry no
+//                         earlier pod takes, else Rpre's node" -- computed as
+//                         deferred acceptance with the pod index as priority,
+//                         which reaches the serial-dictatorship matching
+//   B2  (all waves)       exact decisions given the proposals: every node
+//                         taken by an earlier chunk pod is re-scored for every
+//                         later chunk pod (pairs in parallel), feasible counts
+//                         corrected; the first pod whose exact decision
+//                         differs from its proposal is fixed with the exact one
+//   C   (all waves)       commit the verified pods, extend M, update Rpre / dl
+//                         of every pod after them (pairs in parallel)
+//
+// Proposals differ from the exact decision only where a chunk pod re-takes a
+// node an earlier pod of the same chunk took (Rpre covers every node of the
+// fixed prefix exactly), so a C3 round of 256 pods takes 6-12 passes
+// (tools/jacobi_sim.cpp).  Rounds whose pods pile onto the same nodes (kwok
+// clusters of identical nodes) take many passes; after such a round the next
+// RoundArgs::serial_rounds rounds run the serial kernel (RoundArgs::rmode).
+//
+// Arithmetic is the serial kernel's (exact binary64 rows, one-FMA
+// LeastAllocated, Markstein BalancedAllocation; ksched_eval.hpp), and the
+// outputs are the same: results of the resolved pods, the modified nodes'
+// carry records, the next round's start, the completion signal.
+#include <hip/hip_runtime.h>
+
+#include "ksched_dev.hpp"
+#include "ksched_eval.hpp"
+#include "ksched_kernels.hpp"
+#include "ksched_util.hpp"
+
+namespace ks {
+
+constexpr int PR_THREADS = 1024;
+constexpr int PR_NW = PR_THREADS / WAVE;
+constexpr int PCH = 64;     // pods per chunk: one deferred-acceptance lane each
+constexpr int PNC = 16;     // candidates gathered per chunk pod
+constexpr int PMH = 1024;   // modified-slot hash (rhash: 10 bits), M <= MAX_P nodes
+constexpr int PDH = 2048;   // chunk claim hash (<= PCH * PNC + PCH slots)
+constexpr int PNR = 4;      // candidates per chunk pod whose rows are prefetched (LDS-DMA)
+constexpr int PGH_BITS = 7, PGH = 1 << PGH_BITS;  // chunk slot-group hash (<= PCH slots)
+constexpr int ROW_PIECES = sizeof(CandRow) / 16;
+constexpr uint32_t PNONE = 0xFFFFFFFFu;
+constexpr uint32_t PSRC_M = 0x10000u;  // proposal source: Rpre's node (M index in the low bits)
+static_assert(PCH == WAVE, "B1 runs one chunk pod per lane of one wave");
+
+// decision codes (proposal and exact)
+enum : uint32_t { PD_NODE = 0, PD_UNSCHED = 1, PD_ERROR = 2, PD_STOP = 3, PD_INCOMPLETE = 4 };
+
+// Resource-only pod as the commit evaluates it: Fit thresholds (request, or
+// -inf when Fit does not check the resource), requests, non-zero requests x 100
+struct PQ {
+  double rqc, rqm, rc, rm, zc, zm;
+};
+
+__device__ __forceinline__ PQ make_pq(const PodDev &p) {
+  PQ q;
+  q.rqc = ((p.flags & PF_HAS_REQ) && p.req_cpu > 0) ? p.req_cpu_d : -__builtin_inf();
+  q.rqm = ((p.flags & PF_HAS_REQ) && p.req_mem > 0) ? p.req_mem_d : -__builtin_inf();
+  q.rc = p.req_cpu_d;
+  q.rm = p.req_mem_d;
+  q.zc = p.nz100_cpu;
+  q.zm = p.nz100_mem;
+  return q;
+}
+
+// NodeResourcesFit of a resource-only pod on row r with Requested (rc, rm)
+// and np pods: the serial kernel's fit_q on rnode_regs
+__device__ __forceinline__ bool pq_fit(const PQ &q, const CandRow &r, double rc, double rm, int32_t np) {
+  return np + 1 <= r.apods && !(q.rqc > r.acpu - rc) && !(q.rqm > r.amem - rm);
+}
+
+// packed key of the pod on the row's live state (0: infeasible): key_q on rnode_regs
+__device__ __forceinline__ uint64_t pq_key(const PQ &q, const CandRow &r, uint32_t slot, const Weights &w) {
+  if (!pq_fit(q, r, r.rc, r.rm, r.np)) return 0;
+  NodeRegs g;
+  g.free_cpu = r.acpu - r.rc;
+  g.free_mem = r.amem - r.rm;
+  g.rcpu = r.rc;
+  g.rmem = r.rm;
+  g.lf100_cpu = r.acpu * 100.0 - r.zc100;
+  g.lf100_mem = r.amem * 100.0 - r.zm100;
+  g.acpu_d = r.acpu;
+  g.amem_d = r.amem;
+  g.inv_cpu = r.inv_cpu;
+  g.inv_mem = r.inv_mem;
+  const bool ac = r.acpu != 0.0, am = r.amem != 0.0;
+  g.bamul = (ac && am) ? 0.5 : 0.0;
+  g.lashift = (ac && am) ? 1u : 0u;
+  g.slot = slot;
+  const int32_t la = (least_requested(g.lf100_cpu, q.zc, g.inv_cpu) + least_requested(g.lf100_mem, q.zm, g.inv_mem)) >>
+                     g.lashift;
+  const int32_t ba = score_ba_sum(g.rcpu + q.rc, g.rmem + q.rm, g);
+  const int32_t t = (int32_t)wmul((uint32_t)w.fit, (uint32_t)la) + (int32_t)wmul((uint32_t)w.ba, (uint32_t)ba) + w.tt * 100;
+  return pack_key(t, slot);
+}
+
+__device__ __forceinline__ void pq_add(CandRow &r, const PQ &q) {  // NodeInfo.AddPod: exact binary64 sums
+  r.rc += q.rc;
+  r.rm += q.rm;
+  r.zc100 += q.zc;
+  r.zm100 += q.zm;
+  r.np += 1;
+}
+
+// Phase clock of the parallel commit (ks_debug_set_profile): thread 0 reads
+// s_memtime after each barrier and charges the interval to a phase, in LDS
+// (no registers held across the kernel).
+struct PhaseClock {
+  uint64_t *out, *acc;
+  uint64_t t;
+  __device__ __forceinline__ void tick(int phase) {
+    if (out == nullptr) return;
+    const uint64_t now = __builtin_amdgcn_s_memtime();
+    if (phase >= 0) acc[phase] += now - t;
+    t = now;
+  }
+  __device__ __forceinline__ void flush() {
+    if (out == nullptr) return;
+    acc[9] = 1;
+    for (int i = 0; i < 16; ++i) atomicAdd((unsigned long long *)&out[i], (unsigned long long)acc[i]);
+  }
+};
+
+__device__ __forceinline__ uint32_t key_slot(uint64_t k) { return 0xFFFFFFFFu - (uint32_t)k; }
+__device__ __forceinline__ uint32_t dhash(uint32_t x) { return (x * 2654435761u) >> 21; }  // 11 bits
+
+__global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
+  // ---- per pod of the round
+  __shared__ PQ s_q[MAX_P];
+  __shared__ uint32_t s_fl[MAX_P];
+  __shared__ ShardRecHdr s_hdr[MAX_P];
+  __shared__ uint32_t s_rep[MAX_P];
+  __shared__ uint64_t s_rk[MAX_P];     // Rpre: best key over the fixed prefix's modified nodes (0: none feasible)
+  __shared__ int32_t s_dl[MAX_P];      // feasible nodes lost (Fit) to the fixed prefix's commits
+  __shared__ uint32_t s_dirty[MAX_P];  // Rpre's node was re-taken: recompute before use
+  __shared__ uint32_t s_lptr[MAX_P];   // list entries before it are all in M
+  __shared__ uint4 s_resc[MAX_P];      // result: {win lo, win hi, feasible, status}
+  __shared__ int32_t s_rdl[MAX_P];     // result: Fit failures gained
+  // ---- fixed modified nodes (M): live row, round-start Requested / pod count, slot
+  __shared__ RNode s_m[MAX_P];
+  __shared__ uint32_t s_mh[PMH], s_mi[PMH];  // slot + 1 -> M index
+  // ---- chunk
+  __shared__ uint64_t s_ck[PCH][PNC];  // gathered candidates: keys ...
+  __shared__ uint16_t s_ce[PCH][PNC];  // ... and list entries
+  __shared__ uint4 s_crow[PCH][ROW_PIECES][PNR];  // the first PNR candidates' rows (LDS-DMA)
+  __shared__ uint32_t s_cnc[PCH], s_cmore[PCH], s_cpst[PCH];
+  __shared__ uint32_t s_dh[PDH], s_do[PDH];  // claims: slot + 1 -> lowest claiming chunk pod
+  __shared__ uint32_t s_gh[PGH];             // chunk slot groups: slot + 1 ...
+  __shared__ uint64_t s_gm[PGH];             // ... -> lanes
+  __shared__ uint64_t s_pk[PCH];    // proposal key
+  __shared__ uint32_t s_ps[PCH];    // proposal slot (PNONE: none)
+  __shared__ uint32_t s_pnx[PCH];   // next chunk pod proposing the same slot (PNONE)
+  __shared__ uint32_t s_pfst[PCH];  // first chunk pod proposing its slot
+  __shared__ RNode s_prow[PCH];     // proposed node's state at the chunk start
+  __shared__ uint64_t s_ik[PCH];    // best key over nodes taken earlier in the chunk
+  __shared__ int32_t s_idl[PCH];    // feasible nodes lost to them
+  __shared__ uint32_t s_cdm[PCH];   // distinct nodes committed by the fixed pods: M index,
+  __shared__ double s_cdp[PCH][2];  // Requested before this chunk's commits,
+  __shared__ int32_t s_cdn[PCH];    // pod count before,
+  __shared__ uint32_t s_cdr[PCH];   // node was in M before the chunk
+  // control: [0] f, [1] stopped, [2] cut, [4] distinct nodes, [5] |M|, [6] passes
+  __shared__ uint32_t s_ctl[8];
+
+  const uint32_t tid = threadIdx.x, lane = tid % WAVE, wid = tid / WAVE;
+  if (a.rmode != nullptr && uniform_u32(a.rmode[0]) != 0) return;  // serial rounds: resolve_kernel follows
+  const uint32_t start = uniform_u32(*a.act);
+  if (start >= a.npods || uniform_u32(*a.sstart) != start) {  // the lists belong to other pods
+    if (tid == 0) {
+      *a.act_next = start;
+      *a.d_start = start;
+      *a.carry_out_n = 0;
+      if (start < a.npods) {
+        a.counters[3] += 1;
+        mark_pod(a.marks, start, MARK_AFTER_WASTE);
+      }
+      if (a.rmode != nullptr) a.rmode[1] = a.seq;
+      signal_done(a.flag_res, a.seq, a.stall_us);
+    }
+    return;
+  }
+  const uint32_t n = min(a.P, a.npods - start);
+  const uint32_t RW = rec_words(a.K);
+  const uint64_t lt_mask = (1ull << lane) - 1ull;
+  // phases: 0 stage, 1 gather, 2 proposals, 3 (unused), 4 chunk pairs, 5 (unused), 6 decide + commit, 7 Rpre
+  // updates, 8 epilogue, [9] rounds
+  __shared__ uint64_t s_clk[16];
+  if (tid < 16) s_clk[tid] = 0;
+  PhaseClock clk{tid == 0 ? a.prof : nullptr, s_clk, 0};
+  clk.tick(-1);
+
+  auto mh_find = [&](uint32_t slot) -> uint32_t {
+    uint32_t h = rhash(slot);
+    for (;;) {
+      const uint32_t v = s_mh[h];
+      if (v == 0) return PNONE;
+      if (v == slot + 1) return s_mi[h];
+      h = (h + 1) & (PMH - 1);
+    }
+  };
+  auto dh_insert = [&](uint32_t slot) -> uint32_t {
+    uint32_t h = dhash(slot);
+    for (;;) {
+      const uint32_t old = atomicCAS(&s_dh[h], 0u, slot + 1);
+      if (old == 0 || old == slot + 1) return h;
+      h = (h + 1) & (PDH - 1);
+    }
+  };
+  auto dh_owner = [&](uint32_t slot) -> uint32_t {
+    uint32_t h = dhash(slot);
+    for (;;) {
+      const uint32_t v = s_dh[h];
+      if (v == 0) return PNONE;
+      if (v == slot + 1) return s_do[h];
+      h = (h + 1) & (PDH - 1);
+    }
+  };
+  // wave 0: lanes of the chunk grouped by slot (s_gh / s_gm cleared by the caller)
+  auto group_of = [&](uint32_t slot, bool in) -> uint64_t {
+    uint32_t h = PNONE;
+    if (in) {
+      h = (slot * 2654435761u) >> (32 - PGH_BITS);
+      for (;;) {
+        const uint32_t old = atomicCAS(&s_gh[h], 0u, slot + 1);
+        if (old == 0 || old == slot + 1) break;
+        h = (h + 1) & (PGH - 1);
+      }
+      atomicOr((unsigned long long *)&s_gm[h], (unsigned long long)(1ull << lane));
+    }
+    return in ? s_gm[h] : 0ull;
+  };
+  auto row_of = [&](uint32_t c, uint32_t j, uint32_t cand) -> CandRow {  // a gathered candidate's S0 row
+    CandRow w;
+    if (cand < (uint32_t)PNR) {
+      uint4 *wp = (uint4 *)&w;
+#pragma unroll
+      for (int q = 0; q < ROW_PIECES; ++q) wp[q] = s_crow[c][q][cand];
+    } else {
+      w = a.crow[(size_t)s_rep[j] * a.K + s_ce[c][cand]];
+    }
+    return w;
+  };
+
+  // ---- stage the round
+  for (uint32_t i = tid; i < n; i += PR_THREADS) {
+    const uint32_t ri = a.rep != nullptr ? a.rep[i] : i;
+    const PodDev p = a.pods[start + i];
+    s_rep[i] = ri;
+    s_q[i] = make_pq(p);
+    s_fl[i] = p.flags;
+    s_hdr[i] = *(const ShardRecHdr *)(a.frec + (size_t)ri * RW);
+    s_rk[i] = 0;
+    s_dl[i] = 0;
+    s_dirty[i] = 0;
+    s_lptr[i] = 0;
+  }
+  for (uint32_t i = tid; i < PMH; i += PR_THREADS) s_mh[i] = 0;
+  if (tid < 8) s_ctl[tid] = 0;
+  __syncthreads();
+  clk.tick(0);
+
+  // Each wave gathers chunk pods wid + PR_NW t; their first list windows are
+  // loaded ahead into registers (here for the first chunk, then during the
+  // previous pass's Rpre updates), so a pass starts on resident keys.
+  constexpr int PPW = PCH / PR_NW;
+  uint64_t kw0 = 0, kw1 = 0, kw2 = 0, kw3 = 0;
+  static_assert(PPW == 4, "four chunk pods per wave");
+  auto load_windows = [&](uint32_t f, uint32_t cn) {
+    auto ld = [&](uint32_t c) -> uint64_t {
+      if (c >= cn) return 0ull;
+      const uint32_t j = f + c, e = s_lptr[j] + lane;
+      return e < s_hdr[j].nkeys ? a.frec[(size_t)s_rep[j] * RW + REC_HDR_WORDS + e] : 0ull;
+    };
+    kw0 = ld(wid);
+    kw1 = ld(wid + PR_NW);
+    kw2 = ld(wid + 2 * PR_NW);
+    kw3 = ld(wid + 3 * PR_NW);
+  };
+  load_windows(0, min((uint32_t)PCH, n));
+
+  for (uint32_t guard = 0; guard <= MAX_P; ++guard) {
+    const uint32_t f = s_ctl[0];
+    if (f >= n || s_ctl[1] != 0) break;
+    const uint32_t cn = min((uint32_t)PCH, n - f);
+
+    // ====================== A: gather candidates (all waves, 4 chunk pods each)
+    for (uint32_t i = tid; i < PDH; i += PR_THREADS) {
+      s_dh[i] = 0;
+      s_do[i] = PNONE;
+    }
+    if (a.prof) {  // diagnostic: how long the prefetched windows are still in flight
+      __builtin_amdgcn_s_waitcnt(0);
+      clk.tick(12);
+    }
+    static_for<PPW>([&](auto T) {
+      constexpr int t = T;
+      const uint32_t c = wid + PR_NW * t;
+      if (c >= cn) return;
+      const uint32_t j = f + c;
+      uint64_t rk;
+      if (s_dirty[j]) {  // Rpre's node was re-taken: the max over every M node again
+        const PQ q = s_q[j];
+        uint64_t best = 0;
+        const uint32_t mn = s_ctl[5];
+        for (uint32_t m = lane; m < mn; m += WAVE) best = max64(best, pq_key(q, s_m[m].row, s_m[m].slot, a.w));
+        rk = wave_max_u64_dpp(best);
+        if (lane == 0) {
+          s_rk[j] = rk;
+          s_dirty[j] = 0;
+          if (a.prof) atomicAdd((unsigned long long *)&s_clk[10], 1ull);
+        }
+      } else {
+        rk = s_rk[j];
+      }
+      clk.tick(13);
+      const uint32_t nk = s_hdr[j].nkeys;
+      const uint64_t *keys = a.frec + (size_t)s_rep[j] * RW + REC_HDR_WORDS;
+      uint32_t base = s_lptr[j], cnt = 0, firstu = PNONE;
+      bool more = false;
+      uint64_t k = t == 0 ? kw0 : t == 1 ? kw1 : t == 2 ? kw2 : kw3;
+      while (base < nk) {
+        const uint32_t e = base + lane;
+        const bool valid = e < nk;
+        const bool unt = valid && mh_find(key_slot(k)) == PNONE;
+        const uint64_t um = __ballot(unt);
+        if (firstu == PNONE && um) firstu = base + (uint32_t)__builtin_ctzll(um);
+        const bool take = unt && k > rk;
+        const uint64_t tm = __ballot(take);
+        const uint32_t r = cnt + (uint32_t)__popcll(tm & lt_mask);
+        if (take && r < (uint32_t)PNC) {
+          s_ck[c][r] = k;
+          s_ce[c][r] = (uint16_t)e;
+        }
+        cnt += (uint32_t)__popcll(tm);
+        if (cnt >= (uint32_t)PNC) {
+          more = true;  // there may be more untaken entries above Rpre
+          break;
+        }
+        if (__ballot(valid && k <= rk)) break;  // keys descend: the rest are below Rpre
+        base += WAVE;
+        k = base + lane < nk ? keys[base + lane] : 0ull;
+        if (a.prof && lane == 0) atomicAdd((unsigned long long *)&s_clk[11], 1ull);
+      }
+      if (lane == 0) {
+        s_cnc[c] = min(cnt, (uint32_t)PNC);
+        s_cmore[c] = more ? 1u : 0u;
+        s_lptr[j] = firstu != PNONE ? firstu : min(base + WAVE, nk);
+        const uint32_t feas = s_hdr[j].feasible - (uint32_t)s_dl[j];
+        s_cpst[c] = feas == 0 ? PD_UNSCHED : ((s_fl[j] & PF_PREF_ERR) && feas >= 2) ? PD_ERROR : PD_NODE;
+      }
+    });
+    // the first PNR candidates' rows of the wave's pods by LDS-DMA, lane r ->
+    // row r, issued after every scan (the compiler waits for all outstanding
+    // loads before a scan's key use); landed before the barrier
+    static_for<PPW>([&](auto T) {
+      const uint32_t c = wid + PR_NW * (uint32_t)T;
+      if (c >= cn) return;
+      if (lane < min(s_cnc[c], (uint32_t)PNR)) {
+        const uint4 *src = (const uint4 *)(a.crow + (size_t)s_rep[f + c] * a.K + s_ce[c][lane]);
+#pragma unroll
+        for (int q = 0; q < ROW_PIECES; ++q)
+          __builtin_amdgcn_global_load_lds((gvoid_t *)(src + q), (lvoid_t *)&s_crow[c][q][0], 16, 0, 0);
+      }
+    });
+    clk.tick(3);                    // wave 0's own gathering
+    __builtin_amdgcn_s_waitcnt(0);  // this wave's row DMAs have landed
+    clk.tick(5);                    // ... and its wait for them
+    __syncthreads();
+    clk.tick(1);
+
+    // ================== B: proposals by deferred acceptance (wave 0, lane = pod)
+    if (wid == 0) {
+      const uint32_t c = lane, j = f + c;
+      const bool in = c < cn;
+      const uint32_t pst = in ? s_cpst[c] : PD_INCOMPLETE;
+      const uint32_t nc = in ? s_cnc[c] : 0u;
+      uint32_t ptr = 0, h = PNONE;
+      bool active = in && pst == PD_NODE && nc > 0;
+      // Pod c proposes its candidate ptr; every slot keeps the lowest pod that
+      // ever proposed it (a holder only loses a slot to a lower pod, and a
+      // slot once held stays held), so pods that see another owner move on.
+      // The fixed point is the serial greedy: each pod takes its first
+      // candidate no lower pod takes.
+      for (uint32_t it = 0; it <= (uint32_t)(PCH * PNC); ++it) {
+        if (active && h == PNONE) h = dh_insert(key_slot(s_ck[c][ptr]));
+        if (active) atomicMin(&s_do[h], c);
+        const bool lost = active && s_do[h] != c;
+        if (__ballot(lost) == 0) break;
+        if (lost) {
+          h = PNONE;
+          if (++ptr >= nc) active = false;
+        }
+      }
+      uint32_t code = pst, src = PNONE, ps = PNONE;
+      uint64_t key = 0;
+      if (in && pst == PD_NODE) {
+        if (active) {
+          key = s_ck[c][ptr];
+          ps = key_slot(key);
+          src = ptr;
+        } else if (s_cmore[c]) {
+          code = PD_INCOMPLETE;  // more candidates than gathered may be free
+        } else {
+          const uint64_t rk = s_rk[j];
+          if (rk > s_hdr[j].bound) {
+            key = rk;
+            ps = key_slot(rk);
+            src = PSRC_M | mh_find(ps);
+          } else {
+            code = PD_STOP;
+          }
+        }
+      }
+      // Rpre's node re-taken by a lower chunk pod: its state for this pod
+      // changed, so Rpre is no longer known here
+      const bool rp = in && code == PD_NODE && src >= PSRC_M;
+      uint32_t hh = PNONE;
+      if (rp) {
+        hh = dh_insert(ps);
+        atomicMin(&s_do[hh], c);
+      }
+      if (rp && s_do[hh] != c) {
+        code = PD_INCOMPLETE;
+        key = 0;
+        ps = PNONE;
+      }
+      const uint64_t inc = __ballot(in && code == PD_INCOMPLETE), stp = __ballot(in && code == PD_STOP);
+      uint32_t cut = cn;
+      if (inc) cut = min(cut, (uint32_t)__builtin_ctzll(inc));
+      if (stp) cut = min(cut, (uint32_t)__builtin_ctzll(stp) + 1u);
+      const bool live = c < cut;
+      if (!live) {
+        key = 0;
+        ps = PNONE;
+      }
+      // the proposed node's state at the chunk start
+      if (live && code == PD_NODE) s_prow[c] = src >= PSRC_M ? s_m[src & 0xFFFFu] : rnode_from_row(row_of(c, j, src), ps);
+      // lanes proposing the same slot: first of the group, next member
+      s_gh[lane] = 0;
+      s_gh[lane + WAVE] = 0;
+      s_gm[lane] = 0;
+      s_gm[lane + WAVE] = 0;
+      const uint64_t g = group_of(ps, ps != PNONE);
+      const uint64_t above = lane == 63 ? 0ull : g & ~((2ull << lane) - 1ull);
+      s_pk[c] = key;
+      s_ps[c] = ps;
+      s_pfst[c] = (g & lt_mask) == 0 ? 1u : 0u;
+      s_pnx[c] = above ? (uint32_t)__builtin_ctzll(above) : PNONE;
+      s_ik[c] = 0;
+      s_idl[c] = 0;
+      s_cpst[c] = code;  // proposal code from here on
+      s_cdm[c] = src;    // proposal source (C reads it before reusing the slot)
+      if (lane == 0) s_ctl[2] = cut;
+    }
+    __syncthreads();
+    clk.tick(2);
+    const uint32_t cut = s_ctl[2];
+
+    // ============== chunk pairs: nodes taken earlier in the chunk, for every later pod
+    {
+      const uint32_t npairs = cut * (cut - 1) / 2;
+      for (uint32_t t = tid; t < npairs; t += PR_THREADS) {
+        // pair (jc, ic), ic < jc: t = jc (jc - 1) / 2 + ic
+        uint32_t jc = (uint32_t)((1.0f + __builtin_sqrtf(1.0f + 8.0f * (float)t)) * 0.5f);
+        while (jc * (jc - 1) / 2 > t) --jc;
+        while ((jc + 1) * jc / 2 <= t) ++jc;
+        const uint32_t ic = t - jc * (jc - 1) / 2;
+        if (s_ps[ic] == PNONE || !s_pfst[ic]) continue;
+        CandRow r = s_prow[ic].row;
+        const double rc0 = r.rc, rm0 = r.rm;
+        const int32_t np0 = r.np;
+        for (uint32_t k = ic; k != PNONE && k < jc; k = s_pnx[k]) pq_add(r, s_q[f + k]);
+        const PQ q = s_q[f + jc];
+        const uint64_t key = pq_key(q, r, s_prow[ic].slot, a.w);
+        const int32_t lost = (pq_fit(q, r, rc0, rm0, np0) ? 1 : 0) - (key != 0 ? 1 : 0);
+        if (key) atomicMax((unsigned long long *)&s_ik[jc], (unsigned long long)key);
+        if (lost) atomicAdd(&s_idl[jc], lost);
+      }
+    }
+    __syncthreads();
+    clk.tick(4);
+
+    // ===== C: exact decisions, the verified prefix committed (wave 0, lane = pod)
+    if (wid == 0) {
+      const uint32_t c = lane, j = f + c;
+      const bool live = c < cut;
+      const uint32_t pcode = live ? s_cpst[c] : PD_INCOMPLETE;
+      const uint32_t psrc = live ? s_cdm[c] : PNONE;
+      const uint64_t pkey = live ? s_pk[c] : 0ull;
+      uint32_t code = PD_INCOMPLETE, feas = 0;
+      uint64_t win = 0, ku = 0;
+      uint32_t kidx = PNONE;
+      if (live) {
+        const ShardRecHdr &hd = s_hdr[j];
+        feas = hd.feasible - (uint32_t)s_dl[j] - (uint32_t)s_idl[c];
+        const uint64_t rk = s_rk[j], ik = s_ik[c];
+        code = PD_NODE;
+        if (feas == 0) {
+          code = PD_UNSCHED;
+        } else if ((s_fl[j] & PF_PREF_ERR) && feas >= 2) {
+          code = PD_ERROR;
+        } else {
+          // the first candidate no lower pod took: the proposal's, unless the
+          // pod had no proposal (its status changed with the chunk's commits)
+          if (pcode == PD_NODE) {
+            if (psrc < PSRC_M) {
+              ku = pkey;
+              kidx = psrc;
+            }
+          } else {
+            const uint32_t nc = s_cnc[c];
+            for (uint32_t l = 0; l < nc; ++l) {
+              const uint32_t o = dh_owner(key_slot(s_ck[c][l]));
+              if (o == PNONE || o >= c) {
+                ku = s_ck[c][l];
+                kidx = l;
+                break;
+              }
+            }
+          }
+          // every gathered candidate scores above Rpre: with one free, Rpre's
+          // node (re-taken or not) cannot win over it
+          if (ku) {
+            win = max64(ku, max64(rk, ik));
+          } else {
+            const uint32_t ro = rk ? dh_owner(key_slot(rk)) : PNONE;
+            if (s_cmore[c] || (ro != PNONE && ro < c)) {
+              code = PD_INCOMPLETE;
+            } else {
+              const uint64_t bm = max64(rk, ik);
+              if (bm > hd.bound) win = bm;
+              else code = PD_STOP;
+            }
+          }
+        }
+      }
+      const bool mism = live && code != PD_INCOMPLETE && (code != pcode || (code == PD_NODE && win != pkey));
+      const uint64_t mmask = __ballot(mism), imask = __ballot(live && code == PD_INCOMPLETE);
+      const uint32_t mm = mmask ? (uint32_t)__builtin_ctzll(mmask) : PNONE;
+      uint32_t ccut = cut;
+      if (imask) ccut = min(ccut, (uint32_t)__builtin_ctzll(imask));
+      // pods [0, nfix) get results; `stop`: the round ends at pod f + nfix.
+      // ccut >= 1: the chunk's first pod is always decided (no lower pod
+      // takes its candidates or Rpre's node)
+      uint32_t nfix;
+      bool stop;
+      if (mm < ccut) {
+        stop = __builtin_amdgcn_readlane(code, mm) == PD_STOP;
+        nfix = stop ? mm : mm + 1;
+      } else {
+        stop = ccut > 0 && __builtin_amdgcn_readlane(code, ccut - 1) == PD_STOP;
+        nfix = stop ? ccut - 1 : ccut;
+      }
+      if (c == mm && code == PD_NODE) {
+        // the node the exact decision commits, at the chunk start
+        const uint32_t ws = key_slot(win);
+        if (win == ku) {
+          s_prow[c] = rnode_from_row(row_of(c, j, kidx), ws);
+        } else {
+          uint32_t from = PNONE;
+          for (uint32_t i = 0; i < c && from == PNONE; ++i)
+            if (s_ps[i] == ws) from = i;
+          s_prow[c] = from != PNONE ? s_prow[from] : s_m[mh_find(ws)];
+        }
+      }
+      const bool fx = c < nfix;
+      if (!fx) win = 0;
+      if (fx) {
+        s_resc[j] = make_uint4((uint32_t)win, (uint32_t)(win >> 32), feas,
+                               code == PD_UNSCHED ? 1u : code == PD_ERROR ? 2u : 0u);
+        s_rdl[j] = s_dl[j] + s_idl[c];
+      }
+      // commit: the first fixed pod of each node adds every fixed pod's request on it
+      const uint32_t ws = win ? key_slot(win) : PNONE;
+      s_gh[lane] = 0;
+      s_gh[lane + WAVE] = 0;
+      s_gm[lane] = 0;
+      s_gm[lane + WAVE] = 0;
+      const uint64_t g = group_of(ws, ws != PNONE);
+      const bool first = ws != PNONE && (g & lt_mask) == 0;
+      const uint32_t mi0 = first ? mh_find(ws) : PNONE;
+      const bool isnew = first && mi0 == PNONE;
+      const uint64_t fm = __ballot(first), nm = __ballot(isnew);
+      const uint32_t mn = s_ctl[5];
+      if (first) {
+        const uint32_t mi = isnew ? mn + (uint32_t)__popcll(nm & lt_mask) : mi0;
+        RNode x = isnew ? s_prow[c] : s_m[mi];
+        const uint32_t d = (uint32_t)__popcll(fm & lt_mask);
+        s_cdm[d] = mi;
+        s_cdp[d][0] = x.row.rc;
+        s_cdp[d][1] = x.row.rm;
+        s_cdn[d] = x.row.np;
+        s_cdr[d] = isnew ? 0u : 1u;
+        for (uint64_t m = g; m; m &= m - 1) pq_add(x.row, s_q[f + (uint32_t)__builtin_ctzll(m)]);
+        s_m[mi] = x;
+        if (isnew) {
+          uint32_t h = rhash(ws);
+          while (atomicCAS(&s_mh[h], 0u, ws + 1) != 0u) h = (h + 1) & (PMH - 1);
+          s_mi[h] = mi;
+        }
+      }
+      if (lane == 0) {
+        s_ctl[4] = (uint32_t)__popcll(fm);
+        s_ctl[5] = mn + (uint32_t)__popcll(nm);
+        s_ctl[0] = f + nfix;
+        s_ctl[1] = stop ? 1u : 0u;
+        s_ctl[6] += 1;
+      }
+    }
+    __syncthreads();
+    clk.tick(6);
+
+    // ===== Rpre / feasible-count updates of every later pod (pairs in parallel)
+    {
+      const uint32_t nf = s_ctl[0], nd = s_ctl[4];
+      const uint32_t npend = n > nf ? n - nf : 0u;
+      if (s_ctl[1] == 0 && npend > 0) {
+        load_windows(nf, min((uint32_t)PCH, npend));  // the next chunk's first windows, in flight meanwhile
+        const uint32_t total = nd * npend;
+        for (uint32_t t = tid; t < total; t += PR_THREADS) {
+          const uint32_t d = t / npend, jj = nf + t % npend;
+          const RNode &x = s_m[s_cdm[d]];
+          const PQ q = s_q[jj];
+          const uint64_t key = pq_key(q, x.row, x.slot, a.w);
+          const int32_t lost = (pq_fit(q, x.row, s_cdp[d][0], s_cdp[d][1], s_cdn[d]) ? 1 : 0) - (key != 0 ? 1 : 0);
+          if (lost) atomicAdd(&s_dl[jj], lost);
+          if (s_cdr[d]) {
+            // a re-taken node: its old key may be the one Rpre holds, which a
+            // max cannot take back -- recompute Rpre when the pod is reached
+            // (if another node's key is in Rpre already, the old one is not
+            // the max and the max with the new one is exact)
+            const uint64_t cur = s_rk[jj];
+            if (cur != 0 && key_slot(cur) == x.slot) {
+              s_dirty[jj] = 1;
+              continue;
+            }
+          }
+          if (key) atomicMax((unsigned long long *)&s_rk[jj], (unsigned long long)key);
+        }
+      }
+    }
+    __syncthreads();
+    clk.tick(7);
+  }
+
+  // ---- results of the resolved pods, the modified nodes, the next round's start
+  const uint32_t nres = s_ctl[0];
+  {
+    uint32_t *dst = (uint32_t *)((DevResult *)a.results + start);
+    constexpr uint32_t RW32 = sizeof(DevResult) / 4;
+    for (uint32_t i = tid; i < nres * RW32; i += PR_THREADS) {
+      const uint32_t pr = i / RW32, w = i % RW32;
+      const uint4 c = s_resc[pr];
+      const uint64_t win = ((uint64_t)c.y << 32) | c.x;
+      const int64_t total = win ? (int64_t)(win >> 32) - 1 : 0;
+      uint32_t v;
+      switch (w) {
+        case 0: v = win ? key_slot(win) : 0xFFFFFFFFu; break;            // node_index (-1: none)
+        case 1: v = c.w; break;                                           // status
+        case 2: v = (uint32_t)total; break;                               // total_score
+        case 3: v = (uint32_t)((uint64_t)total >> 32); break;
+        case 4: v = c.z; break;                                           // feasible_nodes
+        case 5: v = a.evaluated; break;                                   // evaluated_nodes
+        case 6: case 7: case 8: case 9: v = s_hdr[pr].fails[w - 6]; break;  // fail_counts
+        case 10: v = s_hdr[pr].fails[KS_PLUGIN_FIT_IDX] + (uint32_t)s_rdl[pr]; break;
+        case 13: v = a.pods[start + pr].prefilter_out; break;            // prefiltered
+        case 14: v = (win && c.z == 1) ? 1u : 0u; break;                  // flags
+        default: v = 0; break;                                            // spread_fail, ipa_fail, _pad
+      }
+      dst[i] = v;
+    }
+  }
+  const uint32_t mn = s_ctl[5];
+  for (uint32_t i = tid; i < mn; i += PR_THREADS) a.carry_out[i] = rnode_carry(s_m[i], CandExt{}, false);
+  if (tid == 0) {
+    *a.carry_out_n = mn;
+    mark_pod(a.marks, start, MARK_ROUND_START);
+    *a.act_next = start + nres;
+    *a.d_start = start + nres;
+    a.counters[0] += 1;     // rounds
+    a.counters[1] += nres;  // pods resolved
+    a.counters[CTR_PAR_PASSES] += s_ctl[6];
+    a.counters[CTR_PAR_ROUNDS] += 1;
+    if (a.rmode != nullptr) {
+      a.rmode[1] = a.seq;  // resolve_kernel, launched after this one, skips the round
+      if (s_ctl[6] > a.par_max_passes) a.rmode[0] = a.serial_rounds;
+    }
+  }
+  __syncthreads();
+  clk.tick(8);
+  clk.flush();
+  if (tid == 0) signal_done(a.flag_res, a.seq, a.stall_us);
+}
+
+hipError_t launch_resolve_par(const RoundArgs &a, hipStream_t st) {
+  resolve_par_kernel<<<1, PR_THREADS, 0, st>>>(a);
+  return hipGetLastError();
+}
+
+}  // namespace ks

@@ -256,7 +256,27 @@ class KsConfig(C.Structure):
         ("weight_topology_spread", C.c_int32),
         ("weight_inter_pod_affinity", C.c_int32),
         ("hard_pod_affinity_weight", C.c_int32),
+        # execution options (include/ksched.h): none changes a result
+        ("resolve_mode", C.c_uint32),
+        ("resolve_par_max_passes", C.c_uint32),
+        ("resolve_serial_rounds", C.c_uint32),
+        ("dedup_identical_pods", C.c_uint32),
+        ("early_fix", C.c_uint32),
+        ("tuple_guess", C.c_uint32),
+        ("ext_nodes_per_lane", C.c_uint32),
+        ("sweep_pairs", C.c_uint32),
+        ("sweep_pairs_ext", C.c_uint32),
+        ("resolve_cus", C.c_uint32),
+        ("side_cus", C.c_uint32),
+        ("value_sync", C.c_uint32),
+        ("sync_timeout_ms", C.c_uint32),
     ]
+
+
+RESOLVE_AUTO, RESOLVE_SERIAL, RESOLVE_PARALLEL = 0, 1, 2
+OPTION_FIELDS = ("resolve_mode", "resolve_par_max_passes", "resolve_serial_rounds", "dedup_identical_pods", "early_fix",
+                 "tuple_guess", "ext_nodes_per_lane", "sweep_pairs", "sweep_pairs_ext", "resolve_cus", "side_cus",
+                 "value_sync", "sync_timeout_ms")
 
 
 class KsStats(C.Structure):
@@ -297,7 +317,7 @@ KSCHED_SYMBOLS = [
     "ks_nodes_delete", "ks_pods_add", "ks_pods_remove", "ks_events_apply", "ks_schedule", "ks_batch_prepare", "ks_batch_run",
     "ks_batch_results", "ks_batch_free", "ks_batch_submit", "ks_batch_wait", "ks_pods_check", "ks_plugin_scores", "ks_node_states", "ks_comm_unique_id", "ks_comm_init_local", "ks_snapshot_update",
     "ks_comm_init", "ks_comm_allreduce_max", "ks_get_stats", "ks_reset_stats", "ks_set_timing",
-    "ks_debug_counters", "ks_debug_round_record", "ks_set_sync_timeout", "ks_debug_stall", "ks_batch_marks",
+    "ks_debug_counters", "ks_debug_set_profile", "ks_debug_resolve_profile", "ks_debug_round_record", "ks_set_sync_timeout", "ks_debug_stall", "ks_batch_marks",
 ]
 KSGATHER_SYMBOLS = [
     "ksg_open", "ksg_close", "ksg_set_members", "ksg_record_and_wait", "ksg_pending", "ksg_fnv1_32", "ksg_target_index",
@@ -370,6 +390,8 @@ def ksched_lib() -> C.CDLL:
     L.ks_reset_stats.argtypes = [vp]
     L.ks_set_timing.argtypes = [vp, C.c_int32]
     L.ks_debug_counters.argtypes = [vp, P(C.c_uint64)]
+    L.ks_debug_set_profile.argtypes = [vp, C.c_int32]
+    L.ks_debug_resolve_profile.argtypes = [vp, P(C.c_uint64)]
     L.ks_set_sync_timeout.argtypes = [vp, C.c_uint32]
     L.ks_debug_stall.argtypes = [vp, C.c_uint32, C.c_uint32]
     L.ks_batch_marks.argtypes = [vp, vp, P(C.c_uint8)]

@@ -117,10 +117,17 @@ class Scheduler:
 
     def __init__(self, node_capacity: int, *, device: int = 0, pods_per_round: int = 256, topk: int = 0,
                  nodes_per_lane: int = 4, world_size: int = 1, rank: int = 0, virtual_shards: int = 1,
-                 weights: Optional[Dict[str, int]] = None):
+                 weights: Optional[Dict[str, int]] = None, options: Optional[Dict[str, int]] = None):
+        """options: ks_config execution options by field name (_abi.OPTION_FIELDS),
+        e.g. {"resolve_mode": _abi.RESOLVE_SERIAL, "dedup_identical_pods": 0};
+        none of them changes a result."""
         self.lib = _abi.ksched_lib()
         cfg = _abi.KsConfig()
         self.lib.ks_config_default(C.byref(cfg))
+        for k, v in (options or {}).items():
+            if k not in _abi.OPTION_FIELDS:
+                raise ValueError(f"unknown ks_config option {k}")
+            setattr(cfg, k, int(v))
         cfg.device = device
         cfg.node_capacity = node_capacity
         cfg.pods_per_round = pods_per_round

@@ -31,7 +31,9 @@ def run(seed):
     slots = synth.slot_array(n)
     o = pyoracle.Oracle(n)
     o.upsert(ns.nodes, slots, n)
-    s = Scheduler(n, pods_per_round=c["P"], topk=c["K"], nodes_per_lane=c["npl"], virtual_shards=c["shards"])
+    # the serial commit kernel (the one whose loop exit the probe build delays)
+    s = Scheduler(n, pods_per_round=c["P"], topk=c["K"], nodes_per_lane=c["npl"], virtual_shards=c["shards"],
+                  options={"resolve_mode": 1})
     try:
         s.lib.ks_set_sync_timeout(s.ctx, 20000)
         s.upsert_nodes_raw(ns.nodes, slots, n)

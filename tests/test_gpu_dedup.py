@@ -5,7 +5,7 @@ reference's own benchmark pods are all alike: kwok/make_pods/main.go:138-148
 creates request-less pods from one template) sweep, merge, gather and patch
 each class once per round window; every pod of the class reads that record.
 Parity: bit-exact results and node states against the CPU oracle, and against
-the same library with the deduplication switched off (KS_DEDUP=0), over
+the same library with the deduplication switched off (dedup_identical_pods = 0), over
 duplicate densities from "every pod alike" to a few repeats, round geometries
 with early stops (short lists) and wasted speculative rounds, virtual shards,
 and calls split so that classes straddle round windows.
@@ -32,20 +32,10 @@ def repeated(src, idx):
     return arr
 
 
-def run_pair(ns, n, pods, m, splits=1, dedup=True, env=None, **kw):
+def run_pair(ns, n, pods, m, splits=1, dedup=True, opts=None, **kw):
     """libksched results + node states for `pods`, with or without dedup
-    (tuning switches are read from the environment when a context opens)."""
-    env = dict(env or {}, KS_DEDUP="1" if dedup else "0")
-    old = {k: os.environ.get(k) for k in env}
-    os.environ.update(env)
-    try:
-        s = Scheduler(n, **kw)
-    finally:
-        for k, v in old.items():
-            if v is None:
-                del os.environ[k]
-            else:
-                os.environ[k] = v
+    (ks_config execution options)."""
+    s = Scheduler(n, options=dict(opts or {}, dedup_identical_pods=1 if dedup else 0), **kw)
     try:
         s.upsert_nodes_raw(ns.nodes, synth.slot_array(n), n)
         bounds = np.linspace(0, m, splits + 1).astype(int)
@@ -67,10 +57,10 @@ def oracle_run(ns, n, pods, m):
     return got, states_np(o.L.oracle_node_states, o.o, n)
 
 
-E = {"KS_TUPLE_GUESS": "0"}   # plain normaliser guesses: FIX re-sweeps happen
-M = {"KS_EARLY_FIX": "0"}     # normaliser maxima measured by the merge
+E = {"tuple_guess": 0}   # plain normaliser guesses: FIX re-sweeps happen
+M = {"early_fix": 0}     # normaliser maxima measured by the merge
 CASES = [
-    # node kind, pod kind, nodes, pods, distinct shapes, P, K, virtual shards, splits, env
+    # node kind, pod kind, nodes, pods, distinct shapes, P, K, virtual shards, splits, options
     (synth.KWOK, synth.HETERO, 2000, 3000, 1, 256, 256, 1, 1, None),   # every pod alike (the published workload)
     (synth.KWOK, synth.HETERO, 1500, 2000, 3, 64, 16, 2, 3, None),     # short lists: rounds stop early
     (synth.HETERO, synth.HETERO, 3000, 2500, 8, 256, 256, 1, 2, None),
@@ -86,15 +76,15 @@ CASES = [
 
 @pytest.mark.parametrize("case", range(len(CASES)))
 def test_dedup_equals_oracle_and_undeduplicated(case):
-    kn, kp, n, m, shapes, P, K, shards, splits, env = CASES[case]
+    kn, kp, n, m, shapes, P, K, shards, splits, opts = CASES[case]
     ns = synth.nodes(kn, n, 31 + case)
     src = synth.pods(kp, max(shapes, 1), 41 + case)
     r = random.Random(case)
     idx = [r.randrange(shapes) for _ in range(m)]
     pods = repeated(src, idx)
     kw = dict(pods_per_round=P, topk=K, virtual_shards=shards)
-    got, gst = run_pair(ns, n, pods, m, splits, True, env, **kw)
-    ref, rst = run_pair(ns, n, pods, m, splits, False, env, **kw)
+    got, gst = run_pair(ns, n, pods, m, splits, True, opts, **kw)
+    ref, rst = run_pair(ns, n, pods, m, splits, False, opts, **kw)
     want, wst = oracle_run(ns, n, pods, m)
     what = f"case {CASES[case]}"
     assert_results_equal_np(got, want, f"{what} dedup vs oracle")

@@ -97,20 +97,11 @@ def pick_windows(marks, m, wlen=WLEN, fixed=WINDOWS, per_kind=3):
     return out
 
 
-def run_fullsize(kind, pods, prefill, *, env=None, **cfg):
+def run_fullsize(kind, pods, prefill, *, opts=None, **cfg):
     nodes = synth.nodes(kind, N, 1)
     slots = synth.slot_array(N)
     pf = synth.prefill(kind, N, 1, 3, 0.5) if prefill else None
-    old = {k: os.environ.get(k) for k in (env or {})}
-    os.environ.update(env or {})
-    try:
-        s = Scheduler(N, **cfg)  # switches are read when the context opens
-    finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+    s = Scheduler(N, options=opts, **cfg)
     s.upsert_nodes_raw(nodes.nodes, slots, N)
     if pf is not None:
         assert s.lib.ks_pods_add(s.ctx, pf.pods, pf.slot_ptr, pf.n_pods) == 0
@@ -152,7 +143,7 @@ def test_c3_hetero_1m_replay():
 def test_c4_labeled_1m_replay_early_fix():
     # the C4 bench path: EXT sweep (2 nodes per lane), early FIX, compacted FIX list
     r, dbg = run_fullsize(synth.LABELED, synth.pods(synth.LABELED, BATCH, 2), prefill=True,
-                          env={"KS_TUPLE_GUESS": "0"})  # simple guesses: the FIX path runs often
+                          opts={"tuple_guess": 0})  # simple guesses: the FIX path runs often
     assert dbg[4] > 0, "no pod was re-swept with a measured normaliser (FIX path not exercised)"
     assert (r["status"] == 1).any() and (r["status"] == 0).mean() > 0.9
 
@@ -160,7 +151,7 @@ def test_c4_labeled_1m_replay_early_fix():
 def test_c4_labeled_1m_replay_merge_fix():
     # the same with the FIX sweep behind the merge (the multi-rank order, one rank)
     r, dbg = run_fullsize(synth.LABELED, synth.pods(synth.LABELED, BATCH, 5), prefill=True,
-                          env={"KS_EARLY_FIX": "0", "KS_TUPLE_GUESS": "0"})
+                          opts={"early_fix": 0, "tuple_guess": 0})
     assert dbg[4] > 0
 
 

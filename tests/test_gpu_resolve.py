@@ -1,0 +1,173 @@
+"""The in-order commit of resource-only rounds: the
+parallel proposal / verify kernel (ksched_resolve.hip), the
+serial kernel, and the automatic hand-over between them, each bit-exact
+against the CPU oracle's one-pod-at-a-time scheduling and against each other.
+
+The cases target what makes the parallel commit hard:
+* BalancedAllocation rising after a commit (a node becomes MORE attractive for
+  the next pods once one pod lands on it), so a node taken earlier in the
+  round wins again -- inside one chunk and across chunks;
+* identical nodes and identical pods (the kwok shape): every pod piles onto
+  the same few nodes, the deferred-acceptance proposals are wrong for most
+  pods and AUTO hands the rounds to the serial kernel;
+* short candidate lists (K = 1, 8, 16): lists run out and rounds stop early;
+* zero-request pods (Fit never fails on resources, LeastAllocated uses the
+  non-zero defaults) and pod-count limits (Fit fails once a node is full, the
+  feasible counts change mid-round);
+* several schedule calls, so node state carried between batches is checked.
+Oracle: oracle/oracle.cpp (parity unpinned).
+"""
+import ctypes as C
+import random
+
+import numpy as np
+import pytest
+
+import pyoracle
+from helpers import assert_results_equal, res_array, states_np
+from ksched import Scheduler, _abi, synth
+from ksched.objects import Arena, nodes_array, pods_array
+from scenarios import node, pod
+
+pytestmark = pytest.mark.gpu
+
+Gi = 1 << 30
+MODES = {"auto": _abi.RESOLVE_AUTO, "serial": _abi.RESOLVE_SERIAL, "parallel": _abi.RESOLVE_PARALLEL}
+
+
+def ba_rise_cluster(n, m, seed):
+    """Nodes with CPU already half used and memory nearly free, pods that ask
+    mostly for memory: each commit moves a node's memory fraction towards its
+    CPU fraction, so its BalancedAllocation for the next such pod rises."""
+    r = random.Random(seed)
+    nodes, pre, pre_slots = [], [], []
+    for i in range(n):
+        cpu = r.choice([8, 16, 32]) * 1000
+        mem = r.choice([32, 64, 128]) * Gi
+        nodes.append(node(f"n{i}", cpu=cpu, mem=mem, pods=r.choice([8, 16, 110])))
+        used = int(cpu * r.uniform(0.3, 0.7)) // 50 * 50
+        pre.append(pod(f"pre{i}", cpu=used, mem=int(mem * r.uniform(0.0, 0.1)) // (1 << 20) << 20))
+        pre_slots.append(i)
+    pods = []
+    for j in range(m):
+        if r.random() < 0.15:
+            pods.append(pod(f"be{j}"))  # no requests: non-zero defaults for LeastAllocated only
+        else:
+            pods.append(pod(f"p{j}", cpu=r.choice([50, 100, 200]), mem=r.choice([2, 4, 6, 8]) * Gi))
+    return nodes, pre, pre_slots, pods
+
+
+def run_modes(nodes_arr, n, pods_arr, m, pre=None, splits=1, modes=("auto", "serial", "parallel"), **kw):
+    """Results + node states of every resolve mode and of the oracle."""
+    slots = (C.c_uint32 * n)(*range(n))
+    o = pyoracle.Oracle(n)
+    o.upsert(nodes_arr, slots, n)
+    if pre is not None:
+        o.add_pods(*pre)
+    bounds = np.linspace(0, m, splits + 1).astype(int)
+    want = np.concatenate([res_array(o.schedule(C.cast(C.addressof(pods_arr) + int(b0) * C.sizeof(_abi.KsPod),
+                                                       C.POINTER(_abi.KsPod)), int(b1 - b0)), int(b1 - b0))
+                           for b0, b1 in zip(bounds, bounds[1:])])
+    wst = states_np(o.L.oracle_node_states, o.o, n)
+    o.close()
+    out = {}
+    for mode in modes:
+        with Scheduler(n, options={"resolve_mode": MODES[mode]}, **kw) as s:
+            s.upsert_nodes_raw(nodes_arr, slots, n)
+            if pre is not None:
+                assert s.lib.ks_pods_add(s.ctx, *pre) == 0, s.lib.ks_last_error(s.ctx)
+            got = []
+            for b0, b1 in zip(bounds, bounds[1:]):
+                k = int(b1 - b0)
+                ptr = C.cast(C.addressof(pods_arr) + int(b0) * C.sizeof(_abi.KsPod), C.POINTER(_abi.KsPod))
+                got.append(res_array(s.schedule_raw(ptr, k), k))
+            dbg = (C.c_uint64 * 16)()
+            assert s.lib.ks_debug_counters(s.ctx, dbg) == 0
+            out[mode] = (np.concatenate(got), states_np(s.lib.ks_node_states, s.ctx, n), list(dbg))
+    return want, wst, out
+
+
+def check_modes(want, wst, out, what):
+    for mode, (got, st, _) in out.items():
+        if not np.array_equal(got, want):
+            bad = np.nonzero(got != want)[0]
+            i = int(bad[0])
+            raise AssertionError(f"{what} [{mode}]: {len(bad)}/{len(want)} results differ; first at pod {i}: "
+                                 f"got {got[i]} want {want[i]}")
+        assert np.array_equal(st, wst), f"{what} [{mode}]: node states differ from the oracle"
+
+
+@pytest.mark.parametrize("seed,n,m,P,K,splits", [
+    (1, 300, 1200, 256, 256, 1),
+    (2, 1000, 2000, 256, 64, 2),
+    (3, 120, 900, 64, 16, 3),
+    (4, 2000, 1500, 256, 8, 1),
+    (5, 500, 1500, 100, 256, 2),
+])
+def test_balanced_allocation_rise(seed, n, m, P, K, splits):
+    nodes, pre, pre_slots, pods = ba_rise_cluster(n, m, seed)
+    a = Arena()
+    na, _ = nodes_array(nodes, a)
+    pa, _ = pods_array(pods, a)
+    fa, nf = pods_array(pre, a)
+    fs = (C.c_uint32 * nf)(*pre_slots)
+    want, wst, out = run_modes(na, n, pa, m, pre=(fa, fs, nf), splits=splits, pods_per_round=P, topk=K)
+    check_modes(want, wst, out, f"BA rise seed {seed}")
+    # the workload does what it is for: some pods win a node an earlier pod of
+    # the same round took (consecutive pods on one node)
+    sched = want[want["status"] == 0]["node_index"]
+    assert (sched[1:] == sched[:-1]).any()
+    par_rounds = out["parallel"][2][13]
+    assert par_rounds > 0, "the parallel kernel resolved no round"
+
+
+@pytest.mark.parametrize("kind,pods,K", [("kwok", "besteffort", 256), ("kwok", "c1", 512), ("kwok", "c1", 16),
+                                         ("hetero", "c1", 256), ("hetero", "besteffort", 32)])
+def test_synthetic_streams(kind, pods, K):
+    n, m = 3000, 5000
+    k = {"kwok": synth.KWOK, "hetero": synth.HETERO}[kind]
+    ns = synth.nodes(k, n, 11)
+    ps = synth.besteffort_pods(m) if pods == "besteffort" else synth.pods(synth.HETERO, m, 12)
+    pf = synth.prefill(k, n, 11, 13, 0.4) if kind == "hetero" else None
+    pre = (pf.pods, pf.slot_ptr, pf.n_pods) if pf is not None else None
+    want, wst, out = run_modes(ns.nodes, n, ps.pods, m, pre=pre, splits=2, topk=K)
+    check_modes(want, wst, out, f"{kind}/{pods}/K={K}")
+    if kind == "kwok" and pods == "besteffort":
+        # identical pods on identical nodes pile up: AUTO hands rounds to the serial kernel
+        auto = out["auto"][2]
+        assert auto[13] < auto[0], f"AUTO never handed a round to the serial kernel: {auto}"
+
+
+def test_pod_count_limits_mid_round():
+    # small pods per node: nodes fill up inside a round, so feasible counts and
+    # Fit failure counts change between consecutive pods
+    r = random.Random(7)
+    nodes = [node(f"n{i}", cpu=64000, mem=256 * Gi, pods=r.choice([1, 2, 3])) for i in range(400)]
+    pods = [pod(f"p{j}", cpu=r.choice([None, 100, 500]), mem=r.choice([None, Gi])) for j in range(1100)]
+    a = Arena()
+    na, n = nodes_array(nodes, a)
+    pa, m = pods_array(pods, a)
+    want, wst, out = run_modes(na, n, pa, m, splits=1)
+    check_modes(want, wst, out, "pod-count limits")
+    assert (want["status"] == 1).any(), "no pod ran out of nodes"
+
+
+@pytest.mark.parametrize("shards", [1, 3])
+def test_parallel_vs_serial_fuzz(shards):
+    # random node / pod shapes, virtual shards, uneven splits: the two kernels
+    # and the oracle agree on every field
+    for seed in range(4):
+        r = random.Random(100 * shards + seed)
+        n = r.choice([97, 640, 1500])
+        m = r.choice([300, 1000])
+        nodes = [node(f"n{i}", cpu=r.choice([2, 4, 8, 16, 64]) * 1000, mem=r.choice([4, 16, 64, 256]) * Gi,
+                      pods=r.choice([4, 16, 110])) for i in range(n)]
+        pods = [pod(f"p{j}", cpu=r.choice([None, 0, 50, 250, 1000, 3000]),
+                    mem=r.choice([None, 0, Gi // 4, Gi, 3 * Gi])) for j in range(m)]
+        a = Arena()
+        na, _ = nodes_array(nodes, a)
+        pa, _ = pods_array(pods, a)
+        P = r.choice([32, 128, 256])
+        want, wst, out = run_modes(na, n, pa, m, splits=r.randrange(1, 4), modes=("serial", "parallel"),
+                                   pods_per_round=P, topk=r.choice([P, 8, 64]), virtual_shards=shards)
+        check_modes(want, wst, out, f"fuzz seed {seed} shards {shards}")

@@ -89,10 +89,9 @@ def test_wrong_normaliser_guess_is_reswept(tuple_guess, fixes, monkeypatch):
     # (pref-one-feasible's NodeAffinity guess is right -- its zone=z2 term is
     # ruled out by nodeSelector zone=z1 -- but its TaintToleration guess is
     # not) and the FIX-mode sweep must run for exactly those; the node-tuple
-    # guesses (KS_TUPLE_GUESS, default) get pref-one-feasible right, and x and
+    # guesses (tuple_guess, default) get pref-one-feasible right, and x and
     # pref stay wrong (their worst node fails on resources, which tuples do
     # not see)
-    monkeypatch.setenv("KS_TUPLE_GUESS", tuple_guess)
     nodes, pods, exp = SCENARIOS["normalizer_guess_wrong"]()
     a = Arena()
     na, n = nodes_array(nodes, a)
@@ -101,7 +100,7 @@ def test_wrong_normaliser_guess_is_reswept(tuple_guess, fixes, monkeypatch):
     o = pyoracle.Oracle(n)
     o.upsert(na, slots, n)
     want = o.schedule(pa, m)
-    with Scheduler(n) as s:
+    with Scheduler(n, options={"tuple_guess": int(tuple_guess)}) as s:
         s.upsert_nodes_raw(na, slots, n)
         got = s.schedule_raw(pa, m)
         dbg = (C.c_uint64 * 16)()
@@ -165,14 +164,12 @@ def test_fix_list_spans_several_groups(early, monkeypatch):
     # matches: their guessed NodeAffinity max (the term weight) is wrong (the
     # measured max is 0), so the compacted FIX list spans 3+ groups of MAX_PG.
     # Interleaved with pods whose guess is right, and with a PreferNoSchedule
-    # taint so TaintToleration normalises too.  KS_EARLY_FIX=0 runs the FIX
+    # taint so TaintToleration normalises too.  early_fix = 0 runs the FIX
     # sweep behind the merge (the multi-rank order) on one rank.
     from ksched.objects import NodeSelectorRequirement as R, NodeSelectorTerm as T, \
         PreferredSchedulingTerm as PT, Taint
     from scenarios import node, pod
 
-    monkeypatch.setenv("KS_EARLY_FIX", early)
-    monkeypatch.setenv("KS_TUPLE_GUESS", "0")  # simple guesses: every no-match term is guessed wrong
     Gi = 1 << 30
     nodes = [node(f"n{i}", cpu=(8 + 8 * (i % 5)) * 1000, mem=(32 << (i % 4)) * Gi,
                   labels={"zone": f"z{i % 3}", "disk": "ssd" if i % 4 == 0 else "hdd"},
@@ -194,7 +191,8 @@ def test_fix_list_spans_several_groups(early, monkeypatch):
     o = pyoracle.Oracle(n)
     o.upsert(na, slots, n)
     want = o.schedule(pa, m)
-    with Scheduler(n, pods_per_round=256) as s:
+    # simple guesses (tuple_guess 0): every no-match term is guessed wrong
+    with Scheduler(n, pods_per_round=256, options={"early_fix": int(early), "tuple_guess": 0}) as s:
         s.upsert_nodes_raw(na, slots, n)
         got = s.schedule_raw(pa, m)
         dbg = (C.c_uint64 * 16)()

@@ -9,7 +9,8 @@
 #   tools/gpu.sh trace TAG [bench args]       rocprofv3 --kernel-trace --stats of a short bench run
 #   tools/gpu.sh pmc TAG [bench args]         PMC passes of one configuration -> gpurun_out/pmc/<key>.json
 #   tools/gpu.sh sq TAG [bench args]          SQ counters per kernel of one short bench run
-#   tools/gpu.sh ab TAG [bench args]          A/B: default library vs lib/alt (or ALT_ENV="VAR=value"), twice each
+#   tools/gpu.sh ab TAG [bench args]          A/B: default library vs lib/alt (or ALT_OPT="name=value": a
+#                                             ks_config option of the alt arm), twice each
 #   tools/gpu.sh variants TAG [bench args]    VARIANTS="default expt2 ..." one configuration on several lib/<name> builds
 #   tools/gpu.sh stamps TAG [kind]            resolve-phase stamps (make stamps stamps2 stamps3 first)
 #   tools/gpu.sh valu                         VALU issue costs (tools/valu_issue, built by hipcc on the CPU side)
@@ -78,8 +79,7 @@ PY
   pmc)
     # one counter group per rocprofv3 run (MI355X_MICROARCH.md); stream
     # wait-value hand-offs stall behind counter collection, so event waits
-    ARGS="--steps 2 --warmup 1 --no-cpu-baseline --no-resident --latency-calls 0 $*"
-    export KS_VALUE_SYNC=0
+    ARGS="--steps 2 --warmup 1 --no-cpu-baseline --no-resident --latency-calls 0 --opt value_sync=0 $*"
     ( while sleep 30; do echo "pmc: alive"; done ) &
     HB=$!
     trap 'kill $HB 2>/dev/null' EXIT
@@ -100,21 +100,21 @@ PY
     # SQ counters per kernel of one short bench run (e.g. the one-pod path:
     # tools/gpu.sh sq TAG --kind zoned --pods spread --batch 128); value sync
     # off as in pmc, small batches: per-dispatch collection slows every launch
-    export KS_VALUE_SYNC=0
     mkdir -p gpurun_out/sq_$TAG
     timeout -s KILL 170 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_WAVES SQ_WAVE_CYCLES \
       SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU -d "$R/gpurun_out/sq_$TAG/p1" -o run --output-format csv -- \
-      python3 "$R/bench.py" --steps 1 --warmup 1 --no-cpu-baseline --no-resident --latency-calls 0 "$@" \
+      python3 "$R/bench.py" --steps 1 --warmup 1 --no-cpu-baseline --no-resident --latency-calls 0 --opt value_sync=0 "$@" \
       > gpurun_out/sq_$TAG/p1.json 2> gpurun_out/sq_$TAG/p1.err
     rc=$?; echo "sq rc=$rc"; exit $rc ;;
   ab)
     for v in new alt new alt; do
+      EXTRA=""
       if [ $v = alt ]; then
-        if [ -n "$ALT_ENV" ]; then export "$ALT_ENV"; else export KSCHED_LIB_DIR=k8s-1m_amd/ksched/lib/alt; fi
+        if [ -n "$ALT_OPT" ]; then EXTRA="--opt $ALT_OPT"; else export KSCHED_LIB_DIR=k8s-1m_amd/ksched/lib/alt; fi
       else
-        unset KSCHED_LIB_DIR; [ -n "$ALT_ENV" ] && unset "${ALT_ENV%%=*}"
+        unset KSCHED_LIB_DIR
       fi
-      timeout -k 10 300 python -u bench.py --no-cpu-baseline --steps 6 --latency-calls 0 "$@" \
+      timeout -k 10 300 python -u bench.py --no-cpu-baseline --steps 6 --latency-calls 0 $EXTRA "$@" \
         > gpurun_out/ab_${TAG}_$v.json 2> gpurun_out/ab_${TAG}_$v.err || { tail -3 gpurun_out/ab_${TAG}_$v.err; exit 1; }
       summary gpurun_out/ab_${TAG}_$v.json $v
     done ;;
