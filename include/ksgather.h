@@ -43,8 +43,15 @@ enum { KSG_TIE_RANDOM = 0, KSG_TIE_LOWEST_NAME = 1, KSG_TIE_LOWEST_INDEX = 2 };
 ksg_evaluator *ksg_open(uint32_t members, uint32_t delay_ms, int32_t tie_mode, uint64_t seed);
 /* Fires every pending evaluation (its waiters return with the scores recorded
  * so far), wakes ksg_next_fired, waits until no thread is inside a call on
- * `ev`, then frees it.  Calls arriving after it started return -1. */
+ * `ev`, then frees it.  Calls arriving after it started return -1; the caller
+ * guarantees that no call STARTS after ksg_close returns (the handle is then
+ * gone): a wrapper that cannot -- threads that may still be about to call --
+ * uses ksg_shutdown first, waits for its own callers, then ksg_close. */
 void ksg_close(ksg_evaluator *ev);
+/* The first half of ksg_close: every later call returns -1 (ksg_next_fired
+ * still reports evaluations fired before), every pending evaluation fires and
+ * its waiters return; nothing is freed.  Idempotent. */
+void ksg_shutdown(ksg_evaluator *ev);
 /* KSG_TIE_LOWEST_INDEX: names[i] is the node of global index i (the hosts'
  * node slots laid end to end); a name not listed sorts after every listed one. */
 void ksg_set_node_order(ksg_evaluator *ev, const char *const *names, uint32_t n);

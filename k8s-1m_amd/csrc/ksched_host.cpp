@@ -10,6 +10,7 @@
 //   k8s.io/api core/v1/toleration.go#ToleratesTaint       (taint masks, A8)
 //   component-helpers nodeaffinity.go#newNodeSelectorTerm (clauses, A9/A15)
 //   apimachinery labels.NewRequirement validation         (parse errors)
+#include <atomic>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -352,7 +353,9 @@ struct ks_ctx {
   // a miss wedges the context.  flag_want[f]: the last round number enqueued
   // to be signalled on hand-off flag f (what a finished stream leaves there)
   uint32_t sync_timeout_ms = 60000;
-  bool wedged = false;
+  // set by the worker thread's drains (sync_bounded), read by API threads
+  std::atomic<bool> wedged{false};
+  hipStream_t diag_stream = nullptr;  // stall_report's read-back stream (created at ks_open)
   uint32_t flag_want[4] = {0, 0, 0, 0};
   uint32_t *h_diag = nullptr;  // pinned: flags read back by the stall report
   // ks_debug_stall: the next round holds back flag stall_flag's signal by stall_us
@@ -611,10 +614,13 @@ ks_status stall_report(ks_ctx *c, hipStream_t st, const char *what, double ms) {
   const std::pair<hipStream_t, const char *> ss[3] = {{c->stream, "main"}, {c->sstream, "side"}, {c->rstream, "resolve"}};
   for (auto &p : ss)
     if (p.first && hipStreamQuery(p.first) == hipErrorNotReady) busy += std::string(busy.empty() ? "" : ", ") + p.second;
-  // the flags through a stream of their own (the context's streams are stuck)
-  std::string flags = "unreadable";
-  hipStream_t d = nullptr;
-  if (c->d_flags && c->h_diag && hipStreamCreateWithFlags(&d, hipStreamNonBlocking) == hipSuccess) {
+  // the flags through a stream of their own (the context's streams are
+  // stuck), created at ks_open so that the report creates and destroys
+  // nothing; best effort: on a hung device the copy may never finish, and
+  // the report then says so rather than waiting for it
+  std::string flags = "unreadable (the device did not answer the read-back within 2 s)";
+  hipStream_t d = c->diag_stream;
+  if (c->d_flags && c->h_diag && d && hipStreamQuery(d) == hipSuccess) {
     if (hipMemcpyAsync(c->h_diag, c->d_flags, 16, hipMemcpyDeviceToHost, d) == hipSuccess) {
       const auto t0 = std::chrono::steady_clock::now();
       while (hipStreamQuery(d) == hipErrorNotReady &&
@@ -636,7 +642,6 @@ ks_status stall_report(ks_ctx *c, hipStream_t st, const char *what, double ms) {
         flags += stuck >= 0 ? std::string("; stuck: flag ") + kFlagName[stuck] : std::string("; every flag reached");
       }
     }
-    (void)hipStreamDestroy(d);  // returns once the copy is done or abandoned
   }
   return c->fail(KS_ERR_DEVICE,
                  "device stall: %s stream work of %s not finished after %.0f ms (round %u); unfinished streams: %s; %s",
@@ -3224,6 +3229,7 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
       HIPC(x, hipStreamCreateWithPriority(&x->sstream, hipStreamNonBlocking, hi));
     }
     x->xm.st = x->stream;
+    HIPC(x, hipStreamCreateWithFlags(&x->diag_stream, hipStreamNonBlocking));
     {  // value_sync = 0: cross-stream hand-offs by event waits instead
       int can = 0;
       (void)hipDeviceGetAttribute(&can, hipDeviceAttributeCanUseStreamWaitValue, cfg->device);
@@ -3322,7 +3328,7 @@ void ks_close(ks_ctx *c) {
   if (c->worker.joinable()) c->worker.join();
   (void)hipSetDevice(c->cfg.device);
   // bounded (a wedged context gets one more full timeout to finish)
-  const bool was_wedged = c->wedged;
+  const bool was_wedged = c->wedged.load();
   c->wedged = false;
   for (hipStream_t st : {c->stream, c->rstream, c->sstream})
     if (st && !c->wedged) (void)sync_bounded(c, st, "ks_close");
@@ -3372,6 +3378,7 @@ void ks_close(ks_ctx *c) {
     if (c->ev_swept[q]) (void)hipEventDestroy(c->ev_swept[q]);
     if (c->ev_fixed[q]) (void)hipEventDestroy(c->ev_fixed[q]);
   }
+  if (c->diag_stream && hipStreamQuery(c->diag_stream) == hipSuccess) (void)hipStreamDestroy(c->diag_stream);
   if (c->rstream) (void)hipStreamDestroy(c->rstream);
   if (c->sstream) (void)hipStreamDestroy(c->sstream);
   if (c->stream) (void)hipStreamDestroy(c->stream);

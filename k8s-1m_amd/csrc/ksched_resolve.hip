@@ -246,16 +246,24 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
     }
     return in ? s_gm[h] : 0ull;
   };
-  auto row_of = [&](uint32_t c, uint32_t j, uint32_t cand) -> CandRow {  // a gathered candidate's S0 row
-    CandRow w;
+  // s_prow[dst] <- a gathered candidate's node at the round start (its S0 row:
+  // live state = round-start state), copied piece by piece
+  auto prow_from_cand = [&](uint32_t dst, uint32_t c, uint32_t j, uint32_t cand, uint32_t slot) {
+    uint4 *d = (uint4 *)&s_prow[dst];
     if (cand < (uint32_t)PNR) {
-      uint4 *wp = (uint4 *)&w;
 #pragma unroll
-      for (int q = 0; q < ROW_PIECES; ++q) wp[q] = s_crow[c][q][cand];
-    } else {
-      w = a.crow[(size_t)s_rep[j] * a.K + s_ce[c][cand]];
+      for (int q = 0; q < ROW_PIECES; ++q) d[q] = s_crow[c][q][cand];
+    } else {  // beyond the prefetched rows: one global round trip
+      const uint4 *g = (const uint4 *)(a.crow + (size_t)s_rep[j] * a.K + s_ce[c][cand]);
+#pragma unroll
+      for (int q = 0; q < ROW_PIECES; ++q) d[q] = g[q];
     }
-    return w;
+    RNode &x = s_prow[dst];
+    x.rc0 = x.row.rc;
+    x.rm0 = x.row.rm;
+    x.np0 = x.row.np;
+    x.slot = slot;
+    x._pad[0] = x._pad[1] = 0;
   };
 
   // ---- stage the round
@@ -309,63 +317,110 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
       __builtin_amdgcn_s_waitcnt(0);
       clk.tick(12);
     }
-    static_for<PPW>([&](auto T) {
-      constexpr int t = T;
-      const uint32_t c = wid + PR_NW * t;
-      if (c >= cn) return;
-      const uint32_t j = f + c;
-      uint64_t rk;
-      if (s_dirty[j]) {  // Rpre's node was re-taken: the max over every M node again
-        const PQ q = s_q[j];
+    {
+      // The wave's four pods side by side, so that their LDS round trips
+      // overlap: scalar state in one batch, then the four first windows'
+      // membership probes of M interleaved.
+      uint32_t jt[PPW], nkt[PPW], bt[PPW], rept[PPW], dirt[PPW];
+      uint64_t rkt[PPW], kt[PPW] = {kw0, kw1, kw2, kw3};
+      bool on[PPW];
+#pragma unroll
+      for (int t = 0; t < PPW; ++t) {
+        const uint32_t c = wid + PR_NW * t;
+        on[t] = c < cn;
+        jt[t] = f + (on[t] ? c : 0u);
+        dirt[t] = s_dirty[jt[t]];
+        rkt[t] = s_rk[jt[t]];
+        nkt[t] = s_hdr[jt[t]].nkeys;
+        bt[t] = s_lptr[jt[t]];
+        rept[t] = s_rep[jt[t]];
+      }
+#pragma unroll
+      for (int t = 0; t < PPW; ++t) {
+        if (!on[t] || !dirt[t]) continue;
+        // Rpre's node was re-taken: the max over every M node again
+        const PQ q = s_q[jt[t]];
         uint64_t best = 0;
         const uint32_t mn = s_ctl[5];
         for (uint32_t m = lane; m < mn; m += WAVE) best = max64(best, pq_key(q, s_m[m].row, s_m[m].slot, a.w));
-        rk = wave_max_u64_dpp(best);
+        rkt[t] = wave_max_u64_dpp(best);
         if (lane == 0) {
-          s_rk[j] = rk;
-          s_dirty[j] = 0;
+          s_rk[jt[t]] = rkt[t];
+          s_dirty[jt[t]] = 0;
           if (a.prof) atomicAdd((unsigned long long *)&s_clk[10], 1ull);
         }
-      } else {
-        rk = s_rk[j];
       }
-      clk.tick(13);
-      const uint32_t nk = s_hdr[j].nkeys;
-      const uint64_t *keys = a.frec + (size_t)s_rep[j] * RW + REC_HDR_WORDS;
-      uint32_t base = s_lptr[j], cnt = 0, firstu = PNONE;
-      bool more = false;
-      uint64_t k = t == 0 ? kw0 : t == 1 ? kw1 : t == 2 ? kw2 : kw3;
-      while (base < nk) {
-        const uint32_t e = base + lane;
-        const bool valid = e < nk;
-        const bool unt = valid && mh_find(key_slot(k)) == PNONE;
-        const uint64_t um = __ballot(unt);
-        if (firstu == PNONE && um) firstu = base + (uint32_t)__builtin_ctzll(um);
-        const bool take = unt && k > rk;
-        const uint64_t tm = __ballot(take);
-        const uint32_t r = cnt + (uint32_t)__popcll(tm & lt_mask);
-        if (take && r < (uint32_t)PNC) {
-          s_ck[c][r] = k;
-          s_ce[c][r] = (uint16_t)e;
+      // membership of the first windows' slots in M: four probe chains at once
+      uint32_t ht[PPW], st[PPW];
+      bool pend[PPW], inm[PPW];
+#pragma unroll
+      for (int t = 0; t < PPW; ++t) {
+        st[t] = key_slot(kt[t]);
+        pend[t] = on[t] && bt[t] + lane < nkt[t];
+        inm[t] = false;
+        ht[t] = rhash(st[t]);
+      }
+      while (__ballot(pend[0] || pend[1] || pend[2] || pend[3])) {
+        uint32_t v[PPW];
+#pragma unroll
+        for (int t = 0; t < PPW; ++t) v[t] = pend[t] ? s_mh[ht[t]] : 0u;
+#pragma unroll
+        for (int t = 0; t < PPW; ++t) {
+          if (!pend[t]) continue;
+          if (v[t] == 0) {
+            pend[t] = false;
+          } else if (v[t] == st[t] + 1) {
+            inm[t] = true;
+            pend[t] = false;
+          } else {
+            ht[t] = (ht[t] + 1) & (PMH - 1);
+          }
         }
-        cnt += (uint32_t)__popcll(tm);
-        if (cnt >= (uint32_t)PNC) {
-          more = true;  // there may be more untaken entries above Rpre
-          break;
+      }
+      static_for<PPW>([&](auto T) {
+        constexpr int t = T;
+        const uint32_t c = wid + PR_NW * t;
+        if (c >= cn) return;
+        const uint32_t j = jt[t], nk = nkt[t];
+        const uint64_t rk = rkt[t];
+        const uint64_t *keys = a.frec + (size_t)rept[t] * RW + REC_HDR_WORDS;
+        uint32_t base = bt[t], cnt = 0, firstu = PNONE;
+        bool more = false;
+        uint64_t k = kt[t];
+        bool in = inm[t];
+        for (bool first_window = true; base < nk; first_window = false) {
+          const uint32_t e = base + lane;
+          const bool valid = e < nk;
+          if (!first_window) in = valid && mh_find(key_slot(k)) != PNONE;  // later windows: one probe chain
+          const bool unt = valid && !in;
+          const uint64_t um = __ballot(unt);
+          if (firstu == PNONE && um) firstu = base + (uint32_t)__builtin_ctzll(um);
+          const bool take = unt && k > rk;
+          const uint64_t tm = __ballot(take);
+          const uint32_t r = cnt + (uint32_t)__popcll(tm & lt_mask);
+          if (take && r < (uint32_t)PNC) {
+            s_ck[c][r] = k;
+            s_ce[c][r] = (uint16_t)e;
+          }
+          cnt += (uint32_t)__popcll(tm);
+          if (cnt >= (uint32_t)PNC) {
+            more = true;  // there may be more untaken entries above Rpre
+            break;
+          }
+          if (__ballot(valid && k <= rk)) break;  // keys descend: the rest are below Rpre
+          base += WAVE;
+          k = base + lane < nk ? keys[base + lane] : 0ull;
+          if (a.prof && lane == 0) atomicAdd((unsigned long long *)&s_clk[11], 1ull);
         }
-        if (__ballot(valid && k <= rk)) break;  // keys descend: the rest are below Rpre
-        base += WAVE;
-        k = base + lane < nk ? keys[base + lane] : 0ull;
-        if (a.prof && lane == 0) atomicAdd((unsigned long long *)&s_clk[11], 1ull);
-      }
-      if (lane == 0) {
-        s_cnc[c] = min(cnt, (uint32_t)PNC);
-        s_cmore[c] = more ? 1u : 0u;
-        s_lptr[j] = firstu != PNONE ? firstu : min(base + WAVE, nk);
-        const uint32_t feas = s_hdr[j].feasible - (uint32_t)s_dl[j];
-        s_cpst[c] = feas == 0 ? PD_UNSCHED : ((s_fl[j] & PF_PREF_ERR) && feas >= 2) ? PD_ERROR : PD_NODE;
-      }
-    });
+        if (lane == 0) {
+          s_cnc[c] = min(cnt, (uint32_t)PNC);
+          s_cmore[c] = more ? 1u : 0u;
+          s_lptr[j] = firstu != PNONE ? firstu : min(base + WAVE, nk);
+          const uint32_t feas = s_hdr[j].feasible - (uint32_t)s_dl[j];
+          s_cpst[c] = feas == 0 ? PD_UNSCHED : ((s_fl[j] & PF_PREF_ERR) && feas >= 2) ? PD_ERROR : PD_NODE;
+        }
+      });
+    }
     // the first PNR candidates' rows of the wave's pods by LDS-DMA, lane r ->
     // row r, issued after every scan (the compiler waits for all outstanding
     // loads before a scan's key use); landed before the barrier
@@ -451,7 +506,10 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
         ps = PNONE;
       }
       // the proposed node's state at the chunk start
-      if (live && code == PD_NODE) s_prow[c] = src >= PSRC_M ? s_m[src & 0xFFFFu] : rnode_from_row(row_of(c, j, src), ps);
+      if (live && code == PD_NODE) {
+        if (src >= PSRC_M) s_prow[c] = s_m[src & 0xFFFFu];
+        else prow_from_cand(c, c, j, src, ps);
+      }
       // lanes proposing the same slot: first of the group, next member
       s_gh[lane] = 0;
       s_gh[lane + WAVE] = 0;
@@ -572,12 +630,12 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
         // the node the exact decision commits, at the chunk start
         const uint32_t ws = key_slot(win);
         if (win == ku) {
-          s_prow[c] = rnode_from_row(row_of(c, j, kidx), ws);
+          prow_from_cand(c, c, j, kidx, ws);
         } else {
           uint32_t from = PNONE;
           for (uint32_t i = 0; i < c && from == PNONE; ++i)
             if (s_ps[i] == ws) from = i;
-          s_prow[c] = from != PNONE ? s_prow[from] : s_m[mh_find(ws)];
+          s_prow[c] = *(from != PNONE ? &s_prow[from] : &s_m[mh_find(ws)]);
         }
       }
       const bool fx = c < nfix;
@@ -601,7 +659,7 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
       const uint32_t mn = s_ctl[5];
       if (first) {
         const uint32_t mi = isnew ? mn + (uint32_t)__popcll(nm & lt_mask) : mi0;
-        RNode x = isnew ? s_prow[c] : s_m[mi];
+        RNode x = *(isnew ? &s_prow[c] : &s_m[mi]);
         const uint32_t d = (uint32_t)__popcll(fm & lt_mask);
         s_cdm[d] = mi;
         s_cdp[d][0] = x.row.rc;

@@ -66,8 +66,27 @@ struct ksg_evaluator {
   std::deque<Fired> fired_q;
   std::condition_variable fired_cv;  // with `lock`: fired_q grew, or closing
   bool closing = false;
-  uint32_t inside = 0;  // threads inside record_and_wait / next_fired (ksg_close waits for 0)
+  uint32_t inside = 0;  // threads inside record_and_wait / record / next_fired (ksg_close waits for 0)
   std::condition_variable idle_cv;
+
+  // Entry into an API call that may touch the evaluator after ksg_close
+  // began: refused once closing, else counted in `inside` until the guard
+  // goes out of scope (the last one out lets ksg_close free the evaluator).
+  struct Inside {
+    ksg_evaluator *ev = nullptr;
+    ~Inside() {
+      if (!ev) return;
+      std::lock_guard<std::mutex> g(ev->lock);
+      if (--ev->inside == 0) ev->idle_cv.notify_all();
+    }
+  };
+  // caller holds `lock`
+  bool enter(Inside &in, bool allow_closing = false) {
+    if (closing && !allow_closing) return false;
+    inside++;
+    in.ev = this;
+    return true;
+  }
 
   uint64_t rank_of(const std::string &node) {  // caller holds `lock`
     auto it = order.find(node);
@@ -164,6 +183,17 @@ ksg_evaluator *ksg_open(uint32_t members, uint32_t delay_ms, int32_t tie_mode, u
 
 // Close: fire every pending evaluation (its waiters return with the scores
 // recorded so far), wake ksg_next_fired, and free once no thread is inside.
+void ksg_shutdown(ksg_evaluator *ev) {
+  if (!ev) return;
+  {
+    std::lock_guard<std::mutex> g(ev->lock);
+    ev->closing = true;
+  }
+  ev->fire_expired(true);
+  std::lock_guard<std::mutex> g(ev->lock);
+  ev->fired_cv.notify_all();
+}
+
 void ksg_close(ksg_evaluator *ev) {
   if (!ev) return;
   {
@@ -197,18 +227,11 @@ int32_t ksg_record_and_wait(ksg_evaluator *ev, const char *key, const char *node
                             uint32_t winner_cap, int32_t *winner_score) {
   if (!ev || !key || !node_name) return -1;
   const std::string k(key);
+  ksg_evaluator::Inside in;
   {
     std::lock_guard<std::mutex> g(ev->lock);
-    if (ev->closing) return -1;
-    ev->inside++;
+    if (!ev->enter(in)) return -1;
   }
-  struct Leave {  // the last thread out lets ksg_close free the evaluator
-    ksg_evaluator *ev;
-    ~Leave() {
-      std::lock_guard<std::mutex> g(ev->lock);
-      if (--ev->inside == 0) ev->idle_cv.notify_all();
-    }
-  } leave{ev};
   std::shared_ptr<One> o;
   std::unique_lock<std::mutex> l;
   for (;;) {  // an evaluation that fired before we locked it: the score starts a new one
@@ -241,12 +264,18 @@ int32_t ksg_record(ksg_evaluator *ev, const char *key, const char *node_name, in
                    char *winner, uint32_t winner_cap, int32_t *winner_score) {
   if (!ev || !key || !node_name || !eval_id) return -1;
   const std::string k(key);
+  // counted in `inside` like the other calls: ksg_close must not free the
+  // evaluator while this call still locks o->m / fires / takes ev->lock
+  ksg_evaluator::Inside in;
+  {
+    std::lock_guard<std::mutex> g(ev->lock);
+    if (!ev->enter(in)) return -1;
+  }
   std::shared_ptr<One> o;
   std::unique_lock<std::mutex> l;
   for (;;) {  // as ksg_record_and_wait: never join an evaluation that already fired
     {
       std::lock_guard<std::mutex> g(ev->lock);
-      if (ev->closing) return -1;
       o = ev->evaluation(k);
     }
     l = std::unique_lock<std::mutex>(o->m);
@@ -273,18 +302,12 @@ int32_t ksg_next_fired(ksg_evaluator *ev, uint32_t timeout_ms, uint64_t *eval_id
                        int32_t *winner_score) {
   if (!ev || !eval_id) return -1;
   const auto until = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms);
+  ksg_evaluator::Inside in;
   {
     std::lock_guard<std::mutex> g(ev->lock);
     if (ev->closing && ev->fired_q.empty()) return -1;
-    ev->inside++;
+    ev->enter(in, true);  // still drains evaluations fired by the close
   }
-  struct Leave {
-    ksg_evaluator *ev;
-    ~Leave() {
-      std::lock_guard<std::mutex> g(ev->lock);
-      if (--ev->inside == 0) ev->idle_cv.notify_all();
-    }
-  } leave{ev};
   for (;;) {
     ev->fire_expired(false);  // deadlines of evaluations nobody waits on synchronously
     std::unique_lock<std::mutex> g(ev->lock);

@@ -321,7 +321,7 @@ KSCHED_SYMBOLS = [
 ]
 KSGATHER_SYMBOLS = [
     "ksg_open", "ksg_close", "ksg_set_members", "ksg_record_and_wait", "ksg_pending", "ksg_fnv1_32", "ksg_target_index",
-    "ksg_record", "ksg_next_fired", "ksg_set_node_order",
+    "ksg_record", "ksg_next_fired", "ksg_set_node_order", "ksg_shutdown",
 ]
 KSYNTH_SYMBOLS = [
     "ksynth_nodes", "ksynth_pods", "ksynth_prefill", "ksynth_besteffort_pods", "ksynth_spread_pods", "ksynth_affinity_pods", "ksynth_node_array",
@@ -451,6 +451,8 @@ def ksgather_lib() -> C.CDLL:
     L.ksg_open.restype = vp
     L.ksg_close.argtypes = [vp]
     L.ksg_close.restype = None
+    L.ksg_shutdown.argtypes = [vp]
+    L.ksg_shutdown.restype = None
     L.ksg_set_members.argtypes = [vp, C.c_uint32]
     L.ksg_set_members.restype = None
     L.ksg_record_and_wait.argtypes = [vp, C.c_char_p, C.c_char_p, C.c_int32, C.c_char_p, C.c_uint32, P(C.c_int32)]

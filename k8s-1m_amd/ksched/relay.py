@@ -19,6 +19,7 @@ this path.
 from __future__ import annotations
 
 import asyncio
+import contextlib
 import ctypes as C
 import threading
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -72,22 +73,45 @@ class ScoreEvaluator:
         self.h = self.lib.ksg_open(members, int(delay_s * 1000), tie, seed)
         if not self.h:
             raise ValueError("ksg_open: bad arguments")
+        # Call gate: a thread holds a use of the handle from before it reads it
+        # until its C call returns, and close() frees only after every use
+        # ended (ksg_shutdown first releases the callers blocked inside), so
+        # no call ever reaches a freed evaluator.
+        self._gate = threading.Condition()
+        self._uses = 0
+
+    @contextlib.contextmanager
+    def _use(self, what: str):
+        with self._gate:
+            if self.h is None:
+                raise ValueError(f"{what}: evaluator closed")
+            self._uses += 1
+            h = self.h
+        try:
+            yield h
+        finally:
+            with self._gate:
+                self._uses -= 1
+                self._gate.notify_all()
 
     def set_members(self, members: int):
-        self.lib.ksg_set_members(self.h, members)
+        with self._use("ksg_set_members") as h:
+            self.lib.ksg_set_members(h, members)
 
     def set_node_order(self, names: Sequence[str]):
         """TIE_LOWEST_INDEX: names[i] is global node index i (the hosts' slots end to end)."""
         arr = (C.c_char_p * max(1, len(names)))(*[n.encode() for n in names])
-        self.lib.ksg_set_node_order(self.h, arr, len(names))
+        with self._use("ksg_set_node_order") as h:
+            self.lib.ksg_set_node_order(h, arr, len(names))
 
     def record(self, key: str, node_name: str, score: int):
         """Non-blocking record: (True/False, winner, score) when this score fired
         the evaluation, else ("pending", evaluation id)."""
         buf = C.create_string_buffer(512)
         ws, eid = C.c_int32(), C.c_uint64()
-        r = self.lib.ksg_record(self.h, key.encode(), node_name.encode(), int(score), C.byref(eid), buf, 512,
-                                C.byref(ws))
+        with self._use("ksg_record") as h:
+            r = self.lib.ksg_record(h, key.encode(), node_name.encode(), int(score), C.byref(eid), buf, 512,
+                                    C.byref(ws))
         if r < 0:
             raise ValueError("ksg_record: bad arguments or closed")
         if r == 2:
@@ -99,7 +123,11 @@ class ScoreEvaluator:
         records that fired, None on timeout, False once closed."""
         buf = C.create_string_buffer(512)
         eid, ws = C.c_uint64(), C.c_int32()
-        r = self.lib.ksg_next_fired(self.h, timeout_ms, C.byref(eid), buf, 512, C.byref(ws))
+        try:
+            with self._use("ksg_next_fired") as h:
+                r = self.lib.ksg_next_fired(h, timeout_ms, C.byref(eid), buf, 512, C.byref(ws))
+        except ValueError:
+            return False  # closed
         if r < 0:
             return False
         if r == 0:
@@ -110,18 +138,27 @@ class ScoreEvaluator:
         """Blocks (without the GIL) until the pod fires; (permit, winner, winner score)."""
         buf = C.create_string_buffer(512)
         ws = C.c_int32()
-        r = self.lib.ksg_record_and_wait(self.h, key.encode(), node_name.encode(), int(score), buf, 512, C.byref(ws))
+        with self._use("ksg_record_and_wait") as h:
+            r = self.lib.ksg_record_and_wait(h, key.encode(), node_name.encode(), int(score), buf, 512, C.byref(ws))
         if r < 0:
             raise ValueError("ksg_record_and_wait: bad arguments")
         return r == 1, buf.value.decode(), ws.value
 
     def pending(self) -> int:
-        return self.lib.ksg_pending(self.h)
+        with self._use("ksg_pending") as h:
+            return self.lib.ksg_pending(h)
 
     def close(self):
-        if self.h:
-            self.lib.ksg_close(self.h)
-            self.h = None
+        """Fires every pending pod (its senders get their answers), refuses
+        later calls, and frees the state machine once no call is inside."""
+        with self._gate:
+            h, self.h = self.h, None
+        if not h:
+            return
+        self.lib.ksg_shutdown(h)  # releases callers blocked in record_and_wait
+        with self._gate:
+            self._gate.wait_for(lambda: self._uses == 0)
+        self.lib.ksg_close(h)
 
 
 def target_index(key: str, members: Sequence[str], leader: Optional[str] = None) -> int:
@@ -153,11 +190,17 @@ class CollectScoreServer:
         self._fired = threading.Thread(target=self._fired_loop, name="collect-score-fired", daemon=True)
         self.port = 0
         self.address = ""
+        self._start_error: Optional[BaseException] = None
 
     # -- event loop thread
     def _serve(self):
         asyncio.set_event_loop(self._loop)
-        self._loop.run_until_complete(self._start())
+        try:
+            self._loop.run_until_complete(self._start())
+        except BaseException as e:  # e.g. the address cannot be bound: start() re-raises it
+            self._start_error = e
+            self._ready.set()
+            return
         self._ready.set()
         self._loop.run_forever()
 
@@ -186,30 +229,41 @@ class CollectScoreServer:
 
     # -- the one thread that waits for evaluations to fire
     def _fired_loop(self):
-        while not self._stopped.is_set():
+        # every evaluation that has fired is reported before the loop ends,
+        # those a closed evaluator fired included (next_fired drains them)
+        while True:
             r = self.evaluator.next_fired(200)
-            if r is False:
+            if r is False:  # closed and drained
                 break
             if r:
                 self._loop.call_soon_threadsafe(self._resolve, r[0], r[1])
+            elif self._stopped.is_set():
+                break
 
     def start(self):
         self._thread.start()
-        self._ready.wait(30)
+        if not self._ready.wait(30):
+            raise TimeoutError("CollectScore server did not start within 30 s")
+        if self._start_error is not None:
+            self._thread.join(5)
+            raise self._start_error
         self._fired.start()
         return self
 
-    def stop(self):
-        """Stops serving; RPCs still parked are answered by the evaluator's
-        close (ScoreEvaluator.close fires every pending pod)."""
+    def stop(self, grace: float = 0.5):
+        """Stops serving.  Senders parked on an evaluation that has fired by
+        now get their answer -- close the ScoreEvaluator first to fire every
+        pending pod with the scores recorded so far; senders still parked after
+        `grace` seconds are cancelled (the sender sees an RPC error: no permit,
+        as DistPermit treats a failed SendScore)."""
         self._stopped.set()
-        fut = asyncio.run_coroutine_threadsafe(self.server.stop(grace=None), self._loop)
+        self._fired.join(30)  # fired evaluations reported to the loop
+        fut = asyncio.run_coroutine_threadsafe(self.server.stop(grace=grace), self._loop)
         try:
-            fut.result(30)
+            fut.result(30 + grace)
         finally:
             self._loop.call_soon_threadsafe(self._loop.stop)
             self._thread.join(30)
-            self._fired.join(30)
 
 
 class ScoreClient:

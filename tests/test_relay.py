@@ -190,3 +190,69 @@ def test_close_releases_waiters():
     assert time.time() - t0 < 5 and len(out) == 3
     assert sorted(o[0] for o in out) == [False, False, True]
     assert all(o[1:] == ("n2", 12) for o in out)
+
+
+def test_close_evaluator_while_rpcs_are_parked():
+    # ScoreEvaluator.close() with CollectScore RPCs parked on an unfired pod
+    # (one member never scores): close fires the pod with the scores recorded
+    # so far and the server answers every parked sender before it stops; the
+    # evaluator is freed only after no server thread is inside a call on it
+    ev = relay.ScoreEvaluator(members=3, delay_s=60, tie=relay.TIE_LOWEST_NAME)
+    srv = relay.CollectScoreServer(ev).start()
+    cli = relay.ScoreClient(srv.address)
+    out = [None, None]
+
+    def send(i, node, score):
+        out[i] = cli.send_score("parked", "ns", node, score, timeout=20)
+
+    th = [threading.Thread(target=send, args=(0, "n1", 400)), threading.Thread(target=send, args=(1, "n2", 300))]
+    for t in th:
+        t.start()
+    deadline = time.time() + 10
+    while ev.pending() == 0 and time.time() < deadline:
+        time.sleep(0.01)
+    time.sleep(0.2)
+    t0 = time.time()
+    ev.close()  # fires "ns/parked": n1 wins
+    for t in th:
+        t.join(15)
+    srv.stop()
+    assert out == [True, False] and time.time() - t0 < 10
+
+
+def test_close_evaluator_races_async_records():
+    # ksg_record calls racing ksg_close: each either records (and is reported
+    # or answered) or is refused; none touches the evaluator after it is freed
+    for _ in range(20):
+        ev = relay.ScoreEvaluator(members=4, delay_s=30, tie=relay.TIE_LOWEST_NAME)
+        stop = threading.Event()
+
+        def spam(k):
+            i = 0
+            while not stop.is_set() and i < 200:
+                try:
+                    ev.record(f"ns/p{k}-{i}", f"n{k}", 10 + i % 7)
+                except ValueError:  # refused: the evaluator is closing / closed
+                    return
+                i += 1
+
+        th = [threading.Thread(target=spam, args=(k,)) for k in range(4)]
+        for t in th:
+            t.start()
+        time.sleep(0.002)
+        ev.close()
+        stop.set()
+        for t in th:
+            t.join(10)
+        assert not any(t.is_alive() for t in th)
+
+
+def test_start_reports_a_bind_failure():
+    # an address gRPC cannot bind: start() raises instead of returning a
+    # server with port 0 and no loop
+    ev = relay.ScoreEvaluator(members=1, delay_s=1, tie=relay.TIE_LOWEST_NAME)
+    try:
+        with pytest.raises(Exception):
+            relay.CollectScoreServer(ev, address="256.256.256.256:70000").start()
+    finally:
+        ev.close()

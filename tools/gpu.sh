@@ -79,7 +79,7 @@ PY
   pmc)
     # one counter group per rocprofv3 run (MI355X_MICROARCH.md); stream
     # wait-value hand-offs stall behind counter collection, so event waits
-    ARGS="--steps 2 --warmup 1 --no-cpu-baseline --no-resident --latency-calls 0 --opt value_sync=0 $*"
+    ARGS="--steps 2 --warmup 1 --no-cpu-baseline --no-resident --latency-calls 0 --opt value_sync=0 --opt sync_timeout_ms=600000 $*"
     ( while sleep 30; do echo "pmc: alive"; done ) &
     HB=$!
     trap 'kill $HB 2>/dev/null' EXIT
@@ -103,7 +103,7 @@ PY
     mkdir -p gpurun_out/sq_$TAG
     timeout -s KILL 170 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_WAVES SQ_WAVE_CYCLES \
       SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU -d "$R/gpurun_out/sq_$TAG/p1" -o run --output-format csv -- \
-      python3 "$R/bench.py" --steps 1 --warmup 1 --no-cpu-baseline --no-resident --latency-calls 0 --opt value_sync=0 "$@" \
+      python3 "$R/bench.py" --steps 1 --warmup 1 --no-cpu-baseline --no-resident --latency-calls 0 --opt value_sync=0 --opt sync_timeout_ms=600000 "$@" \
       > gpurun_out/sq_$TAG/p1.json 2> gpurun_out/sq_$TAG/p1.err
     rc=$?; echo "sq rc=$rc"; exit $rc ;;
   ab)
