@@ -12,6 +12,9 @@ from pathlib import Path
 LIB_DIR = Path(__file__).resolve().parent / "lib"
 # KSCHED_LIB_DIR selects a diagnostic libksched build (e.g. lib/stamps)
 KSCHED_DIR = Path(os.environ.get("KSCHED_LIB_DIR", LIB_DIR))
+# KSCHED_HOST_LIB_DIR selects builds of the host-only libraries (libksynth,
+# libksgather), e.g. lib/asan (make sanitize)
+HOST_DIR = Path(os.environ.get("KSCHED_HOST_LIB_DIR", LIB_DIR))
 
 c_char_p = C.c_char_p
 
@@ -407,7 +410,7 @@ def ksynth_lib() -> C.CDLL:
     global _ksynth
     if _ksynth is not None:
         return _ksynth
-    L = _load("libksynth.so")
+    L = _load("libksynth.so", HOST_DIR)
     vp = C.c_void_p
     P = C.POINTER
     L.ksynth_nodes.argtypes = [C.c_int32, C.c_uint32, C.c_uint64]
@@ -444,7 +447,7 @@ def ksgather_lib() -> C.CDLL:
     global _ksgather
     if _ksgather is not None:
         return _ksgather
-    L = _load("libksgather.so")
+    L = _load("libksgather.so", HOST_DIR)
     vp = C.c_void_p
     P = C.POINTER
     L.ksg_open.argtypes = [C.c_uint32, C.c_uint32, C.c_int32, C.c_uint64]

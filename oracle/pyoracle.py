@@ -7,6 +7,7 @@ PARITY UNPINNED).
 from __future__ import annotations
 
 import ctypes as C
+import os
 import sys
 from pathlib import Path
 
@@ -14,7 +15,8 @@ ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT / "k8s-1m_amd"))
 from ksched import _abi  # noqa: E402  (struct definitions only)
 
-LIB = ROOT / "oracle" / "_build" / "liboracle.so"
+# ORACLE_LIB: another build of the same source (oracle/_build/asan: make sanitize)
+LIB = Path(os.environ.get("ORACLE_LIB", ROOT / "oracle" / "_build" / "liboracle.so"))
 
 
 class ShardPrescore(C.Structure):
