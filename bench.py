@@ -120,6 +120,9 @@ def parse():
     ap.add_argument("--cpu-pods", type=int, default=24, help="oracle sample (pods), single thread")
     ap.add_argument("--cpu-pods-mt", type=int, default=400, help="oracle sample (pods), multi-thread")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch check only: spawn / join the ranks, exchange the rendezvous file, check "
+                         "RANK / LOCAL_RANK / WORLD_SIZE, print one JSON line per rank; no GPU call")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="ks_config execution option (include/ksched.h), e.g. resolve_mode=1; none changes a result")
     ap.add_argument("--resolve-profile", action="store_true",
@@ -172,14 +175,17 @@ def uid_path(world: int) -> Path:
     return Path(os.environ.get("TMPDIR", "/tmp")) / f"ksched_uid_{key}_w{world}.bin"
 
 
-def exchange_unique_id(rank: int, world: int) -> bytes:
-    """Rank 0 publishes the RCCL unique id in a file every local rank reads."""
-    from ksched import Scheduler
-
+def exchange_unique_id(rank: int, world: int, uid: bytes = None) -> bytes:
+    """Rank 0 publishes the RCCL unique id in a file every local rank reads
+    (uid: a given 128-byte id instead of ncclGetUniqueId's, --dry-run)."""
     path = uid_path(world)
     if rank == 0:
+        if uid is None:
+            from ksched import Scheduler
+
+            uid = Scheduler.comm_unique_id()
         tmp = path.with_suffix(".tmp")
-        tmp.write_bytes(Scheduler.comm_unique_id())
+        tmp.write_bytes(uid)
         os.replace(tmp, path)
         return path.read_bytes()
     deadline = time.time() + 300
@@ -202,6 +208,8 @@ def main():
         sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        return dry_run(args, world, rank, local_rank)
     # No torch in this process: torch bundles its own libamdhip64 / librccl
     # (ROCm 7.0) with the same sonames as the /opt/rocm 7.2 libraries
     # libksched links, and one process must not mix the two runtimes.  The
@@ -221,6 +229,26 @@ def main():
     if args.workload == "c5":
         return run_c5(args, kind, sched, world, rank, t_setup)
     return run_batches(args, kind, sched, world, rank, t_setup)
+
+
+def dry_run(args, world, rank, local_rank):
+    """The multi-rank launch without the GPU: the environment every rank
+    reads, the rendezvous file (a synthetic id, checked byte for byte by
+    every rank), the device each rank would open; one JSON line per rank."""
+    ok = 0 <= rank < world and 0 <= local_rank < world and int(os.environ.get("LOCAL_WORLD_SIZE", world)) == world
+    if world > 1:
+        uid = bytes((i * 7 + 3) & 0xFF for i in range(128))  # the same synthetic id on every rank
+        got = exchange_unique_id(rank, world, uid if rank == 0 else None)
+        ok = ok and got == uid
+        if rank == 0:  # every rank has the file open or read by the time rank 0 removes it:
+            time.sleep(1.0)  # (the real launch removes it after ncclCommInitRank returns)
+            uid_path(world).unlink(missing_ok=True)
+    line = {"dry_run": True, "rank": rank, "local_rank": local_rank, "world_size": world,
+            "device": local_rank if world > 1 else 0, "master": f"{os.environ.get('MASTER_ADDR', '')}:"
+                                                               f"{os.environ.get('MASTER_PORT', '')}",
+            "rendezvous_ok": bool(ok)}
+    print(json.dumps(line), flush=True)
+    return 0 if ok else 1
 
 
 def pod_stream(args, kind, n, seed):
@@ -705,4 +733,4 @@ def cpu_baseline(args, nodes, slots, pre, pods):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())
