@@ -437,6 +437,15 @@ int32_t ks_abi_version(void);
  * upstream internal/cache AddNode/UpdateNode/RemoveNode).  Upsert of an
  * existing slot keeps its Requested/NonZeroRequested/pod count. */
 ks_status ks_nodes_upsert(ks_ctx *ctx, const ks_node *nodes, const uint32_t *slots, uint32_t n);
+/* Per-item form: each item is validated on its own (slot, name, cpu / memory
+ * allocatable below 2^44 -- LeastAllocated's exact-floor bound, DESIGN.md §4 --
+ * non-negative extended / ephemeral-storage allocatable, any int64 size) and
+ * status[i] = KS_OK or that item's error; the valid items are applied as one
+ * ks_nodes_upsert.  Returns KS_OK when every item was applied, else the first
+ * failing item's status (ks_last_error names it).  ks_nodes_upsert itself
+ * applies nothing when any item is invalid. */
+ks_status ks_nodes_upsert_each(ks_ctx *ctx, const ks_node *nodes, const uint32_t *slots, uint32_t n,
+                               ks_status *status);
 ks_status ks_nodes_delete(ks_ctx *ctx, const uint32_t *slots, uint32_t n);
 
 /* Generation-based snapshot update (upstream Cache.UpdateSnapshot,

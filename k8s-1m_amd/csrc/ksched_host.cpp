@@ -3554,8 +3554,11 @@ ks_status ks_nodes_upsert(ks_ctx *c, const ks_node *nodes, const uint32_t *slots
           a[it->second] = nd.extended[k].value;
       }
       for (uint32_t col = 0; col < a.size(); ++col) {
-        if (a[col] < 0 || a[col] >= kMaxAlloc)
-          return c->fail(KS_ERR_RANGE, "node %s extended allocatable outside the exact range", str(nd.name).c_str());
+        // extended / ephemeral columns are only compared (Fit: request >
+        // Allocatable - Requested, exact int64), so any non-negative int64 is
+        // exact; the 2^44 bound is LeastAllocated's (cpu and memory only)
+        if (a[col] < 0)
+          return c->fail(KS_ERR_RANGE, "node %s extended allocatable negative", str(nd.name).c_str());
         idx.push_back(col * (uint64_t)c->npos + pos);
         val.push_back(a[col]);
         if (core[(size_t)row_of[kv.first] * 8 + 3]) {  // new node: Requested = 0
@@ -3567,6 +3570,79 @@ ks_status ks_nodes_upsert(ks_ctx *c, const ks_node *nodes, const uint32_t *slots
     if ((st = xres_scatter(c, idx, val, false))) return st;
   }
   return spread_nodes_changed(c, changed.data(), (uint32_t)changed.size(), false);
+}
+
+// Per-item form (include/ksched.h): every item is validated on its own and
+// only the valid ones are applied, as one ks_nodes_upsert call.
+ks_status ks_nodes_upsert_each(ks_ctx *c, const ks_node *nodes, const uint32_t *slots, uint32_t n, ks_status *status) {
+  if (!c || !status || (n && (!nodes || !slots))) return KS_ERR_INVALID;
+  if (ks_status dst_ = drain_async(c)) return dst_;
+  std::vector<ks_node> ok_nodes;
+  std::vector<uint32_t> ok_slots, ok_idx;
+  ks_status first = KS_OK;
+  std::string first_err;
+  std::unordered_map<std::string, uint32_t> call_names;  // accepted items' names -> slot
+  std::unordered_set<uint32_t> in_call;
+  for (uint32_t i = 0; i < n; ++i)
+    if (slots[i] < c->cap) in_call.insert(slots[i]);
+  for (uint32_t i = 0; i < n; ++i) {
+    const ks_node &s = nodes[i];
+    const uint32_t slot = slots[i];
+    ks_status st = KS_OK;
+    std::string why;
+    const std::string nm = str(s.name);
+    if (slot >= c->cap) {
+      st = KS_ERR_NOT_FOUND;
+      why = "slot " + std::to_string(slot) + " >= capacity";
+    } else if (s.alloc_milli_cpu < 0 || s.alloc_milli_cpu >= kMaxAlloc || s.alloc_memory < 0 ||
+               s.alloc_memory >= kMaxAlloc || s.alloc_pods < 0 || s.alloc_pods > INT32_MAX - 1) {
+      st = KS_ERR_RANGE;
+      why = "node " + nm + " allocatable outside the exact range";
+    } else {
+      for (uint32_t k = 0; k < s.n_extended && !st; ++k)
+        if (s.extended[k].value < 0) {
+          st = KS_ERR_RANGE;
+          why = "node " + nm + " extended allocatable negative";
+        }
+    }
+    if (!st) {
+      auto ci = call_names.find(nm);
+      if (ci != call_names.end() && ci->second != slot) {
+        st = KS_ERR_INVALID;
+        why = "node name " + nm + " given to two slots";
+      } else {
+        const int64_t nid = c->lookup(s.name);
+        if (nid >= 0) {
+          auto it = c->name_slot.find((uint32_t)nid);
+          if (it != c->name_slot.end() && it->second != slot && c->nodes[it->second].present &&
+              !in_call.count(it->second)) {
+            st = KS_ERR_INVALID;
+            why = "node name " + nm + " already names another slot";
+          }
+        }
+      }
+    }
+    status[i] = st;
+    if (st) {
+      if (!first) {
+        first = st;
+        first_err = why;
+      }
+      continue;
+    }
+    call_names.emplace(nm, slot);
+    ok_nodes.push_back(s);
+    ok_slots.push_back(slot);
+    ok_idx.push_back(i);
+  }
+  if (!ok_nodes.empty()) {
+    if (ks_status st = ks_nodes_upsert(c, ok_nodes.data(), ok_slots.data(), (uint32_t)ok_nodes.size())) {
+      for (uint32_t i : ok_idx) status[i] = st;  // a call-level failure (capacity, device): nothing applied
+      return st;
+    }
+  }
+  if (first) return c->fail(first, "%s (the other items were applied)", first_err.c_str());
+  return KS_OK;
 }
 
 ks_status ks_nodes_delete(ks_ctx *c, const uint32_t *slots, uint32_t n) {

@@ -317,6 +317,7 @@ STRUCTS = {
 
 KSCHED_SYMBOLS = [
     "ks_config_default", "ks_open", "ks_close", "ks_last_error", "ks_abi_version", "ks_nodes_upsert",
+    "ks_nodes_upsert_each",
     "ks_nodes_delete", "ks_pods_add", "ks_pods_remove", "ks_events_apply", "ks_schedule", "ks_batch_prepare", "ks_batch_run",
     "ks_batch_results", "ks_batch_free", "ks_batch_submit", "ks_batch_wait", "ks_pods_check", "ks_plugin_scores", "ks_node_states", "ks_comm_unique_id", "ks_comm_init_local", "ks_snapshot_update",
     "ks_comm_init", "ks_comm_allreduce_max", "ks_get_stats", "ks_reset_stats", "ks_set_timing",
@@ -368,6 +369,7 @@ def ksched_lib() -> C.CDLL:
     L.ks_last_error.restype = c_char_p
     L.ks_abi_version.restype = C.c_int32
     L.ks_nodes_upsert.argtypes = [vp, P(KsNode), P(C.c_uint32), C.c_uint32]
+    L.ks_nodes_upsert_each.argtypes = [vp, P(KsNode), P(C.c_uint32), C.c_uint32, P(C.c_int32)]
     L.ks_nodes_delete.argtypes = [vp, P(C.c_uint32), C.c_uint32]
     L.ks_pods_add.argtypes = [vp, P(KsPod), P(C.c_uint32), C.c_uint32]
     L.ks_pods_remove.argtypes = [vp, P(KsPod), P(C.c_uint32), C.c_uint32]

@@ -56,6 +56,29 @@ def gpus_and_ephemeral():
 
 
 @case
+def huge_ephemeral():
+    # ephemeral-storage allocatable far above 2^44 (20 TiB, 5 TiB): extended
+    # columns are compared in exact int64, only cpu / memory are bounded by
+    # LeastAllocated's exact-floor range
+    Ti = 1 << 40
+    nodes = [node("n0", {"ephemeral-storage": 5 * Ti}), node("n1", {"ephemeral-storage": 20 * Ti}), node("n2"),
+             node("n3", {"ephemeral-storage": (1 << 62) + 12345})]
+    # every node has the same cpu / memory: equal scores go to the lowest
+    # slot, and a node that took a pod scores lower afterwards (LeastAllocated)
+    pods = [
+        pod("a", {"ephemeral-storage": 8 * Ti}),   # n1, n3 fit: tie -> n1
+        pod("b", {"ephemeral-storage": 8 * Ti}),   # n1 (12 TiB left), n3: n3 is emptier
+        pod("c", {"ephemeral-storage": 8 * Ti}),   # n1, n3 (one pod each): tie -> n1, 4 TiB left
+        pod("d", {"ephemeral-storage": 5 * Ti}),   # n0 (exactly 5 TiB) and n3 fit: n0 is empty
+        pod("e", {"ephemeral-storage": (1 << 62)}),  # n3 has 2^62 + 12345 - 16 TiB left: none
+        pod("f", {"ephemeral-storage": 1}),        # n0 is full: n1, n3
+    ]
+    exp = [dict(node=1, feasible=2), dict(node=3, feasible=2), dict(node=1, feasible=2), dict(node=0, feasible=2),
+           dict(node=None, status=1, fails={FIT: 4}), dict(feasible=2)]
+    return nodes, [], pods, exp, {}
+
+
+@case
 def image_locality():
     MB = Mi
     # nginx:1.25 on n0 (500MB, the first reporter) and n1 (reports 800MB: the

@@ -223,3 +223,42 @@ def test_taint_dictionary_rebuild_after_churn():
         dbg = (C.c_uint64 * 16)()
         assert s.lib.ks_debug_counters(s.ctx, dbg) == 0
         assert dbg[6] >= 1, list(dbg)
+
+
+def test_node_range_errors_fail_their_own_item_only():
+    # ks_nodes_upsert_each: a node whose memory allocatable is >= 2^44
+    # (LeastAllocated's exact-floor bound) fails alone with
+    # KS_ERR_RANGE; the others -- a 20 TiB ephemeral-storage node among them,
+    # which only Fit compares, in exact int64 -- are applied and scheduled
+    # bit-exact against the oracle holding the same nodes.  ks_nodes_upsert
+    # applies nothing from the same call.
+    from ksched.objects import Container, Node, Pod
+
+    Gi, Ti = 1 << 30, 1 << 40
+    nodes = [Node(f"n{i}", {"cpu": 16000, "memory": 64 * Gi, "pods": 110}, {}, [], False) for i in range(6)]
+    nodes[3] = Node("n3", {"cpu": 16000, "memory": 1 << 45, "pods": 110}, {}, [], False)
+    nodes[5] = Node("n5", {"cpu": 16000, "memory": 64 * Gi, "pods": 110}, {}, [], False,
+                    extended={"ephemeral-storage": 20 * Ti})
+    a = Arena()
+    na, n = nodes_array(nodes, a)
+    slots = (C.c_uint32 * n)(*range(n))
+    with Scheduler(n) as s:
+        assert s.lib.ks_nodes_upsert(s.ctx, na, slots, n) == 5  # KS_ERR_RANGE: the whole call refused
+        st = s.node_states(list(range(n)))
+        assert all(x.pod_count == -1 for x in st), "ks_nodes_upsert applied part of a refused call"
+        status = (C.c_int32 * n)()
+        assert s.lib.ks_nodes_upsert_each(s.ctx, na, slots, n, status) == 5
+        assert list(status) == [0, 0, 0, 5, 0, 0]
+        pods = [Pod(f"p{j}", containers=[Container({"cpu": 500, "memory": Gi, "ephemeral-storage": 6 * Ti
+                                                    if j % 3 == 0 else 0})]) for j in range(12)]
+        pa, m = pods_array(pods, a)
+        got = s.schedule_raw(pa, m)
+    keep = [i for i in range(n) if i != 3]
+    ka, nk = nodes_array([nodes[i] for i in keep], a)
+    o = pyoracle.Oracle(n)
+    o.upsert(ka, (C.c_uint32 * nk)(*keep), nk)
+    want = o.schedule(pa, m)
+    assert_results_equal(got, want, m, "per-item upsert")
+    r = res_array(got, m)
+    assert (r["node_index"][[0, 3, 6]] == 5).all()  # 6 TiB each: only the 20 TiB node has it
+    assert r["status"][9] == 1  # 3 x 6 TiB taken: 2 TiB left on the only ephemeral-storage node

@@ -14,6 +14,7 @@ LOG=$OUT/sanitize.log
 B=$R/k8s-1m_amd/build/san
 say() { echo "$*" | tee -a "$LOG"; }
 say "sanitize run $(date -u +%Y-%m-%dT%H:%M:%SZ) on $(uname -m), $(g++ --version | head -1)"
+make -s -C "$R/oracle" sanitize >> "$LOG" 2>&1 || { say "oracle sanitizer build FAILED"; exit 1; }
 
 say "== ksg_stress under ThreadSanitizer"
 TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1" "$B/ksg_stress_tsan" >> "$LOG" 2>&1 || { say "TSAN FAILED"; exit 1; }
