@@ -37,7 +37,7 @@ import pyoracle  # noqa: E402
 from helpers import res_array, states_np  # noqa: E402
 from ksched import Scheduler, synth  # noqa: E402
 from stream import BurstStream, GpuTarget, OracleTarget  # noqa: E402
-from test_gpu_fullsize import pick_windows, replay_check  # noqa: E402
+from test_gpu_fullsize import MIN_CHECKED, pick_windows, replay_check  # noqa: E402
 
 N = 1_000_000
 BATCH = 32_768
@@ -198,11 +198,13 @@ def main(cfg):
         if kind == "spread":  # windows straddle a plain -> spread boundary, sit in a spread run, end the batch
             wins, wlen = [(124, "fixed"), (1400, "fixed"), (mb - 6, "fixed")], 6
         else:
-            wins, wlen = pick_windows(marks[b], mb), 32
+            wins, wlen = pick_windows(marks[b], mb, seed=b), 32
         kinds |= {what for _, what in wins}
         checked += replay_check(o, bursts[b][0], got[b], mb, windows=[w for w, _ in wins], wlen=wlen)
         if b < len(events):
             BurstStream.apply_marshalled(events[b][2], [ot])
+    if kind != "spread" and checked < MIN_CHECKED * nb:
+        raise Fail(f"only {checked} pods checked by the oracle over {nb} bursts")
     ow = states_np(o.L.oracle_node_states, o.o, N)
     if not np.array_equal(ow, tables[0]):
         raise Fail("node tables differ from the oracle's after replaying every decision")

@@ -76,11 +76,17 @@ def replay_check(o, pods, got, m, windows=WINDOWS, wlen=WLEN):
 MARK_FIX, MARK_ROUND_START, MARK_AFTER_WASTE = 1, 2, 4  # ks_batch_marks (include/ksched.h)
 
 
-def pick_windows(marks, m, wlen=WLEN, fixed=WINDOWS, per_kind=3):
-    """The fixed windows plus windows starting where the round machinery changed
+MIN_CHECKED = 512  # pods whose decision the oracle checks in each full-size test (replay windows)
+
+
+def pick_windows(marks, m, wlen=WLEN, fixed=WINDOWS, per_kind=3, round_every=16, min_pods=MIN_CHECKED, seed=0):
+    """The fixed windows; windows starting where the round machinery changed
     course (ks_batch_marks): the first pods re-swept with measured normaliser
     maxima (FIX) and the first pods of rounds that follow a wasted speculated
-    round, up to `per_kind` of each spread over the batch; non-overlapping."""
+    round, up to `per_kind` of each spread over the batch; a window at the
+    start of every `round_every`-th resolved round (where the parallel commit
+    begins with an empty fixed prefix); then seeded random windows until at
+    least `min_pods` pods are checked.  Non-overlapping."""
     mk = np.frombuffer(marks, dtype=np.uint8)
     cand = [(w, "fixed") for w in fixed]
     for bit, what in ((MARK_FIX, "fix"), (MARK_AFTER_WASTE, "after-waste")):
@@ -89,11 +95,26 @@ def pick_windows(marks, m, wlen=WLEN, fixed=WINDOWS, per_kind=3):
         if len(idx):
             for j in np.unique(np.linspace(0, len(idx) - 1, min(per_kind, len(idx))).astype(int)):
                 cand.append((int(idx[j]), what))
-    out, end = [], -1
-    for w, what in sorted(cand):
-        if w >= end:
-            out.append((w, what))
-            end = w + wlen
+    starts = np.nonzero(mk & MARK_ROUND_START)[0]
+    starts = starts[starts + wlen <= m]
+    cand += [(int(w), "round-start") for w in starts[::round_every]]
+
+    def take(cands):
+        out, end = [], -1
+        for w, what in sorted(cands):
+            if w >= end:
+                out.append((w, what))
+                end = w + wlen
+        return out
+
+    out = take(cand)
+    rng = np.random.default_rng(1234 + seed)
+    tries = 0
+    while len(out) * wlen < min(min_pods, m) and tries < 1000:
+        tries += 1
+        w = int(rng.integers(0, m - wlen + 1))
+        if all(w + wlen <= x or w >= x + wlen for x, _ in out):
+            out = take(out + [(w, "random")])
     return out
 
 
@@ -117,7 +138,8 @@ def run_fullsize(kind, pods, prefill, *, opts=None, **cfg):
     if pf is not None:
         o.add_pods(pf.pods, pf.slot_ptr, pf.n_pods)
     wins = pick_windows(marks, BATCH)
-    replay_check(o, pods, got, BATCH, windows=[w for w, _ in wins])
+    checked = replay_check(o, pods, got, BATCH, windows=[w for w, _ in wins])
+    assert checked >= MIN_CHECKED, f"only {checked} pods checked by the oracle"
     mk = np.frombuffer(marks, dtype=np.uint8)
     covered = np.zeros(BATCH, dtype=bool)
     for w, _ in wins:
