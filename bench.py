@@ -12,7 +12,8 @@ TaintToleration (+ NodeAffinity skipped, ImageLocality 0),
 percentageOfNodesToScore = 100, deterministic lowest-slot tie-break,
 sequential-equivalent in-order commit.
 
-A "step" schedules one batch of pods (default 32768) to completion against the
+A "step" schedules one batch of pods (default 50,000: the driver's 20 steps
+are configs[2]'s 1,000,000 pods) to completion against the
 live cluster, through the whole boundary the cgo caller uses: `value` times
 ks_batch_prepare (pod compile + H2D), ks_batch_submit / ks_batch_wait (every
 round + D2H of the results) and ks_batch_results, pipelined so that compiling
@@ -88,7 +89,8 @@ VALU_CYCLES_FALLBACK = 4.0  # when valu_mix.json does not match the kernel sourc
 E2E_DEPTH = 2  # batches submitted ahead in the headline loop (compile of k+1 and k+2 overlaps run k)
 REF_SCHEDULE_ONE_US = 560.0  # README.adoc:786 (per pod per shard, ~195 nodes evaluated)
 KERNEL_SOURCES = ["k8s-1m_amd/csrc/ksched_kernels.hip", "k8s-1m_amd/csrc/ksched_eval.hpp", "k8s-1m_amd/csrc/ksched_dev.hpp",
-                  "k8s-1m_amd/csrc/ksched_kernels.hpp", "k8s-1m_amd/Makefile"]
+                  "k8s-1m_amd/csrc/ksched_kernels.hpp", "k8s-1m_amd/csrc/ksched_util.hpp",
+                  "k8s-1m_amd/csrc/ksched_resolve.hip", "k8s-1m_amd/Makefile"]
 
 
 def parse():
@@ -97,7 +99,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--nodes", type=int, default=1_000_000)
-    ap.add_argument("--batch", type=int, default=32768,
+    ap.add_argument("--batch", type=int, default=50_000,
                     help="pods per step (each batch refills the round pipeline once)")
     ap.add_argument("--pods-per-round", type=int, default=256)
     ap.add_argument("--topk", type=int, default=0)
@@ -135,7 +137,7 @@ def parse():
     if a.prefill is None:
         a.prefill = 0.0 if a.kind == "kwok" else 0.5
     if a.pods in ("spread", "affinity"):  # one pod at a time (spread path): smaller steps and CPU samples
-        if a.batch == 32768:
+        if a.batch == 50_000:
             a.batch = 2048
         a.cpu_pods = min(a.cpu_pods, 4)
         a.cpu_pods_mt = min(a.cpu_pods_mt, 16)
@@ -308,8 +310,9 @@ def run_batches(args, kind, sched, world, rank, t_setup):
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_pods > 0:
         cpu = cpu_baseline(args, nodes, slots, pre, pod_stream(args, kind, args.cpu_pods_mt + args.cpu_pods, 7))
+    swept = e2e.pop("pods_swept")
     line = report(args, sched, st, dbg, world, e2e.pop("pods_timed"), e2e.pop("elapsed"), e2e.pop("scheduled"),
-                  setup_s, cpu)
+                  setup_s, cpu, pods_swept=swept)
     line["extra"]["host_compile_ms_per_step"] = e2e["host_compile_ms_per_step"]
     line["end_to_end"] = e2e
     if res:
@@ -370,15 +373,22 @@ def end_to_end(args, kind, sched, world, barrier):
         run(0, w, False)
     sched.reset_stats()
     sched.set_timing(True)
+    dbg0 = (C.c_uint64 * 16)()
+    sched.lib.ks_debug_counters(ctx, dbg0)
     barrier()
     t0 = time.perf_counter()
     compile_s = run(w, w + n, True)
     barrier()
     elapsed = time.perf_counter() - t0
     sched.set_timing(False)
+    dbg1 = (C.c_uint64 * 16)()
+    sched.lib.ks_debug_counters(ctx, dbg1)
     if world > 1:
         elapsed = sched.allreduce_max([elapsed])[0]
     return {"pods_timed": n * args.batch, "elapsed": elapsed, "scheduled": scheduled,
+            # pods the sweeps evaluated in the timed steps: one per class of a
+            # round's byte-identical pods
+            "pods_swept": int(dbg1[2] - dbg0[2]),
             "host_compile_ms_per_step": round(1e3 * compile_s / max(1, n - 1), 3),
             "what": "value: ks_batch_prepare (compile + H2D) + ks_batch_submit/wait (run + D2H) + "
                     "ks_batch_results per step, batch k+1 compiled while batch k runs; fresh pods (seed 7)"}
@@ -616,6 +626,12 @@ def roofline(args, st, world):
         for k in ("valu_cycles_per_instr", "valu_f64_share", "clock_ghz"):
             if pmc.get(k) is not None:
                 r[k] = pmc[k]
+        if pmc.get("clock_ghz"):
+            # the peak above is at the 2.4 GHz spec clock; the PMC pass
+            # measured the clock the chip held (GRBM_GUI_ACTIVE / 8 / time)
+            f = pmc["clock_ghz"] / 2.4
+            r["peak_at_measured_clock"] = round(peak_wi * f * 64 / 1e12, 2)
+            r["frac_at_measured_clock"] = round(wi / launch_s / (peak_wi * f), 4)
         if pmc.get("valu_busy") is not None:
             r["valu_busy"] = pmc["valu_busy"]  # SQ_ACTIVE_INST_VALU share of SIMD quad-cycles
         if pmc.get("hbm_bytes_per_eval") is not None:
@@ -642,7 +658,7 @@ def roofline(args, st, world):
     return r
 
 
-def report(args, sched, st, dbg, world, pods_timed, elapsed, scheduled, setup_s, cpu, c5=None):
+def report(args, sched, st, dbg, world, pods_timed, elapsed, scheduled, setup_s, cpu, c5=None, pods_swept=None):
     value = pods_timed / elapsed
     line = {
         "metric": "pods scheduled/sec at 1M nodes (1/2/4/8 GPU) + % of HBM roofline",
@@ -684,7 +700,13 @@ def report(args, sched, st, dbg, world, pods_timed, elapsed, scheduled, setup_s,
             # identical pods of a round swept once: pods swept (class
             # representatives) / pods in the swept windows, since open
             "sweep_representative_fraction": round(int(dbg[2]) / max(1, int(dbg[2]) + int(dbg[7])), 4),
-            "node_evals_per_s": round(value * args.nodes, 1),
+            # (pod, node) evaluations: the sweeps' actual ones (pods swept x
+            # nodes; identical pods of a round are swept once) and the nominal
+            # pods x nodes the metric's "1M node evaluations per pod" counts
+            "node_evals_per_s": (round(pods_swept * args.nodes / elapsed, 1) if pods_swept is not None
+                                 else round(value * args.nodes, 1)),
+            "node_evals_per_s_nominal": round(value * args.nodes, 1),
+            "pods_swept_fraction": round(pods_swept / pods_timed, 4) if pods_swept is not None else None,
             "setup_s": round(setup_s, 2),
             "pmc_key": pmc_key(args, world),
         },

@@ -17,6 +17,8 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #define CHECK(x)                                                                              \
@@ -67,12 +69,13 @@ __device__ __forceinline__ void record(unsigned long long *cyc, unsigned long lo
     uint32_t a0 = seed, a1 = seed + 1, a2 = seed + 2, a3 = seed + 3, a4 = seed + 4, a5 = seed + 5, a6 = seed + 6, \
              a7 = seed + 7;                                                                                     \
     const double dc = (double)c;                                                                                \
+    const uint32_t c2 = c + 1u + (threadIdx.x & 1u); /* a second VGPR source */                                 \
     const unsigned long long m = __builtin_amdgcn_read_exec() & 0x5555555555555555ull;                         \
     const unsigned long long t0 = __builtin_readcyclecounter(), r0 = __builtin_amdgcn_s_memrealtime();        \
     for (uint32_t i = 0; i < iters; ++i) {                                                                     \
       asm volatile(REP4(INSTR(0) INSTR(1) INSTR(2) INSTR(3) INSTR(4) INSTR(5) INSTR(6) INSTR(7))               \
                    : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)            \
-                   : "v"(c), "s"(m), "v"(dc)                                                                    \
+                   : "v"(c), "s"(m), "v"(dc), "v"(c2), "s"(c)                                                  \
                    : "vcc", "s0", "s1");                                                                                    \
     }                                                                                                           \
     const unsigned long long t1 = __builtin_readcyclecounter(), r1 = __builtin_amdgcn_s_memrealtime();        \
@@ -80,7 +83,11 @@ __device__ __forceinline__ void record(unsigned long long *cyc, unsigned long lo
     if ((a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7) == 0x12345u) cyc[0] = 0;                                       \
   }
 
-// operand %8: c (32-bit: v, 64-bit: v pair); %9: SGPR mask; %10: c as double
+// operand %8: c (32-bit: v, 64-bit: v pair); %9: SGPR mask; %10: c as double;
+// 32-bit only: %11 a second VGPR (c2), %12 c in an SGPR.  The f32 FMA
+// variants separate the opcode from the encoding and the operand sources:
+// v_fma_f32 is VOP3-only; v_fmac_f32 is its VOP2 form (the destination is the
+// addend); the _e64 adds are VOP2 opcodes forced into the VOP3 encoding.
 #define I_ADD_F64(r) "v_add_f64 %" #r ", %" #r ", %8\n"
 #define I_MUL_F64(r) "v_mul_f64 %" #r ", %" #r ", %8\n"
 #define I_FMA_F64(r) "v_fma_f64 %" #r ", %" #r ", %8, %8\n"
@@ -117,6 +124,13 @@ __device__ __forceinline__ void record(unsigned long long *cyc, unsigned long lo
 #define I_SUB_U32(r) "v_sub_u32 %" #r ", %" #r ", %8\n"
 #define I_ADD3(r) "v_add3_u32 %" #r ", %" #r ", %8, %8\n"
 #define I_BFE(r) "v_bfe_u32 %" #r ", %" #r ", 3, 5\n"
+#define I_FMA_F32_2V(r) "v_fma_f32 %" #r ", %" #r ", %8, %11\n"
+#define I_FMA_F32_SV(r) "v_fma_f32 %" #r ", %" #r ", %12, %8\n"
+#define I_FMAC_F32(r) "v_fmac_f32 %" #r ", %8, %11\n"
+#define I_FMAC_F32_SAME(r) "v_fmac_f32 %" #r ", %8, %8\n"
+#define I_ADD_F32_E64(r) "v_add_f32_e64 %" #r ", %" #r ", %8\n"
+#define I_MUL_F32_E64(r) "v_mul_f32_e64 %" #r ", %" #r ", %8\n"
+#define I_ADD_U32_E64(r) "v_add_u32_e64 %" #r ", %" #r ", %8\n"
 
 K64(k_add_f64, I_ADD_F64)
 K64(k_mul_f64, I_MUL_F64)
@@ -153,6 +167,13 @@ K32(k_mul_f32, I_MUL_F32)
 K32(k_sub_u32, I_SUB_U32)
 K32(k_add3, I_ADD3)
 K32(k_bfe, I_BFE)
+K32(k_fma_f32_2v, I_FMA_F32_2V)
+K32(k_fma_f32_sv, I_FMA_F32_SV)
+K32(k_fmac_f32, I_FMAC_F32)
+K32(k_fmac_f32_same, I_FMAC_F32_SAME)
+K32(k_add_f32_e64, I_ADD_F32_E64)
+K32(k_mul_f32_e64, I_MUL_F32_E64)
+K32(k_add_u32_e64, I_ADD_U32_E64)
 
 // v_readlane_b32: SGPR destinations
 __global__ void k_readlane(unsigned long long *cyc, uint32_t seed, uint32_t c, uint32_t iters) {
@@ -216,7 +237,17 @@ int main() {
       {"v_mul_f32", nullptr, k_mul_f32},         {"v_sub_u32", nullptr, k_sub_u32},
       {"v_add3_u32", nullptr, k_add3},           {"v_bfe_u32", nullptr, k_bfe},
       {"v_readlane_b32", nullptr, k_readlane},
+      // VOP2 vs VOP3 (profiles/valu_vop.jsonl)
+      {"v_fma_f32 (v, v', same v twice)", nullptr, k_fma_f32},
+      {"v_fma_f32 (v, v', v'')", nullptr, k_fma_f32_2v},
+      {"v_fma_f32 (v, s, v')", nullptr, k_fma_f32_sv},
+      {"v_fmac_f32 (VOP2, v', v'')", nullptr, k_fmac_f32},
+      {"v_fmac_f32 (VOP2, same v twice)", nullptr, k_fmac_f32_same},
+      {"v_add_f32_e64 (VOP3)", nullptr, k_add_f32_e64},
+      {"v_mul_f32_e64 (VOP3)", nullptr, k_mul_f32_e64},
+      {"v_add_u32_e64 (VOP3)", nullptr, k_add_u32_e64},
   };
+  const char *only = std::getenv("VALU_ONLY");  // a substring: run the matching entries only
   hipDeviceProp_t prop{};
   CHECK(hipGetDeviceProperties(&prop, 0));
   const int ncu = prop.multiProcessorCount;
@@ -227,6 +258,7 @@ int main() {
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
   for (const Entry &t : tab) {
+    if (only && !std::strstr(t.name, only)) continue;
     for (int w : {1, 2, 4}) {
       const dim3 grid(ncu), block(256 * w);
       for (int rep = 0; rep < 2; ++rep) {  // first launch warms the clocks / caches
