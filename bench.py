@@ -249,7 +249,9 @@ def dry_run(args, world, rank, local_rank):
             "device": local_rank if world > 1 else 0, "master": f"{os.environ.get('MASTER_ADDR', '')}:"
                                                                f"{os.environ.get('MASTER_PORT', '')}",
             "rendezvous_ok": bool(ok)}
-    print(json.dumps(line), flush=True)
+    # one write(2) per line: the ranks share the launcher's stdout pipe
+    sys.stdout.flush()
+    os.write(sys.stdout.fileno(), (json.dumps(line) + "\n").encode())
     return 0 if ok else 1
 
 

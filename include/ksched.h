@@ -584,9 +584,9 @@ ks_status ks_reset_stats(ks_ctx *ctx);
 /* Raw counters: [0] rounds [1] pods resolved [2] pods swept
  * [3] speculated rounds wasted [4] pods re-swept because their guessed
  * normalising maxima were wrong, [5] label-dictionary reclaims, [6] taint
- * dictionary rebuilds, [7] identical pods not swept, [8..11] resolve phase
- * cycle sums (diagnostic KS_STAMPS build only), [12] passes of the parallel
- * commit, [13] rounds it resolved. */
+ * dictionary rebuilds, [7] identical pods not swept, [12] passes of the
+ * parallel commit, [13] rounds it resolved.  (The instrumented stamps builds,
+ * k8s-1m_amd/csrc/ksched_instr.hpp, put phase cycle sums in [8..15].) */
 ks_status ks_debug_counters(ks_ctx *ctx, uint64_t out[16]);
 /* Diagnostics of the parallel commit (resource-only rounds): with the profile
  * on, every round accumulates s_memtime cycles per phase into out[0..8]

@@ -1526,8 +1526,10 @@ ks_status pod_xrequests(ks_ctx *c, const ks_pod &p, bool create, std::vector<std
     for (uint32_t j = 0; j < k.n_extended; ++j) {
       const std::string nm = str(k.extended[j].name);
       if (!xres_name_ok(nm)) continue;
-      if (k.extended[j].value < 0 || k.extended[j].value >= kMaxExact)
-        return c->fail(KS_ERR_RANGE, "pod %s: %s request outside [0, 2^46)", str(p.name).c_str(), nm.c_str());
+      // extended columns are compared in exact int64 (no LeastAllocated
+      // floor): any non-negative request, sums checked for overflow below
+      if (k.extended[j].value < 0)
+        return c->fail(KS_ERR_RANGE, "pod %s: negative %s request", str(p.name).c_str(), nm.c_str());
       uint32_t col;
       if (ks_status st = xres_column(c, c->intern(nm.c_str()), create, &col)) return st;
       if (col == UINT32_MAX) continue;  // ks_pods_check: no column yet (validation only)
@@ -1535,19 +1537,27 @@ ks_status pod_xrequests(ks_ctx *c, const ks_pod &p, bool create, std::vector<std
     }
     return KS_OK;
   };
+  auto add = [&](int64_t &acc, int64_t v) -> ks_status {
+    if (__builtin_add_overflow(acc, v, &acc))
+      return c->fail(KS_ERR_RANGE, "pod %s: extended resource requests overflow int64", str(p.name).c_str());
+    return KS_OK;
+  };
   for (uint32_t i = 0; i < p.n_containers; ++i)
-    if (ks_status st = each(p.containers[i], [&](uint32_t col, int64_t v) { sum[col] += v; return KS_OK; }))
+    if (ks_status st = each(p.containers[i], [&](uint32_t col, int64_t v) { return add(sum[col], v); }))
       return st;
   for (uint32_t i = 0; i < p.n_init_containers; ++i) {
     const ks_container &k = p.init_containers[i];
     std::map<uint32_t, int64_t> use;
     ks_status st;
     if (k.restart_always) {
-      st = each(k, [&](uint32_t col, int64_t v) { sum[col] += v; side[col] += v; return KS_OK; });
+      st = each(k, [&](uint32_t col, int64_t v) {
+        ks_status e = add(sum[col], v);
+        return e ? e : add(side[col], v);
+      });
       use = side;
     } else {
       use = side;
-      st = each(k, [&](uint32_t col, int64_t v) { use[col] += v; return KS_OK; });
+      st = each(k, [&](uint32_t col, int64_t v) { return add(use[col], v); });
     }
     if (st) return st;
     for (auto &kv : use) init[kv.first] = std::max(init[kv.first], kv.second);

@@ -31,6 +31,7 @@
 #include "ksched_dev.hpp"
 #include "ksched_eval.hpp"
 #include "ksched_kernels.hpp"
+#include "ksched_instr.hpp"
 #include "ksched_util.hpp"
 
 namespace ks {
@@ -141,15 +142,6 @@ constexpr double NORM_EPS = 0x1p-40;
 __device__ __forceinline__ uint32_t normalize_inv(uint32_t raw, double inv) {
   return (uint32_t)__builtin_fma((double)(100u * raw), inv, NORM_EPS);
 }
-
-// Timing ablations (-DKS_ABL=mask, diagnostic builds only; results are then
-// wrong): skip the EXT sweep's label programs (1), per-plugin failure counts
-// (2), TaintToleration normalisation (4), BalancedAllocation (8).
-#ifdef KS_ABL
-#define ABL_ON(b) ((KS_ABL & (b)) == 0)
-#else
-#define ABL_ON(b) true
-#endif
 
 
 // =================================================================== sweep
@@ -277,7 +269,7 @@ void sweep_kernel(RoundArgs a) {
       bool aff[NPL], pre[NPL];
       uint32_t praw[NPL];
       static_for<NPL>([&](auto J) { aff[J] = true; pre[J] = true; praw[J] = 0u; });
-      if (ABL_ON(1) && (p.flags & PF_AFF)) required_match_n<NPL, LWU>(p, a.clauses, ne, nr, aff);
+      if (p.flags & PF_AFF) required_match_n<NPL, LWU>(p, a.clauses, ne, nr, aff);
       if (p.flags & PF_PREFILTER) {  // rare: pods naming their nodes by metadata.name
         static_for<NPL>([&](auto J) { pre[J] = false; });
         for (uint32_t k = 0; k < p.pre_len; ++k) {
@@ -286,7 +278,7 @@ void sweep_kernel(RoundArgs a) {
         }
       }
       const bool conflict = p.flags & PF_NA_CONFLICT;
-      if (ABL_ON(1) && (p.flags & PF_NA)) preferred_raw_n<NPL, LWU>(p, a.clauses, ne, nr, praw);
+      if (p.flags & PF_NA) preferred_raw_n<NPL, LWU>(p, a.clauses, ne, nr, praw);
       const double *ip = fix ? a.norm_inv + 2 * r : a.guess_inv + 2 * (size_t)pi;  // RN(1 / max)
       const double inv_tt = (p.flags & PF_TT) ? ip[0] : 0.0;
       const double inv_na = (p.flags & PF_NA) ? ip[1] : 0.0;
@@ -326,7 +318,7 @@ void sweep_kernel(RoundArgs a) {
         uint32_t tts = 100u;
         if (p.flags & PF_TT) {
           const uint32_t raw = (uint32_t)__popcll(ne[j].prefer & ~p.tol_prefer);
-          tts = ABL_ON(4) ? 100u - normalize_inv(raw, inv_tt) : 100u;
+          tts = 100u - normalize_inv(raw, inv_tt);
           ttc += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(raw == tt_max) & fb);
           over_m |= __builtin_amdgcn_ballot_w64(raw > tt_max) & fb;
           tmx = max(tmx, feasible ? raw : 0u);
@@ -339,14 +331,14 @@ void sweep_kernel(RoundArgs a) {
           nmx = max(nmx, feasible ? praw[j] : 0u);
           acc = wmad_s(wn9, nas, acc);
         }
-        acc = wmad_s(wb9, ABL_ON(8) ? (uint32_t)score_ba_sum(sc, sm, nr[j]) : 50u, acc);
+        acc = wmad_s(wb9, (uint32_t)score_ba_sum(sc, sm, nr[j]), acc);
         acc = wmad_s(wf9, (uint32_t)score_la(p, nr[j]), acc);
         const uint32_t key = sel_mask(fb, acc);
         b2 = max(b2, min(b1, key));
         b1 = max(b1, key);
         const uint64_t vb = __builtin_amdgcn_ballot_w64(valid);
         feas += (uint32_t)__popcll(fb);
-        if (ABL_ON(2) && fb != vb) {  // some node failed a filter: per-plugin diagnosis counts
+        if (fb != vb) {  // some node failed a filter: per-plugin diagnosis counts
           f0 += popc_ballot(st == 0);
           f1 += popc_ballot(st == 1);
           f2 += popc_ballot(st == 2);
@@ -992,14 +984,8 @@ constexpr int RES_DEC_WAVE = RES_EVAL_WAVE + 1;
 constexpr int RES_PREV_WAVE = RES_DEC_WAVE + 1;
 constexpr int RES_IDLE = 15;                              // a wave with no role: barriers only
 // Hardware wave h of a workgroup runs on SIMD h % 4 (round-robin dispatch onto
-// the reserved CU).  KS_RES_LAYOUT 1 (default): 16 waves, the decider alone on
-// its SIMD, the eval and prev waves on another, list and owner waves on the
-// last two; 0: 11 waves, roles in wave order (3 per SIMD, the decider with a
-// list and an owner wave).
-#ifndef KS_RES_LAYOUT
-#define KS_RES_LAYOUT 2
-#endif
-#if KS_RES_LAYOUT == 2
+// the reserved CU): 16 waves, the decider with one owner wave on its SIMD,
+// the eval and prev waves with another, list and owner waves on the last two.
 constexpr int RES_HW_WAVES = 16;
 __device__ __forceinline__ uint32_t res_role(uint32_t hw) {
   // SIMD 0: eval, prev, owner 2 | 1: decider, owner 3 | 2: list 0, owner 0, list 2 | 3: list 1, owner 1, list 3
@@ -1007,18 +993,6 @@ __device__ __forceinline__ uint32_t res_role(uint32_t hw) {
                                6,             7,            2, 3, RES_IDLE,      RES_IDLE, RES_IDLE, RES_IDLE};
   return tab[hw & 15];
 }
-#elif KS_RES_LAYOUT == 1
-constexpr int RES_HW_WAVES = 16;
-__device__ __forceinline__ uint32_t res_role(uint32_t hw) {
-  // SIMD 0: eval, prev | 1: decider | 2: list 0, owner 0, list 2, owner 2 | 3: list 1, owner 1, list 3, owner 3
-  constexpr uint8_t tab[16] = {RES_EVAL_WAVE, RES_DEC_WAVE, 0, 1, RES_PREV_WAVE, RES_IDLE, 4, 5,
-                               RES_IDLE,      RES_IDLE,     2, 3, RES_IDLE,      RES_IDLE, 6, 7};
-  return tab[hw & 15];
-}
-#else
-constexpr int RES_HW_WAVES = RES_PREV_WAVE + 1;
-__device__ __forceinline__ uint32_t res_role(uint32_t hw) { return hw; }
-#endif
 constexpr int RESOLVE_THREADS = RES_HW_WAVES * WAVE;
 constexpr int RHASH = 1024;
 constexpr int LSEL = 4;                                   // listed candidates kept per list wave
@@ -1045,66 +1019,15 @@ static_assert(DSUM_LANE >= NCAND && DSUM_LANE + NFILT + 3 <= WAVE, "decider lane
 
 
 
-// Diagnostic build (-DKS_STAMPS): the first lane of the decider and the eval
-// wave accumulate s_memtime of their work and barrier wait, and the decider of
-// its phases, into a.counters[8..15]; never compiled into the measured library.
-// Timing experiments only (-DKS_EXPT=mask): skip the list (1), owner (2) or
-// eval (4) waves' work; results are then wrong.
-#ifdef KS_EXPT
-#define ROLE_ON(b) ((KS_EXPT & (b)) == 0)
-#else
-#define ROLE_ON(b) true
-#endif
-#ifdef KS_STAMPS
-#define STAMP_NOW(t_)                                                         \
-  do {                                                                        \
-    __builtin_amdgcn_sched_barrier(0);                                        \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
-    __builtin_amdgcn_sched_barrier(0);                                        \
-  } while (0)
-#endif
-
-// KS_SINGLE_DONE (diagnostic builds only, make probe_old): the pre-fix
-// single done word, to show the race the double buffer removes
-#ifdef KS_SINGLE_DONE
-#define DONE(b) s_done[0]
-#else
-#define DONE(b) s_done[b]
-#endif
-#ifdef KS_RACE_PROBE
-__device__ __forceinline__ void race_probe_delay() {
-#pragma unroll
-  for (int i = 0; i < 8; ++i) __builtin_amdgcn_s_sleep(127);
-}
-#endif
-
 // Wave-uniform copy of an LDS object: every lane reads it (one address: an
 // LDS broadcast, no bank conflicts).  Round 3: this replaced a copy read by
 // one lane and handed to the SALU by a readfirstlane per dword, which put
 // ~25 dependent readfirstlanes on the owner / eval waves' chains (resolve
 // 0.287 -> 0.279 ms per round on the 125k-node proxy, profiles/r3/bcast_ab/).
-// KS_POD_RFL: the old form (A/B builds only).
 template <class T>
-__device__ __forceinline__ T lds_uniform(const T &src, uint32_t lane) {
+__device__ __forceinline__ T lds_uniform(const T &src) {
   static_assert(sizeof(T) % 4 == 0, "dword object");
-#ifndef KS_POD_RFL
-  (void)lane;
   return src;
-#endif
-  constexpr int N = sizeof(T) / 4;
-  uint32_t tmp[N];
-#pragma unroll
-  for (int i = 0; i < N; ++i) tmp[i] = 0;
-  if (lane == 0) {
-    const uint32_t *sp = (const uint32_t *)&src;
-#pragma unroll
-    for (int i = 0; i < N; ++i) tmp[i] = sp[i];
-  }
-  T out;
-  uint32_t *o = (uint32_t *)&out;
-#pragma unroll
-  for (int i = 0; i < N; ++i) o[i] = __builtin_amdgcn_readfirstlane(tmp[i]);
-  return out;
 }
 
 // Resource-only pods (batches without PF_EXT pods: only NodeResourcesFit can
@@ -1335,40 +1258,23 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
   // hash buckets the last three pods' joins were inserted at (NONE32: no insert)
   uint32_t pb1 = NONE32, pb2 = NONE32, pb3 = NONE32;
   // the decider is the per-pod critical path, the eval wave next: issue priority
-#ifndef KS_EVAL_PRIO
-#define KS_EVAL_PRIO 2
-#endif
-#ifndef KS_OWNER_PRIO
-#define KS_OWNER_PRIO 3
-#endif
   if (wid == RES_DEC_WAVE) __builtin_amdgcn_s_setprio(3);
-  else if (wid == RES_EVAL_WAVE || wid == RES_PREV_WAVE) __builtin_amdgcn_s_setprio(KS_EVAL_PRIO);
-  else if (is_owner) __builtin_amdgcn_s_setprio(KS_OWNER_PRIO);  // owners: the longest chain per pod
-#ifdef KS_STAMPS
-#if KS_STAMPS >= 3  // list wave 0 and owner wave 0 in the decider / eval counters
-  const bool stamper = lane == 0 && (wid == 0 || wid == RES_LIST_WAVES);
-  const uint32_t sidx = wid == 0 ? 0 : 2;
-#else
-  const bool stamper = lane == 0 && (wid == RES_DEC_WAVE || wid == RES_EVAL_WAVE);
-  const uint32_t sidx = wid == RES_DEC_WAVE ? 0 : 2;
-#endif
-  uint64_t st_work = 0, st_wait = 0, t0, t1, t2, ts, sub[4] = {0, 0, 0, 0};
-#endif
+  else if (wid == RES_EVAL_WAVE || wid == RES_PREV_WAVE) __builtin_amdgcn_s_setprio(2);
+  else if (is_owner) __builtin_amdgcn_s_setprio(3);  // owners: the longest chain per pod
+  KS_STAMP_DECL(wid, lane);
   lds_barrier();
 
   // ROLE: 0 decider, 1 eval / prev, 2 owner, 3 list (one loop per role below)
   auto iteration = [&](uint32_t r, auto role) __attribute__((always_inline)) -> bool {
     constexpr int ROLE = decltype(role)::value;
     const uint32_t buf = r & 1u, nb = buf ^ 1u;
-#ifdef KS_STAMPS
-    STAMP_NOW(t0);
-#endif
+    KS_STAMP_BEGIN();
     if constexpr (ROLE == 0) {
       // ------------------------------------------------------------- decider
       if (r >= nround) {
         if (lane == 0) {
           s_pend[buf][0] = 0;
-          DONE(buf) = 1;
+          s_done[buf] = 1;
         }
       } else {
         const uint32_t b4 = r % RSLOTS;
@@ -1395,12 +1301,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
         const uint32_t h_tt = uniform_u32(hd.tt_cnt), h_na = uniform_u32(hd.na_cnt);
         const uint64_t h_bound = ((uint64_t)uniform_u32((uint32_t)(hd.bound >> 32)) << 32) |
                                  uniform_u32((uint32_t)hd.bound);
-#if KS_STAMPS == 1
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        STAMP_NOW(ts);
-        sub[0] += ts - t0;
-        t2 = ts;
-#endif
+        KS_STAMP_SPLIT_LGKM(1, 0);
         const uint64_t vkey = (is_prev && !pvalid) ? 0ull : rkey;
         const uint32_t vslot = is_own ? oslot : is_prev ? pslot : 0xFFFFFFFFu - (uint32_t)vkey;
         // entries computed before the last winners' commits are stale: drop them
@@ -1414,11 +1315,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
         const uint64_t ku = lb ? readlane64(vkey, (int)ulane) : 0ull;
         const int32_t s0 = __builtin_amdgcn_readlane(vd, DSUM_LANE);
         const uint32_t feasible = h_feasible - (uint32_t)s0;
-#if KS_STAMPS == 1
-        STAMP_NOW(ts);
-        sub[1] += ts - t2;
-        t2 = ts;
-#endif
+        KS_STAMP_SPLIT(1, 1);
         int32_t status = 0;
         bool stop = false;
         uint64_t win = 0;
@@ -1440,17 +1337,13 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
           stop_at = r;
           if (lane == 0) {
             s_pend[buf][0] = 0;
-            DONE(buf) = 1;
+            s_done[buf] = 1;
           }
         } else {
           if (lane == 0) s_resc[r] = make_uint4((uint32_t)win, (uint32_t)(win >> 32), feasible, (uint32_t)status);
           if (lane > (uint32_t)DSUM_LANE && lane <= (uint32_t)DSUM_LANE + NFILT)
             s_rfail[r][lane - DSUM_LANE - 1] = hfail + (uint32_t)vd;
-#if KS_STAMPS == 1
-          STAMP_NOW(ts);
-          sub[2] += ts - t2;
-          t2 = ts;
-#endif
+          KS_STAMP_SPLIT(1, 2);
           // commit (AssumePod -> NodeInfo.AddPod): the eval wave holds the
           // committed state of every candidate; record which one won
           uint32_t cand = 0, join = 0, oidx = 0;
@@ -1496,14 +1389,10 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
           pvalid = win ? 1u : 0u;
           pcand = cand;
           if (lane == 0) *(uint4 *)&s_pend[buf][0] = make_uint4(pvalid, cand, join, oidx);
-#if KS_STAMPS == 1
-          STAMP_NOW(ts);
-          sub[3] += ts - t2;
-#endif
+          KS_STAMP_SPLIT(1, 3);
         }
       }
     } else if constexpr (ROLE == 1) {
-      if (ROLE_ON(4)) {
       // ------------------------------------------------ eval and prev waves
       // every candidate of pod r committed, evaluated against pod r+1: the
       // eval wave takes the owner and listed candidates (one per lane) and
@@ -1550,12 +1439,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
           pc = min(uniform_u32(s_pend[nb][1]), (uint32_t)NCAND - 1);
           on = is_prev && pv != 0;
         }
-#if KS_STAMPS == 2
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        STAMP_NOW(ts);
-        sub[0] += ts - t0;
-        t2 = ts;
-#endif
+        KS_STAMP_SPLIT_LGKM(2, 0);
         if (is_lst) {
           pre.rc0 = pre.row.rc;
           pre.rm0 = pre.row.rm;
@@ -1572,14 +1456,9 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
           pre = s_post[nb][pc];
           if (EXT) px = s_postx[nb][pc];
         }
-#if KS_STAMPS == 2
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        STAMP_NOW(ts);
-        sub[1] += ts - t2;
-        t2 = ts;
-#endif
+        KS_STAMP_SPLIT_LGKM(2, 1);
         RNode post = pre;
-        rnode_add(post, lds_uniform(s_pod[r], lane));
+        rnode_add(post, lds_uniform(s_pod[r]));
         if (on && cl < (uint32_t)NCAND) {  // the prev wave of the next iteration reads the winner's
           s_post[buf][cl] = post;
           if (EXT) s_postx[buf][cl] = px;
@@ -1587,7 +1466,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
         if constexpr (!EXT) {
           // straight-line for every lane (no branch keeps the pod loads from
           // being hoisted into the candidate batch); stores predicated
-          const PodDev p1 = lds_uniform(s_pod[min(r + 1, nround - 1)], lane);
+          const PodDev p1 = lds_uniform(s_pod[min(r + 1, nround - 1)]);
           const PodQ q1 = pod_q(p1, a.w);
           const NodeRegs g0 = rnode_regs(pre, pre.row.rc, pre.row.rm, pre.row.np);
           const NodeRegs g1 = rnode_regs(post, post.row.rc, post.row.rm, post.row.np);
@@ -1602,7 +1481,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
             for (int qq = 1; qq < NFILT + 3; ++qq) s_edd[buf][cl][qq] = qq == 1 + KS_PLUGIN_FIT_IDX ? lost : 0;
           }
         } else if (r + 1 < nround) {
-          const PodDev p1 = lds_uniform(s_pod[r + 1], lane);  // every lane
+          const PodDev p1 = lds_uniform(s_pod[r + 1]);  // every lane
           if (on && cl < (uint32_t)NCAND) {
             int64_t tt_max = 0, na_max = 0;
             if (EXT) {
@@ -1624,20 +1503,14 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
             for (int qq = 0; qq < NFILT + 3; ++qq) s_edd[buf][cl][qq] = d[qq];
           }
         }
-#if KS_STAMPS == 2
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        STAMP_NOW(ts);
-        sub[2] += ts - t2;
-#endif
-      }
+        KS_STAMP_SPLIT_LGKM(2, 2);
       }
     } else if constexpr (ROLE == 2) {
-      if (ROLE_ON(2)) {
       // ------------------------------------------------------- owner waves
       if (r >= 1) {  // apply pod r-1's commit: its winner's owner adds the pod
         const uint32_t pv = uniform_u32(s_pend[nb][0]), pc = uniform_u32(s_pend[nb][1]);
         const uint32_t pj = uniform_u32(s_pend[nb][2]), po = uniform_u32(s_pend[nb][3]);
-        const PodDev pp = lds_uniform(s_pod[r - 1], lane);  // every lane (readfirstlane)
+        const PodDev pp = lds_uniform(s_pod[r - 1]);  // every lane (readfirstlane)
         if (pv && pj && po / WAVE == ow) {  // a listed node joins this wave: re-rank
           const uint32_t js = 0xFFFFFFFFu - (uint32_t)s_lkey[(r - 1) % RSLOTS][pc - NCAND_OWN];
           const uint32_t below = (uint32_t)__popcll(__ballot(mine && own.slot < js));
@@ -1664,17 +1537,14 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
           rnode_add(own, pp);
         }
       }
-#if KS_STAMPS == 3
-      STAMP_NOW(t2);
-      sub[0] += t2 - t0;
-#endif
+      KS_STAMP_SPLIT(3, 0);
       if (r + 1 < nround && __ballot(mine) != 0) {
         uint64_t key = 0;
         int32_t d[NFILT + 3] = {0, 0, 0, 0, 0, 0, 0, 0};
         bool dany = false;
         CandExt ox{};
         if constexpr (!EXT) {
-          const PodDev p1 = lds_uniform(s_pod[r + 1], lane);
+          const PodDev p1 = lds_uniform(s_pod[r + 1]);
           const PodQ q1 = pod_q(p1, a.w);
           const NodeRegs g = rnode_regs(own, own.row.rc, own.row.rm, own.row.np);
           const NodeRegs g0 = rnode_regs(own, own.rc0, own.rm0, own.np0);
@@ -1686,7 +1556,7 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
           d[0] = nlost;
           d[1 + KS_PLUGIN_FIT_IDX] = nlost;
         } else {
-          const PodDev p1 = lds_uniform(s_pod[r + 1], lane);
+          const PodDev p1 = lds_uniform(s_pod[r + 1]);
           int64_t tt_max = 0, na_max = 0;
           if (EXT) {
             tt_max = s_norm[r + 1][0];
@@ -1709,20 +1579,12 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
             }
           }
         }
-#if KS_STAMPS == 3
-        STAMP_NOW(ts);
-        sub[1] += ts - t2;
-        t2 = ts;
-#endif
+        KS_STAMP_SPLIT(3, 1);
         // total + 1 < 2^24 (weights capped at 10000), rank < 64
         const uint32_t key32 = key ? (uint32_t)(key >> 32) << 6 | (63u - srank) : 0u;
         const uint32_t k1 = wave_max_u32_dpp(key32);
         const uint32_t k2 = wave_max_u32_dpp(key32 == k1 ? 0u : key32);
-#if KS_STAMPS == 3
-        STAMP_NOW(ts);
-        sub[2] += ts - t2;
-        t2 = ts;
-#endif
+        KS_STAMP_SPLIT(3, 2);
         // the holders publish their node and packed key for the decider and the eval wave
         if (key32 != 0 && (key32 == k1 || key32 == k2)) {
           const uint32_t c = 2 * ow + (key32 == k1 ? 0u : 1u);
@@ -1747,43 +1609,20 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
 #pragma unroll
         for (int qq = 0; qq < NFILT + 3; ++qq) s_dsum[nb][ow][qq] = 0;
       }
-      }
     } else {
       // -------------------------------------------------------- list waves
-      if (ROLE_ON(1)) {
       list_select(r + LAHEAD);
-#if KS_STAMPS == 4
-      STAMP_NOW(ts);
-      sub[0] += ts - t0;
-#endif
+      KS_STAMP_SPLIT(4, 0);
       dma_keys(r + LAHEAD + KAHEAD);
-#if KS_STAMPS == 4
-      STAMP_NOW(t2);
-      sub[1] += t2 - ts;
-#endif
+      KS_STAMP_SPLIT(4, 1);
       list_wait();
-#if KS_STAMPS == 4
-      STAMP_NOW(ts);
-      sub[2] += ts - t2;
-#endif
-      }
+      KS_STAMP_SPLIT(4, 2);
     }
-#ifdef KS_STAMPS
-    STAMP_NOW(t1);
-#endif
+    KS_STAMP_PRE_BARRIER();
     lds_barrier();
-#ifdef KS_STAMPS
-    STAMP_NOW(t2);
-    st_work += t1 - t0;
-    st_wait += t2 - t1;
-#endif
-#ifdef KS_RACE_PROBE
-    // regression build (make probe): every wave but the decider reads the
-    // done word late in the last two iterations, so that the decider's
-    // next-iteration store lands first
-    if (ROLE != 0 && r + 2 >= nround) race_probe_delay();
-#endif
-    return DONE(buf) != 0;
+    KS_STAMP_POST_BARRIER();
+    KS_RACE_DELAY(ROLE != 0 && r + 2 >= nround);  // make probe only (ksched_instr.hpp)
+    return s_done[buf] != 0;
   };
 
   // One loop per role (the barrier counts waves, not program locations): each
@@ -1801,10 +1640,8 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
   } else if (wid == RES_IDLE) {
     for (uint32_t r = 0;; ++r) {
       lds_barrier();
-#ifdef KS_RACE_PROBE
-      if (r + 2 >= nround) race_probe_delay();
-#endif
-      if (DONE(r & 1u) != 0) break;
+      KS_RACE_DELAY(r + 2 >= nround);
+      if (s_done[r & 1u] != 0) break;
     }
   } else {
     for (uint32_t r = 0;; ++r)
@@ -1812,19 +1649,12 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
   }
   if (is_list) __builtin_amdgcn_s_waitcnt(0);  // no DMA outlives the block
   // hand the nodes this round modified to the next round's patch and the write-back
-  if (is_owner && mine && ROLE_ON(7)) {
+  if (is_owner && mine) {
     CandExt ox{};
     if (EXT) ox = s_modx[mj];
     a.carry_out[mj] = rnode_carry(own, ox, EXT);
   }
-#ifdef KS_STAMPS
-  if (stamper) {
-    atomicAdd((unsigned long long *)&a.counters[8 + sidx], (unsigned long long)st_work);
-    atomicAdd((unsigned long long *)&a.counters[9 + sidx], (unsigned long long)st_wait);
-    if (wid == (KS_STAMPS == 4 ? 0u : KS_STAMPS == 3 ? (uint32_t)RES_LIST_WAVES : KS_STAMPS == 2 ? (uint32_t)RES_EVAL_WAVE : (uint32_t)RES_DEC_WAVE))
-      for (int i = 0; i < 4; ++i) atomicAdd((unsigned long long *)&a.counters[12 + i], (unsigned long long)sub[i]);
-  }
-#endif
+  KS_STAMP_FLUSH(a.counters, wid);
   if (wid == RES_DEC_WAVE && lane == 0) s_stop_at = stop_at;
   __syncthreads();
   {
@@ -1854,9 +1684,6 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
     }
   }
   if (wid == RES_DEC_WAVE && lane == 0) {
-#ifdef KS_EXPT
-    nmod = 0;  // timing experiment: never write back garbage rows
-#endif
     *a.carry_out_n = nmod;
     mark_pod(a.marks, start, MARK_ROUND_START);
     *a.act_next = start + stop_at;

@@ -32,7 +32,11 @@ from scenarios import node, pod
 pytestmark = pytest.mark.gpu
 
 Gi = 1 << 30
-MODES = {"auto": _abi.RESOLVE_AUTO, "serial": _abi.RESOLVE_SERIAL, "parallel": _abi.RESOLVE_PARALLEL}
+MODES = {"auto": {"resolve_mode": _abi.RESOLVE_AUTO}, "serial": {"resolve_mode": _abi.RESOLVE_SERIAL},
+         "parallel": {"resolve_mode": _abi.RESOLVE_PARALLEL},
+         # AUTO with a low pass cap: every round that needs more than 2 passes
+         # hands the next 3 rounds to the serial kernel
+         "auto_cap": {"resolve_mode": _abi.RESOLVE_AUTO, "resolve_par_max_passes": 2, "resolve_serial_rounds": 3}}
 
 
 def ba_rise_cluster(n, m, seed):
@@ -57,6 +61,11 @@ def ba_rise_cluster(n, m, seed):
     return nodes, pre, pre_slots, pods
 
 
+def pod_slice(pods_arr, b0):
+    """Pointer to pods_arr[b0:] (pods_arr: a ctypes array or POINTER(KsPod))."""
+    return C.cast(C.cast(pods_arr, C.c_void_p).value + int(b0) * C.sizeof(_abi.KsPod), C.POINTER(_abi.KsPod))
+
+
 def run_modes(nodes_arr, n, pods_arr, m, pre=None, splits=1, modes=("auto", "serial", "parallel"), **kw):
     """Results + node states of every resolve mode and of the oracle."""
     slots = (C.c_uint32 * n)(*range(n))
@@ -65,21 +74,20 @@ def run_modes(nodes_arr, n, pods_arr, m, pre=None, splits=1, modes=("auto", "ser
     if pre is not None:
         o.add_pods(*pre)
     bounds = np.linspace(0, m, splits + 1).astype(int)
-    want = np.concatenate([res_array(o.schedule(C.cast(C.addressof(pods_arr) + int(b0) * C.sizeof(_abi.KsPod),
-                                                       C.POINTER(_abi.KsPod)), int(b1 - b0)), int(b1 - b0))
+    want = np.concatenate([res_array(o.schedule(pod_slice(pods_arr, b0), int(b1 - b0)), int(b1 - b0))
                            for b0, b1 in zip(bounds, bounds[1:])])
     wst = states_np(o.L.oracle_node_states, o.o, n)
     o.close()
     out = {}
     for mode in modes:
-        with Scheduler(n, options={"resolve_mode": MODES[mode]}, **kw) as s:
+        with Scheduler(n, options=MODES[mode], **kw) as s:
             s.upsert_nodes_raw(nodes_arr, slots, n)
             if pre is not None:
                 assert s.lib.ks_pods_add(s.ctx, *pre) == 0, s.lib.ks_last_error(s.ctx)
             got = []
             for b0, b1 in zip(bounds, bounds[1:]):
                 k = int(b1 - b0)
-                ptr = C.cast(C.addressof(pods_arr) + int(b0) * C.sizeof(_abi.KsPod), C.POINTER(_abi.KsPod))
+                ptr = pod_slice(pods_arr, b0)
                 got.append(res_array(s.schedule_raw(ptr, k), k))
             dbg = (C.c_uint64 * 16)()
             assert s.lib.ks_debug_counters(s.ctx, dbg) == 0
@@ -130,12 +138,15 @@ def test_synthetic_streams(kind, pods, K):
     ps = synth.besteffort_pods(m) if pods == "besteffort" else synth.pods(synth.HETERO, m, 12)
     pf = synth.prefill(k, n, 11, 13, 0.4) if kind == "hetero" else None
     pre = (pf.pods, pf.slot_ptr, pf.n_pods) if pf is not None else None
-    want, wst, out = run_modes(ns.nodes, n, ps.pods, m, pre=pre, splits=2, topk=K)
+    want, wst, out = run_modes(ns.nodes, n, ps.pods, m, pre=pre, splits=2, topk=K,
+                               modes=("auto", "serial", "parallel", "auto_cap"))
     check_modes(want, wst, out, f"{kind}/{pods}/K={K}")
-    if kind == "kwok" and pods == "besteffort":
-        # identical pods on identical nodes pile up: AUTO hands rounds to the serial kernel
-        auto = out["auto"][2]
-        assert auto[13] < auto[0], f"AUTO never handed a round to the serial kernel: {auto}"
+    # counters: [0] rounds, [12] parallel passes, [13] rounds the parallel kernel resolved
+    par, cap = out["parallel"][2], out["auto_cap"][2]
+    assert par[13] == par[0], f"RESOLVE_PARALLEL left rounds to the serial kernel: {par}"
+    if par[12] > 2 * par[0]:
+        # some round needed more than 2 passes: the capped AUTO handed later rounds to the serial kernel
+        assert cap[13] < cap[0], f"AUTO never handed a round to the serial kernel: {cap}"
 
 
 def test_pod_count_limits_mid_round():

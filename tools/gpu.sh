@@ -11,7 +11,7 @@
 #   tools/gpu.sh sq TAG [bench args]          SQ counters per kernel of one short bench run
 #   tools/gpu.sh ab TAG [bench args]          A/B: default library vs lib/alt (or ALT_OPT="name=value": a
 #                                             ks_config option of the alt arm), twice each
-#   tools/gpu.sh variants TAG [bench args]    VARIANTS="default expt2 ..." one configuration on several lib/<name> builds
+#   tools/gpu.sh variants TAG [bench args]    VARIANTS="default stamps ..." one configuration on several lib/<name> builds
 #   tools/gpu.sh stamps TAG [kind]            resolve-phase stamps (make stamps stamps2 stamps3 first)
 #   tools/gpu.sh valu                         VALU issue costs (tools/valu_issue, built by hipcc on the CPU side)
 export TMPDIR=/tmp
@@ -119,7 +119,7 @@ PY
       summary gpurun_out/ab_${TAG}_$v.json $v
     done ;;
   variants)
-    # one bench configuration on several library builds: VARIANTS="default expt2 ..." (lib/<name>)
+    # one bench configuration on several library builds: VARIANTS="default stamps ..." (lib/<name>)
     for v in ${VARIANTS:-default}; do
       if [ "$v" = default ]; then unset KSCHED_LIB_DIR; else export KSCHED_LIB_DIR=k8s-1m_amd/ksched/lib/$v; fi
       timeout -k 10 300 python -u bench.py --no-cpu-baseline --steps 4 --warmup 1 --latency-calls 0 "$@" \
