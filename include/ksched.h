@@ -400,8 +400,10 @@ typedef struct {
                                      the parallel proposal / verify kernel, handing rounds where pods pile
                                      onto the same nodes to the serial kernel), KS_RESOLVE_SERIAL,
                                      KS_RESOLVE_PARALLEL */
-  uint32_t resolve_par_max_passes;  /* AUTO: a round taking more chunk passes than this (32) ...        */
-  uint32_t resolve_serial_rounds;   /* ... hands this many following rounds (16) to the serial kernel */
+  uint32_t resolve_par_max_passes;  /* AUTO: a round needing more chunk passes than this (32), or fixing
+                                       fewer than 8 pods per pass after 4, ends early and ...        */
+  uint32_t resolve_serial_rounds;   /* ... hands this many following rounds (16; doubled per consecutive
+                                       cut, up to 16x) to the serial kernel                           */
   uint32_t dedup_identical_pods;  /* 1 (default): a round's byte-identical pods are swept once (§5.5) */
   uint32_t early_fix;             /* 1 (default): on one rank the normaliser FIX re-sweep follows the
                                      sweep on its stream (§5.2); 0: behind the merge (multi-rank order) */
@@ -585,7 +587,8 @@ ks_status ks_reset_stats(ks_ctx *ctx);
  * [3] speculated rounds wasted [4] pods re-swept because their guessed
  * normalising maxima were wrong, [5] label-dictionary reclaims, [6] taint
  * dictionary rebuilds, [7] identical pods not swept, [12] passes of the
- * parallel commit, [13] rounds it resolved.  (The instrumented stamps builds,
+ * parallel commit, [13] rounds it resolved, [14] of those it cut short and
+ * handed over to the serial kernel (AUTO).  (The instrumented stamps builds,
  * k8s-1m_amd/csrc/ksched_instr.hpp, put phase cycle sums in [8..15].) */
 ks_status ks_debug_counters(ks_ctx *ctx, uint64_t out[16]);
 /* Diagnostics of the parallel commit (resource-only rounds): with the profile

@@ -13,7 +13,7 @@ constexpr int MAX_K = 512;    // candidates per pod record (two list entries per
 constexpr uint32_t FIX_NONE = 0xFFFFFFFFu;  // fix_list tail
 // device counters of the parallel commit (ksched_resolve.hip): chunk passes,
 // rounds it resolved
-constexpr int CTR_PAR_PASSES = 12, CTR_PAR_ROUNDS = 13;
+constexpr int CTR_PAR_PASSES = 12, CTR_PAR_ROUNDS = 13, CTR_PAR_BAILS = 14;
 // per-pod round marks (ks_batch_marks, include/ksched.h): where the round
 // machinery changed course, for tests that place checks there
 constexpr uint8_t MARK_FIX = 1;          // re-swept with measured normaliser maxima (FIX sweep)
@@ -64,8 +64,10 @@ struct RoundArgs {
   // kernels are launched, resolve_par_kernel first.  rmode[0]: rounds left for
   // the serial resolve_kernel (the parallel kernel exits at once while > 0);
   // rmode[1]: seq of the last round the parallel kernel resolved (the serial
-  // kernel then exits at once).  A round that took more than par_max_passes
-  // passes hands the next serial_rounds rounds to the serial kernel.
+  // kernel then exits at once).  A round the parallel kernel cuts short (more
+  // than par_max_passes passes, or too few pods per pass) hands the next
+  // rmode[2] (>= serial_rounds, doubling per consecutive cut) rounds to the
+  // serial kernel.
   // nullptr: only one kernel is launched and it resolves every round.
   uint32_t *rmode;
   uint32_t par_max_passes, serial_rounds;

@@ -62,6 +62,7 @@ constexpr uint32_t PSRC_M = 0x10000u;  // proposal source: Rpre's node (M index 
 static_assert(PCH == WAVE, "B1 runs one chunk pod per lane of one wave");
 
 // decision codes (proposal and exact)
+constexpr uint32_t PAR_RATE_PASSES = 4, PAR_MIN_RATE = 8, PAR_MAX_BACKOFF = 16;
 enum : uint32_t { PD_NODE = 0, PD_UNSCHED = 1, PD_ERROR = 2, PD_STOP = 3, PD_INCOMPLETE = 4 };
 
 // Resource-only pod as the commit evaluates it: Fit thresholds (request, or
@@ -303,9 +304,20 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
   };
   load_windows(0, min((uint32_t)PCH, n));
 
+  // Under RESOLVE_AUTO a round that runs past par_max_passes passes, or fixes
+  // fewer than PAR_MIN_RATE pods per pass once PAR_RATE_PASSES passes have
+  // run, ends where it is (as if its next pod had stopped it: the rest is
+  // swept again as the next round) and hands the following rounds to the
+  // serial kernel.  A pass costs ~20 serial pods.
+  const uint32_t pass_cap = a.rmode != nullptr ? a.par_max_passes : (uint32_t)MAX_P + 1;
+  bool bailed = false;
   for (uint32_t guard = 0; guard <= MAX_P; ++guard) {
     const uint32_t f = s_ctl[0];
     if (f >= n || s_ctl[1] != 0) break;
+    if (guard >= pass_cap || (a.rmode != nullptr && guard >= PAR_RATE_PASSES && f < PAR_MIN_RATE * guard)) {
+      bailed = true;  // uniform: guard and s_ctl[0] are
+      break;
+    }
     const uint32_t cn = min((uint32_t)PCH, n - f);
 
     // ====================== A: gather candidates (all waves, 4 chunk pods each)
@@ -758,7 +770,16 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
     a.counters[CTR_PAR_ROUNDS] += 1;
     if (a.rmode != nullptr) {
       a.rmode[1] = a.seq;  // resolve_kernel, launched after this one, skips the round
-      if (s_ctl[6] > a.par_max_passes) a.rmode[0] = a.serial_rounds;
+      if (bailed) {
+        // hand over; every consecutive bail doubles the serial stretch
+        // (rmode[2]), up to PAR_MAX_BACKOFF times serial_rounds
+        const uint32_t b = max(a.rmode[2], a.serial_rounds);
+        a.rmode[0] = b;
+        a.rmode[2] = min(2 * b, PAR_MAX_BACKOFF * a.serial_rounds);
+        a.counters[CTR_PAR_BAILS] += 1;
+      } else {
+        a.rmode[2] = 0;
+      }
     }
   }
   __syncthreads();

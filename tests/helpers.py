@@ -45,3 +45,16 @@ def states_np(fn, ctx, n):
     st = fn(ctx, slots.ctypes.data_as(C.POINTER(C.c_uint32)), n, out)
     assert st == 0, f"node_states failed ({st})"
     return np.frombuffer(C.string_at(C.addressof(out), n * C.sizeof(_abi.KsNodeState)), dtype=STATE_DT).copy()
+
+
+class OracleTarget:
+    """The C++ oracle (oracle/pyoracle.py) behind the C5 stream driver's target
+    interface (ksched.stream.GpuTarget): the stream replays against both."""
+
+    def __init__(self, o):
+        self.o = o
+        for name in ("upsert", "delete", "add_pods", "remove_pods", "schedule"):
+            setattr(self, name, getattr(o, name))
+
+    def states(self, slots):
+        return self.o.node_states(slots)

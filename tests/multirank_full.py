@@ -36,7 +36,8 @@ import numpy as np  # noqa: E402
 import pyoracle  # noqa: E402
 from helpers import res_array, states_np  # noqa: E402
 from ksched import Scheduler, synth  # noqa: E402
-from stream import BurstStream, GpuTarget, OracleTarget  # noqa: E402
+from helpers import OracleTarget  # noqa: E402
+from ksched.stream import BurstStream, GpuTarget  # noqa: E402
 from test_gpu_fullsize import MIN_CHECKED, pick_windows, replay_check  # noqa: E402
 
 N = 1_000_000

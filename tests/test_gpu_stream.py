@@ -16,7 +16,8 @@ import pytest
 import pyoracle
 from helpers import assert_results_equal, res_array, states_np
 from ksched import Scheduler, synth
-from stream import BurstStream, GpuTarget, OracleTarget, Rates
+from helpers import OracleTarget
+from ksched.stream import BurstStream, GpuTarget, Rates
 
 pytestmark = pytest.mark.gpu
 

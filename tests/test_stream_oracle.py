@@ -8,7 +8,8 @@ import pytest
 import pyoracle
 from helpers import assert_results_equal, state_array
 from ksched import synth
-from stream import BurstStream, OracleTarget, Rates
+from helpers import OracleTarget
+from ksched.stream import BurstStream, Rates
 
 RATES = Rates(pod_delete=0.05, node_update=0.02, node_delete=0.01)
 

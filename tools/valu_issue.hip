@@ -131,6 +131,13 @@ __device__ __forceinline__ void record(unsigned long long *cyc, unsigned long lo
 #define I_ADD_F32_E64(r) "v_add_f32_e64 %" #r ", %" #r ", %8\n"
 #define I_MUL_F32_E64(r) "v_mul_f32_e64 %" #r ", %" #r ", %8\n"
 #define I_ADD_U32_E64(r) "v_add_u32_e64 %" #r ", %" #r ", %8\n"
+// an SGPR source (src0) in the 2-cycle class
+#define I_ADD_F32_S(r) "v_add_f32 %" #r ", %12, %" #r "\n"
+#define I_MUL_F32_S(r) "v_mul_f32 %" #r ", %12, %" #r "\n"
+#define I_ADD_U32_S(r) "v_add_u32 %" #r ", %12, %" #r "\n"
+#define I_AND_S(r) "v_and_b32 %" #r ", %12, %" #r "\n"
+#define I_FMAC_F32_S(r) "v_fmac_f32 %" #r ", %12, %8\n"
+#define I_FMA_F32_SS(r) "v_fma_f32 %" #r ", %12, %12, %" #r "\n"
 
 K64(k_add_f64, I_ADD_F64)
 K64(k_mul_f64, I_MUL_F64)
@@ -174,6 +181,12 @@ K32(k_fmac_f32_same, I_FMAC_F32_SAME)
 K32(k_add_f32_e64, I_ADD_F32_E64)
 K32(k_mul_f32_e64, I_MUL_F32_E64)
 K32(k_add_u32_e64, I_ADD_U32_E64)
+K32(k_add_f32_s, I_ADD_F32_S)
+K32(k_mul_f32_s, I_MUL_F32_S)
+K32(k_add_u32_s, I_ADD_U32_S)
+K32(k_and_s, I_AND_S)
+K32(k_fmac_f32_s, I_FMAC_F32_S)
+K32(k_fma_f32_ss, I_FMA_F32_SS)
 
 // v_readlane_b32: SGPR destinations
 __global__ void k_readlane(unsigned long long *cyc, uint32_t seed, uint32_t c, uint32_t iters) {
@@ -246,6 +259,13 @@ int main() {
       {"v_add_f32_e64 (VOP3)", nullptr, k_add_f32_e64},
       {"v_mul_f32_e64 (VOP3)", nullptr, k_mul_f32_e64},
       {"v_add_u32_e64 (VOP3)", nullptr, k_add_u32_e64},
+      // an SGPR source operand
+      {"v_add_f32 (s, v)", nullptr, k_add_f32_s},
+      {"v_mul_f32 (s, v)", nullptr, k_mul_f32_s},
+      {"v_add_u32 (s, v)", nullptr, k_add_u32_s},
+      {"v_and_b32 (s, v)", nullptr, k_and_s},
+      {"v_fmac_f32 (VOP2, s, v')", nullptr, k_fmac_f32_s},
+      {"v_fma_f32 (s, s, v)", nullptr, k_fma_f32_ss},
   };
   const char *only = std::getenv("VALU_ONLY");  // a substring: run the matching entries only
   hipDeviceProp_t prop{};
