@@ -180,7 +180,9 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
   // control: [0] f, [1] stopped, [2] cut, [4] distinct nodes, [5] |M|, [6] passes
   __shared__ uint32_t s_ctl[8];
 
-  const uint32_t tid = threadIdx.x, lane = tid % WAVE, wid = tid / WAVE;
+  // tid / lane are re-materialised at each pass (see the pass loop)
+  uint32_t tid = threadIdx.x, lane = tid % WAVE;
+  const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
   if (a.rmode != nullptr && uniform_u32(a.rmode[0]) != 0) return;  // serial rounds: resolve_kernel follows
   const uint32_t start = uniform_u32(*a.act);
   if (start >= a.npods || uniform_u32(*a.sstart) != start) {  // the lists belong to other pods
@@ -312,6 +314,10 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
   const uint32_t pass_cap = a.rmode != nullptr ? a.par_max_passes : (uint32_t)MAX_P + 1;
   bool bailed = false;
   for (uint32_t guard = 0; guard <= MAX_P; ++guard) {
+    // Opaque per pass: otherwise the compiler hoists every lane-derived LDS
+    // address out of the pass loop, which at the 128-VGPR cap of a
+    // 1024-thread block spills them to scratch.
+    asm volatile("" : "+v"(tid), "+v"(lane));
     const uint32_t f = s_ctl[0];
     if (f >= n || s_ctl[1] != 0) break;
     if (guard >= pass_cap || (a.rmode != nullptr && guard >= PAR_RATE_PASSES && f < PAR_MIN_RATE * guard)) {
@@ -671,15 +677,37 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
       const uint32_t mn = s_ctl[5];
       if (first) {
         const uint32_t mi = isnew ? mn + (uint32_t)__popcll(nm & lt_mask) : mi0;
-        RNode x = *(isnew ? &s_prow[c] : &s_m[mi]);
+        // a new node enters M with its chunk-start row (piece by piece: a
+        // struct copy through a selected pointer goes via scratch); then the
+        // requests are summed in registers, in pod order, and stored back
+        if (isnew) {
+          const uint4 *sp = (const uint4 *)&s_prow[c];
+          uint4 *dp = (uint4 *)&s_m[mi];
+#pragma unroll
+          for (int q = 0; q < (int)(sizeof(RNode) / 16); ++q) dp[q] = sp[q];
+        }
+        CandRow &xr = s_m[mi].row;
+        double rc = xr.rc, rm = xr.rm, zc = xr.zc100, zm = xr.zm100;
+        int32_t np = xr.np;
         const uint32_t d = (uint32_t)__popcll(fm & lt_mask);
         s_cdm[d] = mi;
-        s_cdp[d][0] = x.row.rc;
-        s_cdp[d][1] = x.row.rm;
-        s_cdn[d] = x.row.np;
+        s_cdp[d][0] = rc;
+        s_cdp[d][1] = rm;
+        s_cdn[d] = np;
         s_cdr[d] = isnew ? 0u : 1u;
-        for (uint64_t m = g; m; m &= m - 1) pq_add(x.row, s_q[f + (uint32_t)__builtin_ctzll(m)]);
-        s_m[mi] = x;
+        for (uint64_t m = g; m; m &= m - 1) {  // pq_add
+          const PQ &q = s_q[f + (uint32_t)__builtin_ctzll(m)];
+          rc += q.rc;
+          rm += q.rm;
+          zc += q.zc;
+          zm += q.zm;
+          np += 1;
+        }
+        xr.rc = rc;
+        xr.rm = rm;
+        xr.zc100 = zc;
+        xr.zm100 = zm;
+        xr.np = np;
         if (isnew) {
           uint32_t h = rhash(ws);
           while (atomicCAS(&s_mh[h], 0u, ws + 1) != 0u) h = (h + 1) & (PMH - 1);
