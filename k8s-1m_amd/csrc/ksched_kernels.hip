@@ -826,18 +826,18 @@ __global__ __launch_bounds__(PATCH_THREADS) void patch_kernel(RoundArgs a) {
   for (uint32_t i = tid; i < PHASH; i += PATCH_THREADS) s_hkey[i] = 0;
   __syncthreads();
 
-  // (1) carried node tid: its row at the sweep (rc0 / rm0 / np0) and live
+  // (1) carried node tid: its row at the sweep (rc0 / rm0 / np0) and live.
+  // No row is held across the barriers below (aggregates kept live across
+  // them were put on the stack): step (3) reads the carry record again.
   int32_t d[NFILT + 3] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t k1 = 0;
-  CarryRec cr;
-  CandRow crow_c;
-  NodeExt ce;
   if (tid < nc) {
-    cr = a.carry_in[tid];
+    const CarryRec &cr = a.carry_in[tid];
+    NodeExt ce{};
     if (EXT) ext_from_words(cr.ext, ce);
-    crow_c = cand_row(cr.acpu, cr.amem, cr.rc, cr.rm, cr.zc, cr.zm, cr.apods, cr.np, cr.pos);
+    const double inv_cpu = cr.acpu ? 1.0 / (double)cr.acpu : 0.0, inv_mem = cr.amem ? 1.0 / (double)cr.amem : 0.0;
     const NodeRegs r1 = make_regs_inv(cr.acpu, cr.amem, cr.rc, cr.rm, cr.zc, cr.zm, cr.apods, cr.np, cr.slot,
-                                      crow_c.inv_cpu, crow_c.inv_mem);
+                                      inv_cpu, inv_mem);
     NodeRegs r0 = r1;
     r0.free_cpu = (double)(cr.acpu - cr.rc0);
     r0.free_mem = (double)(cr.amem - cr.rm0);
@@ -859,10 +859,12 @@ __global__ __launch_bounds__(PATCH_THREADS) void patch_kernel(RoundArgs a) {
   __syncthreads();
 
   // (2) list entry tid survives unless its node is carried; compaction keeps key order
+  // the entry's row and label words, as named 16-byte pieces (arrays or
+  // aggregates live across the barriers below stay on the stack)
+  static_assert(sizeof(CandRow) == 80 && sizeof(CandExt) == 64, "patch row pieces");
   uint64_t lk = 0;
   bool keep = false;
-  CandRow lrow;
-  CandExt lext;
+  uint4 lr0, lr1, lr2, lr3, lr4, lx0, lx1, lx2, lx3;
   if (tid < nk) {
     lk = rec[REC_HDR_WORDS + tid];
     const uint32_t slot = 0xFFFFFFFFu - (uint32_t)lk;
@@ -873,8 +875,12 @@ __global__ __launch_bounds__(PATCH_THREADS) void patch_kernel(RoundArgs a) {
       h = (h + 1) & (PHASH - 1);
     }
     if (keep) {
-      lrow = a.crow[(size_t)r * a.K + tid];
-      if (EXT) lext = a.cext[(size_t)r * a.K + tid];
+      const uint4 *sr = (const uint4 *)&a.crow[(size_t)r * a.K + tid];
+      lr0 = sr[0], lr1 = sr[1], lr2 = sr[2], lr3 = sr[3], lr4 = sr[4];
+      if (EXT) {
+        const uint4 *sx = (const uint4 *)&a.cext[(size_t)r * a.K + tid];
+        lx0 = sx[0], lx1 = sx[1], lx2 = sx[2], lx3 = sx[3];
+      }
     }
   }
   const bool cin = k1 > bound;  // carried keys the bound does not cover must be listed
@@ -916,16 +922,21 @@ __global__ __launch_bounds__(PATCH_THREADS) void patch_kernel(RoundArgs a) {
   __syncthreads();  // every old key / row of this record has been read: rewrite in place
   if (keep && pos_l < a.K) {
     rec[REC_HDR_WORDS + pos_l] = lk;
-    a.crow[(size_t)r * a.K + pos_l] = lrow;
-    if (EXT) a.cext[(size_t)r * a.K + pos_l] = lext;
+    uint4 *dr = (uint4 *)&a.crow[(size_t)r * a.K + pos_l];
+    dr[0] = lr0, dr[1] = lr1, dr[2] = lr2, dr[3] = lr3, dr[4] = lr4;
+    if (EXT) {
+      uint4 *dx = (uint4 *)&a.cext[(size_t)r * a.K + pos_l];
+      dx[0] = lx0, dx[1] = lx1, dx[2] = lx2, dx[3] = lx3;
+    }
   }
   if (cin && pos_c < a.K) {
+    const CarryRec &cr = a.carry_in[tid];
     rec[REC_HDR_WORDS + pos_c] = k1;
-    a.crow[(size_t)r * a.K + pos_c] = crow_c;
+    a.crow[(size_t)r * a.K + pos_c] = cand_row(cr.acpu, cr.amem, cr.rc, cr.rm, cr.zc, cr.zm, cr.apods, cr.np, cr.pos);
     if (EXT) {
-      CandExt x;
-      for (int q = 0; q < 2 + LW + NNUM; ++q) x.w[q] = cr.ext[q];
-      a.cext[(size_t)r * a.K + pos_c] = x;
+      uint64_t *dx = a.cext[(size_t)r * a.K + pos_c].w;
+#pragma unroll
+      for (int q = 0; q < 2 + LW + NNUM; ++q) dx[q] = cr.ext[q];
     }
   }
   if (tid == 0) {
@@ -1525,12 +1536,10 @@ __global__ __launch_bounds__(RESOLVE_THREADS) void resolve_kernel(RoundArgs a) {
 #pragma unroll
             for (int j = 0; j < ROW_PIECES; ++j) wp[j] = s_lrowb[b8][cw][j][ck];
             own = rnode_from_row(w, 0xFFFFFFFFu - (uint32_t)s_lkey[b8][c]);
-            if constexpr (EXT) {
-              CandExt x;
-              uint4 *xp = (uint4 *)&x;
+            if constexpr (EXT) {  // piece by piece into LDS (a punned local goes via scratch)
+              uint4 *xp = (uint4 *)&s_modx[mj];
 #pragma unroll
               for (int j = 0; j < EXT_PIECES; ++j) xp[j] = s_lrowb[b8][cw][ROW_PIECES + j][ck];
-              s_modx[mj] = x;
             }
             mine = true;
           }
