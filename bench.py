@@ -90,7 +90,7 @@ E2E_DEPTH = 2  # batches submitted ahead in the headline loop (compile of k+1 an
 REF_SCHEDULE_ONE_US = 560.0  # README.adoc:786 (per pod per shard, ~195 nodes evaluated)
 KERNEL_SOURCES = ["k8s-1m_amd/csrc/ksched_kernels.hip", "k8s-1m_amd/csrc/ksched_eval.hpp", "k8s-1m_amd/csrc/ksched_dev.hpp",
                   "k8s-1m_amd/csrc/ksched_kernels.hpp", "k8s-1m_amd/csrc/ksched_util.hpp",
-                  "k8s-1m_amd/csrc/ksched_resolve.hip", "k8s-1m_amd/Makefile"]
+                  "k8s-1m_amd/csrc/ksched_instr.hpp", "k8s-1m_amd/csrc/ksched_resolve.hip", "k8s-1m_amd/Makefile"]
 
 
 def parse():

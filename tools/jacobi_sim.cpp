@@ -245,6 +245,108 @@ int main(int argc, char **argv) {
       for (uint32_t j = 0; j < seq_stop && okc; ++j) okc = fx[j] == seq[j];
       printf(" C%u:%u%s", C, iters, okc ? "" : "(MISMATCH)");
     }
+    // rewin-aware proposals (chunk 64): after the greedy matching, every pod
+    // re-scores the nodes lower chunk pods claimed (with those pods' requests)
+    // and proposes the best of that and its greedy proposal; R alternations
+    // of greedy (rewinners keep their node) and re-score
+    for (uint32_t R : {1u, 2u, 3u}) {
+      const uint32_t C = 64;
+      std::vector<uint64_t> fx(n, 0);
+      uint32_t ff = 0, iters = 0, cstop = n;
+      while (ff < n) {
+        ++iters;
+        const uint32_t ce = std::min(n, ff + C);
+        std::unordered_map<uint32_t, Node> mod;  // the fixed prefix's nodes, live
+        for (uint32_t i = 0; i < ff; ++i) if (fx[i]) {
+          const uint32_t s = kslot(fx[i]);
+          auto it = mod.find(s);
+          if (it == mod.end()) it = mod.emplace(s, nodes[s]).first;
+          Node &x = it->second; const Pod &q = pods[start + i];
+          x.rc += q.rc; x.rm += q.rm; x.zc += q.zc; x.zm += q.zm; x.np += 1;
+        }
+        std::vector<uint64_t> rp(n, 0);
+        for (uint32_t j = ff; j < ce; ++j)
+          for (auto &kv : mod) rp[j] = std::max(rp[j], key(kv.second, pods[start + j], kv.first));
+        std::vector<uint64_t> pr(fx);
+        std::vector<char> rw(n, 0);  // pr[j] is a rewin
+        for (uint32_t r = 0; r < R; ++r) {
+          // greedy: the first listed node no lower pod claims (rewinners keep theirs)
+          std::unordered_map<uint32_t, int> tk;
+          for (uint32_t i = 0; i < ff; ++i) if (fx[i]) tk[kslot(fx[i])] = 1;
+          for (uint32_t j = ff; j < ce; ++j) {
+            if (!rw[j]) {
+              uint64_t ku = 0;
+              for (uint64_t k : L[j].keys) if (!tk.count(kslot(k))) { ku = k; break; }
+              pr[j] = ku ? std::max(ku, rp[j]) : (rp[j] > L[j].bound ? rp[j] : 0);
+            }
+            if (pr[j]) tk[kslot(pr[j])] = 1;
+          }
+          // re-score (in parallel: from this iteration's claims)
+          std::vector<uint64_t> np(pr);
+          std::vector<char> nrw(n, 0);
+          for (uint32_t j = ff; j < ce; ++j) {
+            std::unordered_map<uint32_t, Node> ch;
+            for (uint32_t i = ff; i < j; ++i) if (pr[i]) {
+              const uint32_t s = kslot(pr[i]);
+              auto it = ch.find(s);
+              if (it == ch.end()) {
+                auto m2 = mod.find(s);
+                it = ch.emplace(s, m2 != mod.end() ? m2->second : nodes[s]).first;
+              }
+              Node &x = it->second; const Pod &q = pods[start + i];
+              x.rc += q.rc; x.rm += q.rm; x.zc += q.zc; x.zm += q.zm; x.np += 1;
+            }
+            uint64_t best = 0;
+            for (auto &kv : ch) best = std::max(best, key(kv.second, pods[start + j], kv.first));
+            if (best > pr[j] && (pr[j] || best > L[j].bound)) { np[j] = best; nrw[j] = 1; }
+          }
+          pr = np;
+          rw = nrw;
+          if (getenv("SIM_FINAL")) {
+            // final greedy with the rewin as a non-exclusive extra candidate:
+            // max(first unclaimed listed node, the rewin key of the re-score)
+            std::unordered_map<uint32_t, int> tk2;
+            for (uint32_t i = 0; i < ff; ++i) if (fx[i]) tk2[kslot(fx[i])] = 1;
+            for (uint32_t j = ff; j < ce; ++j) {
+              uint64_t ku = 0;
+              for (uint64_t k : L[j].keys) if (!tk2.count(kslot(k))) { ku = k; break; }
+              uint64_t g = ku ? std::max(ku, rp[j]) : (rp[j] > L[j].bound ? rp[j] : 0);
+              const uint64_t rk2 = rw[j] ? np[j] : 0;
+              if (rk2 > g) { g = rk2; rw[j] = 1; } else rw[j] = 0;
+              pr[j] = g;
+              if (g && !rw[j]) tk2[kslot(g)] = 1;
+            }
+          }
+        }
+        uint32_t m = ff;
+        bool stopped = false;
+        for (; m < ce; ++m) {
+          bool st;
+          const uint64_t d = decide(m, pr, st);
+          if (st) { stopped = true; break; }
+          if (d != pr[m]) {
+            fx[m] = d;
+            if (R == (uint32_t)atoi(getenv("SIM_R") ? getenv("SIM_R") : "1")) {  // why: d / pr claimed by a lower chunk pod (rewin) or not; their list ranks
+              bool drw = false, prw = false;
+              for (uint32_t i = ff; i < m; ++i) { drw |= pr[i] && kslot(pr[i]) == kslot(d); prw |= pr[i] && kslot(pr[i]) == kslot(pr[m]); }
+              int rd = -1, rpp = -1;
+              for (size_t q = 0; q < L[m].keys.size(); ++q) { if (kslot(L[m].keys[q]) == kslot(d)) rd = (int)q; if (kslot(L[m].keys[q]) == kslot(pr[m])) rpp = (int)q; }
+              fprintf(stderr, "mm pod %u (chunk+%u): d %s rank %d key %llu | pr %s rank %d key %llu | rp %llu\n", m, m - ff,
+                      drw ? "REWIN" : (mod.count(kslot(d)) ? "M" : "list"), rd, (unsigned long long)(d >> 32),
+                      prw ? "REWIN" : (mod.count(kslot(pr[m])) ? "M" : "list"), rpp, (unsigned long long)(pr[m] >> 32),
+                      (unsigned long long)(rp[m] >> 32));
+            }
+            break;
+          }
+          fx[m] = d;
+        }
+        if (stopped) { cstop = m; break; }
+        ff = m < ce ? m + 1 : ce;
+      }
+      bool okc = cstop == seq_stop;
+      for (uint32_t j = 0; j < seq_stop && okc; ++j) okc = fx[j] == seq[j];
+      printf(" RW%u:%u%s", R, iters, okc ? "" : "(MISMATCH)");
+    }
     bool ok = jstop == seq_stop;
     for (uint32_t j = 0; j < seq_stop && ok; ++j) ok = w[j] == seq[j];
     printf("round %ld start %u: seq %u pods, passes %u, changed/pass", tot_rounds, start, seq_stop, passes);

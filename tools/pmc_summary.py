@@ -34,8 +34,17 @@ ROOT = Path(__file__).resolve().parent.parent
 SWEEP = "sweep_kernel"
 # the same list, in the same order, as bench.py's KERNEL_SOURCES (the bench
 # uses a summary only when the hashes agree)
-KERNEL_SOURCES = ["k8s-1m_amd/csrc/ksched_kernels.hip", "k8s-1m_amd/csrc/ksched_eval.hpp", "k8s-1m_amd/csrc/ksched_dev.hpp",
-                  "k8s-1m_amd/csrc/ksched_kernels.hpp", "k8s-1m_amd/Makefile"]
+def bench_kernel_sources(root):
+    """bench.py's KERNEL_SOURCES, read from its text (one list for every hash)."""
+    import ast
+    tree = ast.parse((root / "bench.py").read_text())
+    for node in tree.body:
+        if isinstance(node, ast.Assign) and any(getattr(t, "id", None) == "KERNEL_SOURCES" for t in node.targets):
+            return ast.literal_eval(node.value)
+    raise RuntimeError("bench.py has no KERNEL_SOURCES")
+
+
+KERNEL_SOURCES = bench_kernel_sources(ROOT)
 
 
 def kernel_src_hash() -> str:

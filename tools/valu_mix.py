@@ -37,8 +37,17 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parent.parent
 CSRC = ROOT / "k8s-1m_amd" / "csrc"
 # the hash bench.py keys its per-configuration measurements by (bench.KERNEL_SOURCES)
-KERNEL_SOURCES = ["k8s-1m_amd/csrc/ksched_kernels.hip", "k8s-1m_amd/csrc/ksched_eval.hpp", "k8s-1m_amd/csrc/ksched_dev.hpp",
-                  "k8s-1m_amd/csrc/ksched_kernels.hpp", "k8s-1m_amd/Makefile"]
+def bench_kernel_sources(root):
+    """bench.py's KERNEL_SOURCES, read from its text (one list for every hash)."""
+    import ast
+    tree = ast.parse((root / "bench.py").read_text())
+    for node in tree.body:
+        if isinstance(node, ast.Assign) and any(getattr(t, "id", None) == "KERNEL_SOURCES" for t in node.targets):
+            return ast.literal_eval(node.value)
+    raise RuntimeError("bench.py has no KERNEL_SOURCES")
+
+
+KERNEL_SOURCES = bench_kernel_sources(ROOT)
 OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
 HIPCC = "/opt/rocm/bin/hipcc"
 WAVES = 4  # the sweep's occupancy: 4 waves per SIMD (5 for the EXT kernels; the costs barely differ)
@@ -117,7 +126,15 @@ def template_args(mangled: str) -> str:
     return f"<{m.group(1)}, {'true' if m.group(2) == '1' else 'false'}, {m.group(3)}>"
 
 
-def cost_of(op: str, costs: dict, fast_med: float, slow_med: float):
+SGPR_SRC = re.compile(r"^(s\d|s\[|vcc|exec|m0)")
+
+
+def cost_of(op: str, costs: dict, fast_med: float, slow_med: float, args: str = ""):
+    # the 2-cycle class needs VGPR (or inline-constant) sources: with an SGPR
+    # source it issues like the 4-cycle class (tools/valu_issue.hip "(s, v)"
+    # rows, profiles/r4/valu_vop.jsonl)
+    if FAST.match(op) and any(SGPR_SRC.match(x.strip()) for x in args.split(",")[1:]):
+        return slow_med, "v_add_u32 (s, v)" in costs
     base = re.sub(r"_e(32|64)$", "", op)
     for k in (op, base, base.replace("_dpp", "") + "_dpp" if op.endswith("_dpp") else base):
         if k in costs:
@@ -138,13 +155,14 @@ def main():
            "class_median": {"fast_32bit": fast_med, "other": slow_med}, "kernels": {}}
     for name, ins in kernels(disassemble()).items():
         lo, hi = pod_loop(ins)
-        hist = collections.Counter(op for a, op, _ in ins if lo <= a < hi and op.startswith("v_"))
-        n = sum(hist.values())
+        loop = [(op, args) for a, op, args in ins if lo <= a < hi and op.startswith("v_")]
+        hist = collections.Counter(op for op, _ in loop)
+        n = len(loop)
         cyc = covered = 0.0
-        for op, c in hist.items():
-            v, ok = cost_of(op, costs, fast_med, slow_med)
-            cyc += c * v
-            covered += c if ok else 0
+        for op, args in loop:
+            v, ok = cost_of(op, costs, fast_med, slow_med, args)
+            cyc += v
+            covered += 1 if ok else 0
         res["kernels"][template_args(name)] = {
             "mangled": name, "loop_valu": n, "cycles_per_valu": round(cyc / n, 4),
             "measured_share": round(covered / n, 4),
