@@ -300,14 +300,15 @@ def run_batches(args, kind, sched, world, rank, t_setup):
         pr = (C.c_uint64 * 16)()
         sched.lib.ks_debug_resolve_profile(sched.ctx, pr)
         rounds = max(1, int(pr[9]))
-        names = ["stage", "gather_barrier", "proposals", "gather_w0_scan", "chunk_pairs", "gather_w0_dmawait", "commit",
-                 "rpre_update", "epilogue"]
-        prof = {"rounds": int(pr[9]), "cycles_per_round": {k: round(int(pr[i]) / rounds, 1) for i, k in enumerate(names)}}
-        prof["cycles_per_round"]["total"] = round(sum(int(pr[i]) for i in range(9)) / rounds, 1)
+        # phase clock slots (ksched_resolve.hip resolve_par_kernel); wave 0's
+        # gather is slots 12 (prefetched windows), 13 (probes), 14 (scans), 3 (DMA issue), 5 (DMA wait)
+        names = {0: "stage", 12: "gather_w0_prefetch_wait", 13: "gather_w0_probes", 14: "gather_w0_scans",
+                 3: "gather_w0_dma_issue", 5: "gather_w0_dma_wait", 1: "gather_barrier", 2: "proposals",
+                 4: "chunk_pairs", 6: "commit", 7: "rpre_update", 8: "epilogue"}
+        prof = {"rounds": int(pr[9]), "cycles_per_round": {k: round(int(pr[i]) / rounds, 1) for i, k in names.items()}}
+        prof["cycles_per_round"]["total"] = round(sum(int(pr[i]) for i in names) / rounds, 1)
         prof["dirty_recomputes_per_round"] = round(int(pr[10]) / rounds, 2)
         prof["extra_windows_per_round"] = round(int(pr[11]) / rounds, 2)
-        prof["w0_prefetch_wait"] = round(int(pr[12]) / rounds, 1)
-        prof["w0_pre_scan"] = round(int(pr[13]) / rounds, 1)
     lat = latency(args, kind, sched, world) if args.latency_calls > 0 else None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_pods > 0:

@@ -400,8 +400,8 @@ typedef struct {
                                      the parallel proposal / verify kernel, handing rounds where pods pile
                                      onto the same nodes to the serial kernel), KS_RESOLVE_SERIAL,
                                      KS_RESOLVE_PARALLEL */
-  uint32_t resolve_par_max_passes;  /* AUTO: a round needing more chunk passes than this (32), or fixing
-                                       fewer than 8 pods per pass after 4, ends early and ...        */
+  uint32_t resolve_par_max_passes;  /* AUTO: a round needing more chunk passes than this (32), or on
+                                       pace (after 4) to need more, ends early and ...               */
   uint32_t resolve_serial_rounds;   /* ... hands this many following rounds (16; doubled per consecutive
                                        cut, up to 16x) to the serial kernel                           */
   uint32_t dedup_identical_pods;  /* 1 (default): a round's byte-identical pods are swept once (§5.5) */
@@ -592,9 +592,12 @@ ks_status ks_reset_stats(ks_ctx *ctx);
  * k8s-1m_amd/csrc/ksched_instr.hpp, put phase cycle sums in [8..15].) */
 ks_status ks_debug_counters(ks_ctx *ctx, uint64_t out[16]);
 /* Diagnostics of the parallel commit (resource-only rounds): with the profile
- * on, every round accumulates s_memtime cycles per phase into out[0..8]
- * (stage, gather, proposals, base rows, chunk pairs, decisions, commit,
- * Rpre updates, epilogue) and out[9] counts the rounds profiled. */
+ * on, every round accumulates s_memtime cycles per phase: out[0] stage,
+ * [1] gather barrier, [2] proposals, [3] wave 0's row DMA issue, [4] chunk
+ * pairs, [5] its DMA wait, [6] decide + commit, [7] Rpre updates, [8]
+ * epilogue, [12] wave 0's wait for its prefetched windows, [13] its scalar
+ * state and M probes, [14] its window scans; out[9] counts the rounds
+ * profiled, [10] dirty Rpre recomputes, [11] extra list windows. */
 ks_status ks_debug_set_profile(ks_ctx *ctx, int32_t on);
 ks_status ks_debug_resolve_profile(ks_ctx *ctx, uint64_t out[16]);
 /* Round marks of a finished batch (diagnostics for tests that place parity

@@ -32,8 +32,10 @@
 // node an earlier pod of the same chunk took (Rpre covers every node of the
 // fixed prefix exactly), so a C3 round of 256 pods takes 6-12 passes
 // (tools/jacobi_sim.cpp).  Rounds whose pods pile onto the same nodes (kwok
-// clusters of identical nodes) take many passes; after such a round the next
-// RoundArgs::serial_rounds rounds run the serial kernel (RoundArgs::rmode).
+// clusters of identical nodes) would take many passes: under RESOLVE_AUTO such
+// a round is cut short (pass cap / too few pods per pass) and the following
+// rounds run the serial kernel, a stretch that doubles per consecutive cut
+// (RoundArgs::rmode).
 //
 // Arithmetic is the serial kernel's (exact binary64 rows, one-FMA
 // LeastAllocated, Markstein BalancedAllocation; ksched_eval.hpp), and the
@@ -62,7 +64,7 @@ constexpr uint32_t PSRC_M = 0x10000u;  // proposal source: Rpre's node (M index 
 static_assert(PCH == WAVE, "B1 runs one chunk pod per lane of one wave");
 
 // decision codes (proposal and exact)
-constexpr uint32_t PAR_RATE_PASSES = 4, PAR_MIN_RATE = 8, PAR_MAX_BACKOFF = 16;
+constexpr uint32_t PAR_RATE_PASSES = 4, PAR_MAX_BACKOFF = 16;
 enum : uint32_t { PD_NODE = 0, PD_UNSCHED = 1, PD_ERROR = 2, PD_STOP = 3, PD_INCOMPLETE = 4 };
 
 // Resource-only pod as the commit evaluates it: Fit thresholds (request, or
@@ -155,6 +157,7 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
   __shared__ uint32_t s_lptr[MAX_P];   // list entries before it are all in M
   __shared__ uint4 s_resc[MAX_P];      // result: {win lo, win hi, feasible, status}
   __shared__ int32_t s_rdl[MAX_P];     // result: Fit failures gained
+  __shared__ uint32_t s_pfo[MAX_P];    // result: PodDev::prefilter_out (staged: no global read in the epilogue)
   // ---- fixed modified nodes (M): live row, round-start Requested / pod count, slot
   __shared__ RNode s_m[MAX_P];
   __shared__ uint32_t s_mh[PMH], s_mi[PMH];  // slot + 1 -> M index
@@ -202,8 +205,9 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
   const uint32_t n = min(a.P, a.npods - start);
   const uint32_t RW = rec_words(a.K);
   const uint64_t lt_mask = (1ull << lane) - 1ull;
-  // phases: 0 stage, 1 gather, 2 proposals, 3 (unused), 4 chunk pairs, 5 (unused), 6 decide + commit, 7 Rpre
-  // updates, 8 epilogue, [9] rounds
+  // phases: 0 stage, 1 gather barrier, 2 proposals, 3 wave 0's row DMA issue, 4 chunk pairs, 5 wave 0's
+  // DMA wait, 6 decide + commit, 7 Rpre updates, 8 epilogue, [9] rounds, [10] dirty recomputes, [11] extra
+  // windows, 12 wave 0's wait for the prefetched windows, 13 its scalar state + probes, 14 its window scans
   __shared__ uint64_t s_clk[16];
   if (tid < 16) s_clk[tid] = 0;
   PhaseClock clk{tid == 0 ? a.prof : nullptr, s_clk, 0};
@@ -276,6 +280,7 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
     s_rep[i] = ri;
     s_q[i] = make_pq(p);
     s_fl[i] = p.flags;
+    s_pfo[i] = p.prefilter_out;
     s_hdr[i] = *(const ShardRecHdr *)(a.frec + (size_t)ri * RW);
     s_rk[i] = 0;
     s_dl[i] = 0;
@@ -306,11 +311,11 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
   };
   load_windows(0, min((uint32_t)PCH, n));
 
-  // Under RESOLVE_AUTO a round that runs past par_max_passes passes, or fixes
-  // fewer than PAR_MIN_RATE pods per pass once PAR_RATE_PASSES passes have
-  // run, ends where it is (as if its next pod had stopped it: the rest is
-  // swept again as the next round) and hands the following rounds to the
-  // serial kernel.  A pass costs ~20 serial pods.
+  // Under RESOLVE_AUTO a round that runs past par_max_passes passes, or whose
+  // pace after PAR_RATE_PASSES passes projects more than that many for its n
+  // pods (passes * n > par_max_passes * fixed), ends where it is (as if its
+  // next pod had stopped it: the rest is swept again as the next round) and
+  // hands the following rounds to the serial kernel.
   const uint32_t pass_cap = a.rmode != nullptr ? a.par_max_passes : (uint32_t)MAX_P + 1;
   bool bailed = false;
   for (uint32_t guard = 0; guard <= MAX_P; ++guard) {
@@ -320,7 +325,7 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
     asm volatile("" : "+v"(tid), "+v"(lane));
     const uint32_t f = s_ctl[0];
     if (f >= n || s_ctl[1] != 0) break;
-    if (guard >= pass_cap || (a.rmode != nullptr && guard >= PAR_RATE_PASSES && f < PAR_MIN_RATE * guard)) {
+    if (guard >= pass_cap || (a.rmode != nullptr && guard >= PAR_RATE_PASSES && guard * n > pass_cap * f)) {
       bailed = true;  // uniform: guard and s_ctl[0] are
       break;
     }
@@ -395,6 +400,7 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
           }
         }
       }
+      clk.tick(13);  // wave 0: scalar state, dirty recomputes, M probes of the first windows
       static_for<PPW>([&](auto T) {
         constexpr int t = T;
         const uint32_t c = wid + PR_NW * t;
@@ -438,10 +444,14 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
           s_cpst[c] = feas == 0 ? PD_UNSCHED : ((s_fl[j] & PF_PREF_ERR) && feas >= 2) ? PD_ERROR : PD_NODE;
         }
       });
+      clk.tick(14);  // wave 0: the window scans
     }
     // the first PNR candidates' rows of the wave's pods by LDS-DMA, lane r ->
     // row r, issued after every scan (the compiler waits for all outstanding
-    // loads before a scan's key use); landed before the barrier
+    // loads before a scan's key use); landed before the barrier.  (Issued with
+    // the key windows a phase earlier instead, for the first PNR list entries,
+    // the gather kept its time and the Rpre phase grew by the issue: 55k ->
+    // 76k cycles per round on the proxy.)
     static_for<PPW>([&](auto T) {
       const uint32_t c = wid + PR_NW * (uint32_t)T;
       if (c >= cn) return;
@@ -452,7 +462,7 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
           __builtin_amdgcn_global_load_lds((gvoid_t *)(src + q), (lvoid_t *)&s_crow[c][q][0], 16, 0, 0);
       }
     });
-    clk.tick(3);                    // wave 0's own gathering
+    clk.tick(3);                    // wave 0: the row DMAs issued
     __builtin_amdgcn_s_waitcnt(0);  // this wave's row DMAs have landed
     clk.tick(5);                    // ... and its wait for them
     __syncthreads();
@@ -778,7 +788,7 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
         case 5: v = a.evaluated; break;                                   // evaluated_nodes
         case 6: case 7: case 8: case 9: v = s_hdr[pr].fails[w - 6]; break;  // fail_counts
         case 10: v = s_hdr[pr].fails[KS_PLUGIN_FIT_IDX] + (uint32_t)s_rdl[pr]; break;
-        case 13: v = a.pods[start + pr].prefilter_out; break;            // prefiltered
+        case 13: v = s_pfo[pr]; break;                                    // prefiltered
         case 14: v = (win && c.z == 1) ? 1u : 0u; break;                  // flags
         default: v = 0; break;                                            // spread_fail, ipa_fail, _pad
       }
