@@ -355,7 +355,11 @@ struct ks_ctx {
   uint32_t sync_timeout_ms = 60000;
   // set by the worker thread's drains (sync_bounded), read by API threads
   std::atomic<bool> wedged{false};
-  hipStream_t diag_stream = nullptr;  // stall_report's read-back stream (created at ks_open)
+  // stall_report's read-back stream: created by the first report, not at
+  // ks_open.  A fourth stream alive beside main / side / resolve cost the
+  // round pipeline 37 % (C3, serial resolve: 640k -> 400k pods/s,
+  // profiles/r4/bench_r4q_*.json; the streams then share hardware queues)
+  hipStream_t diag_stream = nullptr;
   uint32_t flag_want[4] = {0, 0, 0, 0};
   uint32_t *h_diag = nullptr;  // pinned: flags read back by the stall report
   // ks_debug_stall: the next round holds back flag stall_flag's signal by stall_us
@@ -615,10 +619,13 @@ ks_status stall_report(ks_ctx *c, hipStream_t st, const char *what, double ms) {
   for (auto &p : ss)
     if (p.first && hipStreamQuery(p.first) == hipErrorNotReady) busy += std::string(busy.empty() ? "" : ", ") + p.second;
   // the flags through a stream of their own (the context's streams are
-  // stuck), created at ks_open so that the report creates and destroys
-  // nothing; best effort: on a hung device the copy may never finish, and
-  // the report then says so rather than waiting for it
+  // stuck), created here on the first report (never at ks_open, see
+  // diag_stream) and kept until ks_close, so a report destroys nothing; best
+  // effort: on a hung device the copy may never finish, and the report then
+  // says so rather than waiting for it
   std::string flags = "unreadable (the device did not answer the read-back within 2 s)";
+  if (!c->diag_stream && hipStreamCreateWithFlags(&c->diag_stream, hipStreamNonBlocking) != hipSuccess)
+    c->diag_stream = nullptr;
   hipStream_t d = c->diag_stream;
   if (c->d_flags && c->h_diag && d && hipStreamQuery(d) == hipSuccess) {
     if (hipMemcpyAsync(c->h_diag, c->d_flags, 16, hipMemcpyDeviceToHost, d) == hipSuccess) {
@@ -3239,7 +3246,6 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
       HIPC(x, hipStreamCreateWithPriority(&x->sstream, hipStreamNonBlocking, hi));
     }
     x->xm.st = x->stream;
-    HIPC(x, hipStreamCreateWithFlags(&x->diag_stream, hipStreamNonBlocking));
     {  // value_sync = 0: cross-stream hand-offs by event waits instead
       int can = 0;
       (void)hipDeviceGetAttribute(&can, hipDeviceAttributeCanUseStreamWaitValue, cfg->device);
