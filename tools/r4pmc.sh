@@ -1,7 +1,9 @@
-# PMC summaries of the non-headline bench configurations (tools/gpu.sh pmc per line)
+# PMC summaries of the non-headline bench configurations (tools/gpu.sh pmc per line);
+# the raw per-pass rocprof output is dropped after each summary (gpurun merges <= 64 MiB)
 set -e
-tools/gpu.sh pmc r4c4 --kind labeled
-tools/gpu.sh pmc r4c2 --nodes 100000 --batch 20000
-tools/gpu.sh pmc r4kw --kind kwok --topk 512
-tools/gpu.sh pmc r4kb --kind kwok --pods besteffort
-tools/gpu.sh pmc r4c5 --workload c5 --steps 2 --warmup 1
+run() { tag=$1; shift; tools/gpu.sh pmc $tag "$@"; rm -rf gpurun_out/pmc_$tag; }
+run r4c4 --kind labeled
+run r4c2 --nodes 100000 --batch 20000
+run r4kw --kind kwok --topk 512
+run r4kb --kind kwok --pods besteffort
+run r4c5 --workload c5 --steps 2 --warmup 1
