@@ -182,3 +182,28 @@ def test_parallel_vs_serial_fuzz(shards):
         want, wst, out = run_modes(na, n, pa, m, splits=r.randrange(1, 4), modes=("serial", "parallel"),
                                    pods_per_round=P, topk=r.choice([P, 8, 64]), virtual_shards=shards)
         check_modes(want, wst, out, f"fuzz seed {seed} shards {shards}")
+
+
+@pytest.mark.parametrize("mode", ["auto", "serial", "parallel"])
+def test_normaliser_max_drops_mid_round(mode):
+    # TaintToleration normalises by the max raw (untolerated PreferNoSchedule
+    # taints) over the FEASIBLE nodes.  The only nodes at the max (two taints)
+    # hold one pod each, and the round's first pods are steered onto them by
+    # a nodeSelector: once they are full the max over feasible nodes drops
+    # 2 -> 1 and every later pod's TaintToleration score changes on every
+    # node.  The round must stop there and the rest be swept again (label /
+    # taint rounds take the serial kernel in every mode).
+    from ksched.objects import Taint
+    p = lambda k: Taint(k, "true", "PreferNoSchedule")  # noqa: E731
+    nodes = ([node(f"max{i}", pods=1, labels={"special": "yes"}, taints=[p("s"), p("t")]) for i in range(2)] +
+             [node(f"one{i}", taints=[p("s")]) for i in range(30)] + [node(f"zero{i}") for i in range(30)])
+    pods = ([pod(f"steer{i}", cpu=500, mem=Gi, node_selector={"special": "yes"}) for i in range(2)] +
+            [pod(f"p{j}", cpu=250 * (1 + j % 4), mem=Gi) for j in range(120)])
+    a = Arena()
+    na, n = nodes_array(nodes, a)
+    pa, m = pods_array(pods, a)
+    want, wst, out = run_modes(na, n, pa, m, modes=(mode,), pods_per_round=256, topk=64)
+    check_modes(want, wst, out, f"normaliser drop [{mode}]")
+    assert sorted(want["node_index"][:2]) == [0, 1], "the steered pods did not fill the max nodes"
+    rounds = out[mode][2][0]
+    assert rounds >= 2, f"one round resolved all {m} pods: the normaliser drop did not stop it ({out[mode][2]})"
