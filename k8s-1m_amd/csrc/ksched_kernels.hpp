@@ -13,7 +13,7 @@ constexpr int MAX_K = 512;    // candidates per pod record (two list entries per
 constexpr uint32_t FIX_NONE = 0xFFFFFFFFu;  // fix_list tail
 // device counters of the parallel commit (ksched_resolve.hip): chunk passes,
 // rounds it resolved
-constexpr int CTR_PAR_PASSES = 12, CTR_PAR_ROUNDS = 13, CTR_PAR_BAILS = 14;
+constexpr int CTR_PAR_PASSES = 12, CTR_PAR_ROUNDS = 13, CTR_PAR_BAILS = 14, CTR_PAR_ONESTEP = 15;
 // per-pod round marks (ks_batch_marks, include/ksched.h): where the round
 // machinery changed course, for tests that place checks there
 constexpr uint8_t MARK_FIX = 1;          // re-swept with measured normaliser maxima (FIX sweep)

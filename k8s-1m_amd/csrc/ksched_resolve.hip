@@ -182,6 +182,12 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
   __shared__ uint32_t s_cdr[PCH];   // node was in M before the chunk
   // control: [0] f, [1] stopped, [2] cut, [4] distinct nodes, [5] |M|, [6] passes
   __shared__ uint32_t s_ctl[8];
+  // a round of identical request-less pods in one step (identical_round below)
+  __shared__ uint64_t s_ek[PR_THREADS];  // entries: node key after k of the round's pods
+  __shared__ uint32_t s_ex[PR_THREADS];  //   list index << 16 | k << 1 | Fit lost by taking it
+  __shared__ uint32_t s_tx[MAX_K];       // pods each listed node takes
+  __shared__ uint32_t s_ic[4];           // [0] entries, [1] not applicable, [2] modified nodes
+  __shared__ uint32_t s_wt[PR_NW];       // per-wave counts (prefix sums)
 
   // tid / lane are re-materialised at each pass (see the pass loop)
   uint32_t tid = threadIdx.x, lane = tid % WAVE;
@@ -309,7 +315,126 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
     kw2 = ld(wid + 2 * PR_NW);
     kw3 = ld(wid + 3 * PR_NW);
   };
-  load_windows(0, min((uint32_t)PCH, n));
+  // ---- a round whose pods are all one identical, request-less pod (kwok's
+  // busybox pods): Requested never changes, so BalancedAllocation is constant
+  // and LeastAllocated (non-zero defaults) only falls; node x's key after k of
+  // these pods, key_x(k), is non-increasing in k.  The sequential greedy then
+  // gives pod j the j-th largest entry of {key_x(k)} in (key desc, k asc)
+  // order (ties are within one node: the key carries the slot), and only
+  // entries at or above the n-th listed key can be among the first n (or,
+  // with a shorter list, above the bound: the round stops where they run
+  // out).  One step instead of a pass per one or two pods.
+  bool fast = false;
+  {
+    if (tid < 4) s_ic[tid] = 0;
+    __syncthreads();
+    const PQ q0 = s_q[0];
+    const ShardRecHdr &h0 = s_hdr[0];
+    if (tid < n && s_rep[tid] != s_rep[0]) s_ic[1] = 1;  // more than one pod class
+    if (tid == 0 && (n < 2 || a.rep == nullptr || q0.rc != 0.0 || q0.rm != 0.0 || h0.feasible == 0 ||
+                     (s_fl[0] & PF_PREF_ERR) || h0.nkeys == 0))
+      s_ic[1] = 1;
+    __syncthreads();
+    if (s_ic[1] == 0) {
+      const uint32_t nk = min(h0.nkeys, (uint32_t)MAX_K);
+      const uint64_t *keys0 = a.frec + (size_t)s_rep[0] * RW + REC_HDR_WORDS;
+      const uint64_t thr = nk >= n ? keys0[n - 1] : h0.bound + 1;
+      if (tid < nk) {
+        CandRow r = a.crow[(size_t)s_rep[0] * a.K + tid];
+        const uint32_t slot = key_slot(keys0[tid]);
+        uint64_t prev = ~0ull;
+        for (uint32_t k = 0; k < n; ++k) {
+          const uint64_t key = pq_key(q0, r, slot, a.w);
+          if (key > prev) {  // not non-increasing after all: the general passes
+            s_ic[1] = 1;
+            break;
+          }
+          if (key < thr) break;
+          prev = key;
+          pq_add(r, q0);
+          const bool lost = !pq_fit(q0, r, r.rc, r.rm, r.np);  // the next identical pod no longer fits
+          const uint32_t e = atomicAdd(&s_ic[0], 1u);
+          if (e < (uint32_t)PR_THREADS) {
+            s_ek[e] = key;
+            s_ex[e] = tid << 16 | k << 1 | (lost ? 1u : 0u);
+          }
+        }
+      }
+      if (tid < MAX_K) s_tx[tid] = 0;
+      __syncthreads();
+      const uint32_t ne = s_ic[0];
+      if (s_ic[1] == 0 && ne <= (uint32_t)PR_THREADS) {
+        // bitonic sort of the entries, padded to a power of two: key desc, then k asc
+        uint32_t p2 = 1;
+        while (p2 < ne) p2 <<= 1;
+        if (tid >= ne && tid < p2) {
+          s_ek[tid] = 0;
+          s_ex[tid] = 0xFFFFFFFFu;
+        }
+        __syncthreads();
+        auto before = [](uint64_t ka, uint32_t xa, uint64_t kb, uint32_t xb) {
+          return ka > kb || (ka == kb && xa < xb);
+        };
+        for (uint32_t size = 2; size <= p2; size <<= 1) {
+          for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+            const uint32_t i = tid, j = tid ^ stride;
+            if (j > i && j < p2) {
+              const uint64_t ki = s_ek[i], kj = s_ek[j];
+              const uint32_t xi = s_ex[i], xj = s_ex[j];
+              const bool up = (i & size) == 0;
+              if (up ? before(kj, xj, ki, xi) : before(ki, xi, kj, xj)) {
+                s_ek[i] = kj;
+                s_ek[j] = ki;
+                s_ex[i] = xj;
+                s_ex[j] = xi;
+              }
+            }
+            __syncthreads();
+          }
+        }
+        // pod j takes entry j; its feasible count = the round start's minus the
+        // nodes earlier pods filled (exclusive prefix sum of the lost flags)
+        const uint32_t nres = min(n, ne);
+        const bool in = tid < nres;
+        const uint32_t x = in ? s_ex[tid] : 0u;
+        const uint64_t bm = __ballot(in && (x & 1u));
+        if (lane == 0) s_wt[wid] = (uint32_t)__popcll(bm);
+        if (in) atomicAdd(&s_tx[x >> 16], 1u);
+        __syncthreads();
+        uint32_t dl = (uint32_t)__popcll(bm & lt_mask);
+        for (uint32_t w = 0; w < wid; ++w) dl += s_wt[w];
+        if (in) {
+          const uint64_t key = s_ek[tid];
+          const uint32_t feas = h0.feasible - dl;  // >= 1: pod tid has a feasible node, the entry's
+          s_resc[tid] = make_uint4((uint32_t)key, (uint32_t)(key >> 32), feas, 0u);
+          s_rdl[tid] = (int32_t)dl;
+        }
+        // the nodes taken: their rows after the round, for the carry / write-back
+        if (tid < nk && s_tx[tid] > 0) {
+          const uint32_t mi = atomicAdd(&s_ic[2], 1u);
+          const CandRow r0 = a.crow[(size_t)s_rep[0] * a.K + tid];
+          RNode &m = s_m[mi];
+          m.row = r0;
+          for (uint32_t k = 0; k < s_tx[tid]; ++k) pq_add(m.row, q0);
+          m.rc0 = r0.rc;
+          m.rm0 = r0.rm;
+          m.np0 = r0.np;
+          m.slot = key_slot(keys0[tid]);
+          m._pad[0] = m._pad[1] = 0;
+        }
+        __syncthreads();
+        if (tid == 0) {
+          s_ctl[0] = nres;
+          s_ctl[1] = nres < n ? 1u : 0u;  // the list ran out: the round stops there
+          s_ctl[5] = s_ic[2];
+          s_ctl[6] = 1;
+        }
+        fast = true;
+      }
+    }
+    __syncthreads();
+  }
+  if (!fast) load_windows(0, min((uint32_t)PCH, n));
 
   // Under RESOLVE_AUTO a round that runs past par_max_passes passes, or whose
   // pace after PAR_RATE_PASSES passes projects more than that many for its n
@@ -806,6 +931,7 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
     a.counters[1] += nres;  // pods resolved
     a.counters[CTR_PAR_PASSES] += s_ctl[6];
     a.counters[CTR_PAR_ROUNDS] += 1;
+    if (fast) a.counters[CTR_PAR_ONESTEP] += 1;
     if (a.rmode != nullptr) {
       a.rmode[1] = a.seq;  // resolve_kernel, launched after this one, skips the round
       if (bailed) {

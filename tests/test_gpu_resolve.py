@@ -129,8 +129,8 @@ def test_balanced_allocation_rise(seed, n, m, P, K, splits):
     assert par_rounds > 0, "the parallel kernel resolved no round"
 
 
-@pytest.mark.parametrize("kind,pods,K", [("kwok", "besteffort", 256), ("kwok", "c1", 512), ("kwok", "c1", 16),
-                                         ("hetero", "c1", 256), ("hetero", "besteffort", 32)])
+@pytest.mark.parametrize("kind,pods,K", [("kwok", "besteffort", 256), ("kwok", "besteffort", 16), ("kwok", "c1", 512),
+                                         ("kwok", "c1", 16), ("hetero", "c1", 256), ("hetero", "besteffort", 32)])
 def test_synthetic_streams(kind, pods, K):
     n, m = 3000, 5000
     k = {"kwok": synth.KWOK, "hetero": synth.HETERO}[kind]
@@ -141,8 +141,11 @@ def test_synthetic_streams(kind, pods, K):
     want, wst, out = run_modes(ns.nodes, n, ps.pods, m, pre=pre, splits=2, topk=K,
                                modes=("auto", "serial", "parallel", "auto_cap"))
     check_modes(want, wst, out, f"{kind}/{pods}/K={K}")
-    # counters: [0] rounds, [12] parallel passes, [13] rounds the parallel kernel resolved
+    # counters: [0] rounds, [12] parallel passes, [13] rounds the parallel
+    # kernel resolved, [15] of those in one step (one class of request-less pods)
     par, cap = out["parallel"][2], out["auto_cap"][2]
+    if pods == "besteffort":
+        assert par[15] > 0, f"no round of identical request-less pods resolved in one step: {par}"
     assert par[13] == par[0], f"RESOLVE_PARALLEL left rounds to the serial kernel: {par}"
     if par[12] > 2 * par[0]:
         # some round needed more than 2 passes: the capped AUTO handed later rounds to the serial kernel
@@ -207,3 +210,21 @@ def test_normaliser_max_drops_mid_round(mode):
     assert sorted(want["node_index"][:2]) == [0, 1], "the steered pods did not fill the max nodes"
     rounds = out[mode][2][0]
     assert rounds >= 2, f"one round resolved all {m} pods: the normaliser drop did not stop it ({out[mode][2]})"
+
+
+@pytest.mark.parametrize("K", [256, 8])
+def test_identical_requestless_pods_fill_nodes(K):
+    # one class of request-less pods (the one-step path): nodes hold 1-3 pods,
+    # so nodes fill up inside a round (Fit losses change every later pod's
+    # feasible count); with K = 8 the list runs out and rounds stop early
+    r = random.Random(11)
+    nodes = [node(f"n{i}", cpu=r.choice([4, 8, 16]) * 1000, mem=r.choice([8, 16]) * Gi, pods=r.choice([1, 2, 3]))
+             for i in range(400)]
+    pods = [pod(f"b{j}") for j in range(1000)]
+    a = Arena()
+    na, n = nodes_array(nodes, a)
+    pa, m = pods_array(pods, a)
+    want, wst, out = run_modes(na, n, pa, m, splits=2, modes=("auto", "serial"), topk=K)
+    check_modes(want, wst, out, f"identical request-less pods K={K}")
+    assert out["auto"][2][15] > 0, "the one-step path never ran"
+    assert (want["status"] == 1).any(), "the cluster never filled up"
