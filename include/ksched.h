@@ -588,7 +588,8 @@ ks_status ks_reset_stats(ks_ctx *ctx);
  * normalising maxima were wrong, [5] label-dictionary reclaims, [6] taint
  * dictionary rebuilds, [7] identical pods not swept, [12] passes of the
  * parallel commit, [13] rounds it resolved, [14] of those it cut short and
- * handed over to the serial kernel (AUTO).  (The instrumented stamps builds,
+ * handed over to the serial kernel (AUTO), [15] of those resolved in one step
+ * (one class of identical request-less pods).  (The instrumented stamps builds,
  * k8s-1m_amd/csrc/ksched_instr.hpp, put phase cycle sums in [8..15].) */
 ks_status ks_debug_counters(ks_ctx *ctx, uint64_t out[16]);
 /* Diagnostics of the parallel commit (resource-only rounds): with the profile
