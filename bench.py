@@ -652,11 +652,12 @@ def roofline(args, st, world):
     r["compulsory_bytes_per_launch"] = int(b_node * local_nodes)
     r["compulsory_hbm_frac"] = round(b_node * local_nodes / launch_s / 1e9 / HBM_PEAK_GBS, 4) if launch_s else None
     # which kernel sets the round time: the sweep (priced above) or the one-workgroup
-    # in-order resolve, a latency chain with no throughput roofline
+    # in-order commit (parallel proposal / verify with the serial fallback, DESIGN
+    # §5.1 / §5.6), a latency chain with no throughput roofline
     resolve_avg_ms = st.resolve_ms / max(1, st.resolve_launches)
     if st.sweep_launches and st.resolve_launches:
         r["critical_path"] = "sweep" if sweep_avg_ms >= resolve_avg_ms else \
-            "resolve (serial in-order commit; the sweep fraction above is for the overlapped sweep)"
+            "resolve (one-workgroup in-order commit, a latency chain; the sweep fraction above is for the overlapped sweep)"
         r["resolve_avg_launch_ms"] = round(resolve_avg_ms, 4)
     return r
 
