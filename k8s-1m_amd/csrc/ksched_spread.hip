@@ -1084,13 +1084,9 @@ __global__ void scatter_i64_kernel(int64_t *col, const uint64_t *idx, const int6
 // ------------------------------------------------------------- launchers
 
 hipError_t launch_spread_pod(const SpreadArgs &args, uint32_t passes, hipStream_t st) {
-  // KS_SPREAD_BLOCKS (diagnostic): the node passes' block cap
-  static const uint32_t cap = [] {
-    const char *e = getenv("KS_SPREAD_BLOCKS");
-    const long v = e ? atol(e) : 0;
-    return v > 0 && v <= 4096 ? (uint32_t)v : (uint32_t)SPREAD_MAX_BLOCKS;
-  }();
-  const uint32_t blocks = std::max<uint32_t>(1, std::min<uint32_t>((args.npos + SP_THREADS - 1) / SP_THREADS, cap));
+  // node passes: at most SPREAD_MAX_BLOCKS blocks (248 measured no better)
+  const uint32_t blocks =
+      std::max<uint32_t>(1, std::min<uint32_t>((args.npos + SP_THREADS - 1) / SP_THREADS, (uint32_t)SPREAD_MAX_BLOCKS));
   const SpreadArgs &a = args;
   if (passes & SPL_PREP) spread_prep_kernel<<<blocks, SP_THREADS, 0, st>>>(a);
   if (passes & SPL_MIN) spread_min_kernel<<<blocks, SP_THREADS, 0, st>>>(a);
