@@ -315,15 +315,19 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
     kw2 = ld(wid + 2 * PR_NW);
     kw3 = ld(wid + 3 * PR_NW);
   };
-  // ---- a round whose pods are all one identical, request-less pod (kwok's
-  // busybox pods): Requested never changes, so BalancedAllocation is constant
-  // and LeastAllocated (non-zero defaults) only falls; node x's key after k of
-  // these pods, key_x(k), is non-increasing in k.  The sequential greedy then
-  // gives pod j the j-th largest entry of {key_x(k)} in (key desc, k asc)
-  // order (ties are within one node: the key carries the slot), and only
-  // entries at or above the n-th listed key can be among the first n (or,
-  // with a shorter list, above the bound: the round stops where they run
-  // out).  One step instead of a pass per one or two pods.
+  // ---- a round whose pods are all one identical pod (kwok's busybox pods, a
+  // deployment's replicas): when node x's key after k of these pods,
+  // key_x(k), is non-increasing in k for every listed node, the sequential
+  // greedy gives pod j the j-th largest entry of {key_x(k)} in (key desc,
+  // k asc) order (ties are within one node: the key carries the slot), and
+  // only entries at or above the n-th listed key can be among the first n
+  // (or, with a shorter list, above the bound: the round stops where they
+  // run out).  Request-less pods never change Requested, so
+  // BalancedAllocation is constant and LeastAllocated only falls: always
+  // non-increasing.  With requests BalancedAllocation can rise, so every
+  // node's sequence is checked to its end (no fit, or n pods) and any rise
+  // sends the round to the passes.  One step instead of a pass per one or
+  // two pods.
   bool fast = false;
   {
     if (tid < 4) s_ic[tid] = 0;
@@ -331,9 +335,9 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
     const PQ q0 = s_q[0];
     const ShardRecHdr &h0 = s_hdr[0];
     if (tid < n && s_rep[tid] != s_rep[0]) s_ic[1] = 1;  // more than one pod class
-    if (tid == 0 && (n < 2 || a.rep == nullptr || q0.rc != 0.0 || q0.rm != 0.0 || h0.feasible == 0 ||
-                     (s_fl[0] & PF_PREF_ERR) || h0.nkeys == 0))
+    if (tid == 0 && (n < 2 || a.rep == nullptr || h0.feasible == 0 || (s_fl[0] & PF_PREF_ERR) || h0.nkeys == 0))
       s_ic[1] = 1;
+    const bool check_all = q0.rc != 0.0 || q0.rm != 0.0;  // requests: BalancedAllocation moves
     __syncthreads();
     if (s_ic[1] == 0) {
       const uint32_t nk = min(h0.nkeys, (uint32_t)MAX_K);
@@ -345,13 +349,14 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
         uint64_t prev = ~0ull;
         for (uint32_t k = 0; k < n; ++k) {
           const uint64_t key = pq_key(q0, r, slot, a.w);
-          if (key > prev) {  // not non-increasing after all: the general passes
+          if (key > prev) {  // not non-increasing: the general passes
             s_ic[1] = 1;
             break;
           }
-          if (key < thr) break;
+          if (key == 0 || (key < thr && !check_all)) break;
           prev = key;
           pq_add(r, q0);
+          if (key < thr) continue;  // checked for monotonicity only
           const bool lost = !pq_fit(q0, r, r.rc, r.rm, r.np);  // the next identical pod no longer fits
           const uint32_t e = atomicAdd(&s_ic[0], 1u);
           if (e < (uint32_t)PR_THREADS) {

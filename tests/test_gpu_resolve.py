@@ -228,3 +228,34 @@ def test_identical_requestless_pods_fill_nodes(K):
     check_modes(want, wst, out, f"identical request-less pods K={K}")
     assert out["auto"][2][15] > 0, "the one-step path never ran"
     assert (want["status"] == 1).any(), "the cluster never filled up"
+
+
+@pytest.mark.parametrize("shape", ["balanced", "ba_rise"])
+def test_identical_pods_with_requests(shape):
+    # one class of pods WITH requests (a deployment's replicas): the one-step
+    # path applies only when every listed node's key sequence is
+    # non-increasing.  "balanced": pods in the nodes' cpu:memory ratio on
+    # empty nodes keep BalancedAllocation at 100, so it must apply;
+    # "ba_rise": memory-heavy pods on nodes whose CPU is half used raise
+    # BalancedAllocation, so those rounds fall back to the passes.  Both
+    # bit-exact against the oracle.
+    r = random.Random(23)
+    if shape == "balanced":
+        nodes = [node(f"n{i}", cpu=16000 * k, mem=64 * Gi * k, pods=110) for i, k in
+                 enumerate(r.choice([1, 2, 4]) for _ in range(600))]
+        pre = None
+        pods = [pod(f"d{j}", cpu=500, mem=2 * Gi) for j in range(1500)]
+    else:
+        nodes, prepods, pre_slots, _ = ba_rise_cluster(600, 0, 23)
+        pods = [pod(f"d{j}", cpu=100, mem=4 * Gi) for j in range(1500)]
+    a = Arena()
+    na, n = nodes_array(nodes, a)
+    pa, m = pods_array(pods, a)
+    if shape == "ba_rise":
+        fa, nf = pods_array(prepods, a)
+        pre = (fa, (C.c_uint32 * nf)(*pre_slots), nf)
+    want, wst, out = run_modes(na, n, pa, m, pre=pre, splits=2, modes=("auto", "serial", "parallel"))
+    check_modes(want, wst, out, f"identical pods with requests ({shape})")
+    onestep = out["parallel"][2][15]
+    if shape == "balanced":
+        assert onestep > 0, f"the one-step path never ran: {out['parallel'][2]}"
