@@ -1,4 +1,5 @@
-# PMC summaries of every bench configuration (tools/gpu.sh pmc per line); the raw
+# PMC summaries of every bench configuration (tools/gpu.sh pmc per line; run through gpurun
+# from the repo root: `bash tools/pmc_all.sh`); the raw
 # per-pass rocprof output is dropped after each summary (gpurun merges <= 64 MiB)
 set -e
 run() { tag=$1; shift; tools/gpu.sh pmc $tag "$@"; rm -rf gpurun_out/pmc_$tag; }
