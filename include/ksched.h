@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define KSCHED_ABI_VERSION 4
+#define KSCHED_ABI_VERSION 5
 
 /* ---------------------------------------------------------------- status */
 typedef int32_t ks_status;
@@ -418,6 +418,10 @@ typedef struct {
                                      0: by events (profilers that serialise dispatches)              */
   uint32_t sync_timeout_ms;       /* bound on every host wait for device work (60000), see
                                      ks_set_sync_timeout                                            */
+  uint32_t spread_replica_runs;   /* 1 (default): runs of >= 4 identical one-pod-path pods whose
+                                     constraints are all ScheduleAnyway (deployment replicas under the
+                                     system defaults) are scheduled by one filter pass and one
+                                     workgroup per run; 0: the per-pod chain       */
 } ks_config;
 
 enum { KS_RESOLVE_AUTO = 0, KS_RESOLVE_SERIAL = 1, KS_RESOLVE_PARALLEL = 2 };
@@ -580,6 +584,9 @@ typedef struct {
   double spread_ms;         /* Σ device time of timed spread-path pods (whole kernel chain) */
   uint64_t spread_pods_timed;
   uint64_t spread_pods;     /* pods scheduled by the spread path           */
+  uint64_t replica_runs;    /* replica runs of the spread path (spread_replica_runs) */
+  uint64_t replica_pods;    /* pods they scheduled (counted in spread_pods too)      */
+  double replica_ms;        /* Σ device time of timed replica runs (in spread_ms too) */
 } ks_stats;
 ks_status ks_get_stats(ks_ctx *ctx, ks_stats *out);
 ks_status ks_reset_stats(ks_ctx *ctx);

@@ -277,6 +277,9 @@ struct ks_batch {
   std::vector<uint32_t> set_ids;
   std::vector<uint8_t> spread;
   bool any_spread = false;
+  // replica runs: 1 the run kernel models the pod's program,
+  // 2 the pod is identical to the one before it (program, labels)
+  std::vector<uint8_t> rep;
   std::vector<uint32_t> class_refs;
   std::vector<uint32_t> term_refs;  // term classes of the batch's pods' own terms (one per pod and term)
   uint64_t *d_cmask = nullptr, *h_cmask = nullptr;
@@ -508,6 +511,14 @@ struct ks_ctx {
   int8_t *d_sst = nullptr;
   int64_t *d_sraw = nullptr;
   uint64_t *d_spart = nullptr;
+  // replica runs: sort keys and positions, group starts, control
+  // words (ReplicaArgs::ctl; pinned copy), radix-sort scratch
+  bool replica_runs = true;
+  uint64_t *d_rk_keys = nullptr, *d_rk_sorted = nullptr;
+  uint32_t *d_rk_pos = nullptr, *d_rk_spos = nullptr, *d_rk_gstart = nullptr, *d_rk_ctl = nullptr;
+  uint8_t *d_rk_tmp = nullptr;
+  size_t rk_tmp_bytes = 0;
+  uint32_t *h_rk_ctl = nullptr;
   uint32_t *h_seg = nullptr;       // pinned: start pod of a round-kernel segment
   // comm: RCCL, or an in-process group of contexts (tests of the multi-rank path on one GPU)
   ncclComm_t comm = nullptr;
@@ -519,6 +530,11 @@ struct ks_ctx {
   ks_stats stats{};
   bool timing = false;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_sweep, ev_resolve, ev_spread;
+  struct RunEv {
+    hipEvent_t e0, e1;
+    uint32_t pods;  // pods the replica run scheduled
+  };
+  std::vector<RunEv> ev_runs;
   std::vector<hipEvent_t> ev_pool;
   uint64_t counters_base[4] = {0, 0, 0, 0};  // device counters at the last ks_reset_stats
   uint64_t sweeps_issued = 0;                // main sweep launches since then (timed or not)
@@ -2220,6 +2236,51 @@ uint32_t solo_passes(const SoloHdr *hd) {
   return f;
 }
 
+// Replica runs: the run kernel models a one-pod program whose
+// constraints are all ScheduleAnyway, with at most one kubernetes.io/hostname
+// and one other key, and no InterPodAffinity, extended-resource or image
+// records.  The inclusion policies need no check: PreScore's per-node
+// nodeAffinityPolicy / nodeTaintsPolicy tests pass on every node a pod can be
+// committed to (a feasible node matches the pod's required affinity and
+// tolerates its hard taints).
+bool replica_program(const PodDev &p, const SoloHdr *hd) {
+  if (hd->n_spread == 0 || hd->n_aff || hd->n_xres || hd->n_img || (p.flags & PF_PREF_ERR)) return false;
+  const SpreadDev *sd = reinterpret_cast<const SpreadDev *>(hd + 1);
+  uint32_t host = 0, other = 0;
+  for (uint32_t k = 0; k < hd->n_spread; ++k) {
+    if (!(sd[k].flags & SP_SCORE)) return false;
+    ++((sd[k].flags & SP_HOST) ? host : other);
+  }
+  return host <= 1 && other <= 1;
+}
+
+// Words of a label program of `terms` terms at `off` (ksched_dev.hpp layout).
+size_t program_words(const uint64_t *w, uint32_t off, uint32_t terms) {
+  size_t n = 0;
+  for (uint32_t k = 0; k < terms; ++k) n += term_words(w[off + n]);
+  return n;
+}
+
+// Two compiled pods the kernels cannot tell apart: equal descriptors up to
+// the program offsets, equal programs (required / preferred / prefilter /
+// one-pod records).  Their labels (class masks) are compared by the caller.
+bool same_pod_program(const PodDev &a, const PodDev &b, const uint64_t *w) {
+  PodDev x = a, y = b;
+  x.req_off = y.req_off = x.pref_off = y.pref_off = x.solo_off = y.solo_off = x.pre_off = y.pre_off = 0;
+  if (std::memcmp(&x, &y, sizeof x) != 0) return false;
+  auto same = [&](uint32_t oa, uint32_t ob, size_t n) { return std::memcmp(w + oa, w + ob, n * 8) == 0; };
+  if (!same(a.req_off, b.req_off, program_words(w, a.req_off, a.req_len))) return false;
+  if (!same(a.pref_off, b.pref_off, program_words(w, a.pref_off, a.pref_len))) return false;
+  if (!same(a.pre_off, b.pre_off, a.pre_len)) return false;
+  if (a.flags & PF_SOLO) {
+    const SoloHdr *h = reinterpret_cast<const SoloHdr *>(w + a.solo_off);
+    const size_t bytes = sizeof(SoloHdr) + h->n_spread * sizeof(SpreadDev) + h->n_xres * sizeof(XResDev) +
+                         h->n_img * sizeof(ImageDev) + h->n_aff * sizeof(AffDev);
+    if (!same(a.solo_off, b.solo_off, bytes / 8)) return false;
+  }
+  return true;
+}
+
 // The one-pod-path program of a pod (ksched_dev.hpp SoloHdr): its spread
 // constraints (SpreadDev), extended-resource requests (XResDev) and the
 // ImageLocality terms of its images present on some node (ImageDev).  Pods
@@ -2506,9 +2567,19 @@ ks_status collect_timing(ks_ctx *c) {
     c->ev_pool.push_back(pr.first);
     c->ev_pool.push_back(pr.second);
   }
+  for (auto &r : c->ev_runs) {
+    float ms = 0;
+    HIPC(c, hipEventElapsedTime(&ms, r.e0, r.e1));
+    c->stats.spread_ms += ms;
+    c->stats.spread_pods_timed += r.pods;
+    c->stats.replica_ms += ms;
+    c->ev_pool.push_back(r.e0);
+    c->ev_pool.push_back(r.e1);
+  }
   c->ev_sweep.clear();
   c->ev_resolve.clear();
   c->ev_spread.clear();
+  c->ev_runs.clear();
   return KS_OK;
 }
 
@@ -2908,6 +2979,67 @@ ks_status upload_batch(ks_ctx *c, ks_batch *b) {
   return KS_OK;
 }
 
+// Replica runs: what the run kernel's key layout holds -- slots
+// below 2^RK_SLOT_BITS, domain ids of the other key below RK_DZ_NONE -- on a
+// single-rank context (the one-pod path's condition).
+bool replica_fits(const ks_ctx *c, const ks_batch *b, const SpreadArgs &sa, uint32_t i) {
+  if (c->has_comm() || c->cap > (1u << RK_SLOT_BITS)) return false;
+  const SoloHdr *hd = reinterpret_cast<const SoloHdr *>(b->h_clauses + b->h_pods[i].solo_off);
+  const SpreadDev *sd = reinterpret_cast<const SpreadDev *>(hd + 1);
+  for (uint32_t k = 0; k < hd->n_spread; ++k)
+    if (!(sd[k].flags & SP_HOST) && sa.ndom[sd[k].key] > RK_DZ_NONE) return false;
+  return true;
+}
+
+// One replica run over pods [lo, hi) of the batch: one filter pass, the sort,
+// the run kernel; waits for it and returns the first pod it did not schedule
+// (lo: refused) and why it stopped (RunStop).
+ks_status replica_run(ks_ctx *c, ks_batch *b, SpreadArgs sa, uint32_t lo, uint32_t hi, uint32_t *next,
+                      uint32_t *stop) {
+  (void)b;
+  if (!c->d_rk_keys) {
+    size_t bytes = 0;
+    HIPC(c, launch_sort_pairs(nullptr, nullptr, nullptr, nullptr, c->npos, nullptr, &bytes, c->stream));
+    ks_status st;
+    if ((st = dalloc(c, &c->d_rk_keys, c->npos)) || (st = dalloc(c, &c->d_rk_sorted, c->npos)) ||
+        (st = dalloc(c, &c->d_rk_pos, c->npos)) || (st = dalloc(c, &c->d_rk_spos, c->npos)) ||
+        (st = dalloc(c, &c->d_rk_gstart, RUN_GROUPS)) || (st = dalloc(c, &c->d_rk_ctl, 4)) ||
+        (st = dalloc(c, &c->d_rk_tmp, std::max<size_t>(bytes, 16))))
+      return st;
+    c->rk_tmp_bytes = bytes;
+    HIPC(c, hipHostMalloc((void **)&c->h_rk_ctl, 16, hipHostMallocDefault));
+  }
+  ReplicaArgs r{c->d_rk_keys, c->d_rk_sorted, c->d_rk_pos, c->d_rk_spos, c->d_rk_gstart, c->d_rk_ctl, hi};
+  sa.pod = lo;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (c->timing) {
+    e0 = get_event(c);
+    e1 = get_event(c);
+    HIPC(c, hipEventRecord(e0, c->stream));
+  }
+  HIPC(c, launch_replica_run(sa, r, c->d_rk_tmp, c->rk_tmp_bytes, c->stream));
+  if (c->timing) HIPC(c, hipEventRecord(e1, c->stream));
+  HIPC(c, hipMemcpyAsync(c->h_rk_ctl, c->d_rk_ctl, 16, hipMemcpyDeviceToHost, c->stream));
+  if (ks_status st = sync_bounded(c, c->stream, "a replica run")) return st;
+  *next = c->h_rk_ctl[2];
+  *stop = c->h_rk_ctl[3];
+  if (*next < lo || *next > hi || (*next == lo) != (*stop == RUN_REFUSED))
+    return c->fail(KS_ERR_DEVICE, "replica run over pods [%u, %u) ended at %u (stop %u)", lo, hi, *next, *stop);
+  const uint32_t done = *next - lo;
+  c->stats.spread_pods += done;
+  c->stats.replica_pods += done;
+  c->stats.replica_runs += done ? 1 : 0;
+  if (c->timing) {
+    if (done) {
+      c->ev_runs.push_back({e0, e1, done});
+    } else {
+      c->ev_pool.push_back(e0);
+      c->ev_pool.push_back(e1);
+    }
+  }
+  return KS_OK;
+}
+
 // Run a prepared batch to completion on the scheduler streams; the results
 // land in the batch's pinned host buffer.
 ks_status run_batch(ks_ctx *c, ks_batch *b) {
@@ -2995,8 +3127,9 @@ ks_status run_batch(ks_ctx *c, ks_batch *b) {
       sa.w_pts = c->cfg.weight_topology_spread;
       sa.w_ipa = c->cfg.weight_inter_pod_affinity;
       sa.evaluated = c->n_present;
-      for (; hi < b->n && b->spread[hi]; ++hi) {
-        sa.pod = hi;
+      // one pod through the per-pod chain
+      auto chain = [&](uint32_t i) -> ks_status {
+        sa.pod = i;
         // timing events on every KS_TIMING_EVERY-th spread pod
         const bool tm = c->timing && ++c->spread_seq % c->timing_every == 0;
         hipEvent_t e0 = nullptr, e1 = nullptr;
@@ -3005,12 +3138,31 @@ ks_status run_batch(ks_ctx *c, ks_batch *b) {
           e1 = get_event(c);
           HIPC(c, hipEventRecord(e0, c->stream));
         }
-        HIPC(c, launch_spread_pod(sa, b->spread[hi] & 0x7Fu, c->stream));
+        HIPC(c, launch_spread_pod(sa, b->spread[i] & 0x7Fu, c->stream));
         if (tm) {
           HIPC(c, hipEventRecord(e1, c->stream));
           c->ev_spread.emplace_back(e0, e1);
         }
         c->stats.spread_pods++;
+        return KS_OK;
+      };
+      uint32_t chain_until = lo;  // pods before it take the chain (runs there stopped short)
+      while (hi < b->n && b->spread[hi]) {
+        // replica run: pod hi and the identical pods after it
+        uint32_t e = hi + 1;
+        if (c->replica_runs && b->rep[hi] && hi >= chain_until)
+          while (e < b->n && (b->rep[e] & 2)) ++e;
+        if (e - hi >= RUN_MIN_PODS && replica_fits(c, b, sa, hi)) {
+          uint32_t next = hi, stop = RUN_END;
+          if (ks_status st = replica_run(c, b, sa, hi, e, &next, &stop)) return st;
+          // refused (more groups than a run holds), or stopped short by a Fit
+          // loss: the rest of these identical pods take the chain
+          if (next == hi || (stop == RUN_FIT && next - hi < RUN_MIN_PODS)) chain_until = e;
+          hi = next;
+          continue;
+        }
+        if (ks_status st = chain(hi)) return st;
+        ++hi;
       }
       HIPC(c, hipMemcpyAsync(b->h_results + lo, b->d_results + lo, (size_t)(hi - lo) * sizeof(DevResult),
                              hipMemcpyDeviceToHost, c->stream));
@@ -3154,6 +3306,7 @@ void ks_config_default(ks_config *cfg) {
   cfg->side_cus = 0;
   cfg->value_sync = 1;
   cfg->sync_timeout_ms = 60000;
+  cfg->spread_replica_runs = 1;
 }
 
 int32_t ks_abi_version(void) { return KSCHED_ABI_VERSION; }
@@ -3207,6 +3360,7 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
     x->sweep_blocks = cfg->sweep_pairs;
     x->sweep_blocks_ext = cfg->sweep_pairs_ext;
     x->sync_timeout_ms = cfg->sync_timeout_ms;
+    x->replica_runs = cfg->spread_replica_runs != 0;
     // diagnostics only (stderr reports, timing sample rate): they change no
     // scheduling decision
     auto env_u = [](const char *name, int dflt) {
@@ -3368,11 +3522,13 @@ void ks_close(ks_ctx *c) {
                   c->d_start, c->d_norm, c->d_norm_inv, c->d_pstat, c->d_fix, c->d_brec, c->d_srec, c->d_frec,
                   c->d_counters, c->d_crow, c->d_cext, c->d_pipe, c->d_carry, c->d_flags, c->d_dom, c->d_dedup,
                   c->d_pos_slot, c->d_dcnt, c->d_dflag, c->d_acc, c->d_sst, c->d_sraw, c->d_spart,
-                  c->d_xalloc, c->d_tcnt, c->d_adcnt, c->d_sraw2};
+                  c->d_xalloc, c->d_tcnt, c->d_adcnt, c->d_sraw2, c->d_rk_keys, c->d_rk_sorted, c->d_rk_pos,
+                  c->d_rk_spos, c->d_rk_gstart, c->d_rk_ctl, c->d_rk_tmp};
   for (void *b : bufs)
     if (b) (void)hipFree(b);
   if (c->h_start) (void)hipHostFree(c->h_start);
   if (c->h_seg) (void)hipHostFree(c->h_seg);
+  if (c->h_rk_ctl) (void)hipHostFree(c->h_rk_ctl);
   if (c->h_diag) (void)hipHostFree(c->h_diag);
   if (c->xm.pin) (void)hipHostFree(c->xm.pin);
   if (c->xm.dscr) (void)hipFree(c->xm.dscr);
@@ -3390,6 +3546,7 @@ void ks_close(ks_ctx *c) {
   for (auto &pr : c->ev_sweep) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
   for (auto &pr : c->ev_resolve) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
   for (auto &pr : c->ev_spread) { (void)hipEventDestroy(pr.first); (void)hipEventDestroy(pr.second); }
+  for (auto &r : c->ev_runs) { (void)hipEventDestroy(r.e0); (void)hipEventDestroy(r.e1); }
   for (auto e : c->ev_pool) (void)hipEventDestroy(e);
   for (int q = 0; q < 2; ++q) {
     if (c->ev_sw[q]) (void)hipEventDestroy(c->ev_sw[q]);
@@ -4037,11 +4194,17 @@ ks_status ks_batch_prepare(ks_ctx *c, const ks_pod *pods, uint32_t n, ks_batch *
   b->term_refs = std::move(term_refs);
   b->spread.assign(n, 0);
   b->any_spread = false;
+  b->rep.assign(n, 0);
   for (uint32_t i = 0; i < n; ++i) {
     if (!(dev[i].flags & PF_SOLO)) continue;
     const SoloHdr *hd = reinterpret_cast<const SoloHdr *>(cl.w.data() + dev[i].solo_off);
     b->spread[i] = (uint8_t)(0x80u | solo_passes(hd));
     b->any_spread = true;
+    if (!replica_program(dev[i], hd)) continue;
+    b->rep[i] = 1;
+    if (i > 0 && b->rep[i - 1] && b->set_ids[i] == b->set_ids[i - 1] &&
+        same_pod_program(dev[i - 1], dev[i], cl.w.data()))
+      b->rep[i] |= 2;
   }
   std::memcpy(b->h_pods, dev.data(), dev.size() * sizeof(PodDev));
   b->dups = pod_classes(dev.data(), n, b->h_cls);

@@ -1043,6 +1043,387 @@ __global__ void spread_commit_kernel(SpreadArgs a) {
   }
 }
 
+// ----------------------------------------------------------- replica runs
+//  Consecutive identical pods whose constraints are all
+// ScheduleAnyway -- deployment replicas under the system default constraints
+// (podtopologyspread systemDefaultConstraints: hostname maxSkew 3, zone
+// maxSkew 5) -- see one Filter result until a commit makes a node infeasible,
+// and with it the same normaliser maxima and Score domain sizes.  A feasible
+// node's TotalScore is then S + w x NormalizeScore(raw): S (LeastAllocated,
+// BalancedAllocation, normalised TaintToleration / NodeAffinity) changes only
+// when a pod of the run takes the node, and raw depends on the node only
+// through its group (its domain of the other key, its own hostname count).
+// One filter pass, the sort keys, a radix sort by (group, S descending, slot
+// ascending) and the group starts; then one workgroup walks the pods.  Each
+// pod's candidates are every group's first untaken node (the group's best:
+// same raw, highest S, lowest slot) and every node the run has taken,
+// re-scored after each commit; min / max raw over the non-ignored ones, the
+// packed-key argmax as spread_select, AssumePod as spread_commit.  The run
+// ends before a pod whose Filter result would differ (a taken node no longer
+// fits) and after RUN_TOUCHED taken nodes; the host starts the next run there.
+
+struct RunCons {
+  uint32_t cz, ch;  // constraint of the other key, of kubernetes.io/hostname (MAX_SPREAD: none)
+};
+__device__ __forceinline__ RunCons run_cons(const SpreadDev *sd, uint32_t n) {
+  RunCons k{(uint32_t)MAX_SPREAD, (uint32_t)MAX_SPREAD};
+  for (uint32_t c = 0; c < n; ++c) {
+    if (sd[c].flags & SP_HOST) k.ch = c;
+    else k.cz = c;
+  }
+  return k;
+}
+
+// spread_select's TotalScore of a feasible node without its PodTopologySpread
+// term (same terms, same integer arithmetic)
+__device__ __forceinline__ uint32_t run_static(const PodDev &p, const Weights &w, uint64_t pk, int64_t tt_max,
+                                               int64_t na_max) {
+  int64_t total = (int64_t)(uint32_t)pk;
+  int64_t tt = 100;
+  if (p.flags & PF_TT) tt = normalize((int64_t)((pk >> 32) & 0xFF), tt_max, true);
+  total += (int64_t)w.tt * tt;
+  if (p.flags & PF_HAS_PREF) {
+    int64_t na = 0;
+    if (p.flags & PF_NA) na = normalize((int64_t)(pk >> 40), na_max, false);
+    total += (int64_t)w.na * na;
+  }
+  return (uint32_t)total;
+}
+
+// Sort key of every position (~0: not feasible) after the run's filter pass.
+__global__ __launch_bounds__(SP_THREADS) void replica_keys_kernel(SpreadArgs a, ReplicaArgs r) {
+  __shared__ SpreadDev s_sd[MAX_SPREAD];
+  __shared__ uint32_t s_max[2];
+  const PodDev p = a.pods[a.pod];
+  const uint32_t n = spread_count(a, p);
+  if (threadIdx.x < n) s_sd[threadIdx.x] = spread_recs(a, p)[threadIdx.x];
+  if (threadIdx.x == 0) {
+    const Totals t = acc_totals(a.acc);
+    s_max[0] = t.tt_max;
+    s_max[1] = t.na_max;
+  }
+  __syncthreads();
+  const RunCons k = run_cons(s_sd, n);
+  const int64_t tt_max = s_max[0], na_max = s_max[1];
+  bool ovf = false;
+  for (uint32_t pos = blockIdx.x * SP_THREADS + threadIdx.x; pos < a.npos; pos += grid_threads()) {
+    const int8_t s = a.st[pos];
+    const uint32_t slot = a.pos_slot[pos];
+    uint64_t key = ~0ull;
+    if ((s == SST_FEASIBLE || s == SST_IGNORED) && slot != SLOT_NONE) {
+      const uint32_t S = run_static(p, a.w, a.part[pos], tt_max, na_max);
+      uint32_t code = RK_IGN;
+      if (s == SST_FEASIBLE) {
+        uint32_t dz = 0, hk = 0;
+        if (k.cz < (uint32_t)MAX_SPREAD) {
+          const uint32_t d = a.dom[(size_t)s_sd[k.cz].key * a.npos + pos];
+          dz = d == DOM_NONE ? RK_DZ_NONE : d;
+        }
+        if (k.ch < (uint32_t)MAX_SPREAD) {
+          const SpreadDev &q = s_sd[k.ch];
+          if (a.dom[(size_t)q.key * a.npos + pos] == DOM_NONE) {
+            hk = RK_HK_NONE;
+          } else if (q.cls != CLS_NONE) {
+            hk = a.cnt[(size_t)q.cls * a.npos + pos];
+            if (hk >= RK_HK_NONE) {
+              ovf = true;
+              hk = RK_HK_NONE - 1;
+            }
+          }
+        }
+        code = dz << 8 | hk;
+      }
+      key = (uint64_t)code << RK_G_SHIFT | (uint64_t)(RK_S_MASK - S) << RK_SLOT_BITS | slot;
+    }
+    r.keys[pos] = key;
+    r.pos[pos] = pos;
+  }
+  if (__syncthreads_or(ovf ? 1 : 0) && threadIdx.x == 0) atomicOr(&r.ctl[1], 1u);
+}
+
+// First sorted index of every group (feasible keys sort first).
+__global__ __launch_bounds__(SP_THREADS) void replica_groups_kernel(SpreadArgs a, ReplicaArgs r) {
+  __shared__ uint32_t s_f;
+  if (threadIdx.x == 0) s_f = acc_totals(a.acc).feasible;
+  __syncthreads();
+  const uint32_t f = s_f;
+  for (uint32_t i = blockIdx.x * SP_THREADS + threadIdx.x; i < f; i += grid_threads()) {
+    const uint64_t g = r.sorted[i] >> RK_G_SHIFT;
+    if (i == 0 || (r.sorted[i - 1] >> RK_G_SHIFT) != g) {
+      const uint32_t q = atomicAdd(&r.ctl[0], 1u);
+      if (q < RUN_GROUPS) r.gstart[q] = i;
+    }
+  }
+}
+
+constexpr int RUN_THREADS = 1024;  // thread g owns group g, thread t the run's t-th taken node
+static_assert(RUN_GROUPS == (uint32_t)RUN_THREADS && RUN_TOUCHED == (uint32_t)RUN_THREADS, "one group / node per thread");
+
+// Workgroup barrier for LDS hand-offs only (__syncthreads() also waits for the
+// group owners' prefetches of their next nodes' rows)
+__device__ __forceinline__ void run_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// A node's row as the run kernel carries it
+struct RunRow {
+  int64_t ac, am, rc, rm, zc, zm;
+  uint64_t pk;  // the filter pass's packed score parts (raw TaintToleration / NodeAffinity)
+  int32_t ap, np;
+};
+__device__ __forceinline__ RunRow run_row(const SpreadArgs &a, uint32_t pos) {
+  RunRow w;
+  w.ac = a.t.acpu[pos];
+  w.am = a.t.amem[pos];
+  w.rc = a.t.rcpu[pos];
+  w.rm = a.t.rmem[pos];
+  w.zc = a.t.zcpu[pos];
+  w.zm = a.t.zmem[pos];
+  w.pk = a.part[pos];
+  w.ap = a.t.apods[pos];
+  w.np = a.t.npods[pos];
+  return w;
+}
+
+__global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, ReplicaArgs r) {
+  __shared__ SpreadDev s_sd[MAX_SPREAD];
+  __shared__ Totals s_tot;
+  __shared__ uint32_t s_dz[RK_DZ_NONE];     // live PreScore counts of the other key's domains
+  __shared__ uint32_t s_gs[RUN_GROUPS];     // group starts, ascending
+  __shared__ uint64_t s_mn[RUN_THREADS / WAVE], s_mx[RUN_THREADS / WAVE], s_bk[RUN_THREADS / WAVE];
+  __shared__ uint32_t s_cls[MAX_CLASSES];   // selector classes the pods match (commit: +1 each)
+  // 0 groups, 1 refused, 2 classes, 3 RunStop, 4 a group's node won, 5 its slot, 6 its group code
+  __shared__ uint32_t s_ctl[8];
+  const uint32_t tid = threadIdx.x, lane = tid % WAVE, wid = tid / WAVE;
+  const PodDev p = a.pods[a.pod];  // every pod of the run is identical (host-checked)
+  const uint32_t n = spread_count(a, p);
+  if (tid < n) s_sd[tid] = spread_recs(a, p)[tid];
+  if (tid == 0) {
+    s_tot = acc_totals(a.acc);
+    const uint32_t g = r.ctl[0];
+    s_ctl[0] = min(g, RUN_GROUPS);
+    s_ctl[1] = g > RUN_GROUPS || r.ctl[1] ? 1u : 0u;
+    uint32_t m = 0;
+    for (int w = 0; w < CMASK_WORDS; ++w) {
+      uint64_t b = a.cmask[(size_t)a.pod * CMASK_WORDS + w];
+      while (b) {
+        s_cls[m++] = 64 * w + (uint32_t)__builtin_ctzll(b);
+        b &= b - 1;
+      }
+    }
+    s_ctl[2] = m;
+    s_ctl[3] = RUN_END;
+    s_ctl[4] = 0;
+  }
+  __syncthreads();
+  const RunCons k = run_cons(s_sd, n);
+  const uint32_t G = s_ctl[0], F = s_tot.feasible;
+  const uint32_t ndz = k.cz < (uint32_t)MAX_SPREAD ? a.ndom[s_sd[k.cz].key] : 0u;
+  for (uint32_t d = tid; d < ndz; d += RUN_THREADS) s_dz[d] = a.dcnt[(size_t)k.cz * a.dom_cap + d];
+  s_gs[tid] = tid < G ? r.gstart[tid] : 0xFFFFFFFFu;
+  // bitonic sort of the group starts
+  for (uint32_t size = 2; size <= RUN_GROUPS; size <<= 1)
+    for (uint32_t stride = size / 2; stride > 0; stride >>= 1) {
+      __syncthreads();
+      const uint32_t j = tid ^ stride;
+      if (j > tid) {
+        const uint32_t x = s_gs[tid], y = s_gs[j];
+        if ((x > y) == ((tid & size) == 0)) {
+          s_gs[tid] = y;
+          s_gs[j] = x;
+        }
+      }
+    }
+  __syncthreads();
+  auto cls_in = [&](uint32_t cls) {
+    if (cls == CLS_NONE) return false;
+    return ((a.cmask[(size_t)a.pod * CMASK_WORDS + cls / 64] >> (cls % 64)) & 1ull) != 0;
+  };
+  const bool inc_h = k.ch < (uint32_t)MAX_SPREAD && cls_in(s_sd[k.ch].cls);
+  const bool inc_z = k.cz < (uint32_t)MAX_SPREAD && cls_in(s_sd[k.cz].cls);
+  // topologyNormalizingWeight per constraint (spread_score)
+  const double w_h = k.ch < (uint32_t)MAX_SPREAD ? go_log((double)(F - s_tot.ignored) + 2.0) : 0.0;
+  const double w_z = k.cz < (uint32_t)MAX_SPREAD ? go_log((double)a.acc->topo_size[k.cz] + 2.0) : 0.0;
+  // raw Score of a group code (spread_score: constraints in order, math.Round)
+  auto raw_of = [&](uint32_t code) -> uint64_t {
+    const uint32_t dz = (code >> 8) & RK_DZ_NONE, hk = code & RK_HK_NONE;
+    double s = 0;
+    for (uint32_t c = 0; c < n; ++c) {
+      if (c == k.ch) {
+        if (hk != RK_HK_NONE) s += (double)hk * w_h + (double)(s_sd[c].max_skew - 1);
+      } else if (dz != RK_DZ_NONE) {
+        s += (double)s_dz[dz] * w_z + (double)(s_sd[c].max_skew - 1);
+      }
+    }
+    return (uint64_t)(int64_t)round(s);
+  };
+  // group tid: its first untaken sorted index (head), the head's key, position
+  // and row (prefetched), the next key and position
+  const bool g_on = tid < G;
+  uint32_t g_i = g_on ? s_gs[tid] : 0u;
+  const uint32_t g_end = tid + 1 < G ? s_gs[tid + 1] : F;
+  uint64_t g_key = g_on ? r.sorted[g_i] : 0ull;
+  uint32_t g_pos = g_on ? r.spos[g_i] : 0u;
+  const bool has_nxt = g_on && g_i + 1 < g_end;
+  uint64_t g_nkey = has_nxt ? r.sorted[g_i + 1] : 0ull;
+  uint32_t g_npos = has_nxt ? r.spos[g_i + 1] : 0u;
+  RunRow g_row{};
+  if (g_on) g_row = run_row(a, g_pos);
+  const uint32_t g_code = (uint32_t)(g_key >> RK_G_SHIFT);
+  // taken node tid: slot, position, group code (live), S, static tt / na part, row
+  bool t_on = false;
+  uint32_t t_slot = 0, t_pos = 0, t_code = 0, t_S = 0, t_stat = 0;
+  RunRow t_row{};
+  __shared__ RunRow s_row;  // a group's head handed to its new owner
+  uint32_t T = 0, next = a.pod, stop = RUN_END;
+  if (s_ctl[1]) {
+    stop = RUN_REFUSED;
+  } else if (F == 0) {
+    // no feasible node: every pod of the run gets the same FitError, nothing is committed
+    for (uint32_t pod = a.pod + tid; pod < r.end; pod += RUN_THREADS) {
+      DevResult res;
+      res.node_index = -1;
+      res.status = 1;  // KS_POD_UNSCHEDULABLE
+      res.total_score = 0;
+      res.feasible_nodes = 0;
+      res.evaluated_nodes = a.evaluated;
+      for (int q = 0; q < NFILT; ++q) res.fail_counts[q] = s_tot.fail[q];
+      res.spread_fail = s_tot.fail[PLUGIN_SPREAD];
+      res.ipa_fail = s_tot.fail[PLUGIN_IPA];
+      res._pad = 0;
+      res.prefiltered = p.prefilter_out;
+      res.flags = 0;
+      a.results[pod] = res;
+    }
+    if (tid == 0) a.counters[1] += r.end - a.pod;
+    next = r.end;
+  } else {
+    const uint64_t tt_max = s_tot.tt_max, na_max = s_tot.na_max;
+    for (uint32_t pod = a.pod; pod < r.end; ++pod) {
+      // min / max raw over the non-ignored feasible nodes
+      const bool g_live = g_on && g_i < g_end;
+      uint64_t graw = 0, traw = 0, mn = ~0ull, mx = 0;
+      if (g_live && !(g_code & RK_IGN)) {
+        graw = raw_of(g_code);
+        mn = min(mn, graw);
+        mx = max(mx, graw);
+      }
+      if (t_on && !(t_code & RK_IGN)) {
+        traw = raw_of(t_code);
+        mn = min(mn, traw);
+        mx = max(mx, traw);
+      }
+      mn = wave_min64(mn);
+      mx = wave_max64(mx);
+      if (lane == 0) {
+        s_mn[wid] = mn;
+        s_mx[wid] = mx;
+      }
+      run_barrier();
+      for (int w = 0; w < RUN_THREADS / WAVE; ++w) {
+        mn = min(mn, s_mn[w]);
+        mx = max(mx, s_mx[w]);
+      }
+      const int64_t pmin = (int64_t)mn, pmax = (int64_t)mx;
+      auto total_of = [&](uint32_t S, uint32_t code, uint64_t raw) -> int64_t {
+        int64_t norm = 0;  // PodTopologySpread NormalizeScore: ignored -> 0, max 0 -> 100
+        if (!(code & RK_IGN)) norm = pmax == 0 ? 100 : 100 * (pmax + pmin - (int64_t)raw) / pmax;
+        return (int64_t)S + (int64_t)a.w_pts * norm;
+      };
+      uint64_t gk = 0, tk = 0;
+      if (g_live)
+        gk = pack_key(total_of(RK_S_MASK - (uint32_t)((g_key >> RK_SLOT_BITS) & RK_S_MASK), g_code, graw),
+                      (uint32_t)g_key & RK_SLOT_MASK);
+      if (t_on) tk = pack_key(total_of(t_S, t_code, traw), t_slot);
+      uint64_t b = wave_max64(gk > tk ? gk : tk);
+      if (lane == 0) s_bk[wid] = b;
+      run_barrier();
+      for (int w = 0; w < RUN_THREADS / WAVE; ++w) b = s_bk[w] > b ? s_bk[w] : b;
+      // a group's head won: it joins the taken nodes (owner: thread T); the
+      // next node becomes the head, its row is fetched, the one after it named
+      if (g_live && gk == b) {
+        s_ctl[4] = 1;
+        s_ctl[5] = (uint32_t)g_key & RK_SLOT_MASK;
+        s_ctl[6] = g_code;
+        s_ctl[7] = g_pos;
+        s_row = g_row;
+        ++g_i;
+        g_key = g_nkey;
+        g_pos = g_npos;
+        if (g_i < g_end) g_row = run_row(a, g_pos);
+        const bool more = g_i + 1 < g_end;
+        g_nkey = more ? r.sorted[g_i + 1] : 0ull;
+        g_npos = more ? r.spos[g_i + 1] : 0u;
+      }
+      run_barrier();
+      const bool from_group = s_ctl[4] != 0;
+      bool mine = !from_group && t_on && tk == b;
+      if (from_group && tid == T) {
+        t_on = mine = true;
+        t_slot = s_ctl[5];
+        t_code = s_ctl[6];
+        t_pos = s_ctl[7];
+        t_row = s_row;
+        t_stat = run_static(p, a.w, t_row.pk & ~0xFFFFFFFFull, (int64_t)tt_max, (int64_t)na_max);
+      }
+      if (mine) {
+        // AssumePod (spread_commit): Requested, NonZeroRequested, pod count, class columns
+        t_row.rc += p.req_cpu;
+        t_row.rm += p.req_mem;
+        t_row.zc += p.nz_cpu;
+        t_row.zm += p.nz_mem;
+        t_row.np += 1;
+        a.t.rcpu[t_pos] = t_row.rc;
+        a.t.rmem[t_pos] = t_row.rm;
+        a.t.zcpu[t_pos] = t_row.zc;
+        a.t.zmem[t_pos] = t_row.zm;
+        a.t.npods[t_pos] = t_row.np;
+        for (uint32_t q = 0; q < s_ctl[2]; ++q) a.cnt[(size_t)s_cls[q] * a.npos + t_pos] += 1;
+        // the next pod's view of the node: own hostname count, its domain's count, S, Fit
+        if (inc_h && (t_code & RK_HK_NONE) != RK_HK_NONE) {
+          t_code += 1;
+          if ((t_code & RK_HK_NONE) == RK_HK_NONE) s_ctl[3] = RUN_FULL;  // beyond the key's range
+        }
+        if (inc_z && !(t_code & RK_IGN)) {
+          const uint32_t dz = (t_code >> 8) & RK_DZ_NONE;
+          s_dz[dz == RK_DZ_NONE ? 0u : dz] += 1;  // PreScore counts a node lacking the key in ""
+        }
+        const NodeRegs g = make_regs(t_row.ac, t_row.am, t_row.rc, t_row.rm, t_row.zc, t_row.zm, t_row.ap, t_row.np, t_slot);
+        t_S = (uint32_t)a.w.fit * (uint32_t)score_la(p, g) + (uint32_t)a.w.ba * (uint32_t)score_ba(p, g) + t_stat;
+        if (filter<false>(p, a.clauses, g, NodeExt{}) != ST_FEASIBLE) s_ctl[3] = RUN_FIT;
+        DevResult res;
+        res.node_index = (int32_t)t_slot;
+        res.status = 0;
+        res.total_score = (int64_t)(b >> 32) - 1;
+        res.feasible_nodes = F;
+        res.evaluated_nodes = a.evaluated;
+        for (int q = 0; q < NFILT; ++q) res.fail_counts[q] = s_tot.fail[q];
+        res.spread_fail = s_tot.fail[PLUGIN_SPREAD];
+        res.ipa_fail = s_tot.fail[PLUGIN_IPA];
+        res._pad = 0;
+        res.prefiltered = p.prefilter_out;
+        res.flags = F == 1 ? 1u : 0u;  // KS_RESULT_SINGLE_FEASIBLE
+        a.results[pod] = res;
+        a.counters[1] += 1;  // pods resolved
+      }
+      run_barrier();
+      T += from_group ? 1u : 0u;
+      next = pod + 1;
+      stop = s_ctl[3];
+      if (stop == RUN_END && T == RUN_TOUCHED && next < r.end) stop = RUN_FULL;
+      if (tid == 0) s_ctl[4] = 0;  // every thread read it before the barrier
+      if (stop != RUN_END) break;
+    }
+  }
+  if (tid == 0) {
+    r.ctl[2] = next;
+    r.ctl[3] = stop;
+  }
+  // clear the domain scratch of the other key (spread_select's clearing)
+  for (uint32_t d = tid; d < ndz; d += RUN_THREADS) {
+    a.dcnt[(size_t)k.cz * a.dom_cap + d] = 0;
+    a.dflag[(size_t)k.cz * a.dom_cap + d] = 0;
+  }
+}
+
 // Selector-class counts of the pods a round-kernel segment [lo, hi) bound.
 __global__ void class_commit_kernel(const DevResult *res, const uint64_t *cmask, const uint32_t *slot_pos,
                                     uint32_t *cnt, uint32_t npos, uint32_t lo, uint32_t hi) {
@@ -1103,6 +1484,21 @@ hipError_t launch_spread_reset(const SpreadArgs &a, hipStream_t st) {
   z.no_commit = 1;  // reset only: no result, no commit
   spread_commit_kernel<<<1, WAVE, 0, st>>>(z);
   return hipGetLastError();
+}
+
+hipError_t launch_replica_run(const SpreadArgs &a, const ReplicaArgs &r, void *sort_tmp, size_t sort_tmp_bytes,
+                              hipStream_t st) {
+  const uint32_t blocks =
+      std::max<uint32_t>(1, std::min<uint32_t>((a.npos + SP_THREADS - 1) / SP_THREADS, (uint32_t)SPREAD_MAX_BLOCKS));
+  hipError_t e = hipMemsetAsync(r.ctl, 0, 4 * sizeof(uint32_t), st);
+  if (e != hipSuccess) return e;
+  spread_filter_kernel<false><<<blocks, SP_THREADS, 0, st>>>(a);
+  replica_keys_kernel<<<blocks, SP_THREADS, 0, st>>>(a, r);
+  size_t bytes = sort_tmp_bytes;
+  if ((e = launch_sort_pairs(r.keys, r.sorted, r.pos, r.spos, a.npos, sort_tmp, &bytes, st)) != hipSuccess) return e;
+  replica_groups_kernel<<<blocks, SP_THREADS, 0, st>>>(a, r);
+  replica_run_kernel<<<1, RUN_THREADS, 0, st>>>(a, r);
+  return launch_spread_reset(a, st);
 }
 
 hipError_t launch_class_commit(const DevResult *res, const uint64_t *cmask, const uint32_t *slot_pos, uint32_t *cnt,

@@ -273,13 +273,14 @@ class KsConfig(C.Structure):
         ("side_cus", C.c_uint32),
         ("value_sync", C.c_uint32),
         ("sync_timeout_ms", C.c_uint32),
+        ("spread_replica_runs", C.c_uint32),
     ]
 
 
 RESOLVE_AUTO, RESOLVE_SERIAL, RESOLVE_PARALLEL = 0, 1, 2
 OPTION_FIELDS = ("resolve_mode", "resolve_par_max_passes", "resolve_serial_rounds", "dedup_identical_pods", "early_fix",
                  "tuple_guess", "ext_nodes_per_lane", "sweep_pairs", "sweep_pairs_ext", "resolve_cus", "side_cus",
-                 "value_sync", "sync_timeout_ms")
+                 "value_sync", "sync_timeout_ms", "spread_replica_runs")
 
 
 class KsStats(C.Structure):
@@ -295,6 +296,9 @@ class KsStats(C.Structure):
         ("spread_ms", C.c_double),
         ("spread_pods_timed", C.c_uint64),
         ("spread_pods", C.c_uint64),
+        ("replica_runs", C.c_uint64),
+        ("replica_pods", C.c_uint64),
+        ("replica_ms", C.c_double),
     ]
 
 
@@ -303,7 +307,7 @@ EXPECTED_SIZES = {
     "ks_label": 16, "ks_taint": 24, "ks_toleration": 24, "ks_node": 88, "ks_container": 48,
     "ks_resource": 16, "ks_image": 16,
     "ks_requirement": 24, "ks_term": 24, "ks_preferred_term": 32, "ks_pod": 184, "ks_event": 24, "ks_result": 64,
-    "ks_node_score": 56, "ks_node_state": 56, "ks_config": 68, "ks_pod_affinity_term": 96, "ks_stats": 88, "ks_label_selector": 32,
+    "ks_node_score": 56, "ks_node_state": 56, "ks_config": 124, "ks_pod_affinity_term": 96, "ks_stats": 112, "ks_label_selector": 32,
     "ks_spread_constraint": 72,
 }
 STRUCTS = {

@@ -29,7 +29,7 @@ def test_libksched_exports_every_declared_symbol():
     lib = _abi.ksched_lib()
     for name in declared("ksched.h", "ks_"):
         assert hasattr(lib, name), name
-    assert lib.ks_abi_version() == 4
+    assert lib.ks_abi_version() == 5
 
 
 def test_libksgather_exports_every_declared_symbol():
@@ -74,7 +74,8 @@ int main(void) {
   O(ks_event, pod) O(ks_event, node) S(ks_node_info) O(ks_node_info, generation) O(ks_node_info, node)
   O(ks_node_score, total_score) O(ks_config, weight_fit) O(ks_config, weight_image)
   O(ks_stats, sweep_ms) O(ks_stats, resolve_launches)
-  O(ks_config, resolve_mode) O(ks_config, early_fix) O(ks_config, sync_timeout_ms)
+  O(ks_config, resolve_mode) O(ks_config, early_fix) O(ks_config, sync_timeout_ms) O(ks_config, spread_replica_runs)
+  O(ks_stats, spread_pods) O(ks_stats, replica_pods) O(ks_stats, replica_ms)
   return 0;
 }
 """

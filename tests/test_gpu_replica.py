@@ -1,0 +1,165 @@
+"""Replica runs of the spread path (ksched_spread.hip replica_*):
+runs of identical pods whose constraints are all ScheduleAnyway -- deployment
+replicas under the system default constraints -- scheduled by one filter pass
+and one workgroup per run.  Results and node states against the oracle
+(upstream v1.31.3 podtopologyspread restated in oracle.cpp) bit for bit, and
+the device counters show which path ran."""
+import random
+
+import pytest
+
+from ksched.objects import (Container, LabelSelector, Node, NodeSelectorRequirement, NodeSelectorTerm, Pod,
+                            PreferredSchedulingTerm, Taint, Toleration, TopologySpreadConstraint as TSC,
+                            system_default_spread)
+from spread_cases import HOST, ZONE
+from test_gpu_spread import Pair, rand_nodes
+
+pytestmark = pytest.mark.gpu
+
+Gi, Mi = 1 << 30, 1 << 20
+RUN_MIN_PODS = 4  # ksched_kernels.hpp
+
+
+def replicas(app, n, req, variant="defaults", j0=0, **kw):
+    """n identical pods of one deployment (only the names differ)."""
+    sel = LabelSelector({"app": app})
+    spread, defaulted = [], False
+    if variant == "defaults":
+        spread, defaulted = system_default_spread(sel), True
+    elif variant == "own":  # the pod's own constraints: requireAllTopologies
+        spread = [TSC(2, ZONE, "ScheduleAnyway", sel), TSC(1, HOST, "ScheduleAnyway", sel)]
+    elif variant == "host":
+        spread = [TSC(1, HOST, "ScheduleAnyway", sel)]
+    elif variant == "rack":
+        spread = [TSC(2, "rack", "ScheduleAnyway", sel)]
+    elif variant == "other-selector":  # the selector does not count the pods themselves
+        spread = system_default_spread(LabelSelector({"app": "other"}))
+    elif variant == "policies":
+        spread = [TSC(3, HOST, "ScheduleAnyway", sel, node_taints_policy="Honor"),
+                  TSC(5, ZONE, "ScheduleAnyway", sel, node_affinity_policy="Honor", node_taints_policy="Honor")]
+    else:
+        raise ValueError(variant)
+    return [Pod(f"{app}-{j0 + j}", containers=[Container(req)], labels={"app": app}, topology_spread=spread,
+                spread_defaulted=defaulted, **kw) for j in range(n)]
+
+
+def counters(x):
+    st = x.s.stats()
+    return int(st.replica_runs), int(st.replica_pods)
+
+
+def prefill(x, rng, n, apps, k):
+    bound = [Pod(f"b{j}", containers=[Container({"cpu": 100, "memory": 128 * Mi})],
+                 labels={"app": rng.choice(apps)}) for j in range(k)]
+    x.add(bound, [rng.randrange(n) for _ in bound])
+
+
+@pytest.mark.parametrize("seed,n,zones", [(41, 600, 4), (42, 1500, 24), (43, 300, 2)])
+def test_replica_deployments(seed, n, zones):
+    # deployments of 1-300 replicas, every variant of program the runs model,
+    # between plain pods and DoNotSchedule spread pods that split the sequences
+    rng = random.Random(seed)
+    x = Pair(n)
+    x.upsert(rand_nodes(rng, n, zones), list(range(n)))
+    apps = [f"app{k}" for k in range(6)]
+    prefill(x, rng, n, apps, n)
+    ssd = {"disk": "ssd"}
+    pref = [PreferredSchedulingTerm(20, NodeSelectorTerm([NodeSelectorRequirement("disk", "In", ["ssd"])]))]
+    tol = [Toleration("ded", "Equal", "x", "NoSchedule")]
+    variants = [("defaults", {}), ("own", {}), ("host", {}), ("rack", {}), ("other-selector", {}),
+                ("defaults", {"node_selector": ssd}), ("policies", {"tolerations": tol}),
+                ("defaults", {"preferred": pref}), ("policies", {"node_selector": ssd, "tolerations": tol})]
+    j = 0
+    for b in range(3):
+        pods = []
+        for v, kw in variants:
+            app = rng.choice(apps)
+            req = {"cpu": rng.randrange(1, 20) * 50, "memory": rng.randrange(1, 32) * 64 * Mi}
+            k = rng.choice([1, 3, 4, 37, 120, 300])
+            pods += replicas(app, k, req, v, j0=j, **kw)
+            j += k
+            if rng.random() < 0.5:  # a plain pod (round kernels) or a DoNotSchedule one between deployments
+                dns = [TSC(1, ZONE, "DoNotSchedule", LabelSelector({"app": app}))] if rng.random() < 0.5 else []
+                pods.append(Pod(f"x{j}", containers=[Container({"cpu": 100})], labels={"app": app},
+                                topology_spread=dns))
+                j += 1
+        x.schedule(pods, f"seed {seed} batch {b}")
+        x.states_equal(f"seed {seed} batch {b}")
+    runs, done = counters(x)
+    assert runs > 0 and done > 0
+    x.close()
+
+
+@pytest.mark.parametrize("replicas_on", [1, 0])
+def test_replica_fit_losses_and_unschedulable(replicas_on):
+    # nodes fill after a few pods: runs end at every Fit loss (and fall back to
+    # the chain when they end short); the last replicas find no node at all
+    rng = random.Random(44)
+    n = 150
+    x = Pair(n, options={"spread_replica_runs": replicas_on})
+    nodes = [Node(f"h{i}", {"cpu": 1000, "memory": 4 * Gi, "pods": rng.choice([2, 3, 5])},
+                  {HOST: f"h{i}", ZONE: f"z{i % 3}"}) for i in range(n)]
+    x.upsert(nodes, list(range(n)))
+    pods = replicas("web", 700, {"cpu": 300, "memory": 256 * Mi})
+    r = x.schedule(pods, "fill")
+    assert (r["status"] == 0).any() and (r["status"] == 1).any()
+    x.states_equal("fill")
+    runs, done = counters(x)
+    assert (done > 0) == bool(replicas_on)
+    x.close()
+
+
+def test_replica_touched_cap():
+    # more distinct nodes than one run may take (RUN_TOUCHED): several runs
+    rng = random.Random(45)
+    n = 2600
+    x = Pair(n)
+    x.upsert(rand_nodes(rng, n, 10, nozone=0.0), list(range(n)))
+    pods = replicas("web", 2200, {"cpu": 100, "memory": 64 * Mi}, "host")
+    r = x.schedule(pods, "touched cap")
+    assert (r["status"] == 0).all()
+    x.states_equal("touched cap")
+    runs, done = counters(x)
+    assert runs >= 3 and done == 2200
+    x.close()
+
+
+def test_replica_refused_runs():
+    # more (domain, hostname count) groups than a run holds, and a hostname
+    # count beyond the key's range: the per-pod chain schedules them
+    n = 1300
+    x = Pair(n)
+    nodes = [Node(f"h{i}", {"cpu": 64000, "memory": 256 * Gi, "pods": 400}, {HOST: f"h{i}", ZONE: f"z{i % 4}",
+                                                                            "rack": f"r{i}"}) for i in range(n)]
+    x.upsert(nodes, list(range(n)))
+    x.schedule(replicas("web", 40, {"cpu": 100}, "rack"), "groups")
+    x.states_equal("groups")
+    assert counters(x) == (0, 0)
+    many = [Pod(f"b{j}", containers=[Container({"cpu": 10})], labels={"app": "api"}) for j in range(300)]
+    x.add(many, [7] * len(many))
+    x.schedule(replicas("api", 30, {"cpu": 100}), "hostname count")
+    x.states_equal("hostname count")
+    assert counters(x) == (0, 0)
+    x.schedule(replicas("db", 30, {"cpu": 100}), "runs again")  # other pods: counts 0, runs
+    x.states_equal("runs again")
+    assert counters(x)[1] == 30
+    x.close()
+
+
+def test_replica_short_sequences_and_taints():
+    # sequences shorter than RUN_MIN_PODS take the chain; normalised
+    # TaintToleration (PreferNoSchedule) and ImageLocality-free pods
+    rng = random.Random(46)
+    n = 500
+    x = Pair(n)
+    nodes = rand_nodes(rng, n, 5)
+    for i in range(0, n, 7):
+        nodes[i].taints = [Taint("soft", "y", "PreferNoSchedule")]
+    x.upsert(nodes, list(range(n)))
+    prefill(x, rng, n, ["web"], 200)
+    pods = replicas("web", RUN_MIN_PODS - 1, {"cpu": 150}) + replicas("web", RUN_MIN_PODS, {"cpu": 200}, j0=10) + \
+        replicas("web", 64, {"cpu": 250, "memory": Gi}, j0=20)
+    x.schedule(pods, "short")
+    x.states_equal("short")
+    assert counters(x)[1] == RUN_MIN_PODS + 64
+    x.close()
