@@ -75,6 +75,13 @@ B_SPREAD_NODE = 275
 # resource row, 32-B label / taint words, 3 domain ids + domain sums, status,
 # packed parts, raw score), select 21 (status, slot, packed parts, raw score)
 B_AFF_NODE = 186
+# Replica runs of --pods deploy, per node per run: the filter
+# pass (B_SPREAD_FILTER: slot, resource row, label / taint words, domain ids,
+# class count, status, packed parts), the sort keys + positions written (12),
+# read and written once by the radix sort (24), the sorted keys read by the
+# group-start pass (8)
+B_SPREAD_FILTER = 109
+B_RUN_NODE = B_SPREAD_FILTER + 12 + 24 + 8
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 # VALU issue peak of the sweep: 256 CUs x 4 SIMDs x 2.4 GHz SIMD cycles per
 # second over the cycles ONE wave64 VALU instruction of the sweep's own mix
@@ -108,10 +115,12 @@ def parse():
                          "shard: a shard's candidate lists hold up to 4 keys per block, and at tied top scores "
                          "a 125k-node shard's lists ran short with 4, DESIGN §6)")
     ap.add_argument("--kind", default="hetero", choices=["hetero", "kwok", "labeled", "zoned"])
-    ap.add_argument("--pods", default="default", choices=["default", "besteffort", "spread", "affinity"],
+    ap.add_argument("--pods", default="default", choices=["default", "besteffort", "spread", "deploy", "affinity"],
                     help="besteffort: request-less pods (kwok/make_pods/main.go:118-148); spread: "
-                         "deployment pods with PodTopologySpread constraints (use with --kind zoned)")
+                         "deployment pods with PodTopologySpread constraints (use with --kind zoned); deploy: "
+                         "deployment replicas under the system default constraints (identical per deployment)")
     ap.add_argument("--apps", type=int, default=64, help="deployments of the --pods spread stream")
+    ap.add_argument("--replicas", type=int, default=256, help="replicas per deployment of the --pods deploy stream")
     ap.add_argument("--workload", default="batch", choices=["batch", "c5"],
                     help="batch: one batch of --batch pods per step; c5: one burst + its event log per step")
     ap.add_argument("--burst", type=int, default=100_000, help="pods per burst (--workload c5)")
@@ -136,7 +145,7 @@ def parse():
         a.nodes_per_lane = 2 if a.gpus > 1 else 4
     if a.prefill is None:
         a.prefill = 0.0 if a.kind == "kwok" else 0.5
-    if a.pods in ("spread", "affinity"):  # one pod at a time (spread path): smaller steps and CPU samples
+    if a.pods in ("spread", "deploy", "affinity"):  # spread path: smaller steps and CPU samples
         if a.batch == 50_000:
             a.batch = 2048
         a.cpu_pods = min(a.cpu_pods, 4)
@@ -262,6 +271,8 @@ def pod_stream(args, kind, n, seed):
         return synth.besteffort_pods(n)
     if args.pods == "spread":
         return synth.spread_pods(n, args.apps, seed)
+    if args.pods == "deploy":
+        return synth.deploy_pods(n, args.replicas, seed)
     if args.pods == "affinity":
         return synth.affinity_pods(n, args.apps, seed)
     return synth.pods(kind, n, seed)
@@ -539,6 +550,11 @@ def workload_name(args) -> str:
                 "maxSkew 3 + zone maxSkew 5 ScheduleAnyway; half zone maxSkew 1 DoNotSchedule + hostname "
                 "maxSkew 1 ScheduleAnyway), every default Filter / Score plugin, pct=100, one pod at a time "
                 "(spread path)")
+    if args.pods == "deploy":
+        return (f"deploy: {n} heterogeneous nodes in 32 zones, prefill<{f:.0%} cpu (pods of 64 apps); "
+                f"deployments of {args.replicas} identical replicas under PodTopologySpread's system defaults "
+                "(hostname maxSkew 3 + zone maxSkew 5, ScheduleAnyway, selecting the deployment), every default "
+                "Filter / Score plugin, pct=100, in queue order (spread path, replica runs)")
     if args.pods == "affinity":
         return (f"affinity: {n} heterogeneous nodes in 32 zones, prefill<{f:.0%} cpu (pods of 64 apps); "
                 f"pods of {args.apps} deployments with InterPodAffinity terms (half required hostname "
@@ -562,7 +578,7 @@ def workload_name(args) -> str:
 
 def pmc_key(args, world) -> str:
     """Name of the PMC summary measured for exactly this configuration."""
-    pods = {"besteffort": "-be", "spread": "-spread", "affinity": "-affinity"}.get(args.pods, "")
+    pods = {"besteffort": "-be", "spread": "-spread", "deploy": "-deploy", "affinity": "-affinity"}.get(args.pods, "")
     return (f"{args.workload}_{args.kind}{pods}_n{args.nodes}_P{args.pods_per_round}_K{args.topk or args.pods_per_round}"
             f"_npl{args.nodes_per_lane}_w{world}")
 
@@ -590,7 +606,30 @@ def roofline_spread(args, st):
                     "time (HIP events on every 8th pod)"}
 
 
+def roofline_deploy(args, st):
+    """Replica runs: per run one filter pass, the sort keys, the radix sort and
+    the group starts over every node (B_RUN_NODE bytes per node), then one
+    workgroup walks the run's pods (latency-bound: three LDS barriers and one
+    commit per pod).  Achieved = B_RUN_NODE x nodes / the mean run's device
+    time (HIP events around every timed run)."""
+    runs = int(st.replica_runs)
+    if not runs or not st.replica_ms:
+        return roofline_spread(args, st)
+    ms_run = st.replica_ms / runs
+    traffic = B_RUN_NODE * args.nodes
+    ach = traffic / (ms_run * 1e-3) / 1e9
+    return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+            "kernel": "replica run (spread_filter, replica_keys, radix sort, replica_groups, replica_run)",
+            "ms_per_run": round(ms_run, 4), "pods_per_run": round(st.replica_pods / runs, 1),
+            "us_per_pod_in_runs": round(1e3 * st.replica_ms / max(1, st.replica_pods), 3),
+            "runs_timed": runs, "algorithmic_bytes_per_run": traffic,
+            "what": "B_RUN_NODE x nodes per run / run time; the in-run walk is one workgroup (not HBM-bound)"}
+
+
 def roofline(args, st, world):
+    if args.pods == "deploy":
+        return roofline_deploy(args, st)
     if args.pods in ("spread", "affinity"):
         return roofline_spread(args, st)
     labeled = args.kind == "labeled"
@@ -695,6 +734,8 @@ def report(args, sched, st, dbg, world, pods_timed, elapsed, scheduled, setup_s,
             "sweep_ms_total": round(st.sweep_ms, 3),
             "resolve_ms_total": round(st.resolve_ms, 3),
             "spread_pods": int(st.spread_pods),
+            "replica_runs": int(st.replica_runs),  # replica runs of the spread path
+            "replica_pods": int(st.replica_pods),
             "scheduled_fraction": round(scheduled / pods_timed, 4),
             "speculated_rounds_wasted": int(dbg[3]),  # since open (warmup included)
             # parallel commit, since open: rounds it resolved and its chunk passes per round

@@ -49,6 +49,12 @@ ksynth *ksynth_besteffort_pods(uint32_t n);
  * own [zone maxSkew 1 DoNotSchedule, hostname maxSkew 1 ScheduleAnyway], all
  * selecting app=app-k. */
 ksynth *ksynth_spread_pods(uint32_t n, uint32_t n_apps, uint64_t seed);
+/* Deployment replicas under PodTopologySpread's system defaults: pod j is
+ * replica j % replicas of deployment deploy-(j / replicas); a deployment's
+ * pods are identical (labels {app: deploy-k}, one C1 request draw per
+ * deployment, kwok tolerations, hostname maxSkew 3 + zone maxSkew 5
+ * ScheduleAnyway selecting app=deploy-k, spread_defaulted). */
+ksynth *ksynth_deploy_pods(uint32_t n, uint32_t replicas, uint64_t seed);
 // InterPodAffinity deployment pods (ksynth.cpp): alternately required hostname
 // anti-affinity + preferred zone affinity to the own app, and preferred
 // hostname anti-affinity + required zone affinity to the next app.

@@ -173,6 +173,7 @@ struct LabelSet {
   // pod adds to the class column (the weight of a preferred term, else 1)
   std::vector<std::pair<uint32_t, uint32_t>> terms;
   std::string key;              // set_of_key entry (sets with namespace labels or terms)
+  bool ever_bound = false;      // some node's pod records held it (never cleared: class creation's shortcut)
 };
 struct SelReq {
   uint32_t key;
@@ -392,7 +393,7 @@ struct ks_ctx {
   // [0] waiting for `mu` at run start, [1] enqueueing rounds, [2] drains, [3] runs,
   // [4] worker runs' wall time, [5] worker idle between submitted runs, [6] worker runs
   bool run_profile = false;
-  double prof[7] = {0, 0, 0, 0, 0, 0, 0};
+  double prof[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};  // [7..9] ks_batch_prepare: drain wait, compile, rest
   struct EvProf {
     uint64_t runs = 0, events = 0;
     double s = 0;
@@ -1720,6 +1721,7 @@ void flush_bound(ks_ctx *c) {
     std::vector<uint32_t> &v = c->nodes[b.slot].pod_sets;
     if (b.op > 0) {
       v.push_back(b.set);
+      c->label_sets[b.set].ever_bound = true;
     } else if (b.op < 0) {
       auto it = std::find(v.begin(), v.end(), b.set);
       if (it != v.end()) {  // never bound here: nothing to remove
@@ -1933,16 +1935,25 @@ ks_status class_get(ks_ctx *c, std::vector<Clause> &&clauses, bool create, uint3
   k.canon = canon;
   k.last_use = ++c->class_seq;
   c->class_of.emplace(canon, (uint32_t)slot);
-  std::vector<int8_t> match(c->label_sets.size(), -1);
+  // the label sets the selector matches; none that a bound pod ever carried
+  // (a new deployment's selector): the column is zero, no walk over the nodes
+  std::vector<int8_t> match(c->label_sets.size(), 0);
+  bool any = false;
+  for (uint32_t set = 0; set < match.size(); ++set) {
+    match[set] = class_matches(c, k, set) ? 1 : 0;
+    any |= match[set] && c->label_sets[set].ever_bound;
+  }
+  if (!any) {
+    HIPC(c, hipMemsetAsync(c->d_cnt + (size_t)slot * c->npos, 0, (size_t)c->npos * 4, c->stream));
+    *out = (uint32_t)slot;
+    return KS_OK;
+  }
   std::vector<uint32_t> col(c->npos, 0);
   for (uint32_t sl = 0; sl < c->cap; ++sl) {
     const HostNode &h = c->nodes[sl];
     if (!h.present) continue;
     uint32_t n = 0;
-    for (uint32_t set : h.pod_sets) {
-      if (match[set] < 0) match[set] = class_matches(c, k, set) ? 1 : 0;
-      n += (uint32_t)match[set];
-    }
+    for (uint32_t set : h.pod_sets) n += (uint32_t)match[set];
     col[c->slot_pos[sl]] = n;
   }
   if ((st = xfer_begin(c, (size_t)c->npos * 4 + 1024, 0)) ||
@@ -2432,6 +2443,7 @@ ks_status spread_pods_delta(ks_ctx *c, const uint32_t *sets, const uint32_t *slo
     HostNode &h = c->nodes[slots[i]];
     if (sign > 0) {
       h.pod_sets.push_back(set);
+      c->label_sets[set].ever_bound = true;
     } else {
       auto it = std::find(h.pod_sets.begin(), h.pod_sets.end(), set);
       if (it == h.pod_sets.end()) continue;  // never bound here: no count to remove
@@ -2979,11 +2991,11 @@ ks_status upload_batch(ks_ctx *c, ks_batch *b) {
   return KS_OK;
 }
 
-// Replica runs: what the run kernel's key layout holds -- slots
-// below 2^RK_SLOT_BITS, domain ids of the other key below RK_DZ_NONE -- on a
-// single-rank context (the one-pod path's condition).
+// Replica runs: what the run kernel's key layout holds --
+// domain ids of the other key below RK_DZ_NONE -- on a single-rank context
+// (the one-pod path's condition).
 bool replica_fits(const ks_ctx *c, const ks_batch *b, const SpreadArgs &sa, uint32_t i) {
-  if (c->has_comm() || c->cap > (1u << RK_SLOT_BITS)) return false;
+  if (c->has_comm()) return false;
   const SoloHdr *hd = reinterpret_cast<const SoloHdr *>(b->h_clauses + b->h_pods[i].solo_off);
   const SpreadDev *sd = reinterpret_cast<const SpreadDev *>(hd + 1);
   for (uint32_t k = 0; k < hd->n_spread; ++k)
@@ -2999,7 +3011,7 @@ ks_status replica_run(ks_ctx *c, ks_batch *b, SpreadArgs sa, uint32_t lo, uint32
   (void)b;
   if (!c->d_rk_keys) {
     size_t bytes = 0;
-    HIPC(c, launch_sort_pairs(nullptr, nullptr, nullptr, nullptr, c->npos, nullptr, &bytes, c->stream));
+    HIPC(c, launch_sort_pairs(nullptr, nullptr, nullptr, nullptr, c->cap, 64, nullptr, &bytes, c->stream));
     ks_status st;
     if ((st = dalloc(c, &c->d_rk_keys, c->npos)) || (st = dalloc(c, &c->d_rk_sorted, c->npos)) ||
         (st = dalloc(c, &c->d_rk_pos, c->npos)) || (st = dalloc(c, &c->d_rk_spos, c->npos)) ||
@@ -3009,7 +3021,14 @@ ks_status replica_run(ks_ctx *c, ks_batch *b, SpreadArgs sa, uint32_t lo, uint32
     c->rk_tmp_bytes = bytes;
     HIPC(c, hipHostMalloc((void **)&c->h_rk_ctl, 16, hipHostMallocDefault));
   }
-  ReplicaArgs r{c->d_rk_keys, c->d_rk_sorted, c->d_rk_pos, c->d_rk_spos, c->d_rk_gstart, c->d_rk_ctl, hi};
+  // static score < 100 x (the weights of LeastAllocated, BalancedAllocation,
+  // TaintToleration, NodeAffinity) + 1; ImageLocality adds 0 (no image records)
+  const uint32_t s_max = 100u * (uint32_t)(c->cfg.weight_fit + c->cfg.weight_balanced + c->cfg.weight_taint +
+                                           c->cfg.weight_affinity);
+  uint32_t s_bits = 1;
+  while (s_bits < 32 && (s_max >> s_bits) != 0) ++s_bits;
+  ReplicaArgs r{c->d_rk_keys, c->d_rk_sorted, c->d_rk_pos, c->d_rk_spos, c->d_rk_gstart, c->d_rk_ctl, hi, c->cap,
+                s_bits};
   sa.pod = lo;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (c->timing) {
@@ -3486,8 +3505,10 @@ void ks_close(ks_ctx *c) {
   if (c->run_profile)
     std::fprintf(stderr,
                  "ksched runs: %.0f runs: lock wait %.3f s, enqueue %.3f s, drains %.3f s; worker: %.0f runs %.3f s, "
-                 "idle with work queued %.3f s\n",
-                 c->prof[3], c->prof[0], c->prof[1], c->prof[2], c->prof[6], c->prof[4], c->prof[5]);
+                 "idle with work queued %.3f s; prepare: drain wait %.3f s, compile %.3f s, acquire / copy / "
+                 "upload %.3f s\n",
+                 c->prof[3], c->prof[0], c->prof[1], c->prof[2], c->prof[6], c->prof[4], c->prof[5], c->prof[7],
+                 c->prof[8], c->prof[9]);
   if (c->ev_profile)
     for (int k = 0; k < 4; ++k)
       std::fprintf(stderr, "ksched events kind %d: %llu runs, %llu events, %.3f s\n", k,
@@ -4148,7 +4169,9 @@ ks_status ks_batch_prepare(ks_ctx *c, const ks_pod *pods, uint32_t n, ks_batch *
     std::lock_guard<std::mutex> g(c->mu);
     for (uint32_t i = 0; i < n && !any_solo; ++i) any_solo = may_need_solo(c, pods[i]);
   }
+  const auto tp0 = std::chrono::steady_clock::now();
   if (any_solo) drain_async(c);
+  const auto tp1 = std::chrono::steady_clock::now();
   std::vector<uint32_t> set_ids(n), refs, term_refs;
   {
     // compile against the host dictionaries (the worker reads t.lw and the
@@ -4174,6 +4197,7 @@ ks_status ks_batch_prepare(ks_ctx *c, const ks_pod *pods, uint32_t n, ks_batch *
     dict_v = c->dict_version;
     names_v = c->compile_used_names ? c->names_version : 0;
   }
+  const auto tp2 = std::chrono::steady_clock::now();
   if (norm) ext = true;
   if (cl.w.empty()) cl.w.push_back(0);
   ks_batch *b = nullptr;
@@ -4233,6 +4257,11 @@ ks_status ks_batch_prepare(ks_ctx *c, const ks_pod *pods, uint32_t n, ks_batch *
       batch_release(c, b);
       return st;
     }
+  }
+  if (c->run_profile) {
+    c->prof[7] += std::chrono::duration<double>(tp1 - tp0).count();
+    c->prof[8] += std::chrono::duration<double>(tp2 - tp1).count();
+    c->prof[9] += std::chrono::duration<double>(std::chrono::steady_clock::now() - tp2).count();
   }
   *out = b;
   return KS_OK;

@@ -12,9 +12,10 @@
 namespace ks {
 
 // tmp == nullptr: *tmp_bytes = the scratch a sort of n pairs needs.
+// Stable: equal keys keep their input order.  Bits [0, end_bit) are sorted.
 hipError_t launch_sort_pairs(const uint64_t *kin, uint64_t *kout, const uint32_t *vin, uint32_t *vout, uint32_t n,
-                             void *tmp, size_t *tmp_bytes, hipStream_t st) {
-  return hipcub::DeviceRadixSort::SortPairs(tmp, *tmp_bytes, kin, kout, vin, vout, (int)n, 0, 64, st);
+                             uint32_t end_bit, void *tmp, size_t *tmp_bytes, hipStream_t st) {
+  return hipcub::DeviceRadixSort::SortPairs(tmp, *tmp_bytes, kin, kout, vin, vout, (int)n, 0, (int)end_bit, st);
 }
 
 }  // namespace ks

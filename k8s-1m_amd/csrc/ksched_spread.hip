@@ -36,6 +36,7 @@
 #include "ksched_dev.hpp"
 #include "ksched_eval.hpp"
 #include "ksched_kernels.hpp"
+#include "ksched_util.hpp"
 
 namespace ks {
 
@@ -1133,10 +1134,14 @@ __global__ __launch_bounds__(SP_THREADS) void replica_keys_kernel(SpreadArgs a, 
         }
         code = dz << 8 | hk;
       }
-      key = (uint64_t)code << RK_G_SHIFT | (uint64_t)(RK_S_MASK - S) << RK_SLOT_BITS | slot;
+      key = (uint64_t)code << r.s_bits | (uint64_t)(((1u << r.s_bits) - 1) - S);
     }
-    r.keys[pos] = key;
-    r.pos[pos] = pos;
+    // indexed by slot: the (stable) radix sort keeps equal keys in slot order,
+    // upstream's tie-break, without the slot in the key
+    if (slot != SLOT_NONE) {
+      r.keys[slot] = key;
+      r.pos[slot] = pos;
+    }
   }
   if (__syncthreads_or(ovf ? 1 : 0) && threadIdx.x == 0) atomicOr(&r.ctl[1], 1u);
 }
@@ -1148,8 +1153,8 @@ __global__ __launch_bounds__(SP_THREADS) void replica_groups_kernel(SpreadArgs a
   __syncthreads();
   const uint32_t f = s_f;
   for (uint32_t i = blockIdx.x * SP_THREADS + threadIdx.x; i < f; i += grid_threads()) {
-    const uint64_t g = r.sorted[i] >> RK_G_SHIFT;
-    if (i == 0 || (r.sorted[i - 1] >> RK_G_SHIFT) != g) {
+    const uint64_t g = r.sorted[i] >> r.s_bits;
+    if (i == 0 || (r.sorted[i - 1] >> r.s_bits) != g) {
       const uint32_t q = atomicAdd(&r.ctl[0], 1u);
       if (q < RUN_GROUPS) r.gstart[q] = i;
     }
@@ -1163,11 +1168,30 @@ static_assert(RUN_GROUPS == (uint32_t)RUN_THREADS && RUN_TOUCHED == (uint32_t)RU
 // group owners' prefetches of their next nodes' rows)
 __device__ __forceinline__ void run_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// floor(a / b) for 0 <= a < 2^53, 0 < b < 2^53: the binary64 quotient is
+// within one of it; one correction each way makes it exact (int64 division is
+// a long software sequence on the VALU)
+__device__ __forceinline__ int64_t run_div(int64_t a, int64_t b) {
+  int64_t q = (int64_t)((double)a / (double)b);
+  q -= q * b > a ? 1 : 0;
+  q += (q + 1) * b <= a ? 1 : 0;
+  return q;
+}
+// the same with inv = RN(1 / b): the product is within one of the quotient too
+__device__ __forceinline__ int64_t run_div_inv(int64_t a, int64_t b, double inv) {
+  int64_t q = (int64_t)((double)a * inv);
+  q -= q * b > a ? 1 : 0;
+  q += (q + 1) * b <= a ? 1 : 0;
+  return q;
+}
+__device__ __forceinline__ uint64_t run_wave_min(uint64_t v) { return ~wave_max_u64_dpp(~v); }
+
 // A node's row as the run kernel carries it
 struct RunRow {
   int64_t ac, am, rc, rm, zc, zm;
   uint64_t pk;  // the filter pass's packed score parts (raw TaintToleration / NodeAffinity)
   int32_t ap, np;
+  uint32_t slot;
 };
 __device__ __forceinline__ RunRow run_row(const SpreadArgs &a, uint32_t pos) {
   RunRow w;
@@ -1180,6 +1204,7 @@ __device__ __forceinline__ RunRow run_row(const SpreadArgs &a, uint32_t pos) {
   w.pk = a.part[pos];
   w.ap = a.t.apods[pos];
   w.np = a.t.npods[pos];
+  w.slot = a.pos_slot[pos];
   return w;
 }
 
@@ -1190,8 +1215,9 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
   __shared__ uint32_t s_gs[RUN_GROUPS];     // group starts, ascending
   __shared__ uint64_t s_mn[RUN_THREADS / WAVE], s_mx[RUN_THREADS / WAVE], s_bk[RUN_THREADS / WAVE];
   __shared__ uint32_t s_cls[MAX_CLASSES];   // selector classes the pods match (commit: +1 each)
-  // 0 groups, 1 refused, 2 classes, 3 RunStop, 4 a group's node won, 5 its slot, 6 its group code
-  __shared__ uint32_t s_ctl[8];
+  // 0 groups, 1 refused, 2 classes, 3 RunStop, 4 a group's node won, 5 its slot, 6 its group code,
+  // 7 its position, 8 the domain whose count the last commit raised (RK_DZ_NONE: none)
+  __shared__ uint32_t s_ctl[9];
   const uint32_t tid = threadIdx.x, lane = tid % WAVE, wid = tid / WAVE;
   const PodDev p = a.pods[a.pod];  // every pod of the run is identical (host-checked)
   const uint32_t n = spread_count(a, p);
@@ -1212,6 +1238,7 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
     s_ctl[2] = m;
     s_ctl[3] = RUN_END;
     s_ctl[4] = 0;
+    s_ctl[8] = RK_DZ_NONE;
   }
   __syncthreads();
   const RunCons k = run_cons(s_sd, n);
@@ -1260,19 +1287,26 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
   const bool g_on = tid < G;
   uint32_t g_i = g_on ? s_gs[tid] : 0u;
   const uint32_t g_end = tid + 1 < G ? s_gs[tid + 1] : F;
+  // (head: key, position, row; next: key, position), so a new head's row is
+  // requested as soon as the old one wins
   uint64_t g_key = g_on ? r.sorted[g_i] : 0ull;
   uint32_t g_pos = g_on ? r.spos[g_i] : 0u;
-  const bool has_nxt = g_on && g_i + 1 < g_end;
-  uint64_t g_nkey = has_nxt ? r.sorted[g_i + 1] : 0ull;
-  uint32_t g_npos = has_nxt ? r.spos[g_i + 1] : 0u;
+  const bool has1 = g_on && g_i + 1 < g_end;
+  uint64_t g_nkey = has1 ? r.sorted[g_i + 1] : 0ull;
+  uint32_t g_npos = has1 ? r.spos[g_i + 1] : 0u;
   RunRow g_row{};
   if (g_on) g_row = run_row(a, g_pos);
-  const uint32_t g_code = (uint32_t)(g_key >> RK_G_SHIFT);
-  // taken node tid: slot, position, group code (live), S, static tt / na part, row
-  bool t_on = false;
+  const uint32_t smask = (1u << r.s_bits) - 1;
+  const uint32_t g_code = (uint32_t)(g_key >> r.s_bits) & 0xFFFFFu;
+  // raw Score of the group (kept; recomputed when its domain's count moves)
+  uint64_t graw = g_on && !(g_code & RK_IGN) ? raw_of(g_code) : 0ull;
+  // taken node tid: slot, position, group code (live), S, static tt / na part,
+  // row, RN(1 / Allocatable) of cpu and memory, raw Score (kept as graw)
+  bool t_on = false, t_dirty = false;
   uint32_t t_slot = 0, t_pos = 0, t_code = 0, t_S = 0, t_stat = 0;
-  RunRow t_row{};
-  __shared__ RunRow s_row;  // a group's head handed to its new owner
+  uint64_t traw = 0;
+  __shared__ RunRow s_trow[RUN_TOUCHED];  // taken node t's row (its owner's; the winning head writes it)
+  __shared__ double s_tinv[RUN_TOUCHED][2];  // its RN(1 / Allocatable) of cpu and memory
   uint32_t T = 0, next = a.pod, stop = RUN_END;
   if (s_ctl[1]) {
     stop = RUN_REFUSED;
@@ -1298,21 +1332,24 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
   } else {
     const uint64_t tt_max = s_tot.tt_max, na_max = s_tot.na_max;
     for (uint32_t pod = a.pod; pod < r.end; ++pod) {
-      // min / max raw over the non-ignored feasible nodes
+      // raw Scores the last commit moved; min / max raw over the non-ignored
+      // feasible nodes
+      const uint32_t chg = s_ctl[8];
       const bool g_live = g_on && g_i < g_end;
-      uint64_t graw = 0, traw = 0, mn = ~0ull, mx = 0;
+      uint64_t mn = ~0ull, mx = 0;
       if (g_live && !(g_code & RK_IGN)) {
-        graw = raw_of(g_code);
+        if (((g_code >> 8) & RK_DZ_NONE) == chg) graw = raw_of(g_code);
         mn = min(mn, graw);
         mx = max(mx, graw);
       }
       if (t_on && !(t_code & RK_IGN)) {
-        traw = raw_of(t_code);
+        if (t_dirty || ((t_code >> 8) & RK_DZ_NONE) == chg) traw = raw_of(t_code);
+        t_dirty = false;
         mn = min(mn, traw);
         mx = max(mx, traw);
       }
-      mn = wave_min64(mn);
-      mx = wave_max64(mx);
+      mn = run_wave_min(mn);
+      mx = wave_max_u64_dpp(mx);
       if (lane == 0) {
         s_mn[wid] = mn;
         s_mx[wid] = mx;
@@ -1323,28 +1360,27 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
         mx = max(mx, s_mx[w]);
       }
       const int64_t pmin = (int64_t)mn, pmax = (int64_t)mx;
+      const double pinv = pmax ? 1.0 / (double)pmax : 0.0;
       auto total_of = [&](uint32_t S, uint32_t code, uint64_t raw) -> int64_t {
         int64_t norm = 0;  // PodTopologySpread NormalizeScore: ignored -> 0, max 0 -> 100
-        if (!(code & RK_IGN)) norm = pmax == 0 ? 100 : 100 * (pmax + pmin - (int64_t)raw) / pmax;
+        if (!(code & RK_IGN)) norm = pmax == 0 ? 100 : run_div_inv(100 * (pmax + pmin - (int64_t)raw), pmax, pinv);
         return (int64_t)S + (int64_t)a.w_pts * norm;
       };
       uint64_t gk = 0, tk = 0;
-      if (g_live)
-        gk = pack_key(total_of(RK_S_MASK - (uint32_t)((g_key >> RK_SLOT_BITS) & RK_S_MASK), g_code, graw),
-                      (uint32_t)g_key & RK_SLOT_MASK);
+      if (g_live) gk = pack_key(total_of(smask - (uint32_t)(g_key & smask), g_code, graw), g_row.slot);
       if (t_on) tk = pack_key(total_of(t_S, t_code, traw), t_slot);
-      uint64_t b = wave_max64(gk > tk ? gk : tk);
+      uint64_t b = wave_max_u64_dpp(gk > tk ? gk : tk);
       if (lane == 0) s_bk[wid] = b;
       run_barrier();
       for (int w = 0; w < RUN_THREADS / WAVE; ++w) b = s_bk[w] > b ? s_bk[w] : b;
       // a group's head won: it joins the taken nodes (owner: thread T); the
-      // next node becomes the head, its row is fetched, the one after it named
+      // next node becomes the head, its row is requested, the one after it named
       if (g_live && gk == b) {
         s_ctl[4] = 1;
-        s_ctl[5] = (uint32_t)g_key & RK_SLOT_MASK;
+        s_ctl[5] = g_row.slot;
         s_ctl[6] = g_code;
         s_ctl[7] = g_pos;
-        s_row = g_row;
+        s_trow[T] = g_row;
         ++g_i;
         g_key = g_nkey;
         g_pos = g_npos;
@@ -1361,10 +1397,13 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
         t_slot = s_ctl[5];
         t_code = s_ctl[6];
         t_pos = s_ctl[7];
-        t_row = s_row;
-        t_stat = run_static(p, a.w, t_row.pk & ~0xFFFFFFFFull, (int64_t)tt_max, (int64_t)na_max);
+        const RunRow &w = s_trow[tid];
+        t_stat = run_static(p, a.w, w.pk & ~0xFFFFFFFFull, (int64_t)tt_max, (int64_t)na_max);
+        s_tinv[tid][0] = w.ac ? 1.0 / (double)w.ac : 0.0;  // as make_regs
+        s_tinv[tid][1] = w.am ? 1.0 / (double)w.am : 0.0;
       }
       if (mine) {
+        RunRow &t_row = s_trow[tid];
         // AssumePod (spread_commit): Requested, NonZeroRequested, pod count, class columns
         t_row.rc += p.req_cpu;
         t_row.rm += p.req_mem;
@@ -1376,17 +1415,23 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
         a.t.zcpu[t_pos] = t_row.zc;
         a.t.zmem[t_pos] = t_row.zm;
         a.t.npods[t_pos] = t_row.np;
-        for (uint32_t q = 0; q < s_ctl[2]; ++q) a.cnt[(size_t)s_cls[q] * a.npos + t_pos] += 1;
+        // no returned value: the stores leave without a round trip on the pod's path
+        for (uint32_t q = 0; q < s_ctl[2]; ++q) atomicAdd(&a.cnt[(size_t)s_cls[q] * a.npos + t_pos], 1u);
         // the next pod's view of the node: own hostname count, its domain's count, S, Fit
         if (inc_h && (t_code & RK_HK_NONE) != RK_HK_NONE) {
           t_code += 1;
           if ((t_code & RK_HK_NONE) == RK_HK_NONE) s_ctl[3] = RUN_FULL;  // beyond the key's range
         }
+        uint32_t moved = RK_DZ_NONE;
         if (inc_z && !(t_code & RK_IGN)) {
           const uint32_t dz = (t_code >> 8) & RK_DZ_NONE;
-          s_dz[dz == RK_DZ_NONE ? 0u : dz] += 1;  // PreScore counts a node lacking the key in ""
+          moved = dz == RK_DZ_NONE ? 0u : dz;  // PreScore counts a node lacking the key in ""
+          s_dz[moved] += 1;
         }
-        const NodeRegs g = make_regs(t_row.ac, t_row.am, t_row.rc, t_row.rm, t_row.zc, t_row.zm, t_row.ap, t_row.np, t_slot);
+        s_ctl[8] = moved;
+        t_dirty = true;
+        const NodeRegs g = make_regs_inv(t_row.ac, t_row.am, t_row.rc, t_row.rm, t_row.zc, t_row.zm, t_row.ap,
+                                         t_row.np, t_slot, s_tinv[tid][0], s_tinv[tid][1]);
         t_S = (uint32_t)a.w.fit * (uint32_t)score_la(p, g) + (uint32_t)a.w.ba * (uint32_t)score_ba(p, g) + t_stat;
         if (filter<false>(p, a.clauses, g, NodeExt{}) != ST_FEASIBLE) s_ctl[3] = RUN_FIT;
         DevResult res;
@@ -1402,7 +1447,6 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
         res.prefiltered = p.prefilter_out;
         res.flags = F == 1 ? 1u : 0u;  // KS_RESULT_SINGLE_FEASIBLE
         a.results[pod] = res;
-        a.counters[1] += 1;  // pods resolved
       }
       run_barrier();
       T += from_group ? 1u : 0u;
@@ -1416,6 +1460,7 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
   if (tid == 0) {
     r.ctl[2] = next;
     r.ctl[3] = stop;
+    if (F != 0) a.counters[1] += next - a.pod;  // pods resolved (F == 0: counted above)
   }
   // clear the domain scratch of the other key (spread_select's clearing)
   for (uint32_t d = tid; d < ndz; d += RUN_THREADS) {
@@ -1495,7 +1540,9 @@ hipError_t launch_replica_run(const SpreadArgs &a, const ReplicaArgs &r, void *s
   spread_filter_kernel<false><<<blocks, SP_THREADS, 0, st>>>(a);
   replica_keys_kernel<<<blocks, SP_THREADS, 0, st>>>(a, r);
   size_t bytes = sort_tmp_bytes;
-  if ((e = launch_sort_pairs(r.keys, r.sorted, r.pos, r.spos, a.npos, sort_tmp, &bytes, st)) != hipSuccess) return e;
+  if ((e = launch_sort_pairs(r.keys, r.sorted, r.pos, r.spos, r.nslots, 20 + r.s_bits, sort_tmp, &bytes, st)) !=
+      hipSuccess)
+    return e;
   replica_groups_kernel<<<blocks, SP_THREADS, 0, st>>>(a, r);
   replica_run_kernel<<<1, RUN_THREADS, 0, st>>>(a, r);
   return launch_spread_reset(a, st);

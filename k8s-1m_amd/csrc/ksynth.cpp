@@ -407,6 +407,46 @@ extern "C" ksynth *ksynth_spread_pods(uint32_t n, uint32_t n_apps, uint64_t seed
   return s;
 }
 
+// Deployment replicas under the system default spread constraints (ksynth.h):
+// the replica set's pod template, so a deployment's pods are identical.
+extern "C" ksynth *ksynth_deploy_pods(uint32_t n, uint32_t replicas, uint64_t seed) {
+  auto *s = new ksynth();
+  reserve_pods(s, n);
+  if (replicas == 0) replicas = 1;
+  for (uint32_t j = 0; j < n; ++j) {
+    const uint32_t d = j / replicas;
+    Rng r(seed, d, 7);  // per deployment: every replica draws the same requests
+    ks_pod p = base_pod(s, j, "deploy-");
+    ks_container c;
+    draw_requests(r, c);
+    p.containers = ksynth::push(s->containers, c);
+    p.n_containers = 1;
+    p.tolerations = s->tolerations.data() + s->tolerations.size();
+    kwok_tolerations(s);
+    p.n_tolerations = 3;
+    const ks_label *lab =
+        ksynth::push(s->labels, ks_label{s->intern("app"), s->intern("deploy-" + std::to_string(d))});
+    p.labels = lab;
+    p.n_labels = 1;
+    ks_spread_constraint a{}, b{};
+    a.selector.match_labels = lab;
+    a.selector.n_match_labels = 1;
+    b.selector = a.selector;
+    a.topology_key = s->intern("kubernetes.io/hostname");
+    a.max_skew = 3;
+    a.when_unsatisfiable = KS_SCHEDULE_ANYWAY;
+    b.topology_key = s->intern("topology.kubernetes.io/zone");
+    b.max_skew = 5;
+    b.when_unsatisfiable = KS_SCHEDULE_ANYWAY;
+    p.spread_defaulted = 1;
+    p.spread = ksynth::push(s->spread, a);
+    ksynth::push(s->spread, b);
+    p.n_spread = 2;
+    s->pods.push_back(p);
+  }
+  return s;
+}
+
 // Deployment pods with pod (anti-)affinity (InterPodAffinity, the one-pod
 // path): app-k pods with, alternately, required hostname anti-affinity to
 // their own app + preferred zone affinity to it (weight 50), and preferred

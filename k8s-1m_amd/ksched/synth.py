@@ -61,6 +61,10 @@ def spread_pods(n: int, n_apps: int, seed: int) -> Synth:
     return Synth(_abi.ksynth_lib().ksynth_spread_pods(n, n_apps, seed))
 
 
+def deploy_pods(n: int, replicas: int, seed: int) -> Synth:
+    return Synth(_abi.ksynth_lib().ksynth_deploy_pods(n, replicas, seed))
+
+
 def affinity_pods(n: int, n_apps: int, seed: int) -> Synth:
     return Synth(_abi.ksynth_lib().ksynth_affinity_pods(n, n_apps, seed))
 

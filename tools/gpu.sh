@@ -4,7 +4,7 @@
 # the script stops at the first failure.
 #
 #   tools/gpu.sh tests TAG [pytest -k expr]   GPU parity suite (one process) + smoke()
-#   tools/gpu.sh lines TAG "c3 c4 ..."        bench lines: c3 c4 c2 kwok kwokbe c5 spread affinity
+#   tools/gpu.sh lines TAG "c3 c4 ..."        bench lines: c3 c4 c2 kwok kwokbe c5 spread deploy affinity
 #                                             (each -> gpurun_out/bench_TAG_<line>.json)
 #   tools/gpu.sh trace TAG [bench args]       rocprofv3 --kernel-trace --stats of a short bench run
 #   tools/gpu.sh pmc TAG [bench args]         PMC passes of one configuration -> gpurun_out/pmc/<key>.json
@@ -31,6 +31,8 @@ line_args() {  # bench.py arguments of a named BASELINE.json configuration
     kwokbe) echo "--kind kwok --pods besteffort --no-cpu-baseline --latency-calls 0" ;;
     c5) echo "--workload c5 --steps 5 --warmup 1 --no-cpu-baseline" ;;
     spread) echo "--kind zoned --pods spread --latency-calls 0" ;;
+    deploy) echo "--kind zoned --pods deploy --latency-calls 0" ;;
+    deploychain) echo "--kind zoned --pods deploy --latency-calls 0 --no-cpu-baseline --opt spread_replica_runs=0" ;;
     affinity) echo "--kind zoned --pods affinity --latency-calls 0" ;;
     proxy) echo "--nodes 125000 --no-cpu-baseline --latency-calls 0" ;;
     *) echo "unknown line $1" >&2; return 1 ;;
