@@ -516,10 +516,13 @@ struct ks_ctx {
   // words (ReplicaArgs::ctl; pinned copy), radix-sort scratch
   bool replica_runs = true;
   uint64_t *d_rk_keys = nullptr, *d_rk_sorted = nullptr;
-  uint32_t *d_rk_pos = nullptr, *d_rk_spos = nullptr, *d_rk_gstart = nullptr, *d_rk_ctl = nullptr;
+  uint64_t *d_rk_val = nullptr, *d_rk_sval = nullptr;
+  uint32_t *d_rk_gstart = nullptr, *d_rk_ctl = nullptr;
   uint8_t *d_rk_tmp = nullptr;
   size_t rk_tmp_bytes = 0;
   uint32_t *h_rk_ctl = nullptr;
+  uint64_t *d_rk_prof = nullptr;  // KS_RUN_PROFILE: replica_run phase clocks (ReplicaArgs::prof)
+  uint64_t rk_prof[4] = {0, 0, 0, 0};  // ... their totals after the last run
   uint32_t *h_seg = nullptr;       // pinned: start pod of a round-kernel segment
   // comm: RCCL, or an in-process group of contexts (tests of the multi-rank path on one GPU)
   ncclComm_t comm = nullptr;
@@ -3014,9 +3017,10 @@ ks_status replica_run(ks_ctx *c, ks_batch *b, SpreadArgs sa, uint32_t lo, uint32
     HIPC(c, launch_sort_pairs(nullptr, nullptr, nullptr, nullptr, c->cap, 64, nullptr, &bytes, c->stream));
     ks_status st;
     if ((st = dalloc(c, &c->d_rk_keys, c->npos)) || (st = dalloc(c, &c->d_rk_sorted, c->npos)) ||
-        (st = dalloc(c, &c->d_rk_pos, c->npos)) || (st = dalloc(c, &c->d_rk_spos, c->npos)) ||
+        (st = dalloc(c, &c->d_rk_val, c->npos)) || (st = dalloc(c, &c->d_rk_sval, c->npos)) ||
         (st = dalloc(c, &c->d_rk_gstart, RUN_GROUPS)) || (st = dalloc(c, &c->d_rk_ctl, 4)) ||
-        (st = dalloc(c, &c->d_rk_tmp, std::max<size_t>(bytes, 16))))
+        (st = dalloc(c, &c->d_rk_tmp, std::max<size_t>(bytes, 16))) ||
+        (c->run_profile && (st = dalloc(c, &c->d_rk_prof, 4))))
       return st;
     c->rk_tmp_bytes = bytes;
     HIPC(c, hipHostMalloc((void **)&c->h_rk_ctl, 16, hipHostMallocDefault));
@@ -3027,8 +3031,8 @@ ks_status replica_run(ks_ctx *c, ks_batch *b, SpreadArgs sa, uint32_t lo, uint32
                                            c->cfg.weight_affinity);
   uint32_t s_bits = 1;
   while (s_bits < 32 && (s_max >> s_bits) != 0) ++s_bits;
-  ReplicaArgs r{c->d_rk_keys, c->d_rk_sorted, c->d_rk_pos, c->d_rk_spos, c->d_rk_gstart, c->d_rk_ctl, hi, c->cap,
-                s_bits};
+  ReplicaArgs r{c->d_rk_keys, c->d_rk_sorted, c->d_rk_val, c->d_rk_sval, c->d_rk_gstart, c->d_rk_ctl, hi, c->cap,
+                s_bits, c->d_rk_prof};
   sa.pod = lo;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (c->timing) {
@@ -3042,6 +3046,7 @@ ks_status replica_run(ks_ctx *c, ks_batch *b, SpreadArgs sa, uint32_t lo, uint32
   if (ks_status st = sync_bounded(c, c->stream, "a replica run")) return st;
   *next = c->h_rk_ctl[2];
   *stop = c->h_rk_ctl[3];
+  if (c->d_rk_prof) HIPC(c, hipMemcpy(c->rk_prof, c->d_rk_prof, sizeof c->rk_prof, hipMemcpyDeviceToHost));
   if (*next < lo || *next > hi || (*next == lo) != (*stop == RUN_REFUSED))
     return c->fail(KS_ERR_DEVICE, "replica run over pods [%u, %u) ended at %u (stop %u)", lo, hi, *next, *stop);
   const uint32_t done = *next - lo;
@@ -3509,6 +3514,11 @@ void ks_close(ks_ctx *c) {
                  "upload %.3f s\n",
                  c->prof[3], c->prof[0], c->prof[1], c->prof[2], c->prof[6], c->prof[4], c->prof[5], c->prof[7],
                  c->prof[8], c->prof[9]);
+  if (c->run_profile && c->rk_prof[3]) {
+    const uint64_t *h = c->rk_prof;
+    std::fprintf(stderr, "ksched replica runs: %llu pods; cycles per pod: min/max raw %.0f, argmax %.0f, commit %.0f\n",
+                 (unsigned long long)h[3], (double)h[0] / h[3], (double)h[1] / h[3], (double)h[2] / h[3]);
+  }
   if (c->ev_profile)
     for (int k = 0; k < 4; ++k)
       std::fprintf(stderr, "ksched events kind %d: %llu runs, %llu events, %.3f s\n", k,
@@ -3543,8 +3553,8 @@ void ks_close(ks_ctx *c) {
                   c->d_start, c->d_norm, c->d_norm_inv, c->d_pstat, c->d_fix, c->d_brec, c->d_srec, c->d_frec,
                   c->d_counters, c->d_crow, c->d_cext, c->d_pipe, c->d_carry, c->d_flags, c->d_dom, c->d_dedup,
                   c->d_pos_slot, c->d_dcnt, c->d_dflag, c->d_acc, c->d_sst, c->d_sraw, c->d_spart,
-                  c->d_xalloc, c->d_tcnt, c->d_adcnt, c->d_sraw2, c->d_rk_keys, c->d_rk_sorted, c->d_rk_pos,
-                  c->d_rk_spos, c->d_rk_gstart, c->d_rk_ctl, c->d_rk_tmp};
+                  c->d_xalloc, c->d_tcnt, c->d_adcnt, c->d_sraw2, c->d_rk_keys, c->d_rk_sorted, c->d_rk_val,
+                  c->d_rk_sval, c->d_rk_gstart, c->d_rk_ctl, c->d_rk_tmp, c->d_rk_prof};
   for (void *b : bufs)
     if (b) (void)hipFree(b);
   if (c->h_start) (void)hipHostFree(c->h_start);

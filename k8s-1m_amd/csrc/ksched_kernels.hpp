@@ -150,8 +150,8 @@ struct SpreadArgs {
 // and one other key), scheduled by one workgroup after one filter pass.  Sort
 // key of a feasible node, at its slot: group code (ignored << 19 | domain << 8
 // | own hostname count) << s_bits | (2^s_bits - 1 - static score).
-constexpr uint32_t RUN_GROUPS = 1024;   // groups a run can hold (more: the run is refused)
-constexpr uint32_t RUN_TOUCHED = 1024;  // distinct nodes one run may take (then it ends)
+constexpr uint32_t RUN_GROUPS = 512;    // groups a run can hold (more: the run is refused)
+constexpr uint32_t RUN_TOUCHED = 512;   // distinct nodes one run may take (then it ends)
 constexpr uint32_t RUN_MIN_PODS = 4;    // shorter sequences take the per-pod chain
 constexpr uint32_t RK_HK_NONE = 255;    // the node lacks the hostname key (counts 0..254)
 constexpr uint32_t RK_DZ_NONE = 2047;   // the node lacks the other key (domain ids 0..2046)
@@ -159,12 +159,13 @@ constexpr uint32_t RK_IGN = 1u << 19;   // PreScore ignores the node (requireAll
 enum RunStop : uint32_t { RUN_END = 0, RUN_FIT = 1, RUN_FULL = 2, RUN_REFUSED = 3 };
 struct ReplicaArgs {
   uint64_t *keys, *sorted;  // [npos] sort keys, sorted
-  uint32_t *pos, *spos;     // [nslots] position of each key, sorted with the keys
+  uint64_t *val, *sval;     // [nslots] slot << 32 | position of each key, sorted with the keys
   uint32_t *gstart;         // [RUN_GROUPS] first sorted index of each group (unordered)
   uint32_t *ctl;            // [4] 0 groups, 1 hostname count beyond RK_HK_NONE - 1, 2 next pod, 3 RunStop
   uint32_t end;             // one past the run's last pod
   uint32_t nslots;          // keys sorted (one per slot)
   uint32_t s_bits;          // bits of the static score (2^s_bits > 100 x the static plugins' weights)
+  uint64_t *prof;           // KS_RUN_PROFILE: [0..2] cycles of the pod loop's phases, [3] pods (null: off)
 };
 
 hipError_t launch_spread_pod(const SpreadArgs &a, uint32_t passes, hipStream_t st);
@@ -172,7 +173,7 @@ hipError_t launch_spread_reset(const SpreadArgs &a, hipStream_t st);
 // filter pass for a.pod, keys, sort, groups, the run kernel; ctl zeroed first
 hipError_t launch_replica_run(const SpreadArgs &a, const ReplicaArgs &r, void *sort_tmp, size_t sort_tmp_bytes,
                               hipStream_t st);
-hipError_t launch_sort_pairs(const uint64_t *kin, uint64_t *kout, const uint32_t *vin, uint32_t *vout, uint32_t n,
+hipError_t launch_sort_pairs(const uint64_t *kin, uint64_t *kout, const uint64_t *vin, uint64_t *vout, uint32_t n,
                              uint32_t end_bit, void *tmp, size_t *tmp_bytes, hipStream_t st);
 hipError_t launch_class_commit(const DevResult *res, const uint64_t *cmask, const uint32_t *slot_pos, uint32_t *cnt,
                                uint32_t npos, uint32_t lo, uint32_t hi, hipStream_t st);

@@ -1140,7 +1140,7 @@ __global__ __launch_bounds__(SP_THREADS) void replica_keys_kernel(SpreadArgs a, 
     // upstream's tie-break, without the slot in the key
     if (slot != SLOT_NONE) {
       r.keys[slot] = key;
-      r.pos[slot] = pos;
+      r.val[slot] = (uint64_t)slot << 32 | pos;
     }
   }
   if (__syncthreads_or(ovf ? 1 : 0) && threadIdx.x == 0) atomicOr(&r.ctl[1], 1u);
@@ -1161,7 +1161,9 @@ __global__ __launch_bounds__(SP_THREADS) void replica_groups_kernel(SpreadArgs a
   }
 }
 
-constexpr int RUN_THREADS = 1024;  // thread g owns group g, thread t the run's t-th taken node
+// 512 threads: 256 VGPRs per lane, so the prefetched rows need no scratch
+// (a spill reload waits for every outstanding load, store and atomic)
+constexpr int RUN_THREADS = 512;  // thread g owns group g, thread t the run's t-th taken node
 static_assert(RUN_GROUPS == (uint32_t)RUN_THREADS && RUN_TOUCHED == (uint32_t)RUN_THREADS, "one group / node per thread");
 
 // Workgroup barrier for LDS hand-offs only (__syncthreads() also waits for the
@@ -1191,7 +1193,6 @@ struct RunRow {
   int64_t ac, am, rc, rm, zc, zm;
   uint64_t pk;  // the filter pass's packed score parts (raw TaintToleration / NodeAffinity)
   int32_t ap, np;
-  uint32_t slot;
 };
 __device__ __forceinline__ RunRow run_row(const SpreadArgs &a, uint32_t pos) {
   RunRow w;
@@ -1204,7 +1205,6 @@ __device__ __forceinline__ RunRow run_row(const SpreadArgs &a, uint32_t pos) {
   w.pk = a.part[pos];
   w.ap = a.t.apods[pos];
   w.np = a.t.npods[pos];
-  w.slot = a.pos_slot[pos];
   return w;
 }
 
@@ -1287,15 +1287,19 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
   const bool g_on = tid < G;
   uint32_t g_i = g_on ? s_gs[tid] : 0u;
   const uint32_t g_end = tid + 1 < G ? s_gs[tid + 1] : F;
-  // (head: key, position, row; next: key, position), so a new head's row is
-  // requested as soon as the old one wins
-  uint64_t g_key = g_on ? r.sorted[g_i] : 0ull;
-  uint32_t g_pos = g_on ? r.spos[g_i] : 0u;
-  const bool has1 = g_on && g_i + 1 < g_end;
-  uint64_t g_nkey = has1 ? r.sorted[g_i + 1] : 0ull;
-  uint32_t g_npos = has1 ? r.spos[g_i + 1] : 0u;
-  RunRow g_row{};
-  if (g_on) g_row = run_row(a, g_pos);
+  // (head: key, slot << 32 | position, row; next: key, value).  The argmax
+  // reads only the head's key and value, which change by register moves at a
+  // win.  Every thread reloads its head's row and its next key / value at the
+  // end of every pod, at clamped indices, with no branch (a load under a
+  // branch leaves a phi copy at the join that waits for it); only a winner
+  // reads them, a pod later.  A head is untaken: no commit of the run writes
+  // its row.
+  const uint32_t g_last = g_on ? g_end - 1 : 0u;
+  uint64_t g_key = r.sorted[g_on ? g_i : 0u];
+  uint64_t g_val = r.sval[g_on ? g_i : 0u];
+  uint64_t g_nkey = r.sorted[min(g_i + 1, g_last)];
+  uint64_t g_nval = r.sval[min(g_i + 1, g_last)];
+  RunRow g_row = run_row(a, (uint32_t)g_val);
   const uint32_t smask = (1u << r.s_bits) - 1;
   const uint32_t g_code = (uint32_t)(g_key >> r.s_bits) & 0xFFFFFu;
   // raw Score of the group (kept; recomputed when its domain's count moves)
@@ -1331,6 +1335,14 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
     next = r.end;
   } else {
     const uint64_t tt_max = s_tot.tt_max, na_max = s_tot.na_max;
+    uint64_t ph[3] = {0, 0, 0}, t0 = r.prof ? __builtin_readcyclecounter() : 0;  // phase clocks (thread 0)
+    auto clock = [&](int q) {
+      if (r.prof && tid == 0) {
+        const uint64_t t1 = __builtin_readcyclecounter();
+        ph[q] += t1 - t0;
+        t0 = t1;
+      }
+    };
     for (uint32_t pod = a.pod; pod < r.end; ++pod) {
       // raw Scores the last commit moved; min / max raw over the non-ignored
       // feasible nodes
@@ -1359,6 +1371,7 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
         mn = min(mn, s_mn[w]);
         mx = max(mx, s_mx[w]);
       }
+      clock(0);
       const int64_t pmin = (int64_t)mn, pmax = (int64_t)mx;
       const double pinv = pmax ? 1.0 / (double)pmax : 0.0;
       auto total_of = [&](uint32_t S, uint32_t code, uint64_t raw) -> int64_t {
@@ -1367,27 +1380,24 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
         return (int64_t)S + (int64_t)a.w_pts * norm;
       };
       uint64_t gk = 0, tk = 0;
-      if (g_live) gk = pack_key(total_of(smask - (uint32_t)(g_key & smask), g_code, graw), g_row.slot);
+      if (g_live) gk = pack_key(total_of(smask - (uint32_t)(g_key & smask), g_code, graw), (uint32_t)(g_val >> 32));
       if (t_on) tk = pack_key(total_of(t_S, t_code, traw), t_slot);
       uint64_t b = wave_max_u64_dpp(gk > tk ? gk : tk);
       if (lane == 0) s_bk[wid] = b;
       run_barrier();
       for (int w = 0; w < RUN_THREADS / WAVE; ++w) b = s_bk[w] > b ? s_bk[w] : b;
-      // a group's head won: it joins the taken nodes (owner: thread T); the
-      // next node becomes the head, its row is requested, the one after it named
+      clock(1);
+      // a group's head won: it joins the taken nodes (owner: thread T) and
+      // the next node becomes the head
       if (g_live && gk == b) {
         s_ctl[4] = 1;
-        s_ctl[5] = g_row.slot;
+        s_ctl[5] = (uint32_t)(g_val >> 32);
         s_ctl[6] = g_code;
-        s_ctl[7] = g_pos;
+        s_ctl[7] = (uint32_t)g_val;
         s_trow[T] = g_row;
         ++g_i;
         g_key = g_nkey;
-        g_pos = g_npos;
-        if (g_i < g_end) g_row = run_row(a, g_pos);
-        const bool more = g_i + 1 < g_end;
-        g_nkey = more ? r.sorted[g_i + 1] : 0ull;
-        g_npos = more ? r.spos[g_i + 1] : 0u;
+        g_val = g_nval;
       }
       run_barrier();
       const bool from_group = s_ctl[4] != 0;
@@ -1448,13 +1458,21 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
         res.flags = F == 1 ? 1u : 0u;  // KS_RESULT_SINGLE_FEASIBLE
         a.results[pod] = res;
       }
+      g_row = run_row(a, (uint32_t)g_val);
+      g_nkey = r.sorted[min(g_i + 1, g_last)];
+      g_nval = r.sval[min(g_i + 1, g_last)];
       run_barrier();
+      clock(2);
       T += from_group ? 1u : 0u;
       next = pod + 1;
       stop = s_ctl[3];
       if (stop == RUN_END && T == RUN_TOUCHED && next < r.end) stop = RUN_FULL;
       if (tid == 0) s_ctl[4] = 0;  // every thread read it before the barrier
       if (stop != RUN_END) break;
+    }
+    if (r.prof && tid == 0) {
+      for (int q = 0; q < 3; ++q) r.prof[q] += ph[q];
+      r.prof[3] += next - a.pod;
     }
   }
   if (tid == 0) {
@@ -1540,7 +1558,7 @@ hipError_t launch_replica_run(const SpreadArgs &a, const ReplicaArgs &r, void *s
   spread_filter_kernel<false><<<blocks, SP_THREADS, 0, st>>>(a);
   replica_keys_kernel<<<blocks, SP_THREADS, 0, st>>>(a, r);
   size_t bytes = sort_tmp_bytes;
-  if ((e = launch_sort_pairs(r.keys, r.sorted, r.pos, r.spos, r.nslots, 20 + r.s_bits, sort_tmp, &bytes, st)) !=
+  if ((e = launch_sort_pairs(r.keys, r.sorted, r.val, r.sval, r.nslots, 20 + r.s_bits, sort_tmp, &bytes, st)) !=
       hipSuccess)
     return e;
   replica_groups_kernel<<<blocks, SP_THREADS, 0, st>>>(a, r);
