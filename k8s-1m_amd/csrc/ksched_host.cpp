@@ -515,6 +515,10 @@ struct ks_ctx {
   // replica runs: sort keys and positions, group starts, control
   // words (ReplicaArgs::ctl; pinned copy), radix-sort scratch
   bool replica_runs = true;
+  // ks_batch_prepare compiling while submitted batches may run: creating a
+  // topology / selector-class / term / extended-resource column is refused
+  // (KS_NEED_DRAIN), the caller drains and compiles again
+  bool undrained = false;
   uint64_t *d_rk_keys = nullptr, *d_rk_sorted = nullptr;
   uint64_t *d_rk_val = nullptr, *d_rk_sval = nullptr;
   uint32_t *d_rk_gstart = nullptr, *d_rk_ctl = nullptr;
@@ -602,6 +606,10 @@ struct ks_ctx {
     return st;
   }
 };
+
+// Internal (never returned through the ABI): a compile that must create a
+// column while batches may be running; ks_batch_prepare drains and retries.
+constexpr ks_status KS_NEED_DRAIN = (ks_status)0x7F;
 
 #define HIPC(ctx, x)                                                                           \
   do {                                                                                         \
@@ -1507,6 +1515,7 @@ ks_status xres_column(ks_ctx *c, uint32_t name, bool create, uint32_t *out) {
     *out = UINT32_MAX;
     return KS_OK;
   }
+  if (c->undrained) return KS_NEED_DRAIN;
   if (c->xres_names.size() >= (size_t)MAX_XRES)
     return c->fail(KS_ERR_UNSUPPORTED, "more than %d extended resource names (%s)", MAX_XRES, c->strs[name].c_str());
   if (!c->d_xalloc) {
@@ -1818,6 +1827,7 @@ ks_status spread_scratch(ks_ctx *c, uint32_t need) {
 
 ks_status spread_alloc(ks_ctx *c) {
   if (c->d_dom) return KS_OK;
+  if (c->undrained) return KS_NEED_DRAIN;
   ks_status st;
   // domain columns then class columns, one allocation (one index space for scatters)
   if ((st = dalloc(c, &c->d_dom, (size_t)(MAX_TOPO_KEYS + MAX_CLASSES) * c->npos)) || (st = dalloc(c, &c->d_pos_slot, c->npos)) ||
@@ -1885,6 +1895,7 @@ ks_status topo_column(ks_ctx *c, uint32_t key, bool create, uint32_t *out) {
     *out = 0;
     return KS_OK;
   }
+  if (c->undrained) return KS_NEED_DRAIN;
   if (c->topo.size() >= (size_t)MAX_TOPO_KEYS)
     return c->fail(KS_ERR_CAPACITY, "more than %d topology keys in spread constraints", MAX_TOPO_KEYS);
   ks_status st;
@@ -1914,6 +1925,7 @@ ks_status class_get(ks_ctx *c, std::vector<Clause> &&clauses, bool create, uint3
     *out = CLS_NONE;
     return KS_OK;
   }
+  if (c->undrained) return KS_NEED_DRAIN;
   ks_status st;
   if ((st = spread_alloc(c))) return st;
   flush_bound(c);  // the column counts every bound pod
@@ -2063,6 +2075,7 @@ ks_status term_get(ks_ctx *c, const ks_pod &p, const ks_pod_affinity_term &t, bo
     *out = UINT32_MAX;
     return KS_OK;
   }
+  if (c->undrained) return KS_NEED_DRAIN;
   int slot = -1;
   for (int i = 0; i < MAX_TERM_CLASSES && slot < 0; ++i)
     if (!c->terms[i].live) slot = i;
@@ -4140,6 +4153,7 @@ static ks_status compile_batch(ks_ctx *c, const ks_pod *pods, uint32_t n, PodDev
     lk.unlock();
     drain_async(c);
     lk.lock();
+    c->undrained = false;  // drained: the retry may create columns
     reset_label_dict(c);
   }
 }
@@ -4172,40 +4186,59 @@ ks_status ks_batch_prepare(ks_ctx *c, const ks_pod *pods, uint32_t n, ks_batch *
   bool ext = false, norm = false;
   uint32_t dict_v, names_v;
   ks_status st;
-  // Spread pods may create topology / selector-class columns, computed from the
-  // host's records of bound pods: let every submitted batch finish first.
+  // Spread pods may create topology / selector-class / term columns, computed
+  // from the host's records of bound pods, which needs every submitted batch
+  // finished.  The compile first runs without waiting and refuses to create
+  // any (KS_NEED_DRAIN): a running deployment's batches reference columns
+  // that exist, and their compile overlaps the batch in flight.  Otherwise it
+  // drains and compiles again.
   bool any_solo = false;
   {
     std::lock_guard<std::mutex> g(c->mu);
     for (uint32_t i = 0; i < n && !any_solo; ++i) any_solo = may_need_solo(c, pods[i]);
   }
+  bool drained = !any_solo;
+  if (!drained) {
+    std::lock_guard<std::mutex> q(c->qmu);
+    drained = c->inflight == 0;
+  }
   const auto tp0 = std::chrono::steady_clock::now();
-  if (any_solo) drain_async(c);
-  const auto tp1 = std::chrono::steady_clock::now();
+  auto tp1 = tp0;
   std::vector<uint32_t> set_ids(n), refs, term_refs;
-  {
-    // compile against the host dictionaries (the worker reads t.lw and the
-    // dirty label rows under mu)
-    std::unique_lock<std::mutex> g(c->mu);
-    // label sets first: they create the term classes of the pods' own terms,
-    // which every later pod of the batch that they select must see
-    st = KS_OK;
-    for (uint32_t i = 0; i < n && !st; ++i) st = intern_set(c, pods[i], &set_ids[i], &term_refs);
-    if (st) {
-      for (uint32_t t : term_refs) term_activate(c, t, 0, -1);
-      return st;
+  for (;;) {
+    {
+      // compile against the host dictionaries (the worker reads t.lw and the
+      // dirty label rows under mu)
+      std::unique_lock<std::mutex> g(c->mu);
+      c->undrained = !drained;
+      // label sets first: they create the term classes of the pods' own terms,
+      // which every later pod of the batch that they select must see
+      st = KS_OK;
+      for (uint32_t i = 0; i < n && !st; ++i) st = intern_set(c, pods[i], &set_ids[i], &term_refs);
+      if (!st) st = compile_batch(c, pods, n, dev.data(), cl, g, true, &refs);
+      c->undrained = false;
+      if (st) {
+        for (uint32_t t : term_refs) term_activate(c, t, 0, -1);
+        class_release(c, &refs);
+        if (st != KS_NEED_DRAIN) return st;
+        term_refs.clear();
+        set_ids.assign(n, 0);
+        dev.assign(std::max<uint32_t>(n, 1), PodDev{});
+        cl = ProgBuf();
+      } else {
+        for (uint32_t i = 0; i < n; ++i) {
+          if (dev[i].flags & PF_SOLO) continue;  // the one-pod path evaluates it
+          if (dev[i].flags & PF_EXT) ext = true;
+          if (dev[i].flags & (PF_TT | PF_NA)) norm = true;
+        }
+        dict_v = c->dict_version;
+        names_v = c->compile_used_names ? c->names_version : 0;
+      }
     }
-    if ((st = compile_batch(c, pods, n, dev.data(), cl, g, true, &refs))) {
-      for (uint32_t t : term_refs) term_activate(c, t, 0, -1);
-      return st;
-    }
-    for (uint32_t i = 0; i < n; ++i) {
-      if (dev[i].flags & PF_SOLO) continue;  // the one-pod path evaluates it
-      if (dev[i].flags & PF_EXT) ext = true;
-      if (dev[i].flags & (PF_TT | PF_NA)) norm = true;
-    }
-    dict_v = c->dict_version;
-    names_v = c->compile_used_names ? c->names_version : 0;
+    if (st != KS_NEED_DRAIN) break;
+    drain_async(c);
+    drained = true;
+    tp1 = std::chrono::steady_clock::now();
   }
   const auto tp2 = std::chrono::steady_clock::now();
   if (norm) ext = true;
