@@ -56,7 +56,7 @@ case $JOB in
     timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1
     rc=$?; cat gpurun_out/smoke_$TAG.log; exit $rc ;;
   lines)
-    for l in ${1:-c3 c4 c2 kwok kwokbe c5 spread affinity}; do
+    for l in ${1:-c3 c4 c2 kwok kwokbe c5 spread deploy affinity}; do
       args=$(line_args $l) || exit 1
       timeout -k 10 420 python -u bench.py $args > gpurun_out/bench_${TAG}_$l.json 2> gpurun_out/bench_${TAG}_$l.err
       rc=$?; echo "$l rc=$rc $(summary gpurun_out/bench_${TAG}_$l.json $l)"
