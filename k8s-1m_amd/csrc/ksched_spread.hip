@@ -1269,16 +1269,25 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
   // topologyNormalizingWeight per constraint (spread_score)
   const double w_h = k.ch < (uint32_t)MAX_SPREAD ? go_log((double)(F - s_tot.ignored) + 2.0) : 0.0;
   const double w_z = k.cz < (uint32_t)MAX_SPREAD ? go_log((double)a.acc->topo_size[k.cz] + 2.0) : 0.0;
-  // raw Score of a group code (spread_score: constraints in order, math.Round)
+  // raw Score of a group code (spread_score: the constraints in their order,
+  // each adding cnt x weight + (maxSkew - 1), math.Round); at most one of
+  // each kind, so the order is one flag
+  const bool host_first = k.ch < k.cz;
+  const double ms_h = k.ch < (uint32_t)MAX_SPREAD ? (double)(s_sd[k.ch].max_skew - 1) : 0.0;
+  const double ms_z = k.cz < (uint32_t)MAX_SPREAD ? (double)(s_sd[k.cz].max_skew - 1) : 0.0;
   auto raw_of = [&](uint32_t code) -> uint64_t {
     const uint32_t dz = (code >> 8) & RK_DZ_NONE, hk = code & RK_HK_NONE;
+    const bool th = k.ch < (uint32_t)MAX_SPREAD && hk != RK_HK_NONE;
+    const bool tz = k.cz < (uint32_t)MAX_SPREAD && dz != RK_DZ_NONE;
+    const double xh = (double)hk * w_h + ms_h;
+    const double xz = tz ? (double)s_dz[dz] * w_z + ms_z : 0.0;
     double s = 0;
-    for (uint32_t c = 0; c < n; ++c) {
-      if (c == k.ch) {
-        if (hk != RK_HK_NONE) s += (double)hk * w_h + (double)(s_sd[c].max_skew - 1);
-      } else if (dz != RK_DZ_NONE) {
-        s += (double)s_dz[dz] * w_z + (double)(s_sd[c].max_skew - 1);
-      }
+    if (host_first) {
+      if (th) s += xh;
+      if (tz) s += xz;
+    } else {
+      if (tz) s += xz;
+      if (th) s += xh;
     }
     return (uint64_t)(int64_t)round(s);
   };

@@ -264,6 +264,38 @@ def test_spread_1m_replay():
     o.close()
 
 
+def test_deploy_1m_replay():
+    # the deploy bench's workload: deployments of 256 identical replicas under
+    # the system default spread constraints on the 1M-node zoned cluster, all
+    # in replica runs; the oracle replays every decision and
+    # schedules windows at a run's first pod, inside runs and at the end
+    n_pods = 2048
+    nodes = synth.nodes(synth.ZONED, N, 1)
+    slots = synth.slot_array(N)
+    pf = synth.prefill(synth.ZONED, N, 1, 3, 0.5)
+    dep = synth.deploy_pods(n_pods, 256, 5)
+    s = Scheduler(N)
+    s.upsert_nodes_raw(nodes.nodes, slots, N)
+    assert s.lib.ks_pods_add(s.ctx, pf.pods, pf.slot_ptr, pf.n_pods) == 0
+    b = s.prepare(dep.pods, n_pods)
+    s.run(b)
+    got = s.results(b, n_pods)
+    s.free(b)
+    st = _abi.KsStats()
+    assert s.lib.ks_get_stats(s.ctx, C.byref(st)) == 0
+    assert st.replica_pods == n_pods and st.replica_runs >= n_pods // 256
+    o = pyoracle.Oracle(N, threads=ORACLE_THREADS)
+    o.upsert(nodes.nodes, slots, N)
+    o.add_pods(pf.pods, pf.slot_ptr, pf.n_pods)
+    replay_check(o, dep, got, n_pods, windows=(0, 130, 512, 1201, n_pods - 4), wlen=4)
+    sg = states_np(s.lib.ks_node_states, s.ctx, N)
+    sw = states_np(o.L.oracle_node_states, o.o, N)
+    assert np.array_equal(sg, sw), "node tables differ after replaying every decision"
+    assert (res_array(got, n_pods)["status"] == 0).all()
+    s.close()
+    o.close()
+
+
 def test_affinity_1m_replay():
     # the affinity bench's cluster with InterPodAffinity deployment pods
     # interleaved with plain pods: term classes of the batch's own pods
