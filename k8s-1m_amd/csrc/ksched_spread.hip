@@ -1216,8 +1216,8 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
   __shared__ uint64_t s_mn[RUN_THREADS / WAVE], s_mx[RUN_THREADS / WAVE], s_bk[RUN_THREADS / WAVE];
   __shared__ uint32_t s_cls[MAX_CLASSES];   // selector classes the pods match (commit: +1 each)
   // 0 groups, 1 refused, 2 classes, 3 RunStop, 4 a group's node won, 5 its slot, 6 its group code,
-  // 7 its position, 8 the domain whose count the last commit raised (RK_DZ_NONE: none)
-  __shared__ uint32_t s_ctl[9];
+  // 7 its position, 8 the domain whose count the last commit raised (RK_DZ_NONE: none), 9 its S
+  __shared__ uint32_t s_ctl[10];
   const uint32_t tid = threadIdx.x, lane = tid % WAVE, wid = tid / WAVE;
   const PodDev p = a.pods[a.pod];  // every pod of the run is identical (host-checked)
   const uint32_t n = spread_count(a, p);
@@ -1343,8 +1343,7 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
     if (tid == 0) a.counters[1] += r.end - a.pod;
     next = r.end;
   } else {
-    const uint64_t tt_max = s_tot.tt_max, na_max = s_tot.na_max;
-    uint64_t ph[3] = {0, 0, 0}, t0 = r.prof ? __builtin_readcyclecounter() : 0;  // phase clocks (thread 0)
+    uint64_t ph[5] = {0, 0, 0, 0, 0}, t0 = r.prof ? __builtin_readcyclecounter() : 0;  // phase clocks (thread 0)
     auto clock = [&](int q) {
       if (r.prof && tid == 0) {
         const uint64_t t1 = __builtin_readcyclecounter();
@@ -1403,12 +1402,14 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
         s_ctl[5] = (uint32_t)(g_val >> 32);
         s_ctl[6] = g_code;
         s_ctl[7] = (uint32_t)g_val;
+        s_ctl[9] = smask - (uint32_t)(g_key & smask);
         s_trow[T] = g_row;
         ++g_i;
         g_key = g_nkey;
         g_val = g_nval;
       }
       run_barrier();
+      clock(2);
       const bool from_group = s_ctl[4] != 0;
       bool mine = !from_group && t_on && tk == b;
       if (from_group && tid == T) {
@@ -1417,7 +1418,9 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
         t_code = s_ctl[6];
         t_pos = s_ctl[7];
         const RunRow &w = s_trow[tid];
-        t_stat = run_static(p, a.w, w.pk & ~0xFFFFFFFFull, (int64_t)tt_max, (int64_t)na_max);
+        // S less its LeastAllocated / BalancedAllocation part (the packed low
+        // word): the normalised TaintToleration / NodeAffinity terms
+        t_stat = s_ctl[9] - (uint32_t)w.pk;
         s_tinv[tid][0] = w.ac ? 1.0 / (double)w.ac : 0.0;  // as make_regs
         s_tinv[tid][1] = w.am ? 1.0 / (double)w.am : 0.0;
       }
@@ -1467,11 +1470,12 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
         res.flags = F == 1 ? 1u : 0u;  // KS_RESULT_SINGLE_FEASIBLE
         a.results[pod] = res;
       }
+      clock(3);
       g_row = run_row(a, (uint32_t)g_val);
       g_nkey = r.sorted[min(g_i + 1, g_last)];
       g_nval = r.sval[min(g_i + 1, g_last)];
       run_barrier();
-      clock(2);
+      clock(4);
       T += from_group ? 1u : 0u;
       next = pod + 1;
       stop = s_ctl[3];
@@ -1480,8 +1484,8 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
       if (stop != RUN_END) break;
     }
     if (r.prof && tid == 0) {
-      for (int q = 0; q < 3; ++q) r.prof[q] += ph[q];
-      r.prof[3] += next - a.pod;
+      for (int q = 0; q < 5; ++q) r.prof[q] += ph[q];
+      r.prof[5] += next - a.pod;
     }
   }
   if (tid == 0) {
