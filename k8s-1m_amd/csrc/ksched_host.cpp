@@ -3531,9 +3531,9 @@ void ks_close(ks_ctx *c) {
     const uint64_t *h = c->rk_prof;
     const double n = (double)h[5];
     std::fprintf(stderr,
-                 "ksched replica runs: %llu pods; cycles per pod: min/max raw %.0f, argmax %.0f, hand-off %.0f, "
-                 "commit %.0f, reloads + barrier %.0f\n",
-                 (unsigned long long)h[5], h[0] / n, h[1] / n, h[2] / n, h[3] / n, h[4] / n);
+                 "ksched replica runs: %llu pods; cycles per pod: min/max raw %.0f, argmax %.0f, commit (thread 0) "
+                 "%.0f, reloads + barrier %.0f\n",
+                 (unsigned long long)h[5], h[0] / n, h[1] / n, h[2] / n, h[3] / n);
   }
   if (c->ev_profile)
     for (int k = 0; k < 4; ++k)

@@ -1215,9 +1215,10 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
   __shared__ uint32_t s_gs[RUN_GROUPS];     // group starts, ascending
   __shared__ uint64_t s_mn[RUN_THREADS / WAVE], s_mx[RUN_THREADS / WAVE], s_bk[RUN_THREADS / WAVE];
   __shared__ uint32_t s_cls[MAX_CLASSES];   // selector classes the pods match (commit: +1 each)
-  // 0 groups, 1 refused, 2 classes, 3 RunStop, 4 a group's node won, 5 its slot, 6 its group code,
-  // 7 its position, 8 the domain whose count the last commit raised (RK_DZ_NONE: none), 9 its S
-  __shared__ uint32_t s_ctl[10];
+  // 0 groups, 1 refused, 2 classes, 3 RunStop, 4 taken nodes, 5-7 a head that joined them: slot,
+  // position, group code, 8 the domain whose count the last commit raised (RK_DZ_NONE: none),
+  // 9-10 the head's static terms and S after its commit
+  __shared__ uint32_t s_ctl[11];
   const uint32_t tid = threadIdx.x, lane = tid % WAVE, wid = tid / WAVE;
   const PodDev p = a.pods[a.pod];  // every pod of the run is identical (host-checked)
   const uint32_t n = spread_count(a, p);
@@ -1395,69 +1396,64 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
       run_barrier();
       for (int w = 0; w < RUN_THREADS / WAVE; ++w) b = s_bk[w] > b ? s_bk[w] : b;
       clock(1);
-      // a group's head won: it joins the taken nodes (owner: thread T) and
-      // the next node becomes the head
-      if (g_live && gk == b) {
-        s_ctl[4] = 1;
-        s_ctl[5] = (uint32_t)(g_val >> 32);
-        s_ctl[6] = g_code;
-        s_ctl[7] = (uint32_t)g_val;
-        s_ctl[9] = smask - (uint32_t)(g_key & smask);
-        s_trow[T] = g_row;
-        ++g_i;
-        g_key = g_nkey;
-        g_val = g_nval;
-      }
-      run_barrier();
-      clock(2);
-      const bool from_group = s_ctl[4] != 0;
-      bool mine = !from_group && t_on && tk == b;
-      if (from_group && tid == T) {
-        t_on = mine = true;
-        t_slot = s_ctl[5];
-        t_code = s_ctl[6];
-        t_pos = s_ctl[7];
-        const RunRow &w = s_trow[tid];
-        // S less its LeastAllocated / BalancedAllocation part (the packed low
-        // word): the normalised TaintToleration / NodeAffinity terms
-        t_stat = s_ctl[9] - (uint32_t)w.pk;
-        s_tinv[tid][0] = w.ac ? 1.0 / (double)w.ac : 0.0;  // as make_regs
-        s_tinv[tid][1] = w.am ? 1.0 / (double)w.am : 0.0;
-      }
-      if (mine) {
-        RunRow &t_row = s_trow[tid];
-        // AssumePod (spread_commit): Requested, NonZeroRequested, pod count, class columns
-        t_row.rc += p.req_cpu;
-        t_row.rm += p.req_mem;
-        t_row.zc += p.nz_cpu;
-        t_row.zm += p.nz_mem;
-        t_row.np += 1;
-        a.t.rcpu[t_pos] = t_row.rc;
-        a.t.rmem[t_pos] = t_row.rm;
-        a.t.zcpu[t_pos] = t_row.zc;
-        a.t.zmem[t_pos] = t_row.zm;
-        a.t.npods[t_pos] = t_row.np;
+      // The winner commits (AssumePod as spread_commit): a group's head from
+      // its row in registers (the node joins the taken nodes as node T: its
+      // state goes to LDS and thread T adopts it after the barrier, the group's
+      // next node becomes the head), or a taken node, by its owner.
+      const bool gwin = g_live && gk == b, twin = !gwin && t_on && tk == b;
+      if (gwin || twin) {
+        RunRow w;
+        uint32_t slot, pos, code, stat;
+        double ic, im;
+        if (gwin) {
+          w = g_row;
+          slot = (uint32_t)(g_val >> 32);
+          pos = (uint32_t)g_val;
+          code = g_code;
+          // S less its LeastAllocated / BalancedAllocation part (the packed
+          // low word): the normalised TaintToleration / NodeAffinity terms
+          stat = (smask - (uint32_t)(g_key & smask)) - (uint32_t)w.pk;
+          ic = w.ac ? 1.0 / (double)w.ac : 0.0;  // as make_regs
+          im = w.am ? 1.0 / (double)w.am : 0.0;
+        } else {
+          w = s_trow[tid];
+          slot = t_slot;
+          pos = t_pos;
+          code = t_code;
+          stat = t_stat;
+          ic = s_tinv[tid][0];
+          im = s_tinv[tid][1];
+        }
+        // Requested, NonZeroRequested, pod count, class columns
+        w.rc += p.req_cpu;
+        w.rm += p.req_mem;
+        w.zc += p.nz_cpu;
+        w.zm += p.nz_mem;
+        w.np += 1;
+        a.t.rcpu[pos] = w.rc;
+        a.t.rmem[pos] = w.rm;
+        a.t.zcpu[pos] = w.zc;
+        a.t.zmem[pos] = w.zm;
+        a.t.npods[pos] = w.np;
         // no returned value: the stores leave without a round trip on the pod's path
-        for (uint32_t q = 0; q < s_ctl[2]; ++q) atomicAdd(&a.cnt[(size_t)s_cls[q] * a.npos + t_pos], 1u);
+        for (uint32_t q = 0; q < s_ctl[2]; ++q) atomicAdd(&a.cnt[(size_t)s_cls[q] * a.npos + pos], 1u);
         // the next pod's view of the node: own hostname count, its domain's count, S, Fit
-        if (inc_h && (t_code & RK_HK_NONE) != RK_HK_NONE) {
-          t_code += 1;
-          if ((t_code & RK_HK_NONE) == RK_HK_NONE) s_ctl[3] = RUN_FULL;  // beyond the key's range
+        if (inc_h && (code & RK_HK_NONE) != RK_HK_NONE) {
+          code += 1;
+          if ((code & RK_HK_NONE) == RK_HK_NONE) s_ctl[3] = RUN_FULL;  // beyond the key's range
         }
         uint32_t moved = RK_DZ_NONE;
-        if (inc_z && !(t_code & RK_IGN)) {
-          const uint32_t dz = (t_code >> 8) & RK_DZ_NONE;
+        if (inc_z && !(code & RK_IGN)) {
+          const uint32_t dz = (code >> 8) & RK_DZ_NONE;
           moved = dz == RK_DZ_NONE ? 0u : dz;  // PreScore counts a node lacking the key in ""
           s_dz[moved] += 1;
         }
         s_ctl[8] = moved;
-        t_dirty = true;
-        const NodeRegs g = make_regs_inv(t_row.ac, t_row.am, t_row.rc, t_row.rm, t_row.zc, t_row.zm, t_row.ap,
-                                         t_row.np, t_slot, s_tinv[tid][0], s_tinv[tid][1]);
-        t_S = (uint32_t)a.w.fit * (uint32_t)score_la(p, g) + (uint32_t)a.w.ba * (uint32_t)score_ba(p, g) + t_stat;
+        const NodeRegs g = make_regs_inv(w.ac, w.am, w.rc, w.rm, w.zc, w.zm, w.ap, w.np, slot, ic, im);
+        const uint32_t S = (uint32_t)a.w.fit * (uint32_t)score_la(p, g) + (uint32_t)a.w.ba * (uint32_t)score_ba(p, g) + stat;
         if (filter<false>(p, a.clauses, g, NodeExt{}) != ST_FEASIBLE) s_ctl[3] = RUN_FIT;
         DevResult res;
-        res.node_index = (int32_t)t_slot;
+        res.node_index = (int32_t)slot;
         res.status = 0;
         res.total_score = (int64_t)(b >> 32) - 1;
         res.feasible_nodes = F;
@@ -1469,18 +1465,46 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
         res.prefiltered = p.prefilter_out;
         res.flags = F == 1 ? 1u : 0u;  // KS_RESULT_SINGLE_FEASIBLE
         a.results[pod] = res;
+        const uint32_t j = gwin ? T : tid;
+        s_trow[j] = w;
+        if (gwin) {
+          s_tinv[j][0] = ic;
+          s_tinv[j][1] = im;
+          s_ctl[5] = slot;
+          s_ctl[6] = pos;
+          s_ctl[7] = code;
+          s_ctl[9] = stat;
+          s_ctl[10] = S;
+          s_ctl[4] = T + 1;  // taken nodes
+          ++g_i;
+          g_key = g_nkey;
+          g_val = g_nval;
+        } else {
+          t_code = code;
+          t_S = S;
+          t_dirty = true;
+        }
       }
-      clock(3);
+      clock(2);
       g_row = run_row(a, (uint32_t)g_val);
       g_nkey = r.sorted[min(g_i + 1, g_last)];
       g_nval = r.sval[min(g_i + 1, g_last)];
       run_barrier();
-      clock(4);
-      T += from_group ? 1u : 0u;
+      clock(3);
+      if (s_ctl[4] != T) {  // a head joined the taken nodes: thread T owns it
+        if (tid == T) {
+          t_on = t_dirty = true;
+          t_slot = s_ctl[5];
+          t_pos = s_ctl[6];
+          t_code = s_ctl[7];
+          t_stat = s_ctl[9];
+          t_S = s_ctl[10];
+        }
+        ++T;
+      }
       next = pod + 1;
       stop = s_ctl[3];
       if (stop == RUN_END && T == RUN_TOUCHED && next < r.end) stop = RUN_FULL;
-      if (tid == 0) s_ctl[4] = 0;  // every thread read it before the barrier
       if (stop != RUN_END) break;
     }
     if (r.prof && tid == 0) {
