@@ -526,7 +526,7 @@ struct ks_ctx {
   size_t rk_tmp_bytes = 0;
   uint32_t *h_rk_ctl = nullptr;
   uint64_t *d_rk_prof = nullptr;  // KS_RUN_PROFILE: replica_run phase clocks (ReplicaArgs::prof)
-  uint64_t rk_prof[6] = {0, 0, 0, 0, 0, 0};  // ... their totals after the last run
+  uint64_t rk_prof[4] = {0, 0, 0, 0};  // ... their totals after the last run
   uint32_t *h_seg = nullptr;       // pinned: start pod of a round-kernel segment
   // comm: RCCL, or an in-process group of contexts (tests of the multi-rank path on one GPU)
   ncclComm_t comm = nullptr;
@@ -3033,7 +3033,7 @@ ks_status replica_run(ks_ctx *c, ks_batch *b, SpreadArgs sa, uint32_t lo, uint32
         (st = dalloc(c, &c->d_rk_val, c->npos)) || (st = dalloc(c, &c->d_rk_sval, c->npos)) ||
         (st = dalloc(c, &c->d_rk_gstart, RUN_GROUPS)) || (st = dalloc(c, &c->d_rk_ctl, 4)) ||
         (st = dalloc(c, &c->d_rk_tmp, std::max<size_t>(bytes, 16))) ||
-        (c->run_profile && (st = dalloc(c, &c->d_rk_prof, 6))))
+        (c->run_profile && (st = dalloc(c, &c->d_rk_prof, 4))))
       return st;
     c->rk_tmp_bytes = bytes;
     HIPC(c, hipHostMalloc((void **)&c->h_rk_ctl, 16, hipHostMallocDefault));
@@ -3527,13 +3527,11 @@ void ks_close(ks_ctx *c) {
                  "upload %.3f s\n",
                  c->prof[3], c->prof[0], c->prof[1], c->prof[2], c->prof[6], c->prof[4], c->prof[5], c->prof[7],
                  c->prof[8], c->prof[9]);
-  if (c->run_profile && c->rk_prof[5]) {
+  if (c->run_profile && c->rk_prof[3]) {
     const uint64_t *h = c->rk_prof;
-    const double n = (double)h[5];
-    std::fprintf(stderr,
-                 "ksched replica runs: %llu pods; cycles per pod: min/max raw %.0f, argmax %.0f, commit (thread 0) "
-                 "%.0f, reloads + barrier %.0f\n",
-                 (unsigned long long)h[5], h[0] / n, h[1] / n, h[2] / n, h[3] / n);
+    const double n = (double)h[3];
+    std::fprintf(stderr, "ksched replica runs: %llu pods; cycles per pod: min/max raw %.0f, argmax %.0f, commit %.0f\n",
+                 (unsigned long long)h[3], h[0] / n, h[1] / n, h[2] / n);
   }
   if (c->ev_profile)
     for (int k = 0; k < 4; ++k)

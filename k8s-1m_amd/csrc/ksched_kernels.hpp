@@ -165,7 +165,7 @@ struct ReplicaArgs {
   uint32_t end;             // one past the run's last pod
   uint32_t nslots;          // keys sorted (one per slot)
   uint32_t s_bits;          // bits of the static score (2^s_bits > 100 x the static plugins' weights)
-  uint64_t *prof;           // KS_RUN_PROFILE: [0..4] cycles of the pod loop's phases, [5] pods (null: off)
+  uint64_t *prof;           // KS_RUN_PROFILE: [0..2] cycles of the pod loop's phases, [3] pods (null: off)
 };
 
 hipError_t launch_spread_pod(const SpreadArgs &a, uint32_t passes, hipStream_t st);

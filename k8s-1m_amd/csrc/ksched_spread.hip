@@ -1344,7 +1344,7 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
     if (tid == 0) a.counters[1] += r.end - a.pod;
     next = r.end;
   } else {
-    uint64_t ph[5] = {0, 0, 0, 0, 0}, t0 = r.prof ? __builtin_readcyclecounter() : 0;  // phase clocks (thread 0)
+    uint64_t ph[3] = {0, 0, 0}, t0 = r.prof ? __builtin_readcyclecounter() : 0;  // phase clocks (thread 0)
     auto clock = [&](int q) {
       if (r.prof && tid == 0) {
         const uint64_t t1 = __builtin_readcyclecounter();
@@ -1485,12 +1485,11 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
           t_dirty = true;
         }
       }
-      clock(2);
       g_row = run_row(a, (uint32_t)g_val);
       g_nkey = r.sorted[min(g_i + 1, g_last)];
       g_nval = r.sval[min(g_i + 1, g_last)];
       run_barrier();
-      clock(3);
+      clock(2);  // the commit: the winner's chain, seen as thread 0's wait here
       if (s_ctl[4] != T) {  // a head joined the taken nodes: thread T owns it
         if (tid == T) {
           t_on = t_dirty = true;
@@ -1508,8 +1507,8 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
       if (stop != RUN_END) break;
     }
     if (r.prof && tid == 0) {
-      for (int q = 0; q < 5; ++q) r.prof[q] += ph[q];
-      r.prof[5] += next - a.pod;
+      for (int q = 0; q < 3; ++q) r.prof[q] += ph[q];
+      r.prof[3] += next - a.pod;
     }
   }
   if (tid == 0) {
