@@ -324,7 +324,10 @@ def run_batches(args, kind, sched, world, rank, t_setup):
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_pods > 0:
         cpu = cpu_baseline(args, nodes, slots, pre, pod_stream(args, kind, args.cpu_pods_mt + args.cpu_pods, 7))
-    swept = e2e.pop("pods_swept")
+    # one-pod-path filter passes over every node count too: one per pod of the
+    # per-pod chain and one per replica run; st covers
+    # the timed steps (reset before them)
+    swept = e2e.pop("pods_swept") + int(st.spread_pods - st.replica_pods) + int(st.replica_runs)
     line = report(args, sched, st, dbg, world, e2e.pop("pods_timed"), e2e.pop("elapsed"), e2e.pop("scheduled"),
                   setup_s, cpu, pods_swept=swept)
     line["extra"]["host_compile_ms_per_step"] = e2e["host_compile_ms_per_step"]
@@ -746,7 +749,8 @@ def report(args, sched, st, dbg, world, pods_timed, elapsed, scheduled, setup_s,
             # representatives) / pods in the swept windows, since open
             "sweep_representative_fraction": round(int(dbg[2]) / max(1, int(dbg[2]) + int(dbg[7])), 4),
             # (pod, node) evaluations: the sweeps' actual ones (pods swept x
-            # nodes; identical pods of a round are swept once) and the nominal
+            # nodes; identical pods of a round are swept once; one-pod-path
+            # filter passes: per-pod chain pods + replica runs) and the nominal
             # pods x nodes the metric's "1M node evaluations per pod" counts
             "node_evals_per_s": (round(pods_swept * args.nodes / elapsed, 1) if pods_swept is not None
                                  else round(value * args.nodes, 1)),

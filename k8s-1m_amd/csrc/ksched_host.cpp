@@ -37,6 +37,7 @@
 #include "ksched.h"
 #include "ksched_dev.hpp"
 #include "ksched_kernels.hpp"
+#include "ksched_sync.hpp"
 
 using namespace ks;
 
@@ -302,41 +303,16 @@ struct ks_batch {
 // second rendezvous whose events hold every rank's stream until all peers have
 // read its buffers: the ordering an RCCL collective gives, without RCCL (which
 // refuses two ranks on one GPU).  Test plumbing for the multi-rank path.
-struct LocalGroup {
-  struct Post {
-    hipEvent_t ev = nullptr;
-    const void *ptr = nullptr;
-    std::vector<double> vals;
-  };
-  explicit LocalGroup(uint32_t n) : world(n), posts(n), snap(n) {}
-  uint32_t world;
-  std::mutex mu;
-  std::condition_variable cv;
-  std::vector<Post> posts, snap;
-  uint32_t arrived = 0;
-  uint64_t gen = 0;
-  bool failed = false;  // a rendezvous timed out: the ranks no longer pair up
-  // Post this rank's entry and wait for every rank's; false after 300 s (a
-  // peer failed and will never arrive).  A timeout fails the group for good:
-  // the late rank's post would otherwise pair with the next collective's.
-  bool exchange(uint32_t rank, Post p, std::vector<Post> &out) {
-    std::unique_lock<std::mutex> g(mu);
-    if (failed) return false;
-    posts[rank] = std::move(p);
-    const uint64_t my = gen;
-    if (++arrived == world) {
-      snap = posts;
-      arrived = 0;
-      ++gen;
-      cv.notify_all();
-    } else if (!cv.wait_for(g, std::chrono::seconds(300), [&] { return gen != my || failed; }) || failed) {
-      failed = true;
-      cv.notify_all();
-      return false;
-    }
-    out = snap;
-    return true;
-  }
+struct LgPost {
+  hipEvent_t ev = nullptr;
+  const void *ptr = nullptr;
+  std::vector<double> vals;
+};
+// (the rendezvous itself: ksched_sync.hpp, exercised under TSan / ASan by
+// tools/sync_stress.cpp)
+struct LocalGroup : Rendezvous<LgPost> {
+  using Post = LgPost;
+  explicit LocalGroup(uint32_t n) : Rendezvous<LgPost>(n) {}
 };
 
 struct ks_ctx {
@@ -574,13 +550,9 @@ struct ks_ctx {
   // host dictionaries / node mirror: ks_batch_prepare vs the worker's reads of t.lw
   std::mutex mu;
   std::mutex err_mu;
-  // asynchronous runs (ks_batch_submit / ks_batch_wait)
-  std::thread worker;
-  std::mutex qmu;
-  std::condition_variable qcv, dcv;
-  std::deque<ks_batch *> queue;
-  uint32_t inflight = 0;
-  bool stop = false;
+  // asynchronous runs (ks_batch_submit / ks_batch_wait): one worker thread
+  // (ksched_sync.hpp), created at ks_open
+  std::unique_ptr<RunQueue<ks_batch>> runq;
 
   uint32_t intern(const char *p) {
     std::string s = str(p);
@@ -2647,7 +2619,7 @@ ks_status lg_finish(ks_ctx *c, hipStream_t st) {
   std::vector<LocalGroup::Post> ps;
   ks_status e = lg_exchange(c, {c->lg_ev[1], nullptr, {}}, ps);
   if (e) return e;
-  for (uint32_t j = 0; j < c->lgroup->world; ++j)
+  for (uint32_t j = 0; j < c->lgroup->world(); ++j)
     if (j != c->cfg.rank) HIPC(c, hipStreamWaitEvent(st, ps[j].ev, 0));
   return KS_OK;
 }
@@ -2663,7 +2635,7 @@ ks_status coll_allgather(ks_ctx *c, void *buf, size_t bytes, hipStream_t st) {
   std::vector<LocalGroup::Post> ps;
   ks_status e = lg_exchange(c, {c->lg_ev[0], buf, {}}, ps);
   if (e) return e;
-  for (uint32_t j = 0; j < c->lgroup->world; ++j) {
+  for (uint32_t j = 0; j < c->lgroup->world(); ++j) {
     if (j == r) continue;
     HIPC(c, hipStreamWaitEvent(st, ps[j].ev, 0));
     HIPC(c, hipMemcpyAsync((uint8_t *)buf + (size_t)j * bytes, (const uint8_t *)ps[j].ptr + (size_t)j * bytes, bytes,
@@ -2684,7 +2656,7 @@ ks_status coll_allreduce_max_u32(ks_ctx *c, uint32_t *buf, size_t n, hipStream_t
   std::vector<LocalGroup::Post> ps;
   ks_status e = lg_exchange(c, {c->lg_ev[0], c->d_lgstage, {}}, ps);
   if (e) return e;
-  for (uint32_t j = 0; j < c->lgroup->world; ++j) {
+  for (uint32_t j = 0; j < c->lgroup->world(); ++j) {
     if (j == c->cfg.rank) continue;
     HIPC(c, hipStreamWaitEvent(st, ps[j].ev, 0));
     HIPC(c, launch_umax_u32(buf, (const uint32_t *)ps[j].ptr, (uint32_t)n, st));
@@ -3262,46 +3234,22 @@ ks_status run_batch(ks_ctx *c, ks_batch *b) {
   return KS_OK;
 }
 
-void worker_main(ks_ctx *c) {
-  (void)hipSetDevice(c->cfg.device);
-  std::unique_lock<std::mutex> lk(c->qmu);
-  for (;;) {
-    c->qcv.wait(lk, [&] { return c->stop || !c->queue.empty(); });
-    if (c->queue.empty()) return;  // stop requested, nothing queued
-    ks_batch *b = c->queue.front();
-    c->queue.pop_front();
-    lk.unlock();
-    const auto t0 = std::chrono::steady_clock::now();
-    const ks_status st = run_batch(c, b);
-    if (c->run_profile) {
-      c->prof[4] += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-      c->prof[6] += 1;
-    }
-    std::string e;
-    if (st) {
-      std::lock_guard<std::mutex> g(c->err_mu);
-      e = c->err;
-    }
-    lk.lock();
-    b->run_status = st;
-    b->run_err = e;
-    b->done = true;
-    c->inflight--;
-    c->dcv.notify_all();
-    if (c->run_profile && !c->queue.empty()) c->prof[5] += 0;  // next run already queued: no idle time
-    else if (c->run_profile) {
-      const auto ti = std::chrono::steady_clock::now();
-      c->qcv.wait(lk, [&] { return c->stop || !c->queue.empty(); });
-      if (!c->queue.empty()) c->prof[5] += std::chrono::duration<double>(std::chrono::steady_clock::now() - ti).count();
-    }
+// RunQueue callbacks (ks_batch_submit's worker thread)
+void worker_init(void *ctx) { (void)hipSetDevice(static_cast<ks_ctx *>(ctx)->cfg.device); }
+int32_t worker_run(void *ctx, ks_batch *b, std::string *err) {
+  ks_ctx *c = static_cast<ks_ctx *>(ctx);
+  const ks_status st = run_batch(c, b);
+  if (st) {
+    std::lock_guard<std::mutex> g(c->err_mu);
+    *err = c->err;
   }
+  return st;
 }
 
 // Every ABI call except prepare / submit / wait / results / free first lets
 // the submitted batches finish (they own the scheduler streams and the table).
 ks_status drain_async(ks_ctx *c) {
-  std::unique_lock<std::mutex> lk(c->qmu);
-  c->dcv.wait(lk, [&] { return c->inflight == 0; });
+  c->runq->drain();
   return KS_OK;
 }
 
@@ -3355,6 +3303,7 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
   *out = nullptr;
   auto c = std::make_unique<ks_ctx>();
   c->cfg = *cfg;
+  c->runq = std::make_unique<RunQueue<ks_batch>>(c.get(), &worker_run, &worker_init);
   if (cfg->node_capacity == 0) return KS_ERR_INVALID;
   c->cap = cfg->node_capacity;
   c->npl = cfg->nodes_per_lane ? cfg->nodes_per_lane : 4;
@@ -3382,7 +3331,10 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
   ks_ctx *x = c.get();
   {
     // execution options (ks_config; none changes a result)
+    // (pass and round caps bounded so the resolve's uint32 products
+    // pass_cap * n and backoff * serial_rounds cannot wrap)
     if (cfg->resolve_mode > KS_RESOLVE_PARALLEL || cfg->resolve_par_max_passes == 0 ||
+        cfg->resolve_par_max_passes > (uint32_t)MAX_P + 1 || cfg->resolve_serial_rounds > (1u << 20) ||
         (cfg->ext_nodes_per_lane != 2 && cfg->ext_nodes_per_lane != 4 && cfg->ext_nodes_per_lane != 8) ||
         cfg->sweep_pairs == 0 || cfg->sweep_pairs_ext == 0 || cfg->sync_timeout_ms == 0 || cfg->resolve_cus > 64 ||
         cfg->side_cus > 64)
@@ -3520,12 +3472,14 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
 
 void ks_close(ks_ctx *c) {
   if (!c) return;
+  double wp[3];
+  c->runq->profile(wp);
   if (c->run_profile)
     std::fprintf(stderr,
                  "ksched runs: %.0f runs: lock wait %.3f s, enqueue %.3f s, drains %.3f s; worker: %.0f runs %.3f s, "
-                 "idle with work queued %.3f s; prepare: drain wait %.3f s, compile %.3f s, acquire / copy / "
+                 "idle between runs %.3f s; prepare: drain wait %.3f s, compile %.3f s, acquire / copy / "
                  "upload %.3f s\n",
-                 c->prof[3], c->prof[0], c->prof[1], c->prof[2], c->prof[6], c->prof[4], c->prof[5], c->prof[7],
+                 c->prof[3], c->prof[0], c->prof[1], c->prof[2], wp[2], wp[0], wp[1], c->prof[7],
                  c->prof[8], c->prof[9]);
   if (c->run_profile && c->rk_prof[3]) {
     const uint64_t *h = c->rk_prof;
@@ -3538,12 +3492,7 @@ void ks_close(ks_ctx *c) {
       std::fprintf(stderr, "ksched events kind %d: %llu runs, %llu events, %.3f s\n", k,
                    (unsigned long long)c->ev_prof[k].runs, (unsigned long long)c->ev_prof[k].events, c->ev_prof[k].s);
   drain_async(c);
-  {
-    std::lock_guard<std::mutex> g(c->qmu);
-    c->stop = true;
-    c->qcv.notify_all();
-  }
-  if (c->worker.joinable()) c->worker.join();
+  c->runq->stop();
   (void)hipSetDevice(c->cfg.device);
   // bounded (a wedged context gets one more full timeout to finish)
   const bool was_wedged = c->wedged.load();
@@ -3630,6 +3579,12 @@ ks_status ks_nodes_upsert(ks_ctx *c, const ks_node *nodes, const uint32_t *slots
       if (s.alloc_milli_cpu < 0 || s.alloc_milli_cpu >= kMaxAlloc || s.alloc_memory < 0 ||
           s.alloc_memory >= kMaxAlloc || s.alloc_pods < 0 || s.alloc_pods > INT32_MAX - 1)
         return c->fail(KS_ERR_RANGE, "node %s allocatable outside the exact range", str(s.name).c_str());
+      // extended / ephemeral columns are only compared (Fit: request >
+      // Allocatable - Requested, exact int64), so any non-negative int64 is
+      // exact; the 2^44 bound is LeastAllocated's (cpu and memory only)
+      for (uint32_t k = 0; k < s.n_extended; ++k)
+        if (s.extended && s.extended[k].value < 0)
+          return c->fail(KS_ERR_RANGE, "node %s extended allocatable negative", str(s.name).c_str());
       // node names are unique (metadata.name matchFields resolve a name to one slot)
       const std::string nm = str(s.name);
       auto ci = call_names.emplace(nm, slot);
@@ -3774,12 +3729,7 @@ ks_status ks_nodes_upsert(ks_ctx *c, const ks_node *nodes, const uint32_t *slots
         if (nd.extended[k].name && it != c->xres_of.end() && xres_name_ok(str(nd.extended[k].name)))
           a[it->second] = nd.extended[k].value;
       }
-      for (uint32_t col = 0; col < a.size(); ++col) {
-        // extended / ephemeral columns are only compared (Fit: request >
-        // Allocatable - Requested, exact int64), so any non-negative int64 is
-        // exact; the 2^44 bound is LeastAllocated's (cpu and memory only)
-        if (a[col] < 0)
-          return c->fail(KS_ERR_RANGE, "node %s extended allocatable negative", str(nd.name).c_str());
+      for (uint32_t col = 0; col < a.size(); ++col) {  // (values validated above: >= 0)
         idx.push_back(col * (uint64_t)c->npos + pos);
         val.push_back(a[col]);
         if (core[(size_t)row_of[kv.first] * 8 + 3]) {  // new node: Requested = 0
@@ -3802,58 +3752,73 @@ ks_status ks_nodes_upsert_each(ks_ctx *c, const ks_node *nodes, const uint32_t *
   std::vector<uint32_t> ok_slots, ok_idx;
   ks_status first = KS_OK;
   std::string first_err;
-  std::unordered_map<std::string, uint32_t> call_names;  // accepted items' names -> slot
-  std::unordered_set<uint32_t> in_call;
-  for (uint32_t i = 0; i < n; ++i)
-    if (slots[i] < c->cap) in_call.insert(slots[i]);
+  std::vector<std::string> why(n);
+  // Pass 1: what each item decides alone (slot, ranges).
   for (uint32_t i = 0; i < n; ++i) {
     const ks_node &s = nodes[i];
     const uint32_t slot = slots[i];
     ks_status st = KS_OK;
-    std::string why;
     const std::string nm = str(s.name);
     if (slot >= c->cap) {
       st = KS_ERR_NOT_FOUND;
-      why = "slot " + std::to_string(slot) + " >= capacity";
+      why[i] = "slot " + std::to_string(slot) + " >= capacity";
     } else if (s.alloc_milli_cpu < 0 || s.alloc_milli_cpu >= kMaxAlloc || s.alloc_memory < 0 ||
                s.alloc_memory >= kMaxAlloc || s.alloc_pods < 0 || s.alloc_pods > INT32_MAX - 1) {
       st = KS_ERR_RANGE;
-      why = "node " + nm + " allocatable outside the exact range";
+      why[i] = "node " + nm + " allocatable outside the exact range";
     } else {
       for (uint32_t k = 0; k < s.n_extended && !st; ++k)
-        if (s.extended[k].value < 0) {
+        if (s.extended && s.extended[k].value < 0) {
           st = KS_ERR_RANGE;
-          why = "node " + nm + " extended allocatable negative";
+          why[i] = "node " + nm + " extended allocatable negative";
         }
     }
-    if (!st) {
-      auto ci = call_names.find(nm);
-      if (ci != call_names.end() && ci->second != slot) {
-        st = KS_ERR_INVALID;
-        why = "node name " + nm + " given to two slots";
-      } else {
-        const int64_t nid = c->lookup(s.name);
-        if (nid >= 0) {
-          auto it = c->name_slot.find((uint32_t)nid);
-          if (it != c->name_slot.end() && it->second != slot && c->nodes[it->second].present &&
-              !in_call.count(it->second)) {
-            st = KS_ERR_INVALID;
-            why = "node name " + nm + " already names another slot";
-          }
+    status[i] = st;
+  }
+  // Pass 2: node-name uniqueness, judged against the items still accepted.
+  // A name may move off a slot only if that slot's own item is applied too,
+  // so a rejection can reject another item: repeat until nothing changes
+  // (rejections only shrink the accepted set, so this ends).
+  for (bool changed = true; changed;) {
+    changed = false;
+    std::unordered_set<uint32_t> in_call;
+    for (uint32_t i = 0; i < n; ++i)
+      if (!status[i]) in_call.insert(slots[i]);
+    std::unordered_map<std::string, uint32_t> call_names;  // accepted items' names -> slot
+    for (uint32_t i = 0; i < n; ++i) {
+      if (status[i]) continue;
+      const ks_node &s = nodes[i];
+      const uint32_t slot = slots[i];
+      const std::string nm = str(s.name);
+      auto ci = call_names.emplace(nm, slot);
+      if (!ci.second && ci.first->second != slot) {
+        status[i] = KS_ERR_INVALID;
+        why[i] = "node name " + nm + " given to two slots";
+        changed = true;
+        continue;
+      }
+      const int64_t nid = c->lookup(s.name);
+      if (nid >= 0) {
+        auto it = c->name_slot.find((uint32_t)nid);
+        if (it != c->name_slot.end() && it->second != slot && c->nodes[it->second].present &&
+            !in_call.count(it->second)) {
+          status[i] = KS_ERR_INVALID;
+          why[i] = "node name " + nm + " already names another slot";
+          changed = true;
         }
       }
     }
-    status[i] = st;
-    if (st) {
+  }
+  for (uint32_t i = 0; i < n; ++i) {
+    if (status[i]) {
       if (!first) {
-        first = st;
-        first_err = why;
+        first = status[i];
+        first_err = why[i];
       }
       continue;
     }
-    call_names.emplace(nm, slot);
-    ok_nodes.push_back(s);
-    ok_slots.push_back(slot);
+    ok_nodes.push_back(nodes[i]);
+    ok_slots.push_back(slots[i]);
     ok_idx.push_back(i);
   }
   if (!ok_nodes.empty()) {
@@ -3962,34 +3927,31 @@ static ks_status pods_delta(ks_ctx *c, const ks_pod *const *pods, const uint32_t
   if (n >= 8192) {
     const uint32_t T = std::min<uint32_t>(8, std::max(1u, std::thread::hardware_concurrency()));
     std::vector<int64_t> affs(T, 0);
-    std::vector<std::thread> th;
-    for (uint32_t t = 0; t < T; ++t)
-      th.emplace_back([&, t] {
-        for (uint32_t i = (uint32_t)((uint64_t)n * t / T), e = (uint32_t)((uint64_t)n * (t + 1) / T); i < e; ++i) {
-          if (slots[i] >= c->cap || !c->present_map[slots[i]]) continue;
-          const ks_pod &pd = *pods[i];
-          if (pd.n_namespace_labels || pd.n_affinity_terms || pd.n_labels) continue;
-          bool ext = false;
-          for (uint32_t k = 0; k < pd.n_containers; ++k) ext |= pd.containers[k].n_extended != 0;
-          for (uint32_t k = 0; k < pd.n_init_containers; ++k) ext |= pd.init_containers[k].n_extended != 0;
-          if (ext) continue;
-          auto it = c->empty_set_of_ns.find(str(pd.ns));  // read-only here: no thread interns
-          if (it == c->empty_set_of_ns.end()) continue;
-          int64_t rc, rm, zc, zm;
-          if (pod_requests(pd, false, &rc, &rm) || pod_requests(pd, true, &zc, &zm)) continue;
-          sets[i] = it->second;
-          if (pd.unmodelled & KS_UNMODELLED_POD_AFFINITY) affs[t] += sign;
-          pos[i] = c->slot_pos[slots[i]];
-          int64_t *x = &d[(size_t)i * 5];
-          x[0] = sign * rc;
-          x[1] = sign * rm;
-          x[2] = sign * zc;
-          x[3] = sign * zm;
-          x[4] = sign;
-          done[i] = 1;
-        }
-      });
-    for (auto &t : th) t.join();
+    parallel_chunks(n, T, [&](uint32_t t, uint32_t lo, uint32_t hi) {
+      for (uint32_t i = lo; i < hi; ++i) {
+        if (slots[i] >= c->cap || !c->present_map[slots[i]]) continue;
+        const ks_pod &pd = *pods[i];
+        if (pd.n_namespace_labels || pd.n_affinity_terms || pd.n_labels) continue;
+        bool ext = false;
+        for (uint32_t k = 0; k < pd.n_containers; ++k) ext |= pd.containers[k].n_extended != 0;
+        for (uint32_t k = 0; k < pd.n_init_containers; ++k) ext |= pd.init_containers[k].n_extended != 0;
+        if (ext) continue;
+        auto it = c->empty_set_of_ns.find(str(pd.ns));  // read-only here: no thread interns
+        if (it == c->empty_set_of_ns.end()) continue;
+        int64_t rc, rm, zc, zm;
+        if (pod_requests(pd, false, &rc, &rm) || pod_requests(pd, true, &zc, &zm)) continue;
+        sets[i] = it->second;
+        if (pd.unmodelled & KS_UNMODELLED_POD_AFFINITY) affs[t] += sign;
+        pos[i] = c->slot_pos[slots[i]];
+        int64_t *x = &d[(size_t)i * 5];
+        x[0] = sign * rc;
+        x[1] = sign * rm;
+        x[2] = sign * zc;
+        x[3] = sign * zm;
+        x[4] = sign;
+        done[i] = 1;
+      }
+    });
     for (int64_t v : affs) aff += v;
   }
   for (uint32_t i = 0; i < n; ++i) {
@@ -4199,10 +4161,7 @@ ks_status ks_batch_prepare(ks_ctx *c, const ks_pod *pods, uint32_t n, ks_batch *
     for (uint32_t i = 0; i < n && !any_solo; ++i) any_solo = may_need_solo(c, pods[i]);
   }
   bool drained = !any_solo;
-  if (!drained) {
-    std::lock_guard<std::mutex> q(c->qmu);
-    drained = c->inflight == 0;
-  }
+  if (!drained) drained = c->runq->idle();
   const auto tp0 = std::chrono::steady_clock::now();
   auto tp1 = tp0;
   std::vector<uint32_t> set_ids(n), refs, term_refs;
@@ -4282,12 +4241,7 @@ ks_status ks_batch_prepare(ks_ctx *c, const ks_pod *pods, uint32_t n, ks_batch *
   }
   std::memcpy(b->h_clauses, cl.w.data(), cl.w.size() * 8);
   b->uploaded = false;
-  bool idle;
-  {
-    std::lock_guard<std::mutex> g(c->qmu);
-    idle = c->inflight == 0;
-  }
-  if (idle) {
+  if (c->runq->idle()) {
     // nothing in flight: upload now, so the run starts with every input
     // resident in HBM (the scheduler stream is ours until ks_batch_submit)
     {
@@ -4320,24 +4274,13 @@ ks_status ks_batch_run(ks_ctx *c, ks_batch *b) {
 
 ks_status ks_batch_submit(ks_ctx *c, ks_batch *b) {
   if (!c || !b) return KS_ERR_INVALID;
-  std::lock_guard<std::mutex> g(c->qmu);
-  if (b->queued && !b->done) return c->fail(KS_ERR_INVALID, "batch already submitted");
-  if (!c->worker.joinable()) c->worker = std::thread(worker_main, c);
-  b->queued = true;
-  b->done = false;
-  b->run_status = KS_OK;
-  b->run_err.clear();
-  c->queue.push_back(b);
-  c->inflight++;
-  c->qcv.notify_one();
+  if (!c->runq->submit(b)) return c->fail(KS_ERR_INVALID, "batch already submitted");
   return KS_OK;
 }
 
 ks_status ks_batch_wait(ks_ctx *c, ks_batch *b) {
   if (!c || !b) return KS_ERR_INVALID;
-  std::unique_lock<std::mutex> lk(c->qmu);
-  if (!b->queued) return c->fail(KS_ERR_INVALID, "batch was not submitted");
-  c->dcv.wait(lk, [&] { return b->done; });
+  if (!c->runq->wait(b)) return c->fail(KS_ERR_INVALID, "batch was not submitted");
   if (b->run_status) c->fail(b->run_status, "%s", b->run_err.c_str());
   return b->run_status;
 }
@@ -4345,10 +4288,7 @@ ks_status ks_batch_wait(ks_ctx *c, ks_batch *b) {
 ks_status ks_batch_results(ks_ctx *c, const ks_batch *b, ks_result *out) {
   if (!c || !b || (b->n && !out)) return KS_ERR_INVALID;
   static_assert(sizeof(ks_result) == sizeof(DevResult), "result layout");
-  {
-    std::lock_guard<std::mutex> g(c->qmu);
-    if (b->queued && !b->done) return c->fail(KS_ERR_INVALID, "batch still running (ks_batch_wait first)");
-  }
+  if (c->runq->running(b)) return c->fail(KS_ERR_INVALID, "batch still running (ks_batch_wait first)");
   // the run copied the results into the batch's pinned buffer
   std::memcpy(out, b->h_results, (size_t)b->n * sizeof(DevResult));
   uint64_t sched = 0;
@@ -4359,10 +4299,7 @@ ks_status ks_batch_results(ks_ctx *c, const ks_batch *b, ks_result *out) {
 
 ks_status ks_batch_marks(ks_ctx *c, const ks_batch *b, uint8_t *out) {
   if (!c || !b || (b->n && !out)) return KS_ERR_INVALID;
-  {
-    std::lock_guard<std::mutex> g(c->qmu);
-    if (b->queued && !b->done) return c->fail(KS_ERR_INVALID, "batch still running (ks_batch_wait first)");
-  }
+  if (c->runq->running(b)) return c->fail(KS_ERR_INVALID, "batch still running (ks_batch_wait first)");
   if (!b->n) return KS_OK;
   ks_status st;
   if ((st = xfer_begin(c, xround(b->n), 0))) return st;
@@ -4373,10 +4310,7 @@ ks_status ks_batch_marks(ks_ctx *c, const ks_batch *b, uint8_t *out) {
 void ks_batch_free(ks_ctx *c, ks_batch *b) {
   if (!b) return;
   if (!c) return;  // pooled buffers belong to the context (ks_close frees them)
-  {
-    std::unique_lock<std::mutex> lk(c->qmu);
-    if (b->queued) c->dcv.wait(lk, [&] { return b->done; });
-  }
+  c->runq->settle(b);
   {
     std::lock_guard<std::mutex> g(c->mu);
     class_release(c, &b->class_refs);

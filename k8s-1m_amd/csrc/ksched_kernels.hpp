@@ -156,6 +156,13 @@ constexpr uint32_t RUN_MIN_PODS = 4;    // shorter sequences take the per-pod ch
 constexpr uint32_t RK_HK_NONE = 255;    // the node lacks the hostname key (counts 0..254)
 constexpr uint32_t RK_DZ_NONE = 2047;   // the node lacks the other key (domain ids 0..2046)
 constexpr uint32_t RK_IGN = 1u << 19;   // PreScore ignores the node (requireAllTopologies)
+// The sort runs over 20 + s_bits bits and an infeasible node's key is ~0 there
+// (code 0xFFFFF).  Every feasible code keeps bit 19 clear and the ignored code
+// keeps bits 0..18 clear, so no feasible or ignored key equals it, whatever the
+// static score (2^s_bits - 1 - S with S = 0 included).
+static_assert((RK_DZ_NONE << 8 | RK_HK_NONE) < RK_IGN && (RK_IGN | 0x7FFFFu) == 0xFFFFFu &&
+                  RK_IGN != 0xFFFFFu,
+              "replica sort keys: feasible / ignored codes stay below the infeasible code");
 enum RunStop : uint32_t { RUN_END = 0, RUN_FIT = 1, RUN_FULL = 2, RUN_REFUSED = 3 };
 struct ReplicaArgs {
   uint64_t *keys, *sorted;  // [npos] sort keys, sorted

@@ -63,12 +63,28 @@ class GpuTarget:
         return self.s.node_states(slots)
 
 
+def _rows(src, T, idx):
+    """numpy rows (bytes) of the T structs src[idx] (src: a ctypes array or pointer)."""
+    idx = np.asarray(idx, dtype=np.int64)
+    if not len(idx):
+        return np.zeros((0, C.sizeof(T)), dtype=np.uint8)
+    sz = C.sizeof(T)
+    base = C.cast(src, C.c_void_p).value
+    view = np.ctypeslib.as_array((C.c_uint8 * (sz * (int(idx.max()) + 1))).from_address(base)).reshape(-1, sz)
+    return view[idx]
+
+
+def _from_rows(rows, T):
+    """ctypes array of T holding `rows` (a struct copy: pointers into the owners' memory stay valid)."""
+    out = (T * max(1, len(rows)))()
+    if len(rows):
+        C.memmove(out, np.ascontiguousarray(rows).ctypes.data, rows.size)
+    return out
+
+
 def _gather(src, idx, T):
     """ctypes array of T copied from src[idx] (structs keep their pointers into src's owner)."""
-    out = (T * max(1, len(idx)))()
-    for j, i in enumerate(idx):
-        out[j] = src[int(i)]
-    return out
+    return _from_rows(_rows(src, T, idx), T)
 
 
 def _u32(a):
@@ -127,11 +143,15 @@ class BurstStream:
 
     # ---------------------------------------------------------------- events
     def _pod_struct_array(self, pods_idx):
-        out = (_abi.KsPod * max(1, len(pods_idx)))()
-        for j, i in enumerate(pods_idx):
-            i = int(i)
-            out[j] = self.pods.pods[i] if i >= 0 else self.prefill.pods[-1 - i]
-        return out
+        """ks_pod array of stream pods (index >= 0) and prefill pods (-1 - index), in order."""
+        pods_idx = np.asarray(pods_idx, dtype=np.int64)
+        rows = np.zeros((len(pods_idx), C.sizeof(_abi.KsPod)), dtype=np.uint8)
+        own = pods_idx >= 0
+        if own.any():
+            rows[own] = _rows(self.pods.pods, _abi.KsPod, pods_idx[own])
+        if (~own).any():
+            rows[~own] = _rows(self.prefill.pods, _abi.KsPod, -1 - pods_idx[~own])
+        return _from_rows(rows, _abi.KsPod)
 
     def make_events(self):
         """The event log after a burst (a list of (op, payload) in log order)."""

@@ -262,3 +262,51 @@ def test_node_range_errors_fail_their_own_item_only():
     r = res_array(got, m)
     assert (r["node_index"][[0, 3, 6]] == 5).all()  # 6 TiB each: only the 20 TiB node has it
     assert r["status"][9] == 1  # 3 x 6 TiB taken: 2 TiB left on the only ephemeral-storage node
+
+
+def test_upsert_refuses_negative_extended_before_applying():
+    # ks_nodes_upsert validates the whole call before it writes anything: one
+    # good node plus one with a negative extended allocatable leaves the good
+    # node absent (include/ksched.h, ks_nodes_upsert)
+    from ksched.objects import Node
+
+    Gi = 1 << 30
+    nodes = [Node("good", {"cpu": 16000, "memory": 64 * Gi, "pods": 110}, {}, [], False,
+                  extended={"example.com/gpu": 4}),
+             Node("bad", {"cpu": 16000, "memory": 64 * Gi, "pods": 110}, {}, [], False,
+                  extended={"example.com/gpu": -1})]
+    a = Arena()
+    na, n = nodes_array(nodes, a)
+    with Scheduler(4) as s:
+        assert s.lib.ks_nodes_upsert(s.ctx, na, (C.c_uint32 * n)(0, 1), n) == 5  # KS_ERR_RANGE
+        assert all(x.pod_count == -1 for x in s.node_states([0, 1])), "refused call applied its good node"
+        # the per-item form applies the good one only
+        status = (C.c_int32 * n)()
+        assert s.lib.ks_nodes_upsert_each(s.ctx, na, (C.c_uint32 * n)(0, 1), n, status) == 5
+        assert list(status) == [0, 5]
+        st = s.node_states([0, 1])
+        assert st[0].pod_count == 0 and st[1].pod_count == -1
+
+
+def test_upsert_each_name_moves_only_with_its_slot():
+    # ks_nodes_upsert_each judges node-name moves against the items it
+    # accepts: a rejected item for slot 0 (which holds "n1") cannot vacate
+    # the name, so the item renaming slot 1 to "n1" is rejected on its own and
+    # the unrelated item is still applied (per-item contract)
+    from ksched.objects import Node
+
+    Gi = 1 << 30
+    res = {"cpu": 16000, "memory": 64 * Gi, "pods": 110}
+    a = Arena()
+    with Scheduler(4) as s:
+        na, n = nodes_array([Node("n1", res, {}, [], False), Node("n2", res, {}, [], False)], a)
+        assert s.lib.ks_nodes_upsert(s.ctx, na, (C.c_uint32 * n)(0, 1), n) == 0
+        items = [Node("renamed", {"cpu": 16000, "memory": 1 << 45, "pods": 110}, {}, [], False),  # out of range
+                 Node("n1", res, {}, [], False),                                                  # slot 1 -> "n1"
+                 Node("n3", res, {}, [], False)]                                                  # slot 2: new
+        na, n = nodes_array(items, a)
+        status = (C.c_int32 * n)()
+        rc = s.lib.ks_nodes_upsert_each(s.ctx, na, (C.c_uint32 * n)(0, 1, 2), n, status)
+        assert rc != 0 and list(status)[:2] == [5, 1] and status[2] == 0, list(status)
+        st = s.node_states([0, 1, 2])
+        assert all(x.pod_count == 0 for x in st), "the valid item was not applied"

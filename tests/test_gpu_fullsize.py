@@ -28,6 +28,7 @@ import pytest
 import pyoracle
 from helpers import assert_results_equal, res_array, states_np
 from ksched import Scheduler, _abi, synth
+from ksched.stream import _gather
 
 pytestmark = pytest.mark.gpu
 
@@ -40,10 +41,7 @@ ORACLE_THREADS = 16  # the GPU box's CPU share
 
 def pod_subset(pods_ptr, idx):
     """Contiguous ks_pod array of pods_ptr[idx] (the structs keep their pointers)."""
-    out = (_abi.KsPod * max(1, len(idx)))()
-    for j, i in enumerate(idx):
-        out[j] = pods_ptr[int(i)]
-    return out
+    return _gather(pods_ptr, idx, _abi.KsPod)
 
 
 def u32(a):
@@ -156,10 +154,66 @@ def run_fullsize(kind, pods, prefill, *, opts=None, **cfg):
     return res_array(got, BATCH), list(dbg)
 
 
-def test_c3_hetero_1m_replay():
-    r, dbg = run_fullsize(synth.HETERO, synth.pods(synth.HETERO, BATCH, 2), prefill=True)
-    assert (r["status"] == 0).all()
-    assert dbg[0] >= BATCH // 256  # rounds
+C3_STEPS, C3_STEP = 20, 50_000  # BASELINE configs[2]: 1M pods; bench.py's headline step size
+
+
+def test_c3_bench_pipeline_1m_replay():
+    # The headline exactly as bench.py runs it (run_batches / end_to_end): the
+    # 1M-node C3 cluster (nodes seed 1, prefill seed 3 to <50 % cpu), the pod
+    # stream of seed 7, 20 steps of 50,000 pods through ks_batch_prepare /
+    # ks_batch_submit / ks_batch_wait / ks_batch_results with bench.E2E_DEPTH
+    # batches in flight (batch k+1 compiled while k runs) = configs[2]'s 1M
+    # pods.  The oracle replays all 1M decisions and schedules >= 512 of the
+    # pods itself in windows over the whole stream: the first pod of steps
+    # (where a batch hands the pipelined rounds to the next), round starts,
+    # FIX / after-waste marks and seeded random windows; then the node tables
+    # must be equal.
+    import sys
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+    import bench
+
+    m = C3_STEPS * C3_STEP
+    nodes = synth.nodes(synth.HETERO, N, 1)
+    slots = synth.slot_array(N)
+    pf = synth.prefill(synth.HETERO, N, 1, 3, 0.5)
+    pods = synth.pods(synth.HETERO, m, 7)
+    s = Scheduler(N)
+    s.upsert_nodes_raw(nodes.nodes, slots, N)
+    assert s.lib.ks_pods_add(s.ctx, pf.pods, pf.slot_ptr, pf.n_pods) == 0
+    got = (_abi.KsResult * m)()
+    marks = bytearray(m)
+    inflight, nxt = [], 0
+    for k in range(C3_STEPS):
+        while nxt < C3_STEPS and len(inflight) < bench.E2E_DEPTH:
+            b = s.prepare(pods.pods_at(nxt * C3_STEP), C3_STEP)
+            assert s.lib.ks_batch_submit(s.ctx, b) == 0, s.lib.ks_last_error(s.ctx)
+            inflight.append(b)
+            nxt += 1
+        cur = inflight.pop(0)
+        assert s.lib.ks_batch_wait(s.ctx, cur) == 0, s.lib.ks_last_error(s.ctx)
+        C.memmove(C.addressof(got) + k * C3_STEP * C.sizeof(_abi.KsResult), s.results(cur, C3_STEP),
+                  C3_STEP * C.sizeof(_abi.KsResult))
+        marks[k * C3_STEP:(k + 1) * C3_STEP] = s.marks(cur, C3_STEP)
+        s.free(cur)
+    dbg = (C.c_uint64 * 16)()
+    assert s.lib.ks_debug_counters(s.ctx, dbg) == 0
+    assert dbg[0] >= m // 256
+    o = pyoracle.Oracle(N, threads=ORACLE_THREADS)
+    o.upsert(nodes.nodes, slots, N)
+    o.add_pods(pf.pods, pf.slot_ptr, pf.n_pods)
+    steps = (0, 1, 2, 7, 13, C3_STEPS - 1)
+    fixed = tuple(k * C3_STEP for k in steps) + (m - WLEN,)
+    wins = pick_windows(bytes(marks), m, fixed=fixed, per_kind=2, round_every=1000, min_pods=MIN_CHECKED)
+    checked = replay_check(o, pods, got, m, windows=[w for w, _ in wins])
+    assert checked >= MIN_CHECKED, f"only {checked} pods checked by the oracle"
+    assert {w for w, _ in wins} >= set(fixed)
+    sg = states_np(s.lib.ks_node_states, s.ctx, N)
+    sw = states_np(o.L.oracle_node_states, o.o, N)
+    assert np.array_equal(sg, sw), "node tables differ after replaying all 1M decisions"
+    assert (res_array(got, m)["status"] == 0).all()
+    s.close()
+    o.close()
 
 
 def test_c4_labeled_1m_replay_early_fix():

@@ -3,10 +3,12 @@ updates between bursts (pod deletes, node updates, node deletes + adds).
 
 * small streams: libksched vs the CPU oracle, bit-exact on every result of
   every burst and on the final node state;
-* the full 1M-node C5 shape: the incrementally updated device cache equals a
-  cache rebuilt from scratch from the live nodes and bound pods, both schedule
-  the next burst identically, and the first pods of that burst equal the
-  oracle on the same 1M-node state.
+* the full C5 stream (1M nodes, 100 bursts x 100k pods, bench.py's path):
+  the oracle replays every decision and event log and schedules windows of
+  pods itself over early, middle and last bursts; the node tables are equal
+  after 10M pods; the incrementally updated device cache equals a cache
+  rebuilt from scratch, both schedule the next burst identically, and its
+  first pods equal the oracle.
 """
 import ctypes as C
 
@@ -41,35 +43,110 @@ def test_c5_stream_vs_oracle(kind, P):
     s.close()
 
 
-def test_c5_1m_incremental_equals_rebuild():
-    n, bursts, burst = 1_000_000, 3, 100_000
-    st = BurstStream(synth.HETERO, n, bursts + 1, burst)  # C5 rates: 5 % pods, 0.1 % / 0.01 % nodes
+# C5 check windows: burst -> first pods of 32-pod windows the oracle schedules
+# itself (early, middle and last bursts; burst starts, ends and offsets that
+# are not round-aligned): 17 windows = 544 pods
+C5_WINDOWS = {0: (0, 40_961, 99_968), 1: (0, 77_777), 2: (5_003,), 33: (12_345, 61_003),
+              50: (0, 50_021, 99_968), 66: (31_337,), 75: (70_001,), 98: (88_001,), 99: (0, 49_999, 99_968)}
+C5_WLEN = 32
+
+
+class _BurstPods:
+    """pods / pods_at of one burst of a BurstStream (the replay's view)."""
+
+    def __init__(self, st, b):
+        self.base = b * st.burst
+        self.st = st
+        self.pods = st.pods.pods_at(self.base)
+
+    def pods_at(self, i):
+        return self.st.pods.pods_at(self.base + i)
+
+
+def test_c5_full_stream_replay():
+    # configs[4] at its full length, as bench.py --workload c5 runs it
+    # (run_c5: the same seeded BurstStream, ks_batch_prepare + ks_batch_run per
+    # burst, the burst's watch-event log through ks_events_apply): 1M nodes,
+    # 100 bursts x 100k pods = 10M pods, C5 rates (5 % of bound pods deleted,
+    # 0.1 % node updates, 0.01 % node deletes + adds per burst).
+    # * The oracle replays every decision and applies the same logs (per-kind
+    #   calls), one burst behind on a thread of its own, and schedules 544 pods
+    #   itself in windows over early, middle and last bursts: bit-exact.
+    # * After the last burst the 1M-node tables are equal (every commit and
+    #   every event of 10M pods booked identically).
+    # * A cache rebuilt from scratch from the live nodes and bound pods equals
+    #   the incremental one, and both schedule a further burst identically;
+    #   its first pods equal the oracle's.
+    import queue
+    import threading
+
+    from test_gpu_fullsize import replay_check
+
+    n, bursts, burst = 1_000_000, 100, 100_000
+    st = BurstStream(synth.HETERO, n, bursts + 1, burst, prefill=3)
     s = Scheduler(n)
     g = GpuTarget(s)
-    st.setup([g])
-    for b in range(bursts):
-        arr, m = st.burst_pods(b)
-        res = g.schedule(arr, m)
-        r = res_array(res, m)
-        assert (r["status"] == 0).all()
-        st.record(b, res)
-        st.apply(st.make_events(), [g])
+    o = pyoracle.Oracle(n, threads=16)
+    ot = OracleTarget(o)
+    st.setup([g, ot])
+    work, errors, checked = queue.Queue(maxsize=3), [], [0]
+
+    def oracle_side():
+        while True:
+            item = work.get()
+            if item is None:
+                return
+            if errors:
+                continue
+            b, res, ops = item
+            try:
+                checked[0] += replay_check(o, _BurstPods(st, b), res, burst, windows=C5_WINDOWS.get(b, ()),
+                                           wlen=C5_WLEN)
+                st.apply_marshalled(ops, [ot])
+            except BaseException as e:  # noqa: BLE001 -- re-raised on the test thread
+                errors.append(e)
+
+    th = threading.Thread(target=oracle_side, daemon=True)
+    th.start()
+    scheduled = 0
+    try:
+        for b in range(bursts):
+            arr, m = st.burst_pods(b)
+            batch = s.prepare(arr, m)
+            s.run(batch)
+            res = s.results(batch, m)
+            s.free(batch)
+            scheduled += int((res_array(res, m)["status"] == 0).sum())
+            st.record(b, res)
+            ops = st.marshal(st.make_events())
+            ev, ne, _keep = st.event_log(ops)
+            assert ne > 0
+            g.apply_events(ev, ne)
+            work.put((b, res, ops))
+            if errors:
+                break
+    finally:
+        work.put(None)
+        th.join()
+    if errors:
+        raise errors[0]
+    assert checked[0] == C5_WLEN * sum(len(w) for w in C5_WINDOWS.values()) >= 512
+    assert scheduled > 0.99 * bursts * burst
+    a = states_np(s.lib.ks_node_states, s.ctx, n)
+    assert np.array_equal(a, states_np(o.L.oracle_node_states, o.o, n)), "node tables differ after 10M pods"
+    # conservation: pods counted on the nodes = the stream's bound pods
+    assert a["pod_count"][a["pod_count"] >= 0].sum() == len(st.bound_pod)
     fresh = Scheduler(n)
     st.rebuild(GpuTarget(fresh))
-    a = states_np(s.lib.ks_node_states, s.ctx, n)
-    assert np.array_equal(a, states_np(fresh.lib.ks_node_states, fresh.ctx, n))
-    # conservation: Requested summed over nodes = Σ requests of the bound pods
-    assert a["pod_count"][a["pod_count"] >= 0].sum() == len(st.bound_pod)
+    assert np.array_equal(a, states_np(fresh.lib.ks_node_states, fresh.ctx, n)), "incremental != rebuilt cache"
     arr, m = st.burst_pods(bursts)
     got = s.schedule_raw(arr, m)
     assert_results_equal(got, fresh.schedule_raw(arr, m), m, "incremental vs rebuilt cache")
     fresh.close()
-    # the first pods of the next burst against the oracle on the same 1M-node state
-    o = OracleTarget(pyoracle.Oracle(n, threads=16))
-    st.rebuild(o)
-    k = 48
-    assert_results_equal(got, o.schedule(arr, k), k, "1M-node C5 state vs oracle")
+    k = 32
+    assert_results_equal(got, o.schedule(arr, k), k, "after 10M pods: incremental cache vs oracle")
     s.close()
+    o.close()
 
 
 def test_event_log_equals_separate_calls():

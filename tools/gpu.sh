@@ -29,7 +29,7 @@ line_args() {  # bench.py arguments of a named BASELINE.json configuration
     c2) echo "--nodes 100000 --batch 20000 --steps 5 --no-cpu-baseline --latency-calls 0" ;;
     kwok) echo "--kind kwok --topk 512 --no-cpu-baseline --latency-calls 0" ;;
     kwokbe) echo "--kind kwok --pods besteffort --no-cpu-baseline --latency-calls 0" ;;
-    c5) echo "--workload c5 --steps 5 --warmup 1 --no-cpu-baseline" ;;
+    c5) echo "--workload c5 --steps 20 --warmup 1 --no-cpu-baseline" ;;
     spread) echo "--kind zoned --pods spread --latency-calls 0" ;;
     deploy) echo "--kind zoned --pods deploy --latency-calls 0" ;;
     deploychain) echo "--kind zoned --pods deploy --latency-calls 0 --no-cpu-baseline --opt spread_replica_runs=0" ;;

@@ -3,11 +3,13 @@
 # first): the ksgather concurrency driver under ThreadSanitizer and under
 # AddressSanitizer + UBSan, then the relay tests (gRPC CollectScore over the
 # ASan libksgather) and the oracle tests (ASan liboracle, ASan libksynth) in a
-# Python whose first preloaded library is the ASan runtime.  Log:
-# profiles/r4/sanitize/sanitize.log; exits non-zero on any report.
+# Python whose first preloaded library is the ASan runtime; libksched's
+# host-thread protocols (ksched_sync.hpp: rendezvous, run queue, thread pool)
+# through tools/sync_stress.cpp under both.  Log:
+# profiles/r5/sanitize/sanitize.log; exits non-zero on any report.
 set -o pipefail
 R=$(cd "$(dirname "$0")/.." && pwd)
-OUT=${SANITIZE_OUT:-$R/profiles/r4/sanitize}
+OUT=${SANITIZE_OUT:-$R/profiles/r5/sanitize}
 mkdir -p "$OUT"
 LOG=$OUT/sanitize.log
 : > "$LOG"
@@ -21,6 +23,11 @@ TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1" "$B/ksg_stress_tsan" >> "
 say "== ksg_stress under AddressSanitizer + UBSan"
 ASAN_OPTIONS="detect_leaks=1 halt_on_error=1" UBSAN_OPTIONS="halt_on_error=1 print_stacktrace=1" \
   "$B/ksg_stress_asan" >> "$LOG" 2>&1 || { say "ASAN FAILED"; exit 1; }
+say "== sync_stress (libksched host threads) under ThreadSanitizer"
+TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1" "$B/sync_stress_tsan" >> "$LOG" 2>&1 || { say "TSAN FAILED"; exit 1; }
+say "== sync_stress under AddressSanitizer + UBSan"
+ASAN_OPTIONS="detect_leaks=1 halt_on_error=1" UBSAN_OPTIONS="halt_on_error=1 print_stacktrace=1" \
+  "$B/sync_stress_asan" >> "$LOG" 2>&1 || { say "ASAN FAILED"; exit 1; }
 
 # Python itself is not instrumented: the ASan runtime goes first in the
 # preload list (whatever is preloaded already stays after it), leaks are not
