@@ -261,67 +261,6 @@ __device__ __forceinline__ int32_t score_ba(const PodDev &p, const NodeRegs &r) 
   return score_ba_sum(r.rcpu + p.req_cpu_d, r.rmem + p.req_mem_d, r);
 }
 
-// ---- resource-only sweep: Fit and BalancedAllocation without the division
-// (DESIGN.md §4 "The fraction bracket").  With y = RN(1 / Allocatable) and
-// ry = RN(Requested * y) per node, q = fma(request, y, ry) is within 3.5
-// ulp(1) of upstream's fraction RN((Requested + request) / Allocatable)
-// whenever both are <= 1.
-// * Fit: Requested + request <= Allocatable iff q <= 1 + 2^-49 (integers
-//   below 2^44: a sum above Allocatable is >= (1 + 2^-44) Allocatable, and q
-//   is within 3u relative of it; a zero Allocatable has ry = 2, q = 2).
-// * BalancedAllocation: v± = RN(100 ± 2^-40 - 50 |q_cpu - q_mem|) bracket
-//   upstream's (1 - std) * 100 strictly, so when trunc(v-) == trunc(v+) that
-//   is the score; otherwise (within 2^-40 of an integer: ~1e-12 of random
-//   pairs, std = 0 included) the wave recomputes it exactly (score_ba_sum).
-//   Pods without cpu and memory requests take the node's precomputed exact
-//   score; nodes with a zero allocatable (one fraction: std = 0) or whose
-//   Requested exceeds its Allocatable (a fraction clamped at 1) are always
-//   recomputed.
-// tools/ba_bracket_check.cpp checks both against the exact arithmetic.
-constexpr double FIT_Q_MAX = 1.0 + 0x1p-49;
-constexpr double BA_LO = 100.0 - 0x1p-40, BA_HI = 100.0 + 0x1p-40;
-
-struct NodeRes {
-  double lf100_cpu, lf100_mem;  // (Allocatable - NonZeroRequested) * 100  (LeastAllocated)
-  double inv_cpu, inv_mem;      // y = RN(1 / Allocatable), 0 when Allocatable == 0
-  double ry_cpu, ry_mem;        // RN(Requested * y); 2 when Allocatable == 0 (Fit, BalancedAllocation)
-  uint32_t lashift;             // 1 with two non-zero allocatables
-  uint32_t ba0;                 // BalancedAllocation of a pod without requests (exact)
-};
-
-__device__ __forceinline__ NodeRes make_res(const NodeRegs &r) {
-  NodeRes n;
-  n.lf100_cpu = r.lf100_cpu;
-  n.lf100_mem = r.lf100_mem;
-  n.inv_cpu = r.inv_cpu;
-  n.inv_mem = r.inv_mem;
-  // a zero allocatable: q = 2 fails Fit for any request of it (no mask)
-  n.ry_cpu = (r.bits & 4u) ? r.rcpu * r.inv_cpu : 2.0;
-  n.ry_mem = (r.bits & 8u) ? r.rmem * r.inv_mem : 2.0;
-  n.lashift = r.lashift;
-  n.ba0 = (uint32_t)score_ba_sum(r.rcpu, r.rmem, r);
-  return n;
-}
-
-__device__ __forceinline__ int32_t score_la_res(const PodDev &p, const NodeRes &r) {
-  return (least_requested(r.lf100_cpu, p.nz100_cpu, r.inv_cpu) + least_requested(r.lf100_mem, p.nz100_mem, r.inv_mem)) >>
-         r.lashift;
-}
-
-// the fractions' approximations q (above)
-__device__ __forceinline__ void res_fractions(const PodDev &p, const NodeRes &r, double &q0, double &q1) {
-  q0 = __builtin_fma(p.req_cpu_d, r.inv_cpu, r.ry_cpu);
-  q1 = __builtin_fma(p.req_mem_d, r.inv_mem, r.ry_mem);
-}
-
-// trunc(v-), trunc(v+) of the bracket (v± >= 49 for q's <= 1 + 4u)
-__device__ __forceinline__ void ba_bracket(double q0, double q1, uint32_t &lo, uint32_t &hi) {
-  const double ad = fabs(q0 - q1);
-  const double vlo = __builtin_fma(ad, -50.0, BA_LO), vhi = __builtin_fma(ad, -50.0, BA_HI);
-  asm("v_cvt_u32_f64 %0, %1" : "=v"(lo) : "v"(vlo));
-  asm("v_cvt_u32_f64 %0, %1" : "=v"(hi) : "v"(vhi));
-}
-
 __device__ __forceinline__ int64_t taint_raw(const PodDev &p, const NodeExt &e) {
   return (int64_t)__popcll(e.prefer & ~p.tol_prefer);
 }

@@ -40,9 +40,27 @@ namespace ks {
 
 
 
+// A wave-uniform pod descriptor.  SCALAR (the resource-only sweep): through
+// the constant address space, i.e. s_load into SGPRs -- the generic pointer
+// gave three vector loads per pod and a compare + readfirstlane per request
+// test (round 5: C3 sweep 0.358 -> 0.355 ms).  The EXT sweep keeps the
+// generic load (the copy took 48 B of scratch there).  Batches are never
+// written while kernels read them.
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(4))) u32x4 *const_words;
+template <bool SCALAR = false>
 __device__ __forceinline__ PodDev load_pod(const PodDev *pods, uint32_t i) {
-  // Wave-uniform: lowered to scalar loads.
-  return pods[i];
+  if constexpr (SCALAR) {
+    const const_words src = (const_words)(pods + i);
+    u32x4 w[sizeof(PodDev) / 16];
+#pragma unroll
+    for (int k = 0; k < (int)(sizeof(PodDev) / 16); ++k) w[k] = src[k];
+    PodDev p;
+    __builtin_memcpy(&p, w, sizeof p);
+    return p;
+  } else {
+    return pods[i];
+  }
 }
 
 
@@ -214,28 +232,17 @@ void sweep_kernel(RoundArgs a) {
   const uint32_t wf9 = (uint32_t)a.w.fit << KEY32_POS_BITS, wb9 = (uint32_t)a.w.ba << KEY32_POS_BITS;
   const uint32_t wt9 = (uint32_t)a.w.tt << KEY32_POS_BITS, wn9 = (uint32_t)a.w.na << KEY32_POS_BITS;
   const uint32_t kpos1 = (1u << KEY32_POS_BITS) + kpos0;  // the + 1 of the key, and the position
-  // resource-only batches: node state for the fraction bracket
-  // (ksched_eval.hpp) and a wave mask of the nodes whose BalancedAllocation
-  // it cannot give (a zero allocatable, Requested > Allocatable: recomputed)
-  NodeRes nf[EXT ? 1 : NPL];
-  uint64_t exact_m[EXT ? 1 : NPL];
   if constexpr (!EXT) {
     const uint32_t cplus = (uint32_t)(a.w.tt * 100) + 1u;
-    static_for<NPL>([&](auto J) {
-      constexpr int j = J;
-      kc[j] = (cplus << KEY32_POS_BITS) + (kpos0 - (uint32_t)j * WAVE);
-      nf[j] = make_res(nr[j]);
-      exact_m[j] = __builtin_amdgcn_ballot_w64((nr[j].bamul == 0.0) | (nr[j].free_cpu < 0.0) | (nr[j].free_mem < 0.0));
-    });
+    static_for<NPL>([&](auto J) { kc[J] = (cplus << KEY32_POS_BITS) + (kpos0 - (uint32_t)J * WAVE); });
   }
-  const uint32_t pos_lane = s.base + kw * WAVE * NPL + lane;  // + j * WAVE: node j's position
 
   for (uint32_t it = p0; it < p1; ++it) {
     // FIX mode: slice entry it - start of the compacted flagged-pod list
     const uint32_t r = fix ? uniform_u32(a.fix_list[it - start]) : dedup ? uniform_u32(a.ulist[it - start]) : it - start;
     if (fix && r == FIX_NONE) continue;
     const uint32_t pi = start + r;
-    const PodDev p = load_pod(a.pods, pi);
+    const PodDev p = load_pod<!EXT>(a.pods, pi);
     uint32_t tt_max = 0, na_max = 0;
     if (EXT && (p.flags & (PF_TT | PF_NA))) {
       tt_max = uniform_u32(fix ? a.norm_max[2 * r + 0] : p.tt_guess);
@@ -256,58 +263,20 @@ void sweep_kernel(RoundArgs a) {
       // Fit as Requested + request > Allocatable on the sums BalancedAllocation
       // divides (exact integers in binary64), so the free columns need no
       // registers; a zero request's check is masked off (all-ones lane mask)
-      const uint32_t zc32 = uniform_u32(p.req_cpu != 0 ? 0u : ~0u), zm32 = uniform_u32(p.req_mem != 0 ? 0u : ~0u);
-      const uint64_t zc = ((uint64_t)zc32 << 32) | zc32, zm = ((uint64_t)zm32 << 32) | zm32;  // SGPR pairs
-      const uint64_t zr = zc & zm;  // no cpu or memory request: every node's precomputed exact BA
-      uint64_t fms[NPL], ambs[NPL];
-      uint32_t bas[NPL];
-      uint64_t amb_any = 0;
+      // (lane masks of the wave-uniform conditions: SGPR pairs)
+      const uint64_t zc = __builtin_amdgcn_ballot_w64(p.req_cpu == 0), zm = __builtin_amdgcn_ballot_w64(p.req_mem == 0);
       static_for<NPL>([&](auto J) {
         constexpr int j = J;
-        // Fit from the fraction bracket (ksched_eval.hpp; a zero allocatable
-        // fits no request of that resource); the wave's feasibility mask, ANDed from the compares' lane masks
+        const double sc = nr[j].rcpu + p.req_cpu_d, sm = nr[j].rmem + p.req_mem_d;
+        // the wave's feasibility mask, ANDed from the compares' lane masks
         // (SALU), selects the key and is counted by s_bcnt1: a bool here
         // made the compiler copy the mask through a VGPR per node
-        double q0, q1;
-        res_fractions(p, nf[j], q0, q1);
-        fms[j] = podfit_m[j] & (zc | __builtin_amdgcn_ballot_w64(!(q0 > FIT_Q_MAX))) &
-                 (zm | __builtin_amdgcn_ballot_w64(!(q1 > FIT_Q_MAX)));
-        uint32_t lo, hi;
-        ba_bracket(q0, q1, lo, hi);
-        bas[j] = sel_mask2(zr, nf[j].ba0, hi);
-        ambs[j] = (__builtin_amdgcn_ballot_w64(lo != hi) | exact_m[j]) & ~zr & fms[j];
-        amb_any |= ambs[j];
-      });
-      if (amb_any) {
-        // feasible lanes the bracket does not decide (rare): recompute
-        // exactly from the node row, re-read (wave-uniform branches)
-        KS_RARE_BEGIN();
-        static_for<NPL>([&](auto J) {
-          constexpr int j = J;
-          if (ambs[j] && ((ambs[j] >> lane) & 1ull)) {
-            uint32_t pos = pos_lane + (uint32_t)j * WAVE;
-            // (opaque here: hoisted out of the pod loop, the four columns'
-            // addresses per node took 32 VGPRs and an occupancy step)
-            asm volatile("" : "+v"(pos));
-            const int64_t ac = a.t.acpu[pos], am = a.t.amem[pos];
-            NodeRegs x;
-            x.acpu_d = (double)ac;
-            x.amem_d = (double)am;
-            x.inv_cpu = nf[j].inv_cpu;
-            x.inv_mem = nf[j].inv_mem;
-            x.bamul = ac && am ? 0.5 : 0.0;
-            const double rc = (double)a.t.rcpu[pos], rm = (double)a.t.rmem[pos];
-            bas[j] = (uint32_t)score_ba_sum(rc + p.req_cpu_d, rm + p.req_mem_d, x);
-          }
-        });
-        KS_RARE_END();
-      }
-      static_for<NPL>([&](auto J) {
-        constexpr int j = J;
-        const uint64_t fm = fms[j];
+        const uint64_t fm = podfit_m[j] & (zc | __builtin_amdgcn_ballot_w64(!(sc > nr[j].acpu_d))) &
+                            (zm | __builtin_amdgcn_ballot_w64(!(sm > nr[j].amem_d)));
         // key = (w_fit LA + w_ba BA) << 9 + kc[j]: two 24-bit multiply-adds
         // with the weights pre-shifted (10000 << 9 < 2^24; the key < 2^31)
-        const uint32_t key = sel_mask(fm, wmad_s(wf9, (uint32_t)score_la_res(p, nf[j]), wmad_s(wb9, bas[j], kc[j])));
+        const uint32_t key = sel_mask(fm, wmad_s(wf9, (uint32_t)score_la(p, nr[j]),
+                                                 wmad_s(wb9, (uint32_t)score_ba_sum(sc, sm, nr[j]), kc[j])));
         b2 = max(b2, min(b1, key));
         b1 = max(b1, key);
         feas += (uint32_t)__popcll(fm);

@@ -65,20 +65,6 @@ __device__ __forceinline__ uint32_t sel_mask(uint64_t m, uint32_t v) {
   return r;
 }
 
-// Rare-path markers: tools/valu_mix.py prices the sweep's pod loop by its
-// opcode mix and leaves out what lies between these (branches the loop
-// takes for a few waves only).  Two s_nop of a count the compiler does not
-// emit for hazards, in pairs.
-#define KS_RARE_BEGIN() asm volatile("s_nop 6\n\ts_nop 6")
-#define KS_RARE_END() asm volatile("s_nop 5\n\ts_nop 5")
-
-// a where the lane's bit of the wave mask m is set, else b
-__device__ __forceinline__ uint32_t sel_mask2(uint64_t m, uint32_t a, uint32_t b) {
-  uint32_t r;
-  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(b), "v"(a), "s"(m));
-  return r;
-}
-
 __device__ __forceinline__ uint32_t uniform_u32(uint32_t v) {
   return __builtin_amdgcn_readfirstlane(v);
 }

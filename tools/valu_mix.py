@@ -8,8 +8,7 @@ for ITS instruction mix, not a constant per instruction.  This tool:
      disassembles it with llvm-objdump;
   2. for every sweep_kernel<NPL, EXT, LWU> instance takes its per-pod loop
      (the longest backward branch: the loop over the pods of a sweep block,
-     nested clause loops counted once, rare-path regions marked in the source
-     left out) and histograms its VALU opcodes;
+     nested clause loops counted once) and histograms its VALU opcodes;
   3. prices each opcode with the issue cost measured on MI355X at 4 waves per
      SIMD by tools/valu_issue.hip (profiles/valu_issue.jsonl); an opcode the
      microbenchmark does not cover takes its class's median (VOP1/VOP2
@@ -122,23 +121,6 @@ def pod_loop(ins):
     return best
 
 
-def without_rare(ins):
-    """ins minus the rare-path regions (KS_RARE_BEGIN / KS_RARE_END in
-    ksched_util.hpp: s_nop 6, s_nop 6 ... s_nop 5, s_nop 5)."""
-    out, rare, i = [], False, 0
-    while i < len(ins):
-        a, op, args = ins[i]
-        nxt = ins[i + 1] if i + 1 < len(ins) else (0, "", "")
-        if op == "s_nop" and nxt[1] == "s_nop" and args.strip() == nxt[2].strip() and args.strip() in ("6", "5"):
-            rare = args.strip() == "6"
-            i += 2
-            continue
-        if not rare:
-            out.append((a, op, args))
-        i += 1
-    return out
-
-
 def template_args(mangled: str) -> str:
     m = re.search(r"sweep_kernelILi(\d+)ELb(\d)ELi(\d+)E", mangled)
     return f"<{m.group(1)}, {'true' if m.group(2) == '1' else 'false'}, {m.group(3)}>"
@@ -173,7 +155,7 @@ def main():
            "class_median": {"fast_32bit": fast_med, "other": slow_med}, "kernels": {}}
     for name, ins in kernels(disassemble()).items():
         lo, hi = pod_loop(ins)
-        loop = [(op, args) for a, op, args in without_rare(ins) if lo <= a < hi and op.startswith("v_")]
+        loop = [(op, args) for a, op, args in ins if lo <= a < hi and op.startswith("v_")]
         hist = collections.Counter(op for op, _ in loop)
         n = len(loop)
         cyc = covered = 0.0
