@@ -97,7 +97,10 @@ PY
       rc=$?; echo "pass $i ($ctr) rc=$rc"
       [ $rc -eq 0 ] || { tail -5 "$OUT/p$i.err"; exit $rc; }
     done
-    python3 tools/pmc_summary.py "$OUT" --tag "$TAG" --out-dir "$R/gpurun_out/pmc" ;;
+    python3 tools/pmc_summary.py "$OUT" --tag "$TAG" --out-dir "$R/gpurun_out/pmc" || exit 1
+    # the raw counter CSVs (~16 MB per configuration) stay on the box unless
+    # PMC_KEEP_RAW=1: gpurun merges at most 64 MiB of gpurun_out/ back
+    [ "${PMC_KEEP_RAW:-0}" = 1 ] || rm -rf "$OUT"/p[0-9]* ;;
   sq)
     # SQ counters per kernel of one short bench run (e.g. the one-pod path:
     # tools/gpu.sh sq TAG --kind zoned --pods spread --batch 128); value sync
