@@ -1214,6 +1214,7 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
   __shared__ uint32_t s_dz[RK_DZ_NONE];     // live PreScore counts of the other key's domains
   __shared__ uint32_t s_gs[RUN_GROUPS];     // group starts, ascending
   __shared__ uint64_t s_mn[RUN_THREADS / WAVE], s_mx[RUN_THREADS / WAVE], s_bk[RUN_THREADS / WAVE];
+  __shared__ uint64_t s_bk2[RUN_THREADS / WAVE];  // the argmax again when min / max raw moved
   __shared__ uint32_t s_cls[MAX_CLASSES];   // selector classes the pods match (commit: +1 each)
   // 0 groups, 1 refused, 2 classes, 3 RunStop, 4 taken nodes, 5-7 a head that joined them: slot,
   // position, group code, 8 the domain whose count the last commit raised (RK_DZ_NONE: none),
@@ -1352,6 +1353,12 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
         t0 = t1;
       }
     };
+    // min / max raw of the previous pod: this pod's keys are taken with them
+    // and reduced together with this pod's min / max; only when those moved
+    // (a domain's count or a taken node's hostname count raised the least or
+    // the greatest raw, or a group ran out) are the keys taken again
+    uint64_t q_mn = ~0ull, q_mx = 0;
+    bool q_ok = false;  // no previous pod yet
     for (uint32_t pod = a.pod; pod < r.end; ++pod) {
       // raw Scores the last commit moved; min / max raw over the non-ignored
       // feasible nodes
@@ -1369,32 +1376,46 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
         mn = min(mn, traw);
         mx = max(mx, traw);
       }
+      // the candidates' packed keys under min / max raw (pmin, pmax)
+      uint64_t gk = 0, tk = 0;
+      auto keys = [&](uint64_t qmn, uint64_t qmx) {
+        const int64_t pmin = (int64_t)qmn, pmax = (int64_t)qmx;
+        const double pinv = pmax ? 1.0 / (double)pmax : 0.0;
+        auto total_of = [&](uint32_t S, uint32_t code, uint64_t raw) -> int64_t {
+          int64_t norm = 0;  // PodTopologySpread NormalizeScore: ignored -> 0, max 0 -> 100
+          if (!(code & RK_IGN)) norm = pmax == 0 ? 100 : run_div_inv(100 * (pmax + pmin - (int64_t)raw), pmax, pinv);
+          return (int64_t)S + (int64_t)a.w_pts * norm;
+        };
+        gk = g_live ? pack_key(total_of(smask - (uint32_t)(g_key & smask), g_code, graw), (uint32_t)(g_val >> 32)) : 0ull;
+        tk = t_on ? pack_key(total_of(t_S, t_code, traw), t_slot) : 0ull;
+      };
+      // this pod's min / max raw and, with the previous pod's, the argmax: one barrier
+      if (q_ok) keys(q_mn, q_mx);
       mn = run_wave_min(mn);
       mx = wave_max_u64_dpp(mx);
+      uint64_t b = wave_max_u64_dpp(gk > tk ? gk : tk);
       if (lane == 0) {
         s_mn[wid] = mn;
         s_mx[wid] = mx;
+        s_bk[wid] = b;
       }
       run_barrier();
       for (int w = 0; w < RUN_THREADS / WAVE; ++w) {
         mn = min(mn, s_mn[w]);
         mx = max(mx, s_mx[w]);
+        b = s_bk[w] > b ? s_bk[w] : b;
       }
       clock(0);
-      const int64_t pmin = (int64_t)mn, pmax = (int64_t)mx;
-      const double pinv = pmax ? 1.0 / (double)pmax : 0.0;
-      auto total_of = [&](uint32_t S, uint32_t code, uint64_t raw) -> int64_t {
-        int64_t norm = 0;  // PodTopologySpread NormalizeScore: ignored -> 0, max 0 -> 100
-        if (!(code & RK_IGN)) norm = pmax == 0 ? 100 : run_div_inv(100 * (pmax + pmin - (int64_t)raw), pmax, pinv);
-        return (int64_t)S + (int64_t)a.w_pts * norm;
-      };
-      uint64_t gk = 0, tk = 0;
-      if (g_live) gk = pack_key(total_of(smask - (uint32_t)(g_key & smask), g_code, graw), (uint32_t)(g_val >> 32));
-      if (t_on) tk = pack_key(total_of(t_S, t_code, traw), t_slot);
-      uint64_t b = wave_max_u64_dpp(gk > tk ? gk : tk);
-      if (lane == 0) s_bk[wid] = b;
-      run_barrier();
-      for (int w = 0; w < RUN_THREADS / WAVE; ++w) b = s_bk[w] > b ? s_bk[w] : b;
+      if (!q_ok || mn != q_mn || mx != q_mx) {  // (workgroup-uniform)
+        keys(mn, mx);
+        b = wave_max_u64_dpp(gk > tk ? gk : tk);
+        if (lane == 0) s_bk2[wid] = b;
+        run_barrier();
+        for (int w = 0; w < RUN_THREADS / WAVE; ++w) b = s_bk2[w] > b ? s_bk2[w] : b;
+      }
+      q_mn = mn;
+      q_mx = mx;
+      q_ok = true;
       clock(1);
       // The winner commits (AssumePod as spread_commit): a group's head from
       // its row in registers (the node joins the taken nodes as node T: its
