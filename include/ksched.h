@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define KSCHED_ABI_VERSION 5
+#define KSCHED_ABI_VERSION 6
 
 /* ---------------------------------------------------------------- status */
 typedef int32_t ks_status;
@@ -587,6 +587,8 @@ typedef struct {
   uint64_t replica_runs;    /* replica runs of the spread path (spread_replica_runs) */
   uint64_t replica_pods;    /* pods they scheduled (counted in spread_pods too)      */
   double replica_ms;        /* Σ device time of timed replica runs (in spread_ms too) */
+  uint64_t classes_inflight; /* selector classes ks_batch_prepare created while batches ran (no drain) */
+  uint64_t late_class_pods;  /* pods those batches bound that a new class selects, counted at their end */
 } ks_stats;
 ks_status ks_get_stats(ks_ctx *ctx, ks_stats *out);
 ks_status ks_reset_stats(ks_ctx *ctx);

@@ -197,6 +197,8 @@ struct SpreadClass {
   std::string canon;
   uint32_t refs = 0;            // prepared batches using the class
   uint64_t last_use = 0;
+  uint64_t born = 0;            // class_epoch at creation (batches whose cmask predates it: run_batch adds their pods)
+  uint64_t held = 0;            // last run whose cmask holds the class (its commits count it): no reuse before it ends
 };
 // A pod (anti-)affinity term some bound pod carries (InterPodAffinity's
 // existing-pod side): device column = bound pods carrying it, per node
@@ -253,6 +255,8 @@ struct NumCol {
 
 struct ks_batch {
   uint32_t n = 0;
+  uint64_t cmask_epoch = 0;  // class_epoch when the run took the pods' class masks
+  uint64_t run_seq = 0;
   uint32_t dict_version = 0;
   uint32_t names_version = 0;  // 0: no pod of the batch resolved a node name
   bool ext = false, norm = false;
@@ -477,6 +481,8 @@ struct ks_ctx {
   SpreadClass classes[MAX_CLASSES];
   std::unordered_map<std::string, uint32_t> class_of;  // canonical selector -> class
   uint64_t class_seq = 0;
+  uint64_t class_epoch = 0;     // selector classes created
+  uint64_t runs_started = 0, runs_done = 0;  // batch runs (in order, on the worker)
   std::vector<TopoKey> topo;                            // topology-key columns
   std::unordered_map<uint32_t, uint32_t> topo_of;       // key id -> column
   uint32_t *d_dom = nullptr;       // [MAX_TOPO_KEYS][npos]
@@ -1883,7 +1889,7 @@ ks_status topo_column(ks_ctx *c, uint32_t key, bool create, uint32_t *out) {
 
 // Selector class of (namespace, requirements): its column counts the bound
 // pods of every node that the selector matches (created when `create`, from
-// the host's records of bound pods; the caller has drained).
+// the host's records of bound pods).
 ks_status class_get(ks_ctx *c, std::vector<Clause> &&clauses, bool create, uint32_t *out) {
   std::string canon;
   for (const Clause &k : clauses) canon += clause_canon(k) + ';';
@@ -1897,39 +1903,51 @@ ks_status class_get(ks_ctx *c, std::vector<Clause> &&clauses, bool create, uint3
     *out = CLS_NONE;
     return KS_OK;
   }
-  if (c->undrained) return KS_NEED_DRAIN;
+  // With batches in flight (undrained), only a class no bound pod matches
+  // so far (a new deployment's selector) is created: its column starts at
+  // zero, and each batch whose class masks predate it adds the pods it bound
+  // at the end of its run (run_batch); no running batch's commits may touch
+  // the slot (a free one, or one whose last holder has ended).  Otherwise the
+  // caller drains and compiles again.
   ks_status st;
   if ((st = spread_alloc(c))) return st;
   flush_bound(c);  // the column counts every bound pod
+  SpreadClass nk;
+  nk.live = true;
+  nk.clauses = std::move(clauses);
+  nk.canon = canon;
+  // the label sets the selector matches; none that a bound pod ever carried
+  // (a new deployment's selector): the column is zero, no walk over the nodes
+  std::vector<int8_t> match(c->label_sets.size(), 0);
+  bool any = false;
+  for (uint32_t set = 0; set < match.size(); ++set) {
+    match[set] = class_matches(c, nk, set) ? 1 : 0;
+    any |= match[set] && c->label_sets[set].ever_bound;
+  }
+  if (c->undrained && any) return KS_NEED_DRAIN;
   int slot = -1;
   for (int k = 0; k < MAX_CLASSES && slot < 0; ++k)
     if (!c->classes[k].live) slot = k;
   if (slot < 0) {  // evict the least recently used class no prepared batch references
     uint64_t best = UINT64_MAX;
     for (int k = 0; k < MAX_CLASSES; ++k)
-      if (c->classes[k].refs == 0 && c->classes[k].last_use < best) {
+      if (c->classes[k].refs == 0 && c->classes[k].last_use < best &&
+          (!c->undrained || c->classes[k].held <= c->runs_done)) {
         best = c->classes[k].last_use;
         slot = k;
       }
-    if (slot < 0)
+    if (slot < 0) {
+      if (c->undrained) return KS_NEED_DRAIN;
       return c->fail(KS_ERR_CAPACITY, "%d spread selector classes referenced by prepared batches", MAX_CLASSES);
+    }
     c->class_of.erase(c->classes[slot].canon);
   }
   SpreadClass &k = c->classes[slot];
-  k = SpreadClass{};
-  k.live = true;
-  k.clauses = std::move(clauses);
-  k.canon = canon;
+  k = std::move(nk);
   k.last_use = ++c->class_seq;
+  k.born = ++c->class_epoch;
+  if (c->undrained) c->stats.classes_inflight++;
   c->class_of.emplace(canon, (uint32_t)slot);
-  // the label sets the selector matches; none that a bound pod ever carried
-  // (a new deployment's selector): the column is zero, no walk over the nodes
-  std::vector<int8_t> match(c->label_sets.size(), 0);
-  bool any = false;
-  for (uint32_t set = 0; set < match.size(); ++set) {
-    match[set] = class_matches(c, k, set) ? 1 : 0;
-    any |= match[set] && c->label_sets[set].ever_bound;
-  }
   if (!any) {
     HIPC(c, hipMemsetAsync(c->d_cnt + (size_t)slot * c->npos, 0, (size_t)c->npos * 4, c->stream));
     *out = (uint32_t)slot;
@@ -3049,6 +3067,37 @@ ks_status replica_run(ks_ctx *c, ks_batch *b, SpreadArgs sa, uint32_t lo, uint32
   return KS_OK;
 }
 
+// Selector classes created while batch b was in flight (class_get,
+// undrained): +1 in their columns for every pod b bound that they select.
+// Called under mu at the end of b's run.
+ks_status late_class_counts(ks_ctx *c, const ks_batch *b) {
+  std::vector<uint64_t> idx;
+  std::vector<int32_t> dv;
+  for (int k = 0; k < MAX_CLASSES; ++k) {
+    const SpreadClass &q = c->classes[k];
+    if (!q.live || q.born <= b->cmask_epoch) continue;
+    std::vector<int8_t> memo(c->label_sets.size(), -1);
+    for (uint32_t i = 0; i < b->n; ++i) {
+      if (b->h_results[i].status != KS_POD_SCHEDULED) continue;
+      const uint32_t set = b->set_ids[i];
+      if (memo[set] < 0) memo[set] = class_matches(c, q, set) ? 1 : 0;
+      if (!memo[set]) continue;
+      idx.push_back((uint64_t)k * c->npos + c->slot_pos[b->h_results[i].node_index]);
+      dv.push_back(1);
+    }
+  }
+  if (idx.empty()) return KS_OK;
+  c->stats.late_class_pods += idx.size();
+  const size_t bytes = idx.size() * 12 + 1024;
+  ks_status st = xfer_begin(c, bytes, bytes);
+  if (st) return st;
+  uint64_t *d_idx = dscratch<uint64_t>(c, idx.size());
+  int32_t *d_dv = dscratch<int32_t>(c, dv.size());
+  if ((st = h2d(c, d_idx, idx.data(), idx.size() * 8)) || (st = h2d(c, d_dv, dv.data(), dv.size() * 4))) return st;
+  HIPC(c, launch_add_u32(c->d_cnt, d_idx, d_dv, (uint32_t)idx.size(), c->stream));
+  return xfer_sync(c);
+}
+
 // Run a prepared batch to completion on the scheduler streams; the results
 // land in the batch's pinned host buffer.
 ks_status run_batch(ks_ctx *c, ks_batch *b) {
@@ -3077,7 +3126,12 @@ ks_status run_batch(ks_ctx *c, ks_batch *b) {
     if (c->run_profile) c->prof[0] += std::chrono::duration<double>(std::chrono::steady_clock::now() - tw).count();
     if ((st0 = upload_dirty_ext(c, c->xm))) return st0;
     c->run_t = c->t;
-    for (int k = 0; k < MAX_CLASSES; ++k) classes |= c->classes[k].live;
+    b->run_seq = ++c->runs_started;
+    b->cmask_epoch = c->class_epoch;
+    for (int k = 0; k < MAX_CLASSES; ++k) {
+      classes |= c->classes[k].live;
+      if (c->classes[k].live) c->classes[k].held = b->run_seq;
+    }
     if (classes || b->any_spread) {
       std::vector<int32_t> memo(c->label_sets.size(), -1);  // set -> first pod index with it
       for (uint32_t i = 0; i < b->n; ++i) {
@@ -3225,6 +3279,11 @@ ks_status run_batch(ks_ctx *c, ks_batch *b) {
         c->pending_bound.push_back({(uint32_t)b->h_results[i].node_index, b->set_ids[i], +1});
         for (auto &t : c->label_sets[b->set_ids[i]].terms) c->terms[t.first].bound++;  // the commit counted it
       }
+    // classes created while this batch ran (after its class masks): its
+    // commits did not count them, so its bound pods are added here, before
+    // any later batch runs on the stream
+    if (ks_status st = late_class_counts(c, b)) return st;
+    c->runs_done = b->run_seq;
   }
   if (c->timing) {
     ks_status st = collect_timing(c);

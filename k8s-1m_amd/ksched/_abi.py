@@ -299,6 +299,8 @@ class KsStats(C.Structure):
         ("replica_runs", C.c_uint64),
         ("replica_pods", C.c_uint64),
         ("replica_ms", C.c_double),
+        ("classes_inflight", C.c_uint64),
+        ("late_class_pods", C.c_uint64),
     ]
 
 

@@ -29,7 +29,7 @@ def test_libksched_exports_every_declared_symbol():
     lib = _abi.ksched_lib()
     for name in declared("ksched.h", "ks_"):
         assert hasattr(lib, name), name
-    assert lib.ks_abi_version() == 5
+    assert lib.ks_abi_version() == 6
 
 
 def test_libksgather_exports_every_declared_symbol():

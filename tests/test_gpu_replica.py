@@ -5,6 +5,7 @@ and one workgroup per run.  Results and node states against the oracle
 (upstream v1.31.3 podtopologyspread restated in oracle.cpp) bit for bit, and
 the device counters show which path ran."""
 import random
+import time
 
 import pytest
 
@@ -162,4 +163,46 @@ def test_replica_short_sequences_and_taints():
     x.schedule(pods, "short")
     x.states_equal("short")
     assert counters(x)[1] == RUN_MIN_PODS + 64
+    x.close()
+
+
+def test_class_created_while_a_batch_runs():
+    # ks_batch_prepare creates a new deployment's selector class while the
+    # batch before it still runs (ABI 6, no drain).  Batch A binds plain pods
+    # labelled app=late, which no class selects yet; its rounds are held back
+    # 0.3 s (ks_debug_stall), so it is in flight while batch B compiles.  B
+    # holds the replicas of a deployment selecting app=late and of a fresh
+    # one.  A's pods are counted into B's class when A ends
+    # (ks_stats.late_class_pods); results and node states equal the oracle's.
+    from helpers import assert_results_equal, res_array
+    from ksched.objects import pods_array
+    rng = random.Random(61)
+    n = 1200
+    x = Pair(n)
+    x.upsert(rand_nodes(rng, n, 6), list(range(n)))
+    x.schedule(replicas("warm", 1, {"cpu": 100}), "columns")  # topology columns exist
+    plain = [Pod(f"late-{j}", containers=[Container({"cpu": 100, "memory": 64 * Mi})], labels={"app": "late"})
+             for j in range(300)]
+    deps = replicas("late", 48, {"cpu": 250, "memory": 256 * Mi}, j0=1000) + \
+        replicas("fresh", 24, {"cpu": 300, "memory": 128 * Mi})
+    pa, ma = pods_array(plain, x.a)
+    pb, mb = pods_array(deps, x.a)
+    want_a, want_b = x.o.schedule(pa, ma), x.o.schedule(pb, mb)
+    s = x.s
+    s.reset_stats()
+    assert s.lib.ks_debug_stall(s.ctx, 0, 300_000) == 0
+    ba = s.prepare(pa, ma)
+    assert s.lib.ks_batch_submit(s.ctx, ba) == 0, s.lib.ks_last_error(s.ctx)
+    time.sleep(0.05)  # the worker has taken A's class masks; A waits in its held-back round
+    bb = s.prepare(pb, mb)  # A is in flight: the classes are created without a drain
+    assert s.lib.ks_batch_submit(s.ctx, bb) == 0, s.lib.ks_last_error(s.ctx)
+    for b, m, want, what in ((ba, ma, want_a, "batch in flight"), (bb, mb, want_b, "new classes")):
+        assert s.lib.ks_batch_wait(s.ctx, b) == 0, s.lib.ks_last_error(s.ctx)
+        assert_results_equal(s.results(b, m), want, m, what)
+        s.free(b)
+    st = s.stats()
+    bound_a = int((res_array(want_a, ma)["status"] == 0).sum())
+    assert bound_a > 0 and st.classes_inflight == 2 and st.late_class_pods == bound_a, \
+        (bound_a, st.classes_inflight, st.late_class_pods)
+    x.states_equal("late class counts")
     x.close()
