@@ -217,18 +217,15 @@ def test_c3_bench_pipeline_1m_replay():
 
 
 def test_c4_labeled_1m_replay_early_fix():
-    # the C4 bench path: EXT sweep (2 nodes per lane), early FIX, compacted FIX list
+    # the C4 bench path: EXT sweep (2 nodes per lane), early FIX, compacted FIX
+    # list.  (The FIX sweep behind the merge, early_fix = 0, runs at 1M nodes in
+    # test_gpu_multirank.py::test_fullsize_eight_ranks[c4] and on one rank in
+    # test_gpu_semantics.py / test_gpu_dedup.py; its one-rank 1M replay was
+    # dropped in round 5 to keep the suite under the driver's 900 s.)
     r, dbg = run_fullsize(synth.LABELED, synth.pods(synth.LABELED, BATCH, 2), prefill=True,
                           opts={"tuple_guess": 0})  # simple guesses: the FIX path runs often
     assert dbg[4] > 0, "no pod was re-swept with a measured normaliser (FIX path not exercised)"
     assert (r["status"] == 1).any() and (r["status"] == 0).mean() > 0.9
-
-
-def test_c4_labeled_1m_replay_merge_fix():
-    # the same with the FIX sweep behind the merge (the multi-rank order, one rank)
-    r, dbg = run_fullsize(synth.LABELED, synth.pods(synth.LABELED, BATCH, 5), prefill=True,
-                          opts={"early_fix": 0, "tuple_guess": 0})
-    assert dbg[4] > 0
 
 
 def test_c4_labeled_1m_replay_tuple_guess():
