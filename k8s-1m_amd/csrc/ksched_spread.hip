@@ -1170,23 +1170,19 @@ static_assert(RUN_GROUPS == (uint32_t)RUN_THREADS && RUN_TOUCHED == (uint32_t)RU
 // group owners' prefetches of their next nodes' rows)
 __device__ __forceinline__ void run_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// floor(a / b) for 0 <= a < 2^53, 0 < b < 2^53: the binary64 quotient is
-// within one of it; one correction each way makes it exact (int64 division is
-// a long software sequence on the VALU)
-__device__ __forceinline__ int64_t run_div(int64_t a, int64_t b) {
-  int64_t q = (int64_t)((double)a / (double)b);
-  q -= q * b > a ? 1 : 0;
-  q += (q + 1) * b <= a ? 1 : 0;
+// floor(a / b) for a < 2^31, 0 < b < 2^24 and a quotient below 2^7 (the
+// normalised PodTopologySpread score: a = 100 (max + min - raw), b = max, raw
+// in [min, max]), with inv = RN(1 / b): the product is within one of it and
+// the corrections' products stay below 2^31
+__device__ __forceinline__ uint32_t run_div32(uint32_t a, uint32_t b, double inv) {
+  uint32_t q = (uint32_t)((double)a * inv);
+  q -= q * b > a ? 1u : 0u;
+  q += (q + 1) * b <= a ? 1u : 0u;
   return q;
 }
-// the same with inv = RN(1 / b): the product is within one of the quotient too
-__device__ __forceinline__ int64_t run_div_inv(int64_t a, int64_t b, double inv) {
-  int64_t q = (int64_t)((double)a * inv);
-  q -= q * b > a ? 1 : 0;
-  q += (q + 1) * b <= a ? 1 : 0;
-  return q;
-}
-__device__ __forceinline__ uint64_t run_wave_min(uint64_t v) { return ~wave_max_u64_dpp(~v); }
+// raws of a run stay below this (checked at its start): 32-bit min / max and
+// normalisation
+constexpr double RUN_RAW_LIMIT = 16777216.0;  // 2^24
 
 // A node's row as the run kernel carries it
 struct RunRow {
@@ -1213,7 +1209,9 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
   __shared__ Totals s_tot;
   __shared__ uint32_t s_dz[RK_DZ_NONE];     // live PreScore counts of the other key's domains
   __shared__ uint32_t s_gs[RUN_GROUPS];     // group starts, ascending
-  __shared__ uint64_t s_mn[RUN_THREADS / WAVE], s_mx[RUN_THREADS / WAVE], s_bk[RUN_THREADS / WAVE];
+  __shared__ uint32_t s_mn[RUN_THREADS / WAVE], s_mx[RUN_THREADS / WAVE];
+  __shared__ uint64_t s_bk[RUN_THREADS / WAVE];
+  __shared__ uint32_t s_dzmax;  // the largest live domain count at the start
   __shared__ uint64_t s_bk2[RUN_THREADS / WAVE];  // the argmax again when min / max raw moved
   __shared__ uint32_t s_cls[MAX_CLASSES];   // selector classes the pods match (commit: +1 each)
   // 0 groups, 1 refused, 2 classes, 3 RunStop, 4 taken nodes, 5-7 a head that joined them: slot,
@@ -1241,12 +1239,17 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
     s_ctl[3] = RUN_END;
     s_ctl[4] = 0;
     s_ctl[8] = RK_DZ_NONE;
+    s_dzmax = 0;
   }
   __syncthreads();
   const RunCons k = run_cons(s_sd, n);
   const uint32_t G = s_ctl[0], F = s_tot.feasible;
   const uint32_t ndz = k.cz < (uint32_t)MAX_SPREAD ? a.ndom[s_sd[k.cz].key] : 0u;
-  for (uint32_t d = tid; d < ndz; d += RUN_THREADS) s_dz[d] = a.dcnt[(size_t)k.cz * a.dom_cap + d];
+  for (uint32_t d = tid; d < ndz; d += RUN_THREADS) {
+    const uint32_t v = a.dcnt[(size_t)k.cz * a.dom_cap + d];
+    s_dz[d] = v;
+    if (v) atomicMax(&s_dzmax, v);
+  }
   s_gs[tid] = tid < G ? r.gstart[tid] : 0xFFFFFFFFu;
   // bitonic sort of the group starts
   for (uint32_t size = 2; size <= RUN_GROUPS; size <<= 1)
@@ -1277,7 +1280,7 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
   const bool host_first = k.ch < k.cz;
   const double ms_h = k.ch < (uint32_t)MAX_SPREAD ? (double)(s_sd[k.ch].max_skew - 1) : 0.0;
   const double ms_z = k.cz < (uint32_t)MAX_SPREAD ? (double)(s_sd[k.cz].max_skew - 1) : 0.0;
-  auto raw_of = [&](uint32_t code) -> uint64_t {
+  auto raw_of = [&](uint32_t code) -> uint32_t {
     const uint32_t dz = (code >> 8) & RK_DZ_NONE, hk = code & RK_HK_NONE;
     const bool th = k.ch < (uint32_t)MAX_SPREAD && hk != RK_HK_NONE;
     const bool tz = k.cz < (uint32_t)MAX_SPREAD && dz != RK_DZ_NONE;
@@ -1291,8 +1294,16 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
       if (tz) s += xz;
       if (th) s += xh;
     }
-    return (uint64_t)(int64_t)round(s);
+    return (uint32_t)round(s);  // < RUN_RAW_LIMIT (checked below)
   };
+  // Every raw of the run is below RUN_RAW_LIMIT: at most 254 own pods per
+  // node and a domain count at most the largest at the start plus one per
+  // pod of the run.  Otherwise the run is refused (the per-pod chain takes
+  // the pods).
+  const double raw_bound =
+      (k.ch < (uint32_t)MAX_SPREAD ? 254.0 * w_h + ms_h : 0.0) +
+      (k.cz < (uint32_t)MAX_SPREAD ? ((double)s_dzmax + (double)(r.end - a.pod)) * w_z + ms_z : 0.0);
+  const bool raw_narrow = raw_bound + 1.0 < RUN_RAW_LIMIT;
   // group tid: its first untaken sorted index (head), the head's key, position
   // and row (prefetched), the next key and position
   const bool g_on = tid < G;
@@ -1314,16 +1325,16 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
   const uint32_t smask = (1u << r.s_bits) - 1;
   const uint32_t g_code = (uint32_t)(g_key >> r.s_bits) & 0xFFFFFu;
   // raw Score of the group (kept; recomputed when its domain's count moves)
-  uint64_t graw = g_on && !(g_code & RK_IGN) ? raw_of(g_code) : 0ull;
+  uint32_t graw = g_on && !(g_code & RK_IGN) ? raw_of(g_code) : 0u;
   // taken node tid: slot, position, group code (live), S, static tt / na part,
   // row, RN(1 / Allocatable) of cpu and memory, raw Score (kept as graw)
   bool t_on = false, t_dirty = false;
   uint32_t t_slot = 0, t_pos = 0, t_code = 0, t_S = 0, t_stat = 0;
-  uint64_t traw = 0;
+  uint32_t traw = 0;
   __shared__ RunRow s_trow[RUN_TOUCHED];  // taken node t's row (its owner's; the winning head writes it)
   __shared__ double s_tinv[RUN_TOUCHED][2];  // its RN(1 / Allocatable) of cpu and memory
   uint32_t T = 0, next = a.pod, stop = RUN_END;
-  if (s_ctl[1]) {
+  if (s_ctl[1] || !raw_narrow) {
     stop = RUN_REFUSED;
   } else if (F == 0) {
     // no feasible node: every pod of the run gets the same FitError, nothing is committed
@@ -1357,14 +1368,14 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
     // and reduced together with this pod's min / max; only when those moved
     // (a domain's count or a taken node's hostname count raised the least or
     // the greatest raw, or a group ran out) are the keys taken again
-    uint64_t q_mn = ~0ull, q_mx = 0;
+    uint32_t q_mn = ~0u, q_mx = 0;
     bool q_ok = false;  // no previous pod yet
     for (uint32_t pod = a.pod; pod < r.end; ++pod) {
       // raw Scores the last commit moved; min / max raw over the non-ignored
       // feasible nodes
       const uint32_t chg = s_ctl[8];
       const bool g_live = g_on && g_i < g_end;
-      uint64_t mn = ~0ull, mx = 0;
+      uint32_t mn = ~0u, mx = 0;
       if (g_live && !(g_code & RK_IGN)) {
         if (((g_code >> 8) & RK_DZ_NONE) == chg) graw = raw_of(g_code);
         mn = min(mn, graw);
@@ -1378,21 +1389,20 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
       }
       // the candidates' packed keys under min / max raw (pmin, pmax)
       uint64_t gk = 0, tk = 0;
-      auto keys = [&](uint64_t qmn, uint64_t qmx) {
-        const int64_t pmin = (int64_t)qmn, pmax = (int64_t)qmx;
+      auto keys = [&](uint32_t pmin, uint32_t pmax) {
         const double pinv = pmax ? 1.0 / (double)pmax : 0.0;
-        auto total_of = [&](uint32_t S, uint32_t code, uint64_t raw) -> int64_t {
-          int64_t norm = 0;  // PodTopologySpread NormalizeScore: ignored -> 0, max 0 -> 100
-          if (!(code & RK_IGN)) norm = pmax == 0 ? 100 : run_div_inv(100 * (pmax + pmin - (int64_t)raw), pmax, pinv);
-          return (int64_t)S + (int64_t)a.w_pts * norm;
+        auto total_of = [&](uint32_t S, uint32_t code, uint32_t raw) -> int64_t {
+          uint32_t norm = 0;  // PodTopologySpread NormalizeScore: ignored -> 0, max 0 -> 100
+          if (!(code & RK_IGN)) norm = pmax == 0 ? 100u : run_div32(100u * (pmax + pmin - raw), pmax, pinv);
+          return (int64_t)S + (int64_t)a.w_pts * (int64_t)norm;
         };
         gk = g_live ? pack_key(total_of(smask - (uint32_t)(g_key & smask), g_code, graw), (uint32_t)(g_val >> 32)) : 0ull;
         tk = t_on ? pack_key(total_of(t_S, t_code, traw), t_slot) : 0ull;
       };
       // this pod's min / max raw and, with the previous pod's, the argmax: one barrier
       if (q_ok) keys(q_mn, q_mx);
-      mn = run_wave_min(mn);
-      mx = wave_max_u64_dpp(mx);
+      mn = ~wave_max_u32_dpp(~mn);
+      mx = wave_max_u32_dpp(mx);
       uint64_t b = wave_max_u64_dpp(gk > tk ? gk : tk);
       if (lane == 0) {
         s_mn[wid] = mn;
