@@ -1370,6 +1370,20 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
     // the greatest raw, or a group ran out) are the keys taken again
     uint32_t q_mn = ~0u, q_mx = 0;
     bool q_ok = false;  // no previous pod yet
+    // the run's constant result fields and selector classes, in registers
+    DevResult res_tpl;
+    res_tpl.node_index = -1;
+    res_tpl.status = 0;
+    res_tpl.total_score = 0;
+    res_tpl.feasible_nodes = F;
+    res_tpl.evaluated_nodes = a.evaluated;
+    for (int q = 0; q < NFILT; ++q) res_tpl.fail_counts[q] = s_tot.fail[q];
+    res_tpl.spread_fail = s_tot.fail[PLUGIN_SPREAD];
+    res_tpl.ipa_fail = s_tot.fail[PLUGIN_IPA];
+    res_tpl._pad = 0;
+    res_tpl.prefiltered = p.prefilter_out;
+    res_tpl.flags = F == 1 ? 1u : 0u;  // KS_RESULT_SINGLE_FEASIBLE
+    const uint32_t ncls = s_ctl[2], cls0 = ncls > 0 ? s_cls[0] : 0u, cls1 = ncls > 1 ? s_cls[1] : 0u;
     for (uint32_t pod = a.pod; pod < r.end; ++pod) {
       // raw Scores the last commit moved; min / max raw over the non-ignored
       // feasible nodes
@@ -1455,20 +1469,18 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
           ic = s_tinv[tid][0];
           im = s_tinv[tid][1];
         }
-        // Requested, NonZeroRequested, pod count, class columns
+        // Requested, NonZeroRequested, pod count
         w.rc += p.req_cpu;
         w.rm += p.req_mem;
         w.zc += p.nz_cpu;
         w.zm += p.nz_mem;
         w.np += 1;
-        a.t.rcpu[pos] = w.rc;
-        a.t.rmem[pos] = w.rm;
-        a.t.zcpu[pos] = w.zc;
-        a.t.zmem[pos] = w.zm;
-        a.t.npods[pos] = w.np;
-        // no returned value: the stores leave without a round trip on the pod's path
-        for (uint32_t q = 0; q < s_ctl[2]; ++q) atomicAdd(&a.cnt[(size_t)s_cls[q] * a.npos + pos], 1u);
-        // the next pod's view of the node: own hostname count, its domain's count, S, Fit
+        // the next pod's view of the node first (its S and Fit: the long
+        // binary64 chain), then the stores nothing in the run reads
+        const NodeRegs g = make_regs_inv(w.ac, w.am, w.rc, w.rm, w.zc, w.zm, w.ap, w.np, slot, ic, im);
+        const uint32_t S = (uint32_t)a.w.fit * (uint32_t)score_la(p, g) + (uint32_t)a.w.ba * (uint32_t)score_ba(p, g) + stat;
+        const bool fit_lost = filter<false>(p, a.clauses, g, NodeExt{}) != ST_FEASIBLE;
+        // own hostname count, its domain's count
         if (inc_h && (code & RK_HK_NONE) != RK_HK_NONE) {
           code += 1;
           if ((code & RK_HK_NONE) == RK_HK_NONE) s_ctl[3] = RUN_FULL;  // beyond the key's range
@@ -1477,24 +1489,21 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
         if (inc_z && !(code & RK_IGN)) {
           const uint32_t dz = (code >> 8) & RK_DZ_NONE;
           moved = dz == RK_DZ_NONE ? 0u : dz;  // PreScore counts a node lacking the key in ""
-          s_dz[moved] += 1;
+          atomicAdd(&s_dz[moved], 1u);          // (no returned value: no LDS round trip)
         }
         s_ctl[8] = moved;
-        const NodeRegs g = make_regs_inv(w.ac, w.am, w.rc, w.rm, w.zc, w.zm, w.ap, w.np, slot, ic, im);
-        const uint32_t S = (uint32_t)a.w.fit * (uint32_t)score_la(p, g) + (uint32_t)a.w.ba * (uint32_t)score_ba(p, g) + stat;
-        if (filter<false>(p, a.clauses, g, NodeExt{}) != ST_FEASIBLE) s_ctl[3] = RUN_FIT;
-        DevResult res;
+        if (fit_lost) s_ctl[3] = RUN_FIT;  // (after RUN_FULL: a Fit loss wins, as before)
+        a.t.rcpu[pos] = w.rc;
+        a.t.rmem[pos] = w.rm;
+        a.t.zcpu[pos] = w.zc;
+        a.t.zmem[pos] = w.zm;
+        a.t.npods[pos] = w.np;
+        // class columns: no returned value, the atomics leave without a round trip
+        for (uint32_t q = 0; q < ncls; ++q)
+          atomicAdd(&a.cnt[(size_t)(q < 2 ? (q ? cls1 : cls0) : s_cls[q]) * a.npos + pos], 1u);
+        DevResult res = res_tpl;
         res.node_index = (int32_t)slot;
-        res.status = 0;
         res.total_score = (int64_t)(b >> 32) - 1;
-        res.feasible_nodes = F;
-        res.evaluated_nodes = a.evaluated;
-        for (int q = 0; q < NFILT; ++q) res.fail_counts[q] = s_tot.fail[q];
-        res.spread_fail = s_tot.fail[PLUGIN_SPREAD];
-        res.ipa_fail = s_tot.fail[PLUGIN_IPA];
-        res._pad = 0;
-        res.prefiltered = p.prefilter_out;
-        res.flags = F == 1 ? 1u : 0u;  // KS_RESULT_SINGLE_FEASIBLE
         a.results[pod] = res;
         const uint32_t j = gwin ? T : tid;
         s_trow[j] = w;
