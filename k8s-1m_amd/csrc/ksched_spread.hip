@@ -1369,6 +1369,7 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
     // (a domain's count or a taken node's hostname count raised the least or
     // the greatest raw, or a group ran out) are the keys taken again
     uint32_t q_mn = ~0u, q_mx = 0;
+    double q_pinv = 0.0;  // RN(1 / q_mx)
     bool q_ok = false;  // no previous pod yet
     // the run's constant result fields and selector classes, in registers
     DevResult res_tpl;
@@ -1403,8 +1404,7 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
       }
       // the candidates' packed keys under min / max raw (pmin, pmax)
       uint64_t gk = 0, tk = 0;
-      auto keys = [&](uint32_t pmin, uint32_t pmax) {
-        const double pinv = pmax ? 1.0 / (double)pmax : 0.0;
+      auto keys = [&](uint32_t pmin, uint32_t pmax, double pinv) {
         auto total_of = [&](uint32_t S, uint32_t code, uint32_t raw) -> int64_t {
           uint32_t norm = 0;  // PodTopologySpread NormalizeScore: ignored -> 0, max 0 -> 100
           if (!(code & RK_IGN)) norm = pmax == 0 ? 100u : run_div32(100u * (pmax + pmin - raw), pmax, pinv);
@@ -1414,7 +1414,7 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
         tk = t_on ? pack_key(total_of(t_S, t_code, traw), t_slot) : 0ull;
       };
       // this pod's min / max raw and, with the previous pod's, the argmax: one barrier
-      if (q_ok) keys(q_mn, q_mx);
+      if (q_ok) keys(q_mn, q_mx, q_pinv);
       mn = ~wave_max_u32_dpp(~mn);
       mx = wave_max_u32_dpp(mx);
       uint64_t b = wave_max_u64_dpp(gk > tk ? gk : tk);
@@ -1431,7 +1431,8 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
       }
       clock(0);
       if (!q_ok || mn != q_mn || mx != q_mx) {  // (workgroup-uniform)
-        keys(mn, mx);
+        if (!q_ok || mx != q_mx) q_pinv = mx ? 1.0 / (double)mx : 0.0;
+        keys(mn, mx, q_pinv);
         b = wave_max_u64_dpp(gk > tk ? gk : tk);
         if (lane == 0) s_bk2[wid] = b;
         run_barrier();
