@@ -3148,7 +3148,9 @@ ks_status run_batch(ks_ctx *c, ks_batch *b) {
       }
     }
   }
+  const auto tu = std::chrono::steady_clock::now();
   if (!b->uploaded && (st0 = upload_batch(c, b))) return st0;
+  if (c->run_profile) c->prof[5] += std::chrono::duration<double>(std::chrono::steady_clock::now() - tu).count();
   if (classes || b->any_spread)
     HIPC(c, hipMemcpyAsync(b->d_cmask, b->h_cmask, (size_t)std::max<uint32_t>(b->n, 1) * 8 * CMASK_WORDS, hipMemcpyHostToDevice,
                            c->stream));
@@ -3272,7 +3274,9 @@ ks_status run_batch(ks_ctx *c, ks_batch *b) {
   {
     // NodeInfo.Pods of the nodes this batch bound pods to (later selector
     // classes count them): appended to a log, applied when read
+    const auto tw = std::chrono::steady_clock::now();
     std::lock_guard<std::mutex> g(c->mu);
+    if (c->run_profile) c->prof[4] += std::chrono::duration<double>(std::chrono::steady_clock::now() - tw).count();
     if (c->pending_bound.size() > (1u << 24)) flush_bound(c);
     for (uint32_t i = 0; i < b->n; ++i)
       if (b->h_results[i].status == KS_POD_SCHEDULED) {
@@ -3286,7 +3290,9 @@ ks_status run_batch(ks_ctx *c, ks_batch *b) {
     c->runs_done = b->run_seq;
   }
   if (c->timing) {
+    const auto tt = std::chrono::steady_clock::now();
     ks_status st = collect_timing(c);
+    if (c->run_profile) c->prof[6] += std::chrono::duration<double>(std::chrono::steady_clock::now() - tt).count();
     if (st) return st;
   }
   c->prof[3] += 1;
@@ -3535,11 +3541,11 @@ void ks_close(ks_ctx *c) {
   c->runq->profile(wp);
   if (c->run_profile)
     std::fprintf(stderr,
-                 "ksched runs: %.0f runs: lock wait %.3f s, enqueue %.3f s, drains %.3f s; worker: %.0f runs %.3f s, "
-                 "idle between runs %.3f s; prepare: drain wait %.3f s, compile %.3f s, acquire / copy / "
-                 "upload %.3f s\n",
-                 c->prof[3], c->prof[0], c->prof[1], c->prof[2], wp[2], wp[0], wp[1], c->prof[7],
-                 c->prof[8], c->prof[9]);
+                 "ksched runs: %.0f runs: lock wait %.3f s (at the end %.3f s), enqueue %.3f s, drains %.3f s; "
+                 "worker: %.0f runs %.3f s, idle between runs %.3f s; prepare: drain wait %.3f s, compile %.3f s, "
+                 "acquire / copy / upload %.3f s; in runs: upload %.3f s, timing read-back %.3f s\n",
+                 c->prof[3], c->prof[0], c->prof[4], c->prof[1], c->prof[2], wp[2], wp[0], wp[1], c->prof[7],
+                 c->prof[8], c->prof[9], c->prof[5], c->prof[6]);
   if (c->run_profile && c->rk_prof[3]) {
     const uint64_t *h = c->rk_prof;
     const double n = (double)h[3];
