@@ -402,8 +402,8 @@ typedef struct {
                                      KS_RESOLVE_PARALLEL */
   uint32_t resolve_par_max_passes;  /* AUTO: a round needing more chunk passes than this (32, 1..257),
                                        or on pace (after 4) to need more, ends early and ...          */
-  uint32_t resolve_serial_rounds;   /* ... hands this many following rounds (16, <= 2^20; doubled per
-                                       consecutive cut, up to 16x) to the serial kernel               */
+  uint32_t resolve_serial_rounds;   /* ... hands this many following rounds (4, <= 2^20; doubled per
+                                       consecutive cut, up to 256 rounds or 16x) to the serial kernel  */
   uint32_t dedup_identical_pods;  /* 1 (default): a round's byte-identical pods are swept once (§5.5) */
   uint32_t early_fix;             /* 1 (default): on one rank the normaliser FIX re-sweep follows the
                                      sweep on its stream (§5.2); 0: behind the merge (multi-rank order) */

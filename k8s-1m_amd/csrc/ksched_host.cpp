@@ -356,7 +356,7 @@ struct ks_ctx {
   // launches the parallel commit with the serial kernel behind it as its
   // fallback (RoundArgs::rmode, the two words at d_flags + 4)
   uint32_t resolve_mode = KS_RESOLVE_AUTO;
-  uint32_t par_max_passes = 32, serial_rounds = 16;
+  uint32_t par_max_passes = 32, serial_rounds = 4;
   bool res_profile = false;  // ks_debug_set_profile: phase clocks of the parallel commit
   bool dedup = true;        // dedup_identical_pods: sweep identical pods of a round once
   bool tuple_guess = true;  // normaliser guesses over node tuples (refine_guesses)
@@ -3345,7 +3345,7 @@ void ks_config_default(ks_config *cfg) {
   cfg->percentage_of_nodes_to_score = 100;
   cfg->resolve_mode = KS_RESOLVE_AUTO;
   cfg->resolve_par_max_passes = 32;
-  cfg->resolve_serial_rounds = 16;
+  cfg->resolve_serial_rounds = 4;
   cfg->dedup_identical_pods = 1;
   cfg->early_fix = 1;
   cfg->tuple_guess = 1;

@@ -64,7 +64,7 @@ constexpr uint32_t PSRC_M = 0x10000u;  // proposal source: Rpre's node (M index 
 static_assert(PCH == WAVE, "B1 runs one chunk pod per lane of one wave");
 
 // decision codes (proposal and exact)
-constexpr uint32_t PAR_RATE_PASSES = 4, PAR_MAX_BACKOFF = 16;
+constexpr uint32_t PAR_RATE_PASSES = 4, PAR_MAX_BACKOFF = 16, PAR_MAX_STRETCH = 256;
 enum : uint32_t { PD_NODE = 0, PD_UNSCHED = 1, PD_ERROR = 2, PD_STOP = 3, PD_INCOMPLETE = 4 };
 
 // Resource-only pod as the commit evaluates it: Fit thresholds (request, or
@@ -941,10 +941,11 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
       a.rmode[1] = a.seq;  // resolve_kernel, launched after this one, skips the round
       if (bailed) {
         // hand over; every consecutive bail doubles the serial stretch
-        // (rmode[2]), up to PAR_MAX_BACKOFF times serial_rounds
+        // (rmode[2]), up to PAR_MAX_STRETCH rounds (PAR_MAX_BACKOFF times
+        // serial_rounds when that is more)
         const uint32_t b = max(a.rmode[2], a.serial_rounds);
         a.rmode[0] = b;
-        a.rmode[2] = min(2 * b, PAR_MAX_BACKOFF * a.serial_rounds);
+        a.rmode[2] = min(2 * b, max(PAR_MAX_STRETCH, PAR_MAX_BACKOFF * a.serial_rounds));
         a.counters[CTR_PAR_BAILS] += 1;
       } else {
         a.rmode[2] = 0;
