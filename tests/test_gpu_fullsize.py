@@ -253,7 +253,16 @@ def test_kwok_1m_c1_pods_k512_replay():
     # survive the previous round's commits to identical nodes
     r, dbg = run_fullsize(synth.KWOK, synth.pods(synth.KWOK, BATCH, 2), prefill=False, topk=512)
     assert (r["status"] == 0).all()
-    assert dbg[3] * 20 < dbg[0], f"wasted speculative rounds {dbg[3]} of {dbg[0]}"
+    # Under resolve AUTO every parallel-commit bail (dbg[14]) cuts its round,
+    # so the next round's speculative sweep is wasted by design; the serial
+    # stretch after a bail starts at 4 rounds and doubles up to 256, so at most
+    # 7 consecutive bails happen before AUTO settles (4, 8, ..., 256).  Those
+    # are bounded on their own; every other wasted round means the 512-entry
+    # lists did not survive the previous round's commits.
+    bails = int(dbg[14])
+    assert bails <= 8, f"parallel-commit bails {bails} of {dbg[0]} rounds"
+    other = max(int(dbg[3]) - bails, 0)
+    assert other * 20 < dbg[0], f"wasted speculative rounds {dbg[3]} ({bails} AUTO cuts) of {dbg[0]}"
 
 
 class MixedStream:
