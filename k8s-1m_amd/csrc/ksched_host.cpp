@@ -2861,12 +2861,12 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k, uint32_t end) {
     ra.par_max_passes = c->par_max_passes;
     ra.prof = c->res_profile ? c->d_counters + 16 : nullptr;
     ra.serial_rounds = c->serial_rounds;
-    if (!b->ext && c->resolve_mode != KS_RESOLVE_SERIAL) {
+    if (c->resolve_mode != KS_RESOLVE_SERIAL) {
       // the parallel commit; under RES_AUTO the serial kernel follows and
       // resolves the round only if the parallel one handed it over
       ra.rmode = c->resolve_mode == KS_RESOLVE_AUTO ? c->d_flags + 4 : nullptr;
-      HIPC(c, launch_resolve_par(ra, c->rstream));
-      if (ra.rmode) HIPC(c, launch_resolve(ra, false, c->rstream));
+      HIPC(c, launch_resolve_par(ra, b->ext, c->rstream));
+      if (ra.rmode) HIPC(c, launch_resolve(ra, b->ext, c->rstream));
     } else {
       ra.rmode = nullptr;
       HIPC(c, launch_resolve(ra, b->ext, c->rstream));

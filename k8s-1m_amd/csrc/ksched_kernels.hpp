@@ -198,7 +198,7 @@ hipError_t launch_merge_shards(const RoundArgs &a, hipStream_t st);
 hipError_t launch_gather_cand(const RoundArgs &a, bool ext, hipStream_t st);
 hipError_t launch_patch(const RoundArgs &a, bool ext, hipStream_t st);
 hipError_t launch_resolve(const RoundArgs &a, bool ext, hipStream_t st);
-hipError_t launch_resolve_par(const RoundArgs &a, hipStream_t st);
+hipError_t launch_resolve_par(const RoundArgs &a, bool ext, hipStream_t st);
 hipError_t launch_advance(const RoundArgs &a, hipStream_t st);
 hipError_t launch_advance_writeback(const RoundArgs &a, const CarryRec *carry, const uint32_t *n, hipStream_t st);
 hipError_t launch_writeback(const NodeTable &t, const CarryRec *carry, const uint32_t *n, hipStream_t st);

@@ -1,5 +1,6 @@
 // ksched_resolve.hip — the round's in-order commit as a parallel proposal /
-// verify over chunks of the window (resource-only rounds).
+// verify over chunks of the window (resource-only and label / taint rounds;
+// DESIGN.md §5.6).
 //
 // Sequential semantics (the serial resolve_kernel in
 // ksched_kernels.hip): pod j's winner is the best of (a) its first listed
@@ -33,9 +34,9 @@
 // fixed prefix exactly), so a C3 round of 256 pods takes 6-12 passes
 // (tools/jacobi_sim.cpp).  Rounds whose pods pile onto the same nodes (kwok
 // clusters of identical nodes) would take many passes: under RESOLVE_AUTO such
-// a round is cut short (pass cap / too few pods per pass) and the following
-// rounds run the serial kernel, a stretch that doubles per consecutive cut
-// (RoundArgs::rmode).
+// a round is handed whole to the serial kernel (pass cap / too few pods per
+// pass), and so are the following rounds, a stretch that doubles per
+// consecutive hand-over (RoundArgs::rmode).
 //
 // Arithmetic is the serial kernel's (exact binary64 rows, one-FMA
 // LeastAllocated, Markstein BalancedAllocation; ksched_eval.hpp), and the
@@ -53,9 +54,8 @@ namespace ks {
 constexpr int PR_THREADS = 1024;
 constexpr int PR_NW = PR_THREADS / WAVE;
 constexpr int PCH = 64;     // pods per chunk: one deferred-acceptance lane each
-constexpr int PNC = 16;     // candidates gathered per chunk pod
+constexpr int PNC = 16;     // candidates gathered per chunk pod (resource-only rounds)
 constexpr int PMH = 1024;   // modified-slot hash (rhash: 10 bits), M <= MAX_P nodes
-constexpr int PDH = 2048;   // chunk claim hash (<= PCH * PNC + PCH slots)
 constexpr int PNR = 4;      // candidates per chunk pod whose rows are prefetched (LDS-DMA)
 constexpr int PGH_BITS = 7, PGH = 1 << PGH_BITS;  // chunk slot-group hash (<= PCH slots)
 constexpr int ROW_PIECES = sizeof(CandRow) / 16;
@@ -90,8 +90,103 @@ __device__ __forceinline__ bool pq_fit(const PQ &q, const CandRow &r, double rc,
   return np + 1 <= r.apods && !(q.rqc > r.acpu - rc) && !(q.rqm > r.amem - rm);
 }
 
-// packed key of the pod on the row's live state (0: infeasible): key_q on rnode_regs
-__device__ __forceinline__ uint64_t pq_key(const PQ &q, const CandRow &r, uint32_t slot, const Weights &w) {
+// Label / taint pods (EXT rounds): the part of the pod the resource-free
+// filters and scores read.  Labels, taints and the normaliser maxima do not
+// change within a round, so a node's status before NodeResourcesFit and its
+// normalised TaintToleration / NodeAffinity scores are fixed for the round.
+struct alignas(16) PX {
+  uint64_t tol_hard, tol_prefer;
+  uint32_t flags;
+  int32_t name_slot;
+  uint32_t req_off, req_len, pref_off, pref_len, pre_off, pre_len;
+  uint32_t tt_max, na_max;  // the measured maxima (norm_check) the sweep scored with
+  uint32_t _pad[2];
+};
+static_assert(sizeof(PX) == 64, "PX layout");
+
+__device__ __forceinline__ PX make_px(const PodDev &p, uint32_t tt_max, uint32_t na_max) {
+  PX x;
+  x.tol_hard = p.tol_hard;
+  x.tol_prefer = p.tol_prefer;
+  x.flags = p.flags;
+  x.name_slot = p.name_slot;
+  x.req_off = p.req_off;
+  x.req_len = p.req_len;
+  x.pref_off = p.pref_off;
+  x.pref_len = p.pref_len;
+  x.pre_off = p.pre_off;
+  x.pre_len = p.pre_len;
+  x.tt_max = tt_max;
+  x.na_max = na_max;
+  x._pad[0] = x._pad[1] = 0;
+  return x;
+}
+
+// The resource-free part of an EXT pod on a node: st = the first failing
+// filter before NodeResourcesFit (filter<true>'s order), ST_FEASIBLE if none;
+// ss = w_tt x TaintToleration + w_na x NodeAffinity as total_score<true>
+// adds them; at = bit 0 / 1: the node's raw TaintToleration / NodeAffinity
+// score is the pod's max (the node counts in ShardRecHdr::tt_cnt / na_cnt
+// while it is feasible).
+struct XS {
+  int32_t st;
+  int32_t ss;
+  uint32_t at;
+};
+__device__ __forceinline__ XS px_static(const PX &x, const uint64_t *clauses, const CandExt &cx, uint32_t slot,
+                                        const Weights &w) {
+  PodDev p;  // the fields the label programs read
+  p.flags = x.flags;
+  p.tol_prefer = x.tol_prefer;
+  p.req_off = x.req_off;
+  p.req_len = x.req_len;
+  p.pref_off = x.pref_off;
+  p.pref_len = x.pref_len;
+  p.pre_off = x.pre_off;
+  p.pre_len = x.pre_len;
+  NodeExt e;
+  e.hard = cx.w[0];
+  e.prefer = cx.w[1];
+#pragma unroll
+  for (int k = 0; k < LW; ++k) e.lab[k] = cx.w[2 + k];
+#pragma unroll
+  for (int k = 0; k < NNUM; ++k) e.num[k] = (int64_t)cx.w[2 + LW + k];
+  XS r;
+  r.st = ST_FEASIBLE;
+  r.ss = w.tt * 100;
+  r.at = 0;
+  if (x.flags & PF_EXT) {
+    const uint64_t untol = e.hard & ~x.tol_hard;
+    if (x.flags & PF_NA_CONFLICT) r.st = 3;
+    else if ((x.flags & PF_PREFILTER) && !prefilter_match(p, clauses, slot)) r.st = ST_PREFILTERED;
+    else if (untol & UNSCHED_BIT) r.st = 0;                                          // NodeUnschedulable
+    else if (x.name_slot != -1 && (int64_t)slot != (int64_t)x.name_slot) r.st = 1;  // NodeName
+    else if (untol) r.st = 2;                                                        // TaintToleration
+    else if ((x.flags & PF_AFF) && !required_match(p, clauses, e, slot)) r.st = 3;   // NodeAffinity
+  }
+  if (r.st != ST_FEASIBLE) return r;
+  if (x.flags & PF_TT) {
+    const int64_t raw = taint_raw(p, e);
+    r.ss = w.tt * (int32_t)normalize(raw, x.tt_max, true);
+    r.at |= raw == (int64_t)x.tt_max ? 1u : 0u;
+  }
+  if (x.flags & PF_HAS_PREF) {
+    int32_t na = 0;
+    if (x.flags & PF_NA) {
+      const int64_t raw = preferred_raw(p, clauses, e, slot);
+      na = (int32_t)normalize(raw, x.na_max, false);
+      r.at |= raw == (int64_t)x.na_max ? 2u : 0u;
+    }
+    r.ss += (int32_t)wmul((uint32_t)w.na, (uint32_t)na);
+  }
+  return r;
+}
+
+// packed key of the pod on the row's live state (0: infeasible): key_q on
+// rnode_regs, with the resource-free score part ss (w_tt x 100 for a
+// resource-only pod)
+__device__ __forceinline__ uint64_t pq_key_ss(const PQ &q, const CandRow &r, uint32_t slot, const Weights &w,
+                                              int32_t ss) {
   if (!pq_fit(q, r, r.rc, r.rm, r.np)) return 0;
   NodeRegs g;
   g.free_cpu = r.acpu - r.rc;
@@ -111,8 +206,45 @@ __device__ __forceinline__ uint64_t pq_key(const PQ &q, const CandRow &r, uint32
   const int32_t la = (least_requested(g.lf100_cpu, q.zc, g.inv_cpu) + least_requested(g.lf100_mem, q.zm, g.inv_mem)) >>
                      g.lashift;
   const int32_t ba = score_ba_sum(g.rcpu + q.rc, g.rmem + q.rm, g);
-  const int32_t t = (int32_t)wmul((uint32_t)w.fit, (uint32_t)la) + (int32_t)wmul((uint32_t)w.ba, (uint32_t)ba) + w.tt * 100;
+  const int32_t t = (int32_t)wmul((uint32_t)w.fit, (uint32_t)la) + (int32_t)wmul((uint32_t)w.ba, (uint32_t)ba) + ss;
   return pack_key(t, slot);
+}
+__device__ __forceinline__ uint64_t pq_key(const PQ &q, const CandRow &r, uint32_t slot, const Weights &w) {
+  return pq_key_ss(q, r, slot, w, w.tt * 100);
+}
+
+// One (pod, node) pair of a round: the key on the node's live row and the
+// status change since `rc0 / rm0 / np0` (the row the pod's counts were taken
+// on): lost = 1 when the node was feasible there and is not now (only
+// NodeResourcesFit can change), `at` the normaliser-at-max bits it takes
+// with it (EXT).  Resource-only pods: every filter but Fit passes.
+struct PairEval {
+  uint64_t key;
+  int32_t lost;
+  uint32_t at_lost;
+};
+template <bool EXT>
+__device__ __forceinline__ PairEval pair_eval(const PQ &q, const PX *px, const uint64_t *clauses, const CandRow &r,
+                                              const CandExt *cx, uint32_t slot, double rc0, double rm0, int32_t np0,
+                                              const Weights &w) {
+  PairEval v;
+  int32_t ss = w.tt * 100;
+  uint32_t at = 0;
+  if constexpr (EXT) {
+    const XS xs = px_static(*px, clauses, *cx, slot, w);
+    if (xs.st != ST_FEASIBLE) {
+      v.key = 0;
+      v.lost = 0;
+      v.at_lost = 0;
+      return v;
+    }
+    ss = xs.ss;
+    at = xs.at;
+  }
+  v.key = pq_key_ss(q, r, slot, w, ss);
+  v.lost = (pq_fit(q, r, rc0, rm0, np0) ? 1 : 0) - (v.key != 0 ? 1 : 0);
+  v.at_lost = v.lost ? at : 0u;
+  return v;
 }
 
 __device__ __forceinline__ void pq_add(CandRow &r, const PQ &q) {  // NodeInfo.AddPod: exact binary64 sums
@@ -143,11 +275,30 @@ struct PhaseClock {
 };
 
 __device__ __forceinline__ uint32_t key_slot(uint64_t k) { return 0xFFFFFFFFu - (uint32_t)k; }
-__device__ __forceinline__ uint32_t dhash(uint32_t x) { return (x * 2654435761u) >> 21; }  // 11 bits
+template <int BITS>
+__device__ __forceinline__ uint32_t dhash(uint32_t x) { return (x * 2654435761u) >> (32 - BITS); }
 
+// EXT rounds carry each M node's and each proposal's label / taint words and
+// each pod's PX beside the resource rows; to stay within the CU's LDS they
+// gather PNC_EXT candidates per chunk pod (claims hash halved accordingly)
+// and prefetch the rows of the first PNR_EXT, and have no one-step path
+// (label / taint batches keep one record per pod: no identical-pod classes).
+constexpr int PNC_EXT = 8, PNR_EXT = 2;
+constexpr int EXT_PIECES = sizeof(CandExt) / 16;
+
+template <bool EXT>
 __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
+  constexpr int NC = EXT ? PNC_EXT : PNC;      // candidates gathered per chunk pod
+  constexpr int NR = EXT ? PNR_EXT : PNR;      // ... whose rows are prefetched
+  constexpr int DH_BITS = EXT ? 10 : 11;
+  constexpr int DH = 1 << DH_BITS;             // chunk claim hash (<= PCH * NC + PCH slots)
+  static_assert(DH >= PCH * NC + PCH, "claims hash: every slot a chunk can claim");
+  constexpr int XP = EXT ? 1 : 0;              // EXT-only arrays: full size, else one element
+  constexpr int FP = EXT ? 0 : 1;              // one-step-path arrays (resource-only rounds)
   // ---- per pod of the round
   __shared__ PQ s_q[MAX_P];
+  __shared__ PX s_px[XP ? MAX_P : 1];          // EXT: labels / taints / normaliser maxima
+  __shared__ uint32_t s_dn[XP ? MAX_P : 1];    // EXT: normaliser-at-max nodes lost to the fixed prefix (tt | na << 16)
   __shared__ uint32_t s_fl[MAX_P];
   __shared__ ShardRecHdr s_hdr[MAX_P];
   __shared__ uint32_t s_rep[MAX_P];
@@ -160,13 +311,15 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
   __shared__ uint32_t s_pfo[MAX_P];    // result: PodDev::prefilter_out (staged: no global read in the epilogue)
   // ---- fixed modified nodes (M): live row, round-start Requested / pod count, slot
   __shared__ RNode s_m[MAX_P];
+  __shared__ CandExt s_mx[XP ? MAX_P : 1];   // EXT: their label / taint words
   __shared__ uint32_t s_mh[PMH], s_mi[PMH];  // slot + 1 -> M index
   // ---- chunk
-  __shared__ uint64_t s_ck[PCH][PNC];  // gathered candidates: keys ...
-  __shared__ uint16_t s_ce[PCH][PNC];  // ... and list entries
-  __shared__ uint4 s_crow[PCH][ROW_PIECES][PNR];  // the first PNR candidates' rows (LDS-DMA)
+  __shared__ uint64_t s_ck[PCH][NC];  // gathered candidates: keys ...
+  __shared__ uint16_t s_ce[PCH][NC];  // ... and list entries
+  __shared__ uint4 s_crow[PCH][ROW_PIECES][NR];  // the first NR candidates' rows (LDS-DMA)
+  __shared__ uint4 s_crowx[XP ? PCH : 1][EXT_PIECES][NR];  // EXT: ... and their label / taint words
   __shared__ uint32_t s_cnc[PCH], s_cmore[PCH], s_cpst[PCH];
-  __shared__ uint32_t s_dh[PDH], s_do[PDH];  // claims: slot + 1 -> lowest claiming chunk pod
+  __shared__ uint32_t s_dh[DH], s_do[DH];    // claims: slot + 1 -> lowest claiming chunk pod
   __shared__ uint32_t s_gh[PGH];             // chunk slot groups: slot + 1 ...
   __shared__ uint64_t s_gm[PGH];             // ... -> lanes
   __shared__ uint64_t s_pk[PCH];    // proposal key
@@ -174,8 +327,10 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
   __shared__ uint32_t s_pnx[PCH];   // next chunk pod proposing the same slot (PNONE)
   __shared__ uint32_t s_pfst[PCH];  // first chunk pod proposing its slot
   __shared__ RNode s_prow[PCH];     // proposed node's state at the chunk start
+  __shared__ CandExt s_prowx[XP ? PCH : 1];  // EXT: its label / taint words
   __shared__ uint64_t s_ik[PCH];    // best key over nodes taken earlier in the chunk
   __shared__ int32_t s_idl[PCH];    // feasible nodes lost to them
+  __shared__ uint32_t s_idn[XP ? PCH : 1];   // EXT: normaliser-at-max nodes lost to them
   __shared__ uint32_t s_cdm[PCH];   // distinct nodes committed by the fixed pods: M index,
   __shared__ double s_cdp[PCH][2];  // Requested before this chunk's commits,
   __shared__ int32_t s_cdn[PCH];    // pod count before,
@@ -183,9 +338,9 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
   // control: [0] f, [1] stopped, [2] cut, [4] distinct nodes, [5] |M|, [6] passes
   __shared__ uint32_t s_ctl[8];
   // a round of identical request-less pods in one step (identical_round below)
-  __shared__ uint64_t s_ek[PR_THREADS];  // entries: node key after k of the round's pods
-  __shared__ uint32_t s_ex[PR_THREADS];  //   list index << 16 | k << 1 | Fit lost by taking it
-  __shared__ uint32_t s_tx[MAX_K];       // pods each listed node takes
+  __shared__ uint64_t s_ek[FP ? PR_THREADS : 1];  // entries: node key after k of the round's pods
+  __shared__ uint32_t s_ex[FP ? PR_THREADS : 1];  //   list index << 16 | k << 1 | Fit lost by taking it
+  __shared__ uint32_t s_tx[FP ? MAX_K : 1];       // pods each listed node takes
   __shared__ uint32_t s_ic[4];           // [0] entries, [1] not applicable, [2] modified nodes
   __shared__ uint32_t s_wt[PR_NW];       // per-wave counts (prefix sums)
 
@@ -229,20 +384,20 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
     }
   };
   auto dh_insert = [&](uint32_t slot) -> uint32_t {
-    uint32_t h = dhash(slot);
+    uint32_t h = dhash<DH_BITS>(slot);
     for (;;) {
       const uint32_t old = atomicCAS(&s_dh[h], 0u, slot + 1);
       if (old == 0 || old == slot + 1) return h;
-      h = (h + 1) & (PDH - 1);
+      h = (h + 1) & (DH - 1);
     }
   };
   auto dh_owner = [&](uint32_t slot) -> uint32_t {
-    uint32_t h = dhash(slot);
+    uint32_t h = dhash<DH_BITS>(slot);
     for (;;) {
       const uint32_t v = s_dh[h];
       if (v == 0) return PNONE;
       if (v == slot + 1) return s_do[h];
-      h = (h + 1) & (PDH - 1);
+      h = (h + 1) & (DH - 1);
     }
   };
   // wave 0: lanes of the chunk grouped by slot (s_gh / s_gm cleared by the caller)
@@ -263,13 +418,25 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
   // live state = round-start state), copied piece by piece
   auto prow_from_cand = [&](uint32_t dst, uint32_t c, uint32_t j, uint32_t cand, uint32_t slot) {
     uint4 *d = (uint4 *)&s_prow[dst];
-    if (cand < (uint32_t)PNR) {
+    if (cand < (uint32_t)NR) {
 #pragma unroll
       for (int q = 0; q < ROW_PIECES; ++q) d[q] = s_crow[c][q][cand];
+      if constexpr (EXT) {
+        uint4 *dx = (uint4 *)&s_prowx[dst];
+#pragma unroll
+        for (int q = 0; q < EXT_PIECES; ++q) dx[q] = s_crowx[c][q][cand];
+      }
     } else {  // beyond the prefetched rows: one global round trip
-      const uint4 *g = (const uint4 *)(a.crow + (size_t)s_rep[j] * a.K + s_ce[c][cand]);
+      const size_t e = (size_t)s_rep[j] * a.K + s_ce[c][cand];
+      const uint4 *g = (const uint4 *)(a.crow + e);
 #pragma unroll
       for (int q = 0; q < ROW_PIECES; ++q) d[q] = g[q];
+      if constexpr (EXT) {
+        const uint4 *gx = (const uint4 *)(a.cext + e);
+        uint4 *dx = (uint4 *)&s_prowx[dst];
+#pragma unroll
+        for (int q = 0; q < EXT_PIECES; ++q) dx[q] = gx[q];
+      }
     }
     RNode &x = s_prow[dst];
     x.rc0 = x.row.rc;
@@ -277,6 +444,20 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
     x.np0 = x.row.np;
     x.slot = slot;
     x._pad[0] = x._pad[1] = 0;
+  };
+
+  // EXT: a normalising plugin's count of feasible nodes at its max has
+  // dropped to 0 (dn: at-max nodes lost, TaintToleration | NodeAffinity << 16):
+  // the max may have moved, the round stops before the pod (the serial
+  // kernel's rule)
+  auto norm_stop = [&](uint32_t j, uint32_t dn) -> bool {
+    if constexpr (!EXT) {
+      return false;
+    } else {
+      const uint32_t fl = s_fl[j];
+      const ShardRecHdr &h = s_hdr[j];
+      return ((fl & PF_TT) && h.tt_cnt - (dn & 0xFFFFu) == 0) || ((fl & PF_NA) && h.na_cnt - (dn >> 16) == 0);
+    }
   };
 
   // ---- stage the round
@@ -292,6 +473,10 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
     s_dl[i] = 0;
     s_dirty[i] = 0;
     s_lptr[i] = 0;
+    if constexpr (EXT) {
+      s_px[i] = make_px(p, a.norm_max[2 * i], a.norm_max[2 * i + 1]);
+      s_dn[i] = 0;
+    }
   }
   for (uint32_t i = tid; i < PMH; i += PR_THREADS) s_mh[i] = 0;
   if (tid < 8) s_ctl[tid] = 0;
@@ -329,7 +514,7 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
   // sends the round to the passes.  One step instead of a pass per one or
   // two pods.
   bool fast = false;
-  {
+  if constexpr (!EXT) {
     if (tid < 4) s_ic[tid] = 0;
     __syncthreads();
     const PQ q0 = s_q[0];
@@ -443,9 +628,8 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
 
   // Under RESOLVE_AUTO a round that runs past par_max_passes passes, or whose
   // pace after PAR_RATE_PASSES passes projects more than that many for its n
-  // pods (passes * n > par_max_passes * fixed), ends where it is (as if its
-  // next pod had stopped it: the rest is swept again as the next round) and
-  // hands the following rounds to the serial kernel.
+  // pods (passes * n > par_max_passes * fixed), is handed whole to the
+  // serial kernel, with the following rounds.
   const uint32_t pass_cap = a.rmode != nullptr ? a.par_max_passes : (uint32_t)MAX_P + 1;
   bool bailed = false;
   for (uint32_t guard = 0; guard <= MAX_P; ++guard) {
@@ -462,7 +646,7 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
     const uint32_t cn = min((uint32_t)PCH, n - f);
 
     // ====================== A: gather candidates (all waves, 4 chunk pods each)
-    for (uint32_t i = tid; i < PDH; i += PR_THREADS) {
+    for (uint32_t i = tid; i < DH; i += PR_THREADS) {
       s_dh[i] = 0;
       s_do[i] = PNONE;
     }
@@ -495,7 +679,11 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
         const PQ q = s_q[jt[t]];
         uint64_t best = 0;
         const uint32_t mn = s_ctl[5];
-        for (uint32_t m = lane; m < mn; m += WAVE) best = max64(best, pq_key(q, s_m[m].row, s_m[m].slot, a.w));
+        for (uint32_t m = lane; m < mn; m += WAVE) {
+          const RNode &x = s_m[m];
+          best = max64(best, pair_eval<EXT>(q, &s_px[EXT ? jt[t] : 0], a.clauses, x.row, &s_mx[EXT ? m : 0], x.slot,
+                                            x.rc0, x.rm0, x.np0, a.w).key);
+        }
         rkt[t] = wave_max_u64_dpp(best);
         if (lane == 0) {
           s_rk[jt[t]] = rkt[t];
@@ -552,12 +740,12 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
           const bool take = unt && k > rk;
           const uint64_t tm = __ballot(take);
           const uint32_t r = cnt + (uint32_t)__popcll(tm & lt_mask);
-          if (take && r < (uint32_t)PNC) {
+          if (take && r < (uint32_t)NC) {
             s_ck[c][r] = k;
             s_ce[c][r] = (uint16_t)e;
           }
           cnt += (uint32_t)__popcll(tm);
-          if (cnt >= (uint32_t)PNC) {
+          if (cnt >= (uint32_t)NC) {
             more = true;  // there may be more untaken entries above Rpre
             break;
           }
@@ -567,29 +755,39 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
           if (a.prof && lane == 0) atomicAdd((unsigned long long *)&s_clk[11], 1ull);
         }
         if (lane == 0) {
-          s_cnc[c] = min(cnt, (uint32_t)PNC);
+          s_cnc[c] = min(cnt, (uint32_t)NC);
           s_cmore[c] = more ? 1u : 0u;
           s_lptr[j] = firstu != PNONE ? firstu : min(base + WAVE, nk);
           const uint32_t feas = s_hdr[j].feasible - (uint32_t)s_dl[j];
-          s_cpst[c] = feas == 0 ? PD_UNSCHED : ((s_fl[j] & PF_PREF_ERR) && feas >= 2) ? PD_ERROR : PD_NODE;
+          s_cpst[c] = feas == 0                                     ? PD_UNSCHED
+                      : ((s_fl[j] & PF_PREF_ERR) && feas >= 2)     ? PD_ERROR
+                      : norm_stop(j, EXT ? s_dn[EXT ? j : 0] : 0u) ? PD_STOP
+                                                                   : PD_NODE;
         }
       });
       clk.tick(14);  // wave 0: the window scans
     }
-    // the first PNR candidates' rows of the wave's pods by LDS-DMA, lane r ->
+    // the first NR candidates' rows of the wave's pods by LDS-DMA, lane r ->
     // row r, issued after every scan (the compiler waits for all outstanding
     // loads before a scan's key use); landed before the barrier.  (Issued with
-    // the key windows a phase earlier instead, for the first PNR list entries,
+    // the key windows a phase earlier instead, for the first NR list entries,
     // the gather kept its time and the Rpre phase grew by the issue: 55k ->
     // 76k cycles per round on the proxy.)
     static_for<PPW>([&](auto T) {
       const uint32_t c = wid + PR_NW * (uint32_t)T;
       if (c >= cn) return;
-      if (lane < min(s_cnc[c], (uint32_t)PNR)) {
-        const uint4 *src = (const uint4 *)(a.crow + (size_t)s_rep[f + c] * a.K + s_ce[c][lane]);
+      if (lane < min(s_cnc[c], (uint32_t)NR)) {
+        const size_t e = (size_t)s_rep[f + c] * a.K + s_ce[c][lane];
+        const uint4 *src = (const uint4 *)(a.crow + e);
 #pragma unroll
         for (int q = 0; q < ROW_PIECES; ++q)
           __builtin_amdgcn_global_load_lds((gvoid_t *)(src + q), (lvoid_t *)&s_crow[c][q][0], 16, 0, 0);
+        if constexpr (EXT) {
+          const uint4 *srx = (const uint4 *)(a.cext + e);
+#pragma unroll
+          for (int q = 0; q < EXT_PIECES; ++q)
+            __builtin_amdgcn_global_load_lds((gvoid_t *)(srx + q), (lvoid_t *)&s_crowx[c][q][0], 16, 0, 0);
+        }
       }
     });
     clk.tick(3);                    // wave 0: the row DMAs issued
@@ -611,7 +809,7 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
       // slot once held stays held), so pods that see another owner move on.
       // The fixed point is the serial greedy: each pod takes its first
       // candidate no lower pod takes.
-      for (uint32_t it = 0; it <= (uint32_t)(PCH * PNC); ++it) {
+      for (uint32_t it = 0; it <= (uint32_t)(PCH * NC); ++it) {
         if (active && h == PNONE) h = dh_insert(key_slot(s_ck[c][ptr]));
         if (active) atomicMin(&s_do[h], c);
         const bool lost = active && s_do[h] != c;
@@ -665,8 +863,12 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
       }
       // the proposed node's state at the chunk start
       if (live && code == PD_NODE) {
-        if (src >= PSRC_M) s_prow[c] = s_m[src & 0xFFFFu];
-        else prow_from_cand(c, c, j, src, ps);
+        if (src >= PSRC_M) {
+          s_prow[c] = s_m[src & 0xFFFFu];
+          if constexpr (EXT) s_prowx[c] = s_mx[src & 0xFFFFu];
+        } else {
+          prow_from_cand(c, c, j, src, ps);
+        }
       }
       // lanes proposing the same slot: first of the group, next member
       s_gh[lane] = 0;
@@ -681,6 +883,7 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
       s_pnx[c] = above ? (uint32_t)__builtin_ctzll(above) : PNONE;
       s_ik[c] = 0;
       s_idl[c] = 0;
+      if constexpr (EXT) s_idn[c] = 0;
       s_cpst[c] = code;  // proposal code from here on
       s_cdm[c] = src;    // proposal source (C reads it before reusing the slot)
       if (lane == 0) s_ctl[2] = cut;
@@ -704,10 +907,11 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
         const int32_t np0 = r.np;
         for (uint32_t k = ic; k != PNONE && k < jc; k = s_pnx[k]) pq_add(r, s_q[f + k]);
         const PQ q = s_q[f + jc];
-        const uint64_t key = pq_key(q, r, s_prow[ic].slot, a.w);
-        const int32_t lost = (pq_fit(q, r, rc0, rm0, np0) ? 1 : 0) - (key != 0 ? 1 : 0);
-        if (key) atomicMax((unsigned long long *)&s_ik[jc], (unsigned long long)key);
-        if (lost) atomicAdd(&s_idl[jc], lost);
+        const PairEval v = pair_eval<EXT>(q, &s_px[EXT ? f + jc : 0], a.clauses, r, &s_prowx[EXT ? ic : 0],
+                                          s_prow[ic].slot, rc0, rm0, np0, a.w);
+        if (v.key) atomicMax((unsigned long long *)&s_ik[jc], (unsigned long long)v.key);
+        if (v.lost) atomicAdd(&s_idl[jc], v.lost);
+        if (EXT && v.at_lost) atomicAdd(&s_idn[EXT ? jc : 0], (v.at_lost & 1u) | (v.at_lost >> 1) << 16);
       }
     }
     __syncthreads();
@@ -732,6 +936,8 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
           code = PD_UNSCHED;
         } else if ((s_fl[j] & PF_PREF_ERR) && feas >= 2) {
           code = PD_ERROR;
+        } else if (norm_stop(j, EXT ? s_dn[EXT ? j : 0] + s_idn[EXT ? c : 0] : 0u)) {
+          code = PD_STOP;
         } else {
           // the first candidate no lower pod took: the proposal's, unless the
           // pod had no proposal (its status changed with the chunk's commits)
@@ -793,7 +999,13 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
           uint32_t from = PNONE;
           for (uint32_t i = 0; i < c && from == PNONE; ++i)
             if (s_ps[i] == ws) from = i;
-          s_prow[c] = *(from != PNONE ? &s_prow[from] : &s_m[mh_find(ws)]);
+          if constexpr (EXT) {
+            const uint32_t mi = from != PNONE ? PNONE : mh_find(ws);
+            s_prow[c] = from != PNONE ? s_prow[from] : s_m[mi];
+            s_prowx[c] = from != PNONE ? s_prowx[from] : s_mx[mi];
+          } else {
+            s_prow[c] = *(from != PNONE ? &s_prow[from] : &s_m[mh_find(ws)]);
+          }
         }
       }
       const bool fx = c < nfix;
@@ -825,6 +1037,12 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
           uint4 *dp = (uint4 *)&s_m[mi];
 #pragma unroll
           for (int q = 0; q < (int)(sizeof(RNode) / 16); ++q) dp[q] = sp[q];
+          if constexpr (EXT) {
+            const uint4 *sx = (const uint4 *)&s_prowx[c];
+            uint4 *dx = (uint4 *)&s_mx[mi];
+#pragma unroll
+            for (int q = 0; q < EXT_PIECES; ++q) dx[q] = sx[q];
+          }
         }
         CandRow &xr = s_m[mi].row;
         double rc = xr.rc, rm = xr.rm, zc = xr.zc100, zm = xr.zm100;
@@ -876,9 +1094,11 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
           const uint32_t d = t / npend, jj = nf + t % npend;
           const RNode &x = s_m[s_cdm[d]];
           const PQ q = s_q[jj];
-          const uint64_t key = pq_key(q, x.row, x.slot, a.w);
-          const int32_t lost = (pq_fit(q, x.row, s_cdp[d][0], s_cdp[d][1], s_cdn[d]) ? 1 : 0) - (key != 0 ? 1 : 0);
-          if (lost) atomicAdd(&s_dl[jj], lost);
+          const PairEval v = pair_eval<EXT>(q, &s_px[EXT ? jj : 0], a.clauses, x.row, &s_mx[EXT ? s_cdm[d] : 0],
+                                            x.slot, s_cdp[d][0], s_cdp[d][1], s_cdn[d], a.w);
+          const uint64_t key = v.key;
+          if (v.lost) atomicAdd(&s_dl[jj], v.lost);
+          if (EXT && v.at_lost) atomicAdd(&s_dn[EXT ? jj : 0], (v.at_lost & 1u) | (v.at_lost >> 1) << 16);
           if (s_cdr[d]) {
             // a re-taken node: its old key may be the one Rpre holds, which a
             // max cannot take back -- recompute Rpre when the pod is reached
@@ -896,6 +1116,25 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
     }
     __syncthreads();
     clk.tick(7);
+  }
+
+  if (bailed) {
+    // Hand the whole round to the serial kernel launched behind this one
+    // (RESOLVE_AUTO): nothing of it is written here, so the serial kernel
+    // resolves it from its first pod, in full, and the next round's
+    // speculative sweep stays valid.  It also takes the following b rounds,
+    // b doubling per consecutive hand-over (rmode[2]) up to PAR_MAX_STRETCH
+    // rounds (PAR_MAX_BACKOFF times serial_rounds when that is more).
+    if (tid == 0) {
+      const uint32_t b = max(a.rmode[2], a.serial_rounds);
+      a.rmode[0] = b + 1;  // this round, then b more (resolve_kernel counts them down)
+      a.rmode[2] = min(2 * b, max(PAR_MAX_STRETCH, PAR_MAX_BACKOFF * a.serial_rounds));
+      a.counters[CTR_PAR_BAILS] += 1;
+      a.counters[CTR_PAR_PASSES] += s_ctl[6];
+    }
+    clk.tick(8);
+    clk.flush();
+    return;  // no completion signal: the serial kernel gives it
   }
 
   // ---- results of the resolved pods, the modified nodes, the next round's start
@@ -926,7 +1165,7 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
     }
   }
   const uint32_t mn = s_ctl[5];
-  for (uint32_t i = tid; i < mn; i += PR_THREADS) a.carry_out[i] = rnode_carry(s_m[i], CandExt{}, false);
+  for (uint32_t i = tid; i < mn; i += PR_THREADS) a.carry_out[i] = rnode_carry(s_m[i], s_mx[EXT ? i : 0], EXT);
   if (tid == 0) {
     *a.carry_out_n = mn;
     mark_pod(a.marks, start, MARK_ROUND_START);
@@ -939,17 +1178,7 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
     if (fast) a.counters[CTR_PAR_ONESTEP] += 1;
     if (a.rmode != nullptr) {
       a.rmode[1] = a.seq;  // resolve_kernel, launched after this one, skips the round
-      if (bailed) {
-        // hand over; every consecutive bail doubles the serial stretch
-        // (rmode[2]), up to PAR_MAX_STRETCH rounds (PAR_MAX_BACKOFF times
-        // serial_rounds when that is more)
-        const uint32_t b = max(a.rmode[2], a.serial_rounds);
-        a.rmode[0] = b;
-        a.rmode[2] = min(2 * b, max(PAR_MAX_STRETCH, PAR_MAX_BACKOFF * a.serial_rounds));
-        a.counters[CTR_PAR_BAILS] += 1;
-      } else {
-        a.rmode[2] = 0;
-      }
+      a.rmode[2] = 0;      // a round resolved here ends a run of hand-overs
     }
   }
   __syncthreads();
@@ -958,8 +1187,9 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
   if (tid == 0) signal_done(a.flag_res, a.seq, a.stall_us);
 }
 
-hipError_t launch_resolve_par(const RoundArgs &a, hipStream_t st) {
-  resolve_par_kernel<<<1, PR_THREADS, 0, st>>>(a);
+hipError_t launch_resolve_par(const RoundArgs &a, bool ext, hipStream_t st) {
+  if (ext) resolve_par_kernel<true><<<1, PR_THREADS, 0, st>>>(a);
+  else resolve_par_kernel<false><<<1, PR_THREADS, 0, st>>>(a);
   return hipGetLastError();
 }
 

@@ -1,5 +1,6 @@
 """Shared comparison helpers for parity tests (oracle vs libksched)."""
 import ctypes as C
+import threading
 
 import numpy as np
 
@@ -58,3 +59,47 @@ class OracleTarget:
 
     def states(self, slots):
         return self.o.node_states(slots)
+
+
+def on_threads(fns):
+    """Run the callables on threads and return their results (libksched's and
+    the oracle's ctypes calls release the GIL, so per-rank setup runs side by
+    side); the first error is raised."""
+    out, errs = [None] * len(fns), []
+
+    def go(i):
+        try:
+            out[i] = fns[i]()
+        except Exception as e:  # noqa: BLE001 -- re-raised below
+            errs.append(e)
+
+    th = [threading.Thread(target=go, args=(i,)) for i in range(len(fns))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    if errs:
+        raise errs[0]
+    return out
+
+
+class Background:
+    """One callable on a thread, its result fetched later (the oracle's 1M-node
+    setup overlaps the GPU work)."""
+
+    def __init__(self, fn):
+        self._out, self._err = [], []
+
+        def run():
+            try:
+                self._out.append(fn())
+            except Exception as e:  # noqa: BLE001 -- re-raised by get()
+                self._err.append(e)
+        self._t = threading.Thread(target=run)
+        self._t.start()
+
+    def get(self):
+        self._t.join()
+        if self._err:
+            raise self._err[0]
+        return self._out[0]

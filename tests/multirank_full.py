@@ -36,7 +36,7 @@ import numpy as np  # noqa: E402
 import pyoracle  # noqa: E402
 from helpers import res_array, states_np  # noqa: E402
 from ksched import Scheduler, synth  # noqa: E402
-from helpers import OracleTarget  # noqa: E402
+from helpers import Background, OracleTarget, on_threads  # noqa: E402
 from ksched.stream import BurstStream, GpuTarget  # noqa: E402
 from test_gpu_fullsize import MIN_CHECKED, pick_windows, replay_check  # noqa: E402
 
@@ -80,7 +80,8 @@ def run_ranks(ranks, pods, m):
     return out[0], marks[0]
 
 
-def one_rank(nodes, slots, pf, stream, bursts, events, npl):
+def one_rank_setup(nodes, slots, pf, stream, npl):
+    """A one-rank context holding the same cluster (built while the ranks run)."""
     s = Scheduler(N, nodes_per_lane=npl)
     t = GpuTarget(s)
     if stream is not None:
@@ -89,6 +90,11 @@ def one_rank(nodes, slots, pf, stream, bursts, events, npl):
         s.upsert_nodes_raw(nodes.nodes, slots, N)
         if pf is not None:
             assert s.lib.ks_pods_add(s.ctx, pf.pods, pf.slot_ptr, pf.n_pods) == 0
+    return s, t
+
+
+def one_rank_run(s, t, bursts, events):
+    """The ranks' stream on the one-rank context: results per burst, node table."""
     res = []
     for i, (pods, m) in enumerate(bursts):
         b = s.prepare(pods.pods, m)
@@ -139,15 +145,31 @@ def main(cfg):
         pf = synth.prefill(k, N, 1, 3, 0.5)
         pods = synth.pods(k, BATCH, 2 if kind == "c3" else 7)
     npl = cfg.get("npl", 2)  # bench.py --gpus N > 1 lays the table out with 2 nodes per lane
+
+    def build_oracle():  # the same cluster in the oracle, built while the GPU runs
+        o = pyoracle.Oracle(N, threads=ORACLE_THREADS)
+        ot = OracleTarget(o)
+        if stream is not None:
+            BurstStream(synth.HETERO, N, 2, BATCH).setup([ot])
+        else:
+            o.upsert(nodes.nodes, slots, N)
+            o.add_pods(pf.pods, pf.slot_ptr, pf.n_pods)
+        return o, ot
+    oracle_job = Background(build_oracle)
+    one_job = Background(lambda: one_rank_setup(nodes, slots, pf, BurstStream(synth.HETERO, N, 2, BATCH)
+                                                if stream is not None else None, npl))
     ranks = [Scheduler(N, world_size=world, rank=r, nodes_per_lane=npl) for r in range(world)]
     Scheduler.comm_init_local(ranks)
     targets = [GpuTarget(s) for s in ranks]
-    if stream is not None:
-        stream.setup(targets)
-    else:
-        for s in ranks:
+
+    def setup_rank(r):
+        if stream is not None:
+            stream.setup([targets[r]])
+        else:
+            s = ranks[r]
             s.upsert_nodes_raw(nodes.nodes, slots, N)
             assert s.lib.ks_pods_add(s.ctx, pf.pods, pf.slot_ptr, pf.n_pods) == 0
+    on_threads([lambda r=r: setup_rank(r) for r in range(world)])
     setup_s = time.time() - t0
     # the stream: one batch (c3 / c4), or burst 0, its event log, burst 1 (c5)
     got, marks, events, bursts = [], [], [], []
@@ -166,8 +188,7 @@ def main(cfg):
             ops = stream.marshal(stream.make_events())
             ev = BurstStream.event_log(ops)
             events.append(ev)
-            for t in targets:
-                t.apply_events(ev[0], ev[1])
+            on_threads([lambda t=t: t.apply_events(ev[0], ev[1]) for t in targets])
     tables = [states_np(s.lib.ks_node_states, s.ctx, N) for s in ranks]
     for r in range(1, world):
         if not np.array_equal(tables[r], tables[0]):
@@ -178,21 +199,14 @@ def main(cfg):
         s.close()
     run_s = time.time() - t0 - setup_s
     # one rank, same stream
-    one, one_table = one_rank(nodes, slots, pf, BurstStream(synth.HETERO, N, 2, BATCH) if stream is not None else None,
-                              bursts, events, npl)
+    one, one_table = one_rank_run(*one_job.get(), bursts, events)
     for b in range(nb):
         if not np.array_equal(one[b], res_array(got[b], bursts[b][1])):
             raise Fail(f"burst {b}: the one-rank context's results differ from the ranks'")
     if not np.array_equal(one_table, tables[0]):
         raise Fail("the one-rank context's node table differs from the ranks'")
     # the oracle replays rank 0's decisions, checking windows
-    o = pyoracle.Oracle(N, threads=ORACLE_THREADS)
-    ot = OracleTarget(o)
-    if stream is not None:
-        BurstStream(synth.HETERO, N, 2, BATCH).setup([ot])
-    else:
-        o.upsert(nodes.nodes, slots, N)
-        o.add_pods(pf.pods, pf.slot_ptr, pf.n_pods)
+    o, ot = oracle_job.get()
     checked, kinds = 0, set()
     for b in range(nb):
         mb = bursts[b][1]

@@ -26,7 +26,7 @@ import numpy as np
 import pytest
 
 import pyoracle
-from helpers import assert_results_equal, res_array, states_np
+from helpers import Background, assert_results_equal, res_array, states_np
 from ksched import Scheduler, _abi, synth
 from ksched.stream import _gather
 
@@ -116,10 +116,20 @@ def pick_windows(marks, m, wlen=WLEN, fixed=WINDOWS, per_kind=3, round_every=16,
     return out
 
 
+def build_oracle(nodes, slots, pf):
+    """The 1M-node cluster (and its prefill pods) in a fresh oracle."""
+    o = pyoracle.Oracle(N, threads=ORACLE_THREADS)
+    o.upsert(nodes.nodes, slots, N)
+    if pf is not None:
+        o.add_pods(pf.pods, pf.slot_ptr, pf.n_pods)
+    return o
+
+
 def run_fullsize(kind, pods, prefill, *, opts=None, **cfg):
     nodes = synth.nodes(kind, N, 1)
     slots = synth.slot_array(N)
     pf = synth.prefill(kind, N, 1, 3, 0.5) if prefill else None
+    oracle_job = Background(lambda: build_oracle(nodes, slots, pf))  # overlaps the GPU run
     s = Scheduler(N, options=opts, **cfg)
     s.upsert_nodes_raw(nodes.nodes, slots, N)
     if pf is not None:
@@ -131,10 +141,7 @@ def run_fullsize(kind, pods, prefill, *, opts=None, **cfg):
     s.free(b)
     dbg = (C.c_uint64 * 16)()
     assert s.lib.ks_debug_counters(s.ctx, dbg) == 0
-    o = pyoracle.Oracle(N, threads=ORACLE_THREADS)
-    o.upsert(nodes.nodes, slots, N)
-    if pf is not None:
-        o.add_pods(pf.pods, pf.slot_ptr, pf.n_pods)
+    o = oracle_job.get()
     wins = pick_windows(marks, BATCH)
     checked = replay_check(o, pods, got, BATCH, windows=[w for w, _ in wins])
     assert checked >= MIN_CHECKED, f"only {checked} pods checked by the oracle"
@@ -157,80 +164,123 @@ def run_fullsize(kind, pods, prefill, *, opts=None, **cfg):
 C3_STEPS, C3_STEP = 20, 50_000  # BASELINE configs[2]: 1M pods; bench.py's headline step size
 
 
-def test_c3_bench_pipeline_1m_replay():
-    # The headline exactly as bench.py runs it (run_batches / end_to_end): the
-    # 1M-node C3 cluster (nodes seed 1, prefill seed 3 to <50 % cpu), the pod
-    # stream of seed 7, 20 steps of 50,000 pods through ks_batch_prepare /
-    # ks_batch_submit / ks_batch_wait / ks_batch_results with bench.E2E_DEPTH
-    # batches in flight (batch k+1 compiled while k runs) = configs[2]'s 1M
-    # pods.  The oracle replays all 1M decisions and schedules >= 512 of the
-    # pods itself in windows over the whole stream: the first pod of steps
-    # (where a batch hands the pipelined rounds to the next), round starts,
-    # FIX / after-waste marks and seeded random windows; then the node tables
-    # must be equal.
+def bench_pipeline_replay(kind, n_nodes, steps, step, *, prefill=0.5, min_checked=MIN_CHECKED, opts=None):
+    """A bench line exactly as bench.py runs it (run_batches / end_to_end):
+    the cluster (nodes seed 1, prefill seed 3), the pod stream of seed 7,
+    `steps` steps of `step` pods through ks_batch_prepare / ks_batch_submit /
+    ks_batch_wait / ks_batch_results with bench.E2E_DEPTH batches in flight
+    (batch k+1 compiled while k runs).  The oracle replays every decision and
+    schedules >= min_checked of the pods itself in windows over the whole
+    stream: the first pod of steps (where a batch hands the pipelined rounds
+    to the next), round starts, FIX / after-waste marks and seeded random
+    windows; then the node tables must be equal.  Returns the results and
+    the debug counters."""
     import sys
     from pathlib import Path
     sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
     import bench
 
-    m = C3_STEPS * C3_STEP
-    nodes = synth.nodes(synth.HETERO, N, 1)
-    slots = synth.slot_array(N)
-    pf = synth.prefill(synth.HETERO, N, 1, 3, 0.5)
-    pods = synth.pods(synth.HETERO, m, 7)
-    s = Scheduler(N)
-    s.upsert_nodes_raw(nodes.nodes, slots, N)
-    assert s.lib.ks_pods_add(s.ctx, pf.pods, pf.slot_ptr, pf.n_pods) == 0
+    m = steps * step
+    nodes = synth.nodes(kind, n_nodes, 1)
+    slots = synth.slot_array(n_nodes)
+    pf = synth.prefill(kind, n_nodes, 1, 3, prefill) if prefill > 0 else None
+    pods = synth.pods(kind, m, 7)
+
+    def build():
+        o = pyoracle.Oracle(n_nodes, threads=ORACLE_THREADS)
+        o.upsert(nodes.nodes, slots, n_nodes)
+        if pf is not None:
+            o.add_pods(pf.pods, pf.slot_ptr, pf.n_pods)
+        return o
+    oracle_job = Background(build)  # overlaps the GPU run
+    s = Scheduler(n_nodes, options=opts)
+    s.upsert_nodes_raw(nodes.nodes, slots, n_nodes)
+    if pf is not None:
+        assert s.lib.ks_pods_add(s.ctx, pf.pods, pf.slot_ptr, pf.n_pods) == 0
     got = (_abi.KsResult * m)()
     marks = bytearray(m)
     inflight, nxt = [], 0
-    for k in range(C3_STEPS):
-        while nxt < C3_STEPS and len(inflight) < bench.E2E_DEPTH:
-            b = s.prepare(pods.pods_at(nxt * C3_STEP), C3_STEP)
+    for k in range(steps):
+        while nxt < steps and len(inflight) < bench.E2E_DEPTH:
+            b = s.prepare(pods.pods_at(nxt * step), step)
             assert s.lib.ks_batch_submit(s.ctx, b) == 0, s.lib.ks_last_error(s.ctx)
             inflight.append(b)
             nxt += 1
         cur = inflight.pop(0)
         assert s.lib.ks_batch_wait(s.ctx, cur) == 0, s.lib.ks_last_error(s.ctx)
-        C.memmove(C.addressof(got) + k * C3_STEP * C.sizeof(_abi.KsResult), s.results(cur, C3_STEP),
-                  C3_STEP * C.sizeof(_abi.KsResult))
-        marks[k * C3_STEP:(k + 1) * C3_STEP] = s.marks(cur, C3_STEP)
+        C.memmove(C.addressof(got) + k * step * C.sizeof(_abi.KsResult), s.results(cur, step),
+                  step * C.sizeof(_abi.KsResult))
+        marks[k * step:(k + 1) * step] = s.marks(cur, step)
         s.free(cur)
     dbg = (C.c_uint64 * 16)()
     assert s.lib.ks_debug_counters(s.ctx, dbg) == 0
-    assert dbg[0] >= m // 256
-    o = pyoracle.Oracle(N, threads=ORACLE_THREADS)
-    o.upsert(nodes.nodes, slots, N)
-    o.add_pods(pf.pods, pf.slot_ptr, pf.n_pods)
-    steps = (0, 1, 2, 7, 13, C3_STEPS - 1)
-    fixed = tuple(k * C3_STEP for k in steps) + (m - WLEN,)
-    wins = pick_windows(bytes(marks), m, fixed=fixed, per_kind=2, round_every=1000, min_pods=MIN_CHECKED)
+    o = oracle_job.get()
+    ks = sorted({0, 1, 2, steps // 2, steps - 1} & set(range(steps)))
+    fixed = tuple(k * step for k in ks) + (m - WLEN,)
+    wins = pick_windows(bytes(marks), m, fixed=fixed, per_kind=2, round_every=1000, min_pods=min_checked)
     checked = replay_check(o, pods, got, m, windows=[w for w, _ in wins])
-    assert checked >= MIN_CHECKED, f"only {checked} pods checked by the oracle"
+    assert checked >= min_checked, f"only {checked} pods checked by the oracle"
     assert {w for w, _ in wins} >= set(fixed)
-    sg = states_np(s.lib.ks_node_states, s.ctx, N)
-    sw = states_np(o.L.oracle_node_states, o.o, N)
-    assert np.array_equal(sg, sw), "node tables differ after replaying all 1M decisions"
-    assert (res_array(got, m)["status"] == 0).all()
+    mk = np.frombuffer(bytes(marks), dtype=np.uint8)
+    covered = np.zeros(m, dtype=bool)
+    for w, _ in wins:
+        covered[w:w + WLEN] = True
+    for bit in (MARK_FIX, MARK_AFTER_WASTE):  # a FIX re-sweep / a wasted round that happened is also checked
+        assert not (mk & bit).any() or (covered & ((mk & bit) != 0)).any(), f"no window on a pod marked {bit}"
+    sg = states_np(s.lib.ks_node_states, s.ctx, n_nodes)
+    sw = states_np(o.L.oracle_node_states, o.o, n_nodes)
+    assert np.array_equal(sg, sw), f"node tables differ after replaying all {m} decisions"
     s.close()
     o.close()
+    return res_array(got, m), list(dbg)
+
+
+def test_c3_bench_pipeline_1m_replay():
+    # configs[2] as the headline runs it: 1M heterogeneous nodes, 20 steps of
+    # 50,000 pods = 1M pods
+    r, dbg = bench_pipeline_replay(synth.HETERO, N, C3_STEPS, C3_STEP)
+    assert dbg[0] >= C3_STEPS * C3_STEP // 256
+    assert (r["status"] == 0).all()
+
+
+def test_c4_bench_pipeline_1m_replay():
+    # configs[3] as `bench.py --kind labeled` runs it: 1M labeled nodes
+    # (zones, instance types, pools, features, taints), labeled pods with
+    # nodeSelectors, required / preferred node affinity and tolerations,
+    # 10 steps of 50,000 pods = 500k pods with the default node-tuple
+    # normaliser guesses; FIX re-sweeps and the parallel commit of label /
+    # taint rounds at bench length
+    r, dbg = bench_pipeline_replay(synth.LABELED, N, 10, 50_000)
+    assert dbg[4] > 0, "no pod was re-swept with a measured normaliser (FIX path not exercised)"
+    assert dbg[13] > 0, "the parallel commit resolved no label / taint round"
+    assert (r["status"] == 0).mean() > 0.9
+
+
+def test_c2_bench_pipeline_100k_replay():
+    # configs[1] as the c2 line runs it (`bench.py --nodes 100000 --batch
+    # 20000`): 100k heterogeneous nodes, 5 steps of 20,000 pods = 100k pods,
+    # 2048 of them scheduled by the oracle itself
+    r, dbg = bench_pipeline_replay(synth.HETERO, 100_000, 5, 20_000, min_checked=2048)
+    assert (r["status"] == 0).mean() > 0.99
 
 
 def test_c4_labeled_1m_replay_early_fix():
-    # the C4 bench path: EXT sweep (2 nodes per lane), early FIX, compacted FIX
-    # list.  (The FIX sweep behind the merge, early_fix = 0, runs at 1M nodes in
-    # test_gpu_multirank.py::test_fullsize_eight_ranks[c4] and on one rank in
-    # test_gpu_semantics.py / test_gpu_dedup.py; its one-rank 1M replay was
-    # dropped in round 5 to keep the suite under the driver's 900 s.)
+    # the C4 sweep path with the FIX sweep right behind it on the main stream
+    # (early FIX, compacted FIX list) and simple normaliser guesses, so that
+    # the FIX path runs often (the default node-tuple guesses run at bench
+    # length in test_c4_bench_pipeline_1m_replay)
     r, dbg = run_fullsize(synth.LABELED, synth.pods(synth.LABELED, BATCH, 2), prefill=True,
-                          opts={"tuple_guess": 0})  # simple guesses: the FIX path runs often
+                          opts={"tuple_guess": 0})
     assert dbg[4] > 0, "no pod was re-swept with a measured normaliser (FIX path not exercised)"
     assert (r["status"] == 1).any() and (r["status"] == 0).mean() > 0.9
 
 
-def test_c4_labeled_1m_replay_tuple_guess():
-    # the default (node-tuple normaliser guesses): the bench configuration
-    r, dbg = run_fullsize(synth.LABELED, synth.pods(synth.LABELED, BATCH, 7), prefill=True)
+def test_c4_labeled_1m_replay_fix_behind_merge():
+    # early_fix = 0: the FIX sweep runs behind the merge on the side stream
+    # (the multi-rank order), here on one rank
+    r, dbg = run_fullsize(synth.LABELED, synth.pods(synth.LABELED, BATCH, 2), prefill=True,
+                          opts={"tuple_guess": 0, "early_fix": 0})
+    assert dbg[4] > 0, "no pod was re-swept with a measured normaliser (FIX path not exercised)"
     assert (r["status"] == 0).mean() > 0.9
 
 
@@ -253,16 +303,11 @@ def test_kwok_1m_c1_pods_k512_replay():
     # survive the previous round's commits to identical nodes
     r, dbg = run_fullsize(synth.KWOK, synth.pods(synth.KWOK, BATCH, 2), prefill=False, topk=512)
     assert (r["status"] == 0).all()
-    # Under resolve AUTO every parallel-commit bail (dbg[14]) cuts its round,
-    # so the next round's speculative sweep is wasted by design; the serial
-    # stretch after a bail starts at 4 rounds and doubles up to 256, so at most
-    # 7 consecutive bails happen before AUTO settles (4, 8, ..., 256).  Those
-    # are bounded on their own; every other wasted round means the 512-entry
-    # lists did not survive the previous round's commits.
-    bails = int(dbg[14])
-    assert bails <= 8, f"parallel-commit bails {bails} of {dbg[0]} rounds"
-    other = max(int(dbg[3]) - bails, 0)
-    assert other * 20 < dbg[0], f"wasted speculative rounds {dbg[3]} ({bails} AUTO cuts) of {dbg[0]}"
+    # Under resolve AUTO a parallel-commit bail (dbg[14]) hands its whole
+    # round to the serial kernel, so a bail wastes no speculative sweep: a
+    # wasted round means the 512-entry lists did not survive the previous
+    # round's commits (round 2's bound: at most 1 in 20)
+    assert dbg[3] * 20 < dbg[0], f"wasted speculative rounds {dbg[3]} ({dbg[14]} AUTO hand-overs) of {dbg[0]}"
 
 
 class MixedStream:
@@ -298,6 +343,7 @@ def test_spread_1m_replay():
     nodes = synth.nodes(synth.ZONED, N, 1)
     slots = synth.slot_array(N)
     pf = synth.prefill(synth.ZONED, N, 1, 3, 0.5)
+    oracle_job = Background(lambda: build_oracle(nodes, slots, pf))  # overlaps the GPU run
     spread, plain = synth.spread_pods(n_pods // 2, 64, 5), synth.pods(synth.HETERO, n_pods // 2, 6)
     mixed = MixedStream(plain, spread, 128)
     s = Scheduler(N)
@@ -310,9 +356,7 @@ def test_spread_1m_replay():
     st = _abi.KsStats()
     assert s.lib.ks_get_stats(s.ctx, C.byref(st)) == 0
     assert st.spread_pods == n_pods // 2
-    o = pyoracle.Oracle(N, threads=ORACLE_THREADS)
-    o.upsert(nodes.nodes, slots, N)
-    o.add_pods(pf.pods, pf.slot_ptr, pf.n_pods)
+    o = oracle_job.get()
     # windows straddle a plain -> spread boundary, sit inside a spread run, and end the batch
     replay_check(o, mixed, got, n_pods, windows=(124, 1400, n_pods - 6), wlen=6)
     sg = states_np(s.lib.ks_node_states, s.ctx, N)
@@ -333,6 +377,7 @@ def test_deploy_1m_replay():
     nodes = synth.nodes(synth.ZONED, N, 1)
     slots = synth.slot_array(N)
     pf = synth.prefill(synth.ZONED, N, 1, 3, 0.5)
+    oracle_job = Background(lambda: build_oracle(nodes, slots, pf))  # overlaps the GPU run
     dep = synth.deploy_pods(n_pods, 256, 5)
     s = Scheduler(N)
     s.upsert_nodes_raw(nodes.nodes, slots, N)
@@ -344,9 +389,7 @@ def test_deploy_1m_replay():
     st = _abi.KsStats()
     assert s.lib.ks_get_stats(s.ctx, C.byref(st)) == 0
     assert st.replica_pods == n_pods and st.replica_runs >= n_pods // 256
-    o = pyoracle.Oracle(N, threads=ORACLE_THREADS)
-    o.upsert(nodes.nodes, slots, N)
-    o.add_pods(pf.pods, pf.slot_ptr, pf.n_pods)
+    o = oracle_job.get()
     replay_check(o, dep, got, n_pods, windows=(0, 130, 512, 1201, n_pods - 4), wlen=4)
     sg = states_np(s.lib.ks_node_states, s.ctx, N)
     sw = states_np(o.L.oracle_node_states, o.o, N)
@@ -365,6 +408,7 @@ def test_affinity_1m_replay():
     nodes = synth.nodes(synth.ZONED, N, 1)
     slots = synth.slot_array(N)
     pf = synth.prefill(synth.ZONED, N, 1, 3, 0.5)
+    oracle_job = Background(lambda: build_oracle(nodes, slots, pf))  # overlaps the GPU run
     aff, plain = synth.affinity_pods(n_pods // 2, 16, 7), synth.pods(synth.HETERO, n_pods // 2, 8)
     mixed = MixedStream(plain, aff, 128)
     s = Scheduler(N)
@@ -377,9 +421,7 @@ def test_affinity_1m_replay():
     st = _abi.KsStats()
     assert s.lib.ks_get_stats(s.ctx, C.byref(st)) == 0
     assert st.spread_pods == n_pods // 2
-    o = pyoracle.Oracle(N, threads=ORACLE_THREADS)
-    o.upsert(nodes.nodes, slots, N)
-    o.add_pods(pf.pods, pf.slot_ptr, pf.n_pods)
+    o = oracle_job.get()
     replay_check(o, mixed, got, n_pods, windows=(124, 900, n_pods - 6), wlen=6)
     sg = states_np(s.lib.ks_node_states, s.ctx, N)
     sw = states_np(o.L.oracle_node_states, o.o, N)

@@ -81,7 +81,7 @@ def test_mid_size(kind):
     ns = synth.nodes(kind, n, 71)
     ps = synth.pods(kind, m, 72)
     slots = synth.slot_array(n)
-    o = pyoracle.Oracle(n)
+    o = pyoracle.Oracle(n, threads=16)  # the GPU box's CPU share
     o.upsert(ns.nodes, slots, n)
     s = Scheduler(n)
     s.upsert_nodes_raw(ns.nodes, slots, n)

@@ -1,5 +1,6 @@
-"""The in-order commit of resource-only rounds: the
-parallel proposal / verify kernel (ksched_resolve.hip), the
+"""The in-order commit of the round kernels, for
+resource-only and for label / taint rounds: the parallel proposal / verify
+kernel (ksched_resolve.hip), the
 serial kernel, and the automatic hand-over between them, each bit-exact
 against the CPU oracle's one-pod-at-a-time scheduling and against each other.
 
@@ -187,6 +188,68 @@ def test_parallel_vs_serial_fuzz(shards):
         check_modes(want, wst, out, f"fuzz seed {seed} shards {shards}")
 
 
+@pytest.mark.parametrize("K,P,shards,splits", [(256, 256, 1, 2), (16, 256, 1, 1), (64, 100, 3, 3), (512, 256, 1, 1)])
+def test_labeled_streams_every_mode(K, P, shards, splits):
+    # label / taint rounds (EXT: NodeAffinity required + preferred terms,
+    # nodeSelectors, hard and PreferNoSchedule taints with their tolerations,
+    # TaintToleration / NodeAffinity normalisation, FIX re-sweeps) through the
+    # parallel commit, the serial kernel and the hand-over between them
+    n, m = 4000, 3000
+    ns = synth.nodes(synth.LABELED, n, 21)
+    ps = synth.pods(synth.LABELED, m, 22)
+    pf = synth.prefill(synth.LABELED, n, 21, 23, 0.5)
+    want, wst, out = run_modes(ns.nodes, n, ps.pods, m, pre=(pf.pods, pf.slot_ptr, pf.n_pods), splits=splits,
+                               modes=("auto", "serial", "parallel", "auto_cap"), pods_per_round=P, topk=K,
+                               virtual_shards=shards)
+    check_modes(want, wst, out, f"labeled K={K} P={P} shards={shards}")
+    par = out["parallel"][2]
+    assert par[0] > 0 and par[13] == par[0], f"RESOLVE_PARALLEL left label / taint rounds to the serial kernel: {par}"
+    assert out["auto"][2][13] > 0, f"AUTO resolved no label / taint round in parallel: {out['auto'][2]}"
+    assert (want["status"] == 0).any() and (want["status"] == 1).any()
+
+
+def test_labeled_normaliser_edges_every_mode():
+    # every pod normalises TaintToleration (PreferNoSchedule taints of 0-3
+    # keys on every node) and most NodeAffinity (preferred terms), the nodes
+    # at the taint max hold one pod each, and a few pods carry a nodeName or a
+    # metadata.name PreFilterResult: normaliser drops stop rounds inside a
+    # chunk of the parallel commit
+    from ksched.objects import (NodeSelectorRequirement as Req, NodeSelectorTerm as Term,
+                                PreferredSchedulingTerm as Pref, Taint)
+    r = random.Random(31)
+    keys = ["a", "b", "c"]
+    nodes = []
+    for i in range(700):
+        tk = r.sample(keys, r.choice([0, 1, 1, 2, 3]))
+        nodes.append(node(f"n{i}", cpu=r.choice([4, 8, 16]) * 1000, mem=r.choice([8, 16, 32]) * Gi,
+                          pods=1 if len(tk) == 3 else r.choice([2, 3, 9]),
+                          labels={"zone": f"z{i % 5}", "tier": r.choice(["a", "b"])},
+                          taints=[Taint(k, "x", "PreferNoSchedule") for k in tk]))
+    pods = []
+    for j in range(1600):
+        kw = {}
+        if r.random() < 0.6:
+            kw["preferred"] = [Pref(r.choice([1, 5, 20]), Term([Req("zone", "In", [f"z{r.randrange(5)}"])])),
+                               Pref(r.choice([1, 3]), Term([Req("tier", "In", [r.choice(["a", "b"])])]))]
+        if r.random() < 0.2:
+            kw["node_selector"] = {"tier": r.choice(["a", "b"])}
+        u = r.random()
+        if u < 0.01:
+            kw["node_name"] = f"n{r.randrange(700)}"
+        elif u < 0.02:
+            names = [f"n{r.randrange(700)}" for _ in range(3)]
+            kw["required_terms"] = [Term(match_fields=[Req("metadata.name", "In", names)])]
+        pods.append(pod(f"p{j}", cpu=r.choice([100, 500, 1000]), mem=r.choice([1, 2]) * Gi, **kw))
+    a = Arena()
+    na, n = nodes_array(nodes, a)
+    pa, m = pods_array(pods, a)
+    want, wst, out = run_modes(na, n, pa, m, splits=2, modes=("auto", "serial", "parallel"), pods_per_round=256,
+                               topk=64)
+    check_modes(want, wst, out, "labeled normaliser edges")
+    par = out["parallel"][2]
+    assert par[0] > 0 and par[13] == par[0], f"parallel commit counters {par}"
+
+
 @pytest.mark.parametrize("mode", ["auto", "serial", "parallel"])
 def test_normaliser_max_drops_mid_round(mode):
     # TaintToleration normalises by the max raw (untolerated PreferNoSchedule
@@ -194,8 +257,8 @@ def test_normaliser_max_drops_mid_round(mode):
     # hold one pod each, and the round's first pods are steered onto them by
     # a nodeSelector: once they are full the max over feasible nodes drops
     # 2 -> 1 and every later pod's TaintToleration score changes on every
-    # node.  The round must stop there and the rest be swept again (label /
-    # taint rounds take the serial kernel in every mode).
+    # node.  The round must stop there and the rest be swept again, in the
+    # serial and in the parallel commit.
     from ksched.objects import Taint
     p = lambda k: Taint(k, "true", "PreferNoSchedule")  # noqa: E731
     nodes = ([node(f"max{i}", pods=1, labels={"special": "yes"}, taints=[p("s"), p("t")]) for i in range(2)] +
