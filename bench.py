@@ -97,7 +97,8 @@ E2E_DEPTH = 2  # batches submitted ahead in the headline loop (compile of k+1 an
 REF_SCHEDULE_ONE_US = 560.0  # README.adoc:786 (per pod per shard, ~195 nodes evaluated)
 KERNEL_SOURCES = ["k8s-1m_amd/csrc/ksched_kernels.hip", "k8s-1m_amd/csrc/ksched_eval.hpp", "k8s-1m_amd/csrc/ksched_dev.hpp",
                   "k8s-1m_amd/csrc/ksched_kernels.hpp", "k8s-1m_amd/csrc/ksched_util.hpp",
-                  "k8s-1m_amd/csrc/ksched_instr.hpp", "k8s-1m_amd/csrc/ksched_resolve.hip", "k8s-1m_amd/Makefile"]
+                  "k8s-1m_amd/csrc/ksched_instr.hpp", "k8s-1m_amd/csrc/ksched_resolve.hip",
+                  "k8s-1m_amd/csrc/ksched_resolve_serial.hpp", "k8s-1m_amd/Makefile"]
 
 
 def parse():
@@ -311,7 +312,7 @@ def run_batches(args, kind, sched, world, rank, t_setup):
         pr = (C.c_uint64 * 16)()
         sched.lib.ks_debug_resolve_profile(sched.ctx, pr)
         rounds = max(1, int(pr[9]))
-        # phase clock slots (ksched_resolve.hip resolve_par_kernel); wave 0's
+        # phase clock slots (ksched_resolve.hip resolve_parallel); wave 0's
         # gather is slots 12 (prefetched windows), 13 (probes), 14 (scans), 3 (DMA issue), 5 (DMA wait)
         names = {0: "stage", 12: "gather_w0_prefetch_wait", 13: "gather_w0_probes", 14: "gather_w0_scans",
                  3: "gather_w0_dma_issue", 5: "gather_w0_dma_wait", 1: "gather_barrier", 2: "proposals",
@@ -327,9 +328,15 @@ def run_batches(args, kind, sched, world, rank, t_setup):
     # one-pod-path filter passes over every node count too: one per pod of the
     # per-pod chain and one per replica run; st covers
     # the timed steps (reset before them)
-    swept = e2e.pop("pods_swept") + int(st.spread_pods - st.replica_pods) + int(st.replica_runs)
+    # (since round 5 pods_swept, node_evals_per_s and pods_swept_fraction
+    # include these one-pod-path passes; round-4 and earlier records counted
+    # the round sweeps only: compare sweep_pods_swept across rounds)
+    one_pod_passes = int(st.spread_pods - st.replica_pods) + int(st.replica_runs)
+    round_swept = e2e.pop("pods_swept")
     line = report(args, sched, st, dbg, world, e2e.pop("pods_timed"), e2e.pop("elapsed"), e2e.pop("scheduled"),
-                  setup_s, cpu, pods_swept=swept)
+                  setup_s, cpu, pods_swept=round_swept + one_pod_passes)
+    line["extra"]["sweep_pods_swept"] = round_swept
+    line["extra"]["one_pod_path_node_passes"] = one_pod_passes
     line["extra"]["host_compile_ms_per_step"] = e2e["host_compile_ms_per_step"]
     line["end_to_end"] = e2e
     if res:

@@ -630,6 +630,10 @@ ks_status ks_set_sync_timeout(ks_ctx *ctx, uint32_t ms);
  * stream done, 2 round resolved, 3 FIX sweep done) by `usec` microseconds of
  * bounded device-side waiting, then signals as usual. */
 ks_status ks_debug_stall(ks_ctx *ctx, uint32_t flag, uint32_t usec);
+/* Batch runs the context has started (the worker took their selector-class
+ * masks and table view); returns at once, without waiting for submitted
+ * batches -- tests order a ks_batch_prepare after a submitted run's start. */
+ks_status ks_debug_runs_started(ks_ctx *ctx, uint64_t *out);
 /* 1 = time sweep / resolve launches with HIP events (every KS_TIMING_EVERY-th
  * round, default 8; sweep_evals counts the timed launches' share), 0 = off. */
 ks_status ks_set_timing(ks_ctx *ctx, int32_t enabled);

@@ -295,4 +295,34 @@ __device__ __forceinline__ uint64_t pack_key(int64_t total, uint32_t slot) {
   return ((uint64_t)(total + 1) << 32) | (uint64_t)(0xFFFFFFFFu - slot);
 }
 
+// label / taint words of a node as gathered next to its key (CandExt::w)
+__device__ __forceinline__ void ext_from_words(const uint64_t *w, NodeExt &e) {
+  e.hard = w[0];
+  e.prefer = w[1];
+#pragma unroll
+  for (int q = 0; q < LW; ++q) e.lab[q] = w[2 + q];
+#pragma unroll
+  for (int q = 0; q < NNUM; ++q) e.num[q] = (int64_t)w[2 + LW + q];
+}
+
+// Status change of one node between the row the counts were taken on (st0)
+// and its live row (st1), as count corrections: d[0] feasible lost,
+// d[1 + q] first failures gained at plugin q, d[6] / d[7] normaliser-at-max lost.
+template <bool EXT>
+__device__ __forceinline__ void status_delta(const PodDev &p, const uint64_t *clauses, int st0, int st1,
+                                            const NodeExt &e, uint32_t slot, int64_t tt_max, int64_t na_max,
+                                            int32_t *d) {
+  d[0] += (st0 == ST_FEASIBLE) - (st1 == ST_FEASIBLE);
+#pragma unroll
+  for (int q = 0; q < NFILT; ++q) d[1 + q] += (st1 == q) - (st0 == q);
+  if (EXT && (p.flags & PF_TT)) {
+    const int at = taint_raw(p, e) == tt_max;
+    d[6] += (st0 == ST_FEASIBLE) * at - (st1 == ST_FEASIBLE) * at;
+  }
+  if (EXT && (p.flags & PF_NA)) {
+    const int at = preferred_raw(p, clauses, e, slot) == na_max;
+    d[7] += (st0 == ST_FEASIBLE) * at - (st1 == ST_FEASIBLE) * at;
+  }
+}
+
 }  // namespace ks

@@ -555,6 +555,10 @@ struct ks_ctx {
   std::vector<ks_batch *> all_batches;
   // host dictionaries / node mirror: ks_batch_prepare vs the worker's reads of t.lw
   std::mutex mu;
+  // the worker waits for `mu` (run start / end): a compile holding it yields
+  // between pods (compile_yield), so a batch's run does not wait for the
+  // whole compile of a later batch
+  std::atomic<uint32_t> mu_wanted{0};
   std::mutex err_mu;
   // asynchronous runs (ks_batch_submit / ks_batch_wait): one worker thread
   // (ksched_sync.hpp), created at ks_open
@@ -2861,16 +2865,11 @@ ks_status enqueue_round(ks_ctx *c, ks_batch *b, uint32_t k, uint32_t end) {
     ra.par_max_passes = c->par_max_passes;
     ra.prof = c->res_profile ? c->d_counters + 16 : nullptr;
     ra.serial_rounds = c->serial_rounds;
-    if (c->resolve_mode != KS_RESOLVE_SERIAL) {
-      // the parallel commit; under RES_AUTO the serial kernel follows and
-      // resolves the round only if the parallel one handed it over
-      ra.rmode = c->resolve_mode == KS_RESOLVE_AUTO ? c->d_flags + 4 : nullptr;
-      HIPC(c, launch_resolve_par(ra, b->ext, c->rstream));
-      if (ra.rmode) HIPC(c, launch_resolve(ra, b->ext, c->rstream));
-    } else {
-      ra.rmode = nullptr;
-      HIPC(c, launch_resolve(ra, b->ext, c->rstream));
-    }
+    // one launch: the parallel commit, and the serial one in the same
+    // workgroup for the rounds it does not take
+    ra.rmode = c->resolve_mode == KS_RESOLVE_AUTO ? c->d_flags + 4 : nullptr;
+    ra.serial_only = c->resolve_mode == KS_RESOLVE_SERIAL ? 1u : 0u;
+    HIPC(c, launch_resolve(ra, b->ext, c->rstream));
   }
   if (tm) {
     HIPC(c, hipEventRecord(e1, c->rstream));
@@ -3122,7 +3121,9 @@ ks_status run_batch(ks_ctx *c, ks_batch *b) {
   bool classes = false;
   {
     const auto tw = std::chrono::steady_clock::now();
+    c->mu_wanted.fetch_add(1);
     std::lock_guard<std::mutex> g(c->mu);
+    c->mu_wanted.fetch_sub(1);
     if (c->run_profile) c->prof[0] += std::chrono::duration<double>(std::chrono::steady_clock::now() - tw).count();
     if ((st0 = upload_dirty_ext(c, c->xm))) return st0;
     c->run_t = c->t;
@@ -3275,7 +3276,9 @@ ks_status run_batch(ks_ctx *c, ks_batch *b) {
     // NodeInfo.Pods of the nodes this batch bound pods to (later selector
     // classes count them): appended to a log, applied when read
     const auto tw = std::chrono::steady_clock::now();
+    c->mu_wanted.fetch_add(1);
     std::lock_guard<std::mutex> g(c->mu);
+    c->mu_wanted.fetch_sub(1);
     if (c->run_profile) c->prof[4] += std::chrono::duration<double>(std::chrono::steady_clock::now() - tw).count();
     if (c->pending_bound.size() > (1u << 24)) flush_bound(c);
     for (uint32_t i = 0; i < b->n; ++i)
@@ -3537,6 +3540,7 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
 
 void ks_close(ks_ctx *c) {
   if (!c) return;
+  drain_async(c);  // batches still queued or running count in the profile below
   double wp[3];
   c->runq->profile(wp);
   if (c->run_profile)
@@ -3556,7 +3560,6 @@ void ks_close(ks_ctx *c) {
     for (int k = 0; k < 4; ++k)
       std::fprintf(stderr, "ksched events kind %d: %llu runs, %llu events, %.3f s\n", k,
                    (unsigned long long)c->ev_prof[k].runs, (unsigned long long)c->ev_prof[k].events, c->ev_prof[k].s);
-  drain_async(c);
   c->runq->stop();
   (void)hipSetDevice(c->cfg.device);
   // bounded (a wedged context gets one more full timeout to finish)
@@ -4167,6 +4170,20 @@ ks_status ks_events_apply(ks_ctx *c, const ks_event *ev, uint32_t n) {
 // Compile a batch's pods into dev / cl under c->mu.  When the label
 // dictionary runs out of bits, reclaim it once (reset_label_dict, after the
 // submitted batches drained) and compile the batch again from its first pod.
+// Between two pods of a compile under `mu`: when the batch worker waits for
+// `mu` (the start or end of a run), let it in.  Every pod's compile leaves the
+// dictionaries, label sets and classes consistent, and what the worker does
+// there reads them or uploads label rows (a superset of what the running
+// batch needs is harmless), so a compile may be interleaved with it.
+static void compile_yield(ks_ctx *c, std::unique_lock<std::mutex> &lk, uint32_t i) {
+  if ((i & 255u) != 255u || c->mu_wanted.load(std::memory_order_relaxed) == 0) return;
+  lk.unlock();
+  const auto t0 = std::chrono::steady_clock::now();
+  while (c->mu_wanted.load() != 0 && std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(20))
+    std::this_thread::yield();
+  lk.lock();
+}
+
 static ks_status compile_batch(ks_ctx *c, const ks_pod *pods, uint32_t n, PodDev *dev, ProgBuf &cl,
                                std::unique_lock<std::mutex> &lk, bool create_spread = false,
                                std::vector<uint32_t> *class_refs = nullptr) {
@@ -4175,7 +4192,10 @@ static ks_status compile_batch(ks_ctx *c, const ks_pod *pods, uint32_t n, PodDev
     c->compile_used_names = false;
     if (class_refs) class_release(c, class_refs);
     ks_status st = KS_OK;
-    for (uint32_t i = 0; i < n && !st; ++i) st = compile_pod(c, pods[i], dev[i], cl, create_spread, class_refs);
+    for (uint32_t i = 0; i < n && !st; ++i) {
+      st = compile_pod(c, pods[i], dev[i], cl, create_spread, class_refs);
+      compile_yield(c, lk, i);
+    }
     if (st && class_refs) class_release(c, class_refs);
     if (st != KS_ERR_CAPACITY || attempt > 0 || c->next_bit == 0) return st;
     lk.unlock();
@@ -4239,7 +4259,10 @@ ks_status ks_batch_prepare(ks_ctx *c, const ks_pod *pods, uint32_t n, ks_batch *
       // label sets first: they create the term classes of the pods' own terms,
       // which every later pod of the batch that they select must see
       st = KS_OK;
-      for (uint32_t i = 0; i < n && !st; ++i) st = intern_set(c, pods[i], &set_ids[i], &term_refs);
+      for (uint32_t i = 0; i < n && !st; ++i) {
+        st = intern_set(c, pods[i], &set_ids[i], &term_refs);
+        compile_yield(c, g, i);
+      }
       if (!st) st = compile_batch(c, pods, n, dev.data(), cl, g, true, &refs);
       c->undrained = false;
       if (st) {
@@ -4740,6 +4763,13 @@ ks_status ks_set_sync_timeout(ks_ctx *c, uint32_t ms) {
   if (!c || ms == 0) return KS_ERR_INVALID;
   if (ks_status dst_ = drain_async(c)) return dst_;
   c->sync_timeout_ms = ms;
+  return KS_OK;
+}
+
+ks_status ks_debug_runs_started(ks_ctx *c, uint64_t *out) {
+  if (!c || !out) return KS_ERR_INVALID;
+  std::lock_guard<std::mutex> g(c->mu);  // run_batch counts under mu; no drain here
+  *out = c->runs_started;
   return KS_OK;
 }
 

@@ -1,5 +1,5 @@
 // ksched_instr.hpp — instrumentation hooks of the serial resolve kernel
-// (ksched_kernels.hip resolve_kernel).  The product library is built without
+// (ksched_resolve_serial.hpp resolve_serial).  The product library is built without
 // any of the switches below and every hook expands to nothing; only the
 // diagnostic variants of k8s-1m_amd/Makefile define them:
 //

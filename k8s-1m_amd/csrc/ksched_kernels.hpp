@@ -60,17 +60,18 @@ struct RoundArgs {
   uint32_t *flag_res;         // resolve: round number `seq` stored here when done (null: the host signals)
   uint32_t seq;
   uint32_t stall_us;          // ks_debug_stall: the resolve holds its signal back this long (0: never)
-  // Resolve-kernel choice of a resource-only round (ksched_resolve.hip): both
-  // kernels are launched, resolve_par_kernel first.  rmode[0]: rounds left for
-  // the serial resolve_kernel (the parallel kernel exits at once while > 0);
-  // rmode[1]: seq of the last round the parallel kernel resolved (the serial
-  // kernel then exits at once).  A round the parallel kernel cuts short (more
-  // than par_max_passes passes, or too few pods per pass) hands the next
-  // rmode[2] (>= serial_rounds, doubling per consecutive cut) rounds to the
-  // serial kernel.
-  // nullptr: only one kernel is launched and it resolves every round.
+  // Which commit resolves a round (ksched_resolve.hip resolve_kernel runs the
+  // parallel one, then the serial one in the same workgroup when needed),
+  // RESOLVE_AUTO: rmode[0]: rounds left for the serial commit (the parallel
+  // one steps aside while > 0); rmode[1]: seq of the last round the parallel
+  // commit resolved; rmode[2]: the next serial stretch.  A round the parallel
+  // commit bails on (more than par_max_passes passes, or too few pods per
+  // pass) is handed whole to the serial commit, with the next rmode[2]
+  // (>= serial_rounds, doubling per consecutive hand-over) rounds.
+  // nullptr: RESOLVE_PARALLEL, or RESOLVE_SERIAL with serial_only set.
   uint32_t *rmode;
   uint32_t par_max_passes, serial_rounds;
+  uint32_t serial_only;       // RESOLVE_SERIAL: the resolve kernel skips the parallel commit
   uint64_t *prof;             // ks_debug_set_profile: resolve_par_kernel phase cycle sums (null: off)
   uint8_t *marks;             // [npods] per-pod round marks of the batch (ks_batch_marks): KS_MARK_*
   // Identical pods (resource-only batches; null otherwise): pods of a round
@@ -198,7 +199,6 @@ hipError_t launch_merge_shards(const RoundArgs &a, hipStream_t st);
 hipError_t launch_gather_cand(const RoundArgs &a, bool ext, hipStream_t st);
 hipError_t launch_patch(const RoundArgs &a, bool ext, hipStream_t st);
 hipError_t launch_resolve(const RoundArgs &a, bool ext, hipStream_t st);
-hipError_t launch_resolve_par(const RoundArgs &a, bool ext, hipStream_t st);
 hipError_t launch_advance(const RoundArgs &a, hipStream_t st);
 hipError_t launch_advance_writeback(const RoundArgs &a, const CarryRec *carry, const uint32_t *n, hipStream_t st);
 hipError_t launch_writeback(const NodeTable &t, const CarryRec *carry, const uint32_t *n, hipStream_t st);

@@ -47,6 +47,7 @@
 #include "ksched_dev.hpp"
 #include "ksched_eval.hpp"
 #include "ksched_kernels.hpp"
+#include "ksched_resolve_serial.hpp"
 #include "ksched_util.hpp"
 
 namespace ks {
@@ -58,7 +59,6 @@ constexpr int PNC = 16;     // candidates gathered per chunk pod (resource-only 
 constexpr int PMH = 1024;   // modified-slot hash (rhash: 10 bits), M <= MAX_P nodes
 constexpr int PNR = 4;      // candidates per chunk pod whose rows are prefetched (LDS-DMA)
 constexpr int PGH_BITS = 7, PGH = 1 << PGH_BITS;  // chunk slot-group hash (<= PCH slots)
-constexpr int ROW_PIECES = sizeof(CandRow) / 16;
 constexpr uint32_t PNONE = 0xFFFFFFFFu;
 constexpr uint32_t PSRC_M = 0x10000u;  // proposal source: Rpre's node (M index in the low bits)
 static_assert(PCH == WAVE, "B1 runs one chunk pod per lane of one wave");
@@ -259,16 +259,17 @@ __device__ __forceinline__ void pq_add(CandRow &r, const PQ &q) {  // NodeInfo.A
 // s_memtime after each barrier and charges the interval to a phase, in LDS
 // (no registers held across the kernel).
 struct PhaseClock {
-  uint64_t *out, *acc;
+  uint64_t *out, *acc;  // out: wave-uniform (wave 0 only), null when off
   uint64_t t;
+  bool lead;            // thread 0: adds the sums to `out`
   __device__ __forceinline__ void tick(int phase) {
     if (out == nullptr) return;
     const uint64_t now = __builtin_amdgcn_s_memtime();
-    if (phase >= 0) acc[phase] += now - t;
+    if (phase >= 0) acc[phase] += now - t;  // every lane of wave 0 stores the same sum
     t = now;
   }
   __device__ __forceinline__ void flush() {
-    if (out == nullptr) return;
+    if (out == nullptr || !lead) return;
     acc[9] = 1;
     for (int i = 0; i < 16; ++i) atomicAdd((unsigned long long *)&out[i], (unsigned long long)acc[i]);
   }
@@ -284,70 +285,150 @@ __device__ __forceinline__ uint32_t dhash(uint32_t x) { return (x * 2654435761u)
 // and prefetch the rows of the first PNR_EXT, and have no one-step path
 // (label / taint batches keep one record per pod: no identical-pod classes).
 constexpr int PNC_EXT = 8, PNR_EXT = 2;
-constexpr int EXT_PIECES = sizeof(CandExt) / 16;
 
+// The parallel commit's LDS, a member of the resolve kernel's LDS union
 template <bool EXT>
-__global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
+struct ParLds {
+  static constexpr int NC = EXT ? PNC_EXT : PNC;      // candidates gathered per chunk pod
+  static constexpr int NR = EXT ? PNR_EXT : PNR;      // ... whose rows are prefetched
+  static constexpr int DH_BITS = EXT ? 10 : 11;
+  static constexpr int DH = 1 << DH_BITS;             // chunk claim hash (<= PCH * NC + PCH slots)
+  static constexpr int XP = EXT ? 1 : 0;              // EXT-only arrays: full size, else one element
+  static constexpr int FP = EXT ? 0 : 1;              // one-step-path arrays (resource-only rounds)
+  // ---- per pod of the round
+  PQ s_q[MAX_P];
+  PX s_px[XP ? MAX_P : 1];          // EXT: labels / taints / normaliser maxima
+  uint32_t s_dn[XP ? MAX_P : 1];    // EXT: normaliser-at-max nodes lost to the fixed prefix (tt | na << 16)
+  uint32_t s_fl[MAX_P];
+  ShardRecHdr s_hdr[MAX_P];
+  uint32_t s_rep[MAX_P];
+  uint64_t s_rk[MAX_P];     // Rpre: best key over the fixed prefix's modified nodes (0: none feasible)
+  int32_t s_dl[MAX_P];      // feasible nodes lost (Fit) to the fixed prefix's commits
+  uint32_t s_dirty[MAX_P];  // Rpre's node was re-taken: recompute before use
+  uint32_t s_lptr[MAX_P];   // list entries before it are all in M
+  uint4 s_resc[MAX_P];      // result: {win lo, win hi, feasible, status}
+  int32_t s_rdl[MAX_P];     // result: Fit failures gained
+  uint32_t s_pfo[MAX_P];    // result: PodDev::prefilter_out (staged: no global read in the epilogue)
+  // ---- fixed modified nodes (M): live row, round-start Requested / pod count, slot
+  RNode s_m[MAX_P];
+  CandExt s_mx[XP ? MAX_P : 1];   // EXT: their label / taint words
+  uint32_t s_mh[PMH], s_mi[PMH];  // slot + 1 -> M index
+  // ---- chunk
+  uint64_t s_ck[PCH][NC];  // gathered candidates: keys ...
+  uint16_t s_ce[PCH][NC];  // ... and list entries
+  uint4 s_crow[PCH][ROW_PIECES][NR];  // the first NR candidates' rows (LDS-DMA)
+  uint4 s_crowx[XP ? PCH : 1][EXT_PIECES][NR];  // EXT: ... and their label / taint words
+  uint32_t s_cnc[PCH], s_cmore[PCH], s_cpst[PCH];
+  uint32_t s_dh[DH], s_do[DH];    // claims: slot + 1 -> lowest claiming chunk pod
+  uint32_t s_gh[PGH];             // chunk slot groups: slot + 1 ...
+  uint64_t s_gm[PGH];             // ... -> lanes
+  uint64_t s_pk[PCH];    // proposal key
+  uint32_t s_ps[PCH];    // proposal slot (PNONE: none)
+  uint32_t s_pnx[PCH];   // next chunk pod proposing the same slot (PNONE)
+  uint32_t s_pfst[PCH];  // first chunk pod proposing its slot
+  RNode s_prow[PCH];     // proposed node's state at the chunk start
+  CandExt s_prowx[XP ? PCH : 1];  // EXT: its label / taint words
+  uint64_t s_ik[PCH];    // best key over nodes taken earlier in the chunk
+  int32_t s_idl[PCH];    // feasible nodes lost to them
+  uint32_t s_idn[XP ? PCH : 1];   // EXT: normaliser-at-max nodes lost to them
+  uint32_t s_cdm[PCH];   // distinct nodes committed by the fixed pods: M index,
+  double s_cdp[PCH][2];  // Requested before this chunk's commits,
+  int32_t s_cdn[PCH];    // pod count before,
+  uint32_t s_cdr[PCH];   // node was in M before the chunk
+  // control: [0] f, [1] stopped, [2] cut, [4] distinct nodes, [5] |M|, [6] passes
+  uint32_t s_ctl[8];
+  // a round of identical request-less pods in one step (identical_round below)
+  uint64_t s_ek[FP ? PR_THREADS : 1];  // entries: node key after k of the round's pods
+  uint32_t s_ex[FP ? PR_THREADS : 1];  //   list index << 16 | k << 1 | Fit lost by taking it
+  uint32_t s_tx[FP ? MAX_K : 1];       // pods each listed node takes
+  uint32_t s_ic[4];           // [0] entries, [1] not applicable, [2] modified nodes
+  uint32_t s_wt[PR_NW];       // per-wave counts (prefix sums)
+  uint64_t s_clk[16];  // phase clock (ks_debug_set_profile)
+};
+
+// The resolve kernel's LDS: one buffer that the parallel commit's and the
+// serial commit's layouts overlay (each fits the CU's 160 KB on its own, not
+// both).  Accessed through a namespace-scope symbol, so that the commits'
+// lambdas read their arrays without capturing a pointer to them.
+constexpr size_t cmax(size_t x, size_t y) { return x > y ? x : y; }
+constexpr size_t RES_LDS_BYTES =
+    cmax(cmax(sizeof(ParLds<true>), sizeof(ParLds<false>)),
+         cmax(cmax(sizeof(SerialLds<true, LIST_SPAN_1>), sizeof(SerialLds<true, LIST_SPAN_2>)),
+              cmax(sizeof(SerialLds<false, LIST_SPAN_1>), sizeof(SerialLds<false, LIST_SPAN_2>))));
+alignas(16) __shared__ uint8_t g_res_lds[RES_LDS_BYTES];
+template <bool EXT>
+__device__ __forceinline__ ParLds<EXT> *par_lds() {
+  return reinterpret_cast<ParLds<EXT> *>(g_res_lds);
+}
+template <bool EXT, int LIST_SPAN>
+__device__ __forceinline__ SerialLds<EXT, LIST_SPAN> *ser_lds() {
+  return reinterpret_cast<SerialLds<EXT, LIST_SPAN> *>(g_res_lds);
+}
+
+// Returns true when it resolved the round (or found it wasted); false when
+// the serial commit must take it (RESOLVE_SERIAL, a serial stretch of
+// RESOLVE_AUTO, or a hand-over from this round)
+template <bool EXT>
+__device__ __forceinline__ bool resolve_parallel(const RoundArgs &a) {
   constexpr int NC = EXT ? PNC_EXT : PNC;      // candidates gathered per chunk pod
   constexpr int NR = EXT ? PNR_EXT : PNR;      // ... whose rows are prefetched
   constexpr int DH_BITS = EXT ? 10 : 11;
   constexpr int DH = 1 << DH_BITS;             // chunk claim hash (<= PCH * NC + PCH slots)
   static_assert(DH >= PCH * NC + PCH, "claims hash: every slot a chunk can claim");
-  constexpr int XP = EXT ? 1 : 0;              // EXT-only arrays: full size, else one element
-  constexpr int FP = EXT ? 0 : 1;              // one-step-path arrays (resource-only rounds)
-  // ---- per pod of the round
-  __shared__ PQ s_q[MAX_P];
-  __shared__ PX s_px[XP ? MAX_P : 1];          // EXT: labels / taints / normaliser maxima
-  __shared__ uint32_t s_dn[XP ? MAX_P : 1];    // EXT: normaliser-at-max nodes lost to the fixed prefix (tt | na << 16)
-  __shared__ uint32_t s_fl[MAX_P];
-  __shared__ ShardRecHdr s_hdr[MAX_P];
-  __shared__ uint32_t s_rep[MAX_P];
-  __shared__ uint64_t s_rk[MAX_P];     // Rpre: best key over the fixed prefix's modified nodes (0: none feasible)
-  __shared__ int32_t s_dl[MAX_P];      // feasible nodes lost (Fit) to the fixed prefix's commits
-  __shared__ uint32_t s_dirty[MAX_P];  // Rpre's node was re-taken: recompute before use
-  __shared__ uint32_t s_lptr[MAX_P];   // list entries before it are all in M
-  __shared__ uint4 s_resc[MAX_P];      // result: {win lo, win hi, feasible, status}
-  __shared__ int32_t s_rdl[MAX_P];     // result: Fit failures gained
-  __shared__ uint32_t s_pfo[MAX_P];    // result: PodDev::prefilter_out (staged: no global read in the epilogue)
-  // ---- fixed modified nodes (M): live row, round-start Requested / pod count, slot
-  __shared__ RNode s_m[MAX_P];
-  __shared__ CandExt s_mx[XP ? MAX_P : 1];   // EXT: their label / taint words
-  __shared__ uint32_t s_mh[PMH], s_mi[PMH];  // slot + 1 -> M index
-  // ---- chunk
-  __shared__ uint64_t s_ck[PCH][NC];  // gathered candidates: keys ...
-  __shared__ uint16_t s_ce[PCH][NC];  // ... and list entries
-  __shared__ uint4 s_crow[PCH][ROW_PIECES][NR];  // the first NR candidates' rows (LDS-DMA)
-  __shared__ uint4 s_crowx[XP ? PCH : 1][EXT_PIECES][NR];  // EXT: ... and their label / taint words
-  __shared__ uint32_t s_cnc[PCH], s_cmore[PCH], s_cpst[PCH];
-  __shared__ uint32_t s_dh[DH], s_do[DH];    // claims: slot + 1 -> lowest claiming chunk pod
-  __shared__ uint32_t s_gh[PGH];             // chunk slot groups: slot + 1 ...
-  __shared__ uint64_t s_gm[PGH];             // ... -> lanes
-  __shared__ uint64_t s_pk[PCH];    // proposal key
-  __shared__ uint32_t s_ps[PCH];    // proposal slot (PNONE: none)
-  __shared__ uint32_t s_pnx[PCH];   // next chunk pod proposing the same slot (PNONE)
-  __shared__ uint32_t s_pfst[PCH];  // first chunk pod proposing its slot
-  __shared__ RNode s_prow[PCH];     // proposed node's state at the chunk start
-  __shared__ CandExt s_prowx[XP ? PCH : 1];  // EXT: its label / taint words
-  __shared__ uint64_t s_ik[PCH];    // best key over nodes taken earlier in the chunk
-  __shared__ int32_t s_idl[PCH];    // feasible nodes lost to them
-  __shared__ uint32_t s_idn[XP ? PCH : 1];   // EXT: normaliser-at-max nodes lost to them
-  __shared__ uint32_t s_cdm[PCH];   // distinct nodes committed by the fixed pods: M index,
-  __shared__ double s_cdp[PCH][2];  // Requested before this chunk's commits,
-  __shared__ int32_t s_cdn[PCH];    // pod count before,
-  __shared__ uint32_t s_cdr[PCH];   // node was in M before the chunk
-  // control: [0] f, [1] stopped, [2] cut, [4] distinct nodes, [5] |M|, [6] passes
-  __shared__ uint32_t s_ctl[8];
-  // a round of identical request-less pods in one step (identical_round below)
-  __shared__ uint64_t s_ek[FP ? PR_THREADS : 1];  // entries: node key after k of the round's pods
-  __shared__ uint32_t s_ex[FP ? PR_THREADS : 1];  //   list index << 16 | k << 1 | Fit lost by taking it
-  __shared__ uint32_t s_tx[FP ? MAX_K : 1];       // pods each listed node takes
-  __shared__ uint32_t s_ic[4];           // [0] entries, [1] not applicable, [2] modified nodes
-  __shared__ uint32_t s_wt[PR_NW];       // per-wave counts (prefix sums)
+#define s_q (par_lds<EXT>()->s_q)
+#define s_px (par_lds<EXT>()->s_px)
+#define s_dn (par_lds<EXT>()->s_dn)
+#define s_fl (par_lds<EXT>()->s_fl)
+#define s_hdr (par_lds<EXT>()->s_hdr)
+#define s_rep (par_lds<EXT>()->s_rep)
+#define s_rk (par_lds<EXT>()->s_rk)
+#define s_dl (par_lds<EXT>()->s_dl)
+#define s_dirty (par_lds<EXT>()->s_dirty)
+#define s_lptr (par_lds<EXT>()->s_lptr)
+#define s_resc (par_lds<EXT>()->s_resc)
+#define s_rdl (par_lds<EXT>()->s_rdl)
+#define s_pfo (par_lds<EXT>()->s_pfo)
+#define s_m (par_lds<EXT>()->s_m)
+#define s_mx (par_lds<EXT>()->s_mx)
+#define s_mh (par_lds<EXT>()->s_mh)
+#define s_mi (par_lds<EXT>()->s_mi)
+#define s_ck (par_lds<EXT>()->s_ck)
+#define s_ce (par_lds<EXT>()->s_ce)
+#define s_crow (par_lds<EXT>()->s_crow)
+#define s_crowx (par_lds<EXT>()->s_crowx)
+#define s_cnc (par_lds<EXT>()->s_cnc)
+#define s_cmore (par_lds<EXT>()->s_cmore)
+#define s_cpst (par_lds<EXT>()->s_cpst)
+#define s_dh (par_lds<EXT>()->s_dh)
+#define s_do (par_lds<EXT>()->s_do)
+#define s_gh (par_lds<EXT>()->s_gh)
+#define s_gm (par_lds<EXT>()->s_gm)
+#define s_pk (par_lds<EXT>()->s_pk)
+#define s_ps (par_lds<EXT>()->s_ps)
+#define s_pnx (par_lds<EXT>()->s_pnx)
+#define s_pfst (par_lds<EXT>()->s_pfst)
+#define s_prow (par_lds<EXT>()->s_prow)
+#define s_prowx (par_lds<EXT>()->s_prowx)
+#define s_ik (par_lds<EXT>()->s_ik)
+#define s_idl (par_lds<EXT>()->s_idl)
+#define s_idn (par_lds<EXT>()->s_idn)
+#define s_cdm (par_lds<EXT>()->s_cdm)
+#define s_cdp (par_lds<EXT>()->s_cdp)
+#define s_cdn (par_lds<EXT>()->s_cdn)
+#define s_cdr (par_lds<EXT>()->s_cdr)
+#define s_ctl (par_lds<EXT>()->s_ctl)
+#define s_ek (par_lds<EXT>()->s_ek)
+#define s_ex (par_lds<EXT>()->s_ex)
+#define s_tx (par_lds<EXT>()->s_tx)
+#define s_ic (par_lds<EXT>()->s_ic)
+#define s_wt (par_lds<EXT>()->s_wt)
+#define s_clk (par_lds<EXT>()->s_clk)
 
   // tid / lane are re-materialised at each pass (see the pass loop)
   uint32_t tid = threadIdx.x, lane = tid % WAVE;
   const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x / WAVE);
-  if (a.rmode != nullptr && uniform_u32(a.rmode[0]) != 0) return;  // serial rounds: resolve_kernel follows
+  if (a.serial_only) return false;                                         // RESOLVE_SERIAL
+  if (a.rmode != nullptr && uniform_u32(a.rmode[0]) != 0) return false;  // a serial stretch (AUTO)
   const uint32_t start = uniform_u32(*a.act);
   if (start >= a.npods || uniform_u32(*a.sstart) != start) {  // the lists belong to other pods
     if (tid == 0) {
@@ -361,17 +442,18 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
       if (a.rmode != nullptr) a.rmode[1] = a.seq;
       signal_done(a.flag_res, a.seq, a.stall_us);
     }
-    return;
+    return true;
   }
   const uint32_t n = min(a.P, a.npods - start);
   const uint32_t RW = rec_words(a.K);
-  const uint64_t lt_mask = (1ull << lane) - 1ull;
+  // lanes below this one (recomputed where used: a 64-bit value held across
+  // the kernel costs two of the 128 VGPRs)
+#define lt_mask ((1ull << lane) - 1ull)
   // phases: 0 stage, 1 gather barrier, 2 proposals, 3 wave 0's row DMA issue, 4 chunk pairs, 5 wave 0's
   // DMA wait, 6 decide + commit, 7 Rpre updates, 8 epilogue, [9] rounds, [10] dirty recomputes, [11] extra
   // windows, 12 wave 0's wait for the prefetched windows, 13 its scalar state + probes, 14 its window scans
-  __shared__ uint64_t s_clk[16];
   if (tid < 16) s_clk[tid] = 0;
-  PhaseClock clk{tid == 0 ? a.prof : nullptr, s_clk, 0};
+  PhaseClock clk{wid == 0 ? a.prof : nullptr, s_clk, 0, tid == 0};
   clk.tick(-1);
 
   auto mh_find = [&](uint32_t slot) -> uint32_t {
@@ -1134,7 +1216,7 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
     }
     clk.tick(8);
     clk.flush();
-    return;  // no completion signal: the serial kernel gives it
+    return false;  // no completion signal: the serial commit gives it
   }
 
   // ---- results of the resolved pods, the modified nodes, the next round's start
@@ -1185,11 +1267,79 @@ __global__ __launch_bounds__(PR_THREADS) void resolve_par_kernel(RoundArgs a) {
   clk.tick(8);
   clk.flush();
   if (tid == 0) signal_done(a.flag_res, a.seq, a.stall_us);
+  return true;
+#undef lt_mask
+#undef s_q
+#undef s_px
+#undef s_dn
+#undef s_fl
+#undef s_hdr
+#undef s_rep
+#undef s_rk
+#undef s_dl
+#undef s_dirty
+#undef s_lptr
+#undef s_resc
+#undef s_rdl
+#undef s_pfo
+#undef s_m
+#undef s_mx
+#undef s_mh
+#undef s_mi
+#undef s_ck
+#undef s_ce
+#undef s_crow
+#undef s_crowx
+#undef s_cnc
+#undef s_cmore
+#undef s_cpst
+#undef s_dh
+#undef s_do
+#undef s_gh
+#undef s_gm
+#undef s_pk
+#undef s_ps
+#undef s_pnx
+#undef s_pfst
+#undef s_prow
+#undef s_prowx
+#undef s_ik
+#undef s_idl
+#undef s_idn
+#undef s_cdm
+#undef s_cdp
+#undef s_cdn
+#undef s_cdr
+#undef s_ctl
+#undef s_ek
+#undef s_ex
+#undef s_tx
+#undef s_ic
+#undef s_wt
+#undef s_clk
 }
 
-hipError_t launch_resolve_par(const RoundArgs &a, bool ext, hipStream_t st) {
-  if (ext) resolve_par_kernel<true><<<1, PR_THREADS, 0, st>>>(a);
-  else resolve_par_kernel<false><<<1, PR_THREADS, 0, st>>>(a);
+// One launch per round on the resolve stream: the parallel commit, and the
+// serial one in the same workgroup when the round is not the parallel
+// commit's (RESOLVE_SERIAL, a serial stretch, a hand-over).  The two share
+// one LDS allocation (a union: each is within the CU's 160 KB on its own);
+// the serial commit reads nothing the parallel one wrote to LDS.
+template <bool EXT, int LIST_SPAN>
+__global__ __launch_bounds__(PR_THREADS) void resolve_kernel(RoundArgs a) {
+  static_assert(PR_THREADS == RESOLVE_THREADS, "both commits run on one 1024-thread workgroup");
+  if (resolve_parallel<EXT>(a)) return;
+  __syncthreads();  // the parallel commit's last LDS reads, its hand-over writes (rmode)
+  resolve_serial<EXT, LIST_SPAN>(a);
+}
+
+hipError_t launch_resolve(const RoundArgs &a, bool ext, hipStream_t st) {
+  if (a.K <= (uint32_t)(RES_LIST_WAVES * LIST_SPAN_1)) {
+    if (ext) resolve_kernel<true, LIST_SPAN_1><<<1, PR_THREADS, 0, st>>>(a);
+    else resolve_kernel<false, LIST_SPAN_1><<<1, PR_THREADS, 0, st>>>(a);
+  } else {
+    if (ext) resolve_kernel<true, LIST_SPAN_2><<<1, PR_THREADS, 0, st>>>(a);
+    else resolve_kernel<false, LIST_SPAN_2><<<1, PR_THREADS, 0, st>>>(a);
+  }
   return hipGetLastError();
 }
 

@@ -97,13 +97,13 @@ def pick_windows(marks, m, wlen=WLEN, fixed=WINDOWS, per_kind=3, round_every=16,
     starts = starts[starts + wlen <= m]
     cand += [(int(w), "round-start") for w in starts[::round_every]]
 
-    def take(cands):
-        out, end = [], -1
-        for w, what in sorted(cands):
-            if w >= end:
-                out.append((w, what))
-                end = w + wlen
-        return out
+    def take(cands):  # non-overlapping; the fixed windows first
+        out = []
+        for fixed_pass in (True, False):
+            for w, what in sorted(cands):
+                if (what == "fixed") == fixed_pass and all(w + wlen <= x or w >= x + wlen for x, _ in out):
+                    out.append((w, what))
+        return sorted(out)
 
     out = take(cand)
     rng = np.random.default_rng(1234 + seed)
@@ -264,20 +264,13 @@ def test_c2_bench_pipeline_100k_replay():
     assert (r["status"] == 0).mean() > 0.99
 
 
-def test_c4_labeled_1m_replay_early_fix():
-    # the C4 sweep path with the FIX sweep right behind it on the main stream
-    # (early FIX, compacted FIX list) and simple normaliser guesses, so that
-    # the FIX path runs often (the default node-tuple guesses run at bench
-    # length in test_c4_bench_pipeline_1m_replay)
-    r, dbg = run_fullsize(synth.LABELED, synth.pods(synth.LABELED, BATCH, 2), prefill=True,
-                          opts={"tuple_guess": 0})
-    assert dbg[4] > 0, "no pod was re-swept with a measured normaliser (FIX path not exercised)"
-    assert (r["status"] == 1).any() and (r["status"] == 0).mean() > 0.9
-
-
 def test_c4_labeled_1m_replay_fix_behind_merge():
-    # early_fix = 0: the FIX sweep runs behind the merge on the side stream
-    # (the multi-rank order), here on one rank
+    # simple normaliser guesses (tuple_guess = 0), so that the FIX path runs
+    # often, with the FIX sweep behind the merge on the side stream
+    # (early_fix = 0, the multi-rank order) on one rank; the early FIX sweep
+    # of the default configuration runs at bench length in
+    # test_c4_bench_pipeline_1m_replay (asserting FIX re-sweeps), and the
+    # default node-tuple guesses there too
     r, dbg = run_fullsize(synth.LABELED, synth.pods(synth.LABELED, BATCH, 2), prefill=True,
                           opts={"tuple_guess": 0, "early_fix": 0})
     assert dbg[4] > 0, "no pod was re-swept with a measured normaliser (FIX path not exercised)"

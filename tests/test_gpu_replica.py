@@ -4,6 +4,7 @@ replicas under the system default constraints -- scheduled by one filter pass
 and one workgroup per run.  Results and node states against the oracle
 (upstream v1.31.3 podtopologyspread restated in oracle.cpp) bit for bit, and
 the device counters show which path ran."""
+import ctypes as C
 import random
 import time
 
@@ -192,8 +193,17 @@ def test_class_created_while_a_batch_runs():
     s.reset_stats()
     assert s.lib.ks_debug_stall(s.ctx, 0, 300_000) == 0
     ba = s.prepare(pa, ma)
+    started = C.c_uint64()
+    assert s.lib.ks_debug_runs_started(s.ctx, C.byref(started)) == 0
+    runs0 = started.value
     assert s.lib.ks_batch_submit(s.ctx, ba) == 0, s.lib.ks_last_error(s.ctx)
-    time.sleep(0.05)  # the worker has taken A's class masks; A waits in its held-back round
+    # wait until the worker has taken A's class masks (its run started); A
+    # then waits in its held-back round
+    deadline = time.monotonic() + 30
+    while started.value == runs0:
+        assert time.monotonic() < deadline, "batch A's run never started"
+        time.sleep(0.001)
+        assert s.lib.ks_debug_runs_started(s.ctx, C.byref(started)) == 0
     bb = s.prepare(pb, mb)  # A is in flight: the classes are created without a drain
     assert s.lib.ks_batch_submit(s.ctx, bb) == 0, s.lib.ks_last_error(s.ctx)
     for b, m, want, what in ((ba, ma, want_a, "batch in flight"), (bb, mb, want_b, "new classes")):
