@@ -396,14 +396,16 @@ typedef struct {
    * sequential loop does (the tests pin each one); they choose how the device
    * gets there.  ks_open reads no environment variable that selects any of
    * this. */
-  uint32_t resolve_mode;          /* in-order commit of resource-only rounds: KS_RESOLVE_AUTO (default:
-                                     the parallel proposal / verify kernel, handing rounds where pods pile
-                                     onto the same nodes to the serial kernel), KS_RESOLVE_SERIAL,
-                                     KS_RESOLVE_PARALLEL */
+  uint32_t resolve_mode;          /* in-order commit of every round (resource-only and label / taint):
+                                     KS_RESOLVE_AUTO (default: the parallel proposal / verify commit,
+                                     handing rounds where pods pile onto the same nodes to the serial
+                                     commit in the same launch), KS_RESOLVE_SERIAL, KS_RESOLVE_PARALLEL
+                                      */
   uint32_t resolve_par_max_passes;  /* AUTO: a round needing more chunk passes than this (32, 1..257),
-                                       or on pace (after 4) to need more, ends early and ...          */
-  uint32_t resolve_serial_rounds;   /* ... hands this many following rounds (4, <= 2^20; doubled per
-                                       consecutive cut, up to 256 rounds or 16x) to the serial kernel  */
+                                       or on pace (after 4) to need more, goes whole to the serial
+                                       commit, with ...                                                */
+  uint32_t resolve_serial_rounds;   /* ... this many following rounds (4, <= 2^20; doubled per
+                                       consecutive hand-over, up to 256 rounds or 16x)                 */
   uint32_t dedup_identical_pods;  /* 1 (default): a round's byte-identical pods are swept once (§5.5) */
   uint32_t early_fix;             /* 1 (default): on one rank the normaliser FIX re-sweep follows the
                                      sweep on its stream (§5.2); 0: behind the merge (multi-rank order) */
@@ -601,7 +603,7 @@ ks_status ks_reset_stats(ks_ctx *ctx);
  * (one class of identical request-less pods).  (The instrumented stamps builds,
  * k8s-1m_amd/csrc/ksched_instr.hpp, put phase cycle sums in [8..15].) */
 ks_status ks_debug_counters(ks_ctx *ctx, uint64_t out[16]);
-/* Diagnostics of the parallel commit (resource-only rounds): with the profile
+/* Diagnostics of the parallel commit: with the profile
  * on, every round accumulates s_memtime cycles per phase: out[0] stage,
  * [1] gather barrier, [2] proposals, [3] wave 0's row DMA issue, [4] chunk
  * pairs, [5] its DMA wait, [6] decide + commit, [7] Rpre updates, [8]
