@@ -2257,21 +2257,30 @@ uint32_t solo_passes(const SoloHdr *hd) {
   return f;
 }
 
-// Replica runs: the run kernel models a one-pod program whose
-// constraints are all ScheduleAnyway, with at most one kubernetes.io/hostname
-// and one other key, and no InterPodAffinity, extended-resource or image
-// records.  The inclusion policies need no check: PreScore's per-node
+// Replica runs: the run kernel models a one-pod program with at
+// most one kubernetes.io/hostname constraint (ScheduleAnyway) and one on
+// another key, and no InterPodAffinity, extended-resource or image records.  The inclusion policies need no check: PreScore's per-node
 // nodeAffinityPolicy / nodeTaintsPolicy tests pass on every node a pod can be
 // committed to (a feasible node matches the pod's required affinity and
 // tolerates its hard taints).
+// Since round 6 the other key's constraint may be DoNotSchedule: the run
+// then blocks and unblocks whole domains as their counts and the minimum
+// move, for pods without a normalised TaintToleration / NodeAffinity score
+// (those maxima range over the feasible nodes, which change in such a run).
 bool replica_program(const PodDev &p, const SoloHdr *hd) {
   if (hd->n_spread == 0 || hd->n_aff || hd->n_xres || hd->n_img || (p.flags & PF_PREF_ERR)) return false;
   const SpreadDev *sd = reinterpret_cast<const SpreadDev *>(hd + 1);
   uint32_t host = 0, other = 0;
+  bool dns = false;
   for (uint32_t k = 0; k < hd->n_spread; ++k) {
-    if (!(sd[k].flags & SP_SCORE)) return false;
-    ++((sd[k].flags & SP_HOST) ? host : other);
+    const bool h = sd[k].flags & SP_HOST;
+    if (!(sd[k].flags & SP_SCORE)) {
+      if (h) return false;
+      dns = true;
+    }
+    ++(h ? host : other);
   }
+  if (dns && (p.flags & (PF_TT | PF_NA))) return false;
   return host <= 1 && other <= 1;
 }
 
@@ -3013,14 +3022,13 @@ bool replica_fits(const ks_ctx *c, const ks_batch *b, const SpreadArgs &sa, uint
 // (lo: refused) and why it stopped (RunStop).
 ks_status replica_run(ks_ctx *c, ks_batch *b, SpreadArgs sa, uint32_t lo, uint32_t hi, uint32_t *next,
                       uint32_t *stop) {
-  (void)b;
   if (!c->d_rk_keys) {
     size_t bytes = 0;
     HIPC(c, launch_sort_pairs(nullptr, nullptr, nullptr, nullptr, c->cap, 64, nullptr, &bytes, c->stream));
     ks_status st;
     if ((st = dalloc(c, &c->d_rk_keys, c->npos)) || (st = dalloc(c, &c->d_rk_sorted, c->npos)) ||
         (st = dalloc(c, &c->d_rk_val, c->npos)) || (st = dalloc(c, &c->d_rk_sval, c->npos)) ||
-        (st = dalloc(c, &c->d_rk_gstart, RUN_GROUPS)) || (st = dalloc(c, &c->d_rk_ctl, 4)) ||
+        (st = dalloc(c, &c->d_rk_gstart, RUN_GROUPS)) || (st = dalloc(c, &c->d_rk_ctl, RUN_CTL_WORDS)) ||
         (st = dalloc(c, &c->d_rk_tmp, std::max<size_t>(bytes, 16))) ||
         (c->run_profile && (st = dalloc(c, &c->d_rk_prof, 4))))
       return st;
@@ -3042,7 +3050,7 @@ ks_status replica_run(ks_ctx *c, ks_batch *b, SpreadArgs sa, uint32_t lo, uint32
     e1 = get_event(c);
     HIPC(c, hipEventRecord(e0, c->stream));
   }
-  HIPC(c, launch_replica_run(sa, r, c->d_rk_tmp, c->rk_tmp_bytes, c->stream));
+  HIPC(c, launch_replica_run(sa, r, c->d_rk_tmp, c->rk_tmp_bytes, b->spread[lo] & 0x7Fu, c->stream));
   if (c->timing) HIPC(c, hipEventRecord(e1, c->stream));
   HIPC(c, hipMemcpyAsync(c->h_rk_ctl, c->d_rk_ctl, 16, hipMemcpyDeviceToHost, c->stream));
   if (ks_status st = sync_bounded(c, c->stream, "a replica run")) return st;

@@ -147,8 +147,9 @@ struct SpreadArgs {
 };
 
 // Replica runs (ksched_spread.hip): consecutive identical pods
-// whose constraints are all ScheduleAnyway (at most one kubernetes.io/hostname
-// and one other key), scheduled by one workgroup after one filter pass.  Sort
+// whose constraints are ScheduleAnyway (at most one kubernetes.io/hostname and
+// one other key; the other may be DoNotSchedule), scheduled by one workgroup
+// after one filter pass.  Sort
 // key of a feasible node, at its slot: group code (ignored << 19 | domain << 8
 // | own hostname count) << s_bits | (2^s_bits - 1 - static score).
 constexpr uint32_t RUN_GROUPS = 512;    // groups a run can hold (more: the run is refused)
@@ -165,11 +166,14 @@ static_assert((RK_DZ_NONE << 8 | RK_HK_NONE) < RK_IGN && (RK_IGN | 0x7FFFFu) == 
                   RK_IGN != 0xFFFFFu,
               "replica sort keys: feasible / ignored codes stay below the infeasible code");
 enum RunStop : uint32_t { RUN_END = 0, RUN_FIT = 1, RUN_FULL = 2, RUN_REFUSED = 3 };
+constexpr uint32_t RUN_CTL_WORDS = 8;
 struct ReplicaArgs {
   uint64_t *keys, *sorted;  // [npos] sort keys, sorted
   uint64_t *val, *sval;     // [nslots] slot << 32 | position of each key, sorted with the keys
   uint32_t *gstart;         // [RUN_GROUPS] first sorted index of each group (unordered)
-  uint32_t *ctl;            // [4] 0 groups, 1 hostname count beyond RK_HK_NONE - 1, 2 next pod, 3 RunStop
+  uint32_t *ctl;            // [RUN_CTL_WORDS] 0 groups, 1 refuse (a hostname count beyond RK_HK_NONE - 1, an
+                            // ignored candidate of a DoNotSchedule run), 2 next pod, 3 RunStop, 4 candidates
+                            // only the skew check rejected (DoNotSchedule runs)
   uint32_t end;             // one past the run's last pod
   uint32_t nslots;          // keys sorted (one per slot)
   uint32_t s_bits;          // bits of the static score (2^s_bits > 100 x the static plugins' weights)
@@ -178,9 +182,11 @@ struct ReplicaArgs {
 
 hipError_t launch_spread_pod(const SpreadArgs &a, uint32_t passes, hipStream_t st);
 hipError_t launch_spread_reset(const SpreadArgs &a, hipStream_t st);
-// filter pass for a.pod, keys, sort, groups, the run kernel; ctl zeroed first
+// [prep + min passes (passes: SPL_PREP / SPL_MIN, a DoNotSchedule
+// constraint)], the filter pass for a.pod, keys, sort, groups, the run
+// kernel; ctl zeroed first
 hipError_t launch_replica_run(const SpreadArgs &a, const ReplicaArgs &r, void *sort_tmp, size_t sort_tmp_bytes,
-                              hipStream_t st);
+                              uint32_t passes, hipStream_t st);
 hipError_t launch_sort_pairs(const uint64_t *kin, uint64_t *kout, const uint64_t *vin, uint64_t *vout, uint32_t n,
                              uint32_t end_bit, void *tmp, size_t *tmp_bytes, hipStream_t st);
 hipError_t launch_class_commit(const DevResult *res, const uint64_t *cmask, const uint32_t *slot_pos, uint32_t *cnt,

@@ -1062,6 +1062,26 @@ __global__ void spread_commit_kernel(SpreadArgs a) {
 // packed-key argmax as spread_select, AssumePod as spread_commit.  The run
 // ends before a pod whose Filter result would differ (a taken node no longer
 // fits) and after RUN_TOUCHED taken nodes; the host starts the next run there.
+//
+// DoNotSchedule on the other key (round 6): the Filter result
+// then also depends on the domain counts -- a domain is blocked while its
+// count + self - minMatch > maxSkew -- and every commit moves one domain's
+// count, and with it perhaps the global minimum.  Blocking depends on the
+// node only through its domain, i.e. its group: the run takes the nodes the
+// skew check alone rejected as candidates too, blocks and unblocks whole
+// domains as counts and the minimum move, and derives each pod's feasible
+// count, PodTopologySpread failures and hostname Score weight
+// (log(filtered - ignored + 2)) from the blocked nodes.  Runs of pods with a
+// normalised TaintToleration / NodeAffinity score (maxima over the feasible
+// nodes) or ignored nodes are not taken (the chain schedules them).
+
+// ReplicaArgs::ctl word 4: candidates the skew check alone rejected
+// (DoNotSchedule runs; the sorted keys hold feasible + these)
+constexpr uint32_t RUN_CTL_SKEW = 4;
+// DoNotSchedule runs track the domains' counts as offsets from the minimum
+// at the run's start: a run whose minimum or blocking threshold would move
+// past RUN_HIST offsets ends there (RUN_FULL)
+constexpr uint32_t RUN_HIST = 512;
 
 struct RunCons {
   uint32_t cz, ch;  // constraint of the other key, of kubernetes.io/hostname (MAX_SPREAD: none)
@@ -1106,15 +1126,32 @@ __global__ __launch_bounds__(SP_THREADS) void replica_keys_kernel(SpreadArgs a, 
   __syncthreads();
   const RunCons k = run_cons(s_sd, n);
   const int64_t tt_max = s_max[0], na_max = s_max[1];
-  bool ovf = false;
+  // DoNotSchedule on the other key: nodes that failed only its skew check are
+  // candidates too (they become feasible when the minimum moves); their
+  // packed score parts (the filter pass writes them for feasible nodes only)
+  // are computed here: no TaintToleration / NodeAffinity normalisation and no
+  // image records in such runs
+  const bool dns = k.cz < (uint32_t)MAX_SPREAD && !(s_sd[k.cz].flags & SP_SCORE);
+  bool ovf = false, refuse = false;
+  uint32_t nskew = 0;
   for (uint32_t pos = blockIdx.x * SP_THREADS + threadIdx.x; pos < a.npos; pos += grid_threads()) {
     const int8_t s = a.st[pos];
     const uint32_t slot = a.pos_slot[pos];
     uint64_t key = ~0ull;
-    if ((s == SST_FEASIBLE || s == SST_IGNORED) && slot != SLOT_NONE) {
+    const bool skew = dns && s == PLUGIN_SPREAD && slot != SLOT_NONE &&
+                      a.dom[(size_t)s_sd[k.cz].key * a.npos + pos] != DOM_NONE;
+    if (skew) {
+      NodeRegs g;
+      load_core(a.t, pos, slot, true, g);
+      a.part[pos] = pack_part((uint32_t)a.w.fit * (uint32_t)score_la(p, g) + (uint32_t)a.w.ba * (uint32_t)score_ba(p, g),
+                              0u, 0u);
+      ++nskew;
+    }
+    if (dns && s == SST_IGNORED) refuse = true;  // an ignored node has no domain in its group code
+    if ((s == SST_FEASIBLE || s == SST_IGNORED || skew) && slot != SLOT_NONE) {
       const uint32_t S = run_static(p, a.w, a.part[pos], tt_max, na_max);
       uint32_t code = RK_IGN;
-      if (s == SST_FEASIBLE) {
+      if (s != SST_IGNORED) {
         uint32_t dz = 0, hk = 0;
         if (k.cz < (uint32_t)MAX_SPREAD) {
           const uint32_t d = a.dom[(size_t)s_sd[k.cz].key * a.npos + pos];
@@ -1143,13 +1180,17 @@ __global__ __launch_bounds__(SP_THREADS) void replica_keys_kernel(SpreadArgs a, 
       r.val[slot] = (uint64_t)slot << 32 | pos;
     }
   }
-  if (__syncthreads_or(ovf ? 1 : 0) && threadIdx.x == 0) atomicOr(&r.ctl[1], 1u);
+  if (__syncthreads_or((ovf || refuse) ? 1 : 0) && threadIdx.x == 0) atomicOr(&r.ctl[1], 1u);
+  if (dns) {
+    nskew = wave_sum(nskew);
+    if (threadIdx.x % WAVE == 0 && nskew) atomicAdd(&r.ctl[RUN_CTL_SKEW], nskew);
+  }
 }
 
 // First sorted index of every group (feasible keys sort first).
 __global__ __launch_bounds__(SP_THREADS) void replica_groups_kernel(SpreadArgs a, ReplicaArgs r) {
   __shared__ uint32_t s_f;
-  if (threadIdx.x == 0) s_f = acc_totals(a.acc).feasible;
+  if (threadIdx.x == 0) s_f = acc_totals(a.acc).feasible + r.ctl[RUN_CTL_SKEW];  // candidates
   __syncthreads();
   const uint32_t f = s_f;
   for (uint32_t i = blockIdx.x * SP_THREADS + threadIdx.x; i < f; i += grid_threads()) {
@@ -1216,8 +1257,13 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
   __shared__ uint32_t s_cls[MAX_CLASSES];   // selector classes the pods match (commit: +1 each)
   // 0 groups, 1 refused, 2 classes, 3 RunStop, 4 taken nodes, 5-7 a head that joined them: slot,
   // position, group code, 8 the domain whose count the last commit raised (RK_DZ_NONE: none),
-  // 9-10 the head's static terms and S after its commit
-  __shared__ uint32_t s_ctl[11];
+  // 9-10 the head's static terms and S after its commit, DoNotSchedule runs: 11 the minimum's
+  // offset, 12 candidate nodes in blocked domains
+  __shared__ uint32_t s_ctl[13];
+  // DoNotSchedule runs: candidate nodes per domain; per offset above the
+  // start's minimum, eligible domains and their candidate nodes
+  __shared__ uint32_t s_nodes[RK_DZ_NONE];
+  __shared__ uint32_t s_hist[RUN_HIST], s_nhist[RUN_HIST];
   const uint32_t tid = threadIdx.x, lane = tid % WAVE, wid = tid / WAVE;
   const PodDev p = a.pods[a.pod];  // every pod of the run is identical (host-checked)
   const uint32_t n = spread_count(a, p);
@@ -1245,6 +1291,12 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
   const RunCons k = run_cons(s_sd, n);
   const uint32_t G = s_ctl[0], F = s_tot.feasible;
   const uint32_t ndz = k.cz < (uint32_t)MAX_SPREAD ? a.ndom[s_sd[k.cz].key] : 0u;
+  // DoNotSchedule on the other key: blocked while count + self - minMatch > maxSkew
+  const bool dns = k.cz < (uint32_t)MAX_SPREAD && !(s_sd[k.cz].flags & SP_SCORE);
+  const uint32_t C = F + (dns ? r.ctl[RUN_CTL_SKEW] : 0u);  // candidates (sorted keys)
+  const bool m_fixed = dns && a.acc->ndomains[k.cz] < (uint32_t)s_sd[k.cz].min_domains;  // minMatch 0
+  const uint32_t m0 = dns && !m_fixed ? a.acc->min_match[k.cz] : 0u;
+  const uint32_t d_skew = dns ? (uint32_t)s_sd[k.cz].max_skew : 0u, d_self = dns && (s_sd[k.cz].flags & SP_SELF) ? 1u : 0u;
   for (uint32_t d = tid; d < ndz; d += RUN_THREADS) {
     const uint32_t v = a.dcnt[(size_t)k.cz * a.dom_cap + d];
     s_dz[d] = v;
@@ -1271,8 +1323,10 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
   };
   const bool inc_h = k.ch < (uint32_t)MAX_SPREAD && cls_in(s_sd[k.ch].cls);
   const bool inc_z = k.cz < (uint32_t)MAX_SPREAD && cls_in(s_sd[k.cz].cls);
-  // topologyNormalizingWeight per constraint (spread_score)
-  const double w_h = k.ch < (uint32_t)MAX_SPREAD ? go_log((double)(F - s_tot.ignored) + 2.0) : 0.0;
+  // topologyNormalizingWeight per constraint (spread_score); the hostname
+  // one, log(filtered - ignored + 2), moves with the feasible count in
+  // DoNotSchedule runs (re-taken per pod there)
+  double w_h = k.ch < (uint32_t)MAX_SPREAD ? go_log((double)(F - s_tot.ignored) + 2.0) : 0.0;
   const double w_z = k.cz < (uint32_t)MAX_SPREAD ? go_log((double)a.acc->topo_size[k.cz] + 2.0) : 0.0;
   // raw Score of a group code (spread_score: the constraints in their order,
   // each adding cnt x weight + (maxSkew - 1), math.Round); at most one of
@@ -1283,7 +1337,7 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
   auto raw_of = [&](uint32_t code) -> uint32_t {
     const uint32_t dz = (code >> 8) & RK_DZ_NONE, hk = code & RK_HK_NONE;
     const bool th = k.ch < (uint32_t)MAX_SPREAD && hk != RK_HK_NONE;
-    const bool tz = k.cz < (uint32_t)MAX_SPREAD && dz != RK_DZ_NONE;
+    const bool tz = k.cz < (uint32_t)MAX_SPREAD && !dns && dz != RK_DZ_NONE;  // DoNotSchedule: no Score term
     const double xh = (double)hk * w_h + ms_h;
     const double xz = tz ? (double)s_dz[dz] * w_z + ms_z : 0.0;
     double s = 0;
@@ -1300,15 +1354,18 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
   // node and a domain count at most the largest at the start plus one per
   // pod of the run.  Otherwise the run is refused (the per-pod chain takes
   // the pods).
+  const double w_h_max = dns && k.ch < (uint32_t)MAX_SPREAD ? go_log((double)(C - s_tot.ignored) + 2.0) : w_h;
   const double raw_bound =
-      (k.ch < (uint32_t)MAX_SPREAD ? 254.0 * w_h + ms_h : 0.0) +
-      (k.cz < (uint32_t)MAX_SPREAD ? ((double)s_dzmax + (double)(r.end - a.pod)) * w_z + ms_z : 0.0);
+      (k.ch < (uint32_t)MAX_SPREAD ? 254.0 * w_h_max + ms_h : 0.0) +
+      (k.cz < (uint32_t)MAX_SPREAD && !dns ? ((double)s_dzmax + (double)(r.end - a.pod)) * w_z + ms_z : 0.0);
   const bool raw_narrow = raw_bound + 1.0 < RUN_RAW_LIMIT;
+  // no ScheduleAnyway constraint (DoNotSchedule only): PreScore skips, no Score term
+  const int64_t w_pts = dns && k.ch >= (uint32_t)MAX_SPREAD ? 0 : (int64_t)a.w_pts;
   // group tid: its first untaken sorted index (head), the head's key, position
   // and row (prefetched), the next key and position
   const bool g_on = tid < G;
   uint32_t g_i = g_on ? s_gs[tid] : 0u;
-  const uint32_t g_end = tid + 1 < G ? s_gs[tid + 1] : F;
+  const uint32_t g_end = tid + 1 < G ? s_gs[tid + 1] : C;
   // (head: key, slot << 32 | position, row; next: key, value).  The argmax
   // reads only the head's key and value, which change by register moves at a
   // win.  Every thread reloads its head's row and its next key / value at the
@@ -1333,8 +1390,35 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
   uint32_t traw = 0;
   __shared__ RunRow s_trow[RUN_TOUCHED];  // taken node t's row (its owner's; the winning head writes it)
   __shared__ double s_tinv[RUN_TOUCHED][2];  // its RN(1 / Allocatable) of cpu and memory
+  // DoNotSchedule runs: candidate nodes per domain, the domains' offsets
+  // above the minimum, the candidates in blocked domains at the start -- which
+  // must be exactly the ones the filter pass's skew check rejected
+  bool dns_bad = false;
+  if (dns) {
+    for (uint32_t d = tid; d < ndz; d += RUN_THREADS) s_nodes[d] = 0;
+    for (uint32_t i = tid; i < RUN_HIST; i += RUN_THREADS) s_hist[i] = s_nhist[i] = 0;
+    if (tid == 0) s_ctl[11] = s_ctl[12] = 0;
+    __syncthreads();
+    if (g_on && !(g_code & RK_IGN)) atomicAdd(&s_nodes[(g_code >> 8) & RK_DZ_NONE], g_end - g_i);
+    __syncthreads();
+    const uint32_t thr0 = m0 + d_skew - d_self;
+    bool bad = false;
+    for (uint32_t d = tid; d < ndz; d += RUN_THREADS) {
+      const bool elig = a.dflag[(size_t)k.cz * a.dom_cap + d] & 1u;
+      const uint32_t v = s_dz[d], nd = s_nodes[d];
+      if (nd && !elig) bad = true;  // (a feasible node is eligible under either policy)
+      if (elig && !m_fixed && v - m0 < RUN_HIST) {
+        atomicAdd(&s_hist[v - m0], 1u);
+        if (nd) atomicAdd(&s_nhist[v - m0], nd);
+      }
+      if (nd && v > thr0) atomicAdd(&s_ctl[12], nd);
+    }
+    dns_bad = __syncthreads_or(bad ? 1 : 0) != 0 || s_ctl[12] != r.ctl[RUN_CTL_SKEW];
+  }
+  const uint32_t dns_fail0 = dns ? s_tot.fail[PLUGIN_SPREAD] - r.ctl[RUN_CTL_SKEW] : 0u;  // PodTopologySpread
+                                                                                        // failures besides the skew
   uint32_t T = 0, next = a.pod, stop = RUN_END;
-  if (s_ctl[1] || !raw_narrow) {
+  if (s_ctl[1] || !raw_narrow || dns_bad) {
     stop = RUN_REFUSED;
   } else if (F == 0) {
     // no feasible node: every pod of the run gets the same FitError, nothing is committed
@@ -1385,20 +1469,45 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
     res_tpl.prefiltered = p.prefilter_out;
     res_tpl.flags = F == 1 ? 1u : 0u;  // KS_RESULT_SINGLE_FEASIBLE
     const uint32_t ncls = s_ctl[2], cls0 = ncls > 0 ? s_cls[0] : 0u, cls1 = ncls > 1 ? s_cls[1] : 0u;
+    uint32_t q_F = F;  // DoNotSchedule runs: the feasible count w_h was taken with
     for (uint32_t pod = a.pod; pod < r.end; ++pod) {
+      // DoNotSchedule runs: this pod's blocking threshold (a domain whose
+      // count exceeds it fails the skew check), feasible count and hostname
+      // Score weight (every raw moves with it)
+      uint32_t thr = 0, n_blk = 0, Fp = F;
+      bool redo = false;
+      if (dns) {
+        thr = (m_fixed ? 0u : m0 + s_ctl[11]) + d_skew - d_self;
+        n_blk = s_ctl[12];
+        Fp = C - n_blk;
+        if (Fp == 0) {  // every candidate blocked: the chain reports it (never the run's first pod)
+          stop = RUN_FIT;
+          break;
+        }
+        if (Fp != q_F) {
+          q_F = Fp;
+          if (k.ch < (uint32_t)MAX_SPREAD) {
+            w_h = go_log((double)(Fp - s_tot.ignored) + 2.0);
+            redo = true;
+          }
+        }
+      }
       // raw Scores the last commit moved; min / max raw over the non-ignored
       // feasible nodes
       const uint32_t chg = s_ctl[8];
-      const bool g_live = g_on && g_i < g_end;
+      const bool g_live = g_on && g_i < g_end && !(dns && s_dz[(g_code >> 8) & RK_DZ_NONE] > thr);
+      const bool t_live = t_on && !(dns && s_dz[(t_code >> 8) & RK_DZ_NONE] > thr);
       uint32_t mn = ~0u, mx = 0;
+      if (g_on && !(g_code & RK_IGN) && (redo || ((g_code >> 8) & RK_DZ_NONE) == chg)) graw = raw_of(g_code);
       if (g_live && !(g_code & RK_IGN)) {
-        if (((g_code >> 8) & RK_DZ_NONE) == chg) graw = raw_of(g_code);
         mn = min(mn, graw);
         mx = max(mx, graw);
       }
       if (t_on && !(t_code & RK_IGN)) {
-        if (t_dirty || ((t_code >> 8) & RK_DZ_NONE) == chg) traw = raw_of(t_code);
+        if (t_dirty || redo || ((t_code >> 8) & RK_DZ_NONE) == chg) traw = raw_of(t_code);
         t_dirty = false;
+      }
+      if (t_live && !(t_code & RK_IGN)) {
         mn = min(mn, traw);
         mx = max(mx, traw);
       }
@@ -1408,10 +1517,10 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
         auto total_of = [&](uint32_t S, uint32_t code, uint32_t raw) -> int64_t {
           uint32_t norm = 0;  // PodTopologySpread NormalizeScore: ignored -> 0, max 0 -> 100
           if (!(code & RK_IGN)) norm = pmax == 0 ? 100u : run_div32(100u * (pmax + pmin - raw), pmax, pinv);
-          return (int64_t)S + (int64_t)a.w_pts * (int64_t)norm;
+          return (int64_t)S + w_pts * (int64_t)norm;
         };
         gk = g_live ? pack_key(total_of(smask - (uint32_t)(g_key & smask), g_code, graw), (uint32_t)(g_val >> 32)) : 0ull;
-        tk = t_on ? pack_key(total_of(t_S, t_code, traw), t_slot) : 0ull;
+        tk = t_live ? pack_key(total_of(t_S, t_code, traw), t_slot) : 0ull;
       };
       // this pod's min / max raw and, with the previous pod's, the argmax: one barrier
       if (q_ok) keys(q_mn, q_mx, q_pinv);
@@ -1446,7 +1555,7 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
       // its row in registers (the node joins the taken nodes as node T: its
       // state goes to LDS and thread T adopts it after the barrier, the group's
       // next node becomes the head), or a taken node, by its owner.
-      const bool gwin = g_live && gk == b, twin = !gwin && t_on && tk == b;
+      const bool gwin = g_live && gk == b, twin = !gwin && t_live && tk == b;
       if (gwin || twin) {
         RunRow w;
         uint32_t slot, pos, code, stat;
@@ -1490,7 +1599,37 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
         if (inc_z && !(code & RK_IGN)) {
           const uint32_t dz = (code >> 8) & RK_DZ_NONE;
           moved = dz == RK_DZ_NONE ? 0u : dz;  // PreScore counts a node lacking the key in ""
-          atomicAdd(&s_dz[moved], 1u);          // (no returned value: no LDS round trip)
+          if (!dns) {
+            atomicAdd(&s_dz[moved], 1u);  // (no returned value: no LDS round trip)
+          } else {
+            // the domain's count (filtering.go: matching pods on eligible
+            // nodes), its offset above the start's minimum, the blocked
+            // candidates: the domain reaches the threshold + 1, or the last
+            // domain at the minimum moves up and the threshold with it
+            const uint32_t old = s_dz[moved], nd = s_nodes[moved];
+            s_dz[moved] = old + 1;
+            uint32_t blk = s_ctl[12], moff = s_ctl[11];
+            if (old == thr) blk += nd;
+            if (!m_fixed) {
+              const uint32_t off = old - m0;
+              if (off + 1 >= RUN_HIST) {
+                s_ctl[3] = RUN_FULL;
+              } else {
+                s_hist[off] -= 1;
+                s_hist[off + 1] += 1;
+                s_nhist[off] -= nd;
+                s_nhist[off + 1] += nd;
+                if (off == moff && s_hist[off] == 0) {
+                  ++moff;
+                  const uint32_t toff = moff + d_skew - d_self;  // the new threshold, as an offset
+                  if (toff >= RUN_HIST) s_ctl[3] = RUN_FULL;
+                  else blk -= s_nhist[toff];  // domains at the new threshold: no longer over the skew
+                }
+              }
+            }
+            s_ctl[11] = moff;
+            s_ctl[12] = blk;
+          }
         }
         s_ctl[8] = moved;
         if (fit_lost) s_ctl[3] = RUN_FIT;  // (after RUN_FULL: a Fit loss wins, as before)
@@ -1505,6 +1644,11 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
         DevResult res = res_tpl;
         res.node_index = (int32_t)slot;
         res.total_score = (int64_t)(b >> 32) - 1;
+        if (dns) {
+          res.feasible_nodes = Fp;
+          res.spread_fail = dns_fail0 + n_blk;
+          res.flags = Fp == 1 ? 1u : 0u;  // KS_RESULT_SINGLE_FEASIBLE
+        }
         a.results[pod] = res;
         const uint32_t j = gwin ? T : tid;
         s_trow[j] = w;
@@ -1627,11 +1771,14 @@ hipError_t launch_spread_reset(const SpreadArgs &a, hipStream_t st) {
 }
 
 hipError_t launch_replica_run(const SpreadArgs &a, const ReplicaArgs &r, void *sort_tmp, size_t sort_tmp_bytes,
-                              hipStream_t st) {
+                              uint32_t passes, hipStream_t st) {
   const uint32_t blocks =
       std::max<uint32_t>(1, std::min<uint32_t>((a.npos + SP_THREADS - 1) / SP_THREADS, (uint32_t)SPREAD_MAX_BLOCKS));
-  hipError_t e = hipMemsetAsync(r.ctl, 0, 4 * sizeof(uint32_t), st);
+  hipError_t e = hipMemsetAsync(r.ctl, 0, RUN_CTL_WORDS * sizeof(uint32_t), st);
   if (e != hipSuccess) return e;
+  // a DoNotSchedule constraint: its domain counts and minimum first, as the chain
+  if (passes & SPL_PREP) spread_prep_kernel<<<blocks, SP_THREADS, 0, st>>>(a);
+  if (passes & SPL_MIN) spread_min_kernel<<<blocks, SP_THREADS, 0, st>>>(a);
   spread_filter_kernel<false><<<blocks, SP_THREADS, 0, st>>>(a);
   replica_keys_kernel<<<blocks, SP_THREADS, 0, st>>>(a, r);
   size_t bytes = sort_tmp_bytes;

@@ -39,6 +39,18 @@ def replicas(app, n, req, variant="defaults", j0=0, **kw):
     elif variant == "policies":
         spread = [TSC(3, HOST, "ScheduleAnyway", sel, node_taints_policy="Honor"),
                   TSC(5, ZONE, "ScheduleAnyway", sel, node_affinity_policy="Honor", node_taints_policy="Honor")]
+    elif variant == "dns":  # DoNotSchedule on the zone (the run's filter follows the counts)
+        spread = [TSC(1, ZONE, "DoNotSchedule", sel)]
+    elif variant == "dns-host":  # ... with a ScheduleAnyway hostname term
+        spread = [TSC(1, ZONE, "DoNotSchedule", sel), TSC(2, HOST, "ScheduleAnyway", sel)]
+    elif variant == "dns-rack":
+        spread = [TSC(2, "rack", "DoNotSchedule", sel), TSC(1, HOST, "ScheduleAnyway", sel)]
+    elif variant == "dns-min":  # minDomains above the domain count: global minimum 0
+        spread = [TSC(3, ZONE, "DoNotSchedule", sel, min_domains=40)]
+    elif variant == "dns-other":  # the selector does not count the pods themselves
+        spread = [TSC(1, ZONE, "DoNotSchedule", LabelSelector({"app": "other"})), TSC(1, HOST, "ScheduleAnyway", sel)]
+    elif variant == "dns-policies":
+        spread = [TSC(2, ZONE, "DoNotSchedule", sel, node_affinity_policy="Honor", node_taints_policy="Honor")]
     else:
         raise ValueError(variant)
     return [Pod(f"{app}-{j0 + j}", containers=[Container(req)], labels={"app": app}, topology_spread=spread,
@@ -85,6 +97,45 @@ def test_replica_deployments(seed, n, zones):
                 pods.append(Pod(f"x{j}", containers=[Container({"cpu": 100})], labels={"app": app},
                                 topology_spread=dns))
                 j += 1
+        x.schedule(pods, f"seed {seed} batch {b}")
+        x.states_equal(f"seed {seed} batch {b}")
+    runs, done = counters(x)
+    assert runs > 0 and done > 0
+    x.close()
+
+
+DNS_VARIANTS = ["dns", "dns-host", "dns-rack", "dns-min", "dns-other", "dns-policies"]
+
+
+@pytest.mark.parametrize("seed,n,zones,fill", [(71, 600, 4, False), (72, 1500, 24, False), (73, 300, 3, True),
+                                               (74, 900, 7, True)])
+def test_replica_dns_deployments(seed, n, zones, fill):
+    # DoNotSchedule on a non-hostname key in replica runs: the start's skew
+    # (prefilled matching pods) blocks domains, placements unblock them (the
+    # minimum moves), nodes lacking the key are never candidates; with fill
+    # the nodes run out of pods so runs end at Fit losses and the last pods
+    # fail the spread filter or find no node
+    rng = random.Random(seed)
+    x = Pair(n)
+    nodes = rand_nodes(rng, n, zones)
+    if fill:
+        for nd in nodes:
+            nd.allocatable["pods"] = rng.choice([1, 2, 4])
+    x.upsert(nodes, list(range(n)))
+    apps = [f"app{k}" for k in range(4)] + ["other"]
+    prefill(x, rng, n, apps, n // 2)
+    ssd = {"disk": "ssd"}
+    tol = [Toleration("ded", "Equal", "x", "NoSchedule")]
+    j = 0
+    for b in range(3):
+        pods = []
+        for v in DNS_VARIANTS:
+            kw = rng.choice([{}, {}, {"node_selector": ssd}, {"tolerations": tol}])
+            app = rng.choice(apps[:4])
+            req = {"cpu": rng.randrange(1, 20) * 50, "memory": rng.randrange(1, 32) * 64 * Mi}
+            k = rng.choice([3, 5, 37, 120, 300])
+            pods += replicas(app, k, req, v, j0=j, **kw)
+            j += k
         x.schedule(pods, f"seed {seed} batch {b}")
         x.states_equal(f"seed {seed} batch {b}")
     runs, done = counters(x)
