@@ -116,10 +116,11 @@ def parse():
                          "shard: a shard's candidate lists hold up to 4 keys per block, and at tied top scores "
                          "a 125k-node shard's lists ran short with 4, DESIGN §6)")
     ap.add_argument("--kind", default="hetero", choices=["hetero", "kwok", "labeled", "zoned"])
-    ap.add_argument("--pods", default="default", choices=["default", "besteffort", "spread", "deploy", "affinity"],
+    ap.add_argument("--pods", default="default", choices=["default", "besteffort", "spread", "deploy", "deploy-dns", "affinity"],
                     help="besteffort: request-less pods (kwok/make_pods/main.go:118-148); spread: "
                          "deployment pods with PodTopologySpread constraints (use with --kind zoned); deploy: "
-                         "deployment replicas under the system default constraints (identical per deployment)")
+                         "deployment replicas under the system default constraints (identical per deployment); deploy-dns: "
+                         "the same deployments under zone maxSkew 1 DoNotSchedule + hostname ScheduleAnyway")
     ap.add_argument("--apps", type=int, default=64, help="deployments of the --pods spread stream")
     ap.add_argument("--replicas", type=int, default=256, help="replicas per deployment of the --pods deploy stream")
     ap.add_argument("--workload", default="batch", choices=["batch", "c5"],
@@ -146,7 +147,7 @@ def parse():
         a.nodes_per_lane = 2 if a.gpus > 1 else 4
     if a.prefill is None:
         a.prefill = 0.0 if a.kind == "kwok" else 0.5
-    if a.pods in ("spread", "deploy", "affinity"):  # spread path: smaller steps and CPU samples
+    if a.pods in ("spread", "deploy", "deploy-dns", "affinity"):  # spread path: smaller steps and CPU samples
         if a.batch == 50_000:
             a.batch = 2048
         a.cpu_pods = min(a.cpu_pods, 4)
@@ -274,6 +275,8 @@ def pod_stream(args, kind, n, seed):
         return synth.spread_pods(n, args.apps, seed)
     if args.pods == "deploy":
         return synth.deploy_pods(n, args.replicas, seed)
+    if args.pods == "deploy-dns":
+        return synth.deploy_dns_pods(n, args.replicas, seed)
     if args.pods == "affinity":
         return synth.affinity_pods(n, args.apps, seed)
     return synth.pods(kind, n, seed)
@@ -565,6 +568,11 @@ def workload_name(args) -> str:
                 f"deployments of {args.replicas} identical replicas under PodTopologySpread's system defaults "
                 "(hostname maxSkew 3 + zone maxSkew 5, ScheduleAnyway, selecting the deployment), every default "
                 "Filter / Score plugin, pct=100, in queue order (spread path, replica runs)")
+    if args.pods == "deploy-dns":
+        return (f"deploy-dns: {n} heterogeneous nodes in 32 zones, prefill<{f:.0%} cpu (pods of 64 apps); "
+                f"deployments of {args.replicas} identical replicas with zone maxSkew 1 DoNotSchedule + "
+                "hostname maxSkew 1 ScheduleAnyway (selecting the deployment), every default Filter / Score "
+                "plugin, pct=100, in queue order (spread path, replica runs)")
     if args.pods == "affinity":
         return (f"affinity: {n} heterogeneous nodes in 32 zones, prefill<{f:.0%} cpu (pods of 64 apps); "
                 f"pods of {args.apps} deployments with InterPodAffinity terms (half required hostname "
@@ -588,7 +596,7 @@ def workload_name(args) -> str:
 
 def pmc_key(args, world) -> str:
     """Name of the PMC summary measured for exactly this configuration."""
-    pods = {"besteffort": "-be", "spread": "-spread", "deploy": "-deploy", "affinity": "-affinity"}.get(args.pods, "")
+    pods = {"besteffort": "-be", "spread": "-spread", "deploy": "-deploy", "deploy-dns": "-deploy-dns", "affinity": "-affinity"}.get(args.pods, "")
     return (f"{args.workload}_{args.kind}{pods}_n{args.nodes}_P{args.pods_per_round}_K{args.topk or args.pods_per_round}"
             f"_npl{args.nodes_per_lane}_w{world}")
 
@@ -638,7 +646,7 @@ def roofline_deploy(args, st):
 
 
 def roofline(args, st, world):
-    if args.pods == "deploy":
+    if args.pods in ("deploy", "deploy-dns"):
         return roofline_deploy(args, st)
     if args.pods in ("spread", "affinity"):
         return roofline_spread(args, st)

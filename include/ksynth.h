@@ -55,6 +55,9 @@ ksynth *ksynth_spread_pods(uint32_t n, uint32_t n_apps, uint64_t seed);
  * deployment, kwok tolerations, hostname maxSkew 3 + zone maxSkew 5
  * ScheduleAnyway selecting app=deploy-k, spread_defaulted). */
 ksynth *ksynth_deploy_pods(uint32_t n, uint32_t replicas, uint64_t seed);
+// The same deployments under their own constraints: zone maxSkew 1
+// DoNotSchedule + hostname maxSkew 1 ScheduleAnyway.
+ksynth *ksynth_deploy_dns_pods(uint32_t n, uint32_t replicas, uint64_t seed);
 // InterPodAffinity deployment pods (ksynth.cpp): alternately required hostname
 // anti-affinity + preferred zone affinity to the own app, and preferred
 // hostname anti-affinity + required zone affinity to the next app.

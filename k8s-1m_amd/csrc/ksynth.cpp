@@ -409,7 +409,7 @@ extern "C" ksynth *ksynth_spread_pods(uint32_t n, uint32_t n_apps, uint64_t seed
 
 // Deployment replicas under the system default spread constraints (ksynth.h):
 // the replica set's pod template, so a deployment's pods are identical.
-extern "C" ksynth *ksynth_deploy_pods(uint32_t n, uint32_t replicas, uint64_t seed) {
+static ksynth *deploy_stream(uint32_t n, uint32_t replicas, uint64_t seed, bool dns) {
   auto *s = new ksynth();
   reserve_pods(s, n);
   if (replicas == 0) replicas = 1;
@@ -432,19 +432,36 @@ extern "C" ksynth *ksynth_deploy_pods(uint32_t n, uint32_t replicas, uint64_t se
     a.selector.match_labels = lab;
     a.selector.n_match_labels = 1;
     b.selector = a.selector;
-    a.topology_key = s->intern("kubernetes.io/hostname");
-    a.max_skew = 3;
-    a.when_unsatisfiable = KS_SCHEDULE_ANYWAY;
-    b.topology_key = s->intern("topology.kubernetes.io/zone");
-    b.max_skew = 5;
-    b.when_unsatisfiable = KS_SCHEDULE_ANYWAY;
-    p.spread_defaulted = 1;
+    if (dns) {  // the pod's own constraints: zone DoNotSchedule, hostname ScheduleAnyway
+      a.topology_key = s->intern("topology.kubernetes.io/zone");
+      a.max_skew = 1;
+      a.when_unsatisfiable = KS_DO_NOT_SCHEDULE;
+      b.topology_key = s->intern("kubernetes.io/hostname");
+      b.max_skew = 1;
+      b.when_unsatisfiable = KS_SCHEDULE_ANYWAY;
+    } else {  // the system defaults
+      a.topology_key = s->intern("kubernetes.io/hostname");
+      a.max_skew = 3;
+      a.when_unsatisfiable = KS_SCHEDULE_ANYWAY;
+      b.topology_key = s->intern("topology.kubernetes.io/zone");
+      b.max_skew = 5;
+      b.when_unsatisfiable = KS_SCHEDULE_ANYWAY;
+      p.spread_defaulted = 1;
+    }
     p.spread = ksynth::push(s->spread, a);
     ksynth::push(s->spread, b);
     p.n_spread = 2;
     s->pods.push_back(p);
   }
   return s;
+}
+
+extern "C" ksynth *ksynth_deploy_pods(uint32_t n, uint32_t replicas, uint64_t seed) {
+  return deploy_stream(n, replicas, seed, false);
+}
+
+extern "C" ksynth *ksynth_deploy_dns_pods(uint32_t n, uint32_t replicas, uint64_t seed) {
+  return deploy_stream(n, replicas, seed, true);
 }
 
 // Deployment pods with pod (anti-)affinity (InterPodAffinity, the one-pod

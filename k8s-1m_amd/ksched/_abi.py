@@ -335,7 +335,7 @@ KSGATHER_SYMBOLS = [
     "ksg_record", "ksg_next_fired", "ksg_set_node_order", "ksg_shutdown",
 ]
 KSYNTH_SYMBOLS = [
-    "ksynth_nodes", "ksynth_pods", "ksynth_prefill", "ksynth_besteffort_pods", "ksynth_spread_pods", "ksynth_deploy_pods", "ksynth_affinity_pods", "ksynth_node_array",
+    "ksynth_nodes", "ksynth_pods", "ksynth_prefill", "ksynth_besteffort_pods", "ksynth_spread_pods", "ksynth_deploy_pods", "ksynth_deploy_dns_pods", "ksynth_affinity_pods", "ksynth_node_array",
     "ksynth_pod_array", "ksynth_slots", "ksynth_free", "ksynth_fnv64",
 ]
 
@@ -436,6 +436,8 @@ def ksynth_lib() -> C.CDLL:
     L.ksynth_affinity_pods.argtypes = [C.c_uint32, C.c_uint32, C.c_uint64]
     L.ksynth_deploy_pods.argtypes = [C.c_uint32, C.c_uint32, C.c_uint64]
     L.ksynth_deploy_pods.restype = vp
+    L.ksynth_deploy_dns_pods.argtypes = [C.c_uint32, C.c_uint32, C.c_uint64]
+    L.ksynth_deploy_dns_pods.restype = vp
     L.ksynth_affinity_pods.restype = vp
     L.ksynth_node_array.argtypes = [vp, P(C.c_uint32)]
     L.ksynth_node_array.restype = P(KsNode)

@@ -65,6 +65,10 @@ def deploy_pods(n: int, replicas: int, seed: int) -> Synth:
     return Synth(_abi.ksynth_lib().ksynth_deploy_pods(n, replicas, seed))
 
 
+def deploy_dns_pods(n: int, replicas: int, seed: int) -> Synth:
+    return Synth(_abi.ksynth_lib().ksynth_deploy_dns_pods(n, replicas, seed))
+
+
 def affinity_pods(n: int, n_apps: int, seed: int) -> Synth:
     return Synth(_abi.ksynth_lib().ksynth_affinity_pods(n, n_apps, seed))
 

@@ -361,17 +361,19 @@ def test_spread_1m_replay():
     o.close()
 
 
-def test_deploy_1m_replay():
+@pytest.mark.parametrize("dns", [False, True])
+def test_deploy_1m_replay(dns):
     # the deploy bench's workload: deployments of 256 identical replicas under
-    # the system default spread constraints on the 1M-node zoned cluster, all
-    # in replica runs; the oracle replays every decision and
-    # schedules windows at a run's first pod, inside runs and at the end
+    # the system default spread constraints (deploy-dns: zone DoNotSchedule +
+    # hostname ScheduleAnyway) on the 1M-node zoned cluster, all in replica
+    # runs; the oracle replays every decision and schedules
+    # windows at a run's first pod, inside runs and at the end
     n_pods = 2048
     nodes = synth.nodes(synth.ZONED, N, 1)
     slots = synth.slot_array(N)
     pf = synth.prefill(synth.ZONED, N, 1, 3, 0.5)
     oracle_job = Background(lambda: build_oracle(nodes, slots, pf))  # overlaps the GPU run
-    dep = synth.deploy_pods(n_pods, 256, 5)
+    dep = (synth.deploy_dns_pods if dns else synth.deploy_pods)(n_pods, 256, 5)
     s = Scheduler(N)
     s.upsert_nodes_raw(nodes.nodes, slots, N)
     assert s.lib.ks_pods_add(s.ctx, pf.pods, pf.slot_ptr, pf.n_pods) == 0

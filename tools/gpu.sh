@@ -4,7 +4,7 @@
 # the script stops at the first failure.
 #
 #   tools/gpu.sh tests TAG [pytest -k expr]   GPU parity suite (one process) + smoke()
-#   tools/gpu.sh lines TAG "c3 c4 ..."        bench lines: c3 c4 c2 kwok kwokbe c5 spread deploy affinity
+#   tools/gpu.sh lines TAG "c3 c4 ..."        bench lines: c3 c4 c2 kwok kwokbe c5 spread deploy deploydns affinity
 #                                             (each -> gpurun_out/bench_TAG_<line>.json)
 #   tools/gpu.sh trace TAG [bench args]       rocprofv3 --kernel-trace --stats of a short bench run
 #   tools/gpu.sh pmc TAG [bench args]         PMC passes of one configuration -> gpurun_out/pmc/<key>.json
@@ -32,6 +32,8 @@ line_args() {  # bench.py arguments of a named BASELINE.json configuration
     c5) echo "--workload c5 --steps 20 --warmup 1 --no-cpu-baseline" ;;
     spread) echo "--kind zoned --pods spread --latency-calls 0" ;;
     deploy) echo "--kind zoned --pods deploy --latency-calls 0" ;;
+    deploydns) echo "--kind zoned --pods deploy-dns --latency-calls 0" ;;
+    deploydnschain) echo "--kind zoned --pods deploy-dns --latency-calls 0 --no-cpu-baseline --opt spread_replica_runs=0" ;;
     deploychain) echo "--kind zoned --pods deploy --latency-calls 0 --no-cpu-baseline --opt spread_replica_runs=0" ;;
     affinity) echo "--kind zoned --pods affinity --latency-calls 0" ;;
     proxy) echo "--nodes 125000 --no-cpu-baseline --latency-calls 0" ;;
@@ -56,7 +58,7 @@ case $JOB in
     timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1
     rc=$?; cat gpurun_out/smoke_$TAG.log; exit $rc ;;
   lines)
-    for l in ${1:-c3 c4 c2 kwok kwokbe c5 spread deploy affinity}; do
+    for l in ${1:-c3 c4 c2 kwok kwokbe c5 spread deploy deploydns affinity}; do
       args=$(line_args $l) || exit 1
       timeout -k 10 420 python -u bench.py $args > gpurun_out/bench_${TAG}_$l.json 2> gpurun_out/bench_${TAG}_$l.err
       rc=$?; echo "$l rc=$rc $(summary gpurun_out/bench_${TAG}_$l.json $l)"
