@@ -836,6 +836,36 @@ bool MatchInclusion(const SpreadConstraint &c, const PodState &st, const Node &n
   return true;
 }
 
+// Parallel node loop: parallelize.Until chunking, chunk = min(sqrt(N), N/threads + 1).
+// fn(lo, hi, thread) over [lo, hi); the reductions built on it are
+// order-independent (sums, min / max, set unions).
+void ParallelNodes(int threads, uint32_t lo, uint32_t hi, const std::function<void(uint32_t, uint32_t, int)> &fn) {
+  const uint32_t N = hi - lo;
+  if (threads <= 1 || N < 1024) {
+    fn(lo, hi, 0);
+    return;
+  }
+  uint32_t chunk = std::min<uint32_t>((uint32_t)std::sqrt((double)N), N / threads + 1);
+  if (chunk == 0) chunk = 1;
+  std::atomic<uint32_t> next{lo};
+  std::vector<std::thread> ws;
+  for (int t = 0; t < threads; ++t) {
+    ws.emplace_back([&, t] {
+      while (true) {
+        uint32_t s = next.fetch_add(chunk);
+        if (s >= hi) break;
+        fn(s, std::min(hi, s + chunk), t);
+      }
+    });
+  }
+  for (auto &w : ws) w.join();
+}
+
+template <class K>
+void MergeCounts(std::map<K, int64_t> &into, const std::map<K, int64_t> &from) {
+  for (auto &kv : from) into[kv.first] += kv.second;
+}
+
 // filtering.go#calPreFilterState: matching pods per topology value of every
 // DoNotSchedule constraint over all nodes, and the global minimum
 // (criticalPaths[0], 0 when fewer domains than minDomains).
@@ -844,19 +874,26 @@ struct SpreadFilterState {
   std::vector<int64_t> min_match;
 };
 
-SpreadFilterState SpreadPreFilter(const PodState &st, const std::vector<Node> &nodes) {
+SpreadFilterState SpreadPreFilter(const PodState &st, const std::vector<Node> &nodes, int threads) {
   SpreadFilterState s;
   const size_t nc = st.spread_filter.size();
   s.counts.resize(nc);
   s.min_match.assign(nc, 0);
-  for (auto &n : nodes) {
-    if (!n.present || !HasAllKeys(n, st.spread_filter)) continue;
-    for (size_t i = 0; i < nc; ++i) {
-      const SpreadConstraint &c = st.spread_filter[i];
-      if (!MatchInclusion(c, st, n)) continue;
-      s.counts[i][n.labels.at(c.key)] += CountPodsMatchSelector(n, c.sel, st.ns);
+  std::vector<std::vector<std::map<std::string, int64_t>>> part(threads < 1 ? 1 : threads,
+                                                                std::vector<std::map<std::string, int64_t>>(nc));
+  ParallelNodes(threads, 0, (uint32_t)nodes.size(), [&](uint32_t a, uint32_t b, int t) {
+    for (uint32_t j = a; j < b; ++j) {
+      const Node &n = nodes[j];
+      if (!n.present || !HasAllKeys(n, st.spread_filter)) continue;
+      for (size_t i = 0; i < nc; ++i) {
+        const SpreadConstraint &c = st.spread_filter[i];
+        if (!MatchInclusion(c, st, n)) continue;
+        part[t][i][n.labels.at(c.key)] += CountPodsMatchSelector(n, c.sel, st.ns);
+      }
     }
-  }
+  });
+  for (auto &q : part)
+    for (size_t i = 0; i < nc; ++i) MergeCounts(s.counts[i], q[i]);
   for (size_t i = 0; i < nc; ++i) {
     int64_t m = INT32_MAX;  // newCriticalPaths: MatchNum = math.MaxInt32
     for (auto &kv : s.counts[i]) m = std::min(m, kv.second);
@@ -890,14 +927,18 @@ struct IpaFilterState {
   std::map<TopoPair, int64_t> existing_anti, aff, anti;
 };
 
-IpaFilterState IpaPreFilter(const PodState &st, const std::vector<Node> &nodes) {
+IpaFilterState IpaPreFilter(const PodState &st, const std::vector<Node> &nodes, int threads) {
   IpaFilterState s;
   const auto &req_aff = st.ipa[KS_POD_AFFINITY_REQUIRED], &req_anti = st.ipa[KS_POD_ANTI_AFFINITY_REQUIRED];
   // getIncomingAffinityAntiAffinityCounts visits every node only for a pod
   // with required terms; getExistingAntiAffinityCounts only the nodes with
   // pods carrying required anti-affinity
   const bool incoming = !req_aff.empty() || !req_anti.empty();
-  for (auto &n : nodes) {
+  std::vector<IpaFilterState> part(threads < 1 ? 1 : threads);
+  ParallelNodes(threads, 0, (uint32_t)nodes.size(), [&](uint32_t a, uint32_t b, int th) {
+  IpaFilterState &s = part[th];
+  for (uint32_t j = a; j < b; ++j) {
+    const Node &n = nodes[j];
     if (!n.present || (!incoming && n.pods_with_req_anti == 0)) continue;
     for (auto &e : n.pod_recs) {
       if (!incoming && e.terms.empty()) continue;
@@ -919,6 +960,12 @@ IpaFilterState IpaPreFilter(const PodState &st, const std::vector<Node> &nodes) 
         if (it != n.labels.end()) s.anti[{t.key, it->second}] += 1;
       }
     }
+  }
+  });
+  for (auto &q : part) {
+    MergeCounts(s.existing_anti, q.existing_anti);
+    MergeCounts(s.aff, q.aff);
+    MergeCounts(s.anti, q.anti);
   }
   s.active = !(s.existing_anti.empty() && req_aff.empty() && req_anti.empty());  // else PreFilter Skip
   return s;
@@ -1082,27 +1129,8 @@ struct oracle {
     n.pods += sign;
   }
 
-  // Parallel node loop: parallelize.Until chunking, chunk = min(sqrt(N), N/threads + 1).
   void for_nodes(uint32_t lo, uint32_t hi, const std::function<void(uint32_t, uint32_t, int)> &fn) const {
-    const uint32_t N = hi - lo;
-    if (threads <= 1 || N < 1024) {
-      fn(lo, hi, 0);
-      return;
-    }
-    uint32_t chunk = std::min<uint32_t>((uint32_t)std::sqrt((double)N), N / threads + 1);
-    if (chunk == 0) chunk = 1;
-    std::atomic<uint32_t> next{lo};
-    std::vector<std::thread> ws;
-    for (int t = 0; t < threads; ++t) {
-      ws.emplace_back([&, t] {
-        while (true) {
-          uint32_t s = next.fetch_add(chunk);
-          if (s >= hi) break;
-          fn(s, std::min(hi, s + chunk), t);
-        }
-      });
-    }
-    for (auto &w : ws) w.join();
+    ParallelNodes(threads, lo, hi, fn);
   }
 
   // PodTopologySpread PreScore / Score / NormalizeScore (scoring.go) over the
@@ -1116,20 +1144,35 @@ struct oracle {
     std::vector<char> ignored(N, 0);
     int64_t n_filtered = 0, n_ignored = 0;
     // initPreScoreState: topology values of the filtered (feasible) nodes
+    struct Part {
+      int64_t filtered = 0, ignored = 0, mn = INT64_MAX, mx = 0;
+      std::vector<std::map<std::string, int64_t>> counts;
+    };
+    std::vector<Part> part(threads < 1 ? 1 : threads);
+    for (auto &q : part) q.counts.resize(nc);
+    for_nodes(0, N, [&](uint32_t a, uint32_t b, int t) {
+      Part &q = part[t];
+      for (uint32_t i = a; i < b; ++i) {
+        if (!nodes[i].present || ev[i].status >= 0) continue;
+        ++q.filtered;
+        if (requireAll && !HasAllKeys(nodes[i], cs)) {
+          ignored[i] = 1;
+          ++q.ignored;
+          continue;
+        }
+        for (size_t c = 0; c < nc; ++c) {
+          if (cs[c].hostname) continue;
+          auto it = nodes[i].labels.find(cs[c].key);
+          q.counts[c].emplace(it == nodes[i].labels.end() ? std::string() : it->second, 0);
+        }
+      }
+    });
     std::vector<std::map<std::string, int64_t>> counts(nc);
-    for (uint32_t i = 0; i < N; ++i) {
-      if (!nodes[i].present || ev[i].status >= 0) continue;
-      ++n_filtered;
-      if (requireAll && !HasAllKeys(nodes[i], cs)) {
-        ignored[i] = 1;
-        ++n_ignored;
-        continue;
-      }
-      for (size_t c = 0; c < nc; ++c) {
-        if (cs[c].hostname) continue;
-        auto it = nodes[i].labels.find(cs[c].key);
-        counts[c].emplace(it == nodes[i].labels.end() ? std::string() : it->second, 0);
-      }
+    for (auto &q : part) {
+      n_filtered += q.filtered;
+      n_ignored += q.ignored;
+      for (size_t c = 0; c < nc; ++c) MergeCounts(counts[c], q.counts[c]);
+      for (auto &m : q.counts) m.clear();
     }
     std::vector<double> weight(nc);
     for (size_t c = 0; c < nc; ++c) {
@@ -1137,33 +1180,45 @@ struct oracle {
       weight[c] = GoLog((double)(sz + 2));  // topologyNormalizingWeight
     }
     // PreScore processAllNode: matching pods of every node in a filtered domain
-    for (uint32_t i = 0; i < N; ++i) {
-      const Node &n = nodes[i];
-      if (!n.present) continue;
-      if (requireAll && !HasAllKeys(n, cs)) continue;
-      for (size_t c = 0; c < nc; ++c) {
-        if (cs[c].hostname || !MatchInclusion(cs[c], st, n)) continue;
-        auto it = n.labels.find(cs[c].key);
-        auto d = counts[c].find(it == n.labels.end() ? std::string() : it->second);
-        if (d == counts[c].end()) continue;
-        d->second += CountPodsMatchSelector(n, cs[c].sel, st.ns);
+    for_nodes(0, N, [&](uint32_t a, uint32_t b, int t) {
+      Part &q = part[t];
+      for (uint32_t i = a; i < b; ++i) {
+        const Node &n = nodes[i];
+        if (!n.present) continue;
+        if (requireAll && !HasAllKeys(n, cs)) continue;
+        for (size_t c = 0; c < nc; ++c) {
+          if (cs[c].hostname || !MatchInclusion(cs[c], st, n)) continue;
+          auto it = n.labels.find(cs[c].key);
+          const std::string &v = it == n.labels.end() ? std::string() : it->second;
+          if (!counts[c].count(v)) continue;
+          q.counts[c][v] += CountPodsMatchSelector(n, cs[c].sel, st.ns);
+        }
       }
-    }
+    });
+    for (auto &q : part)
+      for (size_t c = 0; c < nc; ++c) MergeCounts(counts[c], q.counts[c]);
     // Score: Σ cnt * weight + (maxSkew - 1), math.Round; NormalizeScore: min / max
-    int64_t mn = INT64_MAX, mx = 0;
-    for (uint32_t i = 0; i < N; ++i) {
-      if (!nodes[i].present || ev[i].status >= 0 || ignored[i]) continue;
-      const Node &n = nodes[i];
-      double score = 0;
-      for (size_t c = 0; c < nc; ++c) {
-        auto it = n.labels.find(cs[c].key);
-        if (it == n.labels.end()) continue;
-        const int64_t cnt = cs[c].hostname ? CountPodsMatchSelector(n, cs[c].sel, st.ns) : counts[c].at(it->second);
-        score += (double)cnt * weight[c] + (double)(cs[c].max_skew - 1);  // scoreForCount
+    for_nodes(0, N, [&](uint32_t a, uint32_t b, int t) {
+      Part &q = part[t];
+      for (uint32_t i = a; i < b; ++i) {
+        if (!nodes[i].present || ev[i].status >= 0 || ignored[i]) continue;
+        const Node &n = nodes[i];
+        double score = 0;
+        for (size_t c = 0; c < nc; ++c) {
+          auto it = n.labels.find(cs[c].key);
+          if (it == n.labels.end()) continue;
+          const int64_t cnt = cs[c].hostname ? CountPodsMatchSelector(n, cs[c].sel, st.ns) : counts[c].at(it->second);
+          score += (double)cnt * weight[c] + (double)(cs[c].max_skew - 1);  // scoreForCount
+        }
+        ev[i].pts_raw = (int64_t)std::round(score);
+        q.mn = std::min(q.mn, ev[i].pts_raw);
+        q.mx = std::max(q.mx, ev[i].pts_raw);
       }
-      ev[i].pts_raw = (int64_t)std::round(score);
-      mn = std::min(mn, ev[i].pts_raw);
-      mx = std::max(mx, ev[i].pts_raw);
+    });
+    int64_t mn = INT64_MAX, mx = 0;
+    for (auto &q : part) {
+      mn = std::min(mn, q.mn);
+      mx = std::max(mx, q.mx);
     }
     for (uint32_t i = 0; i < N; ++i) {
       if (!nodes[i].present || ev[i].status >= 0) continue;
@@ -1184,7 +1239,10 @@ struct oracle {
     // scoring.go#PreScore: without preferred terms of its own only the pods
     // with affinity (HavePodsWithAffinityList, NodeInfo.PodsWithAffinity) count
     const bool own = !st.ipa[KS_POD_AFFINITY_PREFERRED].empty() || !st.ipa[KS_POD_ANTI_AFFINITY_PREFERRED].empty();
-    for (uint32_t i = 0; i < N; ++i) {
+    std::vector<std::map<std::string, std::map<std::string, int64_t>>> part(threads < 1 ? 1 : threads);
+    for_nodes(0, N, [&](uint32_t a, uint32_t b, int th) {
+    auto &ts = part[th];
+    for (uint32_t i = a; i < b; ++i) {
       const Node &n = nodes[i];
       if (!n.present || n.labels.empty() || (!own && n.pods_with_affinity == 0)) continue;
       auto add = [&](const AffTerm &t, int64_t w) {
@@ -1205,6 +1263,9 @@ struct oracle {
         }
       }
     }
+    });
+    for (auto &q : part)
+      for (auto &kv : q) MergeCounts(ts[kv.first], kv.second);
     if (ts.empty()) return;  // PreScore Skip: every score stays 0
     int64_t mn = INT64_MAX, mx = INT64_MIN;
     for (uint32_t i = 0; i < N; ++i) {
@@ -1237,8 +1298,8 @@ struct oracle {
     const uint32_t N = (uint32_t)nodes.size();
     ev.resize(N);
     SpreadFilterState sf;
-    if (!st.spread_filter.empty()) sf = SpreadPreFilter(st, nodes);
-    const IpaFilterState af = IpaPreFilter(st, nodes);
+    if (!st.spread_filter.empty()) sf = SpreadPreFilter(st, nodes, threads);
+    const IpaFilterState af = IpaPreFilter(st, nodes, threads);
     // Filter + raw scores in parallel (findNodesThatPassFilters / RunScorePlugins
     // both fan out with parallelize.Until); counts and normaliser maxima are
     // order-independent reductions, combined from per-thread partials.
@@ -1417,8 +1478,8 @@ int32_t oracle_plugin_scores(oracle *o, const ks_pod *pod, ks_node_score *out) {
   std::vector<oracle::Eval> ev(N);
   int64_t tt_max = 0, na_max = 0;
   SpreadFilterState sf;
-  if (!st.spread_filter.empty()) sf = SpreadPreFilter(st, o->nodes);
-  const IpaFilterState af = IpaPreFilter(st, o->nodes);
+  if (!st.spread_filter.empty()) sf = SpreadPreFilter(st, o->nodes, o->threads);
+  const IpaFilterState af = IpaPreFilter(st, o->nodes, o->threads);
   for (uint32_t i = 0; i < N; ++i) {
     if (!o->nodes[i].present) {
       ev[i].status = -2;
