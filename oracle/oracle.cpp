@@ -1002,6 +1002,20 @@ bool IpaFilter(const PodState &st, const IpaFilterState &s, const Node &n) {
   return true;
 }
 
+// schedule_one.go#numFeasibleNodesToFind (minFeasibleNodesToFind 100,
+// minFeasibleNodesPercentageToFind 5; int32 arithmetic, exact for any
+// node count below 2^31 / 100)
+int64_t NumFeasibleNodesToFind(int32_t pct, int64_t n) {
+  if (n < 100) return n;
+  int64_t p = pct;
+  if (p == 0) {
+    p = 50 - n / 125;
+    if (p < 5) p = 5;
+  }
+  const int64_t k = n * p / 100;
+  return k < 100 ? 100 : k;
+}
+
 inline uint64_t PackKey(int64_t total, uint32_t slot) {
   return ((uint64_t)(total + 1) << 32) | (uint64_t)(0xFFFFFFFFu - slot);
 }
@@ -1050,6 +1064,9 @@ struct oracle {
   }
   int64_t w_fit, w_ba, w_tt, w_na, w_il, w_pts = 2, w_ipa = 2, hard_weight = 1;
   int threads = 1;
+  int32_t pct = 100;        // percentageOfNodesToScore
+  uint64_t next_start = 0;  // Scheduler.nextStartNodeIndex
+  static constexpr int kNotVisited = 1000;  // ev[i].status of a node the window skipped
 
   struct Eval {
     int status;
@@ -1290,6 +1307,42 @@ struct oracle {
     }
   }
 
+  // findNodesThatPassFilters with percentageOfNodesToScore < 100
+  // (schedule_one.go:findNodesThatFitPod / findNodesThatPassFilters /
+  // numFeasibleNodesToFind), restated sequentially: upstream checks nodes with
+  // parallelize.Until and keeps the first numNodesToFind that report feasible,
+  // which with parallelism > 1 depends on goroutine timing; with one worker
+  // it is this loop.  The node list is the present nodes in slot order
+  // (upstream: the snapshot's list order), without the nodes a NodeAffinity
+  // PreFilterResult excludes (upstream visits only the PreFilterResult's
+  // nodes; they keep their KS_FAIL_PREFILTER_RESULT status here, never
+  // visited).  Visiting starts at nextStartNodeIndex % len(list) and goes
+  // round the list; the worker cancels at the (k+1)-th feasible node, so the
+  // processed nodes (len(feasibleNodes) + len(NodeToStatus)) are the nodes
+  // before it: k feasible and the infeasible ones between them.  Fewer than
+  // k+1 feasible: every node is processed.  nextStartNodeIndex = (it +
+  // processed) % len(allNodes).  Nodes after the window get kNotVisited.
+  void window() {
+    const uint32_t N = (uint32_t)nodes.size();
+    std::vector<uint32_t> list;
+    for (uint32_t i = 0; i < N; ++i)
+      if (nodes[i].present && ev[i].status != KS_FAIL_PREFILTER_RESULT) list.push_back(i);
+    const uint64_t nl = list.size();
+    const int64_t k = NumFeasibleNodesToFind(pct, (int64_t)nl);
+    uint64_t processed = nl;
+    if (nl) {
+      const uint64_t s = next_start % nl;
+      int64_t found = 0;
+      for (uint64_t j = 0; j < nl; ++j)
+        if (ev[list[(s + j) % nl]].status < 0 && ++found == k + 1) {
+          processed = j;
+          break;
+        }
+      for (uint64_t j = processed; j < nl; ++j) ev[list[(s + j) % nl]].status = kNotVisited;
+    }
+    if (n_present) next_start = (next_start + processed) % (uint64_t)n_present;
+  }
+
   // schedulePod (schedule_one.go): findNodesThatFitPod -> prioritizeNodes -> selectHost.
   ks_result schedule_one(const ks_pod &p) {
     ks_result r{};
@@ -1310,11 +1363,15 @@ struct oracle {
       uint64_t best = 0;
     };
     std::vector<Part> part(threads < 1 ? 1 : threads);
+    for_nodes(0, N, [&](uint32_t a, uint32_t b, int) {
+      for (uint32_t i = a; i < b; ++i)
+        if (nodes[i].present) ev[i] = eval(st, nodes[i], &sf, &af);
+    });
+    if (pct != 100) window();
     for_nodes(0, N, [&](uint32_t a, uint32_t b, int t) {
       Part &q = part[t];
       for (uint32_t i = a; i < b; ++i) {
-        if (!nodes[i].present) continue;
-        ev[i] = eval(st, nodes[i], &sf, &af);
+        if (!nodes[i].present || ev[i].status == kNotVisited) continue;
         ++q.evaluated;
         if (ev[i].status >= 0) {
           q.fail[ev[i].status]++;
@@ -1396,6 +1453,12 @@ void oracle_set_weight_inter_pod_affinity(oracle *o, int32_t w, int32_t hard) {
   o->w_ipa = w;
   o->hard_weight = hard;
 }
+void oracle_set_percentage(oracle *o, int32_t pct) {
+  o->pct = pct;
+  o->next_start = 0;
+}
+uint64_t oracle_next_start(const oracle *o) { return o->next_start; }
+int64_t oracle_num_feasible_nodes_to_find(int32_t pct, int64_t n) { return NumFeasibleNodesToFind(pct, n); }
 double oracle_go_log(double x) { return GoLog(x); }
 
 int32_t oracle_nodes_upsert(oracle *o, const ks_node *nodes, const uint32_t *slots, uint32_t n) {

@@ -36,6 +36,14 @@ void oracle_set_threads(oracle *o, int32_t threads);
 void oracle_set_weight_spread(oracle *o, int32_t w);
 /* InterPodAffinity score weight (2) and hardPodAffinityWeight (1). */
 void oracle_set_weight_inter_pod_affinity(oracle *o, int32_t w, int32_t hard);
+/* KubeSchedulerProfile.percentageOfNodesToScore (default 100; 0 = adaptive).
+ * Below 100 each pod visits the node list from nextStartNodeIndex and stops
+ * at numFeasibleNodesToFind feasible nodes (schedule_one.go; see oracle.cpp
+ * window()).  Resets nextStartNodeIndex to 0. */
+void oracle_set_percentage(oracle *o, int32_t pct);
+uint64_t oracle_next_start(const oracle *o); /* nextStartNodeIndex */
+/* schedule_one.go#numFeasibleNodesToFind */
+int64_t oracle_num_feasible_nodes_to_find(int32_t pct, int64_t num_all_nodes);
 
 int32_t oracle_nodes_upsert(oracle *o, const ks_node *nodes, const uint32_t *slots, uint32_t n);
 int32_t oracle_nodes_delete(oracle *o, const uint32_t *slots, uint32_t n);

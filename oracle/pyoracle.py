@@ -53,6 +53,12 @@ def lib() -> C.CDLL:
     L.oracle_set_weight_spread.restype = None
     L.oracle_set_weight_inter_pod_affinity.argtypes = [vp, C.c_int32, C.c_int32]
     L.oracle_set_weight_inter_pod_affinity.restype = None
+    L.oracle_set_percentage.argtypes = [vp, C.c_int32]
+    L.oracle_set_percentage.restype = None
+    L.oracle_next_start.argtypes = [vp]
+    L.oracle_next_start.restype = C.c_uint64
+    L.oracle_num_feasible_nodes_to_find.argtypes = [C.c_int32, C.c_int64]
+    L.oracle_num_feasible_nodes_to_find.restype = C.c_int64
     L.oracle_nodes_upsert.argtypes = [vp, P(_abi.KsNode), P(C.c_uint32), C.c_uint32]
     L.oracle_nodes_delete.argtypes = [vp, P(C.c_uint32), C.c_uint32]
     L.oracle_pods_add.argtypes = [vp, P(_abi.KsPod), P(C.c_uint32), C.c_uint32]
@@ -75,7 +81,7 @@ def lib() -> C.CDLL:
 
 
 class Oracle:
-    def __init__(self, capacity: int, weights=(1, 1, 3, 2, 1, 2), threads: int = 1):
+    def __init__(self, capacity: int, weights=(1, 1, 3, 2, 1, 2), threads: int = 1, percentage: int = 100):
         self.L = lib()
         self.o = self.L.oracle_new(capacity, *weights[:5])
         if len(weights) > 5:
@@ -83,6 +89,13 @@ class Oracle:
         self.capacity = capacity
         if threads > 1:
             self.L.oracle_set_threads(self.o, threads)
+        if percentage != 100:
+            self.L.oracle_set_percentage(self.o, percentage)
+
+    @property
+    def next_start(self) -> int:
+        """Scheduler.nextStartNodeIndex (percentageOfNodesToScore < 100)."""
+        return int(self.L.oracle_next_start(self.o))
 
     def close(self):
         if self.o:
