@@ -122,6 +122,10 @@ def parse():
                          "deployment replicas under the system default constraints (identical per deployment); deploy-dns: "
                          "the same deployments under zone maxSkew 1 DoNotSchedule + hostname ScheduleAnyway")
     ap.add_argument("--apps", type=int, default=64, help="deployments of the --pods spread stream")
+    ap.add_argument("--pct", type=int, default=100,
+                    help="percentageOfNodesToScore (100: every node; the reference's deployed profile uses 5, "
+                         "terraform/kubernetes/dist-scheduler.tf:562): below 100 every pod takes the one-pod chain "
+                         "with the window pass (DESIGN.md §5.8)")
     ap.add_argument("--replicas", type=int, default=256, help="replicas per deployment of the --pods deploy stream")
     ap.add_argument("--workload", default="batch", choices=["batch", "c5"],
                     help="batch: one batch of --batch pods per step; c5: one burst + its event log per step")
@@ -147,7 +151,7 @@ def parse():
         a.nodes_per_lane = 2 if a.gpus > 1 else 4
     if a.prefill is None:
         a.prefill = 0.0 if a.kind == "kwok" else 0.5
-    if a.pods in ("spread", "deploy", "deploy-dns", "affinity"):  # spread path: smaller steps and CPU samples
+    if a.pods in ("spread", "deploy", "deploy-dns", "affinity") or a.pct != 100:  # one-pod path: smaller steps
         if a.batch == 50_000:
             a.batch = 2048
         a.cpu_pods = min(a.cpu_pods, 4)
@@ -234,7 +238,8 @@ def main():
     t_setup = time.time()
     options = {k: int(v) for k, v in (o.split("=", 1) for o in args.opt)}
     sched = Scheduler(args.nodes, device=local_rank if world > 1 else 0, pods_per_round=args.pods_per_round,
-                      topk=args.topk, nodes_per_lane=args.nodes_per_lane, world_size=world, rank=rank, options=options)
+                      topk=args.topk, nodes_per_lane=args.nodes_per_lane, world_size=world, rank=rank, options=options,
+                      percentage_of_nodes_to_score=args.pct)
     if world > 1:
         sched.comm_init(exchange_unique_id(rank, world))
         if rank == 0:  # ncclCommInitRank returned: every rank has read the id
@@ -552,6 +557,14 @@ def run_c5(args, kind, sched, world, rank, t_setup):
 # ------------------------------------------------------------------ report
 
 def workload_name(args) -> str:
+    name = base_workload_name(args)
+    if args.pct != 100:
+        name = name.replace("pct=100", f"percentageOfNodesToScore={args.pct} (every pod on the one-pod chain with "
+                                       "the window pass, DESIGN §5.8)")
+    return name
+
+
+def base_workload_name(args) -> str:
     n, f = args.nodes, args.prefill
     if args.workload == "c5":
         return (f"C5: {n} heterogeneous nodes, prefill<50% cpu; bursts of {args.burst} resource-only pods, "
@@ -597,6 +610,8 @@ def workload_name(args) -> str:
 def pmc_key(args, world) -> str:
     """Name of the PMC summary measured for exactly this configuration."""
     pods = {"besteffort": "-be", "spread": "-spread", "deploy": "-deploy", "deploy-dns": "-deploy-dns", "affinity": "-affinity"}.get(args.pods, "")
+    if args.pct != 100:
+        pods += f"-pct{args.pct}"
     return (f"{args.workload}_{args.kind}{pods}_n{args.nodes}_P{args.pods_per_round}_K{args.topk or args.pods_per_round}"
             f"_npl{args.nodes_per_lane}_w{world}")
 
@@ -648,7 +663,7 @@ def roofline_deploy(args, st):
 def roofline(args, st, world):
     if args.pods in ("deploy", "deploy-dns"):
         return roofline_deploy(args, st)
-    if args.pods in ("spread", "affinity"):
+    if args.pods in ("spread", "affinity") or args.pct != 100:
         return roofline_spread(args, st)
     labeled = args.kind == "labeled"
     sweep_avg_ms = st.sweep_ms / max(1, st.sweep_launches)
@@ -797,7 +812,7 @@ def cpu_baseline(args, nodes, slots, pre, pods):
     import pyoracle
 
     def timed(threads, n):
-        o = pyoracle.Oracle(args.nodes, threads=threads)
+        o = pyoracle.Oracle(args.nodes, threads=threads, percentage=args.pct)
         o.upsert(nodes.nodes, slots, args.nodes)
         if pre is not None:
             o.add_pods(pre.pods, pre.slot_ptr, pre.n_pods)

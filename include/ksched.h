@@ -381,12 +381,16 @@ typedef struct {
   int32_t weight_affinity;   /* NodeAffinity                                    */
   int32_t weight_image;      /* ImageLocality                                   */
   /* (weight_topology_spread: after percentage_of_nodes_to_score) */
-  /* KubeSchedulerProfile.percentageOfNodesToScore.  100 (the default here and
-   * the reference's dist-scheduler/deployment.yaml:95) scores every node; any
-   * other value (0 = upstream's adaptive 50 - N/125, the published run's 5 at
-   * terraform/kubernetes/dist-scheduler.tf:562) makes ks_open return
-   * KS_ERR_UNSUPPORTED: upstream's early stop is order- and parallelism-
-   * dependent (schedule_one.go#numFeasibleNodesToFind / findNodesThatPassFilters). */
+  /* KubeSchedulerProfile.percentageOfNodesToScore, 0..100.  100 (the default
+   * here and the reference's dist-scheduler/deployment.yaml:95) scores every
+   * node.  Below 100 (0 = upstream's adaptive 50 - N/125; the published run's
+   * 5 at terraform/kubernetes/dist-scheduler.tf:562) each pod visits the node
+   * list (present nodes in slot order) from nextStartNodeIndex and stops at
+   * numFeasibleNodesToFind feasible nodes, as upstream's findNodesThatPassFilters
+   * does with one worker (schedule_one.go; with more workers upstream's set
+   * depends on goroutine timing); nextStartNodeIndex advances by the nodes
+   * processed (ks_next_start_index).  Every pod then takes the one-pod chain.
+   * Below 100 with world_size > 1 or virtual_shards > 1: KS_ERR_UNSUPPORTED. */
   int32_t percentage_of_nodes_to_score;
   int32_t weight_topology_spread; /* PodTopologySpread (default profile: 2)     */
   int32_t weight_inter_pod_affinity; /* InterPodAffinity (default profile: 2)    */
@@ -632,6 +636,9 @@ ks_status ks_set_sync_timeout(ks_ctx *ctx, uint32_t ms);
  * stream done, 2 round resolved, 3 FIX sweep done) by `usec` microseconds of
  * bounded device-side waiting, then signals as usual. */
 ks_status ks_debug_stall(ks_ctx *ctx, uint32_t flag, uint32_t usec);
+/* Scheduler.nextStartNodeIndex (percentageOfNodesToScore < 100; 0 otherwise),
+ * after the submitted batches. */
+ks_status ks_next_start_index(ks_ctx *ctx, uint64_t *out);
 /* Batch runs the context has started (the worker took their selector-class
  * masks and table view); returns at once, without waiting for submitted
  * batches -- tests order a ks_batch_prepare after a submitted run's start. */

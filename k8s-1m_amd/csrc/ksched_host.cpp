@@ -492,6 +492,12 @@ struct ks_ctx {
   uint32_t dom_cap = 0;
   SpreadAcc *d_acc = nullptr;
   int8_t *d_sst = nullptr;
+  // percentageOfNodesToScore < 100: every pod takes the one-pod
+  // chain with a window pass; d_win [WIN_WORDS] (0: nextStartNodeIndex),
+  // d_win_st [cap] list / feasible bytes of the probe pass
+  int32_t pct = 100;
+  uint32_t *d_win = nullptr;
+  uint8_t *d_win_st = nullptr;
   int64_t *d_sraw = nullptr;
   uint64_t *d_spart = nullptr;
   // replica runs: sort keys and positions, group starts, control
@@ -1816,6 +1822,10 @@ ks_status spread_alloc(ks_ctx *c) {
       (st = dalloc(c, &c->d_acc, 1)) || (st = dalloc(c, &c->d_sst, c->npos)) || (st = dalloc(c, &c->d_sraw, c->npos)) ||
       (st = dalloc(c, &c->d_spart, c->npos)) || (st = dalloc(c, &c->d_sraw2, c->npos)))
     return st;
+  if (c->pct != 100) {
+    if ((st = dalloc(c, &c->d_win, WIN_WORDS + 2 * ((size_t)c->cap + 4095) / 4096)) || (st = dalloc(c, &c->d_win_st, ((size_t)c->cap + 15) & ~(size_t)15)))
+      return st;
+  }
   c->d_cnt = c->d_dom + (size_t)MAX_TOPO_KEYS * c->npos;
   HIPC(c, hipMemsetAsync(c->d_dom, 0xFF, (size_t)MAX_TOPO_KEYS * c->npos * 4, c->stream));
   std::vector<uint32_t> ps(c->npos, SLOT_NONE);
@@ -2155,7 +2165,7 @@ bool matched_by_terms(ks_ctx *c, const ks_pod &p) {
 // Whether compiling the pod may create one-pod-path state (columns, label
 // bits, device buffers): ks_batch_prepare drains the submitted batches first.
 bool may_need_solo(ks_ctx *c, const ks_pod &p) {
-  if (p.n_spread || p.n_affinity_terms) return true;
+  if (p.n_spread || p.n_affinity_terms || c->pct != 100) return true;
   if (matched_by_terms(c, p)) return true;
   for (uint32_t i = 0; i < p.n_containers; ++i)
     if (p.containers[i].n_extended || (!c->images.empty() && p.containers[i].image && p.containers[i].image[0]))
@@ -2355,7 +2365,8 @@ ks_status solo_compile(ks_ctx *c, const ks_pod &p, PodDev &d, ProgBuf &cl, bool 
   if (p.n_affinity_terms || c->n_terms) {
     if ((st = ipa_compile(c, p, create, refs, &aff, &aff_flags))) return st;
   }
-  if (!p.n_spread && xr.empty() && imgs.empty() && aff.empty()) return KS_OK;
+  // (percentageOfNodesToScore < 100: every pod takes the chain, which holds the window pass)
+  if (!p.n_spread && xr.empty() && imgs.empty() && aff.empty() && c->pct == 100) return KS_OK;
   // multi-rank contexts run the one-pod path replicated: every rank holds the
   // whole node table and every commit, so each rank's chain over
   // all positions gives the same result with no exchange
@@ -3201,6 +3212,13 @@ ks_status run_batch(ks_ctx *c, ks_batch *b) {
       sa.w_pts = c->cfg.weight_topology_spread;
       sa.w_ipa = c->cfg.weight_inter_pod_affinity;
       sa.evaluated = c->n_present;
+      if (c->pct != 100) {
+        sa.win = c->d_win;
+        sa.win_st = c->d_win_st;
+        sa.nslots = c->cap;
+        sa.win_mode = 2;
+        sa.pct = c->pct;
+      }
       // one pod through the per-pod chain
       auto chain = [&](uint32_t i) -> ks_status {
         sa.pod = i;
@@ -3224,7 +3242,7 @@ ks_status run_batch(ks_ctx *c, ks_batch *b) {
       while (hi < b->n && b->spread[hi]) {
         // replica run: pod hi and the identical pods after it
         uint32_t e = hi + 1;
-        if (c->replica_runs && b->rep[hi] && hi >= chain_until)
+        if (c->replica_runs && c->pct == 100 && b->rep[hi] && hi >= chain_until)
           while (e < b->n && (b->rep[e] & 2)) ++e;
         if (e - hi >= RUN_MIN_PODS && replica_fits(c, b, sa, hi)) {
           uint32_t next = hi, stop = RUN_END;
@@ -3397,9 +3415,10 @@ ks_status ks_open(const ks_config *cfg, ks_ctx **out) {
   for (int32_t w : {cfg->weight_fit, cfg->weight_balanced, cfg->weight_taint, cfg->weight_affinity, cfg->weight_image,
                     cfg->weight_topology_spread, cfg->weight_inter_pod_affinity, cfg->hard_pod_affinity_weight})
     if (w < 0 || w > 10000) return KS_ERR_INVALID;
-  // percentageOfNodesToScore (ksched.h): only 100 (every node) is modelled
+  // percentageOfNodesToScore (ksched.h): below 100 on one GPU shard only
   if (cfg->percentage_of_nodes_to_score < 0 || cfg->percentage_of_nodes_to_score > 100) return KS_ERR_INVALID;
-  if (cfg->percentage_of_nodes_to_score != 100) return KS_ERR_UNSUPPORTED;
+  if (cfg->percentage_of_nodes_to_score != 100 && c->S > 1) return KS_ERR_UNSUPPORTED;
+  c->pct = cfg->percentage_of_nodes_to_score;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return KS_ERR_DEVICE;
   if (cfg->device < 0 || cfg->device >= ndev) return KS_ERR_DEVICE;
@@ -3593,7 +3612,7 @@ void ks_close(ks_ctx *c) {
                   c->d_counters, c->d_crow, c->d_cext, c->d_pipe, c->d_carry, c->d_flags, c->d_dom, c->d_dedup,
                   c->d_pos_slot, c->d_dcnt, c->d_dflag, c->d_acc, c->d_sst, c->d_sraw, c->d_spart,
                   c->d_xalloc, c->d_tcnt, c->d_adcnt, c->d_sraw2, c->d_rk_keys, c->d_rk_sorted, c->d_rk_val,
-                  c->d_rk_sval, c->d_rk_gstart, c->d_rk_ctl, c->d_rk_tmp, c->d_rk_prof};
+                  c->d_rk_sval, c->d_rk_gstart, c->d_rk_ctl, c->d_rk_tmp, c->d_rk_prof, c->d_win, c->d_win_st};
   for (void *b : bufs)
     if (b) (void)hipFree(b);
   if (c->h_start) (void)hipHostFree(c->h_start);
@@ -4771,6 +4790,18 @@ ks_status ks_set_sync_timeout(ks_ctx *c, uint32_t ms) {
   if (!c || ms == 0) return KS_ERR_INVALID;
   if (ks_status dst_ = drain_async(c)) return dst_;
   c->sync_timeout_ms = ms;
+  return KS_OK;
+}
+
+ks_status ks_next_start_index(ks_ctx *c, uint64_t *out) {
+  if (!c || !out) return KS_ERR_INVALID;
+  *out = 0;
+  if (c->pct == 100 || !c->d_win) return KS_OK;
+  if (ks_status dst_ = drain_async(c)) return dst_;
+  uint32_t v = 0;
+  ks_status st;
+  if ((st = xfer_begin(c, 64, 0)) || (st = d2h(c, &v, c->d_win, sizeof v)) || (st = xfer_sync(c))) return st;
+  *out = v;
   return KS_OK;
 }
 

@@ -144,7 +144,19 @@ struct SpreadArgs {
   Weights w;
   int32_t w_pts, w_ipa;
   uint32_t evaluated;         // present nodes
+  // percentageOfNodesToScore < 100 (ksched_spread.hip spread_window_kernel):
+  // win_mode 0 off, 1 the probe filter pass (writes win_st only), 2 the
+  // filter pass over the window; win_st [nslots] bit 0 in the node list, bit 1
+  // feasible; win [WIN_WORDS] 0 nextStartNodeIndex, 1 the window's first slot,
+  // 2 its end slot (exclusive, round the list), 3 every node visited, then
+  // [2 per 4096-slot chunk] the chunk's list / feasible counts
+  uint32_t *win;
+  uint8_t *win_st;
+  uint32_t nslots;
+  uint32_t win_mode;
+  int32_t pct;
 };
+constexpr uint32_t WIN_WORDS = 4;
 
 // Replica runs (ksched_spread.hip): consecutive identical pods
 // whose constraints are ScheduleAnyway (at most one kubernetes.io/hostname and

@@ -598,7 +598,23 @@ __global__ __launch_bounds__(SP_THREADS) void spread_filter_kernel(SpreadArgs a)
   uint32_t fails[RF] = {0, 0, 0, 0, 0, 0, 0};
   uint32_t feasible = 0, ignored = 0, tt_max = 0, na_max = 0;
   uint64_t ipa_mn = ~0ull, ipa_mx = 0;
+  // percentageOfNodesToScore < 100: the probe pass (filter only, win_st) or
+  // the pass over the window spread_window_kernel found
+  const bool probe = a.win_mode == 1, windowed = a.win_mode == 2;
+  const uint32_t w_s0 = windowed ? a.win[1] : 0u, w_x = windowed ? a.win[2] : 0u;
+  const bool w_all = !windowed || a.win[3] != 0;
+  // the window pass of a pod that reads nothing from the nodes outside the
+  // window (no PreScore counts, no per-node topologyScore records) skips them
+  // before loading their rows
+  const bool w_skip = windowed && !w_all && !any_s && !node_score;
   for (uint32_t pos = blockIdx.x * SP_THREADS + threadIdx.x; pos < a.npos; pos += grid_threads()) {
+    if (w_skip) {
+      const uint32_t sl = a.pos_slot[pos];
+      if (sl != SLOT_NONE && !(w_s0 < w_x ? sl >= w_s0 && sl < w_x : sl >= w_s0 || sl < w_x)) {
+        a.st[pos] = SST_EMPTY;
+        continue;
+      }
+    }
     PosIn in;
     AffView av{s_aoff, s_h, {}, {}};
     if (AFF) aff_prefetch(a, ad, na, pos, av);
@@ -609,9 +625,10 @@ __global__ __launch_bounds__(SP_THREADS) void spread_filter_kernel(SpreadArgs a)
     pos_regs(a, pos, in, r);
     if (!(r.bits & 1u)) {
       a.st[pos] = SST_EMPTY;
+      if (probe) a.win_st[slot] = 0;
       continue;
     }
-    if (node_score)
+    if (node_score && !probe)
       for (uint32_t q = 0; q < na; ++q)
         if ((ad[q].kind & (AF_KIND | AF_NODE)) == (AF_SCORE | AF_NODE) && aff_dom(a, ad, av, q, pos) != DOM_NONE &&
             aff_sum(a, ad, av, q, pos, 0))
@@ -621,7 +638,7 @@ __global__ __launch_bounds__(SP_THREADS) void spread_filter_kernel(SpreadArgs a)
     bool all_s = true;
     for (uint32_t c = 0; c < n; ++c)
       if ((sd[c].flags & SP_SCORE) && pos_dom(a, sd, in, c, pos) == DOM_NONE) all_s = false;
-    if (any_s && (!allkeys || all_s)) {
+    if (any_s && (!allkeys || all_s) && !probe) {
       // PreScore counts (scoring.go#PreScore processAllNode) of this node
       const bool aff_ok = !aff_needed || !(p.flags & PF_AFF) || required_match(p, a.clauses, e, slot);
       const bool taint_ok = !taint_needed || (e.hard & ~p.tol_hard & ~UNSCHED_BIT) == 0;
@@ -637,6 +654,13 @@ __global__ __launch_bounds__(SP_THREADS) void spread_filter_kernel(SpreadArgs a)
         if (s_off[c] != SP_OFF_NONE) atomicAdd(&s_h[s_off[c] + d], k);
         else atomicAdd(&a.dcnt[(size_t)c * a.dom_cap + d], k);
       }
+    }
+    // percentageOfNodesToScore < 100: a node outside the visited window is
+    // neither filtered nor counted (its PreScore counts above are: upstream's
+    // PreScore walks every node)
+    if (windowed && !(w_all || (w_s0 < w_x ? slot >= w_s0 && slot < w_x : slot >= w_s0 || slot < w_x))) {
+      a.st[pos] = SST_EMPTY;
+      continue;
     }
     int s = filter<true>(p, a.clauses, r, e);
     if (s == ST_FEASIBLE) {
@@ -665,6 +689,10 @@ __global__ __launch_bounds__(SP_THREADS) void spread_filter_kernel(SpreadArgs a)
       }
     }
     if (s == ST_FEASIBLE && ipa_filter && !ipa_fits(a, ad, na, av, pos, ipa_first_ok)) s = PLUGIN_IPA;
+    if (probe) {  // the node list (PreFilterResult nodes) and the feasible nodes, by slot
+      a.win_st[slot] = (uint8_t)((s != ST_PREFILTERED ? 1u : 0u) | (s == ST_FEASIBLE ? 2u : 0u));
+      continue;
+    }
     int8_t out = (int8_t)s;
     if (s == ST_FEASIBLE) {
       ++feasible;
@@ -708,6 +736,7 @@ __global__ __launch_bounds__(SP_THREADS) void spread_filter_kernel(SpreadArgs a)
     }
     a.st[pos] = out;
   }
+  if (probe) return;  // (uniform: no barrier below is skipped by part of the block)
   // block reduction: counts, maxima
   uint32_t v[R_N];
 #pragma unroll
@@ -835,6 +864,175 @@ __global__ __launch_bounds__(SP_THREADS) void spread_score_kernel(SpreadArgs a) 
     }
     if (mn != ~0ull) atomicMin((unsigned long long *)&acc_shard(a).pts_min, (unsigned long long)mn);
     if (mx) atomicMax((unsigned long long *)&acc_shard(a).pts_max, (unsigned long long)mx);
+  }
+}
+
+// ---------------------------------------------------------------- window
+// percentageOfNodesToScore < 100 (schedule_one.go#numFeasibleNodesToFind,
+// findNodesThatFitPod, findNodesThatPassFilters; restated sequentially as
+// oracle.cpp window()).  The probe filter pass has written
+// every slot's byte: bit 0 the node is in the list (present, not excluded by
+// a NodeAffinity PreFilterResult), bit 1 it passes every filter.  Visiting
+// starts at the list node of rank nextStartNodeIndex % len(list) and goes
+// round the list in slot order; it stops at the (k+1)-th feasible node, k =
+// numFeasibleNodesToFind(pct, len(list)): the window is the nodes before it,
+// k feasible ones and the infeasible ones among them (fewer than k + 1
+// feasible: every node).  nextStartNodeIndex += processed, modulo the present
+// nodes.  One workgroup: per-thread counts over a contiguous slot range, a
+// block scan, then the two threads whose ranges hold the start rank and the
+// stopping rank walk them.
+constexpr int WIN_THREADS = 1024;
+constexpr uint32_t WIN_CHUNK = 4096;  // slots per count of spread_wcount_kernel
+
+__device__ __forceinline__ int64_t num_feasible_to_find(int32_t pct, int64_t n) {
+  if (n < 100) return n;  // minFeasibleNodesToFind
+  int64_t q = pct;
+  if (q == 0) q = max<int64_t>(50 - n / 125, 5);  // adaptive, minFeasibleNodesPercentageToFind
+  const int64_t k = n * q / 100;
+  return k < 100 ? 100 : k;
+}
+
+__device__ __forceinline__ uint32_t byte_bits(uint32_t w, uint32_t bit) {
+  return (uint32_t)__popc(w & (0x01010101u << bit));
+}
+
+// Exclusive block prefix sums of two counts, and their block totals (every
+// thread); sx / sy: WIN_THREADS / WAVE words of LDS each.  Ends with a barrier
+// after its last LDS read, so the next call may reuse them.
+__device__ __forceinline__ void block_scan2(uint32_t x, uint32_t y, uint32_t &ex, uint32_t &ey, uint32_t &tx,
+                                            uint32_t &ty, uint32_t *sx, uint32_t *sy) {
+  const uint32_t lane = threadIdx.x % WAVE, wid = threadIdx.x / WAVE;
+  uint32_t ix = x, iy = y;
+#pragma unroll
+  for (int o = 1; o < WAVE; o <<= 1) {
+    const uint32_t u = __shfl_up(ix, o), v = __shfl_up(iy, o);
+    if (lane >= (uint32_t)o) {
+      ix += u;
+      iy += v;
+    }
+  }
+  if (lane == WAVE - 1) {
+    sx[wid] = ix;
+    sy[wid] = iy;
+  }
+  __syncthreads();
+  ex = ix - x;
+  ey = iy - y;
+  tx = ty = 0;
+  for (uint32_t w = 0; w < WIN_THREADS / WAVE; ++w) {
+    const uint32_t u = sx[w], v = sy[w];
+    if (w < wid) {
+      ex += u;
+      ey += v;
+    }
+    tx += u;
+    ty += v;
+  }
+  __syncthreads();
+}
+
+// The list / feasible counts of every WIN_CHUNK-slot chunk of win_st, into
+// win[WIN_WORDS + 2 c] / [WIN_WORDS + 2 c + 1]: 16 bytes per thread.
+__global__ __launch_bounds__(WIN_CHUNK / 16) void spread_wcount_kernel(SpreadArgs a) {
+  __shared__ uint32_t s_c[WIN_CHUNK / 16 / WAVE][2];
+  const uint32_t ns = a.nslots, j = blockIdx.x * WIN_CHUNK + threadIdx.x * 16;
+  uint32_t cl = 0, cf = 0;
+  if (j + 16 <= ns) {
+    const uint4 v = *reinterpret_cast<const uint4 *>(a.win_st + j);
+    cl = byte_bits(v.x, 0) + byte_bits(v.y, 0) + byte_bits(v.z, 0) + byte_bits(v.w, 0);
+    cf = byte_bits(v.x, 1) + byte_bits(v.y, 1) + byte_bits(v.z, 1) + byte_bits(v.w, 1);
+  } else {
+    for (uint32_t i = j; i < ns && i < j + 16; ++i) {
+      cl += a.win_st[i] & 1u;
+      cf += (a.win_st[i] >> 1) & 1u;
+    }
+  }
+  cl = wave_sum(cl);
+  cf = wave_sum(cf);
+  if (threadIdx.x % WAVE == 0) {
+    s_c[threadIdx.x / WAVE][0] = cl;
+    s_c[threadIdx.x / WAVE][1] = cf;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    uint32_t v = 0;
+    for (int w = 0; w < WIN_CHUNK / 16 / WAVE; ++w) v += s_c[w][threadIdx.x];
+    a.win[WIN_WORDS + 2 * blockIdx.x + threadIdx.x] = v;
+  }
+}
+
+__global__ __launch_bounds__(WIN_THREADS) void spread_window_kernel(SpreadArgs a) {
+  __shared__ uint32_t s_sx[WIN_THREADS / WAVE], s_sy[WIN_THREADS / WAVE];
+  __shared__ uint32_t s_x[8];
+  const uint32_t t = threadIdx.x;
+  const uint32_t ns = a.nslots, nch = (ns + WIN_CHUNK - 1) / WIN_CHUNK;
+  const uint32_t cpt = (nch + WIN_THREADS - 1) / WIN_THREADS;  // chunks per thread
+  const uint32_t c_lo = min(nch, t * cpt), c_hi = min(nch, c_lo + cpt);
+  const uint32_t *cc = a.win + WIN_WORDS;
+  uint32_t cl = 0, cf = 0;  // list / feasible nodes of the thread's chunks
+  for (uint32_t c = c_lo; c < c_hi; ++c) {
+    cl += cc[2 * c];
+    cf += cc[2 * c + 1];
+  }
+  uint32_t pl, pf, nl, nf;
+  block_scan2(cl, cf, pl, pf, nl, nf, s_sx, s_sy);
+  const int64_t k = num_feasible_to_find(a.pct, (int64_t)nl);
+  const uint32_t next = a.win[0];
+  const bool all = (int64_t)nf <= k;  // block-uniform
+  uint32_t s0 = 0, x = 0, processed = nl;
+  const uint8_t *b = a.win_st;
+  // The slot of the node of rank `want` among the nodes whose bit `bit` is
+  // set (and the other bit's count before it): the one thread whose chunks
+  // hold it finds the chunk, then the whole workgroup walks that chunk, a
+  // byte per thread per step, with block scans.
+  auto find = [&](uint32_t want, uint32_t bit, uint32_t *out) {
+    const uint32_t p_mine = bit ? pf : pl, c_mine = bit ? cf : cl;
+    if (want >= p_mine && want < p_mine + c_mine) {
+      uint32_t al = pl, af = pf, c = c_lo;
+      for (; c + 1 < c_hi; ++c) {
+        const uint32_t nl_c = cc[2 * c], nf_c = cc[2 * c + 1];
+        if ((bit ? af + nf_c : al + nl_c) > want) break;
+        al += nl_c;
+        af += nf_c;
+      }
+      s_x[4] = c;
+      s_x[5] = al;
+      s_x[6] = af;
+    }
+    __syncthreads();
+    const uint32_t base = s_x[4] * WIN_CHUNK, end = min(ns, base + WIN_CHUNK);
+    uint32_t al = s_x[5], af = s_x[6];  // counts before the step
+    for (uint32_t off = base; off < end; off += WIN_THREADS) {
+      const uint32_t j = off + t;
+      const uint32_t v = j < end ? b[j] : 0u;
+      uint32_t el, ef, tl, tf;
+      block_scan2(v & 1u, (v >> 1) & 1u, el, ef, tl, tf, s_sx, s_sy);
+      const uint32_t r = bit ? af + ef : al + el;
+      if (((v >> bit) & 1u) && r == want) {
+        out[0] = j;
+        out[1] = bit ? al + el : af + ef;  // the other count before the node
+      }
+      al += tl;
+      af += tf;
+    }
+    __syncthreads();
+  };
+  if (!all) {
+    const uint32_t s = next % nl;
+    find(s, 0, s_x);  // the start node: its slot, the feasible nodes before it
+    s0 = s_x[0];
+    const uint32_t f0 = s_x[1], after = nf - f0;  // feasible nodes at or after the start slot
+    // slot-order rank of the (k+1)-th feasible node in list order
+    const uint32_t target = (int64_t)after >= k + 1 ? f0 + (uint32_t)k : (uint32_t)k - after;
+    find(target, 1, s_x + 2);  // the stopping node: its slot, its list rank
+    x = s_x[2];
+    processed = (s_x[3] + nl - s) % nl;
+  }
+  if (t == 0) {
+    a.win[1] = s0;
+    a.win[2] = x;
+    a.win[3] = all ? 1u : 0u;
+    if (a.evaluated) a.win[0] = (uint32_t)(((uint64_t)next + processed) % a.evaluated);  // % len(allNodes)
   }
 }
 
@@ -983,6 +1181,11 @@ __global__ void spread_commit_kernel(SpreadArgs a) {
   r.total_score = 0;
   r.feasible_nodes = tot.feasible;
   r.evaluated_nodes = a.evaluated;
+  if (a.win_mode) {  // the visited nodes and the PreFilterResult's exclusions
+    uint32_t v = tot.feasible + p.prefilter_out;
+    for (int q = 0; q < NFILT + 2; ++q) v += tot.fail[q];
+    r.evaluated_nodes = v;
+  }
   for (int q = 0; q < NFILT; ++q) r.fail_counts[q] = tot.fail[q];
   r.spread_fail = tot.fail[PLUGIN_SPREAD];
   r.ipa_fail = tot.fail[PLUGIN_IPA];
@@ -1755,6 +1958,14 @@ hipError_t launch_spread_pod(const SpreadArgs &args, uint32_t passes, hipStream_
   const SpreadArgs &a = args;
   if (passes & SPL_PREP) spread_prep_kernel<<<blocks, SP_THREADS, 0, st>>>(a);
   if (passes & SPL_MIN) spread_min_kernel<<<blocks, SP_THREADS, 0, st>>>(a);
+  if (a.win_mode) {  // percentageOfNodesToScore < 100: probe, window, then the pass over the window
+    SpreadArgs pr = a;
+    pr.win_mode = 1;
+    if (passes & SPL_AFF) spread_filter_kernel<true><<<blocks, SP_THREADS, 0, st>>>(pr);
+    else spread_filter_kernel<false><<<blocks, SP_THREADS, 0, st>>>(pr);
+    spread_wcount_kernel<<<(a.nslots + WIN_CHUNK - 1) / WIN_CHUNK, WIN_CHUNK / 16, 0, st>>>(a);
+    spread_window_kernel<<<1, WIN_THREADS, 0, st>>>(a);
+  }
   if (passes & SPL_AFF) spread_filter_kernel<true><<<blocks, SP_THREADS, 0, st>>>(a);
   else spread_filter_kernel<false><<<blocks, SP_THREADS, 0, st>>>(a);
   if (passes & SPL_SCORE) spread_score_kernel<<<blocks, SP_THREADS, 0, st>>>(a);

@@ -328,7 +328,7 @@ KSCHED_SYMBOLS = [
     "ks_batch_results", "ks_batch_free", "ks_batch_submit", "ks_batch_wait", "ks_pods_check", "ks_plugin_scores", "ks_node_states", "ks_comm_unique_id", "ks_comm_init_local", "ks_snapshot_update",
     "ks_comm_init", "ks_comm_allreduce_max", "ks_get_stats", "ks_reset_stats", "ks_set_timing",
     "ks_debug_counters", "ks_debug_set_profile", "ks_debug_resolve_profile", "ks_debug_round_record", "ks_set_sync_timeout", "ks_debug_stall", "ks_batch_marks",
-    "ks_debug_runs_started",
+    "ks_debug_runs_started", "ks_next_start_index",
 ]
 KSGATHER_SYMBOLS = [
     "ksg_open", "ksg_close", "ksg_set_members", "ksg_record_and_wait", "ksg_pending", "ksg_fnv1_32", "ksg_target_index",
@@ -407,6 +407,7 @@ def ksched_lib() -> C.CDLL:
     L.ks_set_sync_timeout.argtypes = [vp, C.c_uint32]
     L.ks_debug_stall.argtypes = [vp, C.c_uint32, C.c_uint32]
     L.ks_debug_runs_started.argtypes = [vp, P(C.c_uint64)]
+    L.ks_next_start_index.argtypes = [vp, P(C.c_uint64)]
     L.ks_batch_marks.argtypes = [vp, vp, P(C.c_uint8)]
     for f in KSCHED_SYMBOLS:
         fn = getattr(L, f)

@@ -117,10 +117,12 @@ class Scheduler:
 
     def __init__(self, node_capacity: int, *, device: int = 0, pods_per_round: int = 256, topk: int = 0,
                  nodes_per_lane: int = 4, world_size: int = 1, rank: int = 0, virtual_shards: int = 1,
-                 weights: Optional[Dict[str, int]] = None, options: Optional[Dict[str, int]] = None):
+                 weights: Optional[Dict[str, int]] = None, options: Optional[Dict[str, int]] = None,
+                 percentage_of_nodes_to_score: int = 100):
         """options: ks_config execution options by field name (_abi.OPTION_FIELDS),
         e.g. {"resolve_mode": _abi.RESOLVE_SERIAL, "dedup_identical_pods": 0};
-        none of them changes a result."""
+        none of them changes a result.  percentage_of_nodes_to_score: the
+        profile's percentageOfNodesToScore (ksched.h; below 100 one shard only)."""
         self.lib = _abi.ksched_lib()
         cfg = _abi.KsConfig()
         self.lib.ks_config_default(C.byref(cfg))
@@ -145,6 +147,7 @@ class Scheduler:
         cfg.weight_topology_spread = w["PodTopologySpread"]
         cfg.weight_inter_pod_affinity = w["InterPodAffinity"]
         cfg.hard_pod_affinity_weight = 1
+        cfg.percentage_of_nodes_to_score = percentage_of_nodes_to_score
         self.weights = w
         self.capacity = node_capacity
         self.ctx = C.c_void_p()
@@ -154,6 +157,12 @@ class Scheduler:
         self.names: Dict[int, str] = {}
         self.slots: Dict[str, int] = {}
         self.slot_gen: Dict[int, int] = {}  # last NodeInfo.Generation applied per slot (snapshot_update)
+
+    def next_start_index(self) -> int:
+        """Scheduler.nextStartNodeIndex (percentageOfNodesToScore < 100)."""
+        v = C.c_uint64()
+        _check(self.lib, self.ctx, self.lib.ks_next_start_index(self.ctx, C.byref(v)))
+        return int(v.value)
 
     # ------------------------------------------------------------ lifecycle
     def close(self):

@@ -32,6 +32,7 @@ line_args() {  # bench.py arguments of a named BASELINE.json configuration
     c5) echo "--workload c5 --steps 20 --warmup 1 --no-cpu-baseline" ;;
     spread) echo "--kind zoned --pods spread --latency-calls 0" ;;
     deploy) echo "--kind zoned --pods deploy --latency-calls 0" ;;
+    pct5) echo "--pct 5 --latency-calls 0" ;;
     deploydns) echo "--kind zoned --pods deploy-dns --latency-calls 0" ;;
     deploydnschain) echo "--kind zoned --pods deploy-dns --latency-calls 0 --no-cpu-baseline --opt spread_replica_runs=0" ;;
     deploychain) echo "--kind zoned --pods deploy --latency-calls 0 --no-cpu-baseline --opt spread_replica_runs=0" ;;
@@ -58,7 +59,7 @@ case $JOB in
     timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1
     rc=$?; cat gpurun_out/smoke_$TAG.log; exit $rc ;;
   lines)
-    for l in ${1:-c3 c4 c2 kwok kwokbe c5 spread deploy deploydns affinity}; do
+    for l in ${1:-c3 c4 c2 kwok kwokbe c5 spread deploy deploydns affinity pct5}; do
       args=$(line_args $l) || exit 1
       timeout -k 10 420 python -u bench.py $args > gpurun_out/bench_${TAG}_$l.json 2> gpurun_out/bench_${TAG}_$l.err
       rc=$?; echo "$l rc=$rc $(summary gpurun_out/bench_${TAG}_$l.json $l)"
