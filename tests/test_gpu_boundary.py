@@ -5,7 +5,8 @@
   scheduled approximately: host ports (NodePorts), topology spread the caller
   could not express, pod (anti-)affinity (InterPodAffinity), volumes, a
   nominated node, resource claims; any batch while a bound pod carries pod
-  (anti-)affinity; percentageOfNodesToScore != 100 at ks_open.
+  (anti-)affinity; percentageOfNodesToScore below 100 with more than one shard
+  at ks_open (below 100 on one shard runs the window pass).
 * A batch that resolved node names goes stale when the node set changes.
 * ks_batch_submit / ks_batch_wait give the results of sequential ks_batch_run
   calls, with the next batch compiled while the previous one runs.
@@ -76,14 +77,17 @@ def test_bound_pod_with_pod_affinity_blocks_batches_until_removed():
         assert s.lib.ks_pods_check(s.ctx, pa, 1, st) == 0
 
 
-@pytest.mark.parametrize("pct,status", [(100, 0), (5, _abi.KS_ERR_UNSUPPORTED), (0, _abi.KS_ERR_UNSUPPORTED),
-                                        (101, _abi.KS_ERR_INVALID)])
-def test_percentage_of_nodes_to_score(pct, status):
+# below 100: the window pass on one shard (tests/test_gpu_pct.py);
+# with more than one shard refused
+@pytest.mark.parametrize("pct,shards,status", [(100, 1, 0), (5, 1, 0), (0, 1, 0), (5, 2, _abi.KS_ERR_UNSUPPORTED),
+                                               (101, 1, _abi.KS_ERR_INVALID), (-1, 1, _abi.KS_ERR_INVALID)])
+def test_percentage_of_nodes_to_score(pct, shards, status):
     lib = _abi.ksched_lib()
     cfg = _abi.KsConfig()
     lib.ks_config_default(C.byref(cfg))
     assert cfg.percentage_of_nodes_to_score == 100
     cfg.node_capacity = 16
+    cfg.virtual_shards = shards
     cfg.percentage_of_nodes_to_score = pct
     ctx = C.c_void_p()
     assert lib.ks_open(C.byref(cfg), C.byref(ctx)) == status
