@@ -38,6 +38,7 @@ line_args() {  # bench.py arguments of a named BASELINE.json configuration
     deploychain) echo "--kind zoned --pods deploy --latency-calls 0 --no-cpu-baseline --opt spread_replica_runs=0" ;;
     affinity) echo "--kind zoned --pods affinity --latency-calls 0" ;;
     proxy) echo "--nodes 125000 --no-cpu-baseline --latency-calls 0" ;;
+    c4proxy) echo "--nodes 125000 --kind labeled --no-cpu-baseline --latency-calls 0" ;;
     *) echo "unknown line $1" >&2; return 1 ;;
   esac
 }
