@@ -1448,6 +1448,10 @@ __device__ __forceinline__ RunRow run_row(const SpreadArgs &a, uint32_t pos) {
   return w;
 }
 
+// DNS: the run's other-key constraint is DoNotSchedule (a template
+// parameter: the ScheduleAnyway runs compile without the blocking code,
+// which costs them registers and ~1k cycles per pod)
+template <bool DNS>
 __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, ReplicaArgs r) {
   __shared__ SpreadDev s_sd[MAX_SPREAD];
   __shared__ Totals s_tot;
@@ -1495,7 +1499,8 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
   const uint32_t G = s_ctl[0], F = s_tot.feasible;
   const uint32_t ndz = k.cz < (uint32_t)MAX_SPREAD ? a.ndom[s_sd[k.cz].key] : 0u;
   // DoNotSchedule on the other key: blocked while count + self - minMatch > maxSkew
-  const bool dns = k.cz < (uint32_t)MAX_SPREAD && !(s_sd[k.cz].flags & SP_SCORE);
+  constexpr bool dns = DNS;
+  const bool dns_prog = k.cz < (uint32_t)MAX_SPREAD && !(s_sd[k.cz].flags & SP_SCORE);  // must equal DNS
   const uint32_t C = F + (dns ? r.ctl[RUN_CTL_SKEW] : 0u);  // candidates (sorted keys)
   const bool m_fixed = dns && a.acc->ndomains[k.cz] < (uint32_t)s_sd[k.cz].min_domains;  // minMatch 0
   const uint32_t m0 = dns && !m_fixed ? a.acc->min_match[k.cz] : 0u;
@@ -1621,7 +1626,7 @@ __global__ __launch_bounds__(RUN_THREADS) void replica_run_kernel(SpreadArgs a, 
   const uint32_t dns_fail0 = dns ? s_tot.fail[PLUGIN_SPREAD] - r.ctl[RUN_CTL_SKEW] : 0u;  // PodTopologySpread
                                                                                         // failures besides the skew
   uint32_t T = 0, next = a.pod, stop = RUN_END;
-  if (s_ctl[1] || !raw_narrow || dns_bad) {
+  if (s_ctl[1] || !raw_narrow || dns_bad || dns_prog != DNS) {
     stop = RUN_REFUSED;
   } else if (F == 0) {
     // no feasible node: every pod of the run gets the same FitError, nothing is committed
@@ -1997,7 +2002,8 @@ hipError_t launch_replica_run(const SpreadArgs &a, const ReplicaArgs &r, void *s
       hipSuccess)
     return e;
   replica_groups_kernel<<<blocks, SP_THREADS, 0, st>>>(a, r);
-  replica_run_kernel<<<1, RUN_THREADS, 0, st>>>(a, r);
+  if (passes & SPL_MIN) replica_run_kernel<true><<<1, RUN_THREADS, 0, st>>>(a, r);  // DoNotSchedule (SPL_MIN)
+  else replica_run_kernel<false><<<1, RUN_THREADS, 0, st>>>(a, r);
   return launch_spread_reset(a, st);
 }
 
