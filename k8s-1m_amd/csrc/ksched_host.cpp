@@ -1813,6 +1813,9 @@ ks_status spread_scratch(ks_ctx *c, uint32_t need) {
   return KS_OK;
 }
 
+// slots per list / feasible count of the window pass (ksched_spread.hip WIN_CHUNK)
+constexpr size_t WIN_CHUNK_SLOTS = 1024;
+
 ks_status spread_alloc(ks_ctx *c) {
   if (c->d_dom) return KS_OK;
   if (c->undrained) return KS_NEED_DRAIN;
@@ -1823,7 +1826,7 @@ ks_status spread_alloc(ks_ctx *c) {
       (st = dalloc(c, &c->d_spart, c->npos)) || (st = dalloc(c, &c->d_sraw2, c->npos)))
     return st;
   if (c->pct != 100) {
-    if ((st = dalloc(c, &c->d_win, WIN_WORDS + 2 * ((size_t)c->cap + 4095) / 4096)) || (st = dalloc(c, &c->d_win_st, ((size_t)c->cap + 15) & ~(size_t)15)))
+    if ((st = dalloc(c, &c->d_win, WIN_WORDS + 2 * (((size_t)c->cap + WIN_CHUNK_SLOTS - 1) / WIN_CHUNK_SLOTS))) || (st = dalloc(c, &c->d_win_st, ((size_t)c->cap + 15) & ~(size_t)15)))
       return st;
   }
   c->d_cnt = c->d_dom + (size_t)MAX_TOPO_KEYS * c->npos;

@@ -882,7 +882,9 @@ __global__ __launch_bounds__(SP_THREADS) void spread_score_kernel(SpreadArgs a) 
 // block scan, then the two threads whose ranges hold the start rank and the
 // stopping rank walk them.
 constexpr int WIN_THREADS = 1024;
-constexpr uint32_t WIN_CHUNK = 4096;  // slots per count of spread_wcount_kernel
+// slots per count of spread_wcount_kernel (one walk step of the window);
+// ksched_host.cpp sizes win[] with the same value (WIN_CHUNK_SLOTS)
+constexpr uint32_t WIN_CHUNK = 1024;
 
 __device__ __forceinline__ int64_t num_feasible_to_find(int32_t pct, int64_t n) {
   if (n < 100) return n;  // minFeasibleNodesToFind
