@@ -6,10 +6,10 @@
 # Python whose first preloaded library is the ASan runtime; libksched's
 # host-thread protocols (ksched_sync.hpp: rendezvous, run queue, thread pool)
 # through tools/sync_stress.cpp under both.  Log:
-# profiles/r5/sanitize/sanitize.log; exits non-zero on any report.
+# profiles/r6/sanitize/sanitize.log; exits non-zero on any report.
 set -o pipefail
 R=$(cd "$(dirname "$0")/.." && pwd)
-OUT=${SANITIZE_OUT:-$R/profiles/r5/sanitize}
+OUT=${SANITIZE_OUT:-$R/profiles/r6/sanitize}
 mkdir -p "$OUT"
 LOG=$OUT/sanitize.log
 : > "$LOG"
