@@ -18,7 +18,7 @@ from ksched import Scheduler
 from ksched.objects import (Container, Node, NodeSelectorRequirement, NodeSelectorTerm, Pod, PreferredSchedulingTerm,
                             Taint, Toleration)
 from spread_cases import HOST, ZONE
-from test_gpu_spread import Pair, rand_ipa_pod, rand_nodes
+from test_gpu_spread import Pair, rand_ipa_pod, rand_nodes, rand_res_nodes, rand_res_pod
 
 pytestmark = pytest.mark.gpu
 
@@ -100,6 +100,48 @@ def test_pct_windows_through_full_nodes():
     x.states_equal("fill")
     x.check_start("fill")
     assert (r["status"] == 1).any() and (r["evaluated"] == n).any() and (r["evaluated"] < n).any()
+    x.close()
+
+
+def test_pct_images_and_extended_resources():
+    # ImageLocality (image states over the present nodes) and extended /
+    # ephemeral resources on the one-pod chain with the window
+    rng = random.Random(88)
+    n = 1200
+    x = PctPair(n, 10)
+    x.upsert(rand_res_nodes(rng, n), list(range(n)))
+    for b in range(3):
+        pods = [rand_res_pod(rng, b * 1000 + j) for j in range(80)]
+        x.schedule(pods, f"res batch {b}")
+        x.states_equal(f"res batch {b}")
+        x.check_start(f"res batch {b}")
+    x.close()
+
+
+def test_pct_batches_in_flight():
+    # ks_batch_submit with the next batch compiled while one runs: the window
+    # state (nextStartNodeIndex) lives on the device and carries from batch to
+    # batch in submission order; results equal the oracle's sequential ones
+    from ksched.objects import pods_array
+    rng = random.Random(89)
+    n = 2000
+    x = PctPair(n, 5)
+    x.upsert(soft_taints(rng, rand_nodes(rng, n, 8)), list(range(n)))
+    batches = [[rand_pct_pod(rng, b * 1000 + j) for j in range(120)] for b in range(4)]
+    arrs = [pods_array(p, x.a) for p in batches]
+    want = [x.o.schedule(pa, m) for pa, m in arrs]
+    s = x.s
+    hs = []
+    for pa, m in arrs:
+        h = s.prepare(pa, m)
+        assert s.lib.ks_batch_submit(s.ctx, h) == 0, s.lib.ks_last_error(s.ctx)
+        hs.append(h)
+    for h, (pa, m), w, b in zip(hs, arrs, want, range(4)):
+        assert s.lib.ks_batch_wait(s.ctx, h) == 0, s.lib.ks_last_error(s.ctx)
+        assert_results_equal(s.results(h, m), w, m, f"in-flight batch {b}")
+        s.free(h)
+    x.states_equal("in flight")
+    x.check_start("in flight")
     x.close()
 
 
