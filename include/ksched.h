@@ -424,10 +424,13 @@ typedef struct {
                                      0: by events (profilers that serialise dispatches)              */
   uint32_t sync_timeout_ms;       /* bound on every host wait for device work (60000), see
                                      ks_set_sync_timeout                                            */
-  uint32_t spread_replica_runs;   /* 1 (default): runs of >= 4 identical one-pod-path pods whose
-                                     constraints are all ScheduleAnyway (deployment replicas under the
-                                     system defaults) are scheduled by one filter pass and one
-                                     workgroup per run; 0: the per-pod chain       */
+  uint32_t spread_replica_runs;   /* 1 (default): runs of >= 4 identical one-pod-path pods with at
+                                     most a kubernetes.io/hostname ScheduleAnyway constraint and one on
+                                     another key (ScheduleAnyway, or since round 6 DoNotSchedule) --
+                                     deployment replicas under the system defaults or their own
+                                     zone constraints -- are scheduled by one filter pass and one
+                                     workgroup per run; 0: the per-pod chain.
+                                     Off when percentage_of_nodes_to_score < 100            */
 } ks_config;
 
 enum { KS_RESOLVE_AUTO = 0, KS_RESOLVE_SERIAL = 1, KS_RESOLVE_PARALLEL = 2 };
