@@ -1826,7 +1826,9 @@ ks_status spread_alloc(ks_ctx *c) {
       (st = dalloc(c, &c->d_spart, c->npos)) || (st = dalloc(c, &c->d_sraw2, c->npos)))
     return st;
   if (c->pct != 100) {
-    if ((st = dalloc(c, &c->d_win, WIN_WORDS + 2 * (((size_t)c->cap + WIN_CHUNK_SLOTS - 1) / WIN_CHUNK_SLOTS))) || (st = dalloc(c, &c->d_win_st, ((size_t)c->cap + 15) & ~(size_t)15)))
+    const size_t pieces = ((size_t)c->cap + WIN_CHUNK_SLOTS - 1) / WIN_CHUNK_SLOTS;
+    if ((st = dalloc(c, &c->d_win, WIN_WORDS + 2 * pieces)) ||
+        (st = dalloc(c, &c->d_win_st, ((size_t)c->cap + 15) & ~(size_t)15)))  // 16-byte loads
       return st;
   }
   c->d_cnt = c->d_dom + (size_t)MAX_TOPO_KEYS * c->npos;
