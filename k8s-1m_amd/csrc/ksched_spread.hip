@@ -527,7 +527,9 @@ constexpr int RF = NFILT + 2, R_FEAS = RF, R_IGN = RF + 1, R_TT = RF + 2, R_NA =
 
 // AFF: the pod has InterPodAffinity records (SPL_AFF); the variant without
 // them keeps their prefetched values out of the registers of spread pods.
-template <bool AFF>
+// PROBE: the percentageOfNodesToScore probe pass (win_mode 1) -- the filter
+// chain only; as a template parameter the score work compiles away there
+template <bool AFF, bool PROBE = false>
 __global__ __launch_bounds__(SP_THREADS) void spread_filter_kernel(SpreadArgs a) {
   __shared__ uint32_t s_seen[SP_LDS / 32];
   __shared__ uint32_t s_h[SP_LDS];
@@ -600,7 +602,8 @@ __global__ __launch_bounds__(SP_THREADS) void spread_filter_kernel(SpreadArgs a)
   uint64_t ipa_mn = ~0ull, ipa_mx = 0;
   // percentageOfNodesToScore < 100: the probe pass (filter only, win_st) or
   // the pass over the window spread_window_kernel found
-  const bool probe = a.win_mode == 1, windowed = a.win_mode == 2;
+  constexpr bool probe = PROBE;  // (the launcher passes win_mode 1 exactly to this instantiation)
+  const bool windowed = !PROBE && a.win_mode == 2;
   const uint32_t w_s0 = windowed ? a.win[1] : 0u, w_x = windowed ? a.win[2] : 0u;
   const bool w_all = !windowed || a.win[3] != 0;
   // the window pass of a pod that reads nothing from the nodes outside the
@@ -1968,8 +1971,11 @@ hipError_t launch_spread_pod(const SpreadArgs &args, uint32_t passes, hipStream_
   if (a.win_mode) {  // percentageOfNodesToScore < 100: probe, window, then the pass over the window
     SpreadArgs pr = a;
     pr.win_mode = 1;
-    if (passes & SPL_AFF) spread_filter_kernel<true><<<blocks, SP_THREADS, 0, st>>>(pr);
-    else spread_filter_kernel<false><<<blocks, SP_THREADS, 0, st>>>(pr);
+    // (the probe instantiation holds half the VGPRs: two workgroups per CU)
+    const uint32_t pblocks = std::max<uint32_t>(
+        1, std::min<uint32_t>((a.npos + SP_THREADS - 1) / SP_THREADS, 2u * (uint32_t)SPREAD_MAX_BLOCKS));
+    if (passes & SPL_AFF) spread_filter_kernel<true, true><<<pblocks, SP_THREADS, 0, st>>>(pr);
+    else spread_filter_kernel<false, true><<<pblocks, SP_THREADS, 0, st>>>(pr);
     spread_wcount_kernel<<<(a.nslots + WIN_CHUNK - 1) / WIN_CHUNK, WIN_CHUNK / 16, 0, st>>>(a);
     spread_window_kernel<<<1, WIN_THREADS, 0, st>>>(a);
   }
