@@ -134,8 +134,8 @@ def parse():
     ap.add_argument("--no-resident", action="store_true",
                     help="skip the secondary inputs-resident pass (batches compiled + uploaded before timing)")
     ap.add_argument("--latency-calls", type=int, default=100, help="ks_schedule calls per latency batch size (0: skip)")
-    ap.add_argument("--cpu-pods", type=int, default=24, help="oracle sample (pods), single thread")
-    ap.add_argument("--cpu-pods-mt", type=int, default=400, help="oracle sample (pods), multi-thread")
+    ap.add_argument("--cpu-pods", type=int, default=48, help="oracle sample (pods), single thread (~4 s at 1M nodes)")
+    ap.add_argument("--cpu-pods-mt", type=int, default=1000, help="oracle sample (pods), multi-thread (~10 s at 1M nodes on 16 threads)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch check only: spawn / join the ranks, exchange the rendezvous file, check "
